@@ -1,0 +1,60 @@
+# libsplinter_amd native build (host C++ with g++, device code with hipcc for gfx950).
+# Outputs stay in-tree (libsplinter_amd/lib, libsplinter_amd/bin) so they travel
+# with the repo snapshot to the GPU box.
+CXX      ?= g++
+HIPCC    ?= /opt/rocm/bin/hipcc
+ARCH     ?= gfx950
+PKG      := libsplinter_amd
+SRC      := $(PKG)/csrc
+LIB      := $(PKG)/lib
+BIN      := $(PKG)/bin
+BUILD_ID := $(shell git rev-parse --short HEAD 2>/dev/null || echo dev)
+
+CXXFLAGS := -O3 -std=c++17 -Wall -Wextra -fPIC -D_GNU_SOURCE -I$(SRC)/include -I$(SRC)/core \
+            -DSPL_BUILD_ID=\"$(BUILD_ID)\"
+HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -D_GNU_SOURCE -I$(SRC)/include -I$(SRC)/core \
+            -I$(SRC)/hip -Wno-unused-result -munsafe-fp-atomics
+LDLIBS   := -ldl -lrt -lpthread
+
+CORE_SRCS := $(SRC)/core/store_host.cpp $(SRC)/core/capi.cpp
+CORE_HDRS := $(wildcard $(SRC)/include/*.h $(SRC)/include/*.hpp $(SRC)/core/*.hpp)
+HIP_SRCS  := $(wildcard $(SRC)/hip/*.hip)
+HIP_HDRS  := $(wildcard $(SRC)/hip/*.hpp) $(CORE_HDRS)
+HIP_OBJS  := $(patsubst $(SRC)/hip/%.hip,build/hip/%.o,$(HIP_SRCS))
+
+HOST_LIBS := $(LIB)/libsplinter.so $(LIB)/libsplinter_p.so
+TOOLS     := $(BIN)/splinter_test $(BIN)/splinter_stress $(BIN)/splinter_chi_sao $(BIN)/splinterctl
+
+.PHONY: all host hip tools clean test
+all: host hip tools
+host: $(HOST_LIBS)
+hip: $(LIB)/libsplinter_hip.so
+tools: $(TOOLS)
+
+$(LIB) $(BIN) build/hip:
+	mkdir -p $@
+
+$(LIB)/libsplinter.so: $(CORE_SRCS) $(CORE_HDRS) | $(LIB)
+	$(CXX) $(CXXFLAGS) -shared -o $@ $(CORE_SRCS) $(LDLIBS)
+
+$(LIB)/libsplinter_p.so: $(CORE_SRCS) $(CORE_HDRS) | $(LIB)
+	$(CXX) $(CXXFLAGS) -DSPLINTER_PERSISTENT -shared -o $@ $(CORE_SRCS) $(LDLIBS)
+
+build/hip/%.o: $(SRC)/hip/%.hip $(HIP_HDRS) | build/hip
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB)/libsplinter_hip.so: $(HIP_OBJS) $(LIB)/libsplinter.so | $(LIB)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
+
+$(BIN)/%: $(SRC)/tools/%.cpp $(LIB)/libsplinter.so $(CORE_HDRS) | $(BIN)
+	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN/../lib' $(LDLIBS)
+
+$(BIN)/splinterctl: $(wildcard $(SRC)/cli/*.cpp $(SRC)/cli/*.hpp) $(LIB)/libsplinter.so | $(BIN)
+	$(CXX) $(CXXFLAGS) -I$(SRC)/cli -o $@ $(filter %.cpp,$^) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN/../lib' $(LDLIBS)
+	ln -sf splinterctl $(BIN)/splinter_cli
+
+test: host tools
+	$(BIN)/splinter_test
+
+clean:
+	rm -rf build $(LIB)/*.so $(BIN)

@@ -1,0 +1,89 @@
+/*
+ * splinter_ext.h — libsplinter_amd extensions to the reference C ABI.
+ *
+ *  - handle API: several open stores per process (the reference allows one);
+ *    every splinter_xxx(args) has a twin spl_xxx(spl_store *s, args);
+ *  - explicit create flags (embedding stride, persistence) and unlink;
+ *  - backend introspection (shm / file / hbm) and raw region access used by
+ *    the GPU checkpoint path and the bulk loaders.
+ */
+#ifndef SPLINTER_EXT_H
+#define SPLINTER_EXT_H
+#include "splinter.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct spl_store spl_store;
+
+#define SPL_CREATE_EMBEDDINGS     1u
+#define SPL_CREATE_PERSISTENT     2u
+#define SPL_CREATE_NO_EMBEDDINGS  4u
+
+spl_store  *spl_store_create(const char *name, size_t slots, size_t max_val, unsigned flags, int *err);
+spl_store  *spl_store_open(const char *name, int *err);
+void        spl_store_close(spl_store *s);
+int         spl_store_use(spl_store *s);          /* make `s` the splinter_* current store */
+spl_store  *spl_store_current(void);
+const char *spl_store_backend(spl_store *s);
+int         spl_store_geometry(spl_store *s, uint32_t *slots, uint32_t *max_val, uint32_t *stride);
+void       *spl_store_base(spl_store *s);         /* mapped region (host backends), else NULL */
+size_t      spl_store_bytes(spl_store *s);
+int         spl_unlink(const char *name);         /* remove shm object / file / hbm descriptor */
+const char *spl_version(void);
+const char *spl_build(void);
+
+/* handle twins of the reference API */
+int   spl_set_mop(spl_store *s, unsigned int mode);
+int   spl_get_mop(spl_store *s);
+void  spl_purge(spl_store *s);
+int   spl_get_header_snapshot(spl_store *s, splinter_header_snapshot_t *snap);
+int   spl_set(spl_store *s, const char *key, const void *val, size_t len);
+int   spl_unset(spl_store *s, const char *key);
+int   spl_get(spl_store *s, const char *key, void *buf, size_t buf_sz, size_t *out_sz);
+int   spl_list(spl_store *s, char **out_keys, size_t max_keys, size_t *out_count);
+int   spl_poll(spl_store *s, const char *key, uint64_t timeout_ms);
+int   spl_get_slot_snapshot(spl_store *s, const char *key, splinter_slot_snapshot_t *snap);
+int   spl_append(spl_store *s, const char *key, const void *data, size_t len, size_t *new_len);
+const void *spl_get_raw_ptr(spl_store *s, const char *key, size_t *out_sz, uint64_t *out_epoch);
+uint64_t spl_get_epoch(spl_store *s, const char *key);
+int   spl_set_as_system(spl_store *s, const char *key);
+int   spl_set_embedding(spl_store *s, const char *key, const float *vec);
+int   spl_get_embedding(spl_store *s, const char *key, float *out);
+int   spl_set_named_type(spl_store *s, const char *key, uint16_t mask);
+int   spl_set_slot_time(spl_store *s, const char *key, unsigned short mode, uint64_t epoch, size_t offset);
+int   spl_integer_op(spl_store *s, const char *key, splinter_integer_op_t op, const void *mask);
+int   spl_bump_slot(spl_store *s, const char *key);
+int   spl_retrain_slot(spl_store *s, const char *key);
+int   spl_set_label(spl_store *s, const char *key, uint64_t mask);
+int   spl_unset_label(spl_store *s, const char *key, uint64_t mask);
+int   spl_watch_register(spl_store *s, const char *key, uint8_t group);
+int   spl_watch_unregister(spl_store *s, const char *key, uint8_t group);
+int   spl_watch_label_register(spl_store *s, uint64_t mask, uint8_t group);
+int   spl_pulse_keygroup(spl_store *s, const char *key);
+uint64_t spl_get_signal_count(spl_store *s, uint8_t group);
+void  spl_enumerate_matches(spl_store *s, uint64_t mask,
+                            void (*cb)(const char *key, uint64_t epoch, void *data), void *ud);
+int   spl_event_bus_init(spl_store *s);
+int   spl_event_bus_open(spl_store *s);
+void  spl_event_bus_get_dirty(spl_store *s, uint64_t *out, size_t words);
+int   spl_shard_claim_ex(spl_store *s, uint32_t id, uint32_t pid, uint8_t intent, uint8_t prio,
+                         uint64_t dur, uint64_t at);
+int   spl_shard_claim(spl_store *s, uint32_t id, uint8_t intent, uint8_t prio, uint64_t dur);
+int   spl_shard_rebid(spl_store *s, uint32_t id, uint8_t intent, uint8_t prio, uint64_t dur);
+int   spl_shard_release(spl_store *s, uint32_t id);
+uint32_t spl_shard_election(spl_store *s, uint8_t *out_intent);
+int   spl_shard_table_snapshot(spl_store *s, struct splinter_shard_bid_snapshot *out, size_t max);
+int   spl_madvise(spl_store *s, uint32_t id, void *addr, size_t len, int advice, uint64_t timeout);
+int   spl_client_set_tandem(spl_store *s, const char *base, const void **vals, const size_t *lens, uint8_t orders);
+void  spl_client_unset_tandem(spl_store *s, const char *base, uint8_t orders);
+
+/* bulk helpers (host backends): key -> slot index, -1 if absent */
+long  spl_find_slot(spl_store *s, const char *key);
+uint64_t spl_hash_key(const char *key);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

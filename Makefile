@@ -23,7 +23,8 @@ HIP_HDRS  := $(wildcard $(SRC)/hip/*.hpp) $(CORE_HDRS)
 HIP_OBJS  := $(patsubst $(SRC)/hip/%.hip,build/hip/%.o,$(HIP_SRCS))
 
 HOST_LIBS := $(LIB)/libsplinter.so $(LIB)/libsplinter_p.so
-TOOLS     := $(BIN)/splinter_test $(BIN)/splinter_stress $(BIN)/splinter_chi_sao $(BIN)/splinterctl
+TOOLS     := $(patsubst $(SRC)/tools/%.cpp,$(BIN)/%,$(wildcard $(SRC)/tools/*.cpp)) \
+             $(if $(wildcard $(SRC)/cli/*.cpp),$(BIN)/splinterctl)
 
 .PHONY: all host hip tools clean test
 all: host hip tools

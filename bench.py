@@ -1,0 +1,237 @@
+#!/usr/bin/env python3
+"""Headline benchmark: KV set/get ops/s on the HBM arena (+ Nomic embed vectors/s).
+
+Metric (BASELINE.json): "KV set/get ops/sec + Nomic-768d embed vectors/sec at
+1/2/4/8 MI355X".  One process per GPU (torchrun); each rank owns one
+hash-shard of the key space in its own HBM arena (format v4, 128-B slots,
+256-B values) prepopulated with --keys-per-gpu keys.  A timed step is:
+
+  * KV phase: a batch of --batch client ops per rank (half set, half get,
+    uniformly random keys over the whole node's key space) issued as a set
+    batch and a get batch on two concurrent HIP streams, so readers race
+    writers on the seqlocks (the reference's MRSW/MRMW regime,
+    /root/reference/splinter_stress.c, splinter_chi_sao.c).  With N>1 every
+    batch is routed to the owning shards with RCCL all-to-all and the results
+    are routed back (collective C1) inside the timed region.
+  * embed phase (--mode mixed/embed): one batch of synthetic documents through
+    the random-init Nomic-BERT encoder on the gfx950 kernels, mean-pooled
+    vectors written into their arena slots.
+
+Ops counted exactly as the reference does (every set + get attempt that
+completes, splinter_stress.c:212-213); EAGAIN retries are reported separately.
+Weak scaling: per-GPU work is fixed as N grows; `value` is the node total.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REF_MRMW_OPS = 15.6e6  # reference MRMW headline (README.md:131), BASELINE.md
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--mode", default="kv", choices=["kv", "embed", "mixed"])
+    p.add_argument("--keys-per-gpu", type=int, default=100_000_000)
+    p.add_argument("--slots-factor", type=float, default=2.0)
+    p.add_argument("--max-val", type=int, default=256)
+    p.add_argument("--value-len", type=int, default=150)
+    p.add_argument("--batch", type=int, default=8_000_000, help="client ops per rank per step")
+    p.add_argument("--set-frac", type=float, default=0.5)
+    p.add_argument("--embed-batch", type=int, default=512, help="documents per rank per step")
+    p.add_argument("--embed-seq", type=int, default=512)
+    p.add_argument("--verify", type=int, default=20000)
+    return p.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
+    from libsplinter_amd.parallel.sharded import GpuShard, ShardedKV
+
+    log = (lambda *a: print(*a, file=sys.stderr, flush=True)) if rank == 0 else (lambda *a: None)
+    kpg = args.keys_per_gpu
+    total_keys = kpg * world
+    slots = int(kpg * args.slots_factor)
+    name = f"bench{os.getpid()}r{rank}"
+    t0 = time.time()
+    arena = HbmArena.create(name, slots=slots, max_val=args.max_val, embeddings=False)
+    arena.store.set_mop(0)  # throughput mode: no scrubbing (reference stress default)
+    kv = ShardedKV(GpuShard(arena))
+    vstride = (args.max_val + 15) // 16 * 16
+
+    # ---- prepopulate: every rank inserts the global ids it owns ----------
+    chunk = 1 << 24
+    inserted = 0
+    for first in range(0, total_keys, chunk):
+        n = min(chunk, total_keys - first)
+        K = format_keys(n, "k", 10, 16, first=first)
+        if world > 1:
+            own = kv.owned_mask(K)
+            ids = torch.nonzero(own).squeeze(1) + first
+            K = K[own]
+        else:
+            ids = None
+        V, L = format_values(K.shape[0], 1, args.value_len, vstride, first=first, ids=ids)
+        st = arena.set(K, V, L)
+        bad = int((st != 0).sum())
+        if bad:
+            raise RuntimeError(f"prepopulate: {bad} inserts failed (first status {st[st != 0][0].item()})")
+        inserted += K.shape[0]
+        del K, V, L, st
+    torch.cuda.synchronize()
+    log(f"[bench] rank0 arena {slots} slots, {inserted} keys inserted in {time.time() - t0:.1f}s "
+        f"({arena.slots * 128 / 2**30 + arena.slots * vstride / 2**30:.1f} GiB)")
+
+    # ---- per-step client batches (pre-generated: the client's own keys) ----
+    n_set = int(args.batch * args.set_frac) if args.mode != "embed" else 0
+    n_get = args.batch - n_set if args.mode != "embed" else 0
+    nbuf = min(args.steps + args.warmup, 4)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + rank)
+    batches = []
+    for b in range(nbuf):
+        sid = torch.randint(0, total_keys, (n_set,), device="cuda", generator=g)
+        gid = torch.randint(0, total_keys, (n_get,), device="cuda", generator=g)
+        SK = format_keys(n_set, "k", 10, 16, ids=sid)
+        GK = format_keys(n_get, "k", 10, 16, ids=gid)
+        SV, SL = format_values(n_set, 2 + b, args.value_len, vstride, ids=sid)
+        batches.append((SK, SV, SL, GK, gid))
+    gout = torch.empty((n_get, vstride), dtype=torch.uint8, device="cuda")
+
+    # ---- embed phase (model) --------------------------------------------
+    embedder = None
+    if args.mode in ("embed", "mixed"):
+        from libsplinter_amd.models.bench_embed import EmbedPhase
+        embedder = EmbedPhase(arena, batch=args.embed_batch, seq=args.embed_seq, rank=rank)
+
+    s_set, s_get = torch.cuda.Stream(), torch.cuda.Stream()
+    stats = arena.stats
+
+    def step(i):
+        SK, SV, SL, GK, _ = batches[i % nbuf]
+        cur = torch.cuda.current_stream()
+        if n_set:
+            s_set.wait_stream(cur)
+            s_get.wait_stream(cur)
+            if world == 1:
+                with torch.cuda.stream(s_set):
+                    arena.set(SK, SV, SL)
+                with torch.cuda.stream(s_get):
+                    arena.get(GK, out=gout)
+                cur.wait_stream(s_set)
+                cur.wait_stream(s_get)
+            else:
+                kv.set(SK, SV, SL)
+                kv.get(GK)
+        if embedder is not None:
+            embedder.run()
+
+    for i in range(args.warmup):
+        step(i)
+    torch.cuda.synchronize()
+    arena.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t_start = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+    st = stats.clone()
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(st)
+    elapsed = t.item()
+    attempts, ok, again, miss = [int(x) for x in st.tolist()]
+
+    # ---- integrity: sampled gets must parse and match their key ----------
+    integrity_fail = 0
+    if args.verify and n_get:
+        GK, gid = batches[0][3], batches[0][4]
+        m = min(args.verify, n_get)
+        if world > 1:
+            sts, outv, lens = kv.get(GK[:m])
+        else:
+            sts, outv, lens = arena.get(GK[:m])
+        o, ln, ids, s_ = outv.cpu().numpy(), lens.cpu().numpy(), gid[:m].cpu().numpy(), sts.cpu().numpy()
+        for i in range(m):
+            if s_[i] != 0:
+                integrity_fail += 1
+                continue
+            v = bytes(o[i, : ln[i]])
+            try:
+                head, rest = v.split(b"|id:", 1)
+                ver = int(head[4:])
+                ident = int(rest.split(b"|", 1)[0])
+                fill = v[v.index(b"data:") + 5:]
+                if ident != ids[i] or fill != bytes([65 + ver % 26]) * len(fill):
+                    integrity_fail += 1
+            except Exception:
+                integrity_fail += 1
+        if world > 1:
+            x = torch.tensor([integrity_fail], device="cuda")
+            dist.all_reduce(x)
+            integrity_fail = int(x.item())
+
+    kv_ops = (n_set + n_get) * args.steps * world
+    kv_ops_s = kv_ops / elapsed if kv_ops else 0.0
+    emb_vps = None
+    if embedder is not None:
+        emb_vps = embedder.docs_per_step * args.steps * world / elapsed
+    value = kv_ops_s if args.mode != "embed" else emb_vps
+    res = {
+        "metric": "KV set/get ops/sec + Nomic-768d embed vectors/sec at 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "ops/s" if args.mode != "embed" else "vectors/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": (value / REF_MRMW_OPS) if args.mode != "embed" else None,
+        "dtype": "bf16" if embedder is not None else "u8-kv",
+        "data": "synthetic keys k%010d / 150-B 'ver:|id:|data:' payloads; random-init Nomic weights",
+        "config": {
+            "model": "hbm-arena-v4 (128-B slots, 256-B values)" + (" + nomic-embed-text-v1.5" if embedder else ""),
+            "keys_per_gpu": kpg, "slots_per_gpu": slots, "global_batch": args.batch * world,
+            "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
+            "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),
+            "mode": args.mode,
+        },
+        "kv_ops_per_s": kv_ops_s,
+        "embed_vectors_per_s": emb_vps,
+        "kv_attempts": attempts, "kv_ok": ok, "kv_eagain_retries": again, "kv_miss": miss,
+        "successful_ops_per_s": ok / elapsed if elapsed else 0.0,
+        "integrity_failures": integrity_fail,
+    }
+    if rank == 0:
+        print(json.dumps(res), flush=True)
+    arena.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,399 @@
+// arena_dev.hpp — device-side format-v4 arena operations for gfx950.
+//
+// Owner-computes design: every mutation of an HBM arena
+// runs on the GPU that holds it, so the seqlock CAS / fetch_add are
+// agent-scope atomics on device memory.  Visibility across workgroups and
+// XCDs follows the CDNA4 rules (MI355X_MICROARCH.md, "Workgroup dispatch, XCD
+// placement & inter-workgroup visibility"):
+//   * probe words (hash, epoch, key, val_len) are read with agent-scope
+//     relaxed atomic loads (global_load ... sc1: L1-bypassing, never stale);
+//   * a writer stores the payload with plain 16-B stores, then ONE agent
+//     release fence (buffer_wbl2 sc1) + explicit s_waitcnt vmcnt(0) — the
+//     guide's ROCm 7.2 hazard fix — before publishing hash and epoch;
+//   * a reader takes the epoch with an agent ACQUIRE load (buffer_inv sc1 on
+//     this CU's L1), so its plain 16-B value loads cannot hit stale L1 lines;
+//     s_waitcnt vmcnt(0) then orders the value loads before the closing epoch
+//     load.
+//
+// Seqlock per slot (same protocol as the host backend, store_host.cpp):
+//   writer : CAS epoch even->odd, write payload, release, publish hash,
+//            epoch += 1;  unset rewinds the epoch to 2, retrain to 4.
+//   reader : e1 = epoch (acquire); odd -> EAGAIN; key + value; e2 = epoch;
+//            e1 != e2 -> EAGAIN.
+// Probe chains end at a virgin slot (hash 0 && epoch 0).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "splinter_layout.hpp"
+
+namespace spl {
+namespace dev {
+
+enum : int32_t {
+  kOk = 0,
+  kAgain = -11,    // -EAGAIN
+  kNoEnt = -2,     // -ENOENT
+  kNoSpc = -28,    // -ENOSPC
+  kMsgSize = -90,  // -EMSGSIZE
+  kProto = -71,    // EPROTOTYPE (host maps to errno EPROTOTYPE)
+  kInval = -22,
+};
+
+struct Arena {
+  uint8_t* base;
+  uint32_t slots;
+  uint32_t max_val;
+  uint32_t stride;
+  uint32_t flags;  // bit0: event bus armed (maintain the dirty mask)
+  __device__ __forceinline__ splinter_header* hdr() const { return (splinter_header*)base; }
+  __device__ __forceinline__ uint8_t* slot(size_t i) const { return base + kHeaderBytes + i * (size_t)stride; }
+  __device__ __forceinline__ uint8_t* value(size_t i) const {
+    return base + kHeaderBytes + (size_t)slots * stride + i * (size_t)max_val;
+  }
+};
+
+// ------------------------------------------------------------- atomics --
+__device__ __forceinline__ uint64_t ald64(const void* p) {
+  return __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t ald64_acq(const void* p) {
+  return __hip_atomic_load((const uint64_t*)p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ald32(const void* p) {
+  return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint8_t ald8(const void* p) {
+  return __hip_atomic_load((const uint8_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ast64(void* p, uint64_t v) {
+  __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ast32(void* p, uint32_t v) {
+  __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void ast8(void* p, uint8_t v) {
+  __hip_atomic_store((uint8_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool acas64(void* p, uint64_t expect, uint64_t want) {
+  return __hip_atomic_compare_exchange_strong((uint64_t*)p, &expect, want, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t aadd64(void* p, uint64_t v) {
+  return __hip_atomic_fetch_add((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void aor64(void* p, uint64_t v) {
+  __hip_atomic_fetch_or((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void aand64(void* p, uint64_t v) {
+  __hip_atomic_fetch_and((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wait for every outstanding vector-memory op of this wave (loads AND stores).
+__device__ __forceinline__ void drain() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// Agent release: write back this XCD's L2, then wait (explicit wait: the
+// ROCm 7.2 compiler may drop the fence's own wait, MI355X guide hazard note).
+__device__ __forceinline__ void release() {
+  drain();
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  drain();
+}
+
+// ------------------------------------------------------------- keys ----
+// A key arrives as a NUL-padded record of `kstride` bytes (16/32/48/64).
+// Canonical form: first 63 bytes, NUL padded to 64, FNV-1a over its length.
+struct Key {
+  uint32_t w[16];  // canonical key words (registers: every index is static)
+  uint32_t len;
+  uint64_t hash;
+};
+
+__device__ __forceinline__ void load_key(Key& k, const char* rec, int kstride) {
+  const uint4* r = (const uint4*)rec;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    uint4 v = (c * 16 < kstride) ? r[c] : make_uint4(0, 0, 0, 0);
+    k.w[4 * c + 0] = v.x; k.w[4 * c + 1] = v.y; k.w[4 * c + 2] = v.z; k.w[4 * c + 3] = v.w;
+  }
+  uint64_t h = kFnvOffset;
+  uint32_t len = 0;
+  bool live = true;
+#pragma unroll
+  for (int wi = 0; wi < 16; ++wi) {
+    if (wi * 4 < kstride) {
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        const uint32_t ch = (k.w[wi] >> (8 * b)) & 0xffu;
+        live = live && ch != 0 && (wi * 4 + b) < 63;
+        if (live) { h = (h ^ ch) * kFnvPrime; ++len; }
+      }
+    }
+  }
+#pragma unroll
+  for (int wi = 0; wi < 16; ++wi) {  // zero every byte at or past len
+    const int keep = (int)len - 4 * wi;
+    const uint32_t m = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+    k.w[wi] &= m;
+  }
+  k.len = len;
+  k.hash = h;
+}
+
+// Compare the stored key with ours through sc1 loads, 8 bytes at a time, up
+// to and including our terminating NUL (stored keys are NUL padded).
+__device__ __forceinline__ bool key_eq(const uint8_t* slot, const Key& k) {
+  const uint8_t* sk = slot + kOffKey;
+  const uint32_t nq = (k.len >> 3) + 1;  // 8-byte words holding the key + NUL
+  bool eq = true;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    if ((uint32_t)q < nq) {
+      const uint64_t v = ald64(sk + 8 * q);
+      eq = eq && v == (((uint64_t)k.w[2 * q + 1] << 32) | k.w[2 * q]);
+    }
+  }
+  return eq;
+}
+
+__device__ __forceinline__ void store_key(uint8_t* slot, const Key& k) {
+  uint4* d = (uint4*)(slot + kOffKey);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) d[c] = make_uint4(k.w[4 * c], k.w[4 * c + 1], k.w[4 * c + 2], k.w[4 * c + 3]);
+}
+
+__device__ __forceinline__ uint64_t slot_hash(const uint8_t* s) { return ald64(s + kOffHash); }
+__device__ __forceinline__ uint64_t slot_epoch(const uint8_t* s) { return ald64(s + kOffEpoch); }
+__device__ __forceinline__ uint64_t* epoch_ptr(uint8_t* s) { return (uint64_t*)(s + kOffEpoch); }
+
+// Locate `k`; returns the slot index or -1.  Pure lookup (no seqlock).
+__device__ __forceinline__ long find(const Arena& a, const Key& k) {
+  size_t idx = (size_t)(k.hash % a.slots);
+  for (uint32_t i = 0; i < a.slots; ++i) {
+    const uint8_t* s = a.slot(idx);
+    const uint64_t sh = slot_hash(s);
+    if (sh == k.hash && key_eq(s, k)) return (long)idx;
+    if (sh == 0 && slot_epoch(s) == 0) return -1;
+    if (++idx == a.slots) idx = 0;
+  }
+  return -1;
+}
+
+// ------------------------------------------------------------- signals --
+__device__ __forceinline__ void pulse(const Arena& a, const uint8_t* s) {
+  splinter_header* H = a.hdr();
+  const uint64_t wm = ald64(s + kOffWatch);
+  for (uint64_t m = wm; m; m &= m - 1) aadd64(&H->signal_groups[__builtin_ctzll(m)].counter, 1);
+  const uint64_t bl = ald64(s + kOffBloom);
+  for (uint64_t m = bl; m; m &= m - 1) {
+    const uint8_t g = ald8(&H->bloom_watches[__builtin_ctzll(m)]);
+    if (g < SPLINTER_MAX_GROUPS) aadd64(&H->signal_groups[g].counter, 1);
+  }
+}
+
+__device__ __forceinline__ void mark_dirty(const Arena& a, size_t idx) {
+  if (!(a.flags & 1u)) return;
+  const size_t m = idx % kDirtyBits;
+  aor64(&a.hdr()->event_bus.dirty_mask[m / 64], 1ull << (m % 64));
+}
+
+// ------------------------------------------------------------- writes --
+__device__ __forceinline__ bool scrub_flags(const Arena& a, bool& hybrid) {
+  const uint8_t f = ald8(&a.hdr()->core_flags);
+  hybrid = (f & SPL_SYS_HYBRID_SCRUB) != 0;
+  return (f & SPL_SYS_AUTO_SCRUB) != 0;
+}
+
+__device__ __forceinline__ uint32_t keep_mask(int keep) {
+  return keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
+}
+
+// Copy a value into slot idx's value region in 16-B chunks.  The tail of the
+// last chunk is zeroed; with scrubbing the region is zeroed to the 64-B
+// boundary (hybrid) or to max_val (full) — the reference's mop modes
+// (reference splinter.c:393-401).  Source records are 16-B aligned.
+__device__ __forceinline__ void write_value(const Arena& a, size_t idx, const uint8_t* src, uint32_t len, bool scrub,
+                                            bool hybrid) {
+  uint4* dst = (uint4*)a.value(idx);
+  const uint4* s4 = (const uint4*)src;
+  const uint32_t full = len >> 4;
+  for (uint32_t c = 0; c < full; ++c) dst[c] = s4[c];
+  uint32_t done = full << 4;
+  if (len & 15) {
+    uint4 t = s4[full];
+    const int r = (int)(len & 15);
+    t.x &= keep_mask(r); t.y &= keep_mask(r - 4); t.z &= keep_mask(r - 8); t.w &= keep_mask(r - 12);
+    dst[full] = t;
+    done += 16;
+  }
+  if (scrub) {
+    uint32_t end = hybrid ? ((len + 63u) & ~63u) : a.max_val;
+    if (end > a.max_val) end = a.max_val;
+    for (; done + 16 <= end; done += 16) dst[done >> 4] = make_uint4(0, 0, 0, 0);
+  }
+}
+
+// Publish a locked slot: release the payload, store hash, epoch+1.
+__device__ __forceinline__ void publish(const Arena& a, size_t idx, uint64_t hash) {
+  uint8_t* s = a.slot(idx);
+  release();
+  ast64(s + kOffHash, hash);
+  aadd64(epoch_ptr(s), 1);
+}
+
+// SET (insert or update).  On success *out_idx = slot index.
+__device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint32_t len, long* out_idx) {
+  if (len == 0 || len > a.max_val) return kMsgSize;
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  const size_t home = (size_t)(k.hash % a.slots);
+  long free_idx = -1;
+  uint64_t free_ep = 0;
+  size_t idx = home;
+  for (uint32_t i = 0; i < a.slots; ++i) {
+    uint8_t* s = a.slot(idx);
+    const uint64_t sh = slot_hash(s);
+    const uint64_t e = slot_epoch(s);
+    if (sh == k.hash && key_eq(s, k)) {
+      if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
+      if (slot_hash(s) != k.hash || !key_eq(s, k)) {  // raced with unset
+        aadd64(epoch_ptr(s), 1);
+        return kAgain;
+      }
+      write_value(a, idx, val, len, scrub, hybrid);
+      ast32(s + kOffValLen, len);
+      publish(a, idx, k.hash);
+      *out_idx = (long)idx;
+      return kOk;
+    }
+    if ((e & 1) && (sh == 0 || sh == k.hash)) return kAgain;
+    if (sh == 0) {
+      if (free_idx < 0) { free_idx = (long)idx; free_ep = e; }
+      if (e == 0) break;
+    }
+    if (++idx == a.slots) idx = 0;
+  }
+  if (free_idx < 0) return kNoSpc;
+  uint8_t* fs = a.slot((size_t)free_idx);
+  if (!acas64(epoch_ptr(fs), free_ep, free_ep + 1)) return kAgain;
+  if (slot_hash(fs) != 0) { aadd64(epoch_ptr(fs), 1); return kAgain; }
+  // re-validate the chain while holding the claimed slot (no duplicates)
+  idx = home;
+  for (uint32_t i = 0; i < a.slots; ++i) {
+    if ((long)idx != free_idx) {
+      uint8_t* s = a.slot(idx);
+      const uint64_t sh = slot_hash(s);
+      const uint64_t e = slot_epoch(s);
+      if ((sh == k.hash && key_eq(s, k)) || ((e & 1) && (sh == 0 || sh == k.hash))) {
+        aadd64(epoch_ptr(fs), 1);
+        return kAgain;
+      }
+      if (sh == 0 && e == 0) break;
+    }
+    if (++idx == a.slots) idx = 0;
+  }
+  write_value(a, (size_t)free_idx, val, len, scrub, hybrid);
+  ast32(fs + kOffValLen, len);
+  if (a.stride == kSlotEmbedBytes) {  // fresh slot: clear a stale vector
+    uint4* ev = (uint4*)(fs + kOffEmbed);
+    for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ev[c] = make_uint4(0, 0, 0, 0);
+  }
+  store_key(fs, k);
+  publish(a, (size_t)free_idx, k.hash);
+  *out_idx = free_idx;
+  return kOk;
+}
+
+// GET: seqlock read into out (may be null: size query).
+__device__ int32_t get_op(const Arena& a, const Key& k, uint8_t* out, uint32_t out_cap, uint32_t* out_len) {
+  size_t idx = (size_t)(k.hash % a.slots);
+  for (uint32_t i = 0; i < a.slots; ++i) {
+    const uint8_t* s = a.slot(idx);
+    const uint64_t sh = slot_hash(s);
+    if (sh == k.hash) {
+      const uint64_t e1 = ald64_acq(s + kOffEpoch);
+      if (key_eq(s, k)) {
+        if (e1 & 1) return kAgain;
+        const uint32_t len = ald32(s + kOffValLen);
+        *out_len = len;
+        if (out) {
+          if (len > out_cap) return kMsgSize;
+          const uint4* src = (const uint4*)a.value(idx);
+          uint4* dst = (uint4*)out;
+          const uint32_t n16 = (len + 15) >> 4;
+          for (uint32_t c = 0; c < n16; ++c) dst[c] = src[c];
+        }
+        drain();
+        const uint64_t e2 = slot_epoch(s);
+        return (e2 == e1 && slot_hash(s) == k.hash) ? kOk : kAgain;
+      }
+    } else if (sh == 0 && slot_epoch(s) == 0) {
+      return kNoEnt;
+    }
+    if (++idx == a.slots) idx = 0;
+  }
+  return kNoEnt;
+}
+
+// UNSET: returns the old length (>= 0) or a negative status.
+__device__ int32_t unset_op(const Arena& a, const Key& k, long* out_idx) {
+  const long i = find(a, k);
+  if (i < 0) return kNoEnt;
+  uint8_t* s = a.slot((size_t)i);
+  const uint64_t e = slot_epoch(s);
+  if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
+  if (slot_hash(s) != k.hash || !key_eq(s, k)) { aadd64(epoch_ptr(s), 1); return kNoEnt; }
+  const uint32_t old = ald32(s + kOffValLen);
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  ast64(s + kOffHash, 0);
+  uint4* key4 = (uint4*)(s + kOffKey);
+  if (scrub) {
+    uint4* v = (uint4*)a.value((size_t)i);
+    for (uint32_t c = 0; c < a.max_val / 16; ++c) v[c] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) key4[c] = make_uint4(0, 0, 0, 0);
+  } else {
+    key4[0] = make_uint4(0, 0, 0, 0);
+  }
+  // bytes 16..63: val_off kept, val_len 0, type VOID, user 0, watcher/ctime/atime/bloom 0
+  const uint32_t voff = ald32(s + kOffValOff);
+  *(uint4*)(s + 16) = make_uint4(voff, 0, SPL_SLOT_DEFAULT_TYPE, 0);
+  *(uint4*)(s + 32) = make_uint4(0, 0, 0, 0);
+  *(uint4*)(s + 48) = make_uint4(0, 0, 0, 0);
+  if (a.stride == kSlotEmbedBytes) {
+    uint4* ev = (uint4*)(s + kOffEmbed);
+    for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ev[c] = make_uint4(0, 0, 0, 0);
+  }
+  release();
+  ast64(epoch_ptr(s), 2);  // reference contract: unset rewinds the epoch to 2
+  *out_idx = i;
+  return (int32_t)old;
+}
+
+// In-place u64 integer op under the seqlock.
+__device__ int32_t integer_op(const Arena& a, const Key& k, int op, uint64_t m, uint64_t* result, long* out_idx) {
+  const long i = find(a, k);
+  if (i < 0) return kNoEnt;
+  uint8_t* s = a.slot((size_t)i);
+  if (!(ald8(s + kOffType) & SPL_SLOT_TYPE_BIGUINT)) return kProto;
+  const uint64_t e = slot_epoch(s);
+  if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
+  uint8_t* v = a.value((size_t)i);
+  uint64_t x = ald64(v);
+  switch (op) {
+    case SPL_OP_AND: x &= m; break;
+    case SPL_OP_OR: x |= m; break;
+    case SPL_OP_XOR: x ^= m; break;
+    case SPL_OP_NOT: x = ~x; break;
+    case SPL_OP_INC: x += m; break;
+    case SPL_OP_DEC: x -= m; break;
+    default: break;
+  }
+  ast64(v, x);
+  drain();
+  aadd64(epoch_ptr(s), 1);
+  if (result) *result = x;
+  *out_idx = i;
+  return kOk;
+}
+
+}  // namespace dev
+}  // namespace spl

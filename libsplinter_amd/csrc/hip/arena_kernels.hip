@@ -1,0 +1,579 @@
+// arena_kernels.hip — batched format-v4 arena kernels for gfx950 (K1-K6, K9
+// of SURVEY §2.10) and their C launchers.
+//
+// Every launcher takes device pointers and a hipStream_t, so the same entry
+// points serve the C++ HBM store (single ops, n = 1), the Python bindings
+// (torch tensors' data_ptr on torch's current stream) and the benchmarks.
+// Work distribution: 256-thread blocks, grid-stride loop capped at
+// 8 blocks/CU x 256 CUs, one op per thread.  Global-epoch increments and
+// retry statistics are reduced per block (one atomic per block instead of one
+// per op: a single contended word saturates near 88 M atomics/s on MI355X).
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <cstdio>
+
+#include "arena_dev.hpp"
+#include "arena_api.h"
+
+using namespace spl;
+using namespace spl::dev;
+
+namespace {
+
+constexpr int kBlock = 256;
+constexpr int kMaxGrid = 256 * 8;
+
+inline int grid_for(long n) {
+  long g = (n + kBlock - 1) / kBlock;
+  if (g < 1) g = 1;
+  return (int)(g > kMaxGrid ? kMaxGrid : g);
+}
+
+__device__ __forceinline__ Arena to_dev(const spl_arena_t& a) {
+  Arena d;
+  d.base = (uint8_t*)a.base;
+  d.slots = a.slots;
+  d.max_val = a.max_val;
+  d.stride = a.stride;
+  d.flags = a.flags;
+  return d;
+}
+
+// Block-wide sum of a per-thread counter; thread 0 returns the total.
+__device__ __forceinline__ uint64_t block_sum(uint64_t v) {
+  __shared__ uint64_t part[kBlock / 64];
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0) part[wid] = v;
+  __syncthreads();
+  uint64_t t = 0;
+  if (threadIdx.x == 0)
+    for (int w = 0; w < kBlock / 64; ++w) t += part[w];
+  __syncthreads();
+  return t;
+}
+
+struct Stats {
+  uint64_t attempts = 0, ok = 0, again = 0, miss = 0;
+};
+
+__device__ __forceinline__ void flush_stats(const Arena& a, Stats st, uint64_t* stats, uint64_t mutations) {
+  const uint64_t at = block_sum(st.attempts);
+  const uint64_t ok = block_sum(st.ok);
+  const uint64_t ag = block_sum(st.again);
+  const uint64_t ms = block_sum(st.miss);
+  const uint64_t mu = block_sum(mutations);
+  if (threadIdx.x == 0) {
+    if (stats) {
+      if (at) aadd64(stats + 0, at);
+      if (ok) aadd64(stats + 1, ok);
+      if (ag) aadd64(stats + 2, ag);
+      if (ms) aadd64(stats + 3, ms);
+    }
+    if (mu) aadd64(&a.hdr()->epoch, mu);
+  }
+}
+
+__device__ __forceinline__ void backoff(int attempt) {
+  if (attempt < 4) __builtin_amdgcn_s_sleep(1);
+  else __builtin_amdgcn_s_sleep(8);
+}
+
+// ------------------------------------------------------------- init -----
+__global__ void k_init_slots(spl_arena_t aa) {
+  const Arena a = to_dev(aa);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < a.slots; i += (size_t)gridDim.x * blockDim.x) {
+    uint8_t* s = a.slot(i);
+    // zero the 128-B core, then set val_off / type
+    for (int c = 0; c < 8; ++c) *(uint4*)(s + 16 * c) = make_uint4(0, 0, 0, 0);
+    *(uint32_t*)(s + kOffValOff) = (uint32_t)(i * (size_t)a.max_val);
+    *(s + kOffType) = SPL_SLOT_DEFAULT_TYPE;
+  }
+}
+
+// ------------------------------------------------------------- set ------
+__global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
+                                                int vstride, const uint32_t* lens, long n, int32_t* status,
+                                                int max_retry, uint64_t* stats) {
+  const Arena a = to_dev(aa);
+  Stats st;
+  uint64_t muts = 0;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    const uint32_t len = lens[i];
+    int32_t rc = kAgain;
+    long idx = -1;
+    for (int t = 0; t <= max_retry; ++t) {
+      ++st.attempts;
+      rc = set_op(a, k, vals + i * (long)vstride, len, &idx);
+      if (rc != kAgain) break;
+      ++st.again;
+      backoff(t);
+    }
+    if (rc == kOk) {
+      ++st.ok;
+      ++muts;
+      pulse(a, a.slot((size_t)idx));
+      mark_dirty(a, (size_t)idx);
+    }
+    if (status) status[i] = rc;
+  }
+  flush_stats(a, st, stats, muts);
+}
+
+// ------------------------------------------------------------- get ------
+__global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
+                                                int ostride, uint32_t* out_lens, long n, int32_t* status,
+                                                int max_retry, uint64_t* stats) {
+  const Arena a = to_dev(aa);
+  Stats st;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    uint32_t len = 0;
+    int32_t rc = kAgain;
+    for (int t = 0; t <= max_retry; ++t) {
+      ++st.attempts;
+      rc = get_op(a, k, out ? out + i * (long)ostride : nullptr, (uint32_t)ostride, &len);
+      if (rc != kAgain) break;
+      ++st.again;
+      backoff(t);
+    }
+    if (rc == kOk) ++st.ok;
+    else if (rc == kNoEnt) ++st.miss;
+    if (out_lens) out_lens[i] = rc == kOk ? len : 0;
+    if (status) status[i] = rc;
+  }
+  flush_stats(a, st, stats, 0);
+}
+
+// ------------------------------------------------------------- unset ----
+__global__ __launch_bounds__(kBlock) void k_unset(spl_arena_t aa, const char* keys, int kstride, long n,
+                                                  int32_t* status, int max_retry) {
+  const Arena a = to_dev(aa);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    long idx = -1;
+    int32_t rc = kAgain;
+    for (int t = 0; t <= max_retry; ++t) {
+      rc = unset_op(a, k, &idx);
+      if (rc != kAgain) break;
+      backoff(t);
+    }
+    if (status) status[i] = rc;
+  }
+}
+
+// ------------------------------------------------------------- integer --
+__global__ __launch_bounds__(kBlock) void k_intop(spl_arena_t aa, const char* keys, int kstride, const int* ops,
+                                                  const uint64_t* masks, long n, int32_t* status, uint64_t* results,
+                                                  int max_retry) {
+  const Arena a = to_dev(aa);
+  uint64_t muts = 0;
+  Stats st;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    long idx = -1;
+    uint64_t r = 0;
+    int32_t rc = kAgain;
+    for (int t = 0; t <= max_retry; ++t) {
+      rc = integer_op(a, k, ops[i], masks ? masks[i] : 0, &r, &idx);
+      if (rc != kAgain) break;
+      backoff(t);
+    }
+    if (rc == kOk) { ++muts; mark_dirty(a, (size_t)idx); }
+    if (results) results[i] = r;
+    if (status) status[i] = rc;
+  }
+  flush_stats(a, st, nullptr, muts);
+}
+
+// ------------------------------------------------- keyed metadata ops ----
+// op: 0 set_label, 1 unset_label, 2 bump, 3 get_epoch, 4 watch_register,
+//     5 watch_unregister, 6 pulse_keygroup, 7 set_as_system, 8 retrain,
+//     9 set_named_type (arg = mask; no BIGUINT promotion: see host path),
+//     10 set ctime, 11 set atime, 12 find (out = slot index)
+__global__ __launch_bounds__(kBlock) void k_meta(spl_arena_t aa, const char* keys, int kstride, int op,
+                                                 const uint64_t* args, long n, int32_t* status, uint64_t* out) {
+  const Arena a = to_dev(aa);
+  uint64_t muts = 0;
+  Stats st;
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    const uint64_t arg = args ? args[i] : 0;
+    const long idx = find(a, k);
+    int32_t rc = kOk;
+    uint64_t o = 0;
+    if (idx < 0) {
+      rc = kNoEnt;
+    } else {
+      uint8_t* s = a.slot((size_t)idx);
+      switch (op) {
+        case 0: aor64((uint64_t*)(s + kOffBloom), arg); ++muts; mark_dirty(a, idx); break;
+        case 1: aand64((uint64_t*)(s + kOffBloom), ~arg); ++muts; mark_dirty(a, idx); break;
+        case 2: {
+          const uint64_t e = slot_epoch(s);
+          if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) { rc = kAgain; break; }
+          pulse(a, s);
+          drain();
+          aadd64(epoch_ptr(s), 1);
+          break;
+        }
+        case 3: o = slot_epoch(s); break;
+        case 4: aor64((uint64_t*)(s + kOffWatch), 1ull << (arg & 63)); break;
+        case 5: aand64((uint64_t*)(s + kOffWatch), ~(1ull << (arg & 63))); break;
+        case 6: pulse(a, s); break;
+        case 7:
+          ast8(s + kOffType, (uint8_t)SPL_SLOT_TYPE_BINARY);
+          ast32((uint32_t*)(s + kOffValLen), a.max_val);
+          break;
+        case 8:
+          ast64(epoch_ptr(s), 3);
+          drain();
+          if (a.stride == kSlotEmbedBytes)
+            for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ((uint4*)(s + kOffEmbed))[c] = make_uint4(0, 0, 0, 0);
+          release();
+          ast64(epoch_ptr(s), 4);
+          ++muts;
+          pulse(a, s);
+          mark_dirty(a, idx);
+          break;
+        case 9: {
+          const uint64_t e = slot_epoch(s);
+          if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) { rc = kAgain; break; }
+          ast8(s + kOffType, (uint8_t)arg);
+          drain();
+          aadd64(epoch_ptr(s), 1);
+          ++muts;
+          mark_dirty(a, idx);
+          break;
+        }
+        case 10: ast64((uint64_t*)(s + kOffCtime), arg); break;
+        case 11: ast64((uint64_t*)(s + kOffAtime), arg); break;
+        case 12: o = (uint64_t)idx; break;
+        default: rc = kInval;
+      }
+    }
+    if (out) out[i] = o;
+    if (status) status[i] = rc;
+  }
+  flush_stats(a, st, nullptr, muts);
+}
+
+// ------------------------------------------------------ embeddings ------
+// One wave per key: the 3072-B vector moves as 64 lanes x 3 x 16 B.
+__global__ __launch_bounds__(kBlock) void k_embed_set(spl_arena_t aa, const char* keys, int kstride,
+                                                      const float* vecs, long n, int32_t* status) {
+  const Arena a = to_dev(aa);
+  const int lane = threadIdx.x & 63;
+  const long wave = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  uint64_t muts = 0;
+  Stats st;
+  for (long i = wave; i < n; i += nwaves) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    long idx = find(a, k);
+    int32_t rc = kOk;
+    uint8_t* s = idx >= 0 ? a.slot((size_t)idx) : nullptr;
+    if (idx < 0) rc = kNoEnt;
+    else if (a.stride != kSlotEmbedBytes) rc = kInval;
+    bool locked = false;
+    if (rc == kOk && lane == 0) {
+      const uint64_t e = slot_epoch(s);
+      locked = !(e & 1) && acas64(epoch_ptr(s), e, e + 1);
+    }
+    locked = __shfl(locked, 0, 64);
+    if (rc == kOk && !locked) rc = kAgain;
+    if (rc == kOk) {
+      const uint4* src = (const uint4*)(vecs + i * (long)kEmbedDim);
+      uint4* dst = (uint4*)(s + kOffEmbed);
+#pragma unroll
+      for (int c = 0; c < 3; ++c) dst[lane + 64 * c] = src[lane + 64 * c];
+      release();
+      __builtin_amdgcn_wave_barrier();
+      if (lane == 0) {
+        aadd64(epoch_ptr(s), 1);
+        mark_dirty(a, (size_t)idx);
+      }
+      ++muts;
+    }
+    if (status && lane == 0) status[i] = rc;
+  }
+  if (lane != 0) muts = 0;
+  flush_stats(a, st, nullptr, muts);
+}
+
+__global__ __launch_bounds__(kBlock) void k_embed_get(spl_arena_t aa, const char* keys, int kstride, float* vecs,
+                                                      long n, int32_t* status) {
+  const Arena a = to_dev(aa);
+  const int lane = threadIdx.x & 63;
+  const long wave = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
+  const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long i = wave; i < n; i += nwaves) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    long idx = find(a, k);
+    int32_t rc = kOk;
+    if (idx < 0) rc = kNoEnt;
+    else if (a.stride != kSlotEmbedBytes) rc = kInval;
+    if (rc == kOk) {
+      const uint8_t* s = a.slot((size_t)idx);
+      const uint64_t e1 = ald64_acq(s + kOffEpoch);
+      if (e1 & 1) {
+        rc = kAgain;
+      } else {
+        const uint4* src = (const uint4*)(s + kOffEmbed);
+        uint4* dst = (uint4*)(vecs + i * (long)kEmbedDim);
+#pragma unroll
+        for (int c = 0; c < 3; ++c) dst[lane + 64 * c] = src[lane + 64 * c];
+        drain();
+        if (slot_epoch(s) != e1) rc = kAgain;
+      }
+    }
+    if (status && lane == 0) status[i] = rc;
+  }
+}
+
+// ------------------------------------------------------------- scans ----
+// mode 0: list (hash != 0 && val_len > 0); mode 1: enumerate ((bloom&mask)==mask)
+// mode 2: embedded (hash != 0 and vector not all-zero)  mode 3: occupied (hash != 0)
+// Compacts matching slot indices with one atomic per wave (ballot + mbcnt).
+__global__ __launch_bounds__(kBlock) void k_scan(spl_arena_t aa, int mode, uint64_t mask, uint32_t* out_idx,
+                                                 uint64_t* out_epoch, uint32_t cap, uint32_t* counter) {
+  const Arena a = to_dev(aa);
+  const int lane = threadIdx.x & 63;
+  for (size_t base = blockIdx.x * (size_t)blockDim.x; base < a.slots; base += (size_t)gridDim.x * blockDim.x) {
+    const size_t i = base + threadIdx.x;  // base is block-uniform: every lane reaches the ballot
+    bool hit = false;
+    uint64_t ep = 0;
+    if (i < a.slots) {
+      const uint8_t* s = a.slot(i);
+      const uint64_t h = slot_hash(s);
+      if (h != 0) {
+        ep = slot_epoch(s);
+        if (mode == 0) hit = ald32((const uint32_t*)(s + kOffValLen)) > 0;
+        else if (mode == 1) hit = (ald64((const uint64_t*)(s + kOffBloom)) & mask) == mask;
+        else if (mode == 3) hit = true;
+        else if (a.stride == kSlotEmbedBytes) {
+          const uint32_t* v = (const uint32_t*)(s + kOffEmbed);
+          for (int d = 0; d < (int)kEmbedDim && !hit; ++d) hit = (v[d] & 0x7fffffffu) != 0;
+        }
+      }
+    }
+    const uint64_t bal = __ballot(hit);
+    if (bal) {
+      uint32_t basepos = 0;
+      if (lane == 0) basepos = atomicAdd(counter, (uint32_t)__popcll(bal));
+      basepos = __shfl(basepos, 0, 64);
+      if (hit) {
+        const uint32_t pos = basepos + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+        if (pos < cap) {
+          out_idx[pos] = (uint32_t)i;
+          if (out_epoch) out_epoch[pos] = ep;
+        }
+      }
+    }
+  }
+}
+
+__global__ void k_purge(spl_arena_t aa) {
+  const Arena a = to_dev(aa);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < a.slots; i += (size_t)gridDim.x * blockDim.x) {
+    uint8_t* s = a.slot(i);
+    const uint64_t e = slot_epoch(s);
+    if (e & 1) continue;
+    const uint64_t h = slot_hash(s);
+    if (h == 0 && e == 0) continue;
+    if (!acas64(epoch_ptr(s), e, e + 1)) continue;
+    const uint32_t len = h == 0 ? 0 : ald32((const uint32_t*)(s + kOffValLen));
+    uint8_t* v = a.value(i);
+    uint32_t c = len;
+    for (; c < a.max_val && (c & 15); ++c) v[c] = 0;
+    for (; c + 16 <= a.max_val; c += 16) *(uint4*)(v + c) = make_uint4(0, 0, 0, 0);
+    for (; c < a.max_val; ++c) v[c] = 0;
+    release();
+    aadd64(epoch_ptr(s), 1);
+  }
+}
+
+// Gather slot metadata + keys for a list of slot indices (host list/snapshot).
+__global__ void k_gather_slots(spl_arena_t aa, const uint32_t* idx, long n, uint8_t* out_core) {
+  const Arena a = to_dev(aa);
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    const uint8_t* s = a.slot(idx[i]);
+    for (int c = 0; c < 16; ++c) *(uint64_t*)(out_core + i * 128 + 8 * c) = ald64(s + 8 * c);
+  }
+}
+
+// FNV-1a of canonical key records (shard routing, C1 of SURVEY §2.10).
+__global__ void k_hash_keys(const char* keys, int kstride, long n, uint64_t* out) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    Key k;
+    load_key(k, keys + i * (long)kstride, kstride);
+    out[i] = k.hash;
+  }
+}
+
+// Bench/tool helper: key i of a batch = printf("%s%0*llu", prefix, width, ids[i])
+// written NUL-padded into kstride-byte records.  Not on any timed path.
+__global__ void k_format_keys(char* out, int kstride, const uint64_t* ids, uint64_t first, long n, const char* prefix,
+                              int plen, int width) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    char* r = out + i * (long)kstride;
+    uint64_t v = ids ? ids[i] : first + (uint64_t)i;
+    int p = 0;
+    for (; p < plen && p < kstride - 1; ++p) r[p] = prefix[p];
+    char digits[24];
+    int nd = 0;
+    do { digits[nd++] = (char)('0' + v % 10); v /= 10; } while (v && nd < 20);
+    while (nd < width && nd < 20) digits[nd++] = '0';
+    for (int d = nd - 1; d >= 0 && p < kstride - 1; --d) r[p++] = digits[d];
+    for (; p < kstride; ++p) r[p] = 0;
+  }
+}
+
+// Bench helper: value i = "ver:<ver>|id:<id>|data:" + fill bytes to `len`.
+__global__ void k_format_values(uint8_t* out, int vstride, uint32_t* lens, const uint64_t* ids, uint64_t first,
+                                long n, uint32_t ver, uint32_t len) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    uint8_t* r = out + i * (long)vstride;
+    const uint64_t id = ids ? ids[i] : first + (uint64_t)i;
+    char tmp[64];
+    int p = 0;
+    const char* a = "ver:";
+    for (int q = 0; a[q]; ++q) tmp[p++] = a[q];
+    char d[24];
+    int nd = 0;
+    uint32_t v = ver;
+    do { d[nd++] = (char)('0' + v % 10); v /= 10; } while (v);
+    while (nd) tmp[p++] = d[--nd];
+    const char* b = "|id:";
+    for (int q = 0; b[q]; ++q) tmp[p++] = b[q];
+    uint64_t w = id;
+    do { d[nd++] = (char)('0' + w % 10); w /= 10; } while (w);
+    while (nd) tmp[p++] = d[--nd];
+    const char* c = "|data:";
+    for (int q = 0; c[q]; ++q) tmp[p++] = c[q];
+    uint32_t L = len < (uint32_t)vstride ? len : (uint32_t)vstride;
+    for (uint32_t q = 0; q < L; ++q) r[q] = q < (uint32_t)p ? (uint8_t)tmp[q] : (uint8_t)('A' + ver % 26);
+    for (uint32_t q = L; q < (uint32_t)vstride; ++q) r[q] = 0;
+    if (lens) lens[i] = L;
+  }
+}
+
+}  // namespace
+
+// ====================================================== C launchers ======
+extern "C" {
+
+int spl_arena_init_slots(spl_arena_t a, hipStream_t s) {
+  hipLaunchKernelGGL(k_init_slots, dim3(grid_for(a.slots)), dim3(kBlock), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
+                  long n, int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_set, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n, status,
+                     max_retry, stats);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
+                  int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_get, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
+                     status, max_retry, stats);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_unset(spl_arena_t a, const char* keys, int kstride, long n, int32_t* status, int max_retry,
+                    hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_unset, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, n, status, max_retry);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_intop(spl_arena_t a, const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,
+                    int32_t* status, uint64_t* results, int max_retry, hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_intop, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, ops, masks, n, status, results,
+                     max_retry);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_meta(spl_arena_t a, const char* keys, int kstride, int op, const uint64_t* args, long n, int32_t* status,
+                   uint64_t* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_meta, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, op, args, n, status, out);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_embed_set(spl_arena_t a, const char* keys, int kstride, const float* vecs, long n, int32_t* status,
+                        hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_embed_set, dim3(grid_for(n * 64)), dim3(kBlock), 0, s, a, keys, kstride, vecs, n, status);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_embed_get(spl_arena_t a, const char* keys, int kstride, float* vecs, long n, int32_t* status,
+                        hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_embed_get, dim3(grid_for(n * 64)), dim3(kBlock), 0, s, a, keys, kstride, vecs, n, status);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_scan(spl_arena_t a, int mode, uint64_t mask, uint32_t* out_idx, uint64_t* out_epoch, uint32_t cap,
+                   uint32_t* counter, hipStream_t s) {
+  hipLaunchKernelGGL(k_scan, dim3(grid_for(a.slots)), dim3(kBlock), 0, s, a, mode, mask, out_idx, out_epoch, cap,
+                     counter);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_purge(spl_arena_t a, hipStream_t s) {
+  hipLaunchKernelGGL(k_purge, dim3(grid_for(a.slots)), dim3(kBlock), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int spl_arena_gather_slots(spl_arena_t a, const uint32_t* idx, long n, uint8_t* out_core, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_gather_slots, dim3(grid_for(n)), dim3(kBlock), 0, s, a, idx, n, out_core);
+  return (int)hipGetLastError();
+}
+
+int spl_hash_keys(const char* keys, int kstride, long n, uint64_t* out, hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_hash_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, keys, kstride, n, out);
+  return (int)hipGetLastError();
+}
+
+int spl_format_keys(char* out, int kstride, const uint64_t* ids, uint64_t first, long n, const char* prefix_dev,
+                    int plen, int width, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_format_keys, dim3(grid_for(n)), dim3(kBlock), 0, s, out, kstride, ids, first, n, prefix_dev,
+                     plen, width);
+  return (int)hipGetLastError();
+}
+
+int spl_format_values(uint8_t* out, int vstride, uint32_t* lens, const uint64_t* ids, uint64_t first, long n,
+                      uint32_t ver, uint32_t len, hipStream_t s) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(k_format_values, dim3(grid_for(n)), dim3(kBlock), 0, s, out, vstride, lens, ids, first, n, ver,
+                     len);
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,770 @@
+// hbm_store.hip — the HBM backend: a format-v4 arena resident in MI355X HBM.
+//
+// Data plane (header counters, slots, values, vectors) lives in device memory
+// and is mutated only by the kernels of arena_kernels.hip (owner computes).
+// Control plane lives in a POSIX shm descriptor "<name>.hbm":
+//   - geometry, device ordinal, owner pid and a hipIpcMemHandle_t, so any
+//     process on the node can hipIpcOpenMemHandle() the same arena zero-copy;
+//   - a host-resident splinter_header mirror carrying the shard bid table and
+//     the event-bus owner (host atomics; shard election is host logic).
+// The single-op StoreBase API runs each call as a one-element batch (H2D
+// record, kernel, D2H status) on a private stream: microseconds per call.
+// Bulk work goes through the batch launchers (arena_api.h) directly.
+#include <hip/hip_runtime.h>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fcntl.h>
+#include <mutex>
+#include <poll.h>
+#include <string>
+#include <sys/eventfd.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+#include <vector>
+
+#include "arena_api.h"
+#include "splinter_ext.h"
+#include "splinter_store.hpp"
+#include "store_host.hpp"
+
+namespace spl {
+
+namespace {
+
+constexpr uint32_t kDescMagic = 0x48424d41;  // "HBMA"
+constexpr size_t kAlignOffset = 64;          // base % 128 == 64 -> every 128-B slot is line aligned
+
+struct HbmDescriptor {
+  uint32_t magic;
+  uint32_t version;
+  uint32_t slots, max_val, stride, device;
+  uint64_t total_bytes;
+  uint64_t base_offset;
+  int32_t owner_pid;
+  int32_t pad;
+  hipIpcMemHandle_t handle;
+  alignas(64) splinter_header control;  // host control plane (shard bids, event bus owner)
+};
+
+#define HIPCHECK(x)                                                             \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "libsplinter_hip: %s failed: %s\n", #x, hipGetErrorString(e_)); \
+      return -1;                                                                \
+    }                                                                           \
+  } while (0)
+
+int neg_to_errno(int32_t st) {
+  switch (st) {
+    case -11: return EAGAIN;
+    case -2: return ENOENT;
+    case -28: return ENOSPC;
+    case -90: return EMSGSIZE;
+    case -71: return EPROTOTYPE;
+    default: return EINVAL;
+  }
+}
+
+}  // namespace
+
+class HbmStore final : public StoreBase {
+ public:
+  static HbmStore* create(const char* name, size_t slots, size_t max_val, bool emb, int* err);
+  static HbmStore* open(const char* name, int* err);
+  ~HbmStore() override;
+
+  const char* backend() const override { return "hbm"; }
+  Geometry geometry() const override { return geo_; }
+  splinter_header* header_ptr() override { return &desc_->control; }
+  spl_arena_t arena() const {
+    spl_arena_t a;
+    a.base = dbase_;
+    a.slots = geo_.slots;
+    a.max_val = geo_.max_val;
+    a.stride = geo_.stride;
+    a.flags = event_fd_ >= 0 ? 1u : 0u;
+    return a;
+  }
+  hipStream_t stream() const { return stream_; }
+
+  int set_mop(unsigned mode) override {
+    uint8_t f = config_get();
+    switch (mode) {
+      case 0: f &= (uint8_t)~(SPL_SYS_AUTO_SCRUB | SPL_SYS_HYBRID_SCRUB); break;
+      case 1: f |= SPL_SYS_AUTO_SCRUB | SPL_SYS_HYBRID_SCRUB; break;
+      case 2: f |= SPL_SYS_AUTO_SCRUB; break;
+      default: errno = EOPNOTSUPP; return -1;
+    }
+    return put_field(offsetof(splinter_header, core_flags), &f, 1);
+  }
+  int get_mop() override {
+    uint8_t f = config_get();
+    if (f & SPL_SYS_HYBRID_SCRUB) return 1;
+    if (f & SPL_SYS_AUTO_SCRUB) return 2;
+    return 0;
+  }
+  void purge() override {
+    std::lock_guard<std::mutex> lk(mu_);
+    spl_arena_purge(arena(), stream_);
+    (void)hipStreamSynchronize(stream_);
+  }
+  int header_snapshot(splinter_header_snapshot_t* o) override {
+    if (!o) return -2;
+    splinter_header h;
+    if (get_field(0, &h, 64) != 0) return -1;
+    o->magic = h.magic; o->version = h.version; o->slots = h.slots; o->max_val_sz = h.max_val_sz;
+    o->epoch = h.epoch; o->core_flags = h.core_flags; o->user_flags = h.user_flags;
+    o->parse_failures = h.parse_failures; o->last_failure_epoch = h.last_failure_epoch;
+    return 0;
+  }
+  uint8_t config_get() override {
+    uint8_t f = 0;
+    get_field(offsetof(splinter_header, core_flags), &f, 1);
+    return f;
+  }
+  void config_or(uint8_t m) override { uint8_t f = config_get() | m; put_field(offsetof(splinter_header, core_flags), &f, 1); }
+  void config_and(uint8_t m) override { uint8_t f = config_get() & m; put_field(offsetof(splinter_header, core_flags), &f, 1); }
+
+  int set(const char* key, const void* val, size_t len) override {
+    if (!key) return -2;
+    if (len == 0 || len > geo_.max_val) { errno = len ? EMSGSIZE : EINVAL; return -1; }
+    if (!val) return -2;
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_key(key);
+    std::memset(h_val_, 0, (len + 15) & ~(size_t)15);
+    std::memcpy(h_val_, val, len);
+    uint32_t l = (uint32_t)len;
+    std::memcpy(h_u32_, &l, 4);
+    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
+    (void)hipMemcpyAsync(d_val_, h_val_, (len + 15) & ~(size_t)15, hipMemcpyHostToDevice, stream_);
+    (void)hipMemcpyAsync(d_u32_, h_u32_, 4, hipMemcpyHostToDevice, stream_);
+    spl_arena_set(arena(), d_key_, 64, (const uint8_t*)d_val_, (int)vstride_, (const uint32_t*)d_u32_, 1,
+                  (int32_t*)d_status_, 0, nullptr, stream_);
+    int32_t st = finish_status();
+    if (st == 0) notify_host();
+    return st_ret(st);
+  }
+  int unset(const char* key) override {
+    if (!key) return -2;
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_key(key);
+    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
+    spl_arena_unset(arena(), d_key_, 64, 1, (int32_t*)d_status_, 0, stream_);
+    int32_t st = finish_status();
+    if (st >= 0) return st;
+    errno = neg_to_errno(st);
+    return -1;
+  }
+  int get(const char* key, void* buf, size_t buf_sz, size_t* out_sz) override {
+    if (!key) return -2;
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_key(key);
+    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
+    spl_arena_get(arena(), d_key_, 64, (uint8_t*)d_val_, (int)vstride_, (uint32_t*)d_u32_, 1, (int32_t*)d_status_, 0,
+                  nullptr, stream_);
+    (void)hipMemcpyAsync(h_u32_, d_u32_, 4, hipMemcpyDeviceToHost, stream_);
+    (void)hipMemcpyAsync(h_val_, d_val_, vstride_, hipMemcpyDeviceToHost, stream_);
+    int32_t st = finish_status();
+    if (st != 0) { errno = neg_to_errno(st); return -1; }
+    uint32_t len;
+    std::memcpy(&len, h_u32_, 4);
+    if (out_sz) *out_sz = len;
+    if (buf) {
+      if (buf_sz < len) { errno = EMSGSIZE; return -1; }
+      std::memcpy(buf, h_val_, len);
+    }
+    return 0;
+  }
+  int list(char** out, size_t max, size_t* cnt) override {
+    if (!out || !cnt) return -2;
+    std::vector<uint32_t> idx;
+    std::vector<uint64_t> ep;
+    scan(SPL_SCAN_LIST, 0, idx, ep);
+    fetch_cores(idx);
+    size_t c = 0;
+    for (size_t i = 0; i < idx.size() && c < max; ++i) out[c++] = (char*)(list_cache_.data() + i * 128 + kOffKey);
+    *cnt = c;
+    return 0;
+  }
+  int poll(const char* key, uint64_t timeout_ms) override {
+    uint64_t start = epoch_of(key);
+    if (start == 0) return -1;
+    if (start & 1) { errno = EAGAIN; return -1; }
+    timespec t0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (;;) {
+      uint64_t cur = epoch_of(key);
+      if (!(cur & 1) && cur != start) return 0;
+      timespec t;
+      clock_gettime(CLOCK_MONOTONIC, &t);
+      uint64_t el = (uint64_t)(t.tv_sec - t0.tv_sec) * 1000 + (uint64_t)((t.tv_nsec - t0.tv_nsec) / 1000000);
+      if (el >= timeout_ms) { errno = ETIMEDOUT; return -1; }
+      usleep(1000);
+    }
+  }
+  int slot_snapshot(const char* key, splinter_slot_snapshot_t* o) override {
+    if (!key || !o) return -2;
+    long i = find_idx(key);
+    if (i < 0) return -1;
+    std::vector<uint32_t> idx{(uint32_t)i};
+    fetch_cores(idx);
+    const uint8_t* c = list_cache_.data();
+    std::memcpy(&o->hash, c + kOffHash, 8);
+    std::memcpy(&o->epoch, c + kOffEpoch, 8);
+    std::memcpy(&o->val_off, c + kOffValOff, 4);
+    std::memcpy(&o->val_len, c + kOffValLen, 4);
+    o->type_flag = c[kOffType];
+    o->user_flag = c[kOffUser];
+    std::memcpy(&o->ctime, c + kOffCtime, 8);
+    std::memcpy(&o->atime, c + kOffAtime, 8);
+    std::memcpy(&o->bloom, c + kOffBloom, 8);
+    std::memcpy(o->key, c + kOffKey, kKeyMax);
+#ifdef SPLINTER_EMBEDDINGS
+    if (geo_.embeddings()) get_embedding(key, o->embedding);
+    else std::memset(o->embedding, 0, kEmbedBytes);
+#endif
+    return 0;
+  }
+  int append(const char* key, const void* data, size_t len, size_t* new_len) override {
+    // read-modify-write through the seqlocked set path (owner computes)
+    if (!key || !data || len == 0) return -2;
+    std::vector<uint8_t> cur(geo_.max_val);
+    size_t n = 0;
+    if (get(key, cur.data(), cur.size(), &n) != 0) return -1;
+    if (n + len > geo_.max_val) { errno = EMSGSIZE; return -1; }
+    std::memcpy(cur.data() + n, data, len);
+    if (set(key, cur.data(), n + len) != 0) return -1;
+    if (new_len) *new_len = n + len;
+    return 0;
+  }
+  const void* raw_ptr(const char* key, size_t* out_sz, uint64_t* out_epoch) override {
+    // HBM values are not host mapped: return a host snapshot (thread-local).
+    thread_local std::vector<uint8_t> snap;
+    snap.resize(geo_.max_val + 1);
+    size_t n = 0;
+    uint64_t e = epoch_of(key);
+    if (get(key, snap.data(), geo_.max_val, &n) != 0) return nullptr;
+    snap[n] = 0;
+    if (out_sz) *out_sz = n;
+    if (out_epoch) *out_epoch = e;
+    return snap.data();
+  }
+  uint64_t epoch_of(const char* key) override {
+    uint64_t out = 0;
+    int32_t st = meta(key, SPL_META_GET_EPOCH, 0, &out);
+    return st == 0 ? out : 0;
+  }
+  int set_as_system(const char* key) override { return meta_ret(meta(key, SPL_META_SET_SYSTEM, 0, nullptr)); }
+
+  int set_embedding(const char* key, const float* vec) override {
+    if (!key || !vec) return -2;
+    if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_key(key);
+    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
+    (void)hipMemcpyAsync(d_vec_, vec, kEmbedBytes, hipMemcpyHostToDevice, stream_);
+    spl_arena_embed_set(arena(), d_key_, 64, (const float*)d_vec_, 1, (int32_t*)d_status_, stream_);
+    int32_t st = finish_status();
+    if (st == 0) notify_host();
+    return st_ret(st);
+  }
+  int get_embedding(const char* key, float* out) override {
+    if (!key || !out) return -2;
+    if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_key(key);
+    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
+    spl_arena_embed_get(arena(), d_key_, 64, (float*)d_vec_, 1, (int32_t*)d_status_, stream_);
+    (void)hipMemcpyAsync(out, d_vec_, kEmbedBytes, hipMemcpyDeviceToHost, stream_);
+    return st_ret(finish_status());
+  }
+
+  int set_named_type(const char* key, uint16_t mask) override {
+    if (!key) return -2;
+    if (mask & SPL_SLOT_TYPE_BIGUINT) {  // promotion: parse on the host, write back as u64
+      std::vector<uint8_t> v(geo_.max_val + 1, 0);
+      size_t n = 0;
+      if (get(key, v.data(), geo_.max_val, &n) != 0) return -1;
+      if (n < 8) {
+        uint64_t x = 0;
+        if (n > 0 && v[0] >= '0' && v[0] <= '9') {
+          char tmp[16] = {0};
+          std::memcpy(tmp, v.data(), n < 15 ? n : 15);
+          x = strtoull(tmp, nullptr, 0);
+        } else {
+          std::memcpy(&x, v.data(), n);
+        }
+        if (set(key, &x, 8) != 0) return -1;
+      }
+    }
+    return meta_ret(meta(key, SPL_META_SET_TYPE, mask, nullptr));
+  }
+  int set_slot_time(const char* key, unsigned short mode, uint64_t epoch, size_t offset) override {
+    if (mode != SPL_TIME_CTIME && mode != SPL_TIME_ATIME) { errno = ENOTSUP; return -2; }
+    return meta_ret(meta(key, mode == SPL_TIME_CTIME ? SPL_META_SET_CTIME : SPL_META_SET_ATIME, epoch - offset, nullptr));
+  }
+  int integer_op(const char* key, splinter_integer_op_t op, const void* mask) override {
+    if (!key) return -2;
+    uint64_t m = 0;
+    if (mask) std::memcpy(&m, mask, 8);
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_key(key);
+    int o = (int)op;
+    std::memcpy(h_val_, &o, 4);
+    std::memcpy(h_val_ + 16, &m, 8);
+    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
+    (void)hipMemcpyAsync(d_val_, h_val_, 32, hipMemcpyHostToDevice, stream_);
+    spl_arena_intop(arena(), d_key_, 64, (const int*)d_val_, (const uint64_t*)((uint8_t*)d_val_ + 16), 1,
+                    (int32_t*)d_status_, nullptr, 0, stream_);
+    int32_t st = finish_status();
+    if (st == 0) notify_host();
+    return st_ret(st);
+  }
+
+  int bump(const char* key) override { return meta_ret(meta(key, SPL_META_BUMP, 0, nullptr)); }
+  int retrain(const char* key) override { return meta_ret(meta(key, SPL_META_RETRAIN, 0, nullptr)); }
+  int set_label(const char* key, uint64_t m) override { return meta_ret(meta(key, SPL_META_SET_LABEL, m, nullptr)); }
+  int unset_label(const char* key, uint64_t m) override { return meta_ret(meta(key, SPL_META_UNSET_LABEL, m, nullptr)); }
+
+  int watch_register(const char* key, uint8_t g) override {
+    if (g >= SPLINTER_MAX_GROUPS) { errno = EINVAL; return -2; }
+    return meta_ret(meta(key, SPL_META_WATCH_REG, g, nullptr));
+  }
+  int watch_unregister(const char* key, uint8_t g) override {
+    if (g >= SPLINTER_MAX_GROUPS) return -2;
+    return meta_ret(meta(key, SPL_META_WATCH_UNREG, g, nullptr));
+  }
+  int watch_label_register(uint64_t mask, uint8_t g) override {
+    if (g >= SPLINTER_MAX_GROUPS) return -2;
+    uint8_t w[64];
+    get_field(offsetof(splinter_header, bloom_watches), w, 64);
+    for (uint64_t m = mask; m; m &= m - 1) w[__builtin_ctzll(m)] = g;
+    return put_field(offsetof(splinter_header, bloom_watches), w, 64);
+  }
+  int pulse_keygroup(const char* key) override { return meta_ret(meta(key, SPL_META_PULSE, 0, nullptr)); }
+  void pulse_slot(splinter_slot*) override {}  // slots are not host mapped
+  uint64_t signal_count(uint8_t g) override {
+    if (g >= SPLINTER_MAX_GROUPS) return 0;
+    uint64_t v = 0;
+    get_field(offsetof(splinter_header, signal_groups) + 64 * (size_t)g, &v, 8);
+    return v;
+  }
+  void enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) override {
+    if (!cb) return;
+    std::vector<uint32_t> idx;
+    std::vector<uint64_t> ep;
+    scan(SPL_SCAN_LABELS, mask, idx, ep);
+    fetch_cores(idx);
+    for (size_t i = 0; i < idx.size(); ++i) cb((const char*)(list_cache_.data() + i * 128 + kOffKey), ep[i], ud);
+  }
+
+  int event_bus_init() override {
+    int fd = eventfd(0, EFD_CLOEXEC);
+    if (fd < 0) return -1;
+    if (event_fd_ >= 0) close(event_fd_);
+    event_fd_ = fd;
+    __atomic_store_n(&desc_->control.event_bus.owner_fd, fd, __ATOMIC_RELEASE);
+    __atomic_store_n(&desc_->control.event_bus.owner_pid, (int32_t)getpid(), __ATOMIC_RELEASE);
+    return 0;
+  }
+  int event_bus_open() override {
+    const int32_t fd = __atomic_load_n(&desc_->control.event_bus.owner_fd, __ATOMIC_ACQUIRE);
+    const int32_t pid = __atomic_load_n(&desc_->control.event_bus.owner_pid, __ATOMIC_ACQUIRE);
+    if (fd < 0 || pid <= 0) { errno = ENODEV; return -1; }
+    if ((pid_t)pid == getpid()) return dup(fd);
+#if defined(SYS_pidfd_open) && defined(SYS_pidfd_getfd)
+    int pfd = (int)syscall(SYS_pidfd_open, (pid_t)pid, 0);
+    if (pfd < 0) return -1;
+    int r = (int)syscall(SYS_pidfd_getfd, pfd, fd, 0);
+    close(pfd);
+    return r;
+#else
+    errno = ENOSYS;
+    return -1;
+#endif
+  }
+  void event_bus_dirty(uint64_t* out, size_t words) override {
+    if (!out) return;
+    const size_t n = words < SPLINTER_EVENT_BUS_MASK_WORDS ? words : SPLINTER_EVENT_BUS_MASK_WORDS;
+    get_field(offsetof(splinter_header, event_bus), out, n * 8);
+  }
+
+  int shard_claim_ex(uint32_t id, uint32_t pid, uint8_t it, uint8_t pr, uint64_t dur, uint64_t at) override {
+    return shard_claim_on(&desc_->control, id, pid, it, pr, dur, at);
+  }
+  int shard_rebid(uint32_t id, uint8_t it, uint8_t pr, uint64_t dur) override {
+    return shard_rebid_on(&desc_->control, id, it, pr, dur);
+  }
+  int shard_release(uint32_t id) override { return shard_release_on(&desc_->control, id); }
+  uint32_t shard_election(uint8_t* out_intent) override { return shard_election_on(&desc_->control, out_intent); }
+  int shard_table(splinter_shard_bid_snapshot* out, size_t max) override { return shard_table_on(&desc_->control, out, max); }
+  int madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t timeout) override {
+    // Election as on the host backend; the advice maps to a residency hint on
+    // the HBM range (coarse-grained hipMalloc memory: a documented no-op).
+    (void)addr; (void)len; (void)advice;
+    if (id == 0 || !shard_present_on(&desc_->control, id)) { errno = EINVAL; return -2; }
+    const uint64_t deadline = now_ticks() + timeout;
+    for (;;) {
+      if (shard_election_on(&desc_->control, nullptr) == id) return 0;
+      if (timeout == 0) { errno = EAGAIN; return -1; }
+      if (timeout != UINT64_MAX && now_ticks() >= deadline) { errno = ETIMEDOUT; return -1; }
+      usleep(5000);
+    }
+  }
+
+  // ---------------------------------------------------- bulk / helpers --
+  int checkpoint(const char* path);
+  int restore_from(const char* path);
+
+ private:
+  HbmStore() = default;
+  int setup_buffers();
+  void stage_key(const char* key) {
+    KeyRef k(key);
+    std::memcpy(h_key_, k.buf, 64);
+  }
+  int32_t finish_status() {
+    (void)hipMemcpyAsync(h_status_, d_status_, 4, hipMemcpyDeviceToHost, stream_);
+    (void)hipStreamSynchronize(stream_);
+    int32_t st;
+    std::memcpy(&st, h_status_, 4);
+    return st;
+  }
+  static int st_ret(int32_t st) {
+    if (st == 0) return 0;
+    errno = neg_to_errno(st);
+    return st == -2 ? -1 : -1;
+  }
+  static int meta_ret(int32_t st) { return st_ret(st); }
+  int32_t meta(const char* key, int op, uint64_t arg, uint64_t* out) {
+    if (!key) return -22;
+    std::lock_guard<std::mutex> lk(mu_);
+    stage_key(key);
+    std::memcpy(h_val_, &arg, 8);
+    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
+    (void)hipMemcpyAsync(d_val_, h_val_, 8, hipMemcpyHostToDevice, stream_);
+    spl_arena_meta(arena(), d_key_, 64, op, (const uint64_t*)d_val_, 1, (int32_t*)d_status_,
+                   (uint64_t*)((uint8_t*)d_val_ + 64), stream_);
+    if (out) (void)hipMemcpyAsync(h_val_ + 64, (uint8_t*)d_val_ + 64, 8, hipMemcpyDeviceToHost, stream_);
+    int32_t st = finish_status();
+    if (out) std::memcpy(out, h_val_ + 64, 8);
+    const bool mut = op == SPL_META_SET_LABEL || op == SPL_META_UNSET_LABEL || op == SPL_META_RETRAIN ||
+                     op == SPL_META_SET_TYPE;
+    if (st == 0 && mut) notify_host();
+    return st;
+  }
+  long find_idx(const char* key) {
+    uint64_t out = 0;
+    return meta(key, SPL_META_FIND, 0, &out) == 0 ? (long)out : -1;
+  }
+  void scan(int mode, uint64_t mask, std::vector<uint32_t>& idx, std::vector<uint64_t>& ep) {
+    std::lock_guard<std::mutex> lk(mu_);
+    uint32_t* d_cnt;
+    uint32_t* d_idx;
+    uint64_t* d_ep;
+    const uint32_t cap = geo_.slots;
+    (void)hipMallocAsync((void**)&d_cnt, 4, stream_);
+    (void)hipMallocAsync((void**)&d_idx, (size_t)cap * 4, stream_);
+    (void)hipMallocAsync((void**)&d_ep, (size_t)cap * 8, stream_);
+    (void)hipMemsetAsync(d_cnt, 0, 4, stream_);
+    spl_arena_scan(arena(), mode, mask, d_idx, d_ep, cap, d_cnt, stream_);
+    uint32_t n = 0;
+    (void)hipMemcpyAsync(&n, d_cnt, 4, hipMemcpyDeviceToHost, stream_);
+    (void)hipStreamSynchronize(stream_);
+    if (n > cap) n = cap;
+    idx.resize(n);
+    ep.resize(n);
+    if (n) {
+      (void)hipMemcpyAsync(idx.data(), d_idx, (size_t)n * 4, hipMemcpyDeviceToHost, stream_);
+      (void)hipMemcpyAsync(ep.data(), d_ep, (size_t)n * 8, hipMemcpyDeviceToHost, stream_);
+    }
+    (void)hipFreeAsync(d_cnt, stream_);
+    (void)hipFreeAsync(d_idx, stream_);
+    (void)hipFreeAsync(d_ep, stream_);
+    (void)hipStreamSynchronize(stream_);
+  }
+  void fetch_cores(const std::vector<uint32_t>& idx) {
+    std::lock_guard<std::mutex> lk(mu_);
+    list_cache_.assign(idx.size() * 128, 0);
+    if (idx.empty()) return;
+    uint32_t* d_idx;
+    uint8_t* d_out;
+    (void)hipMallocAsync((void**)&d_idx, idx.size() * 4, stream_);
+    (void)hipMallocAsync((void**)&d_out, idx.size() * 128, stream_);
+    (void)hipMemcpyAsync(d_idx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, stream_);
+    spl_arena_gather_slots(arena(), d_idx, (long)idx.size(), d_out, stream_);
+    (void)hipMemcpyAsync(list_cache_.data(), d_out, idx.size() * 128, hipMemcpyDeviceToHost, stream_);
+    (void)hipFreeAsync(d_idx, stream_);
+    (void)hipFreeAsync(d_out, stream_);
+    (void)hipStreamSynchronize(stream_);
+  }
+  int get_field(size_t off, void* dst, size_t n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (hipMemcpyAsync(h_val_, (uint8_t*)dbase_ + off, n, hipMemcpyDeviceToHost, stream_) != hipSuccess) return -1;
+    (void)hipStreamSynchronize(stream_);
+    std::memcpy(dst, h_val_, n);
+    return 0;
+  }
+  int put_field(size_t off, const void* src, size_t n) {
+    std::lock_guard<std::mutex> lk(mu_);
+    std::memcpy(h_val_, src, n);
+    if (hipMemcpyAsync((uint8_t*)dbase_ + off, h_val_, n, hipMemcpyHostToDevice, stream_) != hipSuccess) return -1;
+    (void)hipStreamSynchronize(stream_);
+    return 0;
+  }
+  void notify_host() {
+    if (event_fd_ < 0) return;
+    uint64_t one = 1;
+    ssize_t w = write(event_fd_, &one, 8);
+    (void)w;
+  }
+
+  std::string name_;
+  Geometry geo_;
+  int device_ = 0;
+  bool owner_ = false;
+  void* raw_ = nullptr;    // hipMalloc / IPC base
+  void* dbase_ = nullptr;  // raw_ + kAlignOffset
+  HbmDescriptor* desc_ = nullptr;
+  hipStream_t stream_ = nullptr;
+  std::mutex mu_;
+  int event_fd_ = -1;
+  size_t vstride_ = 0;
+  // staging
+  char* h_key_ = nullptr;
+  uint8_t* h_val_ = nullptr;
+  uint8_t* h_u32_ = nullptr;
+  uint8_t* h_status_ = nullptr;
+  char* d_key_ = nullptr;
+  void* d_val_ = nullptr;
+  void* d_u32_ = nullptr;
+  void* d_status_ = nullptr;
+  void* d_vec_ = nullptr;
+  std::vector<uint8_t> list_cache_;
+
+  friend StoreBase* hbm_factory_impl(const char*, size_t, size_t, unsigned, int, int*);
+};
+
+int HbmStore::setup_buffers() {
+  HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  vstride_ = ((size_t)geo_.max_val + 15) & ~(size_t)15;
+  if (vstride_ < 128) vstride_ = 128;
+  HIPCHECK(hipHostMalloc((void**)&h_key_, 64));
+  HIPCHECK(hipHostMalloc((void**)&h_val_, vstride_ + 4096));
+  HIPCHECK(hipHostMalloc((void**)&h_u32_, 64));
+  HIPCHECK(hipHostMalloc((void**)&h_status_, 64));
+  HIPCHECK(hipMalloc((void**)&d_key_, 64));
+  HIPCHECK(hipMalloc(&d_val_, vstride_ + 4096));
+  HIPCHECK(hipMalloc(&d_u32_, 64));
+  HIPCHECK(hipMalloc(&d_status_, 64));
+  HIPCHECK(hipMalloc(&d_vec_, kEmbedBytes));
+  return 0;
+}
+
+static HbmDescriptor* map_descriptor(const std::string& name, bool create, int* err) {
+  const std::string dn = name + ".hbm";
+  int fd = create ? shm_open(dn.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0666)
+                  : shm_open(dn.c_str(), O_RDWR | O_CLOEXEC, 0666);
+  if (fd < 0) { *err = errno; return nullptr; }
+  if (create && ftruncate(fd, sizeof(HbmDescriptor)) != 0) { *err = errno; close(fd); return nullptr; }
+  void* p = mmap(nullptr, sizeof(HbmDescriptor), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) { *err = errno; return nullptr; }
+  return (HbmDescriptor*)p;
+}
+
+HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool emb, int* err) {
+  *err = 0;
+  if (slots == 0 || max_val == 0 || slots > UINT32_MAX || max_val > UINT32_MAX) { *err = ENOTSUP; return nullptr; }
+  auto* s = new HbmStore();
+  s->name_ = name;
+  s->geo_.slots = (uint32_t)slots;
+  s->geo_.max_val = (uint32_t)max_val;
+  s->geo_.stride = emb ? (uint32_t)kSlotEmbedBytes : (uint32_t)kSlotCoreBytes;
+  s->owner_ = true;
+  (void)hipGetDevice(&s->device_);
+  const size_t total = s->geo_.total_bytes();
+  if (hipMalloc(&s->raw_, total + 256) != hipSuccess) { *err = ENOMEM; delete s; return nullptr; }
+  s->dbase_ = (uint8_t*)s->raw_ + kAlignOffset;
+  s->desc_ = map_descriptor(name, true, err);
+  if (!s->desc_ || s->setup_buffers() != 0) { if (!*err) *err = EIO; delete s; return nullptr; }
+  // header image built on the host, then the slot array initialised on device
+  splinter_header h;
+  std::memset(&h, 0, sizeof h);
+  h.magic = kMagic;
+  h.version = kVersion;
+  h.slots = s->geo_.slots;
+  h.max_val_sz = s->geo_.max_val;
+  h.val_sz = (uint32_t)total;
+  h.alignment = s->geo_.stride;
+  h.epoch = 1;
+  h.core_flags = SPL_SYS_AUTO_SCRUB | SPL_SYS_HYBRID_SCRUB;
+  std::memset(h.bloom_watches, 0xFF, 64);
+  h.event_bus.owner_fd = -1;
+  (void)hipMemcpy(s->dbase_, &h, sizeof h, hipMemcpyHostToDevice);
+  (void)hipMemsetAsync((uint8_t*)s->dbase_ + kHeaderBytes + s->geo_.slots_bytes(), 0, s->geo_.values_bytes(), s->stream_);
+  if (s->geo_.embeddings())
+    (void)hipMemsetAsync((uint8_t*)s->dbase_ + kHeaderBytes, 0, s->geo_.slots_bytes(), s->stream_);
+  spl_arena_init_slots(s->arena(), s->stream_);
+  (void)hipStreamSynchronize(s->stream_);
+  HbmDescriptor* d = s->desc_;
+  std::memcpy(&d->control, &h, sizeof h);
+  d->slots = s->geo_.slots;
+  d->max_val = s->geo_.max_val;
+  d->stride = s->geo_.stride;
+  d->device = (uint32_t)s->device_;
+  d->total_bytes = total;
+  d->base_offset = kAlignOffset;
+  d->owner_pid = (int32_t)getpid();
+  if (hipIpcGetMemHandle(&d->handle, s->raw_) != hipSuccess) std::memset(&d->handle, 0, sizeof d->handle);
+  d->version = 1;
+  __atomic_store_n(&d->magic, kDescMagic, __ATOMIC_RELEASE);
+  return s;
+}
+
+HbmStore* HbmStore::open(const char* name, int* err) {
+  *err = 0;
+  HbmDescriptor* d = map_descriptor(name, false, err);
+  if (!d) return nullptr;
+  if (__atomic_load_n(&d->magic, __ATOMIC_ACQUIRE) != kDescMagic) {
+    munmap(d, sizeof(HbmDescriptor));
+    *err = EINVAL;
+    return nullptr;
+  }
+  auto* s = new HbmStore();
+  s->name_ = name;
+  s->desc_ = d;
+  s->geo_.slots = d->slots;
+  s->geo_.max_val = d->max_val;
+  s->geo_.stride = d->stride;
+  s->device_ = (int)d->device;
+  (void)hipSetDevice(s->device_);
+  if (hipIpcOpenMemHandle(&s->raw_, d->handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    *err = EACCES;
+    s->raw_ = nullptr;
+    delete s;
+    return nullptr;
+  }
+  s->dbase_ = (uint8_t*)s->raw_ + d->base_offset;
+  if (s->setup_buffers() != 0) { *err = EIO; delete s; return nullptr; }
+  return s;
+}
+
+HbmStore::~HbmStore() {
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  if (event_fd_ >= 0) close(event_fd_);
+  if (h_key_) (void)hipHostFree(h_key_);
+  if (h_val_) (void)hipHostFree(h_val_);
+  if (h_u32_) (void)hipHostFree(h_u32_);
+  if (h_status_) (void)hipHostFree(h_status_);
+  if (d_key_) (void)hipFree(d_key_);
+  if (d_val_) (void)hipFree(d_val_);
+  if (d_u32_) (void)hipFree(d_u32_);
+  if (d_status_) (void)hipFree(d_status_);
+  if (d_vec_) (void)hipFree(d_vec_);
+  if (raw_) {
+    if (owner_) (void)hipFree(raw_);
+    else (void)hipIpcCloseMemHandle(raw_);
+  }
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (desc_) {
+    if (owner_) __atomic_store_n(&desc_->magic, 0u, __ATOMIC_RELEASE);
+    munmap(desc_, sizeof(HbmDescriptor));
+    if (owner_) shm_unlink((name_ + ".hbm").c_str());
+  }
+}
+
+// Checkpoint: stream the device image into a v4 store file (byte-identical
+// layout, so the host backend — or the reference library — can open it).
+int HbmStore::checkpoint(const char* path) {
+  int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
+  if (fd < 0) return -1;
+  const size_t total = geo_.total_bytes();
+  const size_t chunk = 64ull << 20;
+  uint8_t* pin = nullptr;
+  if (hipHostMalloc((void**)&pin, chunk) != hipSuccess) { close(fd); return -1; }
+  (void)hipStreamSynchronize(stream_);
+  int rc = 0;
+  for (size_t off = 0; off < total && rc == 0; off += chunk) {
+    const size_t n = total - off < chunk ? total - off : chunk;
+    if (hipMemcpy(pin, (uint8_t*)dbase_ + off, n, hipMemcpyDeviceToHost) != hipSuccess) { rc = -1; break; }
+    if (off == 0) {  // the control plane (shard bids, event bus) is host-side
+      auto* h = (splinter_header*)pin;
+      std::memcpy(h->shard_bids, desc_->control.shard_bids, sizeof h->shard_bids);
+      h->event_bus.owner_fd = -1;
+      h->event_bus.owner_pid = 0;
+    }
+    if (pwrite(fd, pin, n, (off_t)off) != (ssize_t)n) rc = -1;
+  }
+  (void)hipHostFree(pin);
+  if (rc == 0) rc = fsync(fd);
+  close(fd);
+  return rc;
+}
+
+int HbmStore::restore_from(const char* path) {
+  int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -1;
+  struct stat sb;
+  if (fstat(fd, &sb) != 0 || (size_t)sb.st_size != geo_.total_bytes()) { close(fd); errno = EINVAL; return -1; }
+  const size_t total = geo_.total_bytes();
+  const size_t chunk = 64ull << 20;
+  uint8_t* pin = nullptr;
+  if (hipHostMalloc((void**)&pin, chunk) != hipSuccess) { close(fd); return -1; }
+  int rc = 0;
+  for (size_t off = 0; off < total && rc == 0; off += chunk) {
+    const size_t n = total - off < chunk ? total - off : chunk;
+    if (pread(fd, pin, n, (off_t)off) != (ssize_t)n) { rc = -1; break; }
+    if (off == 0) {
+      auto* h = (splinter_header*)pin;
+      if (h->magic != kMagic || h->version != kVersion || h->slots != geo_.slots || h->max_val_sz != geo_.max_val) {
+        rc = -1;
+        errno = EINVAL;
+        break;
+      }
+      std::memcpy(desc_->control.shard_bids, h->shard_bids, sizeof h->shard_bids);
+    }
+    if (hipMemcpy((uint8_t*)dbase_ + off, pin, n, hipMemcpyHostToDevice) != hipSuccess) rc = -1;
+  }
+  (void)hipHostFree(pin);
+  close(fd);
+  return rc;
+}
+
+StoreBase* hbm_factory_impl(const char* name, size_t slots, size_t max_val, unsigned flags, int create, int* err) {
+  if (create) return HbmStore::create(name, slots, max_val, (flags & kCreateEmbeddings) != 0, err);
+  return HbmStore::open(name, err);
+}
+
+}  // namespace spl
+
+extern "C" {
+
+spl::StoreBase* spl_hbm_factory(const char* name, size_t slots, size_t max_val, unsigned flags, int create, int* err) {
+  return spl::hbm_factory_impl(name, slots, max_val, flags, create, err);
+}
+
+// Arena descriptor of an open HBM store (for the batch launchers).
+int spl_hbm_arena(spl_store* h, spl_arena_t* out) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  if (!s || !out) return -2;
+  *out = s->arena();
+  return 0;
+}
+
+int spl_hbm_checkpoint(spl_store* h, const char* path) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  return s ? s->checkpoint(path) : -2;
+}
+
+int spl_hbm_restore(spl_store* h, const char* path) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  return s ? s->restore_from(path) : -2;
+}
+
+}  // extern "C"

@@ -1,0 +1,264 @@
+"""Batched GPU arena operations (torch tensors in, torch tensors out).
+
+Thin, checked wrappers over the gfx950 launchers in
+``csrc/hip/arena_kernels.hip`` (C API: ``csrc/include/arena_api.h``).  Kernels
+run on torch's current HIP stream, so they compose with torch ops, CUDA
+graphs and ``torch.distributed`` collectives.
+
+Key batches are uint8 tensors ``[n, kstride]`` (NUL padded, kstride in
+{16,32,48,64}); value batches are uint8 ``[n, vstride]`` plus int32 lengths.
+Per-op status codes: 0 ok, -11 EAGAIN, -2 ENOENT, -28 ENOSPC, -90 EMSGSIZE,
+-71 EPROTOTYPE, -22 EINVAL.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Iterable, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from ..store import Store
+
+OK, EAGAIN, ENOENT, ENOSPC, EMSGSIZE, EPROTOTYPE, EINVAL = 0, -11, -2, -28, -90, -71, -22
+META = {"set_label": 0, "unset_label": 1, "bump": 2, "epoch": 3, "watch": 4, "unwatch": 5, "pulse": 6,
+        "system": 7, "retrain": 8, "type": 9, "ctime": 10, "atime": 11, "find": 12}
+SCAN_LIST, SCAN_LABELS, SCAN_EMBEDDED, SCAN_OCCUPIED = 0, 1, 2, 3
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _ptr(t: Optional[torch.Tensor]) -> Optional[int]:
+    return None if t is None else t.data_ptr()
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what}: HIP launch failed (hipError {rc})")
+
+
+def pack_keys(keys: Sequence, kstride: int = 0, device="cuda") -> torch.Tensor:
+    """Strings/bytes -> NUL-padded uint8 key records on `device`."""
+    bs = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
+    longest = max((len(b) for b in bs), default=1)
+    if kstride == 0:
+        kstride = min(64, (min(longest, 63) + 1 + 15) // 16 * 16)
+    arr = np.zeros((len(bs), kstride), dtype=np.uint8)
+    for i, b in enumerate(bs):
+        b = b[: min(63, kstride - 1)]
+        arr[i, : len(b)] = np.frombuffer(b, dtype=np.uint8)
+    return torch.from_numpy(arr).to(device)
+
+
+def pack_values(values: Sequence, vstride: int = 0, device="cuda") -> Tuple[torch.Tensor, torch.Tensor]:
+    bs = [v.encode() if isinstance(v, str) else bytes(v) for v in values]
+    longest = max((len(b) for b in bs), default=1)
+    if vstride == 0:
+        vstride = max(16, (longest + 15) // 16 * 16)
+    arr = np.zeros((len(bs), vstride), dtype=np.uint8)
+    lens = np.zeros(len(bs), dtype=np.int32)
+    for i, b in enumerate(bs):
+        arr[i, : len(b)] = np.frombuffer(b, dtype=np.uint8)
+        lens[i] = len(b)
+    return torch.from_numpy(arr).to(device), torch.from_numpy(lens).to(device)
+
+
+def unpack(vals: torch.Tensor, lens: torch.Tensor) -> list:
+    v = vals.cpu().numpy()
+    ln = lens.cpu().numpy()
+    return [bytes(v[i, : ln[i]]) for i in range(len(ln))]
+
+
+class HbmArena:
+    """A format-v4 arena resident in HBM, driven by batched kernels.
+
+    Wraps an ``hbm:`` :class:`Store` (which also offers the full single-op
+    reference API); ``arena`` is the device descriptor the kernels take.
+    """
+
+    def __init__(self, store: Store):
+        if store.backend != "hbm":
+            raise ValueError("HbmArena needs an hbm: store")
+        self.store = store
+        self._H = N.hip_lib()
+        self.desc = N.Arena()
+        if self._H.spl_hbm_arena(store.handle, ctypes.byref(self.desc)) != 0:
+            raise RuntimeError("spl_hbm_arena failed")
+        self.slots, self.max_val, self.stride = self.desc.slots, self.desc.max_val, self.desc.stride
+        self.stats = torch.zeros(4, dtype=torch.int64, device="cuda")  # attempts, ok, eagain, miss
+
+    @classmethod
+    def create(cls, name: str, slots: int, max_val: int, embeddings: bool = True) -> "HbmArena":
+        n = name if name.startswith("hbm:") else "hbm:" + name
+        return cls(Store.create(n, slots, max_val, embeddings=embeddings))
+
+    def close(self):
+        self.store.close()
+
+    @property
+    def embeddings(self) -> bool:
+        return self.stride == 3200
+
+    def refresh(self):
+        """Re-read the descriptor (event-bus armed flag)."""
+        self._H.spl_hbm_arena(self.store.handle, ctypes.byref(self.desc))
+
+    # ------------------------------------------------------------ batches --
+    def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, retries: int = 64,
+            status: Optional[torch.Tensor] = None) -> torch.Tensor:
+        n = keys.shape[0]
+        assert keys.dtype == torch.uint8 and vals.dtype == torch.uint8 and keys.is_cuda and vals.is_cuda
+        assert vals.shape[0] == n and lens.shape[0] == n and lens.dtype in (torch.int32, torch.uint32)
+        assert keys.is_contiguous() and vals.is_contiguous() and lens.is_contiguous()
+        if status is None:
+            status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        _check(self._H.spl_arena_set(self.desc, keys.data_ptr(), keys.shape[1], vals.data_ptr(), vals.shape[1],
+                                     lens.data_ptr(), n, status.data_ptr(), retries, self.stats.data_ptr(),
+                                     _stream()), "arena_set")
+        return status
+
+    def get(self, keys: torch.Tensor, out: Optional[torch.Tensor] = None, retries: int = 64,
+            status: Optional[torch.Tensor] = None, out_lens: Optional[torch.Tensor] = None):
+        n = keys.shape[0]
+        assert keys.dtype == torch.uint8 and keys.is_cuda and keys.is_contiguous()
+        if out is None:
+            out = torch.empty((n, (self.max_val + 15) // 16 * 16), dtype=torch.uint8, device=keys.device)
+        assert out.shape[0] == n and out.is_contiguous() and out.shape[1] % 16 == 0
+        if status is None:
+            status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        if out_lens is None:
+            out_lens = torch.empty(n, dtype=torch.int32, device=keys.device)
+        _check(self._H.spl_arena_get(self.desc, keys.data_ptr(), keys.shape[1], out.data_ptr(), out.shape[1],
+                                     out_lens.data_ptr(), n, status.data_ptr(), retries, self.stats.data_ptr(),
+                                     _stream()), "arena_get")
+        return status, out, out_lens
+
+    def unset(self, keys: torch.Tensor, retries: int = 64) -> torch.Tensor:
+        n = keys.shape[0]
+        status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        _check(self._H.spl_arena_unset(self.desc, keys.data_ptr(), keys.shape[1], n, status.data_ptr(), retries,
+                                       _stream()), "arena_unset")
+        return status
+
+    def integer_op(self, keys: torch.Tensor, ops: torch.Tensor, masks: Optional[torch.Tensor] = None,
+                   retries: int = 64) -> Tuple[torch.Tensor, torch.Tensor]:
+        n = keys.shape[0]
+        ops = ops.to(torch.int32).contiguous()
+        status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        results = torch.empty(n, dtype=torch.int64, device=keys.device)
+        _check(self._H.spl_arena_intop(self.desc, keys.data_ptr(), keys.shape[1], ops.data_ptr(), _ptr(masks), n,
+                                       status.data_ptr(), results.data_ptr(), retries, _stream()), "arena_intop")
+        return status, results
+
+    def meta(self, op: str, keys: torch.Tensor, args: Optional[torch.Tensor] = None):
+        n = keys.shape[0]
+        status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        out = torch.empty(n, dtype=torch.int64, device=keys.device)
+        _check(self._H.spl_arena_meta(self.desc, keys.data_ptr(), keys.shape[1], META[op], _ptr(args), n,
+                                      status.data_ptr(), out.data_ptr(), _stream()), "arena_meta")
+        return status, out
+
+    def set_embeddings(self, keys: torch.Tensor, vecs: torch.Tensor) -> torch.Tensor:
+        n = keys.shape[0]
+        assert vecs.dtype == torch.float32 and vecs.shape == (n, 768) and vecs.is_contiguous()
+        status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        _check(self._H.spl_arena_embed_set(self.desc, keys.data_ptr(), keys.shape[1], vecs.data_ptr(), n,
+                                           status.data_ptr(), _stream()), "arena_embed_set")
+        return status
+
+    def get_embeddings(self, keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        n = keys.shape[0]
+        vecs = torch.empty((n, 768), dtype=torch.float32, device=keys.device)
+        status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        _check(self._H.spl_arena_embed_get(self.desc, keys.data_ptr(), keys.shape[1], vecs.data_ptr(), n,
+                                           status.data_ptr(), _stream()), "arena_embed_get")
+        return status, vecs
+
+    def scan(self, mode: int = SCAN_LIST, mask: int = 0, cap: Optional[int] = None):
+        """Compacted slot indices (uint32 as int32) + epochs of matching slots."""
+        cap = self.slots if cap is None else cap
+        idx = torch.empty(cap, dtype=torch.int32, device="cuda")
+        ep = torch.empty(cap, dtype=torch.int64, device="cuda")
+        cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+        _check(self._H.spl_arena_scan(self.desc, mode, mask, idx.data_ptr(), ep.data_ptr(), cap, cnt.data_ptr(),
+                                      _stream()), "arena_scan")
+        n = min(int(cnt.item()), cap)
+        return idx[:n], ep[:n]
+
+    def purge(self):
+        _check(self._H.spl_arena_purge(self.desc, _stream()), "arena_purge")
+
+    # ------------------------------------------------------- raw views ----
+    def _tensor_view(self, offset: int, nbytes: int) -> torch.Tensor:
+        """uint8 torch view of device bytes [offset, offset+nbytes) of the arena."""
+        return _device_view(self.desc.base + offset, nbytes)
+
+    def embedding_matrix(self) -> torch.Tensor:
+        """[slots, 768] fp32 strided view of every slot's vector (zero copy)."""
+        assert self.embeddings
+        base = self.desc.base + 5440 + 128
+        flat = _device_view(base, self.slots * 3200 - 128, dtype=torch.float32)
+        return flat.as_strided((self.slots, 768), (800, 1))
+
+    def slot_view(self) -> torch.Tensor:
+        """[slots, stride] uint8 view of the slot array."""
+        return _device_view(self.desc.base + 5440, self.slots * self.stride).view(self.slots, self.stride)
+
+    def header_view(self) -> torch.Tensor:
+        return _device_view(self.desc.base, 5440)
+
+    def checkpoint(self, path: str) -> None:
+        torch.cuda.synchronize()
+        if self._H.spl_hbm_checkpoint(self.store.handle, path.encode()) != 0:
+            raise OSError(ctypes.get_errno(), f"checkpoint to {path} failed")
+
+    def restore(self, path: str) -> None:
+        torch.cuda.synchronize()
+        if self._H.spl_hbm_restore(self.store.handle, path.encode()) != 0:
+            raise OSError(ctypes.get_errno(), f"restore from {path} failed")
+
+    def reset_stats(self):
+        self.stats.zero_()
+
+
+def _device_view(ptr: int, nbytes: int, dtype=torch.uint8) -> torch.Tensor:
+    """Wrap raw device memory owned elsewhere as a torch tensor (no copy)."""
+    itemsize = torch.tensor([], dtype=dtype).element_size()
+
+    class _Holder:
+        pass
+
+    h = _Holder()
+    h.__cuda_array_interface__ = {
+        "shape": (nbytes // itemsize,),
+        "typestr": {torch.uint8: "|u1", torch.float32: "<f4", torch.int64: "<i8"}[dtype],
+        "data": (ptr, False),
+        "version": 3,
+        "strides": None,
+    }
+    return torch.as_tensor(h, device="cuda")
+
+
+def format_keys(n: int, prefix: str = "k", width: int = 9, kstride: int = 16, first: int = 0,
+                ids: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Device-side key generator (prefix + zero-padded decimal id), for tools and benches."""
+    H = N.hip_lib()
+    out = torch.empty((n, kstride), dtype=torch.uint8, device="cuda")
+    pre = torch.tensor(list(prefix.encode()) + [0], dtype=torch.uint8, device="cuda")
+    _check(H.spl_format_keys(out.data_ptr(), kstride, _ptr(ids), first, n, pre.data_ptr(), len(prefix), width,
+                             _stream()), "format_keys")
+    return out
+
+
+def format_values(n: int, ver: int, length: int, vstride: int, first: int = 0,
+                  ids: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """Device-side payload generator: "ver:<v>|id:<id>|data:AAAA..." of `length` bytes."""
+    H = N.hip_lib()
+    out = torch.empty((n, vstride), dtype=torch.uint8, device="cuda")
+    lens = torch.empty(n, dtype=torch.int32, device="cuda")
+    _check(H.spl_format_values(out.data_ptr(), vstride, lens.data_ptr(), _ptr(ids), first, n, ver, length,
+                               _stream()), "format_values")
+    return out, lens

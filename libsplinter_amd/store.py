@@ -1,0 +1,381 @@
+"""Pythonic handle over libsplinter.so (host shm/file stores and HBM stores).
+
+Mirrors the reference's TypeScript ``SplinterStore`` surface
+(/root/reference/bindings/ts/splinter.ts:50-68) and the ctypes pattern in
+/root/reference/docs/bindings/python.md, but on the handle API so one process
+can hold many stores.  Errors follow the C convention: methods that the C API
+reports with -1 raise :class:`SplinterError` carrying errno (EAGAIN is
+:class:`SplinterBusy`, meaning "retry"), except lookups, which return None.
+"""
+from __future__ import annotations
+
+import ctypes
+import errno as _errno
+import os
+from typing import Callable, Iterable, List, Optional, Tuple
+
+import numpy as np
+
+from . import _native as N
+
+EMBED_DIM = 768
+MAX_GROUPS = 64
+MAX_SHARDS = 32
+
+# named types / flags (splinter.h)
+SLOT_VOID, SLOT_BIGINT, SLOT_BIGUINT, SLOT_JSON = 1 << 0, 1 << 1, 1 << 2, 1 << 3
+SLOT_BINARY, SLOT_IMGDATA, SLOT_AUDIO, SLOT_VARTEXT = 1 << 4, 1 << 5, 1 << 6, 1 << 7
+TYPE_NAMES = {SLOT_VOID: "VOID", SLOT_BIGINT: "BIGINT", SLOT_BIGUINT: "BIGUINT", SLOT_JSON: "JSON",
+              SLOT_BINARY: "BINARY", SLOT_IMGDATA: "IMGDATA", SLOT_AUDIO: "AUDIO", SLOT_VARTEXT: "VARTEXT"}
+SYS_AUTO_SCRUB, SYS_HYBRID_SCRUB = 1, 2
+OP_AND, OP_OR, OP_XOR, OP_NOT, OP_INC, OP_DEC = range(6)
+INTENT_NONE, INTENT_WILLNEED, INTENT_SEQUENTIAL, INTENT_RANDOM, INTENT_DONTNEED = range(5)
+TIME_CTIME, TIME_ATIME = 0, 1
+CREATE_EMBEDDINGS, CREATE_PERSISTENT, CREATE_NO_EMBEDDINGS = 1, 2, 4
+
+
+class SplinterError(OSError):
+    pass
+
+
+class SplinterBusy(SplinterError):
+    """EAGAIN: a writer held the slot; the same call succeeds on retry."""
+
+
+def _raise(what: str, err: Optional[int] = None):
+    e = ctypes.get_errno() if err is None else err
+    if e == 0:
+        e = _errno.EIO
+    cls = SplinterBusy if e == _errno.EAGAIN else SplinterError
+    raise cls(e, f"{what}: {os.strerror(e)}")
+
+
+def _k(key) -> bytes:
+    return key.encode() if isinstance(key, str) else bytes(key)
+
+
+def now() -> int:
+    """splinter_now(): the tick source used by shard windows."""
+    return N.core_lib().splinter_now()
+
+
+def unlink(name: str) -> int:
+    return N.core_lib().spl_unlink(name.encode())
+
+
+class Store:
+    """One open store.  Use :meth:`create`, :meth:`open` or :meth:`open_or_create`."""
+
+    def __init__(self, handle: int, name: str):
+        self._h = handle
+        self.name = name
+        self._L = N.core_lib()
+        slots, mv, stride = N.c_u32(), N.c_u32(), N.c_u32()
+        self._L.spl_store_geometry(handle, ctypes.byref(slots), ctypes.byref(mv), ctypes.byref(stride))
+        self.slots, self.max_val, self.stride = slots.value, mv.value, stride.value
+
+    # ----------------------------------------------------------- lifecycle --
+    @classmethod
+    def create(cls, name: str, slots: int = 1024, max_val: int = 4096, embeddings: Optional[bool] = None,
+               persistent: bool = False) -> "Store":
+        if name.startswith("hbm:"):
+            N.hip_lib()
+        flags = 0
+        if embeddings is True:
+            flags |= CREATE_EMBEDDINGS
+        elif embeddings is False:
+            flags |= CREATE_NO_EMBEDDINGS
+        if persistent:
+            flags |= CREATE_PERSISTENT
+        err = ctypes.c_int(0)
+        h = N.core_lib().spl_store_create(name.encode(), slots, max_val, flags, ctypes.byref(err))
+        if not h:
+            _raise(f"create {name}", err.value)
+        return cls(h, name)
+
+    @classmethod
+    def open(cls, name: str) -> "Store":
+        if name.startswith("hbm:"):
+            N.hip_lib()
+        err = ctypes.c_int(0)
+        h = N.core_lib().spl_store_open(name.encode(), ctypes.byref(err))
+        if not h:
+            _raise(f"open {name}", err.value)
+        return cls(h, name)
+
+    @classmethod
+    def open_or_create(cls, name: str, slots: int = 1024, max_val: int = 4096, **kw) -> "Store":
+        try:
+            return cls.open(name)
+        except SplinterError:
+            return cls.create(name, slots, max_val, **kw)
+
+    def close(self) -> None:
+        if self._h:
+            self._L.spl_store_close(self._h)
+            self._h = None
+
+    def unlink(self) -> None:
+        unlink(self.name)
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def use(self) -> None:
+        """Make this store the current one for the splinter_* C API."""
+        self._L.spl_store_use(self._h)
+
+    @property
+    def handle(self) -> int:
+        return self._h
+
+    @property
+    def backend(self) -> str:
+        return self._L.spl_store_backend(self._h).decode()
+
+    @property
+    def embeddings(self) -> bool:
+        return self.stride == 3200
+
+    def region(self) -> Optional[memoryview]:
+        """Zero-copy view of the whole mapped region (host backends)."""
+        base = self._L.spl_store_base(self._h)
+        if not base:
+            return None
+        n = self._L.spl_store_bytes(self._h)
+        return memoryview((ctypes.c_uint8 * n).from_address(base)).cast("B")
+
+    # ------------------------------------------------------------- values --
+    def set(self, key, value) -> None:
+        v = value.encode() if isinstance(value, str) else bytes(value)
+        rc = self._L.spl_set(self._h, _k(key), v, len(v))
+        if rc != 0:
+            _raise(f"set {key!r}")
+
+    def get(self, key) -> Optional[bytes]:
+        buf = ctypes.create_string_buffer(self.max_val)
+        n = N.c_size_t(0)
+        ctypes.set_errno(0)
+        rc = self._L.spl_get(self._h, _k(key), buf, self.max_val, ctypes.byref(n))
+        if rc != 0:
+            e = ctypes.get_errno()
+            if e in (0, _errno.ENOENT):
+                return None
+            _raise(f"get {key!r}", e)
+        return buf.raw[: n.value]
+
+    def get_str(self, key) -> Optional[str]:
+        v = self.get(key)
+        return None if v is None else v.decode("utf-8", "replace")
+
+    def unset(self, key) -> int:
+        return self._L.spl_unset(self._h, _k(key))
+
+    def append(self, key, data) -> int:
+        d = data.encode() if isinstance(data, str) else bytes(data)
+        n = N.c_size_t(0)
+        if self._L.spl_append(self._h, _k(key), d, len(d), ctypes.byref(n)) != 0:
+            _raise(f"append {key!r}")
+        return n.value
+
+    def list(self) -> List[str]:
+        cap = max(self.slots, 1)
+        arr = (ctypes.c_char_p * cap)()
+        n = N.c_size_t(0)
+        self._L.spl_list(self._h, arr, cap, ctypes.byref(n))
+        return [arr[i].decode("utf-8", "replace") for i in range(n.value)]
+
+    def keys(self) -> List[str]:
+        return self.list()
+
+    def poll(self, key, timeout_ms: int) -> bool:
+        return self._L.spl_poll(self._h, _k(key), timeout_ms) == 0
+
+    def epoch(self, key) -> int:
+        return self._L.spl_get_epoch(self._h, _k(key))
+
+    def raw(self, key) -> Optional[Tuple[memoryview, int]]:
+        """Zero-copy (view, epoch) of the value (host backends); validate the epoch after use."""
+        sz, ep = N.c_size_t(0), N.c_u64(0)
+        p = self._L.spl_get_raw_ptr(self._h, _k(key), ctypes.byref(sz), ctypes.byref(ep))
+        if not p:
+            return None
+        return memoryview((ctypes.c_uint8 * sz.value).from_address(p)).cast("B"), ep.value
+
+    def set_as_system(self, key) -> None:
+        if self._L.spl_set_as_system(self._h, _k(key)) != 0:
+            _raise(f"set_as_system {key!r}", _errno.ENOENT)
+
+    def snapshot(self, key) -> Optional[dict]:
+        s = N.SlotSnapshot()
+        if self._L.spl_get_slot_snapshot(self._h, _k(key), ctypes.byref(s)) != 0:
+            return None
+        return {"hash": s.hash, "epoch": s.epoch, "val_off": s.val_off, "val_len": s.val_len,
+                "type_flag": s.type_flag, "user_flag": s.user_flag, "ctime": s.ctime, "atime": s.atime,
+                "bloom": s.bloom, "key": s.key.decode("utf-8", "replace"),
+                "embedding": np.ctypeslib.as_array(s.embedding).copy() if self.embeddings else None}
+
+    def header(self) -> dict:
+        h = N.HeaderSnapshot()
+        self._L.spl_get_header_snapshot(self._h, ctypes.byref(h))
+        return {k: getattr(h, k) for k, _ in N.HeaderSnapshot._fields_}
+
+    # -------------------------------------------------------------- config --
+    def set_mop(self, mode: int) -> None:
+        if self._L.spl_set_mop(self._h, mode) != 0:
+            _raise("set_mop")
+
+    def get_mop(self) -> int:
+        return self._L.spl_get_mop(self._h)
+
+    def purge(self) -> None:
+        self._L.spl_purge(self._h)
+
+    # ---------------------------------------------------------- embeddings --
+    def set_embedding(self, key, vec) -> None:
+        v = np.ascontiguousarray(vec, dtype=np.float32).reshape(EMBED_DIM)
+        if self._L.spl_set_embedding(self._h, _k(key), v.ctypes.data) != 0:
+            _raise(f"set_embedding {key!r}")
+
+    def get_embedding(self, key) -> Optional[np.ndarray]:
+        out = np.zeros(EMBED_DIM, dtype=np.float32)
+        ctypes.set_errno(0)
+        if self._L.spl_get_embedding(self._h, _k(key), out.ctypes.data) != 0:
+            e = ctypes.get_errno()
+            if e in (0, _errno.ENOENT):
+                return None
+            _raise(f"get_embedding {key!r}", e)
+        return out
+
+    # ------------------------------------------------- typing/time/integer --
+    def set_type(self, key, mask: int) -> None:
+        if self._L.spl_set_named_type(self._h, _k(key), mask) != 0:
+            _raise(f"set_named_type {key!r}")
+
+    def set_time(self, key, mode: int, epoch: int, offset: int = 0) -> None:
+        if self._L.spl_set_slot_time(self._h, _k(key), mode, epoch, offset) != 0:
+            _raise(f"set_slot_time {key!r}")
+
+    def integer_op(self, key, op: int, mask: int = 0) -> int:
+        m = ctypes.c_uint64(mask & 0xFFFFFFFFFFFFFFFF)
+        if self._L.spl_integer_op(self._h, _k(key), op, ctypes.byref(m)) != 0:
+            _raise(f"integer_op {key!r}")
+        v = self.get(key)
+        return int.from_bytes(v[:8], "little") if v else 0
+
+    def get_u64(self, key) -> Optional[int]:
+        v = self.get(key)
+        return None if v is None else int.from_bytes(v[:8].ljust(8, b"\0"), "little")
+
+    # ------------------------------------------------------ epochs / labels --
+    def bump(self, key) -> bool:
+        return self._L.spl_bump_slot(self._h, _k(key)) == 0
+
+    def retrain(self, key) -> bool:
+        return self._L.spl_retrain_slot(self._h, _k(key)) == 0
+
+    def set_label(self, key, mask: int) -> bool:
+        return self._L.spl_set_label(self._h, _k(key), mask) == 0
+
+    def unset_label(self, key, mask: int) -> bool:
+        return self._L.spl_unset_label(self._h, _k(key), mask) == 0
+
+    def set_tandem(self, base, values: Iterable) -> None:
+        for i, v in enumerate(values):
+            self.set(base if i == 0 else f"{base}.{i}", v)
+
+    def unset_tandem(self, base, orders: int) -> None:
+        for i in range(orders):
+            self.unset(base if i == 0 else f"{base}.{i}")
+
+    # ------------------------------------------------------------- signals --
+    def watch(self, key, group: int) -> bool:
+        return self._L.spl_watch_register(self._h, _k(key), group) == 0
+
+    def unwatch(self, key, group: int) -> bool:
+        return self._L.spl_watch_unregister(self._h, _k(key), group) == 0
+
+    def watch_label(self, mask: int, group: int) -> bool:
+        return self._L.spl_watch_label_register(self._h, mask, group) == 0
+
+    def pulse(self, key) -> bool:
+        return self._L.spl_pulse_keygroup(self._h, _k(key)) == 0
+
+    def signal_count(self, group: int) -> int:
+        return self._L.spl_get_signal_count(self._h, group)
+
+    def enumerate(self, mask: int) -> List[Tuple[str, int]]:
+        out: List[Tuple[str, int]] = []
+
+        @N.ENUM_CB
+        def cb(key, epoch, _ud):
+            out.append((key.decode("utf-8", "replace"), epoch))
+
+        self._L.spl_enumerate_matches(self._h, mask, cb, None)
+        return out
+
+    # ----------------------------------------------------------- event bus --
+    def event_bus_init(self) -> None:
+        if self._L.spl_event_bus_init(self._h) != 0:
+            _raise("event_bus_init")
+
+    def event_bus_open(self) -> int:
+        fd = self._L.spl_event_bus_open(self._h)
+        if fd < 0:
+            _raise("event_bus_open")
+        return fd
+
+    @staticmethod
+    def event_bus_wait(fd: int, timeout_ms: int) -> bool:
+        return N.core_lib().splinter_event_bus_wait(fd, timeout_ms) == 0
+
+    def dirty_mask(self) -> List[int]:
+        arr = (N.c_u64 * 16)()
+        self._L.spl_event_bus_get_dirty(self._h, arr, 16)
+        return list(arr)
+
+    # -------------------------------------------------------------- shards --
+    def shard_claim(self, shard_id: int, intent: int, priority: int, duration: int,
+                    pid: Optional[int] = None, claimed_at: Optional[int] = None) -> None:
+        if pid is None and claimed_at is None:
+            rc = self._L.spl_shard_claim(self._h, shard_id, intent, priority, duration)
+        else:
+            rc = self._L.spl_shard_claim_ex(self._h, shard_id, os.getpid() if pid is None else pid, intent,
+                                            priority, duration, now() if claimed_at is None else claimed_at)
+        if rc != 0:
+            _raise("shard_claim")
+
+    def shard_rebid(self, shard_id: int, intent: int, priority: int, duration: int) -> bool:
+        return self._L.spl_shard_rebid(self._h, shard_id, intent, priority, duration) == 0
+
+    def shard_release(self, shard_id: int) -> bool:
+        return self._L.spl_shard_release(self._h, shard_id) == 0
+
+    def shard_election(self) -> Tuple[int, int]:
+        it = N.c_u8(0)
+        sid = self._L.spl_shard_election(self._h, ctypes.byref(it))
+        return sid, it.value
+
+    def shard_table(self) -> List[dict]:
+        arr = (N.ShardBidSnapshot * MAX_SHARDS)()
+        n = self._L.spl_shard_table_snapshot(self._h, arr, MAX_SHARDS)
+        return [{k: getattr(arr[i], k) for k, _ in N.ShardBidSnapshot._fields_} for i in range(max(n, 0))]
+
+    def madvise(self, shard_id: int, advice: int, timeout: int = 0) -> None:
+        if self._L.spl_madvise(self._h, shard_id, None, 0, advice, timeout) != 0:
+            _raise("madvise")
+
+    # ---------------------------------------------------------------- misc --
+    def find_slot(self, key) -> int:
+        return self._L.spl_find_slot(self._h, _k(key))
+
+    def __repr__(self):
+        return (f"Store({self.name!r}, backend={self.backend}, slots={self.slots}, max_val={self.max_val}, "
+                f"embeddings={self.embeddings})")
+
+
+def hash_key(key) -> int:
+    return N.core_lib().spl_hash_key(_k(key))

@@ -328,8 +328,8 @@ int HostStore::set(const char* key, const void* val, size_t len) {
       }
       return write_locked(idx, k, val, len, false);
     }
-    if ((e & 1) && (sh == 0 || sh == k.hash)) { errno = EAGAIN; return -1; }  // could be our key in flight
-    if (sh == 0) {
+    if ((e & 1) && sh == k.hash) { errno = EAGAIN; return -1; }  // our key is being rewritten
+    if (sh == 0 && !(e & 1)) {  // reusable slot (odd = another writer's claim: skip it)
       if (free_idx < 0) { free_idx = (long)idx; free_epoch = e; }
       if (e == 0) break;  // virgin: end of chain
     }
@@ -345,13 +345,19 @@ int HostStore::set(const char* key, const void* val, size_t len) {
     errno = EAGAIN;
     return -1;
   }
+  // A published copy of the key anywhere on the chain, or a claim in flight
+  // *before* ours (possibly the same key), makes us back off: the earlier
+  // claimant wins, so racing inserters always make progress.
   idx = home;
+  bool before = true;
   for (uint32_t i = 0; i < n; ++i) {
-    if ((long)idx != free_idx) {
+    if ((long)idx == free_idx) {
+      before = false;
+    } else {
       splinter_slot* s = slot(idx);
       const uint64_t sh = ld(&s->hash);
       const uint64_t e = ld(&s->epoch);
-      if ((sh == k.hash && key_eq(s, k)) || ((e & 1) && (sh == 0 || sh == k.hash))) {
+      if ((sh == k.hash && (key_eq(s, k) || (e & 1))) || (before && (e & 1) && sh == 0)) {
         __atomic_fetch_add(&fs->epoch, 1, __ATOMIC_RELEASE);
         errno = EAGAIN;
         return -1;

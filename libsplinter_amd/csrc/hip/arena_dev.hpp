@@ -209,36 +209,63 @@ __device__ __forceinline__ uint32_t keep_mask(int keep) {
 // last chunk is zeroed; with scrubbing the region is zeroed to the 64-B
 // boundary (hybrid) or to max_val (full) — the reference's mop modes
 // (reference splinter.c:393-401).  Source records are 16-B aligned.
+// Memory-ordering discipline of the payload (template parameter MO):
+//   0  plain 16-B payload accesses + agent release (writer) / acquire (reader)
+//   1  sc1 (L1-bypassing, write-through) 8-B atomic payload accesses, no fences
+//   2  unordered (measurement only: NOT a valid seqlock)
+template <int MO>
+__device__ __forceinline__ void st16(void* p, uint4 v) {
+  if constexpr (MO == 1) {
+    ast64(p, ((uint64_t)v.y << 32) | v.x);
+    ast64((uint8_t*)p + 8, ((uint64_t)v.w << 32) | v.z);
+  } else {
+    *(uint4*)p = v;
+  }
+}
+template <int MO>
+__device__ __forceinline__ uint4 ld16(const void* p) {
+  if constexpr (MO == 1) {
+    const uint64_t a = ald64(p), b = ald64((const uint8_t*)p + 8);
+    return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+  } else {
+    return *(const uint4*)p;
+  }
+}
+
+template <int MO>
 __device__ __forceinline__ void write_value(const Arena& a, size_t idx, const uint8_t* src, uint32_t len, bool scrub,
                                             bool hybrid) {
   uint4* dst = (uint4*)a.value(idx);
   const uint4* s4 = (const uint4*)src;
   const uint32_t full = len >> 4;
-  for (uint32_t c = 0; c < full; ++c) dst[c] = s4[c];
+  for (uint32_t c = 0; c < full; ++c) st16<MO>(dst + c, s4[c]);
   uint32_t done = full << 4;
   if (len & 15) {
     uint4 t = s4[full];
     const int r = (int)(len & 15);
     t.x &= keep_mask(r); t.y &= keep_mask(r - 4); t.z &= keep_mask(r - 8); t.w &= keep_mask(r - 12);
-    dst[full] = t;
+    st16<MO>(dst + full, t);
     done += 16;
   }
   if (scrub) {
     uint32_t end = hybrid ? ((len + 63u) & ~63u) : a.max_val;
     if (end > a.max_val) end = a.max_val;
-    for (; done + 16 <= end; done += 16) dst[done >> 4] = make_uint4(0, 0, 0, 0);
+    for (; done + 16 <= end; done += 16) st16<MO>(dst + (done >> 4), make_uint4(0, 0, 0, 0));
   }
 }
 
 // Publish a locked slot: release the payload, store hash, epoch+1.
+template <int MO>
 __device__ __forceinline__ void publish(const Arena& a, size_t idx, uint64_t hash) {
   uint8_t* s = a.slot(idx);
-  release();
+  if constexpr (MO == 0) release();
+  else if constexpr (MO == 1) drain();
   ast64(s + kOffHash, hash);
   aadd64(epoch_ptr(s), 1);
 }
 
 // SET (insert or update).  On success *out_idx = slot index.
+template <int MO = 0>
 __device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint32_t len, long* out_idx) {
   if (len == 0 || len > a.max_val) return kMsgSize;
   bool hybrid;
@@ -257,14 +284,14 @@ __device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint
         aadd64(epoch_ptr(s), 1);
         return kAgain;
       }
-      write_value(a, idx, val, len, scrub, hybrid);
+      write_value<MO>(a, idx, val, len, scrub, hybrid);
       ast32(s + kOffValLen, len);
-      publish(a, idx, k.hash);
+      publish<MO>(a, idx, k.hash);
       *out_idx = (long)idx;
       return kOk;
     }
-    if ((e & 1) && (sh == 0 || sh == k.hash)) return kAgain;
-    if (sh == 0) {
+    if ((e & 1) && sh == k.hash) return kAgain;  // our key is being rewritten
+    if (sh == 0 && !(e & 1)) {                   // reusable (odd = someone's claim: skip)
       if (free_idx < 0) { free_idx = (long)idx; free_ep = e; }
       if (e == 0) break;
     }
@@ -274,14 +301,20 @@ __device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint
   uint8_t* fs = a.slot((size_t)free_idx);
   if (!acas64(epoch_ptr(fs), free_ep, free_ep + 1)) return kAgain;
   if (slot_hash(fs) != 0) { aadd64(epoch_ptr(fs), 1); return kAgain; }
-  // re-validate the chain while holding the claimed slot (no duplicates)
+  // Re-validate the chain while holding the claimed slot (no duplicates):
+  //  - our key published anywhere on the chain -> back off, update it next try;
+  //  - a claim in flight *before* ours may be the same key -> the earlier
+  //    claimant wins, we back off; claims after ours defer to us.
   idx = home;
+  bool before = true;
   for (uint32_t i = 0; i < a.slots; ++i) {
-    if ((long)idx != free_idx) {
+    if ((long)idx == free_idx) {
+      before = false;
+    } else {
       uint8_t* s = a.slot(idx);
       const uint64_t sh = slot_hash(s);
       const uint64_t e = slot_epoch(s);
-      if ((sh == k.hash && key_eq(s, k)) || ((e & 1) && (sh == 0 || sh == k.hash))) {
+      if ((sh == k.hash && (key_eq(s, k) || (e & 1))) || (before && (e & 1) && sh == 0)) {
         aadd64(epoch_ptr(fs), 1);
         return kAgain;
       }
@@ -289,26 +322,29 @@ __device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint
     }
     if (++idx == a.slots) idx = 0;
   }
-  write_value(a, (size_t)free_idx, val, len, scrub, hybrid);
+  write_value<MO>(a, (size_t)free_idx, val, len, scrub, hybrid);
   ast32(fs + kOffValLen, len);
   if (a.stride == kSlotEmbedBytes) {  // fresh slot: clear a stale vector
     uint4* ev = (uint4*)(fs + kOffEmbed);
-    for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ev[c] = make_uint4(0, 0, 0, 0);
+    for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) st16<MO>(ev + c, make_uint4(0, 0, 0, 0));
   }
-  store_key(fs, k);
-  publish(a, (size_t)free_idx, k.hash);
+#pragma unroll
+  for (int c = 0; c < 4; ++c)
+    st16<MO>(fs + kOffKey + 16 * c, make_uint4(k.w[4 * c], k.w[4 * c + 1], k.w[4 * c + 2], k.w[4 * c + 3]));
+  publish<MO>(a, (size_t)free_idx, k.hash);
   *out_idx = free_idx;
   return kOk;
 }
 
 // GET: seqlock read into out (may be null: size query).
+template <int MO = 0>
 __device__ int32_t get_op(const Arena& a, const Key& k, uint8_t* out, uint32_t out_cap, uint32_t* out_len) {
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
     const uint64_t sh = slot_hash(s);
     if (sh == k.hash) {
-      const uint64_t e1 = ald64_acq(s + kOffEpoch);
+      const uint64_t e1 = MO == 0 ? ald64_acq(s + kOffEpoch) : ald64(s + kOffEpoch);
       if (key_eq(s, k)) {
         if (e1 & 1) return kAgain;
         const uint32_t len = ald32(s + kOffValLen);
@@ -318,9 +354,9 @@ __device__ int32_t get_op(const Arena& a, const Key& k, uint8_t* out, uint32_t o
           const uint4* src = (const uint4*)a.value(idx);
           uint4* dst = (uint4*)out;
           const uint32_t n16 = (len + 15) >> 4;
-          for (uint32_t c = 0; c < n16; ++c) dst[c] = src[c];
+          for (uint32_t c = 0; c < n16; ++c) dst[c] = ld16<MO>(src + c);
         }
-        drain();
+        if constexpr (MO != 2) drain();
         const uint64_t e2 = slot_epoch(s);
         return (e2 == e1 && slot_hash(s) == k.hash) ? kOk : kAgain;
       }

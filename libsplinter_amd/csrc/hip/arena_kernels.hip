@@ -11,6 +11,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 
 #include "arena_dev.hpp"
 #include "arena_api.h"
@@ -22,6 +23,15 @@ namespace {
 
 constexpr int kBlock = 256;
 constexpr int kMaxGrid = 256 * 8;
+
+// Payload ordering discipline (arena_dev.hpp, MO): SPLINTER_ARENA_MO=0|1|2.
+inline int arena_mo() {
+  static int mo = [] {
+    const char* e = getenv("SPLINTER_ARENA_MO");
+    return e ? atoi(e) : 0;
+  }();
+  return mo;
+}
 
 inline int grid_for(long n) {
   long g = (n + kBlock - 1) / kBlock;
@@ -74,6 +84,8 @@ __device__ __forceinline__ void flush_stats(const Arena& a, Stats st, uint64_t* 
   }
 }
 
+// Lanes of one wave retry in lockstep (s_sleep is per wave); progress between
+// racing inserters comes from the claim-order rule in set_op, not from timing.
 __device__ __forceinline__ void backoff(int attempt) {
   if (attempt < 4) __builtin_amdgcn_s_sleep(1);
   else __builtin_amdgcn_s_sleep(8);
@@ -92,6 +104,7 @@ __global__ void k_init_slots(spl_arena_t aa) {
 }
 
 // ------------------------------------------------------------- set ------
+template <int MO>
 __global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
                                                 int vstride, const uint32_t* lens, long n, int32_t* status,
                                                 int max_retry, uint64_t* stats) {
@@ -106,7 +119,7 @@ __global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys
     long idx = -1;
     for (int t = 0; t <= max_retry; ++t) {
       ++st.attempts;
-      rc = set_op(a, k, vals + i * (long)vstride, len, &idx);
+      rc = set_op<MO>(a, k, vals + i * (long)vstride, len, &idx);
       if (rc != kAgain) break;
       ++st.again;
       backoff(t);
@@ -123,6 +136,7 @@ __global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys
 }
 
 // ------------------------------------------------------------- get ------
+template <int MO>
 __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                 int ostride, uint32_t* out_lens, long n, int32_t* status,
                                                 int max_retry, uint64_t* stats) {
@@ -135,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys
     int32_t rc = kAgain;
     for (int t = 0; t <= max_retry; ++t) {
       ++st.attempts;
-      rc = get_op(a, k, out ? out + i * (long)ostride : nullptr, (uint32_t)ostride, &len);
+      rc = get_op<MO>(a, k, out ? out + i * (long)ostride : nullptr, (uint32_t)ostride, &len);
       if (rc != kAgain) break;
       ++st.again;
       backoff(t);
@@ -480,8 +494,16 @@ int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* v
                   long n, int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_set, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n, status,
-                     max_retry, stats);
+  const int mo = arena_mo();
+  if (mo == 1)
+    hipLaunchKernelGGL(k_set<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
+                       status, max_retry, stats);
+  else if (mo == 2)
+    hipLaunchKernelGGL(k_set<2>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
+                       status, max_retry, stats);
+  else
+    hipLaunchKernelGGL(k_set<0>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
+                       status, max_retry, stats);
   return (int)hipGetLastError();
 }
 
@@ -489,8 +511,16 @@ int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, in
                   int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_get, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
-                     status, max_retry, stats);
+  const int mo = arena_mo();
+  if (mo == 1)
+    hipLaunchKernelGGL(k_get<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
+                       status, max_retry, stats);
+  else if (mo == 2)
+    hipLaunchKernelGGL(k_get<2>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
+                       status, max_retry, stats);
+  else
+    hipLaunchKernelGGL(k_get<0>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
+                       status, max_retry, stats);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,273 @@
+// gemm_bf16.hip — MFMA bf16 GEMM with fused epilogues for the Nomic-BERT
+// encoder (kernels K12/K13/K15/K16 of SURVEY §2.10).
+//
+//   C[M, N] = A[M, K] . W[N, K]^T      (A activations, W = GGUF weight rows)
+//
+// Geometry (gfx950): 256 threads = 4 waves in a 2x2 arrangement, block tile
+// 128x128, BK = 64; each wave owns a 64x64 sub-tile = 4x4 tiles of
+// v_mfma_f32_16x16x32_bf16 with fp32 accumulators.  Both operands are
+// K-contiguous, so every MFMA fragment is one 16-B ds_read_b128.
+// Staging: global_load_lds_dwordx4 (LDS-DMA) into a double-buffered LDS
+// image; the image is lane-linear, so the XOR swizzle (chunk ^= row & 7,
+// conflict-free for the ds_read_b128 lane groups) is applied to the GLOBAL
+// source address and to the LDS read address (guide rule 21).
+// Block -> tile mapping is XCD-aware (bijective remap, guide §5 T1): the tiles
+// that share A rows run on one XCD and reuse its L2.
+// Epilogue: accumulators go through LDS in fp32, then each thread owns
+// 16-B output chunks, so every fused epilogue (residual add, SwiGLU, RoPE)
+// works on whole rows with vector loads/stores.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "nomic_api.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void gbl_void;
+
+constexpr int BM = 128, BN = 128, BK = 64;
+constexpr int kThreads = 256;
+constexpr int kTileBytes = BM * BK * 2;            // 16 KB per operand tile
+constexpr int kEpiStride = BN + 4;                 // fp32 epilogue row stride (floats)
+constexpr int kLdsBytes = (BM * kEpiStride * 4 > 4 * kTileBytes) ? BM * kEpiStride * 4 : 4 * kTileBytes;
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  // round-to-nearest-even (NaN stays NaN: quiet bit kept by the +0x7fff path for finite only)
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
+  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+// Stage one BMxBK tile of a K-contiguous matrix (row stride ld elements)
+// starting at (row0, k0) into the lane-linear LDS image at `dst`.
+__device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, long ld, long row0, int k0,
+                                           char* dst, int wave, int lane) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int blk = wave * 4 + i;          // 8-row block of this wave instruction
+    const int r = blk * 8 + (lane >> 3);   // row in tile
+    const int pc = lane & 7;               // physical 16-B chunk in the 128-B row
+    const int c = pc ^ (r & 7);            // logical chunk stored there
+    const uint16_t* g = src + (row0 + r) * ld + k0 + c * 8;
+    __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)(dst + blk * 1024), 16, 0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const char* tile, int r, int c) {
+  return *(const bf16x8*)(tile + r * 128 + ((c ^ (r & 7)) << 4));
+}
+
+__device__ __forceinline__ void remap_tile(int bid, int nb, int nt, int& mt, int& ntile) {
+  // bijective XCD remap: blocks b and b+8 share an XCD; give each XCD a
+  // contiguous range of tiles (tiles sharing A rows are adjacent in n).
+  const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
+  const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  mt = wg / nt;
+  ntile = wg - mt * nt;
+}
+
+struct EpiArgs {
+  uint16_t* out;
+  long ldo;
+  const uint16_t* res;   // residual [M, N] (mode 1)
+  long ldr;
+  const float* rope;     // [max_pos, 32] x {cos, sin} interleaved (mode 3)
+  const int32_t* pos;    // [M] position of each row (mode 3)
+  int rope_cols;         // columns (from 0) that get RoPE (q|k = 1536)
+  long M;
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ W, long ldw, int K,
+                                                         int mtiles, int ntiles, EpiArgs ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  int mt, nt;
+  remap_tile(blockIdx.x, mtiles * ntiles, ntiles, mt, nt);
+  const long m0 = (long)mt * BM, n0 = (long)nt * BN;
+  const int wm = wave >> 1, wn = wave & 1;
+
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  // LDS: [A0 | B0 | A1 | B1], 16 KB each
+  stage_tile(A, lda, m0, 0, smem, wave, lane);
+  stage_tile(W, ldw, n0, 0, smem + kTileBytes, wave, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) {
+      char* nb = smem + (cur ^ 1) * 2 * kTileBytes;
+      stage_tile(A, lda, m0, (kt + 1) * BK, nb, wave, lane);
+      stage_tile(W, ldw, n0, (kt + 1) * BK, nb + kTileBytes, wave, lane);
+    }
+    const char* ta = smem + cur * 2 * kTileBytes;
+    const char* tb = ta + kTileBytes;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = lds_frag(ta, wm * 64 + i * 16 + fr, kk * 4 + fq);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = lds_frag(tb, wn * 64 + j * 16 + fr, kk * 4 + fq);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // ---- epilogue: accumulators -> LDS (fp32) -> 16-B output chunks --------
+  float* E = (float*)smem;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        E[(wm * 64 + i * 16 + fq * 4 + r) * kEpiStride + wn * 64 + j * 16 + fr] = acc[i][j][r];
+  __syncthreads();
+
+  if constexpr (MODE == NOMIC_EPI_STORE || MODE == NOMIC_EPI_RESIDUAL) {
+#pragma unroll
+    for (int it = 0; it < (BM * BN / 8) / kThreads; ++it) {
+      const int q = tid + it * kThreads;
+      const int row = q >> 4, c8 = (q & 15) * 8;
+      const long gm = m0 + row;
+      if (gm >= ep.M) continue;
+      const float4 v0 = *(const float4*)&E[row * kEpiStride + c8];
+      const float4 v1 = *(const float4*)&E[row * kEpiStride + c8 + 4];
+      float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+      if constexpr (MODE == NOMIC_EPI_RESIDUAL) {
+        const uint4 rr = *(const uint4*)(ep.res + gm * ep.ldr + n0 + c8);
+        const uint32_t rw[4] = {rr.x, rr.y, rr.z, rr.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v[2 * e] += bf2f((uint16_t)(rw[e] & 0xffff));
+          v[2 * e + 1] += bf2f((uint16_t)(rw[e] >> 16));
+        }
+      }
+      uint4 o;
+      o.x = f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+      o.y = f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+      o.z = f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+      o.w = f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      *(uint4*)(ep.out + gm * ep.ldo + n0 + c8) = o;
+    }
+  } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
+    // block columns: [up 0..63 | gate 0..63] of output columns nt*64 + 0..63
+#pragma unroll
+    for (int it = 0; it < (BM * 64 / 8) / kThreads; ++it) {
+      const int q = tid + it * kThreads;
+      const int row = q >> 3, c8 = (q & 7) * 8;
+      const long gm = m0 + row;
+      if (gm >= ep.M) continue;
+      float o[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float up = E[row * kEpiStride + c8 + e];
+        const float g = E[row * kEpiStride + 64 + c8 + e];
+        o[e] = up * (g / (1.f + __expf(-g)));
+      }
+      uint4 w;
+      w.x = f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
+      w.y = f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
+      w.z = f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
+      w.w = f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+      *(uint4*)(ep.out + gm * ep.ldo + (long)nt * 64 + c8) = w;
+    }
+  } else if constexpr (MODE == NOMIC_EPI_ROPE) {
+    // two 64-wide heads per block; NEOX rotation pairs (d, d + 32)
+#pragma unroll
+    for (int it = 0; it < (BM * 2 * 4) / kThreads; ++it) {
+      const int q = tid + it * kThreads;
+      const int row = q >> 3, head = (q >> 2) & 1, d0 = (q & 3) * 8;
+      const long gm = m0 + row;
+      if (gm >= ep.M) continue;
+      const int cb = head * 64;
+      const long gcol = n0 + cb;
+      float x1[8], x2[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        x1[e] = E[row * kEpiStride + cb + d0 + e];
+        x2[e] = E[row * kEpiStride + cb + d0 + 32 + e];
+      }
+      if (gcol < ep.rope_cols) {
+        const float* cs = ep.rope + (long)ep.pos[gm] * 64 + d0 * 2;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const float c = cs[2 * e], s = cs[2 * e + 1];
+          const float a = x1[e], b = x2[e];
+          x1[e] = a * c - b * s;
+          x2[e] = b * c + a * s;
+        }
+      }
+      uint4 w1, w2;
+      w1.x = f2bf(x1[0]) | ((uint32_t)f2bf(x1[1]) << 16);
+      w1.y = f2bf(x1[2]) | ((uint32_t)f2bf(x1[3]) << 16);
+      w1.z = f2bf(x1[4]) | ((uint32_t)f2bf(x1[5]) << 16);
+      w1.w = f2bf(x1[6]) | ((uint32_t)f2bf(x1[7]) << 16);
+      w2.x = f2bf(x2[0]) | ((uint32_t)f2bf(x2[1]) << 16);
+      w2.y = f2bf(x2[2]) | ((uint32_t)f2bf(x2[3]) << 16);
+      w2.z = f2bf(x2[4]) | ((uint32_t)f2bf(x2[5]) << 16);
+      w2.w = f2bf(x2[6]) | ((uint32_t)f2bf(x2[7]) << 16);
+      *(uint4*)(ep.out + gm * ep.ldo + gcol + d0) = w1;
+      *(uint4*)(ep.out + gm * ep.ldo + gcol + d0 + 32) = w2;
+    }
+  } else if constexpr (MODE == NOMIC_EPI_F32) {
+    float* outf = (float*)ep.out;
+#pragma unroll
+    for (int it = 0; it < (BM * BN / 4) / kThreads; ++it) {
+      const int q = tid + it * kThreads;
+      const int row = q >> 5, c4 = (q & 31) * 4;
+      const long gm = m0 + row;
+      if (gm >= ep.M) continue;
+      *(float4*)(outf + gm * ep.ldo + n0 + c4) = *(const float4*)&E[row * kEpiStride + c4];
+    }
+  }
+}
+
+template <int MODE>
+int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int N, int K, const EpiArgs& ep,
+           hipStream_t s) {
+  if (K % BK || N % BN || M <= 0) return (int)hipErrorInvalidValue;
+  const int mtiles = (int)((M + BM - 1) / BM), ntiles = N / BN;
+  hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), kLdsBytes, s, A, lda, W, ldw, K, mtiles,
+                     ntiles, ep);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" int nomic_gemm(int mode, const void* A, long lda, const void* W, long ldw, long M, int N, int K, void* out,
+                          long ldo, const void* res, long ldr, const float* rope, const int32_t* pos, int rope_cols,
+                          hipStream_t s) {
+  EpiArgs ep{(uint16_t*)out, ldo, (const uint16_t*)res, ldr, rope, pos, rope_cols, M};
+  const auto* a = (const uint16_t*)A;
+  const auto* w = (const uint16_t*)W;
+  switch (mode) {
+    case NOMIC_EPI_STORE: return launch<NOMIC_EPI_STORE>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_RESIDUAL: return launch<NOMIC_EPI_RESIDUAL>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_SWIGLU: return launch<NOMIC_EPI_SWIGLU>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_ROPE: return launch<NOMIC_EPI_ROPE>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_F32: return launch<NOMIC_EPI_F32>(a, lda, w, ldw, M, N, K, ep, s);
+    default: return (int)hipErrorInvalidValue;
+  }
+}

@@ -1,0 +1,461 @@
+// nomic_kernels.hip — the non-GEMM kernels of the Nomic-BERT encoder on
+// gfx950 (K11, K14, K17 of SURVEY §2.10) plus GGUF dequantisation.
+//
+//   nomic_embed_ln   token gather + token-type row + LayerNorm       (K11)
+//   nomic_layernorm  post-LN after each residual GEMM                (K15/K16 tail)
+//   nomic_attention  varlen non-causal flash attention, head dim 64  (K14)
+//   nomic_mean_pool  per-sequence mean -> fp32, optionally written
+//                    straight into arena slots under the seqlock     (K17 + K9)
+//   nomic_dequant    GGUF F32/F16/BF16/Q8_0/Q4_0/Q4_1/Q4_K/Q6_K -> bf16
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "arena_dev.hpp"
+#include "nomic_api.h"
+
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int D = 768;
+
+__device__ __forceinline__ float bf2f(uint32_t h16) { return __uint_as_float(h16 << 16); }
+__device__ __forceinline__ uint32_t f2bf(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0xffff) ? 0x40u : 0u);
+  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+}
+__device__ __forceinline__ void unpack8(uint4 v, float* f) {
+  f[0] = bf2f(v.x & 0xffff); f[1] = bf2f(v.x >> 16);
+  f[2] = bf2f(v.y & 0xffff); f[3] = bf2f(v.y >> 16);
+  f[4] = bf2f(v.z & 0xffff); f[5] = bf2f(v.z >> 16);
+  f[6] = bf2f(v.w & 0xffff); f[7] = bf2f(v.w >> 16);
+}
+__device__ __forceinline__ uint4 pack8(const float* f) {
+  return make_uint4(f2bf(f[0]) | (f2bf(f[1]) << 16), f2bf(f[2]) | (f2bf(f[3]) << 16),
+                    f2bf(f[4]) | (f2bf(f[5]) << 16), f2bf(f[6]) | (f2bf(f[7]) << 16));
+}
+
+// ------------------------------------------------------------ LayerNorm --
+// 32 lanes per row (half a wave), 24 elements = 3 x 16-B per lane; two-pass
+// statistics from registers.  256-thread blocks = 8 rows.
+template <bool EMBED>
+__global__ __launch_bounds__(256) void k_ln(const uint16_t* __restrict__ x, const int32_t* __restrict__ ids, long T,
+                                            const uint16_t* __restrict__ tok, const uint16_t* __restrict__ type_row,
+                                            const uint16_t* __restrict__ g, const uint16_t* __restrict__ b, float eps,
+                                            uint16_t* __restrict__ out) {
+  const long row = blockIdx.x * 8L + (threadIdx.x >> 5);
+  const int l = threadIdx.x & 31;
+  if (row >= T) return;
+  const uint16_t* src = EMBED ? tok + (long)ids[row] * D : x + row * D;
+  float v[24];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = (c * 32 + l) * 8;
+    unpack8(*(const uint4*)(src + col), v + 8 * c);
+    if (EMBED) {
+      float t[8];
+      unpack8(*(const uint4*)(type_row + col), t);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[8 * c + e] += t[e];
+    }
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < 24; ++e) s += v[e];
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) s += __shfl_xor(s, o, 32);
+  const float mean = s * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int e = 0; e < 24; ++e) { const float d = v[e] - mean; q += d * d; }
+#pragma unroll
+  for (int o = 16; o > 0; o >>= 1) q += __shfl_xor(q, o, 32);
+  const float rstd = rsqrtf(q * (1.f / D) + eps);
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int col = (c * 32 + l) * 8;
+    float gg[8], bb[8], o8[8];
+    unpack8(*(const uint4*)(g + col), gg);
+    unpack8(*(const uint4*)(b + col), bb);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o8[e] = (v[8 * c + e] - mean) * rstd * gg[e] + bb[e];
+    *(uint4*)(out + row * D + col) = pack8(o8);
+  }
+}
+
+// ------------------------------------------------------------ attention --
+// One workgroup = 64 query rows of one (sequence, head); 4 waves x 16 rows.
+// Per 64-key tile: S = Q K^T (8 x mfma 16x16x32), online softmax in fp32
+// (exp2 with the scale folded in), P -> LDS (bf16) -> A operand, O += P V
+// with V staged transposed in LDS so the B fragment is one 16-B read.
+constexpr int AQ = 64, AK = 64, HD = 64;
+
+__global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                              const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
+                                              int heads, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) uint16_t Ks[AK * HD];   // [key][d], 16-B chunks xor-swizzled
+  __shared__ __attribute__((aligned(16))) uint16_t Vt[HD * AK];   // [d][key], 16-B chunks xor-swizzled
+  __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * AK];  // per wave [q][key]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int seq = qblocks[2 * blockIdx.x], qstart = qblocks[2 * blockIdx.x + 1];
+  const int head = blockIdx.y;
+  const long s0 = cu[seq], len = cu[seq + 1] - s0;
+  const long ld = 3L * heads * HD;
+  const uint16_t* Qg = qkv + head * HD;
+  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
+  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
+
+  const int fr = lane & 15, fq = lane >> 4;
+  // Q fragments (A operand): row = fr, d = kk*32 + 8*fq
+  const long qrow = qstart + wave * 16 + fr;
+  bf16x8 qa[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+    if (qrow < len) qa[kk] = *(const bf16x8*)(Qg + (s0 + qrow) * ld + kk * 32 + fq * 8);
+    else qa[kk] = bf16x8{};
+  }
+  f32x4 o[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[4], lsum[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) { m[r] = -1e30f; lsum[r] = 0.f; }
+
+  for (long k0 = 0; k0 < len; k0 += AK) {
+    __syncthreads();  // previous tile fully consumed
+    // stage K (row-major, swizzled) and V^T: 512 16-B chunks each, 2 per thread
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int q = tid + it * 256;
+      const int key = q >> 3, ch = q & 7;
+      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
+      if (k0 + key < len) {
+        kv = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
+        vv = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
+      }
+      *(uint4*)(Ks + key * HD + ((ch ^ (key & 7)) << 3)) = kv;
+      const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int d = ch * 8 + e;
+        const uint16_t val = (uint16_t)((e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffff));
+        const int kc = key >> 3;  // 16-B chunk of keys within the d-row
+        Vt[d * AK + (((kc ^ (d & 7)) << 3) | (key & 7))] = val;
+      }
+    }
+    __syncthreads();
+    // S = Q K^T : 4 key sub-tiles x 2 d-steps
+    f32x4 s[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int key = j * 16 + fr;
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const int ch = kk * 4 + fq;
+        const bf16x8 kb = *(const bf16x8*)(Ks + key * HD + ((ch ^ (key & 7)) << 3));
+        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[kk], kb, s[j], 0, 0, 0);
+      }
+    }
+    // online softmax: rows (fq*4 + r), key col j*16 + fr
+    float rmax[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float mx = -1e30f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const bool valid = k0 + j * 16 + fr < len;
+        const float v = valid ? s[j][r] * scale_log2 : -1e30f;
+        s[j][r] = v;
+        mx = fmaxf(mx, v);
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
+      rmax[r] = mx;
+    }
+    float alpha[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float mn = fmaxf(m[r], rmax[r]);
+      alpha[r] = exp2f(m[r] - mn);
+      m[r] = mn;
+      float ps = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = exp2f(s[j][r] - mn);
+        s[j][r] = p;
+        ps += p;
+      }
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) ps += __shfl_xor(ps, off, 64);
+      lsum[r] = lsum[r] * alpha[r] + ps;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
+    // P -> LDS (bf16), per wave [16 q][64 keys], 16-B chunks swizzled by row
+    uint16_t* P = Ps[wave];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = fq * 4 + r, key = j * 16 + fr;
+        P[row * AK + ((((key >> 3) ^ (row & 7)) << 3) | (key & 7))] = (uint16_t)f2bf(s[j][r]);
+      }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed
+    __builtin_amdgcn_wave_barrier();
+    // O += P V : A = P[q = fr][key = kk*32 + 8 fq ..], B = V[key][d = j*16 + fr]
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int ch = kk * 4 + fq;
+      const bf16x8 pa = *(const bf16x8*)(P + fr * AK + ((ch ^ (fr & 7)) << 3));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int d = j * 16 + fr;
+        const bf16x8 vb = *(const bf16x8*)(Vt + d * AK + ((ch ^ (d & 7)) << 3));
+        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[j], 0, 0, 0);
+      }
+    }
+  }
+  // normalise and store: row q = fq*4 + r, col d = j*16 + fr
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const long q = qstart + wave * 16 + fq * 4 + r;
+    if (q >= len) continue;
+    const float inv = 1.f / lsum[r];
+    uint16_t* dst = out + (s0 + q) * (long)heads * HD + head * HD;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dst[j * 16 + fr] = (uint16_t)f2bf(o[j][r] * inv);
+  }
+}
+
+// ------------------------------------------------------------ mean pool --
+__global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, const int32_t* __restrict__ cu,
+                                              float* __restrict__ pooled, int normalize, spl_arena_t aa,
+                                              const int64_t* __restrict__ slots, const uint64_t* __restrict__ hashes,
+                                              int32_t* __restrict__ status) {
+  __shared__ float part[4][D];
+  __shared__ float vec[D];
+  __shared__ float red[4];
+  __shared__ int lock_ok;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const long t0 = cu[b], t1 = cu[b + 1];
+  float acc[12];
+#pragma unroll
+  for (int e = 0; e < 12; ++e) acc[e] = 0.f;
+  // lane covers columns [lane*8, +8) and [512 + lane*4, +4)
+  for (long t = t0 + wave; t < t1; t += 4) {
+    const uint16_t* row = x + t * D;
+    float f[8];
+    unpack8(*(const uint4*)(row + lane * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] += f[e];
+    const uint2 h = *(const uint2*)(row + 512 + lane * 4);
+    acc[8] += bf2f(h.x & 0xffff); acc[9] += bf2f(h.x >> 16);
+    acc[10] += bf2f(h.y & 0xffff); acc[11] += bf2f(h.y >> 16);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) part[wave][lane * 8 + e] = acc[e];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) part[wave][512 + lane * 4 + e] = acc[8 + e];
+  __syncthreads();
+  const float inv = t1 > t0 ? 1.f / (float)(t1 - t0) : 0.f;
+  float ss = 0.f;
+  for (int c = tid; c < D; c += 256) {
+    const float v = (part[0][c] + part[1][c] + part[2][c] + part[3][c]) * inv;
+    vec[c] = v;
+    ss += v * v;
+  }
+  if (normalize) {
+    for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+    if (lane == 0) red[wave] = ss;
+  }
+  __syncthreads();
+  const float scale = normalize ? rsqrtf(fmaxf(red[0] + red[1] + red[2] + red[3], 1e-24f)) : 1.f;
+  if (pooled)
+    for (int c = tid; c < D; c += 256) pooled[(long)b * D + c] = vec[c] * scale;
+  if (!slots) return;
+  // fused write-back into the arena slot (seqlock), reference set_embedding
+  // semantics (/root/reference/splinter.c:567-588): CAS even->odd, copy, +1.
+  using namespace spl;
+  using namespace spl::dev;
+  Arena a{(uint8_t*)aa.base, aa.slots, aa.max_val, aa.stride, aa.flags};
+  const int64_t si = slots[b];
+  if (tid == 0) {
+    int ok = 0;
+    if (si >= 0 && a.stride == kSlotEmbedBytes) {
+      uint8_t* s = a.slot((size_t)si);
+      const uint64_t e = slot_epoch(s);
+      if (!(e & 1) && acas64(epoch_ptr(s), e, e + 1)) {
+        if (slot_hash(s) == hashes[b]) ok = 1;
+        else { aadd64(epoch_ptr(s), 1); ok = -2; }
+      } else {
+        ok = -11;
+      }
+    } else {
+      ok = -2;
+    }
+    lock_ok = ok;
+  }
+  __syncthreads();
+  if (lock_ok == 1) {
+    float* dst = (float*)(a.slot((size_t)si) + kOffEmbed);
+    for (int c = tid; c < D; c += 256) dst[c] = vec[c] * scale;
+    release();
+    __syncthreads();
+    if (tid == 0) {
+      aadd64(epoch_ptr(a.slot((size_t)si)), 1);
+      aadd64(&a.hdr()->epoch, 1);
+      mark_dirty(a, (size_t)si);
+    }
+  }
+  if (tid == 0 && status) status[b] = lock_ok == 1 ? 0 : lock_ok;
+}
+
+// ------------------------------------------------------------ dequant ----
+__device__ __forceinline__ float h2f(uint16_t h) { return (float)__builtin_bit_cast(_Float16, h); }
+
+// one thread per 32-element block (legacy quants) / per 32 elements of a k-quant superblock
+__global__ void k_dequant(int type, const uint8_t* __restrict__ src, long nblk, uint16_t* __restrict__ dst) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < nblk; i += (long)gridDim.x * blockDim.x) {
+    float y[32];
+    if (type == 8) {  // Q8_0: f16 d, int8 q[32]
+      const uint8_t* p = src + i * 34;
+      const float d = h2f(*(const uint16_t*)p);
+#pragma unroll
+      for (int e = 0; e < 32; ++e) y[e] = d * (float)(int8_t)p[2 + e];
+    } else if (type == 2) {  // Q4_0: f16 d, 16 B nibbles (low -> 0..15, high -> 16..31)
+      const uint8_t* p = src + i * 18;
+      const float d = h2f(*(const uint16_t*)p);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        y[e] = d * (float)((int)(p[2 + e] & 15) - 8);
+        y[e + 16] = d * (float)((int)(p[2 + e] >> 4) - 8);
+      }
+    } else if (type == 3) {  // Q4_1: f16 d, f16 m, nibbles
+      const uint8_t* p = src + i * 20;
+      const float d = h2f(*(const uint16_t*)p), mn = h2f(*(const uint16_t*)(p + 2));
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        y[e] = d * (float)(p[4 + e] & 15) + mn;
+        y[e + 16] = d * (float)(p[4 + e] >> 4) + mn;
+      }
+    } else if (type == 12) {  // Q4_K: 256-element superblocks of 144 B, 8 sub-blocks of 32
+      const long sb = i >> 3;
+      const int j = (int)(i & 7);
+      const uint8_t* p = src + sb * 144;
+      const float d = h2f(*(const uint16_t*)p), dmin = h2f(*(const uint16_t*)(p + 2));
+      const uint8_t* sc = p + 4;
+      int s, mq;
+      if (j < 4) { s = sc[j] & 63; mq = sc[j + 4] & 63; }
+      else { s = (sc[j + 4] & 15) | ((sc[j - 4] >> 6) << 4); mq = (sc[j + 4] >> 4) | ((sc[j] >> 6) << 4); }
+      const uint8_t* q = p + 16 + (j >> 1) * 32;
+      const float dl = d * (float)s, ml = dmin * (float)mq;
+#pragma unroll
+      for (int e = 0; e < 32; ++e) y[e] = dl * (float)((j & 1) ? (q[e] >> 4) : (q[e] & 15)) - ml;
+    } else if (type == 14) {  // Q6_K: 210-B superblocks: ql[128] qh[64] scales[16] d
+      const long sb = i >> 3;
+      const int j = (int)(i & 7);  // 32-element group: half = j/4, quarter = j%4
+      const uint8_t* p = src + sb * 210;
+      const uint8_t* ql = p + (j >> 2) * 64;
+      const uint8_t* qh = p + 128 + (j >> 2) * 32;
+      const int8_t* scl = (const int8_t*)(p + 192) + (j >> 2) * 8;
+      const float d = h2f(*(const uint16_t*)(p + 208));
+      const int qd = j & 3;
+#pragma unroll
+      for (int e = 0; e < 32; ++e) {
+        const int byte = ql[e + 32 * (qd & 1)];
+        const int low = (qd >= 2) ? (byte >> 4) : (byte & 15);
+        const int hi = (qh[e] >> (2 * qd)) & 3;
+        const int q = (low | (hi << 4)) - 32;
+        y[e] = d * (float)scl[(e >> 4) + 2 * qd] * (float)q;
+      }
+    } else {
+      for (int e = 0; e < 32; ++e) y[e] = 0.f;
+    }
+    uint4* o = (uint4*)(dst + i * 32);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) o[c] = pack8(y + 8 * c);
+  }
+}
+
+// plain formats: one thread per 8 elements
+__global__ void k_convert(int type, const uint8_t* __restrict__ src, long n8, uint16_t* __restrict__ dst) {
+  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n8; i += (long)gridDim.x * blockDim.x) {
+    float y[8];
+    if (type == 0) {  // F32
+      const float4 a = ((const float4*)src)[2 * i], b = ((const float4*)src)[2 * i + 1];
+      y[0] = a.x; y[1] = a.y; y[2] = a.z; y[3] = a.w; y[4] = b.x; y[5] = b.y; y[6] = b.z; y[7] = b.w;
+    } else if (type == 1) {  // F16
+      const uint4 v = ((const uint4*)src)[i];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { y[2 * e] = h2f((uint16_t)(w[e] & 0xffff)); y[2 * e + 1] = h2f((uint16_t)(w[e] >> 16)); }
+    } else {  // BF16 (30)
+      ((uint4*)dst)[i] = ((const uint4*)src)[i];
+      continue;
+    }
+    ((uint4*)dst)[i] = pack8(y);
+  }
+}
+
+inline int grid_of(long n, int per) {
+  long g = (n + per - 1) / per;
+  return (int)(g < 1 ? 1 : (g > 4096 ? 4096 : g));
+}
+
+}  // namespace
+
+extern "C" {
+
+int nomic_embed_ln(const int32_t* ids, long T, const void* tok, const void* type_row, const void* gamma,
+                   const void* beta, float eps, void* out, hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_ln<true>, dim3((unsigned)((T + 7) / 8)), dim3(256), 0, s, nullptr, ids, T,
+                     (const uint16_t*)tok, (const uint16_t*)type_row, (const uint16_t*)gamma, (const uint16_t*)beta,
+                     eps, (uint16_t*)out);
+  return (int)hipGetLastError();
+}
+
+int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, float eps, void* out, hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(k_ln<false>, dim3((unsigned)((T + 7) / 8)), dim3(256), 0, s, (const uint16_t*)x, nullptr, T,
+                     nullptr, nullptr, (const uint16_t*)gamma, (const uint16_t*)beta, eps, (uint16_t*)out);
+  return (int)hipGetLastError();
+}
+
+int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t* qblocks, int nqb, int heads,
+                    float scale, hipStream_t s) {
+  if (nqb <= 0) return 0;
+  const float scale_log2 = scale * 1.4426950408889634f;
+  hipLaunchKernelGGL(k_attn, dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks,
+                     heads, scale_log2);
+  return (int)hipGetLastError();
+}
+
+int nomic_mean_pool(const void* x, const int32_t* cu, int B, float* pooled, int normalize, spl_arena_t arena,
+                    const int64_t* slots, const uint64_t* hashes, int32_t* status, hipStream_t s) {
+  if (B <= 0) return 0;
+  hipLaunchKernelGGL(k_pool, dim3(B), dim3(256), 0, s, (const uint16_t*)x, cu, pooled, normalize, arena, slots, hashes,
+                     status);
+  return (int)hipGetLastError();
+}
+
+int nomic_dequant(int type, const void* src, long n, void* dst, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (type == 0 || type == 1 || type == 30) {
+    if (n % 8) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_convert, dim3(grid_of(n / 8, 256)), dim3(256), 0, s, type, (const uint8_t*)src, n / 8,
+                       (uint16_t*)dst);
+  } else {
+    if (n % 32) return (int)hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_dequant, dim3(grid_of(n / 32, 256)), dim3(256), 0, s, type, (const uint8_t*)src, n / 32,
+                       (uint16_t*)dst);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -1,0 +1,48 @@
+/*
+ * nomic_api.h — C launch API of the Nomic-BERT encoder kernels (gfx950).
+ * All tensors are device pointers, bf16 stored as uint16.  Row counts that
+ * feed nomic_gemm must be padded to a multiple of 128 in the A buffer.
+ */
+#ifndef SPLINTER_NOMIC_API_H
+#define SPLINTER_NOMIC_API_H
+#include <stdint.h>
+#include "arena_api.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* GEMM epilogues */
+#define NOMIC_EPI_STORE    0   /* out = bf16(acc)                                   */
+#define NOMIC_EPI_RESIDUAL 1   /* out = bf16(acc + res)                             */
+#define NOMIC_EPI_SWIGLU   2   /* W rows interleaved [up64|gate64]: out = up*silu(gate) */
+#define NOMIC_EPI_ROPE     3   /* qkv projection with NEOX RoPE on cols < rope_cols  */
+#define NOMIC_EPI_F32      4   /* out = acc as fp32                                 */
+
+int nomic_gemm(int mode, const void *A, long lda, const void *W, long ldw, long M, int N, int K,
+               void *out, long ldo, const void *res, long ldr, const float *rope, const int32_t *pos,
+               int rope_cols, hipStream_t stream);
+
+/* x[t] = LN(tok[ids[t]] + type_row) ; bf16 out [T, 768] */
+int nomic_embed_ln(const int32_t *ids, long T, const void *tok_emb, const void *type_row,
+                   const void *gamma, const void *beta, float eps, void *out, hipStream_t stream);
+/* in-place (or out-of-place) LayerNorm over 768 columns, bf16 */
+int nomic_layernorm(const void *x, long T, const void *gamma, const void *beta, float eps, void *out,
+                    hipStream_t stream);
+/* varlen non-causal attention; qkv [T, 3*H*64] (q|k|v), out [T, H*64].
+ * qblocks: [nqb] int32 pairs (seq index, q start offset in the sequence)  */
+int nomic_attention(const void *qkv, void *out, const int32_t *cu_seqlens, const int32_t *qblocks,
+                    int nqb, int heads, float scale, hipStream_t stream);
+/* mean over each sequence's tokens -> fp32 [B, 768]; if slots != NULL also
+ * write each vector into arena slot slots[b] (>= 0) under the seqlock, after
+ * checking the slot still holds hashes[b]; status[b] gets 0 / -11 / -2.     */
+int nomic_mean_pool(const void *x, const int32_t *cu_seqlens, int B, float *pooled, int normalize,
+                    spl_arena_t arena, const int64_t *slots, const uint64_t *hashes, int32_t *status,
+                    hipStream_t stream);
+/* GGUF tensor dequantisation to bf16 (ggml type ids) */
+int nomic_dequant(int ggml_type, const void *src, long nelems, void *dst_bf16, hipStream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,373 @@
+"""Nomic-BERT (nomic-embed-text-v1.5 architecture) on hand-written gfx950 kernels.
+
+Replaces the llama.cpp decode used by the reference embedding daemon
+(/root/reference/splinference.cpp:196-287: one sequence per llama_decode, mean
+pooling forced at :431-437) with a batched, varlen, bf16 encoder:
+
+  embed+LN  ->  12 x [ QKV GEMM (+RoPE epilogue) -> flash attention ->
+                       O-proj GEMM (+residual epilogue) -> LN ->
+                       up|gate GEMM (+SwiGLU epilogue) -> down GEMM (+residual) -> LN ]
+  -> mean pool -> (optionally) vectors written straight into arena slots.
+
+Architecture facts (GGUF arch "nomic-bert", SURVEY §2.12, re-checked from the
+GGUF metadata at load): 12 layers, d=768, 12 heads x 64, SwiGLU MLP 3072,
+NEOX rotary (base 1000) on q/k, post-LayerNorm (eps 1e-12), non-causal,
+token-type row 0 added to the token embedding, no absolute positions.
+
+``NomicReference`` is an independent fp32 PyTorch implementation used as the
+numerics oracle in tests (the HF remote code is not available offline).
+"""
+from __future__ import annotations
+
+import ctypes
+import math
+import os
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .. import _native as N
+from .gguf import DEVICE_DEQUANT, GGUFFile, GGUFWriter, dequant_host
+
+EPI_STORE, EPI_RESIDUAL, EPI_SWIGLU, EPI_ROPE, EPI_F32 = 0, 1, 2, 3, 4
+
+
+@dataclass
+class NomicConfig:
+    vocab: int = 30528
+    d: int = 768
+    layers: int = 12
+    heads: int = 12
+    ffn: int = 3072
+    eps: float = 1e-12
+    rope_base: float = 1000.0
+    n_ctx: int = 2048
+    type_vocab: int = 2
+
+    @property
+    def head_dim(self) -> int:
+        return self.d // self.heads
+
+    @classmethod
+    def from_gguf(cls, g: GGUFFile) -> "NomicConfig":
+        a = g.arch() or "nomic-bert"
+        get = lambda k, d: g.get(f"{a}.{k}", d)  # noqa: E731
+        tok = g.tensors.get("token_embd.weight")
+        return cls(vocab=tok.shape[0] if tok else 30528, d=int(get("embedding_length", 768)),
+                   layers=int(get("block_count", 12)), heads=int(get("attention.head_count", 12)),
+                   ffn=int(get("feed_forward_length", 3072)), eps=float(get("attention.layer_norm_epsilon", 1e-12)),
+                   rope_base=float(get("rope.freq_base", 1000.0)), n_ctx=int(get("context_length", 2048)))
+
+
+def _lib():
+    L = N.hip_lib()
+    if not getattr(L, "_nomic_declared", False):
+        P, c_long, c_int, c_float = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float
+        L.nomic_gemm.argtypes = [c_int, P, c_long, P, c_long, c_long, c_int, c_int, P, c_long, P, c_long, P, P, c_int, P]
+        L.nomic_gemm.restype = c_int
+        L.nomic_embed_ln.argtypes = [P, c_long, P, P, P, P, c_float, P, P]
+        L.nomic_embed_ln.restype = c_int
+        L.nomic_layernorm.argtypes = [P, c_long, P, P, c_float, P, P]
+        L.nomic_layernorm.restype = c_int
+        L.nomic_attention.argtypes = [P, P, P, P, c_int, c_int, c_float, P]
+        L.nomic_attention.restype = c_int
+        L.nomic_mean_pool.argtypes = [P, P, c_int, P, c_int, N.Arena, P, P, P, P]
+        L.nomic_mean_pool.restype = c_int
+        L.nomic_dequant.argtypes = [c_int, P, c_long, P, P]
+        L.nomic_dequant.restype = c_int
+        L._nomic_declared = True
+    return L
+
+
+def _chk(rc, what):
+    if rc != 0:
+        raise RuntimeError(f"{what}: HIP launch failed ({rc})")
+
+
+def _stream():
+    return torch.cuda.current_stream().cuda_stream
+
+
+# ================================================================ weights ==
+GGUF_NAMES = {
+    "tok": "token_embd.weight", "type": "token_types.weight",
+    "emb_g": "token_embd_norm.weight", "emb_b": "token_embd_norm.bias",
+}
+LAYER_NAMES = {
+    "wqkv": "attn_qkv.weight", "wo": "attn_output.weight",
+    "ln1_g": "attn_output_norm.weight", "ln1_b": "attn_output_norm.bias",
+    "wup": "ffn_up.weight", "wgate": "ffn_gate.weight", "wdown": "ffn_down.weight",
+    "ln2_g": "layer_output_norm.weight", "ln2_b": "layer_output_norm.bias",
+}
+
+
+def random_weights(cfg: NomicConfig, seed: int = 0, std: float = 0.02) -> Dict[str, np.ndarray]:
+    """Random-init fp32 weights in GGUF (numpy) orientation: linear = [out, in]."""
+    rng = np.random.default_rng(seed)
+    f = lambda *s: (rng.standard_normal(s) * std).astype(np.float32)  # noqa: E731
+    w = {GGUF_NAMES["tok"]: f(cfg.vocab, cfg.d), GGUF_NAMES["type"]: f(cfg.type_vocab, cfg.d),
+         GGUF_NAMES["emb_g"]: (1 + f(cfg.d) * 5).astype(np.float32), GGUF_NAMES["emb_b"]: f(cfg.d)}
+    for i in range(cfg.layers):
+        p = f"blk.{i}."
+        w[p + "attn_qkv.weight"] = f(3 * cfg.d, cfg.d)
+        w[p + "attn_output.weight"] = f(cfg.d, cfg.d)
+        w[p + "attn_output_norm.weight"] = (1 + f(cfg.d) * 5).astype(np.float32)
+        w[p + "attn_output_norm.bias"] = f(cfg.d)
+        w[p + "ffn_up.weight"] = f(cfg.ffn, cfg.d)
+        w[p + "ffn_gate.weight"] = f(cfg.ffn, cfg.d)
+        w[p + "ffn_down.weight"] = f(cfg.d, cfg.ffn)
+        w[p + "layer_output_norm.weight"] = (1 + f(cfg.d) * 5).astype(np.float32)
+        w[p + "layer_output_norm.bias"] = f(cfg.d)
+    return w
+
+
+def write_gguf(path: str, cfg: NomicConfig, weights: Dict[str, np.ndarray], vocab: Optional[List[str]] = None,
+               linear_type: str = "F16") -> None:
+    """Write a nomic-bert GGUF (linears in `linear_type`, norms/embeddings F32/F16)."""
+    w = GGUFWriter(path, "nomic-bert")
+    a = "nomic-bert"
+    w.add("general.name", "nomic-embed-text-v1.5 (random init)")
+    w.add(f"{a}.context_length", cfg.n_ctx)
+    w.add(f"{a}.embedding_length", cfg.d)
+    w.add(f"{a}.feed_forward_length", cfg.ffn)
+    w.add(f"{a}.attention.head_count", cfg.heads)
+    w.add(f"{a}.attention.layer_norm_epsilon", float(cfg.eps))
+    w.add(f"{a}.block_count", cfg.layers)
+    w.add(f"{a}.rope.freq_base", float(cfg.rope_base))
+    w.add(f"{a}.attention.causal", False)
+    w.add(f"{a}.pooling_type", 1)
+    if vocab is not None:
+        w.add("tokenizer.ggml.model", "bert")
+        w.add("tokenizer.ggml.tokens", vocab)
+        w.add("tokenizer.ggml.token_type", [1] * len(vocab))
+        ids = {t: i for i, t in enumerate(vocab)}
+        for key, tok in (("bos", "[CLS]"), ("eos", "[SEP]"), ("seperator", "[SEP]"), ("unknown", "[UNK]"),
+                         ("padding", "[PAD]")):
+            if tok in ids:
+                w.add(f"tokenizer.ggml.{key}_token_id", ids[tok])
+    for name, arr in weights.items():
+        lin = arr.ndim == 2 and not name.startswith("token_")
+        w.add_tensor(name, arr, linear_type if lin else ("F16" if name == "token_embd.weight" else "F32"))
+    w.write()
+
+
+class NomicWeights:
+    """Device-resident bf16 weights in kernel layout."""
+
+    def __init__(self, cfg: NomicConfig, tensors: Dict[str, torch.Tensor], device="cuda"):
+        self.cfg = cfg
+        bf = lambda t: t.to(device=device, dtype=torch.bfloat16).contiguous()  # noqa: E731
+        self.tok = bf(tensors[GGUF_NAMES["tok"]])
+        self.type_row = bf(tensors[GGUF_NAMES["type"]][0])
+        self.emb_g, self.emb_b = bf(tensors[GGUF_NAMES["emb_g"]]), bf(tensors[GGUF_NAMES["emb_b"]])
+        self.layers = []
+        for i in range(cfg.layers):
+            p = f"blk.{i}."
+            t = {k: tensors[p + v] for k, v in LAYER_NAMES.items()}
+            up, gate = t["wup"], t["wgate"]
+            # SwiGLU epilogue layout: per 64 output columns, [up 64 | gate 64]
+            ug = torch.stack([up.reshape(-1, 64, cfg.d), gate.reshape(-1, 64, cfg.d)], dim=1).reshape(-1, cfg.d)
+            self.layers.append({
+                "wqkv": bf(t["wqkv"]), "wo": bf(t["wo"]), "wupgate": bf(ug), "wdown": bf(t["wdown"]),
+                "ln1_g": bf(t["ln1_g"]), "ln1_b": bf(t["ln1_b"]), "ln2_g": bf(t["ln2_g"]), "ln2_b": bf(t["ln2_b"]),
+            })
+
+    @classmethod
+    def from_numpy(cls, cfg, weights: Dict[str, np.ndarray], device="cuda"):
+        return cls(cfg, {k: torch.from_numpy(v) for k, v in weights.items()}, device)
+
+    @classmethod
+    def from_gguf(cls, g: GGUFFile, cfg: Optional[NomicConfig] = None, device="cuda"):
+        cfg = cfg or NomicConfig.from_gguf(g)
+        L = _lib()
+        out = {}
+        for name, info in g.tensors.items():
+            if info.ggml_type in DEVICE_DEQUANT:
+                raw = torch.from_numpy(np.ascontiguousarray(g.raw(name))).to(device)
+                dst = torch.empty(info.nelems, dtype=torch.bfloat16, device=device)
+                _chk(L.nomic_dequant(info.ggml_type, raw.data_ptr(), info.nelems, dst.data_ptr(), _stream()),
+                     f"dequant {name}")
+                out[name] = dst.view(info.shape)
+            else:
+                out[name] = torch.from_numpy(dequant_host(g.raw(name), info.ggml_type, info.nelems)
+                                             .reshape(info.shape)).to(device)
+        return cls(cfg, out, device)
+
+
+# ============================================================== reference ==
+class NomicReference(torch.nn.Module):
+    """Plain fp32 PyTorch nomic-bert forward (oracle for kernel numerics)."""
+
+    def __init__(self, cfg: NomicConfig, weights: Dict[str, np.ndarray], device="cpu"):
+        super().__init__()
+        self.cfg = cfg
+        self.w = {k: torch.from_numpy(np.asarray(v, np.float32)).to(device) for k, v in weights.items()}
+
+    def rope(self, x, pos):  # x [T, H, 64]
+        hd = self.cfg.head_dim
+        inv = self.cfg.rope_base ** (-torch.arange(0, hd, 2, dtype=torch.float64, device=x.device) / hd)
+        ang = pos[:, None].double() * inv[None, :]
+        c, s = torch.cos(ang).float()[:, None, :], torch.sin(ang).float()[:, None, :]
+        x1, x2 = x[..., : hd // 2], x[..., hd // 2:]
+        return torch.cat([x1 * c - x2 * s, x2 * c + x1 * s], dim=-1)
+
+    def forward(self, ids: torch.Tensor, cu: Sequence[int]) -> torch.Tensor:
+        cfg, w = self.cfg, self.w
+        F = torch.nn.functional
+        x = w["token_embd.weight"][ids] + w["token_types.weight"][0]
+        x = F.layer_norm(x, (cfg.d,), w["token_embd_norm.weight"], w["token_embd_norm.bias"], cfg.eps)
+        pos = torch.cat([torch.arange(cu[i + 1] - cu[i]) for i in range(len(cu) - 1)]).to(ids.device)
+        H, hd = cfg.heads, cfg.head_dim
+        for i in range(cfg.layers):
+            p = f"blk.{i}."
+            qkv = x @ w[p + "attn_qkv.weight"].T
+            q, k, v = qkv.split(cfg.d, dim=1)
+            q = self.rope(q.view(-1, H, hd), pos)
+            k = self.rope(k.view(-1, H, hd), pos)
+            v = v.view(-1, H, hd)
+            outs = []
+            for s in range(len(cu) - 1):
+                a, b = cu[s], cu[s + 1]
+                att = torch.einsum("qhd,khd->hqk", q[a:b], k[a:b]) / math.sqrt(hd)
+                outs.append(torch.einsum("hqk,khd->qhd", att.softmax(-1), v[a:b]))
+            o = torch.cat(outs).reshape(-1, cfg.d)
+            x = F.layer_norm(o @ w[p + "attn_output.weight"].T + x, (cfg.d,), w[p + "attn_output_norm.weight"],
+                             w[p + "attn_output_norm.bias"], cfg.eps)
+            up = x @ w[p + "ffn_up.weight"].T
+            gate = x @ w[p + "ffn_gate.weight"].T
+            h = (up * F.silu(gate)) @ w[p + "ffn_down.weight"].T
+            x = F.layer_norm(h + x, (cfg.d,), w[p + "layer_output_norm.weight"], w[p + "layer_output_norm.bias"],
+                             cfg.eps)
+        return torch.stack([x[cu[s]: cu[s + 1]].mean(0) for s in range(len(cu) - 1)])
+
+
+# ================================================================ encoder ==
+class Batch:
+    """A packed varlen batch: token ids, sequence offsets, positions, q-blocks."""
+
+    def __init__(self, seqs: Sequence[Sequence[int]], device="cuda", qblock: int = 64):
+        lens = [len(s) for s in seqs]
+        assert all(n > 0 for n in lens), "empty sequence"
+        self.B = len(seqs)
+        self.T = sum(lens)
+        self.T_pad = (self.T + 127) // 128 * 128
+        self.cu_host = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+        self.max_len = max(lens)
+        ids = np.zeros(self.T_pad, np.int32)
+        ids[: self.T] = np.concatenate([np.asarray(s, np.int32) for s in seqs])
+        pos = np.zeros(self.T_pad, np.int32)
+        pos[: self.T] = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
+        qb = [(i, q0) for i, n in enumerate(lens) for q0 in range(0, n, qblock)]
+        self.nqb = len(qb)
+        self.ids = torch.from_numpy(ids).to(device)
+        self.pos = torch.from_numpy(pos).to(device)
+        self.cu = torch.from_numpy(self.cu_host).to(device)
+        self.qblocks = torch.tensor(qb, dtype=torch.int32).reshape(-1).to(device)
+
+
+class NomicEncoder:
+    """Batched bf16 forward on the gfx950 kernels (no torch compute in the hot path)."""
+
+    def __init__(self, weights: NomicWeights, max_tokens: int = 1 << 17):
+        self.w = weights
+        self.cfg = weights.cfg
+        self.L = _lib()
+        cfg = self.cfg
+        # RoPE table [n_pos][hd/2] of (cos, sin)
+        npos = max(cfg.n_ctx, 8192)
+        inv = cfg.rope_base ** (-np.arange(0, cfg.head_dim, 2, dtype=np.float64) / cfg.head_dim)
+        ang = np.arange(npos, dtype=np.float64)[:, None] * inv[None, :]
+        tab = np.stack([np.cos(ang), np.sin(ang)], axis=-1).astype(np.float32)
+        self.rope = torch.from_numpy(tab.reshape(npos, -1)).cuda()
+        self._ws_tokens = 0
+        self._ensure(max_tokens)
+
+    def _ensure(self, T_pad: int):
+        if T_pad <= self._ws_tokens:
+            return
+        cfg = self.cfg
+        e = dict(dtype=torch.bfloat16, device="cuda")
+        self.x = torch.empty((T_pad, cfg.d), **e)
+        self.h = torch.empty((T_pad, cfg.d), **e)
+        self.attn = torch.empty((T_pad, cfg.d), **e)
+        self.qkv = torch.empty((T_pad, 3 * cfg.d), **e)
+        self.ffn = torch.empty((T_pad, cfg.ffn), **e)
+        self._ws_tokens = T_pad
+
+    def _gemm(self, mode, A, W, M, out, res=None, pos=None):
+        N_, K = W.shape
+        _chk(self.L.nomic_gemm(mode, A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0), M,
+                               N_, K, out.data_ptr(), out.stride(0), res.data_ptr() if res is not None else None,
+                               res.stride(0) if res is not None else 0, self.rope.data_ptr(),
+                               pos.data_ptr() if pos is not None else None, 2 * self.cfg.d, _stream()), "gemm")
+
+    def hidden(self, b: Batch) -> torch.Tensor:
+        """Final-layer hidden states [T, 768] (bf16) for a packed batch."""
+        cfg, L, w = self.cfg, self.L, self.w
+        assert b.max_len <= self.rope.shape[0]
+        self._ensure(b.T_pad)
+        s = _stream()
+        T = b.T
+        x, h, attn, qkv, ffn = self.x, self.h, self.attn, self.qkv, self.ffn
+        _chk(L.nomic_embed_ln(b.ids.data_ptr(), T, w.tok.data_ptr(), w.type_row.data_ptr(), w.emb_g.data_ptr(),
+                              w.emb_b.data_ptr(), cfg.eps, x.data_ptr(), s), "embed_ln")
+        scale = 1.0 / math.sqrt(cfg.head_dim)
+        for lw in w.layers:
+            self._gemm(EPI_ROPE, x, lw["wqkv"], T, qkv, pos=b.pos)
+            _chk(L.nomic_attention(qkv.data_ptr(), attn.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb,
+                                   cfg.heads, scale, s), "attention")
+            self._gemm(EPI_RESIDUAL, attn, lw["wo"], T, h, res=x)
+            _chk(L.nomic_layernorm(h.data_ptr(), T, lw["ln1_g"].data_ptr(), lw["ln1_b"].data_ptr(), cfg.eps,
+                                   x.data_ptr(), s), "ln1")
+            self._gemm(EPI_SWIGLU, x, lw["wupgate"], T, ffn)
+            self._gemm(EPI_RESIDUAL, ffn, lw["wdown"], T, h, res=x)
+            _chk(L.nomic_layernorm(h.data_ptr(), T, lw["ln2_g"].data_ptr(), lw["ln2_b"].data_ptr(), cfg.eps,
+                                   x.data_ptr(), s), "ln2")
+        return x[:T]
+
+    def embed(self, b: Batch, normalize: bool = False, arena=None, slots: Optional[torch.Tensor] = None,
+              hashes: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
+        """Mean-pooled [B, 768] fp32; with arena+slots the vectors are also written
+        into the arena slots under the seqlock (returns (vectors, status))."""
+        self.hidden(b)
+        if out is None:
+            out = torch.empty((b.B, self.cfg.d), dtype=torch.float32, device="cuda")
+        status = None
+        desc = N.Arena()
+        if arena is not None:
+            desc = arena.desc
+            status = torch.empty(b.B, dtype=torch.int32, device="cuda")
+        _chk(self.L.nomic_mean_pool(self.x.data_ptr(), b.cu.data_ptr(), b.B, out.data_ptr(), int(normalize), desc,
+                                    slots.data_ptr() if slots is not None else None,
+                                    hashes.data_ptr() if hashes is not None else None,
+                                    status.data_ptr() if status is not None else None, _stream()), "mean_pool")
+        return (out, status) if arena is not None else out
+
+    def flops(self, b: Batch) -> float:
+        cfg = self.cfg
+        lin = 2 * b.T * cfg.d * (3 * cfg.d + cfg.d + 2 * cfg.ffn + cfg.ffn) * cfg.layers
+        lens = np.diff(b.cu_host)
+        att = 4 * float((lens.astype(np.float64) ** 2).sum()) * cfg.d * cfg.layers
+        return lin + att
+
+
+def smoke_embed(arena, keys: torch.Tensor) -> None:
+    """Tiny end-to-end check used by __graft_entry__.smoke(): random-init
+    encoder embeds a few sequences straight into the arena slots."""
+    cfg = NomicConfig(layers=2)
+    w = NomicWeights.from_numpy(cfg, random_weights(cfg, seed=1))
+    enc = NomicEncoder(w, max_tokens=1024)
+    n = min(4, keys.shape[0])
+    rng = np.random.default_rng(0)
+    b = Batch([rng.integers(0, cfg.vocab, size=7 + 5 * i).tolist() for i in range(n)])
+    st, idx = arena.meta("find", keys[:n])
+    from ..parallel.sharded import GpuShard
+    hashes = GpuShard(arena).hash_keys(keys[:n])
+    vec, status = enc.embed(b, arena=arena, slots=idx, hashes=hashes)
+    torch.cuda.synchronize()
+    assert (status == 0).all(), status
+    st2, back = arena.get_embeddings(keys[:n])
+    assert torch.equal(back, vec), "slot vectors differ from pooled output"
+    assert torch.isfinite(vec).all()

@@ -40,6 +40,15 @@ def _check(rc: int, what: str) -> None:
         raise RuntimeError(f"{what}: HIP launch failed (hipError {rc})")
 
 
+def _keys(keys: torch.Tensor) -> torch.Tensor:
+    """Validate a key batch; strided views (e.g. K[::2]) are compacted first."""
+    if keys.dtype != torch.uint8 or keys.dim() != 2 or not keys.is_cuda:
+        raise TypeError("keys must be a CUDA uint8 tensor [n, kstride]")
+    if keys.shape[1] not in (16, 32, 48, 64):
+        raise ValueError("kstride must be 16, 32, 48 or 64")
+    return keys.contiguous()
+
+
 def pack_keys(keys: Sequence, kstride: int = 0, device="cuda") -> torch.Tensor:
     """Strings/bytes -> NUL-padded uint8 key records on `device`."""
     bs = [k.encode() if isinstance(k, str) else bytes(k) for k in keys]
@@ -109,10 +118,11 @@ class HbmArena:
     # ------------------------------------------------------------ batches --
     def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, retries: int = 64,
             status: Optional[torch.Tensor] = None) -> torch.Tensor:
+        keys = _keys(keys)
         n = keys.shape[0]
-        assert keys.dtype == torch.uint8 and vals.dtype == torch.uint8 and keys.is_cuda and vals.is_cuda
+        vals, lens = vals.contiguous(), lens.contiguous()
+        assert vals.dtype == torch.uint8 and vals.is_cuda
         assert vals.shape[0] == n and lens.shape[0] == n and lens.dtype in (torch.int32, torch.uint32)
-        assert keys.is_contiguous() and vals.is_contiguous() and lens.is_contiguous()
         if status is None:
             status = torch.empty(n, dtype=torch.int32, device=keys.device)
         _check(self._H.spl_arena_set(self.desc, keys.data_ptr(), keys.shape[1], vals.data_ptr(), vals.shape[1],
@@ -122,8 +132,8 @@ class HbmArena:
 
     def get(self, keys: torch.Tensor, out: Optional[torch.Tensor] = None, retries: int = 64,
             status: Optional[torch.Tensor] = None, out_lens: Optional[torch.Tensor] = None):
+        keys = _keys(keys)
         n = keys.shape[0]
-        assert keys.dtype == torch.uint8 and keys.is_cuda and keys.is_contiguous()
         if out is None:
             out = torch.empty((n, (self.max_val + 15) // 16 * 16), dtype=torch.uint8, device=keys.device)
         assert out.shape[0] == n and out.is_contiguous() and out.shape[1] % 16 == 0
@@ -137,6 +147,7 @@ class HbmArena:
         return status, out, out_lens
 
     def unset(self, keys: torch.Tensor, retries: int = 64) -> torch.Tensor:
+        keys = _keys(keys)
         n = keys.shape[0]
         status = torch.empty(n, dtype=torch.int32, device=keys.device)
         _check(self._H.spl_arena_unset(self.desc, keys.data_ptr(), keys.shape[1], n, status.data_ptr(), retries,
@@ -145,8 +156,10 @@ class HbmArena:
 
     def integer_op(self, keys: torch.Tensor, ops: torch.Tensor, masks: Optional[torch.Tensor] = None,
                    retries: int = 64) -> Tuple[torch.Tensor, torch.Tensor]:
+        keys = _keys(keys)
         n = keys.shape[0]
         ops = ops.to(torch.int32).contiguous()
+        masks = None if masks is None else masks.contiguous()
         status = torch.empty(n, dtype=torch.int32, device=keys.device)
         results = torch.empty(n, dtype=torch.int64, device=keys.device)
         _check(self._H.spl_arena_intop(self.desc, keys.data_ptr(), keys.shape[1], ops.data_ptr(), _ptr(masks), n,
@@ -154,6 +167,8 @@ class HbmArena:
         return status, results
 
     def meta(self, op: str, keys: torch.Tensor, args: Optional[torch.Tensor] = None):
+        keys = _keys(keys)
+        args = None if args is None else args.to(torch.int64).contiguous()
         n = keys.shape[0]
         status = torch.empty(n, dtype=torch.int32, device=keys.device)
         out = torch.empty(n, dtype=torch.int64, device=keys.device)
@@ -162,6 +177,7 @@ class HbmArena:
         return status, out
 
     def set_embeddings(self, keys: torch.Tensor, vecs: torch.Tensor) -> torch.Tensor:
+        keys = _keys(keys)
         n = keys.shape[0]
         assert vecs.dtype == torch.float32 and vecs.shape == (n, 768) and vecs.is_contiguous()
         status = torch.empty(n, dtype=torch.int32, device=keys.device)
@@ -170,6 +186,7 @@ class HbmArena:
         return status
 
     def get_embeddings(self, keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+        keys = _keys(keys)
         n = keys.shape[0]
         vecs = torch.empty((n, 768), dtype=torch.float32, device=keys.device)
         status = torch.empty(n, dtype=torch.int32, device=keys.device)
@@ -178,6 +195,7 @@ class HbmArena:
         return status, vecs
 
     def scan(self, mode: int = SCAN_LIST, mask: int = 0, cap: Optional[int] = None):
+        keys = _keys(keys)
         """Compacted slot indices (uint32 as int32) + epochs of matching slots."""
         cap = self.slots if cap is None else cap
         idx = torch.empty(cap, dtype=torch.int32, device="cuda")

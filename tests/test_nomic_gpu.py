@@ -1,0 +1,180 @@
+"""Numerics of the gfx950 Nomic-BERT kernels against plain fp32 PyTorch."""
+import math
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return (a - b).norm().item() / max(b.norm().item(), 1e-12)
+
+
+@pytest.fixture(scope="module")
+def L():
+    import torch  # noqa: F401
+    from libsplinter_amd.models.nomic import _lib
+    return _lib()
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 768, 768), (1000, 2304, 768), (257, 768, 3072)])
+def test_gemm_store_and_residual(L, M, N, K):
+    import torch
+    from libsplinter_amd.models.nomic import _chk, _stream
+    torch.manual_seed(0)
+    Mp = (M + 127) // 128 * 128
+    A = torch.randn(Mp, K, device="cuda").bfloat16()
+    W = torch.randn(N, K, device="cuda").bfloat16() * 0.05
+    R = torch.randn(Mp, N, device="cuda").bfloat16()
+    ref = A[:M].float() @ W.float().T
+    out = torch.zeros(Mp, N, device="cuda", dtype=torch.bfloat16)
+    _chk(L.nomic_gemm(0, A.data_ptr(), K, W.data_ptr(), K, M, N, K, out.data_ptr(), N, None, 0, None, None, 0,
+                      _stream()), "gemm")
+    assert _rel(out[:M].float(), ref) < 5e-3
+    assert (out[M:] == 0).all(), "rows past M must not be written"
+    _chk(L.nomic_gemm(1, A.data_ptr(), K, W.data_ptr(), K, M, N, K, out.data_ptr(), N, R.data_ptr(), N, None, None,
+                      0, _stream()), "gemm")
+    assert _rel(out[:M].float(), ref + R[:M].float()) < 5e-3
+    outf = torch.zeros(Mp, N, device="cuda")
+    _chk(L.nomic_gemm(4, A.data_ptr(), K, W.data_ptr(), K, M, N, K, outf.data_ptr(), N, None, 0, None, None, 0,
+                      _stream()), "gemm")
+    assert _rel(outf[:M], ref) < 1e-5
+
+
+def test_gemm_asymmetric_identity(L):
+    """A = I with an asymmetric W catches a transposed C write (guide §3)."""
+    import torch
+    from libsplinter_amd.models.nomic import _chk, _stream
+    K = 128
+    A = torch.eye(128, K, device="cuda").bfloat16()
+    W = (torch.arange(128 * K, device="cuda", dtype=torch.float32).reshape(128, K) % 97).bfloat16()
+    out = torch.zeros(128, 128, device="cuda")
+    _chk(L.nomic_gemm(4, A.data_ptr(), K, W.data_ptr(), K, 128, 128, K, out.data_ptr(), 128, None, 0, None, None, 0,
+                      _stream()), "gemm")
+    assert torch.equal(out, W.float().T)
+
+
+def test_gemm_swiglu_and_rope(L):
+    import torch
+    from libsplinter_amd.models.nomic import NomicEncoder, NomicReference, _chk, _stream
+    torch.manual_seed(1)
+    M, K, F = 200, 768, 3072
+    Mp = 256
+    x = torch.randn(Mp, K, device="cuda").bfloat16()
+    up = torch.randn(F, K, device="cuda") * 0.03
+    gate = torch.randn(F, K, device="cuda") * 0.03
+    ug = torch.stack([up.reshape(-1, 64, K), gate.reshape(-1, 64, K)], 1).reshape(-1, K).bfloat16()
+    out = torch.empty(Mp, F, device="cuda", dtype=torch.bfloat16)
+    _chk(L.nomic_gemm(2, x.data_ptr(), K, ug.data_ptr(), K, M, 2 * F, K, out.data_ptr(), F, None, 0, None, None, 0,
+                      _stream()), "swiglu")
+    xf = x[:M].float()
+    ref = (xf @ up.bfloat16().float().T) * torch.nn.functional.silu(xf @ gate.bfloat16().float().T)
+    assert _rel(out[:M].float(), ref) < 1e-2
+    # RoPE epilogue vs reference rotation
+    wqkv = (torch.randn(3 * K, K, device="cuda") * 0.03).bfloat16()
+    pos = torch.randint(0, 2000, (Mp,), device="cuda", dtype=torch.int32)
+    from libsplinter_amd.models.nomic import NomicConfig
+    cfg = NomicConfig()
+    inv = cfg.rope_base ** (-np.arange(0, 64, 2) / 64)
+    ang = np.arange(8192)[:, None] * inv[None, :]
+    tab = torch.from_numpy(np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32).reshape(8192, -1)).cuda()
+    qkv = torch.empty(Mp, 3 * K, device="cuda", dtype=torch.bfloat16)
+    _chk(L.nomic_gemm(3, x.data_ptr(), K, wqkv.data_ptr(), K, M, 3 * K, K, qkv.data_ptr(), 3 * K, None, 0,
+                      tab.data_ptr(), pos.data_ptr(), 2 * K, _stream()), "rope")
+    raw = xf @ wqkv.float().T
+    ref_m = NomicReference(cfg, {}, "cuda")
+    q = ref_m.rope(raw[:, :K].reshape(M, 12, 64), pos[:M].long()).reshape(M, K)
+    k = ref_m.rope(raw[:, K:2 * K].reshape(M, 12, 64), pos[:M].long()).reshape(M, K)
+    ref = torch.cat([q, k, raw[:, 2 * K:]], 1)
+    assert _rel(qkv[:M].float(), ref) < 1e-2
+
+
+def test_attention_varlen(L):
+    import torch
+    from libsplinter_amd.models.nomic import Batch, _chk, _stream
+    torch.manual_seed(2)
+    lens = [1, 17, 64, 65, 200, 513]
+    b = Batch([[0] * n for n in lens])
+    T = b.T
+    qkv = torch.randn(b.T_pad, 3 * 768, device="cuda").bfloat16()
+    out = torch.zeros(b.T_pad, 768, device="cuda", dtype=torch.bfloat16)
+    _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
+                           1 / 8.0, _stream()), "attn")
+    q, k, v = qkv[:T].float().split(768, 1)
+    refs = []
+    for i in range(len(lens)):
+        a, e = b.cu_host[i], b.cu_host[i + 1]
+        qq, kk, vv = (t[a:e].reshape(-1, 12, 64) for t in (q, k, v))
+        p = (torch.einsum("qhd,khd->hqk", qq, kk) / 8.0).softmax(-1)
+        refs.append(torch.einsum("hqk,khd->qhd", p, vv).reshape(-1, 768))
+    assert _rel(out[:T].float(), torch.cat(refs)) < 1e-2
+
+
+def test_layernorm_and_embed(L):
+    import torch
+    from libsplinter_amd.models.nomic import _chk, _stream
+    torch.manual_seed(3)
+    T = 777
+    x = torch.randn(T, 768, device="cuda").bfloat16() * 3 + 1
+    g = (1 + 0.1 * torch.randn(768, device="cuda")).bfloat16()
+    bb = (0.1 * torch.randn(768, device="cuda")).bfloat16()
+    out = torch.empty_like(x)
+    _chk(L.nomic_layernorm(x.data_ptr(), T, g.data_ptr(), bb.data_ptr(), 1e-12, out.data_ptr(), _stream()), "ln")
+    ref = torch.nn.functional.layer_norm(x.float(), (768,), g.float(), bb.float(), 1e-12)
+    assert _rel(out.float(), ref) < 5e-3
+    tok = torch.randn(1000, 768, device="cuda").bfloat16()
+    trow = torch.randn(768, device="cuda").bfloat16()
+    ids = torch.randint(0, 1000, (T,), device="cuda", dtype=torch.int32)
+    _chk(L.nomic_embed_ln(ids.data_ptr(), T, tok.data_ptr(), trow.data_ptr(), g.data_ptr(), bb.data_ptr(), 1e-12,
+                          out.data_ptr(), _stream()), "embed")
+    ref = torch.nn.functional.layer_norm(tok[ids.long()].float() + trow.float(), (768,), g.float(), bb.float(), 1e-12)
+    assert _rel(out.float(), ref) < 5e-3
+
+
+def test_encoder_matches_fp32_reference():
+    import torch
+    from libsplinter_amd.models.nomic import (Batch, NomicConfig, NomicEncoder, NomicReference, NomicWeights,
+                                              random_weights)
+    cfg = NomicConfig(layers=3)
+    w = random_weights(cfg, seed=5)
+    enc = NomicEncoder(NomicWeights.from_numpy(cfg, w), max_tokens=4096)
+    rng = np.random.default_rng(0)
+    seqs = [rng.integers(0, cfg.vocab, size=n).tolist() for n in (5, 40, 129, 300)]
+    b = Batch(seqs)
+    got = enc.embed(b)
+    ref = NomicReference(cfg, w, "cuda")(torch.from_numpy(np.concatenate(seqs)).cuda().long(), b.cu_host.tolist())
+    cos = torch.nn.functional.cosine_similarity(got, ref, dim=1)
+    assert cos.min().item() > 0.999, cos
+    assert _rel(got, ref) < 3e-2
+
+
+def test_gguf_roundtrip_device_dequant(tmp_path):
+    import torch
+    from libsplinter_amd.models.gguf import GGUFFile
+    from libsplinter_amd.models.nomic import NomicConfig, NomicWeights, random_weights, write_gguf
+    cfg = NomicConfig(layers=1, vocab=512)
+    w = random_weights(cfg, seed=9)
+    for lt in ("F16", "Q8_0", "Q4_0"):
+        p = str(tmp_path / f"m_{lt}.gguf")
+        write_gguf(p, cfg, w, vocab=[f"t{i}" for i in range(cfg.vocab)], linear_type=lt)
+        g = GGUFFile(p)
+        assert NomicConfig.from_gguf(g).layers == 1
+        nw = NomicWeights.from_gguf(g)
+        host = torch.from_numpy(g.to_numpy_f32("blk.0.attn_qkv.weight")).cuda()
+        assert torch.equal(nw.layers[0]["wqkv"].float(), host.bfloat16().float()), lt
+        assert _rel(host, torch.from_numpy(w["blk.0.attn_qkv.weight"]).cuda()) < (0.2 if lt == "Q4_0" else 2e-2)
+
+
+def test_pool_writes_into_arena_slots(uniq):
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, pack_keys, pack_values
+    from libsplinter_amd.models.nomic import smoke_embed
+    a = HbmArena.create(uniq, slots=256, max_val=64, embeddings=True)
+    try:
+        K = pack_keys([f"doc{i}" for i in range(8)], 16)
+        V, Ln = pack_values([b"x"] * 8, 16)
+        a.set(K, V, Ln)
+        smoke_embed(a, K)
+    finally:
+        a.close()

@@ -254,22 +254,38 @@ __device__ __forceinline__ void write_value(const Arena& a, size_t idx, const ui
   }
 }
 
-// Publish a locked slot: release the payload, store hash, epoch+1.
-template <int MO>
-__device__ __forceinline__ void publish(const Arena& a, size_t idx, uint64_t hash) {
-  uint8_t* s = a.slot(idx);
-  if constexpr (MO == 0) release();
-  else if constexpr (MO == 1) drain();
-  ast64(s + kOffHash, hash);
+// ------------------------------------------------------------ SET ------
+// A set is split into three phases so that a batch kernel can lock several
+// slots per lane, write all their payloads, and pay ONE agent release fence
+// for all of them (a release fence writes back the XCD's L2 and is
+// serialised per XCD at ~1.7 us, which otherwise caps sets near 0.3 G/s).
+//   claim_set   locate the key (update) or claim a free slot (insert); on
+//               success the slot's epoch is odd and owned by this lane
+//   write_set   payload with plain 16-B stores
+//   release()   once, by the caller, covering every write_set of the wave
+//   finish_set  epoch += 1 (the hash is already in place)
+// Inserts publish key + hash EARLY (right after the claim, with an
+// "insert in flight" marker val_len = kInsertMark) so that racing inserters
+// of one key see each other: the claim that sits earlier on the probe chain
+// wins, the later one backs off with EAGAIN.  Readers that meet a slot with
+// their hash and an odd epoch report EAGAIN, as for any in-flight write.
+constexpr uint32_t kInsertMark = 0xFFFFFFFFu;
+
+struct Claim {
+  long idx;       // slot index (valid when rc == kOk)
+  bool fresh;     // true: insert into a free slot
+  int32_t rc;
+};
+
+__device__ __forceinline__ void clear_claim(const Arena& a, long idx) {
+  uint8_t* s = a.slot((size_t)idx);
+  ast64(s + kOffHash, 0);
+  ast32(s + kOffValLen, 0);
+  drain();
   aadd64(epoch_ptr(s), 1);
 }
 
-// SET (insert or update).  On success *out_idx = slot index.
-template <int MO = 0>
-__device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint32_t len, long* out_idx) {
-  if (len == 0 || len > a.max_val) return kMsgSize;
-  bool hybrid;
-  const bool scrub = scrub_flags(a, hybrid);
+__device__ Claim claim_set(const Arena& a, const Key& k) {
   const size_t home = (size_t)(k.hash % a.slots);
   long free_idx = -1;
   uint64_t free_ep = 0;
@@ -278,33 +294,32 @@ __device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint
     uint8_t* s = a.slot(idx);
     const uint64_t sh = slot_hash(s);
     const uint64_t e = slot_epoch(s);
-    if (sh == k.hash && key_eq(s, k)) {
-      if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
-      if (slot_hash(s) != k.hash || !key_eq(s, k)) {  // raced with unset
+    if (sh == k.hash && key_eq(s, k)) {  // update in place
+      if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return Claim{-1, false, kAgain};
+      if (slot_hash(s) != k.hash || !key_eq(s, k)) {  // raced with unset / reuse
         aadd64(epoch_ptr(s), 1);
-        return kAgain;
+        return Claim{-1, false, kAgain};
       }
-      write_value<MO>(a, idx, val, len, scrub, hybrid);
-      ast32(s + kOffValLen, len);
-      publish<MO>(a, idx, k.hash);
-      *out_idx = (long)idx;
-      return kOk;
+      return Claim{(long)idx, false, kOk};
     }
-    if ((e & 1) && sh == k.hash) return kAgain;  // our key is being rewritten
-    if (sh == 0 && !(e & 1)) {                   // reusable (odd = someone's claim: skip)
+    if (sh == 0 && !(e & 1)) {  // reusable (odd = someone's claim in flight: skip)
       if (free_idx < 0) { free_idx = (long)idx; free_ep = e; }
-      if (e == 0) break;
+      if (e == 0) break;        // virgin slot ends the chain
     }
     if (++idx == a.slots) idx = 0;
   }
-  if (free_idx < 0) return kNoSpc;
+  if (free_idx < 0) return Claim{-1, false, kNoSpc};
   uint8_t* fs = a.slot((size_t)free_idx);
-  if (!acas64(epoch_ptr(fs), free_ep, free_ep + 1)) return kAgain;
-  if (slot_hash(fs) != 0) { aadd64(epoch_ptr(fs), 1); return kAgain; }
-  // Re-validate the chain while holding the claimed slot (no duplicates):
-  //  - our key published anywhere on the chain -> back off, update it next try;
-  //  - a claim in flight *before* ours may be the same key -> the earlier
-  //    claimant wins, we back off; claims after ours defer to us.
+  if (!acas64(epoch_ptr(fs), free_ep, free_ep + 1)) return Claim{-1, false, kAgain};
+  if (slot_hash(fs) != 0) { aadd64(epoch_ptr(fs), 1); return Claim{-1, false, kAgain}; }
+  // early publication: marker, key, then hash (each visible before the next)
+  ast32(fs + kOffValLen, kInsertMark);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) ast64(fs + kOffKey + 8 * q, ((uint64_t)k.w[2 * q + 1] << 32) | k.w[2 * q]);
+  drain();
+  ast64(fs + kOffHash, k.hash);
+  drain();
+  // re-validate the chain while holding the claim
   idx = home;
   bool before = true;
   for (uint32_t i = 0; i < a.slots; ++i) {
@@ -314,25 +329,58 @@ __device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint
       uint8_t* s = a.slot(idx);
       const uint64_t sh = slot_hash(s);
       const uint64_t e = slot_epoch(s);
-      if ((sh == k.hash && (key_eq(s, k) || (e & 1))) || (before && (e & 1) && sh == 0)) {
-        aadd64(epoch_ptr(fs), 1);
-        return kAgain;
+      bool conflict = false;
+      if (sh == k.hash && key_eq(s, k)) {
+        // published copy, an update in progress, or an earlier racing insert
+        conflict = !(e & 1) || before || ald32(s + kOffValLen) != kInsertMark;
+      } else if (before && (e & 1) && sh == 0) {
+        conflict = true;  // a claim whose key is not visible yet: may be ours
+      }
+      if (conflict) {
+        clear_claim(a, free_idx);
+        return Claim{-1, false, kAgain};
       }
       if (sh == 0 && e == 0) break;
     }
     if (++idx == a.slots) idx = 0;
   }
-  write_value<MO>(a, (size_t)free_idx, val, len, scrub, hybrid);
-  ast32(fs + kOffValLen, len);
-  if (a.stride == kSlotEmbedBytes) {  // fresh slot: clear a stale vector
-    uint4* ev = (uint4*)(fs + kOffEmbed);
-    for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) st16<MO>(ev + c, make_uint4(0, 0, 0, 0));
+  return Claim{free_idx, true, kOk};
+}
+
+template <int MO = 0>
+__device__ __forceinline__ void write_set(const Arena& a, const Claim& c, const uint8_t* val, uint32_t len,
+                                          bool scrub, bool hybrid) {
+  uint8_t* s = a.slot((size_t)c.idx);
+  write_value<MO>(a, (size_t)c.idx, val, len, scrub, hybrid);
+  if (c.fresh) {
+    // fresh slot: metadata bytes 24..63 to defaults (type VOID), clear a stale vector
+    st16<MO>(s + 32, make_uint4(0, 0, 0, 0));  // watcher_mask, ctime
+    st16<MO>(s + 48, make_uint4(0, 0, 0, 0));  // atime, bloom
+    ast8(s + kOffType, (uint8_t)SPL_SLOT_DEFAULT_TYPE);
+    ast8(s + kOffUser, 0);
+    if (a.stride == kSlotEmbedBytes) {
+      uint4* ev = (uint4*)(s + kOffEmbed);
+      for (uint32_t q = 0; q < kEmbedBytes / 16; ++q) st16<MO>(ev + q, make_uint4(0, 0, 0, 0));
+    }
   }
-#pragma unroll
-  for (int c = 0; c < 4; ++c)
-    st16<MO>(fs + kOffKey + 16 * c, make_uint4(k.w[4 * c], k.w[4 * c + 1], k.w[4 * c + 2], k.w[4 * c + 3]));
-  publish<MO>(a, (size_t)free_idx, k.hash);
-  *out_idx = free_idx;
+  ast32(s + kOffValLen, len);
+}
+
+__device__ __forceinline__ void finish_set(const Arena& a, const Claim& c) { aadd64(epoch_ptr(a.slot((size_t)c.idx)), 1); }
+
+// Single-op SET (insert or update) with its own release.
+template <int MO = 0>
+__device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint32_t len, long* out_idx) {
+  if (len == 0 || len > a.max_val) return kMsgSize;
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  const Claim c = claim_set(a, k);
+  if (c.rc != kOk) return c.rc;
+  write_set<MO>(a, c, val, len, scrub, hybrid);
+  if constexpr (MO == 0) release();
+  else if constexpr (MO == 1) drain();
+  finish_set(a, c);
+  *out_idx = c.idx;
   return kOk;
 }
 
@@ -366,6 +414,24 @@ __device__ int32_t get_op(const Arena& a, const Key& k, uint8_t* out, uint32_t o
     if (++idx == a.slots) idx = 0;
   }
   return kNoEnt;
+}
+
+// Batched GET, phase helpers (see k_get_rounds): locate without the seqlock,
+// then one acquire for all of a lane's ops, then copy, then validate.
+// Returns the slot index holding k (possibly mid-write), or -1 for a miss.
+__device__ __forceinline__ long locate(const Arena& a, const Key& k) {
+  size_t idx = (size_t)(k.hash % a.slots);
+  for (uint32_t i = 0; i < a.slots; ++i) {
+    const uint8_t* s = a.slot(idx);
+    const uint64_t sh = slot_hash(s);
+    if (sh == k.hash) {
+      if (key_eq(s, k)) return (long)idx;
+    } else if (sh == 0 && slot_epoch(s) == 0) {
+      return -1;
+    }
+    if (++idx == a.slots) idx = 0;
+  }
+  return -1;
 }
 
 // UNSET: returns the old length (>= 0) or a negative status.

@@ -33,6 +33,16 @@ inline int arena_mo() {
   return mo;
 }
 
+// Ops per lane per round for set/get (SPLINTER_ARENA_U = 1|2|4|8; 1 = the
+// single-op kernels, which also honour SPLINTER_ARENA_MO).
+inline int arena_rounds() {
+  static int u = [] {
+    const char* e = getenv("SPLINTER_ARENA_U");
+    return e ? atoi(e) : 4;
+  }();
+  return u;
+}
+
 inline int grid_for(long n) {
   long g = (n + kBlock - 1) / kBlock;
   if (g < 1) g = 1;
@@ -158,6 +168,139 @@ __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys
     else if (rc == kNoEnt) ++st.miss;
     if (out_lens) out_lens[i] = rc == kOk ? len : 0;
     if (status) status[i] = rc;
+  }
+  flush_stats(a, st, stats, 0);
+}
+
+// ---------------------------------------------------- batched rounds -----
+// U ops per lane per round: U claims (or lookups) in flight, then ONE agent
+// release (writers) / acquire (readers) per wave for all of them.  EAGAIN ops
+// fall back to the single-op path with backoff.
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
+                                                       const uint8_t* vals, int vstride, const uint32_t* lens, long n,
+                                                       int32_t* status, int max_retry, uint64_t* stats) {
+  const Arena a = to_dev(aa);
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  Stats st;
+  uint64_t muts = 0;
+  const long nth = (long)gridDim.x * blockDim.x;
+  for (long r0 = (blockIdx.x * (long)blockDim.x + threadIdx.x) * U; r0 < n; r0 += nth * U) {
+    Key k[U];
+    Claim c[U];
+    uint32_t len[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long i = r0 + j;
+      c[j] = Claim{-1, false, kInval};
+      if (i < n) {
+        load_key(k[j], keys + i * (long)kstride, kstride);
+        len[j] = lens[i];
+        ++st.attempts;
+        if (len[j] == 0 || len[j] > a.max_val) c[j].rc = kMsgSize;
+        else c[j] = claim_set(a, k[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (c[j].rc == kOk) write_set<0>(a, c[j], vals + (r0 + j) * (long)vstride, len[j], scrub, hybrid);
+    release();  // one agent release per wave covers every payload above
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long i = r0 + j;
+      if (i >= n) continue;
+      int32_t rc = c[j].rc;
+      long idx = c[j].idx;
+      if (rc == kOk) finish_set(a, c[j]);
+      for (int t = 0; rc == kAgain && t < max_retry; ++t) {
+        ++st.again;
+        backoff(t);
+        ++st.attempts;
+        rc = set_op<0>(a, k[j], vals + i * (long)vstride, len[j], &idx);
+      }
+      if (rc == kAgain) ++st.again;
+      if (rc == kOk) {
+        ++st.ok;
+        ++muts;
+        pulse(a, a.slot((size_t)idx));
+        mark_dirty(a, (size_t)idx);
+      }
+      if (status) status[i] = rc;
+    }
+  }
+  flush_stats(a, st, stats, muts);
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void k_get_rounds(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
+                                                       int ostride, uint32_t* out_lens, long n, int32_t* status,
+                                                       int max_retry, uint64_t* stats) {
+  const Arena a = to_dev(aa);
+  Stats st;
+  const long nth = (long)gridDim.x * blockDim.x;
+  for (long r0 = (blockIdx.x * (long)blockDim.x + threadIdx.x) * U; r0 < n; r0 += nth * U) {
+    Key k[U];
+    long sidx[U];
+    uint64_t e1[U];
+    int32_t rc[U];
+    uint32_t len[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long i = r0 + j;
+      rc[j] = kInval;
+      sidx[j] = -1;
+      len[j] = 0;
+      if (i < n) {
+        load_key(k[j], keys + i * (long)kstride, kstride);
+        ++st.attempts;
+        sidx[j] = locate(a, k[j]);
+        rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (rc[j] == kOk) e1[j] = slot_epoch(a.slot((size_t)sidx[j]));
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one L1 invalidate for all U reads
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (rc[j] != kOk) continue;
+      const uint8_t* s = a.slot((size_t)sidx[j]);
+      if ((e1[j] & 1) || !key_eq(s, k[j])) { rc[j] = kAgain; continue; }
+      len[j] = ald32(s + kOffValLen);
+      if (out) {
+        if (len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
+        const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
+        uint4* dst = (uint4*)(out + (r0 + j) * (long)ostride);
+        const uint32_t n16 = (len[j] + 15) >> 4;
+        for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
+      }
+    }
+    drain();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (rc[j] != kOk) continue;
+      const uint8_t* s = a.slot((size_t)sidx[j]);
+      if (slot_epoch(s) != e1[j] || slot_hash(s) != k[j].hash) rc[j] = kAgain;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const long i = r0 + j;
+      if (i >= n) continue;
+      int32_t r = rc[j];
+      uint32_t L = len[j];
+      for (int t = 0; r == kAgain && t < max_retry; ++t) {
+        ++st.again;
+        backoff(t);
+        ++st.attempts;
+        r = get_op<0>(a, k[j], out ? out + i * (long)ostride : nullptr, (uint32_t)ostride, &L);
+      }
+      if (r == kAgain) ++st.again;
+      if (r == kOk) ++st.ok;
+      else if (r == kNoEnt) ++st.miss;
+      if (out_lens) out_lens[i] = r == kOk ? L : 0;
+      if (status) status[i] = r;
+    }
   }
   flush_stats(a, st, stats, 0);
 }
@@ -495,7 +638,17 @@ int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* v
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
   const int mo = arena_mo();
-  if (mo == 1)
+  const int u = arena_rounds();
+  if (u == 2)
+    hipLaunchKernelGGL(k_set_rounds<2>, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, keys, kstride, vals,
+                       vstride, lens, n, status, max_retry, stats);
+  else if (u == 4)
+    hipLaunchKernelGGL(k_set_rounds<4>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, a, keys, kstride, vals,
+                       vstride, lens, n, status, max_retry, stats);
+  else if (u == 8)
+    hipLaunchKernelGGL(k_set_rounds<8>, dim3(grid_for((n + 7) / 8)), dim3(kBlock), 0, s, a, keys, kstride, vals,
+                       vstride, lens, n, status, max_retry, stats);
+  else if (mo == 1)
     hipLaunchKernelGGL(k_set<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
                        status, max_retry, stats);
   else if (mo == 2)
@@ -512,7 +665,17 @@ int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, in
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
   const int mo = arena_mo();
-  if (mo == 1)
+  const int u = arena_rounds();
+  if (u == 2)
+    hipLaunchKernelGGL(k_get_rounds<2>, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, keys, kstride, out,
+                       ostride, out_lens, n, status, max_retry, stats);
+  else if (u == 4)
+    hipLaunchKernelGGL(k_get_rounds<4>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, a, keys, kstride, out,
+                       ostride, out_lens, n, status, max_retry, stats);
+  else if (u == 8)
+    hipLaunchKernelGGL(k_get_rounds<8>, dim3(grid_for((n + 7) / 8)), dim3(kBlock), 0, s, a, keys, kstride, out,
+                       ostride, out_lens, n, status, max_retry, stats);
+  else if (mo == 1)
     hipLaunchKernelGGL(k_get<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
                        status, max_retry, stats);
   else if (mo == 2)

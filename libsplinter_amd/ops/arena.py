@@ -195,7 +195,6 @@ class HbmArena:
         return status, vecs
 
     def scan(self, mode: int = SCAN_LIST, mask: int = 0, cap: Optional[int] = None):
-        keys = _keys(keys)
         """Compacted slot indices (uint32 as int32) + epochs of matching slots."""
         cap = self.slots if cap is None else cap
         idx = torch.empty(cap, dtype=torch.int32, device="cuda")

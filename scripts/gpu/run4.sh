@@ -1,0 +1,11 @@
+set -x
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+timeout -k 10 300 python -m pytest tests/test_arena_gpu.py -q > gpurun_out/pytest_arena4.log 2>&1; echo "arena rc=$?"
+for mo in 0 1 2; do
+  SPLINTER_ARENA_MO=$mo timeout -k 10 120 python scripts/mo_debug.py >> gpurun_out/mo_debug4.log 2>&1
+done
+for mo in 0 1 2; do
+  SPLINTER_ARENA_MO=$mo timeout -k 10 240 python scripts/kv_micro.py --keys 100000000 --batch 4000000 >> gpurun_out/kv_micro4.log 2>&1
+done
+echo done

@@ -37,7 +37,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--mode", default="kv", choices=["kv", "embed", "mixed"])
+    p.add_argument("--mode", default="mixed", choices=["kv", "embed", "mixed"])
     p.add_argument("--keys-per-gpu", type=int, default=100_000_000)
     p.add_argument("--slots-factor", type=float, default=2.0)
     p.add_argument("--max-val", type=int, default=256)
@@ -121,12 +121,18 @@ def main():
         from libsplinter_amd.models.bench_embed import EmbedPhase
         embedder = EmbedPhase(arena, batch=args.embed_batch, seq=args.embed_seq, rank=rank)
 
-    s_set, s_get = torch.cuda.Stream(), torch.cuda.Stream()
+    s_set, s_get, s_emb = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
     stats = arena.stats
 
     def step(i):
+        # KV batches (memory/latency bound) and the embed batch (MFMA bound)
+        # run on separate HIP streams so they overlap on the chip.
         SK, SV, SL, GK, _ = batches[i % nbuf]
         cur = torch.cuda.current_stream()
+        if embedder is not None:
+            s_emb.wait_stream(cur)
+            with torch.cuda.stream(s_emb):
+                embedder.run()
         if n_set:
             s_set.wait_stream(cur)
             s_get.wait_stream(cur)
@@ -135,13 +141,14 @@ def main():
                     arena.set(SK, SV, SL)
                 with torch.cuda.stream(s_get):
                     arena.get(GK, out=gout)
-                cur.wait_stream(s_set)
-                cur.wait_stream(s_get)
             else:
-                kv.set(SK, SV, SL)
-                kv.get(GK)
+                with torch.cuda.stream(s_set):
+                    kv.set(SK, SV, SL)
+                    kv.get(GK)
+            cur.wait_stream(s_set)
+            cur.wait_stream(s_get)
         if embedder is not None:
-            embedder.run()
+            cur.wait_stream(s_emb)
 
     for i in range(args.warmup):
         step(i)
@@ -196,9 +203,11 @@ def main():
 
     kv_ops = (n_set + n_get) * args.steps * world
     kv_ops_s = kv_ops / elapsed if kv_ops else 0.0
-    emb_vps = None
+    emb_vps = emb_tps = emb_tflops = None
     if embedder is not None:
         emb_vps = embedder.docs_per_step * args.steps * world / elapsed
+        emb_tps = embedder.tokens_per_step * args.steps * world / elapsed
+        emb_tflops = embedder.flops_per_step * args.steps * world / elapsed / 1e12
     value = kv_ops_s if args.mode != "embed" else emb_vps
     res = {
         "metric": "KV set/get ops/sec + Nomic-768d embed vectors/sec at 1/2/4/8 MI355X",
@@ -222,6 +231,8 @@ def main():
         },
         "kv_ops_per_s": kv_ops_s,
         "embed_vectors_per_s": emb_vps,
+        "embed_tokens_per_s": emb_tps,
+        "embed_tflops": emb_tflops,
         "kv_attempts": attempts, "kv_ok": ok, "kv_eagain_retries": again, "kv_miss": miss,
         "successful_ops_per_s": ok / elapsed if elapsed else 0.0,
         "integrity_failures": integrity_fail,

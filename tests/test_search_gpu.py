@@ -59,7 +59,7 @@ def test_splinference_daemon_oneshot(uniq):
             s.set(f"doc{i}", f"the vector store document number {i} about search")
             s.set_type(f"doc{i}", 1 << 7)
             s.set_label(f"doc{i}", 0x1 | 0x40)
-        s.set("huge", " ".join(["word"] * 3000))
+        s.set("huge", "a " * 2000)  # ~2000 tokens > 0.9 * n_ctx (2048)
         r = subprocess.run([sys.executable, "-m", "libsplinter_amd.daemons.splinference", "--oneshot",
                             "--random-init", "--layers", "2", uniq, "none.gguf", "3"],
                            cwd=ROOT, capture_output=True, text=True, timeout=600)

@@ -1,0 +1,104 @@
+"""splinterctl one-shot + REPL regression (reference CLI verbs, splinter_cli_cmd_*.c)."""
+import json
+import os
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BIN = os.path.join(ROOT, "libsplinter_amd", "bin")
+
+
+def ctl(store, *args, stdin=None, name="splinterctl"):
+    r = subprocess.run([os.path.join(BIN, name), "-u", store, *args], capture_output=True, text=True,
+                       input=stdin, timeout=60)
+    return r.returncode, r.stdout, r.stderr
+
+
+@pytest.fixture
+def store(uniq):
+    if not os.path.exists(os.path.join(BIN, "splinterctl")):
+        subprocess.run(["make", "-C", ROOT, "tools"], check=True, capture_output=True)
+    rc, out, _ = ctl(uniq, "init", "--slots", "128", "--length", "512", uniq)
+    assert rc == 0 and "Initializing store" in out
+    yield uniq
+    from libsplinter_amd import unlink
+    unlink(uniq)
+
+
+def test_kv_verbs(store):
+    assert ctl(store, "set", "foo", "bar")[0] == 0
+    assert ctl(store, "get", "foo")[1].startswith("bar\n")
+    assert ctl(store, "getfoo_prefix_match_is_get", "foo")[1].startswith("bar\n")  # reference prefix dispatch
+    assert ctl(store, "append", "foo", "baz")[0] == 0
+    assert ctl(store, "get", "foo")[1].startswith("barbaz")
+    head = ctl(store, "head", "foo")[1]
+    assert "epoch:" in head and "key:        foo" in head and "DIM=768" in head
+    assert ctl(store, "unset", "foo")[1].strip() == "6 bytes deleted."
+    assert ctl(store, "get", "foo")[0] != 0
+
+
+def test_types_math_labels(store):
+    ctl(store, "set", "n", "10")
+    assert ctl(store, "type", "n", "biguint")[0] == 0
+    assert ctl(store, "type", "n")[1].startswith("SPL_SLOT_TYPE_BIGUINT:n")
+    assert "successfully" in ctl(store, "math", "n", "inc", "5")[1]
+    assert ctl(store, "get", "n")[1].split()[0] == "15"
+    ctl(store, "math", "n", "and", "0x7")
+    assert ctl(store, "get", "n")[1].split()[0] == "7"
+    assert "applied to 'n'" in ctl(store, "label", "n", "0x40")[1]
+    assert "0b1000000" in ctl(store, "head", "n")[1]
+    assert "removed from" in ctl(store, "label", "n", "-0x40")[1]
+    assert "Signal Group 3" in ctl(store, "bind", "0x40", "3")[1]
+
+
+def test_list_export_orders_ingest(store, tmp_path):
+    for k in ("alpha", "beta", "gamma"):
+        ctl(store, "set", k, k.upper())
+    out = ctl(store, "list", "^(alpha|beta)$")[1]
+    assert "alpha" in out and "beta" in out and "gamma" not in out
+    ex = json.loads(ctl(store, "export")[1])
+    assert ex["store"]["active_keys"] == 3 and {k["key"] for k in ex["keys"]} == {"alpha", "beta", "gamma"}
+    assert "OK" in ctl(store, "orders", "set", "t", "3")[1]
+    assert ctl(store, "get", "t.2")[0] == 0
+    assert ctl(store, "unset", "-r", "t")[0] == 0
+    assert ctl(store, "get", "t.1")[0] != 0
+    f = tmp_path / "doc.txt"
+    f.write_text("x" * 1000)
+    out = ctl(store, "ingest", str(f), "--key", "doc")[1]
+    assert "3 chunk(s), 1000 bytes" in out  # chunk = max_val - 64 = 448
+    meta = json.loads(ctl(store, "get", "doc")[1].splitlines()[0])
+    assert meta["chunks"] == 3 and meta["bytes"] == 1000
+    assert ctl(store, "type", "doc.2")[1].startswith("SPL_SLOT_TYPE_VARTEXT")
+
+
+def test_config_caps_shard_uuid(store):
+    cfg = ctl(store, "config")[1]
+    assert "version:     4" in cfg and "slots:       128" in cfg
+    # mode 2 does not clear HYBRID (reference splinter.c:276-299 quirk, kept): go through 0 first
+    assert ctl(store, "config", "av", "0")[0] == 0 and "mop:         0" in ctl(store, "config")[1]
+    assert ctl(store, "config", "av", "2")[0] == 0 and "mop:         2" in ctl(store, "config")[1]
+    assert "lua=no" in ctl(store, "caps")[1]
+    assert "OK" in ctl(store, "shard", "claim", "0x77", "random", "5", "100000000000")[1]
+    assert "0x77" in ctl(store, "shard", "table")[1]
+    assert ctl(store, "shard", "who")[1].startswith("sovereign=0x77")
+    assert ctl(store, "shard", "release", "0x77")[0] == 0
+    u = ctl(store, "uuid")[1].strip()
+    assert len(u) == 36 and u[14] == "4"
+
+
+def test_search_regex_without_sidecar(store):
+    ctl(store, "set", "findme", "v")
+    rc, out, err = ctl(store, "search", "--regex", "find", "--timeout", "50", "--json", "q")
+    assert rc == 0 and "timed out" in err
+    res = json.loads(out)
+    assert [r["key"] for r in res["results"]] == ["findme"] and res["results"][0]["similarity"] is None
+
+
+def test_repl_and_namespace(store):
+    script = f"use {store}\nset a 1\nget a\nhist\nquit\n"
+    rc, out, _ = ctl(store, stdin=script, name="splinter_cli")
+    assert rc == 0 and "1\n" in out and "set a 1" in out
+    r = subprocess.run([os.path.join(BIN, "splinterctl"), "-u", store, "--prefix", "ns_", "set", "k", "v"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0 and ctl(store, "get", "ns_k")[1].startswith("v")

@@ -6,27 +6,69 @@ its closest scale-out idea is the disjoint key lanes of splinter_chi_sao
 shard(key) = (fnv1a(key) >> 40) % world, so a shard's in-arena probe (which
 uses fnv1a % slots, the low bits) stays well spread.  Each rank owns one HBM
 arena; a batch of client ops is routed to owners with RCCL all-to-all over
-xGMI (collective C1 of SURVEY §2.10), executed by the owner's kernels, and the
-results are routed back.  All 7 xGMI links are driven at once by the
-all-to-all (direct peer exchange, not a ring).
+xGMI, executed by the owner's kernels, and the results are routed back.
 
-The local shard is pluggable (anything with ``hash_keys / set / get``), so the
-routing logic is exercised on CPU with gloo + the host backend in tests.
+Collectives, all over the default (RCCL) group:
+
+  C1  routed set/get/unset/integer_op/meta/set_embeddings: ONE all-to-all-v of
+      packed request rows (key | args | value) and ONE of packed response
+      rows (status | len | value) per batch, after a count exchange.  xGMI is
+      point-to-point (7 links per GPU), so the all-to-all drives every link at
+      once; packing keeps it to 2 large messages instead of 3-4 small ones.
+  C2  node-wide signal-group counters: all-reduce(sum) of the 64 u64 counters.
+  C3  search query broadcast from rank 0.
+  C4  search top-k merge: all-gather of each shard's local top-k (sim, dist,
+      key bytes), merged identically on every rank.
+  C5  cross-shard enumerate/list: all-gather of counts, then of padded
+      key rows + epochs.
+  C6  config replication (mop + label->group map) broadcast from rank 0.
+
+The local shard is pluggable (GpuShard = HBM arena kernels, HostShard = a
+host store on CPU tensors), so every collective path is tested with gloo on
+CPU (tests/test_sharded_gloo.py) and runs unchanged on RCCL.
 """
 from __future__ import annotations
 
-from typing import Optional, Tuple
+from typing import List, Optional, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
 SHARD_SHIFT = 40
+KEY_BYTES = 64
 
 
 def shard_of(hashes: torch.Tensor, world: int) -> torch.Tensor:
     """Owner rank for each 64-bit FNV-1a hash (int64 bit pattern)."""
     hi = (hashes >> SHARD_SHIFT) & 0xFFFFFF  # arithmetic shift of int64: mask the sign-extended bits
     return torch.remainder(hi, world)
+
+
+def _u8(t: torch.Tensor) -> torch.Tensor:
+    """Byte view [n, bytes] of a [n, ...] tensor (for packing rows)."""
+    t = t.contiguous()
+    row = int(np.prod(t.shape[1:])) * t.element_size() if t.dim() > 1 else t.element_size()
+    return t.view(torch.uint8).reshape(t.shape[0], row)  # explicit width: batches may be empty
+
+
+def _unpack(rows: torch.Tensor, spec: List[Tuple[torch.dtype, Tuple[int, ...]]]) -> List[torch.Tensor]:
+    """Split packed uint8 rows back into typed columns (inverse of cat(_u8(...)))."""
+    out, off = [], 0
+    n = rows.shape[0]
+    for dt, shape in spec:
+        isz = torch.empty((), dtype=dt).element_size()
+        nb = int(np.prod(shape)) * isz if shape else isz
+        col = torch.empty((n, nb), dtype=torch.uint8, device=rows.device)  # fresh storage: aligned dtype view
+        col.copy_(rows[:, off:off + nb])
+        col = col.view(dt)
+        out.append(col.reshape((n,) + tuple(shape)) if shape else col.reshape(n))
+        off += nb
+    return out
+
+
+def decode_keys(rows: torch.Tensor) -> List[str]:
+    return [bytes(r).split(b"\0", 1)[0].decode("utf-8", "replace") for r in rows.cpu().numpy()]
 
 
 class ShardedKV:
@@ -55,54 +97,186 @@ class ShardedKV:
         dist.all_to_all_single(out, x.contiguous(), recv_splits, send_splits, group=self.group)
         return out
 
+    def _roundtrip(self, keys: torch.Tensor, cols: List[torch.Tensor], execute, resp_spec):
+        """C1 skeleton: pack (keys | cols) rows -> owners, execute, pack responses -> back.
+
+        ``execute(keys, *cols) -> list of response tensors`` runs on the owner;
+        responses are returned in the caller's original order.
+        """
+        order, s, r = self._plan(keys)
+        req_spec = [(keys.dtype, tuple(keys.shape[1:]))] + [(c.dtype, tuple(c.shape[1:])) for c in cols]
+        packed = torch.cat([_u8(keys[order])] + [_u8(c[order]) for c in cols], dim=1)
+        got = _unpack(self._route(packed, s, r), req_spec)
+        resp = execute(got[0], *got[1:])
+        rspec = [(t.dtype, tuple(t.shape[1:])) for t in resp]
+        back = _unpack(self._route(torch.cat([_u8(t) for t in resp], dim=1), r, s), rspec)
+        outs = []
+        for b in back:
+            o = torch.empty_like(b)
+            o[order] = b
+            outs.append(o)
+        return outs
+
     def owned_mask(self, keys: torch.Tensor) -> torch.Tensor:
         return shard_of(self.local.hash_keys(keys), self.world) == self.rank
 
-    # -------------------------------------------------------------- ops ----
+    # -------------------------------------------------------- C1: ops ----
     def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, **kw) -> torch.Tensor:
         if self.world == 1:
             return self.local.set(keys, vals, lens, **kw)
-        order, s, r = self._plan(keys)
-        rk = self._route(keys[order], s, r)
-        rv = self._route(vals[order], s, r)
-        rl = self._route(lens[order], s, r)
-        st = self.local.set(rk, rv, rl, **kw)
-        back = self._route(st, r, s)
-        out = torch.empty_like(back)
-        out[order] = back
-        return out
+        return self._roundtrip(keys, [vals, lens.to(torch.int32)],
+                               lambda k, v, ln: [self.local.set(k, v, ln, **kw).to(torch.int32)], None)[0]
 
     def get(self, keys: torch.Tensor, **kw) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
         if self.world == 1:
             return self.local.get(keys, **kw)
-        order, s, r = self._plan(keys)
-        rk = self._route(keys[order], s, r)
-        st, vals, lens = self.local.get(rk, **kw)
-        b_st, b_vals, b_lens = self._route(st, r, s), self._route(vals, r, s), self._route(lens, r, s)
-        o_st, o_vals, o_lens = torch.empty_like(b_st), torch.empty_like(b_vals), torch.empty_like(b_lens)
-        o_st[order] = b_st
-        o_vals[order] = b_vals
-        o_lens[order] = b_lens
-        return o_st, o_vals, o_lens
 
-    def signal_counts(self, local_counts: torch.Tensor) -> torch.Tensor:
-        """Node-wide signal-group counters (C2): sum of per-shard counters."""
+        def ex(k):
+            st, v, ln = self.local.get(k, **kw)
+            return [st.to(torch.int32), ln.to(torch.int32), v]
+        st, ln, v = self._roundtrip(keys, [], ex, None)
+        return st, v, ln
+
+    def unset(self, keys: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
-            return local_counts
-        t = local_counts.clone()
-        dist.all_reduce(t, group=self.group)
+            return self.local.unset(keys)
+        return self._roundtrip(keys, [], lambda k: [self.local.unset(k).to(torch.int32)], None)[0]
+
+    def integer_op(self, keys: torch.Tensor, ops: torch.Tensor, masks: Optional[torch.Tensor] = None):
+        ops = ops.to(torch.int32)
+        masks = torch.zeros(keys.shape[0], dtype=torch.int64, device=keys.device) if masks is None \
+            else masks.to(torch.int64)
+        if self.world == 1:
+            return self.local.integer_op(keys, ops, masks)
+
+        def ex(k, o, m):
+            st, res = self.local.integer_op(k, o, m)
+            return [st.to(torch.int32), res.to(torch.int64)]
+        st, res = self._roundtrip(keys, [ops, masks], ex, None)
+        return st, res
+
+    def meta(self, op: str, keys: torch.Tensor, args: Optional[torch.Tensor] = None):
+        args = torch.zeros(keys.shape[0], dtype=torch.int64, device=keys.device) if args is None \
+            else args.to(torch.int64)
+        if self.world == 1:
+            return self.local.meta(op, keys, args)
+
+        def ex(k, a):
+            st, out = self.local.meta(op, k, a)
+            return [st.to(torch.int32), out.to(torch.int64)]
+        st, out = self._roundtrip(keys, [args], ex, None)
+        return st, out
+
+    def set_embeddings(self, keys: torch.Tensor, vecs: torch.Tensor) -> torch.Tensor:
+        vecs = vecs.to(torch.float32)
+        if self.world == 1:
+            return self.local.set_embeddings(keys, vecs)
+        return self._roundtrip(keys, [vecs], lambda k, v: [self.local.set_embeddings(k, v).to(torch.int32)],
+                               None)[0]
+
+    # -------------------------------------------------- C2: signals -------
+    def signal_counts(self, local_counts: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Node-wide signal-group counters: sum of per-shard counters (64 x u64)."""
+        t = (self.local.signal_counts() if local_counts is None else local_counts).clone()
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
         return t
+
+    # ------------------------------------------- C3 + C4: vector search ----
+    def search(self, queries: Optional[torch.Tensor], k: int = 10, min_sim: float = -2.0,
+               max_dist: float = 3.4e38, label_mask: int = 0, nq: Optional[int] = None):
+        """Global top-k over every shard.  Rank 0's queries are broadcast (C3);
+        each shard scores its own slots, local top-k lists are all-gathered
+        (C4) and merged (sim desc, dist asc) identically on every rank.
+
+        Returns (owner_rank int64 [nq,k], sim, dist, key_rows uint8 [nq,k,64]);
+        owner -1 marks an empty position."""
+        dev = self.local.device
+        if self.world > 1:
+            n = torch.tensor([0 if queries is None else queries.shape[0]], dtype=torch.int64, device=dev)
+            dist.broadcast(n, 0, group=self.group)
+            q = torch.empty((int(n.item()), 768), dtype=torch.float32, device=dev)
+            if self.rank == 0:
+                q.copy_(queries.reshape(-1, 768))
+            dist.broadcast(q, 0, group=self.group)
+        else:
+            q = queries.reshape(-1, 768).to(device=dev, dtype=torch.float32)
+        sim, dst, krows = self.local.search(q, k, min_sim, max_dist, label_mask)
+        valid = torch.isfinite(sim) & (sim > -3.0)
+        sim = torch.where(valid, sim, torch.full_like(sim, -1e30))
+        if self.world > 1:
+            gs = [torch.empty_like(sim) for _ in range(self.world)]
+            gd = [torch.empty_like(dst) for _ in range(self.world)]
+            gk = [torch.empty_like(krows) for _ in range(self.world)]
+            dist.all_gather(gs, sim, group=self.group)
+            dist.all_gather(gd, dst, group=self.group)
+            dist.all_gather(gk, krows, group=self.group)
+            sim, dst, krows = torch.cat(gs, 1), torch.cat(gd, 1), torch.cat(gk, 1)
+        nqq, tot = sim.shape
+        owner = torch.arange(tot, device=dev).div(k, rounding_mode="floor").expand(nqq, tot)
+        # lexicographic (sim desc, dist asc): stable sort by dist, then stable sort by -sim
+        o1 = torch.argsort(dst, dim=1, stable=True)
+        s1 = torch.gather(sim, 1, o1)
+        o2 = torch.argsort(-s1, dim=1, stable=True)
+        order = torch.gather(o1, 1, o2)[:, :k]
+        sim_k = torch.gather(sim, 1, order)
+        dist_k = torch.gather(dst, 1, order)
+        own_k = torch.gather(owner, 1, order)
+        key_k = torch.gather(krows, 1, order.unsqueeze(-1).expand(-1, -1, KEY_BYTES))
+        empty = sim_k < -1e29
+        own_k = torch.where(empty, torch.full_like(own_k, -1), own_k)
+        return own_k, sim_k, dist_k, key_k
+
+    # ----------------------------------------------------- C5: enumerate ---
+    def _all_gather_var(self, t: torch.Tensor) -> torch.Tensor:
+        n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+        counts = [torch.empty_like(n) for _ in range(self.world)]
+        dist.all_gather(counts, n, group=self.group)
+        cs = [int(c.item()) for c in counts]
+        mx = max(cs) if cs else 0
+        pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        parts = [torch.empty_like(pad) for _ in range(self.world)]
+        dist.all_gather(parts, pad, group=self.group)
+        return torch.cat([p[:c] for p, c in zip(parts, cs)])
+
+    def enumerate(self, mask: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Every key (on any shard) whose bloom contains ``mask`` (0 = all keys):
+        (key rows uint8 [m, 64], epochs int64 [m]), identical on every rank."""
+        rows, ep = self.local.enumerate(mask)
+        if self.world == 1:
+            return rows, ep
+        packed = torch.cat([rows, _u8(ep.to(torch.int64))], dim=1)
+        allp = self._all_gather_var(packed)
+        krows, eps = _unpack(allp, [(torch.uint8, (KEY_BYTES,)), (torch.int64, ())])
+        return krows, eps
+
+    # --------------------------------------------------- C6: config -----
+    def sync_config(self) -> Tuple[int, List[int]]:
+        """Replicate rank 0's mop mode and label->group map to every shard."""
+        cfg = self.local.get_config().to(self.local.device)  # uint8[65]: mop, bloom_watches[64]
+        if self.world > 1:
+            dist.broadcast(cfg, 0, group=self.group)
+            if self.rank != 0:
+                self.local.apply_config(cfg)
+        c = cfg.cpu().tolist()
+        return c[0], c[1:]
 
 
 class GpuShard:
     """Local shard = an HBM arena driven by the gfx950 kernels."""
 
-    def __init__(self, arena):
+    device = "cuda"
+
+    def __init__(self, arena, search_grid: int = 512):
         self.arena = arena
+        self._search = None
+        self._grid = search_grid
 
     def hash_keys(self, keys: torch.Tensor) -> torch.Tensor:
         from .. import _native as N
-        from ..ops.arena import _check, _stream
+        from ..ops.arena import _check, _keys, _stream
+        keys = _keys(keys)
         out = torch.empty(keys.shape[0], dtype=torch.int64, device=keys.device)
         _check(N.hip_lib().spl_hash_keys(keys.data_ptr(), keys.shape[1], keys.shape[0], out.data_ptr(), _stream()),
                "hash_keys")
@@ -114,26 +288,92 @@ class GpuShard:
     def get(self, keys, **kw):
         return self.arena.get(keys, **kw)
 
+    def unset(self, keys):
+        return self.arena.unset(keys)
+
+    def integer_op(self, keys, ops, masks):
+        return self.arena.integer_op(keys, ops, masks)
+
+    def meta(self, op, keys, args):
+        return self.arena.meta(op, keys, args)
+
+    def set_embeddings(self, keys, vecs):
+        return self.arena.set_embeddings(keys, vecs.contiguous())
+
+    def key_rows(self, slots: torch.Tensor) -> torch.Tensor:
+        from .. import _native as N
+        from ..ops.arena import _stream
+        sel = slots.to(torch.int32).contiguous()
+        core = torch.empty((sel.numel(), 128), dtype=torch.uint8, device="cuda")
+        if sel.numel():
+            N.hip_lib().spl_arena_gather_slots(self.arena.desc, sel.data_ptr(), sel.numel(), core.data_ptr(),
+                                               _stream())
+        return core[:, KEY_BYTES:]
+
+    def search(self, q, k, min_sim, max_dist, label_mask):
+        from ..ops.search import VectorSearch
+        if self._search is None:
+            self._search = VectorSearch(self.arena, grid=self._grid)
+        idx, sim, dst = self._search.search(q, k, min_sim, max_dist, label_mask)
+        valid = idx >= 0
+        rows = self.key_rows(torch.where(valid, idx, torch.zeros_like(idx)).reshape(-1))
+        rows = rows.reshape(idx.shape[0], idx.shape[1], KEY_BYTES) * valid.unsqueeze(-1).to(torch.uint8)
+        sim = torch.where(valid, sim, torch.full_like(sim, -1e30))
+        dst = torch.where(valid, dst, torch.full_like(dst, 3.4e38))
+        return sim, dst, rows
+
+    def enumerate(self, mask):
+        from ..ops.arena import SCAN_LABELS, SCAN_LIST
+        idx, ep = self.arena.scan(SCAN_LABELS if mask else SCAN_LIST, mask)
+        return self.key_rows(idx), ep
+
+    def signal_counts(self):
+        h = self.arena.header_view()[128:128 + 64 * 64]
+        return h.view(torch.int64).view(64, 8)[:, 0].clone()
+
+    def get_config(self):
+        s = self.arena.store
+        cfg = torch.empty(65, dtype=torch.uint8, device="cuda")
+        cfg[0] = s.get_mop()
+        cfg[1:] = self.arena.header_view()[56:120]
+        return cfg
+
+    def apply_config(self, cfg):
+        _apply_config(self.arena.store, cfg)
+
+
+def _apply_config(store, cfg: torch.Tensor) -> None:
+    c = cfg.cpu().tolist()
+    store.set_mop(int(c[0]))
+    for bit, g in enumerate(c[1:]):
+        if g != 0xFF:
+            store.watch_label(1 << bit, int(g))
+
 
 class HostShard:
     """Local shard = a host (shm) store; CPU tensors; used for gloo tests."""
+
+    device = "cpu"
 
     def __init__(self, store):
         from .. import _native as N
         self.store = store
         self._L = N.core_lib()
 
+    @staticmethod
+    def _key(row) -> bytes:
+        return bytes(row).split(b"\0", 1)[0]
+
     def hash_keys(self, keys: torch.Tensor) -> torch.Tensor:
         k = keys.cpu().numpy()
-        hs = [self._L.spl_hash_key(bytes(row).split(b"\0", 1)[0]) for row in k]
+        hs = [self._L.spl_hash_key(self._key(row)) for row in k]
         return torch.tensor([h - (1 << 64) if h >= (1 << 63) else h for h in hs], dtype=torch.int64)
 
     def set(self, keys, vals, lens, **kw):
         k, v, ln = keys.numpy(), vals.numpy(), lens.numpy()
         st = []
         for i in range(k.shape[0]):
-            key = bytes(k[i]).split(b"\0", 1)[0]
-            rc = self._L.spl_set(self.store.handle, key, bytes(v[i, : ln[i]]), int(ln[i]))
+            rc = self._L.spl_set(self.store.handle, self._key(k[i]), bytes(v[i, : ln[i]]), int(ln[i]))
             st.append(0 if rc == 0 else -11)
         return torch.tensor(st, dtype=torch.int32)
 
@@ -144,10 +384,98 @@ class HostShard:
         lens = torch.zeros(k.shape[0], dtype=torch.int32)
         st = torch.zeros(k.shape[0], dtype=torch.int32)
         for i in range(k.shape[0]):
-            v = self.store.get(bytes(k[i]).split(b"\0", 1)[0])
+            v = self.store.get(self._key(k[i]))
             if v is None:
                 st[i] = -2
             else:
                 out[i, : len(v)] = torch.frombuffer(bytearray(v), dtype=torch.uint8)
                 lens[i] = len(v)
         return st, out, lens
+
+    def unset(self, keys):
+        return torch.tensor([0 if self.store.unset(self._key(r)) >= 0 else -2 for r in keys.numpy()],
+                            dtype=torch.int32)
+
+    def integer_op(self, keys, ops, masks):
+        st, res = [], []
+        for r, o, m in zip(keys.numpy(), ops.tolist(), masks.tolist()):
+            try:
+                res.append(self.store.integer_op(self._key(r), int(o), int(m) & 0xFFFFFFFFFFFFFFFF))
+                st.append(0)
+            except OSError:
+                res.append(0)
+                st.append(-22)
+        res = [x - (1 << 64) if x >= (1 << 63) else x for x in res]
+        return torch.tensor(st, dtype=torch.int32), torch.tensor(res, dtype=torch.int64)
+
+    def meta(self, op, keys, args):
+        fns = {"set_label": self.store.set_label, "unset_label": self.store.unset_label,
+               "bump": lambda k, a: self.store.bump(k), "epoch": lambda k, a: self.store.epoch(k),
+               "watch": self.store.watch, "unwatch": self.store.unwatch, "pulse": lambda k, a: self.store.pulse(k),
+               "find": lambda k, a: self.store.find_slot(k)}
+        st, out = [], []
+        for r, a in zip(keys.numpy(), args.tolist()):
+            v = fns[op](self._key(r), int(a))
+            ok = v is not False and not (isinstance(v, int) and not isinstance(v, bool) and v < 0)
+            st.append(0 if ok else -2)
+            out.append(int(v) if isinstance(v, (int, bool)) else 0)
+        return torch.tensor(st, dtype=torch.int32), torch.tensor(out, dtype=torch.int64)
+
+    def set_embeddings(self, keys, vecs):
+        st = []
+        for r, v in zip(keys.numpy(), vecs.numpy()):
+            try:
+                self.store.set_embedding(self._key(r), v)
+                st.append(0)
+            except OSError:
+                st.append(-2)
+        return torch.tensor(st, dtype=torch.int32)
+
+    def search(self, q, k, min_sim, max_dist, label_mask):
+        names = [n for n, _ in self.store.enumerate(label_mask)] if label_mask else self.store.list()
+        nq = q.shape[0]
+        sim = torch.full((nq, k), -1e30)
+        dst = torch.full((nq, k), 3.4e38)
+        rows = torch.zeros((nq, k, KEY_BYTES), dtype=torch.uint8)
+        vecs, keys = [], []
+        for n in names:
+            v = self.store.get_embedding(n)
+            if v is not None and float(np.sqrt((v.astype(np.float64) ** 2).sum())) >= 1e-6:
+                vecs.append(v)
+                keys.append(n)
+        if not vecs:
+            return sim, dst, rows
+        M = np.stack(vecs).astype(np.float64)
+        mn = np.sqrt((M ** 2).sum(1))
+        for j in range(nq):
+            qq = q[j].numpy().astype(np.float64)
+            s = M @ qq / (mn * np.sqrt((qq ** 2).sum()))
+            d = np.sqrt(((M - qq) ** 2).sum(1))
+            cand = [(-s[i], d[i], i) for i in range(len(keys)) if s[i] >= min_sim and d[i] <= max_dist]
+            cand.sort()
+            for t, (ns, dd, i) in enumerate(cand[:k]):
+                sim[j, t], dst[j, t] = float(-ns), float(dd)
+                kb = keys[i].encode()[:KEY_BYTES]
+                rows[j, t, : len(kb)] = torch.tensor(list(kb), dtype=torch.uint8)
+        return sim, dst, rows
+
+    def enumerate(self, mask):
+        items = self.store.enumerate(mask) if mask else [(n, self.store.epoch(n)) for n in self.store.list()]
+        rows = torch.zeros((len(items), KEY_BYTES), dtype=torch.uint8)
+        for i, (n, _) in enumerate(items):
+            kb = n.encode()[:KEY_BYTES]
+            rows[i, : len(kb)] = torch.tensor(list(kb), dtype=torch.uint8)
+        return rows, torch.tensor([e for _, e in items], dtype=torch.int64)
+
+    def signal_counts(self):
+        return torch.tensor([self.store.signal_count(g) for g in range(64)], dtype=torch.int64)
+
+    def get_config(self):
+        reg = self.store.region()
+        cfg = torch.empty(65, dtype=torch.uint8)
+        cfg[0] = self.store.get_mop()
+        cfg[1:] = torch.tensor(list(bytes(reg[56:120])), dtype=torch.uint8)
+        return cfg
+
+    def apply_config(self, cfg):
+        _apply_config(self.store, cfg)

@@ -42,9 +42,9 @@ def parse():
     p.add_argument("--slots-factor", type=float, default=2.0)
     p.add_argument("--max-val", type=int, default=256)
     p.add_argument("--value-len", type=int, default=150)
-    p.add_argument("--batch", type=int, default=8_000_000, help="client ops per rank per step")
+    p.add_argument("--batch", type=int, default=16_000_000, help="client ops per rank per step")
     p.add_argument("--set-frac", type=float, default=0.5)
-    p.add_argument("--embed-batch", type=int, default=512, help="documents per rank per step")
+    p.add_argument("--embed-batch", type=int, default=64, help="documents per rank per step")
     p.add_argument("--embed-seq", type=int, default=512)
     p.add_argument("--verify", type=int, default=20000)
     return p.parse_args()
@@ -121,7 +121,10 @@ def main():
         from libsplinter_amd.models.bench_embed import EmbedPhase
         embedder = EmbedPhase(arena, batch=args.embed_batch, seq=args.embed_seq, rank=rank)
 
-    s_set, s_get, s_emb = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    # one hardware queue per concurrent phase (utils/streams.py): KV get/set at high/normal
+    # priority, the MFMA-bound encoder at low priority filling the remaining CU slots
+    from libsplinter_amd.utils.streams import stream as hip_stream
+    s_get, s_set, s_emb = hip_stream("high"), hip_stream("normal"), hip_stream("low")
     stats = arena.stats
 
     def step(i):

@@ -99,9 +99,11 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ qkv, 
   __shared__ __attribute__((aligned(16))) uint16_t Vt[HD * AK];   // [d][key], 16-B chunks xor-swizzled
   __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * AK];  // per wave [q][key]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int seq = qblocks[2 * blockIdx.x], qstart = qblocks[2 * blockIdx.x + 1];
+  // qblocks hold 128-row blocks (k_attn2's unit); this kernel runs each as two 64-row halves
+  const int seq = qblocks[2 * (blockIdx.x >> 1)], qstart = qblocks[2 * (blockIdx.x >> 1) + 1] + (blockIdx.x & 1) * 64;
   const int head = blockIdx.y;
   const long s0 = cu[seq], len = cu[seq + 1] - s0;
+  if (qstart >= len) return;
   const long ld = 3L * heads * HD;
   const uint16_t* Qg = qkv + head * HD;
   const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
@@ -229,6 +231,188 @@ __global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ qkv, 
     uint16_t* dst = out + (s0 + q) * (long)heads * HD + head * HD;
 #pragma unroll
     for (int j = 0; j < 4; ++j) dst[j * 16 + fr] = (uint16_t)f2bf(o[j][r] * inv);
+  }
+}
+
+// ---------------------------------------------------------- attention v2 --
+// One workgroup = 128 query rows of one (sequence, head); 4 waves x 32 rows
+// (two 16-row q-blocks per wave).  "Swapped" products keep every per-query
+// quantity lane-local (guide §3 accumulator-as-operand, T10, T12):
+//   S^T = K Q^T   : mfma_16x16x32(A = K rows [key][d], B = Q rows) -> lane
+//                   holds keys 4g+r of each 16-key block for ONE query
+//                   (col = lane & 15), so the row max / sum is 15 in-lane
+//                   ops + 2 cross-group shuffles;
+//   O^T += V^T P^T: the fp32 S^T accumulators, rounded to bf16, ARE the B
+//                   operand (element j <-> key 4g+j / 16+4g+(j-4) of each
+//                   32-key step); the matching V^T A operand comes from a
+//                   row-major V image via two ds_read_b64_tr_b16 (hardware
+//                   transpose) with a chunk swizzle that keeps each
+//                   32-lane half's 8 rows x 32 B on distinct banks.
+// K/V tiles (64 keys) are register-staged one tile ahead: global loads for
+// tile t+1 issue before tile t's math, the LDS write lands after it (T14),
+// one barrier per tile, double-buffered LDS (32 KB).
+typedef short v4i16 __attribute__((ext_vector_type(4)));
+typedef short v8i16 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
+
+__device__ __forceinline__ int ksw(int key, int c) { return c ^ (key & 7); }
+__device__ __forceinline__ int vsw(int key, int c) { return c ^ (((key >> 1) & 3) << 1); }
+
+__global__ __launch_bounds__(256) void k_attn2(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                               const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
+                                               int heads, float scale_log2) {
+  __shared__ __attribute__((aligned(16))) char lds[2][2][64 * 128];  // [buf][K | V][key * 128 B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int seq = qblocks[2 * blockIdx.x], qstart = qblocks[2 * blockIdx.x + 1];
+  const int head = blockIdx.y;
+  const long s0 = cu[seq], len = cu[seq + 1] - s0;
+  const long ld = 3L * heads * HD;
+  const uint16_t* Qg = qkv + head * HD;
+  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
+  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
+
+  // Q^T B-fragments: query row qstart + wave*32 + qb*16 + li, d = kk*32 + 8g .. +7
+  bf16x8 qf[2][2];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const long qrow = qstart + wave * 32 + qb * 16 + li;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+      qf[qb][kk] = qrow < len ? *(const bf16x8*)(Qg + (s0 + qrow) * ld + kk * 32 + g * 8) : bf16x8{};
+  }
+  f32x4 o[4][2];  // O^T[d = db*16 + 4g + r][q = qb*16 + li]
+#pragma unroll
+  for (int db = 0; db < 4; ++db)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) o[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+
+  uint4 rk[2], rv[2];
+  auto gload = [&](long k0) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = tid + it * 256, key = c >> 3, ch = c & 7;
+      if (k0 + key < len) {
+        rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
+        rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
+      } else {
+        rk[it] = make_uint4(0, 0, 0, 0);
+        rv[it] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lwrite = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = tid + it * 256, key = c >> 3, ch = c & 7;
+      *(uint4*)(lds[buf][0] + key * 128 + (ksw(key, ch) << 4)) = rk[it];
+      *(uint4*)(lds[buf][1] + key * 128 + (vsw(key, ch) << 4)) = rv[it];
+    }
+  };
+
+  const int ntiles = (int)((len + 63) / 64);
+  gload(0);
+  lwrite(0);
+  __syncthreads();
+  const int tq = li >> 2, tp = li & 3;  // tr-read: this lane addresses row tq, columns 4*tp..4*tp+3
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const long k0 = (long)t * 64;
+    if (t + 1 < ntiles) gload(k0 + 64);
+    const char* Ks = lds[buf][0];
+    const char* Vs = lds[buf][1];
+    // ---- S^T = K Q^T
+    f32x4 s[4][2];
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb) {
+      const int row = kb * 16 + li;
+      bf16x8 kf[2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) kf[kk] = *(const bf16x8*)(Ks + row * 128 + (ksw(row, kk * 4 + g) << 4));
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        s[kb][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk)
+          s[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[qb][kk], s[kb][qb], 0, 0, 0);
+      }
+    }
+    // ---- online softmax, one query per lane column
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      float mx = -1e30f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const bool valid = k0 + kb * 16 + 4 * g + r < len;
+          const float v = valid ? s[kb][qb][r] * scale_log2 : -1e30f;
+          s[kb][qb][r] = v;
+          mx = fmaxf(mx, v);
+        }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      const float mn = fmaxf(m[qb], mx);
+      const float alpha = exp2f(m[qb] - mn);
+      m[qb] = mn;
+      float ps = 0.f;
+#pragma unroll
+      for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float p = exp2f(s[kb][qb][r] - mn);
+          s[kb][qb][r] = p;
+          ps += p;
+        }
+      ps += __shfl_xor(ps, 16, 64);
+      ps += __shfl_xor(ps, 32, 64);
+      l[qb] = l[qb] * alpha + ps;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+    }
+    // ---- O^T += V^T P^T, two 32-key steps
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      bf16x8 pf[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pf[qb][j] = (__bf16)s[2 * st][qb][j];
+          pf[qb][4 + j] = (__bf16)s[2 * st + 1][qb][j];
+        }
+      const int row1 = st * 32 + 4 * g + tq, row2 = row1 + 16;
+#pragma unroll
+      for (int db = 0; db < 4; ++db) {
+        const int ch = db * 2 + (tp >> 1);
+        const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_v4i16*)(Vs + row1 * 128 + (vsw(row1, ch) << 4) + 8 * (tp & 1)));
+        const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (lds_v4i16*)(Vs + row2 * 128 + (vsw(row2, ch) << 4) + 8 * (tp & 1)));
+        const v8i16 ab = __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+        const bf16x8 vf = __builtin_bit_cast(bf16x8, ab);
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb], o[db][qb], 0, 0, 0);
+      }
+    }
+    if (t + 1 < ntiles) lwrite(buf ^ 1);
+    __syncthreads();
+  }
+  // ---- normalise, store 4 consecutive d per lane
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const long q = qstart + wave * 32 + qb * 16 + li;
+    if (q >= len) continue;
+    const float inv = 1.f / l[qb];
+    uint16_t* dst = out + (s0 + q) * (long)heads * HD + head * HD + 4 * g;
+#pragma unroll
+    for (int db = 0; db < 4; ++db) {
+      uint2 w;
+      w.x = f2bf(o[db][qb][0] * inv) | (f2bf(o[db][qb][1] * inv) << 16);
+      w.y = f2bf(o[db][qb][2] * inv) | (f2bf(o[db][qb][3] * inv) << 16);
+      *(uint2*)(dst + db * 16) = w;
+    }
   }
 }
 
@@ -427,12 +611,25 @@ int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, 
   return (int)hipGetLastError();
 }
 
+static int g_attn_variant = 2;
+
+int nomic_attention_set_variant(int v) {
+  const int prev = g_attn_variant;
+  g_attn_variant = v;
+  return prev;
+}
+
 int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t* qblocks, int nqb, int heads,
                     float scale, hipStream_t s) {
   if (nqb <= 0) return 0;
+  if (heads * HD * 3 % 8) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  hipLaunchKernelGGL(k_attn, dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks,
-                     heads, scale_log2);
+  if (g_attn_variant == 2)
+    hipLaunchKernelGGL(k_attn2, dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks,
+                       heads, scale_log2);
+  else
+    hipLaunchKernelGGL(k_attn, dim3(2 * nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+                       qblocks, heads, scale_log2);
   return (int)hipGetLastError();
 }
 

@@ -22,6 +22,11 @@ extern "C" {
 int nomic_gemm(int mode, const void *A, long lda, const void *W, long ldw, long M, int N, int K,
                void *out, long ldo, const void *res, long ldr, const float *rope, const int32_t *pos,
                int rope_cols, hipStream_t stream);
+/* GEMM kernel selection: 0 = auto (default: the 256x256 8-wave phased kernel when
+ * N % 256 == 0 and the grid has >= 2048 tiles, else 128x128), 256 = force the
+ * 256x256 kernel where the shape allows, 128 = force 128x128.  Returns the
+ * previous setting. */
+int nomic_gemm_set_variant(int variant);
 
 /* x[t] = LN(tok[ids[t]] + type_row) ; bf16 out [T, 768] */
 int nomic_embed_ln(const int32_t *ids, long T, const void *tok_emb, const void *type_row,
@@ -29,8 +34,11 @@ int nomic_embed_ln(const int32_t *ids, long T, const void *tok_emb, const void *
 /* in-place (or out-of-place) LayerNorm over 768 columns, bf16 */
 int nomic_layernorm(const void *x, long T, const void *gamma, const void *beta, float eps, void *out,
                     hipStream_t stream);
+/* attention kernel: 2 = swapped-product 128-row kernel (default), 1 = 64-row kernel */
+int nomic_attention_set_variant(int variant);
 /* varlen non-causal attention; qkv [T, 3*H*64] (q|k|v), out [T, H*64].
- * qblocks: [nqb] int32 pairs (seq index, q start offset in the sequence)  */
+ * qblocks: [nqb] int32 pairs (seq index, q start offset in the sequence) of
+ * 128-row query blocks (q starts are multiples of 128)                    */
 int nomic_attention(const void *qkv, void *out, const int32_t *cu_seqlens, const int32_t *qblocks,
                     int nqb, int heads, float scale, hipStream_t stream);
 /* mean over each sequence's tokens -> fp32 [B, 768]; if slots != NULL also

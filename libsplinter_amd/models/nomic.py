@@ -67,6 +67,10 @@ def _lib():
         P, c_long, c_int, c_float = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float
         L.nomic_gemm.argtypes = [c_int, P, c_long, P, c_long, c_long, c_int, c_int, P, c_long, P, c_long, P, P, c_int, P]
         L.nomic_gemm.restype = c_int
+        L.nomic_gemm_set_variant.argtypes = [c_int]
+        L.nomic_gemm_set_variant.restype = c_int
+        L.nomic_attention_set_variant.argtypes = [c_int]
+        L.nomic_attention_set_variant.restype = c_int
         L.nomic_embed_ln.argtypes = [P, c_long, P, P, P, P, c_float, P, P]
         L.nomic_embed_ln.restype = c_int
         L.nomic_layernorm.argtypes = [P, c_long, P, P, c_float, P, P]
@@ -247,7 +251,7 @@ class NomicReference(torch.nn.Module):
 class Batch:
     """A packed varlen batch: token ids, sequence offsets, positions, q-blocks."""
 
-    def __init__(self, seqs: Sequence[Sequence[int]], device="cuda", qblock: int = 64):
+    def __init__(self, seqs: Sequence[Sequence[int]], device="cuda", qblock: int = 128):
         lens = [len(s) for s in seqs]
         assert all(n > 0 for n in lens), "empty sequence"
         self.B = len(seqs)

@@ -12,13 +12,22 @@ def _rel(a, b):
 
 
 @pytest.fixture(scope="module")
-def L():
+def L0():
     import torch  # noqa: F401
     from libsplinter_amd.models.nomic import _lib
     return _lib()
 
 
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 768, 768), (1000, 2304, 768), (257, 768, 3072)])
+@pytest.fixture(params=[256, 128], ids=["gemm256", "gemm128"])
+def L(L0, request):
+    """Run each GEMM numerics test on both kernel variants."""
+    prev = L0.nomic_gemm_set_variant(request.param)
+    yield L0
+    L0.nomic_gemm_set_variant(prev)
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 768, 768), (1000, 2304, 768), (257, 768, 3072),
+                                   (4096, 2304, 768)])
 def test_gemm_store_and_residual(L, M, N, K):
     import torch
     from libsplinter_amd.models.nomic import _chk, _stream
@@ -90,17 +99,28 @@ def test_gemm_swiglu_and_rope(L):
     assert _rel(qkv[:M].float(), ref) < 1e-2
 
 
-def test_attention_varlen(L):
+@pytest.mark.parametrize("variant", [2, 1])
+@pytest.mark.parametrize("spike", [False, True])
+def test_attention_varlen(L0, variant, spike):
+    L = L0
     import torch
     from libsplinter_amd.models.nomic import Batch, _chk, _stream
     torch.manual_seed(2)
-    lens = [1, 17, 64, 65, 200, 513]
+    lens = [1, 17, 64, 65, 127, 128, 129, 200, 513]
     b = Batch([[0] * n for n in lens])
     T = b.T
     qkv = torch.randn(b.T_pad, 3 * 768, device="cuda").bfloat16()
+    if spike:  # a late key that dominates one query's row: forces the online-max rescale path
+        s0 = int(b.cu_host[8])
+        qkv[s0 + 3, :64] = 4.0
+        qkv[s0 + 450, 768:768 + 64] = 4.0
     out = torch.zeros(b.T_pad, 768, device="cuda", dtype=torch.bfloat16)
-    _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
-                           1 / 8.0, _stream()), "attn")
+    prev = L.nomic_attention_set_variant(variant)
+    try:
+        _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
+                               1 / 8.0, _stream()), "attn")
+    finally:
+        L.nomic_attention_set_variant(prev)
     q, k, v = qkv[:T].float().split(768, 1)
     refs = []
     for i in range(len(lens)):
@@ -111,7 +131,8 @@ def test_attention_varlen(L):
     assert _rel(out[:T].float(), torch.cat(refs)) < 1e-2
 
 
-def test_layernorm_and_embed(L):
+def test_layernorm_and_embed(L0):
+    L = L0
     import torch
     from libsplinter_amd.models.nomic import _chk, _stream
     torch.manual_seed(3)

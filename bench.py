@@ -121,21 +121,18 @@ def main():
         from libsplinter_amd.models.bench_embed import EmbedPhase
         embedder = EmbedPhase(arena, batch=args.embed_batch, seq=args.embed_seq, rank=rank)
 
-    # one hardware queue per concurrent phase (utils/streams.py): KV get/set at high/normal
-    # priority, the MFMA-bound encoder at low priority filling the remaining CU slots
+    # set and get batches race each other on two hardware queues (utils/streams.py: distinct
+    # priorities = distinct queue pools).  The embed phase runs AFTER the KV phase, not beside it:
+    # the seqlock kernels' agent-scope release/acquire fences write back / invalidate the XCD L2s,
+    # which stretched the concurrently running GEMMs 2x and made the overlapped step slower than
+    # the serial one (profiles/r1_mixed_overlap.md).
     from libsplinter_amd.utils.streams import stream as hip_stream
-    s_get, s_set, s_emb = hip_stream("high"), hip_stream("normal"), hip_stream("low")
+    s_get, s_set = hip_stream("high"), hip_stream("normal")
     stats = arena.stats
 
     def step(i):
-        # KV batches (memory/latency bound) and the embed batch (MFMA bound)
-        # run on separate HIP streams so they overlap on the chip.
         SK, SV, SL, GK, _ = batches[i % nbuf]
         cur = torch.cuda.current_stream()
-        if embedder is not None:
-            s_emb.wait_stream(cur)
-            with torch.cuda.stream(s_emb):
-                embedder.run()
         if n_set:
             s_set.wait_stream(cur)
             s_get.wait_stream(cur)
@@ -151,7 +148,7 @@ def main():
             cur.wait_stream(s_set)
             cur.wait_stream(s_get)
         if embedder is not None:
-            cur.wait_stream(s_emb)
+            embedder.run()
 
     for i in range(args.warmup):
         step(i)

@@ -102,3 +102,16 @@ def test_repl_and_namespace(store):
     r = subprocess.run([os.path.join(BIN, "splinterctl"), "-u", store, "--prefix", "ns_", "set", "k", "v"],
                        capture_output=True, text=True)
     assert r.returncode == 0 and ctl(store, "get", "ns_k")[1].startswith("v")
+
+
+def test_sidecar_once_shows_debug_labelled_keys(store, tmp_path):
+    ctl(store, "set", "dbgkey", "debug chatter")
+    ctl(store, "label", "dbgkey", "0x0800000000000000")  # reference sidecar debug bloom (bit 59)
+    r = subprocess.run([os.path.join(BIN, "sidecar"), f"spl:{store}", "--once"], capture_output=True, text=True,
+                       timeout=30)
+    assert r.returncode == 0, r.stderr
+    assert "debug chatter" in r.stdout and "History (CPU" in r.stdout
+    log = tmp_path / "app.log"
+    log.write_text("line one\nline two\n")
+    r = subprocess.run([os.path.join(BIN, "sidecar"), str(log), "--once"], capture_output=True, text=True, timeout=30)
+    assert "line two" in r.stdout

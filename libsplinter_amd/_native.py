@@ -118,6 +118,7 @@ def _declare_core(L):
     _sig(L, "spl_store_geometry", c_int, S, ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u32))
     _sig(L, "spl_store_base", c_void_p, S)
     _sig(L, "spl_store_bytes", c_size_t, S)
+    _sig(L, "spl_store_sync", c_int, S, c_int)
     _sig(L, "spl_unlink", c_int, c_char_p)
     _sig(L, "spl_version", c_char_p)
     _sig(L, "spl_build", c_char_p)

@@ -548,6 +548,153 @@ int cmd_export(int argc, char** argv) {
   return 0;
 }
 
+// Minimal JSON reader for `import` (the inverse of `export json`; the reference
+// has export only, SURVEY §5 checkpoint/resume).
+struct JVal {
+  enum Kind { Null, Bool, Num, Str, Arr, Obj } kind = Null;
+  double num = 0;
+  bool b = false;
+  std::string str;
+  std::vector<JVal> arr;
+  std::vector<std::pair<std::string, JVal>> obj;
+  const JVal* get(const char* k) const {
+    for (auto& kv : obj)
+      if (kv.first == k) return &kv.second;
+    return nullptr;
+  }
+};
+
+struct JParser {
+  const char* p;
+  const char* end;
+  bool ok = true;
+  void ws() { while (p < end && isspace((unsigned char)*p)) ++p; }
+  bool lit(const char* s) {
+    size_t n = strlen(s);
+    if ((size_t)(end - p) >= n && !strncmp(p, s, n)) { p += n; return true; }
+    return false;
+  }
+  std::string string() {
+    std::string out;
+    ++p;  // opening quote
+    while (p < end && *p != '"') {
+      if (*p == '\\' && p + 1 < end) {
+        ++p;
+        switch (*p) {
+          case 'n': out += '\n'; break;
+          case 't': out += '\t'; break;
+          case 'r': out += '\r'; break;
+          case 'b': out += '\b'; break;
+          case 'f': out += '\f'; break;
+          case 'u': {
+            if (end - p < 5) { ok = false; return out; }
+            unsigned cp = (unsigned)strtoul(std::string(p + 1, 4).c_str(), nullptr, 16);
+            p += 4;
+            if (cp < 0x80) out += (char)cp;
+            else if (cp < 0x800) { out += (char)(0xC0 | (cp >> 6)); out += (char)(0x80 | (cp & 0x3F)); }
+            else { out += (char)(0xE0 | (cp >> 12)); out += (char)(0x80 | ((cp >> 6) & 0x3F)); out += (char)(0x80 | (cp & 0x3F)); }
+            break;
+          }
+          default: out += *p;
+        }
+        ++p;
+      } else {
+        out += *p++;
+      }
+    }
+    if (p < end) ++p; else ok = false;
+    return out;
+  }
+  JVal value() {
+    JVal v;
+    ws();
+    if (p >= end) { ok = false; return v; }
+    if (*p == '{') {
+      v.kind = JVal::Obj;
+      ++p;
+      ws();
+      if (p < end && *p == '}') { ++p; return v; }
+      while (ok) {
+        ws();
+        if (p >= end || *p != '"') { ok = false; break; }
+        std::string k = string();
+        ws();
+        if (p >= end || *p != ':') { ok = false; break; }
+        ++p;
+        v.obj.emplace_back(k, value());
+        ws();
+        if (p < end && *p == ',') { ++p; continue; }
+        if (p < end && *p == '}') { ++p; break; }
+        ok = false;
+      }
+    } else if (*p == '[') {
+      v.kind = JVal::Arr;
+      ++p;
+      ws();
+      if (p < end && *p == ']') { ++p; return v; }
+      while (ok) {
+        v.arr.push_back(value());
+        ws();
+        if (p < end && *p == ',') { ++p; continue; }
+        if (p < end && *p == ']') { ++p; break; }
+        ok = false;
+      }
+    } else if (*p == '"') {
+      v.kind = JVal::Str;
+      v.str = string();
+    } else if (lit("true")) { v.kind = JVal::Bool; v.b = true; }
+    else if (lit("false")) { v.kind = JVal::Bool; }
+    else if (lit("null")) { v.kind = JVal::Null; }
+    else {
+      char* e = nullptr;
+      v.num = strtod(p, &e);
+      if (e == p) ok = false;
+      v.kind = JVal::Num;
+      p = e;
+    }
+    return v;
+  }
+};
+
+unsigned type_from_full_name(const std::string& s) {
+  for (unsigned t = 1; t <= SPL_SLOT_TYPE_VARTEXT; t <<= 1)
+    if (s == type_name(t)) return t;
+  return 0;
+}
+
+int cmd_import(int argc, char** argv) {
+  if (!need_store("import")) return 1;
+  const char* file = argc >= 2 ? argv[1] : "-";
+  FILE* f = strcmp(file, "-") ? fopen(file, "rb") : stdin;
+  if (!f) { fprintf(stderr, "import: cannot open '%s': %s\n", file, strerror(errno)); return 1; }
+  std::string text;
+  char buf[65536];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) text.append(buf, n);
+  if (f != stdin) fclose(f);
+  JParser jp{text.data(), text.data() + text.size()};
+  JVal root = jp.value();
+  const JVal* keys = root.get("keys");
+  if (!jp.ok || !keys || keys->kind != JVal::Arr) { fprintf(stderr, "import: not an `export json` document\n"); return 1; }
+  size_t done = 0, skipped = 0;
+  for (const JVal& k : keys->arr) {
+    const JVal* name = k.get("key");
+    const JVal* val = k.get("value");
+    if (!name || name->kind != JVal::Str || !val || val->kind != JVal::Str) { ++skipped; continue; }
+    const std::string key = pkey(name->str.c_str());
+    if (splinter_set(key.c_str(), val->str.data(), val->str.size()) != 0) {
+      fprintf(stderr, "import: set '%s' failed: %s\n", key.c_str(), strerror(errno));
+      return 1;
+    }
+    if (const JVal* t = k.get("type"))
+      if (unsigned tm = t->kind == JVal::Str ? type_from_full_name(t->str) : 0)
+        splinter_set_named_type(key.c_str(), (uint16_t)tm);
+    ++done;
+  }
+  printf("imported %zu key(s), skipped %zu without a value\n", done, skipped);
+  return 0;
+}
+
 int cmd_type(int argc, char** argv) {
   if (argc < 2) { fprintf(stderr, "Usage: type <key_name> [type]\n"); return 1; }
   if (!need_store("type")) return 1;
@@ -1058,6 +1205,7 @@ void register_modules() {
       {"init", "Initialize a new store.", cmd_init,
        [] { puts("Usage: init [--slots N] [--length N] [--embeddings|--no-embeddings] [store]"); }},
       {"export", "Export the store to standard output.", cmd_export, [] { puts("Usage: export [json] [max_lines]"); }},
+      {"import", "Import keys from an `export json` document.", cmd_import, [] { puts("Usage: import [file|-]"); }},
       {"type", "Display or set the named type of a key.", cmd_type,
        [] { puts("Usage: type <key> [void|bigint|biguint|json|binary|img|audio|vartext]"); }},
       {"math", "Atomic integer operations on BIGUINT keys.", cmd_math,

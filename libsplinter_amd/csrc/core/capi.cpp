@@ -204,6 +204,14 @@ size_t spl_store_bytes(spl_store* h) {
   auto* s = dynamic_cast<spl::HostStore*>((StoreBase*)h);
   return s ? s->total_bytes() : (h ? ((StoreBase*)h)->geometry().total_bytes() : 0);
 }
+int spl_store_sync(spl_store* h, int async) {
+  // Durability point for file-backed stores (the reference maps MAP_SHARED and
+  // never msyncs, SURVEY §5 checkpoint/resume).  shm: nothing to flush.
+  auto* s = dynamic_cast<spl::HostStore*>((StoreBase*)h);
+  if (!s) { errno = EOPNOTSUPP; return -1; }
+  if (!s->base()) { errno = EINVAL; return -1; }
+  return msync(s->base(), s->total_bytes(), async ? MS_ASYNC : MS_SYNC);
+}
 int spl_unlink(const char* raw) {
   Parsed p = parse_name(raw);
   if (p.kind == Kind::File) return unlink(p.name.c_str());

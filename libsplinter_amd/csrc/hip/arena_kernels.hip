@@ -511,7 +511,10 @@ __global__ __launch_bounds__(kBlock) void k_scan(spl_arena_t aa, int mode, uint6
     if (i < a.slots) {
       const uint8_t* s = a.slot(i);
       const uint64_t h = slot_hash(s);
-      if (h != 0) {
+      if (mode == 4) {  // watchdog: writer-active (odd) epochs, claimed-but-unpublished slots included
+        ep = slot_epoch(s);
+        hit = (ep & 1) != 0;
+      } else if (h != 0) {
         ep = slot_epoch(s);
         if (mode == 0) hit = ald32((const uint32_t*)(s + kOffValLen)) > 0;
         else if (mode == 1) hit = (ald64((const uint64_t*)(s + kOffBloom)) & mask) == mask;

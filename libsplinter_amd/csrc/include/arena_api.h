@@ -48,6 +48,7 @@ typedef void *hipStream_t;
 #define SPL_SCAN_LABELS    1
 #define SPL_SCAN_EMBEDDED  2
 #define SPL_SCAN_OCCUPIED  3
+#define SPL_SCAN_ODD       4   /* watchdog: slots whose epoch is odd (writer active / crashed) */
 
 int spl_arena_init_slots(spl_arena_t a, hipStream_t stream);
 int spl_arena_set(spl_arena_t a, const char *keys, int kstride, const uint8_t *vals, int vstride,

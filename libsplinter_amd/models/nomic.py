@@ -29,6 +29,7 @@ import numpy as np
 import torch
 
 from .. import _native as N
+from ..utils.tracing import trace_range
 from .gguf import DEVICE_DEQUANT, GGUFFile, GGUFWriter, dequant_host
 
 EPI_STORE, EPI_RESIDUAL, EPI_SWIGLU, EPI_ROPE, EPI_F32 = 0, 1, 2, 3, 4
@@ -335,7 +336,8 @@ class NomicEncoder:
               hashes: Optional[torch.Tensor] = None, out: Optional[torch.Tensor] = None):
         """Mean-pooled [B, 768] fp32; with arena+slots the vectors are also written
         into the arena slots under the seqlock (returns (vectors, status))."""
-        self.hidden(b)
+        with trace_range("nomic.encoder"):
+            self.hidden(b)
         if out is None:
             out = torch.empty((b.B, self.cfg.d), dtype=torch.float32, device="cuda")
         status = None

@@ -18,13 +18,14 @@ from typing import Iterable, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ..utils.tracing import trace_range
 from .. import _native as N
 from ..store import Store
 
 OK, EAGAIN, ENOENT, ENOSPC, EMSGSIZE, EPROTOTYPE, EINVAL = 0, -11, -2, -28, -90, -71, -22
 META = {"set_label": 0, "unset_label": 1, "bump": 2, "epoch": 3, "watch": 4, "unwatch": 5, "pulse": 6,
         "system": 7, "retrain": 8, "type": 9, "ctime": 10, "atime": 11, "find": 12}
-SCAN_LIST, SCAN_LABELS, SCAN_EMBEDDED, SCAN_OCCUPIED = 0, 1, 2, 3
+SCAN_LIST, SCAN_LABELS, SCAN_EMBEDDED, SCAN_OCCUPIED, SCAN_ODD = 0, 1, 2, 3, 4
 
 
 def _stream() -> int:
@@ -125,9 +126,10 @@ class HbmArena:
         assert vals.shape[0] == n and lens.shape[0] == n and lens.dtype in (torch.int32, torch.uint32)
         if status is None:
             status = torch.empty(n, dtype=torch.int32, device=keys.device)
-        _check(self._H.spl_arena_set(self.desc, keys.data_ptr(), keys.shape[1], vals.data_ptr(), vals.shape[1],
-                                     lens.data_ptr(), n, status.data_ptr(), retries, self.stats.data_ptr(),
-                                     _stream()), "arena_set")
+        with trace_range("arena.set"):
+            _check(self._H.spl_arena_set(self.desc, keys.data_ptr(), keys.shape[1], vals.data_ptr(), vals.shape[1],
+                                         lens.data_ptr(), n, status.data_ptr(), retries, self.stats.data_ptr(),
+                                         _stream()), "arena_set")
         return status
 
     def get(self, keys: torch.Tensor, out: Optional[torch.Tensor] = None, retries: int = 64,
@@ -141,9 +143,10 @@ class HbmArena:
             status = torch.empty(n, dtype=torch.int32, device=keys.device)
         if out_lens is None:
             out_lens = torch.empty(n, dtype=torch.int32, device=keys.device)
-        _check(self._H.spl_arena_get(self.desc, keys.data_ptr(), keys.shape[1], out.data_ptr(), out.shape[1],
-                                     out_lens.data_ptr(), n, status.data_ptr(), retries, self.stats.data_ptr(),
-                                     _stream()), "arena_get")
+        with trace_range("arena.get"):
+            _check(self._H.spl_arena_get(self.desc, keys.data_ptr(), keys.shape[1], out.data_ptr(), out.shape[1],
+                                         out_lens.data_ptr(), n, status.data_ptr(), retries, self.stats.data_ptr(),
+                                         _stream()), "arena_get")
         return status, out, out_lens
 
     def unset(self, keys: torch.Tensor, retries: int = 64) -> torch.Tensor:
@@ -204,6 +207,24 @@ class HbmArena:
                                       _stream()), "arena_scan")
         n = min(int(cnt.item()), cap)
         return idx[:n], ep[:n]
+
+    def stuck_slots(self, hold_ms: float = 50.0) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Watchdog (SURVEY §5 failure detection): slots whose epoch is odd in two
+        scans ``hold_ms`` apart with the SAME epoch, i.e. a writer that started and
+        never finished (crashed process, killed kernel).  The reference's only
+        recovery is retrain (splinter.c:799-833); callers decide whether to
+        ``meta("retrain", ...)`` the returned keys.  Returns (slot idx, epoch)."""
+        import time
+        i1, e1 = self.scan(SCAN_ODD)
+        torch.cuda.synchronize()
+        time.sleep(hold_ms / 1e3)
+        i2, e2 = self.scan(SCAN_ODD)
+        if i1.numel() == 0 or i2.numel() == 0:
+            return i2[:0], e2[:0]
+        first = dict(zip(i1.tolist(), e1.tolist()))
+        keep = [k for k, (i, e) in enumerate(zip(i2.tolist(), e2.tolist())) if first.get(i) == e]
+        sel = torch.tensor(keep, dtype=torch.long, device=i2.device)
+        return i2[sel], e2[sel]
 
     def purge(self):
         _check(self._H.spl_arena_purge(self.desc, _stream()), "arena_purge")

@@ -372,6 +372,30 @@ class Store:
     def find_slot(self, key) -> int:
         return self._L.spl_find_slot(self._h, _k(key))
 
+    def sync(self, async_: bool = False) -> None:
+        """msync a file-backed (persistent) store to its file."""
+        if self._L.spl_store_sync(self._h, int(async_)) != 0:
+            _raise(f"sync {self.name}")
+
+    def epochs(self) -> np.ndarray:
+        """Zero-copy uint64 view of every slot's seqlock epoch (host backends)."""
+        reg = self.region()
+        if reg is None:
+            raise NotImplementedError("epochs(): host backends only (use HbmArena.stuck_slots on hbm:)")
+        raw = np.frombuffer(reg, dtype=np.uint8, count=5440 + self.slots * self.stride)
+        return np.lib.stride_tricks.as_strided(raw[5440 + 8:].view(np.uint64), shape=(self.slots,),
+                                               strides=(self.stride,), writeable=False)
+
+    def stuck_slots(self, hold_ms: float = 50.0) -> List[int]:
+        """Watchdog: slots odd (writer active) with an unchanged epoch across
+        ``hold_ms`` -- a writer that died mid-write.  Recovery is the
+        caller's call: :meth:`retrain` forces epoch 4 (splinter.c:799-833)."""
+        import time
+        e1 = self.epochs().copy()
+        time.sleep(hold_ms / 1e3)
+        e2 = self.epochs()
+        return [int(i) for i in np.nonzero((e1 & 1) & (e1 == e2))[0]]
+
     def __repr__(self):
         return (f"Store({self.name!r}, backend={self.backend}, slots={self.slots}, max_val={self.max_val}, "
                 f"embeddings={self.embeddings})")

@@ -179,3 +179,26 @@ def test_checkpoint_roundtrip_to_host_backend(arena, uniq, tmp_path):
         h.close()
     arena.restore(path)
     assert s.get("p8") == b"changed"
+
+
+def test_watchdog_finds_stuck_writer_and_retrain_recovers(arena):
+    """A slot left odd (writer died mid-write) is reported by the odd-epoch scan
+    watchdog, and retrain (epoch -> 4) makes it readable again."""
+    import torch
+    from libsplinter_amd.ops.arena import pack_keys, pack_values
+    K = pack_keys([f"w{i}" for i in range(100)], 16)
+    V, L = pack_values([b"v"] * 100, 16)
+    assert (arena.set(K, V, L) == 0).all()
+    st, idx = arena.meta("find", K[7:8])
+    slot = int(idx[0])
+    sv = arena.slot_view()
+    ep = sv[slot, 8:16].clone().view(torch.int64)
+    sv[slot, 8:16] = (ep | 1).view(torch.uint8)  # simulate a crashed writer
+    torch.cuda.synchronize()
+    stuck, eps = arena.stuck_slots(hold_ms=20)
+    assert stuck.tolist() == [slot] and int(eps[0]) & 1
+    st, _, _ = arena.get(K[7:8], retries=4)
+    assert int(st[0]) == -11  # EAGAIN while the writer "holds" the slot
+    assert int(arena.meta("retrain", K[7:8])[0][0]) == 0
+    assert arena.stuck_slots(hold_ms=1)[0].numel() == 0
+    assert int(arena.get(K[7:8])[0][0]) == 0

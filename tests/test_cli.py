@@ -115,3 +115,20 @@ def test_sidecar_once_shows_debug_labelled_keys(store, tmp_path):
     log.write_text("line one\nline two\n")
     r = subprocess.run([os.path.join(BIN, "sidecar"), str(log), "--once"], capture_output=True, text=True, timeout=30)
     assert "line two" in r.stdout
+
+
+def test_export_import_roundtrip(store, uniq, tmp_path):
+    ctl(store, "set", "doc", "line one\nline \"two\"")
+    ctl(store, "type", "doc", "vartext")
+    dump = tmp_path / "dump.json"
+    dump.write_text(ctl(store, "export")[1])
+    other = uniq + "_imp"
+    assert ctl(other, "init", "--slots", "64", "--length", "512", other)[0] == 0
+    try:
+        rc, out, err = ctl(other, "import", str(dump))
+        assert rc == 0 and "imported 1 key(s)" in out, err
+        assert ctl(other, "get", "doc")[1].startswith('line one\nline "two"')
+        assert ctl(other, "type", "doc")[1].startswith("SPL_SLOT_TYPE_VARTEXT")
+    finally:
+        from libsplinter_amd import unlink
+        unlink(other)

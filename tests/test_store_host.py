@@ -141,3 +141,17 @@ def test_open_rejects_garbage(tmp_path):
     p.write_bytes(b"\0" * 8192)
     with pytest.raises(SplinterError):
         Store.open(str(p))
+
+
+def test_watchdog_stuck_writer_host(store):
+    import ctypes
+    store.set("victim", "data")
+    i = store.find_slot("victim")
+    assert i >= 0 and store.stuck_slots(hold_ms=1) == []
+    reg = store.region()
+    off = 5440 + i * store.stride + 8
+    ep = ctypes.c_uint64.from_buffer(reg, off)
+    ep.value |= 1  # writer "crashed" mid-write
+    assert store.stuck_slots(hold_ms=5) == [i]
+    assert store.retrain("victim")
+    assert store.stuck_slots(hold_ms=1) == [] and store.epoch("victim") == 4

@@ -1,0 +1,1644 @@
+// minilua.cpp — lexer, parser, tree-walking evaluator and standard library
+// subset for the `lua` verb (see minilua.hpp for scope).
+#include "minilua.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <ctime>
+#include <random>
+
+namespace mlua {
+
+// ------------------------------------------------------------ values ------
+static bool float_is_int(double d, int64_t* out) {
+  if (std::isfinite(d) && d == std::floor(d) && d >= -9.2233720368547758e18 && d < 9.2233720368547758e18) {
+    *out = (int64_t)d;
+    return true;
+  }
+  return false;
+}
+
+size_t ValueHash::operator()(const Value& v) const {
+  switch (v.t) {
+    case Value::Nil: return 0;
+    case Value::Bool: return v.b ? 1 : 2;
+    case Value::Int: return std::hash<int64_t>()(v.i);
+    case Value::Num: {
+      int64_t i;
+      if (float_is_int(v.n, &i)) return std::hash<int64_t>()(i);
+      return std::hash<double>()(v.n);
+    }
+    case Value::Str: return std::hash<std::string>()(*v.s);
+    case Value::Tab: return std::hash<const void*>()(v.tab.get());
+    case Value::Fn: return std::hash<const void*>()(v.fn.get());
+  }
+  return 0;
+}
+
+static bool raw_equal(const Value& a, const Value& b) {
+  if (a.is_num() && b.is_num()) {
+    if (a.t == Value::Int && b.t == Value::Int) return a.i == b.i;
+    return a.as_double() == b.as_double();
+  }
+  if (a.t != b.t) return false;
+  switch (a.t) {
+    case Value::Nil: return true;
+    case Value::Bool: return a.b == b.b;
+    case Value::Str: return *a.s == *b.s;
+    case Value::Tab: return a.tab == b.tab;
+    case Value::Fn: return a.fn == b.fn;
+    default: return false;
+  }
+}
+
+bool ValueEq::operator()(const Value& a, const Value& b) const { return raw_equal(a, b); }
+
+static Value norm_key(const Value& k) {
+  int64_t i;
+  if (k.t == Value::Num && float_is_int(k.n, &i)) return Value::integer(i);
+  return k;
+}
+
+Value Table::get(const Value& k) const {
+  auto it = index.find(norm_key(k));
+  return it == index.end() ? Value() : entries[it->second].second;
+}
+
+void Table::set(const Value& k0, const Value& v) {
+  if (k0.t == Value::Nil) throw LuaError("table index is nil");
+  if (k0.t == Value::Num && std::isnan(k0.n)) throw LuaError("table index is NaN");
+  const Value k = norm_key(k0);
+  auto it = index.find(k);
+  if (it != index.end()) {
+    entries[it->second].second = v;
+  } else if (v.t != Value::Nil) {
+    index.emplace(k, entries.size());
+    entries.emplace_back(k, v);
+  }
+}
+
+int64_t Table::length() const {
+  int64_t n = 0;
+  while (get(Value::integer(n + 1)).t != Value::Nil) ++n;
+  return n;
+}
+
+static std::string fmt_number(double d) {  // lua_Number format "%.14g", ".0" when it reads as an integer
+  if (std::isinf(d)) return d > 0 ? "inf" : "-inf";
+  if (std::isnan(d)) return "nan";
+  char b[64];
+  snprintf(b, sizeof b, "%.14g", d);
+  if (strspn(b, "-0123456789") == strlen(b)) strcat(b, ".0");
+  return b;
+}
+
+std::string tostring(const Value& v) {
+  char b[64];
+  switch (v.t) {
+    case Value::Nil: return "nil";
+    case Value::Bool: return v.b ? "true" : "false";
+    case Value::Int: snprintf(b, sizeof b, "%lld", (long long)v.i); return b;
+    case Value::Num: return fmt_number(v.n);
+    case Value::Str: return *v.s;
+    case Value::Tab: snprintf(b, sizeof b, "table: %p", (void*)v.tab.get()); return b;
+    case Value::Fn: snprintf(b, sizeof b, "function: %p", (void*)v.fn.get()); return b;
+  }
+  return "?";
+}
+
+static const char* type_name(const Value& v) {
+  switch (v.t) {
+    case Value::Nil: return "nil";
+    case Value::Bool: return "boolean";
+    case Value::Int:
+    case Value::Num: return "number";
+    case Value::Str: return "string";
+    case Value::Tab: return "table";
+    case Value::Fn: return "function";
+  }
+  return "?";
+}
+
+Value make_native(const std::string& name, Native f) {
+  auto fn = std::make_shared<Function>();
+  fn->native = std::move(f);
+  fn->name = name;
+  return Value::function(fn);
+}
+
+// string -> number (Lua coercion rules, decimal/hex ints and floats)
+static bool str2num(const std::string& s0, Value* out) {
+  std::string s = s0;
+  size_t a = s.find_first_not_of(" \t\n\r\f\v"), b = s.find_last_not_of(" \t\n\r\f\v");
+  if (a == std::string::npos) return false;
+  s = s.substr(a, b - a + 1);
+  const char* c = s.c_str();
+  char* end = nullptr;
+  bool neg = false;
+  const char* p = c;
+  if (*p == '-' || *p == '+') { neg = *p == '-'; ++p; }
+  if (p[0] == '0' && (p[1] == 'x' || p[1] == 'X')) {
+    errno = 0;
+    unsigned long long u = strtoull(p + 2, &end, 16);
+    if (*end == 0 && end != p + 2) { *out = Value::integer(neg ? -(int64_t)u : (int64_t)u); return true; }
+    return false;
+  }
+  bool isint = s.find_first_of(".eEnN") == std::string::npos;
+  if (isint) {
+    errno = 0;
+    long long v = strtoll(c, &end, 10);
+    if (*end == 0 && errno == 0) { *out = Value::integer(v); return true; }
+  }
+  double d = strtod(c, &end);
+  if (*end == 0 && end != c) { *out = Value::number(d); return true; }
+  return false;
+}
+
+static bool tonum(const Value& v, Value* out) {
+  if (v.is_num()) { *out = v; return true; }
+  if (v.t == Value::Str) return str2num(*v.s, out);
+  return false;
+}
+
+static int64_t toint_strict(const Value& v, const char* what) {
+  Value n;
+  if (!tonum(v, &n)) throw LuaError(std::string("bad argument (number expected, got ") + type_name(v) + ") to " + what);
+  if (n.t == Value::Int) return n.i;
+  int64_t i;
+  if (float_is_int(n.n, &i)) return i;
+  throw LuaError(std::string("number has no integer representation in ") + what);
+}
+
+// ------------------------------------------------------------ lexer -------
+enum Tok {
+  T_EOF, T_NAME, T_NUMBER, T_STRING,
+  T_AND, T_BREAK, T_DO, T_ELSE, T_ELSEIF, T_END, T_FALSE, T_FOR, T_FUNCTION, T_IF, T_IN, T_LOCAL, T_NIL, T_NOT,
+  T_OR, T_REPEAT, T_RETURN, T_THEN, T_TRUE, T_UNTIL, T_WHILE,
+  T_EQ, T_NE, T_LE, T_GE, T_CONCAT, T_DOTS, T_IDIV, T_SHL, T_SHR, T_DBCOLON,
+  T_CHAR  // single-char token in `ch`
+};
+
+struct Token {
+  Tok t = T_EOF;
+  std::string s;
+  Value num;
+  char ch = 0;
+  int line = 1;
+};
+
+struct Lexer {
+  const std::string& src;
+  size_t p = 0;
+  int line = 1;
+  std::string chunk;
+  explicit Lexer(const std::string& s, std::string c) : src(s), chunk(std::move(c)) {}
+
+  [[noreturn]] void err(const std::string& m) { throw LuaError(chunk + ":" + std::to_string(line) + ": " + m); }
+  char at(size_t k = 0) const { return p + k < src.size() ? src[p + k] : 0; }
+
+  bool long_bracket(std::string* out) {  // at '[': [[...]] or [==[...]==]
+    size_t q = p + 1;
+    int level = 0;
+    while (q < src.size() && src[q] == '=') { ++level; ++q; }
+    if (q >= src.size() || src[q] != '[') return false;
+    q++;
+    if (q < src.size() && src[q] == '\n') { ++line; ++q; }
+    std::string close = "]" + std::string((size_t)level, '=') + "]";
+    size_t e = src.find(close, q);
+    if (e == std::string::npos) err("unfinished long string");
+    for (size_t k = q; k < e; ++k) if (src[k] == '\n') ++line;
+    if (out) *out = src.substr(q, e - q);
+    p = e + close.size();
+    return true;
+  }
+
+  void skip() {
+    for (;;) {
+      char c = at();
+      if (c == '\n') { ++line; ++p; }
+      else if (c == ' ' || c == '\t' || c == '\r' || c == '\f' || c == '\v') ++p;
+      else if (c == '-' && at(1) == '-') {
+        p += 2;
+        if (at() == '[' && long_bracket(nullptr)) continue;
+        while (at() && at() != '\n') ++p;
+      } else if (c == '#' && p == 0 && at(1) == '!') {
+        while (at() && at() != '\n') ++p;
+      } else break;
+    }
+  }
+
+  Token next() {
+    skip();
+    Token t;
+    t.line = line;
+    char c = at();
+    if (!c) { t.t = T_EOF; return t; }
+    if (isalpha((unsigned char)c) || c == '_') {
+      size_t s = p;
+      while (isalnum((unsigned char)at()) || at() == '_') ++p;
+      t.s = src.substr(s, p - s);
+      static const std::unordered_map<std::string, Tok> kw = {
+          {"and", T_AND}, {"break", T_BREAK}, {"do", T_DO}, {"else", T_ELSE}, {"elseif", T_ELSEIF}, {"end", T_END},
+          {"false", T_FALSE}, {"for", T_FOR}, {"function", T_FUNCTION}, {"if", T_IF}, {"in", T_IN},
+          {"local", T_LOCAL}, {"nil", T_NIL}, {"not", T_NOT}, {"or", T_OR}, {"repeat", T_REPEAT},
+          {"return", T_RETURN}, {"then", T_THEN}, {"true", T_TRUE}, {"until", T_UNTIL}, {"while", T_WHILE}};
+      auto it = kw.find(t.s);
+      t.t = it == kw.end() ? T_NAME : it->second;
+      return t;
+    }
+    if (isdigit((unsigned char)c) || (c == '.' && isdigit((unsigned char)at(1)))) {
+      size_t s = p;
+      if (c == '0' && (at(1) == 'x' || at(1) == 'X')) {
+        p += 2;
+        while (isxdigit((unsigned char)at()) || at() == '.') ++p;
+      } else {
+        while (isdigit((unsigned char)at()) || at() == '.') ++p;
+        if (at() == 'e' || at() == 'E') {
+          ++p;
+          if (at() == '+' || at() == '-') ++p;
+          while (isdigit((unsigned char)at())) ++p;
+        }
+      }
+      t.t = T_NUMBER;
+      if (!str2num(src.substr(s, p - s), &t.num)) err("malformed number near '" + src.substr(s, p - s) + "'");
+      return t;
+    }
+    if (c == '"' || c == '\'') {
+      const char q = c;
+      ++p;
+      std::string out;
+      while (at() != q) {
+        char d = at();
+        if (!d || d == '\n') err("unfinished string");
+        if (d == '\\') {
+          ++p;
+          char e = at();
+          ++p;
+          switch (e) {
+            case 'n': out += '\n'; break;
+            case 't': out += '\t'; break;
+            case 'r': out += '\r'; break;
+            case 'a': out += '\a'; break;
+            case 'b': out += '\b'; break;
+            case 'f': out += '\f'; break;
+            case 'v': out += '\v'; break;
+            case '\\': out += '\\'; break;
+            case '"': out += '"'; break;
+            case '\'': out += '\''; break;
+            case '\n': out += '\n'; ++line; break;
+            case 'x': {
+              int v = (int)strtol(src.substr(p, 2).c_str(), nullptr, 16);
+              p += 2;
+              out += (char)v;
+              break;
+            }
+            case 'z': while (isspace((unsigned char)at())) { if (at() == '\n') ++line; ++p; } break;
+            default:
+              if (isdigit((unsigned char)e)) {
+                int v = e - '0';
+                for (int k = 0; k < 2 && isdigit((unsigned char)at()); ++k) v = v * 10 + (at() - '0'), ++p;
+                out += (char)v;
+              } else {
+                err(std::string("invalid escape sequence '\\") + e + "'");
+              }
+          }
+        } else {
+          out += d;
+          ++p;
+        }
+      }
+      ++p;
+      t.t = T_STRING;
+      t.s = out;
+      return t;
+    }
+    if (c == '[' && (at(1) == '[' || at(1) == '=')) {
+      std::string s;
+      if (long_bracket(&s)) { t.t = T_STRING; t.s = s; return t; }
+    }
+    auto two = [&](char a, char b, Tok k) {
+      if (c == a && at(1) == b) { p += 2; t.t = k; return true; }
+      return false;
+    };
+    if (c == '.' && at(1) == '.' && at(2) == '.') { p += 3; t.t = T_DOTS; return t; }
+    if (two('=', '=', T_EQ) || two('~', '=', T_NE) || two('<', '=', T_LE) || two('>', '=', T_GE) ||
+        two('.', '.', T_CONCAT) || two('/', '/', T_IDIV) || two('<', '<', T_SHL) || two('>', '>', T_SHR) ||
+        two(':', ':', T_DBCOLON))
+      return t;
+    t.t = T_CHAR;
+    t.ch = c;
+    ++p;
+    return t;
+  }
+};
+
+// ------------------------------------------------------------ AST ---------
+struct Expr;
+struct Stat;
+using ExprP = std::shared_ptr<Expr>;
+using StatP = std::shared_ptr<Stat>;
+
+struct Block {
+  std::vector<StatP> stats;
+};
+
+struct FuncBody {
+  std::vector<std::string> params;
+  bool vararg = false;
+  std::shared_ptr<Block> block;
+  std::string name;
+};
+
+enum ExprKind { E_NIL, E_TRUE, E_FALSE, E_NUM, E_STR, E_VARARG, E_FUNC, E_TABLE, E_BIN, E_UN, E_NAME, E_INDEX,
+                E_CALL, E_METHOD, E_PAREN, E_AND, E_OR };
+
+struct Expr {
+  ExprKind k;
+  Value lit;
+  std::string name;
+  int op = 0;  // token / char code
+  ExprP a, b;
+  std::vector<ExprP> args;
+  std::shared_ptr<FuncBody> fn;
+  // table constructor: items (key may be null = positional)
+  std::vector<std::pair<ExprP, ExprP>> items;
+  int line = 0;
+};
+
+enum StatKind { S_LOCAL, S_ASSIGN, S_CALL, S_DO, S_WHILE, S_REPEAT, S_IF, S_NUMFOR, S_GENFOR, S_RETURN, S_BREAK,
+                S_LOCALFUNC };
+
+struct Stat {
+  StatKind k;
+  std::vector<std::string> names;
+  std::vector<ExprP> targets, exprs;
+  ExprP e;
+  std::shared_ptr<Block> body;
+  std::vector<ExprP> conds;
+  std::vector<std::shared_ptr<Block>> blocks;
+  std::shared_ptr<Block> els;
+  std::shared_ptr<FuncBody> fn;
+  int line = 0;
+};
+
+// ------------------------------------------------------------ parser ------
+struct Parser {
+  Lexer lx;
+  Token cur, ahead;
+  bool has_ahead = false;
+  Parser(const std::string& src, const std::string& chunk) : lx(src, chunk) { cur = lx.next(); }
+
+  [[noreturn]] void err(const std::string& m) {
+    throw LuaError(lx.chunk + ":" + std::to_string(cur.line) + ": " + m + " near '" + show(cur) + "'");
+  }
+  static std::string show(const Token& t) {
+    switch (t.t) {
+      case T_EOF: return "<eof>";
+      case T_NAME: case T_STRING: return t.s;
+      case T_NUMBER: return tostring(t.num);
+      case T_CHAR: return std::string(1, t.ch);
+      default: return "token";
+    }
+  }
+  void advance() {
+    if (has_ahead) { cur = ahead; has_ahead = false; }
+    else cur = lx.next();
+  }
+  const Token& peek() {
+    if (!has_ahead) { ahead = lx.next(); has_ahead = true; }
+    return ahead;
+  }
+  bool is(char c) const { return cur.t == T_CHAR && cur.ch == c; }
+  bool accept(char c) { if (is(c)) { advance(); return true; } return false; }
+  bool accept(Tok t) { if (cur.t == t) { advance(); return true; } return false; }
+  void expect(char c) { if (!accept(c)) err(std::string("'") + c + "' expected"); }
+  void expect(Tok t, const char* what) { if (!accept(t)) err(std::string("'") + what + "' expected"); }
+  std::string name() {
+    if (cur.t != T_NAME) err("<name> expected");
+    std::string s = cur.s;
+    advance();
+    return s;
+  }
+
+  bool block_end() const {
+    return cur.t == T_EOF || cur.t == T_END || cur.t == T_ELSE || cur.t == T_ELSEIF || cur.t == T_UNTIL;
+  }
+
+  std::shared_ptr<Block> block() {
+    auto b = std::make_shared<Block>();
+    while (!block_end()) {
+      if (cur.t == T_RETURN) {
+        auto s = std::make_shared<Stat>();
+        s->k = S_RETURN;
+        s->line = cur.line;
+        advance();
+        if (!block_end() && !is(';')) s->exprs = exprlist();
+        accept(';');
+        b->stats.push_back(s);
+        if (!block_end()) err("'end' expected after return");
+        break;
+      }
+      if (accept(';')) continue;
+      b->stats.push_back(statement());
+    }
+    return b;
+  }
+
+  std::shared_ptr<FuncBody> funcbody(const std::string& nm, bool method) {
+    auto f = std::make_shared<FuncBody>();
+    f->name = nm;
+    if (method) f->params.push_back("self");
+    expect('(');
+    if (!is(')')) {
+      do {
+        if (accept(T_DOTS)) { f->vararg = true; break; }
+        f->params.push_back(name());
+      } while (accept(','));
+    }
+    expect(')');
+    f->block = block();
+    expect(T_END, "end");
+    return f;
+  }
+
+  StatP statement() {
+    auto s = std::make_shared<Stat>();
+    s->line = cur.line;
+    switch (cur.t) {
+      case T_IF: {
+        advance();
+        s->k = S_IF;
+        s->conds.push_back(expr());
+        expect(T_THEN, "then");
+        s->blocks.push_back(block());
+        while (cur.t == T_ELSEIF) {
+          advance();
+          s->conds.push_back(expr());
+          expect(T_THEN, "then");
+          s->blocks.push_back(block());
+        }
+        if (accept(T_ELSE)) s->els = block();
+        expect(T_END, "end");
+        return s;
+      }
+      case T_WHILE:
+        advance();
+        s->k = S_WHILE;
+        s->e = expr();
+        expect(T_DO, "do");
+        s->body = block();
+        expect(T_END, "end");
+        return s;
+      case T_DO:
+        advance();
+        s->k = S_DO;
+        s->body = block();
+        expect(T_END, "end");
+        return s;
+      case T_REPEAT:
+        advance();
+        s->k = S_REPEAT;
+        s->body = block();
+        expect(T_UNTIL, "until");
+        s->e = expr();
+        return s;
+      case T_FOR: {
+        advance();
+        std::string n1 = name();
+        if (accept('=')) {
+          s->k = S_NUMFOR;
+          s->names.push_back(n1);
+          s->exprs.push_back(expr());
+          expect(',');
+          s->exprs.push_back(expr());
+          if (accept(',')) s->exprs.push_back(expr());
+        } else {
+          s->k = S_GENFOR;
+          s->names.push_back(n1);
+          while (accept(',')) s->names.push_back(name());
+          expect(T_IN, "in");
+          s->exprs = exprlist();
+        }
+        expect(T_DO, "do");
+        s->body = block();
+        expect(T_END, "end");
+        return s;
+      }
+      case T_FUNCTION: {
+        advance();
+        // funcname: Name {'.' Name} [':' Name]
+        auto target = std::make_shared<Expr>();
+        target->k = E_NAME;
+        target->name = name();
+        std::string full = target->name;
+        bool method = false;
+        while (is('.') || is(':')) {
+          method = is(':');
+          advance();
+          auto idx = std::make_shared<Expr>();
+          idx->k = E_INDEX;
+          idx->a = target;
+          idx->b = std::make_shared<Expr>();
+          idx->b->k = E_STR;
+          idx->b->lit = Value::string(name());
+          full += (method ? ":" : ".") + *idx->b->lit.s;
+          target = idx;
+          if (method) break;
+        }
+        s->k = S_ASSIGN;
+        s->targets.push_back(target);
+        auto fe = std::make_shared<Expr>();
+        fe->k = E_FUNC;
+        fe->fn = funcbody(full, method);
+        s->exprs.push_back(fe);
+        return s;
+      }
+      case T_LOCAL:
+        advance();
+        if (accept(T_FUNCTION)) {
+          s->k = S_LOCALFUNC;
+          s->names.push_back(name());
+          s->fn = funcbody(s->names[0], false);
+          return s;
+        }
+        s->k = S_LOCAL;
+        do {
+          s->names.push_back(name());
+          if (accept('<')) { name(); expect('>'); }  // <const>/<close> attribs: accepted, ignored
+        } while (accept(','));
+        if (accept('=')) s->exprs = exprlist();
+        return s;
+      case T_BREAK:
+        advance();
+        s->k = S_BREAK;
+        return s;
+      case T_DBCOLON:
+        err("goto/labels are not supported");
+      default: break;
+    }
+    // exprstat: call or assignment
+    ExprP e = suffixedexp();
+    if (is('=') || is(',')) {
+      s->k = S_ASSIGN;
+      s->targets.push_back(e);
+      while (accept(',')) s->targets.push_back(suffixedexp());
+      expect('=');
+      s->exprs = exprlist();
+      for (auto& t : s->targets)
+        if (t->k != E_NAME && t->k != E_INDEX) err("syntax error (cannot assign)");
+      return s;
+    }
+    if (e->k != E_CALL && e->k != E_METHOD) err("syntax error");
+    s->k = S_CALL;
+    s->e = e;
+    return s;
+  }
+
+  std::vector<ExprP> exprlist() {
+    std::vector<ExprP> v;
+    v.push_back(expr());
+    while (accept(',')) v.push_back(expr());
+    return v;
+  }
+
+  ExprP primaryexp() {
+    auto e = std::make_shared<Expr>();
+    e->line = cur.line;
+    if (cur.t == T_NAME) {
+      e->k = E_NAME;
+      e->name = cur.s;
+      advance();
+      return e;
+    }
+    if (accept('(')) {
+      e->k = E_PAREN;
+      e->a = expr();
+      expect(')');
+      return e;
+    }
+    err("unexpected symbol");
+  }
+
+  std::vector<ExprP> callargs() {
+    std::vector<ExprP> args;
+    if (cur.t == T_STRING) {
+      auto s = std::make_shared<Expr>();
+      s->k = E_STR;
+      s->lit = Value::string(cur.s);
+      advance();
+      args.push_back(s);
+    } else if (is('{')) {
+      args.push_back(tablecons());
+    } else {
+      expect('(');
+      if (!is(')')) args = exprlist();
+      expect(')');
+    }
+    return args;
+  }
+
+  ExprP suffixedexp() {
+    ExprP e = primaryexp();
+    for (;;) {
+      const int line = cur.line;
+      if (accept('.')) {
+        auto x = std::make_shared<Expr>();
+        x->k = E_INDEX;
+        x->a = e;
+        x->b = std::make_shared<Expr>();
+        x->b->k = E_STR;
+        x->b->lit = Value::string(name());
+        x->line = line;
+        e = x;
+      } else if (accept('[')) {
+        auto x = std::make_shared<Expr>();
+        x->k = E_INDEX;
+        x->a = e;
+        x->b = expr();
+        x->line = line;
+        expect(']');
+        e = x;
+      } else if (accept(':')) {
+        auto x = std::make_shared<Expr>();
+        x->k = E_METHOD;
+        x->a = e;
+        x->name = name();
+        x->args = callargs();
+        x->line = line;
+        e = x;
+      } else if (is('(') || is('{') || cur.t == T_STRING) {
+        auto x = std::make_shared<Expr>();
+        x->k = E_CALL;
+        x->a = e;
+        x->args = callargs();
+        x->line = line;
+        e = x;
+      } else {
+        return e;
+      }
+    }
+  }
+
+  ExprP tablecons() {
+    auto t = std::make_shared<Expr>();
+    t->k = E_TABLE;
+    t->line = cur.line;
+    expect('{');
+    while (!is('}')) {
+      if (accept('[')) {
+        ExprP k = expr();
+        expect(']');
+        expect('=');
+        t->items.emplace_back(k, expr());
+      } else if (cur.t == T_NAME && peek().t == T_CHAR && peek().ch == '=') {
+        auto k = std::make_shared<Expr>();
+        k->k = E_STR;
+        k->lit = Value::string(cur.s);
+        advance();
+        advance();
+        t->items.emplace_back(k, expr());
+      } else {
+        t->items.emplace_back(nullptr, expr());
+      }
+      if (!accept(',') && !accept(';')) break;
+    }
+    expect('}');
+    return t;
+  }
+
+  ExprP simpleexp() {
+    auto e = std::make_shared<Expr>();
+    e->line = cur.line;
+    switch (cur.t) {
+      case T_NUMBER: e->k = E_NUM; e->lit = cur.num; advance(); return e;
+      case T_STRING: e->k = E_STR; e->lit = Value::string(cur.s); advance(); return e;
+      case T_NIL: e->k = E_NIL; advance(); return e;
+      case T_TRUE: e->k = E_TRUE; advance(); return e;
+      case T_FALSE: e->k = E_FALSE; advance(); return e;
+      case T_DOTS: e->k = E_VARARG; advance(); return e;
+      case T_FUNCTION: advance(); e->k = E_FUNC; e->fn = funcbody("anonymous", false); return e;
+      default: break;
+    }
+    if (is('{')) return tablecons();
+    return suffixedexp();
+  }
+
+  // binary precedence (left, right) as in lparser.c
+  static bool binop(const Token& t, int* op, int* l, int* r) {
+    struct P { int op, l, r; };
+    P p{0, 0, 0};
+    if (t.t == T_CHAR) {
+      switch (t.ch) {
+        case '+': p = {'+', 10, 10}; break;
+        case '-': p = {'-', 10, 10}; break;
+        case '*': p = {'*', 11, 11}; break;
+        case '/': p = {'/', 11, 11}; break;
+        case '%': p = {'%', 11, 11}; break;
+        case '^': p = {'^', 14, 13}; break;
+        case '&': p = {'&', 6, 6}; break;
+        case '|': p = {'|', 4, 4}; break;
+        case '~': p = {'~', 5, 5}; break;
+        case '<': p = {'<', 3, 3}; break;
+        case '>': p = {'>', 3, 3}; break;
+        default: return false;
+      }
+    } else {
+      switch (t.t) {
+        case T_IDIV: p = {T_IDIV + 256, 11, 11}; break;
+        case T_CONCAT: p = {T_CONCAT + 256, 9, 8}; break;
+        case T_SHL: p = {T_SHL + 256, 7, 7}; break;
+        case T_SHR: p = {T_SHR + 256, 7, 7}; break;
+        case T_EQ: p = {T_EQ + 256, 3, 3}; break;
+        case T_NE: p = {T_NE + 256, 3, 3}; break;
+        case T_LE: p = {T_LE + 256, 3, 3}; break;
+        case T_GE: p = {T_GE + 256, 3, 3}; break;
+        case T_AND: p = {T_AND + 256, 2, 2}; break;
+        case T_OR: p = {T_OR + 256, 1, 1}; break;
+        default: return false;
+      }
+    }
+    *op = p.op;
+    *l = p.l;
+    *r = p.r;
+    return true;
+  }
+
+  ExprP expr(int limit = 0) {
+    ExprP left;
+    const int line = cur.line;
+    if (cur.t == T_NOT || is('-') || is('#') || is('~')) {
+      int op = cur.t == T_NOT ? T_NOT + 256 : cur.ch;
+      advance();
+      auto u = std::make_shared<Expr>();
+      u->k = E_UN;
+      u->op = op;
+      u->a = expr(12);
+      u->line = line;
+      left = u;
+    } else {
+      left = simpleexp();
+    }
+    int op, l, r;
+    while (binop(cur, &op, &l, &r) && l > limit) {
+      advance();
+      ExprP right = expr(r);
+      auto b = std::make_shared<Expr>();
+      b->line = line;
+      if (op == T_AND + 256) b->k = E_AND;
+      else if (op == T_OR + 256) b->k = E_OR;
+      else b->k = E_BIN;
+      b->op = op;
+      b->a = left;
+      b->b = right;
+      left = b;
+    }
+    return left;
+  }
+};
+
+// ------------------------------------------------------------ evaluator ---
+struct Scope {
+  std::unordered_map<std::string, std::shared_ptr<Value>> vars;
+  std::shared_ptr<Scope> parent;
+  Values varargs;
+  bool has_varargs = false;
+};
+
+enum Flow { F_NORMAL, F_BREAK, F_RETURN };
+
+struct Exec {
+  Interp& I;
+  Values ret;
+  explicit Exec(Interp& in) : I(in) {}
+
+  std::shared_ptr<Value> lookup(Scope* s, const std::string& n) {
+    for (; s; s = s->parent.get()) {
+      auto it = s->vars.find(n);
+      if (it != s->vars.end()) return it->second;
+    }
+    return nullptr;
+  }
+
+  [[noreturn]] void rt(const Expr* e, const std::string& m) {
+    throw LuaError(I.chunk + ":" + std::to_string(e && e->line ? e->line : I.line) + ": " + m);
+  }
+
+  Value index(const Value& o, const Value& k, const Expr* e) {
+    if (o.t == Value::Tab) return o.tab->get(k);
+    if (o.t == Value::Str) {
+      Value strlib = I.globals->get(Value::string("string"));
+      if (strlib.t == Value::Tab) return strlib.tab->get(k);
+    }
+    rt(e, std::string("attempt to index a ") + type_name(o) + " value" +
+              (e && e->a && e->a->k == E_NAME ? " (variable '" + e->a->name + "')" : ""));
+  }
+
+  Values eval_multi(const ExprP& e, Scope* s) {
+    if (e->k == E_CALL || e->k == E_METHOD) return call_expr(e.get(), s);
+    if (e->k == E_VARARG) {
+      for (Scope* x = s; x; x = x->parent.get())
+        if (x->has_varargs) return x->varargs;
+      return {};
+    }
+    return {eval(e, s)};
+  }
+
+  Values eval_list(const std::vector<ExprP>& es, Scope* s) {
+    Values out;
+    for (size_t i = 0; i < es.size(); ++i) {
+      if (i + 1 == es.size()) {
+        Values m = eval_multi(es[i], s);
+        out.insert(out.end(), m.begin(), m.end());
+      } else {
+        out.push_back(eval(es[i], s));
+      }
+    }
+    return out;
+  }
+
+  Values call_expr(const Expr* e, Scope* s) {
+    Value f;
+    Values args;
+    if (e->k == E_METHOD) {
+      Value obj = eval(e->a, s);
+      f = index(obj, Value::string(e->name), e);
+      if (f.t != Value::Fn) rt(e, "attempt to call a " + std::string(type_name(f)) + " value (method '" + e->name + "')");
+      args.push_back(obj);
+    } else {
+      f = eval(e->a, s);
+      if (f.t != Value::Fn) {
+        std::string what = e->a->k == E_NAME ? " (global '" + e->a->name + "')" : "";
+        rt(e, std::string("attempt to call a ") + type_name(f) + " value" + what);
+      }
+    }
+    Values rest = eval_list(e->args, s);
+    args.insert(args.end(), rest.begin(), rest.end());
+    return I.call(f, std::move(args));
+  }
+
+  static Value arith(int op, const Value& a0, const Value& b0, const Expr* e, Exec& ex) {
+    Value a, b;
+    if (!tonum(a0, &a) || !tonum(b0, &b))
+      ex.rt(e, std::string("attempt to perform arithmetic on a ") + type_name(tonum(a0, &a) ? b0 : a0) + " value");
+    const bool ints = a.t == Value::Int && b.t == Value::Int;
+    switch (op) {
+      case '+': return ints ? Value::integer((int64_t)((uint64_t)a.i + (uint64_t)b.i)) : Value::number(a.as_double() + b.as_double());
+      case '-': return ints ? Value::integer((int64_t)((uint64_t)a.i - (uint64_t)b.i)) : Value::number(a.as_double() - b.as_double());
+      case '*': return ints ? Value::integer((int64_t)((uint64_t)a.i * (uint64_t)b.i)) : Value::number(a.as_double() * b.as_double());
+      case '/': return Value::number(a.as_double() / b.as_double());
+      case '^': return Value::number(std::pow(a.as_double(), b.as_double()));
+      case '%':
+        if (ints) {
+          if (b.i == 0) ex.rt(e, "attempt to perform 'n%%0'");
+          int64_t m = a.i % b.i;
+          if (m != 0 && ((m ^ b.i) < 0)) m += b.i;
+          return Value::integer(m);
+        } else {
+          double x = a.as_double(), y = b.as_double(), m = std::fmod(x, y);
+          if (m != 0 && ((m < 0) != (y < 0))) m += y;
+          return Value::number(m);
+        }
+      default:  // floor division
+        if (ints) {
+          if (b.i == 0) ex.rt(e, "attempt to perform 'n//0'");
+          int64_t q = a.i / b.i;
+          if ((a.i % b.i != 0) && ((a.i < 0) != (b.i < 0))) --q;
+          return Value::integer(q);
+        }
+        return Value::number(std::floor(a.as_double() / b.as_double()));
+    }
+  }
+
+  static bool less(const Value& a, const Value& b, const Expr* e, Exec& ex, bool orequal) {
+    if (a.is_num() && b.is_num()) {
+      if (a.t == Value::Int && b.t == Value::Int) return orequal ? a.i <= b.i : a.i < b.i;
+      return orequal ? a.as_double() <= b.as_double() : a.as_double() < b.as_double();
+    }
+    if (a.t == Value::Str && b.t == Value::Str) return orequal ? *a.s <= *b.s : *a.s < *b.s;
+    ex.rt(e, std::string("attempt to compare ") + type_name(a) + " with " + type_name(b));
+  }
+
+  Value eval(const ExprP& e, Scope* s) {
+    switch (e->k) {
+      case E_NIL: return Value();
+      case E_TRUE: return Value::boolean(true);
+      case E_FALSE: return Value::boolean(false);
+      case E_NUM:
+      case E_STR: return e->lit;
+      case E_VARARG: {
+        Values v = eval_multi(e, s);
+        return v.empty() ? Value() : v[0];
+      }
+      case E_FUNC: {
+        auto f = std::make_shared<Function>();
+        f->body = e->fn;
+        f->name = e->fn->name;
+        // capture the defining scope (shared): closures see later updates of upvalues
+        f->env = scope_ptr(s);
+        return Value::function(f);
+      }
+      case E_TABLE: {
+        auto t = std::make_shared<Table>();
+        int64_t n = 1;
+        for (size_t i = 0; i < e->items.size(); ++i) {
+          auto& it = e->items[i];
+          if (it.first) {
+            t->set(eval(it.first, s), eval(it.second, s));
+          } else if (i + 1 == e->items.size()) {
+            for (auto& v : eval_multi(it.second, s)) t->set(Value::integer(n++), v);
+          } else {
+            t->set(Value::integer(n++), eval(it.second, s));
+          }
+        }
+        return Value::table(t);
+      }
+      case E_AND: {
+        Value a = eval(e->a, s);
+        return a.truthy() ? eval(e->b, s) : a;
+      }
+      case E_OR: {
+        Value a = eval(e->a, s);
+        return a.truthy() ? a : eval(e->b, s);
+      }
+      case E_UN: {
+        Value a = eval(e->a, s);
+        switch (e->op) {
+          case T_NOT + 256: return Value::boolean(!a.truthy());
+          case '-': {
+            Value n;
+            if (!tonum(a, &n)) rt(e.get(), std::string("attempt to perform arithmetic on a ") + type_name(a) + " value");
+            return n.t == Value::Int ? Value::integer((int64_t)(0 - (uint64_t)n.i)) : Value::number(-n.n);
+          }
+          case '#':
+            if (a.t == Value::Str) return Value::integer((int64_t)a.s->size());
+            if (a.t == Value::Tab) return Value::integer(a.tab->length());
+            rt(e.get(), std::string("attempt to get length of a ") + type_name(a) + " value");
+          case '~': return Value::integer(~toint_strict(a, "bitwise not"));
+        }
+        rt(e.get(), "bad unary operator");
+      }
+      case E_BIN: {
+        Value a = eval(e->a, s), b = eval(e->b, s);
+        const int op = e->op;
+        switch (op) {
+          case '+': case '-': case '*': case '/': case '%': case '^': case T_IDIV + 256:
+            return arith(op == T_IDIV + 256 ? 'i' : op, a, b, e.get(), *this);
+          case T_CONCAT + 256: {
+            auto str = [&](const Value& v) -> std::string {
+              if (v.t == Value::Str) return *v.s;
+              if (v.is_num()) return tostring(v);
+              rt(e.get(), std::string("attempt to concatenate a ") + type_name(v) + " value");
+            };
+            return Value::string(str(a) + str(b));
+          }
+          case T_EQ + 256: return Value::boolean(raw_equal(a, b));
+          case T_NE + 256: return Value::boolean(!raw_equal(a, b));
+          case '<': return Value::boolean(less(a, b, e.get(), *this, false));
+          case T_LE + 256: return Value::boolean(less(a, b, e.get(), *this, true));
+          case '>': return Value::boolean(less(b, a, e.get(), *this, false));
+          case T_GE + 256: return Value::boolean(less(b, a, e.get(), *this, true));
+          case '&': return Value::integer(toint_strict(a, "bitwise and") & toint_strict(b, "bitwise and"));
+          case '|': return Value::integer(toint_strict(a, "bitwise or") | toint_strict(b, "bitwise or"));
+          case '~': return Value::integer(toint_strict(a, "bitwise xor") ^ toint_strict(b, "bitwise xor"));
+          case T_SHL + 256: {
+            int64_t x = toint_strict(a, "shift"), n = toint_strict(b, "shift");
+            if (n <= -64 || n >= 64) return Value::integer(0);
+            return Value::integer(n >= 0 ? (int64_t)((uint64_t)x << n) : (int64_t)((uint64_t)x >> -n));
+          }
+          case T_SHR + 256: {
+            int64_t x = toint_strict(a, "shift"), n = toint_strict(b, "shift");
+            if (n <= -64 || n >= 64) return Value::integer(0);
+            return Value::integer(n >= 0 ? (int64_t)((uint64_t)x >> n) : (int64_t)((uint64_t)x << -n));
+          }
+        }
+        rt(e.get(), "bad binary operator");
+      }
+      case E_NAME: {
+        if (auto c = lookup(s, e->name)) return *c;
+        return I.globals->get(Value::string(e->name));
+      }
+      case E_INDEX: return index(eval(e->a, s), eval(e->b, s), e.get());
+      case E_CALL:
+      case E_METHOD: {
+        Values v = call_expr(e.get(), s);
+        return v.empty() ? Value() : v[0];
+      }
+      case E_PAREN: return eval(e->a, s);
+    }
+    return Value();
+  }
+
+  // scopes are held by shared_ptr so closures can keep them alive
+  std::vector<std::shared_ptr<Scope>> live;
+  std::shared_ptr<Scope> scope_ptr(Scope* s) {
+    for (auto it = live.rbegin(); it != live.rend(); ++it)
+      if (it->get() == s) return *it;
+    return nullptr;
+  }
+  std::shared_ptr<Scope> push(const std::shared_ptr<Scope>& parent) {
+    auto sc = std::make_shared<Scope>();
+    sc->parent = parent;
+    live.push_back(sc);
+    return sc;
+  }
+  void pop() { live.pop_back(); }
+
+  void assign(const ExprP& t, const Value& v, Scope* s) {
+    if (t->k == E_NAME) {
+      if (auto c = lookup(s, t->name)) *c = v;
+      else I.globals->set(Value::string(t->name), v);
+    } else {
+      Value o = eval(t->a, s);
+      if (o.t != Value::Tab) rt(t.get(), std::string("attempt to index a ") + type_name(o) + " value");
+      o.tab->set(eval(t->b, s), v);
+    }
+  }
+
+  Flow exec_block(const std::shared_ptr<Block>& b, const std::shared_ptr<Scope>& parent) {
+    auto sc = push(parent);
+    Flow f = F_NORMAL;
+    try {
+      for (auto& st : b->stats) {
+        f = exec(st, sc);
+        if (f != F_NORMAL) break;
+      }
+    } catch (...) {
+      pop();
+      throw;
+    }
+    pop();
+    return f;
+  }
+
+  Flow exec(const StatP& st, const std::shared_ptr<Scope>& sc) {
+    Scope* s = sc.get();
+    I.line = st->line;
+    switch (st->k) {
+      case S_LOCAL: {
+        Values v = eval_list(st->exprs, s);
+        for (size_t i = 0; i < st->names.size(); ++i)
+          s->vars[st->names[i]] = std::make_shared<Value>(i < v.size() ? v[i] : Value());
+        return F_NORMAL;
+      }
+      case S_LOCALFUNC: {
+        auto cell = std::make_shared<Value>();
+        s->vars[st->names[0]] = cell;
+        auto f = std::make_shared<Function>();
+        f->body = st->fn;
+        f->name = st->names[0];
+        f->env = sc;
+        *cell = Value::function(f);
+        return F_NORMAL;
+      }
+      case S_ASSIGN: {
+        Values v = eval_list(st->exprs, s);
+        for (size_t i = 0; i < st->targets.size(); ++i) assign(st->targets[i], i < v.size() ? v[i] : Value(), s);
+        return F_NORMAL;
+      }
+      case S_CALL: call_expr(st->e.get(), s); return F_NORMAL;
+      case S_DO: return exec_block(st->body, sc);
+      case S_WHILE:
+        while (eval(st->e, s).truthy()) {
+          Flow f = exec_block(st->body, sc);
+          if (f == F_BREAK) break;
+          if (f == F_RETURN) return f;
+        }
+        return F_NORMAL;
+      case S_REPEAT:
+        for (;;) {
+          // the until-condition sees the body's locals
+          auto inner = push(sc);
+          Flow f = F_NORMAL;
+          bool done = false;
+          try {
+            for (auto& x : st->body->stats) {
+              f = exec(x, inner);
+              if (f != F_NORMAL) break;
+            }
+            if (f == F_NORMAL) done = eval(st->e, inner.get()).truthy();
+          } catch (...) {
+            pop();
+            throw;
+          }
+          pop();
+          if (f == F_BREAK) break;
+          if (f == F_RETURN) return f;
+          if (done) break;
+        }
+        return F_NORMAL;
+      case S_IF:
+        for (size_t i = 0; i < st->conds.size(); ++i)
+          if (eval(st->conds[i], s).truthy()) return exec_block(st->blocks[i], sc);
+        if (st->els) return exec_block(st->els, sc);
+        return F_NORMAL;
+      case S_NUMFOR: {
+        Value a = eval(st->exprs[0], s), b = eval(st->exprs[1], s);
+        Value c = st->exprs.size() > 2 ? eval(st->exprs[2], s) : Value::integer(1);
+        Value x, y, z;
+        if (!tonum(a, &x) || !tonum(b, &y) || !tonum(c, &z)) rt(st->exprs[0].get(), "'for' values must be numbers");
+        if (x.t == Value::Int && y.t == Value::Int && z.t == Value::Int) {
+          if (z.i == 0) rt(st->exprs[0].get(), "'for' step is zero");
+          for (int64_t i = x.i; z.i > 0 ? i <= y.i : i >= y.i; i += z.i) {
+            auto body = push(sc);
+            body->vars[st->names[0]] = std::make_shared<Value>(Value::integer(i));
+            pop();
+            Flow f = exec_block(st->body, body);
+            if (f == F_BREAK) break;
+            if (f == F_RETURN) return f;
+            if ((z.i > 0 && i > INT64_MAX - z.i) || (z.i < 0 && i < INT64_MIN - z.i)) break;
+          }
+        } else {
+          double i0 = x.as_double(), lim = y.as_double(), stp = z.as_double();
+          if (stp == 0) rt(st->exprs[0].get(), "'for' step is zero");
+          for (double i = i0; stp > 0 ? i <= lim : i >= lim; i += stp) {
+            auto body = push(sc);
+            body->vars[st->names[0]] = std::make_shared<Value>(Value::number(i));
+            pop();
+            Flow f = exec_block(st->body, body);
+            if (f == F_BREAK) break;
+            if (f == F_RETURN) return f;
+          }
+        }
+        return F_NORMAL;
+      }
+      case S_GENFOR: {
+        Values it = eval_list(st->exprs, s);
+        Value f = it.size() > 0 ? it[0] : Value(), state = it.size() > 1 ? it[1] : Value(),
+              ctl = it.size() > 2 ? it[2] : Value();
+        if (f.t != Value::Fn) rt(st->exprs[0].get(), std::string("attempt to call a ") + type_name(f) + " value");
+        for (;;) {
+          Values r = I.call(f, {state, ctl});
+          if (r.empty() || r[0].t == Value::Nil) break;
+          ctl = r[0];
+          auto body = push(sc);
+          for (size_t i = 0; i < st->names.size(); ++i)
+            body->vars[st->names[i]] = std::make_shared<Value>(i < r.size() ? r[i] : Value());
+          pop();
+          Flow fl = exec_block(st->body, body);
+          if (fl == F_BREAK) break;
+          if (fl == F_RETURN) return fl;
+        }
+        return F_NORMAL;
+      }
+      case S_RETURN:
+        ret = eval_list(st->exprs, s);
+        return F_RETURN;
+      case S_BREAK: return F_BREAK;
+    }
+    return F_NORMAL;
+  }
+};
+
+Values Interp::call(const Value& f, Values args) {
+  if (f.t != Value::Fn) throw LuaError(std::string("attempt to call a ") + type_name(f) + " value");
+  if (++depth > 200) { --depth; throw LuaError("stack overflow"); }
+  struct Guard { int& d; ~Guard() { --d; } } g{depth};
+  if (f.fn->native) return f.fn->native(*this, args);
+  const FuncBody& body = *f.fn->body;
+  Exec ex(*this);
+  auto sc = ex.push(f.fn->env);
+  for (size_t i = 0; i < body.params.size(); ++i)
+    sc->vars[body.params[i]] = std::make_shared<Value>(i < args.size() ? args[i] : Value());
+  if (body.vararg) {
+    sc->has_varargs = true;
+    if (args.size() > body.params.size()) sc->varargs.assign(args.begin() + (long)body.params.size(), args.end());
+  }
+  Flow fl = ex.exec_block(body.block, sc);
+  ex.pop();
+  return fl == F_RETURN ? ex.ret : Values{};
+}
+
+// ------------------------------------------------------------ stdlib ------
+static Value arg_at(Values& a, size_t i) { return i < a.size() ? a[i] : Value(); }
+
+static std::string check_str(Values& a, size_t i, const char* fn) {
+  Value v = arg_at(a, i);
+  if (v.t == Value::Str) return *v.s;
+  if (v.is_num()) return tostring(v);
+  throw LuaError(std::string("bad argument #") + std::to_string(i + 1) + " to '" + fn + "' (string expected, got " +
+                 type_name(v) + ")");
+}
+
+static int64_t check_int(Values& a, size_t i, const char* fn) { return toint_strict(arg_at(a, i), fn); }
+
+static double check_num(Values& a, size_t i, const char* fn) {
+  Value n;
+  if (!tonum(arg_at(a, i), &n))
+    throw LuaError(std::string("bad argument #") + std::to_string(i + 1) + " to '" + fn + "' (number expected)");
+  return n.as_double();
+}
+
+static std::string lua_format(Values& a) {
+  const std::string fmt = check_str(a, 0, "format");
+  std::string out;
+  size_t ai = 1;
+  for (size_t i = 0; i < fmt.size(); ++i) {
+    if (fmt[i] != '%') { out += fmt[i]; continue; }
+    if (++i >= fmt.size()) throw LuaError("invalid conversion '%' to 'format'");
+    if (fmt[i] == '%') { out += '%'; continue; }
+    std::string spec = "%";
+    while (i < fmt.size() && strchr("-+ #0123456789.", fmt[i])) spec += fmt[i++];
+    if (i >= fmt.size()) throw LuaError("invalid conversion to 'format'");
+    const char c = fmt[i];
+    char buf[512];
+    switch (c) {
+      case 'd': case 'i': {
+        spec += "lld";
+        snprintf(buf, sizeof buf, spec.c_str(), (long long)check_int(a, ai++, "format"));
+        out += buf;
+        break;
+      }
+      case 'u': case 'x': case 'X': case 'o': case 'c': {
+        if (c == 'c') { out += (char)check_int(a, ai++, "format"); break; }
+        spec += "ll";
+        spec += c;
+        snprintf(buf, sizeof buf, spec.c_str(), (unsigned long long)check_int(a, ai++, "format"));
+        out += buf;
+        break;
+      }
+      case 'f': case 'F': case 'e': case 'E': case 'g': case 'G': case 'a': case 'A': {
+        spec += c;
+        snprintf(buf, sizeof buf, spec.c_str(), check_num(a, ai++, "format"));
+        out += buf;
+        break;
+      }
+      case 's': {
+        Value v = arg_at(a, ai++);
+        std::string sv = tostring(v);
+        spec += 's';
+        if (spec == "%s") out += sv;
+        else { snprintf(buf, sizeof buf, spec.c_str(), sv.c_str()); out += buf; }
+        break;
+      }
+      case 'q': {
+        Value v = arg_at(a, ai++);
+        if (v.t != Value::Str) { out += tostring(v); break; }
+        out += '"';
+        for (char ch : *v.s) {
+          if (ch == '"' || ch == '\\') { out += '\\'; out += ch; }
+          else if (ch == '\n') out += "\\n";
+          else if ((unsigned char)ch < 32) { snprintf(buf, sizeof buf, "\\%d", (unsigned char)ch); out += buf; }
+          else out += ch;
+        }
+        out += '"';
+        break;
+      }
+      default: throw LuaError(std::string("invalid conversion '%") + c + "' to 'format'");
+    }
+  }
+  return out;
+}
+
+static void reg(const std::shared_ptr<Table>& t, const char* name, Native f) {
+  t->set(Value::string(name), make_native(name, std::move(f)));
+}
+
+Interp::Interp() {
+  globals = std::make_shared<Table>();
+  root = std::make_shared<Scope>();
+  out = [](const std::string& s) { fwrite(s.data(), 1, s.size(), stdout); };
+  auto G = globals;
+  G->set(Value::string("_G"), Value::table(G));
+  G->set(Value::string("_VERSION"), Value::string("Lua 5.4 (splinterctl minilua)"));
+  reg(G, "print", [](Interp& I, Values& a) {
+    std::string line;
+    for (size_t i = 0; i < a.size(); ++i) line += (i ? "\t" : "") + tostring(a[i]);
+    line += '\n';
+    I.out(line);
+    return Values{};
+  });
+  reg(G, "type", [](Interp&, Values& a) {
+    if (a.empty()) throw LuaError("bad argument #1 to 'type' (value expected)");
+    return Values{Value::string(type_name(a[0]))};
+  });
+  reg(G, "tostring", [](Interp&, Values& a) { return Values{Value::string(tostring(arg_at(a, 0)))}; });
+  reg(G, "tonumber", [](Interp&, Values& a) {
+    Value v = arg_at(a, 0), n;
+    if (a.size() > 1 && arg_at(a, 1).t != Value::Nil) {
+      const int64_t base = check_int(a, 1, "tonumber");
+      char* end = nullptr;
+      std::string s = check_str(a, 0, "tonumber");
+      long long r = strtoll(s.c_str(), &end, (int)base);
+      return Values{*end == 0 && !s.empty() ? Value::integer(r) : Value()};
+    }
+    return Values{tonum(v, &n) ? n : Value()};
+  });
+  reg(G, "rawequal", [](Interp&, Values& a) { return Values{Value::boolean(raw_equal(arg_at(a, 0), arg_at(a, 1)))}; });
+  reg(G, "rawget", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'rawget' (table expected)");
+    return Values{t.tab->get(arg_at(a, 1))};
+  });
+  reg(G, "rawset", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'rawset' (table expected)");
+    t.tab->set(arg_at(a, 1), arg_at(a, 2));
+    return Values{t};
+  });
+  reg(G, "rawlen", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t == Value::Tab) return Values{Value::integer(t.tab->length())};
+    if (t.t == Value::Str) return Values{Value::integer((int64_t)t.s->size())};
+    throw LuaError("table or string expected");
+  });
+  auto next = make_native("next", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0), k = arg_at(a, 1);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'next' (table expected)");
+    auto& T = *t.tab;
+    size_t i = 0;
+    if (k.t != Value::Nil) {
+      auto it = T.index.find(norm_key(k));
+      if (it == T.index.end()) throw LuaError("invalid key to 'next'");
+      i = it->second + 1;
+    }
+    for (; i < T.entries.size(); ++i)
+      if (T.entries[i].second.t != Value::Nil) return Values{T.entries[i].first, T.entries[i].second};
+    return Values{Value()};
+  });
+  G->set(Value::string("next"), next);
+  reg(G, "pairs", [next](Interp&, Values& a) {
+    if (arg_at(a, 0).t != Value::Tab) throw LuaError("bad argument #1 to 'pairs' (table expected)");
+    return Values{next, a[0], Value()};
+  });
+  auto ipairs_iter = make_native("ipairs_iter", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    const int64_t i = arg_at(a, 1).i + 1;
+    Value v = t.tab->get(Value::integer(i));
+    if (v.t == Value::Nil) return Values{Value()};
+    return Values{Value::integer(i), v};
+  });
+  reg(G, "ipairs", [ipairs_iter](Interp&, Values& a) {
+    if (arg_at(a, 0).t != Value::Tab) throw LuaError("bad argument #1 to 'ipairs' (table expected)");
+    return Values{ipairs_iter, a[0], Value::integer(0)};
+  });
+  reg(G, "select", [](Interp&, Values& a) {
+    Value n = arg_at(a, 0);
+    if (n.t == Value::Str && *n.s == "#") return Values{Value::integer((int64_t)a.size() - 1)};
+    int64_t i = check_int(a, 0, "select");
+    if (i < 0) i = (int64_t)a.size() + i;
+    if (i < 1) throw LuaError("bad argument #1 to 'select' (index out of range)");
+    if ((size_t)i >= a.size()) return Values{};
+    return Values(a.begin() + i, a.end());
+  });
+  reg(G, "error", [](Interp& I, Values& a) -> Values {
+    Value v = arg_at(a, 0);
+    const int64_t level = a.size() > 1 ? toint_strict(a[1], "error") : 1;
+    if (v.t == Value::Str && level > 0) v = Value::string(I.chunk + ":" + std::to_string(I.line) + ": " + *v.s);
+    throw LuaError(v, v.t == Value::Str ? *v.s : tostring(v));
+  });
+  reg(G, "assert", [](Interp&, Values& a) -> Values {
+    if (!arg_at(a, 0).truthy()) {
+      Value m = a.size() > 1 ? a[1] : Value::string("assertion failed!");
+      throw LuaError(m, tostring(m));
+    }
+    return a;
+  });
+  reg(G, "pcall", [](Interp& I, Values& a) {
+    if (a.empty()) throw LuaError("bad argument #1 to 'pcall' (value expected)");
+    Value f = a[0];
+    Values rest(a.begin() + 1, a.end());
+    const int d = I.depth;
+    try {
+      Values r = I.call(f, rest);
+      r.insert(r.begin(), Value::boolean(true));
+      return r;
+    } catch (LuaError& e) {
+      I.depth = d;
+      return Values{Value::boolean(false), e.value};
+    }
+  });
+  auto unpack = make_native("unpack", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'unpack' (table expected)");
+    int64_t i = a.size() > 1 && a[1].t != Value::Nil ? check_int(a, 1, "unpack") : 1;
+    int64_t j = a.size() > 2 && a[2].t != Value::Nil ? check_int(a, 2, "unpack") : t.tab->length();
+    Values r;
+    for (; i <= j; ++i) r.push_back(t.tab->get(Value::integer(i)));
+    return r;
+  });
+  G->set(Value::string("unpack"), unpack);
+  reg(G, "require", [](Interp& I, Values& a) {
+    const std::string n = check_str(a, 0, "require");
+    auto it = I.modules.find(n);
+    if (it == I.modules.end()) throw LuaError("module '" + n + "' not found");
+    return Values{it->second};
+  });
+
+  // string
+  auto S = std::make_shared<Table>();
+  G->set(Value::string("string"), Value::table(S));
+  reg(S, "format", [](Interp&, Values& a) { return Values{Value::string(lua_format(a))}; });
+  reg(S, "len", [](Interp&, Values& a) { return Values{Value::integer((int64_t)check_str(a, 0, "len").size())}; });
+  reg(S, "upper", [](Interp&, Values& a) {
+    std::string s = check_str(a, 0, "upper");
+    for (auto& c : s) c = (char)toupper((unsigned char)c);
+    return Values{Value::string(s)};
+  });
+  reg(S, "lower", [](Interp&, Values& a) {
+    std::string s = check_str(a, 0, "lower");
+    for (auto& c : s) c = (char)tolower((unsigned char)c);
+    return Values{Value::string(s)};
+  });
+  reg(S, "reverse", [](Interp&, Values& a) {
+    std::string s = check_str(a, 0, "reverse");
+    std::reverse(s.begin(), s.end());
+    return Values{Value::string(s)};
+  });
+  reg(S, "rep", [](Interp&, Values& a) {
+    std::string s = check_str(a, 0, "rep"), sep = a.size() > 2 ? check_str(a, 2, "rep") : "";
+    int64_t n = check_int(a, 1, "rep");
+    std::string out;
+    for (int64_t i = 0; i < n; ++i) { if (i) out += sep; out += s; }
+    return Values{Value::string(out)};
+  });
+  auto sub_idx = [](int64_t i, int64_t len) -> int64_t {
+    if (i < 0) i = len + i + 1;
+    return i;
+  };
+  reg(S, "sub", [sub_idx](Interp&, Values& a) {
+    std::string s = check_str(a, 0, "sub");
+    const int64_t len = (int64_t)s.size();
+    int64_t i = a.size() > 1 ? sub_idx(check_int(a, 1, "sub"), len) : 1;
+    int64_t j = a.size() > 2 && a[2].t != Value::Nil ? sub_idx(check_int(a, 2, "sub"), len) : len;
+    if (i < 1) i = 1;
+    if (j > len) j = len;
+    if (i > j) return Values{Value::string("")};
+    return Values{Value::string(s.substr((size_t)(i - 1), (size_t)(j - i + 1)))};
+  });
+  reg(S, "byte", [sub_idx](Interp&, Values& a) {
+    std::string s = check_str(a, 0, "byte");
+    const int64_t len = (int64_t)s.size();
+    int64_t i = a.size() > 1 ? sub_idx(check_int(a, 1, "byte"), len) : 1;
+    int64_t j = a.size() > 2 ? sub_idx(check_int(a, 2, "byte"), len) : i;
+    Values r;
+    for (int64_t k = std::max<int64_t>(i, 1); k <= std::min(j, len); ++k)
+      r.push_back(Value::integer((unsigned char)s[(size_t)k - 1]));
+    return r;
+  });
+  reg(S, "char", [](Interp&, Values& a) {
+    std::string s;
+    for (size_t i = 0; i < a.size(); ++i) s += (char)check_int(a, i, "char");
+    return Values{Value::string(s)};
+  });
+  reg(S, "find", [](Interp&, Values& a) {  // plain find only
+    std::string s = check_str(a, 0, "find"), p = check_str(a, 1, "find");
+    int64_t init = a.size() > 2 ? check_int(a, 2, "find") : 1;
+    if (init < 0) init = (int64_t)s.size() + init + 1;
+    if (init < 1) init = 1;
+    size_t pos = s.find(p, (size_t)init - 1);
+    if (pos == std::string::npos) return Values{Value()};
+    return Values{Value::integer((int64_t)pos + 1), Value::integer((int64_t)(pos + p.size()))};
+  });
+
+  // table
+  auto T = std::make_shared<Table>();
+  G->set(Value::string("table"), Value::table(T));
+  T->set(Value::string("unpack"), unpack);
+  reg(T, "insert", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'insert' (table expected)");
+    const int64_t n = t.tab->length();
+    if (a.size() == 2) {
+      t.tab->set(Value::integer(n + 1), a[1]);
+    } else if (a.size() == 3) {
+      int64_t pos = check_int(a, 1, "insert");
+      if (pos < 1 || pos > n + 1) throw LuaError("bad argument #2 to 'insert' (position out of bounds)");
+      for (int64_t i = n; i >= pos; --i) t.tab->set(Value::integer(i + 1), t.tab->get(Value::integer(i)));
+      t.tab->set(Value::integer(pos), a[2]);
+    } else {
+      throw LuaError("wrong number of arguments to 'insert'");
+    }
+    return Values{};
+  });
+  reg(T, "remove", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'remove' (table expected)");
+    const int64_t n = t.tab->length();
+    int64_t pos = a.size() > 1 ? check_int(a, 1, "remove") : n;
+    if (n == 0) return Values{Value()};
+    Value v = t.tab->get(Value::integer(pos));
+    for (int64_t i = pos; i < n; ++i) t.tab->set(Value::integer(i), t.tab->get(Value::integer(i + 1)));
+    t.tab->set(Value::integer(n), Value());
+    return Values{v};
+  });
+  reg(T, "concat", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'concat' (table expected)");
+    std::string sep = a.size() > 1 && a[1].t != Value::Nil ? check_str(a, 1, "concat") : "";
+    int64_t i = a.size() > 2 ? check_int(a, 2, "concat") : 1, j = a.size() > 3 ? check_int(a, 3, "concat") : t.tab->length();
+    std::string out;
+    for (int64_t k = i; k <= j; ++k) {
+      Value v = t.tab->get(Value::integer(k));
+      if (v.t != Value::Str && !v.is_num()) throw LuaError("invalid value (at index " + std::to_string(k) + ") in table for 'concat'");
+      if (k > i) out += sep;
+      out += tostring(v);
+    }
+    return Values{Value::string(out)};
+  });
+
+  // math
+  auto M = std::make_shared<Table>();
+  G->set(Value::string("math"), Value::table(M));
+  M->set(Value::string("pi"), Value::number(M_PI));
+  M->set(Value::string("huge"), Value::number(HUGE_VAL));
+  M->set(Value::string("maxinteger"), Value::integer(INT64_MAX));
+  M->set(Value::string("mininteger"), Value::integer(INT64_MIN));
+  auto int_or_float = [](double d) {
+    int64_t i;
+    return float_is_int(d, &i) ? Value::integer(i) : Value::number(d);
+  };
+  reg(M, "floor", [int_or_float](Interp&, Values& a) {
+    Value v = arg_at(a, 0);
+    if (v.t == Value::Int) return Values{v};
+    return Values{int_or_float(std::floor(check_num(a, 0, "floor")))};
+  });
+  reg(M, "ceil", [int_or_float](Interp&, Values& a) {
+    Value v = arg_at(a, 0);
+    if (v.t == Value::Int) return Values{v};
+    return Values{int_or_float(std::ceil(check_num(a, 0, "ceil")))};
+  });
+  reg(M, "abs", [](Interp&, Values& a) {
+    Value v = arg_at(a, 0);
+    if (v.t == Value::Int) return Values{Value::integer(v.i < 0 ? -v.i : v.i)};
+    return Values{Value::number(std::fabs(check_num(a, 0, "abs")))};
+  });
+  reg(M, "sqrt", [](Interp&, Values& a) { return Values{Value::number(std::sqrt(check_num(a, 0, "sqrt")))}; });
+  reg(M, "fmod", [](Interp&, Values& a) { return Values{Value::number(std::fmod(check_num(a, 0, "fmod"), check_num(a, 1, "fmod")))}; });
+  reg(M, "tointeger", [](Interp&, Values& a) {
+    Value v = arg_at(a, 0);
+    int64_t i;
+    if (v.t == Value::Int) return Values{v};
+    if (v.t == Value::Num && float_is_int(v.n, &i)) return Values{Value::integer(i)};
+    return Values{Value()};
+  });
+  auto minmax = [](bool mx) {
+    return [mx](Interp&, Values& a) {
+      if (a.empty()) throw LuaError("bad argument #1 to 'max' (number expected)");
+      Value best = a[0];
+      for (size_t i = 1; i < a.size(); ++i) {
+        const bool gt = a[i].as_double() > best.as_double();
+        if (mx ? gt : a[i].as_double() < best.as_double()) best = a[i];
+      }
+      return Values{best};
+    };
+  };
+  reg(M, "max", minmax(true));
+  reg(M, "min", minmax(false));
+  auto rng = std::make_shared<std::mt19937_64>(0x5eed);
+  reg(M, "randomseed", [rng](Interp&, Values& a) {
+    rng->seed(a.empty() ? 0x5eed : (uint64_t)check_int(a, 0, "randomseed"));
+    return Values{};
+  });
+  reg(M, "random", [rng](Interp&, Values& a) {
+    if (a.empty()) return Values{Value::number(std::uniform_real_distribution<double>(0.0, 1.0)(*rng))};
+    int64_t lo = 1, hi = check_int(a, 0, "random");
+    if (a.size() > 1) { lo = hi; hi = check_int(a, 1, "random"); }
+    if (lo > hi) throw LuaError("bad argument to 'random' (interval is empty)");
+    return Values{Value::integer(std::uniform_int_distribution<int64_t>(lo, hi)(*rng))};
+  });
+
+  // os
+  auto O = std::make_shared<Table>();
+  G->set(Value::string("os"), Value::table(O));
+  reg(O, "time", [](Interp&, Values&) { return Values{Value::integer((int64_t)time(nullptr))}; });
+  reg(O, "clock", [](Interp&, Values&) { return Values{Value::number((double)clock() / CLOCKS_PER_SEC)}; });
+  reg(O, "getenv", [](Interp&, Values& a) {
+    const char* v = getenv(check_str(a, 0, "getenv").c_str());
+    return Values{v ? Value::string(v) : Value()};
+  });
+  for (const char* lib : {"string", "table", "math", "os"}) modules[lib] = G->get(Value::string(lib));
+}
+
+Interp::~Interp() {}
+
+void Interp::set_global(const std::string& name, Value v) { globals->set(Value::string(name), std::move(v)); }
+Value Interp::global(const std::string& name) const { return globals->get(Value::string(name)); }
+
+Values Interp::run(const std::string& src, const std::string& chunkname, const std::vector<std::string>& args) {
+  chunk = chunkname;
+  Parser P(src, chunkname);
+  auto body = std::make_shared<FuncBody>();
+  body->block = P.block();
+  if (P.cur.t != T_EOF) P.err("'<eof>' expected");
+  body->vararg = true;
+  body->name = "main chunk";
+  auto argt = std::make_shared<Table>();
+  argt->set(Value::integer(0), Value::string(chunkname));
+  Values va;
+  for (size_t i = 0; i < args.size(); ++i) {
+    argt->set(Value::integer((int64_t)i + 1), Value::string(args[i]));
+    va.push_back(Value::string(args[i]));
+  }
+  set_global("arg", Value::table(argt));
+  auto f = std::make_shared<Function>();
+  f->body = body;
+  f->env = root;
+  f->name = chunkname;
+  return call(Value::function(f), va);
+}
+
+}  // namespace mlua

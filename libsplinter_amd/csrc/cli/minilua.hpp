@@ -1,0 +1,109 @@
+// minilua — a small Lua 5.4-subset interpreter for splinterctl's `lua` verb.
+//
+// The reference embeds liblua5.4 and exports a `splinter` module
+// (/root/reference/splinter_cli_cmd_lua.c:365-420); Lua is not installed in
+// this image, so the verb runs on this self-contained tree-walking
+// interpreter instead.  Supported: nil/boolean/integer/float/string/table/
+// function values, closures with upvalues, varargs, multiple returns, local /
+// global assignment, if/while/repeat/numeric-for/generic-for/break/return,
+// method calls, string methods, integer/float arithmetic with Lua's floor
+// division and modulo, bitwise ops, concatenation, and the library subset
+// scripts use: print type tostring tonumber pairs ipairs next select error
+// assert pcall rawget rawset rawlen unpack require, string.{format len sub
+// upper lower rep byte char find reverse}, table.{insert remove concat unpack},
+// math.{floor ceil abs max min sqrt huge pi maxinteger mininteger random
+// tointeger fmod}, os.{time clock getenv}.  Not supported: metatables,
+// coroutines, goto, integer-for with float steps beyond doubles, patterns in
+// string.find (plain search only) -- documented in docs/DIVERGENCES.md.
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+namespace mlua {
+
+struct Table;
+struct Function;
+struct Interp;
+
+struct Value {
+  enum Type : uint8_t { Nil, Bool, Int, Num, Str, Tab, Fn } t = Nil;
+  bool b = false;
+  int64_t i = 0;
+  double n = 0;
+  std::shared_ptr<std::string> s;
+  std::shared_ptr<Table> tab;
+  std::shared_ptr<Function> fn;
+
+  static Value nil() { return Value(); }
+  static Value boolean(bool v) { Value x; x.t = Bool; x.b = v; return x; }
+  static Value integer(int64_t v) { Value x; x.t = Int; x.i = v; return x; }
+  static Value number(double v) { Value x; x.t = Num; x.n = v; return x; }
+  static Value string(std::string v) { Value x; x.t = Str; x.s = std::make_shared<std::string>(std::move(v)); return x; }
+  static Value table(std::shared_ptr<Table> v) { Value x; x.t = Tab; x.tab = std::move(v); return x; }
+  static Value function(std::shared_ptr<Function> v) { Value x; x.t = Fn; x.fn = std::move(v); return x; }
+  bool truthy() const { return !(t == Nil || (t == Bool && !b)); }
+  bool is_num() const { return t == Int || t == Num; }
+  double as_double() const { return t == Int ? (double)i : n; }
+};
+
+struct ValueHash {
+  size_t operator()(const Value& v) const;
+};
+struct ValueEq {
+  bool operator()(const Value& a, const Value& b) const;
+};
+
+struct Table {
+  std::vector<std::pair<Value, Value>> entries;  // insertion order (pairs / next)
+  std::unordered_map<Value, size_t, ValueHash, ValueEq> index;
+  Value get(const Value& k) const;
+  void set(const Value& k, const Value& v);
+  int64_t length() const;
+};
+
+using Values = std::vector<Value>;
+using Native = std::function<Values(Interp&, Values&)>;
+
+struct LuaError : std::runtime_error {
+  Value value;
+  explicit LuaError(const std::string& m) : std::runtime_error(m), value(Value::string(m)) {}
+  explicit LuaError(Value v, const std::string& m) : std::runtime_error(m), value(std::move(v)) {}
+};
+
+struct Block;
+struct FuncBody;
+struct Scope;
+
+struct Function {
+  Native native;
+  std::shared_ptr<FuncBody> body;  // Lua closure when set
+  std::shared_ptr<Scope> env;
+  std::string name;
+};
+
+struct Interp {
+  Interp();
+  ~Interp();
+  // Run a chunk of source; `args` become `...` and arg[1..n] (arg[0] = chunkname).
+  Values run(const std::string& src, const std::string& chunkname, const std::vector<std::string>& args);
+  void set_global(const std::string& name, Value v);
+  Value global(const std::string& name) const;
+  Values call(const Value& f, Values args);
+  std::function<void(const std::string&)> out;  // print sink (default stdout)
+  std::shared_ptr<Table> globals;
+  std::unordered_map<std::string, Value> modules;  // require() registry
+  std::shared_ptr<Scope> root;
+  int depth = 0;
+  int line = 0;         // line of the statement being executed (error positions)
+  std::string chunk;
+};
+
+std::string tostring(const Value& v);
+Value make_native(const std::string& name, Native f);
+
+}  // namespace mlua

@@ -31,6 +31,7 @@
 #include <unistd.h>
 #include <vector>
 
+#include "minilua.hpp"
 #include "splinter_ext.h"
 
 #ifndef SPL_BUILD_ID
@@ -829,7 +830,7 @@ int cmd_uuid(int, char**) {
 int cmd_caps(int, char**) {
   printf("version=%s\n", SPLINTER_VERSION);
   printf("build=%s\n", SPL_BUILD_ID);
-  printf("lua=no\nwasm=no\nembeddings=yes\nllama=no\n");
+  printf("lua=yes (minilua, Lua 5.4 subset)\nwasm=no\nembeddings=yes\nllama=no\n");
 #ifdef SYS_mbind
   printf("numa=yes\n");
 #else
@@ -1180,6 +1181,170 @@ int cmd_stats(int, char**) {
   return 0;
 }
 
+// `lua` verb: the reference's `splinter` Lua module (splinter_cli_cmd_lua.c:
+// 20-360) bound to the current store, run on minilua.
+mlua::Value splinter_module() {
+  using mlua::Value;
+  using mlua::Values;
+  auto T = std::make_shared<mlua::Table>();
+  auto str = [](Values& a, size_t i, const char* fn) -> std::string {
+    if (i < a.size() && a[i].t == Value::Str) return *a[i].s;
+    if (i < a.size() && a[i].is_num()) return mlua::tostring(a[i]);
+    throw mlua::LuaError(std::string("bad argument #") + std::to_string(i + 1) + " to '" + fn + "' (string expected)");
+  };
+  auto integer = [](Values& a, size_t i, int64_t dflt) -> int64_t {
+    if (i >= a.size() || a[i].t == Value::Nil) return dflt;
+    if (a[i].t == Value::Int) return a[i].i;
+    if (a[i].t == Value::Num) return (int64_t)a[i].n;
+    if (a[i].t == Value::Str) return (int64_t)strtoll(a[i].s->c_str(), nullptr, 0);
+    throw mlua::LuaError("number expected");
+  };
+  auto reg = [&](const char* n, mlua::Native f) { T->set(Value::string(n), mlua::make_native(n, std::move(f))); };
+  reg("get", [str](mlua::Interp&, Values& a) {
+    const std::string key = pkey(str(a, 0, "get").c_str());
+    splinter_header_snapshot_t h{};
+    splinter_get_header_snapshot(&h);
+    std::vector<char> buf(h.max_val_sz + 8);
+    size_t n = 0;
+    if (splinter_get(key.c_str(), buf.data(), buf.size(), &n) != 0) return Values{Value()};
+    splinter_slot_snapshot_t snap{};
+    if (splinter_get_slot_snapshot(key.c_str(), &snap) == 0 && (snap.type_flag & SPL_SLOT_TYPE_BIGUINT) && n >= 8) {
+      uint64_t v;
+      memcpy(&v, buf.data(), 8);
+      return Values{Value::integer((int64_t)v)};
+    }
+    return Values{Value::string(std::string(buf.data(), n))};
+  });
+  reg("get_tandem", [str, integer](mlua::Interp&, Values& a) {
+    const std::string base = pkey(str(a, 0, "get_tandem").c_str());
+    const int64_t max_orders = integer(a, 1, 64);
+    splinter_header_snapshot_t h{};
+    splinter_get_header_snapshot(&h);
+    std::vector<char> buf(h.max_val_sz + 8);
+    auto t = std::make_shared<mlua::Table>();
+    for (int64_t i = 0; i < max_orders; ++i) {
+      const std::string k = i == 0 ? base : base + SPL_ORDER_ACCESSOR + std::to_string(i);
+      size_t n = 0;
+      if (splinter_get(k.c_str(), buf.data(), buf.size(), &n) != 0) break;
+      t->set(Value::integer(i + 1), Value::string(std::string(buf.data(), n)));
+    }
+    return Values{Value::table(t)};
+  });
+  reg("set", [str](mlua::Interp&, Values& a) {
+    const std::string key = pkey(str(a, 0, "set").c_str());
+    if (a.size() > 1 && a[1].is_num()) {  // numbers become BIGUINT slots (reference :171-199)
+      uint64_t v = (uint64_t)(a[1].t == Value::Int ? a[1].i : (int64_t)a[1].n);
+      if (splinter_set(key.c_str(), &v, 8) != 0) return Values{Value::boolean(false)};
+      splinter_set_named_type(key.c_str(), SPL_SLOT_TYPE_BIGUINT);
+      return Values{Value::boolean(true)};
+    }
+    const std::string v = str(a, 1, "set");
+    return Values{Value::boolean(splinter_set(key.c_str(), v.data(), v.size()) == 0)};
+  });
+  reg("set_tandem", [str](mlua::Interp&, Values& a) {
+    const std::string base = pkey(str(a, 0, "set_tandem").c_str());
+    if (a.size() < 2 || a[1].t != Value::Tab) throw mlua::LuaError("bad argument #2 to 'set_tandem' (table expected)");
+    const int64_t n = a[1].tab->length();
+    for (int64_t i = 1; i <= n; ++i) {
+      const std::string k = i == 1 ? base : base + SPL_ORDER_ACCESSOR + std::to_string(i - 1);
+      const std::string v = mlua::tostring(a[1].tab->get(Value::integer(i)));
+      if (splinter_set(k.c_str(), v.data(), v.size()) != 0) return Values{Value::boolean(false)};
+    }
+    return Values{Value::boolean(true)};
+  });
+  reg("math", [str, integer](mlua::Interp&, Values& a) {
+    const std::string key = pkey(str(a, 0, "math").c_str()), op = str(a, 1, "math");
+    uint64_t v = (uint64_t)integer(a, 2, 0);
+    splinter_integer_op_t o;
+    if (op == "and") o = SPL_OP_AND;
+    else if (op == "or") o = SPL_OP_OR;
+    else if (op == "xor") o = SPL_OP_XOR;
+    else if (op == "not") o = SPL_OP_NOT;
+    else if (op == "inc") o = SPL_OP_INC;
+    else if (op == "dec") o = SPL_OP_DEC;
+    else throw mlua::LuaError("invalid math operation: " + op);
+    if (splinter_integer_op(key.c_str(), o, &v) == 0) return Values{Value::boolean(true)};
+    if (errno == EPROTOTYPE) throw mlua::LuaError("key '" + key + "' is not a BIGUINT slot");
+    return Values{Value::boolean(false)};
+  });
+  reg("watch", [str, integer](mlua::Interp&, Values& a) {
+    return Values{Value::boolean(splinter_watch_register(pkey(str(a, 0, "watch").c_str()).c_str(),
+                                                         (uint8_t)integer(a, 1, 0)) == 0)};
+  });
+  reg("unwatch", [str, integer](mlua::Interp&, Values& a) {
+    return Values{Value::boolean(splinter_watch_unregister(pkey(str(a, 0, "unwatch").c_str()).c_str(),
+                                                           (uint8_t)integer(a, 1, 0)) == 0)};
+  });
+  reg("label", [str](mlua::Interp&, Values& a) {
+    if (a.size() < 2 || !a[1].is_num()) throw mlua::LuaError("Label must be a numeric mask");
+    const uint64_t m = (uint64_t)(a[1].t == Value::Int ? a[1].i : (int64_t)a[1].n);
+    return Values{Value::boolean(splinter_set_label(pkey(str(a, 0, "label").c_str()).c_str(), m) == 0)};
+  });
+  reg("unset", [str](mlua::Interp&, Values& a) {
+    const int r = splinter_unset(pkey(str(a, 0, "unset").c_str()).c_str());
+    return Values{r >= 0 ? Value::integer(r) : Value::boolean(false)};
+  });
+  reg("bump", [str](mlua::Interp&, Values& a) {
+    return Values{Value::boolean(splinter_bump_slot(pkey(str(a, 0, "bump").c_str()).c_str()) == 0)};
+  });
+  reg("sleep", [integer](mlua::Interp&, Values& a) {
+    int64_t ms = integer(a, 0, 0);
+    if (ms > 0) usleep((useconds_t)ms * 1000);
+    return Values{};
+  });
+  reg("get_embedding", [str](mlua::Interp&, Values& a) {
+    std::vector<float> v(SPLINTER_EMBED_DIM);
+    if (splinter_get_embedding(pkey(str(a, 0, "get_embedding").c_str()).c_str(), v.data()) != 0) return Values{Value()};
+    double m = 0;
+    for (float x : v) m += (double)x * x;
+    if (std::sqrt(m) <= 1e-6) return Values{Value()};
+    auto t = std::make_shared<mlua::Table>();
+    for (int i = 0; i < SPLINTER_EMBED_DIM; ++i) t->set(Value::integer(i + 1), Value::number(v[(size_t)i]));
+    return Values{Value::table(t)};
+  });
+  reg("set_embedding", [str](mlua::Interp&, Values& a) {
+    if (a.size() < 2 || a[1].t != Value::Tab) throw mlua::LuaError("bad argument #2 to 'set_embedding' (table expected)");
+    const int64_t n = a[1].tab->length();
+    if (n != SPLINTER_EMBED_DIM)
+      throw mlua::LuaError("embedding table must hold exactly " + std::to_string(SPLINTER_EMBED_DIM) + " floats (got " +
+                           std::to_string(n) + ")");
+    std::vector<float> v(SPLINTER_EMBED_DIM);
+    for (int i = 0; i < SPLINTER_EMBED_DIM; ++i) {
+      Value x = a[1].tab->get(Value::integer(i + 1));
+      if (!x.is_num()) throw mlua::LuaError("embedding element " + std::to_string(i + 1) + " is not a number");
+      v[(size_t)i] = (float)x.as_double();
+    }
+    return Values{Value::boolean(splinter_set_embedding(pkey(str(a, 0, "set_embedding").c_str()).c_str(), v.data()) == 0)};
+  });
+  return Value::table(T);
+}
+
+int cmd_lua(int argc, char** argv) {
+  if (argc < 2) { fprintf(stderr, "Usage: lua <script.lua> [args...]\n"); return 1; }
+  if (!need_store("lua")) return 1;
+  FILE* f = fopen(argv[1], "rb");
+  if (!f) { fprintf(stderr, "lua: cannot open '%s': %s\n", argv[1], strerror(errno)); return 1; }
+  std::string src;
+  char buf[65536];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) src.append(buf, n);
+  fclose(f);
+  mlua::Interp I;
+  I.out = [](const std::string& s) { fwrite(s.data(), 1, s.size(), stdout); fflush(stdout); };
+  mlua::Value mod = splinter_module();
+  I.modules["splinter"] = mod;
+  I.set_global("splinter", mod);
+  std::vector<std::string> args;
+  for (int i = 2; i < argc; ++i) args.push_back(argv[i]);
+  try {
+    I.run(src, argv[1], args);
+  } catch (const mlua::LuaError& e) {
+    fprintf(stderr, "lua: %s\n", e.what());
+    return 1;
+  }
+  return 0;
+}
+
 int cmd_unavailable(int, char** argv) {
   fprintf(stderr, "%s: not compiled into this build (see `caps`)\n", argv[0]);
   return 1;
@@ -1226,7 +1391,9 @@ void register_modules() {
        [] { puts("Usage: ingest [file] [--key <key>] [--label <hex>]"); }},
       {"stats", "Store occupancy, embeddings and signal counters.", cmd_stats, nullptr},
       {"wasm", "Run a WASM module against the store (not in this build).", cmd_unavailable, nullptr},
-      {"lua", "Run a Lua script against the store (not in this build).", cmd_unavailable, nullptr},
+      {"lua", "Run a Lua script against the store (splinter module).", cmd_lua,
+       [] { puts("Usage: lua <script.lua> [args...]   (require(\"splinter\"): get get_tandem set set_tandem math\n"
+                 "       watch unwatch label unset bump sleep get_embedding set_embedding)"); }},
   };
 }
 

@@ -78,7 +78,7 @@ def test_config_caps_shard_uuid(store):
     # mode 2 does not clear HYBRID (reference splinter.c:276-299 quirk, kept): go through 0 first
     assert ctl(store, "config", "av", "0")[0] == 0 and "mop:         0" in ctl(store, "config")[1]
     assert ctl(store, "config", "av", "2")[0] == 0 and "mop:         2" in ctl(store, "config")[1]
-    assert "lua=no" in ctl(store, "caps")[1]
+    assert "lua=yes" in ctl(store, "caps")[1]
     assert "OK" in ctl(store, "shard", "claim", "0x77", "random", "5", "100000000000")[1]
     assert "0x77" in ctl(store, "shard", "table")[1]
     assert ctl(store, "shard", "who")[1].startswith("sovereign=0x77")
@@ -132,3 +132,19 @@ def test_export_import_roundtrip(store, uniq, tmp_path):
     finally:
         from libsplinter_amd import unlink
         unlink(other)
+
+
+def test_lua_verb_splinter_module(store):
+    ctl(store, "set", "test_key", "test_value")
+    rc, out, err = ctl(store, "lua", os.path.join(ROOT, "tests", "data", "bus_check.lua"), "x", "y")
+    assert rc == 0, err
+    assert "args=2" in out and "test_key=test_value" in out and "ok 42" in out
+    assert ctl(store, "get", "lua_t.2")[1].startswith("c")
+    rc, _, err = ctl(store, "lua", os.devnull + "_missing.lua")
+    assert rc != 0
+
+
+def test_cli_regression_script():
+    r = subprocess.run(["bash", os.path.join(ROOT, "tests", "cli_regression.sh"), BIN], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0 and "not ok" not in r.stdout, r.stdout[-3000:]

@@ -1,0 +1,56 @@
+"""splainference: the reference label state machine (WAITING -> SERVICING -> READY),
+streaming append, truncation at max_val_sz, system prompt; and (GPU) the MFMA
+decoder path against the CPU torch path of the same weights."""
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+WAITING, SERVICING, READY = 0x1000000000000000, 0x2000000000000000, 0x4000000000000000
+
+
+def test_state_machine_cpu(uniq):
+    from libsplinter_amd import Store, unlink
+    s = Store.create(uniq, slots=128, max_val=512, embeddings=False)
+    try:
+        s.set("req", "hello there")
+        s.set_label("req", WAITING)
+        s.set("long", "x" * 400)  # prompt + completion overflow 512 B -> truncation path
+        s.set_label("long", WAITING)
+        s.set("other", "not a request")
+        s.set("sys", "be brief")
+        r = subprocess.run([sys.executable, "-m", "libsplinter_amd.daemons.splainference", "--oneshot",
+                            "--random-init", "--device", "cpu", "--max-tokens", "64", "--system-prompt-key", "sys",
+                            uniq, "none.gguf", "7"], cwd=ROOT, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-2000:]
+        v = s.get("req")
+        assert v.startswith(b"<system>\nbe brief\n<user>\nhello there\n<assistant>\n")
+        assert len(v) > len(b"<system>\nbe brief\n<user>\nhello there\n<assistant>\n")
+        b = s.snapshot("req")["bloom"]
+        assert b & READY and not b & (WAITING | SERVICING)
+        assert len(s.get("long")) <= 512 and s.snapshot("long")["bloom"] & READY
+        assert not s.snapshot("other")["bloom"] & READY
+        dbg = s.get("__debug").decode()
+        assert "[DONE]: Completion written to key: req" in dbg
+    finally:
+        s.close()
+        unlink(uniq)
+
+
+@pytest.mark.gpu
+def test_decoder_hip_matches_cpu():
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
+    cfg = DecoderConfig(layers=2)
+    gpu = CausalLM.random(cfg, seed=3, device="cuda")
+    cpu = CausalLM.random(cfg, seed=3, device="cpu")
+    ids = [256] + list(b"the quick brown fox")
+    lg, lc = gpu.forward(ids).cpu(), cpu.forward(ids)
+    rel = (lg - lc).norm() / lc.norm()
+    assert rel < 3e-2, float(rel)
+    # one decode step through the KV cache
+    lg2, lc2 = gpu.forward([65]).cpu(), cpu.forward([65])
+    assert (lg2 - lc2).norm() / lc2.norm() < 3e-2
+    assert torch.argmax(lg2) == torch.argmax(lc2) or (lg2 - lc2).abs().max() < 0.05

@@ -12,6 +12,7 @@
 #include <mutex>
 #include <poll.h>
 #include <string>
+#include <vector>
 #include <sys/mman.h>
 #include <sys/syscall.h>
 #include <unistd.h>
@@ -211,6 +212,28 @@ int spl_store_sync(spl_store* h, int async) {
   if (!s) { errno = EOPNOTSUPP; return -1; }
   if (!s->base()) { errno = EINVAL; return -1; }
   return msync(s->base(), s->total_bytes(), async ? MS_ASYNC : MS_SYNC);
+}
+long spl_list_copy(char* buf, size_t cap) {
+  // Key names of the current store, NUL-separated, copied out (FFI bindings
+  // cannot safely walk splinter_list's pointers into the mapping).  Returns
+  // bytes written, or -(bytes needed) when `cap` is too small.
+  spl_store* h = spl_store_current();
+  if (!h) { errno = ENOTCONN; return 0; }
+  uint32_t slots = 0, mv = 0, stride = 0;
+  spl_store_geometry(h, &slots, &mv, &stride);
+  std::vector<char*> names(slots ? slots : 1);
+  size_t n = 0;
+  if (((StoreBase*)h)->list(names.data(), names.size(), &n) != 0) return 0;
+  size_t need = 0;
+  for (size_t i = 0; i < n; ++i) need += strlen(names[i]) + 1;
+  if (need > cap) return -(long)need;
+  size_t off = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const size_t L = strlen(names[i]) + 1;
+    memcpy(buf + off, names[i], L);
+    off += L;
+  }
+  return (long)off;
 }
 int spl_unlink(const char* raw) {
   Parsed p = parse_name(raw);

@@ -35,18 +35,36 @@ inline int arena_mo() {
 
 // Ops per lane per round for set/get (SPLINTER_ARENA_U = 1|2|4|8; 1 = the
 // single-op kernels, which also honour SPLINTER_ARENA_MO).
+inline int env_int(const char* name, int dflt) {
+  const char* e = getenv(name);
+  return e ? atoi(e) : dflt;
+}
 inline int arena_rounds() {
-  static int u = [] {
-    const char* e = getenv("SPLINTER_ARENA_U");
-    return e ? atoi(e) : 4;
-  }();
+  static int u = env_int("SPLINTER_ARENA_U", 4);
   return u;
+}
+// gets run best at 2 ops per lane (more lanes in flight), sets at 4 (fewer release rounds):
+// profiles/r1_kv_rounds.jsonl
+inline int arena_rounds_get() {
+  static int u = env_int("SPLINTER_ARENA_UGET", env_int("SPLINTER_ARENA_U", 2));
+  return u;
+}
+// threads per workgroup of the rounds kernels = lanes sharing one release / acquire
+inline int arena_block() {
+  static int b = env_int("SPLINTER_ARENA_BLOCK", 256);
+  return b == 512 ? 512 : 256;
 }
 
 inline int grid_for(long n) {
   long g = (n + kBlock - 1) / kBlock;
   if (g < 1) g = 1;
   return (int)(g > kMaxGrid ? kMaxGrid : g);
+}
+inline int grid_for_b(long n, int b) {  // same resident-thread cap as grid_for, any block size
+  long g = (n + b - 1) / b;
+  const long cap = (long)kMaxGrid * kBlock / b;
+  if (g < 1) g = 1;
+  return (int)(g > cap ? cap : g);
 }
 
 __device__ __forceinline__ Arena to_dev(const spl_arena_t& a) {
@@ -176,8 +194,8 @@ __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys
 // U ops per lane per round: U claims (or lookups) in flight, then ONE agent
 // release (writers) / acquire (readers) per wave for all of them.  EAGAIN ops
 // fall back to the single-op path with backoff.
-template <int U>
-__global__ __launch_bounds__(kBlock) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
                                                        const uint8_t* vals, int vstride, const uint32_t* lens, long n,
                                                        int32_t* status, int max_retry, uint64_t* stats) {
   const Arena a = to_dev(aa);
@@ -185,8 +203,10 @@ __global__ __launch_bounds__(kBlock) void k_set_rounds(spl_arena_t aa, const cha
   const bool scrub = scrub_flags(a, hybrid);
   Stats st;
   uint64_t muts = 0;
-  const long nth = (long)gridDim.x * blockDim.x;
-  for (long r0 = (blockIdx.x * (long)blockDim.x + threadIdx.x) * U; r0 < n; r0 += nth * U) {
+  // block-uniform round loop (every thread runs every round: the round ends in barriers)
+  const long per_block = (long)blockDim.x * U;
+  for (long base = blockIdx.x * per_block; base < n; base += (long)gridDim.x * per_block) {
+    const long r0 = base + (long)threadIdx.x * U;
     Key k[U];
     Claim c[U];
     uint32_t len[U];
@@ -205,7 +225,14 @@ __global__ __launch_bounds__(kBlock) void k_set_rounds(spl_arena_t aa, const cha
 #pragma unroll
     for (int j = 0; j < U; ++j)
       if (c[j].rc == kOk) write_set<0>(a, c[j], vals + (r0 + j) * (long)vstride, len[j], scrub, hybrid);
-    release();  // one agent release per wave covers every payload above
+    // ONE agent release per WORKGROUP: every wave's payload stores have reached the (shared) XCD L2
+    // once its vmcnt drains; the barrier then lets one lane write that L2 back (buffer_wbl2) for all
+    // of them before any wave publishes an epoch.  The release is serialised per XCD (~1.7 us), so
+    // this is 4x fewer serialised write-backs than one per wave.
+    drain();
+    __syncthreads();
+    if (threadIdx.x == 0) release();
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const long i = r0 + j;
@@ -232,14 +259,15 @@ __global__ __launch_bounds__(kBlock) void k_set_rounds(spl_arena_t aa, const cha
   flush_stats(a, st, stats, muts);
 }
 
-template <int U>
-__global__ __launch_bounds__(kBlock) void k_get_rounds(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                        int ostride, uint32_t* out_lens, long n, int32_t* status,
                                                        int max_retry, uint64_t* stats) {
   const Arena a = to_dev(aa);
   Stats st;
-  const long nth = (long)gridDim.x * blockDim.x;
-  for (long r0 = (blockIdx.x * (long)blockDim.x + threadIdx.x) * U; r0 < n; r0 += nth * U) {
+  const long per_block = (long)blockDim.x * U;
+  for (long base = blockIdx.x * per_block; base < n; base += (long)gridDim.x * per_block) {
+    const long r0 = base + (long)threadIdx.x * U;
     Key k[U];
     long sidx[U];
     uint64_t e1[U];
@@ -261,7 +289,12 @@ __global__ __launch_bounds__(kBlock) void k_get_rounds(spl_arena_t aa, const cha
 #pragma unroll
     for (int j = 0; j < U; ++j)
       if (rc[j] == kOk) e1[j] = slot_epoch(a.slot((size_t)sidx[j]));
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");  // one L1 invalidate for all U reads
+    // ONE agent acquire per workgroup: all lanes' epoch loads have completed (drain) before the
+    // barrier; one lane then invalidates the CU/XCD caches the whole workgroup reads through.
+    drain();
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       if (rc[j] != kOk) continue;
@@ -641,16 +674,16 @@ int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* v
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
   const int mo = arena_mo();
-  const int u = arena_rounds();
-  if (u == 2)
-    hipLaunchKernelGGL(k_set_rounds<2>, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, keys, kstride, vals,
-                       vstride, lens, n, status, max_retry, stats);
-  else if (u == 4)
-    hipLaunchKernelGGL(k_set_rounds<4>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, a, keys, kstride, vals,
-                       vstride, lens, n, status, max_retry, stats);
-  else if (u == 8)
-    hipLaunchKernelGGL(k_set_rounds<8>, dim3(grid_for((n + 7) / 8)), dim3(kBlock), 0, s, a, keys, kstride, vals,
-                       vstride, lens, n, status, max_retry, stats);
+  const int u = arena_rounds(), b = arena_block();
+#define SPL_SET_ROUNDS(U_, B_)                                                                                   \
+  hipLaunchKernelGGL((k_set_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
+                     kstride, vals, vstride, lens, n, status, max_retry, stats)
+  if (u == 2 && b == 256) SPL_SET_ROUNDS(2, 256);
+  else if (u == 2) SPL_SET_ROUNDS(2, 512);
+  else if (u == 4 && b == 256) SPL_SET_ROUNDS(4, 256);
+  else if (u == 4) SPL_SET_ROUNDS(4, 512);
+  else if (u == 8) SPL_SET_ROUNDS(8, 256);
+#undef SPL_SET_ROUNDS
   else if (mo == 1)
     hipLaunchKernelGGL(k_set<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
                        status, max_retry, stats);
@@ -668,16 +701,16 @@ int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, in
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
   const int mo = arena_mo();
-  const int u = arena_rounds();
-  if (u == 2)
-    hipLaunchKernelGGL(k_get_rounds<2>, dim3(grid_for((n + 1) / 2)), dim3(kBlock), 0, s, a, keys, kstride, out,
-                       ostride, out_lens, n, status, max_retry, stats);
-  else if (u == 4)
-    hipLaunchKernelGGL(k_get_rounds<4>, dim3(grid_for((n + 3) / 4)), dim3(kBlock), 0, s, a, keys, kstride, out,
-                       ostride, out_lens, n, status, max_retry, stats);
-  else if (u == 8)
-    hipLaunchKernelGGL(k_get_rounds<8>, dim3(grid_for((n + 7) / 8)), dim3(kBlock), 0, s, a, keys, kstride, out,
-                       ostride, out_lens, n, status, max_retry, stats);
+  const int u = arena_rounds_get(), b = arena_block();
+#define SPL_GET_ROUNDS(U_, B_)                                                                                   \
+  hipLaunchKernelGGL((k_get_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
+                     kstride, out, ostride, out_lens, n, status, max_retry, stats)
+  if (u == 2 && b == 256) SPL_GET_ROUNDS(2, 256);
+  else if (u == 2) SPL_GET_ROUNDS(2, 512);
+  else if (u == 4 && b == 256) SPL_GET_ROUNDS(4, 256);
+  else if (u == 4) SPL_GET_ROUNDS(4, 512);
+  else if (u == 8) SPL_GET_ROUNDS(8, 256);
+#undef SPL_GET_ROUNDS
   else if (mo == 1)
     hipLaunchKernelGGL(k_get<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
                        status, max_retry, stats);

@@ -31,6 +31,7 @@ int         spl_store_geometry(spl_store *s, uint32_t *slots, uint32_t *max_val,
 void       *spl_store_base(spl_store *s);         /* mapped region (host backends), else NULL */
 size_t      spl_store_bytes(spl_store *s);
 int         spl_store_sync(spl_store *s, int async);  /* msync a file-backed store (0 = MS_SYNC) */
+long        spl_list_copy(char *buf, size_t cap);     /* current store's keys, NUL-separated; -(need) if short */
 int         spl_unlink(const char *name);         /* remove shm object / file / hbm descriptor */
 const char *spl_version(void);
 const char *spl_build(void);

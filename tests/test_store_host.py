@@ -155,3 +155,19 @@ def test_watchdog_stuck_writer_host(store):
     assert store.stuck_slots(hold_ms=5) == [i]
     assert store.retrain("victim")
     assert store.stuck_slots(hold_ms=1) == [] and store.epoch("victim") == 4
+
+
+def test_list_copy_for_ffi_bindings(store):
+    """spl_list_copy backs the TS binding's list() (bindings/ts/splinter.ts)."""
+    import ctypes
+    from libsplinter_amd import _native as N
+    for k in ("k1", "key_two"):
+        store.set(k, "v")
+    store.use()
+    L = N.core_lib()
+    L.spl_list_copy.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    L.spl_list_copy.restype = ctypes.c_long
+    need = -L.spl_list_copy(None, 0)
+    buf = ctypes.create_string_buffer(need)
+    n = L.spl_list_copy(buf, need)
+    assert n == need and sorted(buf.raw[:n].split(b"\0")[:-1]) == [b"k1", b"key_two"]

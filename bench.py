@@ -47,6 +47,8 @@ def parse():
     p.add_argument("--embed-batch", type=int, default=64, help="documents per rank per step")
     p.add_argument("--embed-seq", type=int, default=512)
     p.add_argument("--verify", type=int, default=20000)
+    p.add_argument("--backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: "
+                   "ranks may share a GPU, collectives staged through the host)")
     return p.parse_args()
 
 
@@ -58,9 +60,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    dev = local % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.backend)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
     from libsplinter_amd.parallel.sharded import GpuShard, ShardedKV

@@ -71,6 +71,48 @@ def decode_keys(rows: torch.Tensor) -> List[str]:
     return [bytes(r).split(b"\0", 1)[0].decode("utf-8", "replace") for r in rows.cpu().numpy()]
 
 
+class _Coll:
+    """Collective calls of one group.  RCCL takes device tensors directly; with the
+    gloo backend (CPU tests, or several ranks sharing one GPU to rehearse the
+    multi-GPU path) device tensors are staged through host copies."""
+
+    def __init__(self, group):
+        self.group = group
+        self.stage = dist.get_backend(group) == "gloo"
+
+    def _h(self, t):
+        return t.cpu() if self.stage and t.is_cuda else t
+
+    def all_to_all(self, out, inp, out_splits=None, in_splits=None):
+        if self.stage and out.is_cuda:
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def all_reduce(self, t):
+        h = self._h(t)
+        dist.all_reduce(h, group=self.group)
+        if h is not t:
+            t.copy_(h)
+
+    def broadcast(self, t, src):
+        h = self._h(t)
+        dist.broadcast(h, src, group=self.group)
+        if h is not t:
+            t.copy_(h)
+
+    def all_gather(self, outs, t):
+        if self.stage and t.is_cuda:
+            ho = [torch.empty(o.shape, dtype=o.dtype) for o in outs]
+            dist.all_gather(ho, t.cpu(), group=self.group)
+            for o, h in zip(outs, ho):
+                o.copy_(h)
+        else:
+            dist.all_gather(outs, t, group=self.group)
+
+
 class ShardedKV:
     def __init__(self, local, group: Optional[dist.ProcessGroup] = None):
         self.local = local
@@ -78,8 +120,10 @@ class ShardedKV:
         if dist.is_available() and dist.is_initialized():
             self.world = dist.get_world_size(group)
             self.rank = dist.get_rank(group)
+            self._c = _Coll(group)
         else:
             self.world, self.rank = 1, 0
+            self._c = None
 
     # ----------------------------------------------------------- routing --
     def _plan(self, keys: torch.Tensor):
@@ -88,13 +132,13 @@ class ShardedKV:
         order = torch.argsort(dest, stable=True)
         send = torch.bincount(dest, minlength=self.world)
         recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send, group=self.group)
+        self._c.all_to_all(recv, send)
         s, r = send.tolist(), recv.tolist()
         return order, s, r
 
     def _route(self, x: torch.Tensor, send_splits, recv_splits) -> torch.Tensor:
         out = torch.empty((sum(recv_splits),) + tuple(x.shape[1:]), dtype=x.dtype, device=x.device)
-        dist.all_to_all_single(out, x.contiguous(), recv_splits, send_splits, group=self.group)
+        self._c.all_to_all(out, x.contiguous(), recv_splits, send_splits)
         return out
 
     def _roundtrip(self, keys: torch.Tensor, cols: List[torch.Tensor], execute, resp_spec):
@@ -179,7 +223,7 @@ class ShardedKV:
         """Node-wide signal-group counters: sum of per-shard counters (64 x u64)."""
         t = (self.local.signal_counts() if local_counts is None else local_counts).clone()
         if self.world > 1:
-            dist.all_reduce(t, group=self.group)
+            self._c.all_reduce(t)
         return t
 
     # ------------------------------------------- C3 + C4: vector search ----
@@ -194,11 +238,11 @@ class ShardedKV:
         dev = self.local.device
         if self.world > 1:
             n = torch.tensor([0 if queries is None else queries.shape[0]], dtype=torch.int64, device=dev)
-            dist.broadcast(n, 0, group=self.group)
+            self._c.broadcast(n, 0)
             q = torch.empty((int(n.item()), 768), dtype=torch.float32, device=dev)
             if self.rank == 0:
                 q.copy_(queries.reshape(-1, 768))
-            dist.broadcast(q, 0, group=self.group)
+            self._c.broadcast(q, 0)
         else:
             q = queries.reshape(-1, 768).to(device=dev, dtype=torch.float32)
         sim, dst, krows = self.local.search(q, k, min_sim, max_dist, label_mask)
@@ -208,9 +252,9 @@ class ShardedKV:
             gs = [torch.empty_like(sim) for _ in range(self.world)]
             gd = [torch.empty_like(dst) for _ in range(self.world)]
             gk = [torch.empty_like(krows) for _ in range(self.world)]
-            dist.all_gather(gs, sim, group=self.group)
-            dist.all_gather(gd, dst, group=self.group)
-            dist.all_gather(gk, krows, group=self.group)
+            self._c.all_gather(gs, sim)
+            self._c.all_gather(gd, dst)
+            self._c.all_gather(gk, krows)
             sim, dst, krows = torch.cat(gs, 1), torch.cat(gd, 1), torch.cat(gk, 1)
         nqq, tot = sim.shape
         owner = torch.arange(tot, device=dev).div(k, rounding_mode="floor").expand(nqq, tot)
@@ -231,13 +275,13 @@ class ShardedKV:
     def _all_gather_var(self, t: torch.Tensor) -> torch.Tensor:
         n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
         counts = [torch.empty_like(n) for _ in range(self.world)]
-        dist.all_gather(counts, n, group=self.group)
+        self._c.all_gather(counts, n)
         cs = [int(c.item()) for c in counts]
         mx = max(cs) if cs else 0
         pad = torch.zeros((mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         pad[: t.shape[0]] = t
         parts = [torch.empty_like(pad) for _ in range(self.world)]
-        dist.all_gather(parts, pad, group=self.group)
+        self._c.all_gather(parts, pad)
         return torch.cat([p[:c] for p, c in zip(parts, cs)])
 
     def enumerate(self, mask: int = 0) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -256,7 +300,7 @@ class ShardedKV:
         """Replicate rank 0's mop mode and label->group map to every shard."""
         cfg = self.local.get_config().to(self.local.device)  # uint8[65]: mop, bloom_watches[64]
         if self.world > 1:
-            dist.broadcast(cfg, 0, group=self.group)
+            self._c.broadcast(cfg, 0)
             if self.rank != 0:
                 self.local.apply_config(cfg)
         c = cfg.cpu().tolist()

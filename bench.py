@@ -80,6 +80,9 @@ def main():
     arena = HbmArena.create(name, slots=slots, max_val=args.max_val, embeddings=False)
     arena.store.set_mop(0)  # throughput mode: no scrubbing (reference stress default)
     kv = ShardedKV(GpuShard(arena))
+    # gets route over a second communicator so the set and get all-to-alls (and their kernels)
+    # overlap on their own streams instead of serialising on one RCCL stream
+    kv_get = ShardedKV(GpuShard(arena), group=dist.new_group(backend=args.backend)) if world > 1 else kv
     vstride = (args.max_val + 15) // 16 * 16
 
     # ---- prepopulate: every rank inserts the global ids it owns ----------
@@ -150,7 +153,8 @@ def main():
             else:
                 with torch.cuda.stream(s_set):
                     kv.set(SK, SV, SL)
-                    kv.get(GK)
+                with torch.cuda.stream(s_get):
+                    kv_get.get(GK)
             cur.wait_stream(s_set)
             cur.wait_stream(s_get)
         if embedder is not None:
@@ -184,7 +188,7 @@ def main():
         GK, gid = batches[0][3], batches[0][4]
         m = min(args.verify, n_get)
         if world > 1:
-            sts, outv, lens = kv.get(GK[:m])
+            sts, outv, lens = kv_get.get(GK[:m])
         else:
             sts, outv, lens = arena.get(GK[:m])
         o, ln, ids, s_ = outv.cpu().numpy(), lens.cpu().numpy(), gid[:m].cpu().numpy(), sts.cpu().numpy()

@@ -91,9 +91,9 @@ class _Coll:
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 
-    def all_reduce(self, t):
+    def all_reduce(self, t, op=dist.ReduceOp.SUM):
         h = self._h(t)
-        dist.all_reduce(h, group=self.group)
+        dist.all_reduce(h, op=op, group=self.group)
         if h is not t:
             t.copy_(h)
 
@@ -168,6 +168,11 @@ class ShardedKV:
     def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, **kw) -> torch.Tensor:
         if self.world == 1:
             return self.local.set(keys, vals, lens, **kw)
+        # ship only the used prefix of the value rows (16-B multiple): 150-B values in 256-B rows
+        # are 40 % less xGMI traffic
+        w = (int(lens.max().item()) + 15) // 16 * 16 if lens.numel() else 16
+        if 0 < w < vals.shape[1]:
+            vals = vals[:, :w]
         return self._roundtrip(keys, [vals, lens.to(torch.int32)],
                                lambda k, v, ln: [self.local.set(k, v, ln, **kw).to(torch.int32)], None)[0]
 
@@ -177,7 +182,12 @@ class ShardedKV:
 
         def ex(k):
             st, v, ln = self.local.get(k, **kw)
-            return [st.to(torch.int32), ln.to(torch.int32), v]
+            # response rows carry only the longest value any shard returns (one scalar all-reduce)
+            w = torch.tensor([(int(ln.max().item()) + 15) // 16 * 16 if ln.numel() else 16],
+                             dtype=torch.int64, device=v.device)
+            self._c.all_reduce(w, op=dist.ReduceOp.MAX)
+            w = max(16, min(int(w.item()), v.shape[1]))
+            return [st.to(torch.int32), ln.to(torch.int32), v[:, :w]]
         st, ln, v = self._roundtrip(keys, [], ex, None)
         return st, v, ln
 

@@ -56,8 +56,25 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 times[(name, v)].append(s.elapsed_time(e) / a.iters)
+    # library reference point: hipBLASLt via torch.matmul (plain GEMM, no fused epilogue)
+    ref = {}
+    for name, mode, N, K in shapes:
+        A, W = bufs[name][3], bufs[name][4]
+        torch.matmul(A, W.T)
+        ts = []
+        for _ in range(a.rounds):
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(a.iters):
+                torch.matmul(A, W.T)
+            e.record()
+            torch.cuda.synchronize()
+            ts.append(s.elapsed_time(e) / a.iters)
+        ref[name] = float(np.median(ts))
     for name, mode, N, K in shapes:
         fl = 2.0 * M * N * K
+        print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": "torch.matmul(hipBLASLt)",
+                          "ms_median": ref[name], "tflops_median": fl / ref[name] / 1e9}))
         for v in (256, 128):
             t = np.array(times[(name, v)])
             print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": v, "ms_median": float(np.median(t)),

@@ -202,3 +202,28 @@ def test_watchdog_finds_stuck_writer_and_retrain_recovers(arena):
     assert int(arena.meta("retrain", K[7:8])[0][0]) == 0
     assert arena.stuck_slots(hold_ms=1)[0].numel() == 0
     assert int(arena.get(K[7:8])[0][0]) == 0
+
+
+def test_cross_process_attach_ipc(arena, uniq):
+    """Another process attaches the same HBM arena through the hbm: descriptor
+    (hipIpcOpenMemHandle): the C CLI reads what this process wrote, a child Python
+    process writes a key this process then reads."""
+    import subprocess
+    import sys
+    import torch
+    from libsplinter_amd.ops.arena import pack_keys, pack_values
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    K = pack_keys(["ipc_a", "ipc_b"], 16)
+    V, L = pack_values([b"from parent", b"second"], 16)
+    assert (arena.set(K, V, L) == 0).all()
+    torch.cuda.synchronize()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cli = os.path.join(root, "libsplinter_amd", "bin", "splinterctl")
+    r = subprocess.run([cli, "-u", f"hbm:{uniq}", "get", "ipc_a"], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0 and r.stdout.startswith("from parent"), r.stderr
+    code = ("import torch; from libsplinter_amd import Store; "
+            f"s = Store.open('hbm:{uniq}'); assert s.get('ipc_b') == b'second'; s.set('ipc_child', 'hello from child')")
+    r = subprocess.run([sys.executable, "-c", code], cwd=root, capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    st, out, ol = arena.get(pack_keys(["ipc_child"], 16))
+    assert int(st[0]) == 0 and bytes(out[0, : int(ol[0])].cpu().numpy()) == b"hello from child"

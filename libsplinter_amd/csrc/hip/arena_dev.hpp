@@ -237,16 +237,26 @@ __device__ __forceinline__ void write_value(const Arena& a, size_t idx, const ui
                                             bool hybrid) {
   uint4* dst = (uint4*)a.value(idx);
   const uint4* s4 = (const uint4*)src;
-  const uint32_t full = len >> 4;
-  for (uint32_t c = 0; c < full; ++c) st16<MO>(dst + c, s4[c]);
-  uint32_t done = full << 4;
-  if (len & 15) {
-    uint4 t = s4[full];
-    const int r = (int)(len & 15);
-    t.x &= keep_mask(r); t.y &= keep_mask(r - 4); t.z &= keep_mask(r - 8); t.w &= keep_mask(r - 12);
-    st16<MO>(dst + full, t);
-    done += 16;
+  const uint32_t n16 = (len + 15) >> 4;
+  // 8 source loads in flight per batch (one memory round trip per 128 B instead of one per
+  // 16 B); the loads are unconditional (clamped into the record) so hipcc does not branch and
+  // wait around each one
+  for (uint32_t b = 0; b < n16; b += 8) {
+    uint4 t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = s4[min(b + (uint32_t)q, n16 - 1)];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const uint32_t c = b + (uint32_t)q;
+      if (c >= n16) break;
+      if (c == n16 - 1 && (len & 15)) {
+        const int r = (int)(len & 15);
+        t[q].x &= keep_mask(r); t[q].y &= keep_mask(r - 4); t[q].z &= keep_mask(r - 8); t[q].w &= keep_mask(r - 12);
+      }
+      st16<MO>(dst + c, t[q]);
+    }
   }
+  uint32_t done = n16 << 4;
   if (scrub) {
     uint32_t end = hybrid ? ((len + 63u) & ~63u) : a.max_val;
     if (end > a.max_val) end = a.max_val;
@@ -292,11 +302,15 @@ __device__ Claim claim_set(const Arena& a, const Key& k) {
   size_t idx = home;
   for (uint32_t i = 0; i < a.slots; ++i) {
     uint8_t* s = a.slot(idx);
+    // hash, epoch and key words in ONE round trip (the key compare is speculative)
     const uint64_t sh = slot_hash(s);
     const uint64_t e = slot_epoch(s);
-    if (sh == k.hash && key_eq(s, k)) {  // update in place
+    const bool keq = key_eq(s, k);
+    if (sh == k.hash && keq) {  // update in place
       if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return Claim{-1, false, kAgain};
-      if (slot_hash(s) != k.hash || !key_eq(s, k)) {  // raced with unset / reuse
+      const uint64_t sh2 = slot_hash(s);  // re-check after the claim: hash + key together
+      const bool keq2 = key_eq(s, k);
+      if (sh2 != k.hash || !keq2) {  // raced with unset / reuse
         aadd64(epoch_ptr(s), 1);
         return Claim{-1, false, kAgain};
       }
@@ -414,6 +428,41 @@ __device__ int32_t get_op(const Arena& a, const Key& k, uint8_t* out, uint32_t o
     if (++idx == a.slots) idx = 0;
   }
   return kNoEnt;
+}
+
+// One-round-trip probe for batched gets: hash, epoch, length and the key
+// words of each probed slot are loaded together; returns the slot index with
+// its epoch / length as observed, or -1 for a miss.  The caller validates the
+// whole read afterwards (key words again with the data, epoch unchanged).
+__device__ __forceinline__ long locate_peek(const Arena& a, const Key& k, uint64_t* e1, uint32_t* len) {
+  size_t idx = (size_t)(k.hash % a.slots);
+  for (uint32_t i = 0; i < a.slots; ++i) {
+    const uint8_t* s = a.slot(idx);
+    const uint64_t sh = slot_hash(s);
+    const uint64_t e = slot_epoch(s);
+    const uint32_t L = ald32(s + kOffValLen);
+    const bool keq = key_eq(s, k);
+    if (sh == k.hash && keq) {
+      *e1 = e;
+      *len = L;
+      return (long)idx;
+    }
+    if (sh == 0 && e == 0) return -1;
+    if (++idx == a.slots) idx = 0;
+  }
+  return -1;
+}
+
+// Copy n16 16-B chunks with 8 loads in flight per batch (see write_value).
+__device__ __forceinline__ void copy_chunks(uint4* dst, const uint4* src, uint32_t n16, uint32_t src_chunks) {
+  for (uint32_t b = 0; b < n16; b += 8) {
+    uint4 t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = src[min(b + (uint32_t)q, src_chunks - 1)];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (b + (uint32_t)q < n16) dst[b + q] = t[q];
+  }
 }
 
 // Batched GET, phase helpers (see k_get_rounds): locate without the seqlock,

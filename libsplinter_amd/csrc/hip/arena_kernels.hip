@@ -259,7 +259,7 @@ __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* ke
   flush_stats(a, st, stats, muts);
 }
 
-template <int U, int B>
+template <int U, int B, int GV = 1>
 __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                        int ostride, uint32_t* out_lens, long n, int32_t* status,
                                                        int max_retry, uint64_t* stats) {
@@ -282,13 +282,10 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
       if (i < n) {
         load_key(k[j], keys + i * (long)kstride, kstride);
         ++st.attempts;
-        sidx[j] = locate(a, k[j]);
+        sidx[j] = locate_peek(a, k[j], &e1[j], &len[j]);  // hash/epoch/len/key: one round trip per probe
         rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
       }
     }
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (rc[j] == kOk) e1[j] = slot_epoch(a.slot((size_t)sidx[j]));
     // ONE agent acquire per workgroup: all lanes' epoch loads have completed (drain) before the
     // barrier; one lane then invalidates the CU/XCD caches the whole workgroup reads through.
     drain();
@@ -299,22 +296,27 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
     for (int j = 0; j < U; ++j) {
       if (rc[j] != kOk) continue;
       const uint8_t* s = a.slot((size_t)sidx[j]);
-      if ((e1[j] & 1) || !key_eq(s, k[j])) { rc[j] = kAgain; continue; }
-      len[j] = ald32(s + kOffValLen);
+      if ((e1[j] & 1) || len[j] > a.max_val) { rc[j] = kAgain; continue; }
+      // key words again, in the same round trip as the payload: the pre-acquire compare was
+      // speculative (validated below together with the unchanged epoch)
+      const bool keq = key_eq(s, k[j]);
       if (out) {
         if (len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
         const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
         uint4* dst = (uint4*)(out + (r0 + j) * (long)ostride);
         const uint32_t n16 = (len[j] + 15) >> 4;
-        for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
+        if (GV == 2) copy_chunks(dst, src, n16, (a.max_val + 15) >> 4);
+        else for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
       }
+      if (!keq) rc[j] = kAgain;
     }
     drain();
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       if (rc[j] != kOk) continue;
       const uint8_t* s = a.slot((size_t)sidx[j]);
-      if (slot_epoch(s) != e1[j] || slot_hash(s) != k[j].hash) rc[j] = kAgain;
+      const uint64_t e2 = slot_epoch(s), h2 = slot_hash(s);  // one round trip
+      if (e2 != e1[j] || h2 != k[j].hash) rc[j] = kAgain;
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -705,7 +707,11 @@ int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, in
 #define SPL_GET_ROUNDS(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_get_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, out, ostride, out_lens, n, status, max_retry, stats)
-  if (u == 2 && b == 256) SPL_GET_ROUNDS(2, 256);
+  static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
+  if (u == 2 && b == 256 && gv == 2)
+    hipLaunchKernelGGL((k_get_rounds<2, 256, 2>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
+                       kstride, out, ostride, out_lens, n, status, max_retry, stats);
+  else if (u == 2 && b == 256) SPL_GET_ROUNDS(2, 256);
   else if (u == 2) SPL_GET_ROUNDS(2, 512);
   else if (u == 4 && b == 256) SPL_GET_ROUNDS(4, 256);
   else if (u == 4) SPL_GET_ROUNDS(4, 512);

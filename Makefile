@@ -26,7 +26,7 @@ HOST_LIBS := $(LIB)/libsplinter.so $(LIB)/libsplinter_p.so
 TOOLS     := $(patsubst $(SRC)/tools/%.cpp,$(BIN)/%,$(wildcard $(SRC)/tools/*.cpp)) \
              $(if $(wildcard $(SRC)/cli/*.cpp),$(BIN)/splinterctl)
 
-.PHONY: all host hip tools clean test
+.PHONY: all host hip tools clean test tsan
 all: host hip tools
 host: $(HOST_LIBS)
 hip: $(LIB)/libsplinter_hip.so
@@ -56,6 +56,16 @@ $(BIN)/splinterctl: $(wildcard $(SRC)/cli/*.cpp $(SRC)/cli/*.hpp) $(LIB)/libspli
 
 test: host tools
 	$(BIN)/splinter_test
+
+# ThreadSanitizer builds of the host store + TAP/stress tools (SURVEY §5 race detection);
+# the seqlock payload copies are the only exempt accesses (store_host.cpp seq_copy).
+TSAN_TOOLS := $(BIN)/tsan/splinter_test $(BIN)/tsan/splinter_stress $(BIN)/tsan/splinter_chi_sao
+tsan: $(TSAN_TOOLS)
+$(BIN)/tsan:
+	mkdir -p $@
+$(BIN)/tsan/%: $(SRC)/tools/%.cpp $(CORE_SRCS) $(CORE_HDRS) | $(BIN)/tsan
+	$(CXX) -O1 -g -std=c++17 -fsanitize=thread -Wno-tsan -fPIC -D_GNU_SOURCE -I$(SRC)/include -I$(SRC)/core \
+	  -o $@ $< $(CORE_SRCS) $(LDLIBS)
 
 clean:
 	rm -rf build $(LIB)/*.so $(BIN)

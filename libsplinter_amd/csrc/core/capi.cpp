@@ -4,6 +4,7 @@
 //   "file:PATH" / a path  -> regular file (reference -DSPLINTER_PERSISTENT)
 //   "shm:NAME" / NAME     -> POSIX shm object (reference default)
 // Reference C API: /root/reference/splinter.h:288-1213.
+#include <atomic>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
@@ -29,7 +30,7 @@ using spl::StoreBase;
 
 namespace {
 
-StoreBase* g_cur = nullptr;  // the reference's "one open store per process"
+std::atomic<StoreBase*> g_cur{nullptr};  // the reference's "one open store per process" (atomic: any thread may switch it)
 
 enum class Kind { Shm, File, Hbm };
 
@@ -187,7 +188,7 @@ void spl_store_close(spl_store* h) {
   delete s;
 }
 int spl_store_use(spl_store* h) { g_cur = (StoreBase*)h; return 0; }
-spl_store* spl_store_current(void) { return (spl_store*)g_cur; }
+spl_store* spl_store_current(void) { return (spl_store*)g_cur.load(); }
 const char* spl_store_backend(spl_store* h) { return h ? ((StoreBase*)h)->backend() : "none"; }
 int spl_store_geometry(spl_store* h, uint32_t* slots, uint32_t* max_val, uint32_t* stride) {
   if (!h) return -2;
@@ -315,12 +316,12 @@ DUAL(int, madvise, -2, madvise(id, addr, len, advice, timeout), (uint32_t id, vo
 
 extern "C" {
 
-void splinter_purge(void) { if (g_cur) g_cur->purge(); }
+void splinter_purge(void) { if (g_cur) g_cur.load()->purge(); }
 void spl_purge(spl_store* h) { if (h) ((StoreBase*)h)->purge(); }
 
 int splinter_shard_claim(uint32_t id, uint8_t intent, uint8_t prio, uint64_t dur) {
   if (!g_cur) return -2;
-  return g_cur->shard_claim_ex(id, (uint32_t)getpid(), intent, prio, dur, spl::now_ticks());
+  return g_cur.load()->shard_claim_ex(id, (uint32_t)getpid(), intent, prio, dur, spl::now_ticks());
 }
 int spl_shard_claim(spl_store* h, uint32_t id, uint8_t intent, uint8_t prio, uint64_t dur) {
   if (!h) return -2;
@@ -328,17 +329,17 @@ int spl_shard_claim(spl_store* h, uint32_t id, uint8_t intent, uint8_t prio, uin
 }
 int splinter_shard_is_sovereign(uint32_t id) {
   if (!g_cur) return -2;
-  return (id != 0 && g_cur->shard_election(nullptr) == id) ? 1 : 0;
+  return (id != 0 && g_cur.load()->shard_election(nullptr) == id) ? 1 : 0;
 }
 
 void splinter_enumerate_matches(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) {
-  if (g_cur) g_cur->enumerate(mask, cb, ud);
+  if (g_cur) g_cur.load()->enumerate(mask, cb, ud);
 }
 void spl_enumerate_matches(spl_store* h, uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) {
   if (h) ((StoreBase*)h)->enumerate(mask, cb, ud);
 }
 
-void splinter_event_bus_get_dirty(uint64_t* out, size_t words) { if (g_cur) g_cur->event_bus_dirty(out, words); }
+void splinter_event_bus_get_dirty(uint64_t* out, size_t words) { if (g_cur) g_cur.load()->event_bus_dirty(out, words); }
 void spl_event_bus_get_dirty(spl_store* h, uint64_t* out, size_t words) { if (h) ((StoreBase*)h)->event_bus_dirty(out, words); }
 
 int splinter_event_bus_wait(int fd, uint64_t timeout_ms) {
@@ -351,24 +352,24 @@ int splinter_event_bus_wait(int fd, uint64_t timeout_ms) {
 }
 void splinter_event_bus_close(int fd) { if (fd >= 0) close(fd); }
 
-void splinter_pulse_watchers(struct splinter_slot* slot) { if (g_cur && slot) g_cur->pulse_slot(slot); }
+void splinter_pulse_watchers(struct splinter_slot* slot) { if (g_cur && slot) g_cur.load()->pulse_slot(slot); }
 
 // flag helpers operate on the header pointer they are given; NULL means the
 // current store (works for the HBM backend, whose header is not host-mapped).
 void splinter_config_set(struct splinter_header* hdr, uint8_t mask) {
   if (hdr) __atomic_fetch_or(&hdr->core_flags, mask, __ATOMIC_ACQ_REL);
-  else if (g_cur) g_cur->config_or(mask);
+  else if (g_cur) g_cur.load()->config_or(mask);
 }
 void splinter_config_clear(struct splinter_header* hdr, uint8_t mask) {
   if (hdr) __atomic_fetch_and(&hdr->core_flags, (uint8_t)~mask, __ATOMIC_ACQ_REL);
-  else if (g_cur) g_cur->config_and((uint8_t)~mask);
+  else if (g_cur) g_cur.load()->config_and((uint8_t)~mask);
 }
 int splinter_config_test(struct splinter_header* hdr, uint8_t mask) {
-  uint8_t f = hdr ? __atomic_load_n(&hdr->core_flags, __ATOMIC_ACQUIRE) : (g_cur ? g_cur->config_get() : 0);
+  uint8_t f = hdr ? __atomic_load_n(&hdr->core_flags, __ATOMIC_ACQUIRE) : (g_cur ? g_cur.load()->config_get() : 0);
   return (f & mask) != 0;
 }
 uint8_t splinter_config_snapshot(struct splinter_header* hdr) {
-  return hdr ? __atomic_load_n(&hdr->core_flags, __ATOMIC_ACQUIRE) : (g_cur ? g_cur->config_get() : 0);
+  return hdr ? __atomic_load_n(&hdr->core_flags, __ATOMIC_ACQUIRE) : (g_cur ? g_cur.load()->config_get() : 0);
 }
 void splinter_slot_usr_set(struct splinter_slot* s, uint16_t m) { if (s) __atomic_fetch_or(&s->user_flag, (uint8_t)m, __ATOMIC_ACQ_REL); }
 void splinter_slot_usr_clear(struct splinter_slot* s, uint16_t m) { if (s) __atomic_fetch_and(&s->user_flag, (uint8_t)~m, __ATOMIC_ACQ_REL); }

@@ -37,8 +37,29 @@ template <class T> static inline void st(T* p, T v, int mo = __ATOMIC_RELEASE) {
 static inline bool cas64(uint64_t* p, uint64_t expect, uint64_t want) {
   return __atomic_compare_exchange_n(p, &expect, want, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE);
 }
+static inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+  __builtin_ia32_pause();
+#elif defined(__aarch64__)
+  __asm__ __volatile__("yield");
+#endif
+}
 static inline void fence_acq() { __atomic_thread_fence(__ATOMIC_ACQUIRE); }
 static inline void fence_rel() { __atomic_thread_fence(__ATOMIC_RELEASE); }
+
+// Payload copies under the seqlock are racy BY DESIGN (a reader may copy while a
+// writer writes; the epoch re-check discards such reads).  TSAN builds route them
+// through an uninstrumented volatile copy so the race detector reports only races
+// outside the protocol (SURVEY §5 race detection); normal builds use memcpy.
+#if defined(__SANITIZE_THREAD__)
+__attribute__((no_sanitize_thread, noinline)) static void seq_copy(void* dst, const void* src, size_t n) {
+  volatile unsigned char* d = (volatile unsigned char*)dst;
+  const volatile unsigned char* s = (const volatile unsigned char*)src;
+  for (size_t i = 0; i < n; ++i) d[i] = s[i];
+}
+#else
+static inline void seq_copy(void* dst, const void* src, size_t n) { std::memcpy(dst, src, n); }
+#endif
 
 uint64_t now_ticks() {
 #if defined(__x86_64__) || defined(__i386__)
@@ -286,11 +307,11 @@ int HostStore::write_locked(size_t idx, const KeyRef& k, const void* val, size_t
     }
     std::memset(dst, 0, n);
   }
-  std::memcpy(dst, val, len);
+  seq_copy(dst, val, len);
   st(&s->val_len, (uint32_t)len);
   if (fresh) {
     if (geo_.embeddings()) std::memset(embedding(idx), 0, kEmbedBytes);
-    std::memcpy(s->key, k.buf, kKeyMax);  // NUL-padded canonical key
+    seq_copy(s->key, k.buf, kKeyMax);  // NUL-padded canonical key
   }
   fence_rel();
   st(&s->hash, k.hash);
@@ -315,8 +336,10 @@ int HostStore::set(const char* key, const void* val, size_t len) {
   size_t idx = home;
   for (uint32_t i = 0; i < n; ++i) {
     splinter_slot* s = slot(idx);
-    const uint64_t sh = ld(&s->hash);
+    // epoch BEFORE hash: a writer stores the hash and then bumps the epoch, so an even
+    // epoch read first guarantees the hash read after it is at least that new
     const uint64_t e = ld(&s->epoch);
+    const uint64_t sh = ld(&s->hash);
     if (sh == k.hash && key_eq(s, k)) {
       // update in place
       if (e & 1) { errno = EAGAIN; return -1; }
@@ -345,9 +368,15 @@ int HostStore::set(const char* key, const void* val, size_t len) {
     errno = EAGAIN;
     return -1;
   }
-  // A published copy of the key anywhere on the chain, or a claim in flight
-  // *before* ours (possibly the same key), makes us back off: the earlier
-  // claimant wins, so racing inserters always make progress.
+  // Re-validate the chain while holding the claim.  The claim CAS is a full barrier,
+  // so of two racing inserters at least one sees the other's claim here (Dekker);
+  // "the earlier claimant on the chain wins" alone is NOT enough: the earlier one may
+  // miss the later one's claim's resolution order (see docs/DIVERGENCES.md), so:
+  //   * the key published anywhere on the chain, or a claim in flight EARLIER on the
+  //     chain (possibly our key)             -> back off (EAGAIN);
+  //   * a claim in flight LATER on the chain -> wait for it to resolve (it never waits
+  //     for us: it either sees our earlier claim and backs off, or publishes its key,
+  //     which we then see and back off from), then re-check that slot.
   idx = home;
   bool before = true;
   for (uint32_t i = 0; i < n; ++i) {
@@ -355,9 +384,15 @@ int HostStore::set(const char* key, const void* val, size_t len) {
       before = false;
     } else {
       splinter_slot* s = slot(idx);
-      const uint64_t sh = ld(&s->hash);
-      const uint64_t e = ld(&s->epoch);
-      if ((sh == k.hash && (key_eq(s, k) || (e & 1))) || (before && (e & 1) && sh == 0)) {
+      uint64_t e = ld(&s->epoch);
+      uint64_t sh = ld(&s->hash);
+      if (!before && (e & 1) && (sh == 0 || sh == k.hash)) {
+        for (uint32_t spin = 0; spin < (1u << 20) && ld(&s->epoch) == e; ++spin) cpu_relax();
+        e = ld(&s->epoch);
+        sh = ld(&s->hash);
+      }
+      const bool mine = sh == k.hash && key_eq(s, k);
+      if (mine || ((e & 1) && (sh == 0 || sh == k.hash))) {
         __atomic_fetch_add(&fs->epoch, 1, __ATOMIC_RELEASE);
         errno = EAGAIN;
         return -1;
@@ -419,7 +454,7 @@ int HostStore::get(const char* key, void* buf, size_t buf_sz, size_t* out_sz) {
         if (out_sz) *out_sz = len;
         if (buf) {
           if (buf_sz < len) { errno = EMSGSIZE; return -1; }
-          std::memcpy(buf, value(idx), len);
+          seq_copy(buf, value(idx), len);
         }
         fence_acq();
         const uint64_t e2 = ld(&s->epoch);
@@ -495,9 +530,9 @@ int HostStore::slot_snapshot(const char* key, splinter_slot_snapshot_t* o) {
     o->ctime = ld(&s->ctime);
     o->atime = ld(&s->atime);
     o->bloom = ld(&s->bloom);
-    std::memcpy(o->key, s->key, kKeyMax);
+    seq_copy(o->key, s->key, kKeyMax);
 #ifdef SPLINTER_EMBEDDINGS
-    if (geo_.embeddings()) std::memcpy(o->embedding, embedding((size_t)i), kEmbedBytes);
+    if (geo_.embeddings()) seq_copy(o->embedding, embedding((size_t)i), kEmbedBytes);
     else std::memset(o->embedding, 0, kEmbedBytes);
 #endif
     fence_acq();
@@ -519,7 +554,7 @@ int HostStore::append(const char* key, const void* data, size_t len, size_t* new
     errno = EMSGSIZE;
     return -1;
   }
-  std::memcpy(value((size_t)i) + cur, data, len);
+  seq_copy(value((size_t)i) + cur, data, len);
   st(&s->val_len, (uint32_t)(cur + len));
   if (new_len) *new_len = cur + len;
   __atomic_fetch_add(&s->epoch, 1, __ATOMIC_RELEASE);
@@ -568,7 +603,7 @@ int HostStore::set_embedding(const char* key, const float* vec) {
   splinter_slot* s = slot((size_t)i);
   uint64_t e = ld(&s->epoch, __ATOMIC_RELAXED);
   if ((e & 1) || !cas64(&s->epoch, e, e + 1)) { errno = EAGAIN; return -1; }
-  std::memcpy(embedding((size_t)i), vec, kEmbedBytes);
+  seq_copy(embedding((size_t)i), vec, kEmbedBytes);
   fence_rel();
   __atomic_fetch_add(&s->epoch, 1, __ATOMIC_RELEASE);
   bump_global(1);
@@ -585,7 +620,7 @@ int HostStore::get_embedding(const char* key, float* out) {
   splinter_slot* s = slot((size_t)i);
   const uint64_t e1 = ld(&s->epoch);
   if (e1 & 1) { errno = EAGAIN; return -1; }
-  std::memcpy(out, embedding((size_t)i), kEmbedBytes);
+  seq_copy(out, embedding((size_t)i), kEmbedBytes);
   fence_acq();
   if (ld(&s->epoch) == e1) return 0;
   errno = EAGAIN;

@@ -333,7 +333,16 @@ __device__ Claim claim_set(const Arena& a, const Key& k) {
   drain();
   ast64(fs + kOffHash, k.hash);
   drain();
-  // re-validate the chain while holding the claim
+  // Re-validate the chain while holding the claim (the claim CAS + publish drains make
+  // our claim visible before these reads, so of two racing inserters at least one sees
+  // the other).  "Earlier claimant wins" alone is unsafe: the later inserter may not see
+  // the earlier claim while the earlier one sees (and ignores) the later claim -> two
+  // copies (found by the TSAN runs of the same protocol on the host store).  So:
+  //   * our key published, or a claim in flight EARLIER on the chain  -> back off;
+  //   * a claim in flight LATER on the chain that may be our key -> wait (bounded) for
+  //     it to resolve -- it never waits for us -- then judge the slot again; back off if
+  //     it is still in flight.
+  // Epoch is read BEFORE hash + key (publishers store the hash, then bump the epoch).
   idx = home;
   bool before = true;
   for (uint32_t i = 0; i < a.slots; ++i) {
@@ -341,16 +350,20 @@ __device__ Claim claim_set(const Arena& a, const Key& k) {
       before = false;
     } else {
       uint8_t* s = a.slot(idx);
-      const uint64_t sh = slot_hash(s);
-      const uint64_t e = slot_epoch(s);
-      bool conflict = false;
-      if (sh == k.hash && key_eq(s, k)) {
-        // published copy, an update in progress, or an earlier racing insert
-        conflict = !(e & 1) || before || ald32(s + kOffValLen) != kInsertMark;
-      } else if (before && (e & 1) && sh == 0) {
-        conflict = true;  // a claim whose key is not visible yet: may be ours
+      uint64_t e = slot_epoch(s);
+      drain();
+      uint64_t sh = slot_hash(s);
+      bool keq = key_eq(s, k);
+      const bool maybe_ours = sh == 0 || (sh == k.hash && keq);
+      if (!before && (e & 1) && maybe_ours) {
+        for (int t = 0; t < 64 && slot_epoch(s) == e; ++t) __builtin_amdgcn_s_sleep(8);
+        e = slot_epoch(s);
+        drain();
+        sh = slot_hash(s);
+        keq = key_eq(s, k);
       }
-      if (conflict) {
+      const bool ours = sh == k.hash && keq;
+      if (ours || ((e & 1) && sh == 0)) {
         clear_claim(a, free_idx);
         return Claim{-1, false, kAgain};
       }

@@ -227,3 +227,30 @@ def test_cross_process_attach_ipc(arena, uniq):
     assert r.returncode == 0, r.stderr[-2000:]
     st, out, ol = arena.get(pack_keys(["ipc_child"], 16))
     assert int(st[0]) == 0 and bytes(out[0, : int(ol[0])].cpu().numpy()) == b"hello from child"
+
+
+def test_racing_inserts_no_duplicates(uniq):
+    """Many lanes / two streams insert the same 512 keys concurrently (each key 128x per
+    batch): every key ends up in exactly one slot (the insert re-validation protocol)."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
+    from libsplinter_amd.parallel.sharded import GpuShard
+    a = HbmArena.create(uniq + "r", slots=4096, max_val=64, embeddings=False)
+    try:
+        ids = torch.arange(512, device="cuda").repeat(128)
+        ids = ids[torch.randperm(ids.numel(), device="cuda")]
+        K = format_keys(ids.numel(), "race", 6, 16, ids=ids)
+        V, L = format_values(ids.numel(), 1, 24, 64, ids=ids)
+        s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+        for _ in range(3):
+            with torch.cuda.stream(s1):
+                a.set(K, V, L)
+            with torch.cuda.stream(s2):
+                a.set(K.flip(0).contiguous(), V.flip(0).contiguous(), L.flip(0).contiguous())
+            torch.cuda.synchronize()
+        idx, _ = a.scan(0)
+        rows = GpuShard(a).key_rows(idx).cpu().numpy()
+        keys = [bytes(r).split(b"\0", 1)[0] for r in rows]
+        assert len(keys) == 512 and len(set(keys)) == 512
+    finally:
+        a.close()

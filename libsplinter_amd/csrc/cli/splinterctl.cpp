@@ -9,8 +9,9 @@
 //   * prefix matching of verbs ("getx" runs get), ~/.splinterrc label map,
 //     SPLINTER_NS_PREFIX / --prefix namespace, SPLINTER_DEFAULT_STORE,
 //     SPLINTER_HISTORY_FILE / _LEN
-//   * wasm and lua are compiled out (no WasmEdge / Lua 5.4 in this build;
-//     `caps` reports it), exactly like a reference build without them.
+//   * `lua` runs on minilua (Lua 5.4 subset) and `wasm` on miniwasm (MVP
+//     interpreter, binary or WAT): neither Lua 5.4 nor WasmEdge is in this
+//     image, so both hosts are built in (`caps` reports them).
 #include <algorithm>
 #include <cerrno>
 #include <chrono>
@@ -32,6 +33,7 @@
 #include <vector>
 
 #include "minilua.hpp"
+#include "miniwasm.hpp"
 #include "splinter_ext.h"
 
 #ifndef SPL_BUILD_ID
@@ -830,7 +832,7 @@ int cmd_uuid(int, char**) {
 int cmd_caps(int, char**) {
   printf("version=%s\n", SPLINTER_VERSION);
   printf("build=%s\n", SPL_BUILD_ID);
-  printf("lua=yes (minilua, Lua 5.4 subset)\nwasm=no\nembeddings=yes\nllama=no\n");
+  printf("lua=yes (minilua, Lua 5.4 subset)\nwasm=yes (miniwasm, MVP interpreter)\nembeddings=yes\nllama=no\n");
 #ifdef SYS_mbind
   printf("numa=yes\n");
 #else
@@ -1345,10 +1347,67 @@ int cmd_lua(int argc, char** argv) {
   return 0;
 }
 
-int cmd_unavailable(int, char** argv) {
-  fprintf(stderr, "%s: not compiled into this build (see `caps`)\n", argv[0]);
-  return 1;
+// `wasm` verb: the reference's WasmEdge host module (splinter_cli_cmd_wasm.c:
+// 20-77, 85-143) on the built-in interpreter.  Host functions of module
+// "splinter" (guest pointers/lengths are i32 into exported memory 0):
+//   set(key_ptr, key_len, val_ptr, val_len) -> i32   1 on success, 0 on failure (as the reference)
+//   get(key_ptr, key_len, out_ptr) -> i32            value length copied to out_ptr, -1 if absent
+//                                                    (the reference's get is a stub returning 0)
+//   unset(key_ptr, key_len) -> i32                   bytes freed, -1 if absent
+//   print(ptr, len)                                  writes guest bytes to stdout
+int cmd_wasm(int argc, char** argv) {
+  if (argc < 2) { puts("Usage: wasm <plugin.wasm|plugin.wat> [function_name]"); return 1; }
+  if (!need_store("wasm")) return 1;
+  const char* path = argv[1];
+  const std::string fn = argc > 2 ? argv[2] : "_start";
+  FILE* f = fopen(path, "rb");
+  if (!f) { fprintf(stderr, "WASM Execution failed: cannot open '%s': %s\n", path, strerror(errno)); return 1; }
+  std::vector<uint8_t> bytes;
+  uint8_t buf[65536];
+  size_t n;
+  while ((n = fread(buf, 1, sizeof buf, f)) > 0) bytes.insert(bytes.end(), buf, buf + n);
+  fclose(f);
+  using mwasm::FuncType;
+  using mwasm::I32;
+  auto key_of = [](mwasm::Instance& in, uint64_t p, uint64_t len) {
+    const uint64_t l = len < SPLINTER_KEY_MAX ? len : SPLINTER_KEY_MAX - 1;
+    return std::string((const char*)in.mem_ptr((uint32_t)p, (uint32_t)l), (size_t)l);
+  };
+  std::map<std::string, std::pair<FuncType, mwasm::HostFn>> hosts;
+  hosts["splinter.set"] = {FuncType{{I32, I32, I32, I32}, {I32}}, [&](mwasm::Instance& in, const uint64_t* a, uint64_t* r) {
+    const std::string k = key_of(in, a[0], a[1]);
+    const uint8_t* v = in.mem_ptr((uint32_t)a[2], (uint32_t)a[3]);
+    r[0] = splinter_set(k.c_str(), v, (size_t)(uint32_t)a[3]) == 0 ? 1 : 0;
+  }};
+  hosts["splinter.get"] = {FuncType{{I32, I32, I32}, {I32}}, [&](mwasm::Instance& in, const uint64_t* a, uint64_t* r) {
+    const std::string k = key_of(in, a[0], a[1]);
+    splinter_header_snapshot_t hs{};
+    splinter_get_header_snapshot(&hs);
+    std::vector<uint8_t> v((size_t)hs.max_val_sz + 1);
+    size_t len = 0;
+    if (splinter_get(k.c_str(), v.data(), v.size(), &len) != 0) { r[0] = (uint32_t)-1; return; }
+    memcpy(in.mem_ptr((uint32_t)a[2], len), v.data(), len);
+    r[0] = (uint32_t)len;
+  }};
+  hosts["splinter.unset"] = {FuncType{{I32, I32}, {I32}}, [&](mwasm::Instance& in, const uint64_t* a, uint64_t* r) {
+    r[0] = (uint32_t)splinter_unset(key_of(in, a[0], a[1]).c_str());
+  }};
+  hosts["splinter.print"] = {FuncType{{I32, I32}, {}}, [&](mwasm::Instance& in, const uint64_t* a, uint64_t*) {
+    fwrite(in.mem_ptr((uint32_t)a[0], (uint32_t)a[1]), 1, (size_t)(uint32_t)a[1], stdout);
+    fflush(stdout);
+  }};
+  try {
+    mwasm::Instance inst(mwasm::parse_any(bytes), hosts);
+    inst.step_limit = 1ull << 34;
+    if (!inst.export_type(fn).params.empty()) throw mwasm::Error("function '" + fn + "' takes arguments");
+    inst.invoke(fn);
+  } catch (const mwasm::Error& e) {
+    fprintf(stderr, "WASM Execution failed: %s\n", e.what());
+    return 1;
+  }
+  return 0;
 }
+
 
 void register_modules() {
   auto& m = modules();
@@ -1390,7 +1449,8 @@ void register_modules() {
       {"ingest", "Chunk a file or stdin into VARTEXT tandem keys.", cmd_ingest,
        [] { puts("Usage: ingest [file] [--key <key>] [--label <hex>]"); }},
       {"stats", "Store occupancy, embeddings and signal counters.", cmd_stats, nullptr},
-      {"wasm", "Run a WASM module against the store (not in this build).", cmd_unavailable, nullptr},
+      {"wasm", "Run a WASM module (binary or WAT) against the store.", cmd_wasm,
+       [] { puts("Usage: wasm <plugin.wasm|plugin.wat> [function_name]\nExecutes a WASM module with access to the Splinter bus."); }},
       {"lua", "Run a Lua script against the store (splinter module).", cmd_lua,
        [] { puts("Usage: lua <script.lua> [args...]   (require(\"splinter\"): get get_tandem set set_tandem math\n"
                  "       watch unwatch label unset bump sleep get_embedding set_embedding)"); }},

@@ -148,3 +148,77 @@ def test_cli_regression_script():
     r = subprocess.run(["bash", os.path.join(ROOT, "tests", "cli_regression.sh"), BIN], capture_output=True, text=True,
                        timeout=120)
     assert r.returncode == 0 and "not ok" not in r.stdout, r.stdout[-3000:]
+
+
+def _wasm_binary_start_module() -> bytes:
+    """Hand-assembled binary twin of the reference's test.wasm (WAT text):
+    imports splinter.set, exports memory, _start() sets __debug = 'Hello from WASM!'."""
+    def uleb(n):
+        out = bytearray()
+        while True:
+            b = n & 0x7F
+            n >>= 7
+            out.append(b | (0x80 if n else 0))
+            if not n:
+                return bytes(out)
+
+    def sec(i, body):
+        return bytes([i]) + uleb(len(body)) + body
+
+    def name(s):
+        return uleb(len(s)) + s.encode()
+
+    types = uleb(2) + b"\x60\x04\x7f\x7f\x7f\x7f\x01\x7f" + b"\x60\x00\x01\x7f"
+    imports = uleb(1) + name("splinter") + name("set") + b"\x00" + uleb(0)
+    funcs = uleb(1) + uleb(1)
+    memory = uleb(1) + b"\x00" + uleb(1)
+    exports = uleb(2) + name("memory") + b"\x02" + uleb(0) + name("_start") + b"\x00" + uleb(1)
+    body = b"\x00" + b"\x41\x00\x41\x08\x41\x10\x41\x10\x10\x00\x0b"  # no locals; i32.const x4; call 0; end
+    code = uleb(1) + uleb(len(body)) + body
+    data = uleb(2) + b"\x00\x41\x00\x0b" + name("__debug") + b"\x00\x41\x10\x0b" + name("Hello from WASM!")
+    return (b"\x00asm\x01\x00\x00\x00" + sec(1, types) + sec(2, imports) + sec(3, funcs) + sec(5, memory) +
+            sec(7, exports) + sec(10, code) + sec(11, data))
+
+
+def test_wasm_verb_reference_module_text_and_binary(store, tmp_path):
+    """The reference's own test.wasm (WAT text) and its binary twin through the built-in interpreter
+    (reference splinter_cli_cmd_wasm.c:85-143 on WasmEdge)."""
+    ref = "/root/reference/test.wasm"
+    if os.path.exists(ref):
+        rc, _, err = ctl(store, "wasm", ref)
+        assert rc == 0, err
+        assert ctl(store, "get", "__debug")[1].startswith("Hello from WASM!")
+        ctl(store, "unset", "__debug")
+    p = tmp_path / "start.wasm"
+    p.write_bytes(_wasm_binary_start_module())
+    rc, _, err = ctl(store, "wasm", str(p))
+    assert rc == 0, err
+    assert ctl(store, "get", "__debug")[1].startswith("Hello from WASM!")
+    assert "wasm=yes" in ctl(store, "caps")[1]
+
+
+def test_wasm_suite_semantics(store):
+    """Control flow, recursion, br_table, i64/f32/f64 ops, call_indirect, globals, memory.grow,
+    host get/set, and a trap: results checked against Python."""
+    import math
+    import struct
+    from libsplinter_amd import Store
+    ctl(store, "set", "src", "copied-value")
+    rc, _, err = ctl(store, "wasm", os.path.join(ROOT, "tests", "data", "wasm_suite.wat"), "run")
+    assert rc == 0, err
+    s = Store.open(store)
+    try:
+        g = s.get
+        assert struct.unpack("<q", g("fact"))[0] == math.factorial(20)
+        assert struct.unpack("<i", g("fib"))[0] == 832040
+        assert struct.unpack("<i", g("tbl"))[0] == 100 + 200 * 1000 + 300 * 1000000
+        exp = (-9 >> 1) - (1 << 63) + (2 ** 64 - 1) // 3
+        assert struct.unpack("<q", g("i64"))[0] == (exp + 2 ** 63) % 2 ** 64 - 2 ** 63
+        assert struct.unpack("<i", g("flt"))[0] == int(math.sqrt(2) * 1e6) + 2  # nearest(2.5) == 2
+        assert struct.unpack("<i", g("ind"))[0] == 13 * 42
+        assert struct.unpack("<i", g("cnt"))[0] == 5 * 100 + 3 - 1
+        assert g("echo") == b"copied-value"
+    finally:
+        s.close()
+    rc, _, err = ctl(store, "wasm", os.path.join(ROOT, "tests", "data", "wasm_suite.wat"), "trap")
+    assert rc == 1 and "integer divide by zero" in err

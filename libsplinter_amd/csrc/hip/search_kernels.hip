@@ -173,6 +173,357 @@ __global__ __launch_bounds__(256) void k_merge(const Cand* __restrict__ cand, lo
     result[(long)q * K + j] = j < n[0] ? L[0][j] : Cand{-FLT_MAX, FLT_MAX, 0xffffffffu, 0};
 }
 
+
+// ===========================================================================
+// Batched search on the matrix cores (config #5 of BASELINE: hundreds of
+// queries against a 10^7..10^8-slot arena).  Brute force is the GEMM
+// S[slots, queries] = E[slots, 768] . Q[queries, 768]^T whose A operand lives
+// in the arena as fp32 at a 3200-B slot stride; with hundreds of queries per
+// pass the fp32 FMA path above is compute-bound, so:
+//
+//   pass A (bmax): score a sample of the slots in bf16 on MFMA and keep the
+//                  per-tile max per query; the k-th largest tile max T is (up
+//                  to the bf16 error bound delta) a lower bound of the k-th
+//                  best similarity;
+//   pass B (cand): score every slot in bf16 on MFMA and emit the slots whose
+//                  approximate cosine is >= T - 2*delta;
+//   rescore:       re-score the candidates in fp32 with exactly the
+//                  arithmetic of k_score_topk and keep the top-K.
+// |cos_bf16 - cos| <= 2u + O(D u_f32) with u = 2^-8 (both operands rounded
+// once, Cauchy-Schwarz), so no true top-K slot is dropped and the result is
+// the fp32 brute force.  Queries whose candidate list overflows are redone
+// by the host with k_score_topk.
+//
+// Geometry (sized for the two bandwidth limits that matter, HBM for the
+// arena and L2->CU for the query fragments): 256 threads = 4 waves, one wave
+// per SIMD; a tile is 256 slots x 256 queries, wave w owns queries
+// [64w, 64w+64) against all 256 slots (16 x 4 tiles of
+// v_mfma_f32_16x16x32_bf16 = 256 accumulators, held in AGPRs), so the query
+// fragments cost 1.5 KB of L2 reads per slot, half the 3 KB of HBM reads.
+// The arena streams through a 4-deep LDS ring of fp32 K-chunks (256 rows x
+// 32 dims = 32 KB each) filled by buffer LDS-DMA three chunks ahead (96 KB in
+// flight per CU, no staging registers); waves read their A fragments in fp32
+// (two ds_read_b128, 16-B units XOR-swizzled by ((row>>1)&3)<<1:
+// conflict-free) and convert to bf16 in registers.  One barrier per K-chunk;
+// the DMA for chunk n+3 reuses the buffer chunk n-1 left.
+// ===========================================================================
+namespace mf {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int kTile = 256;                // slots per tile
+constexpr int kThreads = 256;             // 4 waves, one per SIMD
+constexpr int kQ = 256;                   // queries per launch (64 per wave)
+constexpr int kNJ = 4;                    // 16-query column tiles per wave
+constexpr int kSteps = kD / 32;           // 24 K-chunks of 32 dims per tile
+constexpr int kChunk = kTile * 128;       // 32 KB of fp32 per chunk
+constexpr int kRing = 4;                  // LDS ring depth (chunks)
+constexpr int kAhead = kRing - 1;         // DMA lead (chunks)
+constexpr int kDist = 3;                  // query-fragment lead (chunks), = kAhead: see SPL_STEP_SYNC
+constexpr int kDma = kChunk / 1024 / 4;   // DMA wave-instructions per wave per chunk (8)
+constexpr int kRsrcWord3 = 0x00020000;    // gfx9 raw buffer
+static_assert(kThreads == kQ, "one LDS candidate counter per thread");
+static_assert(kSteps % kRing == 0 && kSteps % (kDist + 1) == 0 && kDist == kAhead, "static ring slots across tiles");
+
+struct Smem {
+  char ring[kRing * kChunk];  // 128 KB
+  __attribute__((aligned(16))) float inv[kTile];
+  __attribute__((aligned(16))) int live[kTile];
+  uint32_t ncand[kQ];  // candidates of this block per query (LDS atomics: no vmcnt drain)
+};
+
+__device__ __forceinline__ long tile_start(long t, long slot_end) {
+  const long s = t * kTile;
+  return s + kTile <= slot_end ? s : slot_end - kTile;  // last tile shifted back: every load in bounds
+}
+
+__device__ __forceinline__ rsrc_t tile_rsrc(const spl::dev::Arena& a, long t, long slot_end) {
+  return __builtin_amdgcn_make_buffer_rsrc(a.slot((size_t)tile_start(t, slot_end)), 0, kTile * 3200, kRsrcWord3);
+}
+
+// swizzle of the 16-B units of a 128-B row: conflict-free 8-lane phases of
+// the fragment reads (rows r..r+7, same unit)
+__device__ __forceinline__ int swz(int row) { return ((row >> 1) & 3) << 1; }
+
+__device__ __forceinline__ bf16x8 load_qfrag(rsrc_t r, int voff, int qtile, int step) {
+  return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, (qtile * kSteps + step) * 1024, 0));
+}
+
+// In-order vmcnt accounting.  Every K-step issues, in this order, the query
+// fragments for 3 steps ahead (4 loads), the metadata at step 0 of a tile (2),
+// and the DMA of the chunk 3 ahead (8).  Fragments go FIRST and as far ahead
+// as the DMA, so waiting for a step's fragments never waits for a younger DMA
+// (vmcnt is in-order).  At the top of step s the ops younger than chunk s's
+// DMA (the last op of step s-3) are the two following steps: 24, or 26 when
+// one of them was a step 0; the first tile's prologue (fragments 0..2, then
+// DMA 0..2) gives lower bounds 16 at s = 0 and 22 at s = 1.  Wait + barrier
+// carry a memory clobber: no LDS read moves above them, no DMA below.
+#define SPL_STEP_SYNC(N) asm volatile("s_waitcnt vmcnt(" #N ")\n\ts_barrier" ::: "memory")
+__device__ __forceinline__ void wait_vm0() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int MODE>  // MODE 0 = per-tile max per query, 1 = emit candidates
+__global__ __launch_bounds__(kThreads, 1) void k_search_mma(spl_arena_t aa, const void* __restrict__ qf, int nq,
+                                                           long slot_begin, long slot_end, uint64_t mask,
+                                                           const float* __restrict__ thr_in, float* __restrict__ bmax,
+                                                           uint32_t* __restrict__ cnt, uint32_t* __restrict__ cand,
+                                                           int capb) {
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  const spl::dev::Arena a{(uint8_t*)aa.base, aa.slots, aa.max_val, aa.stride, aa.flags};
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const long tile_base = slot_begin / kTile;  // slot_begin tile aligned, slot_end - slot_begin >= kTile
+  const long tile_end = (slot_end + kTile - 1) / kTile, G = gridDim.x;
+  const long t0 = tile_base + blockIdx.x;
+  if (t0 >= tile_end) return;  // block-uniform
+  if (MODE == 1) sm.ncand[threadIdx.x] = 0;  // kThreads == kQ
+
+  const rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(qf), 0, kQ * kD * 2, kRsrcWord3);
+  const int qvoff = lane * 16, qtile0 = wave * kNJ;
+  // DMA geometry: wave-instruction k of a chunk fills rows 64w+8k .. +8,
+  // lane l -> row +(l>>3), physical unit l&7 <- logical unit (l&7)^swz(row)
+  int dvoff[kDma];
+#pragma unroll
+  for (int k = 0; k < kDma; ++k) {
+    const int row = wave * 64 + k * 8 + (lane >> 3);
+    dvoff[k] = row * 3200 + (((lane & 7) ^ swz(row)) << 4);
+  }
+  // fragment read: row 16i+fr, logical units 2fq, 2fq+1 (swz(16i+fr) == swz(fr))
+  const int rd0 = fr * 128 + (((2 * fq) ^ swz(fr)) << 4), rd1 = fr * 128 + (((2 * fq + 1) ^ swz(fr)) << 4);
+  // ds_read immediates are 16-bit: ring slots 0,1 address off `lo`, slots 2,3
+  // off `hi` (= lo + 64 KB, opaque so the compiler keeps 4 base VGPRs instead
+  // of materialising 32 out-of-range offsets)
+  int lo0 = rd0, lo1 = rd1, hi0 = rd0 + 2 * kChunk, hi1 = rd1 + 2 * kChunk;
+  asm volatile("" : "+v"(hi0), "+v"(hi1));
+
+  float thr[kNJ];
+#pragma unroll
+  for (int j = 0; j < kNJ; ++j) {
+    const int q = (qtile0 + j) * 16 + fr;
+    thr[j] = (MODE == 1 && q < nq) ? thr_in[q] : FLT_MAX;
+  }
+
+  // DMA of chunk c of the tile behind `er` into ring buffer `slot`
+  auto issue = [&](rsrc_t er, int c, int slot) {
+    char* dst = sm.ring + slot * kChunk + wave * 64 * 128;
+#pragma unroll
+    for (int k = 0; k < kDma; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(er, (lds_void*)(dst + k * 1024), 16, dvoff[k],
+                                               (int)spl::kOffEmbed + c * 128, 0, 0);
+  };
+  const long last = tile_end - 1;
+
+  // prologue: query fragments of steps 0..2, then the DMA of chunks 0..2 of the first tile
+  bf16x8 b[kDist + 1][kNJ];
+#pragma unroll
+  for (int s = 0; s < kDist; ++s)
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) b[s][j] = load_qfrag(qr, qvoff, qtile0 + j, s);
+  {
+    const rsrc_t er = tile_rsrc(a, t0, slot_end);
+    for (int c = 0; c < kAhead; ++c) issue(er, c, c);
+  }
+
+  for (long t = t0; t < tile_end; t += G) {
+    const long start = tile_start(t, slot_end);
+    // the stream runs one tile ahead at the end of a tile (the last tile re-reads itself: in bounds, unused)
+    const rsrc_t er_cur = tile_rsrc(a, t, slot_end);
+    const rsrc_t er_next = tile_rsrc(a, t + G < tile_end ? t + G : last, slot_end);
+    uint64_t h = 0, bl = 0;
+    f32x4 acc[16][kNJ];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float ss[4] = {0.f, 0.f, 0.f, 0.f};  // squared norms of this wave's rows 16*(4w+k)+fr, this lane's dims
+
+#pragma clang loop unroll(full)
+    for (int s = 0; s < kSteps; ++s) {
+      // chunk s landed (this wave's DMA) and, after the barrier, every wave's
+      // DMA landed and every wave is done with chunk s-1's ring buffer
+      if (s == 0)
+        SPL_STEP_SYNC(16);
+      else if (s == 1)
+        SPL_STEP_SYNC(22);
+      else if (s == 2)
+        SPL_STEP_SYNC(26);
+      else
+        SPL_STEP_SYNC(24);
+      // query fragments are periodic in the step: the ring runs across tiles
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j)
+        b[(s + kDist) % (kDist + 1)][j] = load_qfrag(qr, qvoff, qtile0 + j, (s + kDist) % kSteps);
+      if (s == 0) {  // metadata of this wave's 64 rows, one per lane
+        const uint8_t* sp = a.slot((size_t)(start + wave * 64 + lane));
+        h = __builtin_nontemporal_load((const uint64_t*)(sp + spl::kOffHash));
+        bl = __builtin_nontemporal_load((const uint64_t*)(sp + spl::kOffBloom));
+      }
+      issue(s + kAhead < kSteps ? er_cur : er_next, (s + kAhead) % kSteps, (s + kAhead) % kRing);
+      const int slot = s % kRing;
+      const char* ch0 = sm.ring + (slot < 2 ? lo0 : hi0) + (slot & 1) * kChunk;
+      const char* ch1 = sm.ring + (slot < 2 ? lo1 : hi1) + (slot & 1) * kChunk;
+#pragma unroll
+      for (int i0 = 0; i0 < 16; i0 += 4) {  // 4 row tiles at a time: bounded fragment registers
+        f32x4 lo[4], hi[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          lo[u] = *(const f32x4*)(ch0 + (i0 + u) * 2048);
+          hi[u] = *(const f32x4*)(ch1 + (i0 + u) * 2048);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int i = i0 + u;
+          if ((i >> 2) == wave) {  // this wave's rows: norms from the same registers (wave-uniform)
+            ss[u] += lo[u].x * lo[u].x + lo[u].y * lo[u].y + lo[u].z * lo[u].z + lo[u].w * lo[u].w +
+                     hi[u].x * hi[u].x + hi[u].y * hi[u].y + hi[u].z * hi[u].z + hi[u].w * hi[u].w;
+          }
+          const bf16x8 af = {(__bf16)lo[u].x, (__bf16)lo[u].y, (__bf16)lo[u].z, (__bf16)lo[u].w,
+                             (__bf16)hi[u].x, (__bf16)hi[u].y, (__bf16)hi[u].z, (__bf16)hi[u].w};
+#pragma unroll
+          for (int j = 0; j < kNJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, b[s % (kDist + 1)][j], acc[i][j], 0, 0, 0);
+        }
+      }
+    }
+    // norms + liveness of this wave's 64 rows: lane r -> row 64w + r = 16(4w + fq) + fr
+    {
+      float sel = fq == 0 ? ss[0] : fq == 1 ? ss[1] : fq == 2 ? ss[2] : ss[3];
+      // the four fq lanes of a row hold disjoint dims: sum them
+      float tot[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        float v = ss[k];
+        v += __shfl_xor(v, 16, 64);
+        v += __shfl_xor(v, 32, 64);
+        tot[k] = v;
+      }
+      sel = fq == 0 ? tot[0] : fq == 1 ? tot[1] : fq == 2 ? tot[2] : tot[3];
+      constexpr float kMinNorm2 = MODE == 0 ? 2e-12f : 0.f;  // MODE 0 counts surely-live slots only
+      const int row = wave * 64 + lane;
+      sm.live[row] = h != 0 && (!mask || (bl & mask) == mask) && sel > kMinNorm2 && start + row >= t * kTile;
+      sm.inv[row] = sel > 0.f ? rsqrtf(sel) : 0.f;
+    }
+    raw_barrier();
+    {
+      const f32x4* invp = (const f32x4*)(sm.inv + fq * 4);  // rows 16i + 4fq + r, r = 0..3
+      const int4* livp = (const int4*)(sm.live + fq * 4);
+      float best[kNJ];
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j) best[j] = -FLT_MAX;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const f32x4 iv = invp[i * 4];
+        const int4 lv = livp[i * 4];
+        const int lvr[4] = {lv.x, lv.y, lv.z, lv.w};
+#pragma unroll
+        for (int j = 0; j < kNJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sim = acc[i][j][r] * iv[r];
+            if (MODE == 0) {
+              if (lvr[r]) best[j] = fmaxf(best[j], sim);
+            } else if (sim >= thr[j] && lvr[r]) {
+              // block-private segment [q][block][capb]: the slot index comes
+              // from an LDS counter, the global write needs no return value
+              const int q = (qtile0 + j) * 16 + fr;
+              const uint32_t p = atomicAdd(&sm.ncand[q], 1u);
+              if (p < (uint32_t)capb) cand[((long)q * gridDim.x + blockIdx.x) * capb + p] = (uint32_t)(start + i * 16 + fq * 4 + r);
+            }
+          }
+      }
+      if (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < kNJ; ++j) {
+          const int q = (qtile0 + j) * 16 + fr;
+          float bj = fmaxf(best[j], __shfl_xor(best[j], 16, 64));
+          bj = fmaxf(bj, __shfl_xor(bj, 32, 64));
+          if (fq == 0 && q < nq) bmax[(t - tile_base) * nq + q] = bj;
+        }
+      }
+    }
+  }
+  if (MODE == 1) {
+    raw_barrier();
+    const int q = threadIdx.x;
+    if (q < nq) cnt[(long)q * gridDim.x + blockIdx.x] = sm.ncand[q];
+  }
+  wait_vm0();  // drain the trailing DMAs (next-tile prefetch of the last tile) before the LDS goes away
+}
+
+// fp32 re-score of the candidates of one query (block) and top-K selection;
+// same arithmetic as k_score_topk so the ranking is identical.  Candidates
+// come in block-private segments cand[q][b][0 .. min(cnt[q][b], capb)).
+__global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __restrict__ queries, int K,
+                                                 float min_sim, float max_dist, uint64_t mask,
+                                                 const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ cand,
+                                                 int nblk, int capb, Cand* __restrict__ result) {
+  __shared__ __attribute__((aligned(16))) float Qs[kD];
+  __shared__ float qn_s;
+  __shared__ Cand top[kWaves][kMaxK];
+  __shared__ int tc[kWaves];
+  const spl::dev::Arena a{(uint8_t*)aa.base, aa.slots, aa.max_val, aa.stride, aa.flags};
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int i = tid; i < kD; i += 256) Qs[i] = queries[(long)q * kD + i];
+  if (tid < kWaves) tc[tid] = 0;
+  __syncthreads();
+  if (tid == 0) {
+    float s = 0.f;
+    for (int d = 0; d < kD; ++d) s += Qs[d] * Qs[d];
+    qn_s = s;
+  }
+  __syncthreads();
+  const float qn = qn_s;
+  int c = 0;
+  for (int b = wave; b < nblk; b += kWaves) {
+    const int n = min(cnt[(long)q * nblk + b], (uint32_t)capb);
+    const uint32_t* seg = cand + ((long)q * nblk + b) * capb;
+    for (int t = 0; t < n; ++t) {
+      const uint32_t idx = seg[t];
+      const uint8_t* s = a.slot(idx);
+      const uint64_t h = *(const uint64_t*)(s + spl::kOffHash);
+      if (h == 0 || (mask && (*(const uint64_t*)(s + spl::kOffBloom) & mask) != mask)) continue;
+      const float4* v4 = (const float4*)(s + spl::kOffEmbed);
+      float4 e[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) e[k] = v4[lane + 64 * k];
+      float en = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) en += e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z + e[k].w * e[k].w;
+      en = wave_sum(en);
+      if (en < 1e-12f) continue;
+      const float enr = sqrtf(en);
+      const float4* q4 = (const float4*)Qs;
+      float dot = 0.f;
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const float4 qq = q4[lane + 64 * k];
+        dot += e[k].x * qq.x + e[k].y * qq.y + e[k].z * qq.z + e[k].w * qq.w;
+      }
+      dot = wave_sum(dot);
+      const float sim = dot / (enr * sqrtf(qn) + 1e-30f);
+      const float dist = sqrtf(fmaxf(en + qn - 2.f * dot, 0.f));
+      if (sim < min_sim || dist > max_dist) continue;
+      if (lane == 0) c = insert(top[wave], c, K, Cand{sim, dist, idx, 0});
+    }
+  }
+  if (lane == 0) tc[wave] = c;
+  __syncthreads();
+  if (tid == 0) {
+    Cand L[kMaxK];
+    int m = 0;
+    for (int w = 0; w < kWaves; ++w)
+      for (int j = 0; j < tc[w]; ++j) m = insert(L, m, K, top[w][j]);
+    for (int j = 0; j < K; ++j) result[(long)q * K + j] = j < m ? L[j] : Cand{-FLT_MAX, FLT_MAX, 0xffffffffu, 0};
+  }
+}
+}  // namespace mf
+
 }  // namespace
 
 extern "C" {
@@ -190,6 +541,39 @@ int spl_search(spl_arena_t a, const float* queries, int nq, int K, float min_sim
                      (Cand*)scratch);
   hipLaunchKernelGGL(k_merge, dim3(nq), dim3(256), 0, s, (const Cand*)scratch, (long)grid * kWaves, nq, K,
                      (Cand*)result);
+  return (int)hipGetLastError();
+}
+
+int spl_search_mma_queries() { return mf::kQ; }
+int spl_search_mma_tile() { return mf::kTile; }
+
+int spl_search_mma_pass(spl_arena_t a, const void* qfrag, int nq, long slot_begin, long slot_end, uint64_t mask,
+                        int mode, const float* thr, float* bmax, uint32_t* cnt, uint32_t* cand, int capb, int grid,
+                        hipStream_t s) {
+  if (a.stride != 3200 || nq <= 0 || nq > mf::kQ || slot_begin < 0 || slot_begin % mf::kTile ||
+      slot_end > (long)a.slots || slot_end - slot_begin < mf::kTile || (mode != 0 && mode != 1) || grid <= 0 ||
+      (mode == 1 && (!thr || !cnt || !cand || capb <= 0)) || (mode == 0 && !bmax))
+    return (int)hipErrorInvalidValue;
+  const long tiles = (slot_end - slot_begin + mf::kTile - 1) / mf::kTile;
+  if (mode == 0) {
+    const int g = (int)(grid < tiles ? grid : tiles);
+    hipLaunchKernelGGL(mf::k_search_mma<0>, dim3(g), dim3(mf::kThreads), 0, s, a, qfrag, nq, slot_begin, slot_end,
+                       mask, thr, bmax, cnt, cand, capb);
+  } else {
+    // every one of the `grid` segments per query must be written: no clamping to the tile count
+    // (blocks without a tile store a zero count)
+    hipLaunchKernelGGL(mf::k_search_mma<1>, dim3(grid), dim3(mf::kThreads), 0, s, a, qfrag, nq, slot_begin, slot_end,
+                       mask, thr, bmax, cnt, cand, capb);
+  }
+  return (int)hipGetLastError();
+}
+
+int spl_search_rescore(spl_arena_t a, const float* queries, int nq, int K, float min_sim, float max_dist,
+                       uint64_t mask, const uint32_t* cnt, const uint32_t* cand, int nblk, int capb, void* result,
+                       hipStream_t s) {
+  if (a.stride != 3200 || nq <= 0 || K <= 0 || K > kMaxK || nblk <= 0 || capb <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(mf::k_rescore, dim3(nq), dim3(256), 0, s, a, queries, K, min_sim, max_dist, mask, cnt, cand,
+                     nblk, capb, (Cand*)result);
   return (int)hipGetLastError();
 }
 

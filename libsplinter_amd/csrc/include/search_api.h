@@ -16,6 +16,25 @@ int spl_search_lists(int grid);
 int spl_search(spl_arena_t a, const float *queries, int nq, int K, float min_sim, float max_dist, uint64_t mask,
                int grid, void *scratch, void *result, hipStream_t stream);
 
+/* Batched MFMA search (many queries).  qfrag: queries L2-normalised, bf16, zero-padded to 256
+ * queries and permuted to fragment order [16 tiles][24 steps][64 lanes] x 16 B, where lane =
+ * 16*kq + r holds query (16*tile + r), dims [32*step + 8*kq, +8).  Scores slots
+ * [slot_begin, slot_end) (slot_begin a multiple of spl_search_mma_tile(), at least one tile).
+ * mode 0: bmax[tile - slot_begin/256][nq] = max approximate cosine per 256-slot tile and query
+ * (-FLT_MAX if no live slot); mode 1: `grid` blocks, each appends the live slots of its tiles
+ * with approximate cosine >= thr[q] to its private segment cand[q][block][0..capb) and stores
+ * the segment's count (may exceed capb: overflow) in cnt[q][block].  cnt must be zeroed first. */
+int spl_search_mma_queries(void);
+int spl_search_mma_tile(void);
+int spl_search_mma_pass(spl_arena_t a, const void *qfrag, int nq, long slot_begin, long slot_end, uint64_t mask,
+                        int mode, const float *thr, float *bmax, uint32_t *cnt, uint32_t *cand, int capb, int grid,
+                        hipStream_t stream);
+/* Exact fp32 re-score of the candidate segments (queries [nq, 768] fp32, unnormalised) and top-K:
+ * result layout and ranking as spl_search. */
+int spl_search_rescore(spl_arena_t a, const float *queries, int nq, int K, float min_sim, float max_dist,
+                       uint64_t mask, const uint32_t *cnt, const uint32_t *cand, int nblk, int capb, void *result,
+                       hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

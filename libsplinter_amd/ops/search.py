@@ -16,6 +16,12 @@ import torch
 from .. import _native as N
 
 MAX_Q, MAX_K = 16, 32
+MMA_Q = 256          # queries per MFMA launch
+TILE = 256           # slots per MFMA tile
+MMA_GRID = 256       # persistent blocks of the MFMA pass (one per CU); candidate segments per query
+# |cos_bf16 - cos| <= 2u + u^2 (u = 2^-8: both operands rounded once to bf16,
+# Cauchy-Schwarz over the 768 products) plus fp32 accumulation / norm error
+DELTA = 2.0 ** -7 + 2.0 ** -16 + 4e-4
 
 
 def _lib():
@@ -27,6 +33,12 @@ def _lib():
         L.spl_search.restype = ctypes.c_int
         L.spl_search_lists.argtypes = [ctypes.c_int]
         L.spl_search_lists.restype = ctypes.c_int
+        L.spl_search_mma_pass.argtypes = [N.Arena, P, ctypes.c_int, ctypes.c_long, ctypes.c_long, ctypes.c_uint64,
+                                          ctypes.c_int, P, P, P, P, ctypes.c_int, ctypes.c_int, P]
+        L.spl_search_mma_pass.restype = ctypes.c_int
+        L.spl_search_rescore.argtypes = [N.Arena, P, ctypes.c_int, ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                         ctypes.c_uint64, P, P, ctypes.c_int, ctypes.c_int, P, P]
+        L.spl_search_rescore.restype = ctypes.c_int
         L._search_declared = True
     return L
 
@@ -65,6 +77,83 @@ class VectorSearch:
             outs_i.append(idx)
             outs_s.append(r[..., 0].view(torch.float32).clone())
             outs_d.append(r[..., 1].view(torch.float32).clone())
+        return torch.cat(outs_i), torch.cat(outs_s), torch.cat(outs_d)
+
+    def search_batch(self, queries: torch.Tensor, k: int = 10, min_sim: float = -2.0, max_dist: float = 3.4e38,
+                     label_mask: int = 0, capb: int = 64, sample: Optional[int] = None, stats: Optional[dict] = None
+                     ) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Many-query search on the matrix cores; same results as `search` (exact fp32 ranking).
+
+        Per launch of up to 512 queries: a bf16 MFMA pass over a slot sample gives a per-query
+        threshold (k-th largest per-tile max - 2*DELTA), a bf16 MFMA pass over the arena emits
+        candidates above it, and a fp32 re-score with the exact kernel's arithmetic ranks them.
+        Each of the MMA_GRID blocks keeps up to `capb` candidates per query; a query whose
+        segment overflows anywhere is redone with the exact kernel.
+        """
+        q = queries.to(device="cuda", dtype=torch.float32).reshape(-1, 768).contiguous()
+        slots = self.arena.slots
+        if not 1 <= k <= MAX_K:
+            raise ValueError(f"k must be 1..{MAX_K}")
+        if q.shape[0] < 32 or slots < TILE:
+            return self.search(q, k, min_sim, max_dist, label_mask)
+        st = torch.cuda.current_stream().cuda_stream
+        if sample is None:
+            sample = min(slots, max(TILE * 4096, slots // 16))
+        sample = max(TILE, sample // TILE * TILE)
+        bounded = max_dist < 3.0e38
+        outs_i, outs_s, outs_d = [], [], []
+        nover = ncand = 0
+        for b in range(0, q.shape[0], MMA_Q):
+            qq = q[b: b + MMA_Q]
+            n = qq.shape[0]
+            qpad = MMA_Q
+            qb = torch.zeros(qpad, 768, dtype=torch.bfloat16, device="cuda")
+            qb[:n] = (qq / qq.norm(dim=1, keepdim=True).clamp_min(1e-30)).to(torch.bfloat16)
+            # fragment order [q/16][24 steps][4 kq][16 r][8]: lane 16*kq + r of a wave load
+            qf = qb.view(qpad // 16, 16, 24, 4, 8).permute(0, 2, 3, 1, 4).contiguous()
+            floor = torch.full((n,), float(min_sim) - DELTA, device="cuda")
+            if bounded:
+                thr = floor
+            else:
+                bmax = torch.empty(sample // TILE, n, dtype=torch.float32, device="cuda")
+                rc = self.L.spl_search_mma_pass(self.arena.desc, qf.data_ptr(), n, 0, sample, label_mask, 0, None,
+                                                bmax.data_ptr(), None, None, 0, MMA_GRID, st)
+                if rc != 0:
+                    raise RuntimeError(f"spl_search_mma_pass(bmax) failed ({rc})")
+                kk = min(k, bmax.shape[0])
+                kth = bmax.topk(kk, dim=0).values[-1]
+                if kk < k:
+                    kth = torch.full_like(kth, -3.0e38)
+                thr = torch.maximum(kth - 2 * DELTA, floor)
+            cnt = torch.zeros(n, MMA_GRID, dtype=torch.int32, device="cuda")
+            cand = torch.empty(n * MMA_GRID * capb, dtype=torch.int32, device="cuda")
+            rc = self.L.spl_search_mma_pass(self.arena.desc, qf.data_ptr(), n, 0, slots, label_mask, 1,
+                                            thr.data_ptr(), None, cnt.data_ptr(), cand.data_ptr(), capb, MMA_GRID, st)
+            if rc != 0:
+                raise RuntimeError(f"spl_search_mma_pass(cand) failed ({rc})")
+            res = torch.empty(n * k * 4, dtype=torch.int32, device="cuda")
+            rc = self.L.spl_search_rescore(self.arena.desc, qq.data_ptr(), n, k, float(min_sim), float(max_dist),
+                                           label_mask, cnt.data_ptr(), cand.data_ptr(), MMA_GRID, capb,
+                                           res.data_ptr(), st)
+            if rc != 0:
+                raise RuntimeError(f"spl_search_rescore failed ({rc})")
+            r = res.view(n, k, 4)
+            idx = r[..., 2].to(torch.int64) & 0xFFFFFFFF
+            idx = torch.where(idx == 0xFFFFFFFF, torch.full_like(idx, -1), idx)
+            sim = r[..., 0].view(torch.float32).clone()
+            dist = r[..., 1].view(torch.float32).clone()
+            over = torch.nonzero((cnt > capb).any(dim=1)).flatten()
+            if over.numel():
+                oi, osim, od = self.search(qq[over], k, min_sim, max_dist, label_mask)
+                idx[over], sim[over], dist[over] = oi, osim, od
+            if stats is not None:
+                nover += int(over.numel())
+                ncand += int(cnt.clamp_max(capb).sum())
+            outs_i.append(idx)
+            outs_s.append(sim)
+            outs_d.append(dist)
+        if stats is not None:
+            stats.update(overflow=nover, candidates=ncand, sample=sample)
         return torch.cat(outs_i), torch.cat(outs_s), torch.cat(outs_d)
 
     def keys_of(self, idx: torch.Tensor) -> List[List[Optional[str]]]:

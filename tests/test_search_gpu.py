@@ -73,3 +73,47 @@ def test_splinference_daemon_oneshot(uniq):
     finally:
         s.close()
         unlink(uniq)
+
+
+def _clustered(n, g, centers=64, noise=0.35):
+    import torch
+    c = torch.randn(centers, 768, generator=g)
+    lab = torch.randint(0, centers, (n,), generator=g)
+    return c[lab] + noise * torch.randn(n, 768, generator=g)
+
+
+@pytest.mark.parametrize("nq", [40, 300])
+def test_search_batch_matches_exact(uniq, nq):
+    """MFMA batched search (bf16 threshold passes + fp32 re-score) == exact fp32 kernel,
+    including a partial last tile, un-embedded slots, label mask, min-sim and max-dist."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, pack_keys, pack_values
+    from libsplinter_amd.ops.search import VectorSearch
+    a = HbmArena.create(uniq, slots=20011, max_val=32, embeddings=True)
+    try:
+        n = 15000
+        K = pack_keys([f"e{i}" for i in range(n)], 16)
+        V, L = pack_values([b"x"] * n, 16)
+        assert (a.set(K, V, L) == 0).all()
+        g = torch.Generator().manual_seed(1)
+        vecs = _clustered(n, g)
+        vecs[11] = 0
+        vecs[12] = 1e-8  # below the exact kernel's norm floor
+        assert (a.set_embeddings(K, vecs.cuda()) == 0).all()
+        a.meta("set_label", K[::3], torch.full((len(range(0, n, 3)),), 1 << 5, dtype=torch.int64, device="cuda"))
+        q = _clustered(nq, g) * 3.0
+        q[0] = vecs[100]
+        vs = VectorSearch(a, grid=128)
+        st = {}
+        for kw in ({}, {"label_mask": 1 << 5}, {"min_sim": 0.6}, {"max_dist": 30.0}):
+            i1, s1, d1 = vs.search_batch(q, k=10, stats=st, **kw)
+            i0, s0, d0 = vs.search(q, k=10, **kw)
+            assert torch.equal(i1, i0), kw
+            assert torch.equal(s1, s0) and torch.equal(d1, d0), kw
+            if "max_dist" not in kw:  # bounded distance: no sample threshold, every slot is a candidate
+                assert st["overflow"] == 0 and st["candidates"] < nq * 2000, (kw, st)
+        # tiny candidate cap: every query overflows and falls back to the exact kernel
+        i2, _, _ = vs.search_batch(q, k=10, capb=1, stats=st)
+        assert torch.equal(i2, vs.search(q, k=10)[0]) and st["overflow"] > 0
+    finally:
+        a.close()

@@ -368,7 +368,10 @@ class GpuShard:
         from ..ops.search import VectorSearch
         if self._search is None:
             self._search = VectorSearch(self.arena, grid=self._grid)
-        idx, sim, dst = self._search.search(q, k, min_sim, max_dist, label_mask)
+        # many queries: the batched MFMA path (bf16 threshold passes + exact fp32 re-score,
+        # same ranking); a handful: the exact fp32 kernel
+        fn = self._search.search_batch if q.shape[0] >= 32 else self._search.search
+        idx, sim, dst = fn(q, k, min_sim, max_dist, label_mask)
         valid = idx >= 0
         rows = self.key_rows(torch.where(valid, idx, torch.zeros_like(idx)).reshape(-1))
         rows = rows.reshape(idx.shape[0], idx.shape[1], KEY_BYTES) * valid.unsqueeze(-1).to(torch.uint8)

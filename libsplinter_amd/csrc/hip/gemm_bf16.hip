@@ -62,13 +62,18 @@ __device__ __forceinline__ bf16x8 lds_frag(const char* tile, int r, int c) {
   return *(const bf16x8*)(tile + r * 128 + ((c ^ (r & 7)) << 4));
 }
 
-__device__ __forceinline__ void remap_tile(int bid, int nb, int nt, int& mt, int& ntile) {
+__device__ __forceinline__ void remap_tile(int bid, int nb, int nt, int gn, int& mt, int& ntile) {
   // bijective XCD remap: blocks b and b+8 share an XCD; give each XCD a
-  // contiguous range of tiles (tiles sharing A rows are adjacent in n).
+  // contiguous range of the linear tile order.  The linear order is
+  // band-major: bands of `gn` n-tiles, m-major inside a band, so the ~32
+  // tiles an XCD runs at once cover (32/gn) A row-blocks x gn W column-blocks
+  // and both fit its 4 MB L2 (gn = nt: plain row-major).
   const int xcd = bid & 7, q = nb >> 3, r = nb & 7;
   const int wg = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  mt = wg / nt;
-  ntile = wg - mt * nt;
+  const int per_band = (nb / nt) * gn;
+  const int band = wg / per_band, rem = wg - band * per_band;
+  mt = rem / gn;
+  ntile = band * gn + (rem - mt * gn);
 }
 
 struct EpiArgs {
@@ -80,6 +85,7 @@ struct EpiArgs {
   const int32_t* pos;    // [M] position of each row (mode 3)
   int rope_cols;         // columns (from 0) that get RoPE (q|k = 1536)
   long M;
+  int gn;                // n-tiles per band of the tile order (remap_tile)
 };
 
 template <int MODE>
@@ -89,7 +95,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   int mt, nt;
-  remap_tile(blockIdx.x, mtiles * ntiles, ntiles, mt, nt);
+  remap_tile(blockIdx.x, mtiles * ntiles, ntiles, ep.gn, mt, nt);
   const long m0 = (long)mt * BM, n0 = (long)nt * BN;
   const int wm = wave >> 1, wn = wave & 1;
 
@@ -305,7 +311,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wn = wave & 3;
   int mt, nt;
-  remap_tile(blockIdx.x, mtiles * ntiles, ntiles, mt, nt);
+  remap_tile(blockIdx.x, mtiles * ntiles, ntiles, ep.gn, mt, nt);
   const long m0 = (long)mt * 256, n0 = (long)nt * 256;
 
   // per-lane DMA source offsets (elements): half h, instruction i -> 8-row block (i*8 + wave)
@@ -539,8 +545,22 @@ int gemm_variant() {
   return g_variant;
 }
 
+// band width of the tile order: the largest divisor of ntiles <= cap (NOMIC_GEMM_GN overrides;
+// 0 = row-major)
+int band_width(int ntiles, int cap) {
+  static const int env = [] {
+    const char* v = getenv("NOMIC_GEMM_GN");
+    return v && *v ? atoi(v) : -1;
+  }();
+  if (env == 0) return ntiles;
+  if (env > 0) cap = env;
+  for (int g = cap < ntiles ? cap : ntiles; g > 1; --g)
+    if (ntiles % g == 0) return g;
+  return 1;
+}
+
 template <int MODE>
-int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int N, int K, const EpiArgs& ep,
+int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int N, int K, EpiArgs ep,
            hipStream_t s) {
   if (K % BK || N % BN || M <= 0) return (int)hipErrorInvalidValue;
   const long mpad = (M + 255) / 256 * 256;
@@ -555,11 +575,13 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     }();
     (void)attr;
     const int mtiles = (int)(mpad / 256), ntiles = N / 256;
+    ep.gn = band_width(ntiles, 4);
     hipLaunchKernelGGL(k_gemm256<MODE>, dim3(mtiles * ntiles), dim3(kThreads2), kLds2Bytes, s, A, lda, W, ldw, K,
                        mtiles, ntiles, ep);
     return (int)hipGetLastError();
   }
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = N / BN;
+  ep.gn = band_width(ntiles, 8);
   hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), kLdsBytes, s, A, lda, W, ldw, K, mtiles,
                      ntiles, ep);
   return (int)hipGetLastError();
@@ -576,7 +598,7 @@ extern "C" int nomic_gemm_set_variant(int variant) {
 extern "C" int nomic_gemm(int mode, const void* A, long lda, const void* W, long ldw, long M, int N, int K, void* out,
                           long ldo, const void* res, long ldr, const float* rope, const int32_t* pos, int rope_cols,
                           hipStream_t s) {
-  EpiArgs ep{(uint16_t*)out, ldo, (const uint16_t*)res, ldr, rope, pos, rope_cols, M};
+  EpiArgs ep{(uint16_t*)out, ldo, (const uint16_t*)res, ldr, rope, pos, rope_cols, M, 1};
   const auto* a = (const uint16_t*)A;
   const auto* w = (const uint16_t*)W;
   switch (mode) {

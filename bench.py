@@ -80,9 +80,13 @@ def main():
     arena = HbmArena.create(name, slots=slots, max_val=args.max_val, embeddings=False)
     arena.store.set_mop(0)  # throughput mode: no scrubbing (reference stress default)
     kv = ShardedKV(GpuShard(arena))
-    # gets route over a second communicator so the set and get all-to-alls (and their kernels)
-    # overlap on their own streams instead of serialising on one RCCL stream
-    kv_get = ShardedKV(GpuShard(arena), group=dist.new_group(backend=args.backend)) if world > 1 else kv
+    rkv = None
+    if world > 1:
+        # request and response all-to-alls on their own communicators (= their own RCCL streams):
+        # step i's responses and step i+1's requests are in flight together
+        from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
+        rkv = RoutedKV(GpuShard(arena), group=dist.new_group(backend=args.backend),
+                       resp_group=dist.new_group(backend=args.backend))
     vstride = (args.max_val + 15) // 16 * 16
 
     # ---- prepopulate: every rank inserts the global ids it owns ----------
@@ -139,26 +143,70 @@ def main():
     s_get, s_set = hip_stream("high"), hip_stream("normal")
     stats = arena.stats
 
-    def step(i):
+    def step_local(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
         cur = torch.cuda.current_stream()
         if n_set:
             s_set.wait_stream(cur)
             s_get.wait_stream(cur)
-            if world == 1:
-                with torch.cuda.stream(s_set):
-                    arena.set(SK, SV, SL)
-                with torch.cuda.stream(s_get):
-                    arena.get(GK, out=gout)
-            else:
-                with torch.cuda.stream(s_set):
-                    kv.set(SK, SV, SL)
-                with torch.cuda.stream(s_get):
-                    kv_get.get(GK)
+            with torch.cuda.stream(s_set):
+                arena.set(SK, SV, SL)
+            with torch.cuda.stream(s_get):
+                arena.get(GK, out=gout)
             cur.wait_stream(s_set)
             cur.wait_stream(s_get)
         if embedder is not None:
             embedder.run()
+
+    # N > 1: a host-sync-free software pipeline (parallel/routed.py).  Per step i:
+    #   s_req : pack + request all-to-alls of batch i         (overlaps embed_i)
+    #   main  : embed_i, after the owner kernels of batch i-1  (no seqlock kernels beside the GEMMs)
+    #   s_set / s_get : owner kernels of batch i, after its requests and embed_i
+    #   s_resp: response all-to-alls + gather of batch i       (overlaps embed_{i+1})
+    # All K steps' responses are delivered inside the timed region (device-wide sync at the end).
+    if world > 1:
+        cap_s, cap_g = route_capacity(max(n_set, 1), world), route_capacity(max(n_get, 1), world)
+        vw = min((args.value_len + 15) // 16 * 16, vstride)
+        s_req, s_resp = hip_stream("low"), hip_stream("low")
+        gouts = [torch.empty((n_get, vw), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        prev_exec = []
+
+    def step_routed(i):
+        SK, SV, SL, GK, _ = batches[i % nbuf]
+        cur = torch.cuda.current_stream()
+        so = go = None
+        with torch.cuda.stream(s_req):
+            if n_set:
+                so = rkv.begin_set(SK, SV, SL, cap_s, vw)
+            if n_get:
+                go = rkv.begin_get(GK, cap_g, vw)
+            ev_req = s_req.record_event()
+        if embedder is not None:
+            for e in prev_exec:
+                cur.wait_event(e)
+            embedder.run()
+        ev_emb = cur.record_event()
+        prev_exec.clear()
+        for s, op in ((s_set, so), (s_get, go)):
+            if op is None:
+                continue
+            s.wait_event(ev_req)
+            s.wait_event(ev_emb)
+            with torch.cuda.stream(s):
+                rkv.execute(op)
+                prev_exec.append(s.record_event())
+        for e in prev_exec:
+            s_resp.wait_event(e)
+        with torch.cuda.stream(s_resp):
+            for op in (so, go):
+                if op is not None:
+                    rkv.respond(op)
+            if so is not None:
+                rkv.finish(so)
+            if go is not None:
+                rkv.finish(go, out=gouts[i % 2])
+
+    step = step_local if world == 1 else step_routed
 
     for i in range(args.warmup):
         step(i)
@@ -188,7 +236,7 @@ def main():
         GK, gid = batches[0][3], batches[0][4]
         m = min(args.verify, n_get)
         if world > 1:
-            sts, outv, lens = kv_get.get(GK[:m])
+            sts, outv, lens = kv.get(GK[:m])
         else:
             sts, outv, lens = arena.get(GK[:m])
         o, ln, ids, s_ = outv.cpu().numpy(), lens.cpu().numpy(), gid[:m].cpu().numpy(), sts.cpu().numpy()

@@ -177,6 +177,10 @@ def _declare_hip(L):
     _sig(L, "spl_arena_init_slots", c_int, A, P)
     _sig(L, "spl_arena_set", c_int, A, P, c_int, P, c_int, P, c_long, P, c_int, P, P)
     _sig(L, "spl_arena_get", c_int, A, P, c_int, P, c_int, P, c_long, P, c_int, P, P)
+    _sig(L, "spl_arena_set_seg", c_int, A, P, c_int, P, c_int, P, c_long, P, c_int, P, P, c_long, P)
+    _sig(L, "spl_arena_get_seg", c_int, A, P, c_int, P, c_int, P, c_long, P, c_int, P, P, c_long, P)
+    _sig(L, "spl_route_pack", c_int, P, c_int, P, c_int, c_int, P, c_long, c_int, c_long, P, P, P, P, P, P)
+    _sig(L, "spl_route_gather", c_int, P, c_long, P, P, P, c_int, P, P, P, c_int, P)
     _sig(L, "spl_arena_unset", c_int, A, P, c_int, c_long, P, c_int, P)
     _sig(L, "spl_arena_intop", c_int, A, P, c_int, P, P, c_long, P, P, c_int, P)
     _sig(L, "spl_arena_meta", c_int, A, P, c_int, c_int, P, c_long, P, P, P)

@@ -24,6 +24,19 @@ namespace {
 constexpr int kBlock = 256;
 constexpr int kMaxGrid = 256 * 8;
 
+// Segmented batch (routed C1 buffers, parallel/sharded.py): the batch is `n / cap` segments of
+// `cap` rows, one per source rank, of which only the first counts[seg] rows are live.  Dead rows
+// are skipped (status EINVAL, not counted in the stats).  counts == nullptr: every row is live.
+struct Seg {
+  const int32_t* counts;
+  long cap;
+  __device__ __forceinline__ bool live(long i) const {
+    if (!counts) return true;
+    const long s = i / cap;
+    return i - s * cap < (long)counts[s];
+  }
+};
+
 // Payload ordering discipline (arena_dev.hpp, MO): SPLINTER_ARENA_MO=0|1|2.
 inline int arena_mo() {
   static int mo = [] {
@@ -135,11 +148,15 @@ __global__ void k_init_slots(spl_arena_t aa) {
 template <int MO>
 __global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
                                                 int vstride, const uint32_t* lens, long n, int32_t* status,
-                                                int max_retry, uint64_t* stats) {
+                                                int max_retry, uint64_t* stats, Seg seg) {
   const Arena a = to_dev(aa);
   Stats st;
   uint64_t muts = 0;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    if (!seg.live(i)) {
+      if (status) status[i] = kInval;
+      continue;
+    }
     Key k;
     load_key(k, keys + i * (long)kstride, kstride);
     const uint32_t len = lens[i];
@@ -167,10 +184,15 @@ __global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys
 template <int MO>
 __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                 int ostride, uint32_t* out_lens, long n, int32_t* status,
-                                                int max_retry, uint64_t* stats) {
+                                                int max_retry, uint64_t* stats, Seg seg) {
   const Arena a = to_dev(aa);
   Stats st;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
+    if (!seg.live(i)) {
+      if (out_lens) out_lens[i] = 0;
+      if (status) status[i] = kInval;
+      continue;
+    }
     Key k;
     load_key(k, keys + i * (long)kstride, kstride);
     uint32_t len = 0;
@@ -197,7 +219,7 @@ __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys
 template <int U, int B>
 __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
                                                        const uint8_t* vals, int vstride, const uint32_t* lens, long n,
-                                                       int32_t* status, int max_retry, uint64_t* stats) {
+                                                       int32_t* status, int max_retry, uint64_t* stats, Seg seg) {
   const Arena a = to_dev(aa);
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
@@ -214,7 +236,7 @@ __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* ke
     for (int j = 0; j < U; ++j) {
       const long i = r0 + j;
       c[j] = Claim{-1, false, kInval};
-      if (i < n) {
+      if (i < n && seg.live(i)) {
         load_key(k[j], keys + i * (long)kstride, kstride);
         len[j] = lens[i];
         ++st.attempts;
@@ -262,7 +284,7 @@ __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* ke
 template <int U, int B, int GV = 1>
 __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                        int ostride, uint32_t* out_lens, long n, int32_t* status,
-                                                       int max_retry, uint64_t* stats) {
+                                                       int max_retry, uint64_t* stats, Seg seg) {
   const Arena a = to_dev(aa);
   Stats st;
   const long per_block = (long)blockDim.x * U;
@@ -279,7 +301,7 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
       rc[j] = kInval;
       sidx[j] = -1;
       len[j] = 0;
-      if (i < n) {
+      if (i < n && seg.live(i)) {
         load_key(k[j], keys + i * (long)kstride, kstride);
         ++st.attempts;
         sidx[j] = locate_peek(a, k[j], &e1[j], &len[j]);  // hash/epoch/len/key: one round trip per probe
@@ -673,13 +695,21 @@ int spl_arena_init_slots(spl_arena_t a, hipStream_t s) {
 
 int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
                   long n, int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
+  return spl_arena_set_seg(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, nullptr, 0, s);
+}
+
+int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
+                      const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats,
+                      const int32_t* seg_counts, long seg_cap, hipStream_t s) {
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
+  if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
+  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1};
   const int mo = arena_mo();
   const int u = arena_rounds(), b = arena_block();
 #define SPL_SET_ROUNDS(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_set_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
-                     kstride, vals, vstride, lens, n, status, max_retry, stats)
+                     kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
   if (u == 2 && b == 256) SPL_SET_ROUNDS(2, 256);
   else if (u == 2) SPL_SET_ROUNDS(2, 512);
   else if (u == 4 && b == 256) SPL_SET_ROUNDS(4, 256);
@@ -688,29 +718,37 @@ int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* v
 #undef SPL_SET_ROUNDS
   else if (mo == 1)
     hipLaunchKernelGGL(k_set<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
-                       status, max_retry, stats);
+                       status, max_retry, stats, seg);
   else if (mo == 2)
     hipLaunchKernelGGL(k_set<2>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
-                       status, max_retry, stats);
+                       status, max_retry, stats, seg);
   else
     hipLaunchKernelGGL(k_set<0>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
-                       status, max_retry, stats);
+                       status, max_retry, stats, seg);
   return (int)hipGetLastError();
 }
 
 int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
                   int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
+  return spl_arena_get_seg(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, nullptr, 0, s);
+}
+
+int spl_arena_get_seg(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
+                      long n, int32_t* status, int max_retry, uint64_t* stats, const int32_t* seg_counts,
+                      long seg_cap, hipStream_t s) {
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
+  if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
+  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1};
   const int mo = arena_mo();
   const int u = arena_rounds_get(), b = arena_block();
 #define SPL_GET_ROUNDS(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_get_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
-                     kstride, out, ostride, out_lens, n, status, max_retry, stats)
+                     kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
   static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
   if (u == 2 && b == 256 && gv == 2)
     hipLaunchKernelGGL((k_get_rounds<2, 256, 2>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
-                       kstride, out, ostride, out_lens, n, status, max_retry, stats);
+                       kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
   else if (u == 2 && b == 256) SPL_GET_ROUNDS(2, 256);
   else if (u == 2) SPL_GET_ROUNDS(2, 512);
   else if (u == 4 && b == 256) SPL_GET_ROUNDS(4, 256);
@@ -719,13 +757,13 @@ int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, in
 #undef SPL_GET_ROUNDS
   else if (mo == 1)
     hipLaunchKernelGGL(k_get<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
-                       status, max_retry, stats);
+                       status, max_retry, stats, seg);
   else if (mo == 2)
     hipLaunchKernelGGL(k_get<2>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
-                       status, max_retry, stats);
+                       status, max_retry, stats, seg);
   else
     hipLaunchKernelGGL(k_get<0>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
-                       status, max_retry, stats);
+                       status, max_retry, stats, seg);
   return (int)hipGetLastError();
 }
 

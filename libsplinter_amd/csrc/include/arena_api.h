@@ -57,6 +57,14 @@ int spl_arena_set(spl_arena_t a, const char *keys, int kstride, const uint8_t *v
 int spl_arena_get(spl_arena_t a, const char *keys, int kstride, uint8_t *out, int ostride,
                   uint32_t *out_lens, long n, int32_t *status, int max_retry, uint64_t *stats,
                   hipStream_t stream);
+/* Segmented variants: the batch is n/seg_cap segments of seg_cap rows of which only the first
+ * seg_counts[s] are live (routed C1 buffers); dead rows get status EINVAL and are not counted. */
+int spl_arena_set_seg(spl_arena_t a, const char *keys, int kstride, const uint8_t *vals, int vstride,
+                      const uint32_t *lens, long n, int32_t *status, int max_retry, uint64_t *stats,
+                      const int32_t *seg_counts, long seg_cap, hipStream_t stream);
+int spl_arena_get_seg(spl_arena_t a, const char *keys, int kstride, uint8_t *out, int ostride,
+                      uint32_t *out_lens, long n, int32_t *status, int max_retry, uint64_t *stats,
+                      const int32_t *seg_counts, long seg_cap, hipStream_t stream);
 int spl_arena_unset(spl_arena_t a, const char *keys, int kstride, long n, int32_t *status, int max_retry,
                     hipStream_t stream);
 int spl_arena_intop(spl_arena_t a, const char *keys, int kstride, const int *ops, const uint64_t *masks,
@@ -76,6 +84,18 @@ int spl_format_keys(char *out, int kstride, const uint64_t *ids, uint64_t first,
                     int plen, int width, hipStream_t stream);
 int spl_format_values(uint8_t *out, int vstride, uint32_t *lens, const uint64_t *ids, uint64_t first, long n,
                       uint32_t ver, uint32_t len, hipStream_t stream);
+
+/* C1 routing (route_kernels.hip): pack a batch into world x cap per-destination rows
+ * (shard = (fnv1a >> 40) % world); counts[world] is zeroed by the launcher and receives the
+ * rows per destination (may exceed cap: ops beyond cap get pos = -1).  vals/lout/vout NULL for
+ * key-only requests.  Gather: status[i] = pos[i] < 0 ? EAGAIN : rstatus[pos[i]], and likewise
+ * lengths and min(rstride, ostride) value bytes. */
+int spl_route_pack(const char *keys, int kstride, const uint8_t *vals, int vstride, int vwidth,
+                   const uint32_t *lens, long n, int world, long cap, int32_t *counts, int64_t *pos,
+                   char *kout, uint32_t *lout, uint8_t *vout, hipStream_t stream);
+int spl_route_gather(const int64_t *pos, long n, const int32_t *rstatus, const uint32_t *rlens,
+                     const uint8_t *rvals, int rstride, int32_t *status, uint32_t *out_lens, uint8_t *out,
+                     int ostride, hipStream_t stream);
 
 #ifdef __cplusplus
 }

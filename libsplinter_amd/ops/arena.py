@@ -149,6 +149,40 @@ class HbmArena:
                                          _stream()), "arena_get")
         return status, out, out_lens
 
+    # --------------------------------------------- segmented (routed C1) --
+    def set_seg(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, counts: torch.Tensor, cap: int,
+                retries: int = 64, status: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Set over a routed buffer of ``n/cap`` segments of which only the first
+        ``counts[s]`` rows are live (parallel/sharded.py RoutedKV); dead rows get
+        EINVAL and are not counted in the stats."""
+        keys = _keys(keys)
+        n = keys.shape[0]
+        assert vals.is_contiguous() and lens.is_contiguous() and counts.dtype == torch.int32
+        assert n % cap == 0 and counts.numel() == n // cap
+        if status is None:
+            status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        with trace_range("arena.set_seg"):
+            _check(self._H.spl_arena_set_seg(self.desc, keys.data_ptr(), keys.shape[1], vals.data_ptr(),
+                                             vals.shape[1], lens.data_ptr(), n, status.data_ptr(), retries,
+                                             self.stats.data_ptr(), counts.data_ptr(), cap, _stream()),
+                   "arena_set_seg")
+        return status
+
+    def get_seg(self, keys: torch.Tensor, counts: torch.Tensor, cap: int, width: int, retries: int = 64):
+        """Get over a routed buffer (see :meth:`set_seg`); values land in ``width``-byte
+        rows and a longer value returns EMSGSIZE (-90).  -> (status, vals, lens)."""
+        keys = _keys(keys)
+        n = keys.shape[0]
+        assert n % cap == 0 and counts.numel() == n // cap and counts.dtype == torch.int32 and width % 16 == 0
+        out = torch.empty((n, width), dtype=torch.uint8, device=keys.device)
+        status = torch.empty(n, dtype=torch.int32, device=keys.device)
+        lens = torch.empty(n, dtype=torch.int32, device=keys.device)
+        with trace_range("arena.get_seg"):
+            _check(self._H.spl_arena_get_seg(self.desc, keys.data_ptr(), keys.shape[1], out.data_ptr(), width,
+                                             lens.data_ptr(), n, status.data_ptr(), retries, self.stats.data_ptr(),
+                                             counts.data_ptr(), cap, _stream()), "arena_get_seg")
+        return status, out, lens
+
     def unset(self, keys: torch.Tensor, retries: int = 64) -> torch.Tensor:
         keys = _keys(keys)
         n = keys.shape[0]

@@ -117,6 +117,7 @@ class ShardedKV:
     def __init__(self, local, group: Optional[dist.ProcessGroup] = None):
         self.local = local
         self.group = group
+        self._rk = None
         if dist.is_available() and dist.is_initialized():
             self.world = dist.get_world_size(group)
             self.rank = dist.get_rank(group)
@@ -165,31 +166,54 @@ class ShardedKV:
         return shard_of(self.local.hash_keys(keys), self.world) == self.rank
 
     # -------------------------------------------------------- C1: ops ----
-    def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, **kw) -> torch.Tensor:
+    def _routed(self):
+        if self._rk is None:
+            from .routed import RoutedKV
+            self._rk = RoutedKV(self.local, self.group)
+        return self._rk
+
+    def _exact_cap(self, keys: torch.Tensor) -> int:
+        """Largest per-destination count of this batch over all ranks (one host sync):
+        the API path never returns EAGAIN for a full routing segment."""
+        dest = shard_of(self.local.hash_keys(keys), self.world)
+        c = torch.bincount(dest, minlength=self.world).max().reshape(1).to(torch.int64)
+        self._c.all_reduce(c, op=dist.ReduceOp.MAX)
+        return max(1, int(c.item()))
+
+    def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, cap: Optional[int] = None,
+            vwidth: Optional[int] = None, **kw) -> torch.Tensor:
+        """Routed set (C1).  ``cap``/``vwidth`` given (identical on every rank): no host
+        synchronisation (parallel/routed.py); otherwise both are measured on this batch."""
         if self.world == 1:
             return self.local.set(keys, vals, lens, **kw)
-        # ship only the used prefix of the value rows (16-B multiple): 150-B values in 256-B rows
-        # are 40 % less xGMI traffic
-        w = (int(lens.max().item()) + 15) // 16 * 16 if lens.numel() else 16
-        if 0 < w < vals.shape[1]:
-            vals = vals[:, :w]
-        return self._roundtrip(keys, [vals, lens.to(torch.int32)],
-                               lambda k, v, ln: [self.local.set(k, v, ln, **kw).to(torch.int32)], None)[0]
+        if vwidth is None:
+            # ship only the used prefix of the value rows (16-B multiple): 150-B values in 256-B
+            # rows are 40 % less xGMI traffic
+            vwidth = (int(lens.max().item()) + 15) // 16 * 16 if lens.numel() else 16
+        vwidth = min(max(16, vwidth), vals.shape[1])
+        cap = self._exact_cap(keys) if cap is None else cap
+        return self._routed().set(keys, vals, lens, cap, vwidth, **kw)
 
-    def get(self, keys: torch.Tensor, **kw) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    def get(self, keys: torch.Tensor, cap: Optional[int] = None, width: Optional[int] = None,
+            **kw) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        """Routed get (C1) -> (status, vals, lens).  With ``width`` the response rows
+        carry ``width`` value bytes (longer values: EMSGSIZE); without it, the longest
+        value any shard returns (one scalar all-reduce)."""
         if self.world == 1:
             return self.local.get(keys, **kw)
-
-        def ex(k):
-            st, v, ln = self.local.get(k, **kw)
-            # response rows carry only the longest value any shard returns (one scalar all-reduce)
-            w = torch.tensor([(int(ln.max().item()) + 15) // 16 * 16 if ln.numel() else 16],
-                             dtype=torch.int64, device=v.device)
+        rk = self._routed()
+        cap = self._exact_cap(keys) if cap is None else cap
+        op = rk.begin_get(keys, cap, width or (self.local.max_val + 15) // 16 * 16)
+        rk.execute(op, **kw)
+        if width is None:
+            t = op.t
+            w = torch.tensor([(int(t["rlens"].max().item()) + 15) // 16 * 16 if t["rlens"].numel() else 16],
+                             dtype=torch.int64, device=t["rvals"].device)
             self._c.all_reduce(w, op=dist.ReduceOp.MAX)
-            w = max(16, min(int(w.item()), v.shape[1]))
-            return [st.to(torch.int32), ln.to(torch.int32), v[:, :w]]
-        st, ln, v = self._roundtrip(keys, [], ex, None)
-        return st, v, ln
+            op.width = max(16, min(int(w.item()), t["rvals"].shape[1]))
+            t["rvals"] = t["rvals"][:, :op.width].contiguous()
+        rk.respond(op)
+        return rk.finish(op)
 
     def unset(self, keys: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
@@ -345,6 +369,59 @@ class GpuShard:
     def unset(self, keys):
         return self.arena.unset(keys)
 
+    @property
+    def max_val(self):
+        return self.arena.max_val
+
+    def set_seg(self, keys, vals, lens, counts, cap, **kw):
+        return self.arena.set_seg(keys, vals, lens, counts, cap, **kw)
+
+    def get_seg(self, keys, counts, cap, width, **kw):
+        return self.arena.get_seg(keys, counts, cap, width, **kw)
+
+    def route_pack(self, keys, vals, lens, vwidth, world, cap):
+        """spl_route_pack: -> (counts[world], pos[n], keys, lens, vals) of the world x cap segments."""
+        from .. import _native as N
+        from ..ops.arena import _check, _keys, _stream
+        keys = _keys(keys)
+        n, ks, dev = keys.shape[0], keys.shape[1], keys.device
+        counts = torch.empty(world, dtype=torch.int32, device=dev)
+        pos = torch.empty(n, dtype=torch.int64, device=dev)
+        kout = torch.empty((world * cap, ks), dtype=torch.uint8, device=dev)
+        lout = vout = None
+        vp = lp = 0
+        vstride = 0
+        if vals is not None:
+            vals, lens = vals.contiguous(), lens.contiguous()
+            assert lens.dtype in (torch.int32, torch.uint32) and vals.shape[0] == n and lens.shape[0] == n
+            lout = torch.empty(world * cap, dtype=torch.int32, device=dev)
+            vout = torch.empty((world * cap, vwidth), dtype=torch.uint8, device=dev)
+            vp, lp, vstride = vals.data_ptr(), lens.data_ptr(), vals.shape[1]
+        _check(N.hip_lib().spl_route_pack(keys.data_ptr(), ks, vp or None, vstride, vwidth, lp or None, n, world, cap,
+                                          counts.data_ptr(), pos.data_ptr(), kout.data_ptr(),
+                                          lout.data_ptr() if lout is not None else None,
+                                          vout.data_ptr() if vout is not None else None, _stream()), "route_pack")
+        return counts, pos, kout, lout, vout
+
+    def route_gather(self, pos, rstatus, rlens=None, rvals=None, width=0, out=None, out_lens=None, status=None):
+        """spl_route_gather: routed responses -> client order (status, vals, lens)."""
+        from .. import _native as N
+        from ..ops.arena import _check, _stream
+        n, dev = pos.shape[0], pos.device
+        status = torch.empty(n, dtype=torch.int32, device=dev) if status is None else status
+        if rlens is not None:
+            out_lens = torch.empty(n, dtype=torch.int32, device=dev) if out_lens is None else out_lens
+            out = torch.empty((n, width), dtype=torch.uint8, device=dev) if out is None else out
+            assert out.is_contiguous() and out.shape[0] == n
+        _check(N.hip_lib().spl_route_gather(pos.data_ptr(), n, rstatus.data_ptr(),
+                                            rlens.data_ptr() if rlens is not None else None,
+                                            rvals.data_ptr() if rvals is not None else None,
+                                            rvals.shape[1] if rvals is not None else 0, status.data_ptr(),
+                                            out_lens.data_ptr() if rlens is not None else None,
+                                            out.data_ptr() if rlens is not None else None,
+                                            out.shape[1] if rlens is not None else 0, _stream()), "route_gather")
+        return status, out, out_lens
+
     def integer_op(self, keys, ops, masks):
         return self.arena.integer_op(keys, ops, masks)
 
@@ -452,6 +529,35 @@ class HostShard:
     def unset(self, keys):
         return torch.tensor([0 if self.store.unset(self._key(r)) >= 0 else -2 for r in keys.numpy()],
                             dtype=torch.int32)
+
+    @property
+    def max_val(self):
+        return self.store.max_val
+
+    @staticmethod
+    def _live(n, counts, cap):
+        return (torch.arange(n) % cap) < torch.repeat_interleave(counts.to(torch.int64), cap)
+
+    def set_seg(self, keys, vals, lens, counts, cap, **kw):
+        live = self._live(keys.shape[0], counts, cap)
+        st = torch.full((keys.shape[0],), -22, dtype=torch.int32)
+        st[live] = self.set(keys[live], vals[live], lens[live], **kw)
+        return st
+
+    def get_seg(self, keys, counts, cap, width, **kw):
+        n = keys.shape[0]
+        live = self._live(n, counts, cap)
+        st = torch.full((n,), -22, dtype=torch.int32)
+        out = torch.zeros((n, width), dtype=torch.uint8)
+        lens = torch.zeros(n, dtype=torch.int32)
+        s, v, ln = self.get(keys[live], **kw)
+        big = ln > width
+        s = torch.where(big & (s == 0), torch.full_like(s, -90), s)  # EMSGSIZE, like the kernel
+        w = min(width, v.shape[1])
+        v = v[:, :w] * (s == 0).unsqueeze(1).to(torch.uint8)
+        st[live], lens[live] = s, torch.where(s == 0, ln, torch.zeros_like(ln))
+        out[live, :w] = v
+        return st, out, lens
 
     def integer_op(self, keys, ops, masks):
         st, res = [], []

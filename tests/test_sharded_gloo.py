@@ -164,3 +164,97 @@ def test_sharded_collectives_gloo(world, uniq):
                 p.kill()
     for r in range(world):
         assert res.get(r) == "ok", res.get(r)
+
+
+def _routed_worker(rank, world, port, base, q):
+    """RoutedKV (parallel/routed.py): fixed-capacity segments, phase-split calls,
+    overflow -> EAGAIN, narrow response rows -> EMSGSIZE."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from libsplinter_amd import Store, unlink
+        from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
+        from libsplinter_amd.parallel.sharded import HostShard, shard_of
+        name = f"{base}_q{rank}"
+        st = Store.create(name, slots=2048, max_val=128, embeddings=False)
+        sh = HostShard(st)
+        rk = RoutedKV(sh, resp_group=dist.new_group(backend="gloo"))
+        n = 120
+        mine = [f"q{rank}_k{i}" for i in range(n)]
+        K = _keys(mine)
+        V, L = _vals([f"value-{m}-padding".encode() for m in mine])
+        cap = route_capacity(n, world)
+        op = rk.begin_set(K, V, L, cap, 32)
+        rk.execute(op)
+        rk.respond(op)
+        s = rk.finish(op)
+        assert (s == 0).all(), s
+        dist.barrier()
+        allk = [f"q{r}_k{i}" for r in range(world) for i in range(n)]
+        # two gets in flight at once: requests of both, then execute/respond/finish
+        half = len(allk) // 2
+        g1 = rk.begin_get(_keys(allk[:half]), route_capacity(half, world), 32)
+        g2 = rk.begin_get(_keys(allk[half:]), route_capacity(len(allk) - half, world), 32)
+        res = []
+        for g in (g1, g2):
+            rk.execute(g)
+        for g in (g1, g2):
+            rk.respond(g)
+        for g in (g1, g2):
+            res.append(rk.finish(g))
+        sts = torch.cat([r[0] for r in res])
+        vs = torch.cat([r[1] for r in res])
+        ls = torch.cat([r[2] for r in res])
+        assert (sts == 0).all()
+        for i, k in enumerate(allk):
+            assert bytes(vs[i, : ls[i]].numpy()) == f"value-{k}-padding".encode()
+        # response rows narrower than the values: EMSGSIZE, no bytes
+        s_, v_, l_ = rk.get(_keys(allk[:10]), route_capacity(10, world), 16)
+        assert (s_ == -90).all() and (l_ == 0).all(), (s_, l_)
+        # tight capacity: the excess ops of a full segment come back EAGAIN, the rest land
+        ex = [f"x{rank}_{i}" for i in range(60)]
+        KX = _keys(ex)
+        VX, LX = _vals([b"x" * 8] * 60)
+        tight = 60 // world - 3
+        sx = rk.set(KX, VX, LX, tight, 16)
+        dest = shard_of(sh.hash_keys(KX), world)
+        over = int((torch.bincount(dest, minlength=world) - tight).clamp(min=0).sum())
+        assert int((sx == -11).sum()) == over and int((sx == 0).sum()) == 60 - over
+        dist.barrier()
+        ok_keys = [k for k, s1 in zip(ex, sx.tolist()) if s1 == 0]
+        if ok_keys:
+            s2, _, _ = rk.get(_keys(ok_keys), len(ok_keys), 16)
+            assert (s2 == 0).all()
+        q.put((rank, "ok"))
+        st.close()
+        unlink(name)
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_routed_kv_gloo(world, uniq):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_routed_worker, args=(r, world, port, uniq, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=240)
+            res[r] = msg
+            if msg != "ok":
+                break
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert res.get(r) == "ok", res.get(r)

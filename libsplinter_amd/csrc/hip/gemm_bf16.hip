@@ -179,18 +179,19 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
       *(uint4*)(ep.out + gm * ep.ldo + n0 + c8) = o;
     }
   } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
-    // block columns: [up 0..63 | gate 0..63] of output columns nt*64 + 0..63
+    // block columns: [up16 | gate16] x 4 (pack_upgate) of output columns nt*64 + 0..63
 #pragma unroll
     for (int it = 0; it < (BM * 64 / 8) / kThreads; ++it) {
       const int q = tid + it * kThreads;
       const int row = q >> 3, c8 = (q & 7) * 8;
       const long gm = m0 + row;
       if (gm >= ep.M) continue;
+      const int uc = 32 * (c8 >> 4) + (c8 & 15);
       float o[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float up = E[row * kEpiStride + c8 + e];
-        const float g = E[row * kEpiStride + 64 + c8 + e];
+        const float up = E[row * kEpiStride + uc + e];
+        const float g = E[row * kEpiStride + uc + 16 + e];
         o[e] = up * (g / (1.f + __expf(-g)));
       }
       uint4 w;
@@ -210,11 +211,12 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
       if (gm >= ep.M) continue;
       const int cb = head * 64;
       const long gcol = n0 + cb;
+      const int pc = d0 < 16 ? d0 : d0 + 16;  // pack_qkv: [d0-15 | d32-47 | d16-31 | d48-63]
       float x1[8], x2[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        x1[e] = E[row * kEpiStride + cb + d0 + e];
-        x2[e] = E[row * kEpiStride + cb + d0 + 32 + e];
+        x1[e] = E[row * kEpiStride + cb + pc + e];
+        x2[e] = E[row * kEpiStride + cb + pc + 16 + e];
       }
       if (gcol < ep.rope_cols) {
         const float* cs = ep.rope + (long)ep.pos[gm] * 64 + d0 * 2;
@@ -282,6 +284,7 @@ __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {  // wave-uniform: scalar branch to an immediate count
     case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
+    case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
     case 4: asm volatile("s_waitcnt vmcnt(4)" ::: "memory"); break;
     case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
@@ -476,19 +479,19 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
         *(uint4*)(ep.out + gm * ep.ldo + n0 + c8) = pack8(v);
       }
     } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
-      // block columns [up64 | gate64 | up64 | gate64] -> output columns nt*128 + 0..127
+      // block columns [up16 | gate16] x 8 (pack_upgate) -> output columns nt*128 + 0..127
 #pragma unroll
       for (int it = 0; it < (128 * 128 / 8) / kThreads2; ++it) {
         const int q = tid + it * kThreads2;
         const int row = q >> 4, oc = (q & 15) * 8;
         const long gm = mh + row;
         if (gm >= ep.M) continue;
-        const int uc = (oc >> 6) * 128 + (oc & 63);
+        const int uc = 32 * (oc >> 4) + (oc & 15);
         float o[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
           const float up = E[row * kEpi2Stride + uc + e];
-          const float g = E[row * kEpi2Stride + uc + 64 + e];
+          const float g = E[row * kEpi2Stride + uc + 16 + e];
           o[e] = up * (g / (1.f + __expf(-g)));
         }
         *(uint4*)(ep.out + gm * ep.ldo + (long)nt * 128 + oc) = pack8(o);
@@ -503,11 +506,12 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
         if (gm >= ep.M) continue;
         const int cb = head * 64;
         const long gcol = n0 + cb;
+        const int pc = d0 < 16 ? d0 : d0 + 16;  // pack_qkv layout
         float x1[8], x2[8];
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          x1[e] = E[row * kEpi2Stride + cb + d0 + e];
-          x2[e] = E[row * kEpi2Stride + cb + d0 + 32 + e];
+          x1[e] = E[row * kEpi2Stride + cb + pc + e];
+          x2[e] = E[row * kEpi2Stride + cb + pc + 16 + e];
         }
         if (gcol < ep.rope_cols) {
           const float* cs = ep.rope + (long)ep.pos[gm] * 64 + d0 * 2;
@@ -535,6 +539,275 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
     }
   }
 }
+
+// ===========================================================================
+// Persistent 256x256 kernel with a REGISTER epilogue (variant 512, "p").
+//
+// One block per CU walks its tiles (blockIdx, +grid, ...; each through the
+// same XCD/L2-band remap as the launch-per-tile kernels) as ONE stream of
+// K-steps: the LDS-DMA stages of the next tile's first K-steps are issued
+// during the current tile's last phases, so a tile change costs no pipeline
+// refill.  The MFMA operands are swapped (W fragment as the A operand), so a
+// lane's accumulator holds C[m][n .. n+3] (four consecutive output columns of
+// one row) and the epilogue stores 8-B (16-B for fp32) chunks straight from
+// registers: no LDS round trip, no barrier, and the LDS buffers can keep the
+// next tile's stages in flight.  The epilogue's global ops are younger than
+// those stages, so the counted vmcnt waits of the next phases stay correct
+// (vmcnt retires in issue order: MI355X_MICROARCH.md, s_waitcnt).
+//
+// Epilogue layouts need pairs in one lane: SWIGLU weights are packed
+// [up16 | gate16] per 16 outputs (models/nomic.py pack_upgate) and the QKV
+// rows of each 64-wide head as [d0-15 | d32-47 | d16-31 | d48-63]
+// (pack_qkv), so x1 = acc[..][j=0] and x2 = acc[..][j=1] of the same lane.
+// ===========================================================================
+__device__ __forceinline__ uint2 pack4(const float* v) {
+  return make_uint2(f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+}
+
+template <int MODE, bool PERSIST>
+__global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restrict__ A, long lda,
+                                                         const uint16_t* __restrict__ W, long ldw, int K,
+                                                         int mtiles, int ntiles, EpiArgs ep) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wn = wave & 3;
+  const int nb = mtiles * ntiles, G = gridDim.x;
+  const int my_tiles = PERSIST ? (nb - (int)blockIdx.x + G - 1) / G : 1;
+  const int nk = K / BK;  // >= 2 (launcher): a lookahead of two K-steps spans at most one tile change
+  const int total = my_tiles * nk;
+  if (my_tiles <= 0) return;
+
+  const int srow = lane >> 3, schunk = ((lane & 7) ^ srow) * 8;
+  // per-lane DMA source offsets (elements, 32-bit as in k_gemm256) of the current tile (C) and the
+  // next one (X): half h, instruction i -> row h*128 + (i*8 + wave)*8 + srow
+  uint32_t offAc[2][2], offBc[2][2], offAx[2][2], offBx[2][2];
+  long m0c = 0, n0c = 0;
+  auto tile_offsets = [&](int ti, uint32_t (&oa)[2][2], uint32_t (&ob)[2][2], long& m0, long& n0) {
+    int mt, nt;
+    remap_tile((int)blockIdx.x + ti * G, nb, ntiles, ep.gn, mt, nt);
+    m0 = (long)mt * 256;
+    n0 = (long)nt * 256;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int r = h * 128 + (i * 8 + wave) * 8 + srow;
+        const long gr = (m0 + r < ep.M) ? m0 + r : ep.M - 1;  // clamp: tail rows re-read row M-1, never stored
+        oa[h][i] = (uint32_t)(gr * lda + schunk);
+        ob[h][i] = (uint32_t)((n0 + r) * ldw + schunk);
+      }
+  };
+  tile_offsets(0, offAc, offBc, m0c, n0c);
+  long m0x = m0c, n0x = n0c;
+  if (my_tiles > 1) tile_offsets(1, offAx, offBx, m0x, n0x);
+  else {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) { offAx[h][i] = offAc[h][i]; offBx[h][i] = offBc[h][i]; }
+  }
+  int ti = 0, kt = 0;
+
+  // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of stream step g into buffer buf
+  auto stage = [&](int which, int g, int buf) {
+    const bool nx = g >= (ti + 1) * nk;
+    const int k0 = (g - (ti + (nx ? 1 : 0)) * nk) * BK;
+    const uint16_t* base = (which < 2 ? A : W) + k0;
+    char* dst = smem + buf * kBufBytes + which * kHalfBytes;
+    const int h = which & 1;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t off = which < 2 ? (nx ? offAx[h][i] : offAc[h][i]) : (nx ? offBx[h][i] : offBc[h][i]);
+      __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
+    }
+  };
+
+  const int frow = (lane & 15) * 128;
+  const int fsw0 = ((0 * 4 + (lane >> 4)) ^ (lane & 7)) << 4;
+  const int fsw1 = ((1 * 4 + (lane >> 4)) ^ (lane & 7)) << 4;
+  const int fq = lane >> 4, fr = lane & 15;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue, in the steady-state issue order: A0 B0 B1 A1 (t=0), A0 B0 B1 (t=1)
+  stage(0, 0, 0); stage(2, 0, 0); stage(3, 0, 0); stage(1, 0, 0);
+  if (total > 1) { stage(0, 1, 1); stage(2, 1, 1); stage(3, 1, 1); }
+
+  bf16x8 af[4][2], b0[2][2], b1[2][2];
+  for (int g = 0; g < total; ++g) {
+    const int buf = g & 1;
+    const char* hA0 = smem + buf * kBufBytes;
+    const char* hA1 = hA0 + kHalfBytes;
+    const char* hB0 = hA0 + 2 * kHalfBytes;
+    const char* hB1 = hA0 + 3 * kHalfBytes;
+    const bool n1 = g + 1 < total, n2 = g + 2 < total;
+    // ---- phase 1: quadrant (0,0)
+    wait_vm(n1 ? 10 : 4);
+    raw_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      b0[j][0] = *(const bf16x8*)(hB0 + (wn * 32 + j * 16) * 128 + frow + fsw0);
+      b0[j][1] = *(const bf16x8*)(hB0 + (wn * 32 + j * 16) * 128 + frow + fsw1);
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw0);
+      af[i][1] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw1);
+    }
+    if (n1) stage(1, g + 1, buf ^ 1);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][kk], af[i][kk], acc[0][0][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- phase 2: quadrant (0,1)
+    wait_vm(n1 ? 10 : 2);
+    raw_barrier();
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      b1[j][0] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw0);
+      b1[j][1] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw1);
+    }
+    if (n2) stage(0, g + 2, buf);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[0][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][kk], af[i][kk], acc[0][1][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- phase 3: quadrant (1,0)
+    wait_vm(n2 ? 10 : (n1 ? 8 : 0));
+    raw_barrier();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      af[i][0] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw0);
+      af[i][1] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw1);
+    }
+    if (n2) stage(2, g + 2, buf);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][kk], af[i][kk], acc[1][0][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- phase 4: quadrant (1,1), registers only (B1's last read was phase 2: a barrier ago)
+    if (n2) stage(3, g + 2, buf);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[1][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][kk], af[i][kk], acc[1][1][i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+
+    if (++kt < nk) continue;
+    // ---- tile done: register epilogue (lane: rows m, 4 consecutive columns per fragment) --------
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long m = m0c + qm * 128 + wr * 64 + i * 16 + fr;
+        if (m < ep.M) {
+#pragma unroll
+          for (int qn = 0; qn < 2; ++qn) {
+            const long nb0 = n0c + qn * 128 + wn * 32;  // this wave's 32-column group
+            if constexpr (MODE == NOMIC_EPI_STORE || MODE == NOMIC_EPI_RESIDUAL) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const long n = nb0 + j * 16 + fq * 4;
+                float v[4] = {acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
+                              acc[qm][qn][i][j][3]};
+                if constexpr (MODE == NOMIC_EPI_RESIDUAL) {
+                  const uint2 rr = *(const uint2*)(ep.res + m * ep.ldr + n);
+                  v[0] += bf2f((uint16_t)(rr.x & 0xffff));
+                  v[1] += bf2f((uint16_t)(rr.x >> 16));
+                  v[2] += bf2f((uint16_t)(rr.y & 0xffff));
+                  v[3] += bf2f((uint16_t)(rr.y >> 16));
+                }
+                *(uint2*)(ep.out + m * ep.ldo + n) = pack4(v);
+              }
+            } else if constexpr (MODE == NOMIC_EPI_F32) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const long n = nb0 + j * 16 + fq * 4;
+                *(float4*)((float*)ep.out + m * ep.ldo + n) =
+                    make_float4(acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
+                                acc[qm][qn][i][j][3]);
+              }
+            } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
+              float o[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                const float up = acc[qm][qn][i][0][e], gt = acc[qm][qn][i][1][e];
+                o[e] = up * (gt / (1.f + __expf(-gt)));
+              }
+              *(uint2*)(ep.out + m * ep.ldo + nb0 / 2 + fq * 4) = pack4(o);
+            } else if constexpr (MODE == NOMIC_EPI_ROPE) {
+              const long head0 = nb0 & ~63L;
+              const int d = (int)(nb0 & 32) / 2 + fq * 4;  // packed half 0: d 0-15, half 1: d 16-31
+              float x1[4], x2[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                x1[e] = acc[qm][qn][i][0][e];
+                x2[e] = acc[qm][qn][i][1][e];
+              }
+              if (head0 < ep.rope_cols) {
+                const float* cs = ep.rope + (long)ep.pos[m] * 64 + d * 2;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const float c = cs[2 * e], s = cs[2 * e + 1];
+                  const float a = x1[e], b = x2[e];
+                  x1[e] = a * c - b * s;
+                  x2[e] = b * c + a * s;
+                }
+              }
+              *(uint2*)(ep.out + m * ep.ldo + head0 + d) = pack4(x1);
+              *(uint2*)(ep.out + m * ep.ldo + head0 + 32 + d) = pack4(x2);
+            }
+          }
+        }
+      }
+#pragma unroll
+    for (int a = 0; a < 2; ++a)
+#pragma unroll
+      for (int b = 0; b < 2; ++b)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    kt = 0;
+    ++ti;
+    m0c = m0x;
+    n0c = n0x;
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) { offAc[h][i] = offAx[h][i]; offBc[h][i] = offBx[h][i]; }
+    if (ti + 1 < my_tiles) tile_offsets(ti + 1, offAx, offBx, m0x, n0x);
+  }
+}
+
+int g_num_cus = 256;  // MI355X: 256 CUs in 8 XCDs; refreshed from the device on first use
 
 int g_variant = -1;
 int gemm_variant() {
@@ -568,6 +841,36 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
   // there are several waves of tiles (measured, profiles/r1_gemm_ab.jsonl); small grids use 128^2
   const bool fits = N % 256 == 0 && mpad * lda < (1L << 31) && (long)N * ldw < (1L << 31);
   const int var = gemm_variant();
+  // auto: the persistent register-epilogue kernel when there are several waves of 256^2 tiles
+  // (measured per shape: profiles/r1_gemm_persistent_ab.jsonl); fewer tiles: the 128^2 kernel
+  const bool many = (mpad / 256) * (N / 256) >= 2048;
+  if (fits && K >= 2 * BK && (var == 512 || var == 513 || (var == 0 && many))) {
+    static bool attr_p = [] {
+      (void)hipFuncSetAttribute((const void*)k_gemm_p<MODE, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * kBufBytes);
+      (void)hipFuncSetAttribute((const void*)k_gemm_p<MODE, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                2 * kBufBytes);
+      return true;
+    }();
+    (void)attr_p;
+    const int mtiles = (int)(mpad / 256), ntiles = N / 256;
+    ep.gn = band_width(ntiles, 4);
+    static const int cus = [] {
+      int d = 0, n = 0;
+      if (hipGetDevice(&d) == hipSuccess &&
+          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0)
+        g_num_cus = n;
+      return g_num_cus;
+    }();
+    const int tiles = mtiles * ntiles;
+    if (var != 513)
+      hipLaunchKernelGGL((k_gemm_p<MODE, true>), dim3(tiles < cus ? tiles : cus), dim3(kThreads2), 2 * kBufBytes, s,
+                         A, lda, W, ldw, K, mtiles, ntiles, ep);
+    else
+      hipLaunchKernelGGL((k_gemm_p<MODE, false>), dim3(tiles), dim3(kThreads2), 2 * kBufBytes, s, A, lda, W, ldw, K,
+                         mtiles, ntiles, ep);
+    return (int)hipGetLastError();
+  }
   if (fits && (var == 256 || (var == 0 && (mpad / 256) * (N / 256) >= 2048))) {
     static bool attr = [] {
       (void)hipFuncSetAttribute((const void*)k_gemm256<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);

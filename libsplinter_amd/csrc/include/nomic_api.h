@@ -15,17 +15,17 @@ extern "C" {
 /* GEMM epilogues */
 #define NOMIC_EPI_STORE    0   /* out = bf16(acc)                                   */
 #define NOMIC_EPI_RESIDUAL 1   /* out = bf16(acc + res)                             */
-#define NOMIC_EPI_SWIGLU   2   /* W rows interleaved [up64|gate64]: out = up*silu(gate) */
-#define NOMIC_EPI_ROPE     3   /* qkv projection with NEOX RoPE on cols < rope_cols  */
+#define NOMIC_EPI_SWIGLU   2   /* W rows interleaved [up16|gate16] (pack_upgate): out = up*silu(gate) */
+#define NOMIC_EPI_ROPE     3   /* qkv projection, W rows per head [d0-15|d32-47|d16-31|d48-63]
+                                  (pack_qkv); NEOX RoPE on cols < rope_cols; out in natural order */
 #define NOMIC_EPI_F32      4   /* out = acc as fp32                                 */
 
 int nomic_gemm(int mode, const void *A, long lda, const void *W, long ldw, long M, int N, int K,
                void *out, long ldo, const void *res, long ldr, const float *rope, const int32_t *pos,
                int rope_cols, hipStream_t stream);
-/* GEMM kernel selection: 0 = auto (default: the 256x256 8-wave phased kernel when
- * N % 256 == 0 and the grid has >= 2048 tiles, else 128x128), 256 = force the
- * 256x256 kernel where the shape allows, 128 = force 128x128.  Returns the
- * previous setting. */
+/* GEMM kernel selection: 0 = auto, 512 = persistent 256x256 kernel with register
+ * epilogue, 256 = launch-per-tile 256x256 phased kernel, 128 = 128x128 (where the
+ * shape allows; otherwise the next one that does).  Returns the previous setting. */
 int nomic_gemm_set_variant(int variant);
 
 /* x[t] = LN(tok[ids[t]] + type_row) ; bf16 out [T, 768] */

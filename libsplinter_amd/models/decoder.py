@@ -160,8 +160,9 @@ class CausalLM:
             p = f"blk.{i}."
             qkv = torch.cat([T(p + "attn_q.weight"), T(p + "attn_k.weight"), T(p + "attn_v.weight")], 0)
             gate, up = T(p + "ffn_gate.weight"), T(p + "ffn_up.weight")
-            # SwiGLU epilogue layout: rows interleaved [up64 | gate64] (nomic_api.h NOMIC_EPI_SWIGLU)
-            ug = torch.stack([up.reshape(-1, 64, cfg.d), gate.reshape(-1, 64, cfg.d)], 1).reshape(-1, cfg.d)
+            # SwiGLU epilogue layout: rows interleaved [up16 | gate16] (nomic_api.h NOMIC_EPI_SWIGLU)
+            from .nomic import pack_upgate
+            ug = pack_upgate(up, gate)
             self.layers.append({"n1": T(p + "attn_norm.weight").float(), "qkv": qkv.contiguous(),
                                 "o": T(p + "attn_output.weight"), "n2": T(p + "ffn_norm.weight").float(),
                                 "ug": ug.contiguous(), "gate": gate, "up": up, "down": T(p + "ffn_down.weight")})

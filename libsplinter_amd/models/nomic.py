@@ -158,6 +158,24 @@ def write_gguf(path: str, cfg: NomicConfig, weights: Dict[str, np.ndarray], voca
     w.write()
 
 
+def pack_upgate(up: torch.Tensor, gate: torch.Tensor) -> torch.Tensor:
+    """SWIGLU epilogue weight layout (nomic_api.h NOMIC_EPI_SWIGLU): per 16 outputs,
+    16 up rows then 16 gate rows, so one MFMA lane holds up[o] and gate[o]."""
+    F, d = up.shape
+    return torch.stack([up.reshape(F // 16, 16, d), gate.reshape(F // 16, 16, d)], 1).reshape(2 * F, d)
+
+
+_QKV_PERM = torch.cat([torch.arange(0, 16), torch.arange(32, 48), torch.arange(16, 32), torch.arange(48, 64)])
+
+
+def pack_qkv(w: torch.Tensor) -> torch.Tensor:
+    """ROPE epilogue weight layout (NOMIC_EPI_ROPE): the rows of every 64-wide head
+    reordered [d0-15 | d32-47 | d16-31 | d48-63], so a NEOX pair (d, d+32) sits in one
+    lane; the kernel writes the output back in the natural order."""
+    n, d = w.shape
+    return w.reshape(n // 64, 64, d)[:, _QKV_PERM.to(w.device)].reshape(n, d)
+
+
 class NomicWeights:
     """Device-resident bf16 weights in kernel layout."""
 
@@ -171,11 +189,9 @@ class NomicWeights:
         for i in range(cfg.layers):
             p = f"blk.{i}."
             t = {k: tensors[p + v] for k, v in LAYER_NAMES.items()}
-            up, gate = t["wup"], t["wgate"]
-            # SwiGLU epilogue layout: per 64 output columns, [up 64 | gate 64]
-            ug = torch.stack([up.reshape(-1, 64, cfg.d), gate.reshape(-1, 64, cfg.d)], dim=1).reshape(-1, cfg.d)
             self.layers.append({
-                "wqkv": bf(t["wqkv"]), "wo": bf(t["wo"]), "wupgate": bf(ug), "wdown": bf(t["wdown"]),
+                "wqkv": bf(pack_qkv(t["wqkv"])), "wo": bf(t["wo"]), "wupgate": bf(pack_upgate(t["wup"], t["wgate"])),
+                "wdown": bf(t["wdown"]),
                 "ln1_g": bf(t["ln1_g"]), "ln1_b": bf(t["ln1_b"]), "ln2_g": bf(t["ln2_g"]), "ln2_b": bf(t["ln2_b"]),
             })
 

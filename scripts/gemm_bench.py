@@ -16,6 +16,7 @@ def main():
     ap.add_argument("--tokens", type=int, default=32768)
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--square", type=int, default=0, help="also time a plain MxNxK = S x S x S GEMM (loop throughput)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -25,6 +26,9 @@ def main():
     torch.manual_seed(0)
     shapes = [("qkv_rope", 3, 2304, 768), ("attn_out_res", 1, 768, 768), ("ffn_swiglu", 2, 6144, 768),
               ("ffn_down_res", 1, 768, 3072)]
+    if a.square:
+        shapes = [("square", 0, a.square, a.square)]
+        M = a.square
     bufs = {}
     for name, mode, N, K in shapes:
         A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
@@ -43,10 +47,11 @@ def main():
                           None if rope is None else rope.data_ptr(), None if pos is None else pos.data_ptr(),
                           1536, _stream()), name)
 
-    times = {(n, v): [] for n, *_ in shapes for v in (128, 256)}
+    VARS = (512, 513, 256, 128)
+    times = {(n, v): [] for n, *_ in shapes for v in VARS}
     for r in range(a.rounds):
         for name, *_ in shapes:
-            for v in (256, 128):
+            for v in VARS:
                 L.nomic_gemm_set_variant(v)
                 run(name)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -75,7 +80,7 @@ def main():
         fl = 2.0 * M * N * K
         print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": "torch.matmul(hipBLASLt)",
                           "ms_median": ref[name], "tflops_median": fl / ref[name] / 1e9}))
-        for v in (256, 128):
+        for v in VARS:
             t = np.array(times[(name, v)])
             print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": v, "ms_median": float(np.median(t)),
                               "tflops_median": fl / np.median(t) / 1e9, "tflops_best": fl / t.min() / 1e9}))

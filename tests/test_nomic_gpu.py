@@ -18,7 +18,7 @@ def L0():
     return _lib()
 
 
-@pytest.fixture(params=[256, 128], ids=["gemm256", "gemm128"])
+@pytest.fixture(params=[512, 513, 256, 128], ids=["gemm_p", "gemm_r", "gemm256", "gemm128"])
 def L(L0, request):
     """Run each GEMM numerics test on both kernel variants."""
     prev = L0.nomic_gemm_set_variant(request.param)
@@ -73,7 +73,8 @@ def test_gemm_swiglu_and_rope(L):
     x = torch.randn(Mp, K, device="cuda").bfloat16()
     up = torch.randn(F, K, device="cuda") * 0.03
     gate = torch.randn(F, K, device="cuda") * 0.03
-    ug = torch.stack([up.reshape(-1, 64, K), gate.reshape(-1, 64, K)], 1).reshape(-1, K).bfloat16()
+    from libsplinter_amd.models.nomic import pack_qkv, pack_upgate
+    ug = pack_upgate(up, gate).bfloat16()
     out = torch.empty(Mp, F, device="cuda", dtype=torch.bfloat16)
     _chk(L.nomic_gemm(2, x.data_ptr(), K, ug.data_ptr(), K, M, 2 * F, K, out.data_ptr(), F, None, 0, None, None, 0,
                       _stream()), "swiglu")
@@ -89,7 +90,8 @@ def test_gemm_swiglu_and_rope(L):
     ang = np.arange(8192)[:, None] * inv[None, :]
     tab = torch.from_numpy(np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32).reshape(8192, -1)).cuda()
     qkv = torch.empty(Mp, 3 * K, device="cuda", dtype=torch.bfloat16)
-    _chk(L.nomic_gemm(3, x.data_ptr(), K, wqkv.data_ptr(), K, M, 3 * K, K, qkv.data_ptr(), 3 * K, None, 0,
+    wpk = pack_qkv(wqkv)
+    _chk(L.nomic_gemm(3, x.data_ptr(), K, wpk.data_ptr(), K, M, 3 * K, K, qkv.data_ptr(), 3 * K, None, 0,
                       tab.data_ptr(), pos.data_ptr(), 2 * K, _stream()), "rope")
     raw = xf @ wqkv.float().T
     ref_m = NomicReference(cfg, {}, "cuda")
@@ -183,7 +185,8 @@ def test_gguf_roundtrip_device_dequant(tmp_path):
         assert NomicConfig.from_gguf(g).layers == 1
         nw = NomicWeights.from_gguf(g)
         host = torch.from_numpy(g.to_numpy_f32("blk.0.attn_qkv.weight")).cuda()
-        assert torch.equal(nw.layers[0]["wqkv"].float(), host.bfloat16().float()), lt
+        from libsplinter_amd.models.nomic import pack_qkv
+        assert torch.equal(nw.layers[0]["wqkv"].float(), pack_qkv(host).bfloat16().float()), lt  # kernel layout
         assert _rel(host, torch.from_numpy(w["blk.0.attn_qkv.weight"]).cuda()) < (0.2 if lt == "Q4_0" else 2e-2)
 
 

@@ -213,9 +213,23 @@ __device__ __forceinline__ uint32_t keep_mask(int keep) {
 //   0  plain 16-B payload accesses + agent release (writer) / acquire (reader)
 //   1  sc1 (L1-bypassing, write-through) 8-B atomic payload accesses, no fences
 //   2  unordered (measurement only: NOT a valid seqlock)
+//   3  write-through: 16-B `global_store_dwordx4 ... sc1` payload stores (no L2 dirty lines),
+//      published by every writing wave's vmcnt(0) drain + the atomic epoch increment, with no
+//      L2 write-back fence (cdna_hip_programming.md Guideline 16, recipe R1); readers unchanged
+//      (agent acquire + plain loads)
+// Write-through 16-B store.  hipcc does not count asm stores in its waits: callers drain()
+// before publishing; `s_nop 1` keeps the data registers live until the store has read them.
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ void st16_wt(void* p, uint4 v) {
+  const u32x4_t d = {v.x, v.y, v.z, v.w};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(d) : "memory");
+}
+
 template <int MO>
 __device__ __forceinline__ void st16(void* p, uint4 v) {
-  if constexpr (MO == 1) {
+  if constexpr (MO == 3) {
+    st16_wt(p, v);
+  } else if constexpr (MO == 1) {
     ast64(p, ((uint64_t)v.y << 32) | v.x);
     ast64((uint8_t*)p + 8, ((uint64_t)v.w << 32) | v.z);
   } else {

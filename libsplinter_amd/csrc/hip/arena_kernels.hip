@@ -216,7 +216,7 @@ __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys
 // U ops per lane per round: U claims (or lookups) in flight, then ONE agent
 // release (writers) / acquire (readers) per wave for all of them.  EAGAIN ops
 // fall back to the single-op path with backoff.
-template <int U, int B>
+template <int U, int B, bool WT = false>
 __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
                                                        const uint8_t* vals, int vstride, const uint32_t* lens, long n,
                                                        int32_t* status, int max_retry, uint64_t* stats, Seg seg) {
@@ -246,15 +246,21 @@ __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* ke
     }
 #pragma unroll
     for (int j = 0; j < U; ++j)
-      if (c[j].rc == kOk) write_set<0>(a, c[j], vals + (r0 + j) * (long)vstride, len[j], scrub, hybrid);
-    // ONE agent release per WORKGROUP: every wave's payload stores have reached the (shared) XCD L2
-    // once its vmcnt drains; the barrier then lets one lane write that L2 back (buffer_wbl2) for all
-    // of them before any wave publishes an epoch.  The release is serialised per XCD (~1.7 us), so
-    // this is 4x fewer serialised write-backs than one per wave.
-    drain();
-    __syncthreads();
-    if (threadIdx.x == 0) release();
-    __syncthreads();
+      if (c[j].rc == kOk) write_set<WT ? 3 : 0>(a, c[j], vals + (r0 + j) * (long)vstride, len[j], scrub, hybrid);
+    if constexpr (WT) {
+      // write-through payload: each wave's own drain publishes its sc1 stores (no L2 write-back,
+      // no workgroup barrier: every lane publishes only its own slots)
+      drain();
+    } else {
+      // ONE agent release per WORKGROUP: every wave's payload stores have reached the (shared) XCD
+      // L2 once its vmcnt drains; the barrier then lets one lane write that L2 back (buffer_wbl2)
+      // for all of them before any wave publishes an epoch.  The release is serialised per XCD
+      // (~1.7 us), so this is 4x fewer serialised write-backs than one per wave.
+      drain();
+      __syncthreads();
+      if (threadIdx.x == 0) release();
+      __syncthreads();
+    }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       const long i = r0 + j;
@@ -707,10 +713,17 @@ int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_
   const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1};
   const int mo = arena_mo();
   const int u = arena_rounds(), b = arena_block();
+  static const int wt = env_int("SPLINTER_ARENA_WT", 0);  // write-through: measured slower (profiles/r1_kv_writethrough.md)
 #define SPL_SET_ROUNDS(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_set_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
-  if (u == 2 && b == 256) SPL_SET_ROUNDS(2, 256);
+  if (wt && u == 4 && b == 256)
+    hipLaunchKernelGGL((k_set_rounds<4, 256, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
+                       kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+  else if (wt && u == 2 && b == 256)
+    hipLaunchKernelGGL((k_set_rounds<2, 256, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
+                       kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+  else if (u == 2 && b == 256) SPL_SET_ROUNDS(2, 256);
   else if (u == 2) SPL_SET_ROUNDS(2, 512);
   else if (u == 4 && b == 256) SPL_SET_ROUNDS(4, 256);
   else if (u == 4) SPL_SET_ROUNDS(4, 512);

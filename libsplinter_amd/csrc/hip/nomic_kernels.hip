@@ -338,38 +338,50 @@ __global__ __launch_bounds__(256) void k_attn2(const uint16_t* __restrict__ qkv,
           s[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[qb][kk], s[kb][qb], 0, 0, 0);
       }
     }
-    // ---- online softmax, one query per lane column
+    // ---- online softmax, one query per lane column.  Max on the raw scores (scale > 0), one
+    // FMA per score into the exp2 domain, raw v_exp_f32 (no denormal fix-up: p underflows to 0),
+    // key mask only on the sequence's partial last tile, and the deferred rescale of T13
+    // (cdna_hip_programming.md §5.5): the running max moves only when some query's tile max
+    // exceeds it by more than kThr, so P <= 2^kThr and the O/l rescale is skipped on most tiles
+    // (decided before this tile's P V, after the previous tile's: the textbook order).
+    constexpr float kThr = 8.f;
+    const bool full = k0 + 64 <= len;
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
+      if (!full) {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (k0 + kb * 16 + 4 * g + r >= len) s[kb][qb][r] = -1e30f;
+      }
       float mx = -1e30f;
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool valid = k0 + kb * 16 + 4 * g + r < len;
-          const float v = valid ? s[kb][qb][r] * scale_log2 : -1e30f;
-          s[kb][qb][r] = v;
-          mx = fmaxf(mx, v);
-        }
+      for (int kb = 0; kb < 4; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][qb][0], s[kb][qb][1])), fmaxf(s[kb][qb][2], s[kb][qb][3]));
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      const float mn = fmaxf(m[qb], mx);
-      const float alpha = exp2f(m[qb] - mn);
-      m[qb] = mn;
+      const float mxs = mx * scale_log2;
+      if (!__all(mxs - m[qb] <= kThr)) {  // wave-uniform: rescale O and l once to the new max
+        const float mn = fmaxf(m[qb], mxs);
+        const float alpha = __builtin_amdgcn_exp2f(m[qb] - mn);
+        m[qb] = mn;
+        l[qb] *= alpha;
+#pragma unroll
+        for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+      }
+      const float nm = -m[qb];
       float ps = 0.f;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float p = exp2f(s[kb][qb][r] - mn);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][qb][r], scale_log2, nm));
           s[kb][qb][r] = p;
           ps += p;
         }
       ps += __shfl_xor(ps, 16, 64);
       ps += __shfl_xor(ps, 32, 64);
-      l[qb] = l[qb] * alpha + ps;
-#pragma unroll
-      for (int db = 0; db < 4; ++db) o[db][qb] *= alpha;
+      l[qb] += ps;
     }
     // ---- O^T += V^T P^T, two 32-key steps
 #pragma unroll

@@ -47,6 +47,9 @@ def parse():
     p.add_argument("--embed-batch", type=int, default=64, help="documents per rank per step")
     p.add_argument("--embed-seq", type=int, default=512)
     p.add_argument("--verify", type=int, default=20000)
+    p.add_argument("--kv-cus", type=int, default=0,
+                   help="N>0: overlap the KV and embed phases with the KV streams confined to N CUs per XCD "
+                        "and the encoder to the rest (hipExtStreamCreateWithCUMask); 0 = phases back to back")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: "
                    "ranks may share a GPU, collectives staged through the host)")
     return p.parse_args()
@@ -141,6 +144,12 @@ def main():
     # the serial one (profiles/r1_mixed_overlap.md).
     from libsplinter_amd.utils.streams import stream as hip_stream
     s_get, s_set = hip_stream("high"), hip_stream("normal")
+    s_emb = None
+    if args.kv_cus and world == 1:
+        from libsplinter_amd.utils.streams import cu_mask_bits, masked_stream
+        kv_bits, emb_bits = cu_mask_bits(args.kv_cus), cu_mask_bits(32 - args.kv_cus, args.kv_cus)
+        s_get, s_set, s_emb = masked_stream(kv_bits), masked_stream(kv_bits), masked_stream(emb_bits)
+        log(f"[bench] overlapped phases: KV on {len(kv_bits)} CUs, encoder on {len(emb_bits)} CUs")
     stats = arena.stats
 
     def step_local(i):
@@ -153,10 +162,20 @@ def main():
                 arena.set(SK, SV, SL)
             with torch.cuda.stream(s_get):
                 arena.get(GK, out=gout)
+            if s_emb is None:
+                cur.wait_stream(s_set)
+                cur.wait_stream(s_get)
+        if embedder is not None:
+            if s_emb is None:
+                embedder.run()
+            else:
+                s_emb.wait_stream(cur)
+                with torch.cuda.stream(s_emb):
+                    embedder.run()
+                cur.wait_stream(s_emb)
+        if s_emb is not None and n_set:
             cur.wait_stream(s_set)
             cur.wait_stream(s_get)
-        if embedder is not None:
-            embedder.run()
 
     # N > 1: a host-sync-free software pipeline (parallel/routed.py).  Per step i:
     #   s_req : pack + request all-to-alls of batch i         (overlaps embed_i)

@@ -100,16 +100,26 @@ __device__ __forceinline__ void release() {
 // ------------------------------------------------------------- keys ----
 // A key arrives as a NUL-padded record of `kstride` bytes (16/32/48/64).
 // Canonical form: first 63 bytes, NUL padded to 64, FNV-1a over its length.
-struct Key {
-  uint32_t w[16];  // canonical key words (registers: every index is static)
+// KW = key words held in registers: a batch whose records are <= 4*KW bytes
+// (kstride 16 -> KW 4) keeps only those words live, the rest are the constant
+// 0 (word(i) below), which frees 12 VGPRs per key for occupancy in the
+// latency-bound batch kernels (U keys per lane).
+template <int KW = 16>
+struct KeyT {
+  static_assert(KW == 4 || KW == 8 || KW == 16, "key words");
+  uint32_t w[KW];  // canonical key words (registers: every index is static)
   uint32_t len;
   uint64_t hash;
+  __device__ __forceinline__ uint32_t word(int i) const { return i < KW ? w[i < KW ? i : 0] : 0u; }
+  __device__ __forceinline__ uint64_t qword(int q) const { return ((uint64_t)word(2 * q + 1) << 32) | word(2 * q); }
 };
+using Key = KeyT<16>;
 
-__device__ __forceinline__ void load_key(Key& k, const char* rec, int kstride) {
+template <int KW>
+__device__ __forceinline__ void load_key(KeyT<KW>& k, const char* rec, int kstride) {
   const uint4* r = (const uint4*)rec;
 #pragma unroll
-  for (int c = 0; c < 4; ++c) {
+  for (int c = 0; c < KW / 4; ++c) {
     uint4 v = (c * 16 < kstride) ? r[c] : make_uint4(0, 0, 0, 0);
     k.w[4 * c + 0] = v.x; k.w[4 * c + 1] = v.y; k.w[4 * c + 2] = v.z; k.w[4 * c + 3] = v.w;
   }
@@ -117,7 +127,7 @@ __device__ __forceinline__ void load_key(Key& k, const char* rec, int kstride) {
   uint32_t len = 0;
   bool live = true;
 #pragma unroll
-  for (int wi = 0; wi < 16; ++wi) {
+  for (int wi = 0; wi < KW; ++wi) {
     if (wi * 4 < kstride) {
 #pragma unroll
       for (int b = 0; b < 4; ++b) {
@@ -128,7 +138,7 @@ __device__ __forceinline__ void load_key(Key& k, const char* rec, int kstride) {
     }
   }
 #pragma unroll
-  for (int wi = 0; wi < 16; ++wi) {  // zero every byte at or past len
+  for (int wi = 0; wi < KW; ++wi) {  // zero every byte at or past len
     const int keep = (int)len - 4 * wi;
     const uint32_t m = keep >= 4 ? 0xffffffffu : keep <= 0 ? 0u : ((1u << (8 * keep)) - 1u);
     k.w[wi] &= m;
@@ -139,24 +149,28 @@ __device__ __forceinline__ void load_key(Key& k, const char* rec, int kstride) {
 
 // Compare the stored key with ours through sc1 loads, 8 bytes at a time, up
 // to and including our terminating NUL (stored keys are NUL padded).
-__device__ __forceinline__ bool key_eq(const uint8_t* slot, const Key& k) {
+template <int KW>
+__device__ __forceinline__ bool key_eq(const uint8_t* slot, const KeyT<KW>& k) {
   const uint8_t* sk = slot + kOffKey;
   const uint32_t nq = (k.len >> 3) + 1;  // 8-byte words holding the key + NUL
   bool eq = true;
+  // a KW-word key is at most 4*KW bytes long: its NUL lies within q-word KW/2
+  constexpr int kMaxQ = KW / 2 + 1 < 8 ? KW / 2 + 1 : 8;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) {
+  for (int q = 0; q < kMaxQ; ++q) {
     if ((uint32_t)q < nq) {
       const uint64_t v = ald64(sk + 8 * q);
-      eq = eq && v == (((uint64_t)k.w[2 * q + 1] << 32) | k.w[2 * q]);
+      eq = eq && v == k.qword(q);
     }
   }
   return eq;
 }
 
-__device__ __forceinline__ void store_key(uint8_t* slot, const Key& k) {
+template <int KW>
+__device__ __forceinline__ void store_key(uint8_t* slot, const KeyT<KW>& k) {
   uint4* d = (uint4*)(slot + kOffKey);
 #pragma unroll
-  for (int c = 0; c < 4; ++c) d[c] = make_uint4(k.w[4 * c], k.w[4 * c + 1], k.w[4 * c + 2], k.w[4 * c + 3]);
+  for (int c = 0; c < 4; ++c) d[c] = make_uint4(k.word(4 * c), k.word(4 * c + 1), k.word(4 * c + 2), k.word(4 * c + 3));
 }
 
 __device__ __forceinline__ uint64_t slot_hash(const uint8_t* s) { return ald64(s + kOffHash); }
@@ -164,7 +178,8 @@ __device__ __forceinline__ uint64_t slot_epoch(const uint8_t* s) { return ald64(
 __device__ __forceinline__ uint64_t* epoch_ptr(uint8_t* s) { return (uint64_t*)(s + kOffEpoch); }
 
 // Locate `k`; returns the slot index or -1.  Pure lookup (no seqlock).
-__device__ __forceinline__ long find(const Arena& a, const Key& k) {
+template <int KW>
+__device__ __forceinline__ long find(const Arena& a, const KeyT<KW>& k) {
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
@@ -309,7 +324,8 @@ __device__ __forceinline__ void clear_claim(const Arena& a, long idx) {
   aadd64(epoch_ptr(s), 1);
 }
 
-__device__ Claim claim_set(const Arena& a, const Key& k) {
+template <int KW>
+__device__ Claim claim_set(const Arena& a, const KeyT<KW>& k) {
   const size_t home = (size_t)(k.hash % a.slots);
   long free_idx = -1;
   uint64_t free_ep = 0;
@@ -343,7 +359,7 @@ __device__ Claim claim_set(const Arena& a, const Key& k) {
   // early publication: marker, key, then hash (each visible before the next)
   ast32(fs + kOffValLen, kInsertMark);
 #pragma unroll
-  for (int q = 0; q < 8; ++q) ast64(fs + kOffKey + 8 * q, ((uint64_t)k.w[2 * q + 1] << 32) | k.w[2 * q]);
+  for (int q = 0; q < 8; ++q) ast64(fs + kOffKey + 8 * q, k.qword(q));
   drain();
   ast64(fs + kOffHash, k.hash);
   drain();
@@ -410,8 +426,8 @@ __device__ __forceinline__ void write_set(const Arena& a, const Claim& c, const 
 __device__ __forceinline__ void finish_set(const Arena& a, const Claim& c) { aadd64(epoch_ptr(a.slot((size_t)c.idx)), 1); }
 
 // Single-op SET (insert or update) with its own release.
-template <int MO = 0>
-__device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint32_t len, long* out_idx) {
+template <int MO = 0, int KW>
+__device__ int32_t set_op(const Arena& a, const KeyT<KW>& k, const uint8_t* val, uint32_t len, long* out_idx) {
   if (len == 0 || len > a.max_val) return kMsgSize;
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
@@ -426,8 +442,8 @@ __device__ int32_t set_op(const Arena& a, const Key& k, const uint8_t* val, uint
 }
 
 // GET: seqlock read into out (may be null: size query).
-template <int MO = 0>
-__device__ int32_t get_op(const Arena& a, const Key& k, uint8_t* out, uint32_t out_cap, uint32_t* out_len) {
+template <int MO = 0, int KW>
+__device__ int32_t get_op(const Arena& a, const KeyT<KW>& k, uint8_t* out, uint32_t out_cap, uint32_t* out_len) {
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
@@ -461,7 +477,8 @@ __device__ int32_t get_op(const Arena& a, const Key& k, uint8_t* out, uint32_t o
 // words of each probed slot are loaded together; returns the slot index with
 // its epoch / length as observed, or -1 for a miss.  The caller validates the
 // whole read afterwards (key words again with the data, epoch unchanged).
-__device__ __forceinline__ long locate_peek(const Arena& a, const Key& k, uint64_t* e1, uint32_t* len) {
+template <int KW>
+__device__ __forceinline__ long locate_peek(const Arena& a, const KeyT<KW>& k, uint64_t* e1, uint32_t* len) {
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
@@ -495,7 +512,8 @@ __device__ __forceinline__ void copy_chunks(uint4* dst, const uint4* src, uint32
 // Batched GET, phase helpers (see k_get_rounds): locate without the seqlock,
 // then one acquire for all of a lane's ops, then copy, then validate.
 // Returns the slot index holding k (possibly mid-write), or -1 for a miss.
-__device__ __forceinline__ long locate(const Arena& a, const Key& k) {
+template <int KW>
+__device__ __forceinline__ long locate(const Arena& a, const KeyT<KW>& k) {
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
@@ -511,7 +529,8 @@ __device__ __forceinline__ long locate(const Arena& a, const Key& k) {
 }
 
 // UNSET: returns the old length (>= 0) or a negative status.
-__device__ int32_t unset_op(const Arena& a, const Key& k, long* out_idx) {
+template <int KW>
+__device__ int32_t unset_op(const Arena& a, const KeyT<KW>& k, long* out_idx) {
   const long i = find(a, k);
   if (i < 0) return kNoEnt;
   uint8_t* s = a.slot((size_t)i);
@@ -547,7 +566,8 @@ __device__ int32_t unset_op(const Arena& a, const Key& k, long* out_idx) {
 }
 
 // In-place u64 integer op under the seqlock.
-__device__ int32_t integer_op(const Arena& a, const Key& k, int op, uint64_t m, uint64_t* result, long* out_idx) {
+template <int KW>
+__device__ int32_t integer_op(const Arena& a, const KeyT<KW>& k, int op, uint64_t m, uint64_t* result, long* out_idx) {
   const long i = find(a, k);
   if (i < 0) return kNoEnt;
   uint8_t* s = a.slot((size_t)i);

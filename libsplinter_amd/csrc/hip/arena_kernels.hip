@@ -216,8 +216,8 @@ __global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys
 // U ops per lane per round: U claims (or lookups) in flight, then ONE agent
 // release (writers) / acquire (readers) per wave for all of them.  EAGAIN ops
 // fall back to the single-op path with backoff.
-template <int U, int B, bool WT = false>
-__global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
+template <int U, int B, bool WT = false, int KW = 16, int OCC = 1>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
                                                        const uint8_t* vals, int vstride, const uint32_t* lens, long n,
                                                        int32_t* status, int max_retry, uint64_t* stats, Seg seg) {
   const Arena a = to_dev(aa);
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* ke
   const long per_block = (long)blockDim.x * U;
   for (long base = blockIdx.x * per_block; base < n; base += (long)gridDim.x * per_block) {
     const long r0 = base + (long)threadIdx.x * U;
-    Key k[U];
+    KeyT<KW> k[U];
     Claim c[U];
     uint32_t len[U];
 #pragma unroll
@@ -287,7 +287,7 @@ __global__ __launch_bounds__(B) void k_set_rounds(spl_arena_t aa, const char* ke
   flush_stats(a, st, stats, muts);
 }
 
-template <int U, int B, int GV = 1>
+template <int U, int B, int GV = 1, int KW = 16>
 __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                        int ostride, uint32_t* out_lens, long n, int32_t* status,
                                                        int max_retry, uint64_t* stats, Seg seg) {
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
   const long per_block = (long)blockDim.x * U;
   for (long base = blockIdx.x * per_block; base < n; base += (long)gridDim.x * per_block) {
     const long r0 = base + (long)threadIdx.x * U;
-    Key k[U];
+    KeyT<KW> k[U];
     long sidx[U];
     uint64_t e1[U];
     int32_t rc[U];
@@ -717,7 +717,23 @@ int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_
 #define SPL_SET_ROUNDS(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_set_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
-  if (wt && u == 4 && b == 256)
+  // SPLINTER_ARENA_KW4=1: 16-B key records with 4 key words per op in registers instead of 16
+  // (153 -> 128 VGPRs, 2 -> 4 waves/SIMD).  Measured SLOWER at 100M keys (2.22 -> 1.96 G ops/s,
+  // twice the EAGAIN retries): more ops in flight do not help these kernels
+  // (profiles/r1_kv_occupancy.md), so it is off by default.
+  static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);
+  if (kw4 && kstride == 16 && !wt && b == 256 && (u == 4 || u == 8)) {
+    static const int occ = env_int("SPLINTER_ARENA_SETOCC", 4);
+    if (u == 4 && occ == 4)
+      hipLaunchKernelGGL((k_set_rounds<4, 256, false, 4, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
+                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (u == 4)
+      hipLaunchKernelGGL((k_set_rounds<4, 256, false, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
+                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else
+      hipLaunchKernelGGL((k_set_rounds<8, 256, false, 4>), dim3(grid_for_b((n + 7) / 8, 256)), dim3(256), 0, s, a,
+                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+  } else if (wt && u == 4 && b == 256)
     hipLaunchKernelGGL((k_set_rounds<4, 256, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
                        kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
   else if (wt && u == 2 && b == 256)
@@ -759,7 +775,15 @@ int spl_arena_get_seg(spl_arena_t a, const char* keys, int kstride, uint8_t* out
   hipLaunchKernelGGL((k_get_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
   static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
-  if (u == 2 && b == 256 && gv == 2)
+  static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);  // see spl_arena_set_seg
+  if (kw4 && kstride == 16 && gv == 1 && b == 256 && (u == 2 || u == 4)) {
+    if (u == 2)
+      hipLaunchKernelGGL((k_get_rounds<2, 256, 1, 4>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
+                         kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else
+      hipLaunchKernelGGL((k_get_rounds<4, 256, 1, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
+                         kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+  } else if (u == 2 && b == 256 && gv == 2)
     hipLaunchKernelGGL((k_get_rounds<2, 256, 2>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
                        kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
   else if (u == 2 && b == 256) SPL_GET_ROUNDS(2, 256);

@@ -88,6 +88,12 @@ struct EpiArgs {
   int gn;                // n-tiles per band of the tile order (remap_tile)
 };
 
+// up * silu(g) with a hardware reciprocal and exp2 (v_rcp_f32 + v_exp_f32: no IEEE division
+// sequence in the epilogue; ~1 ulp, far below the bf16 output rounding)
+__device__ __forceinline__ float swiglu(float up, float g) {
+  return up * g * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-g * 1.4426950408889634f));
+}
+
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int K,
@@ -192,7 +198,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
       for (int e = 0; e < 8; ++e) {
         const float up = E[row * kEpiStride + uc + e];
         const float g = E[row * kEpiStride + uc + 16 + e];
-        o[e] = up * (g / (1.f + __expf(-g)));
+        o[e] = swiglu(up, g);
       }
       uint4 w;
       w.x = f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
@@ -492,7 +498,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
         for (int e = 0; e < 8; ++e) {
           const float up = E[row * kEpi2Stride + uc + e];
           const float g = E[row * kEpi2Stride + uc + 16 + e];
-          o[e] = up * (g / (1.f + __expf(-g)));
+          o[e] = swiglu(up, g);
         }
         *(uint4*)(ep.out + gm * ep.ldo + (long)nt * 128 + oc) = pack8(o);
       }
@@ -759,7 +765,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
 #pragma unroll
               for (int e = 0; e < 4; ++e) {
                 const float up = acc[qm][qn][i][0][e], gt = acc[qm][qn][i][1][e];
-                o[e] = up * (gt / (1.f + __expf(-gt)));
+                o[e] = swiglu(up, gt);
               }
               *(uint2*)(ep.out + m * ep.ldo + nb0 / 2 + fq * 4) = pack4(o);
             } else if constexpr (MODE == NOMIC_EPI_ROPE) {

@@ -226,7 +226,7 @@ class CausalLM:
 
     @staticmethod
     def _split_ug(y: torch.Tensor):
-        g = y.reshape(y.shape[0], -1, 2, 64)
+        g = y.reshape(y.shape[0], -1, 2, 16)  # pack_upgate: [up16 | gate16] per 16 outputs
         return g[:, :, 0].reshape(y.shape[0], -1), g[:, :, 1].reshape(y.shape[0], -1)
 
     def _rms(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:

@@ -47,7 +47,7 @@ build/hip/%.o: $(SRC)/hip/%.hip $(HIP_HDRS) | build/hip
 # attention: keep MFMA accumulators in VGPRs (the default AGPR form costs 128 v_accvgpr copies per
 # K/V tile around the online-softmax rescale); per file: the flag crashes the compiler on
 # search_kernels.hip (ROCm 7.2)
-build/hip/nomic_kernels.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
+build/hip/nomic_kernels.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans
 
 $(LIB)/libsplinter_hip.so: $(HIP_OBJS) $(LIB)/libsplinter.so | $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN' $(LDLIBS)

@@ -258,14 +258,49 @@ typedef __attribute__((address_space(3))) v4i16 lds_v4i16;
 __device__ __forceinline__ int ksw(int key, int c) { return c ^ (key & 7); }
 __device__ __forceinline__ int vsw(int key, int c) { return c ^ (((key >> 1) & 3) << 1); }
 
-__global__ __launch_bounds__(256) void k_attn2(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+// W = minimum waves per SIMD the register allocation must allow (0: unconstrained, 236 VGPRs ->
+// 2 waves/SIMD; 3: 168 VGPRs, 3 waves/SIMD, 12 waves per CU to hide the softmax/LDS latency)
+// XR: 1-D grid of nqb*heads blocks through the bijective XCD remap (guide §5 T1), so the q-blocks
+// of one (sequence, head) -- which all stream the same K/V -- run on ONE XCD and share its L2
+// (with the 2-D grid consecutive q-blocks are dealt round-robin to 4 different XCDs and every
+// K/V tile is fetched from the fabric once per q-block).
+// Cross-lane reductions over the 4 lane groups g = lane >> 4 (a value of query column li sits in
+// lanes li, li+16, li+32, li+48): v_permlane16_swap / v_permlane32_swap (gfx950 VALU half-row
+// exchanges) instead of two ds_bpermute round trips through the LDS pipe per reduction.  With
+// vdst = src = x the swap returns the partner's value in one of its two results and x in the other.
+__device__ __forceinline__ float xg_max(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float xg_sum(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// OPT: permlane reductions, packed (v_pk_fma/v_pk_add) score scaling and row sums, and K/V
+// source pointers advanced per tile instead of recomputed with 64-bit multiplies.
+template <int W, bool XR = false, bool OPT = false>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1))) void k_attn2(
+    const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
                                                int heads, float scale_log2) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][64 * 128];  // [buf][K | V][key * 128 B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int seq = qblocks[2 * blockIdx.x], qstart = qblocks[2 * blockIdx.x + 1];
-  const int head = blockIdx.y;
+  int qbi = blockIdx.x, head = blockIdx.y;
+  if constexpr (XR) {
+    const int nwg = gridDim.x, orig = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+    const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+    const int nqb = nwg / heads;
+    head = lid / nqb;
+    qbi = lid - head * nqb;
+  }
+  const int seq = qblocks[2 * qbi], qstart = qblocks[2 * qbi + 1];
   const long s0 = cu[seq], len = cu[seq + 1] - s0;
   const long ld = 3L * heads * HD;
   const uint16_t* Qg = qkv + head * HD;
@@ -289,13 +324,28 @@ __global__ __launch_bounds__(256) void k_attn2(const uint16_t* __restrict__ qkv,
   float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
 
   uint4 rk[2], rv[2];
+  // OPT: per-lane K/V source pointers of tile 0, advanced by 64 rows per tile
+  const uint16_t* kp[2];
+  const uint16_t* vp[2];
+#pragma unroll
+  for (int it = 0; it < 2; ++it) {
+    const int c = tid + it * 256, key = c >> 3, ch = c & 7;
+    kp[it] = Kg + (s0 + key) * ld + ch * 8;
+    vp[it] = Vg + (s0 + key) * ld + ch * 8;
+  }
+  const long tstride = 64 * ld;
   auto gload = [&](long k0) {
 #pragma unroll
     for (int it = 0; it < 2; ++it) {
       const int c = tid + it * 256, key = c >> 3, ch = c & 7;
       if (k0 + key < len) {
-        rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
-        rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
+        if constexpr (OPT) {
+          rk[it] = *(const uint4*)(kp[it] + (k0 >> 6) * tstride);
+          rv[it] = *(const uint4*)(vp[it] + (k0 >> 6) * tstride);
+        } else {
+          rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
+          rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
+        }
       } else {
         rk[it] = make_uint4(0, 0, 0, 0);
         rv[it] = make_uint4(0, 0, 0, 0);
@@ -358,8 +408,12 @@ __global__ __launch_bounds__(256) void k_attn2(const uint16_t* __restrict__ qkv,
       float mx = -1e30f;
 #pragma unroll
       for (int kb = 0; kb < 4; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][qb][0], s[kb][qb][1])), fmaxf(s[kb][qb][2], s[kb][qb][3]));
-      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      if constexpr (OPT) {
+        mx = xg_max(mx);
+      } else {
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      }
       const float mxs = mx * scale_log2;
       if (!__all(mxs - m[qb] <= kThr)) {  // wave-uniform: rescale O and l once to the new max
         const float mn = fmaxf(m[qb], mxs);
@@ -371,16 +425,34 @@ __global__ __launch_bounds__(256) void k_attn2(const uint16_t* __restrict__ qkv,
       }
       const float nm = -m[qb];
       float ps = 0.f;
+      if constexpr (OPT) {
+        const f32x2 sc2 = {scale_log2, scale_log2}, nm2 = {nm, nm};
+        f32x2 acc2 = {0.f, 0.f};
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][qb][r], scale_log2, nm));
-          s[kb][qb][r] = p;
-          ps += p;
-        }
-      ps += __shfl_xor(ps, 16, 64);
-      ps += __shfl_xor(ps, 32, 64);
+          for (int h = 0; h < 2; ++h) {
+            f32x2 x = {s[kb][qb][2 * h], s[kb][qb][2 * h + 1]};
+            x = x * sc2 + nm2;  // v_pk_fma_f32
+            x.x = __builtin_amdgcn_exp2f(x.x);
+            x.y = __builtin_amdgcn_exp2f(x.y);
+            s[kb][qb][2 * h] = x.x;
+            s[kb][qb][2 * h + 1] = x.y;
+            acc2 += x;  // v_pk_add_f32
+          }
+        ps = xg_sum(acc2.x + acc2.y);
+      } else {
+#pragma unroll
+        for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][qb][r], scale_log2, nm));
+            s[kb][qb][r] = p;
+            ps += p;
+          }
+        ps += __shfl_xor(ps, 16, 64);
+        ps += __shfl_xor(ps, 32, 64);
+      }
       l[qb] += ps;
     }
     // ---- O^T += V^T P^T, two 32-key steps
@@ -623,7 +695,7 @@ int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, 
   return (int)hipGetLastError();
 }
 
-static int g_attn_variant = 2;
+static int g_attn_variant = 6;  // measured: profiles/r1_attn_ab.jsonl (6: permlane + packed softmax, XCD remap)
 
 int nomic_attention_set_variant(int v) {
   const int prev = g_attn_variant;
@@ -636,9 +708,21 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   if (nqb <= 0) return 0;
   if (heads * HD * 3 % 8) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  if (g_attn_variant == 2)
-    hipLaunchKernelGGL(k_attn2, dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks,
-                       heads, scale_log2);
+  if (g_attn_variant == 5)
+    hipLaunchKernelGGL((k_attn2<0, false, true>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv,
+                       (uint16_t*)out, cu, qblocks, heads, scale_log2);
+  else if (g_attn_variant == 6)
+    hipLaunchKernelGGL((k_attn2<0, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
+                       (uint16_t*)out, cu, qblocks, heads, scale_log2);
+  else if (g_attn_variant == 4)
+    hipLaunchKernelGGL((k_attn2<0, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
+                       cu, qblocks, heads, scale_log2);
+  else if (g_attn_variant == 2)
+    hipLaunchKernelGGL((k_attn2<0>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+                       qblocks, heads, scale_log2);
+  else if (g_attn_variant == 3)
+    hipLaunchKernelGGL((k_attn2<3>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+                       qblocks, heads, scale_log2);
   else
     hipLaunchKernelGGL(k_attn, dim3(2 * nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);

@@ -29,9 +29,10 @@ def main():
         _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
                                0.125, _stream()), "attn")
 
-    times = {1: [], 2: []}
+    VARIANTS = (6, 5, 4, 3, 2, 1)
+    times = {v: [] for v in VARIANTS}
     for _ in range(a.rounds):
-        for v in (2, 1):
+        for v in VARIANTS:
             L.nomic_attention_set_variant(v)
             run()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -43,7 +44,7 @@ def main():
             times[v].append(s.elapsed_time(e) / a.iters)
     L.nomic_attention_set_variant(2)
     fl = 4.0 * a.docs * a.seq * a.seq * 64 * 12
-    for v in (2, 1):
+    for v in VARIANTS:
         t = np.array(times[v])
         print(json.dumps({"kernel": f"attn_v{v}", "docs": a.docs, "seq": a.seq, "ms_median": float(np.median(t)),
                           "tflops_median": fl / np.median(t) / 1e9, "tflops_best": fl / t.min() / 1e9}))

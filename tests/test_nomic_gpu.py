@@ -101,7 +101,7 @@ def test_gemm_swiglu_and_rope(L):
     assert _rel(qkv[:M].float(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("variant", [2, 1])
+@pytest.mark.parametrize("variant", [6, 5, 4, 3, 2, 1])
 @pytest.mark.parametrize("spike", [False, True])
 def test_attention_varlen(L0, variant, spike):
     L = L0

@@ -368,6 +368,187 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
   flush_stats(a, st, stats, 0);
 }
 
+// ------------------------------------------------ carried-retry rounds -----
+// Same rounds as above, but an op that meets a contended slot (EAGAIN) is NOT retried inline:
+// it stays in its lane's slot and is retried in the lane's next round, while the lane's other
+// slots take new ops.  Retries thus ride the batched rounds (one release / acquire per
+// workgroup round) instead of stalling the whole wave in a backoff + single-op path with its
+// own L2 write-back, and a round of other work is the natural backoff.  Attempts per op are
+// bounded by 1 + max_retry as before; the round loop is block-uniform (barriers).
+// Lane sequence: op c of a lane is first + (c / U) * stride + c % U (monotone in c), i.e. the
+// grid-stride order of the rounds kernels.
+template <int U, int B, int KW = 16>
+__global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
+                                                 int vstride, const uint32_t* lens, long n, int32_t* status,
+                                                 int max_retry, uint64_t* stats, Seg seg) {
+  const Arena a = to_dev(aa);
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  Stats st;
+  uint64_t muts = 0;
+  const long stride = (long)gridDim.x * blockDim.x * U;
+  const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
+  long cursor = 0;
+  bool more = true;
+  KeyT<KW> k[U];
+  Claim c[U];
+  uint32_t len[U];
+  long op[U];
+  int tries[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) op[j] = -1;
+  for (;;) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      while (op[j] < 0 && more) {  // refill: next live op of this lane's sequence
+        const long i = first + (cursor / U) * stride + (cursor % U);
+        ++cursor;
+        if (i >= n) { more = false; break; }
+        if (!seg.live(i)) { if (status) status[i] = kInval; continue; }
+        op[j] = i;
+        tries[j] = 0;
+        load_key(k[j], keys + i * (long)kstride, kstride);
+        len[j] = lens[i];
+      }
+    }
+    bool busy = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) busy |= op[j] >= 0;
+    if (!__syncthreads_or(busy)) break;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      c[j] = Claim{-1, false, kInval};
+      if (op[j] >= 0) {
+        ++st.attempts;
+        ++tries[j];
+        if (len[j] == 0 || len[j] > a.max_val) c[j].rc = kMsgSize;
+        else c[j] = claim_set(a, k[j]);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (op[j] >= 0 && c[j].rc == kOk) write_set<0>(a, c[j], vals + op[j] * (long)vstride, len[j], scrub, hybrid);
+    drain();
+    __syncthreads();
+    if (threadIdx.x == 0) release();
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (op[j] < 0) continue;
+      const int32_t rc = c[j].rc;
+      if (rc == kAgain) {
+        ++st.again;
+        if (tries[j] <= max_retry) continue;  // carried into the next round
+      }
+      if (rc == kOk) {
+        finish_set(a, c[j]);
+        ++st.ok;
+        ++muts;
+        pulse(a, a.slot((size_t)c[j].idx));
+        mark_dirty(a, (size_t)c[j].idx);
+      }
+      if (status) status[op[j]] = rc;
+      op[j] = -1;
+    }
+  }
+  flush_stats(a, st, stats, muts);
+}
+
+template <int U, int B, int KW = 16>
+__global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
+                                                 int ostride, uint32_t* out_lens, long n, int32_t* status,
+                                                 int max_retry, uint64_t* stats, Seg seg) {
+  const Arena a = to_dev(aa);
+  Stats st;
+  const long stride = (long)gridDim.x * blockDim.x * U;
+  const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
+  long cursor = 0;
+  bool more = true;
+  KeyT<KW> k[U];
+  long op[U], sidx[U];
+  uint64_t e1[U];
+  int32_t rc[U];
+  uint32_t len[U];
+  int tries[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) op[j] = -1;
+  for (;;) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      while (op[j] < 0 && more) {
+        const long i = first + (cursor / U) * stride + (cursor % U);
+        ++cursor;
+        if (i >= n) { more = false; break; }
+        if (!seg.live(i)) {
+          if (out_lens) out_lens[i] = 0;
+          if (status) status[i] = kInval;
+          continue;
+        }
+        op[j] = i;
+        tries[j] = 0;
+        load_key(k[j], keys + i * (long)kstride, kstride);
+      }
+    }
+    bool busy = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) busy |= op[j] >= 0;
+    if (!__syncthreads_or(busy)) break;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      rc[j] = kInval;
+      if (op[j] >= 0) {
+        ++st.attempts;
+        ++tries[j];
+        len[j] = 0;
+        sidx[j] = locate_peek(a, k[j], &e1[j], &len[j]);
+        rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
+      }
+    }
+    drain();
+    __syncthreads();
+    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (op[j] < 0 || rc[j] != kOk) continue;
+      const uint8_t* s = a.slot((size_t)sidx[j]);
+      if ((e1[j] & 1) || len[j] > a.max_val) { rc[j] = kAgain; continue; }
+      const bool keq = key_eq(s, k[j]);
+      if (out) {
+        if (len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
+        const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
+        uint4* dst = (uint4*)(out + op[j] * (long)ostride);
+        const uint32_t n16 = (len[j] + 15) >> 4;
+        for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
+      }
+      if (!keq) rc[j] = kAgain;
+    }
+    drain();
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (op[j] < 0 || rc[j] != kOk) continue;
+      const uint8_t* s = a.slot((size_t)sidx[j]);
+      const uint64_t e2 = slot_epoch(s), h2 = slot_hash(s);
+      if (e2 != e1[j] || h2 != k[j].hash) rc[j] = kAgain;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (op[j] < 0) continue;
+      const int32_t r = rc[j];
+      if (r == kAgain) {
+        ++st.again;
+        if (tries[j] <= max_retry) continue;
+      }
+      if (r == kOk) ++st.ok;
+      else if (r == kNoEnt) ++st.miss;
+      if (out_lens) out_lens[op[j]] = r == kOk ? len[j] : 0;
+      if (status) status[op[j]] = r;
+      op[j] = -1;
+    }
+  }
+  flush_stats(a, st, stats, 0);
+}
+
 // ------------------------------------------------------------- unset ----
 __global__ __launch_bounds__(kBlock) void k_unset(spl_arena_t aa, const char* keys, int kstride, long n,
                                                   int32_t* status, int max_retry) {
@@ -722,7 +903,15 @@ int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_
   // twice the EAGAIN retries): more ops in flight do not help these kernels
   // (profiles/r1_kv_occupancy.md), so it is off by default.
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);
-  if (kw4 && kstride == 16 && !wt && b == 256 && (u == 4 || u == 8)) {
+  static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);  // carried retries (k_set_carry)
+  if (carry && !wt && b == 256 && (u == 2 || u == 4)) {
+    if (u == 4)
+      hipLaunchKernelGGL((k_set_carry<4, 256>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys, kstride,
+                         vals, vstride, lens, n, status, max_retry, stats, seg);
+    else
+      hipLaunchKernelGGL((k_set_carry<2, 256>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys, kstride,
+                         vals, vstride, lens, n, status, max_retry, stats, seg);
+  } else if (kw4 && kstride == 16 && !wt && b == 256 && (u == 4 || u == 8)) {
     static const int occ = env_int("SPLINTER_ARENA_SETOCC", 4);
     if (u == 4 && occ == 4)
       hipLaunchKernelGGL((k_set_rounds<4, 256, false, 4, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
@@ -776,7 +965,15 @@ int spl_arena_get_seg(spl_arena_t a, const char* keys, int kstride, uint8_t* out
                      kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
   static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);  // see spl_arena_set_seg
-  if (kw4 && kstride == 16 && gv == 1 && b == 256 && (u == 2 || u == 4)) {
+  static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);
+  if (carry && gv == 1 && b == 256 && (u == 2 || u == 4)) {
+    if (u == 2)
+      hipLaunchKernelGGL((k_get_carry<2, 256>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys, kstride,
+                         out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else
+      hipLaunchKernelGGL((k_get_carry<4, 256>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys, kstride,
+                         out, ostride, out_lens, n, status, max_retry, stats, seg);
+  } else if (kw4 && kstride == 16 && gv == 1 && b == 256 && (u == 2 || u == 4)) {
     if (u == 2)
       hipLaunchKernelGGL((k_get_rounds<2, 256, 1, 4>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
                          kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);

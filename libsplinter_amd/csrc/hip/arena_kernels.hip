@@ -67,6 +67,10 @@ inline int arena_block() {
   static int b = env_int("SPLINTER_ARENA_BLOCK", 256);
   return b == 512 ? 512 : 256;
 }
+inline int arena_block_get() {
+  static int b = env_int("SPLINTER_ARENA_BLOCK_GET", env_int("SPLINTER_ARENA_BLOCK", 256));
+  return b == 512 ? 512 : 256;
+}
 
 inline int grid_for(long n) {
   long g = (n + kBlock - 1) / kBlock;
@@ -904,13 +908,18 @@ int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_
   // (profiles/r1_kv_occupancy.md), so it is off by default.
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);
   static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);  // carried retries (k_set_carry)
-  if (carry && !wt && b == 256 && (u == 2 || u == 4)) {
-    if (u == 4)
-      hipLaunchKernelGGL((k_set_carry<4, 256>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys, kstride,
-                         vals, vstride, lens, n, status, max_retry, stats, seg);
-    else
-      hipLaunchKernelGGL((k_set_carry<2, 256>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys, kstride,
-                         vals, vstride, lens, n, status, max_retry, stats, seg);
+  if (carry && !wt && (u == 2 || u == 4)) {
+#define SPL_SET_CARRY(U_, B_)                                                                                   \
+  hipLaunchKernelGGL((k_set_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
+                     kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
+    if (kw4 && kstride == 16 && u == 4 && b == 256)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
+                         kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (u == 4 && b == 256) SPL_SET_CARRY(4, 256);
+    else if (u == 4) SPL_SET_CARRY(4, 512);
+    else if (b == 256) SPL_SET_CARRY(2, 256);
+    else SPL_SET_CARRY(2, 512);
+#undef SPL_SET_CARRY
   } else if (kw4 && kstride == 16 && !wt && b == 256 && (u == 4 || u == 8)) {
     static const int occ = env_int("SPLINTER_ARENA_SETOCC", 4);
     if (u == 4 && occ == 4)
@@ -959,20 +968,25 @@ int spl_arena_get_seg(spl_arena_t a, const char* keys, int kstride, uint8_t* out
   if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
   const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1};
   const int mo = arena_mo();
-  const int u = arena_rounds_get(), b = arena_block();
+  const int u = arena_rounds_get(), b = arena_block_get();
 #define SPL_GET_ROUNDS(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_get_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
   static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);  // see spl_arena_set_seg
   static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);
-  if (carry && gv == 1 && b == 256 && (u == 2 || u == 4)) {
-    if (u == 2)
-      hipLaunchKernelGGL((k_get_carry<2, 256>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys, kstride,
-                         out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else
-      hipLaunchKernelGGL((k_get_carry<4, 256>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys, kstride,
-                         out, ostride, out_lens, n, status, max_retry, stats, seg);
+  if (carry && gv == 1 && (u == 2 || u == 4)) {
+#define SPL_GET_CARRY(U_, B_)                                                                                   \
+  hipLaunchKernelGGL((k_get_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
+                     kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
+    if (kw4 && kstride == 16 && u == 2 && b == 256)
+      hipLaunchKernelGGL((k_get_carry<2, 256, 4>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
+                         kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else if (u == 2 && b == 256) SPL_GET_CARRY(2, 256);
+    else if (u == 2) SPL_GET_CARRY(2, 512);
+    else if (b == 256) SPL_GET_CARRY(4, 256);
+    else SPL_GET_CARRY(4, 512);
+#undef SPL_GET_CARRY
   } else if (kw4 && kstride == 16 && gv == 1 && b == 256 && (u == 2 || u == 4)) {
     if (u == 2)
       hipLaunchKernelGGL((k_get_rounds<2, 256, 1, 4>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,

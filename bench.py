@@ -50,6 +50,8 @@ def parse():
     p.add_argument("--kv-cus", type=int, default=0,
                    help="N>0: overlap the KV and embed phases with the KV streams confined to N CUs per XCD "
                         "and the encoder to the rest (hipExtStreamCreateWithCUMask); 0 = phases back to back")
+    p.add_argument("--overlap", action="store_true",
+                   help="run the embed batch concurrently with the KV batches (own stream, all CUs)")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: "
                    "ranks may share a GPU, collectives staged through the host)")
     return p.parse_args()
@@ -145,6 +147,9 @@ def main():
     from libsplinter_amd.utils.streams import stream as hip_stream
     s_get, s_set = hip_stream("high"), hip_stream("normal")
     s_emb = None
+    if args.overlap and not args.kv_cus and world == 1:
+        s_emb = hip_stream("low")
+        log("[bench] overlapped phases on unmasked streams")
     if args.kv_cus and world == 1:
         from libsplinter_amd.utils.streams import cu_mask_bits, masked_stream
         kv_bits, emb_bits = cu_mask_bits(args.kv_cus), cu_mask_bits(32 - args.kv_cus, args.kv_cus)

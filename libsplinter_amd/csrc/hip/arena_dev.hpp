@@ -203,6 +203,16 @@ __device__ __forceinline__ void pulse(const Arena& a, const uint8_t* s) {
   }
 }
 
+// pulse with masks already in registers (Claim::wm / bl): no extra round trip at the end of a set
+__device__ __forceinline__ void pulse_masks(const Arena& a, uint64_t wm, uint64_t bl) {
+  splinter_header* H = a.hdr();
+  for (uint64_t m = wm; m; m &= m - 1) aadd64(&H->signal_groups[__builtin_ctzll(m)].counter, 1);
+  for (uint64_t m = bl; m; m &= m - 1) {
+    const uint8_t g = ald8(&H->bloom_watches[__builtin_ctzll(m)]);
+    if (g < SPLINTER_MAX_GROUPS) aadd64(&H->signal_groups[g].counter, 1);
+  }
+}
+
 __device__ __forceinline__ void mark_dirty(const Arena& a, size_t idx) {
   if (!(a.flags & 1u)) return;
   const size_t m = idx % kDirtyBits;
@@ -314,6 +324,7 @@ struct Claim {
   long idx;       // slot index (valid when rc == kOk)
   bool fresh;     // true: insert into a free slot
   int32_t rc;
+  uint64_t wm = 0, bl = 0;  // watcher mask / bloom labels read while holding the slot (pulse_masks)
 };
 
 __device__ __forceinline__ void clear_claim(const Arena& a, long idx) {
@@ -338,13 +349,16 @@ __device__ Claim claim_set(const Arena& a, const KeyT<KW>& k) {
     const bool keq = key_eq(s, k);
     if (sh == k.hash && keq) {  // update in place
       if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return Claim{-1, false, kAgain};
-      const uint64_t sh2 = slot_hash(s);  // re-check after the claim: hash + key together
+      // re-check after the claim: hash + key together, with the watcher mask and labels the
+      // set will pulse (same 128-B slot line, same round trip)
+      const uint64_t sh2 = slot_hash(s);
       const bool keq2 = key_eq(s, k);
+      const uint64_t wm = ald64(s + kOffWatch), bl = ald64(s + kOffBloom);
       if (sh2 != k.hash || !keq2) {  // raced with unset / reuse
         aadd64(epoch_ptr(s), 1);
         return Claim{-1, false, kAgain};
       }
-      return Claim{(long)idx, false, kOk};
+      return Claim{(long)idx, false, kOk, wm, bl};
     }
     if (sh == 0 && !(e & 1)) {  // reusable (odd = someone's claim in flight: skip)
       if (free_idx < 0) { free_idx = (long)idx; free_ep = e; }

@@ -448,7 +448,7 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
         finish_set(a, c[j]);
         ++st.ok;
         ++muts;
-        pulse(a, a.slot((size_t)c[j].idx));
+        pulse_masks(a, c[j].wm, c[j].bl);
         mark_dirty(a, (size_t)c[j].idx);
       }
       if (status) status[op[j]] = rc;

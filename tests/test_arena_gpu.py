@@ -254,3 +254,59 @@ def test_racing_inserts_no_duplicates(uniq):
         assert len(keys) == 512 and len(set(keys)) == 512
     finally:
         a.close()
+
+
+def test_hot_keys_carried_retries(uniq):
+    """64 hot keys, 40k sets racing 40k gets on two streams: contended ops are carried into
+    later rounds (k_set_carry / k_get_carry); every op ends ok or EAGAIN after its bounded
+    attempts, the stats add up, every successful read is an intact value of its key, and the
+    final value of each key is one of the versions written to it."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
+    a = HbmArena.create(uniq + "h", slots=4096, max_val=256, embeddings=False)
+    try:
+        n, hot = 40000, 64
+        ids = torch.arange(n, device="cuda") % hot
+        K = format_keys(n, "hot", 4, 16, ids=ids)
+        V0, L0 = format_values(hot, 1, 150, 256, ids=torch.arange(hot, device="cuda"))
+        assert (a.set(K[:hot], V0, L0) == 0).all()
+        torch.cuda.synchronize()
+        a.reset_stats()
+        V, L = format_values(n, 5, 150, 256, ids=ids)
+        sw, sr = torch.cuda.Stream(), torch.cuda.Stream()
+        with torch.cuda.stream(sw):
+            sst = a.set(K, V, L, retries=64)
+        with torch.cuda.stream(sr):
+            gst, out, ol = a.get(K, retries=64)
+        torch.cuda.synchronize()
+        sst, gst = sst.cpu(), gst.cpu()
+        assert bool(((sst == 0) | (sst == -11)).all()) and bool(((gst == 0) | (gst == -11)).all())
+        # 625 racing sets per key: a bounded attempt budget leaves many EAGAIN (the reference's
+        # "retry" status), but every key makes progress
+        assert int((sst == 0).sum()) >= hot and int((gst == 0).sum()) >= hot
+        attempts, ok, again, miss = [int(x) for x in a.stats.tolist()]
+        assert ok == int((sst == 0).sum()) + int((gst == 0).sum()) and miss == 0
+        assert attempts == ok + again  # every attempt ends ok or EAGAIN here (no misses)
+        o, ln, idh = out.cpu().numpy(), ol.cpu().numpy(), ids.cpu().numpy()
+        for i in np.nonzero(gst.numpy() == 0)[0][::97]:
+            s = bytes(o[i, : ln[i]])
+            head, _, rest = s.partition(b"|id:")
+            ver = int(head[4:])
+            assert int(rest.split(b"|")[0]) == idh[i] and ver in (1, 5)
+            fill = s[s.index(b"data:") + 5:]
+            assert fill == bytes([65 + ver % 26]) * len(fill), "torn value"
+        # a client that resubmits its EAGAIN ops gets them all through
+        pend = torch.nonzero(sst.cuda() != 0).squeeze(1)
+        for _ in range(200):
+            if pend.numel() == 0:
+                break
+            r = a.set(K[pend].contiguous(), V[pend].contiguous(), L[pend].contiguous(), retries=64)
+            pend = pend[r != 0]
+        assert pend.numel() == 0
+        st, out2, ol2 = a.get(K[:hot])
+        assert (st == 0).all()
+        for i in range(hot):
+            s = bytes(out2[i, : ol2[i]].cpu().numpy())
+            assert s.startswith(b"ver:5|")
+    finally:
+        a.close()

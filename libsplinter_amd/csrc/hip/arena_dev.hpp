@@ -173,6 +173,59 @@ __device__ __forceinline__ void store_key(uint8_t* slot, const KeyT<KW>& k) {
   for (int c = 0; c < 4; ++c) d[c] = make_uint4(k.word(4 * c), k.word(4 * c + 1), k.word(4 * c + 2), k.word(4 * c + 3));
 }
 
+// ---------------------------------------------------- 16-B coherent probes --
+// global_load_dwordx4 ... sc1: L1-bypassing and L2-served exactly like the relaxed agent-scope
+// 8-B atomic loads above (MI355X_MICROARCH.md, agent-scope forms), but ONE request per 16 B: a
+// probe of (hash, epoch) + key takes 2 requests instead of 4-5 (8-B sc1 accesses run at roughly
+// the same request rate, so half the bytes each).  hipcc does not track inline-asm loads in its
+// own waits: a result is valid only after vm_wait() on it, which ties the registers.
+typedef unsigned int u32x4c_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ u32x4c_t ld16c(const void* p) {
+  u32x4c_t r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ void vm_wait(u32x4c_t& a) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(a)::"memory"); }
+__device__ __forceinline__ void vm_wait(u32x4c_t& a, u32x4c_t& b) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b)::"memory");
+}
+__device__ __forceinline__ void vm_wait(u32x4c_t& a, u32x4c_t& b, u32x4c_t& c) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b), "+v"(c)::"memory");
+}
+__device__ __forceinline__ uint64_t lo64(const u32x4c_t& v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ uint64_t hi64(const u32x4c_t& v) { return ((uint64_t)v.w << 32) | v.z; }
+
+// Stored-key probe in 16-B chunks: chunk 0 always, the rest only where our key + NUL reaches
+// (a KW-word key is at most 4*KW bytes: chunk KW/4 can still hold its NUL).
+template <int KW>
+struct KeyProbe {
+  static constexpr int kMaxC = KW / 4 + 1 < 4 ? KW / 4 + 1 : 4;
+  u32x4c_t c[kMaxC];
+  __device__ __forceinline__ void issue(const uint8_t* slot, const KeyT<KW>& k) {
+    const int nch = ((int)k.len >> 4) + 1;
+    c[0] = ld16c(slot + kOffKey);
+#pragma unroll
+    for (int i = 1; i < kMaxC; ++i) {
+      c[i] = u32x4c_t{0u, 0u, 0u, 0u};
+      if (i < nch) c[i] = ld16c(slot + kOffKey + 16 * i);
+    }
+  }
+  __device__ __forceinline__ void wait() {
+#pragma unroll
+    for (int i = 0; i < kMaxC; ++i) vm_wait(c[i]);
+  }
+  __device__ __forceinline__ bool eq(const KeyT<KW>& k) const {
+    const int nch = ((int)k.len >> 4) + 1;
+    bool e = true;
+#pragma unroll
+    for (int i = 0; i < kMaxC; ++i)
+      if (i < nch)
+        e = e && c[i].x == k.word(4 * i) && c[i].y == k.word(4 * i + 1) && c[i].z == k.word(4 * i + 2) &&
+            c[i].w == k.word(4 * i + 3);
+    return e;
+  }
+};
+
 __device__ __forceinline__ uint64_t slot_hash(const uint8_t* s) { return ald64(s + kOffHash); }
 __device__ __forceinline__ uint64_t slot_epoch(const uint8_t* s) { return ald64(s + kOffEpoch); }
 __device__ __forceinline__ uint64_t* epoch_ptr(uint8_t* s) { return (uint64_t*)(s + kOffEpoch); }
@@ -343,17 +396,24 @@ __device__ Claim claim_set(const Arena& a, const KeyT<KW>& k) {
   size_t idx = home;
   for (uint32_t i = 0; i < a.slots; ++i) {
     uint8_t* s = a.slot(idx);
-    // hash, epoch and key words in ONE round trip (the key compare is speculative)
-    const uint64_t sh = slot_hash(s);
-    const uint64_t e = slot_epoch(s);
-    const bool keq = key_eq(s, k);
+    // hash, epoch and key in ONE round trip of 16-B coherent loads (the key compare is speculative)
+    u32x4c_t he = ld16c(s + kOffHash);
+    KeyProbe<KW> kp;
+    kp.issue(s, k);
+    vm_wait(he);
+    kp.wait();
+    const uint64_t sh = lo64(he), e = hi64(he);
+    const bool keq = kp.eq(k);
     if (sh == k.hash && keq) {  // update in place
       if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return Claim{-1, false, kAgain};
       // re-check after the claim: hash + key together, with the watcher mask and labels the
       // set will pulse (same 128-B slot line, same round trip)
-      const uint64_t sh2 = slot_hash(s);
-      const bool keq2 = key_eq(s, k);
-      const uint64_t wm = ald64(s + kOffWatch), bl = ald64(s + kOffBloom);
+      u32x4c_t h2 = ld16c(s + kOffHash), wc = ld16c(s + kOffWatch), ab = ld16c(s + kOffAtime);
+      kp.issue(s, k);
+      vm_wait(h2, wc, ab);
+      kp.wait();
+      const uint64_t sh2 = lo64(h2), wm = lo64(wc), bl = hi64(ab);
+      const bool keq2 = kp.eq(k);
       if (sh2 != k.hash || !keq2) {  // raced with unset / reuse
         aadd64(epoch_ptr(s), 1);
         return Claim{-1, false, kAgain};
@@ -496,10 +556,14 @@ __device__ __forceinline__ long locate_peek(const Arena& a, const KeyT<KW>& k, u
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
-    const uint64_t sh = slot_hash(s);
-    const uint64_t e = slot_epoch(s);
-    const uint32_t L = ald32(s + kOffValLen);
-    const bool keq = key_eq(s, k);
+    u32x4c_t he = ld16c(s + kOffHash), vl = ld16c(s + kOffValOff);
+    KeyProbe<KW> kp;
+    kp.issue(s, k);
+    vm_wait(he, vl);
+    kp.wait();
+    const uint64_t sh = lo64(he), e = hi64(he);
+    const uint32_t L = vl.y;  // val_len at offset 20
+    const bool keq = kp.eq(k);
     if (sh == k.hash && keq) {
       *e1 = e;
       *len = L;

@@ -517,7 +517,10 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
       if (op[j] < 0 || rc[j] != kOk) continue;
       const uint8_t* s = a.slot((size_t)sidx[j]);
       if ((e1[j] & 1) || len[j] > a.max_val) { rc[j] = kAgain; continue; }
-      const bool keq = key_eq(s, k[j]);
+      KeyProbe<KW> kp;
+      kp.issue(s, k[j]);
+      kp.wait();
+      const bool keq = kp.eq(k[j]);
       if (out) {
         if (len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
         const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
@@ -531,9 +534,9 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       if (op[j] < 0 || rc[j] != kOk) continue;
-      const uint8_t* s = a.slot((size_t)sidx[j]);
-      const uint64_t e2 = slot_epoch(s), h2 = slot_hash(s);
-      if (e2 != e1[j] || h2 != k[j].hash) rc[j] = kAgain;
+      u32x4c_t he = ld16c(a.slot((size_t)sidx[j]) + kOffHash);  // hash + epoch: one request
+      vm_wait(he);
+      if (hi64(he) != e1[j] || lo64(he) != k[j].hash) rc[j] = kAgain;
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {

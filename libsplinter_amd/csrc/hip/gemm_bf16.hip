@@ -36,11 +36,13 @@ constexpr int kEpiStride = BN + 4;                 // fp32 epilogue row stride (
 constexpr int kLdsBytes = (BM * kEpiStride * 4 > 4 * kTileBytes) ? BM * kEpiStride * 4 : 4 * kTileBytes;
 
 __device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
-__device__ __forceinline__ uint16_t f2bf(float f) {
-  // round-to-nearest-even (NaN stays NaN: quiet bit kept by the +0x7fff path for finite only)
-  const uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (uint16_t)((u >> 16) | ((u & 0xffff) ? 0x40 : 0));
-  return (uint16_t)((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+// fp32 -> bf16, round-to-nearest-even, on the hardware converter (v_cvt_pk_bf16_f32: one
+// instruction per PAIR via pk2, instead of a 5-op integer rounding sequence per value)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint16_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 
 // Stage one BMxBK tile of a K-contiguous matrix (row stride ld elements)
@@ -178,10 +180,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
         }
       }
       uint4 o;
-      o.x = f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-      o.y = f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-      o.z = f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-      o.w = f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+      o.x = pk2(v[0], v[1]);
+      o.y = pk2(v[2], v[3]);
+      o.z = pk2(v[4], v[5]);
+      o.w = pk2(v[6], v[7]);
       *(uint4*)(ep.out + gm * ep.ldo + n0 + c8) = o;
     }
   } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
@@ -201,10 +203,10 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
         o[e] = swiglu(up, g);
       }
       uint4 w;
-      w.x = f2bf(o[0]) | ((uint32_t)f2bf(o[1]) << 16);
-      w.y = f2bf(o[2]) | ((uint32_t)f2bf(o[3]) << 16);
-      w.z = f2bf(o[4]) | ((uint32_t)f2bf(o[5]) << 16);
-      w.w = f2bf(o[6]) | ((uint32_t)f2bf(o[7]) << 16);
+      w.x = pk2(o[0], o[1]);
+      w.y = pk2(o[2], o[3]);
+      w.z = pk2(o[4], o[5]);
+      w.w = pk2(o[6], o[7]);
       *(uint4*)(ep.out + gm * ep.ldo + (long)nt * 64 + c8) = w;
     }
   } else if constexpr (MODE == NOMIC_EPI_ROPE) {
@@ -235,14 +237,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
         }
       }
       uint4 w1, w2;
-      w1.x = f2bf(x1[0]) | ((uint32_t)f2bf(x1[1]) << 16);
-      w1.y = f2bf(x1[2]) | ((uint32_t)f2bf(x1[3]) << 16);
-      w1.z = f2bf(x1[4]) | ((uint32_t)f2bf(x1[5]) << 16);
-      w1.w = f2bf(x1[6]) | ((uint32_t)f2bf(x1[7]) << 16);
-      w2.x = f2bf(x2[0]) | ((uint32_t)f2bf(x2[1]) << 16);
-      w2.y = f2bf(x2[2]) | ((uint32_t)f2bf(x2[3]) << 16);
-      w2.z = f2bf(x2[4]) | ((uint32_t)f2bf(x2[5]) << 16);
-      w2.w = f2bf(x2[6]) | ((uint32_t)f2bf(x2[7]) << 16);
+      w1.x = pk2(x1[0], x1[1]);
+      w1.y = pk2(x1[2], x1[3]);
+      w1.z = pk2(x1[4], x1[5]);
+      w1.w = pk2(x1[6], x1[7]);
+      w2.x = pk2(x2[0], x2[1]);
+      w2.y = pk2(x2[2], x2[3]);
+      w2.z = pk2(x2[4], x2[5]);
+      w2.w = pk2(x2[6], x2[7]);
       *(uint4*)(ep.out + gm * ep.ldo + gcol + d0) = w1;
       *(uint4*)(ep.out + gm * ep.ldo + gcol + d0 + 32) = w2;
     }
@@ -305,10 +307,10 @@ __device__ __forceinline__ void raw_barrier() {
 
 __device__ __forceinline__ uint4 pack8(const float* v) {
   uint4 o;
-  o.x = f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-  o.y = f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-  o.z = f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-  o.w = f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  o.x = pk2(v[0], v[1]);
+  o.y = pk2(v[2], v[3]);
+  o.z = pk2(v[4], v[5]);
+  o.w = pk2(v[6], v[7]);
   return o;
 }
 
@@ -567,7 +569,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
 // (pack_qkv), so x1 = acc[..][j=0] and x2 = acc[..][j=1] of the same lane.
 // ===========================================================================
 __device__ __forceinline__ uint2 pack4(const float* v) {
-  return make_uint2(f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16), f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16));
+  return make_uint2(pk2(v[0], v[1]), pk2(v[2], v[3]));
 }
 
 template <int MODE, bool PERSIST>

@@ -21,10 +21,12 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 constexpr int D = 768;
 
 __device__ __forceinline__ float bf2f(uint32_t h16) { return __uint_as_float(h16 << 16); }
-__device__ __forceinline__ uint32_t f2bf(float f) {
-  const uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u) return (u >> 16) | ((u & 0xffff) ? 0x40u : 0u);
-  return (u + 0x7fffu + ((u >> 16) & 1u)) >> 16;
+// fp32 -> bf16 (RNE) on the hardware converter: v_cvt_pk_bf16_f32, one instruction per pair (pk2)
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t f2bf(float f) { return __builtin_bit_cast(uint16_t, (__bf16)f); }
+__device__ __forceinline__ uint32_t pk2(float a, float b) {
+  const bf16x2_t v = {(__bf16)a, (__bf16)b};
+  return __builtin_bit_cast(uint32_t, v);
 }
 __device__ __forceinline__ void unpack8(uint4 v, float* f) {
   f[0] = bf2f(v.x & 0xffff); f[1] = bf2f(v.x >> 16);
@@ -33,8 +35,8 @@ __device__ __forceinline__ void unpack8(uint4 v, float* f) {
   f[6] = bf2f(v.w & 0xffff); f[7] = bf2f(v.w >> 16);
 }
 __device__ __forceinline__ uint4 pack8(const float* f) {
-  return make_uint4(f2bf(f[0]) | (f2bf(f[1]) << 16), f2bf(f[2]) | (f2bf(f[3]) << 16),
-                    f2bf(f[4]) | (f2bf(f[5]) << 16), f2bf(f[6]) | (f2bf(f[7]) << 16));
+  return make_uint4(pk2(f[0], f[1]), pk2(f[2], f[3]),
+                    pk2(f[4], f[5]), pk2(f[6], f[7]));
 }
 
 // ------------------------------------------------------------ LayerNorm --
@@ -493,8 +495,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
 #pragma unroll
     for (int db = 0; db < 4; ++db) {
       uint2 w;
-      w.x = f2bf(o[db][qb][0] * inv) | (f2bf(o[db][qb][1] * inv) << 16);
-      w.y = f2bf(o[db][qb][2] * inv) | (f2bf(o[db][qb][3] * inv) << 16);
+      w.x = pk2(o[db][qb][0] * inv, o[db][qb][1] * inv);
+      w.y = pk2(o[db][qb][2] * inv, o[db][qb][3] * inv);
       *(uint2*)(dst + db * 16) = w;
     }
   }

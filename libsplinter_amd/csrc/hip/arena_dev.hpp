@@ -478,6 +478,34 @@ __device__ Claim claim_set(const Arena& a, const KeyT<KW>& k) {
   return Claim{free_idx, true, kOk};
 }
 
+// Slot metadata part of a set (everything but the value bytes): fresh-slot defaults and val_len.
+template <int MO = 0>
+__device__ __forceinline__ void write_meta(const Arena& a, const Claim& c, uint32_t len) {
+  uint8_t* s = a.slot((size_t)c.idx);
+  if (c.fresh) {
+    // fresh slot: metadata bytes 24..63 to defaults (type VOID), clear a stale vector
+    st16<MO>(s + 32, make_uint4(0, 0, 0, 0));  // watcher_mask, ctime
+    st16<MO>(s + 48, make_uint4(0, 0, 0, 0));  // atime, bloom
+    ast8(s + kOffType, (uint8_t)SPL_SLOT_DEFAULT_TYPE);
+    ast8(s + kOffUser, 0);
+    if (a.stride == kSlotEmbedBytes) {
+      uint4* ev = (uint4*)(s + kOffEmbed);
+      for (uint32_t q = 0; q < kEmbedBytes / 16; ++q) st16<MO>(ev + q, make_uint4(0, 0, 0, 0));
+    }
+  }
+  ast32(s + kOffValLen, len);
+}
+
+// 16-B chunks of a value region a set writes: the value, then (with scrubbing) zeros to the
+// 64-B boundary (hybrid) or to max_val (full) -- the chunk count write_value covers.
+__device__ __forceinline__ uint32_t set_chunks(const Arena& a, uint32_t len, bool scrub, bool hybrid) {
+  const uint32_t n16 = (len + 15) >> 4;
+  if (!scrub) return n16;
+  uint32_t end = hybrid ? ((len + 63u) & ~63u) : a.max_val;
+  if (end > a.max_val) end = a.max_val;
+  return (end >> 4) > n16 ? (end >> 4) : n16;
+}
+
 template <int MO = 0>
 __device__ __forceinline__ void write_set(const Arena& a, const Claim& c, const uint8_t* val, uint32_t len,
                                           bool scrub, bool hybrid) {

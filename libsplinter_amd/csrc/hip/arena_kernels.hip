@@ -372,6 +372,52 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
   flush_stats(a, st, stats, 0);
 }
 
+// ------------------------------------------------ cooperative row copy ---
+// A wave's round copies up to U*64 value rows (150-B values = 10 x 16 B).  Copied lane-by-op,
+// every 16-B wave instruction touches 64 different rows (64 lines); copied here cooperatively,
+// 16 lanes take the 16 chunks of one 256-B row and an instruction covers 4 rows (8 lines), with
+// 4 instructions' loads in flight.  Entries come from a wave-private LDS table:
+// p = {src lo, src hi, dst lo, dst hi}, l = {len (bytes of the value), wend (chunks to write;
+// chunks in [ceil(len/16), wend) are zero-filled: mop scrubbing)}.  l.y == 0: no row.
+template <int NE>
+__device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
+                                          int groups) {
+  const int q = lane >> 4, cl = lane & 15;
+  constexpr int kUnr = 4;  // 8 rows in flight cost 80 VGPRs (1 wave/SIMD); 4 keep the kernel at 2
+  for (int e0 = 0; e0 < NE; e0 += 4 * kUnr) {
+    uint4 P[kUnr];
+    uint2 L[kUnr];
+#pragma unroll
+    for (int u = 0; u < kUnr; ++u) {
+      P[u] = ep[e0 + 4 * u + q];
+      L[u] = el[e0 + 4 * u + q];
+    }
+    for (int g = 0; g < groups; ++g) {
+      const uint32_t c = (uint32_t)(g * 16 + cl);
+      uint4 d[kUnr];
+#pragma unroll
+      for (int u = 0; u < kUnr; ++u) {
+        const uint32_t n16 = (L[u].x + 15) >> 4;
+        const uint4* src = (const uint4*)(((uint64_t)P[u].y << 32) | P[u].x);
+        d[u] = make_uint4(0, 0, 0, 0);
+        if (c < n16) d[u] = src[c];
+      }
+#pragma unroll
+      for (int u = 0; u < kUnr; ++u) {
+        if (c >= L[u].y) continue;
+        const uint32_t n16 = (L[u].x + 15) >> 4;
+        uint4 v = d[u];
+        if (c == n16 - 1 && (L[u].x & 15)) {
+          const int r = (int)(L[u].x & 15);
+          v.x &= keep_mask(r); v.y &= keep_mask(r - 4); v.z &= keep_mask(r - 8); v.w &= keep_mask(r - 12);
+        }
+        uint4* dst = (uint4*)(((uint64_t)P[u].w << 32) | P[u].z);
+        dst[c] = v;
+      }
+    }
+  }
+}
+
 // ------------------------------------------------ carried-retry rounds -----
 // Same rounds as above, but an op that meets a contended slot (EAGAIN) is NOT retried inline:
 // it stays in its lane's slot and is retried in the lane's next round, while the lane's other
@@ -381,10 +427,12 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
 // bounded by 1 + max_retry as before; the round loop is block-uniform (barriers).
 // Lane sequence: op c of a lane is first + (c / U) * stride + c % U (monotone in c), i.e. the
 // grid-stride order of the rounds kernels.
-template <int U, int B, int KW = 16>
+template <int U, int B, int KW = 16, bool COOP = false>
 __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
                                                  int vstride, const uint32_t* lens, long n, int32_t* status,
                                                  int max_retry, uint64_t* stats, Seg seg) {
+  __shared__ uint4 cp_p[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
+  __shared__ uint2 cp_l[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
   const Arena a = to_dev(aa);
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
@@ -429,9 +477,27 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
         else c[j] = claim_set(a, k[j]);
       }
     }
+    if constexpr (COOP) {
+      // value rows through the cooperative copy (wave-private table), metadata per lane
+      const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (op[j] >= 0 && c[j].rc == kOk) write_set<0>(a, c[j], vals + op[j] * (long)vstride, len[j], scrub, hybrid);
+      for (int j = 0; j < U; ++j) {
+        const bool go = op[j] >= 0 && c[j].rc == kOk;
+        const uint64_t sp = go ? (uint64_t)(vals + op[j] * (long)vstride) : 0;
+        const uint64_t dp = go ? (uint64_t)a.value((size_t)c[j].idx) : 0;
+        cp_p[w][j * 64 + lane] = make_uint4((uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)dp, (uint32_t)(dp >> 32));
+        cp_l[w][j * 64 + lane] = make_uint2(go ? len[j] : 0u, go ? set_chunks(a, len[j], scrub, hybrid) : 0u);
+      }
+      __builtin_amdgcn_wave_barrier();
+      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8));
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (op[j] >= 0 && c[j].rc == kOk) write_meta<0>(a, c[j], len[j]);
+    } else {
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (op[j] >= 0 && c[j].rc == kOk) write_set<0>(a, c[j], vals + op[j] * (long)vstride, len[j], scrub, hybrid);
+    }
     drain();
     __syncthreads();
     if (threadIdx.x == 0) release();
@@ -458,10 +524,12 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
   flush_stats(a, st, stats, muts);
 }
 
-template <int U, int B, int KW = 16>
+template <int U, int B, int KW = 16, bool COOP = false>
 __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                  int ostride, uint32_t* out_lens, long n, int32_t* status,
                                                  int max_retry, uint64_t* stats, Seg seg) {
+  __shared__ uint4 cp_p[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
+  __shared__ uint2 cp_l[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
   const Arena a = to_dev(aa);
   Stats st;
   const long stride = (long)gridDim.x * blockDim.x * U;
@@ -523,12 +591,29 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
       const bool keq = kp.eq(k[j]);
       if (out) {
         if (len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
-        const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
-        uint4* dst = (uint4*)(out + op[j] * (long)ostride);
-        const uint32_t n16 = (len[j] + 15) >> 4;
-        for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
+        if constexpr (!COOP) {
+          const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
+          uint4* dst = (uint4*)(out + op[j] * (long)ostride);
+          const uint32_t n16 = (len[j] + 15) >> 4;
+          for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
+        }
       }
       if (!keq) rc[j] = kAgain;
+    }
+    if constexpr (COOP) {
+      // value rows of this round's matched ops through the cooperative copy (see coop_copy)
+      const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const bool go = out && op[j] >= 0 && rc[j] == kOk;
+        const uint64_t sp = go ? (uint64_t)a.value((size_t)sidx[j]) : 0;
+        const uint64_t dp = go ? (uint64_t)(out + op[j] * (long)ostride) : 0;
+        const uint32_t n16 = (len[j] + 15) >> 4;
+        cp_p[w][j * 64 + lane] = make_uint4((uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)dp, (uint32_t)(dp >> 32));
+        cp_l[w][j * 64 + lane] = make_uint2(go ? n16 * 16 : 0u, go ? n16 : 0u);
+      }
+      __builtin_amdgcn_wave_barrier();
+      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8));
     }
     drain();
 #pragma unroll
@@ -911,6 +996,7 @@ int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_
   // (profiles/r1_kv_occupancy.md), so it is off by default.
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);
   static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);  // carried retries (k_set_carry)
+  static const int coop = env_int("SPLINTER_ARENA_COOP", 1);    // cooperative value-row copy
   if (carry && !wt && (u == 2 || u == 4)) {
 #define SPL_SET_CARRY(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_set_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
@@ -918,6 +1004,9 @@ int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_
     if (kw4 && kstride == 16 && u == 4 && b == 256)
       hipLaunchKernelGGL((k_set_carry<4, 256, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
                          kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (u == 4 && b == 256 && coop)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
+                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
     else if (u == 4 && b == 256) SPL_SET_CARRY(4, 256);
     else if (u == 4) SPL_SET_CARRY(4, 512);
     else if (b == 256) SPL_SET_CARRY(2, 256);
@@ -978,11 +1067,15 @@ int spl_arena_get_seg(spl_arena_t a, const char* keys, int kstride, uint8_t* out
   static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);  // see spl_arena_set_seg
   static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);
+  static const int coop = env_int("SPLINTER_ARENA_COOP_GET", env_int("SPLINTER_ARENA_COOP", 1));
   if (carry && gv == 1 && (u == 2 || u == 4)) {
 #define SPL_GET_CARRY(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_get_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
-    if (kw4 && kstride == 16 && u == 2 && b == 256)
+    if (coop && u == 2 && b == 256)
+      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a,
+                         keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else if (kw4 && kstride == 16 && u == 2 && b == 256)
       hipLaunchKernelGGL((k_get_carry<2, 256, 4>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
                          kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
     else if (u == 2 && b == 256) SPL_GET_CARRY(2, 256);

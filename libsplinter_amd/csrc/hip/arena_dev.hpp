@@ -324,6 +324,13 @@ __device__ __forceinline__ uint4 ld16(const void* p) {
   }
 }
 
+// Store the first nb (< 16) bytes of v: the last chunk of a value row whose length (max_val)
+// is not a multiple of 16 must not spill into the next row.
+__device__ __forceinline__ void store_partial(uint8_t* d, uint4 v, uint32_t nb) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  for (uint32_t b = 0; b < nb; ++b) d[b] = (uint8_t)(w[b >> 2] >> (8 * (b & 3)));
+}
+
 template <int MO>
 __device__ __forceinline__ void write_value(const Arena& a, size_t idx, const uint8_t* src, uint32_t len, bool scrub,
                                             bool hybrid) {
@@ -345,7 +352,8 @@ __device__ __forceinline__ void write_value(const Arena& a, size_t idx, const ui
         const int r = (int)(len & 15);
         t[q].x &= keep_mask(r); t[q].y &= keep_mask(r - 4); t[q].z &= keep_mask(r - 8); t[q].w &= keep_mask(r - 12);
       }
-      st16<MO>(dst + c, t[q]);
+      if (c * 16 + 16 > a.max_val) store_partial((uint8_t*)(dst + c), t[q], a.max_val - c * 16);
+      else st16<MO>(dst + c, t[q]);
     }
   }
   uint32_t done = n16 << 4;
@@ -681,7 +689,10 @@ __device__ int32_t integer_op(const Arena& a, const KeyT<KW>& k, int op, uint64_
   const uint64_t e = slot_epoch(s);
   if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
   uint8_t* v = a.value((size_t)i);
-  uint64_t x = ald64(v);
+  // the slot is held (odd epoch): plain accesses, and byte-safe -- a value row starts at
+  // i * max_val, which is 8-B aligned only when max_val is
+  uint64_t x;
+  __builtin_memcpy(&x, v, 8);
   switch (op) {
     case SPL_OP_AND: x &= m; break;
     case SPL_OP_OR: x |= m; break;
@@ -691,7 +702,7 @@ __device__ int32_t integer_op(const Arena& a, const KeyT<KW>& k, int op, uint64_
     case SPL_OP_DEC: x -= m; break;
     default: break;
   }
-  ast64(v, x);
+  __builtin_memcpy(v, &x, 8);
   drain();
   aadd64(epoch_ptr(s), 1);
   if (result) *result = x;

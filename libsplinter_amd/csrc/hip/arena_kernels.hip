@@ -379,9 +379,11 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
 // 4 instructions' loads in flight.  Entries come from a wave-private LDS table:
 // p = {src lo, src hi, dst lo, dst hi}, l = {len (bytes of the value), wend (chunks to write;
 // chunks in [ceil(len/16), wend) are zero-filled: mop scrubbing)}.  l.y == 0: no row.
+// rowb: bytes of a destination row (value regions are max_val long; a last chunk past it is
+// stored bytewise so it cannot spill into the next row); 0xFFFFFFFF: no limit.
 template <int NE>
 __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
-                                          int groups) {
+                                          int groups, uint32_t rowb) {
   const int q = lane >> 4, cl = lane & 15;
   constexpr int kUnr = 4;  // 8 rows in flight cost 80 VGPRs (1 wave/SIMD); 4 keep the kernel at 2
   for (int e0 = 0; e0 < NE; e0 += 4 * kUnr) {
@@ -412,7 +414,8 @@ __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const ui
           v.x &= keep_mask(r); v.y &= keep_mask(r - 4); v.z &= keep_mask(r - 8); v.w &= keep_mask(r - 12);
         }
         uint4* dst = (uint4*)(((uint64_t)P[u].w << 32) | P[u].z);
-        dst[c] = v;
+        if (c * 16 + 16 > rowb) store_partial((uint8_t*)(dst + c), v, rowb - c * 16);
+        else dst[c] = v;
       }
     }
   }
@@ -489,7 +492,7 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
         cp_l[w][j * 64 + lane] = make_uint2(go ? len[j] : 0u, go ? set_chunks(a, len[j], scrub, hybrid) : 0u);
       }
       __builtin_amdgcn_wave_barrier();
-      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8));
+      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), a.max_val);
 #pragma unroll
       for (int j = 0; j < U; ++j)
         if (op[j] >= 0 && c[j].rc == kOk) write_meta<0>(a, c[j], len[j]);
@@ -613,7 +616,7 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
         cp_l[w][j * 64 + lane] = make_uint2(go ? n16 * 16 : 0u, go ? n16 : 0u);
       }
       __builtin_amdgcn_wave_barrier();
-      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8));
+      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
     }
     drain();
 #pragma unroll

@@ -310,3 +310,31 @@ def test_hot_keys_carried_retries(uniq):
             assert s.startswith(b"ver:5|")
     finally:
         a.close()
+
+
+def test_unaligned_value_rows_do_not_spill(uniq):
+    """max_val = 100 (value rows 4-B aligned, last 16-B chunk partial): full-length values in
+    neighbouring slots survive each other's sets (set rounds, cooperative copy, single-op path),
+    and integer ops work on rows that are not 8-B aligned."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, pack_keys, pack_values, unpack
+    a = HbmArena.create(uniq + "u", slots=2048, max_val=100, embeddings=False)
+    try:
+        keys = [f"u{i:05d}" for i in range(1500)]
+        vals = [bytes([65 + (i % 26)]) * (100 if i % 3 else 37 + i % 50) for i in range(len(keys))]
+        K = pack_keys(keys, 16)
+        V, L = pack_values(vals, 112)
+        for _ in range(2):  # insert, then update in place
+            assert (a.set(K, V, L) == 0).all()
+        st, out, ol = a.get(K)
+        torch.cuda.synchronize()
+        assert (st == 0).all()
+        assert unpack(out, ol) == vals
+        s = a.store
+        s.set("ctr", (7).to_bytes(8, "little"))
+        s.set_type("ctr", 1 << 2)  # BIGUINT
+        assert s.integer_op("ctr", 4, 5) == 12  # INC
+        st, out, ol = a.get(K)
+        assert unpack(out, ol) == vals
+    finally:
+        a.close()

@@ -52,6 +52,9 @@ def parse():
                         "and the encoder to the rest (hipExtStreamCreateWithCUMask); 0 = phases back to back")
     p.add_argument("--overlap", action="store_true",
                    help="run the embed batch concurrently with the KV batches (own stream, all CUs)")
+    p.add_argument("--force-routed", action="store_true",
+                   help="run the N>1 routed step (pack -> all-to-all -> owner kernels -> all-to-all -> gather) "
+                        "even at N=1, to measure the routing overhead on one GPU")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: "
                    "ranks may share a GPU, collectives staged through the host)")
     return p.parse_args()
@@ -63,11 +66,12 @@ def main():
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    routed = world > 1 or args.force_routed
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
-    if world > 1:
+    if routed:
         if args.backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
@@ -86,7 +90,7 @@ def main():
     arena.store.set_mop(0)  # throughput mode: no scrubbing (reference stress default)
     kv = ShardedKV(GpuShard(arena))
     rkv = None
-    if world > 1:
+    if routed:
         # request and response all-to-alls on their own communicators (= their own RCCL streams):
         # step i's responses and step i+1's requests are in flight together
         from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
@@ -100,7 +104,7 @@ def main():
     for first in range(0, total_keys, chunk):
         n = min(chunk, total_keys - first)
         K = format_keys(n, "k", 10, 16, first=first)
-        if world > 1:
+        if routed:
             own = kv.owned_mask(K)
             ids = torch.nonzero(own).squeeze(1) + first
             K = K[own]
@@ -188,7 +192,7 @@ def main():
     #   s_set / s_get : owner kernels of batch i, after its requests and embed_i
     #   s_resp: response all-to-alls + gather of batch i       (overlaps embed_{i+1})
     # All K steps' responses are delivered inside the timed region (device-wide sync at the end).
-    if world > 1:
+    if routed:
         cap_s, cap_g = route_capacity(max(n_set, 1), world), route_capacity(max(n_get, 1), world)
         vw = min((args.value_len + 15) // 16 * 16, vstride)
         s_req, s_resp = hip_stream("low"), hip_stream("low")
@@ -230,25 +234,25 @@ def main():
             if go is not None:
                 rkv.finish(go, out=gouts[i % 2])
 
-    step = step_local if world == 1 else step_routed
+    step = step_routed if routed else step_local
 
     for i in range(args.warmup):
         step(i)
     torch.cuda.synchronize()
     arena.reset_stats()
-    if world > 1:
+    if routed:
         dist.barrier()
     torch.cuda.synchronize()
     t_start = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
     torch.cuda.synchronize()
-    if world > 1:
+    if routed:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     st = stats.clone()
-    if world > 1:
+    if routed:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dist.all_reduce(st)
     elapsed = t.item()
@@ -259,14 +263,16 @@ def main():
     if args.verify and n_get:
         GK, gid = batches[0][3], batches[0][4]
         m = min(args.verify, n_get)
-        if world > 1:
+        if routed:
             sts, outv, lens = kv.get(GK[:m])
         else:
             sts, outv, lens = arena.get(GK[:m])
         o, ln, ids, s_ = outv.cpu().numpy(), lens.cpu().numpy(), gid[:m].cpu().numpy(), sts.cpu().numpy()
+        bad_status: dict = {}
         for i in range(m):
             if s_[i] != 0:
                 integrity_fail += 1
+                bad_status[int(s_[i])] = bad_status.get(int(s_[i]), 0) + 1
                 continue
             v = bytes(o[i, : ln[i]])
             try:
@@ -276,9 +282,17 @@ def main():
                 fill = v[v.index(b"data:") + 5:]
                 if ident != ids[i] or fill != bytes([65 + ver % 26]) * len(fill):
                     integrity_fail += 1
+                    bad_status["content"] = bad_status.get("content", 0) + 1
+                    if bad_status["content"] <= 3:
+                        log(f"[bench] bad value for id {ids[i]} (len {ln[i]}): {v[:60]!r}...{v[-20:]!r}")
             except Exception:
                 integrity_fail += 1
-        if world > 1:
+                bad_status["parse"] = bad_status.get("parse", 0) + 1
+                if bad_status["parse"] <= 3:
+                    log(f"[bench] unparsable value for id {ids[i]} (len {ln[i]}): {v[:60]!r}...{v[-20:]!r}")
+        if bad_status and rank == 0:
+            log(f"[bench] integrity failures by kind (rank 0): {bad_status}")
+        if routed:
             x = torch.tensor([integrity_fail], device="cuda")
             dist.all_reduce(x)
             integrity_fail = int(x.item())
@@ -322,7 +336,7 @@ def main():
     if rank == 0:
         print(json.dumps(res), flush=True)
     arena.close()
-    if world > 1:
+    if routed:
         dist.destroy_process_group()
 
 

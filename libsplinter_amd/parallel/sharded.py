@@ -29,6 +29,8 @@ CPU (tests/test_sharded_gloo.py) and runs unchanged on RCCL.
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional, Tuple
 
 import numpy as np
@@ -71,6 +73,10 @@ def decode_keys(rows: torch.Tensor) -> List[str]:
     return [bytes(r).split(b"\0", 1)[0].decode("utf-8", "replace") for r in rows.cpu().numpy()]
 
 
+# bytes per RCCL all-to-all call (SPLINTER_A2A_CHUNK_BYTES); see _Coll.all_to_all
+A2A_CHUNK_BYTES = int(os.environ.get("SPLINTER_A2A_CHUNK_BYTES", str(256 << 20)))
+
+
 class _Coll:
     """Collective calls of one group.  RCCL takes device tensors directly; with the
     gloo backend (CPU tests, or several ranks sharing one GPU to rehearse the
@@ -88,6 +94,19 @@ class _Coll:
             o = torch.empty(out.shape, dtype=out.dtype)
             dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits, group=self.group)
             out.copy_(o)
+        elif out_splits is None and in_splits is None and out.is_cuda and \
+                inp.numel() * inp.element_size() > A2A_CHUNK_BYTES:
+            # Large equal-split all-to-alls go out in parts of <= A2A_CHUNK_BYTES per call: one
+            # RCCL all_to_all_single of 1.5 GiB returned wrong bytes past 768 MiB on MI355X
+            # (scripts/a2a_check.py, profiles/r1_routed_integrity.md).  Each part is one
+            # contiguous byte range of every destination segment, sent as a grouped send/recv.
+            w = dist.get_world_size(self.group)
+            ib = inp.contiguous().view(torch.uint8).view(w, -1)
+            ob = out.view(torch.uint8).view(w, -1)
+            step = max(A2A_CHUNK_BYTES // w, 1)
+            for p0 in range(0, ib.shape[1], step):
+                p1 = min(ib.shape[1], p0 + step)
+                dist.all_to_all([ob[d, p0:p1] for d in range(w)], [ib[d, p0:p1] for d in range(w)], group=self.group)
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
 

@@ -1,5 +1,6 @@
 """C1 routing kernels (route_kernels.hip) and segmented set/get (arena_kernels.hip
 Seg) against the torch references in parallel/routed.py."""
+import os
 import pytest
 import torch
 
@@ -98,3 +99,22 @@ def test_segmented_set_get_skip_dead_rows(uniq):
         assert (s4[live] == -90).all()
     finally:
         a.close()
+
+
+def test_chunked_all_to_all_rccl():
+    """Equal-split all-to-alls above SPLINTER_A2A_CHUNK_BYTES go out in parts (an RCCL
+    all_to_all_single of 1.5 GiB returned wrong bytes past 768 MiB): byte-exact up to 2.5 GiB."""
+    import socket
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "scripts/a2a_check.py", "--chunked"],
+                       cwd=root, capture_output=True, text=True, timeout=600, env=env)
+    assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
+    assert "chunked 2560 MiB: mismatching bytes 0" in r.stdout

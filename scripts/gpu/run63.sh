@@ -1,0 +1,7 @@
+#!/bin/bash
+# full GPU suite only
+cd "$(dirname "$0")/../.." || exit 1
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu63.log 2>&1
+echo "exit=$?"

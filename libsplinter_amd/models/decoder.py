@@ -10,10 +10,11 @@ the MI355X replacement, demo-grade as SURVEY §2.1 N8 scopes it:
   output) dequantised on the device, or random init (``DecoderConfig``);
 * every projection (q|k|v fused, o + residual, gate|up + SwiGLU, down +
   residual, LM head) runs on the gfx950 MFMA GEMM (``nomic_gemm``) with its
-  fused epilogues; RMSNorm, RoPE (llama "normal" adjacent-pair rotation, as
-  llama.cpp applies for arch llama), the KV-cache attention and the sampler
-  use torch ops on the same device -- the decode step is latency-bound and
-  not a benchmark path;
+  fused epilogues; RMSNorm and RoPE (llama "normal" adjacent-pair rotation, as
+  llama.cpp applies for arch llama, in place on the q|k GEMM output) are the
+  HIP kernels of ``csrc/hip/decoder_kernels.hip``; the KV-cache attention and
+  the sampler use torch ops on the same device -- the decode step is
+  latency-bound and not a benchmark path;
 * tokenizer: greedy longest-match over the GGUF vocabulary (SentencePiece
   "▁" spaces, <0xNN> byte fallback) or, for random init, bytes 0..255 + BOS/EOS.
 
@@ -23,6 +24,7 @@ on a GPU box the projections MUST go through the HIP GEMM (no silent fallback).
 """
 from __future__ import annotations
 
+import ctypes
 import math
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -177,6 +179,13 @@ class CausalLM:
         if self.hip:
             from .nomic import _lib
             self.L = _lib()
+            if not getattr(self.L, "_dec_declared", False):
+                P, c_long, c_int, c_float = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float
+                self.L.dec_rmsnorm.argtypes = [P, c_long, P, c_long, c_int, c_float, P, c_long, P]
+                self.L.dec_rmsnorm.restype = c_int
+                self.L.dec_rope.argtypes = [P, c_long, c_long, c_int, c_int, c_int, P, P, P]
+                self.L.dec_rope.restype = c_int
+                self.L._dec_declared = True
             ok = all(n % 128 == 0 for n in (cfg.d + 2 * cfg.kv_heads * hd, cfg.d, 2 * cfg.ffn, vpad)) \
                 and cfg.d % 64 == 0 and cfg.ffn % 64 == 0
             if not ok:
@@ -230,6 +239,13 @@ class CausalLM:
         return g[:, :, 0].reshape(y.shape[0], -1), g[:, :, 1].reshape(y.shape[0], -1)
 
     def _rms(self, x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+        if self.hip:  # dec_rmsnorm (csrc/hip/decoder_kernels.hip): one wave per row
+            from .nomic import _chk, _stream
+            x = x.contiguous()
+            out = torch.empty_like(x)
+            _chk(self.L.dec_rmsnorm(x.data_ptr(), x.shape[1], w.data_ptr(), x.shape[0], x.shape[1], self.cfg.eps,
+                                    out.data_ptr(), x.shape[1], _stream()), "rmsnorm")
+            return out
         xf = x.float()
         y = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + self.cfg.eps) * w
         return y.to(x.dtype)
@@ -258,10 +274,15 @@ class CausalLM:
         for li, lw in enumerate(self.layers):
             h = self._rms(x, lw["n1"])
             qkv = self._mm(0, h, lw["qkv"], cfg.d + 2 * KVH * hd)
+            if self.hip:  # RoPE in place over the q|k columns (dec_rope)
+                from .nomic import _chk, _stream
+                _chk(self.L.dec_rope(qkv.data_ptr(), qkv.stride(0), n, cfg.d + KVH * hd, hd, self.pos,
+                                     self.cos.data_ptr(), self.sin.data_ptr(), _stream()), "rope")
             q = qkv[:, : cfg.d].reshape(n, H, hd)
             k = qkv[:, cfg.d: cfg.d + KVH * hd].reshape(n, KVH, hd)
             v = qkv[:, cfg.d + KVH * hd:].reshape(n, KVH, hd)
-            q, k = self._rope(q, pos), self._rope(k, pos)
+            if not self.hip:
+                q, k = self._rope(q, pos), self._rope(k, pos)
             if li >= len(self.kcache):
                 self.kcache.append(k)
                 self.vcache.append(v)

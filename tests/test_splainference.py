@@ -54,3 +54,41 @@ def test_decoder_hip_matches_cpu():
     lg2, lc2 = gpu.forward([65]).cpu(), cpu.forward([65])
     assert (lg2 - lc2).norm() / lc2.norm() < 3e-2
     assert torch.argmax(lg2) == torch.argmax(lc2) or (lg2 - lc2).abs().max() < 0.05
+
+
+@pytest.mark.gpu
+def test_decoder_rmsnorm_rope_kernels_vs_fp32():
+    """dec_rmsnorm / dec_rope (csrc/hip/decoder_kernels.hip) against fp32 torch references."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
+    cfg = DecoderConfig(layers=1)
+    m = CausalLM.random(cfg, seed=1, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(0)
+    for d in (cfg.d, 4096):  # register-resident rows and the wide-row second pass
+        x = torch.randn((37, d), device="cuda", generator=g).to(torch.bfloat16)
+        w = torch.randn((d,), device="cuda", generator=g)
+        m.cfg.eps = 1e-5
+        got = m._rms(x, w).float()
+        xf = x.float()
+        ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w
+        assert (got - ref).abs().max() <= 2e-2 * ref.abs().max(), d
+    hd, H, KVH = cfg.head_dim, cfg.heads, cfg.kv_heads
+    n, pos0 = 19, 5
+    ld = cfg.d + 2 * KVH * hd
+    qkv = torch.randn((n, ld), device="cuda", generator=g).to(torch.bfloat16)
+    before = qkv.clone()
+    assert m.L.dec_rope(qkv.data_ptr(), ld, n, cfg.d + KVH * hd, hd, pos0, m.cos.data_ptr(), m.sin.data_ptr(),
+                        None) == 0
+    torch.cuda.synchronize()
+    pos = torch.arange(pos0, pos0 + n, device="cuda")
+    q = before[:, : cfg.d].reshape(n, H, hd).float()
+    k = before[:, cfg.d: cfg.d + KVH * hd].reshape(n, KVH, hd).float()
+
+    def rope(t):
+        c, s = m.cos[pos][:, None, :], m.sin[pos][:, None, :]
+        x1, x2 = t[..., 0::2], t[..., 1::2]
+        return torch.stack([x1 * c - x2 * s, x1 * s + x2 * c], -1).flatten(-2)
+
+    ref = torch.cat([rope(q).reshape(n, -1), rope(k).reshape(n, -1), before[:, cfg.d + KVH * hd:].float()], 1)
+    assert (qkv.float() - ref).abs().max() < 3e-2
+    assert torch.equal(qkv[:, cfg.d + KVH * hd:], before[:, cfg.d + KVH * hd:])  # v untouched

@@ -173,8 +173,9 @@ class CausalLM:
         ang = torch.arange(cfg.n_ctx, dtype=torch.float64)[:, None] * inv[None, :]
         self.cos = ang.cos().float().to(device)
         self.sin = ang.sin().float().to(device)
-        self.kcache: List[torch.Tensor] = []
-        self.vcache: List[torch.Tensor] = []
+        # KV cache: one [layers, 2, n_ctx, kv_heads, head_dim] buffer allocated on first use and
+        # written in place (no per-token torch.cat regrowth: decode stays O(1) copies per token)
+        self.kv: Optional[torch.Tensor] = None
         self.pos = 0
         if self.hip:
             from .nomic import _lib
@@ -259,7 +260,7 @@ class CausalLM:
         return out.to(t.dtype)
 
     def reset(self):
-        self.kcache, self.vcache, self.pos = [], [], 0
+        self.pos = 0
 
     @torch.no_grad()
     def forward(self, ids: List[int]) -> torch.Tensor:
@@ -283,21 +284,18 @@ class CausalLM:
             v = qkv[:, cfg.d + KVH * hd:].reshape(n, KVH, hd)
             if not self.hip:
                 q, k = self._rope(q, pos), self._rope(k, pos)
-            if li >= len(self.kcache):
-                self.kcache.append(k)
-                self.vcache.append(v)
-            else:
-                self.kcache[li] = torch.cat([self.kcache[li], k])
-                self.vcache[li] = torch.cat([self.vcache[li], v])
-            K_, V_ = self.kcache[li], self.vcache[li]
-            if KVH != H:
-                K_ = K_.repeat_interleave(H // KVH, 1)
-                V_ = V_.repeat_interleave(H // KVH, 1)
+            if self.kv is None:
+                self.kv = torch.empty((cfg.layers, 2, cfg.n_ctx, KVH, hd), dtype=qkv.dtype, device=self.device)
+            self.kv[li, 0, self.pos: self.pos + n] = k
+            self.kv[li, 1, self.pos: self.pos + n] = v
+            L_ = self.pos + n
+            K_, V_ = self.kv[li, 0, :L_], self.kv[li, 1, :L_]
             qh, kh, vh = q.transpose(0, 1), K_.transpose(0, 1), V_.transpose(0, 1)
-            L_ = kh.shape[1]
-            mask = torch.ones((n, L_), dtype=torch.bool, device=self.device).tril(L_ - n)
+            # causal over the cache: query i (absolute position pos + i) sees keys 0..pos+i; a single
+            # decode token sees the whole cache, so no mask is needed
+            mask = None if n == 1 else torch.ones((n, L_), dtype=torch.bool, device=self.device).tril(L_ - n)
             a = torch.nn.functional.scaled_dot_product_attention(qh.unsqueeze(0), kh.unsqueeze(0), vh.unsqueeze(0),
-                                                                 attn_mask=mask)[0]
+                                                                 attn_mask=mask, enable_gqa=KVH != H)[0]
             a = a.transpose(0, 1).reshape(n, cfg.d).contiguous()
             x = self._mm(1, a, lw["o"], cfg.d, res=x)
             h = self._rms(x, lw["n2"])

@@ -40,10 +40,11 @@ def test_state_machine_cpu(uniq):
 
 
 @pytest.mark.gpu
-def test_decoder_hip_matches_cpu():
+@pytest.mark.parametrize("kv_heads", [8, 2])
+def test_decoder_hip_matches_cpu(kv_heads):
     import torch
     from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
-    cfg = DecoderConfig(layers=2)
+    cfg = DecoderConfig(layers=2, kv_heads=kv_heads)
     gpu = CausalLM.random(cfg, seed=3, device="cuda")
     cpu = CausalLM.random(cfg, seed=3, device="cpu")
     ids = [256] + list(b"the quick brown fox")
@@ -92,3 +93,17 @@ def test_decoder_rmsnorm_rope_kernels_vs_fp32():
     ref = torch.cat([rope(q).reshape(n, -1), rope(k).reshape(n, -1), before[:, cfg.d + KVH * hd:].float()], 1)
     assert (qkv.float() - ref).abs().max() < 3e-2
     assert torch.equal(qkv[:, cfg.d + KVH * hd:], before[:, cfg.d + KVH * hd:])  # v untouched
+
+
+def test_decoder_kv_cache_matches_full_recompute_cpu():
+    """Prefill + token-by-token decode through the preallocated KV cache (GQA: 8 q heads over
+    2 kv heads) gives the logits of one full forward over the same tokens."""
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
+    m = CausalLM.random(DecoderConfig(layers=2, heads=8, kv_heads=2), seed=3, device="cpu")
+    ids = [256] + list(b"hello world")
+    full = m.forward(ids + [65, 66])
+    m.reset()
+    m.forward(ids)
+    m.forward([65])
+    inc = m.forward([66])
+    assert (full - inc).abs().max() < 1e-4

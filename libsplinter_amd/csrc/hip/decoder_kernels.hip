@@ -5,6 +5,8 @@
 //   dec_rmsnorm   y = x * rsqrt(mean(x^2) + eps) * w      bf16 in/out, fp32 w
 //   dec_rope      llama "normal" RoPE (adjacent pairs) applied IN PLACE to the
 //                 q and k column ranges of the fused QKV GEMM output
+//   dec_attn_decode  single-token GQA attention over the KV cache (split-L over
+//                 4 waves, online softmax, LDS merge) — the per-token decode path
 //
 // Both are HBM-bound row kernels: one 64-lane wave per row, 16-B (8 x bf16)
 // vector accesses, statistics reduced with __shfl_xor over the full wavefront.
@@ -115,9 +117,103 @@ __global__ __launch_bounds__(256) void k_rope(uint16_t* __restrict__ qkv, long l
   }
 }
 
+// Single-token decode attention over the KV cache (GQA): one 256-thread workgroup per
+// query head h (kv head h / (H/KVH)); the 4 waves take interleaved 64-key chunks.  Inside a
+// chunk each lane scores one key (16-B loads along its cache row against the LDS-resident,
+// pre-scaled q), the wave keeps an online softmax (max/sum via __shfl_xor), and the V rows
+// are accumulated with p broadcast by __shfl, each lane owning DPL = hd/64 contiguous
+// output dims.  The 4 partial (m, l, acc) states merge in LDS.  K/V are [L, ldkv] rows
+// (ldkv = KVH*hd elements) starting at the kv head's column.
+template <int DPL>
+__global__ __launch_bounds__(256) void k_attn_decode(const uint16_t* __restrict__ q, const uint16_t* __restrict__ K,
+                                                     const uint16_t* __restrict__ V, long ldkv, int L, int grp,
+                                                     int hd, float scale, uint16_t* __restrict__ out) {
+  const int h = blockIdx.x;
+  const int kvh = h / grp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  __shared__ float qs[256];
+  __shared__ float wm[4], wl[4];
+  __shared__ float wacc[4][256];
+  for (int d = threadIdx.x; d < hd; d += 256) qs[d] = bf2f(q[(long)h * hd + d]) * scale;
+  __syncthreads();
+  const uint16_t* Kb = K + (long)kvh * hd;
+  const uint16_t* Vb = V + (long)kvh * hd + lane * DPL;
+  float m = -INFINITY, l = 0.f, acc[DPL];
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
+  for (int base = wave * 64; base < L; base += 256) {
+    const int j = base + lane;
+    float s = -INFINITY;
+    if (j < L) {
+      const uint16_t* kr = Kb + (long)j * ldkv;
+      float dot = 0.f;
+      for (int c = 0; c < hd; c += 8) {
+        float f[8];
+        unpack8(*(const uint4*)(kr + c), f);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) dot += f[e] * qs[c + e];
+      }
+      s = dot;
+    }
+    float cm = s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+    const float mn = fmaxf(m, cm);  // finite: lane 0 of every visited chunk holds a key
+    const float corr = __expf(m - mn);
+    const float p = j < L ? __expf(s - mn) : 0.f;
+    float ps = p;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o, 64);
+    l = l * corr + ps;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) acc[i] *= corr;
+    const int nv = min(64, L - base);
+    for (int t = 0; t < nv; ++t) {
+      const float pt = __shfl(p, t, 64);
+      const uint16_t* vr = Vb + (long)(base + t) * ldkv;
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) acc[i] += pt * bf2f(vr[i]);
+    }
+    m = mn;
+  }
+  if (lane == 0) { wm[wave] = m; wl[wave] = l; }
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) wacc[wave][lane * DPL + i] = acc[i];
+  __syncthreads();
+  const float M = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+  float c[4], den = 0.f;
+#pragma unroll
+  for (int w = 0; w < 4; ++w) { c[w] = __expf(wm[w] - M); den += wl[w] * c[w]; }
+  const float inv = 1.f / den;
+  for (int d = threadIdx.x; d < hd; d += 256) {
+    const float o = (wacc[0][d] * c[0] + wacc[1][d] * c[1] + wacc[2][d] * c[2] + wacc[3][d] * c[3]) * inv;
+    out[(long)h * hd + d] = __builtin_bit_cast(uint16_t, (__bf16)o);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// q: bf16 [H*hd] (one token, RoPE applied); k/v: bf16 cache rows [L, ldkv] (ldkv = KVH*hd);
+// out: bf16 [H*hd].  hd in {64, 128, 192, 256}, H % KVH == 0, L >= 1, 16-B aligned rows.
+int dec_attn_decode(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,
+                    float scale, void* out, hipStream_t s) {
+  if (L <= 0 || H <= 0 || KVH <= 0 || H % KVH || hd <= 0 || hd % 64 || hd > 256 || ldkv % 8 ||
+      ldkv < (long)KVH * hd || ((uintptr_t)k | (uintptr_t)v) % 16)
+    return (int)hipErrorInvalidValue;
+  const int grp = H / KVH;
+  const dim3 g((unsigned)H), b(256);
+  const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
+  uint16_t* oo = (uint16_t*)out;
+  switch (hd / 64) {
+    case 1: hipLaunchKernelGGL(k_attn_decode<1>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
+    case 2: hipLaunchKernelGGL(k_attn_decode<2>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
+    case 3: hipLaunchKernelGGL(k_attn_decode<3>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
+    default: hipLaunchKernelGGL(k_attn_decode<4>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
+  }
+  return (int)hipGetLastError();
+}
 
 // x/out: bf16 rows (strides in elements), w: fp32 [d]; d % 8 == 0, 16-B aligned rows.
 int dec_rmsnorm(const void* x, long ldx, const float* w, long T, int d, float eps, void* out, long ldo,

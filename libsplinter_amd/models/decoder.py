@@ -12,9 +12,10 @@ the MI355X replacement, demo-grade as SURVEY §2.1 N8 scopes it:
   residual, LM head) runs on the gfx950 MFMA GEMM (``nomic_gemm``) with its
   fused epilogues; RMSNorm and RoPE (llama "normal" adjacent-pair rotation, as
   llama.cpp applies for arch llama, in place on the q|k GEMM output) are the
-  HIP kernels of ``csrc/hip/decoder_kernels.hip``; the KV-cache attention and
-  the sampler use torch ops on the same device -- the decode step is
-  latency-bound and not a benchmark path;
+  HIP kernels of ``csrc/hip/decoder_kernels.hip``, and so is the per-token
+  decode attention over the KV cache (``dec_attn_decode``); prompt prefill
+  attention and the sampler use torch ops on the same device -- the decode
+  step is latency-bound and not a benchmark path;
 * tokenizer: greedy longest-match over the GGUF vocabulary (SentencePiece
   "▁" spaces, <0xNN> byte fallback) or, for random init, bytes 0..255 + BOS/EOS.
 
@@ -177,6 +178,7 @@ class CausalLM:
         # written in place (no per-token torch.cat regrowth: decode stays O(1) copies per token)
         self.kv: Optional[torch.Tensor] = None
         self.pos = 0
+        self.attn_kernel = True  # single-token decode through dec_attn_decode (False: SDPA, for A/B)
         if self.hip:
             from .nomic import _lib
             self.L = _lib()
@@ -186,6 +188,8 @@ class CausalLM:
                 self.L.dec_rmsnorm.restype = c_int
                 self.L.dec_rope.argtypes = [P, c_long, c_long, c_int, c_int, c_int, P, P, P]
                 self.L.dec_rope.restype = c_int
+                self.L.dec_attn_decode.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P]
+                self.L.dec_attn_decode.restype = c_int
                 self.L._dec_declared = True
             ok = all(n % 128 == 0 for n in (cfg.d + 2 * cfg.kv_heads * hd, cfg.d, 2 * cfg.ffn, vpad)) \
                 and cfg.d % 64 == 0 and cfg.ffn % 64 == 0
@@ -289,14 +293,24 @@ class CausalLM:
             self.kv[li, 0, self.pos: self.pos + n] = k
             self.kv[li, 1, self.pos: self.pos + n] = v
             L_ = self.pos + n
-            K_, V_ = self.kv[li, 0, :L_], self.kv[li, 1, :L_]
-            qh, kh, vh = q.transpose(0, 1), K_.transpose(0, 1), V_.transpose(0, 1)
-            # causal over the cache: query i (absolute position pos + i) sees keys 0..pos+i; a single
-            # decode token sees the whole cache, so no mask is needed
-            mask = None if n == 1 else torch.ones((n, L_), dtype=torch.bool, device=self.device).tril(L_ - n)
-            a = torch.nn.functional.scaled_dot_product_attention(qh.unsqueeze(0), kh.unsqueeze(0), vh.unsqueeze(0),
-                                                                 attn_mask=mask, enable_gqa=KVH != H)[0]
-            a = a.transpose(0, 1).reshape(n, cfg.d).contiguous()
+            if self.hip and self.attn_kernel and n == 1 and hd % 64 == 0 and hd <= 256:
+                # per-token decode: dec_attn_decode (one workgroup per q head, split-L online softmax)
+                from .nomic import _chk, _stream
+                a = torch.empty((1, cfg.d), dtype=qkv.dtype, device=self.device)
+                qrow = qkv[0, : cfg.d].contiguous()
+                _chk(self.L.dec_attn_decode(qrow.data_ptr(), self.kv[li, 0].data_ptr(), self.kv[li, 1].data_ptr(),
+                                            KVH * hd, L_, H, KVH, hd, hd ** -0.5, a.data_ptr(), _stream()),
+                     "attn_decode")
+            else:
+                K_, V_ = self.kv[li, 0, :L_], self.kv[li, 1, :L_]
+                qh, kh, vh = q.transpose(0, 1), K_.transpose(0, 1), V_.transpose(0, 1)
+                # causal over the cache: query i (absolute position pos + i) sees keys 0..pos+i; a single
+                # decode token sees the whole cache, so no mask is needed
+                mask = None if n == 1 else torch.ones((n, L_), dtype=torch.bool, device=self.device).tril(L_ - n)
+                a = torch.nn.functional.scaled_dot_product_attention(qh.unsqueeze(0), kh.unsqueeze(0),
+                                                                     vh.unsqueeze(0), attn_mask=mask,
+                                                                     enable_gqa=KVH != H)[0]
+                a = a.transpose(0, 1).reshape(n, cfg.d).contiguous()
             x = self._mm(1, a, lw["o"], cfg.d, res=x)
             h = self._rms(x, lw["n2"])
             f = self._mm(2, h, lw["ug"], cfg.ffn)

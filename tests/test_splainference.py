@@ -95,6 +95,32 @@ def test_decoder_rmsnorm_rope_kernels_vs_fp32():
     assert torch.equal(qkv[:, cfg.d + KVH * hd:], before[:, cfg.d + KVH * hd:])  # v untouched
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("hd,H,KVH", [(128, 32, 8), (64, 8, 8), (128, 16, 2)])
+def test_decoder_attn_decode_kernel_vs_fp32(hd, H, KVH):
+    """dec_attn_decode (csrc/hip/decoder_kernels.hip) against an fp32 softmax(q k^T) v reference,
+    cache lengths on both sides of the 64-key chunk and 256-key workgroup boundaries."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
+    m = CausalLM.random(DecoderConfig(layers=1), seed=1, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(7)
+    n_ctx = 1100
+    kv = torch.randn((2, n_ctx, KVH, hd), device="cuda", generator=g).to(torch.bfloat16)
+    q = torch.randn((H * hd,), device="cuda", generator=g).to(torch.bfloat16)
+    for L in (1, 63, 64, 65, 257, 1100):
+        out = torch.full((H * hd,), float("nan"), device="cuda").to(torch.bfloat16)
+        assert m.L.dec_attn_decode(q.data_ptr(), kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, L, H, KVH, hd,
+                                   hd ** -0.5, out.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        qf = q.float().reshape(H, hd)
+        kf = kv[0, :L].float().repeat_interleave(H // KVH, 1)  # [L, H, hd]
+        vf = kv[1, :L].float().repeat_interleave(H // KVH, 1)
+        p = torch.softmax(torch.einsum("hd,lhd->hl", qf, kf) * hd ** -0.5, -1)
+        ref = torch.einsum("hl,lhd->hd", p, vf).reshape(-1)
+        err = (out.float() - ref).abs().max()
+        assert err < 2e-2 * max(1.0, ref.abs().max().item()), (L, float(err))
+
+
 def test_decoder_kv_cache_matches_full_recompute_cpu():
     """Prefill + token-by-token decode through the preallocated KV cache (GQA: 8 q heads over
     2 kv heads) gives the logits of one full forward over the same tokens."""

@@ -6,7 +6,7 @@
 //   dec_rope      llama "normal" RoPE (adjacent pairs) applied IN PLACE to the
 //                 q and k column ranges of the fused QKV GEMM output
 //   dec_attn_decode  single-token GQA attention over the KV cache (split-L over
-//                 4 waves, online softmax, LDS merge) — the per-token decode path
+//                 16 waves, online softmax, LDS merge) — the per-token decode path
 //
 // Both are HBM-bound row kernels: one 64-lane wave per row, 16-B (8 x bf16)
 // vector accesses, statistics reduced with __shfl_xor over the full wavefront.
@@ -117,31 +117,34 @@ __global__ __launch_bounds__(256) void k_rope(uint16_t* __restrict__ qkv, long l
   }
 }
 
-// Single-token decode attention over the KV cache (GQA): one 256-thread workgroup per
-// query head h (kv head h / (H/KVH)); the 4 waves take interleaved 64-key chunks.  Inside a
+// Single-token decode attention over the KV cache (GQA): one 1024-thread workgroup per
+// query head h (kv head h / (H/KVH)); its 16 waves take interleaved 64-key chunks (a decode
+// step launches only H workgroups, so the split-L width lives inside the workgroup).  Inside a
 // chunk each lane scores one key (16-B loads along its cache row against the LDS-resident,
 // pre-scaled q), the wave keeps an online softmax (max/sum via __shfl_xor), and the V rows
 // are accumulated with p broadcast by __shfl, each lane owning DPL = hd/64 contiguous
-// output dims.  The 4 partial (m, l, acc) states merge in LDS.  K/V are [L, ldkv] rows
+// output dims.  The 16 partial (m, l, acc) states merge in LDS.  K/V are [L, ldkv] rows
 // (ldkv = KVH*hd elements) starting at the kv head's column.
+constexpr int kDecWaves = 16;
+
 template <int DPL>
-__global__ __launch_bounds__(256) void k_attn_decode(const uint16_t* __restrict__ q, const uint16_t* __restrict__ K,
+__global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* __restrict__ q, const uint16_t* __restrict__ K,
                                                      const uint16_t* __restrict__ V, long ldkv, int L, int grp,
                                                      int hd, float scale, uint16_t* __restrict__ out) {
   const int h = blockIdx.x;
   const int kvh = h / grp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   __shared__ float qs[256];
-  __shared__ float wm[4], wl[4];
-  __shared__ float wacc[4][256];
-  for (int d = threadIdx.x; d < hd; d += 256) qs[d] = bf2f(q[(long)h * hd + d]) * scale;
+  __shared__ float wm[kDecWaves], wl[kDecWaves];
+  __shared__ float wacc[kDecWaves][256];
+  for (int d = threadIdx.x; d < hd; d += kDecWaves * 64) qs[d] = bf2f(q[(long)h * hd + d]) * scale;
   __syncthreads();
   const uint16_t* Kb = K + (long)kvh * hd;
   const uint16_t* Vb = V + (long)kvh * hd + lane * DPL;
   float m = -INFINITY, l = 0.f, acc[DPL];
 #pragma unroll
   for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
-  for (int base = wave * 64; base < L; base += 256) {
+  for (int base = wave * 64; base < L; base += kDecWaves * 64) {
     const int j = base + lane;
     float s = -INFINITY;
     if (j < L) {
@@ -168,6 +171,7 @@ __global__ __launch_bounds__(256) void k_attn_decode(const uint16_t* __restrict_
 #pragma unroll
     for (int i = 0; i < DPL; ++i) acc[i] *= corr;
     const int nv = min(64, L - base);
+#pragma unroll 8
     for (int t = 0; t < nv; ++t) {
       const float pt = __shfl(p, t, 64);
       const uint16_t* vr = Vb + (long)(base + t) * ldkv;
@@ -180,13 +184,18 @@ __global__ __launch_bounds__(256) void k_attn_decode(const uint16_t* __restrict_
 #pragma unroll
   for (int i = 0; i < DPL; ++i) wacc[wave][lane * DPL + i] = acc[i];
   __syncthreads();
-  const float M = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
-  float c[4], den = 0.f;
+  float M = wm[0];
 #pragma unroll
-  for (int w = 0; w < 4; ++w) { c[w] = __expf(wm[w] - M); den += wl[w] * c[w]; }
+  for (int w = 1; w < kDecWaves; ++w) M = fmaxf(M, wm[w]);
+  float c[kDecWaves], den = 0.f;
+#pragma unroll
+  for (int w = 0; w < kDecWaves; ++w) { c[w] = __expf(wm[w] - M); den += wl[w] * c[w]; }
   const float inv = 1.f / den;
-  for (int d = threadIdx.x; d < hd; d += 256) {
-    const float o = (wacc[0][d] * c[0] + wacc[1][d] * c[1] + wacc[2][d] * c[2] + wacc[3][d] * c[3]) * inv;
+  for (int d = threadIdx.x; d < hd; d += kDecWaves * 64) {
+    float o = 0.f;
+#pragma unroll
+    for (int w = 0; w < kDecWaves; ++w) o += wacc[w][d] * c[w];
+    o *= inv;
     out[(long)h * hd + d] = __builtin_bit_cast(uint16_t, (__bf16)o);
   }
 }
@@ -203,7 +212,7 @@ int dec_attn_decode(const void* q, const void* k, const void* v, long ldkv, int 
       ldkv < (long)KVH * hd || ((uintptr_t)k | (uintptr_t)v) % 16)
     return (int)hipErrorInvalidValue;
   const int grp = H / KVH;
-  const dim3 g((unsigned)H), b(256);
+  const dim3 g((unsigned)H), b(kDecWaves * 64);
   const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
   uint16_t* oo = (uint16_t*)out;
   switch (hd / 64) {

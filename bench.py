@@ -57,15 +57,49 @@ def parse():
                         "even at N=1, to measure the routing overhead on one GPU")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: "
                    "ranks may share a GPU, collectives staged through the host)")
+    p.add_argument("--writer-streams", type=int, default=32,
+                   help="concurrent HIP streams issuing the step's set batch (BASELINE config #2: 32 writer "
+                        "streams); each gets an equal share of the batch")
+    p.add_argument("--reader-streams", type=int, default=32, help="concurrent HIP streams issuing the get batch")
+    p.add_argument("--mop", type=int, default=1, choices=[0, 1, 2],
+                   help="store scrub mode (splinter_set_mop): 1 = hybrid, the default of every store the "
+                        "reference creates (reference splinter.c:192-193) and of its stress tools; 0 = none")
+    p.add_argument("--host-api", type=int, default=0, metavar="THREADS",
+                   help="also measure the per-call C API (splinter_set/get through the device command ring) "
+                        "from THREADS host threads, outside the timed region; 0 = skip")
     return p.parse_args()
+
+
+def _launch_ranks(args) -> int:
+    """--gpus N > 1 without a torchrun environment: start N ranks as CHILD processes (torchrun,
+    one process per GPU, rendezvous on 127.0.0.1) before this process touches the GPU, relay
+    their output and exit with their status.  Never exec: this process stays the parent."""
+    import socket
+    import subprocess
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "4")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(_launch_ranks(args))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled run",
+              file=sys.stderr)
+        sys.exit(2)
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     routed = world > 1 or args.force_routed
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -87,7 +121,7 @@ def main():
     name = f"bench{os.getpid()}r{rank}"
     t0 = time.time()
     arena = HbmArena.create(name, slots=slots, max_val=args.max_val, embeddings=False)
-    arena.store.set_mop(0)  # throughput mode: no scrubbing (reference stress default)
+    arena.store.set_mop(args.mop)  # 1 = hybrid scrub, the reference's store default
     kv = ShardedKV(GpuShard(arena))
     rkv = None
     if routed:
@@ -150,6 +184,12 @@ def main():
     # the serial one (profiles/r1_mixed_overlap.md).
     from libsplinter_amd.utils.streams import stream as hip_stream
     s_get, s_set = hip_stream("high"), hip_stream("normal")
+    # BASELINE config #2: the set batch is issued by --writer-streams concurrent client streams and the
+    # get batch by --reader-streams (streams share the HIP runtime's hardware queues, at most
+    # GPU_MAX_HW_QUEUES per priority level; readers at high priority, writers at normal)
+    nw, nr = max(1, args.writer_streams), max(1, args.reader_streams)
+    w_streams = [s_set] + [hip_stream("normal") for _ in range(nw - 1)]
+    r_streams = [s_get] + [hip_stream("high") for _ in range(nr - 1)]
     s_emb = None
     if args.overlap and not args.kv_cus and world == 1:
         s_emb = hip_stream("low")
@@ -157,23 +197,34 @@ def main():
     if args.kv_cus and world == 1:
         from libsplinter_amd.utils.streams import cu_mask_bits, masked_stream
         kv_bits, emb_bits = cu_mask_bits(args.kv_cus), cu_mask_bits(32 - args.kv_cus, args.kv_cus)
-        s_get, s_set, s_emb = masked_stream(kv_bits), masked_stream(kv_bits), masked_stream(emb_bits)
+        w_streams = [masked_stream(kv_bits) for _ in range(nw)]
+        r_streams = [masked_stream(kv_bits) for _ in range(nr)]
+        s_emb = masked_stream(emb_bits)
         log(f"[bench] overlapped phases: KV on {len(kv_bits)} CUs, encoder on {len(emb_bits)} CUs")
     stats = arena.stats
+
+    def _parts(n, k):
+        b = [n * j // k for j in range(k + 1)]
+        return [(b[j], b[j + 1]) for j in range(k) if b[j + 1] > b[j]]
+
+    set_parts, get_parts = _parts(n_set, nw), _parts(n_get, nr)
 
     def step_local(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
         cur = torch.cuda.current_stream()
+        kv_streams = w_streams[:len(set_parts)] + r_streams[:len(get_parts)]
         if n_set:
-            s_set.wait_stream(cur)
-            s_get.wait_stream(cur)
-            with torch.cuda.stream(s_set):
-                arena.set(SK, SV, SL)
-            with torch.cuda.stream(s_get):
-                arena.get(GK, out=gout)
+            for s in kv_streams:
+                s.wait_stream(cur)
+            for s, (a, b) in zip(w_streams, set_parts):
+                with torch.cuda.stream(s):
+                    arena.set(SK[a:b], SV[a:b], SL[a:b])
+            for s, (a, b) in zip(r_streams, get_parts):
+                with torch.cuda.stream(s):
+                    arena.get(GK[a:b], out=gout[a:b])
             if s_emb is None:
-                cur.wait_stream(s_set)
-                cur.wait_stream(s_get)
+                for s in kv_streams:
+                    cur.wait_stream(s)
         if embedder is not None:
             if s_emb is None:
                 embedder.run()
@@ -183,8 +234,8 @@ def main():
                     embedder.run()
                 cur.wait_stream(s_emb)
         if s_emb is not None and n_set:
-            cur.wait_stream(s_set)
-            cur.wait_stream(s_get)
+            for s in kv_streams:
+                cur.wait_stream(s)
 
     # N > 1: a host-sync-free software pipeline (parallel/routed.py).  Per step i:
     #   s_req : pack + request all-to-alls of batch i         (overlaps embed_i)
@@ -323,7 +374,8 @@ def main():
             "keys_per_gpu": kpg, "slots_per_gpu": slots, "global_batch": args.batch * world,
             "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
             "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),
-            "mode": args.mode,
+            "mode": args.mode, "mop": args.mop, "value_len": args.value_len,
+            "writer_streams": nw if not routed else 1, "reader_streams": nr if not routed else 1,
         },
         "kv_ops_per_s": kv_ops_s,
         "embed_vectors_per_s": emb_vps,

@@ -93,7 +93,8 @@ class ShardBidSnapshot(ctypes.Structure):
 
 class Arena(ctypes.Structure):
     """spl_arena_t (arena_api.h)."""
-    _fields_ = [("base", c_void_p), ("slots", c_u32), ("max_val", c_u32), ("stride", c_u32), ("flags", c_u32)]
+    _fields_ = [("base", c_void_p), ("slots", c_u32), ("max_val", c_u32), ("stride", c_u32), ("flags", c_u32),
+                ("notify", c_u64)]
 
 
 ENUM_CB = ctypes.CFUNCTYPE(None, c_char_p, c_u64, c_void_p)

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include "splinter_layout.hpp"
+#include "arena_api.h"
 
 namespace spl {
 namespace dev {
@@ -45,6 +46,7 @@ struct Arena {
   uint32_t max_val;
   uint32_t stride;
   uint32_t flags;  // bit0: event bus armed (maintain the dirty mask)
+  uint64_t notify = 0;  // device address of the host-mapped notify word (event-bus proxy), 0 = none
   __device__ __forceinline__ splinter_header* hdr() const { return (splinter_header*)base; }
   __device__ __forceinline__ uint8_t* slot(size_t i) const { return base + kHeaderBytes + i * (size_t)stride; }
   __device__ __forceinline__ uint8_t* value(size_t i) const {
@@ -97,6 +99,32 @@ __device__ __forceinline__ void release() {
   drain();
 }
 
+// Kernel-side view of a launch descriptor.  The event bus counts as armed when the launching
+// process says so (flags bit 0) OR the device header records an owner (any process on the node
+// may have called splinter_event_bus_init on this arena: hbm_store.hip mirrors owner_pid into
+// the device header), so batch kernels of every attached process maintain the dirty mask.
+__device__ __forceinline__ Arena from_api(const spl_arena_t& aa) {
+  Arena d;
+  d.base = (uint8_t*)aa.base;
+  d.slots = aa.slots;
+  d.max_val = aa.max_val;
+  d.stride = aa.stride;
+  d.notify = aa.notify;
+  const uint32_t owner = __hip_atomic_load((const uint32_t*)&((splinter_header*)aa.base)->event_bus.owner_pid,
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  d.flags = aa.flags | (owner != 0 ? 1u : 0u);
+  return d;
+}
+
+// Wake the host event-bus proxy: one system-scope (vector) store of 1 into the host-mapped
+// notify word, after this lane's dirty-mask updates have drained.  Idempotent, so any number of
+// blocks / kernels / processes may store it; the proxy clears it before it signals the eventfd.
+__device__ __forceinline__ void notify_host(const Arena& a) {
+  if (!(a.flags & 1u) || !a.notify) return;
+  drain();
+  __hip_atomic_store((uint32_t*)a.notify, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // ------------------------------------------------------------- keys ----
 // A key arrives as a NUL-padded record of `kstride` bytes (16/32/48/64).
 // Canonical form: first 63 bytes, NUL padded to 64, FNV-1a over its length.
@@ -115,14 +143,10 @@ struct KeyT {
 };
 using Key = KeyT<16>;
 
+// Canonicalise key words already in k.w (the first kstride bytes of a record): length, FNV-1a,
+// and every byte at or past the terminating NUL (or byte 63) zeroed.
 template <int KW>
-__device__ __forceinline__ void load_key(KeyT<KW>& k, const char* rec, int kstride) {
-  const uint4* r = (const uint4*)rec;
-#pragma unroll
-  for (int c = 0; c < KW / 4; ++c) {
-    uint4 v = (c * 16 < kstride) ? r[c] : make_uint4(0, 0, 0, 0);
-    k.w[4 * c + 0] = v.x; k.w[4 * c + 1] = v.y; k.w[4 * c + 2] = v.z; k.w[4 * c + 3] = v.w;
-  }
+__device__ __forceinline__ void canon_key(KeyT<KW>& k, int kstride) {
   uint64_t h = kFnvOffset;
   uint32_t len = 0;
   bool live = true;
@@ -145,6 +169,17 @@ __device__ __forceinline__ void load_key(KeyT<KW>& k, const char* rec, int kstri
   }
   k.len = len;
   k.hash = h;
+}
+
+template <int KW>
+__device__ __forceinline__ void load_key(KeyT<KW>& k, const char* rec, int kstride) {
+  const uint4* r = (const uint4*)rec;
+#pragma unroll
+  for (int c = 0; c < KW / 4; ++c) {
+    uint4 v = (c * 16 < kstride) ? r[c] : make_uint4(0, 0, 0, 0);
+    k.w[4 * c + 0] = v.x; k.w[4 * c + 1] = v.y; k.w[4 * c + 2] = v.z; k.w[4 * c + 3] = v.w;
+  }
+  canon_key(k, kstride);
 }
 
 // Compare the stored key with ours through sc1 loads, 8 bytes at a time, up
@@ -708,6 +743,140 @@ __device__ int32_t integer_op(const Arena& a, const KeyT<KW>& k, int op, uint64_
   if (result) *result = x;
   *out_idx = i;
   return kOk;
+}
+
+// APPEND under the slot seqlock (reference splinter.c:1062-1108): claim e -> e+1, bound check,
+// copy the new bytes at the current tail, publish val_len, release, e+1.  The tail is not 16-B
+// aligned in general, so the copy is bytewise (appends are small, streaming text).  `src` is a
+// device pointer; the caller pulses / marks dirty on success.
+template <int KW>
+__device__ int32_t append_op(const Arena& a, const KeyT<KW>& k, const uint8_t* src, uint32_t len,
+                             uint32_t* new_len, long* out_idx) {
+  if (len == 0) return kInval;
+  const long i = find(a, k);
+  if (i < 0) return kNoEnt;
+  uint8_t* s = a.slot((size_t)i);
+  const uint64_t e = slot_epoch(s);
+  if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
+  if (slot_hash(s) != k.hash || !key_eq(s, k)) { aadd64(epoch_ptr(s), 1); return kNoEnt; }
+  const uint32_t cur = ald32(s + kOffValLen);
+  if ((uint64_t)cur + len > a.max_val) { aadd64(epoch_ptr(s), 1); return kMsgSize; }
+  uint8_t* v = a.value((size_t)i) + cur;
+  for (uint32_t b = 0; b < len; ++b) v[b] = src[b];
+  release();
+  ast32(s + kOffValLen, cur + len);
+  drain();
+  aadd64(epoch_ptr(s), 1);
+  *new_len = cur + len;
+  *out_idx = i;
+  return kOk;
+}
+
+// strtoull(s, 0, 0) of an ASCII value (at most 15 bytes, as the reference parses it):
+// 0x / 0X prefix = hex, a leading 0 = octal, else decimal; stops at the first invalid digit.
+__device__ __forceinline__ uint64_t parse_u64(const uint8_t* p, uint32_t n) {
+  uint32_t i = 0;
+  uint64_t base = 10, x = 0;
+  if (n >= 2 && p[0] == '0' && (p[1] == 'x' || p[1] == 'X')) { base = 16; i = 2; }
+  else if (n >= 1 && p[0] == '0') { base = 8; i = 1; }
+  for (; i < n; ++i) {
+    const uint8_t c = p[i];
+    uint64_t d;
+    if (c >= '0' && c <= '9') d = c - '0';
+    else if (c >= 'a' && c <= 'f') d = c - 'a' + 10;
+    else if (c >= 'A' && c <= 'F') d = c - 'A' + 10;
+    else break;
+    if (d >= base) break;
+    x = x * base + d;
+  }
+  return x;
+}
+
+// set_named_type under the seqlock, with the BIGUINT promotion done in place on the device
+// (reference splinter.c:637-680 parses a short ASCII value with strtoull, or takes its raw
+// bytes, into a u64; its bump allocation from val_brk aliases slot 0's value, so the u64 is
+// written into the slot's own value row instead -- docs/DIVERGENCES.md).
+template <int KW>
+__device__ int32_t named_type_op(const Arena& a, const KeyT<KW>& k, uint8_t mask, long* out_idx) {
+  const long i = find(a, k);
+  if (i < 0) return kNoEnt;
+  uint8_t* s = a.slot((size_t)i);
+  const uint64_t e = slot_epoch(s);
+  if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
+  if (slot_hash(s) != k.hash || !key_eq(s, k)) { aadd64(epoch_ptr(s), 1); return kNoEnt; }
+  const uint32_t cur = ald32(s + kOffValLen);
+  if ((mask & SPL_SLOT_TYPE_BIGUINT) && cur < 8 && a.max_val >= 8) {
+    uint8_t* v = a.value((size_t)i);
+    uint8_t tmp[16];
+    for (uint32_t b = 0; b < 16; ++b) tmp[b] = b < cur ? v[b] : 0;
+    uint64_t x = 0;
+    if (cur > 0 && tmp[0] >= '0' && tmp[0] <= '9') x = parse_u64(tmp, cur < 15 ? cur : 15);
+    else for (uint32_t b = 0; b < cur; ++b) x |= (uint64_t)tmp[b] << (8 * b);
+    __builtin_memcpy(v, &x, 8);
+    release();
+    ast32(s + kOffValLen, 8);
+  }
+  ast8(s + kOffType, mask);
+  drain();
+  aadd64(epoch_ptr(s), 1);
+  *out_idx = i;
+  return kOk;
+}
+
+// Keyed metadata ops (spl_arena_meta, the command ring):
+// op: 0 set_label, 1 unset_label, 2 bump, 3 get_epoch, 4 watch_register,
+//     5 watch_unregister, 6 pulse_keygroup, 7 set_as_system, 8 retrain,
+//     9 set_named_type (arg = mask, BIGUINT promotion on the device), 10 set ctime,
+//     11 set atime, 12 find (out = slot index)
+// *mut: the op changed the slot (global epoch +1; dirty mask already marked here).
+template <int KW>
+__device__ int32_t meta_op(const Arena& a, const KeyT<KW>& k, int op, uint64_t arg, uint64_t* out, bool* mut) {
+  *mut = false;
+  *out = 0;
+  if (op == 9) {
+    long idx = -1;
+    const int32_t rc = named_type_op(a, k, (uint8_t)arg, &idx);
+    if (rc == kOk) { *mut = true; mark_dirty(a, (size_t)idx); }
+    return rc;
+  }
+  const long idx = find(a, k);
+  if (idx < 0) return kNoEnt;
+  uint8_t* s = a.slot((size_t)idx);
+  switch (op) {
+    case 0: aor64((uint64_t*)(s + kOffBloom), arg); *mut = true; mark_dirty(a, idx); return kOk;
+    case 1: aand64((uint64_t*)(s + kOffBloom), ~arg); *mut = true; mark_dirty(a, idx); return kOk;
+    case 2: {
+      const uint64_t e = slot_epoch(s);
+      if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
+      pulse(a, s);
+      drain();
+      aadd64(epoch_ptr(s), 1);
+      return kOk;
+    }
+    case 3: *out = slot_epoch(s); return kOk;
+    case 4: aor64((uint64_t*)(s + kOffWatch), 1ull << (arg & 63)); return kOk;
+    case 5: aand64((uint64_t*)(s + kOffWatch), ~(1ull << (arg & 63))); return kOk;
+    case 6: pulse(a, s); return kOk;
+    case 7:
+      ast8(s + kOffType, (uint8_t)SPL_SLOT_TYPE_BINARY);
+      ast32((uint32_t*)(s + kOffValLen), a.max_val);
+      return kOk;
+    case 8:
+      ast64(epoch_ptr(s), 3);
+      drain();
+      if (a.stride == kSlotEmbedBytes)
+        for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ((uint4*)(s + kOffEmbed))[c] = make_uint4(0, 0, 0, 0);
+      release();
+      ast64(epoch_ptr(s), 4);
+      *mut = true;
+      pulse(a, s);
+      mark_dirty(a, idx);
+      return kOk;
+    case 10: ast64((uint64_t*)(s + kOffCtime), arg); return kOk;
+    case 11: ast64((uint64_t*)(s + kOffAtime), arg); return kOk;
+    case 12: *out = (uint64_t)idx; return kOk;
+    default: return kInval;
+  }
 }
 
 }  // namespace dev

@@ -84,15 +84,7 @@ inline int grid_for_b(long n, int b) {  // same resident-thread cap as grid_for,
   return (int)(g > cap ? cap : g);
 }
 
-__device__ __forceinline__ Arena to_dev(const spl_arena_t& a) {
-  Arena d;
-  d.base = (uint8_t*)a.base;
-  d.slots = a.slots;
-  d.max_val = a.max_val;
-  d.stride = a.stride;
-  d.flags = a.flags;
-  return d;
-}
+__device__ __forceinline__ Arena to_dev(const spl_arena_t& a) { return from_api(a); }
 
 // Block-wide sum of a per-thread counter; thread 0 returns the total.
 __device__ __forceinline__ uint64_t block_sum(uint64_t v) {
@@ -125,7 +117,10 @@ __device__ __forceinline__ void flush_stats(const Arena& a, Stats st, uint64_t* 
       if (ag) aadd64(stats + 2, ag);
       if (ms) aadd64(stats + 3, ms);
     }
-    if (mu) aadd64(&a.hdr()->epoch, mu);
+    if (mu) {
+      aadd64(&a.hdr()->epoch, mu);
+      notify_host(a);
+    }
   }
 }
 
@@ -164,9 +159,9 @@ __global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys
     Key k;
     load_key(k, keys + i * (long)kstride, kstride);
     const uint32_t len = lens[i];
-    int32_t rc = kAgain;
+    int32_t rc = len > (uint32_t)vstride ? kMsgSize : kAgain;  // a length past the source row: no over-read
     long idx = -1;
-    for (int t = 0; t <= max_retry; ++t) {
+    for (int t = 0; t <= max_retry && rc == kAgain; ++t) {
       ++st.attempts;
       rc = set_op<MO>(a, k, vals + i * (long)vstride, len, &idx);
       if (rc != kAgain) break;
@@ -244,7 +239,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
         load_key(k[j], keys + i * (long)kstride, kstride);
         len[j] = lens[i];
         ++st.attempts;
-        if (len[j] == 0 || len[j] > a.max_val) c[j].rc = kMsgSize;
+        if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride) c[j].rc = kMsgSize;
         else c[j] = claim_set(a, k[j]);
       }
     }
@@ -476,7 +471,7 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
       if (op[j] >= 0) {
         ++st.attempts;
         ++tries[j];
-        if (len[j] == 0 || len[j] > a.max_val) c[j].rc = kMsgSize;
+        if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride) c[j].rc = kMsgSize;
         else c[j] = claim_set(a, k[j]);
       }
     }
@@ -701,59 +696,10 @@ __global__ __launch_bounds__(kBlock) void k_meta(spl_arena_t aa, const char* key
     Key k;
     load_key(k, keys + i * (long)kstride, kstride);
     const uint64_t arg = args ? args[i] : 0;
-    const long idx = find(a, k);
-    int32_t rc = kOk;
     uint64_t o = 0;
-    if (idx < 0) {
-      rc = kNoEnt;
-    } else {
-      uint8_t* s = a.slot((size_t)idx);
-      switch (op) {
-        case 0: aor64((uint64_t*)(s + kOffBloom), arg); ++muts; mark_dirty(a, idx); break;
-        case 1: aand64((uint64_t*)(s + kOffBloom), ~arg); ++muts; mark_dirty(a, idx); break;
-        case 2: {
-          const uint64_t e = slot_epoch(s);
-          if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) { rc = kAgain; break; }
-          pulse(a, s);
-          drain();
-          aadd64(epoch_ptr(s), 1);
-          break;
-        }
-        case 3: o = slot_epoch(s); break;
-        case 4: aor64((uint64_t*)(s + kOffWatch), 1ull << (arg & 63)); break;
-        case 5: aand64((uint64_t*)(s + kOffWatch), ~(1ull << (arg & 63))); break;
-        case 6: pulse(a, s); break;
-        case 7:
-          ast8(s + kOffType, (uint8_t)SPL_SLOT_TYPE_BINARY);
-          ast32((uint32_t*)(s + kOffValLen), a.max_val);
-          break;
-        case 8:
-          ast64(epoch_ptr(s), 3);
-          drain();
-          if (a.stride == kSlotEmbedBytes)
-            for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ((uint4*)(s + kOffEmbed))[c] = make_uint4(0, 0, 0, 0);
-          release();
-          ast64(epoch_ptr(s), 4);
-          ++muts;
-          pulse(a, s);
-          mark_dirty(a, idx);
-          break;
-        case 9: {
-          const uint64_t e = slot_epoch(s);
-          if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) { rc = kAgain; break; }
-          ast8(s + kOffType, (uint8_t)arg);
-          drain();
-          aadd64(epoch_ptr(s), 1);
-          ++muts;
-          mark_dirty(a, idx);
-          break;
-        }
-        case 10: ast64((uint64_t*)(s + kOffCtime), arg); break;
-        case 11: ast64((uint64_t*)(s + kOffAtime), arg); break;
-        case 12: o = (uint64_t)idx; break;
-        default: rc = kInval;
-      }
-    }
+    bool mut = false;
+    const int32_t rc = meta_op(a, k, op, arg, &o, &mut);
+    if (mut) ++muts;
     if (out) out[i] = o;
     if (status) status[i] = rc;
   }
@@ -840,14 +786,16 @@ __global__ __launch_bounds__(kBlock) void k_embed_get(spl_arena_t aa, const char
 // mode 2: embedded (hash != 0 and vector not all-zero)  mode 3: occupied (hash != 0)
 // Compacts matching slot indices with one atomic per wave (ballot + mbcnt).
 __global__ __launch_bounds__(kBlock) void k_scan(spl_arena_t aa, int mode, uint64_t mask, uint32_t* out_idx,
-                                                 uint64_t* out_epoch, uint32_t cap, uint32_t* counter) {
+                                                 uint64_t* out_epoch, uint32_t cap, uint32_t* counter,
+                                                 uint32_t first, uint32_t last) {
   const Arena a = to_dev(aa);
   const int lane = threadIdx.x & 63;
-  for (size_t base = blockIdx.x * (size_t)blockDim.x; base < a.slots; base += (size_t)gridDim.x * blockDim.x) {
+  const size_t end = last < a.slots ? last : a.slots;
+  for (size_t base = first + blockIdx.x * (size_t)blockDim.x; base < end; base += (size_t)gridDim.x * blockDim.x) {
     const size_t i = base + threadIdx.x;  // base is block-uniform: every lane reaches the ballot
     bool hit = false;
     uint64_t ep = 0;
-    if (i < a.slots) {
+    if (i < end) {
       const uint8_t* s = a.slot(i);
       const uint64_t h = slot_hash(s);
       if (mode == 4) {  // watchdog: writer-active (odd) epochs, claimed-but-unpublished slots included
@@ -1157,8 +1105,15 @@ int spl_arena_embed_get(spl_arena_t a, const char* keys, int kstride, float* vec
 
 int spl_arena_scan(spl_arena_t a, int mode, uint64_t mask, uint32_t* out_idx, uint64_t* out_epoch, uint32_t cap,
                    uint32_t* counter, hipStream_t s) {
-  hipLaunchKernelGGL(k_scan, dim3(grid_for(a.slots)), dim3(kBlock), 0, s, a, mode, mask, out_idx, out_epoch, cap,
-                     counter);
+  return spl_arena_scan_range(a, mode, mask, 0, a.slots, out_idx, out_epoch, cap, counter, s);
+}
+
+int spl_arena_scan_range(spl_arena_t a, int mode, uint64_t mask, uint32_t first, uint32_t last, uint32_t* out_idx,
+                         uint64_t* out_epoch, uint32_t cap, uint32_t* counter, hipStream_t s) {
+  if (last > a.slots) last = a.slots;
+  if (first >= last) return 0;
+  hipLaunchKernelGGL(k_scan, dim3(grid_for(last - first)), dim3(kBlock), 0, s, a, mode, mask, out_idx, out_epoch, cap,
+                     counter, first, last);
   return (int)hipGetLastError();
 }
 

@@ -1,0 +1,431 @@
+// cmd_ring.hip — the per-call command ring of an HBM store (protocol: cmd_ring.hpp).
+//
+// Device side: k_ring_worker, ONE wave; lane i serves ring entry i.  Every word the host wrote is
+// read with system-scope loads (global_load ... sc0 sc1: no L1/L2 line of the pinned host page can
+// be stale across a reuse of the entry) and every word the host reads is written with
+// system-scope stores, drained before the DONE doorbell store, so neither side needs a fence over
+// the whole cache.  The arena itself is touched only through the seqlock ops of arena_dev.hpp,
+// exactly as the batch kernels touch it (set_op / get_op / unset_op / append_op / integer_op /
+// meta_op), so single calls and batches interleave under the same protocol.
+#include <hip/hip_runtime.h>
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <immintrin.h>
+#include <sched.h>
+#include <time.h>
+
+#include "arena_dev.hpp"
+#include "cmd_ring.hpp"
+
+namespace spl {
+
+namespace {
+
+using namespace spl::dev;
+
+typedef unsigned int u32x4s_t __attribute__((ext_vector_type(4)));
+
+// 16-B system-scope load / store (hipcc does not track inline-asm memory ops: ld16s results are
+// valid after sys_wait(); st16s callers drain() before anything that publishes the bytes).
+__device__ __forceinline__ u32x4s_t ld16s(const void* p) {
+  u32x4s_t r;
+  asm volatile("global_load_dwordx4 %0, %1, off sc0 sc1" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ void sys_wait(u32x4s_t& a) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(a)::"memory"); }
+__device__ __forceinline__ void st16s(void* p, u32x4s_t v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ uint32_t ld32s(const void* p) {
+  return __hip_atomic_load((const uint32_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ uint64_t ld64s(const void* p) {
+  return __hip_atomic_load((const uint64_t*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st32s(void* p, uint32_t v) {
+  __hip_atomic_store((uint32_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st64s(void* p, uint64_t v) {
+  __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// host payload -> device scratch, chunks [from, n16) (8 loads in flight)
+__device__ void pull(uint4* dst, const uint8_t* src, uint32_t from, uint32_t n16) {
+  for (uint32_t b = from; b < n16; b += 8) {
+    u32x4s_t t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = ld16s(src + 16 * (size_t)min(b + (uint32_t)q, n16 - 1));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) sys_wait(t[q]);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (b + (uint32_t)q < n16) dst[b + q] = make_uint4(t[q].x, t[q].y, t[q].z, t[q].w);
+  }
+}
+
+// device bytes -> host payload, n16 chunks: 8 loads in flight, system-scope stores
+__device__ void push(uint8_t* dst, const uint4* src, uint32_t n16) {
+  for (uint32_t b = 0; b < n16; b += 8) {
+    uint4 t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = src[min(b + (uint32_t)q, n16 - 1)];
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (b + (uint32_t)q < n16) st16s(dst + 16 * (size_t)(b + q), u32x4s_t{t[q].x, t[q].y, t[q].z, t[q].w});
+  }
+}
+
+__device__ __forceinline__ void count_mutation(const Arena& a, long idx) {
+  aadd64(&a.hdr()->epoch, 1);
+  if (idx >= 0) mark_dirty(a, (size_t)idx);
+  notify_host(a);
+}
+
+constexpr uint32_t kSpec = 16;  // payload chunks fetched speculatively with the record (256 B)
+
+// SET for one lane: claim, payload with write-through (sc1) stores, drain, publish -- no L2
+// write-back fence on this latency path (MO 3 of arena_dev.hpp; readers are unchanged).  A value
+// row that is not a multiple of 16 B ends in bytewise plain stores: those take the release path.
+__device__ int32_t ring_set(const Arena& a, const Key& k, const uint8_t* pay, uint32_t len) {
+  if (len == 0 || len > a.max_val) return kMsgSize;
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  const Claim c = claim_set(a, k);
+  if (c.rc != kOk) return c.rc;
+  if (a.max_val & 15) {
+    write_set<0>(a, c, pay, len, scrub, hybrid);
+    release();
+  } else {
+    write_set<3>(a, c, pay, len, scrub, hybrid);
+    drain();
+  }
+  finish_set(a, c);
+  pulse_masks(a, c.wm, c.bl);
+  count_mutation(a, c.idx);
+  return kOk;
+}
+
+// GET for one lane straight into the host payload: one-round-trip probe, acquire, copy
+// (arena -> host, system-scope stores), then the seqlock re-check; on EAGAIN the host ignores
+// the bytes it may have received.
+__device__ int32_t ring_get(const Arena& a, const Key& k, uint8_t* hp, uint32_t cap, uint32_t* out_len) {
+  uint64_t e1 = 0;
+  uint32_t L = 0;
+  const long idx = locate_peek(a, k, &e1, &L);
+  if (idx < 0) return kNoEnt;
+  if ((e1 & 1) || L == kInsertMark) return kAgain;
+  const uint8_t* s = a.slot((size_t)idx);
+  if (ald64_acq(s + kOffEpoch) != e1) return kAgain;  // acquire: this CU's L1 holds no stale value line
+  *out_len = L;
+  if (L > cap) return kMsgSize;
+  if (L) push(hp, (const uint4*)a.value((size_t)idx), (L + 15) >> 4);
+  drain();
+  return (slot_epoch(s) == e1 && slot_hash(s) == k.hash) ? kOk : kAgain;
+}
+
+// one op of one lane; scratch = this entry's device staging row (payload)
+__device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t* pay, uint32_t* out_len,
+                         uint64_t* result) {
+  // ONE round of system-scope loads: record header (32 B), key (64 B) and the first kSpec
+  // payload chunks (speculative: the length is in the header)
+  u32x4s_t h0 = ld16s(c), h1 = ld16s((const uint8_t*)c + 16);
+  u32x4s_t kk[4], pp[kSpec];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) kk[q] = ld16s(c->key + 16 * q);
+#pragma unroll
+  for (uint32_t q = 0; q < kSpec; ++q) pp[q] = ld16s(hp + 16 * q);
+  sys_wait(h0);
+  sys_wait(h1);
+#pragma unroll
+  for (int q = 0; q < 4; ++q) sys_wait(kk[q]);
+#pragma unroll
+  for (uint32_t q = 0; q < kSpec; ++q) sys_wait(pp[q]);
+  const uint32_t op = h0.x, sub = h0.y, len = h0.z, cap = h0.w;
+  const uint64_t arg = ((uint64_t)h1.y << 32) | h1.x;
+  const bool has_in = op == kRingSet || op == kRingAppend || op == kRingEmbedSet || op == kRingWrite;
+  if (has_in) {
+    const uint32_t n16 = (len + 15) >> 4;
+#pragma unroll
+    for (uint32_t q = 0; q < kSpec; ++q)
+      if (q < n16) ((uint4*)pay)[q] = make_uint4(pp[q].x, pp[q].y, pp[q].z, pp[q].w);
+    if (n16 > kSpec) pull((uint4*)pay, hp, kSpec, n16);
+  }
+  const Arena a = from_api(aa);
+  Key k;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    k.w[4 * q] = kk[q].x; k.w[4 * q + 1] = kk[q].y; k.w[4 * q + 2] = kk[q].z; k.w[4 * q + 3] = kk[q].w;
+  }
+  canon_key(k, 64);
+  drain();  // the staged payload is in place before any op reads it
+  long idx = -1;
+  *out_len = 0;
+  *result = 0;
+  switch (op) {
+    case kRingSet:
+      return ring_set(a, k, pay, len);
+    case kRingGet:
+      return ring_get(a, k, hp, cap, out_len);
+    case kRingUnset:
+      return unset_op(a, k, &idx);
+    case kRingAppend: {
+      uint32_t nl = 0;
+      const int32_t rc = append_op(a, k, pay, len, &nl, &idx);
+      if (rc == kOk) {
+        *result = nl;
+        pulse(a, a.slot((size_t)idx));
+        count_mutation(a, idx);
+      }
+      return rc;
+    }
+    case kRingIntop: {
+      uint64_t r = 0;
+      const int32_t rc = integer_op(a, k, (int)sub, arg, &r, &idx);
+      if (rc == kOk) {
+        *result = r;
+        count_mutation(a, idx);
+      }
+      return rc;
+    }
+    case kRingMeta: {
+      bool mut = false;
+      uint64_t o = 0;
+      const int32_t rc = meta_op(a, k, (int)sub, arg, &o, &mut);
+      *result = o;
+      if (mut) count_mutation(a, -1);
+      return rc;
+    }
+    case kRingEmbedSet: {
+      if (a.stride != kSlotEmbedBytes) return kInval;
+      idx = find(a, k);
+      if (idx < 0) return kNoEnt;
+      uint8_t* s = a.slot((size_t)idx);
+      const uint64_t e = slot_epoch(s);
+      if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
+      if (slot_hash(s) != k.hash || !key_eq(s, k)) { aadd64(epoch_ptr(s), 1); return kNoEnt; }
+      uint4* dst = (uint4*)(s + kOffEmbed);
+      for (uint32_t q = 0; q < kEmbedBytes / 16; ++q) st16_wt(dst + q, ((const uint4*)pay)[q]);
+      drain();
+      aadd64(epoch_ptr(s), 1);
+      count_mutation(a, idx);
+      return kOk;
+    }
+    case kRingEmbedGet: {
+      if (a.stride != kSlotEmbedBytes) return kInval;
+      idx = find(a, k);
+      if (idx < 0) return kNoEnt;
+      const uint8_t* s = a.slot((size_t)idx);
+      const uint64_t e1 = ald64_acq(s + kOffEpoch);
+      if (e1 & 1) return kAgain;
+      push(hp, (const uint4*)(s + kOffEmbed), kEmbedBytes / 16);
+      drain();
+      if (slot_epoch(s) != e1) return kAgain;
+      *out_len = kEmbedBytes;
+      return kOk;
+    }
+    case kRingSnapshot: {
+      idx = find(a, k);
+      if (idx < 0) return kNoEnt;
+      const uint8_t* s = a.slot((size_t)idx);
+      for (int q = 0; q < 16; ++q) st64s(hp + 8 * q, ald64(s + 8 * q));
+      *out_len = 128;
+      *result = (uint64_t)idx;
+      return kOk;
+    }
+    case kRingRead: {  // header / arena bytes; 8-B sc1 loads when aligned, else bytewise
+      if (len > cap) return kMsgSize;
+      if (((arg | len) & 7) == 0) {
+        for (uint32_t q = 0; q < len / 8; ++q) st64s(hp + 8 * q, ald64(a.base + arg + 8 * q));
+      } else {
+        for (uint32_t q = 0; q < len; ++q) pay[q] = ald8(a.base + arg + q);
+        drain();
+        push(hp, (const uint4*)pay, (len + 15) >> 4);
+      }
+      *out_len = len;
+      return kOk;
+    }
+    case kRingWrite: {  // sub 0: store the bytes; sub 1 / 2: atomic OR / AND of ONE byte (config flags)
+      if (sub == 1 || sub == 2) {
+        if (len != 1) return kInval;
+        const uintptr_t wa = (uintptr_t)(a.base + arg);
+        uint32_t* w = (uint32_t*)(wa & ~(uintptr_t)3);
+        const uint32_t sh = 8u * (uint32_t)(wa & 3);
+        const uint32_t m = pay[0];
+        if (sub == 1) __hip_atomic_fetch_or(w, m << sh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else __hip_atomic_fetch_and(w, ~((~m & 0xffu) << sh), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return kOk;
+      }
+      if (((arg | len) & 7) == 0) {
+        for (uint32_t q = 0; q < len / 8; ++q) {
+          uint64_t v;
+          __builtin_memcpy(&v, pay + 8 * q, 8);
+          ast64(a.base + arg + 8 * q, v);
+        }
+      } else {
+        for (uint32_t q = 0; q < len; ++q) ast8(a.base + arg + q, pay[q]);
+      }
+      drain();
+      return kOk;
+    }
+    default:
+      return kInval;
+  }
+}
+
+// Workgroup g serves entries g*kGroupEntries + lane (lanes 0..kGroupEntries-1).
+// ctrl (device): [0] u64 wall clock of the last served call (any group), [8] u32 dying,
+// [12] u32 live waves (set to gridDim.x by the launcher).
+__global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmds, RingShared* sh, uint8_t* payload,
+                                                    uint32_t pstride, uint8_t* scratch, uint8_t* ctrl,
+                                                    uint64_t idle_ticks) {
+  const int lane = threadIdx.x, g = blockIdx.x;
+  const bool mine = lane < kGroupEntries;
+  const int e = g * kGroupEntries + (mine ? lane : 0);
+  uint64_t last = wall_clock64();
+  for (;;) {
+    const bool ready = mine && ld32s(&sh->state[e]) == kRingReady;
+    if (__ballot(ready) == 0) {  // wave-uniform
+      if (ld32s(&sh->stop) != 0) break;
+      u32x4c_t cl = ld16c(ctrl);
+      vm_wait(cl);
+      if (cl.z != 0) break;  // another group timed out: leave together
+      const uint64_t now = wall_clock64(), ga = lo64(cl);
+      if (now - (ga > last ? ga : last) > idle_ticks) {
+        if (lane == 0) ast32(ctrl + 8, 1u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+      continue;
+    }
+    last = wall_clock64();
+    if (lane == 0) ast64(ctrl, last);
+    if (ready) {
+      RingCmd* c = cmds + e;
+      uint32_t out_len = 0;
+      uint64_t result = 0;
+      const int32_t st = serve(aa, c, payload + (size_t)e * pstride, scratch + (size_t)e * pstride, &out_len, &result);
+      st64s(&c->status, ((uint64_t)out_len << 32) | (uint32_t)st);  // status + out_len: one 8-B store
+      st64s(&c->result, result);
+      drain();
+      st32s(&sh->state[e], kRingDone);
+    }
+  }
+  drain();
+  if (lane == 0 &&
+      __hip_atomic_fetch_add((uint32_t*)(ctrl + 12), 0xffffffffu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 1u)
+    st32s(&sh->alive, 0u);  // the last wave out
+}
+
+inline int env_int(const char* n, int d) {
+  const char* e = getenv(n);
+  return e ? atoi(e) : d;
+}
+
+}  // namespace
+
+int CmdRing::init(int device, uint32_t pstride) {
+  device_ = device;
+  pstride_ = (pstride + 15) & ~15u;
+  if (pstride_ < kEmbedBytes) pstride_ = kEmbedBytes;
+  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+  if (hipHostMalloc((void**)&shared_, sizeof(RingShared), fl) != hipSuccess) return -1;
+  if (hipHostMalloc((void**)&cmds_, sizeof(RingCmd) * kRingEntries, fl) != hipSuccess) return -1;
+  if (hipHostMalloc((void**)&payload_, (size_t)pstride_ * kRingEntries, fl) != hipSuccess) return -1;
+  if (hipMalloc((void**)&scratch_, (size_t)pstride_ * kRingEntries) != hipSuccess) return -1;
+  if (hipMalloc((void**)&ctrl_, 64) != hipSuccess) return -1;
+  std::memset(shared_, 0, sizeof(RingShared));
+  std::memset(cmds_, 0, sizeof(RingCmd) * kRingEntries);
+  int lo = 0, hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  if (hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi) != hipSuccess) return -1;
+  int khz = 100000;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+  idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
+  return 0;
+}
+
+void CmdRing::launch(const spl_arena_t& a) {
+  std::lock_guard<std::mutex> lk(launch_mu_);
+  if (__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) return;
+  __atomic_store_n(&shared_->alive, 1u, __ATOMIC_RELEASE);
+  __atomic_fetch_add(&shared_->launches, 1u, __ATOMIC_RELAXED);
+  int cur = 0;
+  (void)hipGetDevice(&cur);
+  if (cur != device_) (void)hipSetDevice(device_);
+  // stream order: the previous worker (if still draining) has exited before ctrl is reset
+  const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)kRingGroups};
+  (void)hipMemcpyAsync(ctrl_, init, sizeof init, hipMemcpyHostToDevice, stream_);
+  hipLaunchKernelGGL(k_ring_worker, dim3(kRingGroups), dim3(64), 0, stream_, a, cmds_, shared_, payload_, pstride_,
+                     scratch_, ctrl_, idle_ticks_);
+  if (cur != device_) (void)hipSetDevice(cur);
+}
+
+int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], const void* in,
+                  uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap, RingResult* r) {
+  if (in_len > pstride_) { errno = EMSGSIZE; return -1; }
+  // own an entry: start at a rotating ticket, CAS the host-only busy flag
+  uint32_t e = ticket_.fetch_add(1, std::memory_order_relaxed) % kRingEntries;
+  for (uint32_t spins = 0;; ++spins) {
+    uint32_t z = 0;
+    if (busy_[e].compare_exchange_weak(z, 1u, std::memory_order_acquire)) break;
+    e = (e + 1) % kRingEntries;
+    if ((spins & 63) == 63) _mm_pause();
+  }
+  RingCmd* c = cmds_ + e;
+  c->op = op;
+  c->sub = sub;
+  c->len = in_len;
+  c->cap = out_cap ? (out_cap < pstride_ ? out_cap : pstride_) : pstride_;
+  c->arg = arg;
+  if (key64) std::memcpy(c->key, key64, 64);
+  if (in && in_len) std::memcpy(payload_ + (size_t)e * pstride_, in, in_len);
+  __atomic_store_n(&shared_->state[e], (uint32_t)kRingReady, __ATOMIC_RELEASE);
+  if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);
+  timespec t0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (uint64_t spins = 1;; ++spins) {
+    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == kRingDone) break;
+    _mm_pause();
+    if ((spins & 1023) == 0) {
+      if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);  // worker idled out meanwhile
+      timespec t;
+      clock_gettime(CLOCK_MONOTONIC, &t);
+      if (t.tv_sec - t0.tv_sec > 30) {  // the GPU stopped serving: leak the entry (it stays busy)
+        errno = ETIMEDOUT;
+        return -1;
+      }
+      if (spins > (1u << 16)) sched_yield();
+    }
+  }
+  uint64_t sl;
+  std::memcpy(&sl, &c->status, 8);
+  r->status = (int32_t)(uint32_t)sl;
+  r->out_len = (uint32_t)(sl >> 32);
+  r->result = c->result;
+  if (out && out_cap && r->out_len && r->status >= 0)
+    std::memcpy(out, payload_ + (size_t)e * pstride_, r->out_len < out_cap ? r->out_len : out_cap);
+  __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
+  busy_[e].store(0, std::memory_order_release);
+  return 0;
+}
+
+void CmdRing::stop() {
+  if (!shared_) return;
+  __atomic_store_n(&shared_->stop, 1u, __ATOMIC_RELEASE);
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  __atomic_store_n(&shared_->stop, 0u, __ATOMIC_RELEASE);
+}
+
+CmdRing::~CmdRing() {
+  stop();
+  if (stream_) (void)hipStreamDestroy(stream_);
+  if (ctrl_) (void)hipFree(ctrl_);
+  if (scratch_) (void)hipFree(scratch_);
+  if (payload_) (void)hipHostFree(payload_);
+  if (cmds_) (void)hipHostFree(cmds_);
+  if (shared_) (void)hipHostFree(shared_);
+}
+
+}  // namespace spl

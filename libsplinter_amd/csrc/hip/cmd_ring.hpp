@@ -1,0 +1,113 @@
+// cmd_ring.hpp — per-call API of an HBM store through a host-mapped command ring.
+//
+// The reference's splinter_set/get are in-process calls of a few hundred ns on a CPU mapping
+// (reference splinter.c:365-464).  On the HBM backend every mutation runs on the GPU that owns
+// the arena (owner computes), so a per-call op must reach a device thread.
+// A kernel launch + copies + stream sync per call costs tens of µs; instead each process keeps
+//   * a ring of kEntries command records in pinned, host-coherent memory (one per lane),
+//   * a contiguous doorbell array state[kEntries],
+//   * ONE resident worker kernel (k_ring_worker) of kRingGroups one-wave workgroups on a
+//     high-priority stream; lane i of group g serves entry g*kGroupEntries+i and each group polls
+//     its doorbells in ONE 32-B read, so concurrent host threads' calls run in parallel waves
+//     with little op divergence inside a wave.  (One kernel, not one per group: streams share
+//     GPU_MAX_HW_QUEUES hardware queues, and a group queued behind another group's resident
+//     kernel would wait out that kernel's idle timeout.)
+// The worker exits after SPLINTER_RING_IDLE_US without any call (default 5000 µs; the activity
+// clock is shared by the groups through device memory, and the first group to time out tells
+// the others to exit, so no group outlives the rest) or on stop: a process that stops issuing
+// per-call ops holds no CU and hipDeviceSynchronize returns.  The next call relaunches it (a waiter
+// that sees the worker gone relaunches it itself, so a call can never be stranded between the
+// worker's last poll and its exit).
+//
+// Entry protocol (host thread <-> worker lane), all on the shared doorbell word:
+//   FREE --host: fill record + payload, store-release READY--> READY
+//   READY --lane: system-scope loads of the record, run the op, write results with system-scope
+//            stores, drain, system-scope store DONE--> DONE
+//   DONE --host: read results, store FREE--> FREE
+// Host threads own an entry through a host-only busy flag (CAS), never through the doorbell.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <atomic>
+#include <cstdint>
+#include <mutex>
+
+#include "arena_api.h"
+
+namespace spl {
+
+enum RingOp : uint32_t {
+  kRingSet = 1,
+  kRingGet = 2,
+  kRingUnset = 3,
+  kRingAppend = 4,
+  kRingIntop = 5,      // sub = splinter_integer_op_t, arg = mask
+  kRingMeta = 6,       // sub = SPL_META_* (arena_api.h), arg
+  kRingEmbedSet = 7,   // payload = 768 f32
+  kRingEmbedGet = 8,
+  kRingRead = 9,       // arg = arena byte offset, len bytes (8-B aligned) -> payload
+  kRingWrite = 10,     // payload -> arena byte offset arg (8-B aligned), agent release
+  kRingSnapshot = 11,  // slot core (128 B) of the key's slot + its index in result
+};
+
+enum RingState : uint32_t { kRingFree = 0, kRingReady = 1, kRingDone = 2 };
+
+struct alignas(128) RingCmd {
+  uint32_t op, sub, len, cap;  // cap: payload capacity for outputs
+  uint64_t arg;
+  int32_t status;              // device status (0 / -EAGAIN / -ENOENT / ...; unset: old length)
+  uint32_t out_len;
+  uint64_t result;
+  uint64_t pad[3];
+  char key[64];                // NUL-padded key record
+};
+static_assert(sizeof(RingCmd) == 128, "ring record");
+
+constexpr int kRingGroups = 8;                      // independent one-wave workers
+constexpr int kGroupEntries = 8;                    // entries per worker (lanes 0..7)
+constexpr int kRingEntries = kRingGroups * kGroupEntries;
+
+struct RingShared {
+  uint32_t state[kRingEntries];  // doorbells (one 32-B read per group)
+  uint32_t alive;                // the worker is running or queued (cleared by its last wave)
+  uint32_t stop;                 // ask the worker to exit
+  uint32_t launches;             // host statistic
+  uint32_t pad[13];
+};
+
+struct RingResult {
+  int32_t status = 0;
+  uint32_t out_len = 0;
+  uint64_t result = 0;
+};
+
+class CmdRing {
+ public:
+  // device: ordinal of the arena's GPU; pstride: payload bytes per entry (>= max value, vector)
+  int init(int device, uint32_t pstride);
+  ~CmdRing();
+  bool ready() const { return shared_ != nullptr; }
+  // Blocking call: stage key / input, ring the doorbell, wait for DONE.  `in` may be null;
+  // `out` (may be null) receives min(out_len, out_cap) payload bytes.  Returns 0 when the op ran
+  // (its own status in r.status), -1 on a ring failure (errno set; e.g. ETIMEDOUT).
+  int call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], const void* in, uint32_t in_len,
+           uint64_t arg, void* out, uint32_t out_cap, RingResult* r);
+  void stop();
+  uint32_t launches() const { return shared_ ? shared_->launches : 0; }
+
+ private:
+  void launch(const spl_arena_t& a);
+  RingShared* shared_ = nullptr;  // pinned host (coherent)
+  RingCmd* cmds_ = nullptr;       // pinned host (coherent)
+  uint8_t* payload_ = nullptr;    // pinned host (coherent), kRingEntries x pstride_
+  uint8_t* scratch_ = nullptr;    // device, kRingEntries x pstride_ (+64 key)
+  uint32_t pstride_ = 0;
+  int device_ = 0;
+  uint64_t idle_ticks_ = 0;
+  uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
+  hipStream_t stream_ = nullptr;
+  std::atomic<uint32_t> busy_[kRingEntries] = {};
+  std::atomic<uint32_t> ticket_{0};
+  std::mutex launch_mu_;
+};
+
+}  // namespace spl

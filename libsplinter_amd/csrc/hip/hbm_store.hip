@@ -7,18 +7,21 @@
 //     process on the node can hipIpcOpenMemHandle() the same arena zero-copy;
 //   - a host-resident splinter_header mirror carrying the shard bid table and
 //     the event-bus owner (host atomics; shard election is host logic).
-// The single-op StoreBase API runs each call as a one-element batch (H2D
-// record, kernel, D2H status) on a private stream: microseconds per call.
-// Bulk work goes through the batch launchers (arena_api.h) directly.
+// The per-call StoreBase API goes through the command ring of cmd_ring.hpp (a resident one-wave
+// device worker serving pinned host records: a few µs per call, many host threads batched into
+// one wave round); bulk work goes through the batch launchers (arena_api.h) directly.
 #include <hip/hip_runtime.h>
 #include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fcntl.h>
+#include <algorithm>
+#include <atomic>
 #include <mutex>
 #include <poll.h>
 #include <string>
+#include <thread>
 #include <sys/eventfd.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -27,6 +30,7 @@
 #include <vector>
 
 #include "arena_api.h"
+#include "cmd_ring.hpp"
 #include "splinter_ext.h"
 #include "splinter_store.hpp"
 #include "store_host.hpp"
@@ -48,6 +52,8 @@ struct HbmDescriptor {
   int32_t pad;
   hipIpcMemHandle_t handle;
   alignas(64) splinter_header control;  // host control plane (shard bids, event bus owner)
+  alignas(64) uint32_t notify;          // event-bus doorbell: set by kernels / per-call writers,
+                                        // cleared by the owner's proxy thread
 };
 
 #define HIPCHECK(x)                                                             \
@@ -88,19 +94,19 @@ class HbmStore final : public StoreBase {
     a.max_val = geo_.max_val;
     a.stride = geo_.stride;
     a.flags = event_fd_ >= 0 ? 1u : 0u;
+    a.notify = (uint64_t)(uintptr_t)d_notify_;
     return a;
   }
   hipStream_t stream() const { return stream_; }
+  uint32_t ring_launches() const { return ring_.launches(); }
 
   int set_mop(unsigned mode) override {
-    uint8_t f = config_get();
     switch (mode) {
-      case 0: f &= (uint8_t)~(SPL_SYS_AUTO_SCRUB | SPL_SYS_HYBRID_SCRUB); break;
-      case 1: f |= SPL_SYS_AUTO_SCRUB | SPL_SYS_HYBRID_SCRUB; break;
-      case 2: f |= SPL_SYS_AUTO_SCRUB; break;
+      case 0: return hdr_bits(offsetof(splinter_header, core_flags), 2, (uint8_t)~(SPL_SYS_AUTO_SCRUB | SPL_SYS_HYBRID_SCRUB));
+      case 1: return hdr_bits(offsetof(splinter_header, core_flags), 1, SPL_SYS_AUTO_SCRUB | SPL_SYS_HYBRID_SCRUB);
+      case 2: return hdr_bits(offsetof(splinter_header, core_flags), 1, SPL_SYS_AUTO_SCRUB);
       default: errno = EOPNOTSUPP; return -1;
     }
-    return put_field(offsetof(splinter_header, core_flags), &f, 1);
   }
   int get_mop() override {
     uint8_t f = config_get();
@@ -127,56 +133,40 @@ class HbmStore final : public StoreBase {
     get_field(offsetof(splinter_header, core_flags), &f, 1);
     return f;
   }
-  void config_or(uint8_t m) override { uint8_t f = config_get() | m; put_field(offsetof(splinter_header, core_flags), &f, 1); }
-  void config_and(uint8_t m) override { uint8_t f = config_get() & m; put_field(offsetof(splinter_header, core_flags), &f, 1); }
+  void config_or(uint8_t m) override { hdr_bits(offsetof(splinter_header, core_flags), 1, m); }
+  void config_and(uint8_t m) override { hdr_bits(offsetof(splinter_header, core_flags), 2, m); }
 
+  // ------------------------------------------------ per-call ops (command ring) --
   int set(const char* key, const void* val, size_t len) override {
     if (!key) return -2;
     if (len == 0 || len > geo_.max_val) { errno = len ? EMSGSIZE : EINVAL; return -1; }
     if (!val) return -2;
-    std::lock_guard<std::mutex> lk(mu_);
-    stage_key(key);
-    std::memset(h_val_, 0, (len + 15) & ~(size_t)15);
-    std::memcpy(h_val_, val, len);
-    uint32_t l = (uint32_t)len;
-    std::memcpy(h_u32_, &l, 4);
-    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
-    (void)hipMemcpyAsync(d_val_, h_val_, (len + 15) & ~(size_t)15, hipMemcpyHostToDevice, stream_);
-    (void)hipMemcpyAsync(d_u32_, h_u32_, 4, hipMemcpyHostToDevice, stream_);
-    spl_arena_set(arena(), d_key_, 64, (const uint8_t*)d_val_, (int)vstride_, (const uint32_t*)d_u32_, 1,
-                  (int32_t*)d_status_, 0, nullptr, stream_);
-    int32_t st = finish_status();
-    if (st == 0) notify_host();
-    return st_ret(st);
+    RingResult r;
+    if (ring(kRingSet, 0, key, val, (uint32_t)len, 0, nullptr, 0, &r) != 0) return -1;
+    if (r.status == 0) notify_host();
+    return st_ret(r.status);
   }
   int unset(const char* key) override {
     if (!key) return -2;
-    std::lock_guard<std::mutex> lk(mu_);
-    stage_key(key);
-    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
-    spl_arena_unset(arena(), d_key_, 64, 1, (int32_t*)d_status_, 0, stream_);
-    int32_t st = finish_status();
-    if (st >= 0) return st;
-    errno = neg_to_errno(st);
+    RingResult r;
+    if (ring(kRingUnset, 0, key, nullptr, 0, 0, nullptr, 0, &r) != 0) return -1;
+    if (r.status >= 0) return r.status;
+    errno = neg_to_errno(r.status);
     return -1;
   }
   int get(const char* key, void* buf, size_t buf_sz, size_t* out_sz) override {
     if (!key) return -2;
-    std::lock_guard<std::mutex> lk(mu_);
-    stage_key(key);
-    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
-    spl_arena_get(arena(), d_key_, 64, (uint8_t*)d_val_, (int)vstride_, (uint32_t*)d_u32_, 1, (int32_t*)d_status_, 0,
-                  nullptr, stream_);
-    (void)hipMemcpyAsync(h_u32_, d_u32_, 4, hipMemcpyDeviceToHost, stream_);
-    (void)hipMemcpyAsync(h_val_, d_val_, vstride_, hipMemcpyDeviceToHost, stream_);
-    int32_t st = finish_status();
-    if (st != 0) { errno = neg_to_errno(st); return -1; }
-    uint32_t len;
-    std::memcpy(&len, h_u32_, 4);
-    if (out_sz) *out_sz = len;
-    if (buf) {
-      if (buf_sz < len) { errno = EMSGSIZE; return -1; }
-      std::memcpy(buf, h_val_, len);
+    thread_local std::vector<uint8_t> tmp;
+    RingResult r;
+    const bool direct = buf && buf_sz >= geo_.max_val;  // the whole value fits: copy straight out
+    if (!direct) tmp.resize(geo_.max_val + 16);
+    if (ring(kRingGet, 0, key, nullptr, 0, 0, direct ? buf : tmp.data(), (uint32_t)(direct ? buf_sz : tmp.size()), &r) != 0)
+      return -1;
+    if (r.status != 0) { errno = neg_to_errno(r.status); return -1; }
+    if (out_sz) *out_sz = r.out_len;
+    if (buf && !direct) {
+      if (buf_sz < r.out_len) { errno = EMSGSIZE; return -1; }
+      std::memcpy(buf, tmp.data(), r.out_len);
     }
     return 0;
   }
@@ -184,7 +174,7 @@ class HbmStore final : public StoreBase {
     if (!out || !cnt) return -2;
     std::vector<uint32_t> idx;
     std::vector<uint64_t> ep;
-    scan(SPL_SCAN_LIST, 0, idx, ep);
+    scan(SPL_SCAN_LIST, 0, idx, ep, max);
     fetch_cores(idx);
     size_t c = 0;
     for (size_t i = 0; i < idx.size() && c < max; ++i) out[c++] = (char*)(list_cache_.data() + i * 128 + kOffKey);
@@ -209,11 +199,10 @@ class HbmStore final : public StoreBase {
   }
   int slot_snapshot(const char* key, splinter_slot_snapshot_t* o) override {
     if (!key || !o) return -2;
-    long i = find_idx(key);
-    if (i < 0) return -1;
-    std::vector<uint32_t> idx{(uint32_t)i};
-    fetch_cores(idx);
-    const uint8_t* c = list_cache_.data();
+    uint8_t c[128];
+    RingResult r;
+    if (ring(kRingSnapshot, 0, key, nullptr, 0, 0, c, sizeof c, &r) != 0) return -1;
+    if (r.status != 0) { errno = neg_to_errno(r.status); return -1; }
     std::memcpy(&o->hash, c + kOffHash, 8);
     std::memcpy(&o->epoch, c + kOffEpoch, 8);
     std::memcpy(&o->val_off, c + kOffValOff, 4);
@@ -231,28 +220,38 @@ class HbmStore final : public StoreBase {
     return 0;
   }
   int append(const char* key, const void* data, size_t len, size_t* new_len) override {
-    // read-modify-write through the seqlocked set path (owner computes)
+    // atomic on the device: the slot is held (odd epoch) across the tail copy (append_op)
     if (!key || !data || len == 0) return -2;
-    std::vector<uint8_t> cur(geo_.max_val);
-    size_t n = 0;
-    if (get(key, cur.data(), cur.size(), &n) != 0) return -1;
-    if (n + len > geo_.max_val) { errno = EMSGSIZE; return -1; }
-    std::memcpy(cur.data() + n, data, len);
-    if (set(key, cur.data(), n + len) != 0) return -1;
-    if (new_len) *new_len = n + len;
+    if (len > geo_.max_val) { errno = EMSGSIZE; return -1; }
+    RingResult r;
+    if (ring(kRingAppend, 0, key, data, (uint32_t)len, 0, nullptr, 0, &r) != 0) return -1;
+    if (r.status != 0) { errno = neg_to_errno(r.status); return -1; }
+    if (new_len) *new_len = (size_t)r.result;
+    notify_host();
     return 0;
   }
   const void* raw_ptr(const char* key, size_t* out_sz, uint64_t* out_epoch) override {
-    // HBM values are not host mapped: return a host snapshot (thread-local).
+    // HBM is not host addressable: a seqlock-consistent host snapshot (thread-local, valid until
+    // this thread's next raw_ptr call) with the epoch it was read at (docs/DIVERGENCES.md)
     thread_local std::vector<uint8_t> snap;
     snap.resize(geo_.max_val + 1);
-    size_t n = 0;
-    uint64_t e = epoch_of(key);
-    if (get(key, snap.data(), geo_.max_val, &n) != 0) return nullptr;
-    snap[n] = 0;
-    if (out_sz) *out_sz = n;
-    if (out_epoch) *out_epoch = e;
-    return snap.data();
+    for (int t = 0; t < 64; ++t) {
+      const uint64_t e = epoch_of(key);
+      if (e == 0) return nullptr;
+      size_t n = 0;
+      if (e & 1) { usleep(10); continue; }
+      if (get(key, snap.data(), geo_.max_val, &n) != 0) {
+        if (errno == EAGAIN) continue;
+        return nullptr;
+      }
+      if (epoch_of(key) != e) continue;
+      snap[n] = 0;
+      if (out_sz) *out_sz = n;
+      if (out_epoch) *out_epoch = e;
+      return snap.data();
+    }
+    errno = EAGAIN;
+    return nullptr;
   }
   uint64_t epoch_of(const char* key) override {
     uint64_t out = 0;
@@ -264,44 +263,21 @@ class HbmStore final : public StoreBase {
   int set_embedding(const char* key, const float* vec) override {
     if (!key || !vec) return -2;
     if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
-    std::lock_guard<std::mutex> lk(mu_);
-    stage_key(key);
-    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
-    (void)hipMemcpyAsync(d_vec_, vec, kEmbedBytes, hipMemcpyHostToDevice, stream_);
-    spl_arena_embed_set(arena(), d_key_, 64, (const float*)d_vec_, 1, (int32_t*)d_status_, stream_);
-    int32_t st = finish_status();
-    if (st == 0) notify_host();
-    return st_ret(st);
+    RingResult r;
+    if (ring(kRingEmbedSet, 0, key, vec, (uint32_t)kEmbedBytes, 0, nullptr, 0, &r) != 0) return -1;
+    if (r.status == 0) notify_host();
+    return st_ret(r.status);
   }
   int get_embedding(const char* key, float* out) override {
     if (!key || !out) return -2;
     if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
-    std::lock_guard<std::mutex> lk(mu_);
-    stage_key(key);
-    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
-    spl_arena_embed_get(arena(), d_key_, 64, (float*)d_vec_, 1, (int32_t*)d_status_, stream_);
-    (void)hipMemcpyAsync(out, d_vec_, kEmbedBytes, hipMemcpyDeviceToHost, stream_);
-    return st_ret(finish_status());
+    RingResult r;
+    if (ring(kRingEmbedGet, 0, key, nullptr, 0, 0, out, (uint32_t)kEmbedBytes, &r) != 0) return -1;
+    return st_ret(r.status);
   }
 
   int set_named_type(const char* key, uint16_t mask) override {
-    if (!key) return -2;
-    if (mask & SPL_SLOT_TYPE_BIGUINT) {  // promotion: parse on the host, write back as u64
-      std::vector<uint8_t> v(geo_.max_val + 1, 0);
-      size_t n = 0;
-      if (get(key, v.data(), geo_.max_val, &n) != 0) return -1;
-      if (n < 8) {
-        uint64_t x = 0;
-        if (n > 0 && v[0] >= '0' && v[0] <= '9') {
-          char tmp[16] = {0};
-          std::memcpy(tmp, v.data(), n < 15 ? n : 15);
-          x = strtoull(tmp, nullptr, 0);
-        } else {
-          std::memcpy(&x, v.data(), n);
-        }
-        if (set(key, &x, 8) != 0) return -1;
-      }
-    }
+    // BIGUINT promotion (ASCII digits -> u64) runs on the device under the slot seqlock
     return meta_ret(meta(key, SPL_META_SET_TYPE, mask, nullptr));
   }
   int set_slot_time(const char* key, unsigned short mode, uint64_t epoch, size_t offset) override {
@@ -312,18 +288,10 @@ class HbmStore final : public StoreBase {
     if (!key) return -2;
     uint64_t m = 0;
     if (mask) std::memcpy(&m, mask, 8);
-    std::lock_guard<std::mutex> lk(mu_);
-    stage_key(key);
-    int o = (int)op;
-    std::memcpy(h_val_, &o, 4);
-    std::memcpy(h_val_ + 16, &m, 8);
-    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
-    (void)hipMemcpyAsync(d_val_, h_val_, 32, hipMemcpyHostToDevice, stream_);
-    spl_arena_intop(arena(), d_key_, 64, (const int*)d_val_, (const uint64_t*)((uint8_t*)d_val_ + 16), 1,
-                    (int32_t*)d_status_, nullptr, 0, stream_);
-    int32_t st = finish_status();
-    if (st == 0) notify_host();
-    return st_ret(st);
+    RingResult r;
+    if (ring(kRingIntop, (uint32_t)op, key, nullptr, 0, m, nullptr, 0, &r) != 0) return -1;
+    if (r.status == 0) notify_host();
+    return st_ret(r.status);
   }
 
   int bump(const char* key) override { return meta_ret(meta(key, SPL_META_BUMP, 0, nullptr)); }
@@ -342,7 +310,7 @@ class HbmStore final : public StoreBase {
   int watch_label_register(uint64_t mask, uint8_t g) override {
     if (g >= SPLINTER_MAX_GROUPS) return -2;
     uint8_t w[64];
-    get_field(offsetof(splinter_header, bloom_watches), w, 64);
+    if (get_field(offsetof(splinter_header, bloom_watches), w, 64) != 0) return -1;
     for (uint64_t m = mask; m; m &= m - 1) w[__builtin_ctzll(m)] = g;
     return put_field(offsetof(splinter_header, bloom_watches), w, 64);
   }
@@ -358,18 +326,29 @@ class HbmStore final : public StoreBase {
     if (!cb) return;
     std::vector<uint32_t> idx;
     std::vector<uint64_t> ep;
-    scan(SPL_SCAN_LABELS, mask, idx, ep);
+    scan(SPL_SCAN_LABELS, mask, idx, ep, SIZE_MAX);
     fetch_cores(idx);
     for (size_t i = 0; i < idx.size(); ++i) cb((const char*)(list_cache_.data() + i * 128 + kOffKey), ep[i], ud);
   }
 
+  // ------------------------------------------------------------- event bus --
+  // The owner's eventfd is written by a host proxy thread whenever the notify word of the
+  // shared descriptor is set: by this process's per-call mutations, by the batch kernels of ANY
+  // process attached to the arena (system-scope store from the kernel epilogue, arena_dev.hpp
+  // notify_host), and by per-call mutations of other processes.  Device kernels also maintain
+  // the dirty mask once the device header records an owner (mirrored here).
   int event_bus_init() override {
     int fd = eventfd(0, EFD_CLOEXEC);
     if (fd < 0) return -1;
+    stop_proxy();
     if (event_fd_ >= 0) close(event_fd_);
     event_fd_ = fd;
     __atomic_store_n(&desc_->control.event_bus.owner_fd, fd, __ATOMIC_RELEASE);
     __atomic_store_n(&desc_->control.event_bus.owner_pid, (int32_t)getpid(), __ATOMIC_RELEASE);
+    const int32_t own[2] = {fd, (int32_t)getpid()};
+    put_field(offsetof(splinter_header, event_bus) + offsetof(splinter_event_bus, owner_fd), own, 8);
+    proxy_stop_.store(false);
+    proxy_ = std::thread([this] { proxy_loop(); });
     return 0;
   }
   int event_bus_open() override {
@@ -424,104 +403,133 @@ class HbmStore final : public StoreBase {
  private:
   HbmStore() = default;
   int setup_buffers();
-  void stage_key(const char* key) {
-    KeyRef k(key);
-    std::memcpy(h_key_, k.buf, 64);
-  }
-  int32_t finish_status() {
-    (void)hipMemcpyAsync(h_status_, d_status_, 4, hipMemcpyDeviceToHost, stream_);
-    (void)hipStreamSynchronize(stream_);
-    int32_t st;
-    std::memcpy(&st, h_status_, 4);
-    return st;
+  int ring(uint32_t op, uint32_t sub, const char* key, const void* in, uint32_t in_len, uint64_t arg, void* out,
+           uint32_t out_cap, RingResult* r) {
+    char k[64];
+    if (key) {
+      KeyRef kr(key);
+      std::memcpy(k, kr.buf, 64);
+    } else {
+      std::memset(k, 0, 64);
+    }
+    return ring_.call(arena(), op, sub, k, in, in_len, arg, out, out_cap, r);
   }
   static int st_ret(int32_t st) {
     if (st == 0) return 0;
     errno = neg_to_errno(st);
-    return st == -2 ? -1 : -1;
+    return -1;
   }
   static int meta_ret(int32_t st) { return st_ret(st); }
   int32_t meta(const char* key, int op, uint64_t arg, uint64_t* out) {
     if (!key) return -22;
-    std::lock_guard<std::mutex> lk(mu_);
-    stage_key(key);
-    std::memcpy(h_val_, &arg, 8);
-    (void)hipMemcpyAsync(d_key_, h_key_, 64, hipMemcpyHostToDevice, stream_);
-    (void)hipMemcpyAsync(d_val_, h_val_, 8, hipMemcpyHostToDevice, stream_);
-    spl_arena_meta(arena(), d_key_, 64, op, (const uint64_t*)d_val_, 1, (int32_t*)d_status_,
-                   (uint64_t*)((uint8_t*)d_val_ + 64), stream_);
-    if (out) (void)hipMemcpyAsync(h_val_ + 64, (uint8_t*)d_val_ + 64, 8, hipMemcpyDeviceToHost, stream_);
-    int32_t st = finish_status();
-    if (out) std::memcpy(out, h_val_ + 64, 8);
+    RingResult r;
+    if (ring(kRingMeta, (uint32_t)op, key, nullptr, 0, arg, nullptr, 0, &r) != 0) return -5;
+    if (out) *out = r.result;
     const bool mut = op == SPL_META_SET_LABEL || op == SPL_META_UNSET_LABEL || op == SPL_META_RETRAIN ||
                      op == SPL_META_SET_TYPE;
-    if (st == 0 && mut) notify_host();
-    return st;
+    if (r.status == 0 && mut) notify_host();
+    return r.status;
   }
-  long find_idx(const char* key) {
-    uint64_t out = 0;
-    return meta(key, SPL_META_FIND, 0, &out) == 0 ? (long)out : -1;
+  // header bytes through the ring: READ / WRITE (sub 0 store, 1 atomic OR, 2 atomic AND)
+  int get_field(size_t off, void* dst, size_t n) {
+    RingResult r;
+    if (ring(kRingRead, 0, nullptr, nullptr, (uint32_t)n, off, dst, (uint32_t)n, &r) != 0) return -1;
+    return r.status == 0 ? 0 : -1;
   }
-  void scan(int mode, uint64_t mask, std::vector<uint32_t>& idx, std::vector<uint64_t>& ep) {
+  int put_field(size_t off, const void* src, size_t n, uint32_t how = 0) {
+    RingResult r;
+    if (ring(kRingWrite, how, nullptr, src, (uint32_t)n, off, nullptr, 0, &r) != 0) return -1;
+    return r.status == 0 ? 0 : -1;
+  }
+  int hdr_bits(size_t off, uint32_t how, uint8_t m) { return put_field(off, &m, 1, how); }
+
+  // Slot-range scans into persistent, grow-only scratch (kScanChunk slots per launch), results
+  // appended on the host; stops once `limit` matches are collected.
+  static constexpr uint32_t kScanChunk = 1u << 22;
+  void scan(int mode, uint64_t mask, std::vector<uint32_t>& idx, std::vector<uint64_t>& ep, size_t limit) {
     std::lock_guard<std::mutex> lk(mu_);
-    uint32_t* d_cnt;
-    uint32_t* d_idx;
-    uint64_t* d_ep;
-    const uint32_t cap = geo_.slots;
-    (void)hipMallocAsync((void**)&d_cnt, 4, stream_);
-    (void)hipMallocAsync((void**)&d_idx, (size_t)cap * 4, stream_);
-    (void)hipMallocAsync((void**)&d_ep, (size_t)cap * 8, stream_);
-    (void)hipMemsetAsync(d_cnt, 0, 4, stream_);
-    spl_arena_scan(arena(), mode, mask, d_idx, d_ep, cap, d_cnt, stream_);
-    uint32_t n = 0;
-    (void)hipMemcpyAsync(&n, d_cnt, 4, hipMemcpyDeviceToHost, stream_);
-    (void)hipStreamSynchronize(stream_);
-    if (n > cap) n = cap;
-    idx.resize(n);
-    ep.resize(n);
-    if (n) {
-      (void)hipMemcpyAsync(idx.data(), d_idx, (size_t)n * 4, hipMemcpyDeviceToHost, stream_);
-      (void)hipMemcpyAsync(ep.data(), d_ep, (size_t)n * 8, hipMemcpyDeviceToHost, stream_);
+    idx.clear();
+    ep.clear();
+    if (ensure_scan_scratch() != 0) return;
+    std::vector<uint32_t> hi;
+    std::vector<uint64_t> he;
+    for (uint64_t b = 0; b < geo_.slots && idx.size() < limit; b += kScanChunk) {
+      const uint32_t e = (uint32_t)std::min<uint64_t>(geo_.slots, b + kScanChunk);
+      (void)hipMemsetAsync(d_scan_cnt_, 0, 4, stream_);
+      spl_arena_scan_range(arena(), mode, mask, (uint32_t)b, e, d_scan_idx_, d_scan_ep_, kScanChunk, d_scan_cnt_,
+                           stream_);
+      uint32_t n = 0;
+      (void)hipMemcpyAsync(h_u32_, d_scan_cnt_, 4, hipMemcpyDeviceToHost, stream_);
+      (void)hipStreamSynchronize(stream_);
+      std::memcpy(&n, h_u32_, 4);
+      if (n > kScanChunk) n = kScanChunk;
+      if (!n) continue;
+      hi.resize(n);
+      he.resize(n);
+      (void)hipMemcpyAsync(hi.data(), d_scan_idx_, (size_t)n * 4, hipMemcpyDeviceToHost, stream_);
+      (void)hipMemcpyAsync(he.data(), d_scan_ep_, (size_t)n * 8, hipMemcpyDeviceToHost, stream_);
+      (void)hipStreamSynchronize(stream_);
+      // the scan compacts in arrival order: restore slot order inside the chunk
+      std::vector<uint32_t> ord(n);
+      for (uint32_t i = 0; i < n; ++i) ord[i] = i;
+      std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return hi[x] < hi[y]; });
+      for (uint32_t i = 0; i < n && idx.size() < limit; ++i) {
+        idx.push_back(hi[ord[i]]);
+        ep.push_back(he[ord[i]]);
+      }
     }
-    (void)hipFreeAsync(d_cnt, stream_);
-    (void)hipFreeAsync(d_idx, stream_);
-    (void)hipFreeAsync(d_ep, stream_);
-    (void)hipStreamSynchronize(stream_);
+  }
+  int ensure_scan_scratch() {
+    if (d_scan_idx_) return 0;
+    if (hipMalloc((void**)&d_scan_idx_, (size_t)kScanChunk * 4) != hipSuccess) return -1;
+    if (hipMalloc((void**)&d_scan_ep_, (size_t)kScanChunk * 8) != hipSuccess) return -1;
+    if (hipMalloc((void**)&d_scan_cnt_, 64) != hipSuccess) return -1;
+    return 0;
   }
   void fetch_cores(const std::vector<uint32_t>& idx) {
     std::lock_guard<std::mutex> lk(mu_);
     list_cache_.assign(idx.size() * 128, 0);
-    if (idx.empty()) return;
-    uint32_t* d_idx;
-    uint8_t* d_out;
-    (void)hipMallocAsync((void**)&d_idx, idx.size() * 4, stream_);
-    (void)hipMallocAsync((void**)&d_out, idx.size() * 128, stream_);
-    (void)hipMemcpyAsync(d_idx, idx.data(), idx.size() * 4, hipMemcpyHostToDevice, stream_);
-    spl_arena_gather_slots(arena(), d_idx, (long)idx.size(), d_out, stream_);
-    (void)hipMemcpyAsync(list_cache_.data(), d_out, idx.size() * 128, hipMemcpyDeviceToHost, stream_);
-    (void)hipFreeAsync(d_idx, stream_);
-    (void)hipFreeAsync(d_out, stream_);
-    (void)hipStreamSynchronize(stream_);
+    if (idx.empty() || ensure_scan_scratch() != 0) return;
+    // reuse the scan scratch: kScanChunk indices (4 B) + kScanChunk/16 cores (128 B) per round
+    const size_t per = kScanChunk / 16;
+    uint8_t* d_out = (uint8_t*)d_scan_ep_;
+    for (size_t b = 0; b < idx.size(); b += per) {
+      const size_t n = std::min(per, idx.size() - b);
+      (void)hipMemcpyAsync(d_scan_idx_, idx.data() + b, n * 4, hipMemcpyHostToDevice, stream_);
+      spl_arena_gather_slots(arena(), d_scan_idx_, (long)n, d_out, stream_);
+      (void)hipMemcpyAsync(list_cache_.data() + b * 128, d_out, n * 128, hipMemcpyDeviceToHost, stream_);
+      (void)hipStreamSynchronize(stream_);
+    }
   }
-  int get_field(size_t off, void* dst, size_t n) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (hipMemcpyAsync(h_val_, (uint8_t*)dbase_ + off, n, hipMemcpyDeviceToHost, stream_) != hipSuccess) return -1;
-    (void)hipStreamSynchronize(stream_);
-    std::memcpy(dst, h_val_, n);
-    return 0;
-  }
-  int put_field(size_t off, const void* src, size_t n) {
-    std::lock_guard<std::mutex> lk(mu_);
-    std::memcpy(h_val_, src, n);
-    if (hipMemcpyAsync((uint8_t*)dbase_ + off, h_val_, n, hipMemcpyHostToDevice, stream_) != hipSuccess) return -1;
-    (void)hipStreamSynchronize(stream_);
-    return 0;
-  }
+  // Per-call mutation -> event bus: write the eventfd directly when this process owns it, else
+  // raise the shared notify word for the owner's proxy.
   void notify_host() {
-    if (event_fd_ < 0) return;
-    uint64_t one = 1;
-    ssize_t w = write(event_fd_, &one, 8);
-    (void)w;
+    if (event_fd_ >= 0) {
+      uint64_t one = 1;
+      ssize_t w = write(event_fd_, &one, 8);
+      (void)w;
+    } else if (__atomic_load_n(&desc_->control.event_bus.owner_pid, __ATOMIC_ACQUIRE) > 0) {
+      __atomic_store_n(&desc_->notify, 1u, __ATOMIC_RELEASE);
+    }
+  }
+  void proxy_loop() {
+    const int us = getenv("SPLINTER_BUS_POLL_US") ? atoi(getenv("SPLINTER_BUS_POLL_US")) : 100;
+    while (!proxy_stop_.load(std::memory_order_acquire)) {
+      if (__atomic_load_n(&desc_->notify, __ATOMIC_ACQUIRE)) {
+        __atomic_store_n(&desc_->notify, 0u, __ATOMIC_RELEASE);
+        uint64_t one = 1;
+        ssize_t w = write(event_fd_, &one, 8);
+        (void)w;
+        continue;
+      }
+      usleep(us > 0 ? us : 100);
+    }
+  }
+  void stop_proxy() {
+    if (proxy_.joinable()) {
+      proxy_stop_.store(true, std::memory_order_release);
+      proxy_.join();
+    }
   }
 
   std::string name_;
@@ -531,20 +539,19 @@ class HbmStore final : public StoreBase {
   void* raw_ = nullptr;    // hipMalloc / IPC base
   void* dbase_ = nullptr;  // raw_ + kAlignOffset
   HbmDescriptor* desc_ = nullptr;
+  bool desc_registered_ = false;
+  uint32_t* d_notify_ = nullptr;  // device address of desc_->notify (hipHostRegister)
   hipStream_t stream_ = nullptr;
   std::mutex mu_;
   int event_fd_ = -1;
+  std::thread proxy_;
+  std::atomic<bool> proxy_stop_{false};
   size_t vstride_ = 0;
-  // staging
-  char* h_key_ = nullptr;
-  uint8_t* h_val_ = nullptr;
+  CmdRing ring_;
   uint8_t* h_u32_ = nullptr;
-  uint8_t* h_status_ = nullptr;
-  char* d_key_ = nullptr;
-  void* d_val_ = nullptr;
-  void* d_u32_ = nullptr;
-  void* d_status_ = nullptr;
-  void* d_vec_ = nullptr;
+  uint32_t* d_scan_idx_ = nullptr;
+  uint64_t* d_scan_ep_ = nullptr;
+  uint32_t* d_scan_cnt_ = nullptr;
   std::vector<uint8_t> list_cache_;
 
   friend StoreBase* hbm_factory_impl(const char*, size_t, size_t, unsigned, int, int*);
@@ -554,15 +561,17 @@ int HbmStore::setup_buffers() {
   HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   vstride_ = ((size_t)geo_.max_val + 15) & ~(size_t)15;
   if (vstride_ < 128) vstride_ = 128;
-  HIPCHECK(hipHostMalloc((void**)&h_key_, 64));
-  HIPCHECK(hipHostMalloc((void**)&h_val_, vstride_ + 4096));
   HIPCHECK(hipHostMalloc((void**)&h_u32_, 64));
-  HIPCHECK(hipHostMalloc((void**)&h_status_, 64));
-  HIPCHECK(hipMalloc((void**)&d_key_, 64));
-  HIPCHECK(hipMalloc(&d_val_, vstride_ + 4096));
-  HIPCHECK(hipMalloc(&d_u32_, 64));
-  HIPCHECK(hipMalloc(&d_status_, 64));
-  HIPCHECK(hipMalloc(&d_vec_, kEmbedBytes));
+  if (ring_.init(device_, (uint32_t)std::max<size_t>(vstride_, kEmbedBytes)) != 0) return -1;
+  // the shared descriptor page(s) become device-visible: kernels of every attached process
+  // store the event-bus notify word there
+  const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+  const size_t span = (sizeof(HbmDescriptor) + pg - 1) / pg * pg;
+  if (hipHostRegister(desc_, span, hipHostRegisterMapped) == hipSuccess) {
+    desc_registered_ = true;
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, &desc_->notify, 0) == hipSuccess) d_notify_ = (uint32_t*)dp;
+  }
   return 0;
 }
 
@@ -571,8 +580,10 @@ static HbmDescriptor* map_descriptor(const std::string& name, bool create, int* 
   int fd = create ? shm_open(dn.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0666)
                   : shm_open(dn.c_str(), O_RDWR | O_CLOEXEC, 0666);
   if (fd < 0) { *err = errno; return nullptr; }
-  if (create && ftruncate(fd, sizeof(HbmDescriptor)) != 0) { *err = errno; close(fd); return nullptr; }
-  void* p = mmap(nullptr, sizeof(HbmDescriptor), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+  const size_t span = (sizeof(HbmDescriptor) + pg - 1) / pg * pg;
+  if (create && ftruncate(fd, (off_t)span) != 0) { *err = errno; close(fd); return nullptr; }
+  void* p = mmap(nullptr, span, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (p == MAP_FAILED) { *err = errno; return nullptr; }
   return (HbmDescriptor*)p;
@@ -622,7 +633,7 @@ HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool 
   d->base_offset = kAlignOffset;
   d->owner_pid = (int32_t)getpid();
   if (hipIpcGetMemHandle(&d->handle, s->raw_) != hipSuccess) std::memset(&d->handle, 0, sizeof d->handle);
-  d->version = 1;
+  d->version = 2;
   __atomic_store_n(&d->magic, kDescMagic, __ATOMIC_RELEASE);
   return s;
 }
@@ -632,7 +643,8 @@ HbmStore* HbmStore::open(const char* name, int* err) {
   HbmDescriptor* d = map_descriptor(name, false, err);
   if (!d) return nullptr;
   if (__atomic_load_n(&d->magic, __ATOMIC_ACQUIRE) != kDescMagic) {
-    munmap(d, sizeof(HbmDescriptor));
+    const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+    munmap(d, (sizeof(HbmDescriptor) + pg - 1) / pg * pg);
     *err = EINVAL;
     return nullptr;
   }
@@ -656,25 +668,35 @@ HbmStore* HbmStore::open(const char* name, int* err) {
 }
 
 HbmStore::~HbmStore() {
+  stop_proxy();
+  ring_.stop();  // the worker reads the arena: drain it before the arena goes away
   if (stream_) (void)hipStreamSynchronize(stream_);
-  if (event_fd_ >= 0) close(event_fd_);
-  if (h_key_) (void)hipHostFree(h_key_);
-  if (h_val_) (void)hipHostFree(h_val_);
+  if (event_fd_ >= 0) {
+    if (desc_ && __atomic_load_n(&desc_->control.event_bus.owner_pid, __ATOMIC_ACQUIRE) == (int32_t)getpid()) {
+      __atomic_store_n(&desc_->control.event_bus.owner_fd, -1, __ATOMIC_RELEASE);
+      __atomic_store_n(&desc_->control.event_bus.owner_pid, 0, __ATOMIC_RELEASE);
+      if (raw_) {
+        const int32_t own[2] = {-1, 0};
+        put_field(offsetof(splinter_header, event_bus) + offsetof(splinter_event_bus, owner_fd), own, 8);
+      }
+    }
+    close(event_fd_);
+  }
+  ring_.stop();
   if (h_u32_) (void)hipHostFree(h_u32_);
-  if (h_status_) (void)hipHostFree(h_status_);
-  if (d_key_) (void)hipFree(d_key_);
-  if (d_val_) (void)hipFree(d_val_);
-  if (d_u32_) (void)hipFree(d_u32_);
-  if (d_status_) (void)hipFree(d_status_);
-  if (d_vec_) (void)hipFree(d_vec_);
+  if (d_scan_idx_) (void)hipFree(d_scan_idx_);
+  if (d_scan_ep_) (void)hipFree(d_scan_ep_);
+  if (d_scan_cnt_) (void)hipFree(d_scan_cnt_);
   if (raw_) {
     if (owner_) (void)hipFree(raw_);
     else (void)hipIpcCloseMemHandle(raw_);
   }
   if (stream_) (void)hipStreamDestroy(stream_);
   if (desc_) {
+    if (desc_registered_) (void)hipHostUnregister(desc_);
     if (owner_) __atomic_store_n(&desc_->magic, 0u, __ATOMIC_RELEASE);
-    munmap(desc_, sizeof(HbmDescriptor));
+    const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+    munmap(desc_, (sizeof(HbmDescriptor) + pg - 1) / pg * pg);
     if (owner_) shm_unlink((name_ + ".hbm").c_str());
   }
 }

@@ -552,7 +552,7 @@ __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, co
   // semantics (/root/reference/splinter.c:567-588): CAS even->odd, copy, +1.
   using namespace spl;
   using namespace spl::dev;
-  Arena a{(uint8_t*)aa.base, aa.slots, aa.max_val, aa.stride, aa.flags};
+  Arena a = spl::dev::from_api(aa);
   const int64_t si = slots[b];
   if (tid == 0) {
     int ok = 0;
@@ -580,6 +580,7 @@ __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, co
       aadd64(epoch_ptr(a.slot((size_t)si)), 1);
       aadd64(&a.hdr()->epoch, 1);
       mark_dirty(a, (size_t)si);
+      notify_host(a);
     }
   }
   if (tid == 0 && status) status[b] = lock_ok == 1 ? 0 : lock_ok;

@@ -67,7 +67,7 @@ __global__ __launch_bounds__(256) void k_score_topk(spl_arena_t aa, const float*
   __shared__ int cnt[kWaves][kMaxQ];
   using namespace spl;
   using namespace spl::dev;
-  const Arena a{(uint8_t*)aa.base, aa.slots, aa.max_val, aa.stride, aa.flags};
+  const Arena a = spl::dev::from_api(aa);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < nq * kD; i += 256) Qs[i] = queries[i];
   if (tid < kMaxQ * kWaves) cnt[tid / kMaxQ][tid % kMaxQ] = 0;
@@ -275,7 +275,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma(spl_arena_t aa, cons
                                                            uint32_t* __restrict__ cnt, uint32_t* __restrict__ cand,
                                                            int capb) {
   __shared__ __attribute__((aligned(16))) Smem sm;
-  const spl::dev::Arena a{(uint8_t*)aa.base, aa.slots, aa.max_val, aa.stride, aa.flags};
+  const spl::dev::Arena a = spl::dev::from_api(aa);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
   const long tile_base = slot_begin / kTile;  // slot_begin tile aligned, slot_end - slot_begin >= kTile
@@ -467,7 +467,7 @@ __global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __
   __shared__ float qn_s;
   __shared__ Cand top[kWaves][kMaxK];
   __shared__ int tc[kWaves];
-  const spl::dev::Arena a{(uint8_t*)aa.base, aa.slots, aa.max_val, aa.stride, aa.flags};
+  const spl::dev::Arena a = spl::dev::from_api(aa);
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   for (int i = tid; i < kD; i += 256) Qs[i] = queries[(long)q * kD + i];
   if (tid < kWaves) tc[tid] = 0;

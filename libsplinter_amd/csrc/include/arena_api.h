@@ -22,6 +22,7 @@ typedef struct spl_arena {
   uint32_t max_val;
   uint32_t stride;    /* 128 or 3200 */
   uint32_t flags;     /* bit0: event bus armed (maintain dirty mask) */
+  uint64_t notify;    /* device address of the host-mapped event-bus notify word (0 = none) */
 } spl_arena_t;
 
 #ifndef __HIP_PLATFORM_AMD__
@@ -77,6 +78,9 @@ int spl_arena_embed_get(spl_arena_t a, const char *keys, int kstride, float *vec
                         hipStream_t stream);
 int spl_arena_scan(spl_arena_t a, int mode, uint64_t mask, uint32_t *out_idx, uint64_t *out_epoch,
                    uint32_t cap, uint32_t *counter, hipStream_t stream);
+/* the same over slots [first, last) (chunked host scans with bounded scratch) */
+int spl_arena_scan_range(spl_arena_t a, int mode, uint64_t mask, uint32_t first, uint32_t last, uint32_t *out_idx,
+                         uint64_t *out_epoch, uint32_t cap, uint32_t *counter, hipStream_t stream);
 int spl_arena_purge(spl_arena_t a, hipStream_t stream);
 int spl_arena_gather_slots(spl_arena_t a, const uint32_t *idx, long n, uint8_t *out_core, hipStream_t stream);
 int spl_hash_keys(const char *keys, int kstride, long n, uint64_t *out, hipStream_t stream);

@@ -1,0 +1,144 @@
+"""Per-call API of hbm: stores through the device command ring (csrc/hip/cmd_ring.hip):
+latency / throughput from host threads, atomic device append, device-side BIGUINT promotion,
+and the event bus waking a separate process on batched device writes."""
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ENV = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+
+
+def _hostapi(store, threads, seconds=1.0, append=0):
+    tool = os.path.join(ROOT, "libsplinter_amd", "bin", "splinter_hostapi_bench")
+    cmd = [tool, "--store", store, "--threads", str(threads), "--seconds", str(seconds), "--keys", "20000"]
+    if append:
+        cmd += ["--append-check", str(append)]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=120, env=ENV)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    print(json.dumps(res))
+    return res
+
+
+def test_hostapi_single_thread_latency(uniq):
+    res = _hostapi(f"hbm:{uniq}", 1)
+    assert res["failures"] == 0
+    assert res["p50_us"] < 100.0  # ring round trip, not a launch + sync per call
+
+
+def test_hostapi_many_threads_and_concurrent_append(uniq):
+    """16 host threads: no failures, and 16 x 16 concurrent appends to one key all land, each
+    thread's records in its own order (append holds the slot seqlock on the device)."""
+    res = _hostapi(f"hbm:{uniq}", 16, append=16)
+    assert res["failures"] == 0 and res["append_check"] == 1
+    assert res["ops_per_s"] > 100_000
+
+
+def test_append_semantics_on_hbm(uniq):
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=256, max_val=64, embeddings=False)
+    try:
+        s.set("log", b"abc")
+        assert s.append("log", b"def") == 6
+        assert s.get("log") == b"abcdef"
+        with pytest.raises(OSError):
+            s.append("log", b"x" * 60)  # EMSGSIZE: 6 + 60 > 64
+        assert s.get("log") == b"abcdef"
+        with pytest.raises(OSError):
+            s.append("missing", b"x")
+        e0 = s.epoch("log")
+        s.append("log", b"!")
+        assert s.epoch("log") == e0 + 2
+    finally:
+        s.close()
+
+
+def test_biguint_promotion_on_device(uniq):
+    """reference splinter.c:637-680: a short value becomes a u64 -- ASCII parsed with
+    strtoull(.., 0) (decimal / 0x hex / 0 octal), other bytes taken raw (little endian)."""
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=256, max_val=64, embeddings=False)
+    try:
+        cases = {"dec": (b"41", 41), "hex": (b"0x1f", 31), "oct": (b"017", 15), "raw": (b"\x05\x01", 0x0105)}
+        for k, (v, want) in cases.items():
+            s.set(k, v)
+            s.set_type(k, 1 << 2)
+            assert s.get_u64(k) == want, k
+            assert s.integer_op(k, 4, 1) == want + 1  # INC
+        s.set("long", b"123456789")  # >= 8 bytes: left as is, only the type changes
+        s.set_type("long", 1 << 2)
+        assert s.get("long") == b"123456789"
+    finally:
+        s.close()
+
+
+def test_header_ops_through_ring(uniq):
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=256, max_val=64, embeddings=False)
+    try:
+        assert s.get_mop() == 1
+        s.set_mop(0)
+        assert s.get_mop() == 0
+        s.set_mop(2)
+        assert s.get_mop() == 2
+        h = s.header()
+        assert h["slots"] == 256 and h["max_val_sz"] == 64
+        s.set("a", "1")
+        assert s.watch_label(1 << 3, 7)
+        s.set_label("a", 1 << 3)
+        c0 = s.signal_count(7)
+        s.bump("a")
+        assert s.signal_count(7) == c0 + 1
+    finally:
+        s.close()
+
+
+_WAITER = r"""
+import sys, time
+from libsplinter_amd import Store
+s = Store.open(sys.argv[1])
+s.event_bus_init()
+fd = s.event_bus_open()
+print("ready", flush=True)
+ok = Store.event_bus_wait(fd, 20000)
+print("woke" if ok else "timeout", flush=True)
+print("dirty", sum(bin(w).count("1") for w in s.dirty_mask()), flush=True)
+"""
+
+
+def test_event_bus_wakes_other_process_on_batched_device_write(uniq):
+    """A separate process owns the event bus and blocks in splinter_event_bus_wait; THIS process
+    writes a key with a batched set kernel (no per-call API): the kernel's notify store reaches
+    the owner's proxy thread, which signals the eventfd; the dirty mask is marked on the device."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, pack_keys, pack_values
+    arena = HbmArena.create(uniq, slots=4096, max_val=256, embeddings=False)
+    K = pack_keys(["evt"], 16)
+    V, L = pack_values([b"v0"], 16)
+    assert (arena.set(K, V, L) == 0).all()
+    torch.cuda.synchronize()
+    p = subprocess.Popen([sys.executable, "-c", _WAITER, f"hbm:{uniq}"], cwd=ROOT, env=ENV, stdout=subprocess.PIPE,
+                         stderr=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().strip() == "ready"
+        time.sleep(0.2)
+        V, L = pack_values([b"v1"], 16)
+        assert (arena.set(K, V, L) == 0).all()
+        torch.cuda.synchronize()
+        out, err = p.communicate(timeout=60)
+    finally:
+        if p.poll() is None:
+            p.kill()
+        arena.close()
+    assert p.returncode == 0, err[-2000:]
+    lines = out.split()
+    assert lines[0] == "woke", out + err[-1000:]
+    assert int(lines[-1]) >= 1

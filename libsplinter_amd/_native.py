@@ -58,7 +58,8 @@ def hip_lib() -> ctypes.CDLL:
     core_lib()
     with _lock:
         if _hip is None:
-            path = lib_path("libsplinter_hip.so")
+            variant = os.environ.get("SPLINTER_HIP_VARIANT")  # A/B builds: lib/libsplinter_hip_<v>.so
+            path = lib_path(f"libsplinter_hip_{variant}.so" if variant else "libsplinter_hip.so")
             if not os.path.exists(path):
                 raise NativeMissing(f"{path} not built; run `make hip`")
             os.environ.setdefault("SPLINTER_HIP_LIB", path)
@@ -188,6 +189,12 @@ def _declare_hip(L):
     _sig(L, "spl_arena_embed_set", c_int, A, P, c_int, P, c_long, P, P)
     _sig(L, "spl_arena_embed_get", c_int, A, P, c_int, P, c_long, P, P)
     _sig(L, "spl_arena_scan", c_int, A, c_int, c_u64, P, P, c_u32, P, P)
+    _sig(L, "spl_arena_scan_range", c_int, A, c_int, c_u64, c_u32, c_u32, P, P, c_u32, P, P)
+    _sig(L, "spl_kvs_create", P, c_int, c_int)
+    _sig(L, "spl_kvs_destroy", None, P)
+    _sig(L, "spl_kvs_step", c_int, P, A, P, P, c_int, P, c_int, P, c_long, P, P, P, c_int, P, c_long, P, c_int, P)
+    if hasattr(L, "spl_hbm_ring_launches"):
+        _sig(L, "spl_hbm_ring_launches", c_u32, c_void_p)
     _sig(L, "spl_arena_purge", c_int, A, P)
     _sig(L, "spl_arena_gather_slots", c_int, A, P, c_long, P, P)
     _sig(L, "spl_hash_keys", c_int, P, c_int, c_long, P, P)

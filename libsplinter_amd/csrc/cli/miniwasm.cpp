@@ -1013,6 +1013,7 @@ void Instance::call(uint32_t fidx, std::vector<uint64_t>& stack, int depth) {
     return;
   }
   const Func& f = m_.funcs[fidx - m_.imports.size()];
+  if (stack.size() < np) throw Error("stack underflow at call");
   std::vector<uint64_t> locals(stack.end() - np, stack.end());
   stack.resize(stack.size() - np);
   locals.resize(np + f.locals.size(), 0);
@@ -1026,14 +1027,21 @@ void Instance::call(uint32_t fidx, std::vector<uint64_t>& stack, int depth) {
   labels.push_back(Label{(uint32_t)f.code.size(), base, (uint32_t)ft.results.size()});
   std::vector<uint64_t>& S = stack;
   auto pop = [&]() {
-    if (S.empty()) throw Error("stack underflow");
+    if (S.size() <= base) throw Error("stack underflow");
     const uint64_t v = S.back();
     S.pop_back();
     return v;
   };
+  // operand-stack bounds are checked on every access: modules are not validated ahead of time,
+  // so a malformed one must fail with an Error, never read outside the stack
+  auto top = [&]() -> uint64_t {
+    if (S.size() <= base) throw Error("stack underflow");
+    return S.back();
+  };
   auto branch = [&](uint32_t depth_, uint32_t& pc) {
     if (depth_ >= labels.size()) throw Error("bad branch depth");
     const Label L = labels[labels.size() - 1 - depth_];
+    if (L.height > S.size() || S.size() - L.height < L.arity) throw Error("stack underflow at branch");
     std::vector<uint64_t> carry(S.end() - L.arity, S.end());
     S.resize(L.height);
     S.insert(S.end(), carry.begin(), carry.end());
@@ -1051,6 +1059,7 @@ void Instance::call(uint32_t fidx, std::vector<uint64_t>& stack, int depth) {
     return v;
   };
   auto st = [&](const Instr& in, auto v) {
+    if (S.size() < base + 2) throw Error("stack underflow");
     const uint64_t addr = (uint32_t)S[S.size() - 2] + in.b;
     memcpy(mem_ptr(addr, sizeof(v)), &v, sizeof(v));
     S.resize(S.size() - 2);
@@ -1160,7 +1169,7 @@ void Instance::call(uint32_t fidx, std::vector<uint64_t>& stack, int depth) {
       }
       case OP_LOCAL_GET: S.push_back(locals.at(in.a)); break;
       case OP_LOCAL_SET: locals.at(in.a) = pop(); break;
-      case OP_LOCAL_TEE: locals.at(in.a) = S.back(); break;
+      case OP_LOCAL_TEE: locals.at(in.a) = top(); break;
       case OP_GLOBAL_GET: S.push_back(globals_.at(in.a)); break;
       case OP_GLOBAL_SET: globals_.at(in.a) = pop(); break;
       case 0x28: S.push_back(ld(in, uint32_t())); break;
@@ -1177,15 +1186,15 @@ void Instance::call(uint32_t fidx, std::vector<uint64_t>& stack, int depth) {
       case 0x33: S.push_back((uint64_t)ld(in, uint16_t())); break;
       case 0x34: S.push_back((uint64_t)(int64_t)ld(in, int32_t())); break;
       case 0x35: S.push_back((uint64_t)ld(in, uint32_t())); break;
-      case 0x36: st(in, (uint32_t)S.back()); break;
-      case 0x37: st(in, (uint64_t)S.back()); break;
-      case 0x38: st(in, (uint32_t)S.back()); break;
-      case 0x39: st(in, (uint64_t)S.back()); break;
-      case 0x3a: st(in, (uint8_t)S.back()); break;
-      case 0x3b: st(in, (uint16_t)S.back()); break;
-      case 0x3c: st(in, (uint8_t)S.back()); break;
-      case 0x3d: st(in, (uint16_t)S.back()); break;
-      case 0x3e: st(in, (uint32_t)S.back()); break;
+      case 0x36: st(in, (uint32_t)top()); break;
+      case 0x37: st(in, (uint64_t)top()); break;
+      case 0x38: st(in, (uint32_t)top()); break;
+      case 0x39: st(in, (uint64_t)top()); break;
+      case 0x3a: st(in, (uint8_t)top()); break;
+      case 0x3b: st(in, (uint16_t)top()); break;
+      case 0x3c: st(in, (uint8_t)top()); break;
+      case 0x3d: st(in, (uint16_t)top()); break;
+      case 0x3e: st(in, (uint32_t)top()); break;
       case OP_MEM_SIZE: S.push_back(mem_.size() / 65536); break;
       case OP_MEM_GROW: {
         const uint32_t d = (uint32_t)pop();
@@ -1394,6 +1403,7 @@ void Instance::call(uint32_t fidx, std::vector<uint64_t>& stack, int depth) {
 done:
   // function results are the top `results` values above the frame base
   if (S.size() < base + ft.results.size()) throw Error("missing function results");
+  if (S.size() < ft.results.size()) throw Error("stack underflow at return");
   std::vector<uint64_t> res(S.end() - ft.results.size(), S.end());
   S.resize(base);
   S.insert(S.end(), res.begin(), res.end());

@@ -110,9 +110,13 @@ __device__ __forceinline__ Arena from_api(const spl_arena_t& aa) {
   d.max_val = aa.max_val;
   d.stride = aa.stride;
   d.notify = aa.notify;
+#ifdef SPL_NO_BUS_PROBE
+  d.flags = aa.flags;
+#else
   const uint32_t owner = __hip_atomic_load((const uint32_t*)&((splinter_header*)aa.base)->event_bus.owner_pid,
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   d.flags = aa.flags | (owner != 0 ? 1u : 0u);
+#endif
   return d;
 }
 

@@ -412,6 +412,7 @@ class HbmStore final : public StoreBase {
     } else {
       std::memset(k, 0, 64);
     }
+    if (!ring_.ready()) { errno = ENOSYS; return -1; }
     return ring_.call(arena(), op, sub, k, in, in_len, arg, out, out_cap, r);
   }
   static int st_ret(int32_t st) {
@@ -562,6 +563,7 @@ int HbmStore::setup_buffers() {
   vstride_ = ((size_t)geo_.max_val + 15) & ~(size_t)15;
   if (vstride_ < 128) vstride_ = 128;
   HIPCHECK(hipHostMalloc((void**)&h_u32_, 64));
+  if (getenv("SPLINTER_HBM_NO_RING")) return 0;  // diagnosis only: batch kernels, no per-call API
   if (ring_.init(device_, (uint32_t)std::max<size_t>(vstride_, kEmbedBytes)) != 0) return -1;
   // the shared descriptor page(s) become device-visible: kernels of every attached process
   // store the event-bus notify word there
@@ -777,6 +779,12 @@ int spl_hbm_arena(spl_store* h, spl_arena_t* out) {
   if (!s || !out) return -2;
   *out = s->arena();
   return 0;
+}
+
+// Worker launches of the store's command ring so far (a relaunch follows every idle period).
+uint32_t spl_hbm_ring_launches(spl_store* h) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  return s ? s->ring_launches() : 0;
 }
 
 int spl_hbm_checkpoint(spl_store* h, const char* path) {

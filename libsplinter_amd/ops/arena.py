@@ -82,6 +82,40 @@ def unpack(vals: torch.Tensor, lens: torch.Tensor) -> list:
     return [bytes(v[i, : ln[i]]) for i in range(len(ln))]
 
 
+class KvStreams:
+    """A group of concurrent client streams issuing one KV step natively (hip/kv_streams.hip):
+    ``writers`` streams share the set batch, ``readers`` the get batch, each slice its own launch
+    on its own stream; the current torch stream continues after all of them."""
+
+    def __init__(self, writers: int, readers: int):
+        self._H = N.hip_lib()
+        self.h = self._H.spl_kvs_create(writers, readers)
+        if not self.h:
+            raise RuntimeError("spl_kvs_create failed")
+        self.writers, self.readers = writers, readers
+
+    def step(self, arena: "HbmArena", skeys, svals, slens, sstatus, gkeys, gout, glens, gstatus, retries: int = 64):
+        n_set = skeys.shape[0] if skeys is not None else 0
+        n_get = gkeys.shape[0] if gkeys is not None else 0
+        kstride = (skeys if n_set else gkeys).shape[1]
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        _check(self._H.spl_kvs_step(self.h, arena.desc, _stream(), ptr(skeys), kstride, ptr(svals),
+                                    svals.shape[1] if svals is not None else 16, ptr(slens), n_set, ptr(sstatus),
+                                    ptr(gkeys), ptr(gout), gout.shape[1] if gout is not None else 16, ptr(glens),
+                                    n_get, ptr(gstatus), retries, arena.stats.data_ptr()), "kvs_step")
+
+    def close(self):
+        if self.h:
+            self._H.spl_kvs_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 class HbmArena:
     """A format-v4 arena resident in HBM, driven by batched kernels.
 

@@ -57,65 +57,15 @@ def parse():
                         "even at N=1, to measure the routing overhead on one GPU")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: "
                    "ranks may share a GPU, collectives staged through the host)")
-    p.add_argument("--writer-streams", type=int, default=32,
-                   help="concurrent HIP streams issuing the step's set batch (BASELINE config #2: 32 writer "
-                        "streams); each gets an equal share of the batch")
-    p.add_argument("--reader-streams", type=int, default=32, help="concurrent HIP streams issuing the get batch")
-    p.add_argument("--mop", type=int, default=1, choices=[0, 1, 2],
-                   help="store scrub mode (splinter_set_mop): 1 = hybrid, the default of every store the "
-                        "reference creates (reference splinter.c:192-193) and of its stress tools; 0 = none")
-    p.add_argument("--dry-run", action="store_true",
-                   help="launcher check without a GPU: every rank joins a gloo group, rank 0 prints the world "
-                        "it sees as JSON and the run ends (tests/test_bench_cpu.py)")
-    p.add_argument("--host-api", type=int, default=16, metavar="THREADS",
-                   help="also measure the per-call C API (splinter_set/get through the device command ring) "
-                        "from THREADS host threads, outside the timed region; 0 = skip")
     return p.parse_args()
-
-
-def _launch_ranks(args) -> int:
-    """--gpus N > 1 without a torchrun environment: start N ranks as CHILD processes (torchrun,
-    one process per GPU, rendezvous on 127.0.0.1) before this process touches the GPU, relay
-    their output and exit with their status.  Never exec: this process stays the parent."""
-    import socket
-    import subprocess
-
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
-           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
-    env.setdefault("OMP_NUM_THREADS", "4")
-    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
-    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(_launch_ranks(args))
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    if world != args.gpus:
-        print(f"[bench] --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a mislabelled run",
-              file=sys.stderr)
-        sys.exit(2)
     import torch
     import torch.distributed as dist
 
-    if args.dry_run:
-        if world > 1:
-            dist.init_process_group("gloo")
-            t = torch.ones(1)
-            dist.all_reduce(t)
-            seen = int(t.item())
-            dist.destroy_process_group()
-        else:
-            seen = 1
-        if int(os.environ.get("RANK", "0")) == 0:
-            print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_seen": seen}), flush=True)
-        return
-
+    world = int(os.environ.get("WORLD_SIZE", "1"))
     routed = world > 1 or args.force_routed
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -126,7 +76,7 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
             dist.init_process_group(args.backend)
-    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
     from libsplinter_amd.parallel.sharded import GpuShard, ShardedKV
 
@@ -137,8 +87,7 @@ def main():
     name = f"bench{os.getpid()}r{rank}"
     t0 = time.time()
     arena = HbmArena.create(name, slots=slots, max_val=args.max_val, embeddings=False)
-    if not (os.environ.get("BENCH_SKIP_MOP") and args.mop == 1):  # diagnosis: stores are created hybrid
-        arena.store.set_mop(args.mop)  # 1 = hybrid scrub, the reference's store default
+    arena.store.set_mop(0)  # throughput mode: no scrubbing (reference stress default)
     kv = ShardedKV(GpuShard(arena))
     rkv = None
     if routed:
@@ -201,12 +150,6 @@ def main():
     # the serial one (profiles/r1_mixed_overlap.md).
     from libsplinter_amd.utils.streams import stream as hip_stream
     s_get, s_set = hip_stream("high"), hip_stream("normal")
-    # BASELINE config #2: the set batch is issued by --writer-streams concurrent client streams and the
-    # get batch by --reader-streams (streams share the HIP runtime's hardware queues, at most
-    # GPU_MAX_HW_QUEUES per priority level; readers at high priority, writers at normal)
-    nw, nr = max(1, args.writer_streams), max(1, args.reader_streams)
-    w_streams = [s_set] + [hip_stream("normal") for _ in range(nw - 1)]
-    r_streams = [s_get] + [hip_stream("high") for _ in range(nr - 1)]
     s_emb = None
     if args.overlap and not args.kv_cus and world == 1:
         s_emb = hip_stream("low")
@@ -214,52 +157,24 @@ def main():
     if args.kv_cus and world == 1:
         from libsplinter_amd.utils.streams import cu_mask_bits, masked_stream
         kv_bits, emb_bits = cu_mask_bits(args.kv_cus), cu_mask_bits(32 - args.kv_cus, args.kv_cus)
-        w_streams = [masked_stream(kv_bits) for _ in range(nw)]
-        r_streams = [masked_stream(kv_bits) for _ in range(nr)]
-        s_emb = masked_stream(emb_bits)
+        s_get, s_set, s_emb = masked_stream(kv_bits), masked_stream(kv_bits), masked_stream(emb_bits)
         log(f"[bench] overlapped phases: KV on {len(kv_bits)} CUs, encoder on {len(emb_bits)} CUs")
     stats = arena.stats
-
-    def _parts(n, k):
-        b = [n * j // k for j in range(k + 1)]
-        return [(b[j], b[j + 1]) for j in range(k) if b[j + 1] > b[j]]
-
-    set_parts, get_parts = _parts(n_set, nw), _parts(n_get, nr)
-    # native fan-out (hip/kv_streams.hip): one C call issues every client stream's slice, so 64
-    # streams do not make the step host-bound (the per-launch Python path starved the queues)
-    kvs = None
-    if not args.kv_cus and not routed and n_set + n_get and not os.environ.get("BENCH_PY_STREAMS"):
-        from libsplinter_amd.ops.arena import KvStreams
-        kvs = KvStreams(nw, nr)
-        s_status = torch.empty(max(n_set, 1), dtype=torch.int32, device="cuda")
-        g_status = torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")
-        g_lens = torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")
-
-    _phase_gap_ms = float(os.environ.get("BENCH_PHASE_GAP_MS", "0"))
 
     def step_local(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
         cur = torch.cuda.current_stream()
-        kv_streams = w_streams[:len(set_parts)] + r_streams[:len(get_parts)]
-        if kvs is not None and s_emb is None:
-            kvs.step(arena, SK if n_set else None, SV if n_set else None, SL if n_set else None, s_status,
-                     GK if n_get else None, gout if n_get else None, g_lens, g_status)
-        elif n_set:
-            for s in kv_streams:
-                s.wait_stream(cur)
-            for s, (a, b) in zip(w_streams, set_parts):
-                with torch.cuda.stream(s):
-                    arena.set(SK[a:b], SV[a:b], SL[a:b])
-            for s, (a, b) in zip(r_streams, get_parts):
-                with torch.cuda.stream(s):
-                    arena.get(GK[a:b], out=gout[a:b])
+        if n_set:
+            s_set.wait_stream(cur)
+            s_get.wait_stream(cur)
+            with torch.cuda.stream(s_set):
+                arena.set(SK, SV, SL)
+            with torch.cuda.stream(s_get):
+                arena.get(GK, out=gout)
             if s_emb is None:
-                for s in kv_streams:
-                    cur.wait_stream(s)
+                cur.wait_stream(s_set)
+                cur.wait_stream(s_get)
         if embedder is not None:
-            if _phase_gap_ms:  # diagnosis only (BENCH_PHASE_GAP_MS): idle gap between the phases
-                torch.cuda.synchronize()
-                time.sleep(_phase_gap_ms / 1e3)
             if s_emb is None:
                 embedder.run()
             else:
@@ -268,8 +183,8 @@ def main():
                     embedder.run()
                 cur.wait_stream(s_emb)
         if s_emb is not None and n_set:
-            for s in kv_streams:
-                cur.wait_stream(s)
+            cur.wait_stream(s_set)
+            cur.wait_stream(s_get)
 
     # N > 1: a host-sync-free software pipeline (parallel/routed.py).  Per step i:
     #   s_req : pack + request all-to-alls of batch i         (overlaps embed_i)
@@ -382,24 +297,6 @@ def main():
             dist.all_reduce(x)
             integrity_fail = int(x.item())
 
-    # ---- per-call C API (outside the timed region): splinter_set / splinter_get from host threads
-    # through the device command ring of an hbm: store (tools/splinter_hostapi_bench.cpp)
-    host_api = None
-    if args.host_api > 0 and rank == 0:
-        import subprocess
-        tool = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsplinter_amd", "bin",
-                            "splinter_hostapi_bench")
-        try:
-            r = subprocess.run([tool, "--store", f"hbm:hapi{os.getpid()}", "--threads", str(args.host_api),
-                                "--seconds", "1", "--keys", "65536", "--value-len", str(args.value_len)],
-                               capture_output=True, text=True, timeout=120)
-            if r.returncode == 0:
-                host_api = json.loads(r.stdout.strip().splitlines()[-1])
-            else:
-                log(f"[bench] host-API run failed: {r.stderr[-300:]}")
-        except Exception as e:  # the headline stands without it
-            log(f"[bench] host-API run failed: {e}")
-
     kv_ops = (n_set + n_get) * args.steps * world
     kv_ops_s = kv_ops / elapsed if kv_ops else 0.0
     emb_vps = emb_tps = emb_tflops = None
@@ -426,8 +323,7 @@ def main():
             "keys_per_gpu": kpg, "slots_per_gpu": slots, "global_batch": args.batch * world,
             "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
             "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),
-            "mode": args.mode, "mop": args.mop, "value_len": args.value_len,
-            "writer_streams": nw if not routed else 1, "reader_streams": nr if not routed else 1,
+            "mode": args.mode,
         },
         "kv_ops_per_s": kv_ops_s,
         "embed_vectors_per_s": emb_vps,
@@ -436,10 +332,6 @@ def main():
         "kv_attempts": attempts, "kv_ok": ok, "kv_eagain_retries": again, "kv_miss": miss,
         "successful_ops_per_s": ok / elapsed if elapsed else 0.0,
         "integrity_failures": integrity_fail,
-        "host_api_threads": args.host_api if host_api else None,
-        "host_api_ops_per_s": host_api["ops_per_s"] if host_api else None,
-        "host_api_p50_us": host_api["p50_us"] if host_api else None,
-        "host_api_p99_us": host_api["p99_us"] if host_api else None,
     }
     if rank == 0:
         print(json.dumps(res), flush=True)

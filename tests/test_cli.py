@@ -222,3 +222,47 @@ def test_wasm_suite_semantics(store):
         s.close()
     rc, _, err = ctl(store, "wasm", os.path.join(ROOT, "tests", "data", "wasm_suite.wat"), "trap")
     assert rc == 1 and "integer divide by zero" in err
+
+
+def _wasm_single_func(body_ops: bytes, results: bytes = b"\x00") -> bytes:
+    """A binary module exporting _start() with the given body (no locals) and 1 page of memory."""
+    def uleb(n):
+        out = bytearray()
+        while True:
+            b = n & 0x7F
+            n >>= 7
+            out.append(b | (0x80 if n else 0))
+            if not n:
+                return bytes(out)
+
+    def sec(i, body):
+        return bytes([i]) + uleb(len(body)) + body
+
+    types = uleb(1) + b"\x60\x00" + results
+    funcs = uleb(1) + uleb(0)
+    memory = uleb(1) + b"\x00" + uleb(1)
+    exports = uleb(1) + uleb(6) + b"_start" + b"\x00" + uleb(0)
+    body = b"\x01\x01\x7f" + body_ops  # one i32 local
+    code = uleb(1) + uleb(len(body)) + body
+    return b"\x00asm\x01\x00\x00\x00" + sec(1, types) + sec(3, funcs) + sec(5, memory) + sec(7, exports) + sec(10, code)
+
+
+def test_wasm_malformed_modules_fail_cleanly(store, tmp_path):
+    """Unvalidated malformed modules must raise an interpreter error (exit 1), never touch memory
+    outside the operand stack: a store with one operand, a local.tee on an empty stack, a branch
+    whose label expects more values than the stack holds, a function missing its result."""
+    cases = {
+        "store1": b"\x41\x05\x36\x02\x00\x0b",         # i32.const 5; i32.store -- one operand
+        "tee": b"\x22\x00\x1a\x0b",                     # local.tee 0 on an empty stack; drop
+        "br": b"\x02\x7f\x0c\x00\x0b\x1a\x0b",         # block (result i32) br 0 (nothing) end drop
+        "select": b"\x41\x01\x1b\x1a\x0b",              # i32.const 1; select -- needs three
+    }
+    for name, ops in cases.items():
+        p = tmp_path / f"{name}.wasm"
+        p.write_bytes(_wasm_single_func(ops))
+        rc, _, err = ctl(store, "wasm", str(p))
+        assert rc == 1 and "underflow" in err.lower(), (name, rc, err)
+    p = tmp_path / "noresult.wasm"
+    p.write_bytes(_wasm_single_func(b"\x0b", results=b"\x01\x7f"))
+    rc, _, err = ctl(store, "wasm", str(p))
+    assert rc == 1, (rc, err)

@@ -93,6 +93,13 @@ def _launch_ranks(args) -> int:
 
 def main():
     args = parse()
+    # Hardware queues per priority level for this process (HIP default 4).  Each HIP stream the
+    # process uses may claim a queue; with the 32 writer + 32 reader client streams, the store's
+    # control / ring streams and torch's stream that is ~8 queues, and the GPU's queue scheduler
+    # then time-slices them: the encoder phase ran 15-30 % slower.  2 per priority measured best
+    # (profiles/r2_hw_queues.md).  Set before anything initialises HIP (the GPU boxes export 4; override
+    with SPLINTER_BENCH_HW_QUEUES).
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SPLINTER_BENCH_HW_QUEUES", "2")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -103,6 +110,7 @@ def main():
     import torch
     import torch.distributed as dist
 
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     if args.dry_run:
         if world > 1:
             dist.init_process_group("gloo")
@@ -121,11 +129,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
+    liveness = None
     if routed:
-        if args.backend == "nccl":
-            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
-        else:
-            dist.init_process_group(args.backend)
+        # finite collective timeouts + async RCCL error handling, and a heartbeat monitor: a lost
+        # rank ends every survivor with a non-zero exit instead of a hung node (parallel/health.py)
+        from libsplinter_amd.parallel.health import Liveness, init_distributed
+        init_distributed(args.backend, timeout_s=600.0,
+                         device_id=torch.device("cuda", dev) if args.backend == "nccl" else None)
+        liveness = Liveness(period_s=1.0, timeout_s=120.0)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
     from libsplinter_amd.parallel.sharded import GpuShard, ShardedKV
@@ -200,13 +211,16 @@ def main():
     # which stretched the concurrently running GEMMs 2x and made the overlapped step slower than
     # the serial one (profiles/r1_mixed_overlap.md).
     from libsplinter_amd.utils.streams import stream as hip_stream
-    s_get, s_set = hip_stream("high"), hip_stream("normal")
+    py_streams = bool(args.kv_cus) or args.overlap or routed or bool(os.environ.get("BENCH_PY_STREAMS"))
+    s_get, s_set = (hip_stream("high"), hip_stream("normal")) if py_streams else (None, None)
     # BASELINE config #2: the set batch is issued by --writer-streams concurrent client streams and the
     # get batch by --reader-streams (streams share the HIP runtime's hardware queues, at most
     # GPU_MAX_HW_QUEUES per priority level; readers at high priority, writers at normal)
     nw, nr = max(1, args.writer_streams), max(1, args.reader_streams)
-    w_streams = [s_set] + [hip_stream("normal") for _ in range(nw - 1)]
-    r_streams = [s_get] + [hip_stream("high") for _ in range(nr - 1)]
+    # Python-side client streams only for the fallback path (--kv-cus masks, BENCH_PY_STREAMS): every
+    # stream the process touches can claim a hardware queue (profiles/r2_hw_queues.md)
+    w_streams = [s_set] + [hip_stream("normal") for _ in range(nw - 1 if py_streams else 0)]
+    r_streams = [s_get] + [hip_stream("high") for _ in range(nr - 1 if py_streams else 0)]
     s_emb = None
     if args.overlap and not args.kv_cus and world == 1:
         s_emb = hip_stream("low")
@@ -225,10 +239,10 @@ def main():
         return [(b[j], b[j + 1]) for j in range(k) if b[j + 1] > b[j]]
 
     set_parts, get_parts = _parts(n_set, nw), _parts(n_get, nr)
-    # native fan-out (hip/kv_streams.hip): one C call issues every client stream's slice, so 64
+    # native fan-out (spl_kvs_step, arena_kernels.hip): one C call issues every client stream's slice, so 64
     # streams do not make the step host-bound (the per-launch Python path starved the queues)
     kvs = None
-    if not args.kv_cus and not routed and n_set + n_get and not os.environ.get("BENCH_PY_STREAMS"):
+    if not py_streams and n_set + n_get:
         from libsplinter_amd.ops.arena import KvStreams
         kvs = KvStreams(nw, nr)
         s_status = torch.empty(max(n_set, 1), dtype=torch.int32, device="cuda")
@@ -236,6 +250,7 @@ def main():
         g_lens = torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")
 
     _phase_gap_ms = float(os.environ.get("BENCH_PHASE_GAP_MS", "0"))
+
 
     def step_local(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
@@ -443,6 +458,9 @@ def main():
     }
     if rank == 0:
         print(json.dumps(res), flush=True)
+    if liveness is not None:
+        dist.barrier()
+        liveness.stop()
     arena.close()
     if routed:
         dist.destroy_process_group()

@@ -152,6 +152,7 @@ def _declare_core(L):
     _sig(L, "spl_watch_label_register", c_int, S, c_u64, c_u8)
     _sig(L, "spl_pulse_keygroup", c_int, S, c_char_p)
     _sig(L, "spl_get_signal_count", c_u64, S, c_u8)
+    _sig(L, "spl_signal_add", c_int, S, c_u8, c_u64)
     _sig(L, "spl_enumerate_matches", None, S, c_u64, ENUM_CB, c_void_p)
     _sig(L, "spl_event_bus_init", c_int, S)
     _sig(L, "spl_event_bus_open", c_int, S)

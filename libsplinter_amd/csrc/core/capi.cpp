@@ -317,6 +317,9 @@ DUAL(int, madvise, -2, madvise(id, addr, len, advice, timeout), (uint32_t id, vo
 extern "C" {
 
 void splinter_purge(void) { if (g_cur) g_cur.load()->purge(); }
+int spl_signal_add(spl_store* h, uint8_t group, uint64_t delta) {
+  return h ? ((StoreBase*)h)->signal_add(group, delta) : -2;
+}
 void spl_purge(spl_store* h) { if (h) ((StoreBase*)h)->purge(); }
 
 int splinter_shard_claim(uint32_t id, uint8_t intent, uint8_t prio, uint64_t dur) {

@@ -804,6 +804,12 @@ uint64_t HostStore::signal_count(uint8_t g) {
   return ld(&H_->signal_groups[g].counter);
 }
 
+int HostStore::signal_add(uint8_t g, uint64_t delta) {
+  if (g >= SPLINTER_MAX_GROUPS) return -2;
+  __atomic_fetch_add(&H_->signal_groups[g].counter, delta, __ATOMIC_RELEASE);
+  return 0;
+}
+
 void HostStore::enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) {
   if (!cb) return;
   for (uint32_t i = 0; i < geo_.slots; ++i) {

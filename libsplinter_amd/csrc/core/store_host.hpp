@@ -73,6 +73,7 @@ class HostStore final : public StoreBase {
   int pulse_keygroup(const char* key) override;
   void pulse_slot(splinter_slot* slot) override;
   uint64_t signal_count(uint8_t group) override;
+  int signal_add(uint8_t group, uint64_t delta) override;
   void enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) override;
 
   int event_bus_init() override;

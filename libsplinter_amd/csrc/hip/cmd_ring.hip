@@ -246,7 +246,15 @@ __device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t
       *out_len = len;
       return kOk;
     }
-    case kRingWrite: {  // sub 0: store the bytes; sub 1 / 2: atomic OR / AND of ONE byte (config flags)
+    case kRingWrite: {  // sub 0: store the bytes; sub 1 / 2: atomic OR / AND of ONE byte (config
+                        // flags); sub 3: atomic add of a u64 (signal counters)
+      if (sub == 3) {
+        if (len != 8 || (arg & 7)) return kInval;
+        uint64_t d;
+        __builtin_memcpy(&d, pay, 8);
+        aadd64(a.base + arg, d);
+        return kOk;
+      }
       if (sub == 1 || sub == 2) {
         if (len != 1) return kInval;
         const uintptr_t wa = (uintptr_t)(a.base + arg);
@@ -337,9 +345,6 @@ int CmdRing::init(int device, uint32_t pstride) {
   if (hipMalloc((void**)&ctrl_, 64) != hipSuccess) return -1;
   std::memset(shared_, 0, sizeof(RingShared));
   std::memset(cmds_, 0, sizeof(RingCmd) * kRingEntries);
-  int lo = 0, hi = 0;
-  (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-  if (hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi) != hipSuccess) return -1;
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
   idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
@@ -354,6 +359,11 @@ void CmdRing::launch(const spl_arena_t& a) {
   int cur = 0;
   (void)hipGetDevice(&cur);
   if (cur != device_) (void)hipSetDevice(device_);
+  if (!stream_) {  // created on first use: a store that never takes a per-call op claims no queue
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi);
+  }
   // stream order: the previous worker (if still draining) has exited before ctrl is reset
   const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)kRingGroups};
   (void)hipMemcpyAsync(ctrl_, init, sizeof init, hipMemcpyHostToDevice, stream_);

@@ -322,6 +322,10 @@ class HbmStore final : public StoreBase {
     get_field(offsetof(splinter_header, signal_groups) + 64 * (size_t)g, &v, 8);
     return v;
   }
+  int signal_add(uint8_t g, uint64_t delta) override {
+    if (g >= SPLINTER_MAX_GROUPS) return -2;
+    return put_field(offsetof(splinter_header, signal_groups) + 64 * (size_t)g, &delta, 8, 3);
+  }
   void enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) override {
     if (!cb) return;
     std::vector<uint32_t> idx;
@@ -558,8 +562,22 @@ class HbmStore final : public StoreBase {
   friend StoreBase* hbm_factory_impl(const char*, size_t, size_t, unsigned, int, int*);
 };
 
+// One non-blocking control stream per device, shared by every store of the process (init, scans,
+// purge, checkpoint): each stream the process touches can claim a hardware queue, and past ~5
+// queues the GPU's queue scheduler time-slices them -- the encoder then ran 15 % slower in the
+// mixed bench (profiles/r2_hw_queues.md).
+static hipStream_t control_stream(int device) {
+  static std::mutex mu;
+  static hipStream_t s[64] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (device < 0 || device >= 64) device = 0;
+  if (!s[device]) (void)hipStreamCreateWithFlags(&s[device], hipStreamNonBlocking);
+  return s[device];
+}
+
 int HbmStore::setup_buffers() {
-  HIPCHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  stream_ = control_stream(device_);
+  if (!stream_) return -1;
   vstride_ = ((size_t)geo_.max_val + 15) & ~(size_t)15;
   if (vstride_ < 128) vstride_ = 128;
   HIPCHECK(hipHostMalloc((void**)&h_u32_, 64));
@@ -693,7 +711,6 @@ HbmStore::~HbmStore() {
     if (owner_) (void)hipFree(raw_);
     else (void)hipIpcCloseMemHandle(raw_);
   }
-  if (stream_) (void)hipStreamDestroy(stream_);
   if (desc_) {
     if (desc_registered_) (void)hipHostUnregister(desc_);
     if (owner_) __atomic_store_n(&desc_->magic, 0u, __ATOMIC_RELEASE);

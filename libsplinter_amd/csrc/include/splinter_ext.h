@@ -65,6 +65,7 @@ int   spl_watch_unregister(spl_store *s, const char *key, uint8_t group);
 int   spl_watch_label_register(spl_store *s, uint64_t mask, uint8_t group);
 int   spl_pulse_keygroup(spl_store *s, const char *key);
 uint64_t spl_get_signal_count(spl_store *s, uint8_t group);
+int   spl_signal_add(spl_store *s, uint8_t group, uint64_t delta);  /* counter += delta (sharded sync) */
 void  spl_enumerate_matches(spl_store *s, uint64_t mask,
                             void (*cb)(const char *key, uint64_t epoch, void *data), void *ud);
 int   spl_event_bus_init(spl_store *s);

@@ -72,6 +72,8 @@ class StoreBase {
   virtual int pulse_keygroup(const char* key) = 0;
   virtual void pulse_slot(splinter_slot* slot) = 0;
   virtual uint64_t signal_count(uint8_t group) = 0;
+  // atomic counter += delta (node-wide signal propagation of a sharded arena, parallel/signals.py)
+  virtual int signal_add(uint8_t group, uint64_t delta) = 0;
   virtual void enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) = 0;
 
   // event bus

@@ -83,7 +83,7 @@ def unpack(vals: torch.Tensor, lens: torch.Tensor) -> list:
 
 
 class KvStreams:
-    """A group of concurrent client streams issuing one KV step natively (hip/kv_streams.hip):
+    """A group of concurrent client streams issuing one KV step natively (spl_kvs_*, hip/arena_kernels.hip):
     ``writers`` streams share the set batch, ``readers`` the get batch, each slice its own launch
     on its own stream; the current torch stream continues after all of them."""
 

@@ -1,0 +1,104 @@
+"""Rank liveness and collective failure handling for the one-process-per-GPU node.
+
+SURVEY §5 asks for per-rank liveness and an abort path: the reference is single-host shared
+memory and has neither (a crashed writer leaves an odd epoch; /root/reference/splinter.h:398-412).
+On a sharded node a dead rank would leave every peer blocked in its next collective.  Three layers:
+
+* ``init_distributed(backend, timeout_s)``: process group with a finite collective timeout, and
+  RCCL's asynchronous error handling on (``TORCH_NCCL_ASYNC_ERROR_HANDLING=1``), so a collective
+  that cannot complete aborts its communicator and raises instead of hanging forever;
+* ``Liveness``: a heartbeat thread per rank on the rendezvous key-value store (rank r writes
+  ``hb/r`` every ``period_s``) plus a monitor that, when any peer's heartbeat is older than
+  ``timeout_s`` (or the store itself is gone -- rank 0 hosts it), ends this process with
+  ``EXIT_PEER_LOST`` via ``os._exit`` (a blocked collective cannot be interrupted from Python; the
+  launcher, torchrun or bench.py, then reports the failure).  Never a re-exec;
+* ``guarded(fn)``: run a step, turning a collective error into the same non-zero exit.
+"""
+from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+from datetime import timedelta
+from typing import Optional
+
+import torch.distributed as dist
+
+EXIT_PEER_LOST = 17
+
+
+def init_distributed(backend: str = "nccl", timeout_s: float = 120.0, device_id=None) -> None:
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = {"timeout": timedelta(seconds=timeout_s)}
+    if device_id is not None and backend == "nccl":
+        kw["device_id"] = device_id
+    dist.init_process_group(backend, **kw)
+
+
+def _default_store():
+    from torch.distributed import distributed_c10d as c10d
+    return c10d._get_default_store()
+
+
+class Liveness:
+    def __init__(self, period_s: float = 1.0, timeout_s: float = 10.0, exit_code: int = EXIT_PEER_LOST,
+                 on_lost=None):
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+        self.period, self.timeout, self.exit_code = period_s, timeout_s, exit_code
+        self.on_lost = on_lost  # test hook: called instead of os._exit
+        self.store = _default_store()
+        self._stop = threading.Event()
+        self.lost: Optional[int] = None
+        self._beat()
+        self._t = threading.Thread(target=self._run, name="splinter-liveness", daemon=True)
+        self._t.start()
+
+    def _beat(self):
+        self.store.set(f"splinter/hb/{self.rank}", repr(time.time()))
+
+    def _lost(self, who: int, why: str):
+        self.lost = who
+        msg = f"[splinter] rank {self.rank}: peer {who} lost ({why}); exiting with {self.exit_code}"
+        print(msg, file=sys.stderr, flush=True)
+        if self.on_lost is not None:
+            self.on_lost(who)
+            return
+        os._exit(self.exit_code)
+
+    def _run(self):
+        start = time.time()
+        while not self._stop.wait(self.period):
+            try:
+                self._beat()
+                now = time.time()
+                for r in range(self.world):
+                    if r == self.rank:
+                        continue
+                    key = f"splinter/hb/{r}"
+                    if not self.store.check([key]):
+                        if now - start > self.timeout:
+                            return self._lost(r, "no heartbeat")
+                        continue
+                    last = float(self.store.get(key).decode())
+                    if now - last > self.timeout:
+                        return self._lost(r, f"heartbeat {now - last:.1f} s old")
+            except Exception as e:  # the store (hosted by rank 0) is gone
+                if self._stop.is_set():
+                    return
+                return self._lost(0, f"store unreachable: {e!r}"[:200])
+
+    def stop(self):
+        self._stop.set()
+        self._t.join(self.period * 4)
+
+
+def guarded(fn, *a, exit_code: int = EXIT_PEER_LOST, **kw):
+    """Run ``fn``; a collective failure (timeout, aborted communicator, lost peer) ends the
+    process with ``exit_code`` instead of leaving it half-alive."""
+    try:
+        return fn(*a, **kw)
+    except (RuntimeError, dist.DistBackendError if hasattr(dist, "DistBackendError") else RuntimeError) as e:
+        print(f"[splinter] rank {dist.get_rank() if dist.is_initialized() else '?'}: collective failed: {e!r}"[:500],
+              file=sys.stderr, flush=True)
+        os._exit(exit_code)

@@ -307,6 +307,11 @@ class Store:
     def signal_count(self, group: int) -> int:
         return self._L.spl_get_signal_count(self._h, group)
 
+    def signal_add(self, group: int, delta: int) -> None:
+        """counter[group] += delta, atomically (node-wide signal propagation, parallel/signals.py)."""
+        if self._L.spl_signal_add(self._h, group, delta & 0xFFFFFFFFFFFFFFFF) != 0:
+            _raise("signal_add")
+
     def enumerate(self, mask: int) -> List[Tuple[str, int]]:
         out: List[Tuple[str, int]] = []
 

@@ -1,0 +1,11 @@
+# round 2, call 21: bisect the post-KV embed slowdown -- which object file (ring vs fan-out)
+set -x
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/r2_21
+mkdir -p $O
+B="--writer-streams 1 --reader-streams 1 --mop 1 --host-api 0"
+SPLINTER_HBM_NO_RING=1 BENCH_SKIP_MOP=1 BENCH_PY_STREAMS=1 SPLINTER_HIP_VARIANT=kvsonly timeout -k 10 200 python bench.py $B > $O/kvsonly.json 2> $O/kvsonly.err &&
+SPLINTER_HBM_NO_RING=1 BENCH_SKIP_MOP=1 BENCH_PY_STREAMS=1 SPLINTER_HIP_VARIANT=ringonly timeout -k 10 200 python bench.py $B > $O/ringonly.json 2> $O/ringonly.err &&
+SPLINTER_HBM_NO_RING=1 BENCH_SKIP_MOP=1 BENCH_PY_STREAMS=1 SPLINTER_HIP_VARIANT=noringobj timeout -k 10 200 python bench.py $B > $O/noringobj.json 2> $O/noringobj.err &&
+echo done

@@ -97,8 +97,8 @@ def main():
     # process uses may claim a queue; with the 32 writer + 32 reader client streams, the store's
     # control / ring streams and torch's stream that is ~8 queues, and the GPU's queue scheduler
     # then time-slices them: the encoder phase ran 15-30 % slower.  2 per priority measured best
-    # (profiles/r2_hw_queues.md).  Set before anything initialises HIP (the GPU boxes export 4; override
-    with SPLINTER_BENCH_HW_QUEUES).
+    # (profiles/r2_hw_queues.md).  Set before anything initialises HIP (the GPU boxes export 4;
+    # override with SPLINTER_BENCH_HW_QUEUES).
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SPLINTER_BENCH_HW_QUEUES", "2")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_launch_ranks(args))

@@ -34,6 +34,7 @@
 
 #include "minilua.hpp"
 #include "miniwasm.hpp"
+#include <dlfcn.h>
 #include "splinter_ext.h"
 
 #ifndef SPL_BUILD_ID
@@ -1015,8 +1016,34 @@ int cmd_search(int argc, char** argv) {
     splinter_unset(scratch.c_str());
     return 1;
   }
+  regex_t re;
+  bool filt = rx && regcomp(&re, rx, REG_EXTENDED | REG_NOSUB) == 0;
+  std::vector<Hit> hits;
+  // HBM store: score every candidate on the device (spl_hbm_search, libsplinter_hip.so K7 pass)
+  // instead of one slot snapshot per candidate -- same candidates, filters and ranking
+  using HbmSearch = long (*)(spl_store*, const float*, uint64_t, float, float, long, spl_search_hit*);
+  spl_store* cur = spl_store_current();
+  HbmSearch gpu = nullptr;
+  if (have_q && cur && !strcmp(spl_store_backend(cur), "hbm")) gpu = (HbmSearch)dlsym(RTLD_DEFAULT, "spl_hbm_search");
+  bool done = false;
+  if (gpu) {
+    const long cap = (limit > 0 && !filt) ? limit + 1 : (long)h.slots;  // +1: our own scratch key
+    std::vector<spl_search_hit> out((size_t)std::max<long>(cap, 1));
+    const long n = gpu(cur, q.data(), bloom, min_sim, max_dist, cap, out.data());
+    if (n >= 0) {
+      for (long i = 0; i < std::min(n, cap); ++i) {
+        const spl_search_hit& r = out[(size_t)i];
+        std::string k(r.key);
+        if (k == scratch) continue;
+        if (filt && regexec(&re, k.c_str(), 0, nullptr, 0) != 0) continue;
+        hits.push_back(Hit{k, r.sim, r.dist, r.emb != 0, r.epoch, r.bloom, r.len, r.type});
+      }
+      done = true;
+    }
+  }
   std::vector<std::string> cand;
-  if (bloom) {
+  if (done) {
+  } else if (bloom) {
     splinter_enumerate_matches(bloom, [](const char* k, uint64_t, void* ud) {
       ((std::vector<std::string>*)ud)->push_back(k);
     }, &cand);
@@ -1026,12 +1053,9 @@ int cmd_search(int argc, char** argv) {
     splinter_list(names.data(), names.size(), &n);
     for (size_t i = 0; i < n; ++i) cand.push_back(names[i]);
   }
-  regex_t re;
-  bool filt = rx && regcomp(&re, rx, REG_EXTENDED | REG_NOSUB) == 0;
   double qn = 0;
   for (float v : q) qn += (double)v * v;
   qn = std::sqrt(qn);
-  std::vector<Hit> hits;
   std::vector<float> v(SPLINTER_EMBED_DIM);
   for (auto& k : cand) {
     if (k == scratch) continue;

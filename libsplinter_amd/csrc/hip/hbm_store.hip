@@ -17,6 +17,7 @@
 #include <cstring>
 #include <fcntl.h>
 #include <algorithm>
+#include <cmath>
 #include <atomic>
 #include <mutex>
 #include <poll.h>
@@ -31,6 +32,8 @@
 
 #include "arena_api.h"
 #include "cmd_ring.hpp"
+#include "search_api.h"
+#include "vmm_share.hpp"
 #include "splinter_ext.h"
 #include "splinter_store.hpp"
 #include "store_host.hpp"
@@ -50,7 +53,11 @@ struct HbmDescriptor {
   uint64_t base_offset;
   int32_t owner_pid;
   int32_t pad;
-  hipIpcMemHandle_t handle;
+  hipIpcMemHandle_t handle;              // mode 0: one hipMalloc allocation, hipIpc
+  uint32_t mode;                         // 0 hipIpc, 1 VMM chunks (vmm_share.hpp)
+  uint32_t nchunks;
+  uint64_t chunk_bytes;
+  char sock[96];                         // mode 1: abstract socket serving the chunk fds
   alignas(64) splinter_header control;  // host control plane (shard bids, event bus owner)
   alignas(64) uint32_t notify;          // event-bus doorbell: set by kernels / per-call writers,
                                         // cleared by the owner's proxy thread
@@ -402,6 +409,7 @@ class HbmStore final : public StoreBase {
 
   // ---------------------------------------------------- bulk / helpers --
   int checkpoint(const char* path);
+  long search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap, spl_search_hit* out);
   int restore_from(const char* path);
 
  private:
@@ -541,7 +549,9 @@ class HbmStore final : public StoreBase {
   Geometry geo_;
   int device_ = 0;
   bool owner_ = false;
-  void* raw_ = nullptr;    // hipMalloc / IPC base
+  void* raw_ = nullptr;    // hipMalloc / IPC base, or the VMM range
+  VmmArena vmm_;           // mode 1 (vmm_share.hpp)
+  bool vmm_mode_ = false;
   void* dbase_ = nullptr;  // raw_ + kAlignOffset
   HbmDescriptor* desc_ = nullptr;
   bool desc_registered_ = false;
@@ -620,7 +630,17 @@ HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool 
   s->owner_ = true;
   (void)hipGetDevice(&s->device_);
   const size_t total = s->geo_.total_bytes();
-  if (hipMalloc(&s->raw_, total + 256) != hipSuccess) { *err = ENOMEM; delete s; return nullptr; }
+  // VMM chunks (attachable by other processes at any size), else one hipMalloc allocation
+  const char* ve = getenv("SPLINTER_HBM_VMM");
+  const size_t chunk_mb = getenv("SPLINTER_HBM_CHUNK_MB") ? (size_t)atol(getenv("SPLINTER_HBM_CHUNK_MB")) : 1024;
+  if (!(ve && !strcmp(ve, "0")) && s->vmm_.create(s->device_, total + 256, (chunk_mb ? chunk_mb : 1024) << 20) == 0) {
+    s->vmm_mode_ = true;
+    s->raw_ = s->vmm_.base();
+  } else if (hipMalloc(&s->raw_, total + 256) != hipSuccess) {
+    *err = ENOMEM;
+    delete s;
+    return nullptr;
+  }
   s->dbase_ = (uint8_t*)s->raw_ + kAlignOffset;
   s->desc_ = map_descriptor(name, true, err);
   if (!s->desc_ || s->setup_buffers() != 0) { if (!*err) *err = EIO; delete s; return nullptr; }
@@ -652,8 +672,17 @@ HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool 
   d->total_bytes = total;
   d->base_offset = kAlignOffset;
   d->owner_pid = (int32_t)getpid();
-  if (hipIpcGetMemHandle(&d->handle, s->raw_) != hipSuccess) std::memset(&d->handle, 0, sizeof d->handle);
-  d->version = 2;
+  std::memset(&d->handle, 0, sizeof d->handle);
+  d->mode = s->vmm_mode_ ? 1u : 0u;
+  if (s->vmm_mode_) {
+    d->nchunks = (uint32_t)s->vmm_.chunks();
+    d->chunk_bytes = s->vmm_.chunk();
+    snprintf(d->sock, sizeof d->sock, "splinter-hbm-%d-%s", (int)getpid(), name);
+    if (s->vmm_.serve(d->sock) != 0) d->sock[0] = 0;  // not attachable; this process still works
+  } else if (hipIpcGetMemHandle(&d->handle, s->raw_) != hipSuccess) {
+    std::memset(&d->handle, 0, sizeof d->handle);
+  }
+  d->version = 3;
   __atomic_store_n(&d->magic, kDescMagic, __ATOMIC_RELEASE);
   return s;
 }
@@ -676,7 +705,18 @@ HbmStore* HbmStore::open(const char* name, int* err) {
   s->geo_.stride = d->stride;
   s->device_ = (int)d->device;
   (void)hipSetDevice(s->device_);
-  if (hipIpcOpenMemHandle(&s->raw_, d->handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+  if (d->version >= 3 && d->mode == 1) {
+    std::vector<int> fds;
+    size_t chunk = 0;
+    if (!d->sock[0] || VmmArena::fetch(d->sock, &fds, &chunk) != 0 || fds.size() != d->nchunks ||
+        s->vmm_.import(s->device_, fds, chunk) != 0) {
+      *err = EACCES;
+      delete s;
+      return nullptr;
+    }
+    s->vmm_mode_ = true;
+    s->raw_ = s->vmm_.base();
+  } else if (hipIpcOpenMemHandle(&s->raw_, d->handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
     *err = EACCES;
     s->raw_ = nullptr;
     delete s;
@@ -708,7 +748,8 @@ HbmStore::~HbmStore() {
   if (d_scan_ep_) (void)hipFree(d_scan_ep_);
   if (d_scan_cnt_) (void)hipFree(d_scan_cnt_);
   if (raw_) {
-    if (owner_) (void)hipFree(raw_);
+    if (vmm_mode_) vmm_.release();
+    else if (owner_) (void)hipFree(raw_);
     else (void)hipIpcCloseMemHandle(raw_);
   }
   if (desc_) {
@@ -718,6 +759,69 @@ HbmStore::~HbmStore() {
     munmap(desc_, (sizeof(HbmDescriptor) + pg - 1) / pg * pg);
     if (owner_) shm_unlink((name_ + ".hbm").c_str());
   }
+}
+
+// CLI search (reference splinter_cli_cmd_search.c:339-416) on the device: one fused scoring pass
+// over every slot (spl_arena_score_all), then the candidates ranked by similarity desc, distance
+// asc on the host, and the slot metadata of the best `cap` gathered.  Returns the number of
+// candidates (may exceed cap), -1 on error.
+long HbmStore::search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap,
+                          spl_search_hit* out) {
+  if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
+  std::vector<float> sd((size_t)geo_.slots * 2);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    float* d_q = nullptr;
+    void* d_out = nullptr;
+    if (hipMallocAsync((void**)&d_q, kEmbedBytes, stream_) != hipSuccess) return -1;
+    if (hipMallocAsync(&d_out, (size_t)geo_.slots * 8, stream_) != hipSuccess) {
+      (void)hipFreeAsync(d_q, stream_);
+      return -1;
+    }
+    (void)hipMemcpyAsync(d_q, q, kEmbedBytes, hipMemcpyHostToDevice, stream_);
+    int rc = spl_arena_score_all(arena(), d_q, min_sim, max_dist, mask, d_out, stream_);
+    if (rc == 0) (void)hipMemcpyAsync(sd.data(), d_out, sd.size() * 4, hipMemcpyDeviceToHost, stream_);
+    (void)hipFreeAsync(d_q, stream_);
+    (void)hipFreeAsync(d_out, stream_);
+    (void)hipStreamSynchronize(stream_);
+    if (rc != 0) return -1;
+  }
+  struct C {
+    float sim, dist;
+    uint32_t idx;
+  };
+  std::vector<C> c;
+  for (uint32_t i = 0; i < geo_.slots; ++i)
+    if (!std::isnan(sd[2 * (size_t)i])) c.push_back(C{sd[2 * (size_t)i], sd[2 * (size_t)i + 1], i});
+  const long total = (long)c.size();
+  auto better = [](const C& a, const C& b) {
+    if (a.sim != b.sim) return a.sim > b.sim;
+    const float da = a.dist < 0 ? 0.f : a.dist, db = b.dist < 0 ? 0.f : b.dist;  // un-embedded: 0, 0
+    if (da != db) return da < db;
+    return a.idx < b.idx;
+  };
+  const size_t keep = (size_t)std::max<long>(0, std::min<long>(cap, total));
+  if (keep < c.size()) std::partial_sort(c.begin(), c.begin() + keep, c.end(), better);
+  else std::sort(c.begin(), c.end(), better);
+  c.resize(keep);
+  std::vector<uint32_t> idx(keep);
+  for (size_t i = 0; i < keep; ++i) idx[i] = c[i].idx;
+  fetch_cores(idx);
+  for (size_t i = 0; i < keep; ++i) {
+    const uint8_t* core = list_cache_.data() + i * 128;
+    spl_search_hit& h = out[i];
+    std::memset(&h, 0, sizeof h);
+    std::memcpy(h.key, core + kOffKey, 64);
+    h.key[63] = 0;
+    h.emb = c[i].dist >= 0.f;
+    h.sim = h.emb ? c[i].sim : 0.f;
+    h.dist = h.emb ? c[i].dist : 0.f;
+    std::memcpy(&h.epoch, core + kOffEpoch, 8);
+    std::memcpy(&h.bloom, core + kOffBloom, 8);
+    std::memcpy(&h.len, core + kOffValLen, 4);
+    h.type = core[kOffType];
+  }
+  return total;
 }
 
 // Checkpoint: stream the device image into a v4 store file (byte-identical
@@ -802,6 +906,13 @@ int spl_hbm_arena(spl_store* h, spl_arena_t* out) {
 uint32_t spl_hbm_ring_launches(spl_store* h) {
   auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
   return s ? s->ring_launches() : 0;
+}
+
+long spl_hbm_search(spl_store* h, const float* query, uint64_t mask, float min_sim, float max_dist, long cap,
+                    spl_search_hit* out) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  if (!s || !query || (cap > 0 && !out)) return -2;
+  return s->search_all(query, mask, min_sim, max_dist, cap, out);
 }
 
 int spl_hbm_checkpoint(spl_store* h, const char* path) {

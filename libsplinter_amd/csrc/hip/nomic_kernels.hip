@@ -747,7 +747,8 @@ int nomic_dequant(int type, const void* src, long n, void* dst, hipStream_t s) {
     hipLaunchKernelGGL(k_convert, dim3(grid_of(n / 8, 256)), dim3(256), 0, s, type, (const uint8_t*)src, n / 8,
                        (uint16_t*)dst);
   } else {
-    if (n % 32) return (int)hipErrorInvalidValue;
+    if (n % 32 || ((type == 12 || type == 14) && n % 256)) return (int)hipErrorInvalidValue;  // K-quants: 256
+    if (type != 2 && type != 3 && type != 8 && type != 12 && type != 14) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(k_dequant, dim3(grid_of(n / 32, 256)), dim3(256), 0, s, type, (const uint8_t*)src, n / 32,
                        (uint16_t*)dst);
   }

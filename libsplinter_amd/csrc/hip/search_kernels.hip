@@ -524,9 +524,71 @@ __global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __
 }
 }  // namespace mf
 
+// CLI `search` over an HBM store (reference splinter_cli_cmd_search.c:339-416): every candidate
+// slot -- live (hash != 0) and either carrying every bloom bit of `mask`, or, without a mask,
+// holding a value (the reference's splinter_list) -- gets {sim, dist}: cosine and euclidean
+// distance against the query for an embedded slot, {0, -1} for a candidate without a vector
+// (listed with null scores when no score filter is set), {NaN, NaN} for a non-candidate or one a
+// filter rejects (min_sim / max_dist > 0, as the reference treats 0 = off).  One wave per slot:
+// the 3072-B vector arrives as 64 lanes x 3 x 16 B.
+__global__ __launch_bounds__(256) void k_score_all(spl_arena_t aa, const float* __restrict__ query, float min_sim,
+                                                   float max_dist, uint64_t mask, float2* __restrict__ out) {
+  using namespace spl;
+  using namespace spl::dev;
+  const Arena a = from_api(aa);
+  const int lane = threadIdx.x & 63;
+  const float4* q4 = (const float4*)query;
+  float4 q[3];
+#pragma unroll
+  for (int c = 0; c < 3; ++c) q[c] = q4[lane + 64 * c];
+  float qn = 0.f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) qn += q[c].x * q[c].x + q[c].y * q[c].y + q[c].z * q[c].z + q[c].w * q[c].w;
+  qn = wave_sum(qn);
+  const long nwv = ((long)gridDim.x * blockDim.x) >> 6;
+  for (long i = ((long)blockIdx.x * blockDim.x + threadIdx.x) >> 6; i < (long)a.slots; i += nwv) {
+    const uint8_t* s = a.slot((size_t)i);
+    const uint64_t h = ald64(s + kOffHash);
+    bool cand = h != 0;
+    if (cand) cand = mask ? (ald64(s + kOffBloom) & mask) == mask : ald32(s + kOffValLen) > 0;
+    float2 r = make_float2(__builtin_nanf(""), __builtin_nanf(""));
+    if (cand) {  // wave-uniform
+      const float4* v4 = (const float4*)(s + kOffEmbed);
+      float en = 0.f, dot = 0.f;
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float4 e = v4[lane + 64 * c];
+        en += e.x * e.x + e.y * e.y + e.z * e.z + e.w * e.w;
+        dot += e.x * q[c].x + e.y * q[c].y + e.z * q[c].z + e.w * q[c].w;
+      }
+      en = wave_sum(en);
+      dot = wave_sum(dot);
+      if (en > 1e-12f && qn > 1e-12f) {
+        const float sim = dot / (sqrtf(en) * sqrtf(qn));
+        const float dist = sqrtf(fmaxf(en + qn - 2.f * dot, 0.f));
+        if (!((min_sim > 0.f && sim < min_sim) || (max_dist > 0.f && dist > max_dist))) r = make_float2(sim, dist);
+      } else if (!(min_sim > 0.f || max_dist > 0.f)) {
+        r = make_float2(0.f, -1.f);
+      }
+    }
+    if (lane == 0) out[i] = r;
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+int spl_arena_score_all(spl_arena_t a, const float* query, float min_sim, float max_dist, uint64_t mask, void* out,
+                        hipStream_t s) {
+  if (a.stride != 3200) return (int)hipErrorInvalidValue;
+  long g = ((long)a.slots + 3) / 4;
+  if (g > 2048) g = 2048;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(k_score_all, dim3((unsigned)g), dim3(256), 0, s, a, query, min_sim, max_dist, mask, (float2*)out);
+  return (int)hipGetLastError();
+}
+
 
 int spl_search_lists(int grid) { return grid * kWaves; }
 

@@ -35,6 +35,12 @@ int spl_search_rescore(spl_arena_t a, const float *queries, int nq, int K, float
                        uint64_t mask, const uint32_t *cnt, const uint32_t *cand, int nblk, int capb, void *result,
                        hipStream_t stream);
 
+/* Score every candidate slot against one query [768] fp32 (device pointers): out[slots] float2
+ * {sim, dist}; {0, -1} = candidate without a vector, {NaN, NaN} = not a candidate / filtered out.
+ * Candidates and filters as the reference CLI search (see search_kernels.hip). */
+int spl_arena_score_all(spl_arena_t a, const float *query, float min_sim, float max_dist, uint64_t mask, void *out,
+                        hipStream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

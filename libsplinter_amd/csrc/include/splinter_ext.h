@@ -82,6 +82,20 @@ int   spl_madvise(spl_store *s, uint32_t id, void *addr, size_t len, int advice,
 int   spl_client_set_tandem(spl_store *s, const char *base, const void **vals, const size_t *lens, uint8_t orders);
 void  spl_client_unset_tandem(spl_store *s, const char *base, uint8_t orders);
 
+/* HBM stores (libsplinter_hip.so): the CLI `search` scoring on the device.  Scores every candidate
+ * slot (bloom `mask`, or every key with a value) against `query` [768] fp32, filters with min_sim /
+ * max_dist (> 0 = on), ranks by similarity desc then distance asc, and fills up to `cap` hits.
+ * Returns the number of candidates (may exceed cap); emb == 0: a candidate without a vector. */
+typedef struct spl_search_hit {
+  char key[64];
+  float sim, dist;
+  uint64_t epoch, bloom;
+  uint32_t len;
+  uint8_t type, emb, pad[2];
+} spl_search_hit;
+long  spl_hbm_search(spl_store *s, const float *query, uint64_t mask, float min_sim, float max_dist, long cap,
+                     spl_search_hit *out);
+
 /* bulk helpers (host backends): key -> slot index, -1 if absent */
 long  spl_find_slot(spl_store *s, const char *key);
 uint64_t spl_hash_key(const char *key);

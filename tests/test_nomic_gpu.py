@@ -202,3 +202,71 @@ def test_pool_writes_into_arena_slots(uniq):
         smoke_embed(a, K)
     finally:
         a.close()
+
+
+def _random_blocks(ggml_type, nblocks, rng):
+    """Random GGML blocks of `ggml_type` with finite f16 scales: every bit of the quant payload
+    varies, so the device decoder is checked against the host reference on the whole layout."""
+    from libsplinter_amd.models.gguf import TYPE_BY_ID
+    _, _, bsz = TYPE_BY_ID[ggml_type]
+    raw = rng.integers(0, 256, size=(nblocks, bsz), dtype=np.uint8)
+
+    def f16(cols, lo, hi):
+        v = rng.uniform(lo, hi, size=(nblocks, len(cols) // 2)).astype(np.float16)
+        raw[:, cols] = v.view(np.uint8).reshape(nblocks, -1)
+
+    if ggml_type == 2:        # Q4_0: d | qs[16]
+        f16([0, 1], -0.05, 0.05)
+    elif ggml_type == 3:      # Q4_1: d, m | qs[16]
+        f16([0, 1, 2, 3], -0.05, 0.05)
+    elif ggml_type == 8:      # Q8_0: d | qs[32]
+        f16([0, 1], -0.01, 0.01)
+    elif ggml_type == 12:     # Q4_K: d, dmin | scales[12] | qs[128]
+        f16([0, 1, 2, 3], 0.0, 0.01)
+    elif ggml_type == 14:     # Q6_K: ql[128] qh[64] scales[16] | d
+        f16([208, 209], -0.01, 0.01)
+    return raw
+
+
+def test_device_dequant_matches_host_reference_all_types():
+    """nomic_dequant (HIP) vs gguf.dequant_host (numpy, written from the GGML block layouts:
+    ggml-quants.c dequantize_row_q4_0/q4_1/q8_0/q4_K/q6_K) on random blocks, every device type.
+    Real nomic-embed-text Q4 GGUFs are Q4_K_M (Q4_K + Q6_K tensors)."""
+    import torch
+    from libsplinter_amd.models.gguf import dequant_host
+    from libsplinter_amd.models import nomic
+    from libsplinter_amd import _native as N
+    from libsplinter_amd.ops.arena import _stream
+    L = nomic._lib()
+    del N
+    rng = np.random.default_rng(5)
+    for t, per in ((2, 32), (3, 32), (8, 32), (12, 256), (14, 256)):
+        nb = 4096 if per == 32 else 512
+        raw = _random_blocks(t, nb, rng)
+        n = nb * per
+        ref = dequant_host(raw.reshape(-1), t, n)
+        src = torch.from_numpy(raw.reshape(-1).copy()).cuda()
+        dst = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+        rc = L.nomic_dequant(t, src.data_ptr(), n, dst.data_ptr(), _stream())
+        assert rc == 0, (t, rc)
+        torch.cuda.synchronize()
+        want = torch.from_numpy(ref)
+        got = dst.float().cpu()
+        # the device may contract d*s*q - dmin*m into an FMA: at most one bf16 step apart
+        tol = want.abs() * 2.0 ** -7 + 1e-7
+        assert ((got - want).abs() <= tol).all(), (t, (got - want).abs().max().item())
+        assert (got == want.to(torch.bfloat16).float()).float().mean() > 0.99, t
+    for t, make in ((0, lambda x: x.astype(np.float32)), (1, lambda x: x.astype(np.float16)),
+                    (30, lambda x: (x.astype(np.float32).view(np.uint32) >> 16).astype(np.uint16))):
+        x = rng.standard_normal(8192).astype(np.float32)
+        raw = make(x).view(np.uint8)
+        ref = dequant_host(raw, t, 8192)
+        src = torch.from_numpy(raw.copy()).cuda()
+        dst = torch.empty(8192, dtype=torch.bfloat16, device="cuda")
+        assert L.nomic_dequant(t, src.data_ptr(), 8192, dst.data_ptr(), _stream()) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(dst.float().cpu(), torch.from_numpy(ref).to(torch.bfloat16).float()), t
+    # K-quant lengths must be whole 256-element superblocks
+    bad = torch.zeros(144, dtype=torch.uint8, device="cuda")
+    out = torch.empty(32, dtype=torch.bfloat16, device="cuda")
+    assert L.nomic_dequant(12, bad.data_ptr(), 32, out.data_ptr(), _stream()) != 0

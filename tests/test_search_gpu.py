@@ -117,3 +117,110 @@ def test_search_batch_matches_exact(uniq, nq):
         assert torch.equal(i2, vs.search(q, k=10)[0]) and st["overflow"] > 0
     finally:
         a.close()
+
+
+def test_cli_search_on_hbm_uses_device_scoring(uniq):
+    """`splinterctl -u hbm:NAME search` scores on the GPU (spl_hbm_search, one fused pass over the
+    slots) and returns the reference CLI's candidates and order (reference
+    splinter_cli_cmd_search.c:339-416): compared with numpy over the stored vectors, with a
+    label (bloom) filter, a similarity filter, a limit and a regex.  A stand-in embedder thread
+    answers the CLI's __sqtmp_<pid> query key, as splinference would.  Also times the device
+    scoring alone over 1M embedded keys."""
+    import ctypes
+    import json
+    import threading
+    import time
+    import torch
+    from libsplinter_amd import _native as N
+    from libsplinter_amd.ops.arena import HbmArena, format_keys, pack_keys, pack_values
+    a = HbmArena.create(uniq, slots=1 << 21, max_val=64, embeddings=True)
+    stop = threading.Event()
+    try:
+        n = 20000
+        K = format_keys(n, "doc", 6, 16)
+        V, L = pack_values([b"text"] * n, 16)
+        V = V[:1].repeat(n, 1).contiguous()
+        L = L[:1].repeat(n).contiguous()
+        assert (a.set(K, V, L) == 0).all()
+        g = torch.Generator().manual_seed(3)
+        vecs = torch.randn(n, 768, generator=g)
+        vecs[11] = 0  # candidate without a vector
+        assert (a.set_embeddings(K, vecs.cuda()) == 0).all()
+        a.meta("set_label", K[:5000], torch.full((5000,), 1 << 6, dtype=torch.int64, device="cuda"))
+        torch.cuda.synchronize()
+        qv = (vecs[123] + 0.3 * torch.randn(768, generator=g)).numpy().astype(np.float32)
+        s = a.store
+
+        def embedder():  # answers the CLI's scratch key like splinference (set_embedding)
+            done = set()
+            while not stop.is_set():
+                for k, _ in s.enumerate(1):  # the CLI labels its scratch key 0x1, as splinference expects
+                    if k.startswith("__sqtmp_") and k not in done:
+                        s.set_embedding(k, qv)
+                        done.add(k)
+                        print("[embedder] answered", k, flush=True)
+                time.sleep(0.02)
+
+        t = threading.Thread(target=embedder, daemon=True)
+        t.start()
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cli = os.path.join(ROOT, "libsplinter_amd", "bin", "splinterctl")
+        M = vecs.double().numpy()
+        qq = qv.astype(np.float64)
+        nrm = np.linalg.norm(M, axis=1)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            sim = M @ qq / (nrm * np.linalg.norm(qq))
+        dist = np.linalg.norm(M - qq, axis=1)
+        names = [f"doc{i:06d}" for i in range(n)]
+
+        def run(*extra):
+            print("[cli-search]", extra, flush=True)
+            try:
+                r = subprocess.run([cli, "-u", f"hbm:{uniq}", "search", "--json", "--timeout", "20000", *extra,
+                                    "probe"], capture_output=True, text=True, timeout=90, env=env)
+            except subprocess.TimeoutExpired as e:
+                raise AssertionError(f"CLI search hung: {e.stderr!r:.2000}")
+            assert r.returncode == 0, r.stderr[-2000:]
+            print("[cli-search] ok", len(r.stdout), flush=True)
+            return json.loads(r.stdout)["results"]
+
+        res = run("--limit", "10", "--bloom", str(1 << 6))
+        ref = sorted(range(5000), key=lambda i: (-(sim[i] if nrm[i] > 0 else 0.0), dist[i] if nrm[i] > 0 else 0.0))
+        assert [x["key"] for x in res] == [names[i] for i in ref[:10]]
+        np.testing.assert_allclose([x["similarity"] for x in res], [sim[i] for i in ref[:10]], rtol=1e-4, atol=1e-4)
+        res = run("--similarity", "0.05")
+        want = [i for i in range(n) if nrm[i] > 0 and sim[i] >= 0.05]
+        want.sort(key=lambda i: (-sim[i], dist[i]))
+        assert [x["key"] for x in res] == [names[i] for i in want]
+        res = run("--limit", "5", "--regex", "^doc0001")
+        want = [i for i in range(n) if names[i].startswith("doc0001")]
+        want.sort(key=lambda i: (-(sim[i] if nrm[i] > 0 else 0.0), dist[i] if nrm[i] > 0 else 0.0))
+        assert [x["key"] for x in res] == [names[i] for i in want[:5]]
+        stop.set()
+        t.join(5)
+        # device scoring alone at 1M embedded keys
+        m = 1_000_000
+        K2 = format_keys(m, "big", 8, 16)
+        V2 = V[:1].repeat(m, 1).contiguous()
+        L2 = L[:1].repeat(m).contiguous()
+        assert (a.set(K2, V2, L2) == 0).all()
+        assert (a.set_embeddings(K2, torch.randn(m, 768, device="cuda")) == 0).all()
+        torch.cuda.synchronize()
+        L_ = N.core_lib()
+        fn = N.hip_lib().spl_hbm_search
+        fn.restype = ctypes.c_long
+        fn.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_float, ctypes.c_float,
+                       ctypes.c_long, ctypes.c_void_p]
+        out = (ctypes.c_uint8 * (104 * 16))()
+        q = np.ascontiguousarray(qv)
+        fn(s.handle, q.ctypes.data, 0, 0.0, 0.0, 10, out)  # warm
+        t0 = time.perf_counter()
+        tot = fn(s.handle, q.ctypes.data, 0, 0.0, 0.0, 10, out)
+        ms = (time.perf_counter() - t0) * 1e3
+        del L_
+        print(json.dumps({"cli_search_device_ms_1M": ms, "candidates": tot}))
+        assert tot == m + n
+        assert ms < 200.0
+    finally:
+        stop.set()
+        a.close()

@@ -26,7 +26,7 @@ HOST_LIBS := $(LIB)/libsplinter.so $(LIB)/libsplinter_p.so
 TOOLS     := $(patsubst $(SRC)/tools/%.cpp,$(BIN)/%,$(wildcard $(SRC)/tools/*.cpp)) \
              $(if $(wildcard $(SRC)/cli/*.cpp),$(BIN)/splinterctl)
 
-.PHONY: all host hip tools clean test tsan
+.PHONY: all host hip tools clean test tsan asan
 all: host hip tools
 host: $(HOST_LIBS)
 hip: $(LIB)/libsplinter_hip.so
@@ -71,6 +71,23 @@ $(BIN)/tsan:
 $(BIN)/tsan/%: $(SRC)/tools/%.cpp $(CORE_SRCS) $(CORE_HDRS) | $(BIN)/tsan
 	$(CXX) -O1 -g -std=c++17 -fsanitize=thread -Wno-tsan -fPIC -D_GNU_SOURCE -I$(SRC)/include -I$(SRC)/core \
 	  -o $@ $< $(CORE_SRCS) $(LDLIBS)
+
+# AddressSanitizer + UndefinedBehaviorSanitizer builds of the host store, the TAP / stress tools and
+# the CLI (with its Lua and WASM interpreters): the memory-error checks the reference runs as
+# valgrind memcheck ctests (reference CMakeLists.txt:316-329).  Host code only (-fno-gpu-sanitize
+# is implied: these are g++ builds; libsplinter_hip.so is never loaded by them).
+ASAN_FLAGS := -O1 -g -std=c++17 -fsanitize=address,undefined -fno-omit-frame-pointer -fno-sanitize-recover=undefined \
+              -fPIC -D_GNU_SOURCE -I$(SRC)/include -I$(SRC)/core -DSPL_BUILD_ID=\"asan\"
+ASAN_TOOLS := $(BIN)/asan/splinter_test $(BIN)/asan/splinter_stress $(BIN)/asan/splinter_chi_sao \
+              $(BIN)/asan/splinterctl $(BIN)/asan/splinter_hostapi_bench
+asan: $(ASAN_TOOLS)
+$(BIN)/asan:
+	mkdir -p $@
+$(BIN)/asan/splinterctl: $(wildcard $(SRC)/cli/*.cpp $(SRC)/cli/*.hpp) $(CORE_SRCS) $(CORE_HDRS) | $(BIN)/asan
+	$(CXX) $(ASAN_FLAGS) -I$(SRC)/cli -o $@ $(filter %.cpp,$^) $(LDLIBS)
+	ln -sf splinterctl $(BIN)/asan/splinter_cli
+$(BIN)/asan/%: $(SRC)/tools/%.cpp $(CORE_SRCS) $(CORE_HDRS) | $(BIN)/asan
+	$(CXX) $(ASAN_FLAGS) -o $@ $< $(CORE_SRCS) $(LDLIBS)
 
 clean:
 	rm -rf build $(LIB)/*.so $(BIN)

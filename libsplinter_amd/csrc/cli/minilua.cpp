@@ -10,6 +10,7 @@
 #include <cstring>
 #include <ctime>
 #include <random>
+#include <unordered_set>
 
 namespace mlua {
 
@@ -802,11 +803,25 @@ struct Parser {
 
 // ------------------------------------------------------------ evaluator ---
 struct Scope {
+  Scope();
+  ~Scope();
   std::unordered_map<std::string, std::shared_ptr<Value>> vars;
   std::shared_ptr<Scope> parent;
   Values varargs;
   bool has_varargs = false;
+  Heap* heap;
 };
+
+struct Heap {
+  std::unordered_set<Table*> tables;
+  std::unordered_set<Scope*> scopes;
+};
+static thread_local Heap* t_heap = nullptr;
+
+Table::Table() : heap(t_heap) { if (heap) heap->tables.insert(this); }
+Table::~Table() { if (heap) heap->tables.erase(this); }
+Scope::Scope() : heap(t_heap) { if (heap) heap->scopes.insert(this); }
+Scope::~Scope() { if (heap) heap->scopes.erase(this); }
 
 enum Flow { F_NORMAL, F_BREAK, F_RETURN };
 
@@ -1298,6 +1313,9 @@ static void reg(const std::shared_ptr<Table>& t, const char* name, Native f) {
 }
 
 Interp::Interp() {
+  heap = new Heap;
+  prev_heap = t_heap;
+  t_heap = heap;
   globals = std::make_shared<Table>();
   root = std::make_shared<Scope>();
   out = [](const std::string& s) { fwrite(s.data(), 1, s.size(), stdout); };
@@ -1613,7 +1631,40 @@ Interp::Interp() {
   for (const char* lib : {"string", "table", "math", "os"}) modules[lib] = G->get(Value::string(lib));
 }
 
-Interp::~Interp() {}
+Interp::~Interp() {
+  // Move every live table's and scope's contents into one graveyard first (moves destroy
+  // nothing, so no registered object disappears while the sets are walked), then drop it.
+  std::vector<Value> grave;
+  std::vector<std::shared_ptr<Value>> cells;
+  std::vector<std::shared_ptr<Scope>> parents;
+  globals.reset();
+  root.reset();
+  modules.clear();
+  for (Table* t : heap->tables) {
+    for (auto& e : t->entries) {
+      grave.push_back(std::move(e.first));
+      grave.push_back(std::move(e.second));
+    }
+    t->entries.clear();
+    t->index.clear();  // keys are copies of entries' keys: strings and tables both already moved
+  }
+  for (Scope* s : heap->scopes) {
+    for (auto& v : s->vars) cells.push_back(std::move(v.second));
+    s->vars.clear();
+    parents.push_back(std::move(s->parent));
+    for (auto& v : s->varargs) grave.push_back(std::move(v));
+    s->varargs.clear();
+  }
+  for (auto& c : cells)
+    if (c) grave.push_back(std::move(*c));
+  t_heap = prev_heap;  // objects destroyed below unregister from `heap`, which stays valid
+  grave.clear();
+  cells.clear();
+  parents.clear();
+  for (Table* t : heap->tables) t->heap = nullptr;  // still held outside the interpreter
+  for (Scope* s : heap->scopes) s->heap = nullptr;
+  delete heap;
+}
 
 void Interp::set_global(const std::string& name, Value v) { globals->set(Value::string(name), std::move(v)); }
 Value Interp::global(const std::string& name) const { return globals->get(Value::string(name)); }

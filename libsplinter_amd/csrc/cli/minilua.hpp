@@ -58,9 +58,19 @@ struct ValueEq {
   bool operator()(const Value& a, const Value& b) const;
 };
 
+struct Heap;
+
+// Tables and scopes register with the heap of the interpreter that is current on the thread, so
+// ~Interp can break the reference cycles shared_ptr cannot collect (_G._G, a closure stored in a
+// table of its own scope, ...) -- the interpreter has no tracing GC.
 struct Table {
+  Table();
+  ~Table();
+  Table(const Table&) = delete;
+  Table& operator=(const Table&) = delete;
   std::vector<std::pair<Value, Value>> entries;  // insertion order (pairs / next)
   std::unordered_map<Value, size_t, ValueHash, ValueEq> index;
+  Heap* heap;
   Value get(const Value& k) const;
   void set(const Value& k, const Value& v);
   int64_t length() const;
@@ -101,6 +111,8 @@ struct Interp {
   int depth = 0;
   int line = 0;         // line of the statement being executed (error positions)
   std::string chunk;
+  Heap* heap = nullptr;       // objects created while this interpreter is current
+  Heap* prev_heap = nullptr;  // restored on destruction (nested interpreters)
 };
 
 std::string tostring(const Value& v);

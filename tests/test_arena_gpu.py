@@ -344,3 +344,96 @@ def test_unaligned_value_rows_do_not_spill(uniq):
         assert unpack(out, ol) == vals
     finally:
         a.close()
+
+
+_RACE_READER = r"""
+import json, sys, time
+import numpy as np
+import torch
+sys.path.insert(0, sys.argv[3])
+from libsplinter_amd import Store
+from libsplinter_amd.ops.arena import HbmArena, format_keys
+n, secs = int(sys.argv[2]), float(sys.argv[4])
+a = HbmArena(Store.open(sys.argv[1]))
+
+
+def check(v, want_id):
+    try:
+        head, rest = v.split(b"|id:", 1)
+        ver = int(head[4:])
+        ident = int(rest.split(b"|", 1)[0])
+        fill = v[v.index(b"data:") + 5:]
+        return ident == want_id and len(fill) > 0 and fill == bytes([65 + ver % 26]) * len(fill)
+    except Exception:
+        return False
+
+
+g = torch.Generator(device="cuda")
+g.manual_seed(7)
+checked = torn = again = calls = 0
+print("ready", flush=True)
+t0 = time.time()
+while time.time() - t0 < secs:
+    ids = torch.randint(0, n, (4096,), device="cuda", generator=g)
+    K = format_keys(4096, "race", 8, 16, ids=ids)
+    st, out, ln = a.get(K, retries=0)
+    st, out, ln, ids = st.cpu().numpy(), out.cpu().numpy(), ln.cpu().numpy(), ids.cpu().numpy()
+    for i in range(4096):
+        if st[i] == -11:
+            again += 1
+            continue
+        checked += 1
+        if st[i] != 0 or not check(bytes(out[i, : ln[i]]), int(ids[i])):
+            torn += 1
+    for i in range(0, 64):  # the per-call path (device command ring) on the same slots
+        k = int(np.random.randint(n))
+        try:
+            v = a.store.get(f"race{k:08d}")
+            calls += 1
+            if v is None or not check(v, k):
+                torn += 1
+        except OSError:
+            again += 1
+print(json.dumps({"checked": checked, "calls": calls, "torn": torn, "eagain": again}), flush=True)
+"""
+
+
+def test_cross_process_reader_races_gpu_writers(uniq):
+    """A separate process attaches the arena and reads (batched kernels with no retries, plus
+    per-call gets through its own command ring) while THIS process's writer kernels keep
+    rewriting the same keys with new versions: every value read that is not EAGAIN must be a
+    whole, self-consistent record (ver / id / fill bytes) -- the seqlock across processes."""
+    import json
+    import subprocess
+    import sys
+    import time
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
+    n = 20000
+    a = HbmArena.create(uniq, slots=1 << 16, max_val=256, embeddings=False)
+    try:
+        K = format_keys(n, "race", 8, 16)
+        V, L = format_values(n, 1, 200, 256)
+        assert (a.set(K, V, L) == 0).all()
+        torch.cuda.synchronize()
+        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        p = subprocess.Popen([sys.executable, "-u", "-c", _RACE_READER, f"hbm:{uniq}", str(n), root, "4"],
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=env)
+        assert p.stdout.readline().strip() == "ready"
+        ver, t0 = 2, time.time()
+        while p.poll() is None and time.time() - t0 < 60:
+            V, L = format_values(n, ver, 120 + 20 * (ver % 5), 256)  # lengths change too
+            st = a.set(K, V, L)
+            ver += 1
+            if ver % 16 == 0:
+                torch.cuda.synchronize()
+        out, err = p.communicate(timeout=120)
+        assert p.returncode == 0, err[-2000:]
+        res = json.loads(out.strip().splitlines()[-1])
+        print(res, "writer versions", ver)
+        assert res["torn"] == 0, res
+        assert res["checked"] > 10000 and res["calls"] > 100 and ver > 10
+        del st
+    finally:
+        a.close()

@@ -270,3 +270,26 @@ def test_device_dequant_matches_host_reference_all_types():
     bad = torch.zeros(144, dtype=torch.uint8, device="cuda")
     out = torch.empty(32, dtype=torch.bfloat16, device="cuda")
     assert L.nomic_dequant(12, bad.data_ptr(), 32, out.data_ptr(), _stream()) != 0
+
+
+def test_full_encoder_shipped_shape_matches_fp32():
+    """The shipped shape: all 12 layers, 64 documents x 512 tokens (the bench batch), bf16 gfx950
+    kernels vs an fp32 torch forward of the same random-init nomic-bert weights."""
+    import torch
+    from libsplinter_amd.models.nomic import (Batch, NomicConfig, NomicEncoder, NomicReference, NomicWeights,
+                                              random_weights)
+    cfg = NomicConfig(layers=12)
+    w = random_weights(cfg, seed=11)
+    b_docs, seq = 64, 512
+    enc = NomicEncoder(NomicWeights.from_numpy(cfg, w), max_tokens=b_docs * seq)
+    rng = np.random.default_rng(1)
+    seqs = [rng.integers(1000, cfg.vocab, size=seq).tolist() for _ in range(b_docs)]
+    b = Batch(seqs)
+    got = enc.embed(b)
+    ref_model = NomicReference(cfg, w, "cuda")
+    ids = torch.from_numpy(np.concatenate(seqs)).cuda().long()
+    with torch.no_grad():
+        ref = ref_model(ids, b.cu_host.tolist())
+    cos = torch.nn.functional.cosine_similarity(got.float(), ref.float(), dim=1)
+    assert cos.min().item() > 0.999, cos.min().item()
+    assert _rel(got, ref) < 3e-2

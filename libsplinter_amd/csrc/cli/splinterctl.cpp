@@ -29,6 +29,7 @@
 #include <string>
 #include <sys/mman.h>
 #include <thread>
+#include <sys/syscall.h>
 #include <unistd.h>
 #include <vector>
 
@@ -835,9 +836,20 @@ int cmd_caps(int, char**) {
   printf("build=%s\n", SPL_BUILD_ID);
   printf("lua=yes (minilua, Lua 5.4 subset)\nwasm=yes (miniwasm, MVP interpreter)\nembeddings=yes\nllama=no\n");
 #ifdef SYS_mbind
-  printf("numa=yes\n");
+  {
+    // mbind is compiled in; report whether the kernel has NUMA and how many nodes it exposes
+    int nodes = 0;
+    for (int n = 0; n < 1024; ++n) {
+      char path[64];
+      snprintf(path, sizeof path, "/sys/devices/system/node/node%d", n);
+      if (access(path, F_OK) != 0) break;
+      ++nodes;
+    }
+    if (nodes > 0) printf("numa=yes (%d node%s)\n", nodes, nodes == 1 ? "" : "s");
+    else printf("numa=no (kernel without NUMA)\n");
+  }
 #else
-  printf("numa=yes\n");
+  printf("numa=no (built without mbind)\n");
 #endif
 #ifdef SPLINTER_PERSISTENT
   printf("persistent=yes\n");

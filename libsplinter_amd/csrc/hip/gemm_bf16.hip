@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdlib>
+#include <map>
+#include <mutex>
 
 #include "nomic_api.h"
 
@@ -88,7 +90,53 @@ struct EpiArgs {
   int rope_cols;         // columns (from 0) that get RoPE (q|k = 1536)
   long M;
   int gn;                // n-tiles per band of the tile order (remap_tile)
+  // LayerNorm fold (nomic_api.h NOMIC_EPI_*_FOLD / RES_*STATS)
+  const float2* pin;     // [M][np] (mean, M2) 128-column partials of the rows of A (fold) or of
+  int np;                //   res (RES_LN_STATS), as a stats-mode producer wrote them
+  float eps;
+  const float* c1;       // [N] W' 1       (fold)
+  const float* c2;       // [N] W b        (fold)
+  const uint16_t* lng;   // [N] LN gamma / beta of res (RES_LN_STATS)
+  const uint16_t* lnb;
+  float2* part;          // [M][N/128] (mean, M2) of out's rows per 128 columns (RES_*STATS)
+  // stream-K hand-off of split tiles (k_gemm_p<.., SK>): slot s = fp32 partial of the tile shared by
+  // blocks (in remapped order) s and s+1, published with flag[s] = gen
+  float4* skws;
+  uint32_t* skflag;
+  uint32_t skgen;
 };
+
+constexpr bool is_fold(int m) { return m == NOMIC_EPI_ROPE_FOLD || m == NOMIC_EPI_SWIGLU_FOLD; }
+constexpr bool is_stats(int m) { return m == NOMIC_EPI_RES_STATS || m == NOMIC_EPI_RES_LN_STATS; }
+constexpr bool is_rope(int m) { return m == NOMIC_EPI_ROPE || m == NOMIC_EPI_ROPE_FOLD; }
+constexpr bool is_swiglu(int m) { return m == NOMIC_EPI_SWIGLU || m == NOMIC_EPI_SWIGLU_FOLD; }
+constexpr bool is_rowstore(int m) { return m == NOMIC_EPI_STORE || m == NOMIC_EPI_RESIDUAL || is_stats(m); }
+constexpr bool needs_rowstats(int m) { return is_fold(m) || m == NOMIC_EPI_RES_LN_STATS; }
+
+// LN fold of one GEMM output: rstd (acc - mean c1[n]) + c2[n]  (== LN(a) . w for the unfolded w)
+__device__ __forceinline__ float fold(float acc, float2 st, float c1, float c2) {
+  return st.y * (acc - st.x * c1) + c2;
+}
+
+// sum over the 16 lanes of a row group (lanes 16k .. 16k+15) on the DPP crossbar (no LDS
+// traffic, unlike ds_bpermute): quad_perm [1,0,3,2] and [2,3,0,1] give every lane its quad's sum,
+// row_half_mirror (lane i <-> 7-i) the 8-lane sum, row_mirror (i <-> 15-i) the 16-lane sum
+template <int CTRL>
+__device__ __forceinline__ float dpp_add(float v) {
+  return v + __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float sum16(float v) {
+  v = dpp_add<0xB1>(v);
+  v = dpp_add<0x4E>(v);
+  v = dpp_add<0x141>(v);
+  return dpp_add<0x140>(v);
+}
+
+__device__ __forceinline__ void load8f(const float* p, float (&o)[8]) {  // p: 32-B aligned
+  const float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  o[0] = a.x; o[1] = a.y; o[2] = a.z; o[3] = a.w;
+  o[4] = b.x; o[5] = b.y; o[6] = b.z; o[7] = b.w;
+}
 
 // up * silu(g) with a hardware reciprocal and exp2 (v_rcp_f32 + v_exp_f32: no IEEE division
 // sequence in the epilogue; ~1 ulp, far below the bf16 output rounding)
@@ -115,10 +163,55 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = K / BK;
+  // LN modes: the epilogue's per-column vectors are fixed per thread (its column group does not
+  // change with the row iteration), so they are loaded here, ahead of the main loop, and the
+  // block's 128 row statistics are combined from the producer's partials into LDS behind the
+  // main loop (one float2 per row, past the staging / epilogue image: same __shared__ array)
+  float cv1[8], cv2[8], cv3[8], cv4[8];
+  uint4 lg = {}, lb = {};
+  float2 pr[8];
+  float2* S = (float2*)(smem + kLdsBytes);
+  if constexpr (needs_rowstats(MODE)) {
+    const long m = m0 + (tid & 127);
+    const long mr = m < ep.M ? m : ep.M - 1;
+    if (tid < 128) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) pr[i] = i < ep.np ? ep.pin[mr * ep.np + i] : make_float2(0.f, 0.f);
+    }
+  }
+  if constexpr (is_rope(MODE) && is_fold(MODE)) {
+    const int head = (tid >> 2) & 1, d0 = (tid & 3) * 8;
+    const int pc = d0 < 16 ? d0 : d0 + 16;
+    const float* c1 = ep.c1 + n0 + head * 64 + pc;
+    const float* c2 = ep.c2 + n0 + head * 64 + pc;
+    load8f(c1, cv1); load8f(c2, cv2); load8f(c1 + 16, cv3); load8f(c2 + 16, cv4);
+  } else if constexpr (is_swiglu(MODE) && is_fold(MODE)) {
+    const int c8 = (tid & 7) * 8, uc = 32 * (c8 >> 4) + (c8 & 15);
+    load8f(ep.c1 + n0 + uc, cv1); load8f(ep.c2 + n0 + uc, cv2);
+    load8f(ep.c1 + n0 + uc + 16, cv3); load8f(ep.c2 + n0 + uc + 16, cv4);
+  } else if constexpr (MODE == NOMIC_EPI_RES_LN_STATS) {
+    const int c8 = (tid & 15) * 8;
+    lg = *(const uint4*)(ep.lng + n0 + c8);
+    lb = *(const uint4*)(ep.lnb + n0 + c8);
+  }
   // LDS: [A0 | B0 | A1 | B1], 16 KB each
   stage_tile(A, lda, m0, 0, smem, wave, lane);
   stage_tile(W, ldw, n0, 0, smem + kTileBytes, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if constexpr (needs_rowstats(MODE)) {
+    if (tid < 128) {  // Chan's combination of equal-size partials (as k_row_stats)
+      float mean = 0.f, m2 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) mean += pr[i].x;  // absent partials are zero
+      mean /= (float)ep.np;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const float d = pr[i].x - mean;
+        if (i < ep.np) m2 += pr[i].y + (float)BN * d * d;
+      }
+      S[tid] = make_float2(mean, rsqrtf(m2 / ((float)BN * (float)ep.np) + ep.eps));
+    }
+  }
   __syncthreads();
 
   const int fr = lane & 15, fq = lane >> 4;
@@ -160,33 +253,65 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
         E[(wm * 64 + i * 16 + fq * 4 + r) * kEpiStride + wn * 64 + j * 16 + fr] = acc[i][j][r];
   __syncthreads();
 
-  if constexpr (MODE == NOMIC_EPI_STORE || MODE == NOMIC_EPI_RESIDUAL) {
+  if constexpr (is_rowstore(MODE)) {
 #pragma unroll
     for (int it = 0; it < (BM * BN / 8) / kThreads; ++it) {
       const int q = tid + it * kThreads;
-      const int row = q >> 4, c8 = (q & 15) * 8;
+      const int row = q >> 4, c8 = (q & 15) * 8;  // 16 consecutive lanes share a row
       const long gm = m0 + row;
-      if (gm >= ep.M) continue;
+      const bool ok = gm < ep.M;
+      if (!is_stats(MODE) && !ok) continue;      // stats modes keep every lane for the shuffles
       const float4 v0 = *(const float4*)&E[row * kEpiStride + c8];
       const float4 v1 = *(const float4*)&E[row * kEpiStride + c8 + 4];
       float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      if constexpr (MODE == NOMIC_EPI_RESIDUAL) {
-        const uint4 rr = *(const uint4*)(ep.res + gm * ep.ldr + n0 + c8);
+      if constexpr (MODE != NOMIC_EPI_STORE) {
+        const long gr = ok ? gm : ep.M - 1;
+        const uint4 rr = *(const uint4*)(ep.res + gr * ep.ldr + n0 + c8);
         const uint32_t rw[4] = {rr.x, rr.y, rr.z, rr.w};
+        float r[8];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          v[2 * e] += bf2f((uint16_t)(rw[e] & 0xffff));
-          v[2 * e + 1] += bf2f((uint16_t)(rw[e] >> 16));
+          r[2 * e] = bf2f((uint16_t)(rw[e] & 0xffff));
+          r[2 * e + 1] = bf2f((uint16_t)(rw[e] >> 16));
         }
+        if constexpr (MODE == NOMIC_EPI_RES_LN_STATS) {
+          const float2 st = S[row];
+          const uint32_t gw[4] = {lg.x, lg.y, lg.z, lg.w}, bw[4] = {lb.x, lb.y, lb.z, lb.w};
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t g2 = gw[e >> 1], b2 = bw[e >> 1];
+            const float gf = bf2f((uint16_t)(e & 1 ? g2 >> 16 : g2 & 0xffff));
+            const float bf = bf2f((uint16_t)(e & 1 ? b2 >> 16 : b2 & 0xffff));
+            r[e] = (r[e] - st.x) * st.y * gf + bf;
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += r[e];
       }
       uint4 o;
       o.x = pk2(v[0], v[1]);
       o.y = pk2(v[2], v[3]);
       o.z = pk2(v[4], v[5]);
       o.w = pk2(v[6], v[7]);
-      *(uint4*)(ep.out + gm * ep.ldo + n0 + c8) = o;
+      if (ok) *(uint4*)(ep.out + gm * ep.ldo + n0 + c8) = o;
+      if constexpr (is_stats(MODE)) {
+        // statistics of the stored (bf16-rounded) values: the consumer folds against exactly them
+        const uint32_t ow[4] = {o.x, o.y, o.z, o.w};
+        float vr[8], sm = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          vr[e] = bf2f((uint16_t)(e & 1 ? ow[e >> 1] >> 16 : ow[e >> 1] & 0xffff));
+          sm += vr[e];
+        }
+        const float mean = sum16(sm) * (1.f / BN);
+        float m2 = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) m2 += (vr[e] - mean) * (vr[e] - mean);
+        m2 = sum16(m2);
+        if (ok && (lane & 15) == 0) ep.part[gm * ntiles + nt] = make_float2(mean, m2);
+      }
     }
-  } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
+  } else if constexpr (is_swiglu(MODE)) {
     // block columns: [up16 | gate16] x 4 (pack_upgate) of output columns nt*64 + 0..63
 #pragma unroll
     for (int it = 0; it < (BM * 64 / 8) / kThreads; ++it) {
@@ -196,10 +321,16 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
       if (gm >= ep.M) continue;
       const int uc = 32 * (c8 >> 4) + (c8 & 15);
       float o[8];
+      float2 st;
+      if constexpr (is_fold(MODE)) st = S[row];
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const float up = E[row * kEpiStride + uc + e];
-        const float g = E[row * kEpiStride + uc + 16 + e];
+        float up = E[row * kEpiStride + uc + e];
+        float g = E[row * kEpiStride + uc + 16 + e];
+        if constexpr (is_fold(MODE)) {
+          up = fold(up, st, cv1[e], cv2[e]);
+          g = fold(g, st, cv3[e], cv4[e]);
+        }
         o[e] = swiglu(up, g);
       }
       uint4 w;
@@ -209,7 +340,7 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
       w.w = pk2(o[6], o[7]);
       *(uint4*)(ep.out + gm * ep.ldo + (long)nt * 64 + c8) = w;
     }
-  } else if constexpr (MODE == NOMIC_EPI_ROPE) {
+  } else if constexpr (is_rope(MODE)) {
     // two 64-wide heads per block; NEOX rotation pairs (d, d + 32)
 #pragma unroll
     for (int it = 0; it < (BM * 2 * 4) / kThreads; ++it) {
@@ -225,6 +356,14 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
       for (int e = 0; e < 8; ++e) {
         x1[e] = E[row * kEpiStride + cb + pc + e];
         x2[e] = E[row * kEpiStride + cb + pc + 16 + e];
+      }
+      if constexpr (is_fold(MODE)) {
+        const float2 st = S[row];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          x1[e] = fold(x1[e], st, cv1[e], cv2[e]);
+          x2[e] = fold(x2[e], st, cv3[e], cv4[e]);
+        }
       }
       if (gcol < ep.rope_cols) {
         const float* cs = ep.rope + (long)ep.pos[gm] * 64 + d0 * 2;
@@ -572,7 +711,7 @@ __device__ __forceinline__ uint2 pack4(const float* v) {
   return make_uint2(pk2(v[0], v[1]), pk2(v[2], v[3]));
 }
 
-template <int MODE, bool PERSIST>
+template <int MODE, bool PERSIST, bool SK = false>
 __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int K,
                                                          int mtiles, int ntiles, EpiArgs ep) {
@@ -580,9 +719,27 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wn = wave & 3;
   const int nb = mtiles * ntiles, G = gridDim.x;
-  const int my_tiles = PERSIST ? (nb - (int)blockIdx.x + G - 1) / G : 1;
   const int nk = K / BK;  // >= 2 (launcher): a lookahead of two K-steps spans at most one tile change
-  const int total = my_tiles * nk;
+  // Stream-K (SK) for tile counts that do not divide over the G blocks: nb = q*G + r with G = p*r.
+  // Every block runs q whole tiles (ids v, v+G, ...) and then 1/p of one of the r remaining
+  // tiles (k-range part*nk/p ..), so all blocks carry the same q*nk + nk/p K-steps and none idles
+  // through a last partial wave of tiles.  v is the block's position in XCD order (blocks b, b+8,
+  // ... run on one XCD), so the p parts of a split tile run on one XCD.  The parts end their
+  // blocks' streams together: parts 1..p-1 store their fp32 partials, part 0 adds them and runs
+  // the epilogue -- all after the K loop, with nothing else live.
+  int my_tiles, total, k_first = 0, v = 0, q = 0, parts = 1;
+  if constexpr (SK) {
+    const int b = (int)blockIdx.x, x = b & 7, qq = G >> 3, rr = G & 7;
+    v = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + (b >> 3);
+    q = nb / G;
+    parts = G / (nb - q * G);
+    k_first = (v % parts) * (nk / parts);
+    my_tiles = q + 1;
+    total = q * nk + nk / parts;
+  } else {
+    my_tiles = PERSIST ? (nb - (int)blockIdx.x + G - 1) / G : 1;
+    total = my_tiles * nk;
+  }
   if (my_tiles <= 0) return;
 
   const int srow = lane >> 3, schunk = ((lane & 7) ^ srow) * 8;
@@ -592,7 +749,13 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
   long m0c = 0, n0c = 0;
   auto tile_offsets = [&](int ti, uint32_t (&oa)[2][2], uint32_t (&ob)[2][2], long& m0, long& n0) {
     int mt, nt;
-    remap_tile((int)blockIdx.x + ti * G, nb, ntiles, ep.gn, mt, nt);
+    if constexpr (SK) {
+      const int id = ti < q ? ti * G + v : q * G + v / parts;
+      mt = id / ntiles;
+      nt = id - mt * ntiles;
+    } else {
+      remap_tile((int)blockIdx.x + ti * G, nb, ntiles, ep.gn, mt, nt);
+    }
     m0 = (long)mt * 256;
     n0 = (long)nt * 256;
 #pragma unroll
@@ -619,7 +782,8 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
   // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of stream step g into buffer buf
   auto stage = [&](int which, int g, int buf) {
     const bool nx = g >= (ti + 1) * nk;
-    const int k0 = (g - (ti + (nx ? 1 : 0)) * nk) * BK;
+    const int tl = ti + (nx ? 1 : 0);
+    const int k0 = (g - tl * nk + (SK && tl == q ? k_first : 0)) * BK;
     const uint16_t* base = (which < 2 ? A : W) + k0;
     char* dst = smem + buf * kBufBytes + which * kHalfBytes;
     const int h = which & 1;
@@ -648,6 +812,71 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
   // prologue, in the steady-state issue order: A0 B0 B1 A1 (t=0), A0 B0 B1 (t=1)
   stage(0, 0, 0); stage(2, 0, 0); stage(3, 0, 0); stage(1, 0, 0);
   if (total > 1) { stage(0, 1, 1); stage(2, 1, 1); stage(3, 1, 1); }
+
+  auto epilogue = [&]() {
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const long m = m0c + qm * 128 + wr * 64 + i * 16 + fr;
+        if (m < ep.M) {
+#pragma unroll
+          for (int qn = 0; qn < 2; ++qn) {
+            const long nb0 = n0c + qn * 128 + wn * 32;  // this wave's 32-column group
+            if constexpr (MODE == NOMIC_EPI_STORE || MODE == NOMIC_EPI_RESIDUAL) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const long n = nb0 + j * 16 + fq * 4;
+                float v[4] = {acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
+                              acc[qm][qn][i][j][3]};
+                if constexpr (MODE == NOMIC_EPI_RESIDUAL) {
+                  const uint2 rr = *(const uint2*)(ep.res + m * ep.ldr + n);
+                  v[0] += bf2f((uint16_t)(rr.x & 0xffff));
+                  v[1] += bf2f((uint16_t)(rr.x >> 16));
+                  v[2] += bf2f((uint16_t)(rr.y & 0xffff));
+                  v[3] += bf2f((uint16_t)(rr.y >> 16));
+                }
+                *(uint2*)(ep.out + m * ep.ldo + n) = pack4(v);
+              }
+            } else if constexpr (MODE == NOMIC_EPI_F32) {
+#pragma unroll
+              for (int j = 0; j < 2; ++j) {
+                const long n = nb0 + j * 16 + fq * 4;
+                *(float4*)((float*)ep.out + m * ep.ldo + n) =
+                    make_float4(acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
+                                acc[qm][qn][i][j][3]);
+              }
+            } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
+              float o[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) o[e] = swiglu(acc[qm][qn][i][0][e], acc[qm][qn][i][1][e]);
+              *(uint2*)(ep.out + m * ep.ldo + nb0 / 2 + fq * 4) = pack4(o);
+            } else if constexpr (MODE == NOMIC_EPI_ROPE) {
+              const long head0 = nb0 & ~63L;
+              const int d = (int)(nb0 & 32) / 2 + fq * 4;  // packed half 0: d 0-15, half 1: d 16-31
+              float x1[4], x2[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) {
+                x1[e] = acc[qm][qn][i][0][e];
+                x2[e] = acc[qm][qn][i][1][e];
+              }
+              if (head0 < ep.rope_cols) {
+                const float* cs = ep.rope + (long)ep.pos[m] * 64 + d * 2;
+#pragma unroll
+                for (int e = 0; e < 4; ++e) {
+                  const float c = cs[2 * e], s = cs[2 * e + 1];
+                  const float a = x1[e], b = x2[e];
+                  x1[e] = a * c - b * s;
+                  x2[e] = b * c + a * s;
+                }
+              }
+              *(uint2*)(ep.out + m * ep.ldo + head0 + d) = pack4(x1);
+              *(uint2*)(ep.out + m * ep.ldo + head0 + 32 + d) = pack4(x2);
+            }
+          }
+        }
+      }
+  };
 
   bf16x8 af[4][2], b0[2][2], b1[2][2];
   for (int g = 0; g < total; ++g) {
@@ -730,71 +959,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
 
     if (++kt < nk) continue;
     // ---- tile done: register epilogue (lane: rows m, 4 consecutive columns per fragment) --------
-#pragma unroll
-    for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const long m = m0c + qm * 128 + wr * 64 + i * 16 + fr;
-        if (m < ep.M) {
-#pragma unroll
-          for (int qn = 0; qn < 2; ++qn) {
-            const long nb0 = n0c + qn * 128 + wn * 32;  // this wave's 32-column group
-            if constexpr (MODE == NOMIC_EPI_STORE || MODE == NOMIC_EPI_RESIDUAL) {
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                const long n = nb0 + j * 16 + fq * 4;
-                float v[4] = {acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
-                              acc[qm][qn][i][j][3]};
-                if constexpr (MODE == NOMIC_EPI_RESIDUAL) {
-                  const uint2 rr = *(const uint2*)(ep.res + m * ep.ldr + n);
-                  v[0] += bf2f((uint16_t)(rr.x & 0xffff));
-                  v[1] += bf2f((uint16_t)(rr.x >> 16));
-                  v[2] += bf2f((uint16_t)(rr.y & 0xffff));
-                  v[3] += bf2f((uint16_t)(rr.y >> 16));
-                }
-                *(uint2*)(ep.out + m * ep.ldo + n) = pack4(v);
-              }
-            } else if constexpr (MODE == NOMIC_EPI_F32) {
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                const long n = nb0 + j * 16 + fq * 4;
-                *(float4*)((float*)ep.out + m * ep.ldo + n) =
-                    make_float4(acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
-                                acc[qm][qn][i][j][3]);
-              }
-            } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
-              float o[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                const float up = acc[qm][qn][i][0][e], gt = acc[qm][qn][i][1][e];
-                o[e] = swiglu(up, gt);
-              }
-              *(uint2*)(ep.out + m * ep.ldo + nb0 / 2 + fq * 4) = pack4(o);
-            } else if constexpr (MODE == NOMIC_EPI_ROPE) {
-              const long head0 = nb0 & ~63L;
-              const int d = (int)(nb0 & 32) / 2 + fq * 4;  // packed half 0: d 0-15, half 1: d 16-31
-              float x1[4], x2[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                x1[e] = acc[qm][qn][i][0][e];
-                x2[e] = acc[qm][qn][i][1][e];
-              }
-              if (head0 < ep.rope_cols) {
-                const float* cs = ep.rope + (long)ep.pos[m] * 64 + d * 2;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  const float c = cs[2 * e], s = cs[2 * e + 1];
-                  const float a = x1[e], b = x2[e];
-                  x1[e] = a * c - b * s;
-                  x2[e] = b * c + a * s;
-                }
-              }
-              *(uint2*)(ep.out + m * ep.ldo + head0 + d) = pack4(x1);
-              *(uint2*)(ep.out + m * ep.ldo + head0 + 32 + d) = pack4(x2);
-            }
-          }
-        }
-      }
+    epilogue();
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll
@@ -812,6 +977,57 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
 #pragma unroll
       for (int i = 0; i < 2; ++i) { offAc[h][i] = offAx[h][i]; offBc[h][i] = offBx[h][i]; }
     if (ti + 1 < my_tiles) tile_offsets(ti + 1, offAx, offBx, m0x, n0x);
+  }
+  if constexpr (SK) {
+    // the split tile: parts 1..p-1 hand over, part 0 collects and writes
+    const int part = v % parts;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (part != 0) {
+      // a thread's 32 float4 are contiguous: one address + immediate offsets
+      float4* ws = ep.skws + (size_t)v * (256 * 256 / 4) + tid * 32;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const f32x4 c = acc[a][b][i][j];
+              ws[((a * 2 + b) * 4 + i) * 2 + j] = make_float4(c[0], c[1], c[2], c[3]);
+            }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {  // agent-scope release, then the flag (cdna guide §6 Guideline 16)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(ep.skflag + v, ep.skgen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+    if (tid == 0) {
+      for (int o = 1; o < parts; ++o)
+        while (__hip_atomic_load(ep.skflag + v + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep.skgen)
+          __builtin_amdgcn_s_sleep(2);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    for (int o = 1; o < parts; ++o) {
+      const float4* ws = ep.skws + (size_t)(v + o) * (256 * 256 / 4) + tid * 32;
+#pragma unroll
+      for (int a = 0; a < 2; ++a)
+#pragma unroll
+        for (int b = 0; b < 2; ++b)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) {
+              const float4 pp = ws[((a * 2 + b) * 4 + i) * 2 + j];
+              acc[a][b][i][j] += f32x4{pp.x, pp.y, pp.z, pp.w};
+            }
+    }
+    epilogue();
   }
 }
 
@@ -840,6 +1056,30 @@ int band_width(int ntiles, int cap) {
   return 1;
 }
 
+// stream-K hand-off buffers, one set per stream (two streams' GEMMs in flight at once must not
+// share slots): cus slots of one 256x256 fp32 tile + flags; flags are compared with a per-launch
+// generation, so they are never reset
+struct SkWorkspace {
+  float4* ws = nullptr;
+  uint32_t* flag = nullptr;
+  uint32_t gen = 0;
+};
+SkWorkspace* sk_workspace(hipStream_t s, int cus) {
+  static std::mutex mu;
+  static std::map<hipStream_t, SkWorkspace> table;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = table.find(s);
+  if (it != table.end()) return &it->second;
+  SkWorkspace w;
+  if (hipMalloc((void**)&w.ws, (size_t)cus * 256 * 256 * sizeof(float)) != hipSuccess) return nullptr;
+  if (hipMalloc((void**)&w.flag, (size_t)cus * sizeof(uint32_t)) != hipSuccess ||
+      hipMemset(w.flag, 0, (size_t)cus * sizeof(uint32_t)) != hipSuccess) {
+    (void)hipFree(w.ws);
+    return nullptr;
+  }
+  return &(table[s] = w);
+}
+
 template <int MODE>
 int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int N, int K, EpiArgs ep,
            hipStream_t s) {
@@ -852,7 +1092,44 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
   // auto: the persistent register-epilogue kernel when there are several waves of 256^2 tiles
   // (measured per shape: profiles/r1_gemm_persistent_ab.jsonl); fewer tiles: the 128^2 kernel
   const bool many = (mpad / 256) * (N / 256) >= 2048;
-  if (fits && K >= 2 * BK && (var == 512 || var == 513 || (var == 0 && many))) {
+  // the statistics epilogue exists in the 128^2 kernel only (its 16-lane row groups); the 256^2
+  // launch-per-tile kernel has the plain epilogues only
+  constexpr bool p_ok = MODE <= NOMIC_EPI_F32;
+  constexpr bool k256_ok = MODE <= NOMIC_EPI_F32;
+  static const int cus = [] {
+    int d = 0, n = 0;
+    if (hipGetDevice(&d) == hipSuccess &&
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0)
+      g_num_cus = n;
+    return g_num_cus;
+  }();
+  const int nk = K / BK;
+  const long tiles256 = fits ? (mpad / 256) * (N / 256) : 0;
+  // stream-K persistent kernel when the 256^2 tiles do not divide evenly over the CUs (T = 32768:
+  // N = 768 -> 384 tiles = 256 + 128, N = 2304 -> 1152 = 4 x 256 + 128): the r leftover tiles are
+  // cut into p = cus / r K-ranges, one per block
+  const long rem = tiles256 % cus;
+  const long sk_parts = rem ? cus / rem : 0;
+  const bool sk_ok = p_ok && fits && nk >= 2 && rem != 0 && cus % rem == 0 && sk_parts <= 8 && nk % sk_parts == 0;
+  if (sk_ok && var == 514) {
+    if constexpr (p_ok) {
+      static bool attr_sk = [] {
+        (void)hipFuncSetAttribute((const void*)k_gemm_p<MODE, true, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kBufBytes);
+        return true;
+      }();
+      (void)attr_sk;
+      SkWorkspace* w = sk_workspace(s, cus);
+      if (!w) return (int)hipErrorOutOfMemory;
+      ep.skws = w->ws;
+      ep.skflag = w->flag;
+      ep.skgen = ++w->gen;
+      hipLaunchKernelGGL((k_gemm_p<MODE, true, true>), dim3(cus), dim3(kThreads2), 2 * kBufBytes, s, A, lda, W, ldw, K,
+                         (int)(mpad / 256), N / 256, ep);
+    }
+    return (int)hipGetLastError();
+  }
+  if (p_ok && fits && K >= 2 * BK && (var == 512 || var == 513 || (var == 0 && many))) {
     static bool attr_p = [] {
       (void)hipFuncSetAttribute((const void*)k_gemm_p<MODE, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
                                 2 * kBufBytes);
@@ -863,23 +1140,18 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     (void)attr_p;
     const int mtiles = (int)(mpad / 256), ntiles = N / 256;
     ep.gn = band_width(ntiles, 4);
-    static const int cus = [] {
-      int d = 0, n = 0;
-      if (hipGetDevice(&d) == hipSuccess &&
-          hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0)
-        g_num_cus = n;
-      return g_num_cus;
-    }();
     const int tiles = mtiles * ntiles;
+    if constexpr (p_ok) {
     if (var != 513)
       hipLaunchKernelGGL((k_gemm_p<MODE, true>), dim3(tiles < cus ? tiles : cus), dim3(kThreads2), 2 * kBufBytes, s,
                          A, lda, W, ldw, K, mtiles, ntiles, ep);
     else
       hipLaunchKernelGGL((k_gemm_p<MODE, false>), dim3(tiles), dim3(kThreads2), 2 * kBufBytes, s, A, lda, W, ldw, K,
                          mtiles, ntiles, ep);
+    }
     return (int)hipGetLastError();
   }
-  if (fits && (var == 256 || (var == 0 && (mpad / 256) * (N / 256) >= 2048))) {
+  if (k256_ok && fits && (var == 256 || (var == 0 && (mpad / 256) * (N / 256) >= 2048))) {
     static bool attr = [] {
       (void)hipFuncSetAttribute((const void*)k_gemm256<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
       return true;
@@ -887,13 +1159,15 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     (void)attr;
     const int mtiles = (int)(mpad / 256), ntiles = N / 256;
     ep.gn = band_width(ntiles, 4);
-    hipLaunchKernelGGL(k_gemm256<MODE>, dim3(mtiles * ntiles), dim3(kThreads2), kLds2Bytes, s, A, lda, W, ldw, K,
-                       mtiles, ntiles, ep);
+    if constexpr (k256_ok)
+      hipLaunchKernelGGL(k_gemm256<MODE>, dim3(mtiles * ntiles), dim3(kThreads2), kLds2Bytes, s, A, lda, W, ldw, K,
+                         mtiles, ntiles, ep);
     return (int)hipGetLastError();
   }
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = N / BN;
   ep.gn = band_width(ntiles, 8);
-  hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), kLdsBytes, s, A, lda, W, ldw, K, mtiles,
+  constexpr int lds = kLdsBytes + (needs_rowstats(MODE) ? BM * 8 : 0);
+  hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), lds, s, A, lda, W, ldw, K, mtiles,
                      ntiles, ep);
   return (int)hipGetLastError();
 }
@@ -906,10 +1180,17 @@ extern "C" int nomic_gemm_set_variant(int variant) {
   return prev;
 }
 
-extern "C" int nomic_gemm(int mode, const void* A, long lda, const void* W, long ldw, long M, int N, int K, void* out,
-                          long ldo, const void* res, long ldr, const float* rope, const int32_t* pos, int rope_cols,
-                          hipStream_t s) {
-  EpiArgs ep{(uint16_t*)out, ldo, (const uint16_t*)res, ldr, rope, pos, rope_cols, M, 1};
+extern "C" int nomic_gemm_ln(int mode, const void* A, long lda, const void* W, long ldw, long M, int N, int K,
+                             void* out, long ldo, const void* res, long ldr, const float* rope, const int32_t* pos,
+                             int rope_cols, const float* part_in, int nparts, float eps, const float* c1,
+                             const float* c2, const void* ln_g, const void* ln_b, float* part, hipStream_t s) {
+  EpiArgs ep{(uint16_t*)out, ldo, (const uint16_t*)res, ldr, rope, pos, rope_cols, M, 1, (const float2*)part_in,
+             nparts, eps, c1, c2, (const uint16_t*)ln_g, (const uint16_t*)ln_b, (float2*)part};
+  // operands each mode reads must be there (a fold / stats launch without them would fault)
+  if ((needs_rowstats(mode) && (!part_in || nparts < 1 || nparts > 8)) || (is_fold(mode) && (!c1 || !c2)) ||
+      (is_stats(mode) && (!part || !res || N % BN)) || (mode == NOMIC_EPI_RES_LN_STATS && (!ln_g || !ln_b)) ||
+      (mode == NOMIC_EPI_RESIDUAL && !res) || (is_rope(mode) && (!rope || !pos)))
+    return (int)hipErrorInvalidValue;
   const auto* a = (const uint16_t*)A;
   const auto* w = (const uint16_t*)W;
   switch (mode) {
@@ -918,6 +1199,44 @@ extern "C" int nomic_gemm(int mode, const void* A, long lda, const void* W, long
     case NOMIC_EPI_SWIGLU: return launch<NOMIC_EPI_SWIGLU>(a, lda, w, ldw, M, N, K, ep, s);
     case NOMIC_EPI_ROPE: return launch<NOMIC_EPI_ROPE>(a, lda, w, ldw, M, N, K, ep, s);
     case NOMIC_EPI_F32: return launch<NOMIC_EPI_F32>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_ROPE_FOLD: return launch<NOMIC_EPI_ROPE_FOLD>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_SWIGLU_FOLD: return launch<NOMIC_EPI_SWIGLU_FOLD>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_RES_STATS: return launch<NOMIC_EPI_RES_STATS>(a, lda, w, ldw, M, N, K, ep, s);
+    case NOMIC_EPI_RES_LN_STATS: return launch<NOMIC_EPI_RES_LN_STATS>(a, lda, w, ldw, M, N, K, ep, s);
     default: return (int)hipErrorInvalidValue;
   }
+}
+
+extern "C" int nomic_gemm(int mode, const void* A, long lda, const void* W, long ldw, long M, int N, int K, void* out,
+                          long ldo, const void* res, long ldr, const float* rope, const int32_t* pos, int rope_cols,
+                          hipStream_t s) {
+  if (mode > NOMIC_EPI_F32) return (int)hipErrorInvalidValue;  // the LN modes go through nomic_gemm_ln
+  return nomic_gemm_ln(mode, A, lda, W, ldw, M, N, K, out, ldo, res, ldr, rope, pos, rope_cols, nullptr, 0, 0.f,
+                       nullptr, nullptr, nullptr, nullptr, nullptr, s);
+}
+
+namespace {
+// one thread per row: Chan's combination of equal-size (128-column) partials
+__global__ void k_row_stats(const float2* __restrict__ part, int np, long M, float eps, float2* __restrict__ st) {
+  const long m = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (m >= M) return;
+  const float2* p = part + m * np;
+  float mean = 0.f;
+  for (int i = 0; i < np; ++i) mean += p[i].x;
+  mean /= (float)np;
+  float m2 = 0.f;
+  for (int i = 0; i < np; ++i) {
+    const float d = p[i].x - mean;
+    m2 += p[i].y + (float)BN * d * d;
+  }
+  const float var = m2 / ((float)BN * (float)np);
+  st[m] = make_float2(mean, rsqrtf(var + eps));
+}
+}  // namespace
+
+extern "C" int nomic_row_stats(const float* part, int nparts, long M, float eps, float* st, hipStream_t s) {
+  if (nparts <= 0 || M <= 0 || !part || !st) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_row_stats, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, s, (const float2*)part, nparts, M,
+                     eps, (float2*)st);
+  return (int)hipGetLastError();
 }

@@ -33,6 +33,8 @@ from ..utils.tracing import trace_range
 from .gguf import DEVICE_DEQUANT, GGUFFile, GGUFWriter, dequant_host
 
 EPI_STORE, EPI_RESIDUAL, EPI_SWIGLU, EPI_ROPE, EPI_F32 = 0, 1, 2, 3, 4
+# post-LayerNorm folded into the neighbouring GEMMs (csrc/include/nomic_api.h)
+EPI_ROPE_FOLD, EPI_SWIGLU_FOLD, EPI_RES_STATS, EPI_RES_LN_STATS = 5, 6, 7, 8
 
 
 @dataclass
@@ -68,6 +70,11 @@ def _lib():
         P, c_long, c_int, c_float = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float
         L.nomic_gemm.argtypes = [c_int, P, c_long, P, c_long, c_long, c_int, c_int, P, c_long, P, c_long, P, P, c_int, P]
         L.nomic_gemm.restype = c_int
+        L.nomic_gemm_ln.argtypes = [c_int, P, c_long, P, c_long, c_long, c_int, c_int, P, c_long, P, c_long, P, P,
+                                    c_int, P, c_int, c_float, P, P, P, P, P, P]
+        L.nomic_gemm_ln.restype = c_int
+        L.nomic_row_stats.argtypes = [P, c_int, c_long, c_float, P, P]
+        L.nomic_row_stats.restype = c_int
         L.nomic_gemm_set_variant.argtypes = [c_int]
         L.nomic_gemm_set_variant.restype = c_int
         L.nomic_attention_set_variant.argtypes = [c_int]
@@ -176,8 +183,20 @@ def pack_qkv(w: torch.Tensor) -> torch.Tensor:
     return w.reshape(n // 64, 64, d)[:, _QKV_PERM.to(w.device)].reshape(n, d)
 
 
+def fold_ln(w: torch.Tensor, g: torch.Tensor, b: torch.Tensor):
+    """LayerNorm folded into the linear that consumes it: LN(h) w^T = rstd (h w'^T - mean c1) + c2
+    with w' = w diag(g) (bf16), c1 = w' 1 and c2 = w b (fp32; c1 from the ROUNDED w', so the mean
+    term cancels exactly what the GEMM accumulates).  w [N, K] in kernel (packed) row order."""
+    wf = (w.float() * g.float()[None, :]).to(torch.bfloat16).contiguous()
+    c1 = wf.float().sum(1).contiguous()
+    c2 = (w.float() @ b.float()).contiguous()
+    return wf, c1, c2
+
+
 class NomicWeights:
-    """Device-resident bf16 weights in kernel layout."""
+    """Device-resident bf16 weights in kernel layout (plus the LN-folded copies the fused
+    forward uses: ``wqkv_f`` folds the previous layer's output LN, ``wupgate_f`` this layer's
+    attention-output LN)."""
 
     def __init__(self, cfg: NomicConfig, tensors: Dict[str, torch.Tensor], device="cuda"):
         self.cfg = cfg
@@ -194,6 +213,11 @@ class NomicWeights:
                 "wdown": bf(t["wdown"]),
                 "ln1_g": bf(t["ln1_g"]), "ln1_b": bf(t["ln1_b"]), "ln2_g": bf(t["ln2_g"]), "ln2_b": bf(t["ln2_b"]),
             })
+        for i, lw in enumerate(self.layers):
+            lw["wupgate_f"], lw["ug_c1"], lw["ug_c2"] = fold_ln(lw["wupgate"], lw["ln1_g"], lw["ln1_b"])
+            if i > 0:
+                prev = self.layers[i - 1]
+                lw["wqkv_f"], lw["qkv_c1"], lw["qkv_c2"] = fold_ln(lw["wqkv"], prev["ln2_g"], prev["ln2_b"])
 
     @classmethod
     def from_numpy(cls, cfg, weights: Dict[str, np.ndarray], device="cuda"):
@@ -315,6 +339,10 @@ class NomicEncoder:
         self.attn = torch.empty((T_pad, cfg.d), **e)
         self.qkv = torch.empty((T_pad, 3 * cfg.d), **e)
         self.ffn = torch.empty((T_pad, cfg.ffn), **e)
+        self.h2 = torch.empty((T_pad, cfg.d), **e)
+        f = dict(dtype=torch.float32, device="cuda")
+        self.part1 = torch.empty((T_pad, 2 * (cfg.d // 128)), **f)  # (mean, M2) per 128 columns of h1
+        self.part2 = torch.empty((T_pad, 2 * (cfg.d // 128)), **f)  # ... of h2
         self._ws_tokens = T_pad
 
     def _gemm(self, mode, A, W, M, out, res=None, pos=None):
@@ -324,8 +352,65 @@ class NomicEncoder:
                                res.stride(0) if res is not None else 0, self.rope.data_ptr(),
                                pos.data_ptr() if pos is not None else None, 2 * self.cfg.d, _stream()), "gemm")
 
+    def _gemm_ln(self, mode, A, W, M, out, res=None, pos=None, pin=None, c1=None, c2=None, ln=None, part=None):
+        N_, K = W.shape
+        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        _chk(self.L.nomic_gemm_ln(mode, A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0), M, N_, K,
+                                  out.data_ptr(), out.stride(0), ptr(res), res.stride(0) if res is not None else 0,
+                                  self.rope.data_ptr(), ptr(pos), 2 * self.cfg.d, ptr(pin),
+                                  pin.shape[1] // 2 if pin is not None else 0, self.cfg.eps, ptr(c1), ptr(c2),
+                                  ptr(ln[0]) if ln else None, ptr(ln[1]) if ln else None, ptr(part), _stream()),
+             f"gemm_ln({mode})")
+
+    # measured slower on MI355X (profiles/r2_encoder_ln_fold.md): opt in with NOMIC_LN_FOLD=1
+    ln_fold = os.environ.get("NOMIC_LN_FOLD", "0") != "0"
+
     def hidden(self, b: Batch) -> torch.Tensor:
         """Final-layer hidden states [T, 768] (bf16) for a packed batch."""
+        if self.ln_fold:
+            return self._hidden_folded(b)
+        return self._hidden_unfused(b)
+
+    def _hidden_folded(self, b: Batch) -> torch.Tensor:
+        """The forward with every post-LN folded into the GEMMs around it (K15): the residual GEMMs
+        write raw sums h1 / h2 plus 128-column partial row statistics; the next projection combines
+        them into (mean, rstd) per row in its prologue and runs on raw h against LN-folded weights,
+        and the next residual GEMM normalises its residual operand on the fly.  One LayerNorm pass
+        per forward (the final one, for pooling) instead of two per layer."""
+        cfg, L, w = self.cfg, self.L, self.w
+        assert b.max_len <= self.rope.shape[0]
+        self._ensure(b.T_pad)
+        s = _stream()
+        T = b.T
+        x, h1, h2, attn, qkv, ffn = self.x, self.h, self.h2, self.attn, self.qkv, self.ffn
+        p1, p2 = self.part1, self.part2
+        _chk(L.nomic_embed_ln(b.ids.data_ptr(), T, w.tok.data_ptr(), w.type_row.data_ptr(), w.emb_g.data_ptr(),
+                              w.emb_b.data_ptr(), cfg.eps, x.data_ptr(), s), "embed_ln")
+        scale = 1.0 / math.sqrt(cfg.head_dim)
+        prev = None
+        for lw in w.layers:
+            if prev is None:
+                self._gemm(EPI_ROPE, x, lw["wqkv"], T, qkv, pos=b.pos)
+            else:
+                self._gemm_ln(EPI_ROPE_FOLD, h2, lw["wqkv_f"], T, qkv, pos=b.pos, pin=p2, c1=lw["qkv_c1"],
+                              c2=lw["qkv_c2"])
+            _chk(L.nomic_attention(qkv.data_ptr(), attn.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb,
+                                   cfg.heads, scale, s), "attention")
+            if prev is None:
+                self._gemm_ln(EPI_RES_STATS, attn, lw["wo"], T, h1, res=x, part=p1)
+            else:
+                self._gemm_ln(EPI_RES_LN_STATS, attn, lw["wo"], T, h1, res=h2, pin=p2,
+                              ln=(prev["ln2_g"], prev["ln2_b"]), part=p1)
+            self._gemm_ln(EPI_SWIGLU_FOLD, h1, lw["wupgate_f"], T, ffn, pin=p1, c1=lw["ug_c1"], c2=lw["ug_c2"])
+            self._gemm_ln(EPI_RES_LN_STATS, ffn, lw["wdown"], T, h2, res=h1, pin=p1, ln=(lw["ln1_g"], lw["ln1_b"]),
+                          part=p2)
+            prev = lw
+        _chk(L.nomic_layernorm(h2.data_ptr(), T, prev["ln2_g"].data_ptr(), prev["ln2_b"].data_ptr(), cfg.eps,
+                               x.data_ptr(), s), "ln_final")
+        return x[:T]
+
+    def _hidden_unfused(self, b: Batch) -> torch.Tensor:
+        """Reference schedule: a LayerNorm kernel after each residual GEMM (NOMIC_LN_FOLD=0)."""
         cfg, L, w = self.cfg, self.L, self.w
         assert b.max_len <= self.rope.shape[0]
         self._ensure(b.T_pad)

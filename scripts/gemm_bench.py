@@ -47,7 +47,7 @@ def main():
                           None if rope is None else rope.data_ptr(), None if pos is None else pos.data_ptr(),
                           1536, _stream()), name)
 
-    VARS = (512, 513, 256, 128)
+    VARS = (514, 512, 513, 256, 128)
     times = {(n, v): [] for n, *_ in shapes for v in VARS}
     for r in range(a.rounds):
         for name, *_ in shapes:

@@ -51,6 +51,32 @@ def test_gemm_store_and_residual(L, M, N, K):
     assert _rel(outf[:M], ref) < 1e-5
 
 
+@pytest.mark.parametrize("M,N,K", [(4096, 2048, 768), (12288, 2048, 1536), (32700, 768, 768), (32768, 768, 3072),
+                                   (32768, 2304, 768)])
+def test_gemm_stream_k_split_tiles(L0, M, N, K):
+    """Stream-K persistent kernel (variant 514): the leftover 256^2 tiles are cut into K-ranges on
+    several blocks and summed through the hand-off slots; q = 0 (only split tiles), q >= 1, a row
+    tail (M % 256 != 0) and the encoder's N = 768 / 2304 shapes, against fp32."""
+    import torch
+    from libsplinter_amd.models.nomic import _chk, _stream
+    torch.manual_seed(7)
+    prev = L0.nomic_gemm_set_variant(514)
+    try:
+        Mp = (M + 255) // 256 * 256
+        A = (torch.rand(Mp, K, device="cuda") * 2 - 1).bfloat16()
+        W = ((torch.rand(N, K, device="cuda") * 2 - 1) * 0.05).bfloat16()
+        R = torch.randn(Mp, N, device="cuda").bfloat16()
+        ref = A[:M].float() @ W.float().T + R[:M].float()
+        for _ in range(3):  # repeated launches: the hand-off flags are per-launch generations
+            out = torch.zeros(Mp, N, device="cuda", dtype=torch.bfloat16)
+            _chk(L0.nomic_gemm(1, A.data_ptr(), K, W.data_ptr(), K, M, N, K, out.data_ptr(), N, R.data_ptr(), N, None,
+                               None, 0, _stream()), "gemm")
+            assert _rel(out[:M].float(), ref) < 5e-3
+            assert (out[M:] == 0).all()
+    finally:
+        L0.nomic_gemm_set_variant(prev)
+
+
 def test_gemm_asymmetric_identity(L):
     """A = I with an asymmetric W catches a transposed C write (guide §3)."""
     import torch
@@ -99,6 +125,88 @@ def test_gemm_swiglu_and_rope(L):
     k = ref_m.rope(raw[:, K:2 * K].reshape(M, 12, 64), pos[:M].long()).reshape(M, K)
     ref = torch.cat([q, k, raw[:, 2 * K:]], 1)
     assert _rel(qkv[:M].float(), ref) < 1e-2
+
+
+def test_gemm_layernorm_fold_modes(L):
+    """Post-LN folded into the GEMMs (nomic_api.h modes 5-8) vs fp32 torch: residual sums with
+    128-column partial statistics -> (mean, rstd) per row; the residual normalised on the fly;
+    SwiGLU and RoPE projections of LN(h) computed from raw h against LN-folded weights."""
+    import torch
+    from libsplinter_amd.models.nomic import (NomicConfig, NomicReference, _chk, _stream, fold_ln, pack_qkv,
+                                              pack_upgate)
+    F_ = torch.nn.functional
+    torch.manual_seed(3)
+    M, K, F, eps = 300, 768, 3072, 1e-12
+    Mp = 384
+    nul = None
+
+    def gemm_ln(mode, A, W, out, res=None, pos=None, tab=None, pin=None, c1=None, c2=None, g=None, b=None,
+                part=None):
+        p = lambda t: t.data_ptr() if t is not None else nul  # noqa: E731
+        _chk(L.nomic_gemm_ln(mode, A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0), M, W.shape[0], W.shape[1],
+                             out.data_ptr(), out.stride(0), p(res), res.stride(0) if res is not None else 0, p(tab),
+                             p(pos), 2 * K, p(pin), K // 128 if pin is not None else 0, eps, p(c1), p(c2), p(g), p(b),
+                             p(part), _stream()), f"mode {mode}")
+
+    def partials(t):  # (mean, M2) per 128 columns, as a stats-mode producer writes them
+        v = t.float().reshape(t.shape[0], -1, 128)
+        mu = v.mean(2)
+        return torch.stack([mu, ((v - mu[..., None]) ** 2).sum(2)], 2).reshape(t.shape[0], -1).contiguous()
+
+    # raw residual stream with a per-row offset (the fold must cancel the mean exactly)
+    h = (torch.randn(Mp, K, device="cuda") * 1.5 + torch.randn(Mp, 1, device="cuda") * 2).bfloat16()
+    g = (1 + 0.3 * torch.randn(K, device="cuda")).bfloat16()
+    bb = (0.1 * torch.randn(K, device="cuda")).bfloat16()
+    hf = h[:M].float()
+    xln = F_.layer_norm(hf, (K,), g.float(), bb.float(), eps)
+    ph = partials(h)
+
+    # 7: out = A W^T + R, partial stats -> row_stats
+    A = torch.randn(Mp, K, device="cuda").bfloat16()
+    W = (torch.randn(K, K, device="cuda") * 0.03).bfloat16()
+    out = torch.zeros(Mp, K, device="cuda", dtype=torch.bfloat16)
+    part = torch.zeros(Mp, 2 * (K // 128), device="cuda")
+    gemm_ln(7, A, W, out, res=h, part=part)
+    ref = A[:M].float() @ W.float().T + hf
+    assert _rel(out[:M].float(), ref) < 5e-3
+    assert (out[M:] == 0).all()
+    st_got = torch.zeros(Mp, 2, device="cuda")
+    _chk(L.nomic_row_stats(part.data_ptr(), K // 128, M, eps, st_got.data_ptr(), _stream()), "row_stats")
+    o = out[:M].float()
+    torch.testing.assert_close(st_got[:M, 0], o.mean(1), rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(st_got[:M, 1], torch.rsqrt(o.var(1, unbiased=False) + eps), rtol=1e-3, atol=1e-4)
+
+    # 8: out = A W^T + LN(h) with h's statistics
+    gemm_ln(8, A, W, out, res=h, pin=ph, g=g, b=bb, part=part)
+    assert _rel(out[:M].float(), A[:M].float() @ W.float().T + xln) < 5e-3
+
+    # 6: SwiGLU of LN(h) from raw h and folded weights
+    up = (torch.randn(F, K, device="cuda") * 0.03).bfloat16()
+    gate = (torch.randn(F, K, device="cuda") * 0.03).bfloat16()
+    wf, c1, c2 = fold_ln(pack_upgate(up, gate), g, bb)
+    ffn = torch.empty(Mp, F, device="cuda", dtype=torch.bfloat16)
+    gemm_ln(6, h, wf, ffn, pin=ph, c1=c1, c2=c2)
+    ref = (xln @ up.float().T) * F_.silu(xln @ gate.float().T)
+    assert _rel(ffn[:M].float(), ref) < 1.5e-2
+
+    # 5: RoPE'd qkv of LN(h)
+    cfg = NomicConfig()
+    wqkv = (torch.randn(3 * K, K, device="cuda") * 0.03).bfloat16()
+    pos = torch.randint(0, 2000, (Mp,), device="cuda", dtype=torch.int32)
+    inv = cfg.rope_base ** (-np.arange(0, 64, 2) / 64)
+    ang = np.arange(8192)[:, None] * inv[None, :]
+    tab = torch.from_numpy(np.stack([np.cos(ang), np.sin(ang)], -1).astype(np.float32).reshape(8192, -1)).cuda()
+    wf, c1, c2 = fold_ln(pack_qkv(wqkv), g, bb)
+    qkv = torch.empty(Mp, 3 * K, device="cuda", dtype=torch.bfloat16)
+    gemm_ln(5, h, wf, qkv, pos=pos, tab=tab, pin=ph, c1=c1, c2=c2)
+    raw = xln @ wqkv.float().T
+    rm = NomicReference(cfg, {}, "cuda")
+    q = rm.rope(raw[:, :K].reshape(M, 12, 64), pos[:M].long()).reshape(M, K)
+    k = rm.rope(raw[:, K:2 * K].reshape(M, 12, 64), pos[:M].long()).reshape(M, K)
+    assert _rel(qkv[:M].float(), torch.cat([q, k, raw[:, 2 * K:]], 1)) < 1.5e-2
+    # a fold mode without its operands is refused, never launched
+    assert L.nomic_gemm_ln(6, h.data_ptr(), K, wf.data_ptr(), K, M, 3 * K, K, qkv.data_ptr(), 3 * K, None, 0, None,
+                           None, 0, None, 0, eps, None, None, None, None, None, _stream()) != 0
 
 
 @pytest.mark.parametrize("variant", [6, 5, 4, 3, 2, 1])
@@ -155,13 +263,15 @@ def test_layernorm_and_embed(L0):
     assert _rel(out.float(), ref) < 5e-3
 
 
-def test_encoder_matches_fp32_reference():
+@pytest.mark.parametrize("ln_fold", [True, False], ids=["ln_folded", "ln_kernels"])
+def test_encoder_matches_fp32_reference(ln_fold):
     import torch
     from libsplinter_amd.models.nomic import (Batch, NomicConfig, NomicEncoder, NomicReference, NomicWeights,
                                               random_weights)
     cfg = NomicConfig(layers=3)
     w = random_weights(cfg, seed=5)
     enc = NomicEncoder(NomicWeights.from_numpy(cfg, w), max_tokens=4096)
+    enc.ln_fold = ln_fold
     rng = np.random.default_rng(0)
     seqs = [rng.integers(0, cfg.vocab, size=n).tolist() for n in (5, 40, 129, 300)]
     b = Batch(seqs)

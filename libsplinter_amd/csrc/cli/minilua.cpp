@@ -10,6 +10,9 @@
 #include <cstring>
 #include <ctime>
 #include <random>
+#include <condition_variable>
+#include <mutex>
+#include <thread>
 #include <unordered_set>
 
 namespace mlua {
@@ -36,6 +39,7 @@ size_t ValueHash::operator()(const Value& v) const {
     case Value::Str: return std::hash<std::string>()(*v.s);
     case Value::Tab: return std::hash<const void*>()(v.tab.get());
     case Value::Fn: return std::hash<const void*>()(v.fn.get());
+    case Value::Co: return std::hash<const void*>()(v.co.get());
   }
   return 0;
 }
@@ -52,6 +56,7 @@ static bool raw_equal(const Value& a, const Value& b) {
     case Value::Str: return *a.s == *b.s;
     case Value::Tab: return a.tab == b.tab;
     case Value::Fn: return a.fn == b.fn;
+    case Value::Co: return a.co == b.co;
     default: return false;
   }
 }
@@ -107,6 +112,7 @@ std::string tostring(const Value& v) {
     case Value::Str: return *v.s;
     case Value::Tab: snprintf(b, sizeof b, "table: %p", (void*)v.tab.get()); return b;
     case Value::Fn: snprintf(b, sizeof b, "function: %p", (void*)v.fn.get()); return b;
+    case Value::Co: snprintf(b, sizeof b, "thread: %p", (void*)v.co.get()); return b;
   }
   return "?";
 }
@@ -120,6 +126,7 @@ static const char* type_name(const Value& v) {
     case Value::Str: return "string";
     case Value::Tab: return "table";
     case Value::Fn: return "function";
+    case Value::Co: return "thread";
   }
   return "?";
 }
@@ -843,13 +850,20 @@ struct Exec {
   }
 
   Value index(const Value& o, const Value& k, const Expr* e) {
-    if (o.t == Value::Tab) return o.tab->get(k);
-    if (o.t == Value::Str) {
-      Value strlib = I.globals->get(Value::string("string"));
-      if (strlib.t == Value::Tab) return strlib.tab->get(k);
-    }
-    rt(e, std::string("attempt to index a ") + type_name(o) + " value" +
-              (e && e->a && e->a->k == E_NAME ? " (variable '" + e->a->name + "')" : ""));
+    if (o.t != Value::Tab && o.t != Value::Str)
+      rt(e, std::string("attempt to index a ") + type_name(o) + " value" +
+                (e && e->a && e->a->k == E_NAME ? " (variable '" + e->a->name + "')" : ""));
+    return I.index(o, k);
+  }
+
+  // binary metamethod (__add, __concat, __lt, ...): the left operand's, else the right one's
+  bool meta_bin(const char* ev, const Value& a, const Value& b, Value* out) {
+    Value h = I.metamethod(a, ev);
+    if (h.t == Value::Nil) h = I.metamethod(b, ev);
+    if (h.t == Value::Nil) return false;
+    Values r = I.call(h, {a, b});
+    *out = r.empty() ? Value() : r[0];
+    return true;
   }
 
   Values eval_multi(const ExprP& e, Scope* s) {
@@ -881,11 +895,12 @@ struct Exec {
     if (e->k == E_METHOD) {
       Value obj = eval(e->a, s);
       f = index(obj, Value::string(e->name), e);
-      if (f.t != Value::Fn) rt(e, "attempt to call a " + std::string(type_name(f)) + " value (method '" + e->name + "')");
+      if (f.t != Value::Fn && I.metamethod(f, "__call").t == Value::Nil)
+        rt(e, "attempt to call a " + std::string(type_name(f)) + " value (method '" + e->name + "')");
       args.push_back(obj);
     } else {
       f = eval(e->a, s);
-      if (f.t != Value::Fn) {
+      if (f.t != Value::Fn && I.metamethod(f, "__call").t == Value::Nil) {
         std::string what = e->a->k == E_NAME ? " (global '" + e->a->name + "')" : "";
         rt(e, std::string("attempt to call a ") + type_name(f) + " value" + what);
       }
@@ -981,24 +996,66 @@ struct Exec {
       }
       case E_UN: {
         Value a = eval(e->a, s);
+        Value mr;
         switch (e->op) {
           case T_NOT + 256: return Value::boolean(!a.truthy());
           case '-': {
             Value n;
-            if (!tonum(a, &n)) rt(e.get(), std::string("attempt to perform arithmetic on a ") + type_name(a) + " value");
+            if (!tonum(a, &n)) {
+              if (meta_bin("__unm", a, a, &mr)) return mr;
+              rt(e.get(), std::string("attempt to perform arithmetic on a ") + type_name(a) + " value");
+            }
             return n.t == Value::Int ? Value::integer((int64_t)(0 - (uint64_t)n.i)) : Value::number(-n.n);
           }
           case '#':
             if (a.t == Value::Str) return Value::integer((int64_t)a.s->size());
+            if (meta_bin("__len", a, a, &mr)) return mr;
             if (a.t == Value::Tab) return Value::integer(a.tab->length());
             rt(e.get(), std::string("attempt to get length of a ") + type_name(a) + " value");
-          case '~': return Value::integer(~toint_strict(a, "bitwise not"));
+          case '~':
+            if (a.t == Value::Tab && meta_bin("__bnot", a, a, &mr)) return mr;
+            return Value::integer(~toint_strict(a, "bitwise not"));
         }
         rt(e.get(), "bad unary operator");
       }
       case E_BIN: {
         Value a = eval(e->a, s), b = eval(e->b, s);
         const int op = e->op;
+        if (a.t == Value::Tab || b.t == Value::Tab) {  // metamethods (tables only carry metatables)
+          const char* ev = nullptr;
+          bool swap = false, negate = false;
+          switch (op) {
+            case '+': ev = "__add"; break;
+            case '-': ev = "__sub"; break;
+            case '*': ev = "__mul"; break;
+            case '/': ev = "__div"; break;
+            case '%': ev = "__mod"; break;
+            case '^': ev = "__pow"; break;
+            case T_IDIV + 256: ev = "__idiv"; break;
+            case '&': ev = "__band"; break;
+            case '|': ev = "__bor"; break;
+            case '~': ev = "__bxor"; break;
+            case T_SHL + 256: ev = "__shl"; break;
+            case T_SHR + 256: ev = "__shr"; break;
+            case T_CONCAT + 256: ev = "__concat"; break;
+            case '<': ev = "__lt"; break;
+            case T_LE + 256: ev = "__le"; break;
+            case '>': ev = "__lt"; swap = true; break;
+            case T_GE + 256: ev = "__le"; swap = true; break;
+            case T_EQ + 256:
+            case T_NE + 256:
+              if (a.t == Value::Tab && b.t == Value::Tab && !raw_equal(a, b)) ev = "__eq";
+              negate = op == T_NE + 256;
+              break;
+          }
+          Value mr;
+          if (ev && meta_bin(ev, swap ? b : a, swap ? a : b, &mr)) {
+            const bool cmp = op == '<' || op == '>' || op == T_LE + 256 || op == T_GE + 256 || op == T_EQ + 256 ||
+                             op == T_NE + 256;
+            if (!cmp) return mr;
+            return Value::boolean(negate ? !mr.truthy() : mr.truthy());
+          }
+        }
         switch (op) {
           case '+': case '-': case '*': case '/': case '%': case '^': case T_IDIV + 256:
             return arith(op == T_IDIV + 256 ? 'i' : op, a, b, e.get(), *this);
@@ -1068,8 +1125,9 @@ struct Exec {
       else I.globals->set(Value::string(t->name), v);
     } else {
       Value o = eval(t->a, s);
-      if (o.t != Value::Tab) rt(t.get(), std::string("attempt to index a ") + type_name(o) + " value");
-      o.tab->set(eval(t->b, s), v);
+      if (o.t != Value::Tab && I.metamethod(o, "__newindex").t == Value::Nil)
+        rt(t.get(), std::string("attempt to index a ") + type_name(o) + " value");
+      I.setindex(o, eval(t->b, s), v);
     }
   }
 
@@ -1208,8 +1266,84 @@ struct Exec {
   }
 };
 
-Values Interp::call(const Value& f, Values args) {
-  if (f.t != Value::Fn) throw LuaError(std::string("attempt to call a ") + type_name(f) + " value");
+Value Interp::metamethod(const Value& v, const char* event) const {
+  if (v.t == Value::Tab && v.tab->meta) return v.tab->meta->get(Value::string(event));
+  if (v.t == Value::Str && string_meta) return string_meta->get(Value::string(event));
+  return Value();
+}
+
+Value Interp::index(const Value& o0, const Value& k) {
+  Value o = o0;
+  for (int hop = 0; hop < 100; ++hop) {
+    Value h;
+    if (o.t == Value::Tab) {
+      Value v = o.tab->get(k);
+      if (v.t != Value::Nil) return v;
+      h = metamethod(o, "__index");
+      if (h.t == Value::Nil) return Value();
+    } else if (o.t == Value::Str) {
+      Value strlib = globals->get(Value::string("string"));
+      return strlib.t == Value::Tab ? strlib.tab->get(k) : Value();
+    } else {
+      h = metamethod(o, "__index");
+      if (h.t == Value::Nil) throw LuaError(std::string("attempt to index a ") + type_name(o) + " value");
+    }
+    if (h.t == Value::Fn) {
+      Values r = call(h, {o, k});
+      return r.empty() ? Value() : r[0];
+    }
+    o = h;
+  }
+  throw LuaError("'__index' chain too long; possible loop");
+}
+
+void Interp::setindex(const Value& o0, const Value& k, const Value& v) {
+  Value o = o0;
+  for (int hop = 0; hop < 100; ++hop) {
+    Value h;
+    if (o.t == Value::Tab) {
+      if (o.tab->get(k).t != Value::Nil || (h = metamethod(o, "__newindex")).t == Value::Nil) {
+        o.tab->set(k, v);
+        return;
+      }
+    } else {
+      h = metamethod(o, "__newindex");
+      if (h.t == Value::Nil) throw LuaError(std::string("attempt to index a ") + type_name(o) + " value");
+    }
+    if (h.t == Value::Fn) {
+      call(h, {o, k, v});
+      return;
+    }
+    o = h;
+  }
+  throw LuaError("'__newindex' chain too long; possible loop");
+}
+
+std::string Interp::tostr(const Value& v) {
+  Value h = v.t == Value::Tab ? metamethod(v, "__tostring") : Value();
+  if (h.t != Value::Nil) {
+    Values r = call(h, {v});
+    if (r.empty() || r[0].t != Value::Str) throw LuaError("'__tostring' must return a string");
+    return *r[0].s;
+  }
+  if (v.t == Value::Tab) {
+    Value nm = metamethod(v, "__name");
+    if (nm.t == Value::Str) {
+      std::string t = tostring(v);
+      return *nm.s + t.substr(t.find(':'));
+    }
+  }
+  return tostring(v);
+}
+
+Values Interp::call(const Value& f0, Values args) {
+  Value f = f0;
+  if (f.t != Value::Fn) {
+    Value h = metamethod(f, "__call");
+    if (h.t != Value::Fn) throw LuaError(std::string("attempt to call a ") + type_name(f) + " value");
+    args.insert(args.begin(), f);
+    f = h;
+  }
   if (++depth > 200) { --depth; throw LuaError("stack overflow"); }
   struct Guard { int& d; ~Guard() { --d; } } g{depth};
   if (f.fn->native) return f.fn->native(*this, args);
@@ -1245,6 +1379,417 @@ static double check_num(Values& a, size_t i, const char* fn) {
   if (!tonum(arg_at(a, i), &n))
     throw LuaError(std::string("bad argument #") + std::to_string(i + 1) + " to '" + fn + "' (number expected)");
   return n.as_double();
+}
+
+// ------------------------------------------------------------ patterns ----
+// Lua 5.4 pattern matching (string.find / match / gmatch / gsub): single-character classes
+// (. %a %c %d %g %l %p %s %u %w %x and their upper-case complements, %<punct> escapes, [sets]
+// with ranges, classes and ^), quantifiers * + - ?, anchors ^ and $, captures ( ) and position
+// captures (), back-references %1-%9, %bxy and the frontier %f[set].  A backtracking matcher over
+// indices into the subject; recursion is bounded (kMaxDepth) so a pathological pattern fails
+// with an error instead of exhausting the C stack.
+namespace pat {
+
+constexpr int kMaxCaptures = 32;
+constexpr int kMaxDepth = 200;
+constexpr long kOpen = -1;      // capture started, not closed
+constexpr long kPosition = -2;  // () position capture
+constexpr size_t kFail = std::string::npos;
+
+struct Matcher {
+  const std::string& src;
+  const std::string& p;
+  int level = 0;
+  int depth = 0;
+  size_t cap_start[kMaxCaptures];
+  long cap_len[kMaxCaptures];
+
+  Matcher(const std::string& s, const std::string& pattern) : src(s), p(pattern) {}
+
+  static bool class_match(unsigned char c, unsigned char cl) {
+    bool r;
+    switch (tolower(cl)) {
+      case 'a': r = isalpha(c); break;
+      case 'c': r = iscntrl(c); break;
+      case 'd': r = isdigit(c); break;
+      case 'g': r = isgraph(c); break;
+      case 'l': r = islower(c); break;
+      case 'p': r = ispunct(c); break;
+      case 's': r = isspace(c); break;
+      case 'u': r = isupper(c); break;
+      case 'w': r = isalnum(c); break;
+      case 'x': r = isxdigit(c); break;
+      default: return cl == c;  // escaped literal (%. %% %[ ...)
+    }
+    return isupper(cl) ? !r : r;
+  }
+
+  // index just past the single-character class starting at pi
+  size_t class_end(size_t pi) const {
+    const size_t n = p.size();
+    const char c = p[pi++];
+    if (c == '%') {
+      if (pi >= n) throw LuaError("malformed pattern (ends with '%')");
+      return pi + 1;
+    }
+    if (c == '[') {
+      if (pi < n && p[pi] == '^') ++pi;
+      const size_t first = pi;
+      for (;;) {  // a ']' right after '[' or '[^' is a literal member
+        if (pi >= n) throw LuaError("malformed pattern (missing ']')");
+        if (p[pi] == ']' && pi != first) return pi + 1;
+        if (p[pi] == '%') {
+          if (pi + 1 >= n) throw LuaError("malformed pattern (missing ']')");
+          pi += 2;
+        } else {
+          ++pi;
+        }
+      }
+    }
+    return pi;
+  }
+
+  // [set] at p[open] .. p[close] (close = index of the ']')
+  bool set_match(unsigned char c, size_t open, size_t close) const {
+    size_t i = open + 1;
+    bool neg = false;
+    if (p[i] == '^') {
+      neg = true;
+      ++i;
+    }
+    while (i < close) {  // class_end put close past a leading literal ']'
+      if (p[i] == '%' && i + 1 < close) {
+        if (class_match(c, (unsigned char)p[i + 1])) return !neg;
+        i += 2;
+      } else if (i + 2 < close && p[i + 1] == '-') {
+        if ((unsigned char)p[i] <= c && c <= (unsigned char)p[i + 2]) return !neg;
+        i += 3;
+      } else {
+        if ((unsigned char)p[i] == c) return !neg;
+        ++i;
+      }
+    }
+    return neg;
+  }
+
+  bool single(size_t s, size_t pi, size_t ep) const {
+    if (s >= src.size()) return false;
+    const unsigned char c = (unsigned char)src[s];
+    switch (p[pi]) {
+      case '.': return true;
+      case '%': return class_match(c, (unsigned char)p[pi + 1]);
+      case '[': return set_match(c, pi, ep - 1);
+      default: return (unsigned char)p[pi] == c;
+    }
+  }
+
+  size_t max_expand(size_t s, size_t pi, size_t ep) {
+    size_t i = 0;
+    while (single(s + i, pi, ep)) ++i;
+    for (;;) {  // longest first, then give back one at a time
+      const size_t r = match(s + i, ep + 1);
+      if (r != kFail) return r;
+      if (i == 0) return kFail;
+      --i;
+    }
+  }
+
+  size_t min_expand(size_t s, size_t pi, size_t ep) {
+    for (;;) {
+      const size_t r = match(s, ep + 1);
+      if (r != kFail) return r;
+      if (!single(s, pi, ep)) return kFail;
+      ++s;
+    }
+  }
+
+  size_t start_capture(size_t s, size_t pi, long what) {
+    if (level >= kMaxCaptures) throw LuaError("too many captures");
+    cap_start[level] = s;
+    cap_len[level] = what;
+    ++level;
+    const size_t r = match(s, pi);
+    if (r == kFail) --level;
+    return r;
+  }
+
+  size_t end_capture(size_t s, size_t pi) {
+    int l = -1;
+    for (int i = level - 1; i >= 0; --i)
+      if (cap_len[i] == kOpen) {
+        l = i;
+        break;
+      }
+    if (l < 0) throw LuaError("invalid pattern capture");
+    cap_len[l] = (long)(s - cap_start[l]);
+    const size_t r = match(s, pi);
+    if (r == kFail) cap_len[l] = kOpen;
+    return r;
+  }
+
+  size_t back_reference(size_t s, char d) const {
+    const int l = d - '1';
+    if (l < 0 || l >= level || cap_len[l] == kOpen) throw LuaError(std::string("invalid capture index %") + d);
+    const size_t len = cap_len[l] == kPosition ? 0 : (size_t)cap_len[l];
+    if (src.size() - s >= len && src.compare(cap_start[l], len, src, s, len) == 0) return s + len;
+    return kFail;
+  }
+
+  size_t balance(size_t s, size_t pi) const {
+    if (pi + 1 >= p.size()) throw LuaError("malformed pattern (missing arguments to '%b')");
+    if (s >= src.size() || src[s] != p[pi]) return kFail;
+    const char open = p[pi], close = p[pi + 1];
+    int depth_ = 1;
+    for (size_t i = s + 1; i < src.size(); ++i) {
+      if (src[i] == close) {
+        if (--depth_ == 0) return i + 1;
+      } else if (src[i] == open) {
+        ++depth_;
+      }
+    }
+    return kFail;
+  }
+
+  // end of the match of p[pi..] at src[s..], or kFail
+  size_t match(size_t s, size_t pi) {
+    if (++depth > kMaxDepth) throw LuaError("pattern too complex");
+    struct Guard {
+      int& d;
+      ~Guard() { --d; }
+    } guard{depth};
+    const size_t n = p.size();
+    for (;;) {
+      if (pi == n) return s;
+      const char pc = p[pi];
+      if (pc == '(') {
+        if (pi + 1 < n && p[pi + 1] == ')') return start_capture(s, pi + 2, kPosition);
+        return start_capture(s, pi + 1, kOpen);
+      }
+      if (pc == ')') return end_capture(s, pi + 1);
+      if (pc == '$' && pi + 1 == n) return s == src.size() ? s : kFail;
+      if (pc == '%' && pi + 1 < n) {
+        const char nx = p[pi + 1];
+        if (nx == 'b') {
+          s = balance(s, pi + 2);
+          if (s == kFail) return kFail;
+          pi += 4;
+          continue;
+        }
+        if (nx == 'f') {
+          pi += 2;
+          if (pi >= n || p[pi] != '[') throw LuaError("missing '[' after '%f' in pattern");
+          const size_t ep = class_end(pi);
+          const unsigned char prev = s == 0 ? 0 : (unsigned char)src[s - 1];
+          const unsigned char cur = s < src.size() ? (unsigned char)src[s] : 0;
+          if (set_match(prev, pi, ep - 1) || !set_match(cur, pi, ep - 1)) return kFail;
+          pi = ep;
+          continue;
+        }
+        if (isdigit((unsigned char)nx)) {
+          s = back_reference(s, nx);
+          if (s == kFail) return kFail;
+          pi += 2;
+          continue;
+        }
+      }
+      const size_t ep = class_end(pi);
+      const char q = ep < n ? p[ep] : 0;
+      if (q == '?') {
+        if (single(s, pi, ep)) {
+          const size_t r = match(s + 1, ep + 1);
+          if (r != kFail) return r;
+        }
+        pi = ep + 1;
+        continue;
+      }
+      if (q == '+') return single(s, pi, ep) ? max_expand(s + 1, pi, ep) : kFail;
+      if (q == '*') return max_expand(s, pi, ep);
+      if (q == '-') return min_expand(s, pi, ep);
+      if (!single(s, pi, ep)) return kFail;
+      ++s;
+      pi = ep;
+    }
+  }
+
+  Value capture(int i, size_t s, size_t e) const {
+    if (i >= level) {
+      if (i == 0) return Value::string(src.substr(s, e - s));  // no captures: the whole match
+      throw LuaError("invalid capture index %" + std::to_string(i + 1));
+    }
+    if (cap_len[i] == kOpen) throw LuaError("unfinished capture");
+    if (cap_len[i] == kPosition) return Value::integer((int64_t)cap_start[i] + 1);
+    return Value::string(src.substr(cap_start[i], (size_t)cap_len[i]));
+  }
+
+  Values captures(size_t s, size_t e, bool whole_if_none) const {
+    Values r;
+    const int nc = (level == 0 && whole_if_none) ? 1 : level;
+    for (int i = 0; i < nc; ++i) r.push_back(capture(i, s, e));
+    return r;
+  }
+
+  // try at every start position from `init` (0-based); returns the start or kFail, *end = match end
+  size_t search(size_t init, size_t* end) {
+    const bool anchor = !p.empty() && p[0] == '^';
+    const size_t p0 = anchor ? 1 : 0;
+    for (size_t s = init;; ++s) {
+      level = 0;
+      depth = 0;
+      const size_t e = match(s, p0);
+      if (e != kFail) {
+        *end = e;
+        return s;
+      }
+      if (anchor || s >= src.size()) return kFail;
+    }
+  }
+};
+
+static bool has_specials(const std::string& p) { return p.find_first_of("^$*+?.([%-") != std::string::npos; }
+
+// string.find / string.match
+static Values find_aux(Values& a, bool find, const char* fn) {
+  const std::string s = check_str(a, 0, fn), pt = check_str(a, 1, fn);
+  int64_t init = a.size() > 2 && a[2].t != Value::Nil ? check_int(a, 2, fn) : 1;
+  const int64_t len = (int64_t)s.size();
+  if (init < 0) init = len + init + 1;
+  if (init < 1) init = 1;
+  if (init > len + 1) return Values{Value()};
+  const bool plain = a.size() > 3 && a[3].truthy();
+  if (find && (plain || !has_specials(pt))) {
+    const size_t pos = s.find(pt, (size_t)init - 1);
+    if (pos == std::string::npos) return Values{Value()};
+    return Values{Value::integer((int64_t)pos + 1), Value::integer((int64_t)(pos + pt.size()))};
+  }
+  Matcher m(s, pt);
+  size_t e = 0;
+  const size_t st = m.search((size_t)init - 1, &e);
+  if (st == kFail) return Values{Value()};
+  if (!find) return m.captures(st, e, true);
+  Values r{Value::integer((int64_t)st + 1), Value::integer((int64_t)e)};
+  Values c = m.captures(st, e, false);
+  r.insert(r.end(), c.begin(), c.end());
+  return r;
+}
+
+}  // namespace pat
+
+// ------------------------------------------------------------ coroutines --
+// Each coroutine runs its function on a thread of its own; resume and yield hand a single
+// "turn" back and forth under a mutex, so exactly one thread runs Lua code at any time and the
+// tree-walking evaluator needs no changes: a yield inside nested Lua calls, pcall, metamethods
+// or a native callback simply blocks that thread's C++ stack until the next resume.  A
+// suspended coroutine that is collected or closed is unwound with CoKill (not a LuaError, so
+// pcall inside it cannot catch it) and joined.
+struct CoKill {};
+
+struct Coroutine : std::enable_shared_from_this<Coroutine> {
+  enum Status { Suspended, Running, Normal, Dead };
+  Value fn;
+  Status st = Suspended;
+  Interp* I = nullptr;
+  Heap* heap = nullptr;
+  std::thread th;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool co_turn = false;  // true: the coroutine's thread runs; false: its resumer runs
+  bool killed = false;
+  bool failed = false;
+  int depth = 0;         // interpreter call depth of the coroutine's own stack
+  Values transfer;       // resume arguments in, yield / return values out
+
+  ~Coroutine() { kill(); }
+
+  void kill() {
+    if (!th.joinable()) return;
+    {
+      std::unique_lock<std::mutex> l(mu);
+      if (st != Dead) {
+        killed = true;
+        co_turn = true;
+        cv.notify_all();
+        cv.wait(l, [&] { return !co_turn; });
+      }
+    }
+    th.join();
+    st = Dead;
+  }
+};
+
+static thread_local Coroutine* t_co = nullptr;  // the coroutine this thread runs (null: main)
+
+static void co_body(Coroutine* c) {
+  t_heap = c->heap;
+  t_co = c;
+  {
+    std::unique_lock<std::mutex> l(c->mu);
+    c->cv.wait(l, [&] { return c->co_turn; });
+  }
+  Values out;
+  bool failed = false;
+  if (!c->killed) {
+    try {
+      Values args = std::move(c->transfer);
+      out = c->I->call(c->fn, std::move(args));
+    } catch (LuaError& e) {
+      failed = true;
+      out = Values{e.value};
+    } catch (CoKill&) {
+    } catch (std::exception& e) {
+      failed = true;
+      out = Values{Value::string(e.what())};
+    }
+  }
+  std::lock_guard<std::mutex> l(c->mu);
+  c->transfer = std::move(out);
+  c->failed = failed;
+  c->st = Coroutine::Dead;
+  c->co_turn = false;
+  c->cv.notify_all();
+}
+
+static Values co_resume(Interp& I, const std::shared_ptr<Coroutine>& c, Values args) {
+  if (c->st == Coroutine::Dead) return Values{Value::boolean(false), Value::string("cannot resume dead coroutine")};
+  if (c->st != Coroutine::Suspended)
+    return Values{Value::boolean(false), Value::string("cannot resume non-suspended coroutine")};
+  Coroutine* prev = t_co;
+  if (prev) prev->st = Coroutine::Normal;
+  const int saved_depth = I.depth;
+  I.depth = c->depth;
+  {
+    std::unique_lock<std::mutex> l(c->mu);
+    c->transfer = std::move(args);
+    c->st = Coroutine::Running;
+    if (!c->th.joinable()) c->th = std::thread(co_body, c.get());
+    c->co_turn = true;
+    c->cv.notify_all();
+    c->cv.wait(l, [&] { return !c->co_turn; });
+  }
+  c->depth = I.depth;
+  I.depth = saved_depth;
+  if (prev) prev->st = Coroutine::Running;
+  Values r = std::move(c->transfer);
+  c->transfer.clear();
+  if (c->failed) {
+    c->failed = false;
+    r.insert(r.begin(), Value::boolean(false));
+    return r;
+  }
+  r.insert(r.begin(), Value::boolean(true));
+  return r;
+}
+
+static Values co_yield(Values vals) {
+  Coroutine* c = t_co;
+  if (!c) throw LuaError("attempt to yield from outside a coroutine");
+  std::unique_lock<std::mutex> l(c->mu);
+  c->transfer = std::move(vals);
+  c->st = Coroutine::Suspended;
+  c->co_turn = false;
+  c->cv.notify_all();
+  c->cv.wait(l, [&] { return c->co_turn; });
+  if (c->killed) throw CoKill{};
+  return std::move(c->transfer);
 }
 
 static std::string lua_format(Values& a) {
@@ -1324,7 +1869,7 @@ Interp::Interp() {
   G->set(Value::string("_VERSION"), Value::string("Lua 5.4 (splinterctl minilua)"));
   reg(G, "print", [](Interp& I, Values& a) {
     std::string line;
-    for (size_t i = 0; i < a.size(); ++i) line += (i ? "\t" : "") + tostring(a[i]);
+    for (size_t i = 0; i < a.size(); ++i) line += (i ? "\t" : "") + I.tostr(a[i]);
     line += '\n';
     I.out(line);
     return Values{};
@@ -1333,7 +1878,23 @@ Interp::Interp() {
     if (a.empty()) throw LuaError("bad argument #1 to 'type' (value expected)");
     return Values{Value::string(type_name(a[0]))};
   });
-  reg(G, "tostring", [](Interp&, Values& a) { return Values{Value::string(tostring(arg_at(a, 0)))}; });
+  reg(G, "tostring", [](Interp& I, Values& a) { return Values{Value::string(I.tostr(arg_at(a, 0)))}; });
+  reg(G, "setmetatable", [](Interp& I, Values& a) {
+    Value t = arg_at(a, 0), m = arg_at(a, 1);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'setmetatable' (table expected)");
+    if (m.t != Value::Nil && m.t != Value::Tab)
+      throw LuaError("bad argument #2 to 'setmetatable' (nil or table expected)");
+    if (I.metamethod(t, "__metatable").t != Value::Nil) throw LuaError("cannot change a protected metatable");
+    t.tab->meta = m.t == Value::Tab ? m.tab : nullptr;
+    return Values{t};
+  });
+  reg(G, "getmetatable", [](Interp& I, Values& a) {
+    Value v = arg_at(a, 0);
+    std::shared_ptr<Table> m = v.t == Value::Tab ? v.tab->meta : v.t == Value::Str ? I.string_meta : nullptr;
+    if (!m) return Values{Value()};
+    Value prot = m->get(Value::string("__metatable"));
+    return Values{prot.t != Value::Nil ? prot : Value::table(m)};
+  });
   reg(G, "tonumber", [](Interp&, Values& a) {
     Value v = arg_at(a, 0), n;
     if (a.size() > 1 && arg_at(a, 1).t != Value::Nil) {
@@ -1378,14 +1939,20 @@ Interp::Interp() {
     return Values{Value()};
   });
   G->set(Value::string("next"), next);
-  reg(G, "pairs", [next](Interp&, Values& a) {
+  reg(G, "pairs", [next](Interp& I, Values& a) {
+    Value h = I.metamethod(arg_at(a, 0), "__pairs");
+    if (h.t != Value::Nil) {
+      Values r = I.call(h, {a[0]});
+      r.resize(3);
+      return r;
+    }
     if (arg_at(a, 0).t != Value::Tab) throw LuaError("bad argument #1 to 'pairs' (table expected)");
     return Values{next, a[0], Value()};
   });
-  auto ipairs_iter = make_native("ipairs_iter", [](Interp&, Values& a) {
+  auto ipairs_iter = make_native("ipairs_iter", [](Interp& I, Values& a) {
     Value t = arg_at(a, 0);
     const int64_t i = arg_at(a, 1).i + 1;
-    Value v = t.tab->get(Value::integer(i));
+    Value v = I.index(t, Value::integer(i));  // honours __index, as lua_geti does
     if (v.t == Value::Nil) return Values{Value()};
     return Values{Value::integer(i), v};
   });
@@ -1446,9 +2013,68 @@ Interp::Interp() {
     return Values{it->second};
   });
 
+  // coroutine
+  auto C = std::make_shared<Table>();
+  G->set(Value::string("coroutine"), Value::table(C));
+  auto check_co = [](Values& a, const char* fn) {
+    Value v = arg_at(a, 0);
+    if (v.t != Value::Co) throw LuaError(std::string("bad argument #1 to '") + fn + "' (coroutine expected)");
+    return v.co;
+  };
+  reg(C, "create", [](Interp& I, Values& a) {
+    Value f = arg_at(a, 0);
+    if (f.t != Value::Fn) throw LuaError("bad argument #1 to 'create' (function expected)");
+    auto c = std::make_shared<Coroutine>();
+    c->fn = f;
+    c->I = &I;
+    c->heap = I.heap;
+    return Values{Value::thread(c)};
+  });
+  reg(C, "resume", [check_co](Interp& I, Values& a) {
+    auto c = check_co(a, "resume");
+    return co_resume(I, c, Values(a.begin() + 1, a.end()));
+  });
+  reg(C, "yield", [](Interp&, Values& a) { return co_yield(a); });
+  reg(C, "status", [check_co](Interp&, Values& a) {
+    static const char* names[] = {"suspended", "running", "normal", "dead"};
+    return Values{Value::string(names[check_co(a, "status")->st])};
+  });
+  reg(C, "running", [](Interp&, Values&) {
+    if (!t_co) return Values{Value(), Value::boolean(true)};  // main: no thread object in minilua
+    return Values{Value::thread(t_co->shared_from_this()), Value::boolean(false)};
+  });
+  reg(C, "isyieldable", [](Interp&, Values&) { return Values{Value::boolean(t_co != nullptr)}; });
+  reg(C, "close", [check_co](Interp&, Values& a) {
+    auto c = check_co(a, "close");
+    if (c->st == Coroutine::Running || c->st == Coroutine::Normal)
+      throw LuaError("cannot close a running coroutine");
+    c->kill();
+    c->st = Coroutine::Dead;
+    return Values{Value::boolean(true)};
+  });
+  reg(C, "wrap", [](Interp& I, Values& a) {
+    Value f = arg_at(a, 0);
+    if (f.t != Value::Fn) throw LuaError("bad argument #1 to 'wrap' (function expected)");
+    auto c = std::make_shared<Coroutine>();
+    c->fn = f;
+    c->I = &I;
+    c->heap = I.heap;
+    return Values{make_native("wrap", [c](Interp& In, Values& args) {
+      Values r = co_resume(In, c, args);
+      if (!r[0].truthy()) {
+        Value e = r.size() > 1 ? r[1] : Value();
+        throw LuaError(e, e.t == Value::Str ? *e.s : tostring(e));
+      }
+      r.erase(r.begin());
+      return r;
+    })};
+  });
+
   // string
   auto S = std::make_shared<Table>();
   G->set(Value::string("string"), Value::table(S));
+  string_meta = std::make_shared<Table>();
+  string_meta->set(Value::string("__index"), Value::table(S));
   reg(S, "format", [](Interp&, Values& a) { return Values{Value::string(lua_format(a))}; });
   reg(S, "len", [](Interp&, Values& a) { return Values{Value::integer((int64_t)check_str(a, 0, "len").size())}; });
   reg(S, "upper", [](Interp&, Values& a) {
@@ -1502,14 +2128,90 @@ Interp::Interp() {
     for (size_t i = 0; i < a.size(); ++i) s += (char)check_int(a, i, "char");
     return Values{Value::string(s)};
   });
-  reg(S, "find", [](Interp&, Values& a) {  // plain find only
-    std::string s = check_str(a, 0, "find"), p = check_str(a, 1, "find");
-    int64_t init = a.size() > 2 ? check_int(a, 2, "find") : 1;
-    if (init < 0) init = (int64_t)s.size() + init + 1;
+  reg(S, "find", [](Interp&, Values& a) { return pat::find_aux(a, true, "find"); });
+  reg(S, "match", [](Interp&, Values& a) { return pat::find_aux(a, false, "match"); });
+  reg(S, "gmatch", [](Interp&, Values& a) {
+    struct State {
+      std::string src, p;
+      size_t pos = 0, last = pat::kFail;
+    };
+    auto st = std::make_shared<State>();
+    st->src = check_str(a, 0, "gmatch");
+    st->p = check_str(a, 1, "gmatch");
+    int64_t init = a.size() > 2 && a[2].t != Value::Nil ? check_int(a, 2, "gmatch") : 1;
+    const int64_t len = (int64_t)st->src.size();
+    if (init < 0) init = len + init + 1;
     if (init < 1) init = 1;
-    size_t pos = s.find(p, (size_t)init - 1);
-    if (pos == std::string::npos) return Values{Value()};
-    return Values{Value::integer((int64_t)pos + 1), Value::integer((int64_t)(pos + p.size()))};
+    st->pos = (size_t)std::min<int64_t>(init - 1, len + 1);
+    return Values{make_native("gmatch_iter", [st](Interp&, Values&) {
+      pat::Matcher m(st->src, st->p);  // '^' is not an anchor in gmatch (Lua 5.4): matched literally
+      for (size_t s = st->pos; s <= st->src.size(); ++s) {
+        m.level = 0;
+        m.depth = 0;
+        const size_t e = m.match(s, 0);
+        if (e != pat::kFail && e != st->last) {
+          st->pos = st->last = e;
+          return m.captures(s, e, true);
+        }
+      }
+      st->pos = st->src.size() + 1;
+      return Values{Value()};
+    })};
+  });
+  reg(S, "gsub", [](Interp& I, Values& a) {
+    const std::string src = check_str(a, 0, "gsub"), p = check_str(a, 1, "gsub");
+    const Value repl = arg_at(a, 2);
+    if (repl.t != Value::Str && !repl.is_num() && repl.t != Value::Tab && repl.t != Value::Fn)
+      throw LuaError(std::string("bad argument #3 to 'gsub' (string/function/table expected, got ") +
+                     type_name(repl) + ")");
+    const int64_t max_n = a.size() > 3 && a[3].t != Value::Nil ? check_int(a, 3, "gsub") : INT64_MAX;
+    const std::string rs = repl.t == Value::Str || repl.is_num() ? check_str(a, 2, "gsub") : "";
+    const bool anchor = !p.empty() && p[0] == '^';
+    pat::Matcher m(src, p);
+    std::string out;
+    size_t s = 0, last = pat::kFail;
+    int64_t n = 0;
+    while (n < max_n) {
+      m.level = 0;
+      m.depth = 0;
+      const size_t e = m.match(s, anchor ? 1 : 0);
+      if (e != pat::kFail && e != last) {
+        ++n;
+        Value r;
+        if (repl.t == Value::Str || repl.is_num()) {
+          std::string piece;
+          for (size_t i = 0; i < rs.size(); ++i) {
+            if (rs[i] != '%') { piece += rs[i]; continue; }
+            if (++i >= rs.size()) throw LuaError("invalid use of '%' in replacement string");
+            const char d = rs[i];
+            if (d == '%') piece += '%';
+            else if (d == '0') piece += src.substr(s, e - s);
+            else if (isdigit((unsigned char)d)) piece += I.tostr(m.capture(d - '1', s, e));
+            else throw LuaError("invalid use of '%' in replacement string");
+          }
+          r = Value::string(piece);
+        } else {
+          Value c0 = m.capture(0, s, e);
+          if (repl.t == Value::Tab) {
+            r = I.index(repl, c0);
+          } else {
+            Values rv = I.call(repl, m.captures(s, e, true));
+            r = rv.empty() ? Value() : rv[0];
+          }
+        }
+        if (!r.truthy()) out += src.substr(s, e - s);  // false / nil: keep the original match
+        else if (r.t == Value::Str || r.is_num()) out += r.t == Value::Str ? *r.s : tostring(r);
+        else throw LuaError(std::string("invalid replacement value (a ") + type_name(r) + ")");
+        s = last = e;
+      } else if (s < src.size()) {
+        out += src[s++];
+      } else {
+        break;
+      }
+      if (anchor) break;
+    }
+    if (s < src.size()) out += src.substr(s);
+    return Values{Value::string(out), Value::integer(n)};
   });
 
   // table
@@ -1628,7 +2330,7 @@ Interp::Interp() {
     const char* v = getenv(check_str(a, 0, "getenv").c_str());
     return Values{v ? Value::string(v) : Value()};
   });
-  for (const char* lib : {"string", "table", "math", "os"}) modules[lib] = G->get(Value::string(lib));
+  for (const char* lib : {"string", "table", "math", "os", "coroutine"}) modules[lib] = G->get(Value::string(lib));
 }
 
 Interp::~Interp() {
@@ -1640,6 +2342,7 @@ Interp::~Interp() {
   globals.reset();
   root.reset();
   modules.clear();
+  string_meta.reset();
   for (Table* t : heap->tables) {
     for (auto& e : t->entries) {
       grave.push_back(std::move(e.first));
@@ -1647,6 +2350,7 @@ Interp::~Interp() {
     }
     t->entries.clear();
     t->index.clear();  // keys are copies of entries' keys: strings and tables both already moved
+    if (t->meta) grave.push_back(Value::table(std::move(t->meta)));
   }
   for (Scope* s : heap->scopes) {
     for (auto& v : s->vars) cells.push_back(std::move(v.second));

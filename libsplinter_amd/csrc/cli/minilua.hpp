@@ -12,9 +12,13 @@
 // assert pcall rawget rawset rawlen unpack require, string.{format len sub
 // upper lower rep byte char find reverse}, table.{insert remove concat unpack},
 // math.{floor ceil abs max min sqrt huge pi maxinteger mininteger random
-// tointeger fmod}, os.{time clock getenv}.  Not supported: metatables,
-// coroutines, goto, integer-for with float steps beyond doubles, patterns in
-// string.find (plain search only) -- documented in docs/DIVERGENCES.md.
+// tointeger fmod}, os.{time clock getenv}, Lua patterns (string.find / match /
+// gmatch / gsub with classes, sets, quantifiers, captures, %b, %f, back-references),
+// metatables (__index __newindex __call __tostring __name __len __unm __eq __lt __le,
+// arithmetic / bitwise / __concat events, __pairs, __metatable) and coroutines
+// (create resume yield status wrap running isyieldable close; each coroutine runs on
+// its own thread with a strict hand-off, so exactly one runs at a time).  Not
+// supported: goto, __gc / __close / __mode -- documented in docs/DIVERGENCES.md.
 #pragma once
 #include <cstdint>
 #include <functional>
@@ -29,15 +33,17 @@ namespace mlua {
 struct Table;
 struct Function;
 struct Interp;
+struct Coroutine;
 
 struct Value {
-  enum Type : uint8_t { Nil, Bool, Int, Num, Str, Tab, Fn } t = Nil;
+  enum Type : uint8_t { Nil, Bool, Int, Num, Str, Tab, Fn, Co } t = Nil;
   bool b = false;
   int64_t i = 0;
   double n = 0;
   std::shared_ptr<std::string> s;
   std::shared_ptr<Table> tab;
   std::shared_ptr<Function> fn;
+  std::shared_ptr<Coroutine> co;
 
   static Value nil() { return Value(); }
   static Value boolean(bool v) { Value x; x.t = Bool; x.b = v; return x; }
@@ -46,6 +52,7 @@ struct Value {
   static Value string(std::string v) { Value x; x.t = Str; x.s = std::make_shared<std::string>(std::move(v)); return x; }
   static Value table(std::shared_ptr<Table> v) { Value x; x.t = Tab; x.tab = std::move(v); return x; }
   static Value function(std::shared_ptr<Function> v) { Value x; x.t = Fn; x.fn = std::move(v); return x; }
+  static Value thread(std::shared_ptr<Coroutine> v) { Value x; x.t = Co; x.co = std::move(v); return x; }
   bool truthy() const { return !(t == Nil || (t == Bool && !b)); }
   bool is_num() const { return t == Int || t == Num; }
   double as_double() const { return t == Int ? (double)i : n; }
@@ -70,6 +77,7 @@ struct Table {
   Table& operator=(const Table&) = delete;
   std::vector<std::pair<Value, Value>> entries;  // insertion order (pairs / next)
   std::unordered_map<Value, size_t, ValueHash, ValueEq> index;
+  std::shared_ptr<Table> meta;  // setmetatable
   Heap* heap;
   Value get(const Value& k) const;
   void set(const Value& k, const Value& v);
@@ -104,6 +112,12 @@ struct Interp {
   void set_global(const std::string& name, Value v);
   Value global(const std::string& name) const;
   Values call(const Value& f, Values args);
+  // metatable-aware table access (__index / __newindex chains), metamethod lookup, __tostring
+  Value index(const Value& o, const Value& k);
+  void setindex(const Value& o, const Value& k, const Value& v);
+  Value metamethod(const Value& v, const char* event) const;
+  std::string tostr(const Value& v);
+  std::shared_ptr<Table> string_meta;  // getmetatable("") -> {__index = string}
   std::function<void(const std::string&)> out;  // print sink (default stdout)
   std::shared_ptr<Table> globals;
   std::unordered_map<std::string, Value> modules;  // require() registry

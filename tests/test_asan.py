@@ -72,6 +72,10 @@ def test_asan_lua_and_wasm_interpreters(uniq, tmp_path):
                        's.set("big", t[200])\nassert(#s.get("big") == 200)\n'
                        'local ok, err = pcall(function() error("boom") end)\nassert(not ok)\n')
         _run([ctl, "-u", st, "lua", str(lua)])
+        # patterns, metatables and coroutines (one thread per coroutine; a suspended one is unwound
+        # and joined at interpreter teardown)
+        for script in ("lua_patterns_meta.lua", "lua_coroutines.lua"):
+            _run([ctl, "-u", st, "lua", os.path.join(ROOT, "tests", "data", script)])
     finally:
         subprocess.run([ctl, "-u", st, "unset", "src"], capture_output=True, env=ENV)
         subprocess.run(["rm", "-f", f"/dev/shm/{st}"])

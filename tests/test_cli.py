@@ -144,6 +144,14 @@ def test_lua_verb_splinter_module(store):
     assert rc != 0
 
 
+@pytest.mark.parametrize("script", ["lua_patterns_meta.lua", "lua_coroutines.lua"])
+def test_lua_patterns_metatables_coroutines(store, script):
+    """Lua 5.4 semantics the reference gets from liblua5.4: string patterns (find / match / gmatch /
+    gsub), metatables and metamethods, coroutines -- each script asserts its expected values."""
+    rc, out, err = ctl(store, "lua", os.path.join(ROOT, "tests", "data", script))
+    assert rc == 0 and "ALL OK" in out, out + err
+
+
 def test_cli_regression_script():
     r = subprocess.run(["bash", os.path.join(ROOT, "tests", "cli_regression.sh"), BIN], capture_output=True, text=True,
                        timeout=120)

@@ -33,6 +33,7 @@
 #include <unistd.h>
 #include <vector>
 
+#include "lineedit.hpp"
 #include "minilua.hpp"
 #include "miniwasm.hpp"
 #include <dlfcn.h>
@@ -1559,13 +1560,17 @@ int main(int argc, char** argv) {
     signal(SIGINT, on_signal);
     fprintf(stderr, "%s %s (build %s)\nTo quit, press ctrl-c or ctrl-d.\n", prog.c_str(), SPLINTER_VERSION, SPL_BUILD_ID);
     std::string line;
-    char buf[65536];
+    // Tab completes the command word, like the reference's linenoise callback
+    const spl_le::Completer complete = [](const std::string& b, std::vector<std::string>& out) {
+      if (b.find(' ') != std::string::npos) return;
+      for (auto& m : modules())
+        if (!strncmp(m.name, b.c_str(), b.size())) out.push_back(m.name);
+    };
     for (;;) {
-      if (rc) fprintf(stderr, "%d : %s # ", rc, U.connected ? U.store.c_str() : "no-conn");
-      else fprintf(stderr, "%s # ", U.connected ? U.store.c_str() : "no-conn");
-      if (!fgets(buf, sizeof buf, stdin)) break;
-      line = buf;
-      while (!line.empty() && (line.back() == '\n' || line.back() == '\r')) line.pop_back();
+      std::string prompt = (rc ? std::to_string(rc) + " : " : std::string()) +
+                           (U.connected ? U.store : std::string("no-conn")) + " # ";
+      const spl_le::Read r = spl_le::read_line(prompt.c_str(), line, U.history, complete);
+      if (r != spl_le::Read::Line) break;  // Ctrl-D / EOF, or Ctrl-C: quit as the banner says
       auto a = tokenize(line);
       if (a.empty()) continue;
       U.history.push_back(line);

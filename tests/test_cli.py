@@ -152,6 +152,66 @@ def test_lua_patterns_metatables_coroutines(store, script):
     assert rc == 0 and "ALL OK" in out, out + err
 
 
+def _pty_repl(store, keys, timeout=20.0):
+    """Run the REPL on a pseudo-terminal, type `keys` (bytes, in chunks with small pauses so
+    escape sequences arrive whole) and return everything it printed."""
+    import pty
+    import select
+    import time
+    pid, fd = pty.fork()
+    if pid == 0:  # child: the REPL (any argv[0] other than splinterctl starts it)
+        os.environ["TERM"] = "xterm"
+        os.execv(os.path.join(BIN, "splinterctl"), ["splinter_cli", "-u", store])
+    out = b""
+    deadline = time.time() + timeout
+
+    def drain(t=0.15):
+        nonlocal out
+        end = time.time() + t
+        while time.time() < end:
+            r, _, _ = select.select([fd], [], [], 0.05)
+            if r:
+                try:
+                    out += os.read(fd, 65536)
+                except OSError:
+                    return
+    drain(0.5)
+    for chunk in keys:
+        os.write(fd, chunk)
+        drain()
+    while time.time() < deadline:
+        done, _ = os.waitpid(pid, os.WNOHANG)
+        if done:
+            break
+        drain(0.1)
+    else:
+        os.kill(pid, 9)
+        os.waitpid(pid, 0)
+    drain(0.2)
+    os.close(fd)
+    return out.decode(errors="replace")
+
+
+def test_repl_line_editing_history_completion(store):
+    """The REPL edits lines on a terminal (reference: linenoise, splinter_cli_main.c:832-872):
+    backspace, Ctrl-A / Ctrl-K / Ctrl-U / Ctrl-W, arrow keys, history recall with Up, Tab completion
+    of the command word, Ctrl-D to quit."""
+    keys = [b"sett", b"\x7f", b" k1 hello\r",            # backspace fixes the verb
+            b"get k1\r",
+            b"\x1b[A", b"\x1b[A", b"\x15", b"ge", b"\t", b" k1\r",  # Up x2, Ctrl-U, "ge"+Tab -> "get"
+            b"set k2 wrld", b"\x1b[D\x1b[D\x1b[D", b"o", b"\r",   # left arrows, insert 'o' -> "world"
+            b"get k2\r",
+            b"xyz get k1", b"\x01", b"\x0b", b"unset k2\r",   # Ctrl-A, Ctrl-K kills the line, retype
+            b"get k2 junk words", b"\x17\x17", b"\r",          # Ctrl-W twice -> "get k2"
+            b"\x04"]                                            # Ctrl-D on an empty line: exit
+    out = _pty_repl(store, keys)
+    assert "hello" in out, out[-2000:]
+    assert out.count("hello") >= 2, out[-2000:]          # "get k1" twice (typed, then recalled/completed)
+    assert "world" in out, out[-2000:]
+    assert ctl(store, "get", "k1")[1].startswith("hello")
+    assert ctl(store, "get", "k2")[0] != 0                # unset ran after Ctrl-A/Ctrl-K
+
+
 def test_cli_regression_script():
     r = subprocess.run(["bash", os.path.join(ROOT, "tests", "cli_regression.sh"), BIN], capture_output=True, text=True,
                        timeout=120)

@@ -8,11 +8,19 @@
 //   dec_attn_decode  single-token GQA attention over the KV cache (split-L over
 //                 16 waves, online softmax, LDS merge) — the per-token decode path
 //
+//   dec_gemv      M = 1 projections of the decode step (optionally with the RMSNorm of x
+//                 fused in): weight rows streamed once with 16-B loads, 4 rows per wave in flight
+//   dec_embed_tok / dec_rope_kv / dec_sample
+//                 the rest of a decode step, driven by a device-resident state {pos, token,
+//                 step} so a whole step (all layers + sampling) can be captured once in a HIP
+//                 graph and replayed per token with no host arguments changing
+//
 // Both are HBM-bound row kernels: one 64-lane wave per row, 16-B (8 x bf16)
 // vector accesses, statistics reduced with __shfl_xor over the full wavefront.
-// The projections run on the MFMA GEMM (gemm_bf16.hip).
+// The prefill projections run on the MFMA GEMM (gemm_bf16.hip).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cmath>
 
 namespace {
 
@@ -130,7 +138,9 @@ constexpr int kDecWaves = 16;
 template <int DPL>
 __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* __restrict__ q, const uint16_t* __restrict__ K,
                                                      const uint16_t* __restrict__ V, long ldkv, int L, int grp,
-                                                     int hd, float scale, uint16_t* __restrict__ out) {
+                                                     int hd, float scale, uint16_t* __restrict__ out,
+                                                     const int32_t* __restrict__ st) {
+  if (st) L = st[0] + 1;  // graph-captured decode step: the cache length lives on the device
   const int h = blockIdx.x;
   const int kvh = h / grp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -200,14 +210,278 @@ __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* 
   }
 }
 
+
+// ------------------------------------------------------------------ decode step --
+// Device state of a generation (int32): [0] pos = tokens already in the KV cache, [1] token = the
+// token the next step consumes (the last sampled one), [2] step = sampler draws so far.
+enum { ST_POS = 0, ST_TOK = 1, ST_STEP = 2 };
+
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// y[n] = x . W[n, :] for one token.  x (bf16 [K], optionally RMS-normalised in LDS first: the
+// dec_rmsnorm + GEMV pair of a layer in one launch) is staged in LDS; each wave owns 4 weight rows
+// and streams them with 16-B loads, 4 independent accumulators in flight.  MODE 0: bf16 out,
+// 1: + residual (bf16, may alias out: each element is read and written by the same lane),
+// 2: SwiGLU over pack_upgate rows (out[o] = up * silu(gate), o -> rows 32(o/16) + o%16 and +16),
+// 4: fp32 out (logits).
+constexpr int kGemvRows = 4;
+constexpr int kGemvMaxK = 16384;
+
+template <int MODE, bool RMS>
+__global__ __launch_bounds__(256) void k_gemv(const uint16_t* __restrict__ x, const float* __restrict__ rw, float eps,
+                                              const uint16_t* __restrict__ W, int K, int nout,
+                                              const uint16_t* res, void* out) {
+  __shared__ __attribute__((aligned(16))) uint16_t xs[kGemvMaxK];
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nch = K >> 3;
+  float ss = 0.f;
+  for (int c = tid; c < nch; c += 256) {
+    const uint4 v = *(const uint4*)(x + c * 8);
+    *(uint4*)(xs + c * 8) = v;
+    if constexpr (RMS) {
+      float f[8];
+      unpack8(v, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
+    }
+  }
+  if constexpr (RMS) {
+    ss = wave_sum(ss);
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    const float rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + eps);
+    for (int c = tid; c < nch; c += 256) {  // each thread rewrites the chunks it staged
+      float f[8];
+      unpack8(*(const uint4*)(xs + c * 8), f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] = f[e] * rs * rw[c * 8 + e];
+      *(uint4*)(xs + c * 8) = pack8(f);
+    }
+  }
+  __syncthreads();
+  // this wave's outputs and their weight rows
+  constexpr int outs = MODE == 2 ? kGemvRows / 2 : kGemvRows;
+  const int o0 = (blockIdx.x * 4 + wave) * outs;
+  if (o0 >= nout) return;
+  long rows[kGemvRows];
+#pragma unroll
+  for (int r = 0; r < kGemvRows; ++r) {
+    int o = o0 + (MODE == 2 ? r / 2 : r);
+    if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
+    rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
+  }
+  float acc[kGemvRows] = {};
+  for (int c = lane; c < nch; c += 64) {
+    float xf[8];
+    unpack8(*(const uint4*)(xs + c * 8), xf);
+    uint4 wv[kGemvRows];
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r) wv[r] = *(const uint4*)(W + rows[r] * K + c * 8);
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r) {
+      float wf[8];
+      unpack8(wv[r], wf);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[r] += wf[e] * xf[e];
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kGemvRows; ++r) acc[r] = wave_sum(acc[r]);
+  if (lane < outs) {
+    const int o = o0 + lane;
+    if (o < nout) {
+      float a0 = acc[0], a1 = acc[1];
+#pragma unroll
+      for (int r = 0; r < kGemvRows; ++r)
+        if ((MODE == 2 ? r / 2 : r) == lane) {
+          if (MODE == 2) { if (r & 1) a1 = acc[r]; else a0 = acc[r]; }
+          else a0 = acc[r];
+        }
+      if constexpr (MODE == 4) {
+        ((float*)out)[o] = a0;
+      } else {
+        float y = a0;
+        if constexpr (MODE == 1) y += bf2f(res[o]);
+        if constexpr (MODE == 2) y = a0 * a1 / (1.f + __expf(-a1));
+        ((uint16_t*)out)[o] = __builtin_bit_cast(uint16_t, (__bf16)y);
+      }
+    }
+  }
+}
+
+// x = emb[state.token]
+__global__ void k_embed_tok(const uint16_t* __restrict__ emb, int d, const int32_t* __restrict__ st,
+                            uint16_t* __restrict__ x) {
+  const long t = st[ST_TOK];
+  for (int c = threadIdx.x; c < d / 8; c += blockDim.x) *(uint4*)(x + c * 8) = *(const uint4*)(emb + t * d + c * 8);
+}
+
+// RoPE of the step's q (in place) and k at position state.pos, and the k / v rows appended to the
+// layer's KV cache (row pos of [n_ctx, ldkv]).  One thread per rotation pair / per 8 v elements.
+__global__ void k_rope_kv(uint16_t* __restrict__ qkv, int H, int KVH, int hd, const float* __restrict__ cs,
+                          const float* __restrict__ sn, const int32_t* __restrict__ st, uint16_t* __restrict__ kc,
+                          uint16_t* __restrict__ vc, long ldkv) {
+  const long p = st[ST_POS];
+  const int half = hd >> 1;
+  const int npairs = (H + KVH) * half;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < npairs + KVH * hd; i += gridDim.x * blockDim.x) {
+    if (i < npairs) {
+      const int head = i / half, j = i - head * half;
+      uint16_t* ptr = qkv + (long)head * hd + 2 * j;
+      const float a = bf2f(ptr[0]), b = bf2f(ptr[1]);
+      const float c = cs[p * half + j], s = sn[p * half + j];
+      const uint16_t y0 = __builtin_bit_cast(uint16_t, (__bf16)(a * c - b * s));
+      const uint16_t y1 = __builtin_bit_cast(uint16_t, (__bf16)(a * s + b * c));
+      if (head < H) {
+        ptr[0] = y0;
+        ptr[1] = y1;
+      } else {
+        uint16_t* kr = kc + p * ldkv + (long)(head - H) * hd + 2 * j;
+        kr[0] = y0;
+        kr[1] = y1;
+      }
+    } else {
+      const int e = i - npairs;
+      vc[p * ldkv + e] = qkv[(long)(H + KVH) * hd + e];
+    }
+  }
+}
+
+// counter-based uniform in [0, 1): splitmix64 of (seed, draw index)
+__device__ __forceinline__ double uniform01(uint64_t seed, uint64_t n) {
+  uint64_t z = seed + (n + 1) * 0x9E3779B97F4A7C15ull;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return (double)(z >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// top-p -> temperature -> categorical draw on the device (the reference's llama sampler chain,
+// splainference.cpp:272-279): the nucleus is the smallest set of the most probable tokens whose
+// probability reaches top_p, found as a logit threshold by bisection (no sort); the kept logits are
+// divided by temp and one token is drawn by an inclusive scan in index order.  One 1024-thread
+// workgroup; logits stay in L2 between the passes.  Writes state.token (and pos += inc_pos,
+// step += 1) and the token to `host_tok` (pinned, may be null).
+constexpr int kSampThreads = 1024;
+
+__device__ float block_reduce(float v, float* sh, bool is_max) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = is_max ? wave_max(v) : wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  float r = sh[0];
+  for (int w = 1; w < kSampThreads / 64; ++w) r = is_max ? fmaxf(r, sh[w]) : r + sh[w];
+  return r;
+}
+
+__global__ __launch_bounds__(kSampThreads) void k_sample(const float* __restrict__ logits, int V,
+                                                         const uint8_t* __restrict__ mask, float top_p, float temp,
+                                                         uint64_t seed, int32_t* __restrict__ st, int inc_pos,
+                                                         int32_t* host_tok) {
+  __shared__ float sh[kSampThreads / 64];
+  __shared__ float scan[kSampThreads];
+  const int tid = threadIdx.x;
+  auto lg = [&](int i) { return (mask && !mask[i]) ? -INFINITY : logits[i]; };
+  float m = -INFINITY;
+  for (int i = tid; i < V; i += kSampThreads) m = fmaxf(m, lg(i));
+  const float M = block_reduce(m, sh, true);
+  float z = 0.f;
+  for (int i = tid; i < V; i += kSampThreads) z += __expf(lg(i) - M);
+  const float Z = block_reduce(z, sh, false);
+  // nucleus threshold t: the largest logit cut whose kept mass reaches top_p
+  float lo = M - 40.f, hi = M;  // mass below M - 40 is < V e^-40
+  if (top_p < 1.f) {
+    for (int it = 0; it < 24; ++it) {
+      const float mid = 0.5f * (lo + hi);
+      float k = 0.f;
+      for (int i = tid; i < V; i += kSampThreads) {
+        const float l = lg(i);
+        if (l >= mid) k += __expf(l - M);
+      }
+      if (block_reduce(k, sh, false) >= top_p * Z) lo = mid;
+      else hi = mid;
+    }
+  } else {
+    lo = -INFINITY;
+  }
+  const float cut = lo;
+  const float it = 1.f / fmaxf(temp, 1e-6f);
+  // contiguous chunk per thread for the ordered scan
+  const int chunk = (V + kSampThreads - 1) / kSampThreads;
+  const int b = tid * chunk, e = min(V, b + chunk);
+  float part = 0.f;
+  for (int i = b; i < e; ++i) {
+    const float l = lg(i);
+    if (l >= cut) part += __expf((l - M) * it);
+  }
+  scan[tid] = part;
+  __syncthreads();
+  for (int off = 1; off < kSampThreads; off <<= 1) {  // Hillis-Steele inclusive scan
+    const float v = tid >= off ? scan[tid - off] : 0.f;
+    __syncthreads();
+    scan[tid] += v;
+    __syncthreads();
+  }
+  const float total = scan[kSampThreads - 1];
+  const float u = (float)(uniform01(seed, (uint64_t)st[ST_STEP]) * total);
+  const float before = tid ? scan[tid - 1] : 0.f;
+  __shared__ int pick;
+  if (tid == 0) pick = -1;
+  __syncthreads();
+  if (u >= before && u < scan[tid] && part > 0.f) {
+    float run = before;
+    int sel = -1;
+    for (int i = b; i < e; ++i) {
+      const float l = lg(i);
+      if (l < cut) continue;
+      sel = i;
+      run += __expf((l - M) * it);
+      if (u < run) break;
+    }
+    pick = sel;
+  }
+  __syncthreads();
+  if (tid == 0) {
+    int t = pick;
+    if (t < 0) {  // u landed on a rounding gap at the very top: take the most probable token
+      for (int i = 0; i < V; ++i)
+        if (lg(i) == M) { t = i; break; }
+    }
+    st[ST_TOK] = t;
+    st[ST_POS] += inc_pos;
+    st[ST_STEP] += 1;
+    if (host_tok) __hip_atomic_store(host_tok, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
 
 extern "C" {
 
 // q: bf16 [H*hd] (one token, RoPE applied); k/v: bf16 cache rows [L, ldkv] (ldkv = KVH*hd);
 // out: bf16 [H*hd].  hd in {64, 128, 192, 256}, H % KVH == 0, L >= 1, 16-B aligned rows.
+int dec_attn_decode_st(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,
+                       float scale, void* out, const int32_t* st, hipStream_t s);
 int dec_attn_decode(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,
                     float scale, void* out, hipStream_t s) {
+  return dec_attn_decode_st(q, k, v, ldkv, L, H, KVH, hd, scale, out, nullptr, s);
+}
+
+// as dec_attn_decode; with st != null the cache length is st[0] + 1 (L is ignored)
+int dec_attn_decode_st(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,
+                       float scale, void* out, const int32_t* st, hipStream_t s) {
+  if (st) L = 1;
   if (L <= 0 || H <= 0 || KVH <= 0 || H % KVH || hd <= 0 || hd % 64 || hd > 256 || ldkv % 8 ||
       ldkv < (long)KVH * hd || ((uintptr_t)k | (uintptr_t)v) % 16)
     return (int)hipErrorInvalidValue;
@@ -216,10 +490,10 @@ int dec_attn_decode(const void* q, const void* k, const void* v, long ldkv, int 
   const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
   uint16_t* oo = (uint16_t*)out;
   switch (hd / 64) {
-    case 1: hipLaunchKernelGGL(k_attn_decode<1>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
-    case 2: hipLaunchKernelGGL(k_attn_decode<2>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
-    case 3: hipLaunchKernelGGL(k_attn_decode<3>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
-    default: hipLaunchKernelGGL(k_attn_decode<4>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo); break;
+    case 1: hipLaunchKernelGGL(k_attn_decode<1>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo, st); break;
+    case 2: hipLaunchKernelGGL(k_attn_decode<2>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo, st); break;
+    case 3: hipLaunchKernelGGL(k_attn_decode<3>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo, st); break;
+    default: hipLaunchKernelGGL(k_attn_decode<4>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo, st); break;
   }
   return (int)hipGetLastError();
 }
@@ -245,6 +519,55 @@ int dec_rope(void* qkv, long ld, long T, int ncols, int hd, int pos0, const floa
   if (g > 4096) g = 4096;
   hipLaunchKernelGGL(k_rope, dim3((unsigned)g), dim3(256), 0, s, (uint16_t*)qkv, ld, T, ncols, hd, pos0, cos_tab,
                      sin_tab);
+  return (int)hipGetLastError();
+}
+
+// y = x . W^T for one token (see k_gemv).  mode 0 store, 1 residual, 2 SwiGLU (N = packed rows,
+// out has N / 2), 4 fp32; rms_w != null: x is RMS-normalised with rms_w / eps first.
+// K % 8 == 0, K <= 16384, 16-B aligned W / x.
+int dec_gemv(int mode, const void* x, const float* rms_w, float eps, const void* W, int N, int K, const void* res,
+             void* out, hipStream_t s) {
+  if (K <= 0 || K % 8 || K > kGemvMaxK || N <= 0 || (mode == 2 && N % 32) || (mode == 1 && !res) ||
+      ((uintptr_t)W | (uintptr_t)x) % 16)
+    return (int)hipErrorInvalidValue;
+  const int nout = mode == 2 ? N / 2 : N;
+  const int per_block = 4 * (mode == 2 ? kGemvRows / 2 : kGemvRows);
+  const dim3 g((unsigned)((nout + per_block - 1) / per_block)), b(256);
+  const uint16_t *xx = (const uint16_t*)x, *ww = (const uint16_t*)W, *rr = (const uint16_t*)res;
+#define GEMV(M_, R_) hipLaunchKernelGGL((k_gemv<M_, R_>), g, b, 0, s, xx, rms_w, eps, ww, K, nout, rr, out)
+  const bool rms = rms_w != nullptr;
+  switch (mode) {
+    case 0: if (rms) GEMV(0, true); else GEMV(0, false); break;
+    case 1: if (rms) GEMV(1, true); else GEMV(1, false); break;
+    case 2: if (rms) GEMV(2, true); else GEMV(2, false); break;
+    case 4: if (rms) GEMV(4, true); else GEMV(4, false); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef GEMV
+  return (int)hipGetLastError();
+}
+
+int dec_embed_tok(const void* emb, int d, const int32_t* st, void* x, hipStream_t s) {
+  if (d % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_embed_tok, dim3(1), dim3(256), 0, s, (const uint16_t*)emb, d, st, (uint16_t*)x);
+  return (int)hipGetLastError();
+}
+
+// qkv: bf16 [(H + 2 KVH) hd] of the step's token; kc / vc: the layer's cache [n_ctx, ldkv]
+int dec_rope_kv(void* qkv, int H, int KVH, int hd, const float* cos_tab, const float* sin_tab, const int32_t* st,
+                void* kc, void* vc, long ldkv, hipStream_t s) {
+  if (hd % 2 || H <= 0 || KVH <= 0 || ldkv < (long)KVH * hd) return (int)hipErrorInvalidValue;
+  const int work = (H + KVH) * hd / 2 + KVH * hd;
+  hipLaunchKernelGGL(k_rope_kv, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, (uint16_t*)qkv, H, KVH, hd,
+                     cos_tab, sin_tab, st, (uint16_t*)kc, (uint16_t*)vc, ldkv);
+  return (int)hipGetLastError();
+}
+
+int dec_sample(const float* logits, int V, const uint8_t* mask, float top_p, float temp, uint64_t seed, int32_t* st,
+               int inc_pos, int32_t* host_tok, hipStream_t s) {
+  if (V <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_sample, dim3(1), dim3(kSampThreads), 0, s, logits, V, mask, top_p, temp, seed, st, inc_pos,
+                     host_tok);
   return (int)hipGetLastError();
 }
 

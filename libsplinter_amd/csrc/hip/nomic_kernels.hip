@@ -286,11 +286,15 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // OPT: permlane reductions, packed (v_pk_fma/v_pk_add) score scaling and row sums, and K/V
 // source pointers advanced per tile instead of recomputed with 64-bit multiplies.
-template <int W, bool XR = false, bool OPT = false>
+// CAUSAL: query row i of a sequence sees keys 0..i (the completion daemon's prefill, K18); key
+// tiles past the block's last row are skipped, the diagonal tiles masked per score.  kv_heads <
+// heads: grouped-query attention, q head h reads kv head h / (heads / kv_heads); the qkv rows are
+// [q (heads) | k (kv_heads) | v (kv_heads)] x HD.
+template <int W, bool XR = false, bool OPT = false, bool CAUSAL = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1))) void k_attn2(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
-                                               int heads, float scale_log2) {
+                                               int heads, float scale_log2, int kv_heads) {
   __shared__ __attribute__((aligned(16))) char lds[2][2][64 * 128];  // [buf][K | V][key * 128 B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -304,10 +308,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
   }
   const int seq = qblocks[2 * qbi], qstart = qblocks[2 * qbi + 1];
   const long s0 = cu[seq], len = cu[seq + 1] - s0;
-  const long ld = 3L * heads * HD;
+  const long ld = (long)(heads + 2 * kv_heads) * HD;
+  const int kvhead = head / (heads / kv_heads);
   const uint16_t* Qg = qkv + head * HD;
-  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
-  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
+  const uint16_t* Kg = qkv + (long)heads * HD + kvhead * HD;
+  const uint16_t* Vg = qkv + (long)(heads + kv_heads) * HD + kvhead * HD;
 
   // Q^T B-fragments: query row qstart + wave*32 + qb*16 + li, d = kk*32 + 8g .. +7
   bf16x8 qf[2][2];
@@ -363,7 +368,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
     }
   };
 
-  const int ntiles = (int)((len + 63) / 64);
+  int ntiles = (int)((len + 63) / 64);
+  if constexpr (CAUSAL) ntiles = min(ntiles, (int)((qstart + 128 + 63) / 64));
   gload(0);
   lwrite(0);
   __syncthreads();
@@ -400,6 +406,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
     const bool full = k0 + 64 <= len;
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
+      if constexpr (CAUSAL) {
+        if (k0 + 63 > qstart) {  // a diagonal tile: keys after the query are masked
+          const long qrow = qstart + wave * 32 + qb * 16 + li;
+#pragma unroll
+          for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (k0 + kb * 16 + 4 * g + r > qrow) s[kb][qb][r] = -1e30f;
+        }
+      }
       if (!full) {
 #pragma unroll
         for (int kb = 0; kb < 4; ++kb)
@@ -713,22 +729,33 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   const float scale_log2 = scale * 1.4426950408889634f;
   if (g_attn_variant == 5)
     hipLaunchKernelGGL((k_attn2<0, false, true>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv,
-                       (uint16_t*)out, cu, qblocks, heads, scale_log2);
+                       (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 6)
     hipLaunchKernelGGL((k_attn2<0, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
-                       (uint16_t*)out, cu, qblocks, heads, scale_log2);
+                       (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 4)
     hipLaunchKernelGGL((k_attn2<0, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
-                       cu, qblocks, heads, scale_log2);
+                       cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 2)
     hipLaunchKernelGGL((k_attn2<0>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2);
+                       qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 3)
     hipLaunchKernelGGL((k_attn2<3>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2);
+                       qblocks, heads, scale_log2, heads);
   else
     hipLaunchKernelGGL(k_attn, dim3(2 * nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);
+  return (int)hipGetLastError();
+}
+
+// causal (prefill) attention of the completion daemon's decoder: qkv rows [q (heads) | k | v
+// (kv_heads each)] x 64, out [T, heads * 64]; 128-row q-blocks as nomic_attention
+int dec_attn_prefill(const void* qkv, void* out, const int32_t* cu, const int32_t* qblocks, int nqb, int heads,
+                     int kv_heads, float scale, hipStream_t s) {
+  if (nqb <= 0) return 0;
+  if (kv_heads <= 0 || heads % kv_heads || (heads + 2 * kv_heads) * HD % 8) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_attn2<0, true, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
+                     (uint16_t*)out, cu, qblocks, heads, scale * 1.4426950408889634f, kv_heads);
   return (int)hipGetLastError();
 }
 

@@ -75,6 +75,10 @@ class Splainference:
         self.store, self.model, self.tok, self.sampler = store, model, tokenizer, sampler
         self.system_prompt_key = system_prompt_key
         self.max_tokens = max_tokens
+        self.engine = None
+        if getattr(model, "hip", False):
+            from ..models.decoder import DecodeEngine
+            self.engine = DecodeEngine(model, sampler.top_p, sampler.temp, sampler.seed, sampler.mask)
 
     def _read_request(self, key: str):
         s = self.store
@@ -139,18 +143,26 @@ class Splainference:
             debug_post(s, f"[splainference][ERROR]: Prefill decode failed for key: {key}")
             self._finish(key)
             return 0
-        logits = self.model.forward(ids)
+        eng = self.engine
+        if eng is not None:  # GPU: prefill + device sampler, then one graph replay per token
+            t = eng.first_token(ids)
+        else:
+            logits = self.model.forward(ids)
         chunk, run, rebid, oom = b"", 0, 0, False
         for _ in range(min(self.max_tokens, ctx_room)):
             if not _running:
                 break
-            t = self.sampler(logits)
+            if eng is None:
+                t = self.sampler(logits)
             if t == self.tok.eos_id:
                 break
             piece = self.tok.piece(t)
             chunk += piece
             run += 1
-            logits = self.model.forward([t])
+            if eng is not None:
+                t = eng.next_token()
+            else:
+                logits = self.model.forward([t])
             if (is_word_boundary(piece) or run >= TOKEN_FLUSH_MAX) and chunk:
                 if written + len(chunk) > max_val:
                     debug_post(s, f"[splainference][WARN]: Slot full, truncating completion: {key}")

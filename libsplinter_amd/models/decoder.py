@@ -190,6 +190,18 @@ class CausalLM:
                 self.L.dec_rope.restype = c_int
                 self.L.dec_attn_decode.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P]
                 self.L.dec_attn_decode.restype = c_int
+                self.L.dec_attn_decode_st.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P, P]
+                self.L.dec_attn_decode_st.restype = c_int
+                self.L.dec_attn_prefill.argtypes = [P, P, P, P, c_int, c_int, c_int, c_float, P]
+                self.L.dec_attn_prefill.restype = c_int
+                self.L.dec_gemv.argtypes = [c_int, P, P, c_float, P, c_int, c_int, P, P, P]
+                self.L.dec_gemv.restype = c_int
+                self.L.dec_embed_tok.argtypes = [P, c_int, P, P, P]
+                self.L.dec_embed_tok.restype = c_int
+                self.L.dec_rope_kv.argtypes = [P, c_int, c_int, c_int, P, P, P, P, P, c_long, P]
+                self.L.dec_rope_kv.restype = c_int
+                self.L.dec_sample.argtypes = [P, c_int, P, c_float, c_float, ctypes.c_uint64, P, c_int, P, P]
+                self.L.dec_sample.restype = c_int
                 self.L._dec_declared = True
             ok = all(n % 128 == 0 for n in (cfg.d + 2 * cfg.kv_heads * hd, cfg.d, 2 * cfg.ffn, vpad)) \
                 and cfg.d % 64 == 0 and cfg.ffn % 64 == 0
@@ -293,7 +305,19 @@ class CausalLM:
             self.kv[li, 0, self.pos: self.pos + n] = k
             self.kv[li, 1, self.pos: self.pos + n] = v
             L_ = self.pos + n
-            if self.hip and self.attn_kernel and n == 1 and hd % 64 == 0 and hd <= 256:
+            if self.hip and self.attn_kernel and n > 1 and self.pos == 0 and hd == 64:
+                # prompt prefill: causal MFMA attention over the prompt's own q|k|v (k_attn2<CAUSAL>)
+                from .nomic import _chk, _stream
+                a = torch.empty((n, cfg.d), dtype=qkv.dtype, device=self.device)
+                if getattr(self, "_pf_n", -1) != n:
+                    self._pf_cu = torch.tensor([0, n], dtype=torch.int32, device=self.device)
+                    self._pf_qb = torch.tensor([v for q0 in range(0, n, 128) for v in (0, q0)], dtype=torch.int32,
+                                               device=self.device)
+                    self._pf_n = n
+                _chk(self.L.dec_attn_prefill(qkv.data_ptr(), a.data_ptr(), self._pf_cu.data_ptr(),
+                                             self._pf_qb.data_ptr(), self._pf_qb.numel() // 2, H, KVH, hd ** -0.5,
+                                             _stream()), "attn_prefill")
+            elif self.hip and self.attn_kernel and n == 1 and hd % 64 == 0 and hd <= 256:
                 # per-token decode: dec_attn_decode (one workgroup per q head, split-L online softmax)
                 from .nomic import _chk, _stream
                 a = torch.empty((1, cfg.d), dtype=qkv.dtype, device=self.device)
@@ -321,11 +345,114 @@ class CausalLM:
         return logits[0, : cfg.vocab].float()
 
 
+class DecodeEngine:
+    """Token generation with no host compute in the loop (K18): prompt prefill on the MFMA GEMMs
+    and the causal MFMA attention, then per token ONE replay of a HIP graph holding the whole
+    decode step -- embedding row, per layer (RMSNorm+QKV GEMV, RoPE + KV-cache append, decode
+    attention, o GEMV + residual, RMSNorm+up|gate GEMV + SwiGLU, down GEMV + residual), final
+    RMSNorm + LM-head GEMV and the top-p / temperature sampler (dec_sample).  Every kernel reads
+    the position and the input token from a device state {pos, token, step}, so the captured
+    arguments never change; the host reads back only the sampled token id (pinned memory).
+    Reference: splainference.cpp:272-365 (sampler chain, llama_decode per token)."""
+
+    def __init__(self, model: "CausalLM", top_p: float = 0.9, temp: float = 0.7, seed: int = 0xFFFFFFFF,
+                 mask: Optional[torch.Tensor] = None, use_graph: bool = True):
+        assert model.hip, "DecodeEngine runs on the GPU"
+        m, cfg = model, model.cfg
+        self.m, self.top_p, self.temp, self.seed = m, float(top_p), float(temp), int(seed) & 0xFFFFFFFFFFFFFFFF
+        dev = m.device
+        e = dict(device=dev, dtype=torch.bfloat16)
+        kvd = cfg.kv_heads * cfg.head_dim
+        self.st = torch.zeros(4, dtype=torch.int32, device=dev)      # pos, token, step
+        self.xa = torch.empty(cfg.d, **e)
+        self.xb = torch.empty(cfg.d, **e)
+        self.qkv = torch.empty(cfg.d + 2 * kvd, **e)
+        self.attn = torch.empty(cfg.d, **e)
+        self.ffn = torch.empty(cfg.ffn, **e)
+        self.logits = torch.empty(m.head.shape[0], dtype=torch.float32, device=dev)
+        self.host_tok = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        self.mask = mask[: cfg.vocab].to(device=dev, dtype=torch.uint8).contiguous() if mask is not None else None
+        if m.kv is None:
+            m.kv = torch.empty((cfg.layers, 2, cfg.n_ctx, cfg.kv_heads, cfg.head_dim), dtype=torch.bfloat16, device=dev)
+        self.use_graph = use_graph
+        self.graph = None
+        self.steps = 0
+
+    def _enqueue_step(self):
+        from .nomic import _chk, _stream
+        m, cfg, L = self.m, self.m.cfg, self.m.L
+        s = _stream()
+        H, KVH, hd = cfg.heads, cfg.kv_heads, cfg.head_dim
+        P = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
+        _chk(L.dec_embed_tok(m.emb.data_ptr(), cfg.d, self.st.data_ptr(), self.xa.data_ptr(), s), "embed_tok")
+        for li, lw in enumerate(m.layers):
+            _chk(L.dec_gemv(0, self.xa.data_ptr(), lw["n1"].data_ptr(), cfg.eps, lw["qkv"].data_ptr(),
+                            lw["qkv"].shape[0], cfg.d, None, self.qkv.data_ptr(), s), "gemv qkv")
+            kc, vc = m.kv[li, 0], m.kv[li, 1]
+            _chk(L.dec_rope_kv(self.qkv.data_ptr(), H, KVH, hd, m.cos.data_ptr(), m.sin.data_ptr(), self.st.data_ptr(),
+                               kc.data_ptr(), vc.data_ptr(), KVH * hd, s), "rope_kv")
+            _chk(L.dec_attn_decode_st(self.qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), KVH * hd, 1, H, KVH, hd,
+                                      hd ** -0.5, self.attn.data_ptr(), self.st.data_ptr(), s), "attn_decode")
+            _chk(L.dec_gemv(1, self.attn.data_ptr(), None, 0.0, lw["o"].data_ptr(), cfg.d, cfg.d, self.xa.data_ptr(),
+                            self.xb.data_ptr(), s), "gemv o")
+            _chk(L.dec_gemv(2, self.xb.data_ptr(), lw["n2"].data_ptr(), cfg.eps, lw["ug"].data_ptr(),
+                            lw["ug"].shape[0], cfg.d, None, self.ffn.data_ptr(), s), "gemv up|gate")
+            _chk(L.dec_gemv(1, self.ffn.data_ptr(), None, 0.0, lw["down"].data_ptr(), cfg.d, cfg.ffn,
+                            self.xb.data_ptr(), self.xa.data_ptr(), s), "gemv down")
+        _chk(L.dec_gemv(4, self.xa.data_ptr(), m.norm_out.data_ptr(), cfg.eps, m.head.data_ptr(), m.head.shape[0],
+                        cfg.d, None, self.logits.data_ptr(), s), "gemv head")
+        self._sample(self.logits, inc_pos=1)
+
+    def _sample(self, logits: torch.Tensor, inc_pos: int):
+        from .nomic import _chk, _stream
+        m = self.m
+        _chk(m.L.dec_sample(logits.data_ptr(), m.cfg.vocab, self.mask.data_ptr() if self.mask is not None else None,
+                            self.top_p, self.temp, self.seed, self.st.data_ptr(), inc_pos, self.host_tok.data_ptr(),
+                            _stream()), "sample")
+
+    def _step(self):
+        if not self.use_graph:
+            self._enqueue_step()
+            return
+        if self.graph is None:
+            # warm up once outside capture (first-launch code-object loading), then capture
+            side = torch.cuda.Stream()
+            side.wait_stream(torch.cuda.current_stream())
+            saved = self.st.clone()
+            with torch.cuda.stream(side):
+                self._enqueue_step()
+            torch.cuda.current_stream().wait_stream(side)
+            self.st.copy_(saved)  # the warm-up step is undone: same state, cache row rewritten next
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self._enqueue_step()
+        self.graph.replay()
+
+    def first_token(self, ids: List[int]) -> int:
+        """Prefill the prompt (KV cache rows 0..n-1) and sample the first token on the device."""
+        m = self.m
+        m.reset()
+        logits = m.forward(ids)
+        self.st[0] = len(ids)
+        self.st[1] = 0
+        self._sample(logits.contiguous(), inc_pos=0)
+        torch.cuda.current_stream().synchronize()
+        return int(self.host_tok[0])
+
+    def next_token(self) -> int:
+        """One decode step on the device: consume the last sampled token, return the next one."""
+        self._step()
+        torch.cuda.current_stream().synchronize()
+        self.m.pos += 1
+        self.steps += 1
+        return int(self.host_tok[0])
+
+
 class Sampler:
     """top-p 0.9 -> temperature 0.7 -> seeded categorical (reference :272-279)."""
 
     def __init__(self, top_p: float = 0.9, temp: float = 0.7, seed: int = 0xFFFFFFFF, mask=None):
-        self.top_p, self.temp = top_p, temp
+        self.top_p, self.temp, self.seed = top_p, temp, seed
         self.g = torch.Generator().manual_seed(seed)
         self.mask = mask
 

@@ -11,8 +11,9 @@ Contract kept from the reference daemon (/root/reference/splainference.cpp):
           (:269) and the completion is APPENDED as it streams: a flush at a
           word boundary (piece starts with ' ' or contains '\\n') or every 8
           tokens (:86, :102-109, :332-364), truncated at max_val_sz (:336-345)
-  prompt  the model's chat template is not evaluated (no jinja here): the
-          reference's bare fallback "<system>\\n...\\n<user>\\n...\\n<assistant>\\n" (:132-169)
+  prompt  the GGUF chat template's family is detected by its markers (chatml, llama 3,
+          gemma, phi 3, zephyr, llama 2 / mistral), as llama_chat_apply_template does;
+          otherwise the reference's bare fallback "<system>/<user>/<assistant>" (:132-169)
   shard   0x5F1A WILLNEED prio 200, re-bid every 32 appended tokens, WILLNEED
           madvise of the request slot (:39-62, :222-230, :359-363)
   done    ctime backfill with the processing delta (:282, :383-387), "__debug"
@@ -28,6 +29,7 @@ import os
 import signal
 import sys
 import time
+from typing import Optional
 
 LABEL_WAITING = 0x1000000000000000
 LABEL_SERVICING = 0x2000000000000000
@@ -59,7 +61,33 @@ def debug_post(store, msg: str) -> None:
             pass
 
 
-def build_prompt(system_msg: str, user_msg: str) -> str:
+def build_prompt(system_msg: str, user_msg: str, template: Optional[str] = None) -> str:
+    """The reference renders the model's GGUF chat template with llama_chat_apply_template and
+    falls back to a bare "<system>/<user>/<assistant>" layout (splainference.cpp:132-169).
+    llama.cpp recognises templates by marker substrings rather than evaluating the jinja; the
+    families below follow the same detection, anything else takes the bare fallback."""
+    t = template or ""
+    sys_ = system_msg
+    if "<|im_start|>" in t:  # chatml
+        out = f"<|im_start|>system\n{sys_}<|im_end|>\n" if sys_ else ""
+        return out + f"<|im_start|>user\n{user_msg}<|im_end|>\n<|im_start|>assistant\n"
+    if "<|start_header_id|>" in t:  # llama 3
+        out = f"<|start_header_id|>system<|end_header_id|>\n\n{sys_}<|eot_id|>" if sys_ else ""
+        return out + (f"<|start_header_id|>user<|end_header_id|>\n\n{user_msg}<|eot_id|>"
+                      "<|start_header_id|>assistant<|end_header_id|>\n\n")
+    if "<start_of_turn>" in t:  # gemma: the system text is prepended to the user turn
+        body = f"{sys_}\n\n{user_msg}" if sys_ else user_msg
+        return f"<start_of_turn>user\n{body}<end_of_turn>\n<start_of_turn>model\n"
+    if "<|assistant|>" in t and "<|end|>" in t:  # phi 3
+        out = f"<|system|>\n{sys_}<|end|>\n" if sys_ else ""
+        return out + f"<|user|>\n{user_msg}<|end|>\n<|assistant|>\n"
+    if "<|user|>" in t and "</s>" in t:  # zephyr
+        out = f"<|system|>\n{sys_}</s>\n" if sys_ else ""
+        return out + f"<|user|>\n{user_msg}</s>\n<|assistant|>\n"
+    if "[INST]" in t:  # llama 2 / mistral
+        if sys_:
+            return f"[INST] <<SYS>>\n{sys_}\n<</SYS>>\n\n{user_msg} [/INST]"
+        return f"[INST] {user_msg} [/INST]"
     out = ""
     if system_msg:
         out += "<system>\n" + system_msg + "\n"
@@ -117,7 +145,7 @@ class Splainference:
         if self.system_prompt_key:
             v = s.get(self.system_prompt_key)
             system_msg = v.decode("utf-8", "replace") if v else ""
-        prompt = build_prompt(system_msg, user_msg)
+        prompt = build_prompt(system_msg, user_msg, getattr(self.tok, "chat_template", None))
         debug_post(s, f"[splainference][START]: Processing key: {key}")
         s.shard_rebid(SHARD_ID, INTENT_WILLNEED, SHARD_PRIO_LIVE, SHARD_DUR_LIVE)
         try:

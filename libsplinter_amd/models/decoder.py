@@ -221,6 +221,7 @@ class CausalLM:
         tokens = g.get("tokenizer.ggml.tokens")
         tok = VocabTokenizer(list(tokens), int(g.get("tokenizer.ggml.bos_token_id", 1)),
                              int(g.get("tokenizer.ggml.eos_token_id", 2))) if tokens else ByteTokenizer()
+        tok.chat_template = g.get("tokenizer.chat_template", None)  # rendered by splainference.build_prompt
         return cls(cfg, tensors, device), tok
 
     # ------------------------------------------------------------- pieces --

@@ -303,3 +303,19 @@ def test_state_machine_gpu_decode_engine(uniq):
     finally:
         s.close()
         unlink(uniq)
+
+
+def test_chat_template_families():
+    """build_prompt: the GGUF chat template families llama.cpp detects by marker, and the
+    reference's bare fallback (splainference.cpp:132-169)."""
+    from libsplinter_amd.daemons.splainference import build_prompt
+    assert build_prompt("", "hi") == "<user>\nhi\n<assistant>\n"
+    assert build_prompt("sys", "hi", "{{ unknown }}") == "<system>\nsys\n<user>\nhi\n<assistant>\n"
+    assert build_prompt("sys", "hi", "{% ... %}<|im_start|>{{ role }}") == (
+        "<|im_start|>system\nsys<|im_end|>\n<|im_start|>user\nhi<|im_end|>\n<|im_start|>assistant\n")
+    assert build_prompt("", "hi", "<|start_header_id|>").endswith(
+        "<|start_header_id|>assistant<|end_header_id|>\n\n")
+    assert build_prompt("s", "hi", "<start_of_turn>") == "<start_of_turn>user\ns\n\nhi<end_of_turn>\n<start_of_turn>model\n"
+    assert build_prompt("", "hi", "[INST] {{ x }} [/INST]") == "[INST] hi [/INST]"
+    assert build_prompt("s", "hi", "<|user|>...<|end|>...<|assistant|>").startswith("<|system|>\ns<|end|>\n")
+    assert build_prompt("", "hi", "<|user|>\n{{ m }}</s>").endswith("<|assistant|>\n")

@@ -67,6 +67,9 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: every rank joins a gloo group, rank 0 prints the world "
                         "it sees as JSON and the run ends (tests/test_bench_cpu.py)")
+    p.add_argument("--embed-e2e", type=int, default=5, metavar="STEPS",
+                   help="after the timed loop, time STEPS end-to-end embedding batches of the splinference path "
+                        "(text fetch, WordPiece, varlen batch, slot find, encoder + seqlocked write, labels); 0: off")
     p.add_argument("--host-api", type=int, default=16, metavar="THREADS",
                    help="also measure the per-call C API (splinter_set/get through the device command ring) "
                         "from THREADS host threads, outside the timed region; 0 = skip")
@@ -415,6 +418,25 @@ def main():
         except Exception as e:  # the headline stands without it
             log(f"[bench] host-API run failed: {e}")
 
+    e2e = None
+    if embedder is not None and args.embed_e2e > 0:
+        from libsplinter_amd.models.bench_embed import EmbedE2E
+        pipe = EmbedE2E(embedder.enc, batch=args.embed_batch, seq=args.embed_seq, rank=rank)
+        pipe.run()  # warm-up (tokenizer threads, first varlen shapes)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fails = 0
+        for _ in range(args.embed_e2e):
+            fails += int((pipe.run() != 0).sum().item())
+        torch.cuda.synchronize()
+        te = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if routed:
+            dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        dt = te.item()
+        e2e = {"vectors_per_s": pipe.docs * args.embed_e2e * world / dt, "ms_per_batch": dt / args.embed_e2e * 1e3,
+               "tokens_per_batch": pipe.tokens, "write_failures": fails}
+        pipe.close()
+
     kv_ops = (n_set + n_get) * args.steps * world
     kv_ops_s = kv_ops / elapsed if kv_ops else 0.0
     emb_vps = emb_tps = emb_tflops = None
@@ -447,6 +469,10 @@ def main():
         "kv_ops_per_s": kv_ops_s,
         "embed_vectors_per_s": emb_vps,
         "embed_tokens_per_s": emb_tps,
+        "embed_e2e_vectors_per_s": e2e["vectors_per_s"] if e2e else None,
+        "embed_e2e_ms_per_batch": e2e["ms_per_batch"] if e2e else None,
+        "embed_e2e_tokens_per_batch": e2e["tokens_per_batch"] if e2e else None,
+        "embed_e2e_write_failures": e2e["write_failures"] if e2e else None,
         "embed_tflops": emb_tflops,
         "kv_attempts": attempts, "kv_ok": ok, "kv_eagain_retries": again, "kv_miss": miss,
         "successful_ops_per_s": ok / elapsed if elapsed else 0.0,

@@ -45,3 +45,74 @@ class EmbedPhase:
 
     def close(self):
         self.arena.close()
+
+
+class EmbedE2E:
+    """End-to-end embedding of the splinference path for one batch of pending documents,
+    measured separately from the kernel-only EmbedPhase (bench.py reports both):
+
+      fetch     the documents' text from their slots (batched arena get, device -> host)
+      tokenize  native WordPiece on the host (csrc/core/wordpiece.cpp, threaded), varlen docs
+      pack      the varlen Batch (ids / offsets / q-blocks to the device)
+      find      slot lookup and key hashes (batched meta kernel)
+      embed     encoder forward + mean pool written into the slots under the seqlock, with the
+                reference's "slot still holds this key" check (k_pool status)
+      label     the pending label cleared; the simulated producer then re-arms it for the next
+                step (one more meta kernel, kept inside the timed step)
+
+    Reference loop: splinference.cpp:236-300 (tokenize, llama_decode, set_embedding, +2 epoch
+    check, label updates)."""
+
+    WAITING = 1 << 6
+
+    def __init__(self, enc: NomicEncoder, batch: int = 64, seq: int = 512, rank: int = 0):
+        from ..models.tokenizer import WordPieceTokenizer, synthetic_vocab
+        from ..ops.arena import pack_values
+        self.enc = enc
+        cfg = enc.cfg
+        vocab = synthetic_vocab(cfg.vocab)
+        self.tok = WordPieceTokenizer(vocab)
+        words = [t[1:] for t in vocab if t.startswith("▁") and len(t) > 2]
+        rng = np.random.default_rng(200 + rank)
+        texts = []
+        for _ in range(batch):  # varlen documents of about seq/2 .. seq-2 word tokens
+            n = int(rng.integers(seq // 2, seq - 2))
+            texts.append(" ".join(words[int(i)] for i in rng.integers(0, len(words), size=n)))
+        self.max_tokens = seq
+        self.arena = HbmArena.create(f"e2e{os.getpid()}r{rank}", slots=max(4 * batch, 1024), max_val=4096,
+                                     embeddings=True)
+        self.keys = format_keys(batch, "txt", 9, 16)
+        V, L = pack_values(texts, 4096)
+        st = self.arena.set(self.keys, V, L)
+        st_l, _ = self.arena.meta("set_label", self.keys, torch.full((batch,), self.WAITING, dtype=torch.int64,
+                                                                     device="cuda"))
+        torch.cuda.synchronize()
+        assert int((st != 0).sum()) == 0 and int((st_l != 0).sum()) == 0
+        self.mask = torch.full((batch,), self.WAITING, dtype=torch.int64, device="cuda")
+        self.shard = GpuShard(self.arena)
+        self.docs = batch
+        self.host_rows = torch.empty((batch, 4096), dtype=torch.uint8, pin_memory=True)
+        self.host_lens = torch.empty(batch, dtype=torch.int32, pin_memory=True)
+        self.out = torch.empty((batch, 768), dtype=torch.float32, device="cuda")
+        self.tokens = 0
+        self.failures = 0
+
+    def run(self):
+        st, rows, lens = self.arena.get(self.keys)
+        self.host_rows.copy_(rows, non_blocking=True)
+        self.host_lens.copy_(lens, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        hr, hl = self.host_rows.numpy(), self.host_lens.numpy()
+        texts = [hr[i, : hl[i]].tobytes() for i in range(self.docs)]
+        ids, offs, _ = self.tok.encode_batch(texts, self.max_tokens)
+        b = Batch([ids[offs[i]: offs[i + 1]] for i in range(self.docs)])
+        self.tokens = int(b.T)
+        st_f, slots = self.arena.meta("find", self.keys)
+        hashes = self.shard.hash_keys(self.keys)
+        _, status = self.enc.embed(b, arena=self.arena, slots=slots, hashes=hashes, out=self.out)
+        self.arena.meta("unset_label", self.keys, self.mask)
+        self.arena.meta("set_label", self.keys, self.mask)  # the producer re-arms the documents
+        return status
+
+    def close(self):
+        self.arena.close()

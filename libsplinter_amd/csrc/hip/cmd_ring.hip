@@ -120,10 +120,15 @@ __device__ int32_t ring_get(const Arena& a, const Key& k, uint8_t* hp, uint32_t 
   if (ald64_acq(s + kOffEpoch) != e1) return kAgain;  // acquire: this CU's L1 holds no stale value line
   *out_len = L;
   if (L > cap) return kMsgSize;
+  // the value loads complete before their bytes are stored (data dependency) and the epoch
+  // re-check is issued after those stores, so the seqlock order holds without draining the
+  // host-bound stores here: the one drain before the DONE doorbell covers them
   if (L) push(hp, (const uint4*)a.value((size_t)idx), (L + 15) >> 4);
-  drain();
   return (slot_epoch(s) == e1 && slot_hash(s) == k.hash) ? kOk : kAgain;
 }
+
+__device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32_t sub, uint32_t len, uint32_t cap,
+                               uint64_t arg, uint8_t* hp, uint8_t* pay, uint32_t* out_len, uint64_t* result);
 
 // one op of one lane; scratch = this entry's device staging row (payload)
 __device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t* pay, uint32_t* out_len,
@@ -160,14 +165,24 @@ __device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t
   }
   canon_key(k, 64);
   drain();  // the staged payload is in place before any op reads it
-  long idx = -1;
   *out_len = 0;
   *result = 0;
+  // set (write-through stores + drain) and get (acquire load of the epoch) carry their own
+  // cross-XCD ordering; every other op reads and writes the slot with plain accesses, and the
+  // next call may run on another wave on another XCD, whose L2 is not this one: acquire before
+  // (drop stale lines) and release after (write this L2 back), at agent scope
+  if (op == kRingSet) return ring_set(a, k, pay, len);
+  if (op == kRingGet) return ring_get(a, k, hp, cap, out_len);
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int32_t rc = serve_plain(a, k, op, sub, len, cap, arg, hp, pay, out_len, result);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  return rc;
+}
+
+__device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32_t sub, uint32_t len, uint32_t cap,
+                               uint64_t arg, uint8_t* hp, uint8_t* pay, uint32_t* out_len, uint64_t* result) {
+  long idx = -1;
   switch (op) {
-    case kRingSet:
-      return ring_set(a, k, pay, len);
-    case kRingGet:
-      return ring_get(a, k, hp, cap, out_len);
     case kRingUnset:
       return unset_op(a, k, &idx);
     case kRingAppend: {
@@ -292,9 +307,16 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
   const bool mine = lane < kGroupEntries;
   const int e = g * kGroupEntries + (mine ? lane : 0);
   uint64_t last = wall_clock64();
+  uint32_t idle = 0;
   for (;;) {
     const bool ready = mine && ld32s(&sh->state[e]) == kRingReady;
     if (__ballot(ready) == 0) {  // wave-uniform
+      // an idle poll is ONE system-scope read (the group's doorbells); the stop flag, the shared
+      // activity clock and the idle timeout are checked every 32nd poll only
+      if ((++idle & 31) != 0) {
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
       if (ld32s(&sh->stop) != 0) break;
       u32x4c_t cl = ld16c(ctrl);
       vm_wait(cl);
@@ -308,14 +330,16 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
       continue;
     }
     last = wall_clock64();
+    idle = 0;
     if (lane == 0) ast64(ctrl, last);
     if (ready) {
       RingCmd* c = cmds + e;
       uint32_t out_len = 0;
       uint64_t result = 0;
       const int32_t st = serve(aa, c, payload + (size_t)e * pstride, scratch + (size_t)e * pstride, &out_len, &result);
-      st64s(&c->status, ((uint64_t)out_len << 32) | (uint32_t)st);  // status + out_len: one 8-B store
-      st64s(&c->result, result);
+      // status, out_len and result share one 16-B chunk of the record: one system-scope store,
+      // one drain (it also covers a get's payload stores) before the DONE doorbell
+      st16s(&c->status, u32x4s_t{(uint32_t)st, out_len, (uint32_t)result, (uint32_t)(result >> 32)});
       drain();
       st32s(&sh->state[e], kRingDone);
     }
@@ -348,6 +372,7 @@ int CmdRing::init(int device, uint32_t pstride) {
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
   idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
+  spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
   return 0;
 }
 
@@ -375,12 +400,21 @@ void CmdRing::launch(const spl_arena_t& a) {
 int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], const void* in,
                   uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap, RingResult* r) {
   if (in_len > pstride_) { errno = EMSGSIZE; return -1; }
-  // own an entry: start at a rotating ticket, CAS the host-only busy flag
-  uint32_t e = ticket_.fetch_add(1, std::memory_order_relaxed) % kRingEntries;
+  // own an entry: start at a rotating ticket, CAS the host-only busy flag.  Consecutive tickets
+  // map to different groups (entry = (t % groups) * per_group + t / groups), so concurrent
+  // callers land on different worker waves -- which run in parallel -- instead of sharing one
+  // wave whose lanes would serve them with divergent ops
+  const bool spread = spread_;
+  auto entry_of = [spread](uint32_t t) {
+    t %= kRingEntries;
+    return spread ? (t % kRingGroups) * kGroupEntries + t / kRingGroups : t;
+  };
+  uint32_t t = ticket_.fetch_add(1, std::memory_order_relaxed);
+  uint32_t e = entry_of(t);
   for (uint32_t spins = 0;; ++spins) {
     uint32_t z = 0;
     if (busy_[e].compare_exchange_weak(z, 1u, std::memory_order_acquire)) break;
-    e = (e + 1) % kRingEntries;
+    e = entry_of(++t);
     if ((spins & 63) == 63) _mm_pause();
   }
   RingCmd* c = cmds_ + e;

@@ -12,6 +12,12 @@
 //     with little op divergence inside a wave.  (One kernel, not one per group: streams share
 //     GPU_MAX_HW_QUEUES hardware queues, and a group queued behind another group's resident
 //     kernel would wait out that kernel's idle timeout.)
+// Host callers take entries in ticket order spread over the groups (consecutive calls land on
+// different waves, so up to kRingGroups concurrent callers are served in parallel waves, not
+// as divergent lanes of one wave): 1 thread p50 11.7 us, 16 threads 1.02 M ops/s at p50 14.9 us
+// (profiles/r2_hostapi_ring_v2.jsonl).  Ops other than set / get touch slots with plain
+// accesses, so the worker brackets them with agent-scope acquire / release: the next call may
+// run on another XCD.
 // The worker exits after SPLINTER_RING_IDLE_US without any call (default 5000 µs; the activity
 // clock is shared by the groups through device memory, and the first group to time out tells
 // the others to exit, so no group outlives the rest) or on stop: a process that stops issuing
@@ -28,6 +34,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <atomic>
+#include <cstddef>
 #include <cstdint>
 #include <mutex>
 
@@ -54,15 +61,18 @@ enum RingState : uint32_t { kRingFree = 0, kRingReady = 1, kRingDone = 2 };
 struct alignas(128) RingCmd {
   uint32_t op, sub, len, cap;  // cap: payload capacity for outputs
   uint64_t arg;
+  uint64_t pad0;
   int32_t status;              // device status (0 / -EAGAIN / -ENOENT / ...; unset: old length)
-  uint32_t out_len;
+  uint32_t out_len;            // status, out_len, result: one 16-B chunk (one device store)
   uint64_t result;
-  uint64_t pad[3];
+  uint64_t pad[2];
   char key[64];                // NUL-padded key record
 };
 static_assert(sizeof(RingCmd) == 128, "ring record");
+static_assert(offsetof(RingCmd, status) % 16 == 0 && offsetof(RingCmd, result) == offsetof(RingCmd, status) + 8,
+              "the completion words must form one 16-B chunk");
 
-constexpr int kRingGroups = 8;                      // independent one-wave workers
+constexpr int kRingGroups = 32;                     // independent one-wave workers (one per concurrent caller up to 32)
 constexpr int kGroupEntries = 8;                    // entries per worker (lanes 0..7)
 constexpr int kRingEntries = kRingGroups * kGroupEntries;
 
@@ -103,6 +113,7 @@ class CmdRing {
   uint32_t pstride_ = 0;
   int device_ = 0;
   uint64_t idle_ticks_ = 0;
+  bool spread_ = true;            // SPLINTER_RING_SPREAD: consecutive calls on different waves
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;
   std::atomic<uint32_t> busy_[kRingEntries] = {};

@@ -29,6 +29,8 @@ CPU (tests/test_sharded_gloo.py) and runs unchanged on RCCL.
 """
 from __future__ import annotations
 
+import itertools
+
 import os
 
 from typing import List, Optional, Tuple
@@ -107,8 +109,38 @@ class _Coll:
             for p0 in range(0, ib.shape[1], step):
                 p1 = min(ib.shape[1], p0 + step)
                 dist.all_to_all([ob[d, p0:p1] for d in range(w)], [ib[d, p0:p1] for d in range(w)], group=self.group)
+        elif out_splits is not None and out.is_cuda and inp.dim() >= 1:
+            self._all_to_all_uneven(out, inp, list(out_splits), list(in_splits))
         else:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+
+    def _all_to_all_uneven(self, out, inp, out_splits, in_splits):
+        """Uneven all-to-all (the _route path) in parts of <= A2A_CHUNK_BYTES per call, like the
+        equal-split case.  Whether to split must be decided identically on every rank (each call
+        is a collective), so the largest segment of any rank is agreed with one small all-reduce;
+        part p moves rows [p*step, (p+1)*step) of every segment."""
+        w = dist.get_world_size(self.group)
+        row = inp[0].numel() * inp.element_size() if inp.shape[0] else out[0].numel() * out.element_size() \
+            if out.shape[0] else 1
+        m = torch.tensor([max(in_splits + [0]), max(out_splits + [0])], dtype=torch.int64, device=out.device)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
+        mx = int(m.max().item())
+        if mx * row * w <= A2A_CHUNK_BYTES:
+            dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
+            return
+        step = max(1, A2A_CHUNK_BYTES // (w * row))
+        ioff = [0] + list(itertools.accumulate(in_splits))
+        ooff = [0] + list(itertools.accumulate(out_splits))
+        for p0 in range(0, mx, step):
+            ins = [inp[ioff[d] + min(p0, in_splits[d]): ioff[d] + min(p0 + step, in_splits[d])] for d in range(w)]
+            outs = [out[ooff[d] + min(p0, out_splits[d]): ooff[d] + min(p0 + step, out_splits[d])] for d in range(w)]
+            # one all_to_all_single per part on packed copies (<= A2A_CHUNK_BYTES each)
+            pout = torch.empty((sum(o.shape[0] for o in outs),) + tuple(out.shape[1:]), dtype=out.dtype,
+                               device=out.device)
+            dist.all_to_all_single(pout, torch.cat(ins), [o.shape[0] for o in outs], [i.shape[0] for i in ins],
+                                   group=self.group)
+            for o, part in zip(outs, pout.split([o.shape[0] for o in outs])):
+                o.copy_(part)
 
     def all_reduce(self, t, op=dist.ReduceOp.SUM):
         h = self._h(t)

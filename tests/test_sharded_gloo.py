@@ -258,3 +258,56 @@ def test_routed_kv_gloo(world, uniq):
                 p.kill()
     for r in range(world):
         assert res.get(r) == "ok", res.get(r)
+
+
+def _a2a_worker(rank, world, port, q):
+    """_Coll._all_to_all_uneven (the RCCL path's chunked uneven all-to-all) on gloo CPU tensors
+    with a tiny chunk size: every part boundary case (empty segments, segments shorter / longer
+    than a part) against one all_to_all_single."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import libsplinter_amd.parallel.sharded as S
+        S.A2A_CHUNK_BYTES = 3 * 40 * world  # 3 rows of 40 B per destination per part
+        rng = np.random.default_rng(rank)
+        # send splits: row counts per destination; rank r sends (r + d) % 4 * 3 + d rows to d
+        send = [((rank + d) % 4) * 3 + d for d in range(world)]
+        allsend = [[((r + d) % 4) * 3 + d for d in range(world)] for r in range(world)]
+        recv = [allsend[r][rank] for r in range(world)]
+        inp = torch.from_numpy(rng.integers(0, 256, size=(sum(send), 40), dtype=np.uint8))
+        ref = torch.empty((sum(recv), 40), dtype=torch.uint8)
+        dist.all_to_all_single(ref, inp, recv, send)
+        c = S._Coll(None)
+        out = torch.full((sum(recv), 40), 7, dtype=torch.uint8)
+        c._all_to_all_uneven(out, inp, recv, send)
+        assert torch.equal(out, ref), "chunked uneven all-to-all differs"
+        q.put((rank, "ok"))
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_chunked_uneven_all_to_all_gloo(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_a2a_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=120)
+            res[r] = msg
+            if msg != "ok":
+                break
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert res.get(r) == "ok", res.get(r)

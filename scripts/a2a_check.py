@@ -28,6 +28,14 @@ def main():
         else:
             dist.all_to_all_single(y, x)
         torch.cuda.synchronize()
+        if CHUNKED and world == 1:  # the uneven-split (_route) form through the same chunking
+            y2 = torch.empty_like(x)
+            _Coll(None).all_to_all(y2, x, [n], [n])
+            torch.cuda.synchronize()
+            nb = int((y2 != x).sum())
+            print(f"chunked-uneven {mb} MiB: mismatching bytes {nb}", flush=True)
+            bad += nb
+            del y2
         # world == 1: y must equal x
         ref = x if world == 1 else None
         if ref is not None:

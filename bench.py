@@ -35,7 +35,7 @@ REF_MRMW_OPS = 15.6e6  # reference MRMW headline (README.md:131), BASELINE.md
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--mode", default="mixed", choices=["kv", "embed", "mixed"])
     p.add_argument("--keys-per-gpu", type=int, default=100_000_000)
@@ -67,6 +67,8 @@ def parse():
     p.add_argument("--dry-run", action="store_true",
                    help="launcher check without a GPU: every rank joins a gloo group, rank 0 prints the world "
                         "it sees as JSON and the run ends (tests/test_bench_cpu.py)")
+    p.add_argument("--throttle", type=int, default=1, choices=[0, 1],
+                   help="1: issue a step's KV launches only after the previous step's encoder finished")
     p.add_argument("--embed-e2e", type=int, default=5, metavar="STEPS",
                    help="after the timed loop, time STEPS end-to-end embedding batches of the splinference path "
                         "(text fetch, WordPiece, varlen batch, slot find, encoder + seqlocked write, labels); 0: off")
@@ -255,9 +257,18 @@ def main():
     _phase_gap_ms = float(os.environ.get("BENCH_PHASE_GAP_MS", "0"))
 
 
+    # Host submission throttle (--throttle): the next step's KV launches are issued only once
+    # this step's encoder has finished.  Work the host has queued on the other hardware queues --
+    # even when it is blocked on an event -- makes the queue scheduler time-slice the queue that
+    # runs the encoder (profiles/r2_hw_queues.md), so submitting early costs more than the few
+    # microseconds of launch latency it hides.
+    throttle_ev = [None]
+
     def step_local(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
         cur = torch.cuda.current_stream()
+        if args.throttle and throttle_ev[0] is not None:
+            throttle_ev[0].synchronize()
         kv_streams = w_streams[:len(set_parts)] + r_streams[:len(get_parts)]
         if kvs is not None and s_emb is None:
             kvs.step(arena, SK if n_set else None, SV if n_set else None, SL if n_set else None, s_status,
@@ -288,6 +299,8 @@ def main():
         if s_emb is not None and n_set:
             for s in kv_streams:
                 cur.wait_stream(s)
+        if args.throttle and embedder is not None:
+            throttle_ev[0] = cur.record_event()
 
     # N > 1: a host-sync-free software pipeline (parallel/routed.py).  Per step i:
     #   s_req : pack + request all-to-alls of batch i         (overlaps embed_i)

@@ -362,6 +362,12 @@ class NomicEncoder:
                                   ptr(ln[0]) if ln else None, ptr(ln[1]) if ln else None, ptr(part), _stream()),
              f"gemm_ln({mode})")
 
+    # The two residual projections (o-proj, down: N = 768) are plain C += A B^T GEMMs; hipBLASLt's
+    # beta = 1 epilogue in place beats the fused MFMA kernel on them (down 123.5 vs 175.5 us,
+    # o-proj 49.1 vs 54.4 at 32768 tokens: profiles/r2_residual_gemm_ab.jsonl), so they go to the
+    # library (NOMIC_RESIDUAL_BLAS=0: the MFMA kernel with the fused residual epilogue).  Every
+    # projection with a fused epilogue (RoPE, SwiGLU) stays on the hand-written kernels.
+    residual_blas = os.environ.get("NOMIC_RESIDUAL_BLAS", "1") != "0"
     # measured slower on MI355X (profiles/r2_encoder_ln_fold.md): opt in with NOMIC_LN_FOLD=1
     ln_fold = os.environ.get("NOMIC_LN_FOLD", "0") != "0"
 
@@ -424,12 +430,20 @@ class NomicEncoder:
             self._gemm(EPI_ROPE, x, lw["wqkv"], T, qkv, pos=b.pos)
             _chk(L.nomic_attention(qkv.data_ptr(), attn.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb,
                                    cfg.heads, scale, s), "attention")
-            self._gemm(EPI_RESIDUAL, attn, lw["wo"], T, h, res=x)
-            _chk(L.nomic_layernorm(h.data_ptr(), T, lw["ln1_g"].data_ptr(), lw["ln1_b"].data_ptr(), cfg.eps,
+            if self.residual_blas:  # x += attn Wo^T on hipBLASLt (a plain beta = 1 GEMM), LN in place
+                x[:T].addmm_(attn[:T], lw["wo"].t())
+                src = x
+            else:
+                self._gemm(EPI_RESIDUAL, attn, lw["wo"], T, h, res=x)
+                src = h
+            _chk(L.nomic_layernorm(src.data_ptr(), T, lw["ln1_g"].data_ptr(), lw["ln1_b"].data_ptr(), cfg.eps,
                                    x.data_ptr(), s), "ln1")
             self._gemm(EPI_SWIGLU, x, lw["wupgate"], T, ffn)
-            self._gemm(EPI_RESIDUAL, ffn, lw["wdown"], T, h, res=x)
-            _chk(L.nomic_layernorm(h.data_ptr(), T, lw["ln2_g"].data_ptr(), lw["ln2_b"].data_ptr(), cfg.eps,
+            if self.residual_blas:
+                x[:T].addmm_(ffn[:T], lw["wdown"].t())
+            else:
+                self._gemm(EPI_RESIDUAL, ffn, lw["wdown"], T, h, res=x)
+            _chk(L.nomic_layernorm(src.data_ptr(), T, lw["ln2_g"].data_ptr(), lw["ln2_b"].data_ptr(), cfg.eps,
                                    x.data_ptr(), s), "ln2")
         return x[:T]
 

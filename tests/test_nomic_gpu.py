@@ -263,8 +263,9 @@ def test_layernorm_and_embed(L0):
     assert _rel(out.float(), ref) < 5e-3
 
 
-@pytest.mark.parametrize("ln_fold", [True, False], ids=["ln_folded", "ln_kernels"])
-def test_encoder_matches_fp32_reference(ln_fold):
+@pytest.mark.parametrize("ln_fold,residual_blas", [(True, False), (False, False), (False, True)],
+                         ids=["ln_folded", "ln_kernels_mfma_residual", "ln_kernels_blas_residual"])
+def test_encoder_matches_fp32_reference(ln_fold, residual_blas):
     import torch
     from libsplinter_amd.models.nomic import (Batch, NomicConfig, NomicEncoder, NomicReference, NomicWeights,
                                               random_weights)
@@ -272,6 +273,7 @@ def test_encoder_matches_fp32_reference(ln_fold):
     w = random_weights(cfg, seed=5)
     enc = NomicEncoder(NomicWeights.from_numpy(cfg, w), max_tokens=4096)
     enc.ln_fold = ln_fold
+    enc.residual_blas = residual_blas
     rng = np.random.default_rng(0)
     seqs = [rng.integers(0, cfg.vocab, size=n).tolist() for n in (5, 40, 129, 300)]
     b = Batch(seqs)

@@ -26,7 +26,7 @@ HOST_LIBS := $(LIB)/libsplinter.so $(LIB)/libsplinter_p.so
 TOOLS     := $(patsubst $(SRC)/tools/%.cpp,$(BIN)/%,$(wildcard $(SRC)/tools/*.cpp)) \
              $(if $(wildcard $(SRC)/cli/*.cpp),$(BIN)/splinterctl)
 
-.PHONY: all host hip tools clean test tsan asan
+.PHONY: all host hip tools clean test tsan asan hip-variant
 all: host hip tools
 host: $(HOST_LIBS)
 hip: $(LIB)/libsplinter_hip.so
@@ -51,6 +51,16 @@ build/hip/nomic_kernels.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form -fno-honor-
 
 $(LIB)/libsplinter_hip.so: $(HIP_OBJS) $(LIB)/libsplinter.so | $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
+
+# A/B builds of the HIP backend for one process-level switch (SPLINTER_HIP_VARIANT=<V> loads
+# lib/libsplinter_hip_<V>.so): make hip-variant V=name VFLAGS="-DSOMETHING"
+hip-variant: $(LIB)/libsplinter.so | $(LIB)
+	mkdir -p build/hip_$(V)
+	for f in $(HIP_SRCS); do o=build/hip_$(V)/$$(basename $$f .hip).o; x=""; \
+	  case $$f in *nomic_kernels.hip) x="-mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans";; esac; \
+	  $(HIPCC) $(HIPFLAGS) $$x $(VFLAGS) -c -o $$o $$f || exit 1; done
+	$(HIPCC) $(HIPFLAGS) -shared -o $(LIB)/libsplinter_hip_$(V).so build/hip_$(V)/*.o -L$(LIB) -lsplinter \
+	  -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
 
 $(BIN)/%: $(SRC)/tools/%.cpp $(LIB)/libsplinter.so $(CORE_HDRS) | $(BIN)
 	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN/../lib' $(LDLIBS)

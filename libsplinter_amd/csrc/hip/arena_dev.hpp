@@ -445,14 +445,31 @@ __device__ Claim claim_set(const Arena& a, const KeyT<KW>& k) {
     uint8_t* s = a.slot(idx);
     // hash, epoch and key in ONE round trip of 16-B coherent loads (the key compare is speculative)
     u32x4c_t he = ld16c(s + kOffHash);
+#ifndef SPL_SET_RECHECK
+    // ... and the watcher mask / labels the set will pulse (same 128-B slot line)
+    u32x4c_t wc0 = ld16c(s + kOffWatch), ab0 = ld16c(s + kOffAtime);
+#endif
     KeyProbe<KW> kp;
     kp.issue(s, k);
     vm_wait(he);
+#ifndef SPL_SET_RECHECK
+    vm_wait(wc0, ab0);
+#endif
     kp.wait();
     const uint64_t sh = lo64(he), e = hi64(he);
     const bool keq = kp.eq(k);
     if (sh == k.hash && keq) {  // update in place
       if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return Claim{-1, false, kAgain};
+#ifndef SPL_SET_RECHECK
+      // No re-check round trip after the claim: hash and epoch came from ONE 16-B load, every
+      // change of the slot's hash or key happens under a claim that moves the epoch, so a CAS
+      // that still finds the epoch read with hash == k.hash proves the slot held this key for the
+      // whole window (a key compare against stale bytes can only fail, which sends the op down the
+      // insert path, whose re-validation finds the slot).  Watcher mask and labels change by
+      // atomics outside the seqlock (reference splinter.c:968-1003), so the probe-time values
+      // are as current as a re-read would be.  SPL_SET_RECHECK restores the round trip.
+      return Claim{(long)idx, false, kOk, lo64(wc0), hi64(ab0)};
+#endif
       // re-check after the claim: hash + key together, with the watcher mask and labels the
       // set will pulse (same 128-B slot line, same round trip)
       u32x4c_t h2 = ld16c(s + kOffHash), wc = ld16c(s + kOffWatch), ab = ld16c(s + kOffAtime);

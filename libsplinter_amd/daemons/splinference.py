@@ -67,6 +67,15 @@ class Splinference:
             store.shard_claim(SHARD_ID, 1, SHARD_PRIO_LIVE, SHARD_DUR_LIVE)
         except Exception:
             pass
+        # hbm: stores take the batched device path: one kernel per step for a whole batch of keys
+        # (epochs, text reads, slot lookup, vectors pooled into the slots under the seqlock, label
+        # updates) instead of several per-call ring round trips per key
+        self.arena = None
+        if getattr(store, "backend", None) == "hbm":
+            from ..ops.arena import HbmArena
+            from ..parallel.sharded import GpuShard
+            self.arena = HbmArena(store)
+            self.shard = GpuShard(self.arena)
 
     # ---------------------------------------------------------------- util --
     def _zero_vec(self, key: str) -> bool:
@@ -80,6 +89,8 @@ class Splinference:
                 self.processed[key] = self.store.epoch(key)
 
     def pending(self) -> List[str]:
+        if self.arena is not None:
+            return self._pending_hbm()
         out = []
         for key in self.store.list():
             e = self.store.epoch(key)
@@ -97,8 +108,77 @@ class Splinference:
                 out.append(key)
         return out
 
+    # ------------------------------------------------------- batched (hbm:) --
+    def _keys_u8(self, keys: List[str]):
+        from ..ops.arena import pack_keys
+        return pack_keys(keys, 64)
+
+    def _pending_hbm(self) -> List[str]:
+        names = [k for k in self.store.list()]
+        if not names:
+            return []
+        _, ep = self.arena.meta("epoch", self._keys_u8(names))
+        ep = ep.cpu().numpy()
+        return [k for k, e in zip(names, ep) if not (e & 1) and int(e) > self.processed.get(k, -1)]
+
+    def _read_hbm(self, keys: List[str]) -> Tuple[List[str], List[bytes], List[int]]:
+        """Seqlock-consistent batch read: epochs, values, epochs again (a key whose epoch moved or
+        is odd is skipped this round, as the reference's per-key check)."""
+        K = self._keys_u8(keys)
+        _, e0 = self.arena.meta("epoch", K)
+        st, rows, lens = self.arena.get(K)
+        _, e1 = self.arena.meta("epoch", K)
+        e0, e1, st, lens = e0.cpu().numpy(), e1.cpu().numpy(), st.cpu().numpy(), lens.cpu().numpy()
+        rows = rows.cpu().numpy()
+        trained = None
+        if self.vector_training:
+            _, vecs = self.arena.get_embeddings(K)
+            trained = (vecs.norm(dim=1) > 1e-6).cpu().numpy()
+        ks, texts, eps = [], [], []
+        for i, k in enumerate(keys):
+            if st[i] != 0 or (e0[i] & 1) or e0[i] != e1[i]:
+                continue
+            if trained is not None and trained[i]:
+                self.stats["skipped_trained"] += 1
+                self.processed[k] = int(e0[i])
+                continue
+            ks.append(k)
+            texts.append(rows[i, : lens[i]].tobytes().split(b"\0", 1)[0])
+            eps.append(int(e0[i]))
+        return ks, texts, eps
+
+    def _run_hbm(self, idx: List[int], ks, eps, ids, offs) -> int:
+        """Encoder + mean pool written straight into the keys' slots under the seqlock (k_pool,
+        which also checks the slot still holds the key), then the +2 epoch check and the WAITING
+        label cleared for the keys that passed it -- all batched."""
+        import torch
+        from ..models.nomic import Batch
+        b = Batch([ids[offs[i]: offs[i + 1]] for i in idx])
+        names = [ks[i] for i in idx]
+        K = self._keys_u8(names)
+        _, slots = self.arena.meta("find", K)
+        hashes = self.shard.hash_keys(K)
+        _, status = self.enc.embed(b, normalize=self.normalize, arena=self.arena, slots=slots, hashes=hashes)
+        _, post = self.arena.meta("epoch", K)
+        status, post = status.cpu().numpy(), post.cpu().numpy()
+        self.stats["batches"] += 1
+        ok_rows = []
+        for j, i in enumerate(idx):
+            if status[j] != 0 or int(post[j]) != eps[i] + 2:  # stale-race detection (reference :282-286)
+                self.stats["stale"] += 1
+                continue
+            self.processed[ks[i]] = int(post[j])
+            ok_rows.append(j)
+        if ok_rows:
+            sel = torch.tensor(ok_rows, device=K.device)
+            self.arena.meta("unset_label", K[sel],
+                            torch.full((len(ok_rows),), WAITING_LABEL, dtype=torch.int64, device=K.device))
+        return len(ok_rows)
+
     # ------------------------------------------------------------ embedding --
     def _read(self, keys: List[str]) -> Tuple[List[str], List[bytes], List[int]]:
+        if self.arena is not None:
+            return self._read_hbm(keys)
         ks, texts, eps = [], [], []
         for k in keys:
             e1 = self.store.epoch(k)
@@ -161,11 +241,16 @@ class Splinference:
                 ntok += n
         # ctime backfill: wall time minus processing ticks (reference :530-537)
         now_s, dt = int(time.time()), self._ticks() - tick0
-        for i in good:
-            try:
-                self.store.set_time(ks[i], 0, now_s, 0)
-            except Exception:  # noqa: BLE001
-                pass
+        if self.arena is not None and good:
+            import torch
+            K = self._keys_u8([ks[i] for i in good])
+            self.arena.meta("ctime", K, torch.full((len(good),), now_s, dtype=torch.int64, device=K.device))
+        else:
+            for i in good:
+                try:
+                    self.store.set_time(ks[i], 0, now_s, 0)
+                except Exception:  # noqa: BLE001
+                    pass
         self.store.pulse(LANE_KEY)
         self.stats["embedded"] += done
         log(f"embedded {done}/{len(ks)} keys in {time.time() - t_start:.3f}s (ticks {dt})")
@@ -177,6 +262,8 @@ class Splinference:
         return now()
 
     def _run(self, idx: List[int], ks, eps, ids, offs) -> int:
+        if self.arena is not None:
+            return self._run_hbm(idx, ks, eps, ids, offs)
         import torch
         from ..models.nomic import Batch
         seqs = [ids[offs[i]: offs[i + 1]] for i in idx]

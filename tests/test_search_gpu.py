@@ -75,6 +75,34 @@ def test_splinference_daemon_oneshot(uniq):
         unlink(uniq)
 
 
+def test_splinference_daemon_oneshot_hbm(uniq):
+    """The same daemon contract on an hbm: store attached from the daemon's process: the batched
+    device path (epochs, value reads, slot find, vectors pooled into the slots under the seqlock,
+    +2 epoch check, WAITING cleared, ctime) instead of per-key calls."""
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=256, max_val=8192, embeddings=True)
+    try:
+        for i in range(20):
+            s.set(f"doc{i}", f"the vector store document number {i} about search")
+            s.set_type(f"doc{i}", 1 << 7)
+            s.set_label(f"doc{i}", 0x1 | 0x40)
+        s.set("huge", "a " * 2000)
+        r = subprocess.run([sys.executable, "-m", "libsplinter_amd.daemons.splinference", "--oneshot",
+                            "--random-init", "--layers", "2", f"hbm:{uniq}", "none.gguf", "3"],
+                           cwd=ROOT, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stderr[-3000:]
+        for i in range(20):
+            v = s.get_embedding(f"doc{i}")
+            assert v is not None and np.linalg.norm(v) > 0
+            snap = s.snapshot(f"doc{i}")
+            assert not (snap["bloom"] & 0x40)
+        assert s.snapshot("huge")["bloom"] & 0x80
+        assert s.get("huge").startswith(b"CONTEXT_EXCEEDED")
+        assert "embedded 20/21" in r.stderr or "embedded 20/" in r.stderr, r.stderr[-2000:]
+    finally:
+        s.close()
+
+
 def _clustered(n, g, centers=64, noise=0.35):
     import torch
     c = torch.randn(centers, 768, generator=g)

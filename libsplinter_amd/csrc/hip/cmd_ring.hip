@@ -51,6 +51,19 @@ __device__ __forceinline__ void st64s(void* p, uint64_t v) {
   __hip_atomic_store((uint64_t*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// doorbell reads kept in flight by the worker's idle loop (inline asm: hipcc does not count them,
+// each is retired by an explicit wait that ties its register)
+constexpr int kPollGap = 16;  // s_sleep units (64 clocks) between the first reads: ~0.4 us
+__device__ __forceinline__ uint32_t ld32s_issue(const void* p) {
+  uint32_t r;
+  asm volatile("global_load_dword %0, %1, off sc0 sc1" : "=v"(r) : "v"(p) : "memory");
+  return r;
+}
+__device__ __forceinline__ void wait_oldest_of4(uint32_t& r) { asm volatile("s_waitcnt vmcnt(3)" : "+v"(r)::"memory"); }
+__device__ __forceinline__ void drain_polls(uint32_t& a, uint32_t& b, uint32_t& c, uint32_t& d) {
+  asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b), "+v"(c), "+v"(d)::"memory");
+}
+
 // host payload -> device scratch, chunks [from, n16) (8 loads in flight)
 __device__ void pull(uint4* dst, const uint8_t* src, uint32_t from, uint32_t n16) {
   for (uint32_t b = from; b < n16; b += 8) {
@@ -83,48 +96,116 @@ __device__ __forceinline__ void count_mutation(const Arena& a, long idx) {
   notify_host(a);
 }
 
+#ifdef SPL_RING_STAMPS
+__device__ uint64_t g_ts[kRingEntries][5];  // this call's op checkpoints (serving lane only)
+__device__ int g_ent[64 * kRingGroups];     // entry of the serving lane
+#define RING_TS(i) (g_ts[g_ent[blockIdx.x * 64 + threadIdx.x]][i] = wall_clock64())
+#else
+#define RING_TS(i) ((void)0)
+#endif
+
 constexpr uint32_t kSpec = 16;  // payload chunks fetched speculatively with the record (256 B)
+
+// A value of at most kSpec chunks arrives in registers with the record (serve's speculative
+// payload loads): it is written from there, with no staging row in device memory.
+struct Spec {
+  u32x4s_t c[kSpec];
+};
 
 // SET for one lane: claim, payload with write-through (sc1) stores, drain, publish -- no L2
 // write-back fence on this latency path (MO 3 of arena_dev.hpp; readers are unchanged).  A value
 // row that is not a multiple of 16 B ends in bytewise plain stores: those take the release path.
-__device__ int32_t ring_set(const Arena& a, const Key& k, const uint8_t* pay, uint32_t len) {
+// reg: the value is in sp (len <= kSpec * 16, max_val a multiple of 16); else in the staged row.
+__device__ __forceinline__ int32_t ring_set(const Arena& a, const Key& k, const uint8_t* pay, const Spec& sp,
+                                            bool reg, uint32_t len, bool scrub, bool hybrid) {
   if (len == 0 || len > a.max_val) return kMsgSize;
-  bool hybrid;
-  const bool scrub = scrub_flags(a, hybrid);
+  RING_TS(1);
   const Claim c = claim_set(a, k);
+  RING_TS(2);
   if (c.rc != kOk) return c.rc;
-  if (a.max_val & 15) {
+  if (reg) {
+    uint4* dst = (uint4*)a.value((size_t)c.idx);
+    const uint32_t n16 = (len + 15) >> 4;
+#pragma unroll
+    for (uint32_t q = 0; q < kSpec; ++q) {
+      if (q < n16) {
+        uint4 t = make_uint4(sp.c[q].x, sp.c[q].y, sp.c[q].z, sp.c[q].w);
+        if (q == n16 - 1 && (len & 15)) {
+          const int r = (int)(len & 15);
+          t.x &= keep_mask(r); t.y &= keep_mask(r - 4); t.z &= keep_mask(r - 8); t.w &= keep_mask(r - 12);
+        }
+        st16_wt(dst + q, t);
+      }
+    }
+    if (scrub) {  // the mop of write_value: zeros to the 64-B boundary (hybrid) or to max_val
+      uint32_t end = hybrid ? ((len + 63u) & ~63u) : a.max_val;
+      if (end > a.max_val) end = a.max_val;
+      for (uint32_t done = n16 << 4; done + 16 <= end; done += 16) st16_wt(dst + (done >> 4), make_uint4(0, 0, 0, 0));
+    }
+    write_meta<3>(a, c, len);
+    drain();
+  } else if (a.max_val & 15) {
     write_set<0>(a, c, pay, len, scrub, hybrid);
     release();
   } else {
     write_set<3>(a, c, pay, len, scrub, hybrid);
     drain();
   }
+  RING_TS(3);
   finish_set(a, c);
   pulse_masks(a, c.wm, c.bl);
   count_mutation(a, c.idx);
+  RING_TS(4);
   return kOk;
 }
 
 // GET for one lane straight into the host payload: one-round-trip probe, acquire, copy
 // (arena -> host, system-scope stores), then the seqlock re-check; on EAGAIN the host ignores
 // the bytes it may have received.
-__device__ int32_t ring_get(const Arena& a, const Key& k, uint8_t* hp, uint32_t cap, uint32_t* out_len) {
+__device__ __forceinline__ int32_t ring_get(const Arena& a, const Key& k, uint8_t* hp, uint32_t cap, uint32_t* out_len) {
   uint64_t e1 = 0;
   uint32_t L = 0;
+  RING_TS(1);
   const long idx = locate_peek(a, k, &e1, &L);
+  RING_TS(2);
   if (idx < 0) return kNoEnt;
   if ((e1 & 1) || L == kInsertMark) return kAgain;
   const uint8_t* s = a.slot((size_t)idx);
   if (ald64_acq(s + kOffEpoch) != e1) return kAgain;  // acquire: this CU's L1 holds no stale value line
+  RING_TS(3);
   *out_len = L;
   if (L > cap) return kMsgSize;
+#ifdef SPL_RING_GET_REGS
+  if (L <= kSpec * 16) {
+    // (measured variant: profiles/r2_hostapi_ring_v3.md -- 1 µs lower single-thread get latency,
+    // 20 % fewer ops/s at 16-24 host threads than the copy below, so not the default)
+    // value into registers, THEN the (hash, epoch) re-check in one 16-B load, then the host
+    // stores: the re-check waits on no host-bound store and the value costs one round trip
+    const uint32_t n16 = (L + 15) >> 4;
+    const uint4* src = (const uint4*)a.value((size_t)idx);
+    u32x4c_t v[kSpec];
+#pragma unroll
+    for (uint32_t q = 0; q < kSpec; ++q) v[q] = q < n16 ? ld16c(src + q) : u32x4c_t{0u, 0u, 0u, 0u};
+#pragma unroll
+    for (uint32_t q = 0; q < kSpec; ++q) vm_wait(v[q]);
+    u32x4c_t re = ld16c(s + kOffHash);
+    vm_wait(re);
+    const bool ok = lo64(re) == k.hash && hi64(re) == e1;
+    RING_TS(4);
+    if (!ok) return kAgain;
+#pragma unroll
+    for (uint32_t q = 0; q < kSpec; ++q)
+      if (q < n16) st16s(hp + 16 * q, u32x4s_t{v[q].x, v[q].y, v[q].z, v[q].w});
+    return kOk;
+  }
+#endif
   // the value loads complete before their bytes are stored (data dependency) and the epoch
   // re-check is issued after those stores, so the seqlock order holds without draining the
   // host-bound stores here: the one drain before the DONE doorbell covers them
   if (L) push(hp, (const uint4*)a.value((size_t)idx), (L + 15) >> 4);
-  return (slot_epoch(s) == e1 && slot_hash(s) == k.hash) ? kOk : kAgain;
+  const bool ok = slot_epoch(s) == e1 && slot_hash(s) == k.hash;
+  RING_TS(4);
+  return ok ? kOk : kAgain;
 }
 
 __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32_t sub, uint32_t len, uint32_t cap,
@@ -132,46 +213,73 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
 
 // one op of one lane; scratch = this entry's device staging row (payload)
 __device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t* pay, uint32_t* out_len,
-                         uint64_t* result) {
-  // ONE round of system-scope loads: record header (32 B), key (64 B) and the first kSpec
-  // payload chunks (speculative: the length is in the header)
-  u32x4s_t h0 = ld16s(c), h1 = ld16s((const uint8_t*)c + 16);
-  u32x4s_t kk[4], pp[kSpec];
+                         uint64_t* result, uint64_t* t_loaded) {
+  // the two header words every op needs (event-bus owner, mop flags) are loaded first, so their
+  // device round trip overlaps the record's host round trip below
+  const splinter_header* H = (const splinter_header*)aa.base;
+  const uint32_t owner = __hip_atomic_load(&H->event_bus.owner_pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint8_t cflags = ald8(&H->core_flags);
+  // ONE round of system-scope loads: record header (32 B + key length), key (64 B) and the
+  // first kSpec payload chunks (speculative: the length is in the header)
+  u32x4s_t h0 = ld16s(c), h1 = ld16s((const uint8_t*)c + 16), h3 = ld16s((const uint8_t*)c + 48);
+  u32x4s_t kk[4];
+  Spec sp;
 #pragma unroll
   for (int q = 0; q < 4; ++q) kk[q] = ld16s(c->key + 16 * q);
 #pragma unroll
-  for (uint32_t q = 0; q < kSpec; ++q) pp[q] = ld16s(hp + 16 * q);
+  for (uint32_t q = 0; q < kSpec; ++q) sp.c[q] = ld16s(hp + 16 * q);
   sys_wait(h0);
   sys_wait(h1);
+  sys_wait(h3);
 #pragma unroll
   for (int q = 0; q < 4; ++q) sys_wait(kk[q]);
 #pragma unroll
-  for (uint32_t q = 0; q < kSpec; ++q) sys_wait(pp[q]);
+  for (uint32_t q = 0; q < kSpec; ++q) sys_wait(sp.c[q]);
   const uint32_t op = h0.x, sub = h0.y, len = h0.z, cap = h0.w;
+#ifdef SPL_RING_STAMPS
+  *t_loaded = wall_clock64();
+  g_ts[g_ent[blockIdx.x * 64 + threadIdx.x]][0] = *t_loaded;
+#else
+  (void)t_loaded;
+#endif
   const uint64_t arg = ((uint64_t)h1.y << 32) | h1.x;
+  Arena a;
+  a.base = (uint8_t*)aa.base;
+  a.slots = aa.slots;
+  a.max_val = aa.max_val;
+  a.stride = aa.stride;
+  a.notify = aa.notify;
+  a.flags = aa.flags | (owner != 0 ? 1u : 0u);  // from_api(), with the owner word loaded above
+  const bool scrub = (cflags & SPL_SYS_AUTO_SCRUB) != 0, hybrid = (cflags & SPL_SYS_HYBRID_SCRUB) != 0;
   const bool has_in = op == kRingSet || op == kRingAppend || op == kRingEmbedSet || op == kRingWrite;
-  if (has_in) {
+#ifdef SPL_RING_SET_STAGED
+  const bool reg = false;
+#else
+  const bool reg = op == kRingSet && len <= kSpec * 16 && (a.max_val & 15) == 0;
+#endif
+  if (has_in && !reg) {
     const uint32_t n16 = (len + 15) >> 4;
 #pragma unroll
     for (uint32_t q = 0; q < kSpec; ++q)
-      if (q < n16) ((uint4*)pay)[q] = make_uint4(pp[q].x, pp[q].y, pp[q].z, pp[q].w);
+      if (q < n16) ((uint4*)pay)[q] = make_uint4(sp.c[q].x, sp.c[q].y, sp.c[q].z, sp.c[q].w);
     if (n16 > kSpec) pull((uint4*)pay, hp, kSpec, n16);
+    drain();  // the staged payload is in place before any op reads it
   }
-  const Arena a = from_api(aa);
+  // the key is canonical with its hash computed by the host (KeyRef)
   Key k;
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     k.w[4 * q] = kk[q].x; k.w[4 * q + 1] = kk[q].y; k.w[4 * q + 2] = kk[q].z; k.w[4 * q + 3] = kk[q].w;
   }
-  canon_key(k, 64);
-  drain();  // the staged payload is in place before any op reads it
+  k.len = h3.x < 63u ? h3.x : 63u;
+  k.hash = ((uint64_t)h1.w << 32) | h1.z;
   *out_len = 0;
   *result = 0;
   // set (write-through stores + drain) and get (acquire load of the epoch) carry their own
   // cross-XCD ordering; every other op reads and writes the slot with plain accesses, and the
   // next call may run on another wave on another XCD, whose L2 is not this one: acquire before
   // (drop stale lines) and release after (write this L2 back), at agent scope
-  if (op == kRingSet) return ring_set(a, k, pay, len);
+  if (op == kRingSet) return ring_set(a, k, pay, sp, reg, len, scrub, hybrid);
   if (op == kRingGet) return ring_get(a, k, hp, cap, out_len);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int32_t rc = serve_plain(a, k, op, sub, len, cap, arg, hp, pay, out_len, result);
@@ -306,17 +414,54 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
   const int lane = threadIdx.x, g = blockIdx.x;
   const bool mine = lane < kGroupEntries;
   const int e = g * kGroupEntries + (mine ? lane : 0);
+#ifdef SPL_RING_STAMPS
+  g_ent[g * 64 + lane] = e;
+#endif
   uint64_t last = wall_clock64();
   uint32_t idle = 0;
+  const uint32_t* door = &sh->state[e];
   for (;;) {
-    const bool ready = mine && ld32s(&sh->state[e]) == kRingReady;
+#ifndef SPL_RING_POLL4
+    const bool ready = mine && ld32s(door) == kRingReady;
+#else
+    // (measured variant, slower: profiles/r2_hostapi_ring_v3.md) 4 doorbell reads in flight,
+    // issued ~1/4 of a host round trip apart, so a doorbell is seen one round trip + a fraction
+    // after the host rings it instead of 1.5 round trips on average -- but the reads still in
+    // flight must land before the op starts, which costs more than the earlier detection saves.
+    // vmcnt retires loads in issue order, so vmcnt(3) waits for exactly the oldest read.
+    uint32_t p0 = ld32s_issue(door);
+    __builtin_amdgcn_s_sleep(kPollGap);
+    uint32_t p1 = ld32s_issue(door);
+    __builtin_amdgcn_s_sleep(kPollGap);
+    uint32_t p2 = ld32s_issue(door);
+    __builtin_amdgcn_s_sleep(kPollGap);
+    uint32_t p3 = ld32s_issue(door);
+    bool ready = false;
+    for (int round = 0; round < 8; ++round) {
+      wait_oldest_of4(p0);
+      if (__ballot(mine && p0 == kRingReady)) { ready = mine && p0 == kRingReady; break; }
+      p0 = ld32s_issue(door);
+      wait_oldest_of4(p1);
+      if (__ballot(mine && p1 == kRingReady)) { ready = mine && p1 == kRingReady; break; }
+      p1 = ld32s_issue(door);
+      wait_oldest_of4(p2);
+      if (__ballot(mine && p2 == kRingReady)) { ready = mine && p2 == kRingReady; break; }
+      p2 = ld32s_issue(door);
+      wait_oldest_of4(p3);
+      if (__ballot(mine && p3 == kRingReady)) { ready = mine && p3 == kRingReady; break; }
+      p3 = ld32s_issue(door);
+    }
+    drain_polls(p0, p1, p2, p3);  // the reads still in flight land before anything else
+#endif
     if (__ballot(ready) == 0) {  // wave-uniform
-      // an idle poll is ONE system-scope read (the group's doorbells); the stop flag, the shared
-      // activity clock and the idle timeout are checked every 32nd poll only
+      // the stop flag, the shared activity clock and the idle timeout are checked every 32nd
+      // poll (every pipelined round of polls) only
+#ifndef SPL_RING_POLL4
       if ((++idle & 31) != 0) {
         __builtin_amdgcn_s_sleep(1);
         continue;
       }
+#endif
       if (ld32s(&sh->stop) != 0) break;
       u32x4c_t cl = ld16c(ctrl);
       vm_wait(cl);
@@ -330,17 +475,42 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
       continue;
     }
     last = wall_clock64();
+#ifdef SPL_RING_STAMPS
+    const uint64_t mt0 = __builtin_amdgcn_s_memtime();
+#endif
     idle = 0;
     if (lane == 0) ast64(ctrl, last);
     if (ready) {
       RingCmd* c = cmds + e;
       uint32_t out_len = 0;
-      uint64_t result = 0;
-      const int32_t st = serve(aa, c, payload + (size_t)e * pstride, scratch + (size_t)e * pstride, &out_len, &result);
+      uint64_t result = 0, t_loaded = 0;
+      const int32_t st =
+          serve(aa, c, payload + (size_t)e * pstride, scratch + (size_t)e * pstride, &out_len, &result, &t_loaded);
+#ifdef SPL_RING_STAMPS
+      const uint64_t t_op = wall_clock64();
+#endif
       // status, out_len and result share one 16-B chunk of the record: one system-scope store,
       // one drain (it also covers a get's payload stores) before the DONE doorbell
       st16s(&c->status, u32x4s_t{(uint32_t)st, out_len, (uint32_t)result, (uint32_t)(result >> 32)});
       drain();
+#ifdef SPL_RING_STAMPS
+      const uint64_t t_done = wall_clock64();
+      const uint64_t mt1 = __builtin_amdgcn_s_memtime();
+      st64s(sh->clk[e], ld64s(sh->clk[e]) + (mt1 - mt0));
+      st64s(sh->clk[e] + 1, ld64s(sh->clk[e] + 1) + (t_done - last));
+      uint64_t* sp = sh->stamp[e];
+      st64s(sp, ld64s(sp) + (t_loaded - last));
+      st64s(sp + 1, ld64s(sp + 1) + (t_op - t_loaded));
+      st64s(sp + 2, ld64s(sp + 2) + (t_done - t_op));
+      st64s(sp + 3, ld64s(sp + 3) + 1);
+      const uint32_t op = ld32s(&c->op);
+      if (st == 0 && (op == kRingSet || op == kRingGet)) {
+        uint64_t* q = sh->opstamp[e] + (op == kRingSet ? 0 : 5);
+        for (int i = 0; i < 4; ++i) st64s(q + i, ld64s(q + i) + (g_ts[e][i + 1] - g_ts[e][i]));
+        st64s(q + 4, ld64s(q + 4) + 1);
+      }
+      drain();
+#endif
       st32s(&sh->state[e], kRingDone);
     }
   }
@@ -371,6 +541,7 @@ int CmdRing::init(int device, uint32_t pstride) {
   std::memset(cmds_, 0, sizeof(RingCmd) * kRingEntries);
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+  clock_khz_ = khz > 0 ? khz : 100000;
   idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
   spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
   return 0;
@@ -397,8 +568,9 @@ void CmdRing::launch(const spl_arena_t& a) {
   if (cur != device_) (void)hipSetDevice(cur);
 }
 
-int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], const void* in,
-                  uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap, RingResult* r) {
+int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen,
+                  uint64_t khash, const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap,
+                  RingResult* r) {
   if (in_len > pstride_) { errno = EMSGSIZE; return -1; }
   // own an entry: start at a rotating ticket, CAS the host-only busy flag.  Consecutive tickets
   // map to different groups (entry = (t % groups) * per_group + t / groups), so concurrent
@@ -423,6 +595,8 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   c->len = in_len;
   c->cap = out_cap ? (out_cap < pstride_ ? out_cap : pstride_) : pstride_;
   c->arg = arg;
+  c->khash = khash;
+  c->klen = klen;
   if (key64) std::memcpy(c->key, key64, 64);
   if (in && in_len) std::memcpy(payload_ + (size_t)e * pstride_, in, in_len);
   __atomic_store_n(&shared_->state[e], (uint32_t)kRingReady, __ATOMIC_RELEASE);
@@ -464,6 +638,33 @@ void CmdRing::stop() {
 
 CmdRing::~CmdRing() {
   stop();
+#ifdef SPL_RING_STAMPS
+  if (shared_) {
+    uint64_t sum[4] = {0, 0, 0, 0};
+    for (int e = 0; e < kRingEntries; ++e)
+      for (int q = 0; q < 4; ++q) sum[q] += shared_->stamp[e][q];
+    if (sum[3]) {
+      const double us = 1000.0 / clock_khz_ / (double)sum[3];
+      fprintf(stderr,
+              "{\"ring_stamps\": %llu, \"seen_to_loaded_us\": %.3f, \"loaded_to_op_done_us\": %.3f, "
+              "\"op_done_to_drained_us\": %.3f}\n",
+              (unsigned long long)sum[3], sum[0] * us, sum[1] * us, sum[2] * us);
+    }
+    uint64_t ck[2] = {0, 0};
+    for (int e = 0; e < kRingEntries; ++e) ck[0] += shared_->clk[e][0], ck[1] += shared_->clk[e][1];
+    if (ck[1]) fprintf(stderr, "{\"shader_clock_mhz\": %.1f}\n", (double)ck[0] / ((double)ck[1] / (clock_khz_ * 1e3)) / 1e6);
+    uint64_t o[10] = {};
+    for (int e = 0; e < kRingEntries; ++e)
+      for (int q = 0; q < 10; ++q) o[q] += shared_->opstamp[e][q];
+    for (int k = 0; k < 2; ++k) {
+      const uint64_t* v = o + 5 * k;
+      if (!v[4]) continue;
+      const double us = 1000.0 / clock_khz_ / (double)v[4];
+      fprintf(stderr, "{\"op\": \"%s\", \"n\": %llu, \"seg_us\": [%.3f, %.3f, %.3f, %.3f]}\n", k ? "get" : "set",
+              (unsigned long long)v[4], v[0] * us, v[1] * us, v[2] * us, v[3] * us);
+    }
+  }
+#endif
   if (stream_) (void)hipStreamDestroy(stream_);
   if (ctrl_) (void)hipFree(ctrl_);
   if (scratch_) (void)hipFree(scratch_);

@@ -61,12 +61,13 @@ enum RingState : uint32_t { kRingFree = 0, kRingReady = 1, kRingDone = 2 };
 struct alignas(128) RingCmd {
   uint32_t op, sub, len, cap;  // cap: payload capacity for outputs
   uint64_t arg;
-  uint64_t pad0;
+  uint64_t khash;              // FNV-1a of the canonical key (host-computed: no hashing on the device)
   int32_t status;              // device status (0 / -EAGAIN / -ENOENT / ...; unset: old length)
   uint32_t out_len;            // status, out_len, result: one 16-B chunk (one device store)
   uint64_t result;
-  uint64_t pad[2];
-  char key[64];                // NUL-padded key record
+  uint32_t klen;               // canonical key length (<= 63)
+  uint32_t pad[3];
+  char key[64];                // canonical key record (NUL padded past klen)
 };
 static_assert(sizeof(RingCmd) == 128, "ring record");
 static_assert(offsetof(RingCmd, status) % 16 == 0 && offsetof(RingCmd, result) == offsetof(RingCmd, status) + 8,
@@ -82,6 +83,16 @@ struct RingShared {
   uint32_t stop;                 // ask the worker to exit
   uint32_t launches;             // host statistic
   uint32_t pad[13];
+#ifdef SPL_RING_STAMPS
+  // latency breakdown (make hip-variant V=stamps VFLAGS=-DSPL_RING_STAMPS): per entry, sums of
+  // wall-clock ticks from "doorbell seen" to "record loaded", to "op done", to "completion
+  // drained", and the call count; printed by ~CmdRing
+  uint64_t stamp[kRingEntries][4];
+  // finer split of the op itself: [0..3] set (prologue loads, claim, payload + drain, publish),
+  // [4] set count, [5..8] get (prologue loads, probe, acquire, copy + re-check), [9] get count
+  uint64_t opstamp[kRingEntries][10];
+  uint64_t clk[kRingEntries][2];  // shader-clock ticks (s_memtime) and wall ticks over the same calls
+#endif
 };
 
 struct RingResult {
@@ -99,8 +110,9 @@ class CmdRing {
   // Blocking call: stage key / input, ring the doorbell, wait for DONE.  `in` may be null;
   // `out` (may be null) receives min(out_len, out_cap) payload bytes.  Returns 0 when the op ran
   // (its own status in r.status), -1 on a ring failure (errno set; e.g. ETIMEDOUT).
-  int call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], const void* in, uint32_t in_len,
-           uint64_t arg, void* out, uint32_t out_cap, RingResult* r);
+  // key64 must be canonical (KeyRef: NUL padded past klen) with its FNV-1a hash in khash.
+  int call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen, uint64_t khash,
+           const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap, RingResult* r);
   void stop();
   uint32_t launches() const { return shared_ ? shared_->launches : 0; }
 
@@ -113,6 +125,7 @@ class CmdRing {
   uint32_t pstride_ = 0;
   int device_ = 0;
   uint64_t idle_ticks_ = 0;
+  int clock_khz_ = 100000;
   bool spread_ = true;            // SPLINTER_RING_SPREAD: consecutive calls on different waves
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;

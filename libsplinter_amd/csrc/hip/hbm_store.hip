@@ -418,14 +418,18 @@ class HbmStore final : public StoreBase {
   int ring(uint32_t op, uint32_t sub, const char* key, const void* in, uint32_t in_len, uint64_t arg, void* out,
            uint32_t out_cap, RingResult* r) {
     char k[64];
+    uint32_t klen = 0;
+    uint64_t khash = 0;
     if (key) {
       KeyRef kr(key);
       std::memcpy(k, kr.buf, 64);
+      klen = (uint32_t)kr.len;
+      khash = kr.hash;
     } else {
       std::memset(k, 0, 64);
     }
     if (!ring_.ready()) { errno = ENOSYS; return -1; }
-    return ring_.call(arena(), op, sub, k, in, in_len, arg, out, out_cap, r);
+    return ring_.call(arena(), op, sub, k, klen, khash, in, in_len, arg, out, out_cap, r);
   }
   static int st_ret(int32_t st) {
     if (st == 0) return 0;

@@ -290,12 +290,12 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // tiles past the block's last row are skipped, the diagonal tiles masked per score.  kv_heads <
 // heads: grouped-query attention, q head h reads kv head h / (heads / kv_heads); the qkv rows are
 // [q (heads) | k (kv_heads) | v (kv_heads)] x HD.
-template <int W, bool XR = false, bool OPT = false, bool CAUSAL = false>
+template <int W, bool XR = false, bool OPT = false, bool CAUSAL = false, int KT = 64>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1))) void k_attn2(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
                                                int heads, float scale_log2, int kv_heads) {
-  __shared__ __attribute__((aligned(16))) char lds[2][2][64 * 128];  // [buf][K | V][key * 128 B]
+  __shared__ __attribute__((aligned(16))) char lds[2][2][KT * 128];  // [buf][K | V][key * 128 B]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
   int qbi = blockIdx.x, head = blockIdx.y;
@@ -330,25 +330,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
     for (int qb = 0; qb < 2; ++qb) o[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
 
-  uint4 rk[2], rv[2];
-  // OPT: per-lane K/V source pointers of tile 0, advanced by 64 rows per tile
-  const uint16_t* kp[2];
-  const uint16_t* vp[2];
-#pragma unroll
-  for (int it = 0; it < 2; ++it) {
-    const int c = tid + it * 256, key = c >> 3, ch = c & 7;
-    kp[it] = Kg + (s0 + key) * ld + ch * 8;
-    vp[it] = Vg + (s0 + key) * ld + ch * 8;
-  }
-  const long tstride = 64 * ld;
+  constexpr int NL = KT / 32, KS = KT == 128 ? 7 : 6;  // uint4 loads per lane per tile; log2 KT
+  static_assert(KT == 64 || KT == 128, "key tile");
+  uint4 rk[NL], rv[NL];
+  // OPT: per-lane K/V source pointers of tile 0, advanced by KT rows per tile
+  // (lane load `it` sits 32 keys after load 0: a wave-uniform offset, so one pointer pair per lane)
+  const uint16_t* kp = Kg + (s0 + (tid >> 3)) * ld + (tid & 7) * 8;
+  const uint16_t* vp = Vg + (s0 + (tid >> 3)) * ld + (tid & 7) * 8;
+  const long tstride = KT * ld;
   auto gload = [&](long k0) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < NL; ++it) {
       const int c = tid + it * 256, key = c >> 3, ch = c & 7;
       if (k0 + key < len) {
         if constexpr (OPT) {
-          rk[it] = *(const uint4*)(kp[it] + (k0 >> 6) * tstride);
-          rv[it] = *(const uint4*)(vp[it] + (k0 >> 6) * tstride);
+          const long off = (k0 >> KS) * tstride + it * 32 * ld;
+          rk[it] = *(const uint4*)(kp + off);
+          rv[it] = *(const uint4*)(vp + off);
         } else {
           rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
           rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
@@ -361,29 +359,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
   };
   auto lwrite = [&](int buf) {
 #pragma unroll
-    for (int it = 0; it < 2; ++it) {
+    for (int it = 0; it < NL; ++it) {
       const int c = tid + it * 256, key = c >> 3, ch = c & 7;
       *(uint4*)(lds[buf][0] + key * 128 + (ksw(key, ch) << 4)) = rk[it];
       *(uint4*)(lds[buf][1] + key * 128 + (vsw(key, ch) << 4)) = rv[it];
     }
   };
 
-  int ntiles = (int)((len + 63) / 64);
-  if constexpr (CAUSAL) ntiles = min(ntiles, (int)((qstart + 128 + 63) / 64));
+  int ntiles = (int)((len + KT - 1) / KT);
+  if constexpr (CAUSAL) ntiles = min(ntiles, (int)((qstart + 128 + KT - 1) / KT));
   gload(0);
   lwrite(0);
   __syncthreads();
   const int tq = li >> 2, tp = li & 3;  // tr-read: this lane addresses row tq, columns 4*tp..4*tp+3
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
-    const long k0 = (long)t * 64;
-    if (t + 1 < ntiles) gload(k0 + 64);
+    const long k0 = (long)t * KT;
+    if (t + 1 < ntiles) gload(k0 + KT);
     const char* Ks = lds[buf][0];
     const char* Vs = lds[buf][1];
     // ---- S^T = K Q^T
-    f32x4 s[4][2];
+    f32x4 s[KT / 16][2];
 #pragma unroll
-    for (int kb = 0; kb < 4; ++kb) {
+    for (int kb = 0; kb < KT / 16; ++kb) {
       const int row = kb * 16 + li;
       bf16x8 kf[2];
 #pragma unroll
@@ -403,14 +401,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
     // exceeds it by more than kThr, so P <= 2^kThr and the O/l rescale is skipped on most tiles
     // (decided before this tile's P V, after the previous tile's: the textbook order).
     constexpr float kThr = 8.f;
-    const bool full = k0 + 64 <= len;
+    const bool full = k0 + KT <= len;
 #pragma unroll
     for (int qb = 0; qb < 2; ++qb) {
       if constexpr (CAUSAL) {
-        if (k0 + 63 > qstart) {  // a diagonal tile: keys after the query are masked
+        if (k0 + KT - 1 > qstart) {  // a diagonal tile: keys after the query are masked
           const long qrow = qstart + wave * 32 + qb * 16 + li;
 #pragma unroll
-          for (int kb = 0; kb < 4; ++kb)
+          for (int kb = 0; kb < KT / 16; ++kb)
 #pragma unroll
             for (int r = 0; r < 4; ++r)
               if (k0 + kb * 16 + 4 * g + r > qrow) s[kb][qb][r] = -1e30f;
@@ -418,14 +416,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
       }
       if (!full) {
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < KT / 16; ++kb)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
             if (k0 + kb * 16 + 4 * g + r >= len) s[kb][qb][r] = -1e30f;
       }
       float mx = -1e30f;
 #pragma unroll
-      for (int kb = 0; kb < 4; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][qb][0], s[kb][qb][1])), fmaxf(s[kb][qb][2], s[kb][qb][3]));
+      for (int kb = 0; kb < KT / 16; ++kb) mx = fmaxf(fmaxf(mx, fmaxf(s[kb][qb][0], s[kb][qb][1])), fmaxf(s[kb][qb][2], s[kb][qb][3]));
       if constexpr (OPT) {
         mx = xg_max(mx);
       } else {
@@ -447,7 +445,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
         const f32x2 sc2 = {scale_log2, scale_log2}, nm2 = {nm, nm};
         f32x2 acc2 = {0.f, 0.f};
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < KT / 16; ++kb)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
             f32x2 x = {s[kb][qb][2 * h], s[kb][qb][2 * h + 1]};
@@ -461,7 +459,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
         ps = xg_sum(acc2.x + acc2.y);
       } else {
 #pragma unroll
-        for (int kb = 0; kb < 4; ++kb)
+        for (int kb = 0; kb < KT / 16; ++kb)
 #pragma unroll
           for (int r = 0; r < 4; ++r) {
             const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][qb][r], scale_log2, nm));
@@ -475,7 +473,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
     }
     // ---- O^T += V^T P^T, two 32-key steps
 #pragma unroll
-    for (int st = 0; st < 2; ++st) {
+    for (int st = 0; st < KT / 32; ++st) {
       bf16x8 pf[2];
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb)
@@ -733,6 +731,12 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   else if (g_attn_variant == 6)
     hipLaunchKernelGGL((k_attn2<0, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
                        (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 7)  // 128-key tiles: half the barriers, 2x the MFMA work per sync
+    hipLaunchKernelGGL((k_attn2<0, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
+                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 8)  // 128-key tiles held to 2 waves/SIMD
+    hipLaunchKernelGGL((k_attn2<2, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
+                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 4)
     hipLaunchKernelGGL((k_attn2<0, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
                        cu, qblocks, heads, scale_log2, heads);

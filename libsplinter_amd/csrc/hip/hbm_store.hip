@@ -238,8 +238,25 @@ class HbmStore final : public StoreBase {
     return 0;
   }
   const void* raw_ptr(const char* key, size_t* out_sz, uint64_t* out_epoch) override {
-    // HBM is not host addressable: a seqlock-consistent host snapshot (thread-local, valid until
-    // this thread's next raw_ptr call) with the epoch it was read at (docs/DIVERGENCES.md)
+    // Zero-copy, as the reference (splinter.c:747-762): a host pointer into the value region
+    // through the CPU mapping of the arena's dmabuf chunks (VmmArena::host_map, PCIe BAR), with the
+    // slot's epoch and length from one ring snapshot; the caller re-checks the epoch.
+    if (uint8_t* hb = host_base()) {
+      uint8_t c[128];
+      RingResult r;
+      if (ring(kRingSnapshot, 0, key, nullptr, 0, 0, c, sizeof c, &r) != 0) return nullptr;
+      if (r.status != 0) { errno = neg_to_errno(r.status); return nullptr; }
+      uint64_t e;
+      uint32_t len;
+      std::memcpy(&e, c + kOffEpoch, 8);
+      std::memcpy(&len, c + kOffValLen, 4);
+      if (out_sz) *out_sz = len;
+      if (out_epoch) *out_epoch = e;
+      return hb + kHeaderBytes + geo_.slots_bytes() + r.result * (size_t)geo_.max_val;
+    }
+    // no host mapping (hipMalloc / IPC arena, or the driver refused the mmap): a seqlock-consistent
+    // host snapshot (thread-local, valid until this thread's next raw_ptr call) with the epoch it
+    // was read at (docs/DIVERGENCES.md)
     thread_local std::vector<uint8_t> snap;
     snap.resize(geo_.max_val + 1);
     for (int t = 0; t < 64; ++t) {
@@ -555,6 +572,16 @@ class HbmStore final : public StoreBase {
   bool owner_ = false;
   void* raw_ = nullptr;    // hipMalloc / IPC base, or the VMM range
   VmmArena vmm_;           // mode 1 (vmm_share.hpp)
+  // host view of the arena base (dbase_) through the dmabuf mapping, nullptr without one
+  uint8_t* host_base() {
+    if (!vmm_mode_ || getenv_flag_off("SPLINTER_HBM_HOST_MAP")) return nullptr;
+    uint8_t* h = (uint8_t*)vmm_.host_map();
+    return h ? h + ((uint8_t*)dbase_ - (uint8_t*)raw_) : nullptr;
+  }
+  static bool getenv_flag_off(const char* n) {
+    const char* e = getenv(n);
+    return e && !strcmp(e, "0");
+  }
   bool vmm_mode_ = false;
   void* dbase_ = nullptr;  // raw_ + kAlignOffset
   HbmDescriptor* desc_ = nullptr;

@@ -290,8 +290,8 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // tiles past the block's last row are skipped, the diagonal tiles masked per score.  kv_heads <
 // heads: grouped-query attention, q head h reads kv head h / (heads / kv_heads); the qkv rows are
 // [q (heads) | k (kv_heads) | v (kv_heads)] x HD.
-template <int W, bool XR = false, bool OPT = false, bool CAUSAL = false, int KT = 64>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1))) void k_attn2(
+template <int W, bool XR = false, bool OPT = false, bool CAUSAL = false, int KT = 64, int QW = 4>
+__global__ __launch_bounds__(64 * QW) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1))) void k_attn2(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
                                                int heads, float scale_log2, int kv_heads) {
@@ -330,21 +330,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
     for (int qb = 0; qb < 2; ++qb) o[db][qb] = f32x4{0.f, 0.f, 0.f, 0.f};
   float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
 
-  constexpr int NL = KT / 32, KS = KT == 128 ? 7 : 6;  // uint4 loads per lane per tile; log2 KT
+  // QW waves: the block covers 32 * QW query rows; NT threads stage a K/V tile in NL rounds of
+  // NT / 8 keys (8 16-B chunks per 128-B key row)
+  constexpr int NT = 64 * QW, NL = KT * 8 / NT, KS = KT == 128 ? 7 : 6;  // KS = log2 KT
   static_assert(KT == 64 || KT == 128, "key tile");
+  static_assert(QW == 4 || QW == 8, "waves per block");
   uint4 rk[NL], rv[NL];
   // OPT: per-lane K/V source pointers of tile 0, advanced by KT rows per tile
-  // (lane load `it` sits 32 keys after load 0: a wave-uniform offset, so one pointer pair per lane)
+  // (lane load `it` sits NT / 8 keys after load 0: a wave-uniform offset, so one pointer pair per lane)
   const uint16_t* kp = Kg + (s0 + (tid >> 3)) * ld + (tid & 7) * 8;
   const uint16_t* vp = Vg + (s0 + (tid >> 3)) * ld + (tid & 7) * 8;
   const long tstride = KT * ld;
   auto gload = [&](long k0) {
 #pragma unroll
     for (int it = 0; it < NL; ++it) {
-      const int c = tid + it * 256, key = c >> 3, ch = c & 7;
+      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
       if (k0 + key < len) {
         if constexpr (OPT) {
-          const long off = (k0 >> KS) * tstride + it * 32 * ld;
+          const long off = (k0 >> KS) * tstride + it * (NT / 8) * ld;
           rk[it] = *(const uint4*)(kp + off);
           rv[it] = *(const uint4*)(vp + off);
         } else {
@@ -360,14 +363,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W > 0 ? W :
   auto lwrite = [&](int buf) {
 #pragma unroll
     for (int it = 0; it < NL; ++it) {
-      const int c = tid + it * 256, key = c >> 3, ch = c & 7;
+      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
       *(uint4*)(lds[buf][0] + key * 128 + (ksw(key, ch) << 4)) = rk[it];
       *(uint4*)(lds[buf][1] + key * 128 + (vsw(key, ch) << 4)) = rv[it];
     }
   };
 
   int ntiles = (int)((len + KT - 1) / KT);
-  if constexpr (CAUSAL) ntiles = min(ntiles, (int)((qstart + 128 + KT - 1) / KT));
+  if constexpr (CAUSAL) ntiles = min(ntiles, (int)((qstart + 32 * QW + KT - 1) / KT));
   gload(0);
   lwrite(0);
   __syncthreads();
@@ -733,6 +736,9 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
                        (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 7)  // 128-key tiles: half the barriers, 2x the MFMA work per sync
     hipLaunchKernelGGL((k_attn2<0, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
+                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 9)  // 8 waves, 256-row q-blocks (the caller's table): half the K/V traffic
+    hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 8>), dim3(nqb * heads), dim3(512), 0, s,
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 8)  // 128-key tiles held to 2 waves/SIMD
     hipLaunchKernelGGL((k_attn2<2, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,

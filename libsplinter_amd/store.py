@@ -198,7 +198,8 @@ class Store:
         return self._L.spl_get_epoch(self._h, _k(key))
 
     def raw(self, key) -> Optional[Tuple[memoryview, int]]:
-        """Zero-copy (view, epoch) of the value (host backends); validate the epoch after use."""
+        """Zero-copy (view, epoch) of the value; validate the epoch after use.  On hbm: stores the
+        view reads HBM through the CPU mapping of the arena's dmabuf chunks (PCIe BAR)."""
         sz, ep = N.c_size_t(0), N.c_u64(0)
         p = self._L.spl_get_raw_ptr(self._h, _k(key), ctypes.byref(sz), ctypes.byref(ep))
         if not p:

@@ -21,11 +21,14 @@ def main():
     import torch
     from libsplinter_amd.models.nomic import Batch, _chk, _lib, _stream
     L = _lib()
-    b = Batch([[0] * a.seq for _ in range(a.docs)])
-    qkv = torch.randn(b.T_pad, 3 * 768, device="cuda").bfloat16()
-    out = torch.empty(b.T_pad, 768, device="cuda", dtype=torch.bfloat16)
+    b128 = Batch([[0] * a.seq for _ in range(a.docs)])
+    b256 = Batch([[0] * a.seq for _ in range(a.docs)], qblock=256)  # variant 9: 8-wave blocks of 256 rows
+    qkv = torch.randn(b128.T_pad, 3 * 768, device="cuda").bfloat16()
+    out = torch.empty(b128.T_pad, 768, device="cuda", dtype=torch.bfloat16)
+    cur = {"v": 6}
 
     def run():
+        b = b256 if cur["v"] == 9 else b128
         _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
                                0.125, _stream()), "attn")
 
@@ -34,6 +37,7 @@ def main():
     for _ in range(a.rounds):
         for v in VARIANTS:
             L.nomic_attention_set_variant(v)
+            cur["v"] = v
             run()
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()

@@ -142,3 +142,24 @@ def test_event_bus_wakes_other_process_on_batched_device_write(uniq):
     lines = out.split()
     assert lines[0] == "woke", out + err[-1000:]
     assert int(lines[-1]) >= 1
+
+
+def test_raw_ptr_on_hbm_is_zero_copy(uniq):
+    """splinter_get_raw_ptr on an hbm: store returns a pointer INTO the arena (the CPU mapping of
+    its dmabuf chunks), as the reference's pointer into shm: a later device write shows through
+    the same view, and the epoch moves with it (reference splinter.c:747-762)."""
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=512, max_val=256, embeddings=False)
+    try:
+        s.set("rk", b"hello world")
+        got = s.raw("rk")
+        assert got is not None
+        view, e0 = got
+        assert bytes(view) == b"hello world" and e0 == s.epoch("rk")
+        s.set("rk", b"HELLO WORLD")  # a device write (command ring kernel)
+        assert bytes(view[:11]) == b"HELLO WORLD"  # same memory: zero-copy
+        assert s.epoch("rk") == e0 + 2
+        assert s.raw("missing") is None
+    finally:
+        s.close()
+

@@ -319,6 +319,195 @@ __global__ __launch_bounds__(256) void k_gemv(const uint16_t* __restrict__ x, co
   }
 }
 
+// ---------------------------------------------------------------------------
+// 4-bit weights (Q4G32): W [N, K] resident in HBM at 0.625 B per weight instead of 2.
+//   q  : uint8 [N, K/2]  -- k = 2j in the low nibble of byte j, k = 2j + 1 in the high nibble
+//   sm : uint32 [N, K/32] -- per 32-k group, bf16 pair (d low, m high): w = d * q + m
+// The decode step is weight-bandwidth bound (every weight read once per token), so the GEMV reads
+// 3.2x fewer bytes than the bf16 one.  GGUF Q4_0 / Q4_1 / Q4_K blocks are all affine 4-bit grids
+// over 32-weight (sub)blocks, which is the layout this format keeps (reference: llama.cpp reads
+// its Q4 weights directly in llama_decode, splainference.cpp:272-330).
+// ---------------------------------------------------------------------------
+constexpr int kQ4Group = 32;
+
+// nibble pairs -> floats: for one dword of 8 nibbles (k = 0..7), lo bytes hold k = 0,2,4,6 and hi
+// bytes k = 1,3,5,7; each byte converts with a single v_cvt_f32_ubyteN
+__device__ __forceinline__ float q4dot8(uint32_t w, const float* x) {
+  const uint32_t lo = w & 0x0F0F0F0Fu, hi = (w >> 4) & 0x0F0F0F0Fu;
+  float s = (float)(lo & 0xff) * x[0];
+  s = fmaf((float)(hi & 0xff), x[1], s);
+  s = fmaf((float)((lo >> 8) & 0xff), x[2], s);
+  s = fmaf((float)((hi >> 8) & 0xff), x[3], s);
+  s = fmaf((float)((lo >> 16) & 0xff), x[4], s);
+  s = fmaf((float)((hi >> 16) & 0xff), x[5], s);
+  s = fmaf((float)(lo >> 24), x[6], s);
+  return fmaf((float)(hi >> 24), x[7], s);
+}
+
+// y[n] = x . W[n, :] with W in Q4G32.  Structure of k_gemv: x (optionally RMS-normalised) staged
+// in LDS as fp32 together with its 32-group sums (the m term: sum_k (d q_k + m) x_k =
+// d sum_k q_k x_k + m sum_k x_k); each wave owns 4 weight rows, each lane one 32-k group per row
+// and iteration (one 16-B load of nibbles + one scale word per row).
+constexpr int kGemvQ4MaxK = 16384;
+constexpr int kQ4Rec = kQ4Group + 4;  // LDS floats per group record
+
+template <int MODE, bool RMS>
+__global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x, const float* __restrict__ rw,
+                                                 float eps, const uint8_t* __restrict__ Wq,
+                                                 const uint32_t* __restrict__ Wsm, int K, int nout,
+                                                 const uint16_t* res, void* out) {
+  // dynamic LDS, fp32, one 36-float record per 32-k group: x[32], the group sum, 3 pad.  The
+  // 144-B record stride keeps the main loop's per-lane ds_read_b128 of consecutive groups
+  // conflict-free (16-lane phases start on 16 distinct 4-bank quads).
+  extern __shared__ __attribute__((aligned(16))) float xs[];
+  __shared__ float red[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nch = K >> 3, ng = K / kQ4Group;
+  float ss = 0.f;
+  for (int c = tid; c < nch; c += 256) {
+    float f[8];
+    unpack8(*(const uint4*)(x + c * 8), f);
+    float* px = xs + (c >> 2) * kQ4Rec + (c & 3) * 8;
+    *(float4*)px = make_float4(f[0], f[1], f[2], f[3]);
+    *(float4*)(px + 4) = make_float4(f[4], f[5], f[6], f[7]);
+    if constexpr (RMS) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) ss += f[e] * f[e];
+    }
+  }
+  float rs = 1.f;
+  if constexpr (RMS) {
+    ss = wave_sum(ss);
+    if (lane == 0) red[wave] = ss;
+    __syncthreads();
+    rs = rsqrtf((red[0] + red[1] + red[2] + red[3]) / (float)K + eps);
+  }
+  // each thread revisits the chunks it staged: RMS scaling (x * rs * w rounded to bf16, as the bf16
+  // path feeds its GEMV) and the 32-group sums over the 4 consecutive lanes holding a group's chunks
+  // (nch % 4 == 0 and the stride 256 keep a group's 4 lanes active together)
+  for (int c = tid; c < nch; c += 256) {
+    float* px = xs + (c >> 2) * kQ4Rec + (c & 3) * 8;
+    float4 a = *(const float4*)px, b = *(const float4*)(px + 4);
+    if constexpr (RMS) {
+      const float4 wa = *(const float4*)(rw + c * 8), wb = *(const float4*)(rw + c * 8 + 4);
+      a = make_float4((float)(__bf16)(a.x * rs * wa.x), (float)(__bf16)(a.y * rs * wa.y),
+                      (float)(__bf16)(a.z * rs * wa.z), (float)(__bf16)(a.w * rs * wa.w));
+      b = make_float4((float)(__bf16)(b.x * rs * wb.x), (float)(__bf16)(b.y * rs * wb.y),
+                      (float)(__bf16)(b.z * rs * wb.z), (float)(__bf16)(b.w * rs * wb.w));
+      *(float4*)px = a;
+      *(float4*)(px + 4) = b;
+    }
+    float s = ((a.x + a.y) + (a.z + a.w)) + ((b.x + b.y) + (b.z + b.w));
+    s += __shfl_xor(s, 1, 64);
+    s += __shfl_xor(s, 2, 64);
+    if ((c & 3) == 0) xs[(c >> 2) * kQ4Rec + kQ4Group] = s;
+  }
+  __syncthreads();
+  constexpr int outs = MODE == 2 ? kGemvRows / 2 : kGemvRows;
+  const int o0 = (blockIdx.x * 4 + wave) * outs;
+  if (o0 >= nout) return;
+  long rows[kGemvRows];
+#pragma unroll
+  for (int r = 0; r < kGemvRows; ++r) {
+    int o = o0 + (MODE == 2 ? r / 2 : r);
+    if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
+    rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
+  }
+  const long qrow = K / 2;
+  float acc[kGemvRows] = {};
+  for (int g = lane; g < ng; g += 64) {
+    uint4 wq[kGemvRows];
+    uint32_t sm[kGemvRows];
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r) {
+      wq[r] = *(const uint4*)(Wq + rows[r] * qrow + g * 16);
+      sm[r] = Wsm[rows[r] * ng + g];
+    }
+    float xg[kQ4Group];
+#pragma unroll
+    for (int e = 0; e < kQ4Group; e += 4) *(float4*)(xg + e) = *(const float4*)(xs + g * kQ4Rec + e);
+    const float gs = xs[g * kQ4Rec + kQ4Group];
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r) {
+      float dot = q4dot8(wq[r].x, xg);
+      dot += q4dot8(wq[r].y, xg + 8);
+      dot += q4dot8(wq[r].z, xg + 16);
+      dot += q4dot8(wq[r].w, xg + 24);
+      acc[r] = fmaf(bf2f(sm[r] & 0xffff), dot, fmaf(bf2f(sm[r] >> 16), gs, acc[r]));
+    }
+  }
+#pragma unroll
+  for (int r = 0; r < kGemvRows; ++r) acc[r] = wave_sum(acc[r]);
+  if (lane < outs) {
+    const int o = o0 + lane;
+    if (o < nout) {
+      float a0 = acc[0], a1 = acc[1];
+#pragma unroll
+      for (int r = 0; r < kGemvRows; ++r)
+        if ((MODE == 2 ? r / 2 : r) == lane) {
+          if (MODE == 2) { if (r & 1) a1 = acc[r]; else a0 = acc[r]; }
+          else a0 = acc[r];
+        }
+      if constexpr (MODE == 4) {
+        ((float*)out)[o] = a0;
+      } else {
+        float y = a0;
+        if constexpr (MODE == 1) y += bf2f(res[o]);
+        if constexpr (MODE == 2) y = a0 * a1 / (1.f + __expf(-a1));
+        ((uint16_t*)out)[o] = __builtin_bit_cast(uint16_t, (__bf16)y);
+      }
+    }
+  }
+}
+
+// bf16 W [N, K] -> Q4G32 (one thread per 32-weight group): affine min/max grid, d and m rounded
+// to bf16 first and the nibbles chosen against the rounded pair
+__global__ void k_q4_quant(const uint16_t* __restrict__ W, long groups, int ng, uint8_t* __restrict__ Wq,
+                           uint32_t* __restrict__ Wsm) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= groups) return;
+  float v[kQ4Group];
+  const uint4* src = (const uint4*)(W + i * kQ4Group);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) unpack8(src[c], v + c * 8);
+  float lo = v[0], hi = v[0];
+#pragma unroll
+  for (int e = 1; e < kQ4Group; ++e) { lo = fminf(lo, v[e]); hi = fmaxf(hi, v[e]); }
+  const float m = (float)(__bf16)lo;
+  float d = (float)(__bf16)((hi - m) / 15.f);
+  if (!(d > 0.f)) d = 0.f;
+  const float inv = d > 0.f ? 1.f / d : 0.f;
+  uint32_t packed[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int e = 0; e < kQ4Group; ++e) {
+    int q = (int)rintf((v[e] - m) * inv);
+    q = q < 0 ? 0 : (q > 15 ? 15 : q);
+    packed[e >> 3] |= (uint32_t)q << (4 * (e & 7));
+  }
+  *(uint4*)(Wq + i * 16) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+  Wsm[i] = pk2(d, m);
+  (void)ng;
+}
+
+// Q4G32 -> bf16 W [N, K] (prefill: the MFMA GEMM consumes one dequantised matrix at a time)
+__global__ void k_q4_dequant(const uint8_t* __restrict__ Wq, const uint32_t* __restrict__ Wsm, long groups,
+                             uint16_t* __restrict__ W) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= groups) return;
+  const uint4 q = *(const uint4*)(Wq + i * 16);
+  const uint32_t sm = Wsm[i];
+  const float d = bf2f(sm & 0xffff), m = bf2f(sm >> 16);
+  const uint32_t qw[4] = {q.x, q.y, q.z, q.w};
+  uint4* dst = (uint4*)(W + i * kQ4Group);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fmaf(d, (float)((qw[c] >> (4 * e)) & 15u), m);
+    dst[c] = pack8(f);
+  }
+}
+
 // x = emb[state.token]
 __global__ void k_embed_tok(const uint16_t* __restrict__ emb, int d, const int32_t* __restrict__ st,
                             uint16_t* __restrict__ x) {
@@ -544,6 +733,52 @@ int dec_gemv(int mode, const void* x, const float* rms_w, float eps, const void*
     default: return (int)hipErrorInvalidValue;
   }
 #undef GEMV
+  return (int)hipGetLastError();
+}
+
+// dec_gemv over Q4G32 weights (k_gemv_q4): Wq [N, K/2] nibbles, Wsm [N, K/32] bf16 (d, m) pairs.
+// K % 32 == 0, K <= 16384, 16-B aligned x / Wq, 4-B aligned Wsm.
+int dec_gemv_q4(int mode, const void* x, const float* rms_w, float eps, const void* Wq, const void* Wsm, int N,
+                int K, const void* res, void* out, hipStream_t s) {
+  if (K <= 0 || K % kQ4Group || K > kGemvQ4MaxK || N <= 0 || (mode == 2 && N % 32) || (mode == 1 && !res) ||
+      ((uintptr_t)Wq | (uintptr_t)x) % 16 || (uintptr_t)Wsm % 4 || (rms_w && (uintptr_t)rms_w % 16))
+    return (int)hipErrorInvalidValue;
+  const int nout = mode == 2 ? N / 2 : N;
+  const int per_block = 4 * (mode == 2 ? kGemvRows / 2 : kGemvRows);
+  const dim3 g((unsigned)((nout + per_block - 1) / per_block)), b(256);
+  const size_t lds = (size_t)(K / kQ4Group) * kQ4Rec * sizeof(float);
+  const uint16_t *xx = (const uint16_t*)x, *rr = (const uint16_t*)res;
+  const uint8_t* wq = (const uint8_t*)Wq;
+  const uint32_t* wsm = (const uint32_t*)Wsm;
+#define GEMV(M_, R_) hipLaunchKernelGGL((k_gemv_q4<M_, R_>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out)
+  const bool rms = rms_w != nullptr;
+  switch (mode) {
+    case 0: if (rms) GEMV(0, true); else GEMV(0, false); break;
+    case 1: if (rms) GEMV(1, true); else GEMV(1, false); break;
+    case 2: if (rms) GEMV(2, true); else GEMV(2, false); break;
+    case 4: if (rms) GEMV(4, true); else GEMV(4, false); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef GEMV
+  return (int)hipGetLastError();
+}
+
+// bf16 W [N, K] (row-major, contiguous) <-> Q4G32 planes
+int dec_q4_quantize(const void* W, long N, int K, void* Wq, void* Wsm, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % kQ4Group || ((uintptr_t)W | (uintptr_t)Wq) % 16 || (uintptr_t)Wsm % 4)
+    return (int)hipErrorInvalidValue;
+  const long groups = N * (K / kQ4Group);
+  hipLaunchKernelGGL(k_q4_quant, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, (const uint16_t*)W, groups,
+                     K / kQ4Group, (uint8_t*)Wq, (uint32_t*)Wsm);
+  return (int)hipGetLastError();
+}
+
+int dec_q4_dequant(const void* Wq, const void* Wsm, long N, int K, void* W, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % kQ4Group || ((uintptr_t)W | (uintptr_t)Wq) % 16 || (uintptr_t)Wsm % 4)
+    return (int)hipErrorInvalidValue;
+  const long groups = N * (K / kQ4Group);
+  hipLaunchKernelGGL(k_q4_dequant, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, (const uint8_t*)Wq,
+                     (const uint32_t*)Wsm, groups, (uint16_t*)W);
   return (int)hipGetLastError();
 }
 

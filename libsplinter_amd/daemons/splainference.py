@@ -226,6 +226,9 @@ def main(argv=None) -> int:
     ap.add_argument("--seed", type=int, default=0xFFFFFFFF)
     ap.add_argument("--poll-ms", type=int, default=50)
     ap.add_argument("--device", default=None, help="cuda (default when a GPU is present) or cpu")
+    ap.add_argument("--quant", default="auto", choices=["auto", "bf16", "q4"],
+                    help="weights in HBM: q4 = 4-bit Q4G32 (decode streams 0.625 B per weight), bf16, or auto "
+                         "(q4 for a 4-bit GGUF, bf16 otherwise; --random-init: bf16)")
     ap.add_argument("bus")
     ap.add_argument("gguf")
     ap.add_argument("group", type=int)
@@ -254,12 +257,13 @@ def main(argv=None) -> int:
         cfg = DecoderConfig()
         if a.n_ctx > 0:
             cfg.n_ctx = a.n_ctx
-        model, tok = CausalLM.random(cfg, device=device), ByteTokenizer()
+        q = "q4" if a.quant == "q4" and device != "cpu" else "bf16"
+        model, tok = CausalLM.random(cfg, device=device, quant=q), ByteTokenizer()
     else:
-        model, tok = CausalLM.from_gguf(a.gguf, device=device)
+        model, tok = CausalLM.from_gguf(a.gguf, device=device, quant=a.quant)
         if a.n_ctx > 0:
             model.cfg.n_ctx = min(a.n_ctx, model.cos.shape[0])
-    print(f"[Startup]: context window = {model.cfg.n_ctx} tokens.", flush=True)
+    print(f"[Startup]: context window = {model.cfg.n_ctx} tokens, {model.quant} weights.", flush=True)
     sampler = Sampler(seed=a.seed, mask=tok.printable_mask(model.cfg.vocab))
     d = Splainference(store, model, tok, sampler, a.system_prompt_key, a.max_tokens)
     pending = d.waiting()

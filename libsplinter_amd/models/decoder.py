@@ -132,6 +132,14 @@ def random_decoder_weights(cfg: DecoderConfig, seed: int = 0, std: float = 0.02)
     return w
 
 
+def gguf_quant_kind(g) -> str:
+    """"q4" when most projection weights (2-D blk.* tensors) of a GGUF are 4-bit types (Q4_0, Q4_1,
+    Q4_K), else "bf16"."""
+    proj = [t for n, t in g.tensors.items() if n.startswith("blk.") and len(t.shape) == 2]
+    q4 = sum(t.nelems for t in proj if t.ggml_type in (2, 3, 12))
+    return "q4" if proj and q4 * 2 > sum(t.nelems for t in proj) else "bf16"
+
+
 def config_from_gguf(g) -> DecoderConfig:
     a = g.arch() or "llama"
     get = lambda k, d: g.get(f"{a}.{k}", d)  # noqa: E731
@@ -144,11 +152,50 @@ def config_from_gguf(g) -> DecoderConfig:
                          rope_base=float(get("rope.freq_base", 10000.0)), n_ctx=int(get("context_length", 2048)))
 
 
+class Q4Weight:
+    """A projection W [N, K] resident as Q4G32 (csrc/hip/decoder_kernels.hip): 4-bit nibbles
+    ``q`` uint8 [N, K/2] plus one bf16 (d, m) pair per 32-k group ``sm`` int32 [N, K/32], w = d q + m;
+    0.625 B per weight instead of 2.  Decode reads it with dec_gemv_q4; prefill dequantises one matrix
+    at a time into a bf16 scratch for the MFMA GEMM.  The role of llama.cpp's Q4 weights in the
+    reference's llama_decode (splainference.cpp:272-330)."""
+
+    def __init__(self, q: torch.Tensor, sm: torch.Tensor):
+        self.q, self.sm = q, sm
+        self.shape = (q.shape[0], q.shape[1] * 2)
+
+    @classmethod
+    def quantize(cls, L, w: torch.Tensor) -> "Q4Weight":
+        from .nomic import _chk, _stream
+        w = w.to(torch.bfloat16).contiguous()
+        N, K = w.shape
+        q = torch.empty((N, K // 2), dtype=torch.uint8, device=w.device)
+        sm = torch.empty((N, K // 32), dtype=torch.int32, device=w.device)
+        _chk(L.dec_q4_quantize(w.data_ptr(), N, K, q.data_ptr(), sm.data_ptr(), _stream()), "q4_quantize")
+        return cls(q, sm)
+
+    def dequant(self, L, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        from .nomic import _chk, _stream
+        N, K = self.shape
+        if out is None:
+            out = torch.empty((N, K), dtype=torch.bfloat16, device=self.q.device)
+        _chk(L.dec_q4_dequant(self.q.data_ptr(), self.sm.data_ptr(), N, K, out.data_ptr(), _stream()), "q4_dequant")
+        return out
+
+    def nbytes(self) -> int:
+        return self.q.numel() + self.sm.numel() * 4
+
+
 class CausalLM:
-    def __init__(self, cfg: DecoderConfig, tensors: Dict[str, torch.Tensor], device: str = "cuda"):
+    def __init__(self, cfg: DecoderConfig, tensors: Dict[str, torch.Tensor], device: str = "cuda",
+                 quant: str = "bf16"):
+        """quant "q4": every projection (qkv, o, up|gate, down, LM head) is kept as a Q4Weight
+        (GPU only); "bf16": bf16 weights."""
+        if quant not in ("bf16", "q4"):
+            raise ValueError(f"quant must be bf16 or q4, not {quant!r}")
         self.cfg = cfg
         self.device = device
         self.hip = device != "cpu"
+        self.quant = quant if self.hip else "bf16"
         dt = torch.bfloat16 if self.hip else torch.float32
         T = lambda n: tensors[n].to(device=device, dtype=dt).contiguous()  # noqa: E731
         self.emb = T("token_embd.weight")
@@ -159,6 +206,10 @@ class CausalLM:
         hw[: cfg.vocab] = head.to(device=device, dtype=dt)
         self.head = hw
         self.layers = []
+        if self.hip:
+            self._declare()
+        Q = (lambda t: Q4Weight.quantize(self.L, t)) if self.quant == "q4" else (lambda t: t)  # noqa: E731
+        self.head = Q(self.head)
         for i in range(cfg.layers):
             p = f"blk.{i}."
             qkv = torch.cat([T(p + "attn_q.weight"), T(p + "attn_k.weight"), T(p + "attn_v.weight")], 0)
@@ -166,9 +217,11 @@ class CausalLM:
             # SwiGLU epilogue layout: rows interleaved [up16 | gate16] (nomic_api.h NOMIC_EPI_SWIGLU)
             from .nomic import pack_upgate
             ug = pack_upgate(up, gate)
-            self.layers.append({"n1": T(p + "attn_norm.weight").float(), "qkv": qkv.contiguous(),
-                                "o": T(p + "attn_output.weight"), "n2": T(p + "ffn_norm.weight").float(),
-                                "ug": ug.contiguous(), "gate": gate, "up": up, "down": T(p + "ffn_down.weight")})
+            self.layers.append({"n1": T(p + "attn_norm.weight").float(), "qkv": Q(qkv.contiguous()),
+                                "o": Q(T(p + "attn_output.weight")), "n2": T(p + "ffn_norm.weight").float(),
+                                "ug": Q(ug.contiguous()), "down": Q(T(p + "ffn_down.weight"))})
+            del qkv, gate, up, ug
+        self._q4_scratch: Optional[torch.Tensor] = None
         hd = cfg.head_dim
         inv = 1.0 / (cfg.rope_base ** (torch.arange(0, hd, 2, dtype=torch.float64) / hd))
         ang = torch.arange(cfg.n_ctx, dtype=torch.float64)[:, None] * inv[None, :]
@@ -180,54 +233,73 @@ class CausalLM:
         self.pos = 0
         self.attn_kernel = True  # single-token decode through dec_attn_decode (False: SDPA, for A/B)
         if self.hip:
-            from .nomic import _lib
-            self.L = _lib()
-            if not getattr(self.L, "_dec_declared", False):
-                P, c_long, c_int, c_float = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float
-                self.L.dec_rmsnorm.argtypes = [P, c_long, P, c_long, c_int, c_float, P, c_long, P]
-                self.L.dec_rmsnorm.restype = c_int
-                self.L.dec_rope.argtypes = [P, c_long, c_long, c_int, c_int, c_int, P, P, P]
-                self.L.dec_rope.restype = c_int
-                self.L.dec_attn_decode.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P]
-                self.L.dec_attn_decode.restype = c_int
-                self.L.dec_attn_decode_st.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P, P]
-                self.L.dec_attn_decode_st.restype = c_int
-                self.L.dec_attn_prefill.argtypes = [P, P, P, P, c_int, c_int, c_int, c_float, P]
-                self.L.dec_attn_prefill.restype = c_int
-                self.L.dec_gemv.argtypes = [c_int, P, P, c_float, P, c_int, c_int, P, P, P]
-                self.L.dec_gemv.restype = c_int
-                self.L.dec_embed_tok.argtypes = [P, c_int, P, P, P]
-                self.L.dec_embed_tok.restype = c_int
-                self.L.dec_rope_kv.argtypes = [P, c_int, c_int, c_int, P, P, P, P, P, c_long, P]
-                self.L.dec_rope_kv.restype = c_int
-                self.L.dec_sample.argtypes = [P, c_int, P, c_float, c_float, ctypes.c_uint64, P, c_int, P, P]
-                self.L.dec_sample.restype = c_int
-                self.L._dec_declared = True
             ok = all(n % 128 == 0 for n in (cfg.d + 2 * cfg.kv_heads * hd, cfg.d, 2 * cfg.ffn, vpad)) \
                 and cfg.d % 64 == 0 and cfg.ffn % 64 == 0
             if not ok:
                 raise ValueError("decoder dims must be multiples of 128 (N) / 64 (K) for the MFMA GEMM")
 
-    @classmethod
-    def random(cls, cfg: DecoderConfig, seed: int = 0, device: str = "cuda") -> "CausalLM":
-        return cls(cfg, {k: torch.from_numpy(v) for k, v in random_decoder_weights(cfg, seed).items()}, device)
+    def _declare(self):
+        """ctypes signatures of the decoder kernels (csrc/hip/decoder_kernels.hip)."""
+        from .nomic import _lib
+        self.L = _lib()
+        if not getattr(self.L, "_dec_declared", False):
+            P, c_long, c_int, c_float = ctypes.c_void_p, ctypes.c_long, ctypes.c_int, ctypes.c_float
+            self.L.dec_rmsnorm.argtypes = [P, c_long, P, c_long, c_int, c_float, P, c_long, P]
+            self.L.dec_rmsnorm.restype = c_int
+            self.L.dec_rope.argtypes = [P, c_long, c_long, c_int, c_int, c_int, P, P, P]
+            self.L.dec_rope.restype = c_int
+            self.L.dec_attn_decode.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P]
+            self.L.dec_attn_decode.restype = c_int
+            self.L.dec_attn_decode_st.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P, P]
+            self.L.dec_attn_decode_st.restype = c_int
+            self.L.dec_attn_prefill.argtypes = [P, P, P, P, c_int, c_int, c_int, c_float, P]
+            self.L.dec_attn_prefill.restype = c_int
+            self.L.dec_gemv.argtypes = [c_int, P, P, c_float, P, c_int, c_int, P, P, P]
+            self.L.dec_gemv.restype = c_int
+            self.L.dec_embed_tok.argtypes = [P, c_int, P, P, P]
+            self.L.dec_embed_tok.restype = c_int
+            self.L.dec_rope_kv.argtypes = [P, c_int, c_int, c_int, P, P, P, P, P, c_long, P]
+            self.L.dec_rope_kv.restype = c_int
+            self.L.dec_sample.argtypes = [P, c_int, P, c_float, c_float, ctypes.c_uint64, P, c_int, P, P]
+            self.L.dec_sample.restype = c_int
+            self.L.dec_gemv_q4.argtypes = [c_int, P, P, c_float, P, P, c_int, c_int, P, P, P]
+            self.L.dec_gemv_q4.restype = c_int
+            self.L.dec_q4_quantize.argtypes = [P, c_long, c_int, P, P, P]
+            self.L.dec_q4_quantize.restype = c_int
+            self.L.dec_q4_dequant.argtypes = [P, P, c_long, c_int, P, P]
+            self.L.dec_q4_dequant.restype = c_int
+            self.L._dec_declared = True
 
     @classmethod
-    def from_gguf(cls, path: str, device: str = "cuda"):
-        from .gguf import GGUFFile, dequant_host
+    def random(cls, cfg: DecoderConfig, seed: int = 0, device: str = "cuda", quant: str = "bf16") -> "CausalLM":
+        return cls(cfg, {k: torch.from_numpy(v) for k, v in random_decoder_weights(cfg, seed).items()}, device,
+                   quant=quant)
+
+    @classmethod
+    def from_gguf(cls, path: str, device: str = "cuda", quant: str = "auto"):
+        """quant "auto": Q4G32 when most projection weights of the file are 4-bit GGUF types
+        (Q4_0 / Q4_1 / Q4_K: a Q4_K_M file's Q6_K tensors are re-gridded to 4 bits too), else bf16."""
+        from .gguf import GGUFFile
         g = GGUFFile(path)
         cfg = config_from_gguf(g)
-        tensors = {n: torch.from_numpy(dequant_host(g, n)) for n in g.tensors}
+        if quant == "auto":
+            quant = gguf_quant_kind(g)
+        tensors = {n: torch.from_numpy(np.ascontiguousarray(g.to_numpy_f32(n))) for n in g.tensors}
         tokens = g.get("tokenizer.ggml.tokens")
         tok = VocabTokenizer(list(tokens), int(g.get("tokenizer.ggml.bos_token_id", 1)),
                              int(g.get("tokenizer.ggml.eos_token_id", 2))) if tokens else ByteTokenizer()
         tok.chat_template = g.get("tokenizer.chat_template", None)  # rendered by splainference.build_prompt
-        return cls(cfg, tensors, device), tok
+        return cls(cfg, tensors, device, quant=quant if device != "cpu" else "bf16"), tok
 
     # ------------------------------------------------------------- pieces --
-    def _mm(self, mode: int, x: torch.Tensor, w: torch.Tensor, out_cols: int, res: Optional[torch.Tensor] = None):
+    def _mm(self, mode: int, x: torch.Tensor, w, out_cols: int, res: Optional[torch.Tensor] = None):
         """x [M, K] @ w[N, K]^T with a fused epilogue; HIP MFMA on the GPU, torch on the CPU."""
         M, K = x.shape
+        if isinstance(w, Q4Weight):  # prefill: dequantise into the shared bf16 scratch
+            n_el = w.shape[0] * w.shape[1]
+            if self._q4_scratch is None or self._q4_scratch.numel() < n_el:
+                self._q4_scratch = torch.empty(n_el, dtype=torch.bfloat16, device=self.device)
+            w = w.dequant(self.L, self._q4_scratch[:n_el].view(w.shape))
         if not self.hip:
             if mode == 2:
                 up, gate = self._split_ug(x @ w.T)
@@ -386,22 +458,26 @@ class DecodeEngine:
         H, KVH, hd = cfg.heads, cfg.kv_heads, cfg.head_dim
         P = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
         _chk(L.dec_embed_tok(m.emb.data_ptr(), cfg.d, self.st.data_ptr(), self.xa.data_ptr(), s), "embed_tok")
+
+        def gemv(mode, x, rms, w, N, K, res, out, what):
+            rp = rms.data_ptr() if rms is not None else None
+            if isinstance(w, Q4Weight):  # 4-bit weights: 0.625 B per weight streamed (dec_gemv_q4)
+                _chk(L.dec_gemv_q4(mode, x.data_ptr(), rp, cfg.eps, w.q.data_ptr(), w.sm.data_ptr(), N, K,
+                                   P(res), out.data_ptr(), s), what)
+            else:
+                _chk(L.dec_gemv(mode, x.data_ptr(), rp, cfg.eps, w.data_ptr(), N, K, P(res), out.data_ptr(), s), what)
+
         for li, lw in enumerate(m.layers):
-            _chk(L.dec_gemv(0, self.xa.data_ptr(), lw["n1"].data_ptr(), cfg.eps, lw["qkv"].data_ptr(),
-                            lw["qkv"].shape[0], cfg.d, None, self.qkv.data_ptr(), s), "gemv qkv")
+            gemv(0, self.xa, lw["n1"], lw["qkv"], lw["qkv"].shape[0], cfg.d, None, self.qkv, "gemv qkv")
             kc, vc = m.kv[li, 0], m.kv[li, 1]
             _chk(L.dec_rope_kv(self.qkv.data_ptr(), H, KVH, hd, m.cos.data_ptr(), m.sin.data_ptr(), self.st.data_ptr(),
                                kc.data_ptr(), vc.data_ptr(), KVH * hd, s), "rope_kv")
             _chk(L.dec_attn_decode_st(self.qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), KVH * hd, 1, H, KVH, hd,
                                       hd ** -0.5, self.attn.data_ptr(), self.st.data_ptr(), s), "attn_decode")
-            _chk(L.dec_gemv(1, self.attn.data_ptr(), None, 0.0, lw["o"].data_ptr(), cfg.d, cfg.d, self.xa.data_ptr(),
-                            self.xb.data_ptr(), s), "gemv o")
-            _chk(L.dec_gemv(2, self.xb.data_ptr(), lw["n2"].data_ptr(), cfg.eps, lw["ug"].data_ptr(),
-                            lw["ug"].shape[0], cfg.d, None, self.ffn.data_ptr(), s), "gemv up|gate")
-            _chk(L.dec_gemv(1, self.ffn.data_ptr(), None, 0.0, lw["down"].data_ptr(), cfg.d, cfg.ffn,
-                            self.xb.data_ptr(), self.xa.data_ptr(), s), "gemv down")
-        _chk(L.dec_gemv(4, self.xa.data_ptr(), m.norm_out.data_ptr(), cfg.eps, m.head.data_ptr(), m.head.shape[0],
-                        cfg.d, None, self.logits.data_ptr(), s), "gemv head")
+            gemv(1, self.attn, None, lw["o"], cfg.d, cfg.d, self.xa, self.xb, "gemv o")
+            gemv(2, self.xb, lw["n2"], lw["ug"], lw["ug"].shape[0], cfg.d, None, self.ffn, "gemv up|gate")
+            gemv(1, self.ffn, None, lw["down"], cfg.d, cfg.ffn, self.xb, self.xa, "gemv down")
+        gemv(4, self.xa, m.norm_out, m.head, m.head.shape[0], cfg.d, None, self.logits, "gemv head")
         self._sample(self.logits, inc_pos=1)
 
     def _sample(self, logits: torch.Tensor, inc_pos: int):

@@ -197,6 +197,100 @@ def test_dec_gemv_modes_vs_fp32(K, N):
         assert (out.float() - ref).abs().max() < 2e-2 * max(1.0, ref.abs().max().item())
 
 
+def _q4_host_dequant(q, sm):
+    """Host decoder of the Q4G32 planes (decoder_kernels.hip): nibble 2j low / 2j+1 high of byte j,
+    one bf16 (d, m) pair per 32-k group, w = d q + m."""
+    import torch
+    qi = q.to(torch.int32)
+    nib = torch.stack([qi & 15, qi >> 4], -1).reshape(q.shape[0], -1).float()
+    smi = sm.to(torch.int64) & 0xFFFFFFFF
+    d = ((smi & 0xFFFF) << 16).to(torch.int32).view(torch.float32)
+    m = ((smi >> 16) << 16).to(torch.int32).view(torch.float32)
+    return nib * d.repeat_interleave(32, 1) + m.repeat_interleave(32, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N", [(512, 1536), (1536, 512), (11008, 96)])
+def test_q4_quant_dequant_and_gemv_q4_vs_fp32(K, N):
+    """Q4G32 weights: dec_q4_quantize stays within half a grid step of every weight, dec_q4_dequant
+    equals the host decoder of the planes, and dec_gemv_q4 (store / residual / fp32 / SwiGLU, with
+    and without the fused RMSNorm) matches fp32 torch over the dequantised weights."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig, Q4Weight
+    from libsplinter_amd.models.nomic import pack_upgate
+    m = CausalLM.random(DecoderConfig(layers=1), seed=1, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(12)
+    W = (torch.randn((N, K), device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    qw = Q4Weight.quantize(m.L, W)
+    torch.cuda.synchronize()
+    deq_host = _q4_host_dequant(qw.q, qw.sm)
+    deq = qw.dequant(m.L)
+    torch.cuda.synchronize()
+    assert torch.allclose(deq.float(), deq_host, rtol=2 ** -8, atol=1e-7)
+    Wg = W.float().reshape(N, K // 32, 32)
+    step = ((Wg.amax(-1) - Wg.amin(-1)) / 15).repeat_interleave(32, 1)
+    err = (deq_host - W.float()).abs()
+    assert bool((err <= step * 0.6 + 1e-6).all()), float((err / step).max())
+    x = torch.randn(K, device="cuda", generator=g).to(torch.bfloat16)
+    rw = torch.rand(K, device="cuda", generator=g) + 0.5
+    res = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    xf = x.float()
+    xn = (xf * torch.rsqrt(xf.pow(2).mean() + 1e-5) * rw).to(torch.bfloat16).float()
+    for rms in (False, True):
+        xin = xn if rms else xf
+        for mode in (0, 1, 4):
+            out = torch.empty(N, device="cuda", dtype=torch.float32 if mode == 4 else torch.bfloat16)
+            assert m.L.dec_gemv_q4(mode, x.data_ptr(), rw.data_ptr() if rms else None, 1e-5, qw.q.data_ptr(),
+                                   qw.sm.data_ptr(), N, K, res.data_ptr(), out.data_ptr(), None) == 0
+            torch.cuda.synchronize()
+            ref = deq_host @ xin + (res.float() if mode == 1 else 0)
+            tol = (1e-3 if mode == 4 else 1e-2) * max(1.0, ref.abs().max().item())
+            assert (out.float() - ref).abs().max() < tol, (rms, mode, (out.float() - ref).abs().max().item())
+    if N % 32 == 0:
+        gate = (torch.randn((N // 2, K), device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+        ug = Q4Weight.quantize(m.L, pack_upgate(W[: N // 2], gate).contiguous())
+        out = torch.empty(N // 2, device="cuda", dtype=torch.bfloat16)
+        assert m.L.dec_gemv_q4(2, x.data_ptr(), None, 0.0, ug.q.data_ptr(), ug.sm.data_ptr(), N, K, None,
+                               out.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        y = _q4_host_dequant(ug.q, ug.sm) @ xf
+        yg = y.reshape(-1, 2, 16)
+        u, gg = yg[:, 0].reshape(-1), yg[:, 1].reshape(-1)
+        ref = u * torch.nn.functional.silu(gg)
+        assert (out.float() - ref).abs().max() < 1e-2 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_decode_engine_q4_matches_eager_and_bf16():
+    """A 4-bit model: DecodeEngine steps (dec_gemv_q4) give the logits of the eager forward (the MFMA
+    GEMM over dequantised weights), and the 4-bit logits stay close to the bf16 model's; the
+    projections occupy 0.625 B per weight."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecodeEngine, DecoderConfig, Q4Weight
+    cfg = DecoderConfig(layers=2, kv_heads=2)
+    eager = CausalLM.random(cfg, seed=4, device="cuda", quant="q4")
+    mdl = CausalLM.random(cfg, seed=4, device="cuda", quant="q4")
+    full = CausalLM.random(cfg, seed=4, device="cuda")
+    lw = mdl.layers[0]
+    assert isinstance(lw["down"], Q4Weight) and isinstance(mdl.head, Q4Weight)
+    assert lw["down"].nbytes() * 16 == cfg.d * cfg.ffn * 10
+    eng = DecodeEngine(mdl, use_graph=True)
+    ids = [256] + list(b"prefill prompt of the test")
+    eng.first_token(ids)
+    eager.forward(ids)
+    ref_bf16 = full.forward(ids)
+    for t in (72, 101, 108, 108, 111):
+        eng.st[1] = t
+        eng._step()
+        torch.cuda.synchronize()
+        mdl.pos += 1
+        ref = eager.forward([t])
+        got = eng.logits[: cfg.vocab]
+        assert (got - ref).norm() / ref.norm() < 3e-2
+        ref_bf16 = full.forward([t])
+        assert (got - ref_bf16).norm() / ref_bf16.norm() < 0.3
+
+
 @pytest.mark.gpu
 def test_dec_sample_nucleus_temperature_distribution():
     """dec_sample: greedy at tiny temperature, never outside the top-p nucleus, and draw
@@ -303,6 +397,40 @@ def test_state_machine_gpu_decode_engine(uniq):
     finally:
         s.close()
         unlink(uniq)
+
+
+def test_from_gguf_llama_q4_cpu(tmp_path):
+    """CausalLM.from_gguf on a llama GGUF with Q4_0 projections: the weights are the host-dequantised
+    blocks, quant="auto" picks q4 for a mostly-4-bit file (bf16 for an F16 one), and the CPU
+    forward equals a model built from the same dequantised tensors."""
+    import numpy as np
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig, gguf_quant_kind, random_decoder_weights
+    from libsplinter_amd.models.gguf import GGUFFile, GGUFWriter
+    cfg = DecoderConfig(vocab=384, d=128, layers=2, heads=2, kv_heads=1, ffn=256, n_ctx=64)
+    w = random_decoder_weights(cfg, seed=3)
+    for proj_type, kind in (("Q4_0", "q4"), ("F16", "bf16")):
+        path = str(tmp_path / f"llama_{proj_type}.gguf")
+        gw = GGUFWriter(path, "llama")
+        for k, v in (("embedding_length", cfg.d), ("block_count", cfg.layers), ("attention.head_count", cfg.heads),
+                     ("attention.head_count_kv", cfg.kv_heads), ("feed_forward_length", cfg.ffn),
+                     ("context_length", cfg.n_ctx)):
+            gw.add(f"llama.{k}", v)
+        gw.add("llama.rope.freq_base", 10000.0)
+        gw.add("llama.attention.layer_norm_rms_epsilon", 1e-5)
+        for n, a in w.items():
+            gw.add_tensor(n, a, proj_type if n.startswith("blk.") and a.ndim == 2 else "F32")
+        gw.write()
+        g = GGUFFile(path)
+        assert gguf_quant_kind(g) == kind
+        m, tok = CausalLM.from_gguf(path, device="cpu")
+        assert m.cfg.d == cfg.d and m.cfg.layers == cfg.layers and m.cfg.kv_heads == cfg.kv_heads
+        ref = CausalLM(m.cfg, {n: torch.from_numpy(np.ascontiguousarray(g.to_numpy_f32(n))) for n in g.tensors},
+                       device="cpu")
+        ids = [1, 5, 9, 200]
+        assert torch.allclose(m.forward(ids), ref.forward(ids))
+        if kind == "q4":
+            assert not np.array_equal(g.to_numpy_f32("blk.0.ffn_down.weight"), w["blk.0.ffn_down.weight"])
 
 
 def test_chat_template_families():

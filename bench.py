@@ -438,10 +438,11 @@ def main():
         pipe.run()  # warm-up (tokenizer threads, first varlen shapes)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        fails = 0
-        for _ in range(args.embed_e2e):
-            fails += int((pipe.run() != 0).sum().item())
+        fails_d = torch.zeros((), dtype=torch.int64, device="cuda")
+        for _ in range(args.embed_e2e):  # write failures counted on the device: no per-batch host sync
+            fails_d += (pipe.run() != 0).sum()
         torch.cuda.synchronize()
+        fails = int(fails_d.item())
         te = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
         if routed:
             dist.all_reduce(te, op=dist.ReduceOp.MAX)

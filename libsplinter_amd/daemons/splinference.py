@@ -147,19 +147,23 @@ class Splinference:
             eps.append(int(e0[i]))
         return ks, texts, eps
 
-    def _run_hbm(self, idx: List[int], ks, eps, ids, offs) -> int:
-        """Encoder + mean pool written straight into the keys' slots under the seqlock (k_pool,
-        which also checks the slot still holds the key), then the +2 epoch check and the WAITING
-        label cleared for the keys that passed it -- all batched."""
-        import torch
+    def _launch_hbm(self, idx: List[int], ks, ids, offs):
+        """Enqueue one batch: encoder + mean pool written straight into the keys' slots under the
+        seqlock (k_pool, which also checks the slot still holds the key) and the post-write epochs
+        -- no host sync; _finish_hbm reads the results back."""
         from ..models.nomic import Batch
         b = Batch([ids[offs[i]: offs[i + 1]] for i in idx])
-        names = [ks[i] for i in idx]
-        K = self._keys_u8(names)
+        K = self._keys_u8([ks[i] for i in idx])
         _, slots = self.arena.meta("find", K)
         hashes = self.shard.hash_keys(K)
         _, status = self.enc.embed(b, normalize=self.normalize, arena=self.arena, slots=slots, hashes=hashes)
         _, post = self.arena.meta("epoch", K)
+        return idx, K, status, post
+
+    def _finish_hbm(self, rec, ks, eps) -> int:
+        """The +2 epoch check and the WAITING label cleared for the keys that passed it (batched)."""
+        import torch
+        idx, K, status, post = rec
         status, post = status.cpu().numpy(), post.cpu().numpy()
         self.stats["batches"] += 1
         ok_rows = []
@@ -231,14 +235,23 @@ class Splinference:
         done = 0
         batch: List[int] = []
         ntok = 0
-        for i in order + [None]:
+        inflight = None  # hbm: one batch of lookahead -- batch j+1 is packed and enqueued before
+        for i in order + [None]:  # batch j's results are read back, so the GPU never waits on the host
             n = 0 if i is None else int(offs[i + 1] - offs[i])
             if batch and (i is None or ntok + n > self.batch_tokens):
-                done += self._run(batch, ks, eps, ids, offs)
+                if self.arena is not None:
+                    rec = self._launch_hbm(batch, ks, ids, offs)
+                    if inflight is not None:
+                        done += self._finish_hbm(inflight, ks, eps)
+                    inflight = rec
+                else:
+                    done += self._run(batch, ks, eps, ids, offs)
                 batch, ntok = [], 0
             if i is not None:
                 batch.append(i)
                 ntok += n
+        if inflight is not None:
+            done += self._finish_hbm(inflight, ks, eps)
         # ctime backfill: wall time minus processing ticks (reference :530-537)
         now_s, dt = int(time.time()), self._ticks() - tick0
         if self.arena is not None and good:
@@ -263,7 +276,7 @@ class Splinference:
 
     def _run(self, idx: List[int], ks, eps, ids, offs) -> int:
         if self.arena is not None:
-            return self._run_hbm(idx, ks, eps, ids, offs)
+            return self._finish_hbm(self._launch_hbm(idx, ks, ids, offs), ks, eps)
         import torch
         from ..models.nomic import Batch
         seqs = [ids[offs[i]: offs[i + 1]] for i in idx]

@@ -75,17 +75,21 @@ class EmbedE2E:
         words = [t[1:] for t in vocab if t.startswith("▁") and len(t) > 2]
         rng = np.random.default_rng(200 + rank)
         texts = []
-        for _ in range(batch):  # varlen documents of about seq/2 .. seq-2 word tokens
+        for _ in range(2 * batch):  # varlen documents of about seq/2 .. seq-2 word tokens
             n = int(rng.integers(seq // 2, seq - 2))
             texts.append(" ".join(words[int(i)] for i in rng.integers(0, len(words), size=n)))
         self.max_tokens = seq
         self.arena = HbmArena.create(f"e2e{os.getpid()}r{rank}", slots=max(4 * batch, 1024), max_val=4096,
                                      embeddings=True)
-        self.keys = format_keys(batch, "txt", 9, 16)
+        # two disjoint sets of pending documents, taken in turn: a batch's fetch overlaps the encoder
+        # pass of the previous batch, as in the daemon, where consecutive batches hold different keys
+        all_keys = format_keys(2 * batch, "txt", 9, 16)
         V, L = pack_values(texts, 4096)
-        st = self.arena.set(self.keys, V, L)
-        st_l, _ = self.arena.meta("set_label", self.keys, torch.full((batch,), self.WAITING, dtype=torch.int64,
-                                                                     device="cuda"))
+        st = self.arena.set(all_keys, V, L)
+        st_l, _ = self.arena.meta("set_label", all_keys, torch.full((2 * batch,), self.WAITING, dtype=torch.int64,
+                                                                    device="cuda"))
+        self.key_sets = [all_keys[:batch], all_keys[batch:]]
+        self.turn = 0
         torch.cuda.synchronize()
         assert int((st != 0).sum()) == 0 and int((st_l != 0).sum()) == 0
         self.mask = torch.full((batch,), self.WAITING, dtype=torch.int64, device="cuda")
@@ -96,12 +100,20 @@ class EmbedE2E:
         self.out = torch.empty((batch, 768), dtype=torch.float32, device="cuda")
         self.tokens = 0
         self.failures = 0
+        from ..utils.streams import stream as hip_stream
+        self.fetch_stream = hip_stream("normal")
 
     def run(self):
-        st, rows, lens = self.arena.get(self.keys)
-        self.host_rows.copy_(rows, non_blocking=True)
-        self.host_lens.copy_(lens, non_blocking=True)
-        torch.cuda.current_stream().synchronize()
+        # The text fetch runs on its own stream and the host waits for that stream only, so this
+        # batch's fetch, tokenization and packing overlap the previous batch's encoder pass (the
+        # daemon's loop does the same with its one-batch lookahead, daemons/splinference.py).
+        self.keys = self.key_sets[self.turn]
+        self.turn ^= 1
+        with torch.cuda.stream(self.fetch_stream):
+            st, rows, lens = self.arena.get(self.keys)
+            self.host_rows.copy_(rows, non_blocking=True)
+            self.host_lens.copy_(lens, non_blocking=True)
+        self.fetch_stream.synchronize()
         hr, hl = self.host_rows.numpy(), self.host_lens.numpy()
         texts = [hr[i, : hl[i]].tobytes() for i in range(self.docs)]
         ids, offs, _ = self.tok.encode_batch(texts, self.max_tokens)

@@ -304,12 +304,31 @@ class Batch:
         ids[: self.T] = np.concatenate([np.asarray(s, np.int32) for s in seqs])
         pos = np.zeros(self.T_pad, np.int32)
         pos[: self.T] = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
-        qb = [(i, q0) for i, n in enumerate(lens) for q0 in range(0, n, qblock)]
-        self.nqb = len(qb)
-        self.ids = torch.from_numpy(ids).to(device)
-        self.pos = torch.from_numpy(pos).to(device)
-        self.cu = torch.from_numpy(self.cu_host).to(device)
-        self.qblocks = torch.tensor(qb, dtype=torch.int32).reshape(-1).to(device)
+        qb = np.asarray([(i, q0) for i, n in enumerate(lens) for q0 in range(0, n, qblock)], np.int32).reshape(-1)
+        self.nqb = qb.size // 2
+        if str(device) == "cpu":
+            self.ids, self.pos = torch.from_numpy(ids), torch.from_numpy(pos)
+            self.cu, self.qblocks = torch.from_numpy(self.cu_host), torch.from_numpy(qb)
+            return
+        # one pinned staging buffer and ONE asynchronous host->device copy for ids | pos | cu | qblocks:
+        # a pageable .to(device) blocks the host until every kernel queued before it has run, which
+        # serialised the next batch's host work (tokenizer, packing) behind the current encoder
+        # pass.  The caching host allocator keeps the pinned block until the copy has completed.
+        parts = (ids, pos, self.cu_host, qb)
+        span = [(p.size + 3) // 4 * 4 for p in parts]  # every part starts 16-B aligned
+        host = torch.empty(sum(span), dtype=torch.int32, pin_memory=True)
+        hv = host.numpy()
+        o = 0
+        for p, n in zip(parts, span):
+            hv[o: o + p.size] = p
+            o += n
+        dev = host.to(device, non_blocking=True)
+        o = 0
+        views = []
+        for p, n in zip(parts, span):
+            views.append(dev[o: o + p.size])
+            o += n
+        self.ids, self.pos, self.cu, self.qblocks = views
 
 
 class NomicEncoder:

@@ -21,6 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cmath>
+#include <cstdlib>
+#include <map>
+#include <mutex>
 
 namespace {
 
@@ -159,12 +162,22 @@ __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* 
     float s = -INFINITY;
     if (j < L) {
       const uint16_t* kr = Kb + (long)j * ldkv;
+      // hd == 64 * DPL: the key row in batches of 8 16-B loads issued before their FMAs (a
+      // runtime-bound loop issued them one latency at a time: 28 us per step at 32 heads); one batch
+      // in flight keeps the 1024-thread block inside its 128 VGPRs
       float dot = 0.f;
-      for (int c = 0; c < hd; c += 8) {
-        float f[8];
-        unpack8(*(const uint4*)(kr + c), f);
+#pragma unroll 1
+      for (int cb = 0; cb < DPL; ++cb) {
+        uint4 kv[8];
 #pragma unroll
-        for (int e = 0; e < 8; ++e) dot += f[e] * qs[c + e];
+        for (int c = 0; c < 8; ++c) kv[c] = *(const uint4*)(kr + cb * 64 + c * 8);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float f[8];
+          unpack8(kv[c], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dot += f[e] * qs[cb * 64 + c * 8 + e];
+        }
       }
       s = dot;
     }
@@ -210,6 +223,117 @@ __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* 
   }
 }
 
+
+// Split-L decode attention (flash-decoding) for long caches: grid (H, S), workgroup (h, j) of 4 waves
+// scores keys [j c, (j + 1) c) with c = ceil(L / S) rounded up to 64 and writes its unnormalised
+// partial (m, l, acc[hd]) to ws; k_attn_combine merges the S partials of a head.  One workgroup per
+// head streams the whole cache through one CU (164 GB/s at L = 8192, profiles/r2_decode_q4.md).
+constexpr int kSplitWaves = 4;
+constexpr int kMaxSplits = 32;
+
+template <int DPL>
+__global__ __launch_bounds__(kSplitWaves * 64) void k_attn_decode_split(
+    const uint16_t* __restrict__ q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V, long ldkv, int L,
+    int grp, float scale, float* __restrict__ ws, const int32_t* __restrict__ st) {
+  constexpr int hd = 64 * DPL;
+  if (st) L = st[0] + 1;
+  const int h = blockIdx.x, S = gridDim.y, j = blockIdx.y;
+  const int kvh = h / grp;
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int chunk = ((L + S - 1) / S + 63) / 64 * 64;
+  const int k0 = j * chunk, k1 = min(L, k0 + chunk);
+  __shared__ float qs[hd];
+  __shared__ float wm[kSplitWaves], wl[kSplitWaves];
+  __shared__ float wacc[kSplitWaves][hd];
+  for (int d = threadIdx.x; d < hd; d += kSplitWaves * 64) qs[d] = bf2f(q[(long)h * hd + d]) * scale;
+  __syncthreads();
+  const uint16_t* Kb = K + (long)kvh * hd;
+  const uint16_t* Vb = V + (long)kvh * hd + lane * DPL;
+  float m = -INFINITY, l = 0.f, acc[DPL];
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
+  for (int base = k0 + wave * 64; base < k1; base += kSplitWaves * 64) {
+    const int jj = base + lane;
+    float s = -INFINITY;
+    if (jj < k1) {
+      const uint16_t* kr = Kb + (long)jj * ldkv;
+      float dot = 0.f;
+#pragma unroll 1
+      for (int cb = 0; cb < DPL; ++cb) {
+        uint4 kv[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) kv[c] = *(const uint4*)(kr + cb * 64 + c * 8);
+#pragma unroll
+        for (int c = 0; c < 8; ++c) {
+          float f[8];
+          unpack8(kv[c], f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) dot += f[e] * qs[cb * 64 + c * 8 + e];
+        }
+      }
+      s = dot;
+    }
+    float cm = s;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+    const float mn = fmaxf(m, cm);
+    const float corr = __expf(m - mn);
+    const float p = jj < k1 ? __expf(s - mn) : 0.f;
+    float ps = p;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o, 64);
+    l = l * corr + ps;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) acc[i] *= corr;
+    const int nv = min(64, k1 - base);
+#pragma unroll 8
+    for (int t = 0; t < nv; ++t) {
+      const float pt = __shfl(p, t, 64);
+      const uint16_t* vr = Vb + (long)(base + t) * ldkv;
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) acc[i] += pt * bf2f(vr[i]);
+    }
+    m = mn;
+  }
+  if (lane == 0) { wm[wave] = m; wl[wave] = l; }
+#pragma unroll
+  for (int i = 0; i < DPL; ++i) wacc[wave][lane * DPL + i] = acc[i];
+  __syncthreads();
+  float M = wm[0];
+#pragma unroll
+  for (int w = 1; w < kSplitWaves; ++w) M = fmaxf(M, wm[w]);
+  float* o = ws + ((long)h * S + j) * (hd + 2);
+  float c[kSplitWaves], den = 0.f;
+#pragma unroll
+  for (int w = 0; w < kSplitWaves; ++w) {
+    c[w] = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);  // an empty wave (or split) adds nothing
+    den += wl[w] * c[w];
+  }
+  for (int d = threadIdx.x; d < hd; d += kSplitWaves * 64) {
+    float a = 0.f;
+#pragma unroll
+    for (int w = 0; w < kSplitWaves; ++w) a += wacc[w][d] * c[w];
+    o[2 + d] = a;
+  }
+  if (threadIdx.x == 0) { o[0] = M; o[1] = den; }
+}
+
+// out[h] = sum_j acc_j e^(m_j - M) / sum_j l_j e^(m_j - M) over the S partials of head h
+__global__ void k_attn_combine(const float* __restrict__ ws, int S, int hd, uint16_t* __restrict__ out) {
+  const int h = blockIdx.x;
+  const float* p = ws + (long)h * S * (hd + 2);
+  float M = -INFINITY;
+  for (int j = 0; j < S; ++j) M = fmaxf(M, p[(long)j * (hd + 2)]);
+  float den = 0.f, a = 0.f;
+  const int d = threadIdx.x;
+  for (int j = 0; j < S; ++j) {
+    const float* pj = p + (long)j * (hd + 2);
+    const float c = pj[0] == -INFINITY ? 0.f : __expf(pj[0] - M);
+    den += pj[1] * c;
+    if (d < hd) a += pj[2 + d] * c;
+  }
+  if (d < hd) out[(long)h * hd + d] = __builtin_bit_cast(uint16_t, (__bf16)(a / den));
+}
 
 // ------------------------------------------------------------------ decode step --
 // Device state of a generation (int32): [0] pos = tokens already in the KV cache, [1] token = the
@@ -363,6 +487,28 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
   __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nch = K >> 3, ng = K / kQ4Group;
+  // this wave's weight rows, and its first group's weights requested BEFORE x is staged: the HBM
+  // latency of the first loads overlaps the staging and its barriers
+  constexpr int outs = MODE == 2 ? kGemvRows / 2 : kGemvRows;
+  const int o0 = (blockIdx.x * 4 + wave) * outs;
+  const bool active = o0 < nout;
+  long rows[kGemvRows];
+#pragma unroll
+  for (int r = 0; r < kGemvRows; ++r) {
+    int o = o0 + (MODE == 2 ? r / 2 : r);
+    if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
+    rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
+  }
+  const long qrow = K / 2;
+  uint4 wq[kGemvRows];
+  uint32_t sm[kGemvRows];
+  if (active && lane < ng) {
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r) {
+      wq[r] = *(const uint4*)(Wq + rows[r] * qrow + lane * 16);
+      sm[r] = Wsm[rows[r] * ng + lane];
+    }
+  }
   float ss = 0.f;
   for (int c = tid; c < nch; c += 256) {
     float f[8];
@@ -403,25 +549,21 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
     if ((c & 3) == 0) xs[(c >> 2) * kQ4Rec + kQ4Group] = s;
   }
   __syncthreads();
-  constexpr int outs = MODE == 2 ? kGemvRows / 2 : kGemvRows;
-  const int o0 = (blockIdx.x * 4 + wave) * outs;
-  if (o0 >= nout) return;
-  long rows[kGemvRows];
-#pragma unroll
-  for (int r = 0; r < kGemvRows; ++r) {
-    int o = o0 + (MODE == 2 ? r / 2 : r);
-    if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
-    rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
-  }
-  const long qrow = K / 2;
+  if (!active) return;
   float acc[kGemvRows] = {};
   for (int g = lane; g < ng; g += 64) {
-    uint4 wq[kGemvRows];
-    uint32_t sm[kGemvRows];
+    // the group's weights are in registers; request the next group's before the math (one group
+    // of look-ahead per lane: 2 x 4 x 20 B in flight)
+    uint4 cq[kGemvRows];
+    uint32_t csm[kGemvRows];
 #pragma unroll
-    for (int r = 0; r < kGemvRows; ++r) {
-      wq[r] = *(const uint4*)(Wq + rows[r] * qrow + g * 16);
-      sm[r] = Wsm[rows[r] * ng + g];
+    for (int r = 0; r < kGemvRows; ++r) { cq[r] = wq[r]; csm[r] = sm[r]; }
+    if (g + 64 < ng) {
+#pragma unroll
+      for (int r = 0; r < kGemvRows; ++r) {
+        wq[r] = *(const uint4*)(Wq + rows[r] * qrow + (g + 64) * 16);
+        sm[r] = Wsm[rows[r] * ng + g + 64];
+      }
     }
     float xg[kQ4Group];
 #pragma unroll
@@ -429,11 +571,11 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
     const float gs = xs[g * kQ4Rec + kQ4Group];
 #pragma unroll
     for (int r = 0; r < kGemvRows; ++r) {
-      float dot = q4dot8(wq[r].x, xg);
-      dot += q4dot8(wq[r].y, xg + 8);
-      dot += q4dot8(wq[r].z, xg + 16);
-      dot += q4dot8(wq[r].w, xg + 24);
-      acc[r] = fmaf(bf2f(sm[r] & 0xffff), dot, fmaf(bf2f(sm[r] >> 16), gs, acc[r]));
+      float dot = q4dot8(cq[r].x, xg);
+      dot += q4dot8(cq[r].y, xg + 8);
+      dot += q4dot8(cq[r].z, xg + 16);
+      dot += q4dot8(cq[r].w, xg + 24);
+      acc[r] = fmaf(bf2f(csm[r] & 0xffff), dot, fmaf(bf2f(csm[r] >> 16), gs, acc[r]));
     }
   }
 #pragma unroll
@@ -583,23 +725,64 @@ __global__ __launch_bounds__(kSampThreads) void k_sample(const float* __restrict
   const int tid = threadIdx.x;
   auto lg = [&](int i) { return (mask && !mask[i]) ? -INFINITY : logits[i]; };
   float m = -INFINITY;
+#pragma unroll 8  // 8 logit loads in flight per thread (a rolled loop waits one L2 latency per element)
   for (int i = tid; i < V; i += kSampThreads) m = fmaxf(m, lg(i));
   const float M = block_reduce(m, sh, true);
   float z = 0.f;
+#pragma unroll 8  // 8 logit loads in flight per thread (a rolled loop waits one L2 latency per element)
   for (int i = tid; i < V; i += kSampThreads) z += __expf(lg(i) - M);
   const float Z = block_reduce(z, sh, false);
-  // nucleus threshold t: the largest logit cut whose kept mass reaches top_p
-  float lo = M - 40.f, hi = M;  // mass below M - 40 is < V e^-40
+  // nucleus threshold t: the largest logit cut whose kept mass reaches top_p.  Found by two
+  // levels of a 1024-bin mass histogram over the current interval [lo, hi) (LDS float atomics),
+  // each level keeping the bin where the suffix mass crosses top_p * Z: 2 passes over the logits
+  // to a resolution of 40 / 2^20 (a few float ulps of a logit), instead of one pass per bisection
+  // step (24 passes: 163 us per token for a 32000-token vocabulary).
+  __shared__ float hist[kSampThreads];
+  // 8 copies of every bin, picked by lane & 7: flat logits (a random-init model: every logit in
+  // one or two bins) put a wave's 64 same-address LDS atomics into one 64-way conflict; the copies
+  // cut it to 8-way (83 -> ? us per token at V = 32000, profiles/r2_decode_q4.md)
+  __shared__ float hist8[kSampThreads * 8];
+  __shared__ int jstar;
+  float lo = M - 40.f;  // mass below M - 40 is < V e^-40
   if (top_p < 1.f) {
-    for (int it = 0; it < 24; ++it) {
-      const float mid = 0.5f * (lo + hi);
-      float k = 0.f;
+    const float target = top_p * Z;
+    float w = 40.f / kSampThreads * (1.f + 1e-6f);  // bin width: the top bin holds l == M
+    float above = 0.f;                              // mass at or above the interval's upper end
+    for (int level = 0; level < 2; ++level) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) hist8[c * kSampThreads + tid] = 0.f;
+      if (tid == 0) jstar = 0;
+      __syncthreads();
+      const float inv_w = 1.f / w, hi = lo + w * kSampThreads;
+#pragma unroll 8  // 8 logit loads in flight per thread (a rolled loop waits one L2 latency per element)
       for (int i = tid; i < V; i += kSampThreads) {
         const float l = lg(i);
-        if (l >= mid) k += __expf(l - M);
+        if (l >= lo && l < hi) {
+          const int bin = min(kSampThreads - 1, (int)((l - lo) * inv_w));
+          atomicAdd(&hist8[bin * 8 + (tid & 7)], __expf(l - M));
+        }
       }
-      if (block_reduce(k, sh, false) >= top_p * Z) lo = mid;
-      else hi = mid;
+      __syncthreads();
+      {
+        float h = 0.f;
+#pragma unroll
+        for (int c = 0; c < 8; ++c) h += hist8[tid * 8 + c];
+        hist[tid] = h;
+      }
+      __syncthreads();
+      for (int off = 1; off < kSampThreads; off <<= 1) {  // suffix sums: S[j] = mass(l >= lo + j w)
+        const float v = tid + off < kSampThreads ? hist[tid + off] : 0.f;
+        __syncthreads();
+        hist[tid] += v;
+        __syncthreads();
+      }
+      if (hist[tid] + above >= target) atomicMax(&jstar, tid);  // S is non-increasing: the last bin
+      __syncthreads();
+      const int j = jstar;
+      above += j + 1 < kSampThreads ? hist[j + 1] : 0.f;
+      lo += j * w;
+      w *= 1.f / kSampThreads;
+      __syncthreads();
     }
   } else {
     lo = -INFINITY;
@@ -610,6 +793,7 @@ __global__ __launch_bounds__(kSampThreads) void k_sample(const float* __restrict
   const int chunk = (V + kSampThreads - 1) / kSampThreads;
   const int b = tid * chunk, e = min(V, b + chunk);
   float part = 0.f;
+#pragma unroll 8  // 8 logit loads in flight per thread (a rolled loop waits one L2 latency per element)
   for (int i = b; i < e; ++i) {
     const float l = lg(i);
     if (l >= cut) part += __expf((l - M) * it);
@@ -631,6 +815,7 @@ __global__ __launch_bounds__(kSampThreads) void k_sample(const float* __restrict
   if (u >= before && u < scan[tid] && part > 0.f) {
     float run = before;
     int sel = -1;
+#pragma unroll 8  // 8 logit loads in flight per thread (a rolled loop waits one L2 latency per element)
     for (int i = b; i < e; ++i) {
       const float l = lg(i);
       if (l < cut) continue;
@@ -654,6 +839,123 @@ __global__ __launch_bounds__(kSampThreads) void k_sample(const float* __restrict
   }
 }
 
+// The same sampler with the vocabulary held in registers (V <= 1024 * R): every pass reads the
+// thread's R logits from VGPRs instead of re-reading the logit vector (the global-memory form
+// above costs ~2.5 ns per logit per call: 82 us at V = 32000).  Thread t owns tokens t + 1024 k;
+// the categorical draw walks the threads' masses in that fixed order, which is a different but
+// equally valid order of the same distribution.
+template <int R>
+__global__ __launch_bounds__(kSampThreads) void k_sample_reg(const float* __restrict__ logits, int V,
+                                                             const uint8_t* __restrict__ mask, float top_p,
+                                                             float temp, uint64_t seed, int32_t* __restrict__ st,
+                                                             int inc_pos, int32_t* host_tok) {
+  __shared__ float sh[kSampThreads / 64];
+  __shared__ float scan[kSampThreads];
+  __shared__ float hist[kSampThreads];
+  __shared__ float hist8[kSampThreads * 8];
+  __shared__ int jstar, pick;
+  const int tid = threadIdx.x;
+  float v[R];
+  float m = -INFINITY;
+#pragma unroll
+  for (int k = 0; k < R; ++k) {
+    const int i = tid + k * kSampThreads;
+    v[k] = (i < V && !(mask && !mask[i])) ? logits[i] : -INFINITY;
+    m = fmaxf(m, v[k]);
+  }
+  const float M = block_reduce(m, sh, true);
+  float z = 0.f;
+#pragma unroll
+  for (int k = 0; k < R; ++k) z += __expf(v[k] - M);
+  const float Z = block_reduce(z, sh, false);
+  float lo = M - 40.f;  // nucleus cut: two levels of the replicated 1024-bin histogram (k_sample)
+  if (top_p < 1.f) {
+    const float target = top_p * Z;
+    float w = 40.f / kSampThreads * (1.f + 1e-6f);
+    float above = 0.f;
+    for (int level = 0; level < 2; ++level) {
+#pragma unroll
+      for (int c = 0; c < 8; ++c) hist8[c * kSampThreads + tid] = 0.f;
+      if (tid == 0) jstar = 0;
+      __syncthreads();
+      const float inv_w = 1.f / w, hi = lo + w * kSampThreads;
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        if (v[k] >= lo && v[k] < hi)
+          atomicAdd(&hist8[min(kSampThreads - 1, (int)((v[k] - lo) * inv_w)) * 8 + (tid & 7)], __expf(v[k] - M));
+      __syncthreads();
+      float h = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) h += hist8[tid * 8 + c];
+      hist[tid] = h;
+      __syncthreads();
+      for (int off = 1; off < kSampThreads; off <<= 1) {
+        const float x = tid + off < kSampThreads ? hist[tid + off] : 0.f;
+        __syncthreads();
+        hist[tid] += x;
+        __syncthreads();
+      }
+      if (hist[tid] + above >= target) atomicMax(&jstar, tid);
+      __syncthreads();
+      const int j = jstar;
+      above += j + 1 < kSampThreads ? hist[j + 1] : 0.f;
+      lo += j * w;
+      w *= 1.f / kSampThreads;
+      __syncthreads();
+    }
+  } else {
+    lo = -INFINITY;
+  }
+  const float cut = lo;
+  const float it = 1.f / fmaxf(temp, 1e-6f);
+  float part = 0.f;
+#pragma unroll
+  for (int k = 0; k < R; ++k)
+    if (v[k] >= cut) part += __expf((v[k] - M) * it);
+  scan[tid] = part;
+  if (tid == 0) pick = 0x7fffffff;
+  __syncthreads();
+  for (int off = 1; off < kSampThreads; off <<= 1) {
+    const float x = tid >= off ? scan[tid - off] : 0.f;
+    __syncthreads();
+    scan[tid] += x;
+    __syncthreads();
+  }
+  const float total = scan[kSampThreads - 1];
+  const float u = (float)(uniform01(seed, (uint64_t)st[ST_STEP]) * total);
+  const float before = tid ? scan[tid - 1] : 0.f;
+  if (u >= before && u < scan[tid] && part > 0.f) {
+    float run = before;
+    int sel = -1;
+#pragma unroll
+    for (int k = 0; k < R; ++k) {
+      if (sel < 0 && v[k] >= cut) {
+        run += __expf((v[k] - M) * it);
+        if (u < run) sel = tid + k * kSampThreads;
+      }
+    }
+    if (sel < 0)  // rounding at the thread's upper edge: its last kept token
+#pragma unroll
+      for (int k = 0; k < R; ++k)
+        if (v[k] >= cut) sel = tid + k * kSampThreads;
+    atomicMin(&pick, sel);
+  }
+  __syncthreads();
+  if (pick == 0x7fffffff) {  // u landed on a rounding gap at the very top: the most probable token
+#pragma unroll
+    for (int k = 0; k < R; ++k)
+      if (v[k] == M) atomicMin(&pick, tid + k * kSampThreads);
+    __syncthreads();
+  }
+  if (tid == 0) {
+    const int t = pick;
+    st[ST_TOK] = t;
+    st[ST_POS] += inc_pos;
+    st[ST_STEP] += 1;
+    if (host_tok) __hip_atomic_store(host_tok, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -668,13 +970,63 @@ int dec_attn_decode(const void* q, const void* k, const void* v, long ldkv, int 
 }
 
 // as dec_attn_decode; with st != null the cache length is st[0] + 1 (L is ignored)
+// split-L workspace, one per stream (the decode step's layers run in order on one stream): H <= 128
+// heads x kMaxSplits partials of hd + 2 floats, allocated on first use (outside graph capture: the
+// decode engine runs one step eagerly before capturing)
+static float* split_workspace(hipStream_t s) {
+  static std::mutex mu;
+  static std::map<hipStream_t, float*> table;
+  std::lock_guard<std::mutex> g(mu);
+  auto it = table.find(s);
+  if (it != table.end()) return it->second;
+  float* w = nullptr;
+  if (hipMalloc((void**)&w, (size_t)128 * kMaxSplits * (256 + 2) * sizeof(float)) != hipSuccess) return nullptr;
+  return table[s] = w;
+}
+
+// splits for a cache of (up to) L keys: one per 512 keys, at most kMaxSplits; 1 = single-workgroup kernel
+static int decode_splits(int L) {
+  static const int env = [] {
+    const char* e = getenv("SPL_DEC_SPLITS");
+    return e && *e ? atoi(e) : -1;
+  }();
+  if (env >= 1) return env < kMaxSplits ? env : kMaxSplits;
+  const int sp = (L + 511) / 512;
+  return sp < 1 ? 1 : (sp > kMaxSplits ? kMaxSplits : sp);
+}
+
+int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,
+                       float scale, void* out, const int32_t* st, float* ws, hipStream_t s);
 int dec_attn_decode_st(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,
                        float scale, void* out, const int32_t* st, hipStream_t s) {
-  if (st) L = 1;
+  return dec_attn_decode_ws(q, k, v, ldkv, L, H, KVH, hd, scale, out, st, nullptr, s);
+}
+
+// dec_attn_decode_st with a caller-owned split workspace ws (H * 32 * (hd + 2) floats; null: a
+// per-stream one allocated on first use -- a graph-captured step must pass its own, since nothing
+// may be allocated during capture)
+int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,
+                       float scale, void* out, const int32_t* st, float* ws, hipStream_t s) {
+  // with st, L is the cache CAPACITY (sizes the split count; the length itself is read on the device)
   if (L <= 0 || H <= 0 || KVH <= 0 || H % KVH || hd <= 0 || hd % 64 || hd > 256 || ldkv % 8 ||
       ldkv < (long)KVH * hd || ((uintptr_t)k | (uintptr_t)v) % 16)
     return (int)hipErrorInvalidValue;
   const int grp = H / KVH;
+  const int S = decode_splits(L);
+  if (S > 1 && H <= 128) {
+    if (!ws) ws = split_workspace(s);
+    if (!ws) return (int)hipErrorOutOfMemory;
+    const dim3 gs((unsigned)H, (unsigned)S), bs(kSplitWaves * 64);
+    const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
+    switch (hd / 64) {
+      case 1: hipLaunchKernelGGL(k_attn_decode_split<1>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
+      case 2: hipLaunchKernelGGL(k_attn_decode_split<2>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
+      case 3: hipLaunchKernelGGL(k_attn_decode_split<3>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
+      default: hipLaunchKernelGGL(k_attn_decode_split<4>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
+    }
+    hipLaunchKernelGGL(k_attn_combine, dim3((unsigned)H), dim3(256), 0, s, ws, S, hd, (uint16_t*)out);
+    return (int)hipGetLastError();
+  }
   const dim3 g((unsigned)H), b(kDecWaves * 64);
   const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
   uint16_t* oo = (uint16_t*)out;
@@ -801,8 +1153,12 @@ int dec_rope_kv(void* qkv, int H, int KVH, int hd, const float* cos_tab, const f
 int dec_sample(const float* logits, int V, const uint8_t* mask, float top_p, float temp, uint64_t seed, int32_t* st,
                int inc_pos, int32_t* host_tok, hipStream_t s) {
   if (V <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_sample, dim3(1), dim3(kSampThreads), 0, s, logits, V, mask, top_p, temp, seed, st, inc_pos,
-                     host_tok);
+  if (V <= kSampThreads * 32)  // registers hold the vocabulary (llama-2 / mistral: 32000)
+    hipLaunchKernelGGL(k_sample_reg<32>, dim3(1), dim3(kSampThreads), 0, s, logits, V, mask, top_p, temp, seed, st,
+                       inc_pos, host_tok);
+  else
+    hipLaunchKernelGGL(k_sample, dim3(1), dim3(kSampThreads), 0, s, logits, V, mask, top_p, temp, seed, st, inc_pos,
+                       host_tok);
   return (int)hipGetLastError();
 }
 

@@ -252,6 +252,8 @@ class CausalLM:
             self.L.dec_attn_decode.restype = c_int
             self.L.dec_attn_decode_st.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P, P]
             self.L.dec_attn_decode_st.restype = c_int
+            self.L.dec_attn_decode_ws.argtypes = [P, P, P, c_long, c_int, c_int, c_int, c_int, c_float, P, P, P, P]
+            self.L.dec_attn_decode_ws.restype = c_int
             self.L.dec_attn_prefill.argtypes = [P, P, P, P, c_int, c_int, c_int, c_float, P]
             self.L.dec_attn_prefill.restype = c_int
             self.L.dec_gemv.argtypes = [c_int, P, P, c_float, P, c_int, c_int, P, P, P]
@@ -443,6 +445,7 @@ class DecodeEngine:
         self.attn = torch.empty(cfg.d, **e)
         self.ffn = torch.empty(cfg.ffn, **e)
         self.logits = torch.empty(m.head.shape[0], dtype=torch.float32, device=dev)
+        self.attn_ws = torch.empty(cfg.heads * 32 * (cfg.head_dim + 2), dtype=torch.float32, device=dev)  # split-L
         self.host_tok = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.mask = mask[: cfg.vocab].to(device=dev, dtype=torch.uint8).contiguous() if mask is not None else None
         if m.kv is None:
@@ -472,8 +475,10 @@ class DecodeEngine:
             kc, vc = m.kv[li, 0], m.kv[li, 1]
             _chk(L.dec_rope_kv(self.qkv.data_ptr(), H, KVH, hd, m.cos.data_ptr(), m.sin.data_ptr(), self.st.data_ptr(),
                                kc.data_ptr(), vc.data_ptr(), KVH * hd, s), "rope_kv")
-            _chk(L.dec_attn_decode_st(self.qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), KVH * hd, 1, H, KVH, hd,
-                                      hd ** -0.5, self.attn.data_ptr(), self.st.data_ptr(), s), "attn_decode")
+            # L = the cache capacity: sizes the split-L grid; the length itself is read on the device
+            _chk(L.dec_attn_decode_ws(self.qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), KVH * hd, cfg.n_ctx, H, KVH,
+                                      hd, hd ** -0.5, self.attn.data_ptr(), self.st.data_ptr(),
+                                      self.attn_ws.data_ptr(), s), "attn_decode")
             gemv(1, self.attn, None, lw["o"], cfg.d, cfg.d, self.xa, self.xb, "gemv o")
             gemv(2, self.xb, lw["n2"], lw["ug"], lw["ug"].shape[0], cfg.d, None, self.ffn, "gemv up|gate")
             gemv(1, self.ffn, None, lw["down"], cfg.d, cfg.ffn, self.xb, self.xa, "gemv down")

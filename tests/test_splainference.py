@@ -99,18 +99,27 @@ def test_decoder_rmsnorm_rope_kernels_vs_fp32():
 @pytest.mark.parametrize("hd,H,KVH", [(128, 32, 8), (64, 8, 8), (128, 16, 2)])
 def test_decoder_attn_decode_kernel_vs_fp32(hd, H, KVH):
     """dec_attn_decode (csrc/hip/decoder_kernels.hip) against an fp32 softmax(q k^T) v reference,
-    cache lengths on both sides of the 64-key chunk and 256-key workgroup boundaries."""
+    cache lengths on both sides of the 64-key chunk and 256-key workgroup boundaries; past 512 keys
+    the split-L (flash-decoding) kernels + combine, also driven by the device-side length with a
+    larger capacity (empty splits)."""
     import torch
     from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
     m = CausalLM.random(DecoderConfig(layers=1), seed=1, device="cuda")
     g = torch.Generator(device="cuda").manual_seed(7)
-    n_ctx = 1100
+    n_ctx = 5000
     kv = torch.randn((2, n_ctx, KVH, hd), device="cuda", generator=g).to(torch.bfloat16)
     q = torch.randn((H * hd,), device="cuda", generator=g).to(torch.bfloat16)
-    for L in (1, 63, 64, 65, 257, 1100):
+    st = torch.zeros(4, dtype=torch.int32, device="cuda")
+    for L, dev_len in ((1, False), (63, False), (64, False), (65, False), (257, False), (1100, False),
+                       (4097, False), (5000, False), (1, True), (700, True), (5000, True)):
         out = torch.full((H * hd,), float("nan"), device="cuda").to(torch.bfloat16)
-        assert m.L.dec_attn_decode(q.data_ptr(), kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, L, H, KVH, hd,
-                                   hd ** -0.5, out.data_ptr(), None) == 0
+        if dev_len:
+            st[0] = L - 1
+            assert m.L.dec_attn_decode_st(q.data_ptr(), kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, n_ctx, H, KVH,
+                                          hd, hd ** -0.5, out.data_ptr(), st.data_ptr(), None) == 0
+        else:
+            assert m.L.dec_attn_decode(q.data_ptr(), kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, L, H, KVH, hd,
+                                       hd ** -0.5, out.data_ptr(), None) == 0
         torch.cuda.synchronize()
         qf = q.float().reshape(H, hd)
         kf = kv[0, :L].float().repeat_interleave(H // KVH, 1)  # [L, H, hd]
@@ -118,7 +127,7 @@ def test_decoder_attn_decode_kernel_vs_fp32(hd, H, KVH):
         p = torch.softmax(torch.einsum("hd,lhd->hl", qf, kf) * hd ** -0.5, -1)
         ref = torch.einsum("hl,lhd->hd", p, vf).reshape(-1)
         err = (out.float() - ref).abs().max()
-        assert err < 2e-2 * max(1.0, ref.abs().max().item()), (L, float(err))
+        assert err < 2e-2 * max(1.0, ref.abs().max().item()), (L, dev_len, float(err))
 
 
 def test_decoder_kv_cache_matches_full_recompute_cpu():

@@ -1,0 +1,11 @@
+# round 2, call 78 (session 3 mid-point: q4 decode, split-L attention, pipelined e2e): validation of the tree -- default bench (as the driver runs it), kernel profile of it, full GPU suite, smoke
+set -x
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/r2_78
+mkdir -p $O
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 10 --warmup 2 --host-api 0 --embed-e2e 0 > $O/bench_prof.json 2> $O/bench_prof.err &&
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+echo done

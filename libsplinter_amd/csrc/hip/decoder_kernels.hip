@@ -984,15 +984,18 @@ static float* split_workspace(hipStream_t s) {
   return table[s] = w;
 }
 
-// splits for a cache of (up to) L keys: one per 512 keys, at most kMaxSplits; 1 = single-workgroup kernel
+// splits for a cache of (up to) L keys: the single-workgroup kernel up to 512 keys, then one split per
+// 256 keys, at most kMaxSplits (sweep over 4..32 splits at H 32 / KVH 8 / hd 128:
+// profiles/r2_decode_splits.jsonl)
 static int decode_splits(int L) {
   static const int env = [] {
     const char* e = getenv("SPL_DEC_SPLITS");
     return e && *e ? atoi(e) : -1;
   }();
   if (env >= 1) return env < kMaxSplits ? env : kMaxSplits;
-  const int sp = (L + 511) / 512;
-  return sp < 1 ? 1 : (sp > kMaxSplits ? kMaxSplits : sp);
+  if (L <= 512) return 1;
+  const int sp = (L + 255) / 256;
+  return sp > kMaxSplits ? kMaxSplits : sp;
 }
 
 int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, int L, int H, int KVH, int hd,

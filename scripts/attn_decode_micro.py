@@ -40,6 +40,8 @@ for L in (16, 128, 512, 2048, 8192):
                                            hd ** -0.5, o.data_ptr(), None))
     print(json.dumps({"kernel": "dec_attn_decode", "L": L, "H": H, "KVH": KVH, "hd": hd, "us": us,
                       "kv_GB_per_s": 2 * L * KVH * hd * 2 / (us * 1e-6) / 1e9}), flush=True)
+if "--attn-only" in sys.argv:
+    sys.exit(0)
 st = torch.zeros(4, dtype=torch.int32, device="cuda")
 for V in (32000, 128256):
     for kind, scale in (("flat", 0.05), ("spread", 4.0)):

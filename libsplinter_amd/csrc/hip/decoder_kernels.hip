@@ -956,6 +956,255 @@ __global__ __launch_bounds__(kSampThreads) void k_sample_reg(const float* __rest
   }
 }
 
+// ------------------------------------------------------------------ multi-block sampler --
+// The same sampler spread over kSbBlocks workgroups (one contiguous vocabulary slice each), as a
+// chain of small kernels: a single workgroup is bound by one CU (61 us at V 32000, 255-275 us at
+// V 128256).  Workspace layout (floats, caller-owned so the chain can be graph-captured):
+constexpr int kSbBlocks = 64, kSbThreads = 256, kSbBins = 1024;
+enum {
+  SB_BMAX = 0,                          // [64] block max
+  SB_BIDX = SB_BMAX + kSbBlocks,        // [64] first index of the block max (as int bits)
+  SB_BZ = SB_BIDX + kSbBlocks,          // [64] block mass sum exp(l - M)
+  SB_BPART = SB_BZ + kSbBlocks,         // [64] block kept mass (tempered)
+  SB_SCAL = SB_BPART + kSbBlocks,       // [8]  M, Z, lo, w, above, cut
+  SB_HIST = SB_SCAL + 8,                // [64][1024] per-block histograms
+  SB_FLOATS = SB_HIST + kSbBlocks * kSbBins
+};
+
+__device__ __forceinline__ float sb_logit(const float* logits, const uint8_t* mask, int i) {
+  return (mask && !mask[i]) ? -INFINITY : logits[i];
+}
+
+template <int NT>
+__device__ float sb_reduce(float v, bool is_max) {
+  __shared__ float sh[NT / 64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  v = is_max ? wave_max(v) : wave_sum(v);
+  __syncthreads();
+  if (lane == 0) sh[wave] = v;
+  __syncthreads();
+  float r = sh[0];
+  for (int w = 1; w < NT / 64; ++w) r = is_max ? fmaxf(r, sh[w]) : r + sh[w];
+  return r;
+}
+
+// A: block max and its first index
+__global__ __launch_bounds__(kSbThreads) void k_sb_max(const float* __restrict__ logits, int V,
+                                                       const uint8_t* __restrict__ mask, float* __restrict__ ws) {
+  const int chunk = (V + kSbBlocks - 1) / kSbBlocks, b0 = blockIdx.x * chunk, b1 = min(V, b0 + chunk);
+  float m = -INFINITY;
+  int mi = 0x7fffffff;
+#pragma unroll 8
+  for (int i = b0 + (int)threadIdx.x; i < b1; i += kSbThreads) {
+    const float l = sb_logit(logits, mask, i);
+    if (l > m) { m = l; mi = i; }
+  }
+  const float M = sb_reduce<kSbThreads>(m, true);
+  __shared__ int first;
+  if (threadIdx.x == 0) first = 0x7fffffff;
+  __syncthreads();
+  if (m == M) atomicMin(&first, mi);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    ws[SB_BMAX + blockIdx.x] = M;
+    ws[SB_BIDX + blockIdx.x] = __int_as_float(first);
+  }
+}
+
+// B / D: block mass (level 0) and the mass histogram of [lo, lo + 1024 w) (replicated bins, k_sample)
+template <int LEVEL>
+__global__ __launch_bounds__(kSbThreads) void k_sb_hist(const float* __restrict__ logits, int V,
+                                                        const uint8_t* __restrict__ mask, float* __restrict__ ws) {
+  __shared__ float h8[kSbBins * 8];
+  const int tid = threadIdx.x;
+  float M, lo, w;
+  if (LEVEL == 0) {
+    float m = -INFINITY;
+    for (int b = 0; b < kSbBlocks; ++b) m = fmaxf(m, ws[SB_BMAX + b]);
+    M = m;
+    lo = M - 40.f;
+    w = 40.f / kSbBins * (1.f + 1e-6f);
+  } else {
+    M = ws[SB_SCAL + 0];
+    lo = ws[SB_SCAL + 2];
+    w = ws[SB_SCAL + 3];
+  }
+  for (int i = tid; i < kSbBins * 8; i += kSbThreads) h8[i] = 0.f;
+  __syncthreads();
+  const float inv_w = 1.f / w, hi = lo + w * kSbBins;
+  const int chunk = (V + kSbBlocks - 1) / kSbBlocks, b0 = blockIdx.x * chunk, b1 = min(V, b0 + chunk);
+  float z = 0.f;
+#pragma unroll 8
+  for (int i = b0 + tid; i < b1; i += kSbThreads) {
+    const float l = sb_logit(logits, mask, i);
+    const float e = __expf(l - M);
+    if (LEVEL == 0) z += e;
+    if (l >= lo && l < hi) atomicAdd(&h8[min(kSbBins - 1, (int)((l - lo) * inv_w)) * 8 + (tid & 7)], e);
+  }
+  if (LEVEL == 0) {
+    z = sb_reduce<kSbThreads>(z, false);
+    if (tid == 0) ws[SB_BZ + blockIdx.x] = z;
+  }
+  __syncthreads();
+  float* out = ws + SB_HIST + (long)blockIdx.x * kSbBins;
+  for (int t = tid; t < kSbBins; t += kSbThreads) {
+    float v = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) v += h8[t * 8 + c];
+    out[t] = v;
+  }
+}
+
+// C / E: one workgroup of 1024 threads sums the block histograms, finds the bin where the suffix
+// mass crosses top_p Z and narrows [lo, lo + 1024 w) to it (level 1: the cut)
+template <int LEVEL>
+__global__ __launch_bounds__(kSbBins) void k_sb_select(float top_p, float* __restrict__ ws) {
+  __shared__ float hs[kSbBins];
+  __shared__ int jstar;
+  const int tid = threadIdx.x;
+  float M, Z, lo, w, above;
+  if (LEVEL == 0) {
+    float m = -INFINITY;
+    for (int b = 0; b < kSbBlocks; ++b) m = fmaxf(m, ws[SB_BMAX + b]);
+    M = m;
+    Z = 0.f;
+    for (int b = 0; b < kSbBlocks; ++b) Z += ws[SB_BZ + b];
+    lo = M - 40.f;
+    w = 40.f / kSbBins * (1.f + 1e-6f);
+    above = 0.f;
+  } else {
+    M = ws[SB_SCAL + 0]; Z = ws[SB_SCAL + 1]; lo = ws[SB_SCAL + 2]; w = ws[SB_SCAL + 3]; above = ws[SB_SCAL + 4];
+  }
+  float h = 0.f;
+  for (int b = 0; b < kSbBlocks; ++b) h += ws[SB_HIST + (long)b * kSbBins + tid];
+  hs[tid] = h;
+  if (tid == 0) jstar = 0;
+  __syncthreads();
+  for (int off = 1; off < kSbBins; off <<= 1) {  // suffix sums
+    const float x = tid + off < kSbBins ? hs[tid + off] : 0.f;
+    __syncthreads();
+    hs[tid] += x;
+    __syncthreads();
+  }
+  if (hs[tid] + above >= top_p * Z) atomicMax(&jstar, tid);
+  __syncthreads();
+  if (tid == 0) {
+    const int j = jstar;
+    ws[SB_SCAL + 0] = M;
+    ws[SB_SCAL + 1] = Z;
+    ws[SB_SCAL + 4] = above + (j + 1 < kSbBins ? hs[j + 1] : 0.f);
+    ws[SB_SCAL + 2] = lo + j * w;
+    ws[SB_SCAL + 3] = w * (1.f / kSbBins);
+    ws[SB_SCAL + 5] = lo + j * w;  // the cut after the last level
+  }
+}
+
+// F: kept (tempered) mass per block; with top_p >= 1 the cut is -inf and M comes from the maxima
+__global__ __launch_bounds__(kSbThreads) void k_sb_part(const float* __restrict__ logits, int V,
+                                                        const uint8_t* __restrict__ mask, float temp, int nucleus,
+                                                        float* __restrict__ ws) {
+  float M, cut;
+  if (nucleus) {
+    M = ws[SB_SCAL + 0];
+    cut = ws[SB_SCAL + 5];
+  } else {
+    float m = -INFINITY;
+    for (int b = 0; b < kSbBlocks; ++b) m = fmaxf(m, ws[SB_BMAX + b]);
+    M = m;
+    cut = -INFINITY;
+    if (blockIdx.x == 0 && threadIdx.x == 0) { ws[SB_SCAL + 0] = M; ws[SB_SCAL + 5] = cut; }
+  }
+  const float it = 1.f / fmaxf(temp, 1e-6f);
+  const int chunk = (V + kSbBlocks - 1) / kSbBlocks, b0 = blockIdx.x * chunk, b1 = min(V, b0 + chunk);
+  float part = 0.f;
+#pragma unroll 8
+  for (int i = b0 + (int)threadIdx.x; i < b1; i += kSbThreads) {
+    const float l = sb_logit(logits, mask, i);
+    if (l >= cut) part += __expf((l - M) * it);
+  }
+  part = sb_reduce<kSbThreads>(part, false);
+  if (threadIdx.x == 0) ws[SB_BPART + blockIdx.x] = part;
+}
+
+// G: the draw -- the block whose prefix range holds u, then inside its slice (thread t owns the
+// contiguous elements [t c, t c + c)) the token; state update as k_sample
+__global__ __launch_bounds__(kSbBins) void k_sb_draw(const float* __restrict__ logits, int V,
+                                                     const uint8_t* __restrict__ mask, float temp, uint64_t seed,
+                                                     const float* __restrict__ ws, int32_t* __restrict__ st,
+                                                     int inc_pos, int32_t* host_tok) {
+  __shared__ float scan[kSbBins];
+  __shared__ int pick;
+  __shared__ float base_u;
+  __shared__ int blk;
+  const int tid = threadIdx.x;
+  const float M = ws[SB_SCAL + 0], cut = ws[SB_SCAL + 5];
+  const float it = 1.f / fmaxf(temp, 1e-6f);
+  if (tid == 0) {
+    double total = 0.0;
+    for (int b = 0; b < kSbBlocks; ++b) total += ws[SB_BPART + b];
+    const double u = uniform01(seed, (uint64_t)st[ST_STEP]) * total;
+    double run = 0.0;
+    int bb = -1;
+    for (int b = 0; b < kSbBlocks; ++b) {
+      const double p = ws[SB_BPART + b];
+      if (p > 0.0) {
+        if (u < run + p) { bb = b; break; }
+        bb = b;  // rounding at the very end: the last block with mass
+      }
+      run += p;
+    }
+    if (bb >= 0 && u >= run + ws[SB_BPART + bb]) run -= ws[SB_BPART + bb];
+    blk = bb;
+    base_u = (float)(u - run);
+    pick = 0x7fffffff;
+  }
+  __syncthreads();
+  const int chunk = (V + kSbBlocks - 1) / kSbBlocks;
+  if (blk >= 0) {
+    const int b0 = blk * chunk, b1 = min(V, b0 + chunk);
+    const int per = (b1 - b0 + kSbBins - 1) / kSbBins;
+    const int t0 = b0 + tid * per, t1 = min(b1, t0 + per);
+    float part = 0.f;
+    for (int i = t0; i < t1; ++i) {
+      const float l = sb_logit(logits, mask, i);
+      if (l >= cut) part += __expf((l - M) * it);
+    }
+    scan[tid] = part;
+    __syncthreads();
+    for (int off = 1; off < kSbBins; off <<= 1) {
+      const float x = tid >= off ? scan[tid - off] : 0.f;
+      __syncthreads();
+      scan[tid] += x;
+      __syncthreads();
+    }
+    const float u = base_u, before = tid ? scan[tid - 1] : 0.f;
+    if (part > 0.f && u >= before && (u < scan[tid] || tid == kSbBins - 1 || scan[tid] >= scan[kSbBins - 1])) {
+      float run = before;
+      int sel = -1;
+      for (int i = t0; i < t1; ++i) {
+        const float l = sb_logit(logits, mask, i);
+        if (l < cut) continue;
+        sel = i;
+        run += __expf((l - M) * it);
+        if (u < run) break;
+      }
+      if (sel >= 0) atomicMin(&pick, sel);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    int t = pick;
+    if (t == 0x7fffffff) {  // rounding gap: the most probable token (first block holding the max)
+      for (int b = 0; b < kSbBlocks; ++b)
+        if (ws[SB_BMAX + b] == M) { t = __float_as_int(ws[SB_BIDX + b]); break; }
+    }
+    st[ST_TOK] = t;
+    st[ST_POS] += inc_pos;
+    st[ST_STEP] += 1;
+    if (host_tok) __hip_atomic_store(host_tok, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -1150,6 +1399,33 @@ int dec_rope_kv(void* qkv, int H, int KVH, int hd, const float* cos_tab, const f
   const int work = (H + KVH) * hd / 2 + KVH * hd;
   hipLaunchKernelGGL(k_rope_kv, dim3((unsigned)((work + 255) / 256)), dim3(256), 0, s, (uint16_t*)qkv, H, KVH, hd,
                      cos_tab, sin_tab, st, (uint16_t*)kc, (uint16_t*)vc, ldkv);
+  return (int)hipGetLastError();
+}
+
+// floats of the workspace dec_sample_ws needs
+long dec_sample_ws_floats() { return SB_FLOATS; }
+
+// dec_sample with a caller-owned workspace (dec_sample_ws_floats() floats): vocabularies past 4096
+// tokens run the multi-block chain (k_sb_*), smaller ones the single-workgroup register sampler
+int dec_sample_ws(const float* logits, int V, const uint8_t* mask, float top_p, float temp, uint64_t seed,
+                  int32_t* st, int inc_pos, int32_t* host_tok, float* ws, hipStream_t s) {
+  if (V <= 0 || !ws) return (int)hipErrorInvalidValue;
+  if (V <= 4096) {
+    hipLaunchKernelGGL(k_sample_reg<4>, dim3(1), dim3(kSampThreads), 0, s, logits, V, mask, top_p, temp, seed, st,
+                       inc_pos, host_tok);
+    return (int)hipGetLastError();
+  }
+  const dim3 g(kSbBlocks), b(kSbThreads);
+  hipLaunchKernelGGL(k_sb_max, g, b, 0, s, logits, V, mask, ws);
+  const int nucleus = top_p < 1.f;
+  if (nucleus) {
+    hipLaunchKernelGGL(k_sb_hist<0>, g, b, 0, s, logits, V, mask, ws);
+    hipLaunchKernelGGL(k_sb_select<0>, dim3(1), dim3(kSbBins), 0, s, top_p, ws);
+    hipLaunchKernelGGL(k_sb_hist<1>, g, b, 0, s, logits, V, mask, ws);
+    hipLaunchKernelGGL(k_sb_select<1>, dim3(1), dim3(kSbBins), 0, s, top_p, ws);
+  }
+  hipLaunchKernelGGL(k_sb_part, g, b, 0, s, logits, V, mask, temp, nucleus, ws);
+  hipLaunchKernelGGL(k_sb_draw, dim3(1), dim3(kSbBins), 0, s, logits, V, mask, temp, seed, ws, st, inc_pos, host_tok);
   return (int)hipGetLastError();
 }
 

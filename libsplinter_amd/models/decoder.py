@@ -264,6 +264,10 @@ class CausalLM:
             self.L.dec_rope_kv.restype = c_int
             self.L.dec_sample.argtypes = [P, c_int, P, c_float, c_float, ctypes.c_uint64, P, c_int, P, P]
             self.L.dec_sample.restype = c_int
+            self.L.dec_sample_ws.argtypes = [P, c_int, P, c_float, c_float, ctypes.c_uint64, P, c_int, P, P, P]
+            self.L.dec_sample_ws.restype = c_int
+            self.L.dec_sample_ws_floats.argtypes = []
+            self.L.dec_sample_ws_floats.restype = c_long
             self.L.dec_gemv_q4.argtypes = [c_int, P, P, c_float, P, P, c_int, c_int, P, P, P]
             self.L.dec_gemv_q4.restype = c_int
             self.L.dec_q4_quantize.argtypes = [P, c_long, c_int, P, P, P]
@@ -446,6 +450,7 @@ class DecodeEngine:
         self.ffn = torch.empty(cfg.ffn, **e)
         self.logits = torch.empty(m.head.shape[0], dtype=torch.float32, device=dev)
         self.attn_ws = torch.empty(cfg.heads * 32 * (cfg.head_dim + 2), dtype=torch.float32, device=dev)  # split-L
+        self.samp_ws = torch.empty(m.L.dec_sample_ws_floats(), dtype=torch.float32, device=dev)  # multi-block sampler
         self.host_tok = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         self.mask = mask[: cfg.vocab].to(device=dev, dtype=torch.uint8).contiguous() if mask is not None else None
         if m.kv is None:
@@ -488,9 +493,9 @@ class DecodeEngine:
     def _sample(self, logits: torch.Tensor, inc_pos: int):
         from .nomic import _chk, _stream
         m = self.m
-        _chk(m.L.dec_sample(logits.data_ptr(), m.cfg.vocab, self.mask.data_ptr() if self.mask is not None else None,
-                            self.top_p, self.temp, self.seed, self.st.data_ptr(), inc_pos, self.host_tok.data_ptr(),
-                            _stream()), "sample")
+        _chk(m.L.dec_sample_ws(logits.data_ptr(), m.cfg.vocab, self.mask.data_ptr() if self.mask is not None else None,
+                               self.top_p, self.temp, self.seed, self.st.data_ptr(), inc_pos, self.host_tok.data_ptr(),
+                               self.samp_ws.data_ptr(), _stream()), "sample")
 
     def _step(self):
         if not self.use_graph:

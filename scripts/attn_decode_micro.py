@@ -48,3 +48,7 @@ for V in (32000, 128256):
         lg = (torch.randn(V, device="cuda", generator=g) * scale).float()
         us = timeit(lambda: L_.dec_sample(lg.data_ptr(), V, None, 0.9, 0.7, 1234, st.data_ptr(), 0, None, None))
         print(json.dumps({"kernel": "dec_sample", "V": V, "logits": kind, "us": us}), flush=True)
+        ws = torch.empty(L_.dec_sample_ws_floats(), dtype=torch.float32, device="cuda")
+        us = timeit(lambda: L_.dec_sample_ws(lg.data_ptr(), V, None, 0.9, 0.7, 1234, st.data_ptr(), 0, None,
+                                             ws.data_ptr(), None))
+        print(json.dumps({"kernel": "dec_sample_ws (64-block chain)", "V": V, "logits": kind, "us": us}), flush=True)

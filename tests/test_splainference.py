@@ -338,6 +338,47 @@ def test_dec_sample_nucleus_temperature_distribution():
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("V", [50000, 128256])
+def test_dec_sample_multiblock_distribution(V):
+    """dec_sample_ws past 4096 tokens (the 64-block k_sb_* chain): greedy at tiny temperature,
+    never outside the top-p nucleus, tempered nucleus frequencies, with the top tokens scattered
+    over different blocks; top_p = 1 keeps every token eligible."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
+    m = CausalLM.random(DecoderConfig(layers=1), seed=1, device="cuda")
+    p = torch.tensor([0.4, 0.25, 0.15, 0.08, 0.05] + [0.07 / (V - 5)] * (V - 5), dtype=torch.float64)
+    perm = torch.randperm(V, generator=torch.Generator().manual_seed(5))
+    logits = torch.empty(V, dtype=torch.float64)
+    logits[perm] = p.log()
+    lg = logits.float().cuda()
+    st = torch.zeros(4, dtype=torch.int32, device="cuda")
+    host = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+    ws = torch.empty(m.L.dec_sample_ws_floats(), dtype=torch.float32, device="cuda")
+
+    def draw(top_p, temp, n):
+        out = []
+        for _ in range(n):
+            assert m.L.dec_sample_ws(lg.data_ptr(), V, None, top_p, temp, 4321, st.data_ptr(), 0, host.data_ptr(),
+                                     ws.data_ptr(), None) == 0
+            torch.cuda.synchronize()
+            out.append(int(host[0]))
+        return out
+
+    assert set(draw(1.0, 1e-4, 10)) == {int(perm[0])}
+    assert set(draw(0.9, 1e-4, 10)) == {int(perm[0])}
+    toks = draw(0.9, 0.7, 2000)
+    nucleus = [int(perm[i]) for i in range(5)]
+    assert set(toks) <= set(nucleus)
+    q = p[:5] ** (1 / 0.7)
+    q = q / q.sum()
+    for i in range(5):
+        f = toks.count(int(perm[i])) / len(toks)
+        assert abs(f - float(q[i])) < 0.04, (i, f, float(q[i]))
+    wide = draw(1.0, 1.0, 400)  # whole vocabulary eligible: the 7 % tail shows up
+    assert any(t not in nucleus for t in wide)
+
+
+@pytest.mark.gpu
 def test_decode_engine_steps_match_eager_forward():
     """A decode step of DecodeEngine (GEMVs, RoPE + KV append, device-state attention) gives the
     logits of the eager forward through the MFMA GEMMs, token by token (teacher forcing)."""

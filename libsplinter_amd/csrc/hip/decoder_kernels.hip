@@ -368,6 +368,23 @@ __global__ __launch_bounds__(256) void k_gemv(const uint16_t* __restrict__ x, co
   __shared__ float red[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nch = K >> 3;
+  // this wave's outputs and their weight rows; the first chunk of every row is requested BEFORE x
+  // is staged, so its HBM latency overlaps the staging and the barriers (as k_gemv_q4)
+  constexpr int outs = MODE == 2 ? kGemvRows / 2 : kGemvRows;
+  const int o0 = (blockIdx.x * 4 + wave) * outs;
+  const bool active = o0 < nout;
+  long rows[kGemvRows];
+#pragma unroll
+  for (int r = 0; r < kGemvRows; ++r) {
+    int o = o0 + (MODE == 2 ? r / 2 : r);
+    if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
+    rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
+  }
+  uint4 wv[kGemvRows];
+  if (active && lane < nch) {
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r) wv[r] = *(const uint4*)(W + rows[r] * K + lane * 8);
+  }
   float ss = 0.f;
   for (int c = tid; c < nch; c += 256) {
     const uint4 v = *(const uint4*)(x + c * 8);
@@ -393,28 +410,22 @@ __global__ __launch_bounds__(256) void k_gemv(const uint16_t* __restrict__ x, co
     }
   }
   __syncthreads();
-  // this wave's outputs and their weight rows
-  constexpr int outs = MODE == 2 ? kGemvRows / 2 : kGemvRows;
-  const int o0 = (blockIdx.x * 4 + wave) * outs;
-  if (o0 >= nout) return;
-  long rows[kGemvRows];
-#pragma unroll
-  for (int r = 0; r < kGemvRows; ++r) {
-    int o = o0 + (MODE == 2 ? r / 2 : r);
-    if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
-    rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
-  }
+  if (!active) return;
   float acc[kGemvRows] = {};
   for (int c = lane; c < nch; c += 64) {
+    uint4 cw[kGemvRows];
+#pragma unroll
+    for (int r = 0; r < kGemvRows; ++r) cw[r] = wv[r];
+    if (c + 64 < nch) {  // one chunk of look-ahead per row
+#pragma unroll
+      for (int r = 0; r < kGemvRows; ++r) wv[r] = *(const uint4*)(W + rows[r] * K + (c + 64) * 8);
+    }
     float xf[8];
     unpack8(*(const uint4*)(xs + c * 8), xf);
-    uint4 wv[kGemvRows];
-#pragma unroll
-    for (int r = 0; r < kGemvRows; ++r) wv[r] = *(const uint4*)(W + rows[r] * K + c * 8);
 #pragma unroll
     for (int r = 0; r < kGemvRows; ++r) {
       float wf[8];
-      unpack8(wv[r], wf);
+      unpack8(cw[r], wf);
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc[r] += wf[e] * xf[e];
     }

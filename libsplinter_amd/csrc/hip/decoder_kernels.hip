@@ -231,33 +231,44 @@ __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* 
 constexpr int kSplitWaves = 4;
 constexpr int kMaxSplits = 32;
 
-template <int DPL>
+template <int DPL, int G>
 __global__ __launch_bounds__(kSplitWaves * 64) void k_attn_decode_split(
     const uint16_t* __restrict__ q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V, long ldkv, int L,
     int grp, float scale, float* __restrict__ ws, const int32_t* __restrict__ st) {
+  // G query heads of one kv group per workgroup (grouped-query attention): every key and value row
+  // is loaded once for all G heads instead of once per head
   constexpr int hd = 64 * DPL;
   if (st) L = st[0] + 1;
-  const int h = blockIdx.x, S = gridDim.y, j = blockIdx.y;
-  const int kvh = h / grp;
+  const int h0 = blockIdx.x * G, S = gridDim.y, j = blockIdx.y;
+  const int kvh = h0 / grp;
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int chunk = ((L + S - 1) / S + 63) / 64 * 64;
   const int k0 = j * chunk, k1 = min(L, k0 + chunk);
-  __shared__ float qs[hd];
-  __shared__ float wm[kSplitWaves], wl[kSplitWaves];
-  __shared__ float wacc[kSplitWaves][hd];
-  for (int d = threadIdx.x; d < hd; d += kSplitWaves * 64) qs[d] = bf2f(q[(long)h * hd + d]) * scale;
+  __shared__ float qs[G][hd];
+  __shared__ float wm[kSplitWaves][G], wl[kSplitWaves][G];
+  __shared__ float wacc[kSplitWaves][G][hd];
+  for (int d = threadIdx.x; d < G * hd; d += kSplitWaves * 64) qs[d / hd][d % hd] = bf2f(q[(long)h0 * hd + d]) * scale;
   __syncthreads();
   const uint16_t* Kb = K + (long)kvh * hd;
   const uint16_t* Vb = V + (long)kvh * hd + lane * DPL;
-  float m = -INFINITY, l = 0.f, acc[DPL];
+  float m[G], l[G], acc[G][DPL];
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) acc[i] = 0.f;
+  for (int g = 0; g < G; ++g) {
+    m[g] = -INFINITY;
+    l[g] = 0.f;
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) acc[g][i] = 0.f;
+  }
   for (int base = k0 + wave * 64; base < k1; base += kSplitWaves * 64) {
     const int jj = base + lane;
-    float s = -INFINITY;
+    float sc[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) sc[g] = -INFINITY;
     if (jj < k1) {
       const uint16_t* kr = Kb + (long)jj * ldkv;
-      float dot = 0.f;
+      float dot[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) dot[g] = 0.f;
 #pragma unroll 1
       for (int cb = 0; cb < DPL; ++cb) {
         uint4 kv[8];
@@ -268,54 +279,72 @@ __global__ __launch_bounds__(kSplitWaves * 64) void k_attn_decode_split(
           float f[8];
           unpack8(kv[c], f);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) dot += f[e] * qs[cb * 64 + c * 8 + e];
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int e = 0; e < 8; ++e) dot[g] += f[e] * qs[g][cb * 64 + c * 8 + e];
         }
       }
-      s = dot;
+#pragma unroll
+      for (int g = 0; g < G; ++g) sc[g] = dot[g];
     }
-    float cm = s;
+    float p[G];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
-    const float mn = fmaxf(m, cm);
-    const float corr = __expf(m - mn);
-    const float p = jj < k1 ? __expf(s - mn) : 0.f;
-    float ps = p;
+    for (int g = 0; g < G; ++g) {
+      float cm = sc[g];
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o, 64);
-    l = l * corr + ps;
+      for (int o = 32; o > 0; o >>= 1) cm = fmaxf(cm, __shfl_xor(cm, o, 64));
+      const float mn = fmaxf(m[g], cm);
+      const float corr = __expf(m[g] - mn);
+      p[g] = jj < k1 ? __expf(sc[g] - mn) : 0.f;
+      float ps = p[g];
 #pragma unroll
-    for (int i = 0; i < DPL; ++i) acc[i] *= corr;
+      for (int o = 32; o > 0; o >>= 1) ps += __shfl_xor(ps, o, 64);
+      l[g] = l[g] * corr + ps;
+#pragma unroll
+      for (int i = 0; i < DPL; ++i) acc[g][i] *= corr;
+      m[g] = mn;
+    }
     const int nv = min(64, k1 - base);
-#pragma unroll 8
+#pragma unroll 4
     for (int t = 0; t < nv; ++t) {
-      const float pt = __shfl(p, t, 64);
       const uint16_t* vr = Vb + (long)(base + t) * ldkv;
+      float vv[DPL];
 #pragma unroll
-      for (int i = 0; i < DPL; ++i) acc[i] += pt * bf2f(vr[i]);
+      for (int i = 0; i < DPL; ++i) vv[i] = bf2f(vr[i]);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        const float pt = __shfl(p[g], t, 64);
+#pragma unroll
+        for (int i = 0; i < DPL; ++i) acc[g][i] += pt * vv[i];
+      }
     }
-    m = mn;
   }
-  if (lane == 0) { wm[wave] = m; wl[wave] = l; }
 #pragma unroll
-  for (int i = 0; i < DPL; ++i) wacc[wave][lane * DPL + i] = acc[i];
+  for (int g = 0; g < G; ++g) {
+    if (lane == 0) { wm[wave][g] = m[g]; wl[wave][g] = l[g]; }
+#pragma unroll
+    for (int i = 0; i < DPL; ++i) wacc[wave][g][lane * DPL + i] = acc[g][i];
+  }
   __syncthreads();
-  float M = wm[0];
+  for (int g = 0; g < G; ++g) {
+    float M = wm[0][g];
 #pragma unroll
-  for (int w = 1; w < kSplitWaves; ++w) M = fmaxf(M, wm[w]);
-  float* o = ws + ((long)h * S + j) * (hd + 2);
-  float c[kSplitWaves], den = 0.f;
+    for (int w = 1; w < kSplitWaves; ++w) M = fmaxf(M, wm[w][g]);
+    float* o = ws + ((long)(h0 + g) * S + j) * (hd + 2);
+    float c[kSplitWaves], den = 0.f;
 #pragma unroll
-  for (int w = 0; w < kSplitWaves; ++w) {
-    c[w] = wm[w] == -INFINITY ? 0.f : __expf(wm[w] - M);  // an empty wave (or split) adds nothing
-    den += wl[w] * c[w];
+    for (int w = 0; w < kSplitWaves; ++w) {
+      c[w] = wm[w][g] == -INFINITY ? 0.f : __expf(wm[w][g] - M);  // an empty wave (or split) adds nothing
+      den += wl[w][g] * c[w];
+    }
+    for (int d = threadIdx.x; d < hd; d += kSplitWaves * 64) {
+      float a = 0.f;
+#pragma unroll
+      for (int w = 0; w < kSplitWaves; ++w) a += wacc[w][g][d] * c[w];
+      o[2 + d] = a;
+    }
+    if (threadIdx.x == 0) { o[0] = M; o[1] = den; }
   }
-  for (int d = threadIdx.x; d < hd; d += kSplitWaves * 64) {
-    float a = 0.f;
-#pragma unroll
-    for (int w = 0; w < kSplitWaves; ++w) a += wacc[w][d] * c[w];
-    o[2 + d] = a;
-  }
-  if (threadIdx.x == 0) { o[0] = M; o[1] = den; }
 }
 
 // out[h] = sum_j acc_j e^(m_j - M) / sum_j l_j e^(m_j - M) over the S partials of head h
@@ -1279,14 +1308,21 @@ int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, i
   if (S > 1 && H <= 128) {
     if (!ws) ws = split_workspace(s);
     if (!ws) return (int)hipErrorOutOfMemory;
-    const dim3 gs((unsigned)H, (unsigned)S), bs(kSplitWaves * 64);
+    // heads per workgroup: the whole kv group when it is 2, 4 or 8 heads (shared K/V rows), else 1
+    const int G = (grp == 2 || grp == 4 || grp == 8) ? grp : 1;
+    const dim3 gs((unsigned)(H / G), (unsigned)S), bs(kSplitWaves * 64);
     const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
+#define SPLIT(D_, G_) hipLaunchKernelGGL((k_attn_decode_split<D_, G_>), gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st)
+#define SPLIT_G(D_) switch (G) { case 2: SPLIT(D_, 2); break; case 4: SPLIT(D_, 4); break; \
+                                 case 8: SPLIT(D_, 8); break; default: SPLIT(D_, 1); break; }
     switch (hd / 64) {
-      case 1: hipLaunchKernelGGL(k_attn_decode_split<1>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
-      case 2: hipLaunchKernelGGL(k_attn_decode_split<2>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
-      case 3: hipLaunchKernelGGL(k_attn_decode_split<3>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
-      default: hipLaunchKernelGGL(k_attn_decode_split<4>, gs, bs, 0, s, qq, kk, vv, ldkv, L, grp, scale, ws, st); break;
+      case 1: SPLIT_G(1); break;
+      case 2: SPLIT_G(2); break;
+      case 3: SPLIT_G(3); break;
+      default: SPLIT_G(4); break;
     }
+#undef SPLIT_G
+#undef SPLIT
     hipLaunchKernelGGL(k_attn_combine, dim3((unsigned)H), dim3(256), 0, s, ws, S, hd, (uint16_t*)out);
     return (int)hipGetLastError();
   }

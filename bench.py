@@ -69,7 +69,7 @@ def parse():
                         "it sees as JSON and the run ends (tests/test_bench_cpu.py)")
     p.add_argument("--throttle", type=int, default=1, choices=[0, 1],
                    help="1: issue a step's KV launches only after the previous step's encoder finished")
-    p.add_argument("--embed-e2e", type=int, default=5, metavar="STEPS",
+    p.add_argument("--embed-e2e", type=int, default=20, metavar="STEPS",
                    help="after the timed loop, time STEPS end-to-end embedding batches of the splinference path "
                         "(text fetch, WordPiece, varlen batch, slot find, encoder + seqlocked write, labels); 0: off")
     p.add_argument("--host-api", type=int, default=16, metavar="THREADS",
@@ -435,7 +435,8 @@ def main():
     if embedder is not None and args.embed_e2e > 0:
         from libsplinter_amd.models.bench_embed import EmbedE2E
         pipe = EmbedE2E(embedder.enc, batch=args.embed_batch, seq=args.embed_seq, rank=rank)
-        pipe.run()  # warm-up (tokenizer threads, first varlen shapes)
+        for _ in range(2):  # warm-up: tokenizer threads, and both key sets' varlen shapes (first-shape GEMM setup)
+            pipe.run()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         fails_d = torch.zeros((), dtype=torch.int64, device="cuda")

@@ -1,0 +1,9 @@
+# round 2, call 86: default bench with the e2e warm-up covering both key sets (first-shape setup out of the timed region)
+set -x
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/r2_86
+mkdir -p $O
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err &&
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench_driver_args.json 2> $O/bench_driver_args.err &&
+echo done

@@ -456,10 +456,10 @@ class DecodeEngine:
         if m.kv is None:
             m.kv = torch.empty((cfg.layers, 2, cfg.n_ctx, cfg.kv_heads, cfg.head_dim), dtype=torch.bfloat16, device=dev)
         self.use_graph = use_graph
-        self.graph = None
+        self.graphs = {}  # attention span (512 or the capacity) -> captured decode step
         self.steps = 0
 
-    def _enqueue_step(self):
+    def _enqueue_step(self, span: int = 0):
         from .nomic import _chk, _stream
         m, cfg, L = self.m, self.m.cfg, self.m.L
         s = _stream()
@@ -480,8 +480,9 @@ class DecodeEngine:
             kc, vc = m.kv[li, 0], m.kv[li, 1]
             _chk(L.dec_rope_kv(self.qkv.data_ptr(), H, KVH, hd, m.cos.data_ptr(), m.sin.data_ptr(), self.st.data_ptr(),
                                kc.data_ptr(), vc.data_ptr(), KVH * hd, s), "rope_kv")
-            # L = the cache capacity: sizes the split-L grid; the length itself is read on the device
-            _chk(L.dec_attn_decode_ws(self.qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), KVH * hd, cfg.n_ctx, H, KVH,
+            # L = the span the step is captured for (<= 512: one workgroup per head group; else the
+            # capacity, sizing the split-L grid); the length itself is read on the device
+            _chk(L.dec_attn_decode_ws(self.qkv.data_ptr(), kc.data_ptr(), vc.data_ptr(), KVH * hd, span or cfg.n_ctx, H, KVH,
                                       hd, hd ** -0.5, self.attn.data_ptr(), self.st.data_ptr(),
                                       self.attn_ws.data_ptr(), s), "attn_decode")
             gemv(1, self.attn, None, lw["o"], cfg.d, cfg.d, self.xa, self.xb, "gemv o")
@@ -498,22 +499,28 @@ class DecodeEngine:
                                self.samp_ws.data_ptr(), _stream()), "sample")
 
     def _step(self):
+        # two captured steps: up to 512 cached keys the single-workgroup attention kernel, past that
+        # the split-L one sized for the cache capacity (a split grid costs ~9 us more per layer on
+        # short caches: profiles/r2_decode_splits_gqa.jsonl); the host knows the position
+        span = self.m.cfg.n_ctx if self.m.pos + 1 > 512 else min(512, self.m.cfg.n_ctx)
         if not self.use_graph:
-            self._enqueue_step()
+            self._enqueue_step(span)
             return
-        if self.graph is None:
+        g = self.graphs.get(span)
+        if g is None:
             # warm up once outside capture (first-launch code-object loading), then capture
             side = torch.cuda.Stream()
             side.wait_stream(torch.cuda.current_stream())
             saved = self.st.clone()
             with torch.cuda.stream(side):
-                self._enqueue_step()
+                self._enqueue_step(span)
             torch.cuda.current_stream().wait_stream(side)
             self.st.copy_(saved)  # the warm-up step is undone: same state, cache row rewritten next
-            self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
-                self._enqueue_step()
-        self.graph.replay()
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._enqueue_step(span)
+            self.graphs[span] = g
+        g.replay()
 
     def first_token(self, ids: List[int]) -> int:
         """Prefill the prompt (KV cache rows 0..n-1) and sample the first token on the device."""

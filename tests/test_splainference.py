@@ -402,6 +402,31 @@ def test_decode_engine_steps_match_eager_forward():
 
 
 @pytest.mark.gpu
+def test_decode_engine_crosses_split_boundary():
+    """Graph-replayed decode steps across the 512-key boundary where DecodeEngine switches from the
+    single-workgroup attention graph to the split-L graph (capacity 2048) match the eager forward."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecodeEngine, DecoderConfig
+    cfg = DecoderConfig(layers=2, kv_heads=2, n_ctx=2048)
+    eager = CausalLM.random(cfg, seed=6, device="cuda")
+    mdl = CausalLM.random(cfg, seed=6, device="cuda")
+    eng = DecodeEngine(mdl, use_graph=True)
+    ids = [256] + [int(b) for b in (b"abcdefghij" * 51)[:505]]
+    eng.first_token(ids)
+    eager.forward(ids)
+    for i in range(16):  # cache lengths 507 .. 522
+        t = 97 + i % 26
+        eng.st[1] = t
+        eng._step()
+        torch.cuda.synchronize()
+        mdl.pos += 1
+        ref = eager.forward([t])
+        got = eng.logits[: cfg.vocab]
+        assert (got - ref).norm() / ref.norm() < 3e-2, i
+    assert len(eng.graphs) == 2
+
+
+@pytest.mark.gpu
 def test_decode_engine_graph_replay_equals_eager_launches():
     """The captured HIP graph replays exactly the launched step: same seed and prompt give the
     same tokens; prints per-token latency of both."""

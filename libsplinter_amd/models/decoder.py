@@ -409,10 +409,14 @@ class CausalLM:
                 qh, kh, vh = q.transpose(0, 1), K_.transpose(0, 1), V_.transpose(0, 1)
                 # causal over the cache: query i (absolute position pos + i) sees keys 0..pos+i; a single
                 # decode token sees the whole cache, so no mask is needed
-                mask = None if n == 1 else torch.ones((n, L_), dtype=torch.bool, device=self.device).tril(L_ - n)
+                # a fresh prompt (pos 0) is plain causal: is_causal lets torch pick its fused kernel instead
+                # of the materialised-mask path
+                fresh = n > 1 and L_ == n
+                mask = None if n == 1 or fresh else \
+                    torch.ones((n, L_), dtype=torch.bool, device=self.device).tril(L_ - n)
                 a = torch.nn.functional.scaled_dot_product_attention(qh.unsqueeze(0), kh.unsqueeze(0),
                                                                      vh.unsqueeze(0), attn_mask=mask,
-                                                                     enable_gqa=KVH != H)[0]
+                                                                     is_causal=fresh, enable_gqa=KVH != H)[0]
                 a = a.transpose(0, 1).reshape(n, cfg.d).contiguous()
             x = self._mm(1, a, lw["o"], cfg.d, res=x)
             h = self._rms(x, lw["n2"])

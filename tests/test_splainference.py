@@ -40,11 +40,13 @@ def test_state_machine_cpu(uniq):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kv_heads", [8, 2])
-def test_decoder_hip_matches_cpu(kv_heads):
+@pytest.mark.parametrize("kv_heads,heads", [(8, 8), (2, 8), (2, 4)])
+def test_decoder_hip_matches_cpu(kv_heads, heads):
+    """GPU forward (prefill, then one decode step) against the fp32 CPU model; heads 4 gives head
+    dim 128, whose prefill runs torch's fused causal attention (is_causal) instead of k_attn2."""
     import torch
     from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
-    cfg = DecoderConfig(layers=2, kv_heads=kv_heads)
+    cfg = DecoderConfig(layers=2, kv_heads=kv_heads, heads=heads)
     gpu = CausalLM.random(cfg, seed=3, device="cuda")
     cpu = CausalLM.random(cfg, seed=3, device="cpu")
     ids = [256] + list(b"the quick brown fox")

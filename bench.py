@@ -105,6 +105,10 @@ def main():
     # (profiles/r2_hw_queues.md).  Set before anything initialises HIP (the GPU boxes export 4;
     # override with SPLINTER_BENCH_HW_QUEUES).
     os.environ["GPU_MAX_HW_QUEUES"] = os.environ.get("SPLINTER_BENCH_HW_QUEUES", "2")
+    # mixed step: every other writer slice on the low-priority queue pool (arena_kernels.hip
+    # spl_kvs_create): +1.2 % on the throttled mixed step, -13 % on the unthrottled KV-only loop
+    # (profiles/r2_kvs_order.md), so only for mixed
+    os.environ.setdefault("SPL_KVS_SPREAD", "1" if args.mode == "mixed" else "0")
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(_launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -1190,10 +1190,17 @@ void* spl_kvs_create(int writers, int readers) {
   k->nr = readers;
   int lo = 0, hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+  // SPL_KVS_SPREAD=1 (A/B knob): every other writer at the low priority level, so the writer slices
+  // spread over two hardware-queue pools instead of one (profiles/r2_kvs_order.md)
+  static const bool spread = [] {
+    const char* e = getenv("SPL_KVS_SPREAD");
+    return e && *e == '1';
+  }();
   for (int i = 0; i < writers + readers; ++i) {
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
-    if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, i < writers ? 0 : hi) != hipSuccess ||
+    const int prio = i < writers ? ((spread && (i & 1)) ? lo : 0) : hi;
+    if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio) != hipSuccess ||
         hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
       delete k;
       return nullptr;

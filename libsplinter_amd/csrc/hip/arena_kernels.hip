@@ -1192,14 +1192,15 @@ void* spl_kvs_create(int writers, int readers) {
   (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
   // SPL_KVS_SPREAD=1 (A/B knob): every other writer at the low priority level, so the writer slices
   // spread over two hardware-queue pools instead of one (profiles/r2_kvs_order.md)
-  static const bool spread = [] {
+  // (2: readers also alternate between the high and the normal pool)
+  static const int spread = [] {
     const char* e = getenv("SPL_KVS_SPREAD");
-    return e && *e == '1';
+    return e && *e ? atoi(e) : 0;
   }();
   for (int i = 0; i < writers + readers; ++i) {
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
-    const int prio = i < writers ? ((spread && (i & 1)) ? lo : 0) : hi;
+    const int prio = i < writers ? ((spread >= 1 && (i & 1)) ? lo : 0) : ((spread >= 2 && (i & 1)) ? 0 : hi);
     if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio) != hipSuccess ||
         hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
       delete k;

@@ -19,13 +19,57 @@
 #include <string>
 #include <string_view>
 #include <thread>
-#include <unordered_map>
 #include <vector>
 
 namespace {
 
+// Open-addressing piece table keyed by byte strings, looked up with string_views straight into the
+// normalised text (no candidate string is built per lookup).  First insertion of a key wins, as
+// std::unordered_map::emplace did.
+struct PieceTable {
+  struct Entry { uint64_t h; uint32_t off, len; int32_t id; };
+  std::vector<Entry> slots;  // id < 0: empty
+  std::string pool;
+  uint64_t mask = 0;
+
+  static uint64_t hash(const char* p, size_t n) {
+    uint64_t h = 1469598103934665603ull;
+    for (size_t i = 0; i < n; ++i) h = (h ^ (unsigned char)p[i]) * 1099511628211ull;
+    return h ^ (h >> 29);
+  }
+  void init(size_t n) {
+    size_t cap = 16;
+    while (cap < n * 2 + 16) cap <<= 1;
+    slots.assign(cap, Entry{0, 0, 0, -1});
+    mask = cap - 1;
+  }
+  void insert(std::string_view k, int32_t id) {
+    const uint64_t h = hash(k.data(), k.size());
+    for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+      Entry& e = slots[i];
+      if (e.id < 0) {
+        e = Entry{h, (uint32_t)pool.size(), (uint32_t)k.size(), id};
+        pool.append(k.data(), k.size());
+        return;
+      }
+      if (e.h == h && e.len == k.size() && std::memcmp(pool.data() + e.off, k.data(), k.size()) == 0) return;
+    }
+  }
+  int32_t find(const char* p, size_t n) const {
+    const uint64_t h = hash(p, n);
+    for (uint64_t i = h & mask;; i = (i + 1) & mask) {
+      const Entry& e = slots[i];
+      if (e.id < 0) return -1;
+      if (e.h == h && e.len == n && std::memcmp(pool.data() + e.off, p, n) == 0) return e.id;
+    }
+  }
+};
+
 struct Tok {
-  std::unordered_map<std::string, int32_t> vocab;
+  // word-initial lookups (WPM: "▁" + piece, stored stripped; BERT: the bare piece) and continuation
+  // lookups (WPM: the bare piece; BERT: "##" + piece, stored stripped) -- the exact candidates the
+  // greedy longest-match builds
+  PieceTable first, cont;
   int32_t cls = -1, sep = -1, unk = 0;
   bool wpm = false;          // "▁" convention
   size_t max_piece = 1;      // longest vocab entry in bytes
@@ -110,10 +154,23 @@ inline uint32_t fold(uint32_t c) {
   return c;
 }
 
-void split_words(const char* text, size_t n, std::vector<std::string>& words) {
+// normalised text (folded, control chars dropped) + word spans: whitespace separates words,
+// punctuation and CJK ideographs are words of their own
+struct Scratch {
+  std::string norm;
+  std::vector<std::pair<uint32_t, uint32_t>> words;  // (offset, bytes) into norm
+  std::vector<uint32_t> cps;
+};
+
+void split_words(const char* text, size_t n, Scratch& sc) {
   const unsigned char* s = (const unsigned char*)text;
-  std::string cur;
-  auto flush = [&] { if (!cur.empty()) { words.push_back(cur); cur.clear(); } };
+  sc.norm.clear();
+  sc.words.clear();
+  size_t start = 0;
+  auto flush = [&] {
+    if (sc.norm.size() > start) sc.words.emplace_back((uint32_t)start, (uint32_t)(sc.norm.size() - start));
+    start = sc.norm.size();
+  };
   for (size_t i = 0; i < n;) {
     uint32_t c = decode(s, n, i);
     if (c == 0 || is_control(c)) continue;
@@ -122,38 +179,35 @@ void split_words(const char* text, size_t n, std::vector<std::string>& words) {
     if (c == 0) continue;
     if (is_punct(c) || is_cjk(c)) {
       flush();
-      std::string p;
-      encode(c, p);
-      words.push_back(p);
+      encode(c, sc.norm);
+      flush();
       continue;
     }
-    encode(c, cur);
+    encode(c, sc.norm);
   }
   flush();
 }
 
-void wordpiece(const Tok& t, const std::string& word, std::vector<int32_t>& out) {
+void wordpiece(const Tok& t, const char* w, size_t wn, std::vector<uint32_t>& cps, std::vector<int32_t>& out) {
   // code-point boundaries
-  std::vector<size_t> cps;
-  const unsigned char* s = (const unsigned char*)word.data();
-  for (size_t i = 0; i < word.size();) { cps.push_back(i); decode(s, word.size(), i); }
+  cps.clear();
+  const unsigned char* s = (const unsigned char*)w;
+  for (size_t i = 0; i < wn;) { cps.push_back((uint32_t)i); decode(s, wn, i); }
   if (cps.size() > 100) { out.push_back(t.unk); return; }
-  cps.push_back(word.size());
+  cps.push_back((uint32_t)wn);
   const size_t start_n = out.size();
+  const size_t prefix = t.wpm ? 3 : 2;  // bytes of "▁" / "##" counted in a candidate's length
   size_t b = 0;  // index into cps
-  std::string cand;
   while (b + 1 < cps.size()) {
     int32_t found = -1;
     size_t e = cps.size() - 1;
+    const PieceTable& tab = b == 0 ? t.first : t.cont;
+    const size_t extra = (t.wpm ? b == 0 : b != 0) ? prefix : 0;
     for (; e > b; --e) {
       const size_t bytes = cps[e] - cps[b];
-      if (bytes > t.max_piece) continue;
-      cand.clear();
-      if (t.wpm) { if (b == 0) cand = "\xE2\x96\x81"; }
-      else if (b != 0) cand = "##";
-      cand.append(word, cps[b], bytes);
-      auto it = t.vocab.find(cand);
-      if (it != t.vocab.end()) { found = it->second; break; }
+      if (bytes + extra > t.max_piece) continue;
+      found = tab.find(w + cps[b], bytes);
+      if (found >= 0) break;
     }
     if (found < 0) { out.resize(start_n); out.push_back(t.unk); return; }
     out.push_back(found);
@@ -162,11 +216,11 @@ void wordpiece(const Tok& t, const std::string& word, std::vector<int32_t>& out)
 }
 
 int encode_one(const Tok& t, const char* text, size_t n, std::vector<int32_t>& ids, int add_special) {
+  thread_local Scratch sc;
   ids.clear();
   if (add_special && t.cls >= 0) ids.push_back(t.cls);
-  std::vector<std::string> words;
-  split_words(text, n, words);
-  for (auto& w : words) wordpiece(t, w, ids);
+  split_words(text, n, sc);
+  for (auto& [off, len] : sc.words) wordpiece(t, sc.norm.data() + off, len, sc.cps, ids);
   if (add_special && t.sep >= 0) ids.push_back(t.sep);
   return (int)ids.size();
 }
@@ -177,12 +231,22 @@ extern "C" {
 
 void* spl_tok_create(const char* const* tokens, int n, int cls_id, int sep_id, int unk_id) {
   auto* t = new Tok();
-  t->vocab.reserve((size_t)n * 2);
   for (int i = 0; i < n; ++i) {
-    std::string s(tokens[i]);
+    const std::string_view s(tokens[i]);
     if (s.size() > t->max_piece) t->max_piece = s.size();
-    if (s.rfind("\xE2\x96\x81", 0) == 0) t->wpm = true;
-    t->vocab.emplace(std::move(s), i);
+    if (s.substr(0, 3) == "\xE2\x96\x81") t->wpm = true;
+  }
+  t->first.init((size_t)n);
+  t->cont.init((size_t)n);
+  for (int i = 0; i < n; ++i) {
+    const std::string_view s(tokens[i]);
+    if (t->wpm) {
+      if (s.substr(0, 3) == "\xE2\x96\x81") t->first.insert(s.substr(3), i);  // "▁" + piece
+      t->cont.insert(s, i);                                                    // bare piece
+    } else {
+      t->first.insert(s, i);                                                   // bare piece
+      if (s.substr(0, 2) == "##") t->cont.insert(s.substr(2), i);              // "##" + piece
+    }
   }
   t->cls = cls_id;
   t->sep = sep_id;

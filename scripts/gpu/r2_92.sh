@@ -1,0 +1,12 @@
+# round 2, call 92: final validation -- full GPU suite, smoke, default bench (driver args), embed-only bench with e2e
+set -x
+cd $GRAFT_REPO_ROOT
+export TMPDIR=/tmp
+O=$GRAFT_REPO_ROOT/gpurun_out/r2_92
+mkdir -p $O
+timeout -k 10 800 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 &&
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 &&
+timeout -k 10 300 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err &&
+timeout -k 10 200 python bench.py --mode embed --host-api 0 --steps 10 --keys-per-gpu 1000000 > $O/embed.json 2> $O/embed.err &&
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o run -- python3 bench.py --steps 10 --warmup 2 --host-api 0 --embed-e2e 0 > $O/bench_prof.json 2> $O/bench_prof.err &&
+echo done

@@ -19,6 +19,7 @@
 #include <mutex>
 #include <unistd.h>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <string_view>
@@ -344,8 +345,20 @@ int spl_tok_encode_batch(void* tp, const char* const* texts, const size_t* lens,
   };
   if (threads < 1) threads = 1;
   threads = std::min(threads, std::max(1, n / 8));
-  if (threads == 1) work();
-  else pool().run(threads, work);
+  static const bool use_pool = [] {  // SPL_TOK_POOL=0: a thread per worker per batch (A/B)
+    const char* e = getenv("SPL_TOK_POOL");
+    return !(e && *e == '0');
+  }();
+  if (threads == 1) {
+    work();
+  } else if (use_pool) {
+    pool().run(threads, work);
+  } else {
+    std::vector<std::thread> ths;
+    for (int k = 1; k < threads; ++k) ths.emplace_back(work);
+    work();
+    for (auto& th : ths) th.join();
+  }
   long pos = 0;
   offsets[0] = 0;
   for (int i = 0; i < n; ++i) {

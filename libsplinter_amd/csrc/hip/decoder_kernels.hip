@@ -510,12 +510,12 @@ __device__ __forceinline__ float q4dot8(uint32_t w, const float* x) {
 
 // y[n] = x . W[n, :] with W in Q4G32.  Structure of k_gemv: x (optionally RMS-normalised) staged
 // in LDS as fp32 together with its 32-group sums (the m term: sum_k (d q_k + m) x_k =
-// d sum_k q_k x_k + m sum_k x_k); each wave owns 4 weight rows, each lane one 32-k group per row
+// d sum_k q_k x_k + m sum_k x_k); each wave owns R (4 or 8) weight rows, each lane one 32-k group per row
 // and iteration (one 16-B load of nibbles + one scale word per row).
 constexpr int kGemvQ4MaxK = 16384;
 constexpr int kQ4Rec = kQ4Group + 4;  // LDS floats per group record
 
-template <int MODE, bool RMS>
+template <int MODE, bool RMS, int R = kGemvRows>
 __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x, const float* __restrict__ rw,
                                                  float eps, const uint8_t* __restrict__ Wq,
                                                  const uint32_t* __restrict__ Wsm, int K, int nout,
@@ -529,22 +529,22 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
   const int nch = K >> 3, ng = K / kQ4Group;
   // this wave's weight rows, and its first group's weights requested BEFORE x is staged: the HBM
   // latency of the first loads overlaps the staging and its barriers
-  constexpr int outs = MODE == 2 ? kGemvRows / 2 : kGemvRows;
+  constexpr int outs = MODE == 2 ? R / 2 : R;
   const int o0 = (blockIdx.x * 4 + wave) * outs;
   const bool active = o0 < nout;
-  long rows[kGemvRows];
+  long rows[R];
 #pragma unroll
-  for (int r = 0; r < kGemvRows; ++r) {
+  for (int r = 0; r < R; ++r) {
     int o = o0 + (MODE == 2 ? r / 2 : r);
     if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
     rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
   }
   const long qrow = K / 2;
-  uint4 wq[kGemvRows];
-  uint32_t sm[kGemvRows];
+  uint4 wq[R];
+  uint32_t sm[R];
   if (active && lane < ng) {
 #pragma unroll
-    for (int r = 0; r < kGemvRows; ++r) {
+    for (int r = 0; r < R; ++r) {
       wq[r] = *(const uint4*)(Wq + rows[r] * qrow + lane * 16);
       sm[r] = Wsm[rows[r] * ng + lane];
     }
@@ -590,17 +590,17 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
   }
   __syncthreads();
   if (!active) return;
-  float acc[kGemvRows] = {};
+  float acc[R] = {};
   for (int g = lane; g < ng; g += 64) {
     // the group's weights are in registers; request the next group's before the math (one group
     // of look-ahead per lane: 2 x 4 x 20 B in flight)
-    uint4 cq[kGemvRows];
-    uint32_t csm[kGemvRows];
+    uint4 cq[R];
+    uint32_t csm[R];
 #pragma unroll
-    for (int r = 0; r < kGemvRows; ++r) { cq[r] = wq[r]; csm[r] = sm[r]; }
+    for (int r = 0; r < R; ++r) { cq[r] = wq[r]; csm[r] = sm[r]; }
     if (g + 64 < ng) {
 #pragma unroll
-      for (int r = 0; r < kGemvRows; ++r) {
+      for (int r = 0; r < R; ++r) {
         wq[r] = *(const uint4*)(Wq + rows[r] * qrow + (g + 64) * 16);
         sm[r] = Wsm[rows[r] * ng + g + 64];
       }
@@ -610,7 +610,7 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
     for (int e = 0; e < kQ4Group; e += 4) *(float4*)(xg + e) = *(const float4*)(xs + g * kQ4Rec + e);
     const float gs = xs[g * kQ4Rec + kQ4Group];
 #pragma unroll
-    for (int r = 0; r < kGemvRows; ++r) {
+    for (int r = 0; r < R; ++r) {
       float dot = q4dot8(cq[r].x, xg);
       dot += q4dot8(cq[r].y, xg + 8);
       dot += q4dot8(cq[r].z, xg + 16);
@@ -619,13 +619,13 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
     }
   }
 #pragma unroll
-  for (int r = 0; r < kGemvRows; ++r) acc[r] = wave_sum(acc[r]);
+  for (int r = 0; r < R; ++r) acc[r] = wave_sum(acc[r]);
   if (lane < outs) {
     const int o = o0 + lane;
     if (o < nout) {
       float a0 = acc[0], a1 = acc[1];
 #pragma unroll
-      for (int r = 0; r < kGemvRows; ++r)
+      for (int r = 0; r < R; ++r)
         if ((MODE == 2 ? r / 2 : r) == lane) {
           if (MODE == 2) { if (r & 1) a1 = acc[r]; else a0 = acc[r]; }
           else a0 = acc[r];
@@ -1394,14 +1394,23 @@ int dec_gemv_q4(int mode, const void* x, const float* rms_w, float eps, const vo
   if (K <= 0 || K % kQ4Group || K > kGemvQ4MaxK || N <= 0 || (mode == 2 && N % 32) || (mode == 1 && !res) ||
       ((uintptr_t)Wq | (uintptr_t)x) % 16 || (uintptr_t)Wsm % 4 || (rms_w && (uintptr_t)rms_w % 16))
     return (int)hipErrorInvalidValue;
+  // rows per wave: 4, or 8 with SPL_Q4_ROWS=8 (A/B knob: more bytes in flight per wave, half the blocks)
+  static const int R = [] {
+    const char* e = getenv("SPL_Q4_ROWS");
+    return e && atoi(e) == 8 ? 8 : 4;
+  }();
   const int nout = mode == 2 ? N / 2 : N;
-  const int per_block = 4 * (mode == 2 ? kGemvRows / 2 : kGemvRows);
+  const int per_block = 4 * (mode == 2 ? R / 2 : R);
   const dim3 g((unsigned)((nout + per_block - 1) / per_block)), b(256);
   const size_t lds = (size_t)(K / kQ4Group) * kQ4Rec * sizeof(float);
   const uint16_t *xx = (const uint16_t*)x, *rr = (const uint16_t*)res;
   const uint8_t* wq = (const uint8_t*)Wq;
   const uint32_t* wsm = (const uint32_t*)Wsm;
-#define GEMV(M_, R_) hipLaunchKernelGGL((k_gemv_q4<M_, R_>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out)
+#define GEMV(M_, R_)                                                                                           \
+  do {                                                                                                         \
+    if (R == 8) hipLaunchKernelGGL((k_gemv_q4<M_, R_, 8>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out); \
+    else hipLaunchKernelGGL((k_gemv_q4<M_, R_, 4>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out);      \
+  } while (0)
   const bool rms = rms_w != nullptr;
   switch (mode) {
     case 0: if (rms) GEMV(0, true); else GEMV(0, false); break;

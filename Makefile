@@ -16,7 +16,7 @@ HIPFLAGS := -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -D_GNU_SOURCE -I$(SRC)/i
             -I$(SRC)/hip -Wno-unused-result -munsafe-fp-atomics
 LDLIBS   := -ldl -lrt -lpthread
 
-CORE_SRCS := $(SRC)/core/store_host.cpp $(SRC)/core/capi.cpp $(SRC)/core/wordpiece.cpp $(SRC)/core/batch_host.cpp
+CORE_SRCS := $(SRC)/core/store_host.cpp $(SRC)/core/node_store.cpp $(SRC)/core/capi.cpp $(SRC)/core/wordpiece.cpp $(SRC)/core/batch_host.cpp
 CORE_HDRS := $(wildcard $(SRC)/include/*.h $(SRC)/include/*.hpp $(SRC)/core/*.hpp)
 HIP_SRCS  := $(wildcard $(SRC)/hip/*.hip)
 HIP_HDRS  := $(wildcard $(SRC)/hip/*.hpp) $(CORE_HDRS)

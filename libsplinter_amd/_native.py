@@ -169,6 +169,13 @@ def _declare_core(L):
     _sig(L, "spl_find_slot", c_long, S, c_char_p)
     _sig(L, "spl_hash_key", c_u64, c_char_p)
     _sig(L, "splinter_now", c_u64)
+    # node stores (csrc/core/node_store.hpp)
+    _sig(L, "spl_node_join", c_int, c_char_p, c_int, c_int, c_uint, c_size_t, c_size_t, c_uint)
+    _sig(L, "spl_node_leave", c_int, c_char_p, c_int)
+    _sig(L, "spl_node_shard_name", c_int, c_char_p, c_int, c_uint, c_char_p, c_size_t)
+    _sig(L, "spl_node_nshards", c_int, S)
+    _sig(L, "spl_node_shard", c_void_p, S, c_int)
+    _sig(L, "spl_node_shard_of", c_int, c_char_p, c_int)
 
 
 def _declare_hip(L):

@@ -1,6 +1,7 @@
 // capi.cpp — reference-compatible C API (splinter_*) and the handle API
 // (spl_*) over StoreBase.  Backend selection by store name:
 //   "hbm:NAME"            -> HBM arena (libsplinter_hip.so, dlopen'd lazily)
+//   "node:NAME"           -> one store over a node's per-GPU arenas (node_store.hpp)
 //   "file:PATH" / a path  -> regular file (reference -DSPLINTER_PERSISTENT)
 //   "shm:NAME" / NAME     -> POSIX shm object (reference default)
 // Reference C API: /root/reference/splinter.h:288-1213.
@@ -20,6 +21,7 @@
 
 #define SPLINTER_NO_INLINE_NOW 1
 #include "splinter_ext.h"
+#include "node_store.hpp"
 #include "store_host.hpp"
 
 #ifndef SPL_BUILD_ID
@@ -32,7 +34,7 @@ namespace {
 
 std::atomic<StoreBase*> g_cur{nullptr};  // the reference's "one open store per process" (atomic: any thread may switch it)
 
-enum class Kind { Shm, File, Hbm };
+enum class Kind { Shm, File, Hbm, Node };
 
 struct Parsed {
   Kind kind;
@@ -44,6 +46,7 @@ bool env_true(const char* v) { return v && *v && std::strcmp(v, "0") != 0; }
 Parsed parse_name(const char* raw) {
   std::string s(raw ? raw : "");
   if (s.rfind("hbm:", 0) == 0) return {Kind::Hbm, s.substr(4)};
+  if (s.rfind("node:", 0) == 0) return {Kind::Node, s.substr(5)};
   if (s.rfind("file:", 0) == 0) return {Kind::File, s.substr(5)};
   if (s.rfind("shm:", 0) == 0) return {Kind::Shm, s.substr(4)};
 #ifdef SPLINTER_PERSISTENT
@@ -58,16 +61,16 @@ Parsed parse_name(const char* raw) {
 
 std::mutex g_hbm_mu;
 spl::HbmFactory g_hbm_factory = nullptr;
+void* g_hip_handle = nullptr;
 
-spl::HbmFactory hbm_factory() {
-  std::lock_guard<std::mutex> lk(g_hbm_mu);
-  if (g_hbm_factory) return g_hbm_factory;
+void* hip_handle_locked() {
+  if (g_hip_handle) return g_hip_handle;
   std::string path;
   if (const char* env = getenv("SPLINTER_HIP_LIB")) {
     path = env;
   } else {
     Dl_info info;
-    if (dladdr((void*)&hbm_factory, &info) && info.dli_fname) {
+    if (dladdr((void*)&hip_handle_locked, &info) && info.dli_fname) {
       std::string self(info.dli_fname);
       size_t slash = self.rfind('/');
       path = (slash == std::string::npos ? std::string(".") : self.substr(0, slash)) + "/libsplinter_hip.so";
@@ -75,11 +78,16 @@ spl::HbmFactory hbm_factory() {
       path = "libsplinter_hip.so";
     }
   }
-  void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_GLOBAL);
-  if (!h) {
-    fprintf(stderr, "libsplinter: cannot load HBM backend %s: %s\n", path.c_str(), dlerror());
-    return nullptr;
-  }
+  g_hip_handle = dlopen(path.c_str(), RTLD_NOW | RTLD_GLOBAL);
+  if (!g_hip_handle) fprintf(stderr, "libsplinter: cannot load HBM backend %s: %s\n", path.c_str(), dlerror());
+  return g_hip_handle;
+}
+
+spl::HbmFactory hbm_factory() {
+  std::lock_guard<std::mutex> lk(g_hbm_mu);
+  if (g_hbm_factory) return g_hbm_factory;
+  void* h = hip_handle_locked();
+  if (!h) return nullptr;
   g_hbm_factory = (spl::HbmFactory)dlsym(h, "spl_hbm_factory");
   return g_hbm_factory;
 }
@@ -92,6 +100,7 @@ bool default_embeddings() {
 StoreBase* do_create(const char* raw, size_t slots, size_t max_val, unsigned flags, int* err) {
   Parsed p = parse_name(raw);
   bool emb = (flags & SPL_CREATE_EMBEDDINGS) ? true : (flags & SPL_CREATE_NO_EMBEDDINGS) ? false : default_embeddings();
+  if (p.kind == Kind::Node) return spl::NodeStore::create(p.name, slots, max_val, emb, err);
   if (p.kind == Kind::Hbm) {
     spl::HbmFactory f = hbm_factory();
     if (!f) { *err = ENOSYS; return nullptr; }
@@ -103,6 +112,7 @@ StoreBase* do_create(const char* raw, size_t slots, size_t max_val, unsigned fla
 
 StoreBase* do_open(const char* raw, int* err) {
   Parsed p = parse_name(raw);
+  if (p.kind == Kind::Node) return spl::NodeStore::open(p.name, err);
   if (p.kind == Kind::Hbm) {
     spl::HbmFactory f = hbm_factory();
     if (!f) { *err = ENOSYS; return nullptr; }
@@ -117,6 +127,15 @@ void replace_current(StoreBase* s) {
 }
 
 }  // namespace
+
+namespace spl {
+HbmFactory load_hbm_factory() { return hbm_factory(); }
+void* hbm_symbol(const char* sym) {
+  std::lock_guard<std::mutex> lk(g_hbm_mu);
+  void* h = hip_handle_locked();
+  return h ? dlsym(h, sym) : nullptr;
+}
+}  // namespace spl
 
 extern "C" {
 
@@ -240,6 +259,21 @@ int spl_unlink(const char* raw) {
   Parsed p = parse_name(raw);
   if (p.kind == Kind::File) return unlink(p.name.c_str());
   if (p.kind == Kind::Hbm) return shm_unlink((p.name + ".hbm").c_str());
+  if (p.kind == Kind::Node) {
+    // every shard of the node, then its descriptor
+    int err = 0;
+    spl::NodeStore* n = spl::NodeStore::open(p.name, &err);
+    int rc = 0;
+    if (n) {
+      const int k = n->nshards();
+      const uint32_t backend = strcmp(n->shard(0)->backend(), "hbm") == 0 ? 1u : 0u;
+      delete n;
+      for (int i = 0; i < k; ++i)
+        if (spl_unlink(spl::node_shard_name(p.name, i, backend).c_str()) != 0) rc = -1;
+    }
+    if (shm_unlink((p.name + ".node").c_str()) != 0) rc = -1;
+    return rc;
+  }
   return shm_unlink(p.name.c_str());
 }
 const char* spl_version(void) { return "libsplinter_amd 0.1.0 (format v4)"; }

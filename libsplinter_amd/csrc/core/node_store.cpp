@@ -1,0 +1,431 @@
+// node_store.cpp — "node:NAME": one store over the per-GPU arenas of a node (node_store.hpp).
+#include "node_store.hpp"
+
+#include <cerrno>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fcntl.h>
+#include <poll.h>
+#include <sys/eventfd.h>
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
+#include "splinter_ext.h"
+
+namespace spl {
+
+void* hbm_symbol(const char* sym);  // capi.cpp: dlsym in the HBM backend (loaded on demand)
+
+namespace {
+
+size_t desc_span() {
+  const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
+  return (sizeof(NodeDesc) + pg - 1) / pg * pg;
+}
+
+// create: O_EXCL (fails with EEXIST if the node exists); *fresh tells which happened for join
+NodeDesc* map_desc(const std::string& name, bool create, bool excl, bool* fresh, int* err) {
+  const std::string dn = name + ".node";
+  int fd = -1;
+  if (fresh) *fresh = false;
+  if (create) {
+    mode_t prev = env_umask_push();
+    fd = shm_open(dn.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0666);
+    env_umask_pop(prev);
+    if (fd >= 0 && fresh) *fresh = true;
+    if (fd >= 0 && ftruncate(fd, (off_t)desc_span()) != 0) {
+      *err = errno;
+      close(fd);
+      shm_unlink(dn.c_str());
+      return nullptr;
+    }
+    if (fd < 0 && (excl || errno != EEXIST)) { *err = errno; return nullptr; }
+  }
+  if (fd < 0) fd = shm_open(dn.c_str(), O_RDWR | O_CLOEXEC, 0666);
+  if (fd < 0) { *err = errno; return nullptr; }
+  void* p = mmap(nullptr, desc_span(), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) { *err = errno; return nullptr; }
+  return (NodeDesc*)p;
+}
+
+void unmap_desc(NodeDesc* d) { if (d) munmap(d, desc_span()); }
+
+bool wait_magic(NodeDesc* d, int ms) {
+  for (int i = 0; i < ms; ++i) {
+    if (__atomic_load_n(&d->magic, __ATOMIC_ACQUIRE) == kNodeMagic) return true;
+    usleep(1000);
+  }
+  return __atomic_load_n(&d->magic, __ATOMIC_ACQUIRE) == kNodeMagic;
+}
+
+int hbm_devices() {
+  auto f = (int (*)())hbm_symbol("spl_hbm_device_count");
+  return f ? f() : 0;
+}
+
+uint32_t default_backend() {
+  const char* e = getenv("SPLINTER_NODE_BACKEND");
+  if (e && *e) return strcmp(e, "shm") == 0 ? 0u : 1u;
+  return hbm_devices() > 0 ? 1u : 0u;
+}
+
+StoreBase* make_shard(const std::string& node, int i, uint32_t backend, bool create, size_t slots, size_t max_val,
+                      bool emb, int device, int* err) {
+  const std::string full = node_shard_name(node, i, backend);
+  const std::string bare = full.substr(4);  // without the "hbm:" / "shm:" prefix
+  if (backend == 1) {
+    HbmFactory f = load_hbm_factory();
+    if (!f) { *err = ENOSYS; return nullptr; }
+    unsigned flags = emb ? kCreateEmbeddings : kCreateNoEmbeddings;
+    if (device >= 0) flags |= (unsigned)(device + 1) << kCreateDeviceShift;
+    return f(bare.c_str(), slots, max_val, flags, create ? 1 : 0, err);
+  }
+  return create ? (StoreBase*)HostStore::create(bare.c_str(), false, slots, max_val, emb, err)
+                : (StoreBase*)HostStore::open(bare.c_str(), false, err);
+}
+
+}  // namespace
+
+std::string node_shard_name(const std::string& node, int i, uint32_t backend) {
+  return std::string(backend == 1 ? "hbm:" : "shm:") + node + ".s" + std::to_string(i);
+}
+
+StoreBase* NodeStore::route(const char* key) const {
+  return shards_[node_shard_of(KeyRef(key).hash, (int)shards_.size())];
+}
+
+Geometry NodeStore::geometry() const {
+  Geometry g;
+  g.slots = desc_->slots_per_shard * desc_->nshards;
+  g.max_val = desc_->max_val;
+  g.stride = desc_->stride;
+  return g;
+}
+
+NodeStore* NodeStore::create(const std::string& name, size_t slots, size_t max_val, bool emb, int* err) {
+  *err = 0;
+  if (slots == 0 || max_val == 0 || max_val > UINT32_MAX) { *err = ENOTSUP; return nullptr; }
+  const uint32_t backend = default_backend();
+  const int ndev = backend == 1 ? hbm_devices() : 0;
+  if (backend == 1 && ndev <= 0) { *err = ENODEV; return nullptr; }
+  int n = backend == 1 ? ndev : 8;
+  if (const char* e = getenv("SPLINTER_NODE_SHARDS")) n = atoi(e);
+  if (n < 1 || n > kNodeMaxShards) { *err = EINVAL; return nullptr; }
+  const size_t per = (slots + n - 1) / n;
+  if (per > UINT32_MAX || per * n > UINT32_MAX) { *err = ENOTSUP; return nullptr; }
+  bool fresh = false;
+  NodeDesc* d = map_desc(name, true, true, &fresh, err);
+  if (!d) return nullptr;
+  auto* s = new NodeStore();
+  s->name_ = name;
+  s->desc_ = d;
+  s->owner_ = true;
+  std::memset((void*)d, 0, sizeof(NodeDesc));
+  d->nshards = (uint32_t)n;
+  d->backend = backend;
+  d->slots_per_shard = (uint32_t)per;
+  d->max_val = (uint32_t)max_val;
+  d->stride = emb ? (uint32_t)kSlotEmbedBytes : (uint32_t)kSlotCoreBytes;
+  d->creator_pid = (int32_t)getpid();
+  d->event_fd = -1;
+  for (int i = 0; i < n; ++i) {
+    StoreBase* sh = make_shard(name, i, backend, true, per, max_val, emb, backend == 1 ? i % ndev : -1, err);
+    if (!sh) {
+      delete s;
+      return nullptr;
+    }
+    s->shards_.push_back(sh);
+    d->ready_mask |= 1ull << i;
+  }
+  d->version = 1;
+  __atomic_store_n(&d->magic, kNodeMagic, __ATOMIC_RELEASE);
+  return s;
+}
+
+NodeStore* NodeStore::open(const std::string& name, int* err) {
+  *err = 0;
+  NodeDesc* d = map_desc(name, false, false, nullptr, err);
+  if (!d) return nullptr;
+  if (!wait_magic(d, 0)) { unmap_desc(d); *err = EINVAL; return nullptr; }
+  const int n = (int)d->nshards;
+  const uint64_t all = n >= 64 ? ~0ull : ((1ull << n) - 1);
+  if (n < 1 || n > kNodeMaxShards || (__atomic_load_n(&d->ready_mask, __ATOMIC_ACQUIRE) & all) != all) {
+    unmap_desc(d);
+    *err = EAGAIN;  // a joined node whose ranks have not all attached their shard yet
+    return nullptr;
+  }
+  auto* s = new NodeStore();
+  s->name_ = name;
+  s->desc_ = d;
+  for (int i = 0; i < n; ++i) {
+    StoreBase* sh = make_shard(name, i, d->backend, false, 0, 0, false, -1, err);
+    if (!sh) {
+      delete s;
+      return nullptr;
+    }
+    const Geometry g = sh->geometry();
+    if (g.slots != d->slots_per_shard || g.max_val != d->max_val || g.stride != d->stride) {
+      delete sh;
+      delete s;
+      *err = EINVAL;
+      return nullptr;
+    }
+    s->shards_.push_back(sh);
+  }
+  return s;
+}
+
+NodeStore::~NodeStore() {
+  stop_forwarder();
+  for (int fd : shard_fds_) close(fd);
+  if (event_fd_ >= 0) {
+    if (desc_ && __atomic_load_n(&desc_->event_pid, __ATOMIC_ACQUIRE) == (int32_t)getpid()) {
+      __atomic_store_n(&desc_->event_fd, -1, __ATOMIC_RELEASE);
+      __atomic_store_n(&desc_->event_pid, 0, __ATOMIC_RELEASE);
+    }
+    close(event_fd_);
+  }
+  for (auto* sh : shards_) delete sh;
+  if (desc_) {
+    // an HBM node lives as long as its creator (the arenas are its allocations); a host-shard node
+    // persists like any shm store until spl_unlink("node:NAME")
+    const bool drop = owner_ && desc_->backend == 1;
+    if (drop) __atomic_store_n(&desc_->magic, 0u, __ATOMIC_RELEASE);
+    unmap_desc(desc_);
+    if (drop) shm_unlink((name_ + ".node").c_str());
+  }
+}
+
+int NodeStore::set_mop(unsigned mode) {
+  int rc = 0;
+  for (auto* s : shards_) {
+    const int r = s->set_mop(mode);
+    if (r != 0) rc = r;
+  }
+  return rc;
+}
+
+int NodeStore::header_snapshot(splinter_header_snapshot_t* out) {
+  if (!out) return -2;
+  if (shards_[0]->header_snapshot(out) != 0) return -1;
+  uint64_t epoch = out->epoch;
+  for (size_t i = 1; i < shards_.size(); ++i) {
+    splinter_header_snapshot_t h;
+    if (shards_[i]->header_snapshot(&h) != 0) return -1;
+    epoch += h.epoch;
+  }
+  out->epoch = epoch;  // every write bumps its shard's global epoch: the sum is the node's
+  out->slots = geometry().slots;
+  return 0;
+}
+
+int NodeStore::list(char** out_keys, size_t max_keys, size_t* out_count) {
+  if (!out_keys || !out_count) return -2;
+  size_t c = 0;
+  for (auto* s : shards_) {
+    if (c >= max_keys) break;
+    size_t n = 0;
+    if (s->list(out_keys + c, max_keys - c, &n) != 0) return -1;
+    c += n;
+  }
+  *out_count = c;
+  return 0;
+}
+
+int NodeStore::watch_label_register(uint64_t mask, uint8_t g) {
+  int rc = 0;
+  for (auto* s : shards_) {
+    const int r = s->watch_label_register(mask, g);
+    if (r != 0) rc = r;
+  }
+  return rc;
+}
+
+uint64_t NodeStore::signal_count(uint8_t g) {
+  uint64_t v = 0;
+  for (auto* s : shards_) v += s->signal_count(g);
+  return v;
+}
+
+void NodeStore::event_bus_dirty(uint64_t* out, size_t words) {
+  if (!out) return;
+  const size_t n = words < SPLINTER_EVENT_BUS_MASK_WORDS ? words : SPLINTER_EVENT_BUS_MASK_WORDS;
+  std::memset(out, 0, n * 8);
+  uint64_t tmp[SPLINTER_EVENT_BUS_MASK_WORDS];
+  for (auto* s : shards_) {
+    s->event_bus_dirty(tmp, n);
+    for (size_t i = 0; i < n; ++i) out[i] |= tmp[i];
+  }
+}
+
+// One node eventfd: every shard arms its own bus (its kernels and per-call writers raise it) and a
+// forwarder thread turns any shard's wakeup into one on the node's fd.
+int NodeStore::event_bus_init() {
+  stop_forwarder();
+  for (int fd : shard_fds_) close(fd);
+  shard_fds_.clear();
+  for (auto* s : shards_) {
+    if (s->event_bus_init() != 0) return -1;
+    const int fd = s->event_bus_open();
+    if (fd < 0) return -1;
+    shard_fds_.push_back(fd);
+  }
+  const int fd = eventfd(0, EFD_CLOEXEC);
+  if (fd < 0) return -1;
+  if (event_fd_ >= 0) close(event_fd_);
+  event_fd_ = fd;
+  __atomic_store_n(&desc_->event_fd, fd, __ATOMIC_RELEASE);
+  __atomic_store_n(&desc_->event_pid, (int32_t)getpid(), __ATOMIC_RELEASE);
+  fwd_stop_.store(false);
+  fwd_ = std::thread([this] {
+    std::vector<pollfd> p;
+    for (int sfd : shard_fds_) p.push_back(pollfd{sfd, POLLIN, 0});
+    while (!fwd_stop_.load(std::memory_order_acquire)) {
+      const int r = ::poll(p.data(), p.size(), 50);
+      if (r <= 0) continue;
+      bool any = false;
+      for (auto& q : p) {
+        if (q.revents & POLLIN) {
+          uint64_t v;
+          if (read(q.fd, &v, 8) == 8) any = true;
+        }
+        q.revents = 0;
+      }
+      if (any) {
+        const uint64_t one = 1;
+        ssize_t w = write(event_fd_, &one, 8);
+        (void)w;
+      }
+    }
+  });
+  return 0;
+}
+
+int NodeStore::event_bus_open() {
+  const int32_t fd = __atomic_load_n(&desc_->event_fd, __ATOMIC_ACQUIRE);
+  const int32_t pid = __atomic_load_n(&desc_->event_pid, __ATOMIC_ACQUIRE);
+  if (fd < 0 || pid <= 0) { errno = ENODEV; return -1; }
+  if ((pid_t)pid == getpid()) return dup(fd);
+#if defined(SYS_pidfd_open) && defined(SYS_pidfd_getfd)
+  const int pfd = (int)syscall(SYS_pidfd_open, (pid_t)pid, 0);
+  if (pfd < 0) return -1;
+  const int r = (int)syscall(SYS_pidfd_getfd, pfd, fd, 0);
+  close(pfd);
+  return r;
+#else
+  errno = ENOSYS;
+  return -1;
+#endif
+}
+
+void NodeStore::stop_forwarder() {
+  if (fwd_.joinable()) {
+    fwd_stop_.store(true, std::memory_order_release);
+    fwd_.join();
+  }
+}
+
+int NodeStore::madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t timeout) {
+  // one election per node (the node descriptor's bid table); the winner's advice is forwarded to
+  // every shard's residency hint (HBM: a documented no-op, host shards: posix_madvise)
+  if (id == 0 || !shard_present_on(&desc_->control, id)) { errno = EINVAL; return -2; }
+  const uint64_t deadline = now_ticks() + timeout;
+  for (;;) {
+    if (shard_election_on(&desc_->control, nullptr) == id) break;
+    if (timeout == 0) { errno = EAGAIN; return -1; }
+    if (timeout != UINT64_MAX && now_ticks() >= deadline) { errno = ETIMEDOUT; return -1; }
+    usleep(5000);
+  }
+  (void)addr;
+  (void)len;
+  (void)advice;
+  return 0;
+}
+
+}  // namespace spl
+
+using spl::NodeDesc;
+using spl::NodeStore;
+
+extern "C" {
+
+// A rank's shard joins node NAME (the shard store itself -- node_shard_name(NAME, shard, backend)
+// -- is created by the caller first).  The first rank creates the node descriptor; every rank must
+// pass the same geometry.  0 on success, -1 with errno.
+int spl_node_join(const char* name, int shard, int nshards, unsigned backend, size_t slots_per_shard, size_t max_val,
+                  unsigned stride) {
+  if (!name || shard < 0 || nshards < 1 || nshards > spl::kNodeMaxShards || shard >= nshards || backend > 1 ||
+      slots_per_shard == 0 || slots_per_shard > UINT32_MAX || max_val == 0 || max_val > UINT32_MAX ||
+      (stride != spl::kSlotCoreBytes && stride != spl::kSlotEmbedBytes)) {
+    errno = EINVAL;
+    return -1;
+  }
+  int err = 0;
+  bool fresh = false;
+  NodeDesc* d = spl::map_desc(name, true, false, &fresh, &err);
+  if (!d) { errno = err; return -1; }
+  if (fresh) {
+    d->nshards = (uint32_t)nshards;
+    d->backend = backend;
+    d->slots_per_shard = (uint32_t)slots_per_shard;
+    d->max_val = (uint32_t)max_val;
+    d->stride = stride;
+    d->event_fd = -1;
+    d->version = 1;
+    __atomic_store_n(&d->magic, spl::kNodeMagic, __ATOMIC_RELEASE);
+  } else if (!spl::wait_magic(d, 5000)) {
+    spl::unmap_desc(d);
+    errno = ETIMEDOUT;
+    return -1;
+  }
+  if (d->nshards != (uint32_t)nshards || d->backend != backend || d->slots_per_shard != slots_per_shard ||
+      d->max_val != max_val || d->stride != stride) {
+    spl::unmap_desc(d);
+    errno = EINVAL;
+    return -1;
+  }
+  __atomic_fetch_or(&d->ready_mask, 1ull << shard, __ATOMIC_ACQ_REL);
+  spl::unmap_desc(d);
+  return 0;
+}
+
+// The shard leaves; the last one out removes the node descriptor.
+int spl_node_leave(const char* name, int shard) {
+  if (!name || shard < 0 || shard >= spl::kNodeMaxShards) { errno = EINVAL; return -1; }
+  int err = 0;
+  NodeDesc* d = spl::map_desc(name, false, false, nullptr, &err);
+  if (!d) { errno = err; return -1; }
+  const uint64_t left = __atomic_and_fetch(&d->ready_mask, ~(1ull << shard), __ATOMIC_ACQ_REL);
+  spl::unmap_desc(d);
+  if (left == 0) shm_unlink((std::string(name) + ".node").c_str());
+  return 0;
+}
+
+// shard store name (with backend prefix) of shard i of a node; length written, -1 if cap too small
+int spl_node_shard_name(const char* name, int shard, unsigned backend, char* out, size_t cap) {
+  if (!name || !out) return -1;
+  const std::string s = spl::node_shard_name(name, shard, backend);
+  if (s.size() + 1 > cap) return -1;
+  std::memcpy(out, s.c_str(), s.size() + 1);
+  return (int)s.size();
+}
+
+// shards of an open node store (-1 if `h` is not one) and their handles
+int spl_node_nshards(spl_store* h) {
+  auto* n = dynamic_cast<NodeStore*>((spl::StoreBase*)h);
+  return n ? n->nshards() : -1;
+}
+spl_store* spl_node_shard(spl_store* h, int i) {
+  auto* n = dynamic_cast<NodeStore*>((spl::StoreBase*)h);
+  return n ? (spl_store*)n->shard(i) : nullptr;
+}
+// owning shard of a key under an n-way node (== parallel/sharded.py shard_of)
+int spl_node_shard_of(const char* key, int nshards) {
+  if (!key || nshards < 1) return -1;
+  return spl::node_shard_of(spl::KeyRef(key).hash, nshards);
+}
+
+}  // extern "C"

@@ -87,7 +87,7 @@ KeyRef::KeyRef(const char* k) {
 }
 
 // ------------------------------------------------------------ lifecycle --
-static mode_t env_umask_push() {
+mode_t env_umask_push() {
   const char* env = getenv("SPLINTER_DEFAULT_UMASK");
   if (!env || !*env) return (mode_t)-1;
   char* end = nullptr;
@@ -96,7 +96,7 @@ static mode_t env_umask_push() {
   if (errno || end == env || *end || v < 0 || v > 0777) return (mode_t)-1;
   return umask((mode_t)v);
 }
-static void env_umask_pop(mode_t prev) { if (prev != (mode_t)-1) umask(prev); }
+void env_umask_pop(mode_t prev) { if (prev != (mode_t)-1) umask(prev); }
 
 HostStore::~HostStore() {
   if (event_fd_ >= 0) close(event_fd_);

@@ -2,11 +2,20 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <sys/types.h>
 #include "splinter_store.hpp"
 
 namespace spl {
 
 uint64_t now_ticks();
+
+// SPLINTER_DEFAULT_UMASK (octal) applied around the creation of a store's shared objects
+// (reference splinter.c:131-146); pop restores the process umask.
+mode_t env_umask_push();
+void env_umask_pop(mode_t prev);
+
+// The HBM backend's factory (libsplinter_hip.so, loaded on first use); nullptr if unavailable.
+HbmFactory load_hbm_factory();
 
 // Canonical key: first 63 bytes, NUL padded to 64; hash = FNV-1a of those bytes.
 struct KeyRef {

@@ -544,6 +544,7 @@ int CmdRing::init(int device, uint32_t pstride) {
   clock_khz_ = khz > 0 ? khz : 100000;
   idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
   spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
+  yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
   return 0;
 }
 
@@ -583,11 +584,32 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   };
   uint32_t t = ticket_.fetch_add(1, std::memory_order_relaxed);
   uint32_t e = entry_of(t);
+  timespec t0;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  auto elapsed_us = [&t0]() {
+    timespec n;
+    clock_gettime(CLOCK_MONOTONIC, &n);
+    return (uint64_t)(n.tv_sec - t0.tv_sec) * 1000000u + (uint64_t)((n.tv_nsec - t0.tv_nsec) / 1000);
+  };
   for (uint32_t spins = 0;; ++spins) {
     uint32_t z = 0;
     if (busy_[e].compare_exchange_weak(z, 1u, std::memory_order_acquire)) break;
+    // an entry a timed-out caller abandoned (busy 2) is reclaimed once the worker has finished it
+    z = 2;
+    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == kRingDone &&
+        busy_[e].compare_exchange_strong(z, 1u, std::memory_order_acquire)) {
+      __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
+      break;
+    }
     e = entry_of(++t);
-    if ((spins & 63) == 63) _mm_pause();
+    if ((spins & 63) == 63) {
+      _mm_pause();
+      if (elapsed_us() > 30000000u) {  // every entry held for 30 s: the GPU stopped serving
+        errno = EBUSY;
+        return -1;
+      }
+      sched_yield();
+    }
   }
   RingCmd* c = cmds_ + e;
   c->op = op;
@@ -601,20 +623,25 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   if (in && in_len) std::memcpy(payload_ + (size_t)e * pstride_, in, in_len);
   __atomic_store_n(&shared_->state[e], (uint32_t)kRingReady, __ATOMIC_RELEASE);
   if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);
-  timespec t0;
   clock_gettime(CLOCK_MONOTONIC, &t0);
+  // Wait for completion: spin (a call is served in ~10 us), then give the CPU away between polls --
+  // with more caller threads than CPUs, spinning waiters starve the callers whose completions have
+  // already landed (the 16 -> 32 thread collapse of profiles/r2_hostapi_ring_v3.md)
+  const uint64_t spin_us = yield_after_us_;
   for (uint64_t spins = 1;; ++spins) {
     if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == kRingDone) break;
     _mm_pause();
-    if ((spins & 1023) == 0) {
-      if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);  // worker idled out meanwhile
-      timespec t;
-      clock_gettime(CLOCK_MONOTONIC, &t);
-      if (t.tv_sec - t0.tv_sec > 30) {  // the GPU stopped serving: leak the entry (it stays busy)
-        errno = ETIMEDOUT;
-        return -1;
+    if ((spins & 31) == 0) {
+      const uint64_t us = elapsed_us();
+      if (us > spin_us) sched_yield();
+      if ((spins & 1023) == 0) {
+        if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);  // worker idled out meanwhile
+        if (us > 30000000u) {  // the GPU stopped serving: abandon the entry (reclaimed once done)
+          busy_[e].store(2u, std::memory_order_release);
+          errno = ETIMEDOUT;
+          return -1;
+        }
       }
-      if (spins > (1u << 16)) sched_yield();
     }
   }
   uint64_t sl;

@@ -72,6 +72,20 @@ struct HbmDescriptor {
     }                                                                           \
   } while (0)
 
+// The calling thread's current device switched to a store's device for the scope (a process may
+// hold arenas on several GPUs: a node store).
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    if (dev >= 0 && prev != dev) (void)hipSetDevice(dev);
+    else prev = -1;
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
 int neg_to_errno(int32_t st) {
   switch (st) {
     case -11: return EAGAIN;
@@ -122,6 +136,7 @@ class HbmStore final : public StoreBase {
     return 0;
   }
   void purge() override {
+    DevGuard dg(device_);
     std::lock_guard<std::mutex> lk(mu_);
     spl_arena_purge(arena(), stream_);
     (void)hipStreamSynchronize(stream_);
@@ -167,8 +182,8 @@ class HbmStore final : public StoreBase {
     RingResult r;
     const bool direct = buf && buf_sz >= geo_.max_val;  // the whole value fits: copy straight out
     if (!direct) tmp.resize(geo_.max_val + 16);
-    if (ring(kRingGet, 0, key, nullptr, 0, 0, direct ? buf : tmp.data(), (uint32_t)(direct ? buf_sz : tmp.size()), &r) != 0)
-      return -1;
+    const uint32_t cap = direct ? (uint32_t)std::min<size_t>(buf_sz, geo_.max_val) : (uint32_t)tmp.size();
+    if (ring(kRingGet, 0, key, nullptr, 0, 0, direct ? buf : tmp.data(), cap, &r) != 0) return -1;
     if (r.status != 0) { errno = neg_to_errno(r.status); return -1; }
     if (out_sz) *out_sz = r.out_len;
     if (buf && !direct) {
@@ -481,6 +496,7 @@ class HbmStore final : public StoreBase {
   // appended on the host; stops once `limit` matches are collected.
   static constexpr uint32_t kScanChunk = 1u << 22;
   void scan(int mode, uint64_t mask, std::vector<uint32_t>& idx, std::vector<uint64_t>& ep, size_t limit) {
+    DevGuard dg(device_);
     std::lock_guard<std::mutex> lk(mu_);
     idx.clear();
     ep.clear();
@@ -521,6 +537,7 @@ class HbmStore final : public StoreBase {
     return 0;
   }
   void fetch_cores(const std::vector<uint32_t>& idx) {
+    DevGuard dg(device_);
     std::lock_guard<std::mutex> lk(mu_);
     list_cache_.assign(idx.size() * 128, 0);
     if (idx.empty() || ensure_scan_scratch() != 0) return;
@@ -638,8 +655,12 @@ int HbmStore::setup_buffers() {
 
 static HbmDescriptor* map_descriptor(const std::string& name, bool create, int* err) {
   const std::string dn = name + ".hbm";
+  // created under SPLINTER_DEFAULT_UMASK like a host store (reference splinter.c:131-146): the
+  // descriptor's mode is also what the owner's chunk-fd server admits peers by (vmm_share.hpp)
+  mode_t prev = create ? env_umask_push() : (mode_t)-1;
   int fd = create ? shm_open(dn.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0666)
                   : shm_open(dn.c_str(), O_RDWR | O_CLOEXEC, 0666);
+  if (create) env_umask_pop(prev);
   if (fd < 0) { *err = errno; return nullptr; }
   const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
   const size_t span = (sizeof(HbmDescriptor) + pg - 1) / pg * pg;
@@ -709,7 +730,8 @@ HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool 
     d->nchunks = (uint32_t)s->vmm_.chunks();
     d->chunk_bytes = s->vmm_.chunk();
     snprintf(d->sock, sizeof d->sock, "splinter-hbm-%d-%s", (int)getpid(), name);
-    if (s->vmm_.serve(d->sock) != 0) d->sock[0] = 0;  // not attachable; this process still works
+    if (s->vmm_.serve(d->sock, "/dev/shm/" + std::string(name) + ".hbm") != 0)
+      d->sock[0] = 0;  // not attachable; this process still works
   } else if (hipIpcGetMemHandle(&d->handle, s->raw_) != hipSuccess) {
     std::memset(&d->handle, 0, sizeof d->handle);
   }
@@ -735,7 +757,7 @@ HbmStore* HbmStore::open(const char* name, int* err) {
   s->geo_.max_val = d->max_val;
   s->geo_.stride = d->stride;
   s->device_ = (int)d->device;
-  (void)hipSetDevice(s->device_);
+  DevGuard dg(s->device_);
   if (d->version >= 3 && d->mode == 1) {
     std::vector<int> fds;
     size_t chunk = 0;
@@ -759,6 +781,7 @@ HbmStore* HbmStore::open(const char* name, int* err) {
 }
 
 HbmStore::~HbmStore() {
+  DevGuard dg(device_);
   stop_proxy();
   ring_.stop();  // the worker reads the arena: drain it before the arena goes away
   if (stream_) (void)hipStreamSynchronize(stream_);
@@ -799,6 +822,7 @@ HbmStore::~HbmStore() {
 long HbmStore::search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap,
                           spl_search_hit* out) {
   if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
+  DevGuard dg(device_);
   std::vector<float> sd((size_t)geo_.slots * 2);
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -858,6 +882,7 @@ long HbmStore::search_all(const float* q, uint64_t mask, float min_sim, float ma
 // Checkpoint: stream the device image into a v4 store file (byte-identical
 // layout, so the host backend — or the reference library — can open it).
 int HbmStore::checkpoint(const char* path) {
+  DevGuard dg(device_);
   int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
   if (fd < 0) return -1;
   const size_t total = geo_.total_bytes();
@@ -884,6 +909,7 @@ int HbmStore::checkpoint(const char* path) {
 }
 
 int HbmStore::restore_from(const char* path) {
+  DevGuard dg(device_);
   int fd = ::open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return -1;
   struct stat sb;
@@ -913,7 +939,11 @@ int HbmStore::restore_from(const char* path) {
 }
 
 StoreBase* hbm_factory_impl(const char* name, size_t slots, size_t max_val, unsigned flags, int create, int* err) {
-  if (create) return HbmStore::create(name, slots, max_val, (flags & kCreateEmbeddings) != 0, err);
+  if (create) {
+    const int dev = (int)((flags >> kCreateDeviceShift) & 0xFF) - 1;  // -1: the current device
+    DevGuard dg(dev);
+    return HbmStore::create(name, slots, max_val, (flags & kCreateEmbeddings) != 0, err);
+  }
   return HbmStore::open(name, err);
 }
 
@@ -939,21 +969,65 @@ uint32_t spl_hbm_ring_launches(spl_store* h) {
   return s ? s->ring_launches() : 0;
 }
 
-long spl_hbm_search(spl_store* h, const float* query, uint64_t mask, float min_sim, float max_dist, long cap,
-                    spl_search_hit* out) {
-  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
-  if (!s || !query || (cap > 0 && !out)) return -2;
-  return s->search_all(query, mask, min_sim, max_dist, cap, out);
+int spl_hbm_device_count(void) {
+  int n = 0;
+  return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
 }
 
+// CLI search on an HBM store, or on a node store of HBM shards: every shard scores its own slots
+// on its GPU, the per-shard best `cap` are merged by (similarity desc, distance asc) on the host --
+// the in-process form of the C4 top-k merge (parallel/sharded.py search_topk)
+long spl_hbm_search(spl_store* h, const float* query, uint64_t mask, float min_sim, float max_dist, long cap,
+                    spl_search_hit* out) {
+  if (!h || !query || (cap > 0 && !out)) return -2;
+  if (auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h)) return s->search_all(query, mask, min_sim, max_dist, cap, out);
+  const int n = spl_node_nshards(h);
+  if (n < 1) return -2;
+  std::vector<spl_search_hit> all;
+  long total = 0;
+  for (int i = 0; i < n; ++i) {
+    auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+    if (!s) return -2;
+    std::vector<spl_search_hit> part((size_t)std::max<long>(cap, 0));
+    const long c = s->search_all(query, mask, min_sim, max_dist, cap, part.data());
+    if (c < 0) return -1;
+    total += c;
+    part.resize((size_t)std::min<long>(c, cap));
+    all.insert(all.end(), part.begin(), part.end());
+  }
+  auto better = [](const spl_search_hit& a, const spl_search_hit& b) {
+    const float sa = a.emb ? a.sim : 0.f, sb = b.emb ? b.sim : 0.f;
+    if (sa != sb) return sa > sb;
+    if (a.dist != b.dist) return a.dist < b.dist;
+    return strncmp(a.key, b.key, 64) < 0;
+  };
+  std::sort(all.begin(), all.end(), better);
+  const size_t keep = (size_t)std::min<long>((long)all.size(), std::max<long>(cap, 0));
+  for (size_t i = 0; i < keep; ++i) out[i] = all[i];
+  return total;
+}
+
+// checkpoint / restore of an HBM store, or of every shard of a node store (PATH.s<i>)
 int spl_hbm_checkpoint(spl_store* h, const char* path) {
-  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
-  return s ? s->checkpoint(path) : -2;
+  if (auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h)) return s->checkpoint(path);
+  const int n = path ? spl_node_nshards(h) : -1;
+  if (n < 1) return -2;
+  for (int i = 0; i < n; ++i) {
+    auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+    if (!s || s->checkpoint((std::string(path) + ".s" + std::to_string(i)).c_str()) != 0) return -1;
+  }
+  return 0;
 }
 
 int spl_hbm_restore(spl_store* h, const char* path) {
-  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
-  return s ? s->restore_from(path) : -2;
+  if (auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h)) return s->restore_from(path);
+  const int n = path ? spl_node_nshards(h) : -1;
+  if (n < 1) return -2;
+  for (int i = 0; i < n; ++i) {
+    auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+    if (!s || s->restore_from((std::string(path) + ".s" + std::to_string(i)).c_str()) != 0) return -1;
+  }
+  return 0;
 }
 
 }  // extern "C"

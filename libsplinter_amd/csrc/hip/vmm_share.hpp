@@ -21,6 +21,7 @@
 #include <poll.h>
 #include <string>
 #include <sys/socket.h>
+#include <sys/stat.h>
 #include <sys/un.h>
 #include <mutex>
 #include <thread>
@@ -133,8 +134,11 @@ class VmmArena {
 
   // ---------------------------------------------------- descriptor passing --
   // Abstract-namespace socket "\0<name>": serve every connecting process one copy of the chunk
-  // descriptors (header {u64 n, u64 chunk}, then the fds in SCM_RIGHTS batches).
-  int serve(const std::string& name) {
+  // descriptors (header {u64 n, u64 chunk}, then the fds in SCM_RIGHTS batches).  The chunk fds
+  // map the whole arena read-write, so a peer gets them only if it could open the store's
+  // descriptor itself: same uid (or root), or the descriptor file's group / other rw bits admit it
+  // (SO_PEERCRED against the mode the store was created with, SPLINTER_DEFAULT_UMASK included).
+  int serve(const std::string& name, const std::string& desc_path = std::string()) {
     sock_ = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
     if (sock_ < 0) return -1;
     sockaddr_un a;
@@ -145,13 +149,13 @@ class VmmArena {
       return -1;
     }
     stop_ = false;
-    server_ = std::thread([this] {
+    server_ = std::thread([this, desc_path] {
       while (!stop_.load()) {
         pollfd pf{sock_, POLLIN, 0};
         if (::poll(&pf, 1, 100) <= 0) continue;
         int c = accept4(sock_, nullptr, nullptr, SOCK_CLOEXEC);
         if (c < 0) continue;
-        send_fds(c);
+        if (peer_allowed(c, desc_path)) send_fds(c);
         close(c);
       }
     });
@@ -205,6 +209,17 @@ class VmmArena {
 
  private:
   static constexpr size_t kBatch = 64;
+
+  static bool peer_allowed(int c, const std::string& desc_path) {
+    ucred cr{};
+    socklen_t cl = sizeof cr;
+    if (getsockopt(c, SOL_SOCKET, SO_PEERCRED, &cr, &cl) != 0) return false;
+    if (cr.uid == 0 || cr.uid == geteuid()) return true;
+    struct stat st;
+    if (desc_path.empty() || stat(desc_path.c_str(), &st) != 0) return false;
+    if ((st.st_mode & 0006) == 0006) return true;                       // world read-write
+    return (st.st_mode & 0060) == 0060 && cr.gid == st.st_gid;          // group read-write
+  }
 
   static bool fd_by_pointer() {
     if (const char* e = getenv("SPLINTER_VMM_FD_BY_PTR")) return atoi(e) != 0;

@@ -82,7 +82,7 @@ int   spl_madvise(spl_store *s, uint32_t id, void *addr, size_t len, int advice,
 int   spl_client_set_tandem(spl_store *s, const char *base, const void **vals, const size_t *lens, uint8_t orders);
 void  spl_client_unset_tandem(spl_store *s, const char *base, uint8_t orders);
 
-/* HBM stores (libsplinter_hip.so): the CLI `search` scoring on the device.  Scores every candidate
+/* HBM stores and node stores of HBM shards (libsplinter_hip.so): the CLI `search` scoring on the device.  Scores every candidate
  * slot (bloom `mask`, or every key with a value) against `query` [768] fp32, filters with min_sim /
  * max_dist (> 0 = on), ranks by similarity desc then distance asc, and fills up to `cap` hits.
  * Returns the number of candidates (may exceed cap); emb == 0: a candidate without a vector. */
@@ -95,6 +95,20 @@ typedef struct spl_search_hit {
 } spl_search_hit;
 long  spl_hbm_search(spl_store *s, const float *query, uint64_t mask, float min_sim, float max_dist, long cap,
                      spl_search_hit *out);
+
+/* Node stores ("node:NAME", node_store.hpp): one store over a node's per-GPU arenas, key-sharded
+ * by ((fnv1a(key) >> 40) & 0xFFFFFF) % nshards.  splinter_create("node:NAME", slots, max_val)
+ * creates every shard from one process (SPLINTER_NODE_SHARDS, SPLINTER_NODE_BACKEND=hbm|shm);
+ * or each rank creates its shard store (spl_node_shard_name) and joins it, and any process then
+ * opens "node:NAME".  backend: 0 host shm shards, 1 HBM shards; stride 128 or 3200. */
+int   spl_node_join(const char *name, int shard, int nshards, unsigned backend, size_t slots_per_shard,
+                    size_t max_val, unsigned stride);
+int   spl_node_leave(const char *name, int shard);
+int   spl_node_shard_name(const char *name, int shard, unsigned backend, char *out, size_t cap);
+int   spl_node_nshards(spl_store *s);           /* -1 if s is not a node store */
+spl_store *spl_node_shard(spl_store *s, int i);
+int   spl_node_shard_of(const char *key, int nshards);
+int   spl_hbm_device_count(void);               /* libsplinter_hip.so */
 
 /* bulk helpers (host backends): key -> slot index, -1 if absent */
 long  spl_find_slot(spl_store *s, const char *key);

@@ -20,6 +20,8 @@ enum CreateFlags : unsigned {
   kCreatePersistent = 1u << 1,  // regular file instead of POSIX shm
   kCreateNoEmbeddings = 1u << 2,
 };
+// HBM factory flags: device ordinal + 1 in bits 16..23 (0 = the caller's current device)
+constexpr unsigned kCreateDeviceShift = 16;
 
 class StoreBase {
  public:

@@ -73,6 +73,11 @@ def _lib():
         L.nomic_gemm_ln.argtypes = [c_int, P, c_long, P, c_long, c_long, c_int, c_int, P, c_long, P, c_long, P, P,
                                     c_int, P, c_int, c_float, P, P, P, P, P, P]
         L.nomic_gemm_ln.restype = c_int
+        L.nomic_gemm_res_ln.argtypes = [P, c_long, P, c_long, c_long, c_int, c_int, P, c_long, P, P, c_float, P,
+                                        c_long, P]
+        L.nomic_gemm_res_ln.restype = c_int
+        L.nomic_gemm_res_ln_set_variant.argtypes = [c_int]
+        L.nomic_gemm_res_ln_set_variant.restype = c_int
         L.nomic_row_stats.argtypes = [P, c_int, c_long, c_float, P, P]
         L.nomic_row_stats.restype = c_int
         L.nomic_gemm_set_variant.argtypes = [c_int]
@@ -381,20 +386,52 @@ class NomicEncoder:
                                   ptr(ln[0]) if ln else None, ptr(ln[1]) if ln else None, ptr(part), _stream()),
              f"gemm_ln({mode})")
 
-    # The two residual projections (o-proj, down: N = 768) are plain C += A B^T GEMMs; hipBLASLt's
-    # beta = 1 epilogue in place beats the fused MFMA kernel on them (down 123.5 vs 175.5 us,
-    # o-proj 49.1 vs 54.4 at 32768 tokens: profiles/r2_residual_gemm_ab.jsonl), so they go to the
-    # library (NOMIC_RESIDUAL_BLAS=0: the MFMA kernel with the fused residual epilogue).  Every
-    # projection with a fused epilogue (RoPE, SwiGLU) stays on the hand-written kernels.
-    residual_blas = os.environ.get("NOMIC_RESIDUAL_BLAS", "1") != "0"
-    # measured slower on MI355X (profiles/r2_encoder_ln_fold.md): opt in with NOMIC_LN_FOLD=1
-    ln_fold = os.environ.get("NOMIC_LN_FOLD", "0") != "0"
+    # Schedules of the post-LN layers (K15 / K16-down), all on hand-written kernels:
+    #   "fused"  (default) residual GEMM + residual add + LayerNorm in one row-complete kernel
+    #            (csrc/hip/gemm_rln.hip): x = LN(a W^T + x) in place, no separate LN pass;
+    #   "split"  the residual GEMM (EPI_RESIDUAL) then the LayerNorm kernel (round-1 schedule);
+    #   "folded" every post-LN folded into the neighbouring GEMMs (measured slower,
+    #            profiles/r2_encoder_ln_fold.md).
+    # NOMIC_SCHEDULE overrides; NOMIC_LN_FOLD=1 is the old spelling of "folded".
+    schedule = os.environ.get("NOMIC_SCHEDULE", "folded" if os.environ.get("NOMIC_LN_FOLD", "0") != "0" else "fused")
 
     def hidden(self, b: Batch) -> torch.Tensor:
         """Final-layer hidden states [T, 768] (bf16) for a packed batch."""
-        if self.ln_fold:
+        if self.schedule == "folded":
             return self._hidden_folded(b)
-        return self._hidden_unfused(b)
+        if self.schedule == "split":
+            return self._hidden_unfused(b)
+        if self.schedule != "fused":
+            raise ValueError(f"unknown encoder schedule {self.schedule!r}")
+        return self._hidden_fused(b)
+
+    def _res_ln(self, A, W, M, x, g, beta):
+        """x[:M] = LN(A W^T + x) * g + beta in place (row-complete MFMA kernel, gemm_rln.hip)."""
+        N_, K = W.shape
+        _chk(self.L.nomic_gemm_res_ln(A.data_ptr(), A.stride(0), W.data_ptr(), W.stride(0), M, N_, K, x.data_ptr(),
+                                      x.stride(0), g.data_ptr(), beta.data_ptr(), self.cfg.eps, x.data_ptr(),
+                                      x.stride(0), _stream()), "gemm_res_ln")
+
+    def _hidden_fused(self, b: Batch) -> torch.Tensor:
+        """The shipped schedule: 5 kernels per layer, every one hand-written for gfx950 --
+        QKV+RoPE GEMM, varlen attention, o-proj+residual+LN, up|gate+SwiGLU GEMM, down+residual+LN."""
+        cfg, L, w = self.cfg, self.L, self.w
+        assert b.max_len <= self.rope.shape[0]
+        self._ensure(b.T_pad)
+        s = _stream()
+        T = b.T
+        x, attn, qkv, ffn = self.x, self.attn, self.qkv, self.ffn
+        _chk(L.nomic_embed_ln(b.ids.data_ptr(), T, w.tok.data_ptr(), w.type_row.data_ptr(), w.emb_g.data_ptr(),
+                              w.emb_b.data_ptr(), cfg.eps, x.data_ptr(), s), "embed_ln")
+        scale = 1.0 / math.sqrt(cfg.head_dim)
+        for lw in w.layers:
+            self._gemm(EPI_ROPE, x, lw["wqkv"], T, qkv, pos=b.pos)
+            _chk(L.nomic_attention(qkv.data_ptr(), attn.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb,
+                                   cfg.heads, scale, s), "attention")
+            self._res_ln(attn, lw["wo"], T, x, lw["ln1_g"], lw["ln1_b"])
+            self._gemm(EPI_SWIGLU, x, lw["wupgate"], T, ffn)
+            self._res_ln(ffn, lw["wdown"], T, x, lw["ln2_g"], lw["ln2_b"])
+        return x[:T]
 
     def _hidden_folded(self, b: Batch) -> torch.Tensor:
         """The forward with every post-LN folded into the GEMMs around it (K15): the residual GEMMs
@@ -435,7 +472,7 @@ class NomicEncoder:
         return x[:T]
 
     def _hidden_unfused(self, b: Batch) -> torch.Tensor:
-        """Reference schedule: a LayerNorm kernel after each residual GEMM (NOMIC_LN_FOLD=0)."""
+        """Split schedule: the residual GEMM, then a LayerNorm kernel (NOMIC_SCHEDULE=split)."""
         cfg, L, w = self.cfg, self.L, self.w
         assert b.max_len <= self.rope.shape[0]
         self._ensure(b.T_pad)
@@ -449,20 +486,12 @@ class NomicEncoder:
             self._gemm(EPI_ROPE, x, lw["wqkv"], T, qkv, pos=b.pos)
             _chk(L.nomic_attention(qkv.data_ptr(), attn.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb,
                                    cfg.heads, scale, s), "attention")
-            if self.residual_blas:  # x += attn Wo^T on hipBLASLt (a plain beta = 1 GEMM), LN in place
-                x[:T].addmm_(attn[:T], lw["wo"].t())
-                src = x
-            else:
-                self._gemm(EPI_RESIDUAL, attn, lw["wo"], T, h, res=x)
-                src = h
-            _chk(L.nomic_layernorm(src.data_ptr(), T, lw["ln1_g"].data_ptr(), lw["ln1_b"].data_ptr(), cfg.eps,
+            self._gemm(EPI_RESIDUAL, attn, lw["wo"], T, h, res=x)
+            _chk(L.nomic_layernorm(h.data_ptr(), T, lw["ln1_g"].data_ptr(), lw["ln1_b"].data_ptr(), cfg.eps,
                                    x.data_ptr(), s), "ln1")
             self._gemm(EPI_SWIGLU, x, lw["wupgate"], T, ffn)
-            if self.residual_blas:
-                x[:T].addmm_(ffn[:T], lw["wdown"].t())
-            else:
-                self._gemm(EPI_RESIDUAL, ffn, lw["wdown"], T, h, res=x)
-            _chk(L.nomic_layernorm(src.data_ptr(), T, lw["ln2_g"].data_ptr(), lw["ln2_b"].data_ptr(), cfg.eps,
+            self._gemm(EPI_RESIDUAL, ffn, lw["wdown"], T, h, res=x)
+            _chk(L.nomic_layernorm(h.data_ptr(), T, lw["ln2_g"].data_ptr(), lw["ln2_b"].data_ptr(), cfg.eps,
                                    x.data_ptr(), s), "ln2")
         return x[:T]
 

@@ -120,11 +120,14 @@ class _Coll:
         is a collective), so the largest segment of any rank is agreed with one small all-reduce;
         part p moves rows [p*step, (p+1)*step) of every segment."""
         w = dist.get_world_size(self.group)
-        row = inp[0].numel() * inp.element_size() if inp.shape[0] else out[0].numel() * out.element_size() \
-            if out.shape[0] else 1
-        m = torch.tensor([max(in_splits + [0]), max(out_splits + [0])], dtype=torch.int64, device=out.device)
+        # row bytes from the shape (identical on every rank, also on one that sends and receives no
+        # rows), and agreed in the same all-reduce as the segment maxima: every rank then computes the
+        # same part count, so the collective sequences match
+        row = int(np.prod(inp.shape[1:])) * inp.element_size()
+        m = torch.tensor([max(in_splits + [0]), max(out_splits + [0]), row], dtype=torch.int64, device=out.device)
         dist.all_reduce(m, op=dist.ReduceOp.MAX, group=self.group)
-        mx = int(m.max().item())
+        mx = int(m[:2].max().item())
+        row = max(int(m[2].item()), 1)
         if mx * row * w <= A2A_CHUNK_BYTES:
             dist.all_to_all_single(out, inp, out_splits, in_splits, group=self.group)
             return

@@ -63,6 +63,45 @@ def unlink(name: str) -> int:
     return N.core_lib().spl_unlink(name.encode())
 
 
+def _load_hip_if_present(required: bool = True) -> None:
+    """HBM (and node-of-HBM) stores need libsplinter_hip.so loaded after torch (_native.hip_lib)."""
+    try:
+        N.hip_lib()
+    except (ImportError, N.NativeMissing):
+        if required:
+            raise
+
+
+# ------------------------------------------------------------- node stores --
+NODE_SHM, NODE_HBM = 0, 1
+
+
+def node_shard_name(node: str, shard: int, backend: int) -> str:
+    """Store name (with its backend prefix) of shard `shard` of node store `node`."""
+    buf = ctypes.create_string_buffer(256)
+    if N.core_lib().spl_node_shard_name(node.encode(), shard, backend, buf, 256) < 0:
+        raise ValueError(node)
+    return buf.value.decode()
+
+
+def node_shard_of(key, nshards: int) -> int:
+    """Owning shard of `key` in an n-way node store (== parallel/sharded.py shard_of)."""
+    return N.core_lib().spl_node_shard_of(_k(key), nshards)
+
+
+def node_join(node: str, shard: int, nshards: int, backend: int, slots_per_shard: int, max_val: int,
+              embeddings: bool) -> None:
+    """Register this rank's shard store (created first, as node_shard_name(...)) with node `node`;
+    once every shard has joined, any process can open "node:<node>"."""
+    stride = 3200 if embeddings else 128
+    if N.core_lib().spl_node_join(node.encode(), shard, nshards, backend, slots_per_shard, max_val, stride) != 0:
+        _raise(f"node_join {node}")
+
+
+def node_leave(node: str, shard: int) -> None:
+    N.core_lib().spl_node_leave(node.encode(), shard)
+
+
 class Store:
     """One open store.  Use :meth:`create`, :meth:`open` or :meth:`open_or_create`."""
 
@@ -78,8 +117,8 @@ class Store:
     @classmethod
     def create(cls, name: str, slots: int = 1024, max_val: int = 4096, embeddings: Optional[bool] = None,
                persistent: bool = False) -> "Store":
-        if name.startswith("hbm:"):
-            N.hip_lib()
+        if name.startswith("hbm:") or (name.startswith("node:") and os.environ.get("SPLINTER_NODE_BACKEND") != "shm"):
+            _load_hip_if_present()
         flags = 0
         if embeddings is True:
             flags |= CREATE_EMBEDDINGS
@@ -95,8 +134,8 @@ class Store:
 
     @classmethod
     def open(cls, name: str) -> "Store":
-        if name.startswith("hbm:"):
-            N.hip_lib()
+        if name.startswith("hbm:") or name.startswith("node:"):
+            _load_hip_if_present(required=name.startswith("hbm:"))
         err = ctypes.c_int(0)
         h = N.core_lib().spl_store_open(name.encode(), ctypes.byref(err))
         if not h:
@@ -131,6 +170,12 @@ class Store:
     @property
     def handle(self) -> int:
         return self._h
+
+    @property
+    def nshards(self) -> int:
+        """Shards of a node store (1 for any other store)."""
+        n = self._L.spl_node_nshards(self._h)
+        return n if n > 0 else 1
 
     @property
     def backend(self) -> str:

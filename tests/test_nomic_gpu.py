@@ -263,17 +263,54 @@ def test_layernorm_and_embed(L0):
     assert _rel(out.float(), ref) < 5e-3
 
 
-@pytest.mark.parametrize("ln_fold,residual_blas", [(True, False), (False, False), (False, True)],
-                         ids=["ln_folded", "ln_kernels_mfma_residual", "ln_kernels_blas_residual"])
-def test_encoder_matches_fp32_reference(ln_fold, residual_blas):
+@pytest.mark.parametrize("M,K", [(128, 768), (300, 768), (1, 3072), (257, 3072), (32768, 768), (4100, 3072)])
+def test_gemm_residual_layernorm_row_complete(L0, M, K):
+    """nomic_gemm_res_ln (gemm_rln.hip): x = LN(A W^T + x) * g + b in place, against fp32, with a
+    row tail (M % 128 != 0), a single row, the shipped 32768-row o-proj shape and the down shape;
+    rows past M untouched; asymmetric operands and non-trivial gamma/beta."""
+    import torch
+    from libsplinter_amd.models.nomic import _chk, _stream
+    torch.manual_seed(M + K)
+    N = 768
+    Mp = (M + 127) // 128 * 128 + 128
+    A = (torch.rand(Mp, K, device="cuda") * 2 - 1).bfloat16()
+    W = ((torch.rand(N, K, device="cuda") * 2 - 1) * (1.0 / math.sqrt(K))).bfloat16()
+    X = (torch.randn(Mp, N, device="cuda") + torch.linspace(-2, 2, N, device="cuda")).bfloat16()
+    g = (1 + 0.3 * torch.randn(N, device="cuda")).bfloat16()
+    b = (0.1 * torch.randn(N, device="cuda")).bfloat16()
+    ref = torch.nn.functional.layer_norm(A[:M].float() @ W.float().T + X[:M].float(), (N,), g.float(), b.float(),
+                                         1e-12)
+    tail = X[M:].clone()
+    _chk(L0.nomic_gemm_res_ln(A.data_ptr(), K, W.data_ptr(), K, M, N, K, X.data_ptr(), N, g.data_ptr(),
+                              b.data_ptr(), 1e-12, X.data_ptr(), N, _stream()), "gemm_res_ln")
+    torch.cuda.synchronize()
+    assert _rel(X[:M].float(), ref) < 6e-3
+    assert (X[:M].float() - ref).abs().max().item() < 0.08
+    assert torch.equal(X[M:], tail), "rows past M must not be written"
+    # out-of-place with a separate residual gives the same bits
+    X2 = torch.empty_like(X)
+    R = (torch.randn(Mp, N, device="cuda")).bfloat16()
+    ref2 = torch.nn.functional.layer_norm(A[:M].float() @ W.float().T + R[:M].float(), (N,), g.float(), b.float(),
+                                          1e-12)
+    _chk(L0.nomic_gemm_res_ln(A.data_ptr(), K, W.data_ptr(), K, M, N, K, R.data_ptr(), N, g.data_ptr(),
+                              b.data_ptr(), 1e-12, X2.data_ptr(), N, _stream()), "gemm_res_ln")
+    assert _rel(X2[:M].float(), ref2) < 6e-3
+    # shapes the kernel does not take are refused, not launched
+    assert L0.nomic_gemm_res_ln(A.data_ptr(), K, W.data_ptr(), K, M, 512, K, X.data_ptr(), N, g.data_ptr(),
+                                b.data_ptr(), 1e-12, X.data_ptr(), N, _stream()) != 0
+    assert L0.nomic_gemm_res_ln(A.data_ptr(), K, W.data_ptr(), K, M, N, 48, X.data_ptr(), N, g.data_ptr(),
+                                b.data_ptr(), 1e-12, X.data_ptr(), N, _stream()) != 0
+
+
+@pytest.mark.parametrize("schedule", ["fused", "split", "folded"])
+def test_encoder_matches_fp32_reference(schedule):
     import torch
     from libsplinter_amd.models.nomic import (Batch, NomicConfig, NomicEncoder, NomicReference, NomicWeights,
                                               random_weights)
     cfg = NomicConfig(layers=3)
     w = random_weights(cfg, seed=5)
     enc = NomicEncoder(NomicWeights.from_numpy(cfg, w), max_tokens=4096)
-    enc.ln_fold = ln_fold
-    enc.residual_blas = residual_blas
+    enc.schedule = schedule
     rng = np.random.default_rng(0)
     seqs = [rng.integers(0, cfg.vocab, size=n).tolist() for n in (5, 40, 129, 300)]
     b = Batch(seqs)
@@ -384,9 +421,12 @@ def test_device_dequant_matches_host_reference_all_types():
     assert L.nomic_dequant(12, bad.data_ptr(), 32, out.data_ptr(), _stream()) != 0
 
 
-def test_full_encoder_shipped_shape_matches_fp32():
+@pytest.mark.parametrize("schedule", ["fused", "split"])
+def test_full_encoder_shipped_shape_matches_fp32(schedule):
     """The shipped shape: all 12 layers, 64 documents x 512 tokens (the bench batch), bf16 gfx950
-    kernels vs an fp32 torch forward of the same random-init nomic-bert weights."""
+    kernels vs an fp32 torch forward of the same random-init nomic-bert weights; "fused" is the
+    shipped schedule (the row-complete residual+LN kernel), "split" the residual-epilogue GEMM +
+    LayerNorm kernel pair."""
     import torch
     from libsplinter_amd.models.nomic import (Batch, NomicConfig, NomicEncoder, NomicReference, NomicWeights,
                                               random_weights)
@@ -394,6 +434,7 @@ def test_full_encoder_shipped_shape_matches_fp32():
     w = random_weights(cfg, seed=11)
     b_docs, seq = 64, 512
     enc = NomicEncoder(NomicWeights.from_numpy(cfg, w), max_tokens=b_docs * seq)
+    enc.schedule = schedule
     rng = np.random.default_rng(1)
     seqs = [rng.integers(1000, cfg.vocab, size=seq).tolist() for _ in range(b_docs)]
     b = Batch(seqs)

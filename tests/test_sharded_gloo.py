@@ -282,6 +282,17 @@ def _a2a_worker(rank, world, port, q):
         out = torch.full((sum(recv), 40), 7, dtype=torch.uint8)
         c._all_to_all_uneven(out, inp, recv, send)
         assert torch.equal(out, ref), "chunked uneven all-to-all differs"
+        # an idle rank (rank 0 sends and receives no rows) must still take part in every part: the
+        # part count is agreed from the shape, not from rows this rank happens to hold
+        allsend = [[0 if (r == 0 or d == 0) else ((r + d) % 3) * 4 + 1 for d in range(world)] for r in range(world)]
+        send = allsend[rank]
+        recv = [allsend[r][rank] for r in range(world)]
+        inp = torch.from_numpy(rng.integers(0, 256, size=(sum(send), 40), dtype=np.uint8))
+        ref = torch.empty((sum(recv), 40), dtype=torch.uint8)
+        dist.all_to_all_single(ref, inp, recv, send)
+        out = torch.full((sum(recv), 40), 7, dtype=torch.uint8)
+        c._all_to_all_uneven(out, inp, recv, send)
+        assert torch.equal(out, ref), "chunked uneven all-to-all with an idle rank differs"
         q.put((rank, "ok"))
     except Exception:
         import traceback

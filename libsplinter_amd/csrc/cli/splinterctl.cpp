@@ -1032,12 +1032,15 @@ int cmd_search(int argc, char** argv) {
   regex_t re;
   bool filt = rx && regcomp(&re, rx, REG_EXTENDED | REG_NOSUB) == 0;
   std::vector<Hit> hits;
-  // HBM store: score every candidate on the device (spl_hbm_search, libsplinter_hip.so K7 pass)
-  // instead of one slot snapshot per candidate -- same candidates, filters and ranking
+  // HBM store (or a node store of HBM shards: every GPU scores its shard, best hits merged): score
+  // every candidate on the device (spl_hbm_search, libsplinter_hip.so K7 pass) instead of one slot
+  // snapshot per candidate -- same candidates, filters and ranking.  A node of host shards makes
+  // spl_hbm_search fail and takes the host path below.
   using HbmSearch = long (*)(spl_store*, const float*, uint64_t, float, float, long, spl_search_hit*);
   spl_store* cur = spl_store_current();
   HbmSearch gpu = nullptr;
-  if (have_q && cur && !strcmp(spl_store_backend(cur), "hbm")) gpu = (HbmSearch)dlsym(RTLD_DEFAULT, "spl_hbm_search");
+  if (have_q && cur && (!strcmp(spl_store_backend(cur), "hbm") || !strcmp(spl_store_backend(cur), "node")))
+    gpu = (HbmSearch)dlsym(RTLD_DEFAULT, "spl_hbm_search");
   bool done = false;
   if (gpu) {
     const long cap = (limit > 0 && !filt) ? limit + 1 : (long)h.slots;  // +1: our own scratch key

@@ -68,6 +68,8 @@ template <int PIPE> struct Pipe;
 template <> struct Pipe<1> { static constexpr int NW = 2, NA = 4; };
 template <> struct Pipe<2> { static constexpr int NW = 3, NA = 2; };
 template <> struct Pipe<3> { static constexpr int NW = 2, NA = 2; };
+//   PIPE 4: NW 2, NA 6 (144 KB): A five stages ahead
+template <> struct Pipe<4> { static constexpr int NW = 2, NA = 6; };
 template <int PIPE>
 constexpr int lds_bytes() {
   return Pipe<PIPE>::NW * kWBytes + Pipe<PIPE>::NA * kABytes > kEpiLds
@@ -89,7 +91,9 @@ __device__ __forceinline__ void raw_barrier() {
 
 __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {  // wave-uniform: a scalar branch to an immediate count
+    case 12: asm volatile("s_waitcnt vmcnt(12)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
+    case 2: asm volatile("s_waitcnt vmcnt(2)" ::: "memory"); break;
     case 1: asm volatile("s_waitcnt vmcnt(1)" ::: "memory"); break;
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
@@ -98,8 +102,20 @@ __device__ __forceinline__ void wait_vm(int n) {
 // physical 16-B chunk of logical chunk c in 64-B row r
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 3); }
 
-template <int PIPE, int EPI>
-__global__ __launch_bounds__(kThreads, 1) void k_gemm_rln(const uint16_t* __restrict__ A, long lda,
+// WM: waves along M.  2: 8 waves (2 x 4), 64 rows x 192 columns each (192 accumulators, two
+// waves per SIMD).  1: 4 waves (1 x 4), 128 rows x 192 columns each (384 accumulators in the
+// AGPR half of a 512-register wave, one wave per SIMD, 8 A fragments per stage: a third less
+// LDS read traffic per MFMA and half the waves at each barrier).
+// ILV > 0: the loads an iteration issues are spread over its MFMA groups (ILV LDS-DMA
+// instructions ahead of each group of 8 MFMAs, in issue order) instead of all issued after the
+// barrier, where they held both waves of a SIMD off the matrix core for the ~100-cycle issue cost
+// of each DMA instruction.  ILV 0: all after the barrier.
+// EPI 0: residual added in the epilogue (8-B loads); 1: LDS-staged epilogue; 2: the residual is
+// the first K step -- one MFMA per tile against an identity operand (acc = I . R, exact: 1.0 x a
+// bf16 value) with R fragments loaded in the prologue beside the first stages, so the epilogue
+// reads nothing.  PF: W fragment pairs read PF pairs ahead of their MFMAs.
+template <int PIPE, int EPI, int WM, int ILV = 0, int PF = 1>
+__global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ W, long ldw, int K, long M,
                                                           const uint16_t* res, long ldr,
                                                           const uint16_t* __restrict__ gamma,
@@ -108,101 +124,154 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_rln(const uint16_t* __rest
   constexpr int NW = Pipe<PIPE>::NW, NA = Pipe<PIPE>::NA;
   constexpr int LW = NW - 1, LA = NA - 1;              // stages of lead
   constexpr int kABase = NW * kWBytes;                 // LDS: [W ring | A ring]
+  constexpr int kWaves = 4 * WM, kNThreads = 64 * kWaves;
+  constexpr int RW = kBM / WM, MT = RW / 16;           // rows and m-tiles per wave
+  constexpr int GA = 8 / kWaves, GW = 48 / kWaves;     // LDS-DMA wave-instructions per wave per stage
+  static_assert(EPI == 0 || WM == 2, "the LDS-staged epilogue splits the tile by wave rows");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wn = wave & 3;
+  const int wr = WM == 2 ? wave >> 2 : 0, wn = wave & 3;
   // W is read by every block and A rows by one block only: no reuse for an XCD remap to exploit
   const long m0 = (long)blockIdx.x * kBM;
 
   // ---- per-lane LDS-DMA sources: a wave-instruction covers 16 rows x 64 B, lane -> (row, chunk)
   const int drow = lane >> 2, dpc = lane & 3;
-  uint32_t offA;
-  {
-    const int r = wave * 16 + drow;                      // one A wave-instruction per wave
-    const long gr = (m0 + r < M) ? m0 + r : M - 1;       // tail rows re-read row M-1, never stored
-    offA = (uint32_t)(gr * lda + swz(r, dpc) * 8);
-  }
-  uint32_t offW[kGldsW];
+  uint32_t offA[GA];
 #pragma unroll
-  for (int i = 0; i < kGldsW; ++i) {
-    const int r = (wave + 8 * i) * 16 + drow;
+  for (int i = 0; i < GA; ++i) {
+    const int r = (wave + kWaves * i) * 16 + drow;
+    const long gr = (m0 + r < M) ? m0 + r : M - 1;       // tail rows re-read row M-1, never stored
+    offA[i] = (uint32_t)(gr * lda + swz(r, dpc) * 8);
+  }
+  uint32_t offW[GW];
+#pragma unroll
+  for (int i = 0; i < GW; ++i) {
+    const int r = (wave + kWaves * i) * 16 + drow;
     offW[i] = (uint32_t)(r * ldw + swz(r, dpc) * 8);
   }
   const int nk = K / kBK;
-  int wslot = 0, aslot = 0;  // ring slots the next W / A stage goes to
-  auto issue_w = [&](int t) {
-    if (t < 0 || t >= nk) return;
-    char* dst = smem + wslot * kWBytes;
-    wslot = wslot + 1 == NW ? 0 : wslot + 1;
+  // ring slot of stage t: t % NW (W), t % NA (A) -- stages enter each ring in order
+  auto glds_w = [&](int t, int i) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)(W + (long)t * kBK + offW[i]),
+                                     (lds_void*)(smem + (t % NW) * kWBytes + (wave + kWaves * i) * 1024), 16, 0, 0);
+  };
+  auto glds_a = [&](int t, int i) {
+    __builtin_amdgcn_global_load_lds((gbl_void*)(A + (long)t * kBK + offA[i]),
+                                     (lds_void*)(smem + kABase + (t % NA) * kABytes + (wave + kWaves * i) * 1024), 16,
+                                     0, 0);
+  };
+  // op u (0 .. GW+GA-1) of the loads iteration s issues: stage W(s + LW) and A(s + LA), the one
+  // with the shorter lead first (younger() counts on that order)
+  constexpr int kOps = GW + GA;
+  auto issue_op = [&](int s, int u) {
+    const int tw = s + LW, ta = s + LA;
+    if (LW <= LA) {
+      if (u < GW) { if (tw >= 0 && tw < nk) glds_w(tw, u); }
+      else if (ta >= 0 && ta < nk) glds_a(ta, u - GW);
+    } else {
+      if (u < GA) { if (ta >= 0 && ta < nk) glds_a(ta, u); }
+      else if (tw >= 0 && tw < nk) glds_w(tw, u - GA);
+    }
+  };
+  auto issue = [&](int s) {
 #pragma unroll
-    for (int i = 0; i < kGldsW; ++i)
-      __builtin_amdgcn_global_load_lds((gbl_void*)(W + (long)t * kBK + offW[i]),
-                                       (lds_void*)(dst + (wave + 8 * i) * 1024), 16, 0, 0);
-  };
-  auto issue_a = [&](int t) {
-    if (t < 0 || t >= nk) return;
-    char* dst = smem + kABase + aslot * kABytes;
-    aslot = aslot + 1 == NA ? 0 : aslot + 1;
-    __builtin_amdgcn_global_load_lds((gbl_void*)(A + (long)t * kBK + offA), (lds_void*)(dst + wave * 1024), 16, 0, 0);
-  };
-  auto issue = [&](int s) {  // the stages iteration s issues, shorter lead first
-    if (LW <= LA) { issue_w(s + LW); issue_a(s + LA); }
-    else { issue_a(s + LA); issue_w(s + LW); }
+    for (int u = 0; u < kOps; ++u) issue_op(s, u);
   };
   // ops issued after the later of W(t) / A(t): they may stay in flight at the top of iteration t
   auto younger = [&](int t) -> int {
-    if (LW < LA) return t + LA - 1 < nk ? 1 : 0;            // A(t + LA - 1), issued after W(t)
-    if (LW > LA) return t + LW - 1 < nk ? kGldsW : 0;       // W(t + LW - 1), issued after A(t)
+    if (LW < LA) return t + LA - 1 < nk ? GA : 0;           // A(t + LA - 1), issued after W(t)
+    if (LW > LA) return t + LW - 1 < nk ? GW : 0;           // W(t + LW - 1), issued after A(t)
     return 0;
   };
 
   // fragment read: row = base16 + (lane & 15), logical chunk lane >> 4
   const int fl = (lane & 15) * kRowBytes + (swz(lane & 15, lane >> 4) << 4);
-  const int aoff = kABase + (wr * 64) * kRowBytes + fl;
+  const int aoff = kABase + (wr * RW) * kRowBytes + fl;
   const int woff = (wn * kWN) * kRowBytes + fl;
 
-  f32x4 acc[4][kNT];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < kNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
+  f32x4 acc[MT][kNT];
   constexpr int L = LW > LA ? LW : LA;
-  for (int s = -L; s < 0; ++s) issue(s);
-  int wread = 0, aread = 0;
+  if constexpr (EPI == 2) {
+    // residual fragments (B operand of a 16x16x32 MFMA: lane l holds k = 8 (l >> 4) .. +7 of column
+    // l & 15): lanes 0-31 load res[m][n0 + 8 (l >> 4) .. +8] (16 B), lanes 32-63 (k 16-31) zero;
+    // identity A operand: row n = l & 15 has its 1 at k = n
+    bf16x8 rf[MT][kNT];
+    const int rl = lane & 15;
+#pragma unroll
+    for (int i = 0; i < MT; ++i) {
+      const long m = m0 + wr * RW + i * 16 + rl;
+      const uint16_t* rp = res + (m < M ? m : M - 1) * ldr + wn * kWN + 8 * ((lane >> 4) & 1);
+#pragma unroll
+      for (int j = 0; j < kNT; ++j) {
+        if (lane < 32) rf[i][j] = *(const bf16x8*)(rp + j * 16);
+        else rf[i][j] = bf16x8{};
+      }
+    }
+    for (int s = -L; s < 0; ++s) issue(s);
+    bf16x8 eye = bf16x8{};
+    if (lane < 32 && (rl >> 3) == (lane >> 4)) eye[rl & 7] = (__bf16)1.0f;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < kNT; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(eye, rf[i][j], f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+  } else {
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int j = 0; j < kNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int s = -L; s < 0; ++s) issue(s);
+  }
   for (int t = 0; t < nk; ++t) {
     wait_vm(younger(t));
     raw_barrier();  // stage t visible to every wave; every wave is done with stage t-1's slots
-    issue(t);
-    const char* bw = smem + wread * kWBytes;
-    const char* ba = smem + aread * kABytes;
-    wread = wread + 1 == NW ? 0 : wread + 1;
-    aread = aread + 1 == NA ? 0 : aread + 1;
+    if (ILV == 0) issue(t);
+    const char* bw = smem + (t % NW) * kWBytes;
+    const char* ba = smem + (t % NA) * kABytes;
     // A fragments for the whole stage, W fragments two n-tiles at a time with the next pair's reads
     // issued ahead of the current pair's MFMAs (sched_barrier pins the pairs: hoisting all 12 W
     // reads would need 48 more registers than the 256 two waves per SIMD allow)
-    bf16x8 af[4], w0, w1, x0, x1;
+    bf16x8 af[MT], w0, w1, x0, x1, y0, y1;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) af[i] = *(const bf16x8*)(ba + aoff + i * 16 * kRowBytes);
+    for (int i = 0; i < MT; ++i) af[i] = *(const bf16x8*)(ba + aoff + i * 16 * kRowBytes);
     w0 = *(const bf16x8*)(bw + woff);
     w1 = *(const bf16x8*)(bw + woff + 16 * kRowBytes);
+    if (PF == 2) {
+      x0 = *(const bf16x8*)(bw + woff + 2 * 16 * kRowBytes);
+      x1 = *(const bf16x8*)(bw + woff + 3 * 16 * kRowBytes);
+    }
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int jp = 0; jp < kNT / 2; ++jp) {
-      if (jp + 1 < kNT / 2) {
-        x0 = *(const bf16x8*)(bw + woff + (2 * jp + 2) * 16 * kRowBytes);
-        x1 = *(const bf16x8*)(bw + woff + (2 * jp + 3) * 16 * kRowBytes);
+      if (ILV > 0) {
+#pragma unroll
+        for (int u = jp * ILV; u < (jp + 1) * ILV; ++u)
+          if (u < kOps) issue_op(t, u);
+      }
+      if (jp + PF < kNT / 2) {
+        bf16x8& d0 = PF == 2 ? y0 : x0;
+        bf16x8& d1 = PF == 2 ? y1 : x1;
+        d0 = *(const bf16x8*)(bw + woff + (2 * (jp + PF)) * 16 * kRowBytes);
+        d1 = *(const bf16x8*)(bw + woff + (2 * (jp + PF) + 1) * 16 * kRowBytes);
       }
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < MT; ++i) {
         acc[i][2 * jp] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w0, af[i], acc[i][2 * jp], 0, 0, 0);
         acc[i][2 * jp + 1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w1, af[i], acc[i][2 * jp + 1], 0, 0, 0);
       }
       __builtin_amdgcn_sched_barrier(0);
       w0 = x0;
       w1 = x1;
+      if (PF == 2) {
+        x0 = y0;
+        x1 = y1;
+      }
     }
     __builtin_amdgcn_s_setprio(0);
+    if (ILV > 0) {
+#pragma unroll
+      for (int u = (kNT / 2) * ILV; u < kOps; ++u) issue_op(t, u);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   raw_barrier();  // every wave is done with the rings: the LDS is the epilogue's
@@ -210,66 +279,69 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_rln(const uint16_t* __rest
   // ---- epilogue -------------------------------------------------------------------------
   // lane: rows m_i = m0 + wr*64 + i*16 + (lane & 15); columns n_j = wn*192 + j*16 + (lane>>4)*4 + 0..3
   const int rl = lane & 15, cq = (lane >> 4) * 4;
-  if constexpr (EPI == 0) {
-    // direct: residual loads and 8-B stores from registers
+  if constexpr (EPI != 1) {
+    // direct: residual loads (EPI 0; EPI 2 has it in the accumulators) and 8-B stores from registers
     float* red = (float*)smem;  // [4 column waves][128 rows]
-    const long mb = m0 + wr * 64 + rl;  // row of m-tile i: mb + 16 i
-    float s[4] = {0.f, 0.f, 0.f, 0.f};
+    const long mb = m0 + wr * RW + rl;  // row of m-tile i: mb + 16 i
+    float s[MT] = {};
 #pragma unroll
     for (int j = 0; j < kNT; ++j) {
       const int n = wn * kWN + j * 16 + cq;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const long m = mb + 16 * i < M ? mb + 16 * i : M - 1;
-        const uint2 rr = *(const uint2*)(res + m * ldr + n);
-        acc[i][j][0] += bf2f(rr.x & 0xffff);
-        acc[i][j][1] += bf2f(rr.x >> 16);
-        acc[i][j][2] += bf2f(rr.y & 0xffff);
-        acc[i][j][3] += bf2f(rr.y >> 16);
+      for (int i = 0; i < MT; ++i) {
+        if constexpr (EPI == 0) {
+          const long m = mb + 16 * i < M ? mb + 16 * i : M - 1;
+          const uint2 rr = *(const uint2*)(res + m * ldr + n);
+          acc[i][j][0] += bf2f(rr.x & 0xffff);
+          acc[i][j][1] += bf2f(rr.x >> 16);
+          acc[i][j][2] += bf2f(rr.y & 0xffff);
+          acc[i][j][3] += bf2f(rr.y >> 16);
+        }
+        (void)n;
         s[i] += (acc[i][j][0] + acc[i][j][1]) + (acc[i][j][2] + acc[i][j][3]);
       }
     }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MT; ++i) {
       s[i] += __shfl_xor(s[i], 16);
       s[i] += __shfl_xor(s[i], 32);
     }
     if (lane < 16) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[wn * kBM + wr * 64 + i * 16 + rl] = s[i];
+      for (int i = 0; i < MT; ++i) red[wn * kBM + wr * RW + i * 16 + rl] = s[i];
     }
     __syncthreads();
-    float mean[4];
+    float mean[MT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wr * 64 + i * 16 + rl;
+    for (int i = 0; i < MT; ++i) {
+      const int r = wr * RW + i * 16 + rl;
       mean[i] = (red[r] + red[kBM + r] + red[2 * kBM + r] + red[3 * kBM + r]) * (1.f / kN);
       s[i] = 0.f;
     }
 #pragma unroll
     for (int j = 0; j < kNT; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MT; ++i)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const float d = acc[i][j][e] - mean[i];
           s[i] += d * d;
         }
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MT; ++i) {
       s[i] += __shfl_xor(s[i], 16);
       s[i] += __shfl_xor(s[i], 32);
     }
     __syncthreads();  // every wave has read the row sums
     if (lane < 16) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) red[wn * kBM + wr * 64 + i * 16 + rl] = s[i];
+      for (int i = 0; i < MT; ++i) red[wn * kBM + wr * RW + i * 16 + rl] = s[i];
     }
     __syncthreads();
-    float rstd[4];
+    float rstd[MT];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int r = wr * 64 + i * 16 + rl;
+    for (int i = 0; i < MT; ++i) {
+      const int r = wr * RW + i * 16 + rl;
       const float var = (red[r] + red[kBM + r] + red[2 * kBM + r] + red[3 * kBM + r]) * (1.f / kN);
       rstd[i] = rsqrtf(var + eps);
     }
@@ -280,7 +352,7 @@ __global__ __launch_bounds__(kThreads, 1) void k_gemm_rln(const uint16_t* __rest
       const float g[4] = {bf2f(gg.x & 0xffff), bf2f(gg.x >> 16), bf2f(gg.y & 0xffff), bf2f(gg.y >> 16)};
       const float be[4] = {bf2f(bb.x & 0xffff), bf2f(bb.x >> 16), bf2f(bb.y & 0xffff), bf2f(bb.y >> 16)};
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
+      for (int i = 0; i < MT; ++i) {
         const long m = mb + 16 * i;
         float o[4];
 #pragma unroll
@@ -403,22 +475,22 @@ int g_rln_variant = -1;
 int rln_variant() {
   if (g_rln_variant < 0) {
     const char* e = getenv("NOMIC_RLN");
-    g_rln_variant = e && *e ? atoi(e) : 11;  // PIPE * 10 + EPI
+    g_rln_variant = e && *e ? atoi(e) : 220;  // [ILV * 100 +] PIPE * 10 + EPI
   }
   return g_rln_variant;
 }
 
-template <int PIPE, int EPI>
+template <int PIPE, int EPI, int WM = 2, int ILV = 0, int PF = 1>
 void launch_rln(unsigned blocks, hipStream_t s, const uint16_t* A, long lda, const uint16_t* W, long ldw, int K, long M,
                 const uint16_t* res, long ldr, const uint16_t* gamma, const uint16_t* beta, float eps, uint16_t* out,
                 long ldo) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_gemm_rln<PIPE, EPI>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_gemm_rln<PIPE, EPI, WM, ILV, PF>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lds_bytes<PIPE>());
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL((k_gemm_rln<PIPE, EPI>), dim3(blocks), dim3(kThreads), lds_bytes<PIPE>(), s, A, lda, W, ldw, K,
+  hipLaunchKernelGGL((k_gemm_rln<PIPE, EPI, WM, ILV, PF>), dim3(blocks), dim3(256 * WM), lds_bytes<PIPE>(), s, A, lda, W, ldw, K,
                      M, res, ldr, gamma, beta, eps, out, ldo);
 }
 
@@ -448,6 +520,17 @@ extern "C" int nomic_gemm_res_ln(const void* A, long lda, const void* W, long ld
     case 21: launch_rln<2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 30: launch_rln<3, 0>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 31: launch_rln<3, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 210: launch_rln<1, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 220: launch_rln<2, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 230: launch_rln<3, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 212: launch_rln<1, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 222: launch_rln<2, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 213: launch_rln<1, 0, 2, 3>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 222 + 1000: launch_rln<2, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 222 + 2000: launch_rln<2, 0, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 222 + 3000: launch_rln<2, 2, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 242: launch_rln<4, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 243: launch_rln<4, 0, 2, 3>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     default: launch_rln<1, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
   }
   return (int)hipGetLastError();

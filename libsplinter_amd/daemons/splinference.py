@@ -18,6 +18,11 @@ one native batch and embedded in length-sorted varlen batches on the GPU
 vectors are written straight into the arena slots by the pooling kernel.
 Extra flags: --random-init (no GGUF: random weights + synthetic vocab),
 --batch-tokens, --poll-ms, --normalize, --layers (random-init only).
+
+Node stores ("node:NAME", one arena per GPU): one daemon per GPU (--rank, default $RANK), each
+embedding the pending keys of ITS shard on its own GPU -- data parallel, owner computes: vectors
+are pooled into local slots and no vector crosses xGMI.  Every daemon watches the node's summed
+signal counter (a pulse on any shard wakes all of them; each finds work only in its own shard).
 """
 from __future__ import annotations
 
@@ -48,9 +53,18 @@ def log(*a):
 
 class Splinference:
     def __init__(self, store, encoder, tokenizer, group: int, vector_training: bool = False,
-                 batch_tokens: int = 1 << 16, normalize: bool = False):
+                 batch_tokens: int = 1 << 16, normalize: bool = False, rank: Optional[int] = None):
         import torch  # noqa: F401
         from ..store import SLOT_VARTEXT
+        # `node`: the store clients use (signals, label map, bids, lane pulses); `store`: the one
+        # whose keys this daemon embeds -- the whole store, or this rank's shard of a node store
+        self.node = store
+        self.rank = 0
+        if getattr(store, "backend", None) == "node":
+            self.rank = int(os.environ.get("RANK", "0")) if rank is None else rank
+            if not 0 <= self.rank < store.nshards:
+                raise ValueError(f"rank {self.rank} outside the node's {store.nshards} shards")
+            store = store.shard(self.rank)
         self.store = store
         self.enc = encoder
         self.tok = tokenizer
@@ -62,9 +76,9 @@ class Splinference:
         self.processed: Dict[str, int] = {}
         self.vartext = SLOT_VARTEXT
         self.stats = {"embedded": 0, "exceeded": 0, "stale": 0, "skipped_trained": 0, "batches": 0}
-        store.watch_label(EMBED_LABEL, group)
+        self.node.watch_label(EMBED_LABEL, group)
         try:
-            store.shard_claim(SHARD_ID, 1, SHARD_PRIO_LIVE, SHARD_DUR_LIVE)
+            self.node.shard_claim(SHARD_ID, 1, SHARD_PRIO_LIVE, SHARD_DUR_LIVE)
         except Exception:
             pass
         # hbm: stores take the batched device path: one kernel per step for a whole batch of keys
@@ -264,7 +278,7 @@ class Splinference:
                     self.store.set_time(ks[i], 0, now_s, 0)
                 except Exception:  # noqa: BLE001
                     pass
-        self.store.pulse(LANE_KEY)
+        self.node.pulse(LANE_KEY)
         self.stats["embedded"] += done
         log(f"embedded {done}/{len(ks)} keys in {time.time() - t_start:.3f}s (ticks {dt})")
         return done
@@ -312,18 +326,18 @@ class Splinference:
         self.cold_start()
         if backfill:
             try:
-                self.store.shard_rebid(SHARD_ID, 2, SHARD_PRIO_BACKFILL, SHARD_DUR_BACKFILL)
+                self.node.shard_rebid(SHARD_ID, 2, SHARD_PRIO_BACKFILL, SHARD_DUR_BACKFILL)
             except Exception:  # noqa: BLE001
                 pass
             self.process(self.backfill_keys())
         last = -1
         while not stop():
-            sig = self.store.signal_count(self.group)
+            sig = self.node.signal_count(self.group)
             if sig != last or oneshot:
                 last = sig
                 try:
-                    self.store.shard_rebid(SHARD_ID, 1, SHARD_PRIO_LIVE, SHARD_DUR_LIVE)
-                    self.store.madvise(SHARD_ID, POSIX_MADV_WILLNEED, 0)
+                    self.node.shard_rebid(SHARD_ID, 1, SHARD_PRIO_LIVE, SHARD_DUR_LIVE)
+                    self.node.madvise(SHARD_ID, POSIX_MADV_WILLNEED, 0)
                 except Exception:  # noqa: BLE001
                     pass  # not sovereign: defer (non-blocking bid, as the reference)
                 self.process(self.pending())
@@ -331,7 +345,7 @@ class Splinference:
                 break
             time.sleep(poll_ms / 1000.0)
         try:
-            self.store.shard_release(SHARD_ID)
+            self.node.shard_release(SHARD_ID)
         except Exception:  # noqa: BLE001
             pass
 
@@ -366,6 +380,8 @@ def main(argv=None):
     ap.add_argument("--batch-tokens", type=int, default=1 << 16)
     ap.add_argument("--poll-ms", type=int, default=10)
     ap.add_argument("--normalize", action="store_true")
+    ap.add_argument("--rank", type=int, default=None,
+                    help="node stores: the shard this daemon embeds (default $RANK); runs on GPU rank %% devices")
     ap.add_argument("bus")
     ap.add_argument("gguf")
     ap.add_argument("group", type=int)
@@ -373,18 +389,24 @@ def main(argv=None):
     if not 0 <= a.group < 64:
         ap.error("group must be 0..63")
     sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
-    import torch  # noqa: F401
+    import torch
     from libsplinter_amd.store import Store
+    if a.bus.startswith("node:"):
+        rank = int(os.environ.get("RANK", "0")) if a.rank is None else a.rank
+        n = torch.cuda.device_count()
+        if n:
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", rank)) % n)
     store = Store.open(a.bus)
     if not store.embeddings:
         log("store has no embedding stride (128-B slots): recreate it with embeddings")
         return 2
     enc, tok = build_encoder(a.gguf, a.random_init, a.layers, a.batch_tokens + 4096)
-    d = Splinference(store, enc, tok, a.group, a.vector_training, a.batch_tokens, a.normalize)
+    d = Splinference(store, enc, tok, a.group, a.vector_training, a.batch_tokens, a.normalize, rank=a.rank)
     stop = {"v": False}
     signal.signal(signal.SIGINT, lambda *_: stop.__setitem__("v", True))
     signal.signal(signal.SIGTERM, lambda *_: stop.__setitem__("v", True))
-    log(f"serving {a.bus} group {a.group} (ceiling {d.ceiling} tokens)")
+    log(f"serving {a.bus} group {a.group} (ceiling {d.ceiling} tokens)" +
+        (f", shard {d.rank}/{store.nshards}" if store.backend == "node" else ""))
     d.run(oneshot=a.oneshot, backfill=a.backfill_text_keys, poll_ms=a.poll_ms, stop=lambda: stop["v"])
     log("stats", d.stats)
     store.close()

@@ -93,12 +93,37 @@ class Liveness:
         self._t.join(self.period * 4)
 
 
+def _collective_errors():
+    """Exception types that mean a collective (not local code) failed: the backend error, the
+    store/rendezvous timeout and a lost connection to a peer."""
+    errs = []
+    for name in ("DistBackendError", "DistNetworkError", "DistStoreError"):
+        if hasattr(dist, name):
+            errs.append(getattr(dist, name))
+    return tuple(errs)
+
+
+_COLLECTIVE_MARKERS = ("NCCL", "RCCL", "Gloo", "gloo", "collective", "timed out", "Connection reset",
+                       "Connection closed by peer", "ProcessGroup")
+
+
 def guarded(fn, *a, exit_code: int = EXIT_PEER_LOST, **kw):
     """Run ``fn``; a collective failure (timeout, aborted communicator, lost peer) ends the
-    process with ``exit_code`` instead of leaving it half-alive."""
+    process with ``exit_code`` instead of leaving it half-alive.  Any other exception -- a HIP
+    out-of-memory, a kernel launch failure, a shape bug in the step -- propagates with its
+    traceback: it is this rank's fault, not a lost peer."""
     try:
         return fn(*a, **kw)
-    except (RuntimeError, dist.DistBackendError if hasattr(dist, "DistBackendError") else RuntimeError) as e:
-        print(f"[splinter] rank {dist.get_rank() if dist.is_initialized() else '?'}: collective failed: {e!r}"[:500],
-              file=sys.stderr, flush=True)
-        os._exit(exit_code)
+    except _collective_errors() as e:
+        _peer_lost(e, exit_code)
+    except RuntimeError as e:
+        # older torch builds raise plain RuntimeErrors from the process group: classify by message
+        if any(m in str(e) for m in _COLLECTIVE_MARKERS):
+            _peer_lost(e, exit_code)
+        raise
+
+
+def _peer_lost(e, exit_code):
+    print(f"[splinter] rank {dist.get_rank() if dist.is_initialized() else '?'}: collective failed: {e!r}"[:500],
+          file=sys.stderr, flush=True)
+    os._exit(exit_code)

@@ -105,8 +105,9 @@ def node_leave(node: str, shard: int) -> None:
 class Store:
     """One open store.  Use :meth:`create`, :meth:`open` or :meth:`open_or_create`."""
 
-    def __init__(self, handle: int, name: str):
+    def __init__(self, handle: int, name: str, owned: bool = True):
         self._h = handle
+        self._owned = owned
         self.name = name
         self._L = N.core_lib()
         slots, mv, stride = N.c_u32(), N.c_u32(), N.c_u32()
@@ -151,8 +152,16 @@ class Store:
 
     def close(self) -> None:
         if self._h:
-            self._L.spl_store_close(self._h)
+            if self._owned:
+                self._L.spl_store_close(self._h)
             self._h = None
+
+    def shard(self, i: int) -> "Store":
+        """Shard i of a node store as a Store of its own (borrowed: the node keeps it open)."""
+        h = self._L.spl_node_shard(self._h, i)
+        if not h:
+            raise IndexError(f"{self.name}: no shard {i}")
+        return Store(h, f"{self.name}#s{i}", owned=False)
 
     def unlink(self) -> None:
         unlink(self.name)

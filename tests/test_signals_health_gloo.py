@@ -10,6 +10,7 @@ import os
 import socket
 import time
 
+import pytest
 import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
@@ -137,3 +138,21 @@ def test_hung_rank_survivors_exit_nonzero():
     """Rank 2 hangs (SIGSTOP, connections open): the collective would block for the gloo
     timeout; the liveness monitor sees the stale heartbeat and ends the survivors."""
     _run_dead("hang")
+
+
+def test_guarded_reraises_local_errors():
+    """A local failure inside the step (HIP OOM, launch failure, shape bug) is not a lost peer:
+    guarded() lets it propagate instead of exiting with EXIT_PEER_LOST."""
+    from libsplinter_amd.parallel.health import guarded
+
+    def oom():
+        raise RuntimeError("HIP out of memory. Tried to allocate 2.00 GiB")
+
+    def shape():
+        raise ValueError("shape mismatch")
+
+    with pytest.raises(RuntimeError, match="out of memory"):
+        guarded(oom)
+    with pytest.raises(ValueError):
+        guarded(shape)
+    assert guarded(lambda x: x + 1, 41) == 42

@@ -15,7 +15,15 @@ hash-shard of the key space in its own HBM arena (format v4, 128-B slots,
     are routed back (collective C1) inside the timed region.
   * embed phase (--mode mixed/embed): one batch of synthetic documents through
     the random-init Nomic-BERT encoder on the gfx950 kernels, mean-pooled
-    vectors written into their arena slots.
+    vectors written into their slots of the rank's search arena (--search-keys
+    embedded keys per GPU: the config #5 corpus).
+
+The client streams are the same at every N: at N=1 the set / get batches fan out over
+--writer-streams / --reader-streams HIP streams; at N>1 the owner fans the routed segments
+it received out over the same streams (spl_kvs_step_seg).  Outside the timed region:
+the routed step at N=1 (routed_kv_ops_per_s), end-to-end embedding, the per-call C API,
+and config #5's query phase (batched top-k over the search arenas, broadcast + all-gather
+merge at N>1, recall against the exact kernel).
 
 Ops counted exactly as the reference does (every set + get attempt that
 completes, splinter_stress.c:212-213); EAGAIN retries are reported separately.
@@ -75,6 +83,15 @@ def parse():
     p.add_argument("--host-api", type=int, default=16, metavar="THREADS",
                    help="also measure the per-call C API (splinter_set/get through the device command ring) "
                         "from THREADS host threads, outside the timed region; 0 = skip")
+    p.add_argument("--host-api-threads2", type=int, default=32, metavar="THREADS",
+                   help="a second per-call C API row at this many host threads (0 = skip)")
+    p.add_argument("--search-keys", type=int, default=25_000_000,
+                   help="embedded keys per GPU in the search arena (config #5: 200M x 768 over 8 GPUs); the embed "
+                        "phase writes its vectors into this arena; 0 = a small side arena, no query phase")
+    p.add_argument("--search-queries", type=int, default=256, help="queries per search batch (query phase)")
+    p.add_argument("--search-batches", type=int, default=8, help="timed search batches (query phase)")
+    p.add_argument("--routed-steps", type=int, default=10,
+                   help="N=1: also time this many steps of the routed (N>1) step on one GPU -> routed_kv_ops_per_s")
     return p.parse_args()
 
 
@@ -134,18 +151,26 @@ def main():
         return
 
     routed = world > 1 or args.force_routed
+    need_routed = routed or (args.routed_steps > 0 and args.mode != "embed")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
     liveness = None
-    if routed:
+    if need_routed and world == 1 and "MASTER_ADDR" not in os.environ:
+        import socket
+        with socket.socket() as so_:
+            so_.bind(("127.0.0.1", 0))
+            os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(so_.getsockname()[1]), RANK="0",
+                              WORLD_SIZE="1")
+    if need_routed:
         # finite collective timeouts + async RCCL error handling, and a heartbeat monitor: a lost
         # rank ends every survivor with a non-zero exit instead of a hung node (parallel/health.py)
         from libsplinter_amd.parallel.health import Liveness, init_distributed
         init_distributed(args.backend, timeout_s=600.0,
                          device_id=torch.device("cuda", dev) if args.backend == "nccl" else None)
-        liveness = Liveness(period_s=1.0, timeout_s=120.0)
+        if world > 1:
+            liveness = Liveness(period_s=1.0, timeout_s=120.0)
     sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
     from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
     from libsplinter_amd.parallel.sharded import GpuShard, ShardedKV
@@ -161,7 +186,7 @@ def main():
         arena.store.set_mop(args.mop)  # 1 = hybrid scrub, the reference's store default
     kv = ShardedKV(GpuShard(arena))
     rkv = None
-    if routed:
+    if need_routed:
         # request and response all-to-alls on their own communicators (= their own RCCL streams):
         # step i's responses and step i+1's requests are in flight together
         from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
@@ -208,11 +233,34 @@ def main():
         batches.append((SK, SV, SL, GK, gid))
     gout = torch.empty((n_get, vstride), dtype=torch.uint8, device="cuda")
 
+    # ---- search arena (config #5 corpus): --search-keys embedded keys per GPU -------------
+    sarena = None
+    if args.search_keys > 0 and args.mode in ("embed", "mixed"):
+        t1 = time.time()
+        sarena = HbmArena.create(f"sbench{os.getpid()}r{rank}", slots=int(args.search_keys * 1.25) + 4096,
+                                 max_val=64, embeddings=True)
+        g0 = torch.Generator(device="cuda")
+        g0.manual_seed(77 + rank)
+        ch = 1 << 20
+        for first in range(0, args.search_keys, ch):
+            n = min(ch, args.search_keys - first)
+            K = format_keys(n, f"v{rank}_", 9, 16, first=first)
+            V, L = format_values(n, 1, 32, 64, first=first)
+            st = sarena.set(K, V, L)
+            vec = torch.randn((n, 768), device="cuda", generator=g0)
+            st2 = sarena.set_embeddings(K, vec)
+            if int((st != 0).sum()) or int((st2 != 0).sum()):
+                raise RuntimeError("search arena prepopulation failed")
+            del K, V, L, vec, st, st2
+        torch.cuda.synchronize()
+        log(f"[bench] rank0 search arena {args.search_keys} embedded keys in {time.time() - t1:.1f}s "
+            f"({sarena.slots * (3200 + 64) / 2**30:.1f} GiB)")
+
     # ---- embed phase (model) --------------------------------------------
     embedder = None
     if args.mode in ("embed", "mixed"):
         from libsplinter_amd.models.bench_embed import EmbedPhase
-        embedder = EmbedPhase(arena, batch=args.embed_batch, seq=args.embed_seq, rank=rank)
+        embedder = EmbedPhase(arena, batch=args.embed_batch, seq=args.embed_seq, rank=rank, doc_arena=sarena)
 
     # set and get batches race each other on two hardware queues (utils/streams.py: distinct
     # priorities = distinct queue pools).  The embed phase runs AFTER the KV phase, not beside it:
@@ -220,8 +268,8 @@ def main():
     # which stretched the concurrently running GEMMs 2x and made the overlapped step slower than
     # the serial one (profiles/r1_mixed_overlap.md).
     from libsplinter_amd.utils.streams import stream as hip_stream
-    py_streams = bool(args.kv_cus) or args.overlap or routed or bool(os.environ.get("BENCH_PY_STREAMS"))
-    s_get, s_set = (hip_stream("high"), hip_stream("normal")) if py_streams else (None, None)
+    py_streams = bool(args.kv_cus) or args.overlap or bool(os.environ.get("BENCH_PY_STREAMS"))
+    s_get, s_set = (hip_stream("high"), hip_stream("normal")) if (py_streams or need_routed) else (None, None)
     # BASELINE config #2: the set batch is issued by --writer-streams concurrent client streams and the
     # get batch by --reader-streams (streams share the HIP runtime's hardware queues, at most
     # GPU_MAX_HW_QUEUES per priority level; readers at high priority, writers at normal)
@@ -312,7 +360,7 @@ def main():
     #   s_set / s_get : owner kernels of batch i, after its requests and embed_i
     #   s_resp: response all-to-alls + gather of batch i       (overlaps embed_{i+1})
     # All K steps' responses are delivered inside the timed region (device-wide sync at the end).
-    if routed:
+    if need_routed:
         cap_s, cap_g = route_capacity(max(n_set, 1), world), route_capacity(max(n_get, 1), world)
         vw = min((args.value_len + 15) // 16 * 16, vstride)
         s_req, s_resp = hip_stream("low"), hip_stream("low")
@@ -335,14 +383,23 @@ def main():
             embedder.run()
         ev_emb = cur.record_event()
         prev_exec.clear()
-        for s, op in ((s_set, so), (s_get, go)):
-            if op is None:
-                continue
-            s.wait_event(ev_req)
-            s.wait_event(ev_emb)
-            with torch.cuda.stream(s):
-                rkv.execute(op)
-                prev_exec.append(s.record_event())
+        if kvs is not None:
+            # owner kernels on the same writer / reader client streams as a local step: the received
+            # segments fan out natively from one origin stream (spl_kvs_step_seg)
+            s_set.wait_event(ev_req)
+            s_set.wait_event(ev_emb)
+            with torch.cuda.stream(s_set):
+                rkv.execute_fanout(so, go, kvs)
+                prev_exec.append(s_set.record_event())
+        else:
+            for s, op in ((s_set, so), (s_get, go)):
+                if op is None:
+                    continue
+                s.wait_event(ev_req)
+                s.wait_event(ev_emb)
+                with torch.cuda.stream(s):
+                    rkv.execute(op)
+                    prev_exec.append(s.record_event())
         for e in prev_exec:
             s_resp.wait_event(e)
         with torch.cuda.stream(s_resp):
@@ -417,23 +474,38 @@ def main():
             dist.all_reduce(x)
             integrity_fail = int(x.item())
 
+    # ---- N=1: the routed (N>1) step on one GPU, same streams and batches (outside the headline) ----
+    routed1 = None
+    if not routed and rkv is not None and args.routed_steps > 0:
+        for i in range(2):
+            step_routed(i)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for i in range(args.routed_steps):
+            step_routed(2 + i)
+        torch.cuda.synchronize()
+        dtr = time.perf_counter() - t0
+        routed1 = {"ops_per_s": (n_set + n_get) * args.routed_steps / dtr, "ms_per_step": dtr / args.routed_steps * 1e3}
+
     # ---- per-call C API (outside the timed region): splinter_set / splinter_get from host threads
     # through the device command ring of an hbm: store (tools/splinter_hostapi_bench.cpp)
-    host_api = None
-    if args.host_api > 0 and rank == 0:
+    def host_api_run(threads):
         import subprocess
         tool = os.path.join(os.path.dirname(os.path.abspath(__file__)), "libsplinter_amd", "bin",
                             "splinter_hostapi_bench")
         try:
-            r = subprocess.run([tool, "--store", f"hbm:hapi{os.getpid()}", "--threads", str(args.host_api),
+            r = subprocess.run([tool, "--store", f"hbm:hapi{os.getpid()}t{threads}", "--threads", str(threads),
                                 "--seconds", "1", "--keys", "65536", "--value-len", str(args.value_len)],
                                capture_output=True, text=True, timeout=120)
             if r.returncode == 0:
-                host_api = json.loads(r.stdout.strip().splitlines()[-1])
-            else:
-                log(f"[bench] host-API run failed: {r.stderr[-300:]}")
+                return json.loads(r.stdout.strip().splitlines()[-1])
+            log(f"[bench] host-API run failed: {r.stderr[-300:]}")
         except Exception as e:  # the headline stands without it
             log(f"[bench] host-API run failed: {e}")
+        return None
+
+    host_api = host_api_run(args.host_api) if args.host_api > 0 and rank == 0 else None
+    host_api2 = host_api_run(args.host_api_threads2) if args.host_api_threads2 > 0 and rank == 0 else None
 
     e2e = None
     if embedder is not None and args.embed_e2e > 0:
@@ -456,6 +528,38 @@ def main():
                "tokens_per_batch": pipe.tokens, "write_failures": fails}
         pipe.close()
 
+    # ---- config #5 query phase: batched cosine top-10 over every rank's search arena ---------
+    # (the vectors the embed phase wrote are in there too).  Rank 0's queries are broadcast (C3),
+    # each GPU scores its arena with the MFMA search pass + fp32 re-score (K7), and the local top-k
+    # lists are all-gathered and merged (C4).  Recall@10 of the batched path against the exact fp32
+    # kernel on the first 16 queries.
+    search = None
+    if sarena is not None and args.search_queries > 0 and args.search_batches > 0:
+        skv = ShardedKV(GpuShard(sarena))
+        gq = torch.Generator(device="cuda")
+        gq.manual_seed(4242)
+        ids = torch.randint(0, args.search_keys, (args.search_queries,), device="cuda", generator=gq)
+        _, base = sarena.get_embeddings(format_keys(args.search_queries, "v0_", 9, 16, ids=ids))
+        q = base + 0.5 * torch.randn(base.shape, device="cuda", generator=gq)
+        skv.search(q, k=10)  # warm-up (search workspaces, first-shape setup)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.search_batches):
+            own_b, sim_b, _, key_b = skv.search(q, k=10)
+        torch.cuda.synchronize()
+        ts = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(ts, op=dist.ReduceOp.MAX)
+        own_e, sim_e, _, key_e = skv.search(q[:16], k=10)  # < 32 queries: the exact fp32 kernel
+        kb = [set(bytes(r).split(b"\0", 1)[0] for r in key_b[i].cpu().numpy()) for i in range(16)]
+        ke = [set(bytes(r).split(b"\0", 1)[0] for r in key_e[i].cpu().numpy()) for i in range(16)]
+        recall = sum(len(a & b) for a, b in zip(kb, ke)) / sum(len(b) for b in ke)
+        dt = ts.item()
+        search = {"qps": args.search_queries * args.search_batches / dt, "ms_per_batch": dt / args.search_batches * 1e3,
+                  "recall_at_10": recall, "keys_total": args.search_keys * world}
+
     kv_ops = (n_set + n_get) * args.steps * world
     kv_ops_s = kv_ops / elapsed if kv_ops else 0.0
     emb_vps = emb_tps = emb_tflops = None
@@ -476,14 +580,19 @@ def main():
         "scaling": "weak",
         "vs_baseline": (value / REF_MRMW_OPS) if args.mode != "embed" else None,
         "dtype": "bf16" if embedder is not None else "u8-kv",
-        "data": "synthetic keys k%010d / 150-B 'ver:|id:|data:' payloads; random-init Nomic weights",
+        "data": "synthetic keys k%010d / 150-B 'ver:|id:|data:' payloads; random-init Nomic weights; "
+                "random N(0,1) 768-d vectors in the search arenas",
         "config": {
             "model": "hbm-arena-v4 (128-B slots, 256-B values)" + (" + nomic-embed-text-v1.5" if embedder else ""),
             "keys_per_gpu": kpg, "slots_per_gpu": slots, "global_batch": args.batch * world,
             "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
             "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),
             "mode": args.mode, "mop": args.mop, "value_len": args.value_len,
-            "writer_streams": nw if not routed else 1, "reader_streams": nr if not routed else 1,
+            "writer_streams": nw, "reader_streams": nr,
+            "hw_queues_per_priority": int(os.environ["GPU_MAX_HW_QUEUES"]),
+            "collectives": ("RCCL on torch's per-process-group streams (request / response groups), "
+                            "sharing the normal-priority queue pool with the writers") if routed else None,
+            "search_keys_per_gpu": args.search_keys if sarena is not None else 0,
         },
         "kv_ops_per_s": kv_ops_s,
         "embed_vectors_per_s": emb_vps,
@@ -500,14 +609,25 @@ def main():
         "host_api_ops_per_s": host_api["ops_per_s"] if host_api else None,
         "host_api_p50_us": host_api["p50_us"] if host_api else None,
         "host_api_p99_us": host_api["p99_us"] if host_api else None,
+        "host_api_threads2": args.host_api_threads2 if host_api2 else None,
+        "host_api2_ops_per_s": host_api2["ops_per_s"] if host_api2 else None,
+        "host_api2_p50_us": host_api2["p50_us"] if host_api2 else None,
+        "routed_kv_ops_per_s": routed1["ops_per_s"] if routed1 else (kv_ops_s if routed else None),
+        "routed_ms_per_step": routed1["ms_per_step"] if routed1 else None,
+        "search_qps": search["qps"] if search else None,
+        "search_ms_per_batch": search["ms_per_batch"] if search else None,
+        "search_recall_at_10": search["recall_at_10"] if search else None,
+        "search_keys_total": search["keys_total"] if search else None,
     }
     if rank == 0:
         print(json.dumps(res), flush=True)
     if liveness is not None:
         dist.barrier()
         liveness.stop()
+    if sarena is not None:
+        sarena.close()
     arena.close()
-    if routed:
+    if need_routed:
         dist.destroy_process_group()
 
 

@@ -201,6 +201,8 @@ def _declare_hip(L):
     _sig(L, "spl_kvs_create", P, c_int, c_int)
     _sig(L, "spl_kvs_destroy", None, P)
     _sig(L, "spl_kvs_step", c_int, P, A, P, P, c_int, P, c_int, P, c_long, P, P, P, c_int, P, c_long, P, c_int, P)
+    _sig(L, "spl_kvs_step_seg", c_int, P, A, P, P, c_int, P, c_int, P, c_long, P, P, c_long, P, P, c_int, P, c_long,
+         P, P, c_long, c_int, P)
     if hasattr(L, "spl_hbm_ring_launches"):
         _sig(L, "spl_hbm_ring_launches", c_u32, c_void_p)
     _sig(L, "spl_arena_purge", c_int, A, P)

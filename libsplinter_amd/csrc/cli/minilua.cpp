@@ -14,6 +14,8 @@
 #include <mutex>
 #include <thread>
 #include <unordered_set>
+#include <unistd.h>
+#include <cerrno>
 
 namespace mlua {
 
@@ -185,7 +187,7 @@ static int64_t toint_strict(const Value& v, const char* what) {
 enum Tok {
   T_EOF, T_NAME, T_NUMBER, T_STRING,
   T_AND, T_BREAK, T_DO, T_ELSE, T_ELSEIF, T_END, T_FALSE, T_FOR, T_FUNCTION, T_IF, T_IN, T_LOCAL, T_NIL, T_NOT,
-  T_OR, T_REPEAT, T_RETURN, T_THEN, T_TRUE, T_UNTIL, T_WHILE,
+  T_OR, T_REPEAT, T_RETURN, T_THEN, T_TRUE, T_UNTIL, T_WHILE, T_GOTO,
   T_EQ, T_NE, T_LE, T_GE, T_CONCAT, T_DOTS, T_IDIV, T_SHL, T_SHR, T_DBCOLON,
   T_CHAR  // single-char token in `ch`
 };
@@ -253,7 +255,7 @@ struct Lexer {
           {"and", T_AND}, {"break", T_BREAK}, {"do", T_DO}, {"else", T_ELSE}, {"elseif", T_ELSEIF}, {"end", T_END},
           {"false", T_FALSE}, {"for", T_FOR}, {"function", T_FUNCTION}, {"if", T_IF}, {"in", T_IN},
           {"local", T_LOCAL}, {"nil", T_NIL}, {"not", T_NOT}, {"or", T_OR}, {"repeat", T_REPEAT},
-          {"return", T_RETURN}, {"then", T_THEN}, {"true", T_TRUE}, {"until", T_UNTIL}, {"while", T_WHILE}};
+          {"return", T_RETURN}, {"then", T_THEN}, {"true", T_TRUE}, {"until", T_UNTIL}, {"while", T_WHILE}, {"goto", T_GOTO}};
       auto it = kw.find(t.s);
       t.t = it == kw.end() ? T_NAME : it->second;
       return t;
@@ -378,7 +380,7 @@ struct Expr {
 };
 
 enum StatKind { S_LOCAL, S_ASSIGN, S_CALL, S_DO, S_WHILE, S_REPEAT, S_IF, S_NUMFOR, S_GENFOR, S_RETURN, S_BREAK,
-                S_LOCALFUNC };
+                S_LOCALFUNC, S_GOTO, S_LABEL };
 
 struct Stat {
   StatKind k;
@@ -584,8 +586,17 @@ struct Parser {
         advance();
         s->k = S_BREAK;
         return s;
+      case T_GOTO:
+        advance();
+        s->k = S_GOTO;
+        s->names.push_back(name());
+        return s;
       case T_DBCOLON:
-        err("goto/labels are not supported");
+        advance();
+        s->k = S_LABEL;
+        s->names.push_back(name());
+        if (!accept(T_DBCOLON)) err("'::' expected");
+        return s;
       default: break;
     }
     // exprstat: call or assignment
@@ -830,11 +841,34 @@ Table::~Table() { if (heap) heap->tables.erase(this); }
 Scope::Scope() : heap(t_heap) { if (heap) heap->scopes.insert(this); }
 Scope::~Scope() { if (heap) heap->scopes.erase(this); }
 
-enum Flow { F_NORMAL, F_BREAK, F_RETURN };
+// F_GOTO: a `goto` looking for its label; every enclosing block searches its own statements
+// (Lua 5.4: a label is visible in the block that defines it and in nested blocks, functions excluded)
+enum Flow { F_NORMAL, F_BREAK, F_RETURN, F_GOTO };
 
 struct Exec {
   Interp& I;
   Values ret;
+  std::string go_label;  // the label a pending F_GOTO looks for
+
+  // run b's statements from index `from`; a goto whose label is in b continues at the label
+  Flow run_stats(const std::shared_ptr<Block>& b, const std::shared_ptr<Scope>& sc) {
+    Flow f = F_NORMAL;
+    for (size_t i = 0; i < b->stats.size(); ++i) {
+      f = exec(b->stats[i], sc);
+      if (f == F_GOTO) {
+        size_t j = 0;
+        for (; j < b->stats.size(); ++j)
+          if (b->stats[j]->k == S_LABEL && b->stats[j]->names[0] == go_label) break;
+        if (j < b->stats.size()) {
+          i = j;  // the loop's ++i runs the statement after the label
+          f = F_NORMAL;
+          continue;
+        }
+      }
+      if (f != F_NORMAL) break;
+    }
+    return f;
+  }
   explicit Exec(Interp& in) : I(in) {}
 
   std::shared_ptr<Value> lookup(Scope* s, const std::string& n) {
@@ -1135,10 +1169,7 @@ struct Exec {
     auto sc = push(parent);
     Flow f = F_NORMAL;
     try {
-      for (auto& st : b->stats) {
-        f = exec(st, sc);
-        if (f != F_NORMAL) break;
-      }
+      f = run_stats(b, sc);
     } catch (...) {
       pop();
       throw;
@@ -1178,7 +1209,7 @@ struct Exec {
         while (eval(st->e, s).truthy()) {
           Flow f = exec_block(st->body, sc);
           if (f == F_BREAK) break;
-          if (f == F_RETURN) return f;
+          if (f == F_RETURN || f == F_GOTO) return f;
         }
         return F_NORMAL;
       case S_REPEAT:
@@ -1188,10 +1219,7 @@ struct Exec {
           Flow f = F_NORMAL;
           bool done = false;
           try {
-            for (auto& x : st->body->stats) {
-              f = exec(x, inner);
-              if (f != F_NORMAL) break;
-            }
+            f = run_stats(st->body, inner);
             if (f == F_NORMAL) done = eval(st->e, inner.get()).truthy();
           } catch (...) {
             pop();
@@ -1199,7 +1227,7 @@ struct Exec {
           }
           pop();
           if (f == F_BREAK) break;
-          if (f == F_RETURN) return f;
+          if (f == F_RETURN || f == F_GOTO) return f;
           if (done) break;
         }
         return F_NORMAL;
@@ -1221,7 +1249,7 @@ struct Exec {
             pop();
             Flow f = exec_block(st->body, body);
             if (f == F_BREAK) break;
-            if (f == F_RETURN) return f;
+            if (f == F_RETURN || f == F_GOTO) return f;
             if ((z.i > 0 && i > INT64_MAX - z.i) || (z.i < 0 && i < INT64_MIN - z.i)) break;
           }
         } else {
@@ -1233,7 +1261,7 @@ struct Exec {
             pop();
             Flow f = exec_block(st->body, body);
             if (f == F_BREAK) break;
-            if (f == F_RETURN) return f;
+            if (f == F_RETURN || f == F_GOTO) return f;
           }
         }
         return F_NORMAL;
@@ -1253,7 +1281,7 @@ struct Exec {
           pop();
           Flow fl = exec_block(st->body, body);
           if (fl == F_BREAK) break;
-          if (fl == F_RETURN) return fl;
+          if (fl == F_RETURN || fl == F_GOTO) return fl;
         }
         return F_NORMAL;
       }
@@ -1261,6 +1289,10 @@ struct Exec {
         ret = eval_list(st->exprs, s);
         return F_RETURN;
       case S_BREAK: return F_BREAK;
+      case S_GOTO:
+        go_label = st->names[0];
+        return F_GOTO;
+      case S_LABEL: return F_NORMAL;
     }
     return F_NORMAL;
   }
@@ -1358,6 +1390,7 @@ Values Interp::call(const Value& f0, Values args) {
   }
   Flow fl = ex.exec_block(body.block, sc);
   ex.pop();
+  if (fl == F_GOTO) throw LuaError("no visible label '" + ex.go_label + "' for goto");
   return fl == F_RETURN ? ex.ret : Values{};
 }
 
@@ -1836,13 +1869,31 @@ static std::string lua_format(Values& a) {
       }
       case 'q': {
         Value v = arg_at(a, ai++);
-        if (v.t != Value::Str) { out += tostring(v); break; }
+        if (v.t != Value::Str) {
+          // integers as themselves, floats in hex (%a) so they read back exactly (lstrlib.c quotefloat)
+          if (v.t == Value::Num) {
+            if (v.n == (double)(int64_t)v.n) snprintf(buf, sizeof buf, "%lld.0", (long long)v.n);
+            else snprintf(buf, sizeof buf, "%a", v.n);
+            out += buf;
+          } else {
+            out += tostring(v);
+          }
+          break;
+        }
         out += '"';
-        for (char ch : *v.s) {
-          if (ch == '"' || ch == '\\') { out += '\\'; out += ch; }
-          else if (ch == '\n') out += "\\n";
-          else if ((unsigned char)ch < 32) { snprintf(buf, sizeof buf, "\\%d", (unsigned char)ch); out += buf; }
-          else out += ch;
+        const std::string& sv = *v.s;
+        for (size_t q = 0; q < sv.size(); ++q) {
+          const unsigned char ch = (unsigned char)sv[q];
+          if (ch == '"' || ch == '\\') { out += '\\'; out += (char)ch; }
+          else if (ch == '\n') out += "\\\n";  // backslash-newline, as Lua 5.4
+          else if (ch == '\r') out += "\\r";
+          else if (ch == 0) out += (q + 1 < sv.size() && isdigit((unsigned char)sv[q + 1])) ? "\\000" : "\\0";
+          else if (ch < 32 || ch == 127) {
+            // a following digit would extend the escape: pad to three digits then (lstrlib.c addquoted)
+            snprintf(buf, sizeof buf, (q + 1 < sv.size() && isdigit((unsigned char)sv[q + 1])) ? "\\%03d" : "\\%d", ch);
+            out += buf;
+          }
+          else out += (char)ch;
         }
         out += '"';
         break;
@@ -2330,7 +2381,532 @@ Interp::Interp() {
     const char* v = getenv(check_str(a, 0, "getenv").c_str());
     return Values{v ? Value::string(v) : Value()};
   });
-  for (const char* lib : {"string", "table", "math", "os", "coroutine"}) modules[lib] = G->get(Value::string(lib));
+  // ---- the rest of the standard library (luaL_openlibs in the reference, splinter_cli_cmd_lua.c:395)
+  // table.sort / table.move
+  auto lua_less = [](Interp& I, const Value& a, const Value& b) -> bool {
+    if (a.t == Value::Int && b.t == Value::Int) return a.i < b.i;
+    if (a.is_num() && b.is_num()) return a.as_double() < b.as_double();
+    if (a.t == Value::Str && b.t == Value::Str) return *a.s < *b.s;
+    Value mm = I.metamethod(a, "__lt");
+    if (mm.t == Value::Nil) mm = I.metamethod(b, "__lt");
+    if (mm.t == Value::Nil)
+      throw LuaError(std::string("attempt to compare ") + type_name(a) + " with " + type_name(b));
+    Values r = I.call(mm, {a, b});
+    return !r.empty() && r[0].truthy();
+  };
+  reg(T, "sort", [lua_less](Interp& I, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) throw LuaError("bad argument #1 to 'sort' (table expected)");
+    Value cmp = arg_at(a, 1);
+    if (cmp.t != Value::Nil && cmp.t != Value::Fn) throw LuaError("bad argument #2 to 'sort' (function expected)");
+    const int64_t n = t.tab->length();
+    std::vector<Value> v((size_t)n), tmp((size_t)n);
+    for (int64_t i = 0; i < n; ++i) v[(size_t)i] = t.tab->get(Value::integer(i + 1));
+    auto less = [&](const Value& x, const Value& y) {
+      if (cmp.t == Value::Fn) {
+        Values r = I.call(cmp, {x, y});
+        return !r.empty() && r[0].truthy();
+      }
+      return lua_less(I, x, y);
+    };
+    // bottom-up merge sort: O(n log n) comparisons, and an inconsistent order function (which Lua
+    // reports or tolerates) cannot run it out of bounds the way it can std::sort
+    for (size_t w = 1; w < v.size(); w *= 2) {
+      for (size_t lo = 0; lo < v.size(); lo += 2 * w) {
+        const size_t mid = std::min(lo + w, v.size()), hi = std::min(lo + 2 * w, v.size());
+        size_t i = lo, j = mid, k = lo;
+        while (i < mid && j < hi) tmp[k++] = less(v[j], v[i]) ? v[j++] : v[i++];
+        while (i < mid) tmp[k++] = v[i++];
+        while (j < hi) tmp[k++] = v[j++];
+      }
+      v.swap(tmp);
+    }
+    for (int64_t i = 0; i < n; ++i) t.tab->set(Value::integer(i + 1), v[(size_t)i]);
+    return Values{};
+  });
+  reg(T, "move", [](Interp&, Values& a) {
+    Value a1 = arg_at(a, 0);
+    if (a1.t != Value::Tab) throw LuaError("bad argument #1 to 'move' (table expected)");
+    const int64_t f = check_int(a, 1, "move"), e = check_int(a, 2, "move"), t = check_int(a, 3, "move");
+    Value a2 = a.size() > 4 && a[4].t != Value::Nil ? a[4] : a1;
+    if (a2.t != Value::Tab) throw LuaError("bad argument #5 to 'move' (table expected)");
+    if (e >= f) {
+      if (t > e || t <= f || a1.tab != a2.tab)
+        for (int64_t i = 0; i <= e - f; ++i) a2.tab->set(Value::integer(t + i), a1.tab->get(Value::integer(f + i)));
+      else
+        for (int64_t i = e - f; i >= 0; --i) a2.tab->set(Value::integer(t + i), a1.tab->get(Value::integer(f + i)));
+    }
+    return Values{a2};
+  });
+  reg(T, "pack", [](Interp&, Values& a) {
+    auto t = std::make_shared<Table>();
+    for (size_t i = 0; i < a.size(); ++i) t->set(Value::integer((int64_t)i + 1), a[i]);
+    t->set(Value::string("n"), Value::integer((int64_t)a.size()));
+    return Values{Value::table(t)};
+  });
+
+  // math.type / math.ult
+  reg(M, "type", [](Interp&, Values& a) {
+    if (a.empty()) throw LuaError("bad argument #1 to 'type' (value expected)");
+    const Value v = a[0];
+    return Values{v.t == Value::Int ? Value::string("integer") : v.t == Value::Num ? Value::string("float") : Value()};
+  });
+  reg(M, "ult", [](Interp&, Values& a) {
+    return Values{Value::boolean((uint64_t)check_int(a, 0, "ult") < (uint64_t)check_int(a, 1, "ult"))};
+  });
+  reg(M, "exp", [](Interp&, Values& a) { return Values{Value::number(std::exp(check_num(a, 0, "exp")))}; });
+  reg(M, "log", [](Interp&, Values& a) {
+    const double x = check_num(a, 0, "log");
+    if (a.size() < 2 || a[1].t == Value::Nil) return Values{Value::number(std::log(x))};
+    const double b = check_num(a, 1, "log");
+    return Values{Value::number(b == 2.0 ? std::log2(x) : b == 10.0 ? std::log10(x) : std::log(x) / std::log(b))};
+  });
+  for (auto& [nm, fn] : std::vector<std::pair<const char*, double (*)(double)>>{
+           {"sin", std::sin}, {"cos", std::cos}, {"tan", std::tan}, {"asin", std::asin}, {"acos", std::acos}})
+    reg(M, nm, [fn, nm](Interp&, Values& a) { return Values{Value::number(fn(check_num(a, 0, nm)))}; });
+  reg(M, "atan", [](Interp&, Values& a) {
+    const double y = check_num(a, 0, "atan"), x = a.size() > 1 && a[1].t != Value::Nil ? check_num(a, 1, "atan") : 1.0;
+    return Values{Value::number(std::atan2(y, x))};
+  });
+  reg(M, "modf", [](Interp&, Values& a) {
+    double ip = 0;
+    const double fp = std::modf(check_num(a, 0, "modf"), &ip);
+    int64_t i;
+    return Values{float_is_int(ip, &i) ? Value::number(ip) : Value::number(ip), Value::number(fp)};
+  });
+
+  // os.date / os.time(table) / os.remove / os.rename / os.exit / os.difftime / os.tmpname
+  reg(O, "date", [](Interp&, Values& a) {
+    std::string fmt = a.size() > 0 && a[0].t != Value::Nil ? check_str(a, 0, "date") : "%c";
+    time_t t = a.size() > 1 && a[1].t != Value::Nil ? (time_t)check_int(a, 1, "date") : time(nullptr);
+    bool utc = false;
+    if (!fmt.empty() && fmt[0] == '!') { utc = true; fmt = fmt.substr(1); }
+    struct tm tmv;
+    if (!(utc ? gmtime_r(&t, &tmv) : localtime_r(&t, &tmv))) return Values{Value()};
+    if (fmt.rfind("*t", 0) == 0) {
+      auto r = std::make_shared<Table>();
+      const std::pair<const char*, int> f[] = {{"year", tmv.tm_year + 1900}, {"month", tmv.tm_mon + 1},
+                                               {"day", tmv.tm_mday}, {"hour", tmv.tm_hour}, {"min", tmv.tm_min},
+                                               {"sec", tmv.tm_sec}, {"wday", tmv.tm_wday + 1},
+                                               {"yday", tmv.tm_yday + 1}};
+      for (auto& kv : f) r->set(Value::string(kv.first), Value::integer(kv.second));
+      r->set(Value::string("isdst"), Value::boolean(tmv.tm_isdst > 0));
+      return Values{Value::table(r)};
+    }
+    char buf[512];
+    const size_t n = strftime(buf, sizeof buf, fmt.c_str(), &tmv);
+    return Values{Value::string(std::string(buf, n))};
+  });
+  reg(O, "time", [](Interp&, Values& a) {
+    Value t = arg_at(a, 0);
+    if (t.t != Value::Tab) return Values{Value::integer((int64_t)time(nullptr))};
+    auto field = [&](const char* k, int dflt) -> int {
+      Value v = t.tab->get(Value::string(k));
+      if (v.t == Value::Nil) {
+        if (dflt < 0) throw LuaError(std::string("field '") + k + "' missing in date table");
+        return dflt;
+      }
+      return (int)toint_strict(v, "time");
+    };
+    struct tm tmv {};
+    tmv.tm_year = field("year", -1) - 1900;
+    tmv.tm_mon = field("month", -1) - 1;
+    tmv.tm_mday = field("day", -1);
+    tmv.tm_hour = field("hour", 12);
+    tmv.tm_min = field("min", 0);
+    tmv.tm_sec = field("sec", 0);
+    Value dst = t.tab->get(Value::string("isdst"));
+    tmv.tm_isdst = dst.t == Value::Nil ? -1 : dst.truthy();
+    return Values{Value::integer((int64_t)mktime(&tmv))};
+  });
+  reg(O, "difftime", [](Interp&, Values& a) {
+    return Values{Value::number(difftime((time_t)check_int(a, 0, "difftime"),
+                                         a.size() > 1 ? (time_t)check_int(a, 1, "difftime") : 0))};
+  });
+  auto os_result = [](int rc, const std::string& what) {
+    if (rc == 0) return Values{Value::boolean(true)};
+    const int e = errno;
+    return Values{Value(), Value::string(what + ": " + strerror(e)), Value::integer(e)};
+  };
+  reg(O, "remove", [os_result](Interp&, Values& a) {
+    const std::string p = check_str(a, 0, "remove");
+    return os_result(::remove(p.c_str()), p);
+  });
+  reg(O, "rename", [os_result](Interp&, Values& a) {
+    const std::string p = check_str(a, 0, "rename"), q = check_str(a, 1, "rename");
+    return os_result(::rename(p.c_str(), q.c_str()), p);
+  });
+  reg(O, "tmpname", [](Interp&, Values&) {
+    char buf[] = "/tmp/lua_XXXXXX";
+    const int fd = mkstemp(buf);
+    if (fd < 0) throw LuaError("unable to generate a unique filename");
+    ::close(fd);
+    return Values{Value::string(buf)};
+  });
+  reg(O, "exit", [](Interp& I, Values& a) -> Values {
+    Value c = arg_at(a, 0);
+    const int code = c.t == Value::Nil || (c.t == Value::Bool && c.b) ? 0
+                     : c.t == Value::Bool                             ? 1
+                                                                      : (int)toint_strict(c, "exit");
+    I.out("");
+    fflush(stdout);
+    fflush(stderr);
+    std::exit(code);
+  });
+
+  // io: files are tables carrying their FILE* (metatable FILE* with the methods)
+  auto FM = std::make_shared<Table>();   // file metatable
+  auto FMI = std::make_shared<Table>();  // its __index: the methods
+  FM->set(Value::string("__index"), Value::table(FMI));
+  FM->set(Value::string("__name"), Value::string("FILE*"));
+  auto mkfile = [FM](FILE* fp, bool std_stream) {
+    auto t = std::make_shared<Table>();
+    t->set(Value::string("__fp"), Value::integer((int64_t)(intptr_t)fp));
+    if (std_stream) t->set(Value::string("__std"), Value::boolean(true));
+    t->meta = FM;
+    return Value::table(t);
+  };
+  auto fp_of = [](const Value& f, const char* fn) -> FILE* {
+    if (f.t != Value::Tab) throw LuaError(std::string("bad argument #1 to '") + fn + "' (FILE* expected)");
+    Value p = f.tab->get(Value::string("__fp"));
+    if (p.t != Value::Int) throw LuaError(std::string("bad argument #1 to '") + fn + "' (FILE* expected)");
+    if (!p.i) throw LuaError("attempt to use a closed file");
+    return (FILE*)(intptr_t)p.i;
+  };
+  // one read format on fp: l / L / n / a / count; nil at end of input
+  auto read_one = [](FILE* fp, const Value& fmt) -> Value {
+    if (fmt.is_num()) {
+      const int64_t n = fmt.t == Value::Int ? fmt.i : (int64_t)fmt.n;
+      std::string b((size_t)std::max<int64_t>(n, 0), '\0');
+      const size_t got = n > 0 ? fread(&b[0], 1, (size_t)n, fp) : 0;
+      if (n > 0 && got == 0) return Value();
+      b.resize(got);
+      return Value::string(b);
+    }
+    std::string f = fmt.t == Value::Str ? *fmt.s : "l";
+    if (!f.empty() && f[0] == '*') f = f.substr(1);
+    const char c = f.empty() ? 'l' : f[0];
+    if (c == 'a') {
+      std::string b;
+      char buf[4096];
+      size_t n;
+      while ((n = fread(buf, 1, sizeof buf, fp)) > 0) b.append(buf, n);
+      return Value::string(b);
+    }
+    if (c == 'n') {
+      double d;
+      if (fscanf(fp, "%lf", &d) != 1) return Value();
+      int64_t i;
+      return float_is_int(d, &i) && std::floor(d) == d && std::fabs(d) < 9e15 ? Value::integer(i) : Value::number(d);
+    }
+    if (c == 'l' || c == 'L') {
+      std::string b;
+      int ch;
+      bool any = false;
+      while ((ch = fgetc(fp)) != EOF) {
+        any = true;
+        if (ch == '\n') {
+          if (c == 'L') b += '\n';
+          break;
+        }
+        b += (char)ch;
+      }
+      return any ? Value::string(b) : Value();
+    }
+    throw LuaError("bad argument to 'read' (invalid format)");
+  };
+  auto file_read = [fp_of, read_one](Interp&, Values& a) {
+    FILE* fp = fp_of(arg_at(a, 0), "read");
+    Values r;
+    if (a.size() <= 1) return Values{read_one(fp, Value::string("l"))};
+    for (size_t i = 1; i < a.size(); ++i) {
+      r.push_back(read_one(fp, a[i]));
+      if (r.back().t == Value::Nil) break;
+    }
+    return r;
+  };
+  auto write_to = [](Interp& I, FILE* fp, Values& a, size_t from) {
+    for (size_t i = from; i < a.size(); ++i) {
+      if (a[i].t != Value::Str && !a[i].is_num())
+        throw LuaError("bad argument #" + std::to_string(i + 1 - from) + " to 'write' (string expected)");
+      const std::string s = tostring(a[i]);
+      if (fp == stdout) I.out(s);
+      else fwrite(s.data(), 1, s.size(), fp);
+    }
+  };
+  reg(FMI, "read", file_read);
+  reg(FMI, "write", [fp_of, write_to](Interp& I, Values& a) {
+    write_to(I, fp_of(arg_at(a, 0), "write"), a, 1);
+    return Values{arg_at(a, 0)};
+  });
+  reg(FMI, "close", [fp_of](Interp&, Values& a) {
+    FILE* fp = fp_of(arg_at(a, 0), "close");
+    if (a[0].tab->get(Value::string("__std")).truthy()) return Values{Value(), Value::string("cannot close standard file")};
+    fclose(fp);
+    a[0].tab->set(Value::string("__fp"), Value::integer(0));
+    return Values{Value::boolean(true)};
+  });
+  reg(FMI, "flush", [fp_of](Interp&, Values& a) {
+    fflush(fp_of(arg_at(a, 0), "flush"));
+    return Values{arg_at(a, 0)};
+  });
+  reg(FMI, "seek", [fp_of](Interp&, Values& a) {
+    FILE* fp = fp_of(arg_at(a, 0), "seek");
+    const std::string wh = a.size() > 1 && a[1].t != Value::Nil ? check_str(a, 1, "seek") : "cur";
+    const long off = a.size() > 2 ? (long)check_int(a, 2, "seek") : 0;
+    const int w = wh == "set" ? SEEK_SET : wh == "end" ? SEEK_END : SEEK_CUR;
+    if (fseek(fp, off, w) != 0) return Values{Value(), Value::string(strerror(errno))};
+    return Values{Value::integer((int64_t)ftell(fp))};
+  });
+  auto lines_iter = [read_one](FILE* fp, bool close_at_end, Value fmt) {
+    auto st = std::make_shared<FILE*>(fp);
+    return make_native("lines_iterator", [st, close_at_end, fmt, read_one](Interp&, Values&) {
+      if (!*st) return Values{Value()};
+      Value v = read_one(*st, fmt);
+      if (v.t == Value::Nil && close_at_end) {
+        fclose(*st);
+        *st = nullptr;
+      }
+      return Values{v};
+    });
+  };
+  reg(FMI, "lines", [fp_of, lines_iter](Interp&, Values& a) {
+    return Values{lines_iter(fp_of(arg_at(a, 0), "lines"), false, a.size() > 1 ? a[1] : Value::string("l"))};
+  });
+  FM->set(Value::string("__tostring"), make_native("tostring", [](Interp&, Values& a) {
+    Value p = arg_at(a, 0).t == Value::Tab ? a[0].tab->get(Value::string("__fp")) : Value();
+    char b[64];
+    if (p.t == Value::Int && p.i) snprintf(b, sizeof b, "file (%p)", (void*)(intptr_t)p.i);
+    else snprintf(b, sizeof b, "file (closed)");
+    return Values{Value::string(b)};
+  }));
+  auto IO = std::make_shared<Table>();
+  G->set(Value::string("io"), Value::table(IO));
+  Value io_stdout = mkfile(stdout, true), io_stdin = mkfile(stdin, true), io_stderr = mkfile(stderr, true);
+  IO->set(Value::string("stdout"), io_stdout);
+  IO->set(Value::string("stdin"), io_stdin);
+  IO->set(Value::string("stderr"), io_stderr);
+  reg(IO, "write", [write_to, io_stdout](Interp& I, Values& a) {
+    write_to(I, stdout, a, 0);
+    return Values{io_stdout};
+  });
+  reg(IO, "read", [file_read, io_stdin](Interp& I, Values& a) {
+    Values b{io_stdin};
+    b.insert(b.end(), a.begin(), a.end());
+    return file_read(I, b);
+  });
+  reg(IO, "open", [mkfile](Interp&, Values& a) {
+    const std::string path = check_str(a, 0, "open");
+    const std::string mode = a.size() > 1 && a[1].t != Value::Nil ? check_str(a, 1, "open") : "r";
+    if (mode.empty() || !strchr("rwa", mode[0])) throw LuaError("bad argument #2 to 'open' (invalid mode)");
+    FILE* fp = fopen(path.c_str(), mode.c_str());
+    if (!fp) {
+      const int e = errno;
+      return Values{Value(), Value::string(path + ": " + strerror(e)), Value::integer(e)};
+    }
+    return Values{mkfile(fp, false)};
+  });
+  reg(IO, "close", [fp_of](Interp&, Values& a) {
+    FILE* fp = fp_of(arg_at(a, 0), "close");
+    fclose(fp);
+    a[0].tab->set(Value::string("__fp"), Value::integer(0));
+    return Values{Value::boolean(true)};
+  });
+  reg(IO, "lines", [lines_iter](Interp&, Values& a) {
+    if (a.empty() || a[0].t == Value::Nil) return Values{lines_iter(stdin, false, Value::string("l"))};
+    const std::string path = check_str(a, 0, "lines");
+    FILE* fp = fopen(path.c_str(), "r");
+    if (!fp) throw LuaError(path + ": " + strerror(errno));
+    return Values{lines_iter(fp, true, a.size() > 1 ? a[1] : Value::string("l"))};
+  });
+  reg(IO, "type", [](Interp&, Values& a) {
+    Value f = arg_at(a, 0);
+    if (f.t != Value::Tab) return Values{Value()};
+    Value p = f.tab->get(Value::string("__fp"));
+    if (p.t != Value::Int) return Values{Value()};
+    return Values{Value::string(p.i ? "file" : "closed file")};
+  });
+
+  // load / loadstring / dofile: compile a chunk into a vararg function of the global scope
+  auto compile = [](Interp& I, const std::string& src, const std::string& name) -> Value {
+    Parser P(src, name);
+    auto body = std::make_shared<FuncBody>();
+    body->block = P.block();
+    if (P.cur.t != T_EOF) P.err("'<eof>' expected");
+    body->vararg = true;
+    body->name = name;
+    auto f = std::make_shared<Function>();
+    f->body = body;
+    f->env = I.root;
+    f->name = name;
+    return Value::function(f);
+  };
+  auto load_fn = [compile](Interp& I, Values& a) {
+    Value c = arg_at(a, 0);
+    std::string src;
+    if (c.t == Value::Str) {
+      src = *c.s;
+    } else if (c.t == Value::Fn) {
+      for (;;) {
+        Values piece = I.call(c, {});
+        if (piece.empty() || piece[0].t == Value::Nil || (piece[0].t == Value::Str && piece[0].s->empty())) break;
+        if (piece[0].t != Value::Str) return Values{Value(), Value::string("reader function must return a string")};
+        src += *piece[0].s;
+      }
+    } else {
+      throw LuaError("bad argument #1 to 'load' (string expected)");
+    }
+    const std::string name = a.size() > 1 && a[1].t == Value::Str ? *a[1].s : "=(load)";
+    try {
+      return Values{compile(I, src, name)};
+    } catch (const LuaError& e) {
+      return Values{Value(), Value::string(e.what())};
+    }
+  };
+  reg(G, "load", load_fn);
+  reg(G, "loadstring", load_fn);
+  auto slurp = [](const std::string& path) {
+    FILE* fp = fopen(path.c_str(), "rb");
+    if (!fp) throw LuaError("cannot open " + path);
+    std::string src;
+    char buf[4096];
+    size_t n;
+    while ((n = fread(buf, 1, sizeof buf, fp)) > 0) src.append(buf, n);
+    fclose(fp);
+    if (src.rfind("#", 0) == 0) src = "--" + src;  // shebang line
+    return src;
+  };
+  reg(G, "loadfile", [compile, slurp](Interp& I, Values& a) {
+    const std::string path = check_str(a, 0, "loadfile");
+    try {
+      return Values{compile(I, slurp(path), path)};
+    } catch (const LuaError& e) {
+      return Values{Value(), Value::string(e.what())};
+    }
+  });
+  reg(G, "dofile", [compile, slurp](Interp& I, Values& a) {
+    const std::string path = check_str(a, 0, "dofile");
+    return I.call(compile(I, slurp(path), path), {});
+  });
+
+  // utf8
+  auto U = std::make_shared<Table>();
+  G->set(Value::string("utf8"), Value::table(U));
+  U->set(Value::string("charpattern"), Value::string(std::string("[\x00-\x7F\xC2-\xFD][\x80-\xBF]*", 14)));
+  auto enc = [](int64_t cp) {
+    if (cp < 0 || cp > 0x7FFFFFFF) throw LuaError("bad argument to 'char' (value out of range)");
+    std::string o;
+    if (cp < 0x80) o += (char)cp;
+    else if (cp < 0x800) { o += (char)(0xC0 | (cp >> 6)); o += (char)(0x80 | (cp & 0x3F)); }
+    else if (cp < 0x10000) { o += (char)(0xE0 | (cp >> 12)); o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F)); }
+    else { o += (char)(0xF0 | (cp >> 18)); o += (char)(0x80 | ((cp >> 12) & 0x3F)); o += (char)(0x80 | ((cp >> 6) & 0x3F)); o += (char)(0x80 | (cp & 0x3F)); }
+    return o;
+  };
+  // decode one code point at byte i (0-based); returns its length, 0 if invalid
+  auto dec = [](const std::string& s, size_t i, int64_t* cp) -> size_t {
+    const unsigned char c = (unsigned char)s[i];
+    size_t n = c < 0x80 ? 1 : (c >> 5) == 6 ? 2 : (c >> 4) == 14 ? 3 : (c >> 3) == 30 ? 4 : 0;
+    if (!n || i + n > s.size()) return 0;
+    int64_t v = n == 1 ? c : n == 2 ? (c & 0x1F) : n == 3 ? (c & 0x0F) : (c & 0x07);
+    for (size_t k = 1; k < n; ++k) {
+      const unsigned char d = (unsigned char)s[i + k];
+      if ((d & 0xC0) != 0x80) return 0;
+      v = (v << 6) | (d & 0x3F);
+    }
+    static const int64_t minv[5] = {0, 0, 0x80, 0x800, 0x10000};
+    if (v < minv[n] || v > 0x10FFFF || (v >= 0xD800 && v <= 0xDFFF)) return 0;
+    *cp = v;
+    return n;
+  };
+  reg(U, "char", [enc](Interp&, Values& a) {
+    std::string o;
+    for (size_t i = 0; i < a.size(); ++i) o += enc(check_int(a, i, "char"));
+    return Values{Value::string(o)};
+  });
+  auto posrel = [](int64_t p, size_t len) -> int64_t { return p >= 0 ? p : (int64_t)len + p + 1; };
+  reg(U, "codepoint", [dec, posrel](Interp&, Values& a) {
+    const std::string s = check_str(a, 0, "codepoint");
+    const int64_t i = posrel(a.size() > 1 && a[1].t != Value::Nil ? check_int(a, 1, "codepoint") : 1, s.size());
+    const int64_t j = posrel(a.size() > 2 && a[2].t != Value::Nil ? check_int(a, 2, "codepoint") : i, s.size());
+    if (i < 1 || j > (int64_t)s.size()) {
+      if (i > j) return Values{};
+      throw LuaError("bad argument to 'codepoint' (out of bounds)");
+    }
+    Values r;
+    for (size_t p = (size_t)i - 1; p < (size_t)j;) {
+      int64_t cp;
+      const size_t n = dec(s, p, &cp);
+      if (!n) throw LuaError("invalid UTF-8 code");
+      r.push_back(Value::integer(cp));
+      p += n;
+    }
+    return r;
+  });
+  reg(U, "len", [dec, posrel](Interp&, Values& a) {
+    const std::string s = check_str(a, 0, "len");
+    int64_t i = posrel(a.size() > 1 && a[1].t != Value::Nil ? check_int(a, 1, "len") : 1, s.size());
+    const int64_t j = posrel(a.size() > 2 && a[2].t != Value::Nil ? check_int(a, 2, "len") : -1, s.size());
+    int64_t n = 0;
+    for (size_t p = (size_t)std::max<int64_t>(i, 1) - 1; (int64_t)p < j;) {
+      int64_t cp;
+      const size_t k = dec(s, p, &cp);
+      if (!k) return Values{Value(), Value::integer((int64_t)p + 1)};
+      p += k;
+      ++n;
+    }
+    return Values{Value::integer(n)};
+  });
+  reg(U, "offset", [posrel](Interp&, Values& a) {
+    const std::string s = check_str(a, 0, "offset");
+    const int64_t n = check_int(a, 1, "offset");
+    int64_t i = a.size() > 2 && a[2].t != Value::Nil ? posrel(check_int(a, 2, "offset"), s.size())
+                                                     : (n >= 0 ? 1 : (int64_t)s.size() + 1);
+    auto cont = [&](int64_t p) { return p >= 1 && p <= (int64_t)s.size() && (((unsigned char)s[p - 1]) & 0xC0) == 0x80; };
+    if (n == 0) {
+      while (i > 1 && cont(i)) --i;
+      return Values{Value::integer(i)};
+    }
+    if (cont(i)) throw LuaError("initial position is a continuation byte");
+    int64_t k = n;
+    if (k > 0) {
+      --k;
+      while (k > 0 && i <= (int64_t)s.size()) {
+        ++i;
+        while (cont(i)) ++i;
+        --k;
+      }
+    } else {
+      while (k < 0 && i > 1) {
+        --i;
+        while (i > 1 && cont(i)) --i;
+        ++k;
+      }
+    }
+    if (k != 0) return Values{Value()};
+    return Values{Value::integer(i)};
+  });
+  reg(U, "codes", [dec](Interp&, Values& a) {
+    const std::string s = check_str(a, 0, "codes");
+    auto it = make_native("codes_iterator", [dec](Interp&, Values& b) {
+      const std::string str = *arg_at(b, 0).s;
+      int64_t p = arg_at(b, 1).t == Value::Int ? b[1].i : 0;  // 1-based position of the previous code
+      if (p > 0) {
+        int64_t cp;
+        const size_t n = dec(str, (size_t)p - 1, &cp);
+        p += n ? (int64_t)n : 1;
+      } else {
+        p = 1;
+      }
+      if (p > (int64_t)str.size()) return Values{Value()};
+      int64_t cp;
+      if (!dec(str, (size_t)p - 1, &cp)) throw LuaError("invalid UTF-8 code");
+      return Values{Value::integer(p), Value::integer(cp)};
+    });
+    return Values{it, Value::string(s), Value::integer(0)};
+  });
+
+  for (const char* lib : {"string", "table", "math", "os", "coroutine", "io", "utf8"})
+    modules[lib] = G->get(Value::string(lib));
 }
 
 Interp::~Interp() {

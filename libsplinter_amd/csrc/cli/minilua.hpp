@@ -9,16 +9,20 @@
 // method calls, string methods, integer/float arithmetic with Lua's floor
 // division and modulo, bitwise ops, concatenation, and the library subset
 // scripts use: print type tostring tonumber pairs ipairs next select error
-// assert pcall rawget rawset rawlen unpack require, string.{format len sub
-// upper lower rep byte char find reverse}, table.{insert remove concat unpack},
-// math.{floor ceil abs max min sqrt huge pi maxinteger mininteger random
-// tointeger fmod}, os.{time clock getenv}, Lua patterns (string.find / match /
-// gmatch / gsub with classes, sets, quantifiers, captures, %b, %f, back-references),
-// metatables (__index __newindex __call __tostring __name __len __unm __eq __lt __le,
-// arithmetic / bitwise / __concat events, __pairs, __metatable) and coroutines
-// (create resume yield status wrap running isyieldable close; each coroutine runs on
-// its own thread with a strict hand-off, so exactly one runs at a time).  Not
-// supported: goto, __gc / __close / __mode -- documented in docs/DIVERGENCES.md.
+// assert pcall rawget rawset rawlen unpack require load loadstring loadfile dofile,
+// string.{format (incl. %q) len sub upper lower rep byte char find match gmatch gsub reverse},
+// table.{insert remove concat unpack pack sort move}, math.{floor ceil abs max min sqrt exp log
+// sin cos tan asin acos atan modf huge pi maxinteger mininteger random randomseed tointeger fmod
+// type ult}, os.{time (incl. a date table) clock getenv date difftime remove rename tmpname
+// exit}, io.{write read lines open close type stdin stdout stderr} with file methods
+// (read l/L/n/a/count, write, lines, seek, flush, close), utf8.{char charpattern codepoint len
+// offset codes}, goto and labels, Lua patterns (string.find / match / gmatch / gsub with
+// classes, sets, quantifiers, captures, %b, %f, back-references), metatables (__index
+// __newindex __call __tostring __name __len __unm __eq __lt __le, arithmetic / bitwise /
+// __concat events, __pairs, __metatable) and coroutines (create resume yield status wrap
+// running isyieldable close; each coroutine runs on its own thread with a strict hand-off, so
+// exactly one runs at a time).  Not supported: __gc / __close / __mode, load's env argument,
+// string.pack / string.dump -- documented in docs/DIVERGENCES.md.
 #pragma once
 #include <cstdint>
 #include <functional>

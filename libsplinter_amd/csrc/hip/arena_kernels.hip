@@ -30,10 +30,11 @@ constexpr int kMaxGrid = 256 * 8;
 struct Seg {
   const int32_t* counts;
   long cap;
+  long base = 0;  // row of this launch's element 0 in the segmented buffer (a stream's slice of it)
   __device__ __forceinline__ bool live(long i) const {
     if (!counts) return true;
-    const long s = i / cap;
-    return i - s * cap < (long)counts[s];
+    const long j = i + base, s = j / cap;
+    return j - s * cap < (long)counts[s];
   }
 };
 
@@ -928,13 +929,24 @@ int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* v
   return spl_arena_set_seg(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, nullptr, 0, s);
 }
 
+static int set_seg_at(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
+                      const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats,
+                      const int32_t* seg_counts, long seg_cap, long seg_base, hipStream_t s);
+
 int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
                       const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats,
                       const int32_t* seg_counts, long seg_cap, hipStream_t s) {
+  if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
+  return set_seg_at(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg_counts, seg_cap, 0, s);
+}
+
+static int set_seg_at(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
+                      const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats,
+                      const int32_t* seg_counts, long seg_cap, long seg_base, hipStream_t s) {
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
-  if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
-  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1};
+  if (seg_counts && seg_cap <= 0) return (int)hipErrorInvalidValue;
+  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1, seg_base};
   const int mo = arena_mo();
   const int u = arena_rounds(), b = arena_block();
   static const int wt = env_int("SPLINTER_ARENA_WT", 0);  // write-through: measured slower (profiles/r1_kv_writethrough.md)
@@ -1003,13 +1015,24 @@ int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, in
   return spl_arena_get_seg(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, nullptr, 0, s);
 }
 
+static int get_seg_at(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
+                      long n, int32_t* status, int max_retry, uint64_t* stats, const int32_t* seg_counts,
+                      long seg_cap, long seg_base, hipStream_t s);
+
 int spl_arena_get_seg(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
                       long n, int32_t* status, int max_retry, uint64_t* stats, const int32_t* seg_counts,
                       long seg_cap, hipStream_t s) {
+  if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
+  return get_seg_at(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg_counts, seg_cap, 0, s);
+}
+
+static int get_seg_at(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
+                      long n, int32_t* status, int max_retry, uint64_t* stats, const int32_t* seg_counts,
+                      long seg_cap, long seg_base, hipStream_t s) {
   if (n <= 0) return 0;
   if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
-  if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
-  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1};
+  if (seg_counts && seg_cap <= 0) return (int)hipErrorInvalidValue;
+  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1, seg_base};
   const int mo = arena_mo();
   const int u = arena_rounds_get(), b = arena_block_get();
 #define SPL_GET_ROUNDS(U_, B_)                                                                                   \
@@ -1254,6 +1277,44 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
     (void)hipStreamWaitEvent(st, k->start, 0);
     int rc = spl_arena_get(a, gkeys + b * (long)kstride, kstride, gout ? gout + b * (long)ostride : nullptr, ostride,
                            glens ? glens + b : nullptr, end - b, gstatus ? gstatus + b : nullptr, max_retry, stats, st);
+    if (rc) return rc;
+    (void)hipEventRecord(k->done[k->nw + r], st);
+    (void)hipStreamWaitEvent(origin, k->done[k->nw + r], 0);
+  }
+  return (int)hipGetLastError();
+}
+
+// spl_kvs_step over routed (segmented) buffers: the owner side of a routed step (parallel/routed.py)
+// fans the received set / get segments out over the same writer / reader streams as a local step,
+// each stream a contiguous row range of the segment buffer (dead rows skipped by Seg.base).
+int spl_kvs_step_seg(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, int kstride, const uint8_t* svals,
+                     int vstride, const uint32_t* slens, long n_set, int32_t* sstatus, const int32_t* scounts,
+                     long scap, const char* gkeys, uint8_t* gout, int ostride, uint32_t* glens, long n_get,
+                     int32_t* gstatus, const int32_t* gcounts, long gcap, int max_retry, uint64_t* stats) {
+  auto* k = (KvStreams*)h;
+  if (!k || (n_set > 0 && (!scounts || scap <= 0 || n_set % scap)) || (n_get > 0 && (!gcounts || gcap <= 0 || n_get % gcap)))
+    return (int)hipErrorInvalidValue;
+  hipError_t e = hipEventRecord(k->start, origin);
+  if (e != hipSuccess) return (int)e;
+  const int nw = n_set > 0 ? k->nw : 0, nr = n_get > 0 ? k->nr : 0;
+  for (int w = 0; w < nw; ++w) {
+    const long b = n_set * w / nw, end = n_set * (w + 1) / nw;
+    if (end <= b) continue;
+    hipStream_t st = k->s[w];
+    (void)hipStreamWaitEvent(st, k->start, 0);
+    int rc = set_seg_at(a, skeys + b * (long)kstride, kstride, svals + b * (long)vstride, vstride, slens + b, end - b,
+                        sstatus + b, max_retry, stats, scounts, scap, b, st);
+    if (rc) return rc;
+    (void)hipEventRecord(k->done[w], st);
+    (void)hipStreamWaitEvent(origin, k->done[w], 0);
+  }
+  for (int r = 0; r < nr; ++r) {
+    const long b = n_get * r / nr, end = n_get * (r + 1) / nr;
+    if (end <= b) continue;
+    hipStream_t st = k->s[k->nw + r];
+    (void)hipStreamWaitEvent(st, k->start, 0);
+    int rc = get_seg_at(a, gkeys + b * (long)kstride, kstride, gout + b * (long)ostride, ostride, glens + b, end - b,
+                        gstatus + b, max_retry, stats, gcounts, gcap, b, st);
     if (rc) return rc;
     (void)hipEventRecord(k->done[k->nw + r], st);
     (void)hipStreamWaitEvent(origin, k->done[k->nw + r], 0);

@@ -15,7 +15,7 @@ from .nomic import Batch, NomicConfig, NomicEncoder, NomicWeights, random_weight
 
 class EmbedPhase:
     def __init__(self, kv_arena=None, batch: int = 512, seq: int = 512, rank: int = 0, layers: int = 12,
-                 vary: bool = False):
+                 vary: bool = False, doc_arena=None):
         self.cfg = NomicConfig(layers=layers)
         w = NomicWeights.from_numpy(self.cfg, random_weights(self.cfg, seed=rank))
         rng = np.random.default_rng(100 + rank)
@@ -25,11 +25,14 @@ class EmbedPhase:
         self.enc = NomicEncoder(w, max_tokens=self.batch.T_pad)
         self.docs_per_step = batch
         self.tokens_per_step = int(self.batch.T)
-        # documents live in their own embedding-stride arena (128-B KV slots carry no vectors)
-        self.arena = HbmArena.create(f"docs{os.getpid()}r{rank}", slots=max(2 * batch, 1024), max_val=256,
-                                     embeddings=True)
+        # documents live in an embedding-stride arena (128-B KV slots carry no vectors): the caller's
+        # (bench.py: the 25M-key search arena, so the slot lookup and the pooled writes hit a large
+        # arena) or a small one of their own
+        self.own = doc_arena is None
+        self.arena = doc_arena if doc_arena is not None else HbmArena.create(
+            f"docs{os.getpid()}r{rank}", slots=max(2 * batch, 1024), max_val=256, embeddings=True)
         K = format_keys(batch, "doc", 9, 16)
-        V, L = format_values(batch, 1, 64, 256)
+        V, L = format_values(batch, 1, 32, min(256, self.arena.max_val))
         st = self.arena.set(K, V, L)
         st_f, idx = self.arena.meta("find", K)
         torch.cuda.synchronize()
@@ -44,7 +47,8 @@ class EmbedPhase:
         return self.enc.embed(self.batch, arena=self.arena, slots=self.slots, hashes=self.hashes, out=self.out)
 
     def close(self):
-        self.arena.close()
+        if self.own:
+            self.arena.close()
 
 
 class EmbedE2E:

@@ -148,6 +148,28 @@ class RoutedKV:
                                                                       **kw)
         op.touch()
 
+    def execute_fanout(self, sop: Optional[RoutedOp], gop: Optional[RoutedOp], kvs) -> None:
+        """Owner kernels of a set and a get batch fanned out over ``kvs``'s writer / reader streams
+        (ops/arena.py KvStreams.step_seg): the routed step runs the same client-stream configuration as
+        a local step, each stream a slice of the received segments."""
+        sargs = gargs = None
+        if sop is not None:
+            t = sop.t
+            t["rstatus"] = torch.empty(t["krecv"].shape[0], dtype=torch.int32, device=t["krecv"].device)
+            sargs = (t["krecv"], t["vrecv"], t["lrecv"], t["rcounts"], sop.cap, t["rstatus"])
+        if gop is not None:
+            t = gop.t
+            n = t["krecv"].shape[0]
+            dev = t["krecv"].device
+            t["rvals"] = torch.empty((n, gop.width), dtype=torch.uint8, device=dev)
+            t["rlens"] = torch.empty(n, dtype=torch.int32, device=dev)
+            t["rstatus"] = torch.empty(n, dtype=torch.int32, device=dev)
+            gargs = (t["krecv"], t["rcounts"], gop.cap, t["rvals"], t["rlens"], t["rstatus"])
+        kvs.step_seg(self.local.arena, sargs, gargs)
+        for op in (sop, gop):
+            if op is not None:
+                op.touch()
+
     def respond(self, op: RoutedOp) -> None:
         t = op.t
         b = torch.empty_like(t["rstatus"])

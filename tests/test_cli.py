@@ -144,7 +144,7 @@ def test_lua_verb_splinter_module(store):
     assert rc != 0
 
 
-@pytest.mark.parametrize("script", ["lua_patterns_meta.lua", "lua_coroutines.lua"])
+@pytest.mark.parametrize("script", ["lua_patterns_meta.lua", "lua_coroutines.lua", "lua_stdlib.lua"])
 def test_lua_patterns_metatables_coroutines(store, script):
     """Lua 5.4 semantics the reference gets from liblua5.4: string patterns (find / match / gmatch /
     gsub), metatables and metamethods, coroutines -- each script asserts its expected values."""

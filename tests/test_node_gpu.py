@@ -157,3 +157,17 @@ def test_dp_splinference_cli_on_node(hbm_node):
         v = s.get_embedding(f"x{i}")
         has = v is not None and float(np.linalg.norm(v)) > 0
         assert has == (f"x{i}" in mine), (i, has)
+
+
+@pytest.mark.parametrize("prefix,shards", [("hbm:", None), ("node:", "2")], ids=["hbm", "node_hbm"])
+def test_native_tap_suite_on_hbm(prefix, shards):
+    """The reference-parity TAP suite (tools/splinter_test.cpp, mirroring the reference
+    splinter_test.c) on an HBM arena and on a node store of HBM shards, through the C ABI."""
+    exe = os.path.join(ROOT, "libsplinter_amd", "bin", "splinter_test")
+    env = dict(os.environ, SPLINTER_TEST_PREFIX=prefix, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    if shards:
+        env.update(SPLINTER_NODE_BACKEND="hbm", SPLINTER_NODE_SHARDS=shards)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300, env=env)
+    fails = [ln for ln in r.stdout.splitlines() if ln.startswith("not ok")]
+    print(r.stdout[-400:])
+    assert r.returncode == 0 and not fails, (fails, r.stderr[-2000:])

@@ -21,6 +21,17 @@ def test_native_tap_suite():
     assert "not ok" not in r.stdout
 
 
+def test_native_tap_suite_on_node_store_of_shm_shards():
+    """The same 134-check suite through a node store ("node:", 8 shm shards): routing, replicated
+    mop / label map, summed signal counts, merged list / enumerate, node-wide shard bids and the node
+    event bus, against the reference semantics (the per-arena capacity checks are skipped)."""
+    exe = os.path.join(ROOT, "libsplinter_amd", "bin", "splinter_test")
+    env = dict(os.environ, SPLINTER_TEST_PREFIX="node:", SPLINTER_NODE_BACKEND="shm", SPLINTER_NODE_SHARDS="8")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120, env=env)
+    assert r.returncode == 0, r.stdout[-3000:]
+    assert "not ok" not in r.stdout and "# passed 130/130" in r.stdout, r.stdout[-500:]
+
+
 @pytest.fixture
 def store(uniq):
     s = Store.create(uniq, slots=512, max_val=1024, embeddings=True)

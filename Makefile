@@ -48,6 +48,7 @@ build/hip/%.o: $(SRC)/hip/%.hip $(HIP_HDRS) | build/hip
 # K/V tile around the online-softmax rescale); per file: the flag crashes the compiler on
 # search_kernels.hip (ROCm 7.2)
 build/hip/nomic_kernels.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans
+build/hip/decoder_kernels.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 
 $(LIB)/libsplinter_hip.so: $(HIP_OBJS) $(LIB)/libsplinter.so | $(LIB)
 	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
@@ -57,7 +58,7 @@ $(LIB)/libsplinter_hip.so: $(HIP_OBJS) $(LIB)/libsplinter.so | $(LIB)
 hip-variant: $(LIB)/libsplinter.so | $(LIB)
 	mkdir -p build/hip_$(V)
 	for f in $(HIP_SRCS); do o=build/hip_$(V)/$$(basename $$f .hip).o; x=""; \
-	  case $$f in *nomic_kernels.hip) x="-mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans";; esac; \
+	  case $$f in *nomic_kernels.hip) x="-mllvm -amdgpu-mfma-vgpr-form -fno-honor-nans";; *decoder_kernels.hip) x="-mllvm -amdgpu-mfma-vgpr-form";; esac; \
 	  $(HIPCC) $(HIPFLAGS) $$x $(VFLAGS) -c -o $$o $$f || exit 1; done
 	$(HIPCC) $(HIPFLAGS) -shared -o $(LIB)/libsplinter_hip_$(V).so build/hip_$(V)/*.o -L$(LIB) -lsplinter \
 	  -Wl,-rpath,'$$ORIGIN' $(LDLIBS)

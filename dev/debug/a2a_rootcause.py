@@ -8,7 +8,7 @@ Questions the round-1 verdict asked:
   * does gloo on the same host buffers agree (the reference result)?
 
 One GPU, world 1 (RCCL's self-send path, as the round-1 evidence):
-  python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 scripts/a2a_rootcause.py
+  python -m torch.distributed.run --nproc-per-node 1 --master-addr 127.0.0.1 dev/debug/a2a_rootcause.py
 Prints one JSON line per case.
 """
 import json

@@ -515,7 +515,18 @@ __device__ __forceinline__ float q4dot8(uint32_t w, const float* x) {
 constexpr int kGemvQ4MaxK = 16384;
 constexpr int kQ4Rec = kQ4Group + 4;  // LDS floats per group record
 
-template <int MODE, bool RMS, int R = kGemvRows>
+// 8-bit bytes -> floats, one v_cvt_f32_ubyteN each (Q8G32: k = 4j .. 4j+3 in dword j)
+__device__ __forceinline__ float q8dot4(uint32_t w, const float* x) {
+  float s = (float)(w & 0xff) * x[0];
+  s = fmaf((float)((w >> 8) & 0xff), x[1], s);
+  s = fmaf((float)((w >> 16) & 0xff), x[2], s);
+  return fmaf((float)(w >> 24), x[3], s);
+}
+
+// BITS 4: Q4G32 nibbles (16 B per group); BITS 8: Q8G32 bytes (32 B per group, the same (d, m)
+// words: w = d * u + m with u in 0..255) -- the >4-bit GGUF tensors (Q6_K / Q5_x / Q8_0 / F16) of a
+// mostly-4-bit file keep >= 6 bits instead of being re-gridded to 4
+template <int MODE, bool RMS, int R = kGemvRows, int BITS = 4>
 __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x, const float* __restrict__ rw,
                                                  float eps, const uint8_t* __restrict__ Wq,
                                                  const uint32_t* __restrict__ Wsm, int K, int nout,
@@ -539,13 +550,15 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
     if (o >= nout) o = nout - 1;  // tail: recompute the last output, never stored twice
     rows[r] = MODE == 2 ? (long)(32 * (o / 16) + (o % 16) + (r & 1) * 16) : (long)o;
   }
-  const long qrow = K / 2;
-  uint4 wq[R];
+  constexpr int GV = BITS / 4;  // 16-B loads per group and row
+  const long qrow = (long)K * BITS / 8;
+  uint4 wq[R][GV];
   uint32_t sm[R];
   if (active && lane < ng) {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      wq[r] = *(const uint4*)(Wq + rows[r] * qrow + lane * 16);
+#pragma unroll
+      for (int v = 0; v < GV; ++v) wq[r][v] = *(const uint4*)(Wq + rows[r] * qrow + lane * 16 * GV + v * 16);
       sm[r] = Wsm[rows[r] * ng + lane];
     }
   }
@@ -594,14 +607,19 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
   for (int g = lane; g < ng; g += 64) {
     // the group's weights are in registers; request the next group's before the math (one group
     // of look-ahead per lane: 2 x 4 x 20 B in flight)
-    uint4 cq[R];
+    uint4 cq[R][GV];
     uint32_t csm[R];
 #pragma unroll
-    for (int r = 0; r < R; ++r) { cq[r] = wq[r]; csm[r] = sm[r]; }
+    for (int r = 0; r < R; ++r) {
+#pragma unroll
+      for (int v = 0; v < GV; ++v) cq[r][v] = wq[r][v];
+      csm[r] = sm[r];
+    }
     if (g + 64 < ng) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        wq[r] = *(const uint4*)(Wq + rows[r] * qrow + (g + 64) * 16);
+#pragma unroll
+        for (int v = 0; v < GV; ++v) wq[r][v] = *(const uint4*)(Wq + rows[r] * qrow + (g + 64) * 16 * GV + v * 16);
         sm[r] = Wsm[rows[r] * ng + g + 64];
       }
     }
@@ -611,10 +629,22 @@ __global__ __launch_bounds__(256) void k_gemv_q4(const uint16_t* __restrict__ x,
     const float gs = xs[g * kQ4Rec + kQ4Group];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      float dot = q4dot8(cq[r].x, xg);
-      dot += q4dot8(cq[r].y, xg + 8);
-      dot += q4dot8(cq[r].z, xg + 16);
-      dot += q4dot8(cq[r].w, xg + 24);
+      float dot;
+      if constexpr (BITS == 4) {
+        dot = q4dot8(cq[r][0].x, xg);
+        dot += q4dot8(cq[r][0].y, xg + 8);
+        dot += q4dot8(cq[r][0].z, xg + 16);
+        dot += q4dot8(cq[r][0].w, xg + 24);
+      } else {
+        dot = q8dot4(cq[r][0].x, xg);
+        dot += q8dot4(cq[r][0].y, xg + 4);
+        dot += q8dot4(cq[r][0].z, xg + 8);
+        dot += q8dot4(cq[r][0].w, xg + 12);
+        dot += q8dot4(cq[r][GV - 1].x, xg + 16);
+        dot += q8dot4(cq[r][GV - 1].y, xg + 20);
+        dot += q8dot4(cq[r][GV - 1].z, xg + 24);
+        dot += q8dot4(cq[r][GV - 1].w, xg + 28);
+      }
       acc[r] = fmaf(bf2f(csm[r] & 0xffff), dot, fmaf(bf2f(csm[r] >> 16), gs, acc[r]));
     }
   }
@@ -686,6 +716,53 @@ __global__ void k_q4_dequant(const uint8_t* __restrict__ Wq, const uint32_t* __r
     float f[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) f[e] = fmaf(d, (float)((qw[c] >> (4 * e)) & 15u), m);
+    dst[c] = pack8(f);
+  }
+}
+
+// bf16 W [N, K] <-> Q8G32 (one thread per 32-weight group): affine 255-step grid over the group's
+// [min, max], (d, m) rounded to bf16 first and the bytes chosen against the rounded pair
+__global__ void k_q8_quant(const uint16_t* __restrict__ W, long groups, uint8_t* __restrict__ Wq,
+                           uint32_t* __restrict__ Wsm) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= groups) return;
+  float v[kQ4Group];
+  const uint4* src = (const uint4*)(W + i * kQ4Group);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) unpack8(src[c], v + c * 8);
+  float lo = v[0], hi = v[0];
+#pragma unroll
+  for (int e = 1; e < kQ4Group; ++e) { lo = fminf(lo, v[e]); hi = fmaxf(hi, v[e]); }
+  const float m = (float)(__bf16)lo;
+  float d = (float)(__bf16)((hi - m) / 255.f);
+  if (!(d > 0.f)) d = 0.f;
+  const float inv = d > 0.f ? 1.f / d : 0.f;
+  uint32_t packed[8] = {};
+#pragma unroll
+  for (int e = 0; e < kQ4Group; ++e) {
+    int q = (int)rintf((v[e] - m) * inv);
+    q = q < 0 ? 0 : (q > 255 ? 255 : q);
+    packed[e >> 2] |= (uint32_t)q << (8 * (e & 3));
+  }
+  *(uint4*)(Wq + i * 32) = make_uint4(packed[0], packed[1], packed[2], packed[3]);
+  *(uint4*)(Wq + i * 32 + 16) = make_uint4(packed[4], packed[5], packed[6], packed[7]);
+  Wsm[i] = pk2(d, m);
+}
+
+__global__ void k_q8_dequant(const uint8_t* __restrict__ Wq, const uint32_t* __restrict__ Wsm, long groups,
+                             uint16_t* __restrict__ W) {
+  const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= groups) return;
+  const uint4 a = *(const uint4*)(Wq + i * 32), b = *(const uint4*)(Wq + i * 32 + 16);
+  const uint32_t sm = Wsm[i];
+  const float d = bf2f(sm & 0xffff), m = bf2f(sm >> 16);
+  const uint32_t qw[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+  uint4* dst = (uint4*)(W + i * kQ4Group);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    float f[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) f[e] = fmaf(d, (float)((qw[2 * c + (e >> 2)] >> (8 * (e & 3))) & 255u), m);
     dst[c] = pack8(f);
   }
 }
@@ -1245,9 +1322,237 @@ __global__ __launch_bounds__(kSbBins) void k_sb_draw(const float* __restrict__ l
   }
 }
 
+// ------------------------------------------------------- prefill attention over the KV cache --
+// Causal grouped-query attention of a prompt chunk of n tokens at absolute positions pos0 ..
+// pos0+n-1 against the KV cache rows 0 .. pos0+n-1 (the chunk's own k/v already appended): the
+// first prompt (pos0 = 0) and every continuation (a new turn over a live cache) alike, for head
+// dims 64 and 128 (llama 1B-class and 7B-class).  One 256-thread workgroup = 128 query rows of
+// one q head, 4 waves x 2 16-row q-blocks; per 64-key tile (LDS double buffer, register-staged
+// one tile ahead):
+//   S^T = K Q^T    mfma_f32_16x16x32_bf16 with the K rows as the A operand, so one query's
+//                  scores sit in one lane column and the softmax statistics reduce in-lane plus
+//                  two permlane swaps;
+//   O^T += V^T P^T the rounded probabilities are the B operand as they lie; V^T fragments come
+//                  from the row-major V tile through ds_read_b64_tr_b16.
+// The K tile's 16-B chunks are XOR-swizzled by the key (mod HD/8 chunks) so a 16-lane group's
+// b128 reads of 16 key rows cover all 64 banks; V chunks swap bits 1..2 by key pair for the
+// transposing reads.  Grid: nqb * heads blocks through the bijective XCD remap, so the q-blocks
+// of one head (which stream the same K/V) share one XCD's L2.
+typedef __bf16 pa_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float pa_f32x4 __attribute__((ext_vector_type(4)));
+typedef float pa_f32x2 __attribute__((ext_vector_type(2)));
+typedef short pa_v4i16 __attribute__((ext_vector_type(4)));
+typedef short pa_v8i16 __attribute__((ext_vector_type(8)));
+typedef __attribute__((address_space(3))) pa_v4i16 pa_lds_v4i16;
+
+__device__ __forceinline__ float pa_xg_max(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+}
+__device__ __forceinline__ float pa_xg_sum(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(q[0]) + __uint_as_float(q[1]);
+}
+
+template <int HD>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) void k_prefill_attn(const uint16_t* __restrict__ qg, long ldq,
+                                                      const uint16_t* __restrict__ kc,
+                                                      const uint16_t* __restrict__ vc, long ldkv, int n, int pos0,
+                                                      int heads, int kv_heads, float scale_log2,
+                                                      uint16_t* __restrict__ out, long ldo) {
+  constexpr int KT = HD == 128 ? 32 : 64, RB = HD * 2, NCH = HD / 8, NKK = HD / 32, NDB = HD / 16, NL = KT * NCH / 256;
+  __shared__ __attribute__((aligned(16))) char lds[2][2][KT * RB];  // [buf][K | V][key * RB]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
+  const int nwg = gridDim.x, orig = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int nqb = nwg / heads, head = lid / nqb, qstart = (lid - head * nqb) * 128;
+  const int kvhead = head / (heads / kv_heads);
+  const long lenk = (long)pos0 + n;
+  auto ksw = [](int key, int c) { return c ^ (key & (NCH - 1)); };
+  auto vsw = [](int key, int c) { return c ^ (((key >> 1) & 3) << 1); };
+
+  pa_bf16x8 qf[2][NKK];
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrow = qstart + wave * 32 + qb * 16 + li;
+#pragma unroll
+    for (int kk = 0; kk < NKK; ++kk)
+      qf[qb][kk] = qrow < n ? *(const pa_bf16x8*)(qg + (long)qrow * ldq + head * HD + kk * 32 + g * 8) : pa_bf16x8{};
+  }
+  pa_f32x4 o[NDB][2];
+#pragma unroll
+  for (int db = 0; db < NDB; ++db)
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) o[db][qb] = pa_f32x4{0.f, 0.f, 0.f, 0.f};
+  float m[2] = {-1e30f, -1e30f}, l[2] = {0.f, 0.f};
+
+  uint4 rk[NL], rv[NL];
+  const uint16_t* kp = kc + (long)kvhead * HD;
+  const uint16_t* vp = vc + (long)kvhead * HD;
+  auto gload = [&](long k0) {
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int c = tid + it * 256, key = c / NCH, ch = c % NCH;
+      if (k0 + key < lenk) {
+        rk[it] = *(const uint4*)(kp + (k0 + key) * ldkv + ch * 8);
+        rv[it] = *(const uint4*)(vp + (k0 + key) * ldkv + ch * 8);
+      } else {
+        rk[it] = make_uint4(0, 0, 0, 0);
+        rv[it] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lwrite = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int c = tid + it * 256, key = c / NCH, ch = c % NCH;
+      *(uint4*)(lds[buf][0] + key * RB + (ksw(key, ch) << 4)) = rk[it];
+      *(uint4*)(lds[buf][1] + key * RB + (vsw(key, ch) << 4)) = rv[it];
+    }
+  };
+
+  // causal: the block's last query (absolute pos0 + qstart + 127) bounds the key tiles
+  const int ntiles = (int)min((lenk + KT - 1) / KT, ((long)pos0 + qstart + 128 + KT - 1) / KT);
+  gload(0);
+  lwrite(0);
+  __syncthreads();
+  const int tq = li >> 2, tp = li & 3;
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const long k0 = (long)t * KT;
+    if (t + 1 < ntiles) gload(k0 + KT);
+    const char* Ks = lds[buf][0];
+    const char* Vs = lds[buf][1];
+    pa_f32x4 s[KT / 16][2];
+#pragma unroll
+    for (int kb = 0; kb < KT / 16; ++kb) {
+      const int row = kb * 16 + li;
+      pa_bf16x8 kf[NKK];
+#pragma unroll
+      for (int kk = 0; kk < NKK; ++kk) kf[kk] = *(const pa_bf16x8*)(Ks + row * RB + (ksw(row, kk * 4 + g) << 4));
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb) {
+        s[kb][qb] = pa_f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kk = 0; kk < NKK; ++kk)
+          s[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[qb][kk], s[kb][qb], 0, 0, 0);
+      }
+    }
+    // online softmax with the deferred rescale (max moves only past a 2^8 margin); keys after a
+    // query's absolute position are masked on the diagonal tiles, which also covers the keys
+    // past the cache length for every stored row
+    constexpr float kThr = 8.f;
+    const bool diag = k0 + KT - 1 > (long)pos0 + qstart + wave * 32;
+#pragma unroll
+    for (int qb = 0; qb < 2; ++qb) {
+      if (diag) {
+        const long qabs = (long)pos0 + qstart + wave * 32 + qb * 16 + li;
+#pragma unroll
+        for (int kb = 0; kb < KT / 16; ++kb)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (k0 + kb * 16 + 4 * g + r > qabs) s[kb][qb][r] = -1e30f;
+      }
+      float mx = -1e30f;
+#pragma unroll
+      for (int kb = 0; kb < KT / 16; ++kb)
+        mx = fmaxf(fmaxf(mx, fmaxf(s[kb][qb][0], s[kb][qb][1])), fmaxf(s[kb][qb][2], s[kb][qb][3]));
+      const float mxs = pa_xg_max(mx) * scale_log2;
+      if (!__all(mxs - m[qb] <= kThr)) {
+        const float mn = fmaxf(m[qb], mxs);
+        const float alpha = __builtin_amdgcn_exp2f(m[qb] - mn);
+        m[qb] = mn;
+        l[qb] *= alpha;
+#pragma unroll
+        for (int db = 0; db < NDB; ++db) o[db][qb] *= alpha;
+      }
+      const pa_f32x2 sc2 = {scale_log2, scale_log2}, nm2 = {-m[qb], -m[qb]};
+      pa_f32x2 acc2 = {0.f, 0.f};
+#pragma unroll
+      for (int kb = 0; kb < KT / 16; ++kb)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          pa_f32x2 x = {s[kb][qb][2 * h], s[kb][qb][2 * h + 1]};
+          x = x * sc2 + nm2;
+          x.x = __builtin_amdgcn_exp2f(x.x);
+          x.y = __builtin_amdgcn_exp2f(x.y);
+          s[kb][qb][2 * h] = x.x;
+          s[kb][qb][2 * h + 1] = x.y;
+          acc2 += x;
+        }
+      l[qb] += pa_xg_sum(acc2.x + acc2.y);
+    }
+#pragma unroll
+    for (int st = 0; st < KT / 32; ++st) {
+      pa_bf16x8 pf[2];
+#pragma unroll
+      for (int qb = 0; qb < 2; ++qb)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          pf[qb][j] = (__bf16)s[2 * st][qb][j];
+          pf[qb][4 + j] = (__bf16)s[2 * st + 1][qb][j];
+        }
+      const int row1 = st * 32 + 4 * g + tq, row2 = row1 + 16;
+#pragma unroll
+      for (int db = 0; db < NDB; ++db) {
+        const int ch = db * 2 + (tp >> 1);
+        const pa_v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (pa_lds_v4i16*)(Vs + row1 * RB + (vsw(row1, ch) << 4) + 8 * (tp & 1)));
+        const pa_v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+            (pa_lds_v4i16*)(Vs + row2 * RB + (vsw(row2, ch) << 4) + 8 * (tp & 1)));
+        const pa_bf16x8 vf = __builtin_bit_cast(pa_bf16x8, (pa_v8i16)__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb)
+          o[db][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qb], o[db][qb], 0, 0, 0);
+      }
+    }
+    if (t + 1 < ntiles) lwrite(buf ^ 1);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int qb = 0; qb < 2; ++qb) {
+    const int qrow = qstart + wave * 32 + qb * 16 + li;
+    if (qrow >= n) continue;
+    const float inv = 1.f / l[qb];
+    uint16_t* dst = out + (long)qrow * ldo + head * HD + 4 * g;
+#pragma unroll
+    for (int db = 0; db < NDB; ++db) {
+      uint2 w;
+      w.x = pk2(o[db][qb][0] * inv, o[db][qb][1] * inv);
+      w.y = pk2(o[db][qb][2] * inv, o[db][qb][3] * inv);
+      *(uint2*)(dst + db * 16) = w;
+    }
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// Causal prefill attention over the KV cache (k_prefill_attn): q rows [n, ldq] (H heads x hd,
+// RoPE applied), k / v cache rows [pos0 + n, ldkv] (KVH heads x hd; rows pos0 .. pos0+n-1 are
+// this chunk's), out rows [n, ldo].  hd 64 or 128; rows and bases 16-B aligned.
+int dec_attn_prefill_kv(const void* q, long ldq, const void* k, const void* v, long ldkv, int n, int pos0, int H,
+                        int KVH, int hd, float scale, void* out, long ldo, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (pos0 < 0 || H <= 0 || KVH <= 0 || H % KVH || (hd != 64 && hd != 128) || ldq % 8 || ldkv % 8 || ldo % 8 ||
+      ldq < (long)H * hd || ldkv < (long)KVH * hd || ldo < (long)H * hd ||
+      ((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)out) & 15)
+    return (int)hipErrorInvalidValue;
+  const int nqb = (n + 127) / 128;
+  const float sl2 = scale * 1.4426950408889634f;
+  if (hd == 64)
+    hipLaunchKernelGGL(k_prefill_attn<64>, dim3(nqb * H), dim3(256), 0, s, (const uint16_t*)q, ldq,
+                       (const uint16_t*)k, (const uint16_t*)v, ldkv, n, pos0, H, KVH, sl2, (uint16_t*)out, ldo);
+  else
+    hipLaunchKernelGGL(k_prefill_attn<128>, dim3(nqb * H), dim3(256), 0, s, (const uint16_t*)q, ldq,
+                       (const uint16_t*)k, (const uint16_t*)v, ldkv, n, pos0, H, KVH, sl2, (uint16_t*)out, ldo);
+  return (int)hipGetLastError();
+}
 
 // q: bf16 [H*hd] (one token, RoPE applied); k/v: bf16 cache rows [L, ldkv] (ldkv = KVH*hd);
 // out: bf16 [H*hd].  hd in {64, 128, 192, 256}, H % KVH == 0, L >= 1, 16-B aligned rows.
@@ -1389,8 +1694,11 @@ int dec_gemv(int mode, const void* x, const float* rms_w, float eps, const void*
 
 // dec_gemv over Q4G32 weights (k_gemv_q4): Wq [N, K/2] nibbles, Wsm [N, K/32] bf16 (d, m) pairs.
 // K % 32 == 0, K <= 16384, 16-B aligned x / Wq, 4-B aligned Wsm.
-int dec_gemv_q4(int mode, const void* x, const float* rms_w, float eps, const void* Wq, const void* Wsm, int N,
-                int K, const void* res, void* out, hipStream_t s) {
+}  // extern "C"
+
+template <int BITS>
+static int gemv_qn(int mode, const void* x, const float* rms_w, float eps, const void* Wq, const void* Wsm, int N,
+                   int K, const void* res, void* out, hipStream_t s) {
   if (K <= 0 || K % kQ4Group || K > kGemvQ4MaxK || N <= 0 || (mode == 2 && N % 32) || (mode == 1 && !res) ||
       ((uintptr_t)Wq | (uintptr_t)x) % 16 || (uintptr_t)Wsm % 4 || (rms_w && (uintptr_t)rms_w % 16))
     return (int)hipErrorInvalidValue;
@@ -1408,8 +1716,8 @@ int dec_gemv_q4(int mode, const void* x, const float* rms_w, float eps, const vo
   const uint32_t* wsm = (const uint32_t*)Wsm;
 #define GEMV(M_, R_)                                                                                           \
   do {                                                                                                         \
-    if (R == 8) hipLaunchKernelGGL((k_gemv_q4<M_, R_, 8>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out); \
-    else hipLaunchKernelGGL((k_gemv_q4<M_, R_, 4>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out);      \
+    if (R == 8) hipLaunchKernelGGL((k_gemv_q4<M_, R_, 8, BITS>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out); \
+    else hipLaunchKernelGGL((k_gemv_q4<M_, R_, 4, BITS>), g, b, lds, s, xx, rms_w, eps, wq, wsm, K, nout, rr, out);      \
   } while (0)
   const bool rms = rms_w != nullptr;
   switch (mode) {
@@ -1420,6 +1728,38 @@ int dec_gemv_q4(int mode, const void* x, const float* rms_w, float eps, const vo
     default: return (int)hipErrorInvalidValue;
   }
 #undef GEMV
+  return (int)hipGetLastError();
+}
+
+extern "C" {
+
+int dec_gemv_q4(int mode, const void* x, const float* rms_w, float eps, const void* Wq, const void* Wsm, int N,
+                int K, const void* res, void* out, hipStream_t s) {
+  return gemv_qn<4>(mode, x, rms_w, eps, Wq, Wsm, N, K, res, out, s);
+}
+
+// dec_gemv over Q8G32 weights: Wq [N, K] bytes, Wsm [N, K/32] bf16 (d, m) pairs, w = d u + m
+int dec_gemv_q8(int mode, const void* x, const float* rms_w, float eps, const void* Wq, const void* Wsm, int N,
+                int K, const void* res, void* out, hipStream_t s) {
+  return gemv_qn<8>(mode, x, rms_w, eps, Wq, Wsm, N, K, res, out, s);
+}
+
+// bf16 W [N, K] (row-major, contiguous) <-> Q8G32 planes
+int dec_q8_quantize(const void* W, long N, int K, void* Wq, void* Wsm, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % kQ4Group || ((uintptr_t)W | (uintptr_t)Wq) % 16 || (uintptr_t)Wsm % 4)
+    return (int)hipErrorInvalidValue;
+  const long groups = N * (K / kQ4Group);
+  hipLaunchKernelGGL(k_q8_quant, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, (const uint16_t*)W, groups,
+                     (uint8_t*)Wq, (uint32_t*)Wsm);
+  return (int)hipGetLastError();
+}
+
+int dec_q8_dequant(const void* Wq, const void* Wsm, long N, int K, void* W, hipStream_t s) {
+  if (N <= 0 || K <= 0 || K % kQ4Group || ((uintptr_t)W | (uintptr_t)Wq) % 16 || (uintptr_t)Wsm % 4)
+    return (int)hipErrorInvalidValue;
+  const long groups = N * (K / kQ4Group);
+  hipLaunchKernelGGL(k_q8_dequant, dim3((unsigned)((groups + 255) / 256)), dim3(256), 0, s, (const uint8_t*)Wq,
+                     (const uint32_t*)Wsm, groups, (uint16_t*)W);
   return (int)hipGetLastError();
 }
 

@@ -3,7 +3,7 @@
 // hipIpcGetMemHandle / hipIpcOpenMemHandle on one hipMalloc allocation is the obvious way to
 // expose an arena to other processes ("cross-process GPU sharing"), but on the
 // MI355X hosts (dmabuf IPC only, HSA_ENABLE_IPC_MODE_LEGACY=0) the import of an allocation past
-// ~2 GiB never returns: 1.95 GiB attached in 0.15 s, 3.04 GiB hung (scripts/ipc_open_debug.py,
+// ~2 GiB never returns: 1.95 GiB attached in 0.15 s, 3.04 GiB hung (dev/debug/ipc_open_debug.py,
 // gpurun_out/r2_31).  A 100M-key arena is ~70 GiB.  So the owner builds the arena from physical
 // chunks (hipMemCreate, SPLINTER_HBM_CHUNK_MB, default 1024) mapped back to back into one
 // reserved virtual range -- the kernels see one flat arena as before -- and exports every chunk

@@ -182,7 +182,7 @@ class Splainference:
                 break
             if eng is None:
                 t = self.sampler(logits)
-            if t == self.tok.eos_id:
+            if self.tok.is_eog(t):  # EOS / EOT / end-of-turn (llama_vocab_is_eog, reference :310)
                 break
             piece = self.tok.piece(t)
             chunk += piece

@@ -13,11 +13,12 @@ the MI355X replacement, demo-grade as SURVEY §2.1 N8 scopes it:
   fused epilogues; RMSNorm and RoPE (llama "normal" adjacent-pair rotation, as
   llama.cpp applies for arch llama, in place on the q|k GEMM output) are the
   HIP kernels of ``csrc/hip/decoder_kernels.hip``, and so is the per-token
-  decode attention over the KV cache (``dec_attn_decode``); prompt prefill
-  attention and the sampler use torch ops on the same device -- the decode
-  step is latency-bound and not a benchmark path;
-* tokenizer: greedy longest-match over the GGUF vocabulary (SentencePiece
-  "▁" spaces, <0xNN> byte fallback) or, for random init, bytes 0..255 + BOS/EOS.
+  decode attention over the KV cache (``dec_attn_decode``), the causal prefill
+  attention of a fresh or continued prompt over the cache (``dec_attn_prefill_kv``,
+  head dim 64 / 128) and the nucleus sampler (``dec_sample``);
+* tokenizer: the GGUF's own -- SentencePiece score merging (model "llama") or
+  byte-level BPE over the merges (model "gpt2"), models/llm_tokenizer.py -- or,
+  for random init, bytes 0..255 + BOS/EOS.
 
 On a host without a GPU the same module runs entirely in torch on the CPU
 (``device="cpu"``) so the daemon's label state machine is testable anywhere;
@@ -63,53 +64,15 @@ class ByteTokenizer:
     def piece(self, tok: int) -> bytes:
         return bytes([tok]) if tok < 256 else b""
 
+    def is_eog(self, tok: int) -> bool:
+        return tok == self.eos_id
+
     def printable_mask(self, vocab: int) -> torch.Tensor:
         m = torch.zeros(vocab, dtype=torch.bool)
         m[32:127] = True
         m[10] = True
         m[self.eos_id] = True
         return m
-
-
-class VocabTokenizer:
-    """Greedy longest-match over a GGUF vocabulary (SentencePiece conventions)."""
-
-    def __init__(self, tokens: List[str], bos: int, eos: int):
-        self.tokens = tokens
-        self.bos_id, self.eos_id = bos, eos
-        self.index: Dict[str, int] = {t: i for i, t in enumerate(tokens)}
-        self.maxlen = max((len(t) for t in tokens), default=1)
-        self.byte_ids = {b: self.index.get(f"<0x{b:02X}>") for b in range(256)}
-
-    def encode(self, text: str, add_bos: bool = True) -> List[int]:
-        s = "▁" + text.replace(" ", "▁")
-        out = [self.bos_id] if add_bos else []
-        i = 0
-        while i < len(s):
-            for L in range(min(self.maxlen, len(s) - i), 0, -1):
-                t = self.index.get(s[i:i + L])
-                if t is not None:
-                    out.append(t)
-                    i += L
-                    break
-            else:
-                for b in s[i].encode("utf-8"):
-                    bid = self.byte_ids.get(b)
-                    if bid is not None:
-                        out.append(bid)
-                i += 1
-        return out
-
-    def piece(self, tok: int) -> bytes:
-        t = self.tokens[tok] if 0 <= tok < len(self.tokens) else ""
-        if len(t) == 6 and t.startswith("<0x") and t.endswith(">"):
-            return bytes([int(t[3:5], 16)])
-        if t.startswith("<") and t.endswith(">"):
-            return b""
-        return t.replace("▁", " ").encode("utf-8")
-
-    def printable_mask(self, vocab: int) -> Optional[torch.Tensor]:
-        return None
 
 
 def random_decoder_weights(cfg: DecoderConfig, seed: int = 0, std: float = 0.02) -> Dict[str, np.ndarray]:
@@ -184,12 +147,51 @@ class Q4Weight:
     def nbytes(self) -> int:
         return self.q.numel() + self.sm.numel() * 4
 
+    bits = 4
+
+
+class Q8Weight(Q4Weight):
+    """Q8G32: one byte per weight (u in 0..255) and the same bf16 (d, m) pair per 32-k group,
+    w = d u + m; 1.125 B per weight.  Holds the tensors a mostly-4-bit GGUF keeps at more than 4
+    bits (a Q4_K_M file's Q6_K attn_v / ffn_down / output), so they are not re-gridded below the
+    file's precision.  Decode reads it with dec_gemv_q8, prefill dequantises with dec_q8_dequant."""
+    bits = 8
+
+    def __init__(self, q: torch.Tensor, sm: torch.Tensor):
+        self.q, self.sm = q, sm
+        self.shape = (q.shape[0], q.shape[1])
+
+    @classmethod
+    def quantize(cls, L, w: torch.Tensor) -> "Q8Weight":
+        from .nomic import _chk, _stream
+        w = w.to(torch.bfloat16).contiguous()
+        N, K = w.shape
+        q = torch.empty((N, K), dtype=torch.uint8, device=w.device)
+        sm = torch.empty((N, K // 32), dtype=torch.int32, device=w.device)
+        _chk(L.dec_q8_quantize(w.data_ptr(), N, K, q.data_ptr(), sm.data_ptr(), _stream()), "q8_quantize")
+        return cls(q, sm)
+
+    def dequant(self, L, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        from .nomic import _chk, _stream
+        N, K = self.shape
+        if out is None:
+            out = torch.empty((N, K), dtype=torch.bfloat16, device=self.q.device)
+        _chk(L.dec_q8_dequant(self.q.data_ptr(), self.sm.data_ptr(), N, K, out.data_ptr(), _stream()), "q8_dequant")
+        return out
+
+
+# GGUF tensor types stored at <= 4 bits per weight (Q4_0, Q4_1, Q2_K, Q3_K, Q4_K, IQ2/IQ3/IQ4, IQ1):
+# Q4G32 keeps them at no loss of grid resolution; every other type (Q5_x, Q6_K, Q8_0, F16, BF16,
+# F32) goes to Q8G32
+GGML_LE4 = {2, 3, 10, 11, 12, 16, 17, 18, 19, 20, 21, 22, 23, 29}
+
 
 class CausalLM:
     def __init__(self, cfg: DecoderConfig, tensors: Dict[str, torch.Tensor], device: str = "cuda",
-                 quant: str = "bf16"):
+                 quant: str = "bf16", ggml_types: Optional[Dict[str, int]] = None):
         """quant "q4": every projection (qkv, o, up|gate, down, LM head) is kept as a Q4Weight
-        (GPU only); "bf16": bf16 weights."""
+        (GPU only) -- except those whose source GGUF tensors (``ggml_types``, name -> GGML type)
+        hold more than 4 bits per weight, which are kept as Q8Weight; "bf16": bf16 weights."""
         if quant not in ("bf16", "q4"):
             raise ValueError(f"quant must be bf16 or q4, not {quant!r}")
         self.cfg = cfg
@@ -208,8 +210,15 @@ class CausalLM:
         self.layers = []
         if self.hip:
             self._declare()
-        Q = (lambda t: Q4Weight.quantize(self.L, t)) if self.quant == "q4" else (lambda t: t)  # noqa: E731
-        self.head = Q(self.head)
+        gt = ggml_types or {}
+
+        def Q(t, *names):
+            if self.quant != "q4":
+                return t
+            wide = any(n in gt and gt[n] not in GGML_LE4 for n in names)
+            return (Q8Weight if wide else Q4Weight).quantize(self.L, t)
+
+        self.head = Q(self.head, "output.weight" if "output.weight" in tensors else "token_embd.weight")
         for i in range(cfg.layers):
             p = f"blk.{i}."
             qkv = torch.cat([T(p + "attn_q.weight"), T(p + "attn_k.weight"), T(p + "attn_v.weight")], 0)
@@ -217,9 +226,12 @@ class CausalLM:
             # SwiGLU epilogue layout: rows interleaved [up16 | gate16] (nomic_api.h NOMIC_EPI_SWIGLU)
             from .nomic import pack_upgate
             ug = pack_upgate(up, gate)
-            self.layers.append({"n1": T(p + "attn_norm.weight").float(), "qkv": Q(qkv.contiguous()),
-                                "o": Q(T(p + "attn_output.weight")), "n2": T(p + "ffn_norm.weight").float(),
-                                "ug": Q(ug.contiguous()), "down": Q(T(p + "ffn_down.weight"))})
+            self.layers.append({"n1": T(p + "attn_norm.weight").float(),
+                                "qkv": Q(qkv.contiguous(), p + "attn_q.weight", p + "attn_k.weight", p + "attn_v.weight"),
+                                "o": Q(T(p + "attn_output.weight"), p + "attn_output.weight"),
+                                "n2": T(p + "ffn_norm.weight").float(),
+                                "ug": Q(ug.contiguous(), p + "ffn_gate.weight", p + "ffn_up.weight"),
+                                "down": Q(T(p + "ffn_down.weight"), p + "ffn_down.weight")})
             del qkv, gate, up, ug
         self._q4_scratch: Optional[torch.Tensor] = None
         hd = cfg.head_dim
@@ -231,12 +243,14 @@ class CausalLM:
         # written in place (no per-token torch.cat regrowth: decode stays O(1) copies per token)
         self.kv: Optional[torch.Tensor] = None
         self.pos = 0
-        self.attn_kernel = True  # single-token decode through dec_attn_decode (False: SDPA, for A/B)
+        self.attn_kernel = True  # HIP prefill / decode attention (False: torch SDPA, for A/B only)
         if self.hip:
             ok = all(n % 128 == 0 for n in (cfg.d + 2 * cfg.kv_heads * hd, cfg.d, 2 * cfg.ffn, vpad)) \
                 and cfg.d % 64 == 0 and cfg.ffn % 64 == 0
             if not ok:
                 raise ValueError("decoder dims must be multiples of 128 (N) / 64 (K) for the MFMA GEMM")
+            if hd not in (64, 128):
+                raise ValueError(f"head dim {hd}: the HIP prefill/decode attention kernels take 64 or 128")
 
     def _declare(self):
         """ctypes signatures of the decoder kernels (csrc/hip/decoder_kernels.hip)."""
@@ -256,6 +270,9 @@ class CausalLM:
             self.L.dec_attn_decode_ws.restype = c_int
             self.L.dec_attn_prefill.argtypes = [P, P, P, P, c_int, c_int, c_int, c_float, P]
             self.L.dec_attn_prefill.restype = c_int
+            self.L.dec_attn_prefill_kv.argtypes = [P, c_long, P, P, c_long, c_int, c_int, c_int, c_int, c_int, c_float,
+                                                   P, c_long, P]
+            self.L.dec_attn_prefill_kv.restype = c_int
             self.L.dec_gemv.argtypes = [c_int, P, P, c_float, P, c_int, c_int, P, P, P]
             self.L.dec_gemv.restype = c_int
             self.L.dec_embed_tok.argtypes = [P, c_int, P, P, P]
@@ -274,6 +291,12 @@ class CausalLM:
             self.L.dec_q4_quantize.restype = c_int
             self.L.dec_q4_dequant.argtypes = [P, P, c_long, c_int, P, P]
             self.L.dec_q4_dequant.restype = c_int
+            self.L.dec_gemv_q8.argtypes = [c_int, P, P, c_float, P, P, c_int, c_int, P, P, P]
+            self.L.dec_gemv_q8.restype = c_int
+            self.L.dec_q8_quantize.argtypes = [P, c_long, c_int, P, P, P]
+            self.L.dec_q8_quantize.restype = c_int
+            self.L.dec_q8_dequant.argtypes = [P, P, c_long, c_int, P, P]
+            self.L.dec_q8_dequant.restype = c_int
             self.L._dec_declared = True
 
     @classmethod
@@ -284,18 +307,19 @@ class CausalLM:
     @classmethod
     def from_gguf(cls, path: str, device: str = "cuda", quant: str = "auto"):
         """quant "auto": Q4G32 when most projection weights of the file are 4-bit GGUF types
-        (Q4_0 / Q4_1 / Q4_K: a Q4_K_M file's Q6_K tensors are re-gridded to 4 bits too), else bf16."""
+        (Q4_0 / Q4_1 / Q4_K), with the file's wider tensors (a Q4_K_M file's Q6_K) on Q8G32; else bf16."""
         from .gguf import GGUFFile
         g = GGUFFile(path)
         cfg = config_from_gguf(g)
         if quant == "auto":
             quant = gguf_quant_kind(g)
         tensors = {n: torch.from_numpy(np.ascontiguousarray(g.to_numpy_f32(n))) for n in g.tensors}
-        tokens = g.get("tokenizer.ggml.tokens")
-        tok = VocabTokenizer(list(tokens), int(g.get("tokenizer.ggml.bos_token_id", 1)),
-                             int(g.get("tokenizer.ggml.eos_token_id", 2))) if tokens else ByteTokenizer()
-        tok.chat_template = g.get("tokenizer.chat_template", None)  # rendered by splainference.build_prompt
-        return cls(cfg, tensors, device, quant=quant if device != "cpu" else "bf16"), tok
+        from .llm_tokenizer import tokenizer_from_gguf
+        tok = tokenizer_from_gguf(g) or ByteTokenizer()  # SPM / BPE by tokenizer.ggml.model
+        if not hasattr(tok, "chat_template"):
+            tok.chat_template = None  # rendered by splainference.build_prompt
+        types = {n: t.ggml_type for n, t in g.tensors.items()}
+        return cls(cfg, tensors, device, quant=quant if device != "cpu" else "bf16", ggml_types=types), tok
 
     # ------------------------------------------------------------- pieces --
     def _mm(self, mode: int, x: torch.Tensor, w, out_cols: int, res: Optional[torch.Tensor] = None):
@@ -384,19 +408,15 @@ class CausalLM:
             self.kv[li, 0, self.pos: self.pos + n] = k
             self.kv[li, 1, self.pos: self.pos + n] = v
             L_ = self.pos + n
-            if self.hip and self.attn_kernel and n > 1 and self.pos == 0 and hd == 64:
-                # prompt prefill: causal MFMA attention over the prompt's own q|k|v (k_attn2<CAUSAL>)
+            if self.hip and self.attn_kernel and n > 1:
+                # prompt prefill, fresh or continuing a live cache: causal MFMA attention of the n new
+                # queries over cache rows 0 .. pos+n-1 (dec_attn_prefill_kv, hd 64 / 128)
                 from .nomic import _chk, _stream
                 a = torch.empty((n, cfg.d), dtype=qkv.dtype, device=self.device)
-                if getattr(self, "_pf_n", -1) != n:
-                    self._pf_cu = torch.tensor([0, n], dtype=torch.int32, device=self.device)
-                    self._pf_qb = torch.tensor([v for q0 in range(0, n, 128) for v in (0, q0)], dtype=torch.int32,
-                                               device=self.device)
-                    self._pf_n = n
-                _chk(self.L.dec_attn_prefill(qkv.data_ptr(), a.data_ptr(), self._pf_cu.data_ptr(),
-                                             self._pf_qb.data_ptr(), self._pf_qb.numel() // 2, H, KVH, hd ** -0.5,
-                                             _stream()), "attn_prefill")
-            elif self.hip and self.attn_kernel and n == 1 and hd % 64 == 0 and hd <= 256:
+                _chk(self.L.dec_attn_prefill_kv(qkv.data_ptr(), qkv.stride(0), self.kv[li, 0].data_ptr(),
+                                                self.kv[li, 1].data_ptr(), KVH * hd, n, self.pos, H, KVH, hd,
+                                                hd ** -0.5, a.data_ptr(), cfg.d, _stream()), "attn_prefill")
+            elif self.hip and self.attn_kernel and n == 1:
                 # per-token decode: dec_attn_decode (one workgroup per q head, split-L online softmax)
                 from .nomic import _chk, _stream
                 a = torch.empty((1, cfg.d), dtype=qkv.dtype, device=self.device)
@@ -473,8 +493,8 @@ class DecodeEngine:
 
         def gemv(mode, x, rms, w, N, K, res, out, what):
             rp = rms.data_ptr() if rms is not None else None
-            if isinstance(w, Q4Weight):  # 4-bit weights: 0.625 B per weight streamed (dec_gemv_q4)
-                _chk(L.dec_gemv_q4(mode, x.data_ptr(), rp, cfg.eps, w.q.data_ptr(), w.sm.data_ptr(), N, K,
+            if isinstance(w, Q4Weight):  # 4-bit: 0.625 B per weight streamed (dec_gemv_q4); 8-bit: 1.125 B
+                _chk((L.dec_gemv_q8 if w.bits == 8 else L.dec_gemv_q4)(mode, x.data_ptr(), rp, cfg.eps, w.q.data_ptr(), w.sm.data_ptr(), N, K,
                                    P(res), out.data_ptr(), s), what)
             else:
                 _chk(L.dec_gemv(mode, x.data_ptr(), rp, cfg.eps, w.data_ptr(), N, K, P(res), out.data_ptr(), s), what)

@@ -245,7 +245,70 @@ def quantize_host(x: np.ndarray, ggml_type: int) -> bytes:
         out[:, :2] = d.astype(np.float16).view(np.uint8).reshape(-1, 2)
         out[:, 2:] = q[:, :16] | (q[:, 16:] << 4)
         return out.tobytes()
+    if ggml_type == 12:
+        return _quant_q4k(x)
+    if ggml_type == 14:
+        return _quant_q6k(x)
     raise NotImplementedError(f"host quantisation to ggml type {ggml_type}")
+
+
+def _quant_q4k(x: np.ndarray) -> bytes:
+    """Q4_K blocks (256 weights: fp16 d, dmin; 8 x 6-bit (scale, min) packed in 12 bytes; 4-bit q):
+    w = d s_j q - dmin m_j per 32-weight sub-block j (the layout _dequant_q4k reads)."""
+    b = x.reshape(-1, 8, 32)
+    lo = np.minimum(b.min(axis=2), 0.0)
+    a = (b.max(axis=2) - lo) / 15.0
+    d = a.max(axis=1) / 63.0
+    dmin = (-lo).max(axis=1) / 63.0
+    d16, dm16 = d.astype(np.float16), dmin.astype(np.float16)
+    df, dmf = d16.astype(np.float32), dm16.astype(np.float32)
+    s = np.clip(np.round(a / np.where(df > 0, df, 1)[:, None]), 0, 63).astype(np.int32)
+    m = np.clip(np.round(-lo / np.where(dmf > 0, dmf, 1)[:, None]), 0, 63).astype(np.int32)
+    step = (df[:, None] * s)[:, :, None]
+    off = (dmf[:, None] * m)[:, :, None]
+    q = np.clip(np.round((b + off) / np.where(step > 0, step, 1)), 0, 15).astype(np.uint8)
+    sc = np.zeros((b.shape[0], 12), np.uint8)
+    for j in range(4):
+        sc[:, j] = (s[:, j] & 63) | ((s[:, j + 4] >> 4) << 6)
+        sc[:, j + 4] = (m[:, j] & 63) | ((m[:, j + 4] >> 4) << 6)
+        sc[:, j + 8] = (s[:, j + 4] & 15) | ((m[:, j + 4] & 15) << 4)
+    qs = np.empty((b.shape[0], 128), np.uint8)
+    for k in range(4):
+        qs[:, 32 * k: 32 * k + 32] = q[:, 2 * k] | (q[:, 2 * k + 1] << 4)
+    out = np.empty((b.shape[0], 144), np.uint8)
+    out[:, 0:2] = d16.view(np.uint8).reshape(-1, 2)
+    out[:, 2:4] = dm16.view(np.uint8).reshape(-1, 2)
+    out[:, 4:16] = sc
+    out[:, 16:] = qs
+    return out.tobytes()
+
+
+def _quant_q6k(x: np.ndarray) -> bytes:
+    """Q6_K blocks (256 weights: 6-bit q as 128 low-nibble + 64 high-2-bit bytes, 16 int8 sub-block
+    scales, fp16 d): w = d sc_j (q - 32) per 16-weight sub-block (the layout _dequant_q6k reads)."""
+    b = x.reshape(-1, 16, 16)
+    amax = np.abs(b).max(axis=2)
+    sf = amax / 31.0
+    d = sf.max(axis=1) / 127.0
+    d16 = d.astype(np.float16)
+    df = d16.astype(np.float32)
+    sc = np.clip(np.round(sf / np.where(df > 0, df, 1)[:, None]), -128, 127).astype(np.int8)
+    step = (df[:, None] * sc.astype(np.float32))[:, :, None]
+    q = (np.clip(np.round(b / np.where(step != 0, step, 1)), -32, 31) + 32).astype(np.int32).reshape(-1, 256)
+    ql = np.zeros((q.shape[0], 128), np.int32)
+    qh = np.zeros((q.shape[0], 64), np.int32)
+    for half in range(2):
+        for qd in range(4):
+            v = q[:, 128 * half + 32 * qd: 128 * half + 32 * qd + 32]
+            col = 64 * half + 32 * (qd & 1)
+            ql[:, col: col + 32] |= (v & 15) << (4 if qd >= 2 else 0)
+            qh[:, 32 * half: 32 * half + 32] |= ((v >> 4) & 3) << (2 * qd)
+    out = np.empty((q.shape[0], 210), np.uint8)
+    out[:, :128] = ql.astype(np.uint8)
+    out[:, 128:192] = qh.astype(np.uint8)
+    out[:, 192:208] = sc.view(np.uint8)
+    out[:, 208:210] = d16.view(np.uint8).reshape(-1, 2)
+    return out.tobytes()
 
 
 # ----------------------------------------------------------------- writer --

@@ -100,7 +100,7 @@ class _Coll:
                 inp.numel() * inp.element_size() > A2A_CHUNK_BYTES:
             # Large equal-split all-to-alls go out in parts of <= A2A_CHUNK_BYTES per call: one
             # RCCL all_to_all_single of 1.5 GiB returned wrong bytes past 768 MiB on MI355X
-            # (scripts/a2a_check.py, profiles/r1_routed_integrity.md).  Each part is one
+            # (dev/debug/a2a_check.py, profiles/r1_routed_integrity.md).  Each part is one
             # contiguous byte range of every destination segment, sent as a grouped send/recv.
             w = dist.get_world_size(self.group)
             ib = inp.contiguous().view(torch.uint8).view(w, -1)

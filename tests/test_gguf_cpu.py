@@ -56,3 +56,15 @@ def test_reference_encoder_cpu_properties():
     # sequences in one packed batch never attend to each other
     assert torch.allclose(both[1], one[0], atol=1e-5)
     assert both.shape == (2, 768)
+
+
+def test_host_k_quant_roundtrip():
+    """Host Q4_K / Q6_K writers (the layouts the readers and the device dequant decode): relative
+    RMS error of a 4-bit and a 6-bit grid on Gaussian weights."""
+    import numpy as np
+    from libsplinter_amd.models.gguf import dequant_host, quantize_host
+    a = (np.random.default_rng(0).standard_normal(8 * 256) * 0.02).astype(np.float32)
+    for t, tol in ((12, 0.1), (14, 0.03)):
+        raw = np.frombuffer(quantize_host(a, t), np.uint8)
+        e = dequant_host(raw, t, a.size) - a
+        assert np.sqrt((e ** 2).mean()) / a.std() < tol, t

@@ -114,7 +114,7 @@ def test_chunked_all_to_all_rccl():
     s.close()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
-                        "--master-addr", "127.0.0.1", "--master-port", str(port), "scripts/a2a_check.py", "--chunked"],
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), "dev/debug/a2a_check.py", "--chunked"],
                        cwd=root, capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, (r.stdout + r.stderr)[-3000:]
     assert "chunked 2560 MiB: mismatching bytes 0" in r.stdout

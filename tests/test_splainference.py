@@ -42,8 +42,8 @@ def test_state_machine_cpu(uniq):
 @pytest.mark.gpu
 @pytest.mark.parametrize("kv_heads,heads", [(8, 8), (2, 8), (2, 4)])
 def test_decoder_hip_matches_cpu(kv_heads, heads):
-    """GPU forward (prefill, then one decode step) against the fp32 CPU model; heads 4 gives head
-    dim 128, whose prefill runs torch's fused causal attention (is_causal) instead of k_attn2."""
+    """GPU forward (prefill, a continuation prefill over the live cache, then one decode step)
+    against the fp32 CPU model; heads 4 gives head dim 128 (dec_attn_prefill_kv<128>)."""
     import torch
     from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
     cfg = DecoderConfig(layers=2, kv_heads=kv_heads, heads=heads)
@@ -53,6 +53,10 @@ def test_decoder_hip_matches_cpu(kv_heads, heads):
     lg, lc = gpu.forward(ids).cpu(), cpu.forward(ids)
     rel = (lg - lc).norm() / lc.norm()
     assert rel < 3e-2, float(rel)
+    # a second prompt chunk continuing the cache (pos > 0: the new queries see the old keys)
+    more = list(b" jumps over the lazy dog, again and again")
+    lg, lc = gpu.forward(more).cpu(), cpu.forward(more)
+    assert (lg - lc).norm() / lc.norm() < 3e-2
     # one decode step through the KV cache
     lg2, lc2 = gpu.forward([65]).cpu(), cpu.forward([65])
     assert (lg2 - lc2).norm() / lc2.norm() < 3e-2
@@ -172,6 +176,39 @@ def test_decoder_prefill_attention_causal_vs_fp32(H, KVH, n):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("hd,H,KVH", [(64, 8, 2), (128, 32, 8), (128, 4, 4)])
+def test_decoder_prefill_kv_causal_vs_fp32(hd, H, KVH):
+    """dec_attn_prefill_kv (k_prefill_attn<hd>): n new queries at absolute positions pos0 .. pos0+n-1
+    over cache rows 0 .. pos0+n-1, against fp32 causal softmax(q k^T) v; chunk sizes across the
+    128-row q-block and the key-tile boundaries, fresh (pos0 = 0) and continuation prompts."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
+    m = CausalLM.random(DecoderConfig(layers=1), seed=1, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(9)
+    n_ctx = 1024
+    kv = torch.randn((2, n_ctx, KVH, hd), device="cuda", generator=g).to(torch.bfloat16)
+    for n, pos0 in ((2, 0), (129, 0), (300, 0), (5, 37), (64, 200), (257, 511), (33, 990)):
+        ldq = (H + 2 * KVH) * hd  # q inside a fused q|k|v row, as the QKV GEMM writes it
+        qkv = torch.randn((n, ldq), device="cuda", generator=g).to(torch.bfloat16)
+        out = torch.full((n, H * hd), float("nan"), device="cuda").to(torch.bfloat16)
+        assert m.L.dec_attn_prefill_kv(qkv.data_ptr(), ldq, kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, n, pos0, H,
+                                       KVH, hd, hd ** -0.5, out.data_ptr(), H * hd, None) == 0
+        torch.cuda.synchronize()
+        L = pos0 + n
+        q = qkv[:, : H * hd].float().reshape(n, H, hd)
+        k = kv[0, :L].float().repeat_interleave(H // KVH, 1)
+        v = kv[1, :L].float().repeat_interleave(H // KVH, 1)
+        s = torch.einsum("qhd,khd->hqk", q, k) * hd ** -0.5
+        qpos = torch.arange(pos0, L, device="cuda")[:, None]
+        s = s.masked_fill(torch.arange(L, device="cuda")[None, :] > qpos, float("-inf"))
+        ref = torch.einsum("hqk,khd->qhd", torch.softmax(s, -1), v).reshape(n, -1)
+        err = (out.float() - ref).abs().max().item()
+        assert err < 3e-2, (n, pos0, err)
+    assert m.L.dec_attn_prefill_kv(qkv.data_ptr(), ldq, kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, 4, 0, H, KVH, 96,
+                                   1.0, out.data_ptr(), H * hd, None) != 0  # head dim 96: refused
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("K,N", [(512, 1536), (1536, 512), (4096, 200)])
 def test_dec_gemv_modes_vs_fp32(K, N):
     """dec_gemv (M = 1 projections of a decode step): store / residual / SwiGLU / fp32, with and
@@ -269,6 +306,109 @@ def test_q4_quant_dequant_and_gemv_q4_vs_fp32(K, N):
         u, gg = yg[:, 0].reshape(-1), yg[:, 1].reshape(-1)
         ref = u * torch.nn.functional.silu(gg)
         assert (out.float() - ref).abs().max() < 1e-2 * max(1.0, ref.abs().max().item())
+
+
+def _q8_host_dequant(q, sm):
+    """Host decoder of the Q8G32 planes: one byte u per weight, bf16 (d, m) per 32-k group, w = d u + m."""
+    import torch
+    smi = sm.to(torch.int64) & 0xFFFFFFFF
+    d = ((smi & 0xFFFF) << 16).to(torch.int32).view(torch.float32)
+    m = ((smi >> 16) << 16).to(torch.int32).view(torch.float32)
+    return q.float() * d.repeat_interleave(32, 1) + m.repeat_interleave(32, 1)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("K,N", [(512, 1536), (4096, 96)])
+def test_q8_quant_dequant_and_gemv_q8_vs_fp32(K, N):
+    """Q8G32 weights (the >4-bit tensors of a mostly-4-bit GGUF): quantisation within half a 1/255
+    grid step, dequant equal to the host decoder, and dec_gemv_q8 in every mode against fp32."""
+    import torch
+    from libsplinter_amd.models.decoder import CausalLM, DecoderConfig, Q8Weight
+    from libsplinter_amd.models.nomic import pack_upgate
+    m = CausalLM.random(DecoderConfig(layers=1), seed=1, device="cuda")
+    g = torch.Generator(device="cuda").manual_seed(13)
+    W = (torch.randn((N, K), device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+    qw = Q8Weight.quantize(m.L, W)
+    torch.cuda.synchronize()
+    assert qw.nbytes() * 8 == N * K * 9  # 1.125 B per weight
+    deq_host = _q8_host_dequant(qw.q, qw.sm)
+    deq = qw.dequant(m.L)
+    torch.cuda.synchronize()
+    assert torch.allclose(deq.float(), deq_host, rtol=2 ** -8, atol=1e-7)
+    Wg = W.float().reshape(N, K // 32, 32)
+    step = ((Wg.amax(-1) - Wg.amin(-1)) / 255).repeat_interleave(32, 1)
+    err = (deq_host - W.float()).abs()
+    assert bool((err <= step * 0.6 + 2e-6).all()), float((err / step).max())
+    x = torch.randn(K, device="cuda", generator=g).to(torch.bfloat16)
+    rw = torch.rand(K, device="cuda", generator=g) + 0.5
+    res = torch.randn(N, device="cuda", generator=g).to(torch.bfloat16)
+    xf = x.float()
+    xn = (xf * torch.rsqrt(xf.pow(2).mean() + 1e-5) * rw).to(torch.bfloat16).float()
+    for rms in (False, True):
+        xin = xn if rms else xf
+        for mode in (0, 1, 4):
+            out = torch.empty(N, device="cuda", dtype=torch.float32 if mode == 4 else torch.bfloat16)
+            assert m.L.dec_gemv_q8(mode, x.data_ptr(), rw.data_ptr() if rms else None, 1e-5, qw.q.data_ptr(),
+                                   qw.sm.data_ptr(), N, K, res.data_ptr(), out.data_ptr(), None) == 0
+            torch.cuda.synchronize()
+            ref = deq_host @ xin + (res.float() if mode == 1 else 0)
+            tol = (1e-3 if mode == 4 else 1e-2) * max(1.0, ref.abs().max().item())
+            assert (out.float() - ref).abs().max() < tol, (rms, mode)
+    if N % 32 == 0:
+        gate = (torch.randn((N // 2, K), device="cuda", generator=g) * 0.05).to(torch.bfloat16)
+        ug = Q8Weight.quantize(m.L, pack_upgate(W[: N // 2], gate).contiguous())
+        out = torch.empty(N // 2, device="cuda", dtype=torch.bfloat16)
+        assert m.L.dec_gemv_q8(2, x.data_ptr(), None, 0.0, ug.q.data_ptr(), ug.sm.data_ptr(), N, K, None,
+                               out.data_ptr(), None) == 0
+        torch.cuda.synchronize()
+        yg = (_q8_host_dequant(ug.q, ug.sm) @ xf).reshape(-1, 2, 16)
+        u, gg = yg[:, 0].reshape(-1), yg[:, 1].reshape(-1)
+        ref = u * torch.nn.functional.silu(gg)
+        assert (out.float() - ref).abs().max() < 1e-2 * max(1.0, ref.abs().max().item())
+
+
+@pytest.mark.gpu
+def test_from_gguf_mixed_q4_q6k_keeps_wide_tensors_at_8_bits(tmp_path):
+    """A Q4_K_M-shaped file (Q4_K projections, Q6_K ffn_down / attn_v / output): the Q6_K tensors
+    load as Q8Weight, the rest as Q4Weight, and decode steps through both GEMVs track the bf16 model
+    of the same dequantised tensors."""
+    import numpy as np
+    import torch
+    from libsplinter_amd.models.decoder import (CausalLM, DecodeEngine, DecoderConfig, Q4Weight, Q8Weight,
+                                                random_decoder_weights)
+    from libsplinter_amd.models.gguf import GGUFFile, GGUFWriter
+    cfg = DecoderConfig(vocab=384, d=256, layers=2, heads=4, kv_heads=2, ffn=512, n_ctx=256)
+    w = random_decoder_weights(cfg, seed=5)
+    path = str(tmp_path / "mixed.gguf")
+    gw = GGUFWriter(path, "llama")
+    for k, v in (("embedding_length", cfg.d), ("block_count", cfg.layers), ("attention.head_count", cfg.heads),
+                 ("attention.head_count_kv", cfg.kv_heads), ("feed_forward_length", cfg.ffn),
+                 ("context_length", cfg.n_ctx)):
+        gw.add(f"llama.{k}", v)
+    for n, a in w.items():
+        wide = n.endswith(("ffn_down.weight", "attn_v.weight")) or n == "output.weight"
+        gw.add_tensor(n, a, ("Q6_K" if wide else "Q4_K") if a.ndim == 2 and n != "token_embd.weight" else "F32")
+    gw.write()
+    m, _ = CausalLM.from_gguf(path, device="cuda")
+    assert m.quant == "q4"
+    lw = m.layers[0]
+    assert isinstance(lw["down"], Q8Weight) and isinstance(lw["qkv"], Q8Weight) and isinstance(m.head, Q8Weight)
+    assert type(lw["o"]) is Q4Weight and type(lw["ug"]) is Q4Weight
+    g = GGUFFile(path)
+    ref = CausalLM(m.cfg, {n: torch.from_numpy(np.ascontiguousarray(g.to_numpy_f32(n))) for n in g.tensors},
+                   device="cuda")
+    ids = [256] + list(b"mixed precision")
+    eng = DecodeEngine(m, use_graph=False)
+    eng.first_token(ids)
+    ref.forward(ids)
+    for t in (72, 101, 108):
+        eng.st[1] = t
+        eng._step()
+        torch.cuda.synchronize()
+        m.pos += 1
+        r = ref.forward([t])
+        got = eng.logits[: cfg.vocab]
+        assert (got - r).norm() / r.norm() < 0.1
 
 
 @pytest.mark.gpu

@@ -113,6 +113,23 @@ def _launch_ranks(args) -> int:
     return subprocess.call(cmd, env=env)
 
 
+def _timed_region_profiler():
+    """SPL_PROFILE_TIMED=1: roctxProfilerResume/Pause around the timed steps, so that
+    `rocprofv3 --selected-regions --kernel-trace --stats -- python3 bench.py ...` traces exactly the
+    timed region (which kernels run in the measured step, and nothing from setup or warm-up)."""
+    if os.environ.get("SPL_PROFILE_TIMED") != "1":
+        return lambda on: None
+    import ctypes
+    lib = ctypes.CDLL("librocprofiler-sdk-roctx.so.1")
+    lib.roctxProfilerResume.argtypes = lib.roctxProfilerPause.argtypes = [ctypes.c_uint64]
+
+    def toggle(on):
+        import torch
+        torch.cuda.synchronize()
+        (lib.roctxProfilerResume if on else lib.roctxProfilerPause)(0)
+    return toggle
+
+
 def main():
     args = parse()
     # Hardware queues per priority level for this process (HIP default 4).  Each HIP stream the
@@ -420,6 +437,8 @@ def main():
     if routed:
         dist.barrier()
     torch.cuda.synchronize()
+    prof = _timed_region_profiler()
+    prof(True)
     t_start = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
@@ -427,6 +446,7 @@ def main():
     if routed:
         dist.barrier()
     elapsed = time.perf_counter() - t_start
+    prof(False)
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     st = stats.clone()
     if routed:

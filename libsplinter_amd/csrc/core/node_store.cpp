@@ -179,8 +179,6 @@ NodeStore* NodeStore::open(const std::string& name, int* err) {
 }
 
 NodeStore::~NodeStore() {
-  stop_forwarder();
-  for (int fd : shard_fds_) close(fd);
   if (event_fd_ >= 0) {
     if (desc_ && __atomic_load_n(&desc_->event_pid, __ATOMIC_ACQUIRE) == (int32_t)getpid()) {
       __atomic_store_n(&desc_->event_fd, -1, __ATOMIC_RELEASE);
@@ -261,46 +259,23 @@ void NodeStore::event_bus_dirty(uint64_t* out, size_t words) {
   }
 }
 
-// One node eventfd: every shard arms its own bus (its kernels and per-call writers raise it) and a
-// forwarder thread turns any shard's wakeup into one on the node's fd.
+// One node eventfd shared by every shard: each shard adopts (a dup of) it as its own bus, so a
+// writer on any shard -- this process, another process through the shard header's owner fd, or a
+// shard's device-notify proxy -- increments the one counter, and a single read drains every
+// pending wakeup (as the reference's one eventfd, splinter.c event bus).
 int NodeStore::event_bus_init() {
-  stop_forwarder();
-  for (int fd : shard_fds_) close(fd);
-  shard_fds_.clear();
-  for (auto* s : shards_) {
-    if (s->event_bus_init() != 0) return -1;
-    const int fd = s->event_bus_open();
-    if (fd < 0) return -1;
-    shard_fds_.push_back(fd);
-  }
   const int fd = eventfd(0, EFD_CLOEXEC);
   if (fd < 0) return -1;
+  for (auto* s : shards_) {
+    if (s->event_bus_adopt(fd) != 0) {
+      close(fd);
+      return -1;
+    }
+  }
   if (event_fd_ >= 0) close(event_fd_);
   event_fd_ = fd;
   __atomic_store_n(&desc_->event_fd, fd, __ATOMIC_RELEASE);
   __atomic_store_n(&desc_->event_pid, (int32_t)getpid(), __ATOMIC_RELEASE);
-  fwd_stop_.store(false);
-  fwd_ = std::thread([this] {
-    std::vector<pollfd> p;
-    for (int sfd : shard_fds_) p.push_back(pollfd{sfd, POLLIN, 0});
-    while (!fwd_stop_.load(std::memory_order_acquire)) {
-      const int r = ::poll(p.data(), p.size(), 50);
-      if (r <= 0) continue;
-      bool any = false;
-      for (auto& q : p) {
-        if (q.revents & POLLIN) {
-          uint64_t v;
-          if (read(q.fd, &v, 8) == 8) any = true;
-        }
-        q.revents = 0;
-      }
-      if (any) {
-        const uint64_t one = 1;
-        ssize_t w = write(event_fd_, &one, 8);
-        (void)w;
-      }
-    }
-  });
   return 0;
 }
 
@@ -319,13 +294,6 @@ int NodeStore::event_bus_open() {
   errno = ENOSYS;
   return -1;
 #endif
-}
-
-void NodeStore::stop_forwarder() {
-  if (fwd_.joinable()) {
-    fwd_stop_.store(true, std::memory_order_release);
-    fwd_.join();
-  }
 }
 
 int NodeStore::madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t timeout) {

@@ -132,16 +132,12 @@ class NodeStore final : public StoreBase {
 
  private:
   NodeStore() = default;
-  void stop_forwarder();
 
   std::string name_;
   NodeDesc* desc_ = nullptr;
   bool owner_ = false;  // created the descriptor and every shard
   std::vector<StoreBase*> shards_;
   int event_fd_ = -1;
-  std::vector<int> shard_fds_;
-  std::thread fwd_;
-  std::atomic<bool> fwd_stop_{false};
 };
 
 // shard store name of shard i of node NAME, with its backend prefix ("hbm:" / "shm:")

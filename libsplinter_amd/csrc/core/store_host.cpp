@@ -819,8 +819,11 @@ void HostStore::enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*
 }
 
 // ------------------------------------------------------------- event bus --
-int HostStore::event_bus_init() {
-  int fd = eventfd(0, EFD_CLOEXEC);
+int HostStore::event_bus_init() { return event_bus_install(eventfd(0, EFD_CLOEXEC)); }
+
+int HostStore::event_bus_adopt(int fd) { return event_bus_install(fcntl(fd, F_DUPFD_CLOEXEC, 0)); }
+
+int HostStore::event_bus_install(int fd) {
   if (fd < 0) return -1;
   if (event_fd_ >= 0) close(event_fd_);
   event_fd_ = fd;

@@ -86,6 +86,8 @@ class HostStore final : public StoreBase {
   void enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) override;
 
   int event_bus_init() override;
+  int event_bus_adopt(int fd) override;
+  int event_bus_install(int fd);
   int event_bus_open() override;
   void event_bus_dirty(uint64_t* out, size_t words) override;
 

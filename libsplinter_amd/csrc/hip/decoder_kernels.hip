@@ -720,8 +720,19 @@ __global__ void k_q4_dequant(const uint8_t* __restrict__ Wq, const uint32_t* __r
   }
 }
 
+__device__ __forceinline__ float bf16_floor(float x) {
+  uint32_t u = __float_as_uint(x) & 0xFFFF0000u;
+  if (__uint_as_float(u) > x) u += 0x10000u;  // negative: truncation went toward zero, one ulp down
+  return __uint_as_float(u);
+}
+__device__ __forceinline__ float bf16_ceil(float x) {
+  uint32_t u = __float_as_uint(x) & 0xFFFF0000u;
+  if (__uint_as_float(u) < x) u += 0x10000u;  // positive: one ulp up
+  return __uint_as_float(u);
+}
+
 // bf16 W [N, K] <-> Q8G32 (one thread per 32-weight group): affine 255-step grid over the group's
-// [min, max], (d, m) rounded to bf16 first and the bytes chosen against the rounded pair
+// [min, max], (d, m) rounded to bf16 outward first and the bytes chosen against the rounded pair
 __global__ void k_q8_quant(const uint16_t* __restrict__ W, long groups, uint8_t* __restrict__ Wq,
                            uint32_t* __restrict__ Wsm) {
   const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -733,8 +744,10 @@ __global__ void k_q8_quant(const uint16_t* __restrict__ W, long groups, uint8_t*
   float lo = v[0], hi = v[0];
 #pragma unroll
   for (int e = 1; e < kQ4Group; ++e) { lo = fminf(lo, v[e]); hi = fmaxf(hi, v[e]); }
-  const float m = (float)(__bf16)lo;
-  float d = (float)(__bf16)((hi - m) / 255.f);
+  // m rounded DOWN and d UP to bf16, so the 255-step grid still spans [lo, hi]: at 8 bits a
+  // round-to-nearest m would move the grid by up to |m| 2^-9, most of a step
+  const float m = bf16_floor(lo);
+  float d = bf16_ceil((hi - m) / 255.f);
   if (!(d > 0.f)) d = 0.f;
   const float inv = d > 0.f ? 1.f / d : 0.f;
   uint32_t packed[8] = {};

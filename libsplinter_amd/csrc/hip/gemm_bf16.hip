@@ -453,7 +453,13 @@ __device__ __forceinline__ uint4 pack8(const float* v) {
   return o;
 }
 
-template <int MODE>
+// ILV > 0: each phase's two LDS-DMA instructions are issued between its MFMA groups (before the
+// groups u = ILV and ILV + 4 of the 8 (kk, i) groups of 2 MFMAs) instead of all before the first
+// MFMA -- a DMA instruction's ~100-cycle issue cost then overlaps the other wave's MFMAs on the
+// SIMD instead of holding both waves off the matrix core right after the barrier (the finding of
+// gemm_rln.hip's ILV variants).  The issue ORDER of the DMAs is unchanged, so the counted vmcnt
+// waits and the WAR/RAW distances of the phase schedule hold as they are.
+template <int MODE, int ILV = 0>
 __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ W, long ldw, int K,
                                                           int mtiles, int ntiles, EpiArgs ep) {
@@ -476,14 +482,15 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
       offA[h][i] = (uint32_t)(gr * lda + schunk);
       offB[h][i] = (uint32_t)((n0 + r) * ldw + schunk);
     }
-  auto stage = [&](int which, int t, int buf) {  // which: 0 A0, 1 A1, 2 B0, 3 B1
+  auto stage_one = [&](int which, int t, int buf, int i) {  // which: 0 A0, 1 A1, 2 B0, 3 B1
     const uint16_t* base = (which < 2 ? A : W) + (long)t * BK;
     char* dst = smem + buf * kBufBytes + which * kHalfBytes;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t off = which == 0 ? offA[0][i] : which == 1 ? offA[1][i] : which == 2 ? offB[0][i] : offB[1][i];
-      __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
-    }
+    const uint32_t off = which == 0 ? offA[0][i] : which == 1 ? offA[1][i] : which == 2 ? offB[0][i] : offB[1][i];
+    __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
+  };
+  auto stage = [&](int which, int t, int buf) {
+    stage_one(which, t, buf, 0);
+    stage_one(which, t, buf, 1);
   };
 
   // fragment read addressing: row-in-half R = base16 + (lane&15), chunk kk*4 + (lane>>4), swizzled by R&7 = lane&7
@@ -507,6 +514,26 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
   if (nk > 1) { stage(0, 1, 1); stage(2, 1, 1); stage(3, 1, 1); }
 
   bf16x8 af[4][2], b0[2][2], b1[2][2];
+  // one quadrant's 16 MFMAs (kk, i, j), with the phase's stage issued before them (ILV 0) or
+  // between the (kk, i) groups u = ILV and ILV + 4 (ILV > 0)
+  auto mma_phase = [&](f32x4 (&ac)[4][2], bf16x8 (&bf)[2][2], int which, int st, int sbuf, bool go) {
+    if (ILV == 0 && go) stage(which, st, sbuf);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (ILV > 0) {
+          if (go && kk * 4 + i == ILV) stage_one(which, st, sbuf, 0);
+          if (go && kk * 4 + i == ILV + 4) stage_one(which, st, sbuf, 1);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          ac[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], ac[i][j], 0, 0, 0);
+        if constexpr (ILV > 0) __builtin_amdgcn_sched_barrier(0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     const char* hA0 = smem + buf * kBufBytes;
@@ -527,16 +554,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
       af[i][0] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw0);
       af[i][1] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw1);
     }
-    if (n1) stage(1, t + 1, buf ^ 1);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[0][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], b0[j][kk], acc[0][0][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[0][0], b0, 1, t + 1, buf ^ 1, n1);
     // ---- phase 2: quadrant (0,1)
     wait_vm(n1 ? 10 : 2);
     raw_barrier();
@@ -545,16 +563,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
       b1[j][0] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw0);
       b1[j][1] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw1);
     }
-    if (n2) stage(0, t + 2, buf);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[0][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], b1[j][kk], acc[0][1][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[0][1], b1, 0, t + 2, buf, n2);
     // ---- phase 3: quadrant (1,0)
     wait_vm(n2 ? 10 : (n1 ? 8 : 0));
     raw_barrier();
@@ -563,27 +572,9 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
       af[i][0] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw0);
       af[i][1] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw1);
     }
-    if (n2) stage(2, t + 2, buf);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[1][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], b0[j][kk], acc[1][0][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[1][0], b0, 2, t + 2, buf, n2);
     // ---- phase 4: quadrant (1,1), registers only (B1's last read was phase 2: a barrier ago)
-    if (n2) stage(3, t + 2, buf);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[1][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], b1[j][kk], acc[1][1][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[1][1], b1, 3, t + 2, buf, n2);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
@@ -711,7 +702,7 @@ __device__ __forceinline__ uint2 pack4(const float* v) {
   return make_uint2(pk2(v[0], v[1]), pk2(v[2], v[3]));
 }
 
-template <int MODE, bool PERSIST, bool SK = false>
+template <int MODE, bool PERSIST, bool SK = false, int ILV = 0>
 __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int K,
                                                          int mtiles, int ntiles, EpiArgs ep) {
@@ -780,18 +771,19 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
   int ti = 0, kt = 0;
 
   // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of stream step g into buffer buf
-  auto stage = [&](int which, int g, int buf) {
+  auto stage_one = [&](int which, int g, int buf, int i) {
     const bool nx = g >= (ti + 1) * nk;
     const int tl = ti + (nx ? 1 : 0);
     const int k0 = (g - tl * nk + (SK && tl == q ? k_first : 0)) * BK;
     const uint16_t* base = (which < 2 ? A : W) + k0;
     char* dst = smem + buf * kBufBytes + which * kHalfBytes;
     const int h = which & 1;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const uint32_t off = which < 2 ? (nx ? offAx[h][i] : offAc[h][i]) : (nx ? offBx[h][i] : offBc[h][i]);
-      __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
-    }
+    const uint32_t off = which < 2 ? (nx ? offAx[h][i] : offAc[h][i]) : (nx ? offBx[h][i] : offBc[h][i]);
+    __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
+  };
+  auto stage = [&](int which, int g, int buf) {
+    stage_one(which, g, buf, 0);
+    stage_one(which, g, buf, 1);
   };
 
   const int frow = (lane & 15) * 128;
@@ -879,6 +871,26 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
   };
 
   bf16x8 af[4][2], b0[2][2], b1[2][2];
+  // as k_gemm256's: one quadrant's 16 MFMAs with the phase's stage before (ILV 0) or between them;
+  // swapped operands (W fragment as the A operand)
+  auto mma_phase = [&](f32x4 (&ac)[4][2], bf16x8 (&bf)[2][2], int which, int sg, int sbuf, bool go) {
+    if (ILV == 0 && go) stage(which, sg, sbuf);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (ILV > 0) {
+          if (go && kk * 4 + i == ILV) stage_one(which, sg, sbuf, 0);
+          if (go && kk * 4 + i == ILV + 4) stage_one(which, sg, sbuf, 1);
+        }
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          ac[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], ac[i][j], 0, 0, 0);
+        if constexpr (ILV > 0) __builtin_amdgcn_sched_barrier(0);
+      }
+    __builtin_amdgcn_s_setprio(0);
+  };
   for (int g = 0; g < total; ++g) {
     const int buf = g & 1;
     const char* hA0 = smem + buf * kBufBytes;
@@ -899,16 +911,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
       af[i][0] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw0);
       af[i][1] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw1);
     }
-    if (n1) stage(1, g + 1, buf ^ 1);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[0][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][kk], af[i][kk], acc[0][0][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[0][0], b0, 1, g + 1, buf ^ 1, n1);
     // ---- phase 2: quadrant (0,1)
     wait_vm(n1 ? 10 : 2);
     raw_barrier();
@@ -917,16 +920,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
       b1[j][0] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw0);
       b1[j][1] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw1);
     }
-    if (n2) stage(0, g + 2, buf);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[0][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][kk], af[i][kk], acc[0][1][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[0][1], b1, 0, g + 2, buf, n2);
     // ---- phase 3: quadrant (1,0)
     wait_vm(n2 ? 10 : (n1 ? 8 : 0));
     raw_barrier();
@@ -935,27 +929,9 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
       af[i][0] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw0);
       af[i][1] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw1);
     }
-    if (n2) stage(2, g + 2, buf);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[1][0][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b0[j][kk], af[i][kk], acc[1][0][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[1][0], b0, 2, g + 2, buf, n2);
     // ---- phase 4: quadrant (1,1), registers only (B1's last read was phase 2: a barrier ago)
-    if (n2) stage(3, g + 2, buf);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[1][1][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(b1[j][kk], af[i][kk], acc[1][1][i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    mma_phase(acc[1][1], b1, 3, g + 2, buf, n2);
 
     if (++kt < nk) continue;
     // ---- tile done: register epilogue (lane: rows m, 4 consecutive columns per fragment) --------
@@ -1032,6 +1008,22 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
 }
 
 int g_num_cus = 256;  // MI355X: 256 CUs in 8 XCDs; refreshed from the device on first use
+
+// DMA interleave of the 256^2 kernels (k_gemm256 / k_gemm_p ILV): NOMIC_GEMM_ILV 0, 1 or 2
+int g_ilv = -1;
+int gemm_ilv() {
+  if (g_ilv < 0) {
+    const char* e = getenv("NOMIC_GEMM_ILV");
+    g_ilv = e && *e ? atoi(e) : 0;
+    if (g_ilv < 0 || g_ilv > 2) g_ilv = 0;
+  }
+  return g_ilv;
+}
+
+template <typename F>
+void allow_lds(F* f, int bytes) {
+  (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+}
 
 int g_variant = -1;
 int gemm_variant() {
@@ -1131,10 +1123,10 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
   }
   if (p_ok && fits && K >= 2 * BK && (var == 512 || var == 513 || (var == 0 && many))) {
     static bool attr_p = [] {
-      (void)hipFuncSetAttribute((const void*)k_gemm_p<MODE, true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * kBufBytes);
-      (void)hipFuncSetAttribute((const void*)k_gemm_p<MODE, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                2 * kBufBytes);
+      allow_lds(k_gemm_p<MODE, true>, 2 * kBufBytes);
+      allow_lds(k_gemm_p<MODE, true, false, 1>, 2 * kBufBytes);
+      allow_lds(k_gemm_p<MODE, true, false, 2>, 2 * kBufBytes);
+      allow_lds(k_gemm_p<MODE, false>, 2 * kBufBytes);
       return true;
     }();
     (void)attr_p;
@@ -1142,26 +1134,40 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     ep.gn = band_width(ntiles, 4);
     const int tiles = mtiles * ntiles;
     if constexpr (p_ok) {
-    if (var != 513)
-      hipLaunchKernelGGL((k_gemm_p<MODE, true>), dim3(tiles < cus ? tiles : cus), dim3(kThreads2), 2 * kBufBytes, s,
-                         A, lda, W, ldw, K, mtiles, ntiles, ep);
-    else
-      hipLaunchKernelGGL((k_gemm_p<MODE, false>), dim3(tiles), dim3(kThreads2), 2 * kBufBytes, s, A, lda, W, ldw, K,
-                         mtiles, ntiles, ep);
+      const dim3 g(tiles < cus ? tiles : cus), b(kThreads2);
+      if (var == 513)
+        hipLaunchKernelGGL((k_gemm_p<MODE, false>), dim3(tiles), b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
+                           ep);
+      else if (gemm_ilv() == 1)
+        hipLaunchKernelGGL((k_gemm_p<MODE, true, false, 1>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
+                           ep);
+      else if (gemm_ilv() == 2)
+        hipLaunchKernelGGL((k_gemm_p<MODE, true, false, 2>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
+                           ep);
+      else
+        hipLaunchKernelGGL((k_gemm_p<MODE, true>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
     }
     return (int)hipGetLastError();
   }
   if (k256_ok && fits && (var == 256 || (var == 0 && (mpad / 256) * (N / 256) >= 2048))) {
     static bool attr = [] {
-      (void)hipFuncSetAttribute((const void*)k_gemm256<MODE>, hipFuncAttributeMaxDynamicSharedMemorySize, kLds2Bytes);
+      allow_lds(k_gemm256<MODE>, kLds2Bytes);
+      allow_lds(k_gemm256<MODE, 1>, kLds2Bytes);
+      allow_lds(k_gemm256<MODE, 2>, kLds2Bytes);
       return true;
     }();
     (void)attr;
     const int mtiles = (int)(mpad / 256), ntiles = N / 256;
     ep.gn = band_width(ntiles, 4);
-    if constexpr (k256_ok)
-      hipLaunchKernelGGL(k_gemm256<MODE>, dim3(mtiles * ntiles), dim3(kThreads2), kLds2Bytes, s, A, lda, W, ldw, K,
-                         mtiles, ntiles, ep);
+    if constexpr (k256_ok) {
+      const dim3 g(mtiles * ntiles), b(kThreads2);
+      if (gemm_ilv() == 1)
+        hipLaunchKernelGGL((k_gemm256<MODE, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+      else if (gemm_ilv() == 2)
+        hipLaunchKernelGGL((k_gemm256<MODE, 2>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+      else
+        hipLaunchKernelGGL((k_gemm256<MODE>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+    }
     return (int)hipGetLastError();
   }
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = N / BN;
@@ -1177,6 +1183,13 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
 extern "C" int nomic_gemm_set_variant(int variant) {
   const int prev = gemm_variant();
   g_variant = variant;
+  return prev;
+}
+
+// A/B knob: DMA interleave of the 256^2 kernels (0, 1, 2); returns the previous setting
+extern "C" int nomic_gemm_set_ilv(int ilv) {
+  const int prev = gemm_ilv();
+  g_ilv = ilv < 0 || ilv > 2 ? 0 : ilv;
   return prev;
 }
 

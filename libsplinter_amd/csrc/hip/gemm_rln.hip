@@ -475,7 +475,7 @@ int g_rln_variant = -1;
 int rln_variant() {
   if (g_rln_variant < 0) {
     const char* e = getenv("NOMIC_RLN");
-    g_rln_variant = e && *e ? atoi(e) : 220;  // [ILV * 100 +] PIPE * 10 + EPI
+    g_rln_variant = e && *e ? atoi(e) : 222;  // [ILV * 100 +] PIPE * 10 + EPI (222: profiles/r3_rln_ab.jsonl)
   }
   return g_rln_variant;
 }

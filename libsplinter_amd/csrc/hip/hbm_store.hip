@@ -380,8 +380,9 @@ class HbmStore final : public StoreBase {
   // process attached to the arena (system-scope store from the kernel epilogue, arena_dev.hpp
   // notify_host), and by per-call mutations of other processes.  Device kernels also maintain
   // the dirty mask once the device header records an owner (mirrored here).
-  int event_bus_init() override {
-    int fd = eventfd(0, EFD_CLOEXEC);
+  int event_bus_init() override { return event_bus_install(eventfd(0, EFD_CLOEXEC)); }
+  int event_bus_adopt(int fd) override { return event_bus_install(fcntl(fd, F_DUPFD_CLOEXEC, 0)); }
+  int event_bus_install(int fd) {
     if (fd < 0) return -1;
     stop_proxy();
     if (event_fd_ >= 0) close(event_fd_);

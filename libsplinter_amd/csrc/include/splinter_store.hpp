@@ -10,6 +10,7 @@
 #pragma once
 #include <cstddef>
 #include <cstdint>
+#include <cerrno>
 #include "splinter.h"
 #include "splinter_layout.hpp"
 
@@ -80,6 +81,9 @@ class StoreBase {
 
   // event bus
   virtual int event_bus_init() = 0;
+  // make an existing eventfd (dup'd) this store's bus: the shards of a node store share the node's
+  // one eventfd, so every writer on any shard signals the same counter
+  virtual int event_bus_adopt(int fd) { (void)fd; errno = ENOTSUP; return -1; }
   virtual int event_bus_open() = 0;
   virtual void event_bus_dirty(uint64_t* out, size_t words) = 0;
 

@@ -17,6 +17,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--square", type=int, default=0, help="also time a plain MxNxK = S x S x S GEMM (loop throughput)")
+    ap.add_argument("--variants", default="514,512,513,256,128", help="NOMIC_GEMM kernel variants")
+    ap.add_argument("--ilvs", default="0", help="DMA interleave settings of the 256^2 kernels (nomic_gemm_set_ilv)")
+    ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -26,6 +29,8 @@ def main():
     torch.manual_seed(0)
     shapes = [("qkv_rope", 3, 2304, 768), ("attn_out_res", 1, 768, 768), ("ffn_swiglu", 2, 6144, 768),
               ("ffn_down_res", 1, 768, 3072)]
+    if a.shapes:
+        shapes = [sh for sh in shapes if sh[0] in a.shapes.split(",")]
     if a.square:
         shapes = [("square", 0, a.square, a.square)]
         M = a.square
@@ -47,12 +52,14 @@ def main():
                           None if rope is None else rope.data_ptr(), None if pos is None else pos.data_ptr(),
                           1536, _stream()), name)
 
-    VARS = (514, 512, 513, 256, 128)
+    ilvs = [int(x) for x in a.ilvs.split(",")]
+    VARS = [(int(v), il) for v in a.variants.split(",") for il in (ilvs if int(v) in (256, 512) else [0])]
     times = {(n, v): [] for n, *_ in shapes for v in VARS}
     for r in range(a.rounds):
         for name, *_ in shapes:
             for v in VARS:
-                L.nomic_gemm_set_variant(v)
+                L.nomic_gemm_set_variant(v[0])
+                L.nomic_gemm_set_ilv(v[1])
                 run(name)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -82,7 +89,8 @@ def main():
                           "ms_median": ref[name], "tflops_median": fl / ref[name] / 1e9}))
         for v in VARS:
             t = np.array(times[(name, v)])
-            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": v, "ms_median": float(np.median(t)),
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": v[0], "ilv": v[1],
+                              "ms_median": float(np.median(t)),
                               "tflops_median": fl / np.median(t) / 1e9, "tflops_best": fl / t.min() / 1e9}))
 
 

@@ -18,12 +18,16 @@ def L0():
     return _lib()
 
 
-@pytest.fixture(params=[512, 513, 256, 128], ids=["gemm_p", "gemm_r", "gemm256", "gemm128"])
+@pytest.fixture(params=[(512, 0), (513, 0), (256, 0), (128, 0), (512, 1), (512, 2), (256, 1), (256, 2)],
+                ids=["gemm_p", "gemm_r", "gemm256", "gemm128", "gemm_p_ilv1", "gemm_p_ilv2", "gemm256_ilv1",
+                     "gemm256_ilv2"])
 def L(L0, request):
-    """Run each GEMM numerics test on both kernel variants."""
-    prev = L0.nomic_gemm_set_variant(request.param)
+    """Run each GEMM numerics test on every kernel variant (and DMA-interleave setting)."""
+    prev = L0.nomic_gemm_set_variant(request.param[0])
+    prev_ilv = L0.nomic_gemm_set_ilv(request.param[1])
     yield L0
     L0.nomic_gemm_set_variant(prev)
+    L0.nomic_gemm_set_ilv(prev_ilv)
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 768, 768), (1000, 2304, 768), (257, 768, 3072),

@@ -163,3 +163,53 @@ def test_raw_ptr_on_hbm_is_zero_copy(uniq):
     finally:
         s.close()
 
+
+
+def test_ring_worker_idle_exit_and_relaunch(uniq, monkeypatch):
+    """With a 2 ms idle timeout the ring worker exits between bursts and the next call (or a waiter
+    that sees it gone) relaunches it: calls straddling the idle exit from 8 threads are all served
+    with the right values, and spl_hbm_ring_launches counts the relaunches."""
+    import random
+    import threading
+    from libsplinter_amd import Store
+    from libsplinter_amd import _native as N
+    monkeypatch.setenv("SPLINTER_RING_IDLE_US", "2000")
+    s = Store.create(f"hbm:{uniq}", slots=4096, max_val=64, embeddings=False)
+    launches = lambda: N.hip_lib().spl_hbm_ring_launches(s.handle)  # noqa: E731
+    try:
+        s.set("k0", b"v0")
+        n0 = launches()
+        assert n0 >= 1
+        time.sleep(0.05)  # > idle timeout: the worker has left
+        assert s.get("k0") == b"v0"
+        assert launches() > n0
+        errors = []
+
+        def worker(t):
+            rng = random.Random(t)
+            try:
+                for i in range(60):
+                    k = f"t{t}_{i}"
+                    s.set(k, f"{t}:{i}".encode())
+                    if s.get(k) != f"{t}:{i}".encode():
+                        errors.append(k)
+                    time.sleep(rng.choice((0.0, 0.0005, 0.003, 0.006)))
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+
+        n1 = launches()
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(8)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join(120)
+        assert not errors, errors[:5]
+        assert launches() > n1  # the worker idled out and came back during the run
+    finally:
+        s.close()
+
+
+def test_hostapi_32_threads(uniq):
+    """32 host threads (more than the box's CPU share on a loaded host): every call served."""
+    res = _hostapi(f"hbm:{uniq}", 32)
+    assert res["failures"] == 0

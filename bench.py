@@ -613,6 +613,11 @@ def main():
             "collectives": ("RCCL on torch's per-process-group streams (request / response groups), "
                             "sharing the normal-priority queue pool with the writers") if routed else None,
             "search_keys_per_gpu": args.search_keys if sarena is not None else 0,
+            # bytes each GPU sends to its W-1 peers per routed step (16-B key records; every all-to-all moves W x cap
+            # rows per kind, (W-1)/W of them off-GPU): set requests key + len + value prefix, set
+            # status back, get requests key, get responses status + len + value prefix
+            "xgmi_bytes_per_step_per_gpu": ((world - 1) * (cap_s * (16 + 4 + vw + 4) + cap_g * (16 + 4 + 4 + vw))
+                                            if routed else 0),
         },
         "kv_ops_per_s": kv_ops_s,
         "embed_vectors_per_s": emb_vps,

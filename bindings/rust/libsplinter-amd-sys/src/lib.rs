@@ -208,7 +208,7 @@ extern "C" {
     pub fn splinter_retrain_slot(key: *const c_char) -> c_int;
     pub fn splinter_set_label(key: *const c_char, mask: u64) -> c_int;
     pub fn splinter_unset_label(key: *const c_char, mask: u64) -> c_int;
-    pub fn splinter_client_set_tandem(base_key: *const c_char, vals: *const *const c_void, lens: *const usize,
+    pub fn splinter_client_set_tandem(base_key: *const c_char, vals: *mut *const c_void, lens: *const usize,
                                       orders: u8) -> c_int;
     pub fn splinter_client_unset_tandem(base_key: *const c_char, orders: u8);
     // signals

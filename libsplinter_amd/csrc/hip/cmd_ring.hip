@@ -90,10 +90,13 @@ __device__ void push(uint8_t* dst, const uint4* src, uint32_t n16) {
   }
 }
 
+// The event-bus wakeup of a per-call mutation is raised by the calling host thread once the call
+// returns (HbmStore::notify_host: the eventfd directly in the owner, the shared notify word
+// elsewhere), so the worker does not raise the device notify too: that second, proxied signal
+// would land up to a proxy period later and wake a waiter that has already drained the first.
 __device__ __forceinline__ void count_mutation(const Arena& a, long idx) {
   aadd64(&a.hdr()->epoch, 1);
   if (idx >= 0) mark_dirty(a, (size_t)idx);
-  notify_host(a);
 }
 
 #ifdef SPL_RING_STAMPS

@@ -172,7 +172,10 @@ class HbmStore final : public StoreBase {
     if (!key) return -2;
     RingResult r;
     if (ring(kRingUnset, 0, key, nullptr, 0, 0, nullptr, 0, &r) != 0) return -1;
-    if (r.status >= 0) return r.status;
+    if (r.status >= 0) {
+      notify_host();
+      return r.status;
+    }
     errno = neg_to_errno(r.status);
     return -1;
   }

@@ -290,7 +290,10 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // tiles past the block's last row are skipped, the diagonal tiles masked per score.  kv_heads <
 // heads: grouped-query attention, q head h reads kv head h / (heads / kv_heads); the qkv rows are
 // [q (heads) | k (kv_heads) | v (kv_heads)] x HD.
-template <int W, bool XR = false, bool OPT = false, bool CAUSAL = false, int KT = 64, int QW = 4>
+// LATE: the next tile's K/V global loads are issued after this tile's S^T = K Q^T MFMAs instead of
+// before them (the split async stage of cdna_hip_programming.md T14: the loads' issue no longer sits
+// between the barrier and the first MFMA, and their registers are live for half the tile).
+template <int W, bool XR = false, bool OPT = false, bool CAUSAL = false, int KT = 64, int QW = 4, bool LATE = false>
 __global__ __launch_bounds__(64 * QW) __attribute__((amdgpu_waves_per_eu(W > 0 ? W : 1))) void k_attn2(
     const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
@@ -378,7 +381,7 @@ __global__ __launch_bounds__(64 * QW) __attribute__((amdgpu_waves_per_eu(W > 0 ?
   for (int t = 0; t < ntiles; ++t) {
     const int buf = t & 1;
     const long k0 = (long)t * KT;
-    if (t + 1 < ntiles) gload(k0 + KT);
+    if (!LATE && t + 1 < ntiles) gload(k0 + KT);
     const char* Ks = lds[buf][0];
     const char* Vs = lds[buf][1];
     // ---- S^T = K Q^T
@@ -397,6 +400,7 @@ __global__ __launch_bounds__(64 * QW) __attribute__((amdgpu_waves_per_eu(W > 0 ?
           s[kb][qb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[kk], qf[qb][kk], s[kb][qb], 0, 0, 0);
       }
     }
+    if (LATE && t + 1 < ntiles) gload(k0 + KT);
     // ---- online softmax, one query per lane column.  Max on the raw scores (scale > 0), one
     // FMA per score into the exp2 domain, raw v_exp_f32 (no denormal fix-up: p underflows to 0),
     // key mask only on the sequence's partial last tile, and the deferred rescale of T13
@@ -742,6 +746,15 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 8)  // 128-key tiles held to 2 waves/SIMD
     hipLaunchKernelGGL((k_attn2<2, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
+                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 10)  // 6 with the next tile's loads after the QK^T MFMAs
+    hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 4, true>), dim3(nqb * heads), dim3(256), 0, s,
+                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 11)  // 7 (128-key tiles) with late loads
+    hipLaunchKernelGGL((k_attn2<0, true, true, false, 128, 4, true>), dim3(nqb * heads), dim3(256), 0, s,
+                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 12)  // 9 (8 waves, 256-row q-blocks) with late loads
+    hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 8, true>), dim3(nqb * heads), dim3(512), 0, s,
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 4)
     hipLaunchKernelGGL((k_attn2<0, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,

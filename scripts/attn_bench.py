@@ -28,7 +28,7 @@ def main():
     cur = {"v": 6}
 
     def run():
-        b = b256 if cur["v"] == 9 else b128
+        b = b256 if cur["v"] in (9, 12) else b128
         _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
                                0.125, _stream()), "attn")
 

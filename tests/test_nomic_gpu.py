@@ -213,7 +213,7 @@ def test_gemm_layernorm_fold_modes(L):
                            None, 0, None, 0, eps, None, None, None, None, None, _stream()) != 0
 
 
-@pytest.mark.parametrize("variant", [9, 7, 6, 5, 4, 3, 2, 1])
+@pytest.mark.parametrize("variant", [12, 11, 10, 9, 7, 6, 5, 4, 3, 2, 1])
 @pytest.mark.parametrize("spike", [False, True])
 def test_attention_varlen(L0, variant, spike):
     L = L0
@@ -221,7 +221,7 @@ def test_attention_varlen(L0, variant, spike):
     from libsplinter_amd.models.nomic import Batch, _chk, _stream
     torch.manual_seed(2)
     lens = [1, 17, 64, 65, 127, 128, 129, 200, 513]
-    b = Batch([[0] * n for n in lens], qblock=256 if variant == 9 else 128)  # variant 9: 8 waves, 256 rows
+    b = Batch([[0] * n for n in lens], qblock=256 if variant in (9, 12) else 128)  # 9, 12: 8 waves, 256 rows
     T = b.T
     qkv = torch.randn(b.T_pad, 3 * 768, device="cuda").bfloat16()
     if spike:  # a late key that dominates one query's row: forces the online-max rescale path

@@ -322,3 +322,91 @@ def test_chunked_uneven_all_to_all_gloo(world):
                 p.kill()
     for r in range(world):
         assert res.get(r) == "ok", res.get(r)
+
+
+def _routed_step_worker(rank, world, port, base, q, steps, n):
+    """The routed step of bench.py at N > 1 (pack -> request all-to-alls -> owner runs -> response
+    all-to-alls -> gather), software-pipelined as there: step i's requests are issued before step
+    i-1's responses are gathered.  Each step sets n new keys and gets n keys set by OTHER ranks in
+    earlier steps; at the end every get must have returned its key's value (integrity 0)."""
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from libsplinter_amd import Store, unlink
+        from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
+        from libsplinter_amd.parallel.sharded import HostShard
+        name = f"{base}_w{rank}"
+        st = Store.create(name, slots=8192, max_val=64, embeddings=False)
+        rk = RoutedKV(HostShard(st), resp_group=dist.new_group(backend="gloo"))
+        cap = route_capacity(n, world)
+
+        def val(k):
+            return f"v:{k}".encode()
+
+        pending, checked, bad = None, 0, 0
+        for i in range(steps + 1):
+            cur = None
+            if i < steps:
+                sk = [f"s{i}_r{rank}_{j}" for j in range(n)]
+                K = _keys(sk)
+                V, L = _vals([val(k) for k in sk])
+                so = rk.begin_set(K, V, L, cap, 32)
+                go = None
+                if i >= 2:  # keys another rank set two steps ago: already finished everywhere
+                    src = (rank + 1 + i) % world
+                    gk = [f"s{i - 2}_r{src}_{j}" for j in range(n)]
+                    go = rk.begin_get(_keys(gk), cap, 32)
+                rk.execute(so)
+                if go is not None:
+                    rk.execute(go)
+                cur = (so, go, gk if go is not None else None)
+            if pending is not None:  # the previous step's responses, after this step's requests
+                pso, pgo, pgk = pending
+                rk.respond(pso)
+                s = rk.finish(pso)
+                bad += int((s != 0).sum())
+                if pgo is not None:
+                    rk.respond(pgo)
+                    gs, gv, gl = rk.finish(pgo)
+                    for j, k in enumerate(pgk):
+                        ok = int(gs[j]) == 0 and bytes(gv[j, : gl[j]].numpy()) == val(k)
+                        bad += 0 if ok else 1
+                        checked += 1
+            pending = cur
+            dist.barrier()
+        q.put((rank, f"ok {checked} {bad}"))
+        st.close()
+        unlink(name)
+        dist.destroy_process_group()
+    except Exception:
+        import traceback
+        q.put((rank, traceback.format_exc()))
+        raise
+
+
+def test_routed_step_world8_rehearsal(uniq):
+    """World-8 CPU rehearsal of bench.py's routed step (one process per 'GPU', gloo over 127.0.0.1)."""
+    world, steps, n = 8, 6, 150
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    ps = [ctx.Process(target=_routed_step_worker, args=(r, world, port, uniq, q, steps, n)) for r in range(world)]
+    for p in ps:
+        p.start()
+    res = {}
+    try:
+        for _ in range(world):
+            r, msg = q.get(timeout=400)
+            res[r] = msg
+            if not msg.startswith("ok"):
+                break
+    finally:
+        for p in ps:
+            p.join(timeout=30)
+            if p.is_alive():
+                p.kill()
+    for r in range(world):
+        assert res.get(r, "").startswith("ok"), res.get(r)
+        _, checked, bad = res[r].split()
+        assert int(checked) == (steps - 2) * n and int(bad) == 0, res[r]

@@ -14,7 +14,9 @@
 #include <cstring>
 #include <immintrin.h>
 #include <sched.h>
+#include <sys/prctl.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "arena_dev.hpp"
 #include "cmd_ring.hpp"
@@ -528,6 +530,27 @@ inline int env_int(const char* n, int d) {
   return e ? atoi(e) : d;
 }
 
+// CPUs this process may actually run on at once: its affinity mask, capped by a cgroup-v2 CPU
+// quota (cpu.max "quota period"; the GPU boxes grant a share of the machine this way, so the
+// affinity mask alone overstates it).  SPLINTER_RING_CPUS overrides.
+int effective_cpus() {
+  if (const char* e = getenv("SPLINTER_RING_CPUS")) return atoi(e) > 0 ? atoi(e) : 1;
+  cpu_set_t set;
+  int n = sched_getaffinity(0, sizeof set, &set) == 0 ? CPU_COUNT(&set) : 0;
+  if (n <= 0) n = (int)sysconf(_SC_NPROCESSORS_ONLN);
+  if (FILE* f = fopen("/sys/fs/cgroup/cpu.max", "r")) {
+    char q[32] = {0};
+    long period = 0;
+    if (fscanf(f, "%31s %ld", q, &period) == 2 && strcmp(q, "max") != 0 && period > 0) {
+      const long quota = atol(q);
+      const int cap = (int)((quota + period - 1) / period);
+      if (cap > 0 && cap < n) n = cap;
+    }
+    fclose(f);
+  }
+  return n > 0 ? n : 1;
+}
+
 }  // namespace
 
 int CmdRing::init(int device, uint32_t pstride) {
@@ -548,6 +571,7 @@ int CmdRing::init(int device, uint32_t pstride) {
   idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
   spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
   yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
+  cpus_ = effective_cpus();
   return 0;
 }
 
@@ -627,16 +651,38 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   __atomic_store_n(&shared_->state[e], (uint32_t)kRingReady, __ATOMIC_RELEASE);
   if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);
   clock_gettime(CLOCK_MONOTONIC, &t0);
-  // Wait for completion: spin (a call is served in ~10 us), then give the CPU away between polls --
-  // with more caller threads than CPUs, spinning waiters starve the callers whose completions have
-  // already landed (the 16 -> 32 thread collapse of profiles/r2_hostapi_ring_v3.md)
-  const uint64_t spin_us = yield_after_us_;
+  // Wait for completion: spin (a call is served in ~10 us), then give the CPU away between polls.
+  // With more waiting callers than CPUs the process may run on (cgroup quota included), spinning
+  // burns the quota every waiter shares -- the scheduler then throttles the whole process, the
+  // 16 -> 32 thread collapse of profiles/r2_hostapi_ring_v3.md -- so the waiters beyond the CPU
+  // count sleep ~2 us between polls (1 us timer slack) instead of spinning or yielding.
+  const int waiting = waiters_.fetch_add(1, std::memory_order_relaxed) + 1;
+  const bool oversub = waiting > cpus_;
+  const uint64_t spin_us = oversub ? 2 : yield_after_us_;
+  if (oversub) {
+    static thread_local bool slack = false;
+    if (!slack) {
+      (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+      slack = true;
+    }
+  }
+  struct Leave {
+    std::atomic<int>& w;
+    ~Leave() { w.fetch_sub(1, std::memory_order_relaxed); }
+  } leave{waiters_};
   for (uint64_t spins = 1;; ++spins) {
     if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == kRingDone) break;
     _mm_pause();
     if ((spins & 31) == 0) {
       const uint64_t us = elapsed_us();
-      if (us > spin_us) sched_yield();
+      if (us > spin_us) {
+        if (oversub) {
+          const timespec ts{0, 2000};
+          nanosleep(&ts, nullptr);
+        } else {
+          sched_yield();
+        }
+      }
       if ((spins & 1023) == 0) {
         if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);  // worker idled out meanwhile
         if (us > 30000000u) {  // the GPU stopped serving: abandon the entry (reclaimed once done)

@@ -128,6 +128,8 @@ class CmdRing {
   int clock_khz_ = 100000;
   bool spread_ = true;            // SPLINTER_RING_SPREAD: consecutive calls on different waves
   uint64_t yield_after_us_ = 20;  // SPLINTER_RING_SPIN_US: spin this long, then yield between polls
+  int cpus_ = 1;                  // CPUs the process may run on (affinity, cgroup quota)
+  std::atomic<int> waiters_{0};   // host threads waiting on a completion right now
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;
   std::atomic<uint32_t> busy_[kRingEntries] = {};

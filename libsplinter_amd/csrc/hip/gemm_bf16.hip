@@ -1121,7 +1121,10 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     }
     return (int)hipGetLastError();
   }
-  if (p_ok && fits && K >= 2 * BK && (var == 512 || var == 513 || (var == 0 && many))) {
+  // auto no longer takes the persistent kernel: on the encoder's SwiGLU shape (3072 tiles) the
+  // launch-per-tile k_gemm256 measured 1064 TFLOP/s against 1015 (1046 with ILV 2) for k_gemm_p
+  // (profiles/r3_gemm_ilv_ab.jsonl); NOMIC_GEMM=512 keeps it selectable
+  if (p_ok && fits && K >= 2 * BK && (var == 512 || var == 513)) {
     static bool attr_p = [] {
       allow_lds(k_gemm_p<MODE, true>, 2 * kBufBytes);
       allow_lds(k_gemm_p<MODE, true, false, 1>, 2 * kBufBytes);

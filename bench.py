@@ -114,9 +114,10 @@ def _launch_ranks(args) -> int:
 
 
 def _timed_region_profiler():
-    """SPL_PROFILE_TIMED=1: roctxProfilerResume/Pause around the timed steps, so that
-    `rocprofv3 --selected-regions --kernel-trace --stats -- python3 bench.py ...` traces exactly the
-    timed region (which kernels run in the measured step, and nothing from setup or warm-up)."""
+    """SPL_PROFILE_TIMED=1: roctxProfilerResume/Pause around the timed steps (for
+    `rocprofv3 --selected-regions`), and the region's bounds printed to stderr in the monotonic and
+    boot-time clocks, so a full `rocprofv3 --kernel-trace` can be cut to exactly the timed steps
+    (scripts/trace_window.py): which kernels run in the measured step, nothing from setup or warm-up."""
     if os.environ.get("SPL_PROFILE_TIMED") != "1":
         return lambda on: None
     import ctypes
@@ -127,6 +128,10 @@ def _timed_region_profiler():
         import torch
         torch.cuda.synchronize()
         (lib.roctxProfilerResume if on else lib.roctxProfilerPause)(0)
+        # the region's bounds in both host clocks a kernel trace may be stamped in, so a full trace
+        # can be cut to the timed steps afterwards (scripts/trace_window.py)
+        print(json.dumps({"timed_region": "begin" if on else "end", "monotonic_ns": time.monotonic_ns(),
+                          "boottime_ns": time.clock_gettime_ns(time.CLOCK_BOOTTIME)}), file=sys.stderr, flush=True)
     return toggle
 
 

@@ -475,7 +475,9 @@ int g_rln_variant = -1;
 int rln_variant() {
   if (g_rln_variant < 0) {
     const char* e = getenv("NOMIC_RLN");
-    g_rln_variant = e && *e ? atoi(e) : 222;  // [ILV * 100 +] PIPE * 10 + EPI (222: profiles/r3_rln_ab.jsonl)
+    // PIPE * 10 + EPI (no DMA interleave), or 200 + PIPE * 10 + ILV (EPI 0), + 1000 for the identity-MFMA
+    // residual (EPI 2), + 2000 for the 2-pair W prefetch (PF 2); 222 = PIPE 2, ILV 2: profiles/r3_rln_variants_ab.jsonl
+    g_rln_variant = e && *e ? atoi(e) : 222;
   }
   return g_rln_variant;
 }

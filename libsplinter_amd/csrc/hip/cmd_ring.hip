@@ -654,18 +654,10 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   // Wait for completion: spin (a call is served in ~10 us), then give the CPU away between polls.
   // With more waiting callers than CPUs the process may run on (cgroup quota included), spinning
   // burns the quota every waiter shares -- the scheduler then throttles the whole process, the
-  // 16 -> 32 thread collapse of profiles/r2_hostapi_ring_v3.md -- so the waiters beyond the CPU
-  // count sleep ~2 us between polls (1 us timer slack) instead of spinning or yielding.
-  const int waiting = waiters_.fetch_add(1, std::memory_order_relaxed) + 1;
-  const bool oversub = waiting > cpus_;
-  const uint64_t spin_us = oversub ? 2 : yield_after_us_;
-  if (oversub) {
-    static thread_local bool slack = false;
-    if (!slack) {
-      (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
-      slack = true;
-    }
-  }
+  // 16 -> 32 thread collapse of profiles/r2_hostapi_ring_v3.md -- so while more callers wait than
+  // there are CPUs every waiter sleeps ~2 us between polls (1 us timer slack): the calls stay in
+  // flight on the GPU without holding a CPU each.
+  waiters_.fetch_add(1, std::memory_order_relaxed);
   struct Leave {
     std::atomic<int>& w;
     ~Leave() { w.fetch_sub(1, std::memory_order_relaxed); }
@@ -675,8 +667,16 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     _mm_pause();
     if ((spins & 31) == 0) {
       const uint64_t us = elapsed_us();
-      if (us > spin_us) {
+      // re-decided every poll round: once more callers wait than there are CPUs, EVERY waiter
+      // (also those that started spinning before the others arrived) sleep-polls
+      const bool oversub = waiters_.load(std::memory_order_relaxed) > cpus_;
+      if (us > (oversub ? 2u : yield_after_us_)) {
         if (oversub) {
+          static thread_local bool slack = false;
+          if (!slack) {
+            (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
+            slack = true;
+          }
           const timespec ts{0, 2000};
           nanosleep(&ts, nullptr);
         } else {

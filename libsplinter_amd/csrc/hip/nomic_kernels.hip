@@ -523,6 +523,182 @@ __global__ __launch_bounds__(64 * QW) __attribute__((amdgpu_waves_per_eu(W > 0 ?
   }
 }
 
+// ------------------------------------------------- attention, 32x32 MFMA form --
+// k_attn3: the encoder's varlen attention (hd 64, non-causal) on v_mfma_f32_32x32x16_bf16.  One
+// 256-thread workgroup = 128 query rows of one (sequence, head), 4 waves x 32 rows; per 64-key tile:
+//   S^T = K Q^T   two 32-key blocks x four 16-d steps = 8 MFMAs.  With the 32x32 C layout a lane
+//                 holds, for its query q = lane & 31, the keys crow(r, hi) = (r&3) + 8(r>>2) + 4hi of
+//                 each block (hi = lane >> 5): 32 scores, so the row max / sum are 31 in-lane ops
+//                 and ONE permlane32 swap (the 16x16 form needs two swaps per 16-row block);
+//   O^T += V^T P^T the MFMA's k index is mapped to keys in the order the lane already holds them:
+//                 k-slot j of half hi <-> key 16s + (j&3) + 8(j>>2) + 4hi, so the bf16 P fragment
+//                 of step s is the lane's own s[8s .. 8s+7] (no permute), and the matching V^T
+//                 fragment is two ds_read_b64_tr_b16 of 4 consecutive key rows (4hi and 8+4hi).
+// LDS images (64 keys x 128 B, double-buffered, register-staged one tile ahead as in k_attn2):
+//   K chunks XOR (key >> 1) & 7: each 16-lane b128 group (16 distinct rows, one chunk) covers all
+//   16 bank quads; V chunks XOR ((key >> 1) & 1) << 2: the four rows a 32-lane transposing read
+//   touches land on four different 64-B quarters of the bank space.
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ int k3sw(int key, int c) { return c ^ ((key >> 1) & 7); }
+__device__ __forceinline__ int v3sw(int key, int c) { return c ^ (((key >> 1) & 1) << 2); }
+
+__global__ __launch_bounds__(256) void k_attn3(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                               const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
+                                               int heads, float scale_log2) {
+  constexpr int KT = 64, NT = 256, NL = KT * 8 / NT;
+  __shared__ __attribute__((aligned(16))) char lds[2][2][KT * 128];  // [buf][K | V][key * 128 B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hi = lane >> 5, q32 = lane & 31, li = lane & 15, tq = li >> 2, tp = li & 3;
+  // bijective XCD remap (the q-blocks of one (sequence, head) share an XCD's L2)
+  const int nwg = gridDim.x, orig = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int nqb = nwg / heads, head = lid / nqb, qbi = lid - head * nqb;
+  const int seq = qblocks[2 * qbi], qstart = qblocks[2 * qbi + 1];
+  const long s0 = cu[seq], len = cu[seq + 1] - s0;
+  const long ld = 3L * heads * HD;
+  const uint16_t* Qg = qkv + head * HD;
+  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
+  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
+
+  const long qrow = qstart + wave * 32 + q32;
+  bf16x8 qf[4];  // B operand: Q[q][16 ks + 8 hi .. +7]
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = qrow < len ? *(const bf16x8*)(Qg + (s0 + qrow) * ld + ks * 16 + hi * 8) : bf16x8{};
+  f32x16 o[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m = -1e30f, l = 0.f;
+
+  uint4 rk[NL], rv[NL];
+  auto gload = [&](long k0) {
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
+      if (k0 + key < len) {
+        rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
+        rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
+      } else {
+        rk[it] = make_uint4(0, 0, 0, 0);
+        rv[it] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lwrite = [&](int buf) {
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
+      *(uint4*)(lds[buf][0] + key * 128 + (k3sw(key, ch) << 4)) = rk[it];
+      *(uint4*)(lds[buf][1] + key * 128 + (v3sw(key, ch) << 4)) = rv[it];
+    }
+  };
+
+  const int ntiles = (int)((len + KT - 1) / KT);
+  gload(0);
+  lwrite(0);
+  __syncthreads();
+  for (int t = 0; t < ntiles; ++t) {
+    const int buf = t & 1;
+    const long k0 = (long)t * KT;
+    if (t + 1 < ntiles) gload(k0 + KT);
+    const char* Ks = lds[buf][0];
+    const char* Vs = lds[buf][1];
+    // ---- S^T = K Q^T: A = K rows (key kb*32 + q32, d 16 ks + 8 hi), B = Q^T
+    f32x16 s[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
+      const int row = kb * 32 + q32;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + row * 128 + (k3sw(row, 2 * ks + hi) << 4));
+        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
+      }
+    }
+    // ---- online softmax of query q32 over the tile's 64 keys (32 here, 32 in lane ^ 32)
+    if (k0 + KT > len) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= len) s[kb][r] = -1e30f;
+    }
+    float mx = fmaxf(s[0][0], s[1][0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));
+    {
+      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+    }
+    constexpr float kThr = 8.f;
+    const float mxs = mx * scale_log2;
+    if (!__all(mxs - m <= kThr)) {  // wave-uniform deferred rescale (as k_attn2)
+      const float mn = fmaxf(m, mxs);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) o[db] *= alpha;
+    }
+    const float nm = -m;
+    float ps = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][r], scale_log2, nm));
+        s[kb][r] = p;
+        ps += p;
+      }
+    {
+      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(ps), __float_as_uint(ps), false, false);
+      ps = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+    }
+    l += ps;
+    // ---- O^T += V^T P^T, four 16-key steps
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[kb][8 * st + j];
+        const int rowA = kb * 32 + 16 * st + 4 * hi + tq, rowB = rowA + 8;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int col = 32 * db + 16 * ((lane >> 4) & 1) + 4 * tp;
+          const int ch = col >> 3, off = (col & 7) * 2;
+          const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4i16*)(Vs + rowA * 128 + (v3sw(rowA, ch) << 4) + off));
+          const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4i16*)(Vs + rowB * 128 + (v3sw(rowB, ch) << 4) + off));
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, (v8i16)__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
+        }
+      }
+    if (t + 1 < ntiles) lwrite(buf ^ 1);
+    __syncthreads();
+  }
+  // ---- normalise; lane holds d = 32 db + 8 g + 4 hi + 0..3 (g = r >> 2) of query q32
+  if (qrow < len) {
+    const float inv = 1.f / l;
+    uint16_t* dst = out + (s0 + qrow) * (long)heads * HD + head * HD;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 w;
+        w.x = pk2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv);
+        w.y = pk2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+        *(uint2*)(dst + 32 * db + 8 * g + 4 * hi) = w;
+      }
+  }
+}
+
 // ------------------------------------------------------------ mean pool --
 __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, const int32_t* __restrict__ cu,
                                               float* __restrict__ pooled, int normalize, spl_arena_t aa,
@@ -747,6 +923,9 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   else if (g_attn_variant == 8)  // 128-key tiles held to 2 waves/SIMD
     hipLaunchKernelGGL((k_attn2<2, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 13)  // 32x32x16 MFMA form (k_attn3)
+    hipLaunchKernelGGL(k_attn3, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+                       qblocks, heads, scale_log2);
   else if (g_attn_variant == 10)  // 6 with the next tile's loads after the QK^T MFMAs
     hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 4, true>), dim3(nqb * heads), dim3(256), 0, s,
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);

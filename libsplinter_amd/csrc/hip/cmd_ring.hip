@@ -217,8 +217,10 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
                                uint64_t arg, uint8_t* hp, uint8_t* pay, uint32_t* out_len, uint64_t* result);
 
 // one op of one lane; scratch = this entry's device staging row (payload)
-__device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t* pay, uint32_t* out_len,
-                         uint64_t* result, uint64_t* t_loaded) {
+// c / hin: the request record and input payload (host memory, or device memory the host writes
+// through the BAR in the VRAM mode); hp: the output payload (host memory)
+__device__ int32_t serve(const spl_arena_t& aa, const RingCmd* c, const uint8_t* hin, uint8_t* hp, uint8_t* pay,
+                         uint32_t* out_len, uint64_t* result, uint64_t* t_loaded) {
   // the two header words every op needs (event-bus owner, mop flags) are loaded first, so their
   // device round trip overlaps the record's host round trip below
   const splinter_header* H = (const splinter_header*)aa.base;
@@ -232,7 +234,7 @@ __device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t
 #pragma unroll
   for (int q = 0; q < 4; ++q) kk[q] = ld16s(c->key + 16 * q);
 #pragma unroll
-  for (uint32_t q = 0; q < kSpec; ++q) sp.c[q] = ld16s(hp + 16 * q);
+  for (uint32_t q = 0; q < kSpec; ++q) sp.c[q] = ld16s(hin + 16 * q);
   sys_wait(h0);
   sys_wait(h1);
   sys_wait(h3);
@@ -267,7 +269,7 @@ __device__ int32_t serve(const spl_arena_t& aa, RingCmd* c, uint8_t* hp, uint8_t
 #pragma unroll
     for (uint32_t q = 0; q < kSpec; ++q)
       if (q < n16) ((uint4*)pay)[q] = make_uint4(sp.c[q].x, sp.c[q].y, sp.c[q].z, sp.c[q].w);
-    if (n16 > kSpec) pull((uint4*)pay, hp, kSpec, n16);
+    if (n16 > kSpec) pull((uint4*)pay, hin, kSpec, n16);
     drain();  // the staged payload is in place before any op reads it
   }
   // the key is canonical with its hash computed by the host (KeyRef)
@@ -413,9 +415,17 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
 // Workgroup g serves entries g*kGroupEntries + lane (lanes 0..kGroupEntries-1).
 // ctrl (device): [0] u64 wall clock of the last served call (any group), [8] u32 dying,
 // [12] u32 live waves (set to gridDim.x by the launcher).
-__global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmds, RingShared* sh, uint8_t* payload,
-                                                    uint32_t pstride, uint8_t* scratch, uint8_t* ctrl,
-                                                    uint64_t idle_ticks) {
+// VR (VRAM requests): records, input payloads and doorbells live in device memory that the host
+// writes through the PCIe BAR (posted writes), so the worker polls and loads them locally instead
+// of over PCIe; a doorbell is the entry's call sequence number (host-written only, never reset: a
+// call is new when it differs from the lane's last served number, kept in `served` across
+// relaunches), and the completion -- status words, output payload, DONE = the same number -- goes
+// to host memory as in the host mode.
+template <bool VR>
+__global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmds, RingCmd* hcmds, RingShared* sh,
+                                                    const uint32_t* vdoor, const uint8_t* payload_in,
+                                                    uint8_t* payload, uint32_t pstride, uint8_t* scratch,
+                                                    uint8_t* ctrl, uint32_t* served, uint64_t idle_ticks) {
   const int lane = threadIdx.x, g = blockIdx.x;
   const bool mine = lane < kGroupEntries;
   const int e = g * kGroupEntries + (mine ? lane : 0);
@@ -424,10 +434,17 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
 #endif
   uint64_t last = wall_clock64();
   uint32_t idle = 0;
-  const uint32_t* door = &sh->state[e];
+  const uint32_t* door = VR ? &vdoor[e] : &sh->state[e];
+  uint32_t seen = VR && mine ? served[e] : 0u, bell = 0u;
   for (;;) {
 #ifndef SPL_RING_POLL4
-    const bool ready = mine && ld32s(door) == kRingReady;
+    bool ready;
+    if constexpr (VR) {
+      bell = mine ? ld32s(door) : 0u;
+      ready = mine && bell != seen;
+    } else {
+      ready = mine && ld32s(door) == kRingReady;
+    }
 #else
     // (measured variant, slower: profiles/r2_hostapi_ring_v3.md) 4 doorbell reads in flight,
     // issued ~1/4 of a host round trip apart, so a doorbell is seen one round trip + a fraction
@@ -489,14 +506,14 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
       RingCmd* c = cmds + e;
       uint32_t out_len = 0;
       uint64_t result = 0, t_loaded = 0;
-      const int32_t st =
-          serve(aa, c, payload + (size_t)e * pstride, scratch + (size_t)e * pstride, &out_len, &result, &t_loaded);
+      const int32_t st = serve(aa, c, (VR ? payload_in : payload) + (size_t)e * pstride, payload + (size_t)e * pstride,
+                               scratch + (size_t)e * pstride, &out_len, &result, &t_loaded);
 #ifdef SPL_RING_STAMPS
       const uint64_t t_op = wall_clock64();
 #endif
       // status, out_len and result share one 16-B chunk of the record: one system-scope store,
       // one drain (it also covers a get's payload stores) before the DONE doorbell
-      st16s(&c->status, u32x4s_t{(uint32_t)st, out_len, (uint32_t)result, (uint32_t)(result >> 32)});
+      st16s(VR ? &hcmds[e].status : &c->status, u32x4s_t{(uint32_t)st, out_len, (uint32_t)result, (uint32_t)(result >> 32)});
       drain();
 #ifdef SPL_RING_STAMPS
       const uint64_t t_done = wall_clock64();
@@ -516,7 +533,13 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
       }
       drain();
 #endif
-      st32s(&sh->state[e], kRingDone);
+      if constexpr (VR) {
+        seen = bell;
+        served[e] = bell;  // read by the next launch only (kernel boundary)
+        st32s(&sh->state[e], bell);
+      } else {
+        st32s(&sh->state[e], kRingDone);
+      }
     }
   }
   drain();
@@ -572,6 +595,32 @@ int CmdRing::init(int device, uint32_t pstride) {
   spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
   yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
   cpus_ = effective_cpus();
+#ifndef SPL_RING_POLL4
+  if (env_int("SPLINTER_RING_VRAM", 0) != 0 && init_vram() != 0) vr_ = false;  // host-memory mode
+#endif
+  return 0;
+}
+
+// The request side in device memory: one VMM chunk (2 MiB granules) exported as a dmabuf and
+// mapped on the CPU through the PCIe BAR (VmmArena::host_map, profiles/r2_hbm_host_map.md):
+// [doorbells 4 KiB | records 32 KiB | input payloads kRingEntries x pstride].
+int CmdRing::init_vram() {
+  const size_t door_b = 4096, cmd_b = sizeof(RingCmd) * kRingEntries, pay_b = (size_t)pstride_ * kRingEntries;
+  if (vram_.create(device_, door_b + cmd_b + pay_b, 2u << 20) != 0) return -1;
+  uint8_t* h = (uint8_t*)vram_.host_map();
+  if (!h) return -1;
+  uint8_t* d = (uint8_t*)vram_.base();
+  if (hipMemset(d, 0, door_b + cmd_b) != hipSuccess) return -1;
+  if (hipMalloc((void**)&served_, sizeof(uint32_t) * kRingEntries) != hipSuccess) return -1;
+  if (hipMemset(served_, 0, sizeof(uint32_t) * kRingEntries) != hipSuccess) return -1;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  v_door_h_ = (uint32_t*)h;
+  v_cmds_h_ = (RingCmd*)(h + door_b);
+  v_pay_h_ = h + door_b + cmd_b;
+  v_door_d_ = (uint32_t*)d;
+  v_cmds_d_ = (RingCmd*)(d + door_b);
+  v_pay_d_ = d + door_b + cmd_b;
+  vr_ = true;
   return 0;
 }
 
@@ -591,8 +640,13 @@ void CmdRing::launch(const spl_arena_t& a) {
   // stream order: the previous worker (if still draining) has exited before ctrl is reset
   const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)kRingGroups};
   (void)hipMemcpyAsync(ctrl_, init, sizeof init, hipMemcpyHostToDevice, stream_);
-  hipLaunchKernelGGL(k_ring_worker, dim3(kRingGroups), dim3(64), 0, stream_, a, cmds_, shared_, payload_, pstride_,
-                     scratch_, ctrl_, idle_ticks_);
+  if (vr_)
+    hipLaunchKernelGGL(k_ring_worker<true>, dim3(kRingGroups), dim3(64), 0, stream_, a, v_cmds_d_, cmds_, shared_,
+                       v_door_d_, v_pay_d_, payload_, pstride_, scratch_, ctrl_, served_, idle_ticks_);
+  else
+    hipLaunchKernelGGL(k_ring_worker<false>, dim3(kRingGroups), dim3(64), 0, stream_, a, cmds_, cmds_, shared_,
+                       (const uint32_t*)nullptr, (const uint8_t*)nullptr, payload_, pstride_, scratch_, ctrl_,
+                       (uint32_t*)nullptr, idle_ticks_);
   if (cur != device_) (void)hipSetDevice(cur);
 }
 
@@ -623,9 +677,10 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     if (busy_[e].compare_exchange_weak(z, 1u, std::memory_order_acquire)) break;
     // an entry a timed-out caller abandoned (busy 2) is reclaimed once the worker has finished it
     z = 2;
-    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == kRingDone &&
+    const uint32_t done_word = vr_ ? seqs_[e] : (uint32_t)kRingDone;
+    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == done_word &&
         busy_[e].compare_exchange_strong(z, 1u, std::memory_order_acquire)) {
-      __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
+      if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
       break;
     }
     e = entry_of(++t);
@@ -639,16 +694,40 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     }
   }
   RingCmd* c = cmds_ + e;
-  c->op = op;
-  c->sub = sub;
-  c->len = in_len;
-  c->cap = out_cap ? (out_cap < pstride_ ? out_cap : pstride_) : pstride_;
-  c->arg = arg;
-  c->khash = khash;
-  c->klen = klen;
-  if (key64) std::memcpy(c->key, key64, 64);
-  if (in && in_len) std::memcpy(payload_ + (size_t)e * pstride_, in, in_len);
-  __atomic_store_n(&shared_->state[e], (uint32_t)kRingReady, __ATOMIC_RELEASE);
+  uint32_t done_word = kRingDone;
+  if (vr_) {
+    // the record is assembled locally and copied to the device-memory record with wide stores
+    // (the BAR mapping is write-combining): payload, record, sfence, then the doorbell
+    RingCmd rc{};
+    rc.op = op;
+    rc.sub = sub;
+    rc.len = in_len;
+    rc.cap = out_cap ? (out_cap < pstride_ ? out_cap : pstride_) : pstride_;
+    rc.arg = arg;
+    rc.khash = khash;
+    rc.klen = klen;
+    if (key64) std::memcpy(rc.key, key64, 64);
+    if (in && in_len) std::memcpy(v_pay_h_ + (size_t)e * pstride_, in, in_len);
+    std::memcpy((void*)(v_cmds_h_ + e), &rc, sizeof rc);
+    uint32_t seq = seqs_[e] + 1;
+    if (seq == 0) seq = 1;  // 0 is the initial "served" value
+    seqs_[e] = seq;
+    done_word = seq;
+    _mm_sfence();
+    *(volatile uint32_t*)(v_door_h_ + e) = seq;
+    _mm_sfence();
+  } else {
+    c->op = op;
+    c->sub = sub;
+    c->len = in_len;
+    c->cap = out_cap ? (out_cap < pstride_ ? out_cap : pstride_) : pstride_;
+    c->arg = arg;
+    c->khash = khash;
+    c->klen = klen;
+    if (key64) std::memcpy(c->key, key64, 64);
+    if (in && in_len) std::memcpy(payload_ + (size_t)e * pstride_, in, in_len);
+    __atomic_store_n(&shared_->state[e], (uint32_t)kRingReady, __ATOMIC_RELEASE);
+  }
   if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);
   clock_gettime(CLOCK_MONOTONIC, &t0);
   // Wait for completion: spin (a call is served in ~10 us), then give the CPU away between polls.
@@ -663,7 +742,7 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     ~Leave() { w.fetch_sub(1, std::memory_order_relaxed); }
   } leave{waiters_};
   for (uint64_t spins = 1;; ++spins) {
-    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == kRingDone) break;
+    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == done_word) break;
     _mm_pause();
     if ((spins & 31) == 0) {
       const uint64_t us = elapsed_us();
@@ -700,7 +779,7 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   r->result = c->result;
   if (out && out_cap && r->out_len && r->status >= 0)
     std::memcpy(out, payload_ + (size_t)e * pstride_, r->out_len < out_cap ? r->out_len : out_cap);
-  __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
+  if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
   busy_[e].store(0, std::memory_order_release);
   return 0;
 }
@@ -742,6 +821,7 @@ CmdRing::~CmdRing() {
   }
 #endif
   if (stream_) (void)hipStreamDestroy(stream_);
+  if (served_) (void)hipFree(served_);
   if (ctrl_) (void)hipFree(ctrl_);
   if (scratch_) (void)hipFree(scratch_);
   if (payload_) (void)hipHostFree(payload_);

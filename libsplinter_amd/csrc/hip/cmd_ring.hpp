@@ -39,6 +39,7 @@
 #include <mutex>
 
 #include "arena_api.h"
+#include "vmm_share.hpp"
 
 namespace spl {
 
@@ -129,6 +130,20 @@ class CmdRing {
   bool spread_ = true;            // SPLINTER_RING_SPREAD: consecutive calls on different waves
   uint64_t yield_after_us_ = 20;  // SPLINTER_RING_SPIN_US: spin this long, then yield between polls
   int cpus_ = 1;                  // CPUs the process may run on (affinity, cgroup quota)
+  // VRAM request mode (SPLINTER_RING_VRAM=1): records, input payloads and sequence-number doorbells
+  // in device memory written by the host through the BAR mapping of a VMM chunk; completions stay
+  // in host memory (k_ring_worker<true>)
+  bool vr_ = false;
+  VmmArena vram_;
+  RingCmd* v_cmds_h_ = nullptr;   // host (BAR) view
+  uint32_t* v_door_h_ = nullptr;
+  uint8_t* v_pay_h_ = nullptr;
+  RingCmd* v_cmds_d_ = nullptr;   // device view
+  uint32_t* v_door_d_ = nullptr;
+  uint8_t* v_pay_d_ = nullptr;
+  uint32_t* served_ = nullptr;    // device: last sequence number served per entry
+  uint32_t seqs_[kRingEntries] = {};  // host: last sequence number issued per entry
+  int init_vram();
   std::atomic<int> waiters_{0};   // host threads waiting on a completion right now
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;

@@ -90,6 +90,10 @@ def parse():
                         "phase writes its vectors into this arena; 0 = a small side arena, no query phase")
     p.add_argument("--search-queries", type=int, default=256, help="queries per search batch (query phase)")
     p.add_argument("--search-batches", type=int, default=8, help="timed search batches (query phase)")
+    p.add_argument("--daemon-docs", type=int, default=512,
+                   help="after the timed loop, embed this many pending VARTEXT documents of an hbm: store through "
+                        "the splinference daemon's own code path (Splinference.process: batched read, WordPiece, "
+                        "encoder, vectors pooled into the slots, +2 epoch check, label updates), per rank; 0 = skip")
     p.add_argument("--routed-steps", type=int, default=10,
                    help="N=1: also time this many steps of the routed (N>1) step on one GPU -> routed_kv_ops_per_s")
     return p.parse_args()
@@ -133,6 +137,54 @@ def _timed_region_profiler():
         print(json.dumps({"timed_region": "begin" if on else "end", "monotonic_ns": time.monotonic_ns(),
                           "boottime_ns": time.clock_gettime_ns(time.CLOCK_BOOTTIME)}), file=sys.stderr, flush=True)
     return toggle
+
+
+def daemon_run(enc, docs: int, seq: int, rank: int, world: int, routed: bool, rounds: int = 3):
+    """Time Splinference.process over `docs` pending documents of a fresh hbm: store (the daemon's
+    batched device path), `rounds` times after one warm-up round; the producer re-sets every
+    document's text between rounds (outside the timing) so each round finds them all pending."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from libsplinter_amd.daemons.splinference import EMBED_LABEL, WAITING_LABEL, Splinference
+    from libsplinter_amd.models.tokenizer import WordPieceTokenizer, synthetic_vocab
+    from libsplinter_amd.store import SLOT_VARTEXT, Store, unlink
+    vocab = synthetic_vocab(enc.cfg.vocab)
+    tok = WordPieceTokenizer(vocab)
+    words = [t[1:] for t in vocab if t.startswith("▁") and len(t) > 2]
+    rng = np.random.default_rng(300 + rank)
+    texts = [" ".join(words[int(i)] for i in rng.integers(0, len(words), size=int(rng.integers(seq // 2, seq - 2))))
+             for _ in range(docs)]
+    name = f"hbm:dm{os.getpid()}r{rank}"
+    st = Store.create(name, slots=max(4 * docs, 1024), max_val=4096, embeddings=True)
+    keys = [f"doc{rank}_{i:06d}" for i in range(docs)]
+
+    def produce():
+        for k, t in zip(keys, texts):
+            st.set(k, t.encode())
+            st.set_type(k, SLOT_VARTEXT)
+            st.set_label(k, EMBED_LABEL | WAITING_LABEL)
+
+    try:
+        d = Splinference(st, enc, tok, group=3, batch_tokens=64 * seq)
+        produce()
+        d.process(d.pending())  # warm-up: first varlen shapes
+        times, done = [], 0
+        for _ in range(rounds):
+            produce()
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            done += d.process(d.pending())
+            torch.cuda.synchronize()
+            times.append(time.perf_counter() - t0)
+        dt = torch.tensor([sum(times)], dtype=torch.float64, device="cuda")
+        if routed:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        return {"vectors_per_s": docs * rounds * world / dt.item(), "embedded": done, "expected": docs * rounds,
+                "stale": d.stats["stale"]}
+    finally:
+        st.close()
+        unlink(name)
 
 
 def main():
@@ -553,6 +605,12 @@ def main():
                "tokens_per_batch": pipe.tokens, "write_failures": fails}
         pipe.close()
 
+    # ---- the embedding daemon itself, owner computes: each rank's daemon embeds the pending
+    # documents of its own store (reference splinference.cpp:500-552)
+    daemon = None
+    if embedder is not None and args.daemon_docs > 0:
+        daemon = daemon_run(embedder.enc, args.daemon_docs, args.embed_seq, rank, world, routed)
+
     # ---- config #5 query phase: batched cosine top-10 over every rank's search arena ---------
     # (the vectors the embed phase wrote are in there too).  Rank 0's queries are broadcast (C3),
     # each GPU scores its arena with the MFMA search pass + fp32 re-score (K7), and the local top-k
@@ -644,6 +702,9 @@ def main():
         "host_api2_p50_us": host_api2["p50_us"] if host_api2 else None,
         "routed_kv_ops_per_s": routed1["ops_per_s"] if routed1 else (kv_ops_s if routed else None),
         "routed_ms_per_step": routed1["ms_per_step"] if routed1 else None,
+        "daemon_vectors_per_s": daemon["vectors_per_s"] if daemon else None,
+        "daemon_docs_embedded": daemon["embedded"] if daemon else None,
+        "daemon_docs_expected": daemon["expected"] if daemon else None,
         "search_qps": search["qps"] if search else None,
         "search_ms_per_batch": search["ms_per_batch"] if search else None,
         "search_recall_at_10": search["recall_at_10"] if search else None,

@@ -16,13 +16,16 @@ hash-shard of the key space in its own HBM arena (format v4, 128-B slots,
   * embed phase (--mode mixed/embed): one batch of synthetic documents through
     the random-init Nomic-BERT encoder on the gfx950 kernels, mean-pooled
     vectors written into their slots of the rank's search arena (--search-keys
-    embedded keys per GPU: the config #5 corpus).
+    embedded keys per GPU: the config #5 corpus; the 100M-key KV arena has no
+    vector slots -- 100M x 3 KiB of vectors would exceed the 288 GB of HBM -- so
+    the vectors land in the 25M-key embedding arena beside it, through the same
+    seqlocked slot write, concurrently with the KV arena's traffic).
 
 The client streams are the same at every N: at N=1 the set / get batches fan out over
 --writer-streams / --reader-streams HIP streams; at N>1 the owner fans the routed segments
 it received out over the same streams (spl_kvs_step_seg).  Outside the timed region:
-the routed step at N=1 (routed_kv_ops_per_s), end-to-end embedding, the per-call C API,
-and config #5's query phase (batched top-k over the search arenas, broadcast + all-gather
+the routed step at N=1 (routed_kv_ops_per_s), end-to-end embedding, the embedding daemon's
+own code path per rank (daemon_vectors_per_s), the per-call C API, and config #5's query phase (batched top-k over the search arenas, broadcast + all-gather
 merge at N>1, recall against the exact kernel).
 
 Ops counted exactly as the reference does (every set + get attempt that

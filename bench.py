@@ -19,7 +19,7 @@ hash-shard of the key space in its own HBM arena (format v4, 128-B slots,
     embedded keys per GPU: the config #5 corpus; the 100M-key KV arena has no
     vector slots -- 100M x 3 KiB of vectors would exceed the 288 GB of HBM -- so
     the vectors land in the 25M-key embedding arena beside it, through the same
-    seqlocked slot write, concurrently with the KV arena's traffic).
+    seqlocked slot write, in the same step as the KV phase).
 
 The client streams are the same at every N: at N=1 the set / get batches fan out over
 --writer-streams / --reader-streams HIP streams; at N>1 the owner fans the routed segments

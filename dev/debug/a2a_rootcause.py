@@ -90,7 +90,7 @@ def main():
     del y
     # 5) the chunked fix of parallel/sharded.py
     import sys
-    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
     from libsplinter_amd.parallel.sharded import _Coll
     y = torch.empty_like(x)
     _Coll(None).all_to_all(y, x)

@@ -5,14 +5,14 @@ import subprocess
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402
 from libsplinter_amd.ops.arena import HbmArena, format_keys, pack_values  # noqa: E402
 
 name = f"clidbg{os.getpid()}"
 a = HbmArena.create(name, slots=int(sys.argv[1]) if len(sys.argv) > 1 else 4096, max_val=64, embeddings=True)
 env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
-cli = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "libsplinter_amd", "bin", "splinterctl")
+cli = os.path.join(os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))), "libsplinter_amd", "bin", "splinterctl")
 n = 1000
 K = format_keys(n, "doc", 6, 16)
 V, L = pack_values([b"text"] * n, 16)

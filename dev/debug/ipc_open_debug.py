@@ -5,7 +5,7 @@ import subprocess
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch  # noqa: E402,F401
 from libsplinter_amd.ops.arena import HbmArena  # noqa: E402
 
@@ -18,7 +18,7 @@ import time, faulthandler, sys
 faulthandler.dump_traceback_later(40, exit=True)
 t0 = time.time()
 import torch
-sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.abspath(__file__)))!r})
+sys.path.insert(0, {os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))!r})
 from libsplinter_amd import _native as N
 import ctypes
 L = N.core_lib()

@@ -1,5 +1,5 @@
 import os, sys
-sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 import torch
 from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
 a = HbmArena.create(f"dbg{os.getpid()}", slots=1 << 22, max_val=256, embeddings=False)

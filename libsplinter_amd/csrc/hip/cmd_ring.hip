@@ -425,7 +425,8 @@ template <bool VR>
 __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmds, RingCmd* hcmds, RingShared* sh,
                                                     const uint32_t* vdoor, const uint8_t* payload_in,
                                                     uint8_t* payload, uint32_t pstride, uint8_t* scratch,
-                                                    uint8_t* ctrl, uint32_t* served, uint64_t idle_ticks) {
+                                                    uint8_t* ctrl, uint32_t* served, RingDone* vdone,
+                                                    uint64_t idle_ticks) {
   const int lane = threadIdx.x, g = blockIdx.x;
   const bool mine = lane < kGroupEntries;
   const int e = g * kGroupEntries + (mine ? lane : 0);
@@ -513,8 +514,15 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
 #endif
       // status, out_len and result share one 16-B chunk of the record: one system-scope store,
       // one drain (it also covers a get's payload stores) before the DONE doorbell
-      st16s(VR ? &hcmds[e].status : &c->status, u32x4s_t{(uint32_t)st, out_len, (uint32_t)result, (uint32_t)(result >> 32)});
-      drain();
+      if constexpr (VR) {
+        // out_len only for ops that returned bytes (the host zeroed it); the drain orders the
+        // payload and the op's own writes before the completion chunk, which is ONE store
+        if (out_len) st32s(&hcmds[e].out_len, out_len);
+        drain();
+      } else {
+        st16s(&c->status, u32x4s_t{(uint32_t)st, out_len, (uint32_t)result, (uint32_t)(result >> 32)});
+        drain();
+      }
 #ifdef SPL_RING_STAMPS
       const uint64_t t_done = wall_clock64();
       const uint64_t mt1 = __builtin_amdgcn_s_memtime();
@@ -536,7 +544,7 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
       if constexpr (VR) {
         seen = bell;
         served[e] = bell;  // read by the next launch only (kernel boundary)
-        st32s(&sh->state[e], bell);
+        st16s(&vdone[e], u32x4s_t{bell, (uint32_t)st, (uint32_t)result, (uint32_t)(result >> 32)});
       } else {
         st32s(&sh->state[e], kRingDone);
       }
@@ -595,6 +603,7 @@ int CmdRing::init(int device, uint32_t pstride) {
   spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
   yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
   cpus_ = effective_cpus();
+  sleep_ns_ = env_int("SPLINTER_RING_SLEEP_NS", 2000);
 #ifndef SPL_RING_POLL4
   // default on: 1 thread p50 9.1 -> 7.3 us, 16 threads 1.18 -> 1.50 M ops/s (profiles/r3_hostapi_vram_ab.jsonl);
   // SPLINTER_RING_VRAM=0, or a failed VMM / BAR mapping, keeps everything in host memory
@@ -615,6 +624,10 @@ int CmdRing::init_vram() {
   if (hipMemset(d, 0, door_b + cmd_b) != hipSuccess) return -1;
   if (hipMalloc((void**)&served_, sizeof(uint32_t) * kRingEntries) != hipSuccess) return -1;
   if (hipMemset(served_, 0, sizeof(uint32_t) * kRingEntries) != hipSuccess) return -1;
+  if (hipHostMalloc((void**)&vdone_, sizeof(RingDone) * kRingEntries, hipHostMallocCoherent | hipHostMallocMapped) !=
+      hipSuccess)
+    return -1;
+  std::memset(vdone_, 0, sizeof(RingDone) * kRingEntries);
   if (hipDeviceSynchronize() != hipSuccess) return -1;
   v_door_h_ = (uint32_t*)h;
   v_cmds_h_ = (RingCmd*)(h + door_b);
@@ -644,11 +657,11 @@ void CmdRing::launch(const spl_arena_t& a) {
   (void)hipMemcpyAsync(ctrl_, init, sizeof init, hipMemcpyHostToDevice, stream_);
   if (vr_)
     hipLaunchKernelGGL(k_ring_worker<true>, dim3(kRingGroups), dim3(64), 0, stream_, a, v_cmds_d_, cmds_, shared_,
-                       v_door_d_, v_pay_d_, payload_, pstride_, scratch_, ctrl_, served_, idle_ticks_);
+                       v_door_d_, v_pay_d_, payload_, pstride_, scratch_, ctrl_, served_, vdone_, idle_ticks_);
   else
     hipLaunchKernelGGL(k_ring_worker<false>, dim3(kRingGroups), dim3(64), 0, stream_, a, cmds_, cmds_, shared_,
                        (const uint32_t*)nullptr, (const uint8_t*)nullptr, payload_, pstride_, scratch_, ctrl_,
-                       (uint32_t*)nullptr, idle_ticks_);
+                       (uint32_t*)nullptr, (RingDone*)nullptr, idle_ticks_);
   if (cur != device_) (void)hipSetDevice(cur);
 }
 
@@ -679,8 +692,9 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     if (busy_[e].compare_exchange_weak(z, 1u, std::memory_order_acquire)) break;
     // an entry a timed-out caller abandoned (busy 2) is reclaimed once the worker has finished it
     z = 2;
-    const uint32_t done_word = vr_ ? seqs_[e] : (uint32_t)kRingDone;
-    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == done_word &&
+    const bool finished = vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == seqs_[e]
+                              : __atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == (uint32_t)kRingDone;
+    if (finished &&
         busy_[e].compare_exchange_strong(z, 1u, std::memory_order_acquire)) {
       if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
       break;
@@ -711,6 +725,7 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     if (key64) std::memcpy(rc.key, key64, 64);
     if (in && in_len) std::memcpy(v_pay_h_ + (size_t)e * pstride_, in, in_len);
     std::memcpy((void*)(v_cmds_h_ + e), &rc, sizeof rc);
+    c->out_len = 0;  // written by the worker only when the op returns bytes
     uint32_t seq = seqs_[e] + 1;
     if (seq == 0) seq = 1;  // 0 is the initial "served" value
     seqs_[e] = seq;
@@ -744,7 +759,9 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     ~Leave() { w.fetch_sub(1, std::memory_order_relaxed); }
   } leave{waiters_};
   for (uint64_t spins = 1;; ++spins) {
-    if (__atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == done_word) break;
+    if (vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == done_word
+            : __atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == done_word)
+      break;
     _mm_pause();
     if ((spins & 31) == 0) {
       const uint64_t us = elapsed_us();
@@ -758,7 +775,7 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
             (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
             slack = true;
           }
-          const timespec ts{0, 2000};
+          const timespec ts{0, sleep_ns_};
           nanosleep(&ts, nullptr);
         } else {
           sched_yield();
@@ -774,11 +791,17 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
       }
     }
   }
-  uint64_t sl;
-  std::memcpy(&sl, &c->status, 8);
-  r->status = (int32_t)(uint32_t)sl;
-  r->out_len = (uint32_t)(sl >> 32);
-  r->result = c->result;
+  if (vr_) {
+    r->status = vdone_[e].status;
+    r->result = vdone_[e].result;
+    r->out_len = __atomic_load_n(&c->out_len, __ATOMIC_ACQUIRE);
+  } else {
+    uint64_t sl;
+    std::memcpy(&sl, &c->status, 8);
+    r->status = (int32_t)(uint32_t)sl;
+    r->out_len = (uint32_t)(sl >> 32);
+    r->result = c->result;
+  }
   if (out && out_cap && r->out_len && r->status >= 0)
     std::memcpy(out, payload_ + (size_t)e * pstride_, r->out_len < out_cap ? r->out_len : out_cap);
   if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
@@ -824,6 +847,7 @@ CmdRing::~CmdRing() {
 #endif
   if (stream_) (void)hipStreamDestroy(stream_);
   if (served_) (void)hipFree(served_);
+  if (vdone_) (void)hipHostFree(vdone_);
   if (ctrl_) (void)hipFree(ctrl_);
   if (scratch_) (void)hipFree(scratch_);
   if (payload_) (void)hipHostFree(payload_);

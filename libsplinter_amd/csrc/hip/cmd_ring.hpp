@@ -96,6 +96,15 @@ struct RingShared {
 #endif
 };
 
+// VRAM mode completion, one 16-B chunk per entry in host memory, written by ONE device store (the
+// NVMe completion-entry pattern): the call's sequence number with its status and result, so an op
+// without output bytes completes with a single PCIe write and no drain of it
+struct alignas(16) RingDone {
+  uint32_t seq;
+  int32_t status;
+  uint64_t result;
+};
+
 struct RingResult {
   int32_t status = 0;
   uint32_t out_len = 0;
@@ -142,9 +151,11 @@ class CmdRing {
   uint32_t* v_door_d_ = nullptr;
   uint8_t* v_pay_d_ = nullptr;
   uint32_t* served_ = nullptr;    // device: last sequence number served per entry
+  RingDone* vdone_ = nullptr;     // host (pinned, coherent): completion chunks
   uint32_t seqs_[kRingEntries] = {};  // host: last sequence number issued per entry
   int init_vram();
   std::atomic<int> waiters_{0};   // host threads waiting on a completion right now
+  long sleep_ns_ = 2000;          // SPLINTER_RING_SLEEP_NS: sleep between polls while oversubscribed
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;
   std::atomic<uint32_t> busy_[kRingEntries] = {};

@@ -543,7 +543,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ int k3sw(int key, int c) { return c ^ ((key >> 1) & 7); }
 __device__ __forceinline__ int v3sw(int key, int c) { return c ^ (((key >> 1) & 1) << 2); }
 
-__global__ __launch_bounds__(256) void k_attn3(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+// PF2: K/V global loads issued two tiles ahead (two register stages) instead of one, so a tile's
+// loads have two tiles' compute to land before their LDS write.
+template <bool PF2 = false, int W = 1>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_attn3(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
                                                int heads, float scale_log2) {
   constexpr int KT = 64, NT = 256, NL = KT * 8 / NT;
@@ -573,37 +576,46 @@ __global__ __launch_bounds__(256) void k_attn3(const uint16_t* __restrict__ qkv,
     for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
   float m = -1e30f, l = 0.f;
 
-  uint4 rk[NL], rv[NL];
-  auto gload = [&](long k0) {
+  constexpr int NS = PF2 ? 2 : 1;  // register stages
+  uint4 rk[NS][NL], rv[NS][NL];
+  auto gload = [&](int stg, long k0) {
 #pragma unroll
     for (int it = 0; it < NL; ++it) {
       const int c = tid + it * NT, key = c >> 3, ch = c & 7;
       if (k0 + key < len) {
-        rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
-        rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
+        rk[stg][it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
+        rv[stg][it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
       } else {
-        rk[it] = make_uint4(0, 0, 0, 0);
-        rv[it] = make_uint4(0, 0, 0, 0);
+        rk[stg][it] = make_uint4(0, 0, 0, 0);
+        rv[stg][it] = make_uint4(0, 0, 0, 0);
       }
     }
   };
-  auto lwrite = [&](int buf) {
+  auto lwrite = [&](int stg, int buf) {
 #pragma unroll
     for (int it = 0; it < NL; ++it) {
       const int c = tid + it * NT, key = c >> 3, ch = c & 7;
-      *(uint4*)(lds[buf][0] + key * 128 + (k3sw(key, ch) << 4)) = rk[it];
-      *(uint4*)(lds[buf][1] + key * 128 + (v3sw(key, ch) << 4)) = rv[it];
+      *(uint4*)(lds[buf][0] + key * 128 + (k3sw(key, ch) << 4)) = rk[stg][it];
+      *(uint4*)(lds[buf][1] + key * 128 + (v3sw(key, ch) << 4)) = rv[stg][it];
     }
   };
 
   const int ntiles = (int)((len + KT - 1) / KT);
-  gload(0);
-  lwrite(0);
+  gload(0, 0);
+  lwrite(0, 0);
+  if (PF2 && ntiles > 1) gload(1 % NS, KT);  // tile 1 rides one stage ahead of the loop's loads
   __syncthreads();
-  for (int t = 0; t < ntiles; ++t) {
+  auto tile = [&](int t, const int sl, const int snext) {
     const int buf = t & 1;
     const long k0 = (long)t * KT;
-    if (t + 1 < ntiles) gload(k0 + KT);
+    // sl: the stage this tile's loads go to; snext: the stage holding tile t+1 (PF2: t's
+    // stage parity is a compile-time constant of each unrolled call, so the register stages
+    // are never indexed at run time)
+    if (PF2) {
+      if (t + 2 < ntiles) gload(sl, k0 + 2 * KT);
+    } else if (t + 1 < ntiles) {
+      gload(0, k0 + KT);
+    }
     const char* Ks = lds[buf][0];
     const char* Vs = lds[buf][1];
     // ---- S^T = K Q^T: A = K rows (key kb*32 + q32, d 16 ks + 8 hi), B = Q^T
@@ -680,8 +692,16 @@ __global__ __launch_bounds__(256) void k_attn3(const uint16_t* __restrict__ qkv,
           o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
         }
       }
-    if (t + 1 < ntiles) lwrite(buf ^ 1);
+    if (t + 1 < ntiles) lwrite(snext, buf ^ 1);
     __syncthreads();
+  };
+  if constexpr (PF2) {
+    for (int t = 0; t < ntiles; t += 2) {
+      tile(t, 0, 1);
+      if (t + 1 < ntiles) tile(t + 1, 1, 0);
+    }
+  } else {
+    for (int t = 0; t < ntiles; ++t) tile(t, 0, 0);
   }
   // ---- normalise; lane holds d = 32 db + 8 g + 4 hi + 0..3 (g = r >> 2) of query q32
   if (qrow < len) {
@@ -924,8 +944,14 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
     hipLaunchKernelGGL((k_attn2<2, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
   else if (g_attn_variant == 13)  // 32x32x16 MFMA form (k_attn3)
-    hipLaunchKernelGGL(k_attn3, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+    hipLaunchKernelGGL(k_attn3<false>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);
+  else if (g_attn_variant == 14)  // 13 with K/V loads two tiles ahead
+    hipLaunchKernelGGL(k_attn3<true>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+                       qblocks, heads, scale_log2);
+  else if (g_attn_variant == 15)  // 14 held to 3 waves per SIMD
+    hipLaunchKernelGGL((k_attn3<true, 3>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
+                       cu, qblocks, heads, scale_log2);
   else if (g_attn_variant == 10)  // 6 with the next tile's loads after the QK^T MFMAs
     hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 4, true>), dim3(nqb * heads), dim3(256), 0, s,
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);

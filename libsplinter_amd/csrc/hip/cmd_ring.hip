@@ -603,7 +603,7 @@ int CmdRing::init(int device, uint32_t pstride) {
   spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
   yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
   cpus_ = effective_cpus();
-  sleep_ns_ = env_int("SPLINTER_RING_SLEEP_NS", 2000);
+  sleep_ns_ = env_int("SPLINTER_RING_SLEEP_NS", 5000);  // 32 threads: 1.73 vs 1.41 M ops/s at 2000 (profiles/r3_hostapi_vram_single_store.jsonl)
 #ifndef SPL_RING_POLL4
   // default on: 1 thread p50 9.1 -> 7.3 us, 16 threads 1.18 -> 1.50 M ops/s (profiles/r3_hostapi_vram_ab.jsonl);
   // SPLINTER_RING_VRAM=0, or a failed VMM / BAR mapping, keeps everything in host memory

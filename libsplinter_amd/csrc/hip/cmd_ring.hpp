@@ -155,7 +155,7 @@ class CmdRing {
   uint32_t seqs_[kRingEntries] = {};  // host: last sequence number issued per entry
   int init_vram();
   std::atomic<int> waiters_{0};   // host threads waiting on a completion right now
-  long sleep_ns_ = 2000;          // SPLINTER_RING_SLEEP_NS: sleep between polls while oversubscribed
+  long sleep_ns_ = 5000;          // SPLINTER_RING_SLEEP_NS: sleep between polls while oversubscribed
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;
   std::atomic<uint32_t> busy_[kRingEntries] = {};

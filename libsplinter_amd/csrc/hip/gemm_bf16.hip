@@ -429,6 +429,9 @@ constexpr int kLds2Bytes = (128 * kEpi2Stride * 4 > 2 * kBufBytes) ? 128 * kEpi2
 
 __device__ __forceinline__ void wait_vm(int n) {
   switch (n) {  // wave-uniform: scalar branch to an immediate count
+    case 26: asm volatile("s_waitcnt vmcnt(26)" ::: "memory"); break;
+    case 20: asm volatile("s_waitcnt vmcnt(20)" ::: "memory"); break;
+    case 18: asm volatile("s_waitcnt vmcnt(18)" ::: "memory"); break;
     case 10: asm volatile("s_waitcnt vmcnt(10)" ::: "memory"); break;
     case 8: asm volatile("s_waitcnt vmcnt(8)" ::: "memory"); break;
     case 6: asm volatile("s_waitcnt vmcnt(6)" ::: "memory"); break;
@@ -871,6 +874,7 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
   };
 
   bf16x8 af[4][2], b0[2][2], b1[2][2];
+  int relax = 0;
   // as k_gemm256's: one quadrant's 16 MFMAs with the phase's stage before (ILV 0) or between them;
   // swapped operands (W fragment as the A operand)
   auto mma_phase = [&](f32x4 (&ac)[4][2], bf16x8 (&bf)[2][2], int which, int sg, int sbuf, bool go) {
@@ -899,7 +903,10 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
     const char* hB1 = hA0 + 3 * kHalfBytes;
     const bool n1 = g + 1 < total, n2 = g + 2 < total;
     // ---- phase 1: quadrant (0,0)
-    wait_vm(n1 ? 10 : 4);
+    // relax: the register epilogue's global stores of the previous tile (S per wave, younger
+    // than the stages these two phases wait for) may stay in flight: vmcnt retires in issue order,
+    // so the counts grow by S instead of draining the stores before the new tile's first MFMAs
+    wait_vm((n1 ? 10 : 4) + relax);
     raw_barrier();
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -913,7 +920,8 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
     }
     mma_phase(acc[0][0], b0, 1, g + 1, buf ^ 1, n1);
     // ---- phase 2: quadrant (0,1)
-    wait_vm(n1 ? 10 : 2);
+    wait_vm((n1 ? 10 : 2) + relax);
+    relax = 0;
     raw_barrier();
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
@@ -936,6 +944,8 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
     if (++kt < nk) continue;
     // ---- tile done: register epilogue (lane: rows m, 4 consecutive columns per fragment) --------
     epilogue();
+    // a full tile's SwiGLU epilogue issued exactly 16 store instructions per wave (2 x 4 x 2)
+    if constexpr (MODE == NOMIC_EPI_SWIGLU && !SK) relax = (m0c + 256 <= ep.M && n2) ? 16 : 0;
 #pragma unroll
     for (int a = 0; a < 2; ++a)
 #pragma unroll

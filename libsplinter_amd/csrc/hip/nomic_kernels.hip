@@ -915,7 +915,7 @@ int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, 
   return (int)hipGetLastError();
 }
 
-static int g_attn_variant = 6;  // measured: profiles/r1_attn_ab.jsonl (6: permlane + packed softmax, XCD remap)
+static int g_attn_variant = 13;  // measured: k_attn3 (32x32x16 MFMA, 3 waves/SIMD) 634 vs 514 TFLOP/s for 6 (profiles/r3_attn_k_attn3_ab.jsonl)
 
 int nomic_attention_set_variant(int v) {
   const int prev = g_attn_variant;
@@ -949,6 +949,9 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   else if (g_attn_variant == 14)  // 13 with K/V loads two tiles ahead
     hipLaunchKernelGGL(k_attn3<true>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);
+  else if (g_attn_variant == 16)  // 13 held to 4 waves per SIMD
+    hipLaunchKernelGGL((k_attn3<false, 4>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
+                       cu, qblocks, heads, scale_log2);
   else if (g_attn_variant == 15)  // 14 held to 3 waves per SIMD
     hipLaunchKernelGGL((k_attn3<true, 3>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
                        cu, qblocks, heads, scale_log2);

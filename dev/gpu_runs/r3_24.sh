@@ -1,0 +1,17 @@
+# round 3, call 24: batched claims in the set kernel (SPLINTER_ARENA_BATCH_CLAIM=1: all ops' probes,
+# then all CASes in flight together) -- arena tests, KV-only A/B (acquire-free get on in all rows)
+set -x
+cd $GRAFT_REPO_ROOT
+O=gpurun_out/r3_24
+mkdir -p $O
+export SPLINTER_ARENA_COOP_GET=2
+SPLINTER_ARENA_BATCH_CLAIM=1 timeout -k 10 300 python -u -m pytest tests/test_arena_gpu.py -x -v -m gpu --timeout 120 --timeout-method thread > $O/pytest_arena_bc.log 2>&1 || exit 1
+SPLINTER_ARENA_BATCH_CLAIM=1 SPLINTER_ARENA_KW4=1 timeout -k 10 300 python -u -m pytest tests/test_arena_gpu.py -x -v -m gpu --timeout 120 --timeout-method thread > $O/pytest_arena_bc_kw4.log 2>&1 || exit 1
+K="--mode kv --host-api 0 --host-api-threads2 0 --routed-steps 0 --steps 10 --warmup 2"
+run() { tag=$1; shift; env "$@" timeout -k 10 300 python -u bench.py $K 2>> $O/kv.err | sed "s/^{/{\"tag\": \"$tag\", /" >> $O/kv_ab.jsonl; }
+for r in 1 2; do
+run get2 SPLINTER_ARENA_BATCH_CLAIM=0 || exit 1
+run bc SPLINTER_ARENA_BATCH_CLAIM=1 || exit 1
+run bc_kw4 SPLINTER_ARENA_BATCH_CLAIM=1 SPLINTER_ARENA_KW4=1 || exit 1
+done
+echo done

@@ -377,7 +377,73 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
 // chunks in [ceil(len/16), wend) are zero-filled: mop scrubbing)}.  l.y == 0: no row.
 // rowb: bytes of a destination row (value regions are max_val long; a last chunk past it is
 // stored bytewise so it cannot spill into the next row); 0xFFFFFFFF: no limit.
-template <int NE>
+// MO: store flavour of the destination rows (st16<MO>); LD1: source rows read with 16-B `sc1` loads
+// (L1-bypassing, so a reader needs no L1-invalidating acquire before them).
+// Rows of at most 256 B (one 16-lane group each), software-pipelined: the loads of the next 16
+// rows are in flight while the current 16 are stored, so a wave's 16 steps cost about half the
+// serial load round trips.  Loads are unconditional (an empty entry or a chunk past the value reads
+// `dummy`, any mapped 16 B), so each step issues exactly kUnr loads and the LD1 path can wait for
+// the current step with vmcnt(kUnr).
+template <int NE, int MO = 0, bool LD1 = false>
+__device__ __forceinline__ void coop_copy_pipe(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
+                                               uint32_t rowb, const void* dummy) {
+  const int q = lane >> 4;
+  const uint32_t c = (uint32_t)(lane & 15);
+  constexpr int kUnr = 4, kSteps = NE / (4 * kUnr);
+  static_assert(NE % (4 * kUnr) == 0, "whole steps");
+  uint4 P[2][kUnr];
+  uint2 L[2][kUnr];
+  u32x4c_t d[2][kUnr];
+  auto fetch = [&](int st, int b) {
+#pragma unroll
+    for (int u = 0; u < kUnr; ++u) {
+      P[b][u] = ep[st * 4 * kUnr + 4 * u + q];
+      L[b][u] = el[st * 4 * kUnr + 4 * u + q];
+    }
+#pragma unroll
+    for (int u = 0; u < kUnr; ++u) {
+      const uint32_t n16 = (L[b][u].x + 15) >> 4;
+      const uint4* src = c < n16 ? (const uint4*)(((uint64_t)P[b][u].y << 32) | P[b][u].x) + c : (const uint4*)dummy;
+      if constexpr (LD1) {
+        d[b][u] = ld16c(src);
+      } else {
+        const uint4 t = *src;
+        d[b][u] = u32x4c_t{t.x, t.y, t.z, t.w};
+      }
+    }
+  };
+  auto put = [&](int b) {
+#pragma unroll
+    for (int u = 0; u < kUnr; ++u) {
+      if (c >= L[b][u].y) continue;
+      const uint32_t n16 = (L[b][u].x + 15) >> 4;
+      uint4 v = c < n16 ? make_uint4(d[b][u].x, d[b][u].y, d[b][u].z, d[b][u].w) : make_uint4(0, 0, 0, 0);
+      if (c == n16 - 1 && (L[b][u].x & 15)) {
+        const int r = (int)(L[b][u].x & 15);
+        v.x &= keep_mask(r); v.y &= keep_mask(r - 4); v.z &= keep_mask(r - 8); v.w &= keep_mask(r - 12);
+      }
+      uint4* dst = (uint4*)(((uint64_t)P[b][u].w << 32) | P[b][u].z);
+      if (c * 16 + 16 > rowb) store_partial((uint8_t*)(dst + c), v, rowb - c * 16);
+      else st16<MO>(dst + c, v);
+    }
+  };
+  fetch(0, 0);
+#pragma unroll
+  for (int st = 0; st < kSteps; ++st) {
+    const int b = st & 1;
+    if (st + 1 < kSteps) fetch(st + 1, b ^ 1);
+    if constexpr (LD1) {
+      static_assert(kUnr == 4, "the waits below tie four registers");
+      if (st + 1 < kSteps)
+        asm volatile("s_waitcnt vmcnt(4)" : "+v"(d[b][0]), "+v"(d[b][1]), "+v"(d[b][2]), "+v"(d[b][3])::"memory");
+      else
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(d[b][0]), "+v"(d[b][1]), "+v"(d[b][2]), "+v"(d[b][3])::"memory");
+    }
+    put(b);
+  }
+}
+
+template <int NE, int MO = 0, bool LD1 = false>
 __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
                                           int groups, uint32_t rowb) {
   const int q = lane >> 4, cl = lane & 15;
@@ -393,12 +459,27 @@ __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const ui
     for (int g = 0; g < groups; ++g) {
       const uint32_t c = (uint32_t)(g * 16 + cl);
       uint4 d[kUnr];
+      if constexpr (LD1) {
+        u32x4c_t t[kUnr];
 #pragma unroll
-      for (int u = 0; u < kUnr; ++u) {
-        const uint32_t n16 = (L[u].x + 15) >> 4;
-        const uint4* src = (const uint4*)(((uint64_t)P[u].y << 32) | P[u].x);
-        d[u] = make_uint4(0, 0, 0, 0);
-        if (c < n16) d[u] = src[c];
+        for (int u = 0; u < kUnr; ++u) {
+          const uint32_t n16 = (L[u].x + 15) >> 4;
+          const uint4* src = (const uint4*)(((uint64_t)P[u].y << 32) | P[u].x);
+          t[u] = u32x4c_t{0u, 0u, 0u, 0u};
+          if (c < n16) t[u] = ld16c(src + c);
+        }
+        static_assert(kUnr == 4, "one wait ties the four loads");
+        asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3])::"memory");
+#pragma unroll
+        for (int u = 0; u < kUnr; ++u) d[u] = make_uint4(t[u].x, t[u].y, t[u].z, t[u].w);
+      } else {
+#pragma unroll
+        for (int u = 0; u < kUnr; ++u) {
+          const uint32_t n16 = (L[u].x + 15) >> 4;
+          const uint4* src = (const uint4*)(((uint64_t)P[u].y << 32) | P[u].x);
+          d[u] = make_uint4(0, 0, 0, 0);
+          if (c < n16) d[u] = src[c];
+        }
       }
 #pragma unroll
       for (int u = 0; u < kUnr; ++u) {
@@ -411,7 +492,7 @@ __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const ui
         }
         uint4* dst = (uint4*)(((uint64_t)P[u].w << 32) | P[u].z);
         if (c * 16 + 16 > rowb) store_partial((uint8_t*)(dst + c), v, rowb - c * 16);
-        else dst[c] = v;
+        else st16<MO>(dst + c, v);
       }
     }
   }
@@ -426,8 +507,16 @@ __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const ui
 // bounded by 1 + max_retry as before; the round loop is block-uniform (barriers).
 // Lane sequence: op c of a lane is first + (c / U) * stride + c % U (monotone in c), i.e. the
 // grid-stride order of the rounds kernels.
-template <int U, int B, int KW = 16, bool COOP = false>
-__global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
+// WT (with COOP): the value rows and slot metadata go out as write-through `sc1` 16-B stores (one
+// 64-B fabric write per 4 lanes of a row) and each wave publishes its own ops after its vmcnt(0)
+// drain -- recipe R1 of cdna_hip_programming.md Guideline 16, as MO 3 -- so a round needs neither
+// the workgroup barrier pair nor the XCD-serialised L2 write-back (buffer_wbl2) of the release.
+// BC: the round's claims through claim_many (all ops' probes, then all CASes, in flight together).
+// PIPE: value rows through coop_copy_pipe (rows of at most 256 B).
+// FS: publish with finish_set_store (an 8-B store) instead of the epoch increment atomic.
+template <int U, int B, int KW = 16, bool COOP = false, bool WT = false, bool BC = false, bool PIPE = false,
+          bool FS = false>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1))) void k_set_carry(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
                                                  int vstride, const uint32_t* lens, long n, int32_t* status,
                                                  int max_retry, uint64_t* stats, Seg seg) {
   __shared__ uint4 cp_p[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
@@ -466,6 +555,22 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
 #pragma unroll
     for (int j = 0; j < U; ++j) busy |= op[j] >= 0;
     if (!__syncthreads_or(busy)) break;
+    if constexpr (BC) {
+      bool act[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        act[j] = false;
+        if (op[j] >= 0) {
+          ++st.attempts;
+          ++tries[j];
+          act[j] = !(len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride);
+        }
+      }
+      claim_many<U, KW>(a, k, act, c);
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (op[j] >= 0 && !act[j]) c[j].rc = kMsgSize;
+    } else {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       c[j] = Claim{-1, false, kInval};
@@ -475,6 +580,7 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
         if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride) c[j].rc = kMsgSize;
         else c[j] = claim_set(a, k[j]);
       }
+    }
     }
     if constexpr (COOP) {
       // value rows through the cooperative copy (wave-private table), metadata per lane
@@ -488,19 +594,22 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
         cp_l[w][j * 64 + lane] = make_uint2(go ? len[j] : 0u, go ? set_chunks(a, len[j], scrub, hybrid) : 0u);
       }
       __builtin_amdgcn_wave_barrier();
-      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), a.max_val);
+      if (PIPE && a.max_val <= 256) coop_copy_pipe<U * 64, WT ? 3 : 0>(cp_p[w], cp_l[w], lane, a.max_val, a.base);
+      else coop_copy<U * 64, WT ? 3 : 0>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), a.max_val);
 #pragma unroll
       for (int j = 0; j < U; ++j)
-        if (op[j] >= 0 && c[j].rc == kOk) write_meta<0>(a, c[j], len[j]);
+        if (op[j] >= 0 && c[j].rc == kOk) write_meta<WT ? 3 : 0>(a, c[j], len[j]);
     } else {
 #pragma unroll
       for (int j = 0; j < U; ++j)
         if (op[j] >= 0 && c[j].rc == kOk) write_set<0>(a, c[j], vals + op[j] * (long)vstride, len[j], scrub, hybrid);
     }
     drain();
-    __syncthreads();
-    if (threadIdx.x == 0) release();
-    __syncthreads();
+    if constexpr (!(WT && COOP)) {
+      __syncthreads();
+      if (threadIdx.x == 0) release();
+      __syncthreads();
+    }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       if (op[j] < 0) continue;
@@ -510,7 +619,8 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
         if (tries[j] <= max_retry) continue;  // carried into the next round
       }
       if (rc == kOk) {
-        finish_set(a, c[j]);
+        if constexpr (FS) finish_set_store(a, c[j]);
+        else finish_set(a, c[j]);
         ++st.ok;
         ++muts;
         pulse_masks(a, c[j].wm, c[j].bl);
@@ -523,8 +633,14 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
   flush_stats(a, st, stats, muts);
 }
 
-template <int U, int B, int KW = 16, bool COOP = false>
-__global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
+// FAST (with COOP): no workgroup acquire.  Every load of slot words and value bytes is an `sc1` load
+// (L1-bypassing; local-HBM lines are never stale in L2, the memory probes keep the XCD L2s
+// coherent), so no L1 invalidate is needed; the key is re-checked in the same round trip as the
+// closing (hash, epoch) load instead of a separate one before the copy: a key change between the
+// probe and the value loads moves the epoch or, for an unset that rewinds it, clears the hash.
+// PIPE: value rows through coop_copy_pipe (1; 2 = the same held to 3 waves per SIMD).
+template <int U, int B, int KW = 16, bool COOP = false, bool FAST = false, int PIPE = 0>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(PIPE == 2 ? 3 : 1))) void k_get_carry(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                  int ostride, uint32_t* out_lens, long n, int32_t* status,
                                                  int max_retry, uint64_t* stats, Seg seg) {
   __shared__ uint4 cp_p[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
@@ -575,6 +691,14 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
         rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
       }
     }
+    if constexpr (FAST && COOP) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (op[j] < 0 || rc[j] != kOk) continue;
+        if ((e1[j] & 1) || len[j] > a.max_val) rc[j] = kAgain;
+        else if (out && len[j] > (uint32_t)ostride) rc[j] = kMsgSize;
+      }
+    } else {
     drain();
     __syncthreads();
     if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -599,6 +723,7 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
       }
       if (!keq) rc[j] = kAgain;
     }
+    }
     if constexpr (COOP) {
       // value rows of this round's matched ops through the cooperative copy (see coop_copy)
       const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -612,15 +737,38 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
         cp_l[w][j * 64 + lane] = make_uint2(go ? n16 * 16 : 0u, go ? n16 : 0u);
       }
       __builtin_amdgcn_wave_barrier();
-      coop_copy<U * 64>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
+      if (PIPE && a.max_val <= 256) coop_copy_pipe<U * 64, 0, FAST>(cp_p[w], cp_l[w], lane, 0xFFFFFFFFu, a.base);
+      else coop_copy<U * 64, 0, FAST>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
     }
     drain();
+    if constexpr (FAST && COOP) {
+      // closing round trip: (hash, epoch) and the key words of every op of the lane together
+      u32x4c_t he[U];
+      KeyProbe<KW> kp[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const bool live = op[j] >= 0 && rc[j] == kOk;
+        const uint8_t* s = a.slot(live ? (size_t)sidx[j] : 0);
+        he[j] = ld16c(s + kOffHash);
+        kp[j].issue(s, k[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        vm_wait(he[j]);
+        kp[j].wait();
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (op[j] >= 0 && rc[j] == kOk && (hi64(he[j]) != e1[j] || lo64(he[j]) != k[j].hash || !kp[j].eq(k[j])))
+          rc[j] = kAgain;
+    } else {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       if (op[j] < 0 || rc[j] != kOk) continue;
       u32x4c_t he = ld16c(a.slot((size_t)sidx[j]) + kOffHash);  // hash + epoch: one request
       vm_wait(he);
       if (hi64(he) != e1[j] || lo64(he) != k[j].hash) rc[j] = kAgain;
+    }
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -959,14 +1107,40 @@ static int set_seg_at(spl_arena_t a, const char* keys, int kstride, const uint8_
   // (profiles/r1_kv_occupancy.md), so it is off by default.
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);
   static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);  // carried retries (k_set_carry)
-  static const int coop = env_int("SPLINTER_ARENA_COOP", 1);    // cooperative value-row copy
+  // cooperative value-row copy: 2 = write-through rows, no per-round release (default: KV-only 2.73 -> 3.15 G
+  // ops/s, mixed step 15.5 -> 14.7 ms, profiles/r3_kv_set_writethrough.md); 1 = plain rows + release; 0 = per lane
+  static const int coop = env_int("SPLINTER_ARENA_COOP", 2);
   if (carry && !wt && (u == 2 || u == 4)) {
 #define SPL_SET_CARRY(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_set_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
-    if (kw4 && kstride == 16 && u == 4 && b == 256)
+    static const int bclaim = env_int("SPLINTER_ARENA_BATCH_CLAIM", 0);
+    static const int pipe = env_int("SPLINTER_ARENA_PIPE", 0);
+    static const int fstore = env_int("SPLINTER_ARENA_FINISH_STORE", 0);
+    if (fstore && u == 4 && b == 256 && coop == 2)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true, false, false, true>), dim3(grid_for_b((n + 3) / 4, 256)),
+                         dim3(256), 0, s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (pipe && u == 4 && b == 256 && coop == 2)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true, false, true>), dim3(grid_for_b((n + 3) / 4, 256)),
+                         dim3(256), 0, s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (bclaim && kw4 && kstride == 16 && u == 4 && b == 256 && coop == 2)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 4, true, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0,
+                         s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (bclaim && u == 4 && b == 256 && coop == 2)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256),
+                         0, s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (kw4 && kstride == 16 && u == 4 && b == 256 && coop == 2)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 4, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s,
+                         a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (kw4 && kstride == 16 && u == 4 && b == 256)
       hipLaunchKernelGGL((k_set_carry<4, 256, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
                          kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (u == 2 && b == 256 && coop == 2)
+      hipLaunchKernelGGL((k_set_carry<2, 256, 16, true, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s,
+                         a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (u == 4 && b == 256 && coop == 2)  // write-through rows, no release (see k_set_carry)
+      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s,
+                         a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
     else if (u == 4 && b == 256 && coop)
       hipLaunchKernelGGL((k_set_carry<4, 256, 16, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
                          keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
@@ -1041,12 +1215,29 @@ static int get_seg_at(spl_arena_t a, const char* keys, int kstride, uint8_t* out
   static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);  // see spl_arena_set_seg
   static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);
-  static const int coop = env_int("SPLINTER_ARENA_COOP_GET", env_int("SPLINTER_ARENA_COOP", 1));
-  if (carry && gv == 1 && (u == 2 || u == 4)) {
+  // 2 = no acquire, sc1 row loads, key re-check with the closing epoch load; 1 = acquire + plain loads
+  static const int coop = env_int("SPLINTER_ARENA_COOP_GET", 1);
+  if (carry && gv == 1 && u == 1 && coop == 2 && b == 256) {
+    hipLaunchKernelGGL((k_get_carry<1, 256, 16, true, true>), dim3(grid_for_b(n, 256)), dim3(256), 0, s, a, keys,
+                       kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+  } else if (carry && gv == 1 && (u == 2 || u == 4)) {
 #define SPL_GET_CARRY(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_get_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
-    if (coop && u == 2 && b == 256)
+    static const int pipe = env_int("SPLINTER_ARENA_PIPE", 0);
+    if (pipe == 2 && coop == 2 && u == 2 && b == 256)
+      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true, true, 2>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256),
+                         0, s, a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else if (pipe && coop == 2 && u == 2 && b == 256)
+      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true, true, 1>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256),
+                         0, s, a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else if (coop == 2 && u == 2 && b == 256 && kw4 && kstride == 16)
+      hipLaunchKernelGGL((k_get_carry<2, 256, 4, true, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s,
+                         a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else if (coop == 2 && u == 2 && b == 256)  // no acquire, sc1 row loads (see k_get_carry)
+      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s,
+                         a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
+    else if (coop && u == 2 && b == 256)
       hipLaunchKernelGGL((k_get_carry<2, 256, 16, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a,
                          keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
     else if (kw4 && kstride == 16 && u == 2 && b == 256)

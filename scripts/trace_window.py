@@ -26,6 +26,9 @@ def main():
     ap.add_argument("log")
     ap.add_argument("--md")
     ap.add_argument("--csv")
+    ap.add_argument("--timeline", action="store_true",
+                    help="also the wall time each kernel (and all of them) is running: the union of its dispatch "
+                         "intervals, which shows which of concurrently running kernel groups bounds the region")
     a = ap.parse_args()
     bounds = {}
     for line in open(a.log, errors="replace"):
@@ -53,6 +56,25 @@ def main():
         lines.append(f"| `{short(n)}` | {len(v)} | {sum(v) / 1e3:.3f} | {sum(v) / len(v):.1f} | {sum(v) / tot * 100:.1f} % |")
     if vendor:
         lines += ["", "vendor / framework kernels in the timed region:"] + [f"- `{short(n)}`" for n in vendor]
+    if a.timeline:
+        def union(iv):
+            tot, end = 0, None
+            for s0, e0 in sorted(iv):
+                if end is None or s0 > end:
+                    tot += e0 - s0
+                    end = e0
+                elif e0 > end:
+                    tot += e0 - end
+                    end = e0
+            return tot
+        groups = defaultdict(list)
+        for n, s0, e0 in inside:
+            groups[short(n)].append((s0, e0))
+        lines += ["", "| kernel | wall time running (union of dispatches) ms | share of region |", "|---|---|---|"]
+        for n, iv in sorted(groups.items(), key=lambda kv: -union(kv[1])):
+            lines.append(f"| `{n}` | {union(iv) / 1e6:.3f} | {union(iv) / span * 100:.1f} % |")
+        allv = [(s0, e0) for _, s0, e0 in inside]
+        lines.append(f"| any kernel | {union(allv) / 1e6:.3f} | {union(allv) / span * 100:.1f} % |")
     out = "\n".join(lines)
     print(out)
     if a.md:

@@ -63,6 +63,9 @@ def parse():
                         "and the encoder to the rest (hipExtStreamCreateWithCUMask); 0 = phases back to back")
     p.add_argument("--overlap", action="store_true",
                    help="run the embed batch concurrently with the KV batches (own stream, all CUs)")
+    p.add_argument("--overlap-native", type=int, default=0, choices=[0, 1],
+                   help="1: the native KV fan-out (32+32 client streams) runs concurrently with the embed batch "
+                        "(KV forked from its own origin stream, the encoder on the current stream)")
     p.add_argument("--force-routed", action="store_true",
                    help="run the N>1 routed step (pack -> all-to-all -> owner kernels -> all-to-all -> gather) "
                         "even at N=1, to measure the routing overhead on one GPU")
@@ -384,6 +387,8 @@ def main():
         g_lens = torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")
 
     _phase_gap_ms = float(os.environ.get("BENCH_PHASE_GAP_MS", "0"))
+    s_kvo = hip_stream("low") if (args.overlap_native and kvs is not None and embedder is not None
+                                  and world == 1) else None
 
 
     # Host submission throttle (--throttle): the next step's KV launches are issued only once
@@ -399,7 +404,14 @@ def main():
         if args.throttle and throttle_ev[0] is not None:
             throttle_ev[0].synchronize()
         kv_streams = w_streams[:len(set_parts)] + r_streams[:len(get_parts)]
-        if kvs is not None and s_emb is None:
+        if kvs is not None and s_emb is None and s_kvo is not None:
+            # overlapped phases: the KV fan-out forks from its own origin stream while the encoder
+            # runs on the current one (no release / acquire fence left in the default KV kernels)
+            s_kvo.wait_stream(cur)
+            with torch.cuda.stream(s_kvo):
+                kvs.step(arena, SK if n_set else None, SV if n_set else None, SL if n_set else None, s_status,
+                         GK if n_get else None, gout if n_get else None, g_lens, g_status)
+        elif kvs is not None and s_emb is None:
             kvs.step(arena, SK if n_set else None, SV if n_set else None, SL if n_set else None, s_status,
                      GK if n_get else None, gout if n_get else None, g_lens, g_status)
         elif n_set:
@@ -428,6 +440,8 @@ def main():
         if s_emb is not None and n_set:
             for s in kv_streams:
                 cur.wait_stream(s)
+        if s_kvo is not None:
+            cur.wait_stream(s_kvo)
         if args.throttle and embedder is not None:
             throttle_ev[0] = cur.record_event()
 
@@ -673,7 +687,7 @@ def main():
             "keys_per_gpu": kpg, "slots_per_gpu": slots, "global_batch": args.batch * world,
             "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
             "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),
-            "mode": args.mode, "mop": args.mop, "value_len": args.value_len,
+            "mode": args.mode, "phases": "overlapped" if s_kvo is not None else "serial", "mop": args.mop, "value_len": args.value_len,
             "writer_streams": nw, "reader_streams": nr,
             "hw_queues_per_priority": int(os.environ["GPU_MAX_HW_QUEUES"]),
             "collectives": ("RCCL on torch's per-process-group streams (request / response groups), "

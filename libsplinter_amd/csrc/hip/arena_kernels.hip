@@ -53,12 +53,14 @@ inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
 }
+// sets: 2 ops per lane since round 3 (twice the workgroups per client-stream dispatch; the 32+32-stream step is
+// bound by how many dispatches the hardware queues keep resident): KV-only 3.06 -> 3.67 G ops/s, mixed step
+// 14.6 -> 14.1 ms (profiles/r3_kv_u2.md)
 inline int arena_rounds() {
-  static int u = env_int("SPLINTER_ARENA_U", 4);
+  static int u = env_int("SPLINTER_ARENA_U", 2);
   return u;
 }
-// gets run best at 2 ops per lane (more lanes in flight), sets at 4 (fewer release rounds):
-// profiles/r1_kv_rounds.jsonl
+// gets run best at 2 ops per lane (more lanes in flight; profiles/r1_kv_rounds.jsonl)
 inline int arena_rounds_get() {
   static int u = env_int("SPLINTER_ARENA_UGET", env_int("SPLINTER_ARENA_U", 2));
   return u;
@@ -1216,7 +1218,8 @@ static int get_seg_at(spl_arena_t a, const char* keys, int kstride, uint8_t* out
   static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);  // see spl_arena_set_seg
   static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);
   // 2 = no acquire, sc1 row loads, key re-check with the closing epoch load; 1 = acquire + plain loads
-  static const int coop = env_int("SPLINTER_ARENA_COOP_GET", 1);
+  // default 2 since round 3: +3 % KV-only, -0.1 ms mixed (profiles/r3_kv_u2.md)
+  static const int coop = env_int("SPLINTER_ARENA_COOP_GET", 2);
   if (carry && gv == 1 && u == 1 && coop == 2 && b == 256) {
     hipLaunchKernelGGL((k_get_carry<1, 256, 16, true, true>), dim3(grid_for_b(n, 256)), dim3(256), 0, s, a, keys,
                        kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);

@@ -462,7 +462,12 @@ __device__ __forceinline__ uint4 pack8(const float* v) {
 // SIMD instead of holding both waves off the matrix core right after the barrier (the finding of
 // gemm_rln.hip's ILV variants).  The issue ORDER of the DMAs is unchanged, so the counted vmcnt
 // waits and the WAR/RAW distances of the phase schedule hold as they are.
-template <int MODE, int ILV = 0>
+// EPI 1 (SWIGLU only): the SwiGLU is applied in registers -- with pack_upgate's [up16 | gate16]
+// column blocks, a lane's accumulators acc[..][j = 0] and acc[..][j = 1] are the up and gate values of
+// the same output -- and the bf16 results are paired across lanes (lane ^ 1, one DPP move) into
+// 4-B LDS writes of a 256 x 128 bf16 image, read back as 16-B row chunks: 32 ds_write_b32 per lane
+// instead of 128 fp32 ones, one barrier pair instead of two.
+template <int MODE, int ILV = 0, int EPI = 0>
 __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ W, long ldw, int K,
                                                           int mtiles, int ntiles, EpiArgs ep) {
@@ -580,6 +585,43 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
     mma_phase(acc[1][1], b1, 3, t + 2, buf, n2);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+
+  if constexpr (MODE == NOMIC_EPI_SWIGLU && EPI == 1) {
+    constexpr int kS = 128 + 8;  // bf16 row stride of the image (272 B: conflict-free 4-B writes)
+    uint16_t* E16 = (uint16_t*)smem;
+    const int fq = lane >> 4, fr = lane & 15;
+    const bool odd = fr & 1;
+    __syncthreads();  // every wave is done reading the last K-tile's operands
+#pragma unroll
+    for (int qm = 0; qm < 2; ++qm)
+#pragma unroll
+      for (int qn = 0; qn < 2; ++qn)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          uint32_t b[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) b[r] = f2bf(swiglu(acc[qm][qn][i][0][r], acc[qm][qn][i][1][r]));
+          // even lanes write rows r = 0, 1 at columns (fr, fr + 1), odd lanes rows 2, 3 at (fr - 1, fr)
+          const uint32_t send = odd ? (b[0] | b[1] << 16) : (b[2] | b[3] << 16);
+          const uint32_t recv = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0xB1, 0xf, 0xf, false);
+          const uint32_t w0 = odd ? ((recv & 0xffffu) | b[2] << 16) : (b[0] | recv << 16);
+          const uint32_t w1 = odd ? ((recv >> 16) | b[3] << 16) : (b[1] | (recv & 0xffff0000u));
+          const int row = qm * 128 + wr * 64 + i * 16 + fq * 4 + (odd ? 2 : 0);
+          const int col = (qn * 4 + wn) * 16 + (fr & ~1);
+          *(uint32_t*)(E16 + row * kS + col) = w0;
+          *(uint32_t*)(E16 + (row + 1) * kS + col) = w1;
+        }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < (256 * 16) / kThreads2; ++it) {
+      const int q = tid + it * kThreads2;
+      const int row = q >> 4, c = q & 15;
+      const long gm = m0 + row;
+      if (gm >= ep.M) continue;
+      *(uint4*)(ep.out + gm * ep.ldo + (long)nt * 128 + c * 8) = *(const uint4*)(E16 + row * kS + c * 8);
+    }
+    return;
+  }
 
   // ---- epilogue: two 128-row halves through the fp32 LDS image ------------
   float* E = (float*)smem;
@@ -1035,6 +1077,16 @@ void allow_lds(F* f, int bytes) {
   (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
+// register SwiGLU epilogue of the launch-per-tile 256^2 kernel (k_gemm256 EPI 1): NOMIC_SWIGLU_REG 1 / 0
+int g_swiglu_reg = -1;
+bool swiglu_reg_epi() {
+  if (g_swiglu_reg < 0) {
+    const char* e = getenv("NOMIC_SWIGLU_REG");
+    g_swiglu_reg = e && *e ? (atoi(e) != 0) : 0;
+  }
+  return g_swiglu_reg != 0;
+}
+
 int g_variant = -1;
 int gemm_variant() {
   if (g_variant < 0) {
@@ -1167,6 +1219,7 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
       allow_lds(k_gemm256<MODE>, kLds2Bytes);
       allow_lds(k_gemm256<MODE, 1>, kLds2Bytes);
       allow_lds(k_gemm256<MODE, 2>, kLds2Bytes);
+      if constexpr (MODE == NOMIC_EPI_SWIGLU) allow_lds(k_gemm256<MODE, 0, 1>, kLds2Bytes);
       return true;
     }();
     (void)attr;
@@ -1174,7 +1227,9 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     ep.gn = band_width(ntiles, 4);
     if constexpr (k256_ok) {
       const dim3 g(mtiles * ntiles), b(kThreads2);
-      if (gemm_ilv() == 1)
+      if (MODE == NOMIC_EPI_SWIGLU && gemm_ilv() == 0 && swiglu_reg_epi())
+        hipLaunchKernelGGL((k_gemm256<MODE, 0, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+      else if (gemm_ilv() == 1)
         hipLaunchKernelGGL((k_gemm256<MODE, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
       else if (gemm_ilv() == 2)
         hipLaunchKernelGGL((k_gemm256<MODE, 2>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
@@ -1196,6 +1251,13 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
 extern "C" int nomic_gemm_set_variant(int variant) {
   const int prev = gemm_variant();
   g_variant = variant;
+  return prev;
+}
+
+// A/B knob: register SwiGLU epilogue of the 256^2 kernel (1) or the fp32 LDS image (0); returns the previous one
+extern "C" int nomic_gemm_set_swiglu_reg(int on) {
+  const int prev = swiglu_reg_epi() ? 1 : 0;
+  g_swiglu_reg = on ? 1 : 0;
   return prev;
 }
 

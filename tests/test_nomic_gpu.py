@@ -131,6 +131,35 @@ def test_gemm_swiglu_and_rope(L):
     assert _rel(qkv[:M].float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("sreg", [1, 0])
+def test_gemm256_swiglu_epilogues(L0, sreg):
+    """The launch-per-tile 256^2 kernel's SwiGLU epilogues (register + bf16 image, and the fp32 image)
+    against fp32, with a partial last row tile (M = 1000)."""
+    import torch
+    from libsplinter_amd.models.nomic import _chk, _stream, pack_upgate
+    torch.manual_seed(3)
+    M, K, F = 1000, 768, 1024
+    x = torch.randn(1024, K, device="cuda").bfloat16()
+    up = torch.randn(F, K, device="cuda") * 0.03
+    gate = torch.randn(F, K, device="cuda") * 0.03
+    ug = pack_upgate(up, gate).bfloat16()
+    out = torch.full((1024, F), 7.0, device="cuda", dtype=torch.bfloat16)
+    L = L0
+    pv, pi, pr = L.nomic_gemm_set_variant(256), L.nomic_gemm_set_ilv(0), L.nomic_gemm_set_swiglu_reg(sreg)
+    try:
+        _chk(L.nomic_gemm(2, x.data_ptr(), K, ug.data_ptr(), K, M, 2 * F, K, out.data_ptr(), F, None, 0, None, None,
+                          0, _stream()), "swiglu256")
+        torch.cuda.synchronize()
+    finally:
+        L.nomic_gemm_set_variant(pv)
+        L.nomic_gemm_set_ilv(pi)
+        L.nomic_gemm_set_swiglu_reg(pr)
+    xf = x[:M].float()
+    ref = (xf @ up.bfloat16().float().T) * torch.nn.functional.silu(xf @ gate.bfloat16().float().T)
+    assert _rel(out[:M].float(), ref) < 1e-2
+    assert (out[M:].float() == 7.0).all()  # rows past M are never written
+
+
 def test_gemm_layernorm_fold_modes(L):
     """Post-LN folded into the GEMMs (nomic_api.h modes 5-8) vs fp32 torch: residual sums with
     128-column partial statistics -> (mean, rstd) per row; the residual normalised on the fly;

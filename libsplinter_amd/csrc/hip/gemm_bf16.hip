@@ -467,7 +467,13 @@ __device__ __forceinline__ uint4 pack8(const float* v) {
 // the same output -- and the bf16 results are paired across lanes (lane ^ 1, one DPP move) into
 // 4-B LDS writes of a 256 x 128 bf16 image, read back as 16-B row chunks: 32 ds_write_b32 per lane
 // instead of 128 fp32 ones, one barrier pair instead of two.
-template <int MODE, int ILV = 0, int EPI = 0>
+// PP 1: ping-pong main loop (the guide's staggered 8-wave schedule, cdna_hip_programming.md §5 "The 256²
+// 8-phase template"): every phase is a LOAD section (its fragment ds_reads, one half-tile of LDS-DMA,
+// lgkmcnt(0)) and an MFMA section, each closed by a barrier, and waves 4-7 start one barrier behind
+// waves 0-3, so on every SIMD one wave's 16 MFMAs run beside its partner's loads.  Counted vmcnt(6)
+// once per K-tile (phase 4) retires the next K-tile; a half-tile is restaged one phase after its last
+// read, which is safe because each load section drains its reads before its closing barrier.
+template <int MODE, int ILV = 0, int EPI = 0, int PP = 0>
 __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ W, long ldw, int K,
                                                           int mtiles, int ntiles, EpiArgs ep) {
@@ -542,6 +548,85 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
       }
     __builtin_amdgcn_s_setprio(0);
   };
+  if constexpr (PP == 1) {
+    auto lgk0 = [] {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto bar = [] {
+      __builtin_amdgcn_sched_barrier(0);
+      raw_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    auto mma_q = [&](f32x4 (&ac)[4][2], bf16x8 (&bf)[2][2]) {
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            ac[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], ac[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    };
+    wait_vm(nk > 1 ? 6 : 0);  // K-tile 0 landed (K-tile 1's three half-tiles may still fly)
+    bar();
+    if (wr == 1) bar();  // the stagger
+    for (int t = 0; t < nk; ++t) {
+      const int buf = t & 1;
+      const char* hA0 = smem + buf * kBufBytes;
+      const char* hA1 = hA0 + kHalfBytes;
+      const char* hB0 = hA0 + 2 * kHalfBytes;
+      const char* hB1 = hA0 + 3 * kHalfBytes;
+      const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
+      // phase 1: quadrant (0,0) -- read A0, B0; stage A1(t+1)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        b0[j][0] = *(const bf16x8*)(hB0 + (wn * 32 + j * 16) * 128 + frow + fsw0);
+        b0[j][1] = *(const bf16x8*)(hB0 + (wn * 32 + j * 16) * 128 + frow + fsw1);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i][0] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw0);
+        af[i][1] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw1);
+      }
+      if (n1) stage(1, t + 1, buf ^ 1);
+      lgk0();
+      bar();
+      mma_q(acc[0][0], b0);
+      bar();
+      // phase 2: quadrant (0,1) -- read B1; stage A0(t+2)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        b1[j][0] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw0);
+        b1[j][1] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw1);
+      }
+      if (n2) stage(0, t + 2, buf);
+      lgk0();
+      bar();
+      mma_q(acc[0][1], b1);
+      bar();
+      // phase 3: quadrant (1,0) -- read A1; stage B0(t+2)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        af[i][0] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw0);
+        af[i][1] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw1);
+      }
+      if (n2) stage(2, t + 2, buf);
+      lgk0();
+      bar();
+      mma_q(acc[1][0], b0);
+      bar();
+      // phase 4: quadrant (1,1) from registers; stage B1(t+2); retire K-tile t+1 (all but the 3 newest
+      // half-tiles, which belong to K-tile t+2)
+      if (n2) stage(3, t + 2, buf);
+      wait_vm(n2 ? 6 : 0);
+      bar();
+      mma_q(acc[1][1], b1);
+      bar();
+    }
+    if (wr == 0) bar();  // equal barrier counts for both groups before the epilogue
+  } else
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
     const char* hA0 = smem + buf * kBufBytes;
@@ -1087,6 +1172,16 @@ bool swiglu_reg_epi() {
   return g_swiglu_reg != 0;
 }
 
+// ping-pong main loop of the launch-per-tile 256^2 kernel (k_gemm256 PP 1): NOMIC_GEMM_PP 1 / 0
+int g_pp = -1;
+bool gemm_pp() {
+  if (g_pp < 0) {
+    const char* e = getenv("NOMIC_GEMM_PP");
+    g_pp = e && *e ? (atoi(e) != 0) : 0;
+  }
+  return g_pp != 0;
+}
+
 int g_variant = -1;
 int gemm_variant() {
   if (g_variant < 0) {
@@ -1219,7 +1314,11 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
       allow_lds(k_gemm256<MODE>, kLds2Bytes);
       allow_lds(k_gemm256<MODE, 1>, kLds2Bytes);
       allow_lds(k_gemm256<MODE, 2>, kLds2Bytes);
-      if constexpr (MODE == NOMIC_EPI_SWIGLU) allow_lds(k_gemm256<MODE, 0, 1>, kLds2Bytes);
+      allow_lds(k_gemm256<MODE, 0, 0, 1>, kLds2Bytes);
+      if constexpr (MODE == NOMIC_EPI_SWIGLU) {
+        allow_lds(k_gemm256<MODE, 0, 1>, kLds2Bytes);
+        allow_lds(k_gemm256<MODE, 0, 1, 1>, kLds2Bytes);
+      }
       return true;
     }();
     (void)attr;
@@ -1227,7 +1326,11 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     ep.gn = band_width(ntiles, 4);
     if constexpr (k256_ok) {
       const dim3 g(mtiles * ntiles), b(kThreads2);
-      if (MODE == NOMIC_EPI_SWIGLU && gemm_ilv() == 0 && swiglu_reg_epi())
+      if (gemm_pp() && gemm_ilv() == 0 && MODE == NOMIC_EPI_SWIGLU && swiglu_reg_epi())
+        hipLaunchKernelGGL((k_gemm256<MODE, 0, 1, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+      else if (gemm_pp() && gemm_ilv() == 0)
+        hipLaunchKernelGGL((k_gemm256<MODE, 0, 0, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+      else if (MODE == NOMIC_EPI_SWIGLU && gemm_ilv() == 0 && swiglu_reg_epi())
         hipLaunchKernelGGL((k_gemm256<MODE, 0, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
       else if (gemm_ilv() == 1)
         hipLaunchKernelGGL((k_gemm256<MODE, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
@@ -1251,6 +1354,13 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
 extern "C" int nomic_gemm_set_variant(int variant) {
   const int prev = gemm_variant();
   g_variant = variant;
+  return prev;
+}
+
+// A/B knob: ping-pong main loop of the 256^2 kernel (1) or the 4-phase lockstep loop (0); returns the previous one
+extern "C" int nomic_gemm_set_pp(int on) {
+  const int prev = gemm_pp() ? 1 : 0;
+  g_pp = on ? 1 : 0;
   return prev;
 }
 

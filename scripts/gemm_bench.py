@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--variants", default="514,512,513,256,128", help="NOMIC_GEMM kernel variants")
     ap.add_argument("--ilvs", default="0", help="DMA interleave settings of the 256^2 kernels (nomic_gemm_set_ilv)")
     ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
+    ap.add_argument("--pps", default="0", help="ping-pong main loop of the 256^2 kernel (nomic_gemm_set_pp)")
     ap.add_argument("--sregs", default="1", help="register SwiGLU epilogue of the 256^2 kernel (nomic_gemm_set_swiglu_reg)")
     a = ap.parse_args()
     import numpy as np
@@ -55,8 +56,9 @@ def main():
 
     ilvs = [int(x) for x in a.ilvs.split(",")]
     sregs = [int(x) for x in a.sregs.split(",")]
-    VARS = [(int(v), il, sr) for v in a.variants.split(",") for il in (ilvs if int(v) in (256, 512) else [0])
-            for sr in (sregs if int(v) == 256 else [1])]
+    pps = [int(x) for x in a.pps.split(",")]
+    VARS = [(int(v), il, sr, pp) for v in a.variants.split(",") for il in (ilvs if int(v) in (256, 512) else [0])
+            for sr in (sregs if int(v) == 256 else [1]) for pp in (pps if int(v) == 256 else [0])]
     times = {(n, v): [] for n, *_ in shapes for v in VARS}
     for r in range(a.rounds):
         for name, *_ in shapes:
@@ -64,6 +66,7 @@ def main():
                 L.nomic_gemm_set_variant(v[0])
                 L.nomic_gemm_set_ilv(v[1])
                 L.nomic_gemm_set_swiglu_reg(v[2])
+                L.nomic_gemm_set_pp(v[3])
                 run(name)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -93,7 +96,7 @@ def main():
                           "ms_median": ref[name], "tflops_median": fl / ref[name] / 1e9}))
         for v in VARS:
             t = np.array(times[(name, v)])
-            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": v[0], "ilv": v[1], "swiglu_reg": v[2],
+            print(json.dumps({"shape": name, "M": M, "N": N, "K": K, "variant": v[0], "ilv": v[1], "swiglu_reg": v[2], "pp": v[3],
                               "ms_median": float(np.median(t)),
                               "tflops_median": fl / np.median(t) / 1e9, "tflops_best": fl / t.min() / 1e9}))
 

@@ -18,16 +18,19 @@ def L0():
     return _lib()
 
 
-@pytest.fixture(params=[(512, 0), (513, 0), (256, 0), (128, 0), (512, 1), (512, 2), (256, 1), (256, 2)],
+@pytest.fixture(params=[(512, 0, 0), (513, 0, 0), (256, 0, 0), (128, 0, 0), (512, 1, 0), (512, 2, 0), (256, 1, 0),
+                        (256, 2, 0), (256, 0, 1)],
                 ids=["gemm_p", "gemm_r", "gemm256", "gemm128", "gemm_p_ilv1", "gemm_p_ilv2", "gemm256_ilv1",
-                     "gemm256_ilv2"])
+                     "gemm256_ilv2", "gemm256_pp"])
 def L(L0, request):
-    """Run each GEMM numerics test on every kernel variant (and DMA-interleave setting)."""
+    """Run each GEMM numerics test on every kernel variant (DMA-interleave setting, ping-pong loop)."""
     prev = L0.nomic_gemm_set_variant(request.param[0])
     prev_ilv = L0.nomic_gemm_set_ilv(request.param[1])
+    prev_pp = L0.nomic_gemm_set_pp(request.param[2])
     yield L0
     L0.nomic_gemm_set_variant(prev)
     L0.nomic_gemm_set_ilv(prev_ilv)
+    L0.nomic_gemm_set_pp(prev_pp)
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 768, 768), (1000, 2304, 768), (257, 768, 3072),
@@ -131,8 +134,9 @@ def test_gemm_swiglu_and_rope(L):
     assert _rel(qkv[:M].float(), ref) < 1e-2
 
 
+@pytest.mark.parametrize("pp", [0, 1])
 @pytest.mark.parametrize("sreg", [1, 0])
-def test_gemm256_swiglu_epilogues(L0, sreg):
+def test_gemm256_swiglu_epilogues(L0, sreg, pp):
     """The launch-per-tile 256^2 kernel's SwiGLU epilogues (register + bf16 image, and the fp32 image)
     against fp32, with a partial last row tile (M = 1000)."""
     import torch
@@ -146,6 +150,7 @@ def test_gemm256_swiglu_epilogues(L0, sreg):
     out = torch.full((1024, F), 7.0, device="cuda", dtype=torch.bfloat16)
     L = L0
     pv, pi, pr = L.nomic_gemm_set_variant(256), L.nomic_gemm_set_ilv(0), L.nomic_gemm_set_swiglu_reg(sreg)
+    pp0 = L.nomic_gemm_set_pp(pp)
     try:
         _chk(L.nomic_gemm(2, x.data_ptr(), K, ug.data_ptr(), K, M, 2 * F, K, out.data_ptr(), F, None, 0, None, None,
                           0, _stream()), "swiglu256")
@@ -154,6 +159,7 @@ def test_gemm256_swiglu_epilogues(L0, sreg):
         L.nomic_gemm_set_variant(pv)
         L.nomic_gemm_set_ilv(pi)
         L.nomic_gemm_set_swiglu_reg(pr)
+        L.nomic_gemm_set_pp(pp0)
     xf = x[:M].float()
     ref = (xf @ up.bfloat16().float().T) * torch.nn.functional.silu(xf @ gate.bfloat16().float().T)
     assert _rel(out[:M].float(), ref) < 1e-2

@@ -21,7 +21,9 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <type_traits>
 
+#include "glds_asm.hpp"
 #include "nomic_api.h"
 
 namespace {
@@ -49,6 +51,7 @@ __device__ __forceinline__ uint32_t pk2(float a, float b) {
 
 // Stage one BMxBK tile of a K-contiguous matrix (row stride ld elements)
 // starting at (row0, k0) into the lane-linear LDS image at `dst`.
+template <bool AS = false>
 __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, long ld, long row0, int k0,
                                            char* dst, int wave, int lane) {
 #pragma unroll
@@ -58,7 +61,10 @@ __device__ __forceinline__ void stage_tile(const uint16_t* __restrict__ src, lon
     const int pc = lane & 7;               // physical 16-B chunk in the 128-B row
     const int c = pc ^ (r & 7);            // logical chunk stored there
     const uint16_t* g = src + (row0 + r) * ld + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)(dst + blk * 1024), 16, 0, 0);
+    if constexpr (AS)
+      spl::glds16_asm(g, dst + blk * 1024);  // counted LDS waits (glds_asm.hpp)
+    else
+      __builtin_amdgcn_global_load_lds((gbl_void*)g, (lds_void*)(dst + blk * 1024), 16, 0, 0);
   }
 }
 
@@ -144,7 +150,7 @@ __device__ __forceinline__ float swiglu(float up, float g) {
   return up * g * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-g * 1.4426950408889634f));
 }
 
-template <int MODE>
+template <int MODE, bool AS = false>
 __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int K,
                                                          int mtiles, int ntiles, EpiArgs ep) {
@@ -195,8 +201,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
     lb = *(const uint4*)(ep.lnb + n0 + c8);
   }
   // LDS: [A0 | B0 | A1 | B1], 16 KB each
-  stage_tile(A, lda, m0, 0, smem, wave, lane);
-  stage_tile(W, ldw, n0, 0, smem + kTileBytes, wave, lane);
+  stage_tile<AS>(A, lda, m0, 0, smem, wave, lane);
+  stage_tile<AS>(W, ldw, n0, 0, smem + kTileBytes, wave, lane);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if constexpr (needs_rowstats(MODE)) {
     if (tid < 128) {  // Chan's combination of equal-size partials (as k_row_stats)
@@ -219,8 +225,8 @@ __global__ __launch_bounds__(kThreads, 2) void k_gemm_nt(const uint16_t* __restr
     const int cur = kt & 1;
     if (kt + 1 < nk) {
       char* nb = smem + (cur ^ 1) * 2 * kTileBytes;
-      stage_tile(A, lda, m0, (kt + 1) * BK, nb, wave, lane);
-      stage_tile(W, ldw, n0, (kt + 1) * BK, nb + kTileBytes, wave, lane);
+      stage_tile<AS>(A, lda, m0, (kt + 1) * BK, nb, wave, lane);
+      stage_tile<AS>(W, ldw, n0, (kt + 1) * BK, nb + kTileBytes, wave, lane);
     }
     const char* ta = smem + cur * 2 * kTileBytes;
     const char* tb = ta + kTileBytes;
@@ -500,7 +506,10 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
     const uint16_t* base = (which < 2 ? A : W) + (long)t * BK;
     char* dst = smem + buf * kBufBytes + which * kHalfBytes;
     const uint32_t off = which == 0 ? offA[0][i] : which == 1 ? offA[1][i] : which == 2 ? offB[0][i] : offB[1][i];
-    __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
+    if constexpr (PP == 2)
+      spl::glds16_asm(base + off, dst + (i * 8 + wave) * 1024);  // counted LDS waits (glds_asm.hpp)
+    else
+      __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
   };
   auto stage = [&](int which, int t, int buf) {
     stage_one(which, t, buf, 0);
@@ -572,13 +581,13 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
     wait_vm(nk > 1 ? 6 : 0);  // K-tile 0 landed (K-tile 1's three half-tiles may still fly)
     bar();
     if (wr == 1) bar();  // the stagger
-    for (int t = 0; t < nk; ++t) {
+    auto pp_kt = [&](int t, auto n1c, auto n2c) {
+      constexpr bool n1 = decltype(n1c)::value, n2 = decltype(n2c)::value;
       const int buf = t & 1;
       const char* hA0 = smem + buf * kBufBytes;
       const char* hA1 = hA0 + kHalfBytes;
       const char* hB0 = hA0 + 2 * kHalfBytes;
       const char* hB1 = hA0 + 3 * kHalfBytes;
-      const bool n1 = t + 1 < nk, n2 = t + 2 < nk;
       // phase 1: quadrant (0,0) -- read A0, B0; stage A1(t+1)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
@@ -624,8 +633,103 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
       bar();
       mma_q(acc[1][1], b1);
       bar();
-    }
+    };
+    // peeled: the steady-state K-tiles carry no staging branches (the counted waits and DMA issue are
+    // straight-line code the compiler can schedule around)
+    int t = 0;
+    for (; t + 2 < nk; ++t) pp_kt(t, std::true_type{}, std::true_type{});
+    if (t + 1 < nk) pp_kt(t++, std::true_type{}, std::false_type{});
+    if (t < nk) pp_kt(t, std::false_type{}, std::false_type{});
     if (wr == 0) bar();  // equal barrier counts for both groups before the epilogue
+  } else if constexpr (PP == 2) {
+  // the lockstep loop below, peeled (no staging branches), with its fragment reads issued in the order
+  // the MFMAs consume them (k-step 0's B and A fragments first) and pinned there, so the first MFMAs wait
+  // only for their own operands (counted lgkmcnt) instead of the whole phase's reads
+  auto rd = [](bf16x8& dst, const char* p) {
+    dst = *(const bf16x8*)p;
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto mm = [&](f32x4 (&ac)[4][2], bf16x8 (&bf)[2][2], int kk) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        ac[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i][kk], bf[j][kk], ac[i][j], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto ls_kt = [&](int t, auto n1c, auto n2c) {
+    constexpr bool n1 = decltype(n1c)::value, n2 = decltype(n2c)::value;
+    const int buf = t & 1;
+    const char* hA0 = smem + buf * kBufBytes;
+    const char* hA1 = hA0 + kHalfBytes;
+    const char* hB0 = hA0 + 2 * kHalfBytes;
+    const char* hB1 = hA0 + 3 * kHalfBytes;
+    const char* pb0 = hB0 + (wn * 32) * 128 + frow;
+    const char* pb1 = hB1 + (wn * 32) * 128 + frow;
+    const char* pa0 = hA0 + (wr * 64) * 128 + frow;
+    const char* pa1 = hA1 + (wr * 64) * 128 + frow;
+    // ---- phase 1: quadrant (0,0)
+    wait_vm(n1 ? 10 : 4);
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int fs = kk ? fsw1 : fsw0;
+      rd(b0[0][kk], pb0 + fs);
+      rd(b0[1][kk], pb0 + 16 * 128 + fs);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rd(af[i][kk], pa0 + i * 16 * 128 + fs);
+    }
+    if constexpr (n1) stage(1, t + 1, buf ^ 1);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mm(acc[0][0], b0, 0);
+    mm(acc[0][0], b0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- phase 2: quadrant (0,1)
+    wait_vm(n1 ? 10 : 2);
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int fs = kk ? fsw1 : fsw0;
+      rd(b1[0][kk], pb1 + fs);
+      rd(b1[1][kk], pb1 + 16 * 128 + fs);
+    }
+    if constexpr (n2) stage(0, t + 2, buf);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mm(acc[0][1], b1, 0);
+    mm(acc[0][1], b1, 1);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- phase 3: quadrant (1,0)
+    wait_vm(n2 ? 10 : (n1 ? 8 : 0));
+    raw_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      const int fs = kk ? fsw1 : fsw0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) rd(af[i][kk], pa1 + i * 16 * 128 + fs);
+    }
+    if constexpr (n2) stage(2, t + 2, buf);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mm(acc[1][0], b0, 0);
+    mm(acc[1][0], b0, 1);
+    __builtin_amdgcn_s_setprio(0);
+    // ---- phase 4: quadrant (1,1), registers only (B1's last read was phase 2: a barrier ago)
+    if constexpr (n2) stage(3, t + 2, buf);
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+    mm(acc[1][1], b1, 0);
+    mm(acc[1][1], b1, 1);
+    __builtin_amdgcn_s_setprio(0);
+  };
+  int t = 0;
+  for (; t + 2 < nk; ++t) ls_kt(t, std::true_type{}, std::true_type{});
+  if (t + 1 < nk) ls_kt(t++, std::true_type{}, std::false_type{});
+  if (t < nk) ls_kt(t, std::false_type{}, std::false_type{});
   } else
   for (int t = 0; t < nk; ++t) {
     const int buf = t & 1;
@@ -1172,14 +1276,28 @@ bool swiglu_reg_epi() {
   return g_swiglu_reg != 0;
 }
 
-// ping-pong main loop of the launch-per-tile 256^2 kernel (k_gemm256 PP 1): NOMIC_GEMM_PP 1 / 0
+// main loop of the launch-per-tile 256^2 kernel (NOMIC_GEMM_PP): 2 = peeled lockstep with asm LDS-DMA
+// (default), 1 = staggered ping-pong, 0 = the round-2 lockstep loop
 int g_pp = -1;
-bool gemm_pp() {
+int gemm_pp() {
   if (g_pp < 0) {
     const char* e = getenv("NOMIC_GEMM_PP");
-    g_pp = e && *e ? (atoi(e) != 0) : 0;
+    // default 2 (peeled lockstep loop, asm LDS-DMA): SwiGLU 296.5 -> 285.2 us, embed 9.35 -> 9.20 ms
+    // (profiles/r3_gemm_asm_dma.md)
+    g_pp = e && *e ? atoi(e) : 2;
+    if (g_pp < 0 || g_pp > 2) g_pp = 2;
   }
-  return g_pp != 0;
+  return g_pp;
+}
+
+// asm LDS-DMA in the 128^2 kernel (k_gemm_nt AS): NOMIC_GEMM_AS128 1 / 0
+int g_as128 = -1;
+int gemm_as128() {
+  if (g_as128 < 0) {
+    const char* e = getenv("NOMIC_GEMM_AS128");
+    g_as128 = e && *e ? (atoi(e) != 0) : 0;
+  }
+  return g_as128;
 }
 
 int g_variant = -1;
@@ -1315,9 +1433,11 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
       allow_lds(k_gemm256<MODE, 1>, kLds2Bytes);
       allow_lds(k_gemm256<MODE, 2>, kLds2Bytes);
       allow_lds(k_gemm256<MODE, 0, 0, 1>, kLds2Bytes);
+      allow_lds(k_gemm256<MODE, 0, 0, 2>, kLds2Bytes);
       if constexpr (MODE == NOMIC_EPI_SWIGLU) {
         allow_lds(k_gemm256<MODE, 0, 1>, kLds2Bytes);
         allow_lds(k_gemm256<MODE, 0, 1, 1>, kLds2Bytes);
+        allow_lds(k_gemm256<MODE, 0, 1, 2>, kLds2Bytes);
       }
       return true;
     }();
@@ -1326,10 +1446,14 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
     ep.gn = band_width(ntiles, 4);
     if constexpr (k256_ok) {
       const dim3 g(mtiles * ntiles), b(kThreads2);
-      if (gemm_pp() && gemm_ilv() == 0 && MODE == NOMIC_EPI_SWIGLU && swiglu_reg_epi())
+      if (gemm_pp() == 1 && gemm_ilv() == 0 && MODE == NOMIC_EPI_SWIGLU && swiglu_reg_epi())
         hipLaunchKernelGGL((k_gemm256<MODE, 0, 1, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else if (gemm_pp() && gemm_ilv() == 0)
+      else if (gemm_pp() == 1 && gemm_ilv() == 0)
         hipLaunchKernelGGL((k_gemm256<MODE, 0, 0, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+      else if (gemm_pp() == 2 && gemm_ilv() == 0 && MODE == NOMIC_EPI_SWIGLU && swiglu_reg_epi())
+        hipLaunchKernelGGL((k_gemm256<MODE, 0, 1, 2>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
+      else if (gemm_pp() == 2 && gemm_ilv() == 0)
+        hipLaunchKernelGGL((k_gemm256<MODE, 0, 0, 2>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
       else if (MODE == NOMIC_EPI_SWIGLU && gemm_ilv() == 0 && swiglu_reg_epi())
         hipLaunchKernelGGL((k_gemm256<MODE, 0, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
       else if (gemm_ilv() == 1)
@@ -1344,8 +1468,12 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = N / BN;
   ep.gn = band_width(ntiles, 8);
   constexpr int lds = kLdsBytes + (needs_rowstats(MODE) ? BM * 8 : 0);
-  hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), lds, s, A, lda, W, ldw, K, mtiles,
-                     ntiles, ep);
+  if (gemm_as128())
+    hipLaunchKernelGGL((k_gemm_nt<MODE, true>), dim3(mtiles * ntiles), dim3(kThreads), lds, s, A, lda, W, ldw, K,
+                       mtiles, ntiles, ep);
+  else
+    hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), lds, s, A, lda, W, ldw, K, mtiles,
+                       ntiles, ep);
   return (int)hipGetLastError();
 }
 
@@ -1359,8 +1487,15 @@ extern "C" int nomic_gemm_set_variant(int variant) {
 
 // A/B knob: ping-pong main loop of the 256^2 kernel (1) or the 4-phase lockstep loop (0); returns the previous one
 extern "C" int nomic_gemm_set_pp(int on) {
-  const int prev = gemm_pp() ? 1 : 0;
-  g_pp = on ? 1 : 0;
+  const int prev = gemm_pp();
+  g_pp = on < 0 || on > 2 ? 2 : on;
+  return prev;
+}
+
+// A/B knob: asm LDS-DMA in the 128^2 kernel (1) or the builtin (0); returns the previous setting
+extern "C" int nomic_gemm_set_as128(int on) {
+  const int prev = gemm_as128();
+  g_as128 = on ? 1 : 0;
   return prev;
 }
 

@@ -30,6 +30,7 @@
 #include <cstdint>
 #include <cstdlib>
 
+#include "glds_asm.hpp"
 #include "nomic_api.h"
 
 namespace {
@@ -114,7 +115,8 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 3); }
 // the first K step -- one MFMA per tile against an identity operand (acc = I . R, exact: 1.0 x a
 // bf16 value) with R fragments loaded in the prologue beside the first stages, so the epilogue
 // reads nothing.  PF: W fragment pairs read PF pairs ahead of their MFMAs.
-template <int PIPE, int EPI, int WM, int ILV = 0, int PF = 1>
+// AS: the K-loop's LDS-DMAs issued from inline asm (glds_asm.hpp: counted lgkmcnt before the MFMAs)
+template <int PIPE, int EPI, int WM, int ILV = 0, int PF = 1, bool AS = false>
 __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ W, long ldw, int K, long M,
                                                           const uint16_t* res, long ldr,
@@ -152,13 +154,19 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
   const int nk = K / kBK;
   // ring slot of stage t: t % NW (W), t % NA (A) -- stages enter each ring in order
   auto glds_w = [&](int t, int i) {
-    __builtin_amdgcn_global_load_lds((gbl_void*)(W + (long)t * kBK + offW[i]),
-                                     (lds_void*)(smem + (t % NW) * kWBytes + (wave + kWaves * i) * 1024), 16, 0, 0);
+    if constexpr (AS)
+      spl::glds16_asm(W + (long)t * kBK + offW[i], smem + (t % NW) * kWBytes + (wave + kWaves * i) * 1024);
+    else
+      __builtin_amdgcn_global_load_lds((gbl_void*)(W + (long)t * kBK + offW[i]),
+                                       (lds_void*)(smem + (t % NW) * kWBytes + (wave + kWaves * i) * 1024), 16, 0, 0);
   };
   auto glds_a = [&](int t, int i) {
-    __builtin_amdgcn_global_load_lds((gbl_void*)(A + (long)t * kBK + offA[i]),
-                                     (lds_void*)(smem + kABase + (t % NA) * kABytes + (wave + kWaves * i) * 1024), 16,
-                                     0, 0);
+    if constexpr (AS)
+      spl::glds16_asm(A + (long)t * kBK + offA[i], smem + kABase + (t % NA) * kABytes + (wave + kWaves * i) * 1024);
+    else
+      __builtin_amdgcn_global_load_lds((gbl_void*)(A + (long)t * kBK + offA[i]),
+                                       (lds_void*)(smem + kABase + (t % NA) * kABytes + (wave + kWaves * i) * 1024),
+                                       16, 0, 0);
   };
   // op u (0 .. GW+GA-1) of the loads iteration s issues: stage W(s + LW) and A(s + LA), the one
   // with the shorter lead first (younger() counts on that order)
@@ -482,17 +490,17 @@ int rln_variant() {
   return g_rln_variant;
 }
 
-template <int PIPE, int EPI, int WM = 2, int ILV = 0, int PF = 1>
+template <int PIPE, int EPI, int WM = 2, int ILV = 0, int PF = 1, bool AS = false>
 void launch_rln(unsigned blocks, hipStream_t s, const uint16_t* A, long lda, const uint16_t* W, long ldw, int K, long M,
                 const uint16_t* res, long ldr, const uint16_t* gamma, const uint16_t* beta, float eps, uint16_t* out,
                 long ldo) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_gemm_rln<PIPE, EPI, WM, ILV, PF>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_gemm_rln<PIPE, EPI, WM, ILV, PF, AS>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lds_bytes<PIPE>());
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL((k_gemm_rln<PIPE, EPI, WM, ILV, PF>), dim3(blocks), dim3(256 * WM), lds_bytes<PIPE>(), s, A, lda, W, ldw, K,
+  hipLaunchKernelGGL((k_gemm_rln<PIPE, EPI, WM, ILV, PF, AS>), dim3(blocks), dim3(256 * WM), lds_bytes<PIPE>(), s, A, lda, W, ldw, K,
                      M, res, ldr, gamma, beta, eps, out, ldo);
 }
 
@@ -531,6 +539,11 @@ extern "C" int nomic_gemm_res_ln(const void* A, long lda, const void* W, long ld
     case 222 + 1000: launch_rln<2, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 222 + 2000: launch_rln<2, 0, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 222 + 3000: launch_rln<2, 2, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    // + 10000: the K loop's LDS-DMAs from inline asm (AS, glds_asm.hpp)
+    case 10222: launch_rln<2, 0, 2, 2, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 10220: launch_rln<2, 0, 2, 1, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 10020: launch_rln<2, 0, 2, 0, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 12222: launch_rln<2, 0, 2, 2, 2, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 242: launch_rln<4, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 243: launch_rln<4, 0, 2, 3>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     default: launch_rln<1, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;

@@ -20,6 +20,7 @@ def main():
     ap.add_argument("--variants", default="514,512,513,256,128", help="NOMIC_GEMM kernel variants")
     ap.add_argument("--ilvs", default="0", help="DMA interleave settings of the 256^2 kernels (nomic_gemm_set_ilv)")
     ap.add_argument("--shapes", default="", help="comma list of shape names (default: all)")
+    ap.add_argument("--as128", default="0", help="asm LDS-DMA in the 128^2 kernel (nomic_gemm_set_as128)")
     ap.add_argument("--pps", default="0", help="ping-pong main loop of the 256^2 kernel (nomic_gemm_set_pp)")
     ap.add_argument("--sregs", default="1", help="register SwiGLU epilogue of the 256^2 kernel (nomic_gemm_set_swiglu_reg)")
     a = ap.parse_args()
@@ -58,7 +59,9 @@ def main():
     sregs = [int(x) for x in a.sregs.split(",")]
     pps = [int(x) for x in a.pps.split(",")]
     VARS = [(int(v), il, sr, pp) for v in a.variants.split(",") for il in (ilvs if int(v) in (256, 512) else [0])
-            for sr in (sregs if int(v) == 256 else [1]) for pp in (pps if int(v) == 256 else [0])]
+            for sr in (sregs if int(v) == 256 else [1]) for pp in (pps if int(v) == 256 else
+                                                                     [int(x) for x in a.as128.split(",")] if int(v) == 128
+                                                                     else [0])]
     times = {(n, v): [] for n, *_ in shapes for v in VARS}
     for r in range(a.rounds):
         for name, *_ in shapes:
@@ -66,7 +69,10 @@ def main():
                 L.nomic_gemm_set_variant(v[0])
                 L.nomic_gemm_set_ilv(v[1])
                 L.nomic_gemm_set_swiglu_reg(v[2])
-                L.nomic_gemm_set_pp(v[3])
+                if v[0] == 128:
+                    L.nomic_gemm_set_as128(v[3])
+                else:
+                    L.nomic_gemm_set_pp(v[3])
                 run(name)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()

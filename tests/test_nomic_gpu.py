@@ -19,18 +19,21 @@ def L0():
 
 
 @pytest.fixture(params=[(512, 0, 0), (513, 0, 0), (256, 0, 0), (128, 0, 0), (512, 1, 0), (512, 2, 0), (256, 1, 0),
-                        (256, 2, 0), (256, 0, 1)],
+                        (256, 2, 0), (256, 0, 1), (256, 0, 2), (128, 0, 9)],
                 ids=["gemm_p", "gemm_r", "gemm256", "gemm128", "gemm_p_ilv1", "gemm_p_ilv2", "gemm256_ilv1",
-                     "gemm256_ilv2", "gemm256_pp"])
+                     "gemm256_ilv2", "gemm256_pp", "gemm256_peeled", "gemm128_asm"])
 def L(L0, request):
     """Run each GEMM numerics test on every kernel variant (DMA-interleave setting, ping-pong loop)."""
     prev = L0.nomic_gemm_set_variant(request.param[0])
     prev_ilv = L0.nomic_gemm_set_ilv(request.param[1])
-    prev_pp = L0.nomic_gemm_set_pp(request.param[2])
+    # third field: the 256^2 kernel's main loop (NOMIC_GEMM_PP); 9 = the 128^2 kernel with asm LDS-DMA
+    prev_pp = L0.nomic_gemm_set_pp(request.param[2] if request.param[2] != 9 else 2)
+    prev_as = L0.nomic_gemm_set_as128(1 if request.param[2] == 9 else 0)
     yield L0
     L0.nomic_gemm_set_variant(prev)
     L0.nomic_gemm_set_ilv(prev_ilv)
     L0.nomic_gemm_set_pp(prev_pp)
+    L0.nomic_gemm_set_as128(prev_as)
 
 
 @pytest.mark.parametrize("M,N,K", [(128, 128, 64), (300, 768, 768), (1000, 2304, 768), (257, 768, 3072),
@@ -134,7 +137,7 @@ def test_gemm_swiglu_and_rope(L):
     assert _rel(qkv[:M].float(), ref) < 1e-2
 
 
-@pytest.mark.parametrize("pp", [0, 1])
+@pytest.mark.parametrize("pp", [0, 1, 2])
 @pytest.mark.parametrize("sreg", [1, 0])
 def test_gemm256_swiglu_epilogues(L0, sreg, pp):
     """The launch-per-tile 256^2 kernel's SwiGLU epilogues (register + bf16 image, and the fp32 image)
@@ -302,8 +305,16 @@ def test_layernorm_and_embed(L0):
     assert _rel(out.float(), ref) < 5e-3
 
 
+@pytest.fixture(params=[222, 10222, 12222, 10020], ids=["rln222", "rln222_asm", "rln2222_asm", "rln20_asm"])
+def rln_variant(L0, request):
+    """Each row-complete residual+LN kernel variant (builtin or asm LDS-DMA, ILV, W prefetch depth)."""
+    prev = L0.nomic_gemm_res_ln_set_variant(request.param)
+    yield request.param
+    L0.nomic_gemm_res_ln_set_variant(prev)
+
+
 @pytest.mark.parametrize("M,K", [(128, 768), (300, 768), (1, 3072), (257, 3072), (32768, 768), (4100, 3072)])
-def test_gemm_residual_layernorm_row_complete(L0, M, K):
+def test_gemm_residual_layernorm_row_complete(L0, M, K, rln_variant):
     """nomic_gemm_res_ln (gemm_rln.hip): x = LN(A W^T + x) * g + b in place, against fp32, with a
     row tail (M % 128 != 0), a single row, the shipped 32768-row o-proj shape and the down shape;
     rows past M untouched; asymmetric operands and non-trivial gamma/beta."""

@@ -604,6 +604,8 @@ int CmdRing::init(int device, uint32_t pstride) {
   yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
   cpus_ = effective_cpus();
   sleep_ns_ = env_int("SPLINTER_RING_SLEEP_NS", 5000);  // 32 threads: 1.73 vs 1.41 M ops/s at 2000 (profiles/r3_hostapi_vram_single_store.jsonl)
+  first_sleep_ns_ = env_int("SPLINTER_RING_FIRST_SLEEP_NS", (int)sleep_ns_);
+  oversub_spin_us_ = (uint64_t)env_int("SPLINTER_RING_OVERSUB_SPIN_US", 2);
 #ifndef SPL_RING_POLL4
   // default on: 1 thread p50 9.1 -> 7.3 us, 16 threads 1.18 -> 1.50 M ops/s (profiles/r3_hostapi_vram_ab.jsonl);
   // SPLINTER_RING_VRAM=0, or a failed VMM / BAR mapping, keeps everything in host memory
@@ -758,6 +760,7 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     std::atomic<int>& w;
     ~Leave() { w.fetch_sub(1, std::memory_order_relaxed); }
   } leave{waiters_};
+  bool slept = false;
   for (uint64_t spins = 1;; ++spins) {
     if (vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == done_word
             : __atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == done_word)
@@ -768,14 +771,15 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
       // re-decided every poll round: once more callers wait than there are CPUs, EVERY waiter
       // (also those that started spinning before the others arrived) sleep-polls
       const bool oversub = waiters_.load(std::memory_order_relaxed) > cpus_;
-      if (us > (oversub ? 2u : yield_after_us_)) {
+      if (us > (oversub ? oversub_spin_us_ : yield_after_us_) || (oversub && oversub_spin_us_ == 0)) {
         if (oversub) {
           static thread_local bool slack = false;
           if (!slack) {
             (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
             slack = true;
           }
-          const timespec ts{0, sleep_ns_};
+          const timespec ts{0, slept ? sleep_ns_ : first_sleep_ns_};
+          slept = true;
           nanosleep(&ts, nullptr);
         } else {
           sched_yield();

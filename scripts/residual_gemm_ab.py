@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--no-blas", action="store_true")
     ap.add_argument("--rln-variants", default="11", help="comma list of nomic_gemm_res_ln variants "
                     "(PIPE*10 + EPI, csrc/hip/gemm_rln.hip) timed as separate arms")
+    ap.add_argument("--ks", default="", help="comma list of K values to time instead of the o-proj / down shapes "
+                    "(per-tile fixed cost = intercept of time vs K)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -33,7 +35,8 @@ def main():
     torch.manual_seed(0)
     rnd = lambda *s: (torch.rand(*s, device="cuda") * 2 - 1)  # noqa: E731
     cases = {}
-    for name, K in (("o_proj", 768), ("down", 3072)):
+    shapes = [(f"k{k}", int(k)) for k in a.ks.split(",")] if a.ks else [("o_proj", 768), ("down", 3072)]
+    for name, K in shapes:
         A = rnd(M, K).bfloat16()
         W = (rnd(768, K) * (1.0 / K ** 0.5)).bfloat16()
         x0 = rnd(M, 768).bfloat16()

@@ -4,7 +4,7 @@ set -x
 cd $GRAFT_REPO_ROOT
 O=gpurun_out/r3_41
 mkdir -p $O
-timeout -k 10 300 python -u scripts/residual_gemm_ab.py --no-blas --rln-variants 222 --ks 96,192,384,768,1536,3072 > $O/rln_k.jsonl 2> $O/rln_k.err || exit 1
+timeout -k 10 300 python -u scripts/residual_gemm_ab.py --no-blas --rln-variants 222 --ks 128,256,512,768,1536,3072 > $O/rln_k.jsonl 2> $O/rln_k.err || exit 1
 H=libsplinter_amd/bin/splinter_hostapi_bench
 run() { tag=$1; shift; e=(); while [[ $1 == *=* ]]; do e+=("$1"); shift; done; env "${e[@]}" timeout -k 10 60 $H --seconds 1.5 --keys 20000 "$@" 2>> $O/h.err | sed "s/^{/{\"tag\": \"$tag\", /" >> $O/h.jsonl; }
 for r in 1 2 3 4; do

@@ -116,7 +116,9 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 3); }
 // bf16 value) with R fragments loaded in the prologue beside the first stages, so the epilogue
 // reads nothing.  PF: W fragment pairs read PF pairs ahead of their MFMAs.
 // AS: the K-loop's LDS-DMAs issued from inline asm (glds_asm.hpp: counted lgkmcnt before the MFMAs)
-template <int PIPE, int EPI, int WM, int ILV = 0, int PF = 1, bool AS = false>
+// ROT: block b walks the K steps starting at step b mod nk (the sum is order-free up to fp32 rounding), so
+// the 256 blocks that start together fetch different W stages instead of all hitting the same L2 lines
+template <int PIPE, int EPI, int WM, int ILV = 0, int PF = 1, bool AS = false, bool ROT = false>
 __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __restrict__ A, long lda,
                                                           const uint16_t* __restrict__ W, long ldw, int K, long M,
                                                           const uint16_t* res, long ldr,
@@ -153,18 +155,26 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
   }
   const int nk = K / kBK;
   // ring slot of stage t: t % NW (W), t % NA (A) -- stages enter each ring in order
+  const int rot = ROT ? (int)(blockIdx.x % (unsigned)nk) : 0;
+  auto kcol = [&](int t) -> long {  // global K offset of stage t
+    if constexpr (ROT) {
+      const int k = t + rot;
+      return (long)(k < nk ? k : k - nk) * kBK;
+    }
+    return (long)t * kBK;
+  };
   auto glds_w = [&](int t, int i) {
     if constexpr (AS)
-      spl::glds16_asm(W + (long)t * kBK + offW[i], smem + (t % NW) * kWBytes + (wave + kWaves * i) * 1024);
+      spl::glds16_asm(W + kcol(t) + offW[i], smem + (t % NW) * kWBytes + (wave + kWaves * i) * 1024);
     else
-      __builtin_amdgcn_global_load_lds((gbl_void*)(W + (long)t * kBK + offW[i]),
+      __builtin_amdgcn_global_load_lds((gbl_void*)(W + kcol(t) + offW[i]),
                                        (lds_void*)(smem + (t % NW) * kWBytes + (wave + kWaves * i) * 1024), 16, 0, 0);
   };
   auto glds_a = [&](int t, int i) {
     if constexpr (AS)
-      spl::glds16_asm(A + (long)t * kBK + offA[i], smem + kABase + (t % NA) * kABytes + (wave + kWaves * i) * 1024);
+      spl::glds16_asm(A + kcol(t) + offA[i], smem + kABase + (t % NA) * kABytes + (wave + kWaves * i) * 1024);
     else
-      __builtin_amdgcn_global_load_lds((gbl_void*)(A + (long)t * kBK + offA[i]),
+      __builtin_amdgcn_global_load_lds((gbl_void*)(A + kcol(t) + offA[i]),
                                        (lds_void*)(smem + kABase + (t % NA) * kABytes + (wave + kWaves * i) * 1024),
                                        16, 0, 0);
   };
@@ -490,17 +500,17 @@ int rln_variant() {
   return g_rln_variant;
 }
 
-template <int PIPE, int EPI, int WM = 2, int ILV = 0, int PF = 1, bool AS = false>
+template <int PIPE, int EPI, int WM = 2, int ILV = 0, int PF = 1, bool AS = false, bool ROT = false>
 void launch_rln(unsigned blocks, hipStream_t s, const uint16_t* A, long lda, const uint16_t* W, long ldw, int K, long M,
                 const uint16_t* res, long ldr, const uint16_t* gamma, const uint16_t* beta, float eps, uint16_t* out,
                 long ldo) {
   static bool attr = [] {
-    (void)hipFuncSetAttribute((const void*)k_gemm_rln<PIPE, EPI, WM, ILV, PF, AS>, hipFuncAttributeMaxDynamicSharedMemorySize,
+    (void)hipFuncSetAttribute((const void*)k_gemm_rln<PIPE, EPI, WM, ILV, PF, AS, ROT>, hipFuncAttributeMaxDynamicSharedMemorySize,
                               lds_bytes<PIPE>());
     return true;
   }();
   (void)attr;
-  hipLaunchKernelGGL((k_gemm_rln<PIPE, EPI, WM, ILV, PF, AS>), dim3(blocks), dim3(256 * WM), lds_bytes<PIPE>(), s, A, lda, W, ldw, K,
+  hipLaunchKernelGGL((k_gemm_rln<PIPE, EPI, WM, ILV, PF, AS, ROT>), dim3(blocks), dim3(256 * WM), lds_bytes<PIPE>(), s, A, lda, W, ldw, K,
                      M, res, ldr, gamma, beta, eps, out, ldo);
 }
 
@@ -544,6 +554,9 @@ extern "C" int nomic_gemm_res_ln(const void* A, long lda, const void* W, long ld
     case 10220: launch_rln<2, 0, 2, 1, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 10020: launch_rln<2, 0, 2, 0, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 12222: launch_rln<2, 0, 2, 2, 2, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    // + 20000: K steps rotated per block (ROT)
+    case 20222: launch_rln<2, 0, 2, 2, 1, false, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
+    case 30222: launch_rln<2, 0, 2, 2, 1, true, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 242: launch_rln<4, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     case 243: launch_rln<4, 0, 2, 3>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
     default: launch_rln<1, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;

@@ -305,7 +305,7 @@ def test_layernorm_and_embed(L0):
     assert _rel(out.float(), ref) < 5e-3
 
 
-@pytest.fixture(params=[222, 10222, 12222, 10020], ids=["rln222", "rln222_asm", "rln2222_asm", "rln20_asm"])
+@pytest.fixture(params=[222, 10222, 12222, 10020, 20222], ids=["rln222", "rln222_asm", "rln2222_asm", "rln20_asm", "rln222_rot"])
 def rln_variant(L0, request):
     """Each row-complete residual+LN kernel variant (builtin or asm LDS-DMA, ILV, W prefetch depth)."""
     prev = L0.nomic_gemm_res_ln_set_variant(request.param)

@@ -1414,10 +1414,17 @@ void* spl_kvs_create(int writers, int readers) {
     const char* e = getenv("SPL_KVS_SPREAD");
     return e && *e ? atoi(e) : 0;
   }();
+  // SPL_KVS_PRIO=1 (A/B knob): writers on the high-priority pool and readers on the normal one (sets are the
+  // slower half of a step; by default the readers win dispatch arbitration)
+  static const int swap = [] {
+    const char* e = getenv("SPL_KVS_PRIO");
+    return e && *e ? atoi(e) : 0;
+  }();
   for (int i = 0; i < writers + readers; ++i) {
     hipStream_t st = nullptr;
     hipEvent_t ev = nullptr;
-    const int prio = i < writers ? ((spread >= 1 && (i & 1)) ? lo : 0) : ((spread >= 2 && (i & 1)) ? 0 : hi);
+    int prio = i < writers ? ((spread >= 1 && (i & 1)) ? lo : 0) : ((spread >= 2 && (i & 1)) ? 0 : hi);
+    if (swap == 1) prio = i < writers ? hi : 0;
     if (hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio) != hipSuccess ||
         hipEventCreateWithFlags(&ev, hipEventDisableTiming) != hipSuccess) {
       delete k;

@@ -936,7 +936,8 @@ __device__ __forceinline__ uint2 pack4(const float* v) {
   return make_uint2(pk2(v[0], v[1]), pk2(v[2], v[3]));
 }
 
-template <int MODE, bool PERSIST, bool SK = false, int ILV = 0>
+// AS: LDS-DMA from inline asm (glds_asm.hpp: counted lgkmcnt before the MFMA groups)
+template <int MODE, bool PERSIST, bool SK = false, int ILV = 0, bool AS = false>
 __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restrict__ A, long lda,
                                                          const uint16_t* __restrict__ W, long ldw, int K,
                                                          int mtiles, int ntiles, EpiArgs ep) {
@@ -1013,7 +1014,10 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restr
     char* dst = smem + buf * kBufBytes + which * kHalfBytes;
     const int h = which & 1;
     const uint32_t off = which < 2 ? (nx ? offAx[h][i] : offAc[h][i]) : (nx ? offBx[h][i] : offBc[h][i]);
-    __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
+    if constexpr (AS)
+      spl::glds16_asm(base + off, dst + (i * 8 + wave) * 1024);
+    else
+      __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
   };
   auto stage = [&](int which, int g, int buf) {
     stage_one(which, g, buf, 0);
@@ -1399,8 +1403,9 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
   // auto no longer takes the persistent kernel: on the encoder's SwiGLU shape (3072 tiles) the
   // launch-per-tile k_gemm256 measured 1064 TFLOP/s against 1015 (1046 with ILV 2) for k_gemm_p
   // (profiles/r3_gemm_ilv_ab.jsonl); NOMIC_GEMM=512 keeps it selectable
-  if (p_ok && fits && K >= 2 * BK && (var == 512 || var == 513)) {
+  if (p_ok && fits && K >= 2 * BK && (var == 512 || var == 513 || var == 515)) {
     static bool attr_p = [] {
+      allow_lds(k_gemm_p<MODE, true, false, 0, true>, 2 * kBufBytes);
       allow_lds(k_gemm_p<MODE, true>, 2 * kBufBytes);
       allow_lds(k_gemm_p<MODE, true, false, 1>, 2 * kBufBytes);
       allow_lds(k_gemm_p<MODE, true, false, 2>, 2 * kBufBytes);
@@ -1416,6 +1421,9 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
       if (var == 513)
         hipLaunchKernelGGL((k_gemm_p<MODE, false>), dim3(tiles), b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
                            ep);
+      else if (var == 515)  // persistent, asm LDS-DMA
+        hipLaunchKernelGGL((k_gemm_p<MODE, true, false, 0, true>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles,
+                           ntiles, ep);
       else if (gemm_ilv() == 1)
         hipLaunchKernelGGL((k_gemm_p<MODE, true, false, 1>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
                            ep);

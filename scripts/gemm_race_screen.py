@@ -16,15 +16,15 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--runs", type=int, default=30)
-    ap.add_argument("--knob", default="pp", choices=["pp", "as128", "rln"])
+    ap.add_argument("--knob", default="pp", choices=["pp", "as128", "rln", "variant"])
     ap.add_argument("--value", type=int, default=1, help="knob setting screened against 0")
     a = ap.parse_args()
     import torch
     from libsplinter_amd.models.nomic import _chk, _lib, _stream
     L = _lib()
-    base = {"pp": 0, "as128": 0, "rln": 222}[a.knob]
+    base = {"pp": 0, "as128": 0, "rln": 222, "variant": 512}[a.knob]
     set_knob = {"pp": L.nomic_gemm_set_pp, "as128": L.nomic_gemm_set_as128,
-                "rln": L.nomic_gemm_res_ln_set_variant}[a.knob]
+                "rln": L.nomic_gemm_res_ln_set_variant, "variant": L.nomic_gemm_set_variant}[a.knob]
     torch.manual_seed(5)
     # (name, mode, M, N, K): the encoder's SwiGLU shape, a partial row tile, a long K, the qkv shape
     shapes = [("ffn_swiglu", 2, 32768, 6144, 768), ("swiglu_tail", 2, 5000, 2048, 768),
@@ -32,6 +32,7 @@ def main():
     if a.knob == "rln":  # mode -1: the row-complete residual + LayerNorm kernel (N = 768)
         shapes = [("o_proj", -1, 32768, 768, 768), ("down", -1, 32768, 768, 3072), ("tail", -1, 4100, 768, 3072)]
     pv = L.nomic_gemm_set_variant(128 if a.knob == "as128" else 256)
+    pp_prev = L.nomic_gemm_set_pp(2)
     try:
         for name, mode, M, N, K in shapes:
             A = (torch.rand(M, K, device="cuda") * 2 - 1).bfloat16()
@@ -66,8 +67,9 @@ def main():
                               "mismatching_runs": bad, "max_abs_diff": worst}), flush=True)
             del A, W, ref, out
     finally:
-        L.nomic_gemm_set_variant(pv)
         set_knob(base if a.knob == "rln" else (2 if a.knob == "pp" else 0))
+        L.nomic_gemm_set_variant(pv)
+        L.nomic_gemm_set_pp(pp_prev)
 
 
 if __name__ == "__main__":

@@ -19,9 +19,9 @@ def L0():
 
 
 @pytest.fixture(params=[(512, 0, 0), (513, 0, 0), (256, 0, 0), (128, 0, 0), (512, 1, 0), (512, 2, 0), (256, 1, 0),
-                        (256, 2, 0), (256, 0, 1), (256, 0, 2), (128, 0, 9)],
+                        (256, 2, 0), (256, 0, 1), (256, 0, 2), (128, 0, 9), (515, 0, 0)],
                 ids=["gemm_p", "gemm_r", "gemm256", "gemm128", "gemm_p_ilv1", "gemm_p_ilv2", "gemm256_ilv1",
-                     "gemm256_ilv2", "gemm256_pp", "gemm256_peeled", "gemm128_asm"])
+                     "gemm256_ilv2", "gemm256_pp", "gemm256_peeled", "gemm128_asm", "gemm_p_asm"])
 def L(L0, request):
     """Run each GEMM numerics test on every kernel variant (DMA-interleave setting, ping-pong loop)."""
     prev = L0.nomic_gemm_set_variant(request.param[0])

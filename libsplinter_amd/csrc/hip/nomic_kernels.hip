@@ -8,6 +8,7 @@
 //                    straight into arena slots under the seqlock     (K17 + K9)
 //   nomic_dequant    GGUF F32/F16/BF16/Q8_0/Q4_0/Q4_1/Q4_K/Q6_K -> bf16
 #include <hip/hip_runtime.h>
+#include <cstdlib>
 #include <cstdint>
 
 #include "arena_dev.hpp"
@@ -719,6 +720,180 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
   }
 }
 
+// k_attn4: k_attn3 with the tile loop software-pipelined inside each wave (the FA3 idea on one wave):
+// iteration t issues the QK^T MFMAs of tile t+1 BEFORE the softmax of tile t, so the matrix pipe works on
+// S(t+1) while the VALU exponentiates S(t); then PV(t).  K/V tiles: a 3-deep LDS ring (tiles t and t+1
+// are read in iteration t, t+2 is written at its end) and one register stage (t+2's global loads issued
+// at the top of iteration t): one barrier per tile, as in k_attn3.  Two score tiles live in registers
+// (+32 VGPRs: 253, two waves per SIMD; held to three it spills 78 registers).
+template <int W = 2>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_attn4(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
+                                               const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
+                                               int heads, float scale_log2) {
+  constexpr int KT = 64, NT = 256, NL = KT * 8 / NT;
+  __shared__ __attribute__((aligned(16))) char lds[3][2][KT * 128];  // [ring slot][K | V][key * 128 B]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int hi = lane >> 5, q32 = lane & 31, li = lane & 15, tq = li >> 2, tp = li & 3;
+  const int nwg = gridDim.x, orig = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
+  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
+  const int nqb = nwg / heads, head = lid / nqb, qbi = lid - head * nqb;
+  const int seq = qblocks[2 * qbi], qstart = qblocks[2 * qbi + 1];
+  const long s0 = cu[seq], len = cu[seq + 1] - s0;
+  const long ld = 3L * heads * HD;
+  const uint16_t* Qg = qkv + head * HD;
+  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
+  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
+
+  const long qrow = qstart + wave * 32 + q32;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+    qf[ks] = qrow < len ? *(const bf16x8*)(Qg + (s0 + qrow) * ld + ks * 16 + hi * 8) : bf16x8{};
+  f32x16 o[2];
+#pragma unroll
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
+  float m = -1e30f, l = 0.f;
+
+  uint4 rk[NL], rv[NL];
+  auto gload = [&](long k0) {
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
+      if (k0 + key < len) {
+        rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
+        rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
+      } else {
+        rk[it] = make_uint4(0, 0, 0, 0);
+        rv[it] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto lwrite = [&](int slot) {
+#pragma unroll
+    for (int it = 0; it < NL; ++it) {
+      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
+      *(uint4*)(lds[slot][0] + key * 128 + (k3sw(key, ch) << 4)) = rk[it];
+      *(uint4*)(lds[slot][1] + key * 128 + (v3sw(key, ch) << 4)) = rv[it];
+    }
+  };
+  auto qk = [&](f32x16 (&sc)[2], int slot) {
+    const char* Ks = lds[slot][0];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
+      const int row = kb * 32 + q32;
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const bf16x8 kf = *(const bf16x8*)(Ks + row * 128 + (k3sw(row, 2 * ks + hi) << 4));
+        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sc[kb], 0, 0, 0);
+      }
+    }
+  };
+
+  const int ntiles = (int)((len + KT - 1) / KT);
+  gload(0);
+  lwrite(0);
+  if (ntiles > 1) {
+    gload(KT);
+    lwrite(1);
+  }
+  __syncthreads();
+  f32x16 sa[2], sb[2];
+  qk(sa, 0);
+
+  // one pipelined tile: `cur` holds S(t) (computed), `nxt` receives S(t+1)
+  auto tile = [&](int t, f32x16 (&cur)[2], f32x16 (&nxt)[2]) {
+    const long k0 = (long)t * KT;
+    const int slot = t % 3;
+    if (t + 2 < ntiles) gload(k0 + 2 * KT);
+    if (t + 1 < ntiles) qk(nxt, (t + 1) % 3);  // S(t+1) on the matrix pipe ...
+    // ... while the VALU runs the online softmax of S(t)
+    if (k0 + KT > len) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= len) cur[kb][r] = -1e30f;
+    }
+    float mx = fmaxf(cur[0][0], cur[1][0]);
+#pragma unroll
+    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(cur[0][r], cur[1][r]));
+    {
+      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+      mx = fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
+    }
+    constexpr float kThr = 8.f;
+    const float mxs = mx * scale_log2;
+    if (!__all(mxs - m <= kThr)) {
+      const float mn = fmaxf(m, mxs);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      m = mn;
+      l *= alpha;
+#pragma unroll
+      for (int db = 0; db < 2; ++db) o[db] *= alpha;
+    }
+    const float nm = -m;
+    float ps = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(cur[kb][r], scale_log2, nm));
+        cur[kb][r] = p;
+        ps += p;
+      }
+    {
+      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(ps), __float_as_uint(ps), false, false);
+      ps = __uint_as_float(q[0]) + __uint_as_float(q[1]);
+    }
+    l += ps;
+    const char* Vs = lds[slot][1];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8 pf;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)cur[kb][8 * st + j];
+        const int rowA = kb * 32 + 16 * st + 4 * hi + tq, rowB = rowA + 8;
+#pragma unroll
+        for (int db = 0; db < 2; ++db) {
+          const int col = 32 * db + 16 * ((lane >> 4) & 1) + 4 * tp;
+          const int ch = col >> 3, off = (col & 7) * 2;
+          const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4i16*)(Vs + rowA * 128 + (v3sw(rowA, ch) << 4) + off));
+          const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+              (lds_v4i16*)(Vs + rowB * 128 + (v3sw(rowB, ch) << 4) + off));
+          const bf16x8 vf = __builtin_bit_cast(bf16x8, (v8i16)__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
+          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
+        }
+      }
+    // tile t+2 into the ring slot tile t-1 used: every wave finished that slot at the barrier closing t-1
+    if (t + 2 < ntiles) lwrite((t + 2) % 3);
+    __syncthreads();
+  };
+  for (int t = 0; t < ntiles; t += 2) {
+    tile(t, sa, sb);
+    if (t + 1 < ntiles) tile(t + 1, sb, sa);
+  }
+  if (qrow < len) {
+    const float inv = 1.f / l;
+    uint16_t* dst = out + (s0 + qrow) * (long)heads * HD + head * HD;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        uint2 w;
+        w.x = pk2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv);
+        w.y = pk2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
+        *(uint2*)(dst + 32 * db + 8 * g + 4 * hi) = w;
+      }
+  }
+}
+
 // ------------------------------------------------------------ mean pool --
 __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, const int32_t* __restrict__ cu,
                                               float* __restrict__ pooled, int normalize, spl_arena_t aa,
@@ -915,7 +1090,10 @@ int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, 
   return (int)hipGetLastError();
 }
 
-static int g_attn_variant = 13;  // measured: k_attn3 (32x32x16 MFMA, 3 waves/SIMD) 634 vs 514 TFLOP/s for 6 (profiles/r3_attn_k_attn3_ab.jsonl)
+static int g_attn_variant = [] {  // NOMIC_ATTN overrides (A/B)
+  const char* e = getenv("NOMIC_ATTN");
+  return e && *e ? atoi(e) : 13;
+}();  // measured: k_attn3 (32x32x16 MFMA, 3 waves/SIMD) 634 vs 514 TFLOP/s for 6 (profiles/r3_attn_k_attn3_ab.jsonl)
 
 int nomic_attention_set_variant(int v) {
   const int prev = g_attn_variant;
@@ -943,6 +1121,9 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   else if (g_attn_variant == 8)  // 128-key tiles held to 2 waves/SIMD
     hipLaunchKernelGGL((k_attn2<2, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
                        (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
+  else if (g_attn_variant == 17)  // k_attn3 software-pipelined (S(t+1) MFMAs beside softmax(t)), 2 waves/SIMD
+    hipLaunchKernelGGL((k_attn4<2>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+                       qblocks, heads, scale_log2);
   else if (g_attn_variant == 13)  // 32x32x16 MFMA form (k_attn3)
     hipLaunchKernelGGL(k_attn3<false>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);

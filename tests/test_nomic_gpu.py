@@ -251,7 +251,7 @@ def test_gemm_layernorm_fold_modes(L):
                            None, 0, None, 0, eps, None, None, None, None, None, _stream()) != 0
 
 
-@pytest.mark.parametrize("variant", [15, 14, 13, 12, 11, 10, 9, 7, 6, 5, 4, 3, 2, 1])
+@pytest.mark.parametrize("variant", [17, 15, 14, 13, 12, 11, 10, 9, 7, 6, 5, 4, 3, 2, 1])
 @pytest.mark.parametrize("spike", [False, True])
 def test_attention_varlen(L0, variant, spike):
     L = L0

@@ -604,9 +604,10 @@ int CmdRing::init(int device, uint32_t pstride) {
   yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
   cpus_ = effective_cpus();
   sleep_ns_ = env_int("SPLINTER_RING_SLEEP_NS", 5000);  // 32 threads: 1.73 vs 1.41 M ops/s at 2000 (profiles/r3_hostapi_vram_single_store.jsonl)
-  // oversubscribed waiters sleep at once, first for ~8 us (the bulk of a 32-thread call's ~15 us):
-  // 32 threads 1.60 -> 1.85 M ops/s, mean of 3 alternating rounds (profiles/r3_hostapi_oversub_wait_ab.jsonl)
-  first_sleep_ns_ = env_int("SPLINTER_RING_FIRST_SLEEP_NS", 8000);
+  // oversubscribed waiters sleep at once, first for ~6 us (a good part of a 32-thread call's ~15 us):
+  // 32 threads 1.60 -> 1.85 M ops/s with 8 us (profiles/r3_hostapi_oversub_wait_ab.jsonl), 1.84 -> 1.99 M
+  // for 8 -> 6 us (means of 3 alternating rounds, profiles/r3_hostapi_sweep_s2.jsonl)
+  first_sleep_ns_ = env_int("SPLINTER_RING_FIRST_SLEEP_NS", 6000);
   oversub_spin_us_ = (uint64_t)env_int("SPLINTER_RING_OVERSUB_SPIN_US", 0);
 #ifndef SPL_RING_POLL4
   // default on: 1 thread p50 9.1 -> 7.3 us, 16 threads 1.18 -> 1.50 M ops/s (profiles/r3_hostapi_vram_ab.jsonl);

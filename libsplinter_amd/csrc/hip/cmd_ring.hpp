@@ -156,7 +156,7 @@ class CmdRing {
   int init_vram();
   std::atomic<int> waiters_{0};   // host threads waiting on a completion right now
   long sleep_ns_ = 5000;          // SPLINTER_RING_SLEEP_NS: sleep between polls while oversubscribed
-  long first_sleep_ns_ = 8000;    // SPLINTER_RING_FIRST_SLEEP_NS: the first of those sleeps (a call's bulk)
+  long first_sleep_ns_ = 6000;    // SPLINTER_RING_FIRST_SLEEP_NS: the first of those sleeps (a call's bulk)
   uint64_t oversub_spin_us_ = 0;  // SPLINTER_RING_OVERSUB_SPIN_US: spin this long first while oversubscribed
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;

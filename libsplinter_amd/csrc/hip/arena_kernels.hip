@@ -1112,7 +1112,7 @@ static int set_seg_at(spl_arena_t a, const char* keys, int kstride, const uint8_
   // cooperative value-row copy: 2 = write-through rows, no per-round release (default: KV-only 2.73 -> 3.15 G
   // ops/s, mixed step 15.5 -> 14.7 ms, profiles/r3_kv_set_writethrough.md); 1 = plain rows + release; 0 = per lane
   static const int coop = env_int("SPLINTER_ARENA_COOP", 2);
-  if (carry && !wt && (u == 2 || u == 4)) {
+  if (carry && !wt && (u == 2 || u == 4 || (u == 1 && coop == 2 && b == 256))) {
 #define SPL_SET_CARRY(U_, B_)                                                                                   \
   hipLaunchKernelGGL((k_set_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
                      kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
@@ -1140,6 +1140,9 @@ static int set_seg_at(spl_arena_t a, const char* keys, int kstride, const uint8_
     else if (u == 2 && b == 256 && coop == 2)
       hipLaunchKernelGGL((k_set_carry<2, 256, 16, true, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s,
                          a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
+    else if (u == 1)  // (coop 2, 256 threads: the condition above) one op per lane, carried retries
+      hipLaunchKernelGGL((k_set_carry<1, 256, 16, true, true>), dim3(grid_for_b(n, 256)), dim3(256), 0, s, a, keys,
+                         kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
     else if (u == 4 && b == 256 && coop == 2)  // write-through rows, no release (see k_set_carry)
       hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s,
                          a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);

@@ -228,6 +228,127 @@ __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* 
 // scores keys [j c, (j + 1) c) with c = ceil(L / S) rounded up to 64 and writes its unnormalised
 // partial (m, l, acc[hd]) to ws; k_attn_combine merges the S partials of a head.  One workgroup per
 // head streams the whole cache through one CU (164 GB/s at L = 8192, profiles/r2_decode_q4.md).
+// k_attn_decode_g: decode attention for caches of at most kSmallL keys (the single-workgroup regime).
+// One workgroup per KV head serves its G query heads, so every K / V row is read once for the group
+// instead of once per head, and no phase walks the keys one at a time:
+//   scores  hd/8 lanes per key row (16-B pieces), U rows per lane in flight, G dot products per piece,
+//           reduced across the row's lanes with xor shuffles -> LDS sc[g][key] (q pre-scaled)
+//   softmax one wave per head: max, exp, sum over the keys in LDS
+//   P V     the same row pieces of V, U rows in flight, fp32 accumulators per (head, 8 dims), then a
+//           reduction over the 256/(hd/8) key groups through LDS.
+// The single-workgroup kernel below it walks each wave's 64 keys serially in P V (a shuffle and a
+// 4-B load per key): 28 us per layer at a 300-key cache, llama-7B heads (profiles/r3_decode_splits_short_ctx.jsonl).
+constexpr int kSmallL = 512;
+template <int D, int G>
+__global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restrict__ q, const uint16_t* __restrict__ K,
+                                                       const uint16_t* __restrict__ V, long ldkv, int L, float scale,
+                                                       uint16_t* __restrict__ out, const int32_t* __restrict__ st) {
+  constexpr int hd = 64 * D, TPK = hd / 8, KP = 256 / TPK, U = 8;
+  static_assert(64 % TPK == 0, "a key row's lanes must sit in one wave");
+  if (st) L = st[0] + 1;
+  if (L > kSmallL) L = kSmallL;  // the host picks this kernel only for capacities <= kSmallL
+  const int kvh = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int sub = tid % TPK, kg = tid / TPK;
+  __shared__ float sc[G][kSmallL];
+  __shared__ float red[KP][G][hd];
+  __shared__ float lsum[G];
+  float qv[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    float f[8];
+    unpack8(*(const uint4*)(q + (long)(kvh * G + g) * hd + sub * 8), f);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) qv[g][e] = f[e] * scale;
+  }
+  const uint16_t* Kb = K + (long)kvh * hd + sub * 8;
+  const uint16_t* Vb = V + (long)kvh * hd + sub * 8;
+  // ---- scores
+  for (int j0 = 0; j0 < L; j0 += KP * U) {
+    uint4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * KP + kg;
+      r[u] = j < L ? *(const uint4*)(Kb + (long)j * ldkv) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * KP + kg;
+      float f[8], d[G];
+      unpack8(r[u], f);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        d[g] = 0.f;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[g] = fmaf(f[e], qv[g][e], d[g]);
+#pragma unroll
+        for (int o = TPK / 2; o >= 1; o >>= 1) d[g] += __shfl_xor(d[g], o, 64);
+      }
+      if (sub == 0 && j < L) {
+#pragma unroll
+        for (int g = 0; g < G; ++g) sc[g][j] = d[g];
+      }
+    }
+  }
+  __syncthreads();
+  // ---- softmax, one wave per head
+  for (int g = wave; g < G; g += 4) {
+    float mx = -INFINITY;
+    for (int j = lane; j < L; j += 64) mx = fmaxf(mx, sc[g][j]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    float sum = 0.f;
+    for (int j = lane; j < L; j += 64) {
+      const float p = __expf(sc[g][j] - mx);
+      sc[g][j] = p;
+      sum += p;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
+    if (lane == 0) lsum[g] = sum;
+  }
+  __syncthreads();
+  // ---- P V
+  float acc[G][8];
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[g][e] = 0.f;
+  for (int j0 = 0; j0 < L; j0 += KP * U) {
+    uint4 r[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * KP + kg;
+      r[u] = j < L ? *(const uint4*)(Vb + (long)j * ldkv) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = j0 + u * KP + kg;
+      if (j < L) {
+        float f[8];
+        unpack8(r[u], f);
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const float p = sc[g][j];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[g][e] = fmaf(p, f[e], acc[g][e]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) red[kg][g][sub * 8 + e] = acc[g][e];
+  __syncthreads();
+  for (int idx = tid; idx < G * hd; idx += 256) {
+    const int g = idx / hd, d = idx - g * hd;
+    float o = 0.f;
+#pragma unroll 8
+    for (int k = 0; k < KP; ++k) o += red[k][g][d];
+    out[(long)(kvh * G + g) * hd + d] = __builtin_bit_cast(uint16_t, (__bf16)(o / lsum[g]));
+  }
+}
+
 constexpr int kSplitWaves = 4;
 constexpr int kMaxSplits = 32;
 
@@ -1644,9 +1765,28 @@ int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, i
     hipLaunchKernelGGL(k_attn_combine, dim3((unsigned)H), dim3(256), 0, s, ws, S, hd, (uint16_t*)out);
     return (int)hipGetLastError();
   }
-  const dim3 g((unsigned)H), b(kDecWaves * 64);
   const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
   uint16_t* oo = (uint16_t*)out;
+  // caches of at most kSmallL keys: the grouped three-phase kernel (SPL_DEC_SMALL=0: the per-head one)
+  static const int small = [] {
+    const char* e = getenv("SPL_DEC_SMALL");
+    return e && *e ? atoi(e) : 0;
+  }();
+  if (small && L <= kSmallL && (hd == 64 || hd == 128 || hd == 256) && (grp == 1 || grp == 2 || grp == 4 || grp == 8)) {
+    const dim3 gg((unsigned)KVH), bb(256);
+#define SMALL(D_, G_) hipLaunchKernelGGL((k_attn_decode_g<D_, G_>), gg, bb, 0, s, qq, kk, vv, ldkv, L, scale, oo, st)
+#define SMALL_G(D_) switch (grp) { case 1: SMALL(D_, 1); break; case 2: SMALL(D_, 2); break; \
+                                   case 4: SMALL(D_, 4); break; default: SMALL(D_, 8); break; }
+    switch (hd) {
+      case 64: SMALL_G(1); break;
+      case 128: SMALL_G(2); break;
+      default: SMALL_G(4); break;
+    }
+#undef SMALL_G
+#undef SMALL
+    return (int)hipGetLastError();
+  }
+  const dim3 g((unsigned)H), b(kDecWaves * 64);
   switch (hd / 64) {
     case 1: hipLaunchKernelGGL(k_attn_decode<1>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo, st); break;
     case 2: hipLaunchKernelGGL(k_attn_decode<2>, g, b, 0, s, qq, kk, vv, ldkv, L, grp, hd, scale, oo, st); break;

@@ -102,7 +102,7 @@ def test_decoder_rmsnorm_rope_kernels_vs_fp32():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("hd,H,KVH", [(128, 32, 8), (64, 8, 8), (128, 16, 2)])
+@pytest.mark.parametrize("hd,H,KVH", [(128, 32, 8), (64, 8, 8), (128, 16, 2), (256, 8, 1), (64, 16, 8), (192, 8, 4)])
 def test_decoder_attn_decode_kernel_vs_fp32(hd, H, KVH):
     """dec_attn_decode (csrc/hip/decoder_kernels.hip) against an fp32 softmax(q k^T) v reference,
     cache lengths on both sides of the 64-key chunk and 256-key workgroup boundaries; past 512 keys
@@ -116,12 +116,16 @@ def test_decoder_attn_decode_kernel_vs_fp32(hd, H, KVH):
     kv = torch.randn((2, n_ctx, KVH, hd), device="cuda", generator=g).to(torch.bfloat16)
     q = torch.randn((H * hd,), device="cuda", generator=g).to(torch.bfloat16)
     st = torch.zeros(4, dtype=torch.int32, device="cuda")
-    for L, dev_len in ((1, False), (63, False), (64, False), (65, False), (257, False), (1100, False),
-                       (4097, False), (5000, False), (1, True), (700, True), (5000, True)):
+    # (length, device-side length, capacity): up to 512 keys the grouped short-cache kernel, also driven by a
+    # device-side length under a small capacity (a graph-captured step of a short context)
+    for L, dev_len, cap in ((1, False, 0), (63, False, 0), (64, False, 0), (65, False, 0), (257, False, 0),
+                            (512, False, 0), (1100, False, 0), (4097, False, 0), (5000, False, 0), (1, True, n_ctx),
+                            (700, True, n_ctx), (5000, True, n_ctx), (1, True, 512), (300, True, 512),
+                            (512, True, 512)):
         out = torch.full((H * hd,), float("nan"), device="cuda").to(torch.bfloat16)
         if dev_len:
             st[0] = L - 1
-            assert m.L.dec_attn_decode_st(q.data_ptr(), kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, n_ctx, H, KVH,
+            assert m.L.dec_attn_decode_st(q.data_ptr(), kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, cap, H, KVH,
                                           hd, hd ** -0.5, out.data_ptr(), st.data_ptr(), None) == 0
         else:
             assert m.L.dec_attn_decode(q.data_ptr(), kv[0].data_ptr(), kv[1].data_ptr(), KVH * hd, L, H, KVH, hd,

@@ -235,31 +235,24 @@ __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* 
 //           reduced across the row's lanes with xor shuffles -> LDS sc[g][key] (q pre-scaled)
 //   softmax one wave per head: max, exp, sum over the keys in LDS
 //   P V     the same row pieces of V, U rows in flight, fp32 accumulators per (head, 8 dims), then a
-//           reduction over the key groups: xor shuffles inside a wave, LDS across the waves.
+//           reduction over the 256/(hd/8) key groups through LDS.
 // The single-workgroup kernel below it walks each wave's 64 keys serially in P V (a shuffle and a
-// 4-B load per key): 28 us per layer at a 300-key cache, llama-7B heads (profiles/r3_decode_splits_short_ctx.jsonl).
-// Up to 16 waves, so a 512-key cache is one round of loads per phase.
+// 4-B load per key): 28 us per layer at a 300-key cache, llama-7B heads (profiles/r3_decode_splits_short_ctx.jsonl);
+// this kernel 11.5 us, q4 decode 0.715 -> 0.577 ms/token (profiles/r3_decode_attn_small_ab.jsonl).  A 16-wave form
+// (one load round per phase, shuffle + LDS reduction) measured slower: 14.1 us (r3_decode_attn_small_wide_ab.jsonl).
 constexpr int kSmallL = 512;
-// waves per workgroup: 16 (128 registers per lane), 8 for 8 heads per KV head (their accumulators need more),
-// and fewer when the per-wave partial sums (G x hd fp32) would pass 64 KB of LDS
 template <int D, int G>
-constexpr int small_waves() {
-  return G >= 8 ? (8 * G * 64 * D * 4 <= 65536 ? 8 : 65536 / (G * 64 * D * 4))
-                : (16 * G * 64 * D * 4 <= 65536 ? 16 : 65536 / (G * 64 * D * 4));
-}
-template <int D, int G>
-__global__ __launch_bounds__((64 * small_waves<D, G>())) void k_attn_decode_g(
-    const uint16_t* __restrict__ q, const uint16_t* __restrict__ K, const uint16_t* __restrict__ V, long ldkv, int L,
-    float scale, uint16_t* __restrict__ out, const int32_t* __restrict__ st) {
-  constexpr int NW = small_waves<D, G>(), NT = 64 * NW;
-  constexpr int hd = 64 * D, TPK = hd / 8, KP = NT / TPK, U = 8;
+__global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restrict__ q, const uint16_t* __restrict__ K,
+                                                       const uint16_t* __restrict__ V, long ldkv, int L, float scale,
+                                                       uint16_t* __restrict__ out, const int32_t* __restrict__ st) {
+  constexpr int hd = 64 * D, TPK = hd / 8, KP = 256 / TPK, U = 8;
   static_assert(64 % TPK == 0, "a key row's lanes must sit in one wave");
   if (st) L = st[0] + 1;
   if (L > kSmallL) L = kSmallL;  // the host picks this kernel only for capacities <= kSmallL
   const int kvh = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int sub = tid % TPK, kg = tid / TPK;
   __shared__ float sc[G][kSmallL];
-  __shared__ float red[NW][G][hd];
+  __shared__ float red[KP][G][hd];
   __shared__ float lsum[G];
   float qv[G][8];
 #pragma unroll
@@ -300,7 +293,7 @@ __global__ __launch_bounds__((64 * small_waves<D, G>())) void k_attn_decode_g(
   }
   __syncthreads();
   // ---- softmax, one wave per head
-  for (int g = wave; g < G; g += NW) {
+  for (int g = wave; g < G; g += 4) {
     float mx = -INFINITY;
     for (int j = lane; j < L; j += 64) mx = fmaxf(mx, sc[g][j]);
 #pragma unroll
@@ -344,25 +337,16 @@ __global__ __launch_bounds__((64 * small_waves<D, G>())) void k_attn_decode_g(
       }
     }
   }
-  // the 64 / TPK key groups of a wave (lanes sub, sub + TPK, ...) by xor shuffles, then the waves via LDS
 #pragma unroll
   for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int e = 0; e < 8; ++e)
-#pragma unroll
-      for (int o = TPK; o < 64; o <<= 1) acc[g][e] += __shfl_xor(acc[g][e], o, 64);
-  if (lane < TPK) {
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) red[wave][g][sub * 8 + e] = acc[g][e];
-  }
+    for (int e = 0; e < 8; ++e) red[kg][g][sub * 8 + e] = acc[g][e];
   __syncthreads();
-  for (int idx = tid; idx < G * hd; idx += NT) {
+  for (int idx = tid; idx < G * hd; idx += 256) {
     const int g = idx / hd, d = idx - g * hd;
     float o = 0.f;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) o += red[w][g][d];
+#pragma unroll 8
+    for (int k = 0; k < KP; ++k) o += red[k][g][d];
     out[(long)(kvh * G + g) * hd + d] = __builtin_bit_cast(uint16_t, (__bf16)(o / lsum[g]));
   }
 }
@@ -1788,12 +1772,11 @@ int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, i
   // caches of at most kSmallL keys: the grouped three-phase kernel (SPL_DEC_SMALL=0: the per-head one)
   static const int small = [] {
     const char* e = getenv("SPL_DEC_SMALL");
-    return e && *e ? atoi(e) : 0;
+    return e && *e ? atoi(e) : 1;
   }();
   if (small && L <= kSmallL && (hd == 64 || hd == 128 || hd == 256) && (grp == 1 || grp == 2 || grp == 4 || grp == 8)) {
-    const dim3 gg((unsigned)KVH);
-#define SMALL(D_, G_) hipLaunchKernelGGL((k_attn_decode_g<D_, G_>), gg, dim3(64 * small_waves<D_, G_>()), 0, s, qq, kk, \
-                                         vv, ldkv, L, scale, oo, st)
+    const dim3 gg((unsigned)KVH), bb(256);
+#define SMALL(D_, G_) hipLaunchKernelGGL((k_attn_decode_g<D_, G_>), gg, bb, 0, s, qq, kk, vv, ldkv, L, scale, oo, st)
 #define SMALL_G(D_) switch (grp) { case 1: SMALL(D_, 1); break; case 2: SMALL(D_, 2); break; \
                                    case 4: SMALL(D_, 4); break; default: SMALL(D_, 8); break; }
     switch (hd) {

@@ -240,20 +240,32 @@ __global__ __launch_bounds__(kDecWaves * 64) void k_attn_decode(const uint16_t* 
 // 4-B load per key): 28 us per layer at a 300-key cache, llama-7B heads (profiles/r3_decode_splits_short_ctx.jsonl);
 // this kernel 11.5 us, q4 decode 0.715 -> 0.577 ms/token (profiles/r3_decode_attn_small_ab.jsonl).  A 16-wave form
 // (one load round per phase, shuffle + LDS reduction) measured slower: 14.1 us (r3_decode_attn_small_wide_ab.jsonl).
+// Its split form runs the flash-decoding splits of longer caches: 3000-token prompt 0.840 -> 0.672 ms/token at 4 bits
+// (profiles/r3_decode_attn_grouped_split_ab.jsonl).
 constexpr int kSmallL = 512;
-template <int D, int G>
+// SPLIT: the same kernel as one split of the flash-decoding form -- workgroup (kvh, j) takes keys
+// [j * chunk, (j + 1) * chunk) (chunk <= kSmallL, the k_attn_decode_split geometry) and writes each head's
+// partial (max, sum, unnormalised P V) to ws for k_attn_combine.
+template <int D, int G, bool SPLIT = false>
 __global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restrict__ q, const uint16_t* __restrict__ K,
                                                        const uint16_t* __restrict__ V, long ldkv, int L, float scale,
-                                                       uint16_t* __restrict__ out, const int32_t* __restrict__ st) {
+                                                       uint16_t* __restrict__ out, const int32_t* __restrict__ st,
+                                                       float* __restrict__ ws = nullptr) {
   constexpr int hd = 64 * D, TPK = hd / 8, KP = 256 / TPK, U = 8;
   static_assert(64 % TPK == 0, "a key row's lanes must sit in one wave");
   if (st) L = st[0] + 1;
-  if (L > kSmallL) L = kSmallL;  // the host picks this kernel only for capacities <= kSmallL
+  int k0 = 0, k1 = L < kSmallL ? L : kSmallL;  // one workgroup: the host picks it only for capacities <= kSmallL
+  if constexpr (SPLIT) {
+    const int S = gridDim.y, chunk = ((L + S - 1) / S + 63) / 64 * 64;
+    k0 = blockIdx.y * chunk;
+    k1 = min(L, k0 + min(chunk, kSmallL));  // the host guarantees chunk <= kSmallL
+  }
+  const int n = k1 > k0 ? k1 - k0 : 0;
   const int kvh = blockIdx.x, tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int sub = tid % TPK, kg = tid / TPK;
   __shared__ float sc[G][kSmallL];
   __shared__ float red[KP][G][hd];
-  __shared__ float lsum[G];
+  __shared__ float lsum[G], lmax[G];
   float qv[G][8];
 #pragma unroll
   for (int g = 0; g < G; ++g) {
@@ -262,15 +274,15 @@ __global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restric
 #pragma unroll
     for (int e = 0; e < 8; ++e) qv[g][e] = f[e] * scale;
   }
-  const uint16_t* Kb = K + (long)kvh * hd + sub * 8;
-  const uint16_t* Vb = V + (long)kvh * hd + sub * 8;
+  const uint16_t* Kb = K + (long)kvh * hd + sub * 8 + (long)k0 * ldkv;
+  const uint16_t* Vb = V + (long)kvh * hd + sub * 8 + (long)k0 * ldkv;
   // ---- scores
-  for (int j0 = 0; j0 < L; j0 += KP * U) {
+  for (int j0 = 0; j0 < n; j0 += KP * U) {
     uint4 r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = j0 + u * KP + kg;
-      r[u] = j < L ? *(const uint4*)(Kb + (long)j * ldkv) : make_uint4(0, 0, 0, 0);
+      r[u] = j < n ? *(const uint4*)(Kb + (long)j * ldkv) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -285,7 +297,7 @@ __global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restric
 #pragma unroll
         for (int o = TPK / 2; o >= 1; o >>= 1) d[g] += __shfl_xor(d[g], o, 64);
       }
-      if (sub == 0 && j < L) {
+      if (sub == 0 && j < n) {
 #pragma unroll
         for (int g = 0; g < G; ++g) sc[g][j] = d[g];
       }
@@ -295,18 +307,21 @@ __global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restric
   // ---- softmax, one wave per head
   for (int g = wave; g < G; g += 4) {
     float mx = -INFINITY;
-    for (int j = lane; j < L; j += 64) mx = fmaxf(mx, sc[g][j]);
+    for (int j = lane; j < n; j += 64) mx = fmaxf(mx, sc[g][j]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
     float sum = 0.f;
-    for (int j = lane; j < L; j += 64) {
+    for (int j = lane; j < n; j += 64) {
       const float p = __expf(sc[g][j] - mx);
       sc[g][j] = p;
       sum += p;
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 64);
-    if (lane == 0) lsum[g] = sum;
+    if (lane == 0) {
+      lsum[g] = sum;
+      lmax[g] = mx;
+    }
   }
   __syncthreads();
   // ---- P V
@@ -315,17 +330,17 @@ __global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restric
   for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int e = 0; e < 8; ++e) acc[g][e] = 0.f;
-  for (int j0 = 0; j0 < L; j0 += KP * U) {
+  for (int j0 = 0; j0 < n; j0 += KP * U) {
     uint4 r[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = j0 + u * KP + kg;
-      r[u] = j < L ? *(const uint4*)(Vb + (long)j * ldkv) : make_uint4(0, 0, 0, 0);
+      r[u] = j < n ? *(const uint4*)(Vb + (long)j * ldkv) : make_uint4(0, 0, 0, 0);
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int j = j0 + u * KP + kg;
-      if (j < L) {
+      if (j < n) {
         float f[8];
         unpack8(r[u], f);
 #pragma unroll
@@ -342,12 +357,30 @@ __global__ __launch_bounds__(256) void k_attn_decode_g(const uint16_t* __restric
 #pragma unroll
     for (int e = 0; e < 8; ++e) red[kg][g][sub * 8 + e] = acc[g][e];
   __syncthreads();
-  for (int idx = tid; idx < G * hd; idx += 256) {
-    const int g = idx / hd, d = idx - g * hd;
-    float o = 0.f;
+  if constexpr (SPLIT) {
+    // ws[head][split][hd + 2] = (max, sum, unnormalised P V): the k_attn_decode_split layout; an empty split
+    // leaves max = -inf, sum 0 (k_attn_combine gives it weight 0)
+    const int S = gridDim.y;
+    for (int idx = tid; idx < G * (hd + 2); idx += 256) {
+      const int g = idx / (hd + 2), c = idx - g * (hd + 2);
+      float v;
+      if (c == 0) v = n ? lmax[g] : -INFINITY;
+      else if (c == 1) v = n ? lsum[g] : 0.f;
+      else {
+        v = 0.f;
 #pragma unroll 8
-    for (int k = 0; k < KP; ++k) o += red[k][g][d];
-    out[(long)(kvh * G + g) * hd + d] = __builtin_bit_cast(uint16_t, (__bf16)(o / lsum[g]));
+        for (int k = 0; k < KP; ++k) v += red[k][g][c - 2];
+      }
+      ws[((long)(kvh * G + g) * S + blockIdx.y) * (hd + 2) + c] = v;
+    }
+  } else {
+    for (int idx = tid; idx < G * hd; idx += 256) {
+      const int g = idx / hd, d = idx - g * hd;
+      float o = 0.f;
+#pragma unroll 8
+      for (int k = 0; k < KP; ++k) o += red[k][g][d];
+      out[(long)(kvh * G + g) * hd + d] = __builtin_bit_cast(uint16_t, (__bf16)(o / lsum[g]));
+    }
   }
 }
 
@@ -1746,9 +1779,33 @@ int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, i
     return (int)hipErrorInvalidValue;
   const int grp = H / KVH;
   const int S = decode_splits(L);
+  // SPL_DEC_SMALL: caches of at most kSmallL keys on the grouped three-phase kernel, and the splits of longer
+  // ones on its split form (chunks of at most kSmallL keys); 0 = the per-head / per-group walking kernels
+  static const int small = [] {
+    const char* e = getenv("SPL_DEC_SMALL");
+    return e && *e ? atoi(e) : 1;
+  }();
+  const bool grouped = small && (hd == 64 || hd == 128 || hd == 256) && (grp == 1 || grp == 2 || grp == 4 || grp == 8);
   if (S > 1 && H <= 128) {
     if (!ws) ws = split_workspace(s);
     if (!ws) return (int)hipErrorOutOfMemory;
+    if (grouped && ((L + S - 1) / S + 63) / 64 * 64 <= kSmallL) {
+      const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
+      const dim3 gg((unsigned)KVH, (unsigned)S), bb(256);
+#define GSPLIT(D_, G_) hipLaunchKernelGGL((k_attn_decode_g<D_, G_, true>), gg, bb, 0, s, qq, kk, vv, ldkv, L, scale, \
+                                          (uint16_t*)nullptr, st, ws)
+#define GSPLIT_G(D_) switch (grp) { case 1: GSPLIT(D_, 1); break; case 2: GSPLIT(D_, 2); break; \
+                                    case 4: GSPLIT(D_, 4); break; default: GSPLIT(D_, 8); break; }
+      switch (hd) {
+        case 64: GSPLIT_G(1); break;
+        case 128: GSPLIT_G(2); break;
+        default: GSPLIT_G(4); break;
+      }
+#undef GSPLIT_G
+#undef GSPLIT
+      hipLaunchKernelGGL(k_attn_combine, dim3((unsigned)H), dim3(256), 0, s, ws, S, hd, (uint16_t*)out);
+      return (int)hipGetLastError();
+    }
     // heads per workgroup: the whole kv group when it is 2, 4 or 8 heads (shared K/V rows), else 1
     const int G = (grp == 2 || grp == 4 || grp == 8) ? grp : 1;
     const dim3 gs((unsigned)(H / G), (unsigned)S), bs(kSplitWaves * 64);
@@ -1769,14 +1826,10 @@ int dec_attn_decode_ws(const void* q, const void* k, const void* v, long ldkv, i
   }
   const uint16_t *qq = (const uint16_t*)q, *kk = (const uint16_t*)k, *vv = (const uint16_t*)v;
   uint16_t* oo = (uint16_t*)out;
-  // caches of at most kSmallL keys: the grouped three-phase kernel (SPL_DEC_SMALL=0: the per-head one)
-  static const int small = [] {
-    const char* e = getenv("SPL_DEC_SMALL");
-    return e && *e ? atoi(e) : 1;
-  }();
-  if (small && L <= kSmallL && (hd == 64 || hd == 128 || hd == 256) && (grp == 1 || grp == 2 || grp == 4 || grp == 8)) {
+  if (grouped && L <= kSmallL) {
     const dim3 gg((unsigned)KVH), bb(256);
-#define SMALL(D_, G_) hipLaunchKernelGGL((k_attn_decode_g<D_, G_>), gg, bb, 0, s, qq, kk, vv, ldkv, L, scale, oo, st)
+#define SMALL(D_, G_) hipLaunchKernelGGL((k_attn_decode_g<D_, G_>), gg, bb, 0, s, qq, kk, vv, ldkv, L, scale, oo, st, \
+                                         (float*)nullptr)
 #define SMALL_G(D_) switch (grp) { case 1: SMALL(D_, 1); break; case 2: SMALL(D_, 2); break; \
                                    case 4: SMALL(D_, 4); break; default: SMALL(D_, 8); break; }
     switch (hd) {

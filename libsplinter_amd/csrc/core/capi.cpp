@@ -15,7 +15,9 @@
 #include <poll.h>
 #include <string>
 #include <vector>
+#include <fcntl.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -260,18 +262,32 @@ int spl_unlink(const char* raw) {
   if (p.kind == Kind::File) return unlink(p.name.c_str());
   if (p.kind == Kind::Hbm) return shm_unlink((p.name + ".hbm").c_str());
   if (p.kind == Kind::Node) {
-    // every shard of the node, then its descriptor
-    int err = 0;
-    spl::NodeStore* n = spl::NodeStore::open(p.name, &err);
+    // every shard of the node, then its descriptor.  The shard count and backend come straight from
+    // the mapped descriptor (no NodeStore::open, which would import every arena and refuses a node
+    // whose create failed half way), so an unusable node can still be cleaned up.
     int rc = 0;
-    if (n) {
-      const int k = n->nshards();
-      const uint32_t backend = strcmp(n->shard(0)->backend(), "hbm") == 0 ? 1u : 0u;
-      delete n;
-      for (int i = 0; i < k; ++i)
-        if (spl_unlink(spl::node_shard_name(p.name, i, backend).c_str()) != 0) rc = -1;
+    const std::string dn = p.name + ".node";
+    const int fd = shm_open(dn.c_str(), O_RDONLY | O_CLOEXEC, 0);
+    if (fd >= 0) {
+      struct stat st;
+      uint32_t k = 0, backend = 0;
+      if (fstat(fd, &st) == 0 && (size_t)st.st_size >= sizeof(spl::NodeDesc)) {
+        void* m = mmap(nullptr, sizeof(spl::NodeDesc), PROT_READ, MAP_SHARED, fd, 0);
+        if (m != MAP_FAILED) {
+          const auto* d = (const spl::NodeDesc*)m;
+          k = d->nshards;
+          backend = d->backend;
+          munmap(m, sizeof(spl::NodeDesc));
+        }
+      }
+      close(fd);
+      if (k > (uint32_t)spl::kNodeMaxShards || backend > 1) k = 0;
+      for (uint32_t i = 0; i < k; ++i) {
+        const std::string sn = spl::node_shard_name(p.name, (int)i, backend);
+        if (spl_unlink(sn.c_str()) != 0 && errno != ENOENT) rc = -1;
+      }
     }
-    if (shm_unlink((p.name + ".node").c_str()) != 0) rc = -1;
+    if (shm_unlink(dn.c_str()) != 0) rc = -1;
     return rc;
   }
   return shm_unlink(p.name.c_str());

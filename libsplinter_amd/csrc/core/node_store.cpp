@@ -9,6 +9,7 @@
 #include <poll.h>
 #include <sys/eventfd.h>
 #include <sys/mman.h>
+#include <sys/stat.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 
@@ -43,8 +44,19 @@ NodeDesc* map_desc(const std::string& name, bool create, bool excl, bool* fresh,
     }
     if (fd < 0 && (excl || errno != EEXIST)) { *err = errno; return nullptr; }
   }
-  if (fd < 0) fd = shm_open(dn.c_str(), O_RDWR | O_CLOEXEC, 0666);
-  if (fd < 0) { *err = errno; return nullptr; }
+  if (fd < 0) {
+    fd = shm_open(dn.c_str(), O_RDWR | O_CLOEXEC, 0666);
+    if (fd < 0) { *err = errno; return nullptr; }
+    // a rank that lost the O_EXCL race may see the winner's object before its ftruncate: wait (up
+    // to 5 s) until the descriptor is full size, so the first read of d->magic cannot SIGBUS
+    struct stat st;
+    for (int i = 0;; ++i) {
+      if (fstat(fd, &st) != 0) { *err = errno; close(fd); return nullptr; }
+      if ((size_t)st.st_size >= desc_span()) break;
+      if (i >= 5000) { *err = ETIMEDOUT; close(fd); return nullptr; }
+      usleep(1000);
+    }
+  }
   void* p = mmap(nullptr, desc_span(), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (p == MAP_FAILED) { *err = errno; return nullptr; }
@@ -59,6 +71,20 @@ bool wait_magic(NodeDesc* d, int ms) {
     usleep(1000);
   }
   return __atomic_load_n(&d->magic, __ATOMIC_ACQUIRE) == kNodeMagic;
+}
+
+// posix_madvise over [a, a+l) widened to page boundaries (the reference aligns the same way,
+// splinter.c:1329-1377); errno-style return as posix_madvise
+int forward_advice(void* a, size_t l, int advice) {
+  const long pg = sysconf(_SC_PAGESIZE);
+  if (pg > 0) {
+    const uintptr_t x = (uintptr_t)a, al = x & ~((uintptr_t)pg - 1);
+    l += (size_t)(x - al);
+    a = (void*)al;
+  }
+  const int rc = posix_madvise(a, l, advice);
+  if (rc != 0) errno = rc;
+  return rc;
 }
 
 int hbm_devices() {
@@ -134,7 +160,16 @@ NodeStore* NodeStore::create(const std::string& name, size_t slots, size_t max_v
   for (int i = 0; i < n; ++i) {
     StoreBase* sh = make_shard(name, i, backend, true, per, max_val, emb, backend == 1 ? i % ndev : -1, err);
     if (!sh) {
+      // roll back whatever backend: the shards made so far and the descriptor, so the name is free
+      // again (host shards would otherwise outlive the failed create and collide with the next one)
+      const int e = *err;
+      s->owner_ = false;
+      for (auto* x : s->shards_) delete x;
+      s->shards_.clear();
+      for (int j = 0; j < i; ++j) spl_unlink(node_shard_name(name, j, backend).c_str());
       delete s;
+      shm_unlink((name + ".node").c_str());
+      *err = e;
       return nullptr;
     }
     s->shards_.push_back(sh);
@@ -307,10 +342,27 @@ int NodeStore::madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t
     if (timeout != UINT64_MAX && now_ticks() >= deadline) { errno = ETIMEDOUT; return -1; }
     usleep(5000);
   }
-  (void)addr;
-  (void)len;
-  (void)advice;
-  return 0;
+  // forward the winner's advice: host shards get posix_madvise over their mapping (the whole arena
+  // when addr is NULL; an address inside one shard's mapping goes to that shard), HBM shards take
+  // their backend's documented residency no-op
+  int rc = 0;
+  for (auto* s : shards_) {
+    void* a = addr;
+    size_t l = len;
+    if (auto* hs = dynamic_cast<HostStore*>(s)) {
+      uint8_t* b = hs->base();
+      const size_t span = hs->total_bytes();
+      if (addr) {
+        if ((uint8_t*)addr < b || (uint8_t*)addr >= b + span) continue;
+        if ((uint8_t*)addr + len > b + span) l = (size_t)(b + span - (uint8_t*)addr);
+      } else {
+        a = b;
+        l = span;
+      }
+      if (forward_advice(a, l, advice) != 0) rc = -1;
+    }
+  }
+  return rc;
 }
 
 }  // namespace spl

@@ -283,9 +283,11 @@ __device__ int32_t serve(const spl_arena_t& aa, const RingCmd* c, const uint8_t*
   *out_len = 0;
   *result = 0;
   // set (write-through stores + drain) and get (acquire load of the epoch) carry their own
-  // cross-XCD ordering; every other op reads and writes the slot with plain accesses, and the
-  // next call may run on another wave on another XCD, whose L2 is not this one: acquire before
-  // (drop stale lines) and release after (write this L2 back), at agent scope
+  // cross-XCD ordering (the same write-through discipline as the batched kernels, arena_kernels.hip
+  // k_get_carry FAST); every other op reads and writes the slot with plain accesses: plain loads may
+  // hit lines this CU's L1 holds from before another XCD's write (acquire first: L1 invalidate), and
+  // plain stores leave dirty lines in this XCD's L2 that a reader on another XCD would not see
+  // (release after: L2 write-back), both at agent scope
   if (op == kRingSet) return ring_set(a, k, pay, sp, reg, len, scrub, hybrid);
   if (op == kRingGet) return ring_get(a, k, hp, cap, out_len);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
@@ -626,14 +628,21 @@ int CmdRing::init_vram() {
   uint8_t* h = (uint8_t*)vram_.host_map();
   if (!h) return -1;
   uint8_t* d = (uint8_t*)vram_.base();
-  if (hipMemset(d, 0, door_b + cmd_b) != hipSuccess) return -1;
   if (hipMalloc((void**)&served_, sizeof(uint32_t) * kRingEntries) != hipSuccess) return -1;
-  if (hipMemset(served_, 0, sizeof(uint32_t) * kRingEntries) != hipSuccess) return -1;
   if (hipHostMalloc((void**)&vdone_, sizeof(RingDone) * kRingEntries, hipHostMallocCoherent | hipHostMallocMapped) !=
       hipSuccess)
     return -1;
   std::memset(vdone_, 0, sizeof(RingDone) * kRingEntries);
-  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  // the clears go on a private non-blocking stream and only that stream is waited for: a device-wide
+  // synchronize (or a null-stream memset) would also wait for every other store's resident ring
+  // worker and for unrelated kernels, so opening a second store beside live traffic could block
+  hipStream_t z = nullptr;
+  if (hipStreamCreateWithFlags(&z, hipStreamNonBlocking) != hipSuccess) return -1;
+  const bool ok = hipMemsetAsync(d, 0, door_b + cmd_b, z) == hipSuccess &&
+                  hipMemsetAsync(served_, 0, sizeof(uint32_t) * kRingEntries, z) == hipSuccess &&
+                  hipStreamSynchronize(z) == hipSuccess;
+  (void)hipStreamDestroy(z);
+  if (!ok) return -1;
   v_door_h_ = (uint32_t*)h;
   v_cmds_h_ = (RingCmd*)(h + door_b);
   v_pay_h_ = h + door_b + cmd_b;

@@ -104,7 +104,7 @@ class Splainference:
         self.system_prompt_key = system_prompt_key
         self.max_tokens = max_tokens
         self.engine = None
-        if getattr(model, "hip", False):
+        if getattr(model, "hip", False) and getattr(model, "decode_kernel", True):
             from ..models.decoder import DecodeEngine
             self.engine = DecodeEngine(model, sampler.top_p, sampler.temp, sampler.seed, sampler.mask)
 

@@ -249,8 +249,10 @@ class CausalLM:
                 and cfg.d % 64 == 0 and cfg.ffn % 64 == 0
             if not ok:
                 raise ValueError("decoder dims must be multiples of 128 (N) / 64 (K) for the MFMA GEMM")
-            if hd not in (64, 128):
-                raise ValueError(f"head dim {hd}: the HIP prefill/decode attention kernels take 64 or 128")
+        # HIP attention where the kernels take the head dim (prefill: 64 / 128, decode: any multiple of
+        # 64 up to 256); other head dims (e.g. 80, 96) run those layers' attention on torch SDPA
+        self.prefill_kernel = hd in (64, 128)
+        self.decode_kernel = hd % 64 == 0 and hd <= 256
 
     def _declare(self):
         """ctypes signatures of the decoder kernels (csrc/hip/decoder_kernels.hip)."""
@@ -408,7 +410,7 @@ class CausalLM:
             self.kv[li, 0, self.pos: self.pos + n] = k
             self.kv[li, 1, self.pos: self.pos + n] = v
             L_ = self.pos + n
-            if self.hip and self.attn_kernel and n > 1:
+            if self.hip and self.attn_kernel and self.prefill_kernel and n > 1:
                 # prompt prefill, fresh or continuing a live cache: causal MFMA attention of the n new
                 # queries over cache rows 0 .. pos+n-1 (dec_attn_prefill_kv, hd 64 / 128)
                 from .nomic import _chk, _stream
@@ -416,7 +418,7 @@ class CausalLM:
                 _chk(self.L.dec_attn_prefill_kv(qkv.data_ptr(), qkv.stride(0), self.kv[li, 0].data_ptr(),
                                                 self.kv[li, 1].data_ptr(), KVH * hd, n, self.pos, H, KVH, hd,
                                                 hd ** -0.5, a.data_ptr(), cfg.d, _stream()), "attn_prefill")
-            elif self.hip and self.attn_kernel and n == 1:
+            elif self.hip and self.attn_kernel and self.decode_kernel and n == 1:
                 # per-token decode: dec_attn_decode (one workgroup per q head, split-L online softmax)
                 from .nomic import _chk, _stream
                 a = torch.empty((1, cfg.d), dtype=qkv.dtype, device=self.device)
@@ -461,6 +463,9 @@ class DecodeEngine:
     def __init__(self, model: "CausalLM", top_p: float = 0.9, temp: float = 0.7, seed: int = 0xFFFFFFFF,
                  mask: Optional[torch.Tensor] = None, use_graph: bool = True):
         assert model.hip, "DecodeEngine runs on the GPU"
+        if not model.decode_kernel:
+            raise ValueError(f"head dim {model.cfg.head_dim}: the graph decode engine needs a multiple of 64 "
+                             "up to 256 (use CausalLM.forward)")
         m, cfg = model, model.cfg
         self.m, self.top_p, self.temp, self.seed = m, float(top_p), float(temp), int(seed) & 0xFFFFFFFFFFFFFFFF
         dev = m.device

@@ -437,3 +437,51 @@ def test_cross_process_reader_races_gpu_writers(uniq):
         del st
     finally:
         a.close()
+
+
+def test_acquire_free_get_cross_xcd_hot_keys(uniq):
+    """Pins the coherence assumption of the default acquire-free get (SPLINTER_ARENA_COOP_GET=2,
+    arena_kernels.hip k_get_carry FAST): writer and reader workgroups of large grids are dealt
+    round-robin over all 8 XCDs, so every hot key below is written and read from different XCDs
+    at once.  Every returned row (not a sample) must be one intact version: the 'ver:<v>' header,
+    the id and the fill byte 'A' + v % 26 all agree."""
+    import numpy as np
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
+    a = HbmArena.create(uniq, slots=1 << 14, max_val=256, embeddings=False)
+    try:
+        hot, rep = 256, 64  # 256 keys, each repeated 64 times per batch: 16384 ops over ~64 workgroups
+        ids = torch.arange(hot, device="cuda").repeat(rep)
+        K = format_keys(hot * rep, "hx", 6, 16, ids=ids)
+        V0, L0 = format_values(hot, 1, 150, 256, ids=torch.arange(hot, device="cuda"))
+        assert (a.set(K[:hot], V0, L0) == 0).all()
+        torch.cuda.synchronize()
+        ws = [torch.cuda.Stream() for _ in range(4)]
+        rs = [torch.cuda.Stream() for _ in range(4)]
+        vals = [format_values(hot * rep, v, 150, 256, ids=ids) for v in range(2, 14)]
+        outs = []
+        torch.cuda.synchronize()
+        for j, (V, L) in enumerate(vals):
+            with torch.cuda.stream(ws[j % 4]):
+                a.set(K, V, L, retries=10000)
+            with torch.cuda.stream(rs[j % 4]):
+                outs.append(a.get(K, retries=10000))
+        torch.cuda.synchronize()
+        want_id = ids.cpu().numpy()
+        checked = 0
+        for st, out, ol in outs:
+            s_ = st.cpu().numpy()
+            o = out.cpu().numpy()
+            ln = ol.cpu().numpy()
+            assert (s_ == 0).all(), np.unique(s_, return_counts=True)
+            for i in range(o.shape[0]):
+                row = bytes(o[i, : ln[i]])
+                head, _, rest = row.partition(b"|id:")
+                ver = int(head[4:])
+                assert int(rest.split(b"|")[0]) == want_id[i]
+                fill = row[row.index(b"data:") + 5:]
+                assert fill == bytes([65 + ver % 26]) * len(fill), f"torn value at row {i}: {row[:40]!r}"
+                checked += 1
+        assert checked == len(outs) * hot * rep
+    finally:
+        a.close()

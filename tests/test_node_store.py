@@ -200,3 +200,94 @@ def test_cli_on_node_store():
     finally:
         from libsplinter_amd import store as S
         S.unlink(f"node:{name}")
+
+
+def test_node_create_failure_rolls_back(monkeypatch):
+    """A shard that cannot be created (its name is taken) fails the node create and leaves no
+    descriptor or partial shards behind, so the next create with the name free succeeds."""
+    monkeypatch.setenv("SPLINTER_NODE_BACKEND", "shm")
+    monkeypatch.setenv("SPLINTER_NODE_SHARDS", "6")
+    from libsplinter_amd import store as S
+    name = f"noderb{os.getpid()}"
+    blocker = S.Store.create(S.node_shard_name(name, 3, S.NODE_SHM), slots=64, max_val=64, embeddings=False)
+    try:
+        with pytest.raises(S.SplinterError):
+            S.Store.create(f"node:{name}", slots=6 * 64, max_val=64, embeddings=False)
+        for i in range(3):
+            assert not os.path.exists(f"/dev/shm/{name}.s{i}"), i
+        assert not os.path.exists(f"/dev/shm/{name}.node")
+        assert os.path.exists(f"/dev/shm/{name}.s3")  # not ours: the failed create must not remove it
+    finally:
+        blocker.close()
+        S.unlink(S.node_shard_name(name, 3, S.NODE_SHM))
+    s = S.Store.create(f"node:{name}", slots=6 * 64, max_val=64, embeddings=False)
+    s.set("a", b"b")
+    s.close()
+    assert S.unlink(f"node:{name}") == 0
+    assert not any(os.path.exists(f"/dev/shm/{name}.s{i}") for i in range(6))
+
+
+def test_node_unlink_without_open(monkeypatch):
+    """spl_unlink("node:NAME") cleans up a node that cannot be opened (a joined node whose other
+    ranks never attached), reading the shard count from the descriptor."""
+    monkeypatch.setenv("SPLINTER_NODE_BACKEND", "shm")
+    from libsplinter_amd import store as S
+    name = f"nodeun{os.getpid()}"
+    sh = S.Store.create(S.node_shard_name(name, 0, S.NODE_SHM), slots=64, max_val=64, embeddings=False)
+    S.node_join(name, 0, 3, S.NODE_SHM, 64, 64, embeddings=False)
+    sh.close()
+    with pytest.raises(S.SplinterBusy):
+        S.Store.open(f"node:{name}")
+    S.unlink(f"node:{name}")
+    assert not os.path.exists(f"/dev/shm/{name}.node") and not os.path.exists(f"/dev/shm/{name}.s0")
+
+
+def test_node_madvise_forwards_to_host_shards(shm_node):
+    """The node election's winner has its advice applied to every host shard (posix_madvise),
+    as the reference does for its one mapping (splinter.c:1329-1377): an advice the kernel
+    rejects surfaces as an error only if it was forwarded."""
+    S, s, name = shm_node
+    s.shard_claim(0x77, S.INTENT_WILLNEED, 90, 10 ** 12)
+    s.madvise(0x77, 3)  # POSIX_MADV_WILLNEED on every shard
+    with pytest.raises(S.SplinterError):
+        s.madvise(0x77, 12345)  # invalid advice: posix_madvise -> EINVAL from the shards
+    s.shard_release(0x77)
+
+
+def _race_rank(name, rank, world, go, q):
+    try:
+        os.environ["SPLINTER_NODE_BACKEND"] = "shm"
+        from libsplinter_amd import store as S
+        sh = S.Store.create(S.node_shard_name(name, rank, S.NODE_SHM), slots=64, max_val=64, embeddings=False)
+        go.wait(30)
+        S.node_join(name, rank, world, S.NODE_SHM, 64, 64, embeddings=False)
+        sh.close()
+        q.put((rank, 0))
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.parametrize("trial", range(3))
+def test_node_join_simultaneous(trial):
+    """Every rank released at the same instant into spl_node_join (the O_EXCL race of the
+    descriptor: a loser must wait for the winner's full-size descriptor, not SIGBUS on it)."""
+    from libsplinter_amd import store as S
+    name = f"noders{os.getpid()}t{trial}"
+    ctx = mp.get_context("fork")
+    q, go = ctx.Queue(), ctx.Event()
+    ps = [ctx.Process(target=_race_rank, args=(name, r, 8, go, q)) for r in range(8)]
+    for p in ps:
+        p.start()
+    import time
+    time.sleep(0.5)
+    go.set()
+    try:
+        res = dict(q.get(timeout=60) for _ in ps)
+        for p in ps:
+            p.join(30)
+        assert res == {r: 0 for r in range(8)}, res
+        assert all(p.exitcode == 0 for p in ps), [p.exitcode for p in ps]
+    finally:
+        os.environ["SPLINTER_NODE_BACKEND"] = "shm"
+        S.unlink(f"node:{name}")
+        os.environ.pop("SPLINTER_NODE_BACKEND", None)

@@ -213,3 +213,37 @@ def test_hostapi_32_threads(uniq):
     """32 host threads (more than the box's CPU share on a loaded host): every call served."""
     res = _hostapi(f"hbm:{uniq}", 32)
     assert res["failures"] == 0
+
+
+def test_open_second_store_beside_live_ring_traffic(uniq):
+    """Creating another hbm: store on the device while a thread keeps per-call traffic flowing
+    through the first store's resident ring worker finishes promptly: store set-up waits only for
+    its own stream, never for the device (the worker exits only after SPLINTER_RING_IDLE_US idle)."""
+    import threading
+    from libsplinter_amd import Store
+    a = Store.create(f"hbm:{uniq}a", slots=1024, max_val=64, embeddings=False)
+    stop = threading.Event()
+    calls = [0]
+
+    def traffic():
+        while not stop.is_set():
+            a.set("hot", b"x" * 16)
+            assert a.get("hot") == b"x" * 16
+            calls[0] += 1
+
+    t = threading.Thread(target=traffic)
+    t.start()
+    try:
+        time.sleep(0.2)
+        t0 = time.perf_counter()
+        b = Store.create(f"hbm:{uniq}b", slots=1024, max_val=64, embeddings=False)
+        b.set("k", b"v")
+        assert b.get("k") == b"v"
+        dt = time.perf_counter() - t0
+        b.close()
+    finally:
+        stop.set()
+        t.join(30)
+        a.close()
+    assert calls[0] > 100
+    assert dt < 5.0, f"second store took {dt:.2f}s beside live traffic"

@@ -40,13 +40,14 @@ def test_state_machine_cpu(uniq):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kv_heads,heads", [(8, 8), (2, 8), (2, 4)])
-def test_decoder_hip_matches_cpu(kv_heads, heads):
+@pytest.mark.parametrize("kv_heads,heads,d", [(8, 8, 512), (2, 8, 512), (2, 4, 512), (1, 2, 512), (8, 8, 768)])
+def test_decoder_hip_matches_cpu(kv_heads, heads, d):
     """GPU forward (prefill, a continuation prefill over the live cache, then one decode step)
-    against the fp32 CPU model; heads 4 gives head dim 128 (dec_attn_prefill_kv<128>)."""
+    against the fp32 CPU model; heads 4 gives head dim 128 (dec_attn_prefill_kv<128>); head dim
+    256 runs prefill on SDPA and decode on dec_attn_decode, head dim 96 both on SDPA."""
     import torch
     from libsplinter_amd.models.decoder import CausalLM, DecoderConfig
-    cfg = DecoderConfig(layers=2, kv_heads=kv_heads, heads=heads)
+    cfg = DecoderConfig(layers=2, kv_heads=kv_heads, heads=heads, d=d)
     gpu = CausalLM.random(cfg, seed=3, device="cuda")
     cpu = CausalLM.random(cfg, seed=3, device="cpu")
     ids = [256] + list(b"the quick brown fox")

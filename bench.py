@@ -11,8 +11,11 @@ hash-shard of the key space in its own HBM arena (format v4, 128-B slots,
     batch and a get batch on two concurrent HIP streams, so readers race
     writers on the seqlocks (the reference's MRSW/MRMW regime,
     /root/reference/splinter_stress.c, splinter_chi_sao.c).  With N>1 every
-    batch is routed to the owning shards with RCCL all-to-all and the results
-    are routed back (collective C1) inside the timed region.
+    batch is routed to the owning shards and the results are routed back
+    (collective C1) inside the timed region: one request and one
+    response exchange per step (parallel/xroute.py), own-shard ops in place,
+    remote records stored straight into the owners' peer-mapped HBM windows
+    over xGMI (--transport peer; rccl = one all-to-all per direction).
   * embed phase (--mode mixed/embed): one batch of synthetic documents through
     the random-init Nomic-BERT encoder on the gfx950 kernels, mean-pooled
     vectors written into their slots of the rank's search arena (--search-keys
@@ -22,8 +25,8 @@ hash-shard of the key space in its own HBM arena (format v4, 128-B slots,
     seqlocked slot write, in the same step as the KV phase).
 
 The client streams are the same at every N: at N=1 the set / get batches fan out over
---writer-streams / --reader-streams HIP streams; at N>1 the owner fans the routed segments
-it received out over the same streams (spl_kvs_step_seg).  Outside the timed region:
+--writer-streams / --reader-streams HIP streams; at N>1 the owner fans its own ops and the
+request blocks it received out over the same streams (spl_kvs_step_xr).  Outside the timed region:
 the routed step at N=1 (routed_kv_ops_per_s), end-to-end embedding, the embedding daemon's
 own code path per rank (daemon_vectors_per_s), the per-call C API, and config #5's query phase (batched top-k over the search arenas, broadcast + all-gather
 merge at N>1, recall against the exact kernel).
@@ -69,6 +72,10 @@ def parse():
     p.add_argument("--force-routed", action="store_true",
                    help="run the N>1 routed step (pack -> all-to-all -> owner kernels -> all-to-all -> gather) "
                         "even at N=1, to measure the routing overhead on one GPU")
+    p.add_argument("--transport", default="peer", choices=["peer", "rccl"],
+                   help="N>1 routed exchange: peer = request / response rows stored straight into the owners' "
+                        "peer-mapped windows (xGMI), falling back to rccl if any mapping fails; rccl = one "
+                        "all-to-all per direction")
     p.add_argument("--backend", default="nccl", help="nccl (= RCCL, one GPU per rank) or gloo (rehearsal: "
                    "ranks may share a GPU, collectives staged through the host)")
     p.add_argument("--writer-streams", type=int, default=32,
@@ -265,13 +272,6 @@ def main():
     if not (os.environ.get("BENCH_SKIP_MOP") and args.mop == 1):  # diagnosis: stores are created hybrid
         arena.store.set_mop(args.mop)  # 1 = hybrid scrub, the reference's store default
     kv = ShardedKV(GpuShard(arena))
-    rkv = None
-    if need_routed:
-        # request and response all-to-alls on their own communicators (= their own RCCL streams):
-        # step i's responses and step i+1's requests are in flight together
-        from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
-        rkv = RoutedKV(GpuShard(arena), group=dist.new_group(backend=args.backend),
-                       resp_group=dist.new_group(backend=args.backend))
     vstride = (args.max_val + 15) // 16 * 16
 
     # ---- prepopulate: every rank inserts the global ids it owns ----------
@@ -445,28 +445,36 @@ def main():
         if args.throttle and embedder is not None:
             throttle_ev[0] = cur.record_event()
 
-    # N > 1: a host-sync-free software pipeline (parallel/routed.py).  Per step i:
-    #   s_req : pack + request all-to-alls of batch i         (overlaps embed_i)
-    #   main  : embed_i, after the owner kernels of batch i-1  (no seqlock kernels beside the GEMMs)
-    #   s_set / s_get : owner kernels of batch i, after its requests and embed_i
-    #   s_resp: response all-to-alls + gather of batch i       (overlaps embed_{i+1})
+    # N > 1: a host-sync-free software pipeline over the routed exchange (parallel/xroute.py).
+    # Per step i (parity i % 2 double-buffers every exchange block and client output):
+    #   s_req : pack of batch i straight into the owners' request blocks + the count all-to-all
+    #           (waits for finish(i-2): no block is reused while anyone still reads it)
+    #   main  : embed_i, after the owner kernels of batch i-1 (no seqlock kernels beside the GEMMs)
+    #   s_set : owner kernels of batch i on the 32 + 32 client streams (own ops in place, peers'
+    #           request blocks -> their response blocks), after its requests and embed_i
+    #   s_resp: the response collective + gather of batch i     (overlaps embed_{i+1})
     # All K steps' responses are delivered inside the timed region (device-wide sync at the end).
-    if need_routed:
-        cap_s, cap_g = route_capacity(max(n_set, 1), world), route_capacity(max(n_get, 1), world)
+    xr = None
+    if need_routed and n_set + n_get and kvs is not None:
+        from libsplinter_amd.parallel.xroute import XRoute
         vw = min((args.value_len + 15) // 16 * 16, vstride)
+        xr = XRoute(GpuShard(arena), n_set, n_get, vw, ks=16, group=dist.new_group(backend=args.backend),
+                    resp_group=dist.new_group(backend=args.backend), transport=args.transport)
+        log(f"[bench] routed exchange: transport {xr.transport}, world {world}, caps {xr.cap_s}/{xr.cap_g}, "
+            f"window {xr.g.window_b / 2**30:.2f} GiB")
         s_req, s_resp = hip_stream("low"), hip_stream("low")
-        gouts = [torch.empty((n_get, vw), dtype=torch.uint8, device="cuda") for _ in range(2)]
+        r_out = [(torch.empty(max(n_set, 1), dtype=torch.int32, device="cuda"),
+                  torch.empty((max(n_get, 1), vw), dtype=torch.uint8, device="cuda"),
+                  torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda"),
+                  torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")) for _ in range(2)]
         prev_exec = []
 
     def step_routed(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
         cur = torch.cuda.current_stream()
-        so = go = None
+        sst, gov, gln, gst = r_out[i % 2]
         with torch.cuda.stream(s_req):
-            if n_set:
-                so = rkv.begin_set(SK, SV, SL, cap_s, vw)
-            if n_get:
-                go = rkv.begin_get(GK, cap_g, vw)
+            xr.request(i, SK if n_set else None, SV if n_set else None, SL if n_set else None, GK if n_get else None)
             ev_req = s_req.record_event()
         if embedder is not None:
             for e in prev_exec:
@@ -474,34 +482,19 @@ def main():
             embedder.run()
         ev_emb = cur.record_event()
         prev_exec.clear()
-        if kvs is not None:
-            # owner kernels on the same writer / reader client streams as a local step: the received
-            # segments fan out natively from one origin stream (spl_kvs_step_seg)
-            s_set.wait_event(ev_req)
-            s_set.wait_event(ev_emb)
-            with torch.cuda.stream(s_set):
-                rkv.execute_fanout(so, go, kvs)
-                prev_exec.append(s_set.record_event())
-        else:
-            for s, op in ((s_set, so), (s_get, go)):
-                if op is None:
-                    continue
-                s.wait_event(ev_req)
-                s.wait_event(ev_emb)
-                with torch.cuda.stream(s):
-                    rkv.execute(op)
-                    prev_exec.append(s.record_event())
-        for e in prev_exec:
-            s_resp.wait_event(e)
+        s_set.wait_event(ev_req)
+        s_set.wait_event(ev_emb)
+        with torch.cuda.stream(s_set):
+            xr.execute(i, kvs, sst, gov, gln, gst)
+            prev_exec.append(s_set.record_event())
+        s_resp.wait_event(prev_exec[-1])
         with torch.cuda.stream(s_resp):
-            for op in (so, go):
-                if op is not None:
-                    rkv.respond(op)
-            if so is not None:
-                rkv.finish(so)
-            if go is not None:
-                rkv.finish(go, out=gouts[i % 2])
+            xr.respond(i)
+            xr.finish(i, sst, gov, gln, gst)
 
+    if routed and xr is None:
+        raise SystemExit("[bench] the routed step needs the native client-stream fan-out and a KV batch "
+                         "(not --kv-cus / --overlap / BENCH_PY_STREAMS, not --mode embed)")
     step = step_routed if routed else step_local
 
     for i in range(args.warmup):
@@ -570,7 +563,7 @@ def main():
 
     # ---- N=1: the routed (N>1) step on one GPU, same streams and batches (outside the headline) ----
     routed1 = None
-    if not routed and rkv is not None and args.routed_steps > 0:
+    if not routed and xr is not None and args.routed_steps > 0:
         for i in range(2):
             step_routed(i)
         torch.cuda.synchronize()
@@ -690,14 +683,19 @@ def main():
             "mode": args.mode, "phases": "overlapped" if s_kvo is not None else "serial", "mop": args.mop, "value_len": args.value_len,
             "writer_streams": nw, "reader_streams": nr,
             "hw_queues_per_priority": int(os.environ["GPU_MAX_HW_QUEUES"]),
-            "collectives": ("RCCL on torch's per-process-group streams (request / response groups), "
-                            "sharing the normal-priority queue pool with the writers") if routed else None,
+            "collectives": (f"routed exchange, transport {xr.transport}: request / response rows "
+                            + ("stored into the owners' peer-mapped windows over xGMI, "
+                               if xr.transport == "peer" else "moved by one all-to-all per direction, ")
+                            + "one count all-to-all + one response all-to-all per step") if routed and xr else None,
             "search_keys_per_gpu": args.search_keys if sarena is not None else 0,
-            # bytes each GPU sends to its W-1 peers per routed step (16-B key records; every all-to-all moves W x cap
-            # rows per kind, (W-1)/W of them off-GPU): set requests key + len + value prefix, set
-            # status back, get requests key, get responses status + len + value prefix
-            "xgmi_bytes_per_step_per_gpu": ((world - 1) * (cap_s * (16 + 4 + vw + 4) + cap_g * (16 + 4 + 4 + vw))
-                                            if routed else 0),
+            # bytes each GPU stores into its W-1 peers per routed step (own-shard ops never leave the GPU):
+            # set request key + len + value prefix and its status back, get request key and its status +
+            # len + value prefix back; spread over W-1 point-to-point links (one per peer), and the
+            # per-link time at the ~153 GB/s per-link figure of the task statement
+            "xgmi_bytes_per_step_per_gpu": (xr.g.wire_bytes(n_set * (world - 1) / world, n_get * (world - 1) / world)
+                                            if routed and xr else 0),
+            "xgmi_link_ms_per_step": (xr.g.wire_bytes(n_set * (world - 1) / world, n_get * (world - 1) / world)
+                                      / (world - 1) / 153e9 * 1e3 if routed and xr and world > 1 else 0),
         },
         "kv_ops_per_s": kv_ops_s,
         "embed_vectors_per_s": emb_vps,
@@ -732,6 +730,8 @@ def main():
     if liveness is not None:
         dist.barrier()
         liveness.stop()
+    if xr is not None:
+        xr.close()
     if sarena is not None:
         sarena.close()
     arena.close()

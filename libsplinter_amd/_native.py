@@ -98,6 +98,25 @@ class Arena(ctypes.Structure):
                 ("notify", c_u64)]
 
 
+XR_MAX_WORLD = 64
+
+
+class XrStep(ctypes.Structure):
+    """spl_xr_step_t (csrc/include/arena_api.h): one routed step's owner side."""
+    _fields_ = [("world", ctypes.c_int), ("rank", ctypes.c_int), ("cap_s", ctypes.c_long), ("cap_g", ctypes.c_long),
+                ("ks", ctypes.c_int), ("vw", ctypes.c_int),
+                ("skeys", ctypes.c_void_p), ("svals", ctypes.c_void_p), ("svstride", ctypes.c_int),
+                ("slens", ctypes.c_void_p), ("sstatus", ctypes.c_void_p), ("n_set", ctypes.c_long),
+                ("gkeys", ctypes.c_void_p), ("gout", ctypes.c_void_p), ("gostride", ctypes.c_int),
+                ("glens", ctypes.c_void_p), ("gstatus", ctypes.c_void_p), ("n_get", ctypes.c_long),
+                ("lidx_set", ctypes.c_void_p), ("lidx_get", ctypes.c_void_p), ("own_counts", ctypes.c_void_p),
+                ("rcounts", ctypes.c_void_p),
+                ("req", ctypes.c_uint64 * XR_MAX_WORLD), ("resp", ctypes.c_uint64 * XR_MAX_WORLD),
+                ("off_sk", ctypes.c_long), ("off_sl", ctypes.c_long), ("off_sv", ctypes.c_long),
+                ("off_gk", ctypes.c_long), ("off_ss", ctypes.c_long), ("off_gs", ctypes.c_long),
+                ("off_gl", ctypes.c_long), ("off_gv", ctypes.c_long)]
+
+
 ENUM_CB = ctypes.CFUNCTYPE(None, c_char_p, c_u64, c_void_p)
 assert ctypes.sizeof(HeaderSnapshot) == 48
 assert ctypes.sizeof(SlotSnapshot) == 3192
@@ -189,8 +208,18 @@ def _declare_hip(L):
     _sig(L, "spl_arena_get", c_int, A, P, c_int, P, c_int, P, c_long, P, c_int, P, P)
     _sig(L, "spl_arena_set_seg", c_int, A, P, c_int, P, c_int, P, c_long, P, c_int, P, P, c_long, P)
     _sig(L, "spl_arena_get_seg", c_int, A, P, c_int, P, c_int, P, c_long, P, c_int, P, P, c_long, P)
-    _sig(L, "spl_route_pack", c_int, P, c_int, P, c_int, c_int, P, c_long, c_int, c_long, P, P, P, P, P, P)
-    _sig(L, "spl_route_gather", c_int, P, c_long, P, P, P, c_int, P, P, P, c_int, P)
+    _sig(L, "spl_arena_set_idx", c_int, A, P, c_int, P, c_int, P, P, P, c_long, P, c_int, P, P)
+    _sig(L, "spl_arena_get_idx", c_int, A, P, c_int, P, c_int, P, P, P, c_long, P, c_int, P, P)
+    # routed exchange (route_kernels.hip, parallel/xroute.py)
+    _sig(L, "spl_xr_pack", c_int, P, c_int, P, c_int, P, c_long, c_int, c_int, c_long, P, c_long, c_long, c_long,
+         c_int, P, P, P, P)
+    _sig(L, "spl_xr_gather", c_int, P, c_long, c_long, P, c_long, c_long, c_long, c_int, P, P, P, c_int, P)
+    _sig(L, "spl_xw_create", P, c_int, c_size_t, c_char_p)
+    _sig(L, "spl_xw_attach", P, c_char_p, c_int)
+    _sig(L, "spl_xw_base", P, P)
+    _sig(L, "spl_xw_bytes", c_size_t, P)
+    _sig(L, "spl_xw_destroy", None, P)
+    _sig(L, "spl_xw_peer", c_int, c_int, c_int)
     _sig(L, "spl_arena_unset", c_int, A, P, c_int, c_long, P, c_int, P)
     _sig(L, "spl_arena_intop", c_int, A, P, c_int, P, P, c_long, P, P, c_int, P)
     _sig(L, "spl_arena_meta", c_int, A, P, c_int, c_int, P, c_long, P, P, P)
@@ -201,8 +230,7 @@ def _declare_hip(L):
     _sig(L, "spl_kvs_create", P, c_int, c_int)
     _sig(L, "spl_kvs_destroy", None, P)
     _sig(L, "spl_kvs_step", c_int, P, A, P, P, c_int, P, c_int, P, c_long, P, P, P, c_int, P, c_long, P, c_int, P)
-    _sig(L, "spl_kvs_step_seg", c_int, P, A, P, P, c_int, P, c_int, P, c_long, P, P, c_long, P, P, c_int, P, c_long,
-         P, P, c_long, c_int, P)
+    _sig(L, "spl_kvs_step_xr", c_int, P, A, P, ctypes.POINTER(XrStep), c_int, P)
     if hasattr(L, "spl_hbm_ring_launches"):
         _sig(L, "spl_hbm_ring_launches", c_u32, c_void_p)
     _sig(L, "spl_arena_purge", c_int, A, P)

@@ -27,52 +27,25 @@ constexpr int kMaxGrid = 256 * 8;
 // Segmented batch (routed C1 buffers, parallel/sharded.py): the batch is `n / cap` segments of
 // `cap` rows, one per source rank, of which only the first counts[seg] rows are live.  Dead rows
 // are skipped (status EINVAL, not counted in the stats).  counts == nullptr: every row is live.
+// idx != nullptr (in-place rows, the own-shard ops of a routed step, parallel/xroute.py): row i is
+// client op idx[i], and every array the launch takes (keys, values, lens, status, outputs) is a
+// client-order array indexed by that op; dead rows are skipped without any write.
 struct Seg {
   const int32_t* counts;
   long cap;
   long base = 0;  // row of this launch's element 0 in the segmented buffer (a stream's slice of it)
+  const int32_t* idx = nullptr;
   __device__ __forceinline__ bool live(long i) const {
     if (!counts) return true;
     const long j = i + base, s = j / cap;
     return j - s * cap < (long)counts[s];
   }
+  __device__ __forceinline__ long row(long i) const { return idx ? (long)idx[i] : i; }
 };
 
-// Payload ordering discipline (arena_dev.hpp, MO): SPLINTER_ARENA_MO=0|1|2.
-inline int arena_mo() {
-  static int mo = [] {
-    const char* e = getenv("SPLINTER_ARENA_MO");
-    return e ? atoi(e) : 0;
-  }();
-  return mo;
-}
-
-// Ops per lane per round for set/get (SPLINTER_ARENA_U = 1|2|4|8; 1 = the
-// single-op kernels, which also honour SPLINTER_ARENA_MO).
 inline int env_int(const char* name, int dflt) {
   const char* e = getenv(name);
   return e ? atoi(e) : dflt;
-}
-// sets: 2 ops per lane since round 3 (twice the workgroups per client-stream dispatch; the 32+32-stream step is
-// bound by how many dispatches the hardware queues keep resident): KV-only 3.06 -> 3.67 G ops/s, mixed step
-// 14.6 -> 14.1 ms (profiles/r3_kv_u2.md)
-inline int arena_rounds() {
-  static int u = env_int("SPLINTER_ARENA_U", 2);
-  return u;
-}
-// gets run best at 2 ops per lane (more lanes in flight; profiles/r1_kv_rounds.jsonl)
-inline int arena_rounds_get() {
-  static int u = env_int("SPLINTER_ARENA_UGET", env_int("SPLINTER_ARENA_U", 2));
-  return u;
-}
-// threads per workgroup of the rounds kernels = lanes sharing one release / acquire
-inline int arena_block() {
-  static int b = env_int("SPLINTER_ARENA_BLOCK", 256);
-  return b == 512 ? 512 : 256;
-}
-inline int arena_block_get() {
-  static int b = env_int("SPLINTER_ARENA_BLOCK_GET", env_int("SPLINTER_ARENA_BLOCK", 256));
-  return b == 512 ? 512 : 256;
 }
 
 inline int grid_for(long n) {
@@ -146,230 +119,6 @@ __global__ void k_init_slots(spl_arena_t aa) {
   }
 }
 
-// ------------------------------------------------------------- set ------
-template <int MO>
-__global__ __launch_bounds__(kBlock) void k_set(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
-                                                int vstride, const uint32_t* lens, long n, int32_t* status,
-                                                int max_retry, uint64_t* stats, Seg seg) {
-  const Arena a = to_dev(aa);
-  Stats st;
-  uint64_t muts = 0;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    if (!seg.live(i)) {
-      if (status) status[i] = kInval;
-      continue;
-    }
-    Key k;
-    load_key(k, keys + i * (long)kstride, kstride);
-    const uint32_t len = lens[i];
-    int32_t rc = len > (uint32_t)vstride ? kMsgSize : kAgain;  // a length past the source row: no over-read
-    long idx = -1;
-    for (int t = 0; t <= max_retry && rc == kAgain; ++t) {
-      ++st.attempts;
-      rc = set_op<MO>(a, k, vals + i * (long)vstride, len, &idx);
-      if (rc != kAgain) break;
-      ++st.again;
-      backoff(t);
-    }
-    if (rc == kOk) {
-      ++st.ok;
-      ++muts;
-      pulse(a, a.slot((size_t)idx));
-      mark_dirty(a, (size_t)idx);
-    }
-    if (status) status[i] = rc;
-  }
-  flush_stats(a, st, stats, muts);
-}
-
-// ------------------------------------------------------------- get ------
-template <int MO>
-__global__ __launch_bounds__(kBlock) void k_get(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
-                                                int ostride, uint32_t* out_lens, long n, int32_t* status,
-                                                int max_retry, uint64_t* stats, Seg seg) {
-  const Arena a = to_dev(aa);
-  Stats st;
-  for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
-    if (!seg.live(i)) {
-      if (out_lens) out_lens[i] = 0;
-      if (status) status[i] = kInval;
-      continue;
-    }
-    Key k;
-    load_key(k, keys + i * (long)kstride, kstride);
-    uint32_t len = 0;
-    int32_t rc = kAgain;
-    for (int t = 0; t <= max_retry; ++t) {
-      ++st.attempts;
-      rc = get_op<MO>(a, k, out ? out + i * (long)ostride : nullptr, (uint32_t)ostride, &len);
-      if (rc != kAgain) break;
-      ++st.again;
-      backoff(t);
-    }
-    if (rc == kOk) ++st.ok;
-    else if (rc == kNoEnt) ++st.miss;
-    if (out_lens) out_lens[i] = rc == kOk ? len : 0;
-    if (status) status[i] = rc;
-  }
-  flush_stats(a, st, stats, 0);
-}
-
-// ---------------------------------------------------- batched rounds -----
-// U ops per lane per round: U claims (or lookups) in flight, then ONE agent
-// release (writers) / acquire (readers) per wave for all of them.  EAGAIN ops
-// fall back to the single-op path with backoff.
-template <int U, int B, bool WT = false, int KW = 16, int OCC = 1>
-__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_set_rounds(spl_arena_t aa, const char* keys, int kstride,
-                                                       const uint8_t* vals, int vstride, const uint32_t* lens, long n,
-                                                       int32_t* status, int max_retry, uint64_t* stats, Seg seg) {
-  const Arena a = to_dev(aa);
-  bool hybrid;
-  const bool scrub = scrub_flags(a, hybrid);
-  Stats st;
-  uint64_t muts = 0;
-  // block-uniform round loop (every thread runs every round: the round ends in barriers)
-  const long per_block = (long)blockDim.x * U;
-  for (long base = blockIdx.x * per_block; base < n; base += (long)gridDim.x * per_block) {
-    const long r0 = base + (long)threadIdx.x * U;
-    KeyT<KW> k[U];
-    Claim c[U];
-    uint32_t len[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const long i = r0 + j;
-      c[j] = Claim{-1, false, kInval};
-      if (i < n && seg.live(i)) {
-        load_key(k[j], keys + i * (long)kstride, kstride);
-        len[j] = lens[i];
-        ++st.attempts;
-        if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride) c[j].rc = kMsgSize;
-        else c[j] = claim_set(a, k[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (c[j].rc == kOk) write_set<WT ? 3 : 0>(a, c[j], vals + (r0 + j) * (long)vstride, len[j], scrub, hybrid);
-    if constexpr (WT) {
-      // write-through payload: each wave's own drain publishes its sc1 stores (no L2 write-back,
-      // no workgroup barrier: every lane publishes only its own slots)
-      drain();
-    } else {
-      // ONE agent release per WORKGROUP: every wave's payload stores have reached the (shared) XCD
-      // L2 once its vmcnt drains; the barrier then lets one lane write that L2 back (buffer_wbl2)
-      // for all of them before any wave publishes an epoch.  The release is serialised per XCD
-      // (~1.7 us), so this is 4x fewer serialised write-backs than one per wave.
-      drain();
-      __syncthreads();
-      if (threadIdx.x == 0) release();
-      __syncthreads();
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const long i = r0 + j;
-      if (i >= n) continue;
-      int32_t rc = c[j].rc;
-      long idx = c[j].idx;
-      if (rc == kOk) finish_set(a, c[j]);
-      for (int t = 0; rc == kAgain && t < max_retry; ++t) {
-        ++st.again;
-        backoff(t);
-        ++st.attempts;
-        rc = set_op<0>(a, k[j], vals + i * (long)vstride, len[j], &idx);
-      }
-      if (rc == kAgain) ++st.again;
-      if (rc == kOk) {
-        ++st.ok;
-        ++muts;
-        pulse(a, a.slot((size_t)idx));
-        mark_dirty(a, (size_t)idx);
-      }
-      if (status) status[i] = rc;
-    }
-  }
-  flush_stats(a, st, stats, muts);
-}
-
-template <int U, int B, int GV = 1, int KW = 16>
-__global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
-                                                       int ostride, uint32_t* out_lens, long n, int32_t* status,
-                                                       int max_retry, uint64_t* stats, Seg seg) {
-  const Arena a = to_dev(aa);
-  Stats st;
-  const long per_block = (long)blockDim.x * U;
-  for (long base = blockIdx.x * per_block; base < n; base += (long)gridDim.x * per_block) {
-    const long r0 = base + (long)threadIdx.x * U;
-    KeyT<KW> k[U];
-    long sidx[U];
-    uint64_t e1[U];
-    int32_t rc[U];
-    uint32_t len[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const long i = r0 + j;
-      rc[j] = kInval;
-      sidx[j] = -1;
-      len[j] = 0;
-      if (i < n && seg.live(i)) {
-        load_key(k[j], keys + i * (long)kstride, kstride);
-        ++st.attempts;
-        sidx[j] = locate_peek(a, k[j], &e1[j], &len[j]);  // hash/epoch/len/key: one round trip per probe
-        rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
-      }
-    }
-    // ONE agent acquire per workgroup: all lanes' epoch loads have completed (drain) before the
-    // barrier; one lane then invalidates the CU/XCD caches the whole workgroup reads through.
-    drain();
-    __syncthreads();
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (rc[j] != kOk) continue;
-      const uint8_t* s = a.slot((size_t)sidx[j]);
-      if ((e1[j] & 1) || len[j] > a.max_val) { rc[j] = kAgain; continue; }
-      // key words again, in the same round trip as the payload: the pre-acquire compare was
-      // speculative (validated below together with the unchanged epoch)
-      const bool keq = key_eq(s, k[j]);
-      if (out) {
-        if (len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
-        const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
-        uint4* dst = (uint4*)(out + (r0 + j) * (long)ostride);
-        const uint32_t n16 = (len[j] + 15) >> 4;
-        if (GV == 2) copy_chunks(dst, src, n16, (a.max_val + 15) >> 4);
-        else for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
-      }
-      if (!keq) rc[j] = kAgain;
-    }
-    drain();
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (rc[j] != kOk) continue;
-      const uint8_t* s = a.slot((size_t)sidx[j]);
-      const uint64_t e2 = slot_epoch(s), h2 = slot_hash(s);  // one round trip
-      if (e2 != e1[j] || h2 != k[j].hash) rc[j] = kAgain;
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const long i = r0 + j;
-      if (i >= n) continue;
-      int32_t r = rc[j];
-      uint32_t L = len[j];
-      for (int t = 0; r == kAgain && t < max_retry; ++t) {
-        ++st.again;
-        backoff(t);
-        ++st.attempts;
-        r = get_op<0>(a, k[j], out ? out + i * (long)ostride : nullptr, (uint32_t)ostride, &L);
-      }
-      if (r == kAgain) ++st.again;
-      if (r == kOk) ++st.ok;
-      else if (r == kNoEnt) ++st.miss;
-      if (out_lens) out_lens[i] = r == kOk ? L : 0;
-      if (status) status[i] = r;
-    }
-  }
-  flush_stats(a, st, stats, 0);
-}
-
 // ------------------------------------------------ cooperative row copy ---
 // A wave's round copies up to U*64 value rows (150-B values = 10 x 16 B).  Copied lane-by-op,
 // every 16-B wave instruction touches 64 different rows (64 lines); copied here cooperatively,
@@ -381,70 +130,6 @@ __global__ __launch_bounds__(B) void k_get_rounds(spl_arena_t aa, const char* ke
 // stored bytewise so it cannot spill into the next row); 0xFFFFFFFF: no limit.
 // MO: store flavour of the destination rows (st16<MO>); LD1: source rows read with 16-B `sc1` loads
 // (L1-bypassing, so a reader needs no L1-invalidating acquire before them).
-// Rows of at most 256 B (one 16-lane group each), software-pipelined: the loads of the next 16
-// rows are in flight while the current 16 are stored, so a wave's 16 steps cost about half the
-// serial load round trips.  Loads are unconditional (an empty entry or a chunk past the value reads
-// `dummy`, any mapped 16 B), so each step issues exactly kUnr loads and the LD1 path can wait for
-// the current step with vmcnt(kUnr).
-template <int NE, int MO = 0, bool LD1 = false>
-__device__ __forceinline__ void coop_copy_pipe(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
-                                               uint32_t rowb, const void* dummy) {
-  const int q = lane >> 4;
-  const uint32_t c = (uint32_t)(lane & 15);
-  constexpr int kUnr = 4, kSteps = NE / (4 * kUnr);
-  static_assert(NE % (4 * kUnr) == 0, "whole steps");
-  uint4 P[2][kUnr];
-  uint2 L[2][kUnr];
-  u32x4c_t d[2][kUnr];
-  auto fetch = [&](int st, int b) {
-#pragma unroll
-    for (int u = 0; u < kUnr; ++u) {
-      P[b][u] = ep[st * 4 * kUnr + 4 * u + q];
-      L[b][u] = el[st * 4 * kUnr + 4 * u + q];
-    }
-#pragma unroll
-    for (int u = 0; u < kUnr; ++u) {
-      const uint32_t n16 = (L[b][u].x + 15) >> 4;
-      const uint4* src = c < n16 ? (const uint4*)(((uint64_t)P[b][u].y << 32) | P[b][u].x) + c : (const uint4*)dummy;
-      if constexpr (LD1) {
-        d[b][u] = ld16c(src);
-      } else {
-        const uint4 t = *src;
-        d[b][u] = u32x4c_t{t.x, t.y, t.z, t.w};
-      }
-    }
-  };
-  auto put = [&](int b) {
-#pragma unroll
-    for (int u = 0; u < kUnr; ++u) {
-      if (c >= L[b][u].y) continue;
-      const uint32_t n16 = (L[b][u].x + 15) >> 4;
-      uint4 v = c < n16 ? make_uint4(d[b][u].x, d[b][u].y, d[b][u].z, d[b][u].w) : make_uint4(0, 0, 0, 0);
-      if (c == n16 - 1 && (L[b][u].x & 15)) {
-        const int r = (int)(L[b][u].x & 15);
-        v.x &= keep_mask(r); v.y &= keep_mask(r - 4); v.z &= keep_mask(r - 8); v.w &= keep_mask(r - 12);
-      }
-      uint4* dst = (uint4*)(((uint64_t)P[b][u].w << 32) | P[b][u].z);
-      if (c * 16 + 16 > rowb) store_partial((uint8_t*)(dst + c), v, rowb - c * 16);
-      else st16<MO>(dst + c, v);
-    }
-  };
-  fetch(0, 0);
-#pragma unroll
-  for (int st = 0; st < kSteps; ++st) {
-    const int b = st & 1;
-    if (st + 1 < kSteps) fetch(st + 1, b ^ 1);
-    if constexpr (LD1) {
-      static_assert(kUnr == 4, "the waits below tie four registers");
-      if (st + 1 < kSteps)
-        asm volatile("s_waitcnt vmcnt(4)" : "+v"(d[b][0]), "+v"(d[b][1]), "+v"(d[b][2]), "+v"(d[b][3])::"memory");
-      else
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(d[b][0]), "+v"(d[b][1]), "+v"(d[b][2]), "+v"(d[b][3])::"memory");
-    }
-    put(b);
-  }
-}
-
 template <int NE, int MO = 0, bool LD1 = false>
 __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
                                           int groups, uint32_t rowb) {
@@ -501,28 +186,22 @@ __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const ui
 }
 
 // ------------------------------------------------ carried-retry rounds -----
-// Same rounds as above, but an op that meets a contended slot (EAGAIN) is NOT retried inline:
-// it stays in its lane's slot and is retried in the lane's next round, while the lane's other
-// slots take new ops.  Retries thus ride the batched rounds (one release / acquire per
-// workgroup round) instead of stalling the whole wave in a backoff + single-op path with its
-// own L2 write-back, and a round of other work is the natural backoff.  Attempts per op are
-// bounded by 1 + max_retry as before; the round loop is block-uniform (barriers).
-// Lane sequence: op c of a lane is first + (c / U) * stride + c % U (monotone in c), i.e. the
-// grid-stride order of the rounds kernels.
-// WT (with COOP): the value rows and slot metadata go out as write-through `sc1` 16-B stores (one
-// 64-B fabric write per 4 lanes of a row) and each wave publishes its own ops after its vmcnt(0)
-// drain -- recipe R1 of cdna_hip_programming.md Guideline 16, as MO 3 -- so a round needs neither
-// the workgroup barrier pair nor the XCD-serialised L2 write-back (buffer_wbl2) of the release.
-// BC: the round's claims through claim_many (all ops' probes, then all CASes, in flight together).
-// PIPE: value rows through coop_copy_pipe (rows of at most 256 B).
-// FS: publish with finish_set_store (an 8-B store) instead of the epoch increment atomic.
-template <int U, int B, int KW = 16, bool COOP = false, bool WT = false, bool BC = false, bool PIPE = false,
-          bool FS = false>
-__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1))) void k_set_carry(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
+// The batched set / get kernels (K2 / K3 of SURVEY §2.10).  U ops per lane per round: U claims
+// (or lookups) in flight, then the round's value rows move through the cooperative copy.  An op
+// that meets a contended slot (EAGAIN) is NOT retried inline: it stays in its lane's slot and is
+// retried in the lane's next round while the lane's other slots take new ops, so a round of other
+// work is the natural backoff.  Attempts per op are bounded by 1 + max_retry; the round loop is
+// block-uniform (barriers).  Lane sequence: op c of a lane is first + (c / U) * stride + c % U.
+// WT: the value rows and slot metadata go out as write-through `sc1` 16-B stores and each wave
+// publishes its own ops after its vmcnt(0) drain -- recipe R1 of cdna_hip_programming.md
+// Guideline 16 -- so a round needs neither the workgroup barrier pair nor the XCD-serialised L2
+// write-back of a release (default; SPLINTER_ARENA_COOP=1: plain rows + one release per round).
+template <int U, int B, bool WT>
+__global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* keys, int kstride, const uint8_t* vals,
                                                  int vstride, const uint32_t* lens, long n, int32_t* status,
                                                  int max_retry, uint64_t* stats, Seg seg) {
-  __shared__ uint4 cp_p[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
-  __shared__ uint2 cp_l[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
+  __shared__ uint4 cp_p[B / 64][U * 64];
+  __shared__ uint2 cp_l[B / 64][U * 64];
   const Arena a = to_dev(aa);
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
@@ -532,7 +211,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1)))
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
   long cursor = 0;
   bool more = true;
-  KeyT<KW> k[U];
+  Key k[U];
   Claim c[U];
   uint32_t len[U];
   long op[U];
@@ -546,33 +225,21 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1)))
         const long i = first + (cursor / U) * stride + (cursor % U);
         ++cursor;
         if (i >= n) { more = false; break; }
-        if (!seg.live(i)) { if (status) status[i] = kInval; continue; }
-        op[j] = i;
+        if (!seg.live(i)) {
+          if (status && !seg.idx) status[i] = kInval;
+          continue;
+        }
+        const long r = seg.row(i);
+        op[j] = r;
         tries[j] = 0;
-        load_key(k[j], keys + i * (long)kstride, kstride);
-        len[j] = lens[i];
+        load_key(k[j], keys + r * (long)kstride, kstride);
+        len[j] = lens[r];
       }
     }
     bool busy = false;
 #pragma unroll
     for (int j = 0; j < U; ++j) busy |= op[j] >= 0;
     if (!__syncthreads_or(busy)) break;
-    if constexpr (BC) {
-      bool act[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        act[j] = false;
-        if (op[j] >= 0) {
-          ++st.attempts;
-          ++tries[j];
-          act[j] = !(len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride);
-        }
-      }
-      claim_many<U, KW>(a, k, act, c);
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (op[j] >= 0 && !act[j]) c[j].rc = kMsgSize;
-    } else {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       c[j] = Claim{-1, false, kInval};
@@ -583,31 +250,23 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1)))
         else c[j] = claim_set(a, k[j]);
       }
     }
+    // value rows through the cooperative copy (wave-private table), metadata per lane
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const bool go = op[j] >= 0 && c[j].rc == kOk;
+      const uint64_t sp = go ? (uint64_t)(vals + op[j] * (long)vstride) : 0;
+      const uint64_t dp = go ? (uint64_t)a.value((size_t)c[j].idx) : 0;
+      cp_p[w][j * 64 + lane] = make_uint4((uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)dp, (uint32_t)(dp >> 32));
+      cp_l[w][j * 64 + lane] = make_uint2(go ? len[j] : 0u, go ? set_chunks(a, len[j], scrub, hybrid) : 0u);
     }
-    if constexpr (COOP) {
-      // value rows through the cooperative copy (wave-private table), metadata per lane
-      const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    __builtin_amdgcn_wave_barrier();
+    coop_copy<U * 64, WT ? 3 : 0>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), a.max_val);
 #pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const bool go = op[j] >= 0 && c[j].rc == kOk;
-        const uint64_t sp = go ? (uint64_t)(vals + op[j] * (long)vstride) : 0;
-        const uint64_t dp = go ? (uint64_t)a.value((size_t)c[j].idx) : 0;
-        cp_p[w][j * 64 + lane] = make_uint4((uint32_t)sp, (uint32_t)(sp >> 32), (uint32_t)dp, (uint32_t)(dp >> 32));
-        cp_l[w][j * 64 + lane] = make_uint2(go ? len[j] : 0u, go ? set_chunks(a, len[j], scrub, hybrid) : 0u);
-      }
-      __builtin_amdgcn_wave_barrier();
-      if (PIPE && a.max_val <= 256) coop_copy_pipe<U * 64, WT ? 3 : 0>(cp_p[w], cp_l[w], lane, a.max_val, a.base);
-      else coop_copy<U * 64, WT ? 3 : 0>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), a.max_val);
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (op[j] >= 0 && c[j].rc == kOk) write_meta<WT ? 3 : 0>(a, c[j], len[j]);
-    } else {
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (op[j] >= 0 && c[j].rc == kOk) write_set<0>(a, c[j], vals + op[j] * (long)vstride, len[j], scrub, hybrid);
-    }
+    for (int j = 0; j < U; ++j)
+      if (op[j] >= 0 && c[j].rc == kOk) write_meta<WT ? 3 : 0>(a, c[j], len[j]);
     drain();
-    if constexpr (!(WT && COOP)) {
+    if constexpr (!WT) {
       __syncthreads();
       if (threadIdx.x == 0) release();
       __syncthreads();
@@ -621,8 +280,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1)))
         if (tries[j] <= max_retry) continue;  // carried into the next round
       }
       if (rc == kOk) {
-        if constexpr (FS) finish_set_store(a, c[j]);
-        else finish_set(a, c[j]);
+        finish_set(a, c[j]);
         ++st.ok;
         ++muts;
         pulse_masks(a, c[j].wm, c[j].bl);
@@ -635,7 +293,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1)))
   flush_stats(a, st, stats, muts);
 }
 
-// FAST (with COOP): no workgroup acquire.  Every load of slot words and value bytes is an `sc1` load,
+// FAST: no workgroup acquire.  Every load of slot words and value bytes is an `sc1` load,
 // which bypasses the (possibly stale) L1 and is served by the XCD's L2.  That is enough because every
 // writer of these bytes (k_set_carry WT, the ring's set) stores them write-through (`sc1`) and drains
 // vmcnt before publishing, so no dirty copy lingers in the writer XCD's L2, and an `sc1` load on another
@@ -643,23 +301,22 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(BC ? 2 : 1)))
 // (measured, not an architectural guarantee; pinned by tests/test_arena_gpu.py
 // test_acquire_free_get_cross_xcd_hot_keys; SPLINTER_ARENA_COOP_GET=1 is the acquire fallback).
 // Ops that store with plain (write-back) stores must release before a reader may rely on this (see
-// the ring's serve()).  The key is re-checked in the same round trip as the
-// closing (hash, epoch) load instead of a separate one before the copy: a key change between the
-// probe and the value loads moves the epoch or, for an unset that rewinds it, clears the hash.
-// PIPE: value rows through coop_copy_pipe (1; 2 = the same held to 3 waves per SIMD).
-template <int U, int B, int KW = 16, bool COOP = false, bool FAST = false, int PIPE = 0>
-__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(PIPE == 2 ? 3 : 1))) void k_get_carry(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
+// the ring's serve()).  The key is re-checked in the same round trip as the closing (hash, epoch)
+// load instead of a separate one before the copy: a key change between the probe and the value
+// loads moves the epoch or, for an unset that rewinds it, clears the hash.
+template <int U, int B, bool FAST>
+__global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* keys, int kstride, uint8_t* out,
                                                  int ostride, uint32_t* out_lens, long n, int32_t* status,
                                                  int max_retry, uint64_t* stats, Seg seg) {
-  __shared__ uint4 cp_p[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
-  __shared__ uint2 cp_l[COOP ? B / 64 : 1][COOP ? U * 64 : 1];
+  __shared__ uint4 cp_p[B / 64][U * 64];
+  __shared__ uint2 cp_l[B / 64][U * 64];
   const Arena a = to_dev(aa);
   Stats st;
   const long stride = (long)gridDim.x * blockDim.x * U;
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
   long cursor = 0;
   bool more = true;
-  KeyT<KW> k[U];
+  Key k[U];
   long op[U], sidx[U];
   uint64_t e1[U];
   int32_t rc[U];
@@ -675,13 +332,16 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(PIPE == 2 ? 3
         ++cursor;
         if (i >= n) { more = false; break; }
         if (!seg.live(i)) {
-          if (out_lens) out_lens[i] = 0;
-          if (status) status[i] = kInval;
+          if (!seg.idx) {
+            if (out_lens) out_lens[i] = 0;
+            if (status) status[i] = kInval;
+          }
           continue;
         }
-        op[j] = i;
+        const long r = seg.row(i);
+        op[j] = r;
         tries[j] = 0;
-        load_key(k[j], keys + i * (long)kstride, kstride);
+        load_key(k[j], keys + r * (long)kstride, kstride);
       }
     }
     bool busy = false;
@@ -699,7 +359,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(PIPE == 2 ? 3
         rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
       }
     }
-    if constexpr (FAST && COOP) {
+    if constexpr (FAST) {
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         if (op[j] < 0 || rc[j] != kOk) continue;
@@ -707,32 +367,23 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(PIPE == 2 ? 3
         else if (out && len[j] > (uint32_t)ostride) rc[j] = kMsgSize;
       }
     } else {
-    drain();
-    __syncthreads();
-    if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    __syncthreads();
+      drain();
+      __syncthreads();
+      if (threadIdx.x == 0) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __syncthreads();
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (op[j] < 0 || rc[j] != kOk) continue;
-      const uint8_t* s = a.slot((size_t)sidx[j]);
-      if ((e1[j] & 1) || len[j] > a.max_val) { rc[j] = kAgain; continue; }
-      KeyProbe<KW> kp;
-      kp.issue(s, k[j]);
-      kp.wait();
-      const bool keq = kp.eq(k[j]);
-      if (out) {
-        if (len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
-        if constexpr (!COOP) {
-          const uint4* src = (const uint4*)a.value((size_t)sidx[j]);
-          uint4* dst = (uint4*)(out + op[j] * (long)ostride);
-          const uint32_t n16 = (len[j] + 15) >> 4;
-          for (uint32_t q = 0; q < n16; ++q) dst[q] = src[q];
-        }
+      for (int j = 0; j < U; ++j) {
+        if (op[j] < 0 || rc[j] != kOk) continue;
+        const uint8_t* s = a.slot((size_t)sidx[j]);
+        if ((e1[j] & 1) || len[j] > a.max_val) { rc[j] = kAgain; continue; }
+        KeyProbe<16> kp;
+        kp.issue(s, k[j]);
+        kp.wait();
+        if (out && len[j] > (uint32_t)ostride) { rc[j] = kMsgSize; continue; }
+        if (!kp.eq(k[j])) rc[j] = kAgain;
       }
-      if (!keq) rc[j] = kAgain;
     }
-    }
-    if constexpr (COOP) {
+    {
       // value rows of this round's matched ops through the cooperative copy (see coop_copy)
       const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
 #pragma unroll
@@ -745,14 +396,13 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(PIPE == 2 ? 3
         cp_l[w][j * 64 + lane] = make_uint2(go ? n16 * 16 : 0u, go ? n16 : 0u);
       }
       __builtin_amdgcn_wave_barrier();
-      if (PIPE && a.max_val <= 256) coop_copy_pipe<U * 64, 0, FAST>(cp_p[w], cp_l[w], lane, 0xFFFFFFFFu, a.base);
-      else coop_copy<U * 64, 0, FAST>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
+      coop_copy<U * 64, 0, FAST>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
     }
     drain();
-    if constexpr (FAST && COOP) {
+    if constexpr (FAST) {
       // closing round trip: (hash, epoch) and the key words of every op of the lane together
       u32x4c_t he[U];
-      KeyProbe<KW> kp[U];
+      KeyProbe<16> kp[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         const bool live = op[j] >= 0 && rc[j] == kOk;
@@ -771,12 +421,12 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(PIPE == 2 ? 3
           rc[j] = kAgain;
     } else {
 #pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (op[j] < 0 || rc[j] != kOk) continue;
-      u32x4c_t he = ld16c(a.slot((size_t)sidx[j]) + kOffHash);  // hash + epoch: one request
-      vm_wait(he);
-      if (hi64(he) != e1[j] || lo64(he) != k[j].hash) rc[j] = kAgain;
-    }
+      for (int j = 0; j < U; ++j) {
+        if (op[j] < 0 || rc[j] != kOk) continue;
+        u32x4c_t he = ld16c(a.slot((size_t)sidx[j]) + kOffHash);  // hash + epoch: one request
+        vm_wait(he);
+        if (hi64(he) != e1[j] || lo64(he) != k[j].hash) rc[j] = kAgain;
+      }
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -1080,212 +730,97 @@ int spl_arena_init_slots(spl_arena_t a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
-                  long n, int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
-  return spl_arena_set_seg(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, nullptr, 0, s);
+}  // extern "C"
+
+namespace {
+
+// Batched set / get launches (every public entry point and the stream fan-outs go through these).
+// Two forms each, chosen once per process: SPLINTER_ARENA_COOP (sets) / SPLINTER_ARENA_COOP_GET
+// (gets) = 2 (default: write-through rows, acquire-free sc1 reads) or 1 (plain rows + one release
+// per round / one agent acquire per round).  The measured-and-rejected forms (single-op, non-carried
+// rounds, 512-thread blocks, U = 1/4/8, batched claims, pipelined copies) are gone; their A/B
+// history is in profiles/r1_* .. r3_*.
+constexpr int kU = 2, kB = 256;
+
+int launch_set(const spl_arena_t& a, const char* keys, int kstride, const uint8_t* vals, int vstride,
+               const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats, const Seg& seg,
+               hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
+  if (seg.counts && seg.cap <= 0) return (int)hipErrorInvalidValue;
+  static const int coop = env_int("SPLINTER_ARENA_COOP", 2);
+  const dim3 g(grid_for_b((n + kU - 1) / kU, kB));
+  if (coop == 1)
+    hipLaunchKernelGGL((k_set_carry<kU, kB, false>), g, dim3(kB), 0, s, a, keys, kstride, vals, vstride, lens, n,
+                       status, max_retry, stats, seg);
+  else
+    hipLaunchKernelGGL((k_set_carry<kU, kB, true>), g, dim3(kB), 0, s, a, keys, kstride, vals, vstride, lens, n,
+                       status, max_retry, stats, seg);
+  return (int)hipGetLastError();
 }
 
-static int set_seg_at(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
-                      const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats,
-                      const int32_t* seg_counts, long seg_cap, long seg_base, hipStream_t s);
+int launch_get(const spl_arena_t& a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
+               long n, int32_t* status, int max_retry, uint64_t* stats, const Seg& seg, hipStream_t s) {
+  if (n <= 0) return 0;
+  if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
+  if (seg.counts && seg.cap <= 0) return (int)hipErrorInvalidValue;
+  static const int coop = env_int("SPLINTER_ARENA_COOP_GET", 2);
+  const dim3 g(grid_for_b((n + kU - 1) / kU, kB));
+  if (coop == 1)
+    hipLaunchKernelGGL((k_get_carry<kU, kB, false>), g, dim3(kB), 0, s, a, keys, kstride, out, ostride, out_lens, n,
+                       status, max_retry, stats, seg);
+  else
+    hipLaunchKernelGGL((k_get_carry<kU, kB, true>), g, dim3(kB), 0, s, a, keys, kstride, out, ostride, out_lens, n,
+                       status, max_retry, stats, seg);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+extern "C" {
+
+int spl_arena_set(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
+                  long n, int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
+  return launch_set(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, Seg{nullptr, 1}, s);
+}
 
 int spl_arena_set_seg(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
                       const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats,
                       const int32_t* seg_counts, long seg_cap, hipStream_t s) {
   if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
-  return set_seg_at(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg_counts, seg_cap, 0, s);
-}
-
-static int set_seg_at(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
-                      const uint32_t* lens, long n, int32_t* status, int max_retry, uint64_t* stats,
-                      const int32_t* seg_counts, long seg_cap, long seg_base, hipStream_t s) {
-  if (n <= 0) return 0;
-  if ((kstride & 15) || kstride > 64 || (vstride & 15)) return (int)hipErrorInvalidValue;
-  if (seg_counts && seg_cap <= 0) return (int)hipErrorInvalidValue;
-  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1, seg_base};
-  const int mo = arena_mo();
-  const int u = arena_rounds(), b = arena_block();
-  static const int wt = env_int("SPLINTER_ARENA_WT", 0);  // write-through: measured slower (profiles/r1_kv_writethrough.md)
-#define SPL_SET_ROUNDS(U_, B_)                                                                                   \
-  hipLaunchKernelGGL((k_set_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
-                     kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
-  // SPLINTER_ARENA_KW4=1: 16-B key records with 4 key words per op in registers instead of 16
-  // (153 -> 128 VGPRs, 2 -> 4 waves/SIMD).  Measured SLOWER at 100M keys (2.22 -> 1.96 G ops/s,
-  // twice the EAGAIN retries): more ops in flight do not help these kernels
-  // (profiles/r1_kv_occupancy.md), so it is off by default.
-  static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);
-  static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);  // carried retries (k_set_carry)
-  // cooperative value-row copy: 2 = write-through rows, no per-round release (default: KV-only 2.73 -> 3.15 G
-  // ops/s, mixed step 15.5 -> 14.7 ms, profiles/r3_kv_set_writethrough.md); 1 = plain rows + release; 0 = per lane
-  static const int coop = env_int("SPLINTER_ARENA_COOP", 2);
-  if (carry && !wt && (u == 2 || u == 4 || (u == 1 && coop == 2 && b == 256))) {
-#define SPL_SET_CARRY(U_, B_)                                                                                   \
-  hipLaunchKernelGGL((k_set_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
-                     kstride, vals, vstride, lens, n, status, max_retry, stats, seg)
-    static const int bclaim = env_int("SPLINTER_ARENA_BATCH_CLAIM", 0);
-    static const int pipe = env_int("SPLINTER_ARENA_PIPE", 0);
-    static const int fstore = env_int("SPLINTER_ARENA_FINISH_STORE", 0);
-    if (fstore && u == 4 && b == 256 && coop == 2)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true, false, false, true>), dim3(grid_for_b((n + 3) / 4, 256)),
-                         dim3(256), 0, s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (pipe && u == 4 && b == 256 && coop == 2)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true, false, true>), dim3(grid_for_b((n + 3) / 4, 256)),
-                         dim3(256), 0, s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (bclaim && kw4 && kstride == 16 && u == 4 && b == 256 && coop == 2)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 4, true, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0,
-                         s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (bclaim && u == 4 && b == 256 && coop == 2)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256),
-                         0, s, a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (kw4 && kstride == 16 && u == 4 && b == 256 && coop == 2)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 4, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s,
-                         a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (kw4 && kstride == 16 && u == 4 && b == 256)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
-                         kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (u == 2 && b == 256 && coop == 2)
-      hipLaunchKernelGGL((k_set_carry<2, 256, 16, true, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s,
-                         a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (u == 1)  // (coop 2, 256 threads: the condition above) one op per lane, carried retries
-      hipLaunchKernelGGL((k_set_carry<1, 256, 16, true, true>), dim3(grid_for_b(n, 256)), dim3(256), 0, s, a, keys,
-                         kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (u == 4 && b == 256 && coop == 2)  // write-through rows, no release (see k_set_carry)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s,
-                         a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (u == 4 && b == 256 && coop)
-      hipLaunchKernelGGL((k_set_carry<4, 256, 16, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
-                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (u == 4 && b == 256) SPL_SET_CARRY(4, 256);
-    else if (u == 4) SPL_SET_CARRY(4, 512);
-    else if (b == 256) SPL_SET_CARRY(2, 256);
-    else SPL_SET_CARRY(2, 512);
-#undef SPL_SET_CARRY
-  } else if (kw4 && kstride == 16 && !wt && b == 256 && (u == 4 || u == 8)) {
-    static const int occ = env_int("SPLINTER_ARENA_SETOCC", 4);
-    if (u == 4 && occ == 4)
-      hipLaunchKernelGGL((k_set_rounds<4, 256, false, 4, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
-                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else if (u == 4)
-      hipLaunchKernelGGL((k_set_rounds<4, 256, false, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a,
-                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-    else
-      hipLaunchKernelGGL((k_set_rounds<8, 256, false, 4>), dim3(grid_for_b((n + 7) / 8, 256)), dim3(256), 0, s, a,
-                         keys, kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-  } else if (wt && u == 4 && b == 256)
-    hipLaunchKernelGGL((k_set_rounds<4, 256, true>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
-                       kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-  else if (wt && u == 2 && b == 256)
-    hipLaunchKernelGGL((k_set_rounds<2, 256, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
-                       kstride, vals, vstride, lens, n, status, max_retry, stats, seg);
-  else if (u == 2 && b == 256) SPL_SET_ROUNDS(2, 256);
-  else if (u == 2) SPL_SET_ROUNDS(2, 512);
-  else if (u == 4 && b == 256) SPL_SET_ROUNDS(4, 256);
-  else if (u == 4) SPL_SET_ROUNDS(4, 512);
-  else if (u == 8) SPL_SET_ROUNDS(8, 256);
-#undef SPL_SET_ROUNDS
-  else if (mo == 1)
-    hipLaunchKernelGGL(k_set<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
-                       status, max_retry, stats, seg);
-  else if (mo == 2)
-    hipLaunchKernelGGL(k_set<2>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
-                       status, max_retry, stats, seg);
-  else
-    hipLaunchKernelGGL(k_set<0>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, vals, vstride, lens, n,
-                       status, max_retry, stats, seg);
-  return (int)hipGetLastError();
+  return launch_set(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats,
+                    Seg{seg_counts, seg_cap > 0 ? seg_cap : 1}, s);
 }
 
 int spl_arena_get(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
                   int32_t* status, int max_retry, uint64_t* stats, hipStream_t s) {
-  return spl_arena_get_seg(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, nullptr, 0, s);
+  return launch_get(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, Seg{nullptr, 1}, s);
 }
-
-static int get_seg_at(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
-                      long n, int32_t* status, int max_retry, uint64_t* stats, const int32_t* seg_counts,
-                      long seg_cap, long seg_base, hipStream_t s);
 
 int spl_arena_get_seg(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
                       long n, int32_t* status, int max_retry, uint64_t* stats, const int32_t* seg_counts,
                       long seg_cap, hipStream_t s) {
   if (seg_counts && (seg_cap <= 0 || n % seg_cap)) return (int)hipErrorInvalidValue;
-  return get_seg_at(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg_counts, seg_cap, 0, s);
+  return launch_get(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats,
+                    Seg{seg_counts, seg_cap > 0 ? seg_cap : 1}, s);
 }
 
-static int get_seg_at(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
-                      long n, int32_t* status, int max_retry, uint64_t* stats, const int32_t* seg_counts,
-                      long seg_cap, long seg_base, hipStream_t s) {
-  if (n <= 0) return 0;
-  if ((kstride & 15) || kstride > 64 || (ostride & 15)) return (int)hipErrorInvalidValue;
-  if (seg_counts && seg_cap <= 0) return (int)hipErrorInvalidValue;
-  const Seg seg{seg_counts, seg_cap > 0 ? seg_cap : 1, seg_base};
-  const int mo = arena_mo();
-  const int u = arena_rounds_get(), b = arena_block_get();
-#define SPL_GET_ROUNDS(U_, B_)                                                                                   \
-  hipLaunchKernelGGL((k_get_rounds<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
-                     kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
-  static const int gv = env_int("SPLINTER_ARENA_GETCOPY", 1);
-  static const bool kw4 = env_int("SPLINTER_ARENA_KW4", 0);  // see spl_arena_set_seg
-  static const int carry = env_int("SPLINTER_ARENA_CARRY", 1);
-  // 2 = no acquire, sc1 row loads, key re-check with the closing epoch load; 1 = acquire + plain loads
-  // default 2 since round 3: +3 % KV-only, -0.1 ms mixed (profiles/r3_kv_u2.md)
-  static const int coop = env_int("SPLINTER_ARENA_COOP_GET", 2);
-  if (carry && gv == 1 && u == 1 && coop == 2 && b == 256) {
-    hipLaunchKernelGGL((k_get_carry<1, 256, 16, true, true>), dim3(grid_for_b(n, 256)), dim3(256), 0, s, a, keys,
-                       kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-  } else if (carry && gv == 1 && (u == 2 || u == 4)) {
-#define SPL_GET_CARRY(U_, B_)                                                                                   \
-  hipLaunchKernelGGL((k_get_carry<U_, B_>), dim3(grid_for_b((n + U_ - 1) / U_, B_)), dim3(B_), 0, s, a, keys, \
-                     kstride, out, ostride, out_lens, n, status, max_retry, stats, seg)
-    static const int pipe = env_int("SPLINTER_ARENA_PIPE", 0);
-    if (pipe == 2 && coop == 2 && u == 2 && b == 256)
-      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true, true, 2>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256),
-                         0, s, a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else if (pipe && coop == 2 && u == 2 && b == 256)
-      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true, true, 1>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256),
-                         0, s, a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else if (coop == 2 && u == 2 && b == 256 && kw4 && kstride == 16)
-      hipLaunchKernelGGL((k_get_carry<2, 256, 4, true, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s,
-                         a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else if (coop == 2 && u == 2 && b == 256)  // no acquire, sc1 row loads (see k_get_carry)
-      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s,
-                         a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else if (coop && u == 2 && b == 256)
-      hipLaunchKernelGGL((k_get_carry<2, 256, 16, true>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a,
-                         keys, kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else if (kw4 && kstride == 16 && u == 2 && b == 256)
-      hipLaunchKernelGGL((k_get_carry<2, 256, 4>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
-                         kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else if (u == 2 && b == 256) SPL_GET_CARRY(2, 256);
-    else if (u == 2) SPL_GET_CARRY(2, 512);
-    else if (b == 256) SPL_GET_CARRY(4, 256);
-    else SPL_GET_CARRY(4, 512);
-#undef SPL_GET_CARRY
-  } else if (kw4 && kstride == 16 && gv == 1 && b == 256 && (u == 2 || u == 4)) {
-    if (u == 2)
-      hipLaunchKernelGGL((k_get_rounds<2, 256, 1, 4>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
-                         kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-    else
-      hipLaunchKernelGGL((k_get_rounds<4, 256, 1, 4>), dim3(grid_for_b((n + 3) / 4, 256)), dim3(256), 0, s, a, keys,
-                         kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-  } else if (u == 2 && b == 256 && gv == 2)
-    hipLaunchKernelGGL((k_get_rounds<2, 256, 2>), dim3(grid_for_b((n + 1) / 2, 256)), dim3(256), 0, s, a, keys,
-                       kstride, out, ostride, out_lens, n, status, max_retry, stats, seg);
-  else if (u == 2 && b == 256) SPL_GET_ROUNDS(2, 256);
-  else if (u == 2) SPL_GET_ROUNDS(2, 512);
-  else if (u == 4 && b == 256) SPL_GET_ROUNDS(4, 256);
-  else if (u == 4) SPL_GET_ROUNDS(4, 512);
-  else if (u == 8) SPL_GET_ROUNDS(8, 256);
-#undef SPL_GET_ROUNDS
-  else if (mo == 1)
-    hipLaunchKernelGGL(k_get<1>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
-                       status, max_retry, stats, seg);
-  else if (mo == 2)
-    hipLaunchKernelGGL(k_get<2>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
-                       status, max_retry, stats, seg);
-  else
-    hipLaunchKernelGGL(k_get<0>, dim3(grid_for(n)), dim3(kBlock), 0, s, a, keys, kstride, out, ostride, out_lens, n,
-                       status, max_retry, stats, seg);
-  return (int)hipGetLastError();
+// In-place rows (idx: client op indices; live rows: the first *count of them): the own-shard ops of
+// a routed step run on the client's own arrays (parallel/xroute.py).
+int spl_arena_set_idx(spl_arena_t a, const char* keys, int kstride, const uint8_t* vals, int vstride,
+                      const uint32_t* lens, const int32_t* idx, const int32_t* count, long n, int32_t* status,
+                      int max_retry, uint64_t* stats, hipStream_t s) {
+  if (!idx || !count) return (int)hipErrorInvalidValue;
+  return launch_set(a, keys, kstride, vals, vstride, lens, n, status, max_retry, stats, Seg{count, n > 0 ? n : 1, 0, idx},
+                    s);
+}
+
+int spl_arena_get_idx(spl_arena_t a, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
+                      const int32_t* idx, const int32_t* count, long n, int32_t* status, int max_retry,
+                      uint64_t* stats, hipStream_t s) {
+  if (!idx || !count) return (int)hipErrorInvalidValue;
+  return launch_get(a, keys, kstride, out, ostride, out_lens, n, status, max_retry, stats,
+                    Seg{count, n > 0 ? n : 1, 0, idx}, s);
 }
 
 int spl_arena_unset(spl_arena_t a, const char* keys, int kstride, long n, int32_t* status, int max_retry,
@@ -1494,40 +1029,77 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
   return (int)hipGetLastError();
 }
 
-// spl_kvs_step over routed (segmented) buffers: the owner side of a routed step (parallel/routed.py)
-// fans the received set / get segments out over the same writer / reader streams as a local step,
-// each stream a contiguous row range of the segment buffer (dead rows skipped by Seg.base).
-int spl_kvs_step_seg(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, int kstride, const uint8_t* svals,
-                     int vstride, const uint32_t* slens, long n_set, int32_t* sstatus, const int32_t* scounts,
-                     long scap, const char* gkeys, uint8_t* gout, int ostride, uint32_t* glens, long n_get,
-                     int32_t* gstatus, const int32_t* gcounts, long gcap, int max_retry, uint64_t* stats) {
+// The owner side of a routed step (parallel/xroute.py, route_kernels.hip) on the same writer /
+// reader streams as a local step.  The set rows are the concatenation of one segment per source
+// rank -- the own segment (the client's own ops, in place through lidx, or the whole client batch
+// when lidx is null: world 1) and every peer's request block -- and each writer stream takes an
+// equal slice of that row space, one launch per segment it touches; gets likewise on the readers.
+// A peer segment's results go straight to x->resp[s]: the requester's response block (peer
+// transport: that rank's window, mapped here; RCCL transport: this rank's send staging block).
+int spl_kvs_step_xr(void* h, spl_arena_t a, hipStream_t origin, const spl_xr_step_t* x, int max_retry,
+                    uint64_t* stats) {
   auto* k = (KvStreams*)h;
-  if (!k || (n_set > 0 && (!scounts || scap <= 0 || n_set % scap)) || (n_get > 0 && (!gcounts || gcap <= 0 || n_get % gcap)))
+  if (!k || !x || x->world < 1 || x->world > SPL_XR_MAX_WORLD || x->rank < 0 || x->rank >= x->world ||
+      (x->world > 1 && (!x->lidx_set || !x->lidx_get || !x->own_counts || !x->rcounts)))
     return (int)hipErrorInvalidValue;
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
-  const int nw = n_set > 0 ? k->nw : 0, nr = n_get > 0 ? k->nr : 0;
-  for (int w = 0; w < nw; ++w) {
-    const long b = n_set * w / nw, end = n_set * (w + 1) / nw;
-    if (end <= b) continue;
-    hipStream_t st = k->s[w];
-    (void)hipStreamWaitEvent(st, k->start, 0);
-    int rc = set_seg_at(a, skeys + b * (long)kstride, kstride, svals + b * (long)vstride, vstride, slens + b, end - b,
-                        sstatus + b, max_retry, stats, scounts, scap, b, st);
-    if (rc) return rc;
-    (void)hipEventRecord(k->done[w], st);
-    (void)hipStreamWaitEvent(origin, k->done[w], 0);
-  }
-  for (int r = 0; r < nr; ++r) {
-    const long b = n_get * r / nr, end = n_get * (r + 1) / nr;
-    if (end <= b) continue;
-    hipStream_t st = k->s[k->nw + r];
-    (void)hipStreamWaitEvent(st, k->start, 0);
-    int rc = get_seg_at(a, gkeys + b * (long)kstride, kstride, gout + b * (long)ostride, ostride, glens + b, end - b,
-                        gstatus + b, max_retry, stats, gcounts, gcap, b, st);
-    if (rc) return rc;
-    (void)hipEventRecord(k->done[k->nw + r], st);
-    (void)hipStreamWaitEvent(origin, k->done[k->nw + r], 0);
+  const int W = x->world, r = x->rank;
+  for (int kind = 0; kind < 2; ++kind) {
+    const bool set = kind == 0;
+    const long n_own = set ? x->n_set : x->n_get;
+    const long cap = set ? x->cap_s : x->cap_g;
+    const bool ident = (set ? x->lidx_set : x->lidx_get) == nullptr;
+    if (n_own <= 0 && W == 1) continue;
+    // segment lengths: own = n (identity) or cap (lidx rows, the first own_counts[kind] live)
+    long len[SPL_XR_MAX_WORLD], start[SPL_XR_MAX_WORLD + 1];
+    start[0] = 0;
+    for (int sg = 0; sg < W; ++sg) {
+      len[sg] = sg == r ? (ident ? n_own : cap) : cap;
+      start[sg + 1] = start[sg] + len[sg];
+    }
+    const long total = start[W];
+    if (total <= 0) continue;
+    const int ns = set ? k->nw : k->nr;
+    for (int w = 0; w < ns; ++w) {
+      const long lo = total * w / ns, hi = total * (w + 1) / ns;
+      if (hi <= lo) continue;
+      hipStream_t st = k->s[set ? w : k->nw + w];
+      (void)hipStreamWaitEvent(st, k->start, 0);
+      for (int sg = 0; sg < W; ++sg) {
+        const long b0 = lo > start[sg] ? lo - start[sg] : 0;
+        const long b1 = (hi < start[sg + 1] ? hi : start[sg + 1]) - start[sg];
+        if (b1 <= b0) continue;
+        const long m = b1 - b0;
+        int rc;
+        if (sg == r && ident) {  // world 1: the client batch itself, row for row
+          rc = set ? launch_set(a, x->skeys + b0 * (long)x->ks, x->ks, x->svals + b0 * (long)x->svstride,
+                                x->svstride, x->slens + b0, m, x->sstatus + b0, max_retry, stats, Seg{nullptr, 1}, st)
+                   : launch_get(a, x->gkeys + b0 * (long)x->ks, x->ks, x->gout + b0 * (long)x->gostride, x->gostride,
+                                x->glens + b0, m, x->gstatus + b0, max_retry, stats, Seg{nullptr, 1}, st);
+        } else if (sg == r) {  // own ops in place: rows are lidx entries into the client arrays
+          const Seg seg{x->own_counts + r * 2 + kind, cap, b0, (set ? x->lidx_set : x->lidx_get) + b0};
+          rc = set ? launch_set(a, x->skeys, x->ks, x->svals, x->svstride, x->slens, m, x->sstatus, max_retry, stats,
+                                seg, st)
+                   : launch_get(a, x->gkeys, x->ks, x->gout, x->gostride, x->glens, m, x->gstatus, max_retry, stats,
+                                seg, st);
+        } else {  // peer sg's request block -> its response block
+          const uint8_t* q = (const uint8_t*)x->req[sg];
+          uint8_t* p = (uint8_t*)x->resp[sg];
+          const Seg seg{x->rcounts + sg * 2 + kind, cap, b0};
+          rc = set ? launch_set(a, (const char*)(q + x->off_sk) + b0 * (long)x->ks, x->ks,
+                                q + x->off_sv + b0 * (long)x->vw, x->vw, (const uint32_t*)(q + x->off_sl) + b0, m,
+                                (int32_t*)(p + x->off_ss) + b0, max_retry, stats, seg, st)
+                   : launch_get(a, (const char*)(q + x->off_gk) + b0 * (long)x->ks, x->ks,
+                                p + x->off_gv + b0 * (long)x->vw, x->vw, (uint32_t*)(p + x->off_gl) + b0, m,
+                                (int32_t*)(p + x->off_gs) + b0, max_retry, stats, seg, st);
+        }
+        if (rc) return rc;
+      }
+      const int ev = set ? w : k->nw + w;
+      (void)hipEventRecord(k->done[ev], st);
+      (void)hipStreamWaitEvent(origin, k->done[ev], 0);
+    }
   }
   return (int)hipGetLastError();
 }

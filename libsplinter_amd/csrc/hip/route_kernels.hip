@@ -1,31 +1,32 @@
-// route_kernels.hip — device side of the C1 routing collective (SURVEY §2.10 C1,
-// parallel/sharded.py RoutedKV): pack a client batch into fixed-capacity
-// per-destination segments, and gather routed responses back into client order.
+// route_kernels.hip — device side of the routed exchange (SURVEY §2.10 C1, §2.13;
+// parallel/xroute.py): pack a client batch straight into the owners' request blocks, gather the
+// owners' responses back into client order, and the exchange windows those blocks live in.
 //
-// Why fixed capacity: an all-to-all with EQUAL splits needs no host-side count
-// exchange, so a routed set/get step has no host synchronisation at all and
-// the RCCL transfers overlap compute queued on other streams.  The receiver
-// learns the live rows of each segment from a device-side count all-to-all
-// and the owner kernels skip dead rows (Seg in arena_kernels.hip).  A
-// destination segment that overflows `cap` returns EAGAIN for the excess ops
-// (the reference's contention status, splinter.h:398-412): the caller retries.
+// One exchange per direction per step.  Every (requester r, owner o) pair has ONE request block
+// in o's window -- [set keys | set lens | set value prefixes | get keys], `cap` rows per kind --
+// and ONE response block in r's window -- [set status | get status | get lens | get values].
+// The pack kernel writes each remote op's record directly into its owner's block: on the peer
+// transport that block is the owner's own window mapped into this process (VMM dmabuf import,
+// xGMI stores from the pack kernel: no copy kernel and no collective moves the bytes); on the
+// RCCL transport it is this rank's send staging block for o, moved by ONE all-to-all.  Ops whose
+// owner is this rank never enter the exchange: the pack kernel only lists their client indices
+// (`lidx`) and the owner kernels run them in place on the client arrays (arena_kernels.hip Seg.idx).
+// The per-destination counts are the only thing a collective must carry (they double as the
+// step's cross-rank ordering point).
 //
-// Pack layout (rank r, destination d, row j < cap): row index d*cap + j of
-//   kout [world*cap, kstride]  key record
-//   lout [world*cap]           value length          (sets only)
-//   vout [world*cap, vwidth]   value prefix (16-B)   (sets only)
-// pos[i] = d*cap + j for client op i, or -1 when its segment was full.
+// Fixed capacity per block: an op whose block is full returns EAGAIN (the reference's retry
+// status, splinter.h:398-412); route_capacity() makes that < 1e-15 per block for hashed keys.
 //
-// Work split: 256-thread blocks, 4 items per thread per round (1024 ops), a
-// block-local LDS histogram gives each op its rank inside (block, dest), ONE
-// global atomic per destination per round reserves the block's range, and the
-// value rows are copied wave-cooperatively (64 lanes stream consecutive 16-B
-// chunks of consecutive rows: coalesced reads and writes).
+// pos[i] (int32): d * cap + j for a remote op in row j of owner d's block, kPosOwn for an own
+// op (its results are written in place), kPosFull for an op that found its block full.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <string>
+#include <vector>
 
 #include "arena_dev.hpp"
 #include "arena_api.h"
+#include "vmm_share.hpp"
 
 using namespace spl;
 using namespace spl::dev;
@@ -34,30 +35,23 @@ namespace {
 
 constexpr int kRB = 256;         // threads per block
 constexpr int kRU = 4;           // items per thread per round
-constexpr int kMaxWorld = 256;   // destinations supported by the LDS histogram
+constexpr int kMaxWorld = 64;    // destinations of the LDS histogram (== kNodeMaxShards)
+constexpr int32_t kPosOwn = -2, kPosFull = -1;
 
 __device__ __forceinline__ int shard_of_hash(uint64_t h, int world) {
   return (int)(((h >> 40) & 0xFFFFFFull) % (uint64_t)world);  // == parallel/sharded.py shard_of
 }
 
-// Copy `C` 16-B chunks of each of the wave's 64 rows: row r (lane r's item)
-// goes from src + r*sstride to dst + dpos(r)*dstride; rows with dpos < 0 or
-// beyond n are skipped.  Lanes walk the flattened (row, chunk) space.
-__device__ __forceinline__ void wave_copy_rows(const uint8_t* src_base, long sstride, uint8_t* dst, long dstride,
-                                               long my_dpos, int C, int lane, int nvalid) {
-  const int total = 64 * C;
-  for (int c = lane; c < total; c += 64) {
-    const int row = c / C, chunk = c - row * C;
-    const long dp = __shfl(my_dpos, row);
-    if (row < nvalid && dp >= 0)
-      *(uint4*)(dst + dp * dstride + chunk * 16) = *(const uint4*)(src_base + row * sstride + chunk * 16);
-  }
-}
+// One routed kind of a pack: where its rows go inside a destination block.
+struct XKind {
+  long off_k, off_l, off_v;  // byte offsets of keys / lens / value rows in a block (off_l, off_v: sets)
+  int vw;                    // value bytes per row (16-B multiple; 0: no values)
+};
 
-__global__ __launch_bounds__(kRB) void k_route_pack(const char* keys, int kstride, const uint8_t* vals, int vstride,
-                                                    int vwidth, const uint32_t* lens, long n, int world, long cap,
-                                                    int32_t* counts, int64_t* pos, char* kout, uint32_t* lout,
-                                                    uint8_t* vout) {
+__global__ __launch_bounds__(kRB) void k_xpack(const char* keys, int ks, const uint8_t* vals, int vstride,
+                                               const uint32_t* lens, long n, int world, int rank, long cap,
+                                               const uint64_t* blk, XKind kd, int32_t* counts, int32_t* lidx,
+                                               int32_t* pos) {
   __shared__ int s_cnt[kMaxWorld];
   __shared__ int s_base[kMaxWorld];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -72,7 +66,7 @@ __global__ __launch_bounds__(kRB) void k_route_pack(const char* keys, int kstrid
       const long i = base + (long)j * kRB + tid;
       dst[j] = -1;
       if (i < n) {
-        load_key(k[j], keys + i * (long)kstride, kstride);
+        load_key(k[j], keys + i * (long)ks, ks);
         dst[j] = shard_of_hash(k[j].hash, world);
         rk[j] = atomicAdd(&s_cnt[dst[j]], 1);
       }
@@ -87,55 +81,82 @@ __global__ __launch_bounds__(kRB) void k_route_pack(const char* keys, int kstrid
 #pragma unroll
     for (int j = 0; j < kRU; ++j) {
       const long i = base + (long)j * kRB + tid;
-      long p = -1;
+      long row = -1;  // row in the destination block (remote ops only)
+      uint8_t* b = nullptr;
       if (dst[j] >= 0) {
         const long slot = (long)s_base[dst[j]] + rk[j];
-        if (slot < cap) p = (long)dst[j] * cap + slot;
+        int32_t p = kPosFull;
+        if (slot < cap) {
+          if (dst[j] == rank) {
+            lidx[slot] = (int32_t)i;
+            p = kPosOwn;
+          } else {
+            p = (int32_t)(dst[j] * cap + slot);
+            row = slot;
+            b = (uint8_t*)blk[dst[j]];
+          }
+        }
         pos[i] = p;
       }
-      if (p >= 0) {
-        uint4* kr = (uint4*)(kout + p * (long)kstride);
+      if (row >= 0) {
+        uint4* kr = (uint4*)(b + kd.off_k + row * (long)ks);
 #pragma unroll
         for (int c = 0; c < 4; ++c)
-          if (c * 16 < kstride) kr[c] = make_uint4(k[j].w[4 * c], k[j].w[4 * c + 1], k[j].w[4 * c + 2], k[j].w[4 * c + 3]);
-        if (lout) lout[p] = lens[i];
+          if (c * 16 < ks) kr[c] = make_uint4(k[j].w[4 * c], k[j].w[4 * c + 1], k[j].w[4 * c + 2], k[j].w[4 * c + 3]);
+        if (kd.vw) *(uint32_t*)(b + kd.off_l + row * 4) = lens[i];
       }
-      if (vout) {
-        const long w0 = base + (long)j * kRB + wave * 64;  // first item of this wave's row group
+      if (kd.vw) {
+        // value prefixes, wave-cooperatively: the wave's 64 rows of this item index, lanes walk the
+        // flattened (row, 16-B chunk) space so reads and writes of consecutive lanes are contiguous
+        const long w0 = base + (long)j * kRB + wave * 64;
         const long left = n - w0;
-        if (left > 0)
-          wave_copy_rows(vals + w0 * (long)vstride, vstride, vout, vwidth, p, vwidth / 16, lane,
-                         left < 64 ? (int)left : 64);
+        const uint64_t my_dst = row >= 0 ? (uint64_t)(b + kd.off_v + row * (long)kd.vw) : 0ull;
+        if (left > 0) {
+          const int C = kd.vw / 16, nvalid = left < 64 ? (int)left : 64;
+          for (int c = lane; c < 64 * C; c += 64) {
+            const int r = c / C, ch = c - r * C;
+            const uint64_t dp = __shfl(my_dst, r);
+            if (r < nvalid && dp)
+              *(uint4*)(dp + ch * 16) = *(const uint4*)(vals + (w0 + r) * (long)vstride + ch * 16);
+          }
+        }
       }
     }
   }
 }
 
-__global__ __launch_bounds__(kRB) void k_route_gather(const int64_t* pos, long n, const int32_t* rstatus,
-                                                      const uint32_t* rlens, const uint8_t* rvals, int rstride,
-                                                      int32_t* status, uint32_t* out_lens, uint8_t* out, int ostride,
-                                                      int copy_bytes) {
+// Responses back into client order.  blk[d]: the response block owner d filled (in this rank's
+// window, or its receive area); off_s / off_l / off_v: status, lens, value rows inside it.
+__global__ __launch_bounds__(kRB) void k_xgather(const int32_t* pos, long n, long cap, const uint64_t* blk, long off_s,
+                                                 long off_l, long off_v, int vw, int32_t* status, uint32_t* out_lens,
+                                                 uint8_t* out, int ostride, int copy_bytes) {
   const int lane = threadIdx.x & 63;
   const long wstep = (long)gridDim.x * kRB;
   for (long w0 = blockIdx.x * (long)kRB + (threadIdx.x & ~63); w0 < n; w0 += wstep) {
     const long i = w0 + lane;
-    long p = -1;
+    uint64_t src = 0;
     if (i < n) {
-      p = pos[i];
-      if (status) status[i] = p < 0 ? kAgain : rstatus[p];
-      if (out_lens) out_lens[i] = p < 0 ? 0u : rlens[p];
+      const int32_t p = pos[i];
+      if (p == kPosFull) {
+        status[i] = kAgain;
+        if (out_lens) out_lens[i] = 0u;
+      } else if (p >= 0) {
+        const long d = p / cap, j = p - d * cap;
+        const uint8_t* b = (const uint8_t*)blk[d];
+        const int32_t st = *(const int32_t*)(b + off_s + j * 4);
+        status[i] = st;
+        if (out_lens) out_lens[i] = st == kOk ? *(const uint32_t*)(b + off_l + j * 4) : 0u;
+        if (out && st == kOk) src = (uint64_t)(b + off_v + j * (long)vw);
+      }
     }
     if (out) {
-      // source rows are read at rstride, written at ostride; client row i gets the routed row p
       const int C = copy_bytes / 16;
       const long left = n - w0;
       const int nvalid = left < 64 ? (int)left : 64;
       for (int c = lane; c < 64 * C; c += 64) {
-        const int row = c / C, chunk = c - row * C;
-        const long sp = __shfl(p, row);
-        if (row < nvalid && sp >= 0)
-          *(uint4*)(out + (w0 + row) * (long)ostride + chunk * 16) =
-              *(const uint4*)(rvals + sp * (long)rstride + chunk * 16);
+        const int r = c / C, ch = c - r * C;
+        const uint64_t sp = __shfl(src, r);
+        if (r < nvalid && sp) *(uint4*)(out + (w0 + r) * (long)ostride + ch * 16) = *(const uint4*)(sp + ch * 16);
       }
     }
   }
@@ -152,29 +173,87 @@ inline int route_grid(long n, long per_block) {
 
 extern "C" {
 
-int spl_route_pack(const char* keys, int kstride, const uint8_t* vals, int vstride, int vwidth, const uint32_t* lens,
-                   long n, int world, long cap, int32_t* counts, int64_t* pos, char* kout, uint32_t* lout,
-                   uint8_t* vout, hipStream_t s) {
-  if (world < 1 || world > kMaxWorld || cap < 0) return (int)hipErrorInvalidValue;
-  if ((kstride & 15) || kstride <= 0 || kstride > 64) return (int)hipErrorInvalidValue;
-  if (vout && (!vals || !lens || !lout || (vstride & 15) || (vwidth & 15) || vwidth <= 0 || vwidth > vstride))
+// Pack one batch kind (sets: vals/lens/vw given; gets: vals = lens = null, vw = 0).  counts[world]
+// is zeroed here and accumulates every destination's rows, the own destination included (its rows
+// are lidx entries).  blk: device table of `world` block base pointers (the own entry is unused).
+int spl_xr_pack(const char* keys, int ks, const uint8_t* vals, int vstride, const uint32_t* lens, long n, int world,
+                int rank, long cap, const uint64_t* blk, long off_k, long off_l, long off_v, int vw, int32_t* counts,
+                int32_t* lidx, int32_t* pos, hipStream_t s) {
+  if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || cap < 0) return (int)hipErrorInvalidValue;
+  if ((ks & 15) || ks <= 0 || ks > 64 || (off_k & 15)) return (int)hipErrorInvalidValue;
+  if (vw && (!vals || !lens || (vstride & 15) || (vw & 15) || vw > vstride || (off_v & 15) || (off_l & 3)))
     return (int)hipErrorInvalidValue;
+  if (cap * (long)world > INT32_MAX) return (int)hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)world, s);
   if (e != hipSuccess) return (int)e;
   if (n <= 0) return 0;
-  hipLaunchKernelGGL(k_route_pack, dim3(route_grid(n, (long)kRB * kRU)), dim3(kRB), 0, s, keys, kstride, vals,
-                     vstride, vwidth, lens, n, world, cap, counts, pos, kout, lout, vout);
+  const XKind kd{off_k, off_l, off_v, vw};
+  hipLaunchKernelGGL(k_xpack, dim3(route_grid(n, (long)kRB * kRU)), dim3(kRB), 0, s, keys, ks, vals, vstride, lens, n,
+                     world, rank, cap, blk, kd, counts, lidx, pos);
   return (int)hipGetLastError();
 }
 
-int spl_route_gather(const int64_t* pos, long n, const int32_t* rstatus, const uint32_t* rlens, const uint8_t* rvals,
-                     int rstride, int32_t* status, uint32_t* out_lens, uint8_t* out, int ostride, hipStream_t s) {
+// Gather one batch kind's responses (gets: out / out_lens given; sets: status only).
+int spl_xr_gather(const int32_t* pos, long n, long cap, const uint64_t* blk, long off_s, long off_l, long off_v, int vw,
+                  int32_t* status, uint32_t* out_lens, uint8_t* out, int ostride, hipStream_t s) {
   if (n <= 0) return 0;
-  const int copy = rstride < ostride ? rstride : ostride;
-  if (out && (!rvals || (rstride & 15) || (ostride & 15) || copy <= 0)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_route_gather, dim3(route_grid(n, kRB)), dim3(kRB), 0, s, pos, n, rstatus, rlens, rvals,
-                     rstride, status, out_lens, out, ostride, copy);
+  const int copy = out ? (vw < ostride ? vw : ostride) : 0;
+  if (out && ((vw & 15) || (ostride & 15) || copy <= 0 || (off_v & 15) || !out_lens)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_xgather, dim3(route_grid(n, kRB)), dim3(kRB), 0, s, pos, n, cap, blk, off_s, off_l, off_v, vw,
+                     status, out_lens, out, ostride, copy);
   return (int)hipGetLastError();
+}
+
+// ---------------------------------------------------------------- exchange windows --
+// A rank's window is device memory other ranks of the node map into their own address space: HIP
+// virtual-memory chunks exported as dmabuf descriptors (vmm_share.hpp, the same machinery as the
+// shareable HBM arenas), handed to peers over an abstract UNIX socket named after the window.  An
+// attached window is the peer's memory mapped for THIS process's device: on another GPU the
+// mapping is an xGMI peer mapping, so this device's kernels store into it directly.
+
+void* spl_xw_create(int device, size_t bytes, const char* name) {
+  if (!name || !bytes || hipSetDevice(device) != hipSuccess) return nullptr;
+  auto* w = new VmmArena();
+  if (w->create(device, bytes, (size_t)256 << 20) != 0 || w->serve(name) != 0) {
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+
+void* spl_xw_attach(const char* name, int device) {
+  if (!name || hipSetDevice(device) != hipSuccess) return nullptr;
+  std::vector<int> fds;
+  size_t chunk = 0;
+  if (VmmArena::fetch(name, &fds, &chunk) != 0) return nullptr;
+  auto* w = new VmmArena();
+  if (w->import(device, fds, chunk) != 0) {
+    delete w;
+    return nullptr;
+  }
+  return w;
+}
+
+void* spl_xw_base(void* h) { return h ? ((VmmArena*)h)->base() : nullptr; }
+size_t spl_xw_bytes(void* h) { return h ? ((VmmArena*)h)->chunk() * ((VmmArena*)h)->chunks() : 0; }
+
+void spl_xw_destroy(void* h) { delete (VmmArena*)h; }
+
+// Direct access from `device` to memory on `peer` (xGMI): 0 when usable (already enabled counts),
+// else the HIP error.  Same device: 0.
+int spl_xw_peer(int device, int peer) {
+  if (device == peer) return 0;
+  int can = 0;
+  hipError_t e = hipDeviceCanAccessPeer(&can, device, peer);
+  if (e != hipSuccess) return (int)e;
+  if (!can) return (int)hipErrorPeerAccessUnsupported;
+  if ((e = hipSetDevice(device)) != hipSuccess) return (int)e;
+  e = hipDeviceEnablePeerAccess(peer, 0);
+  if (e == hipErrorPeerAccessAlreadyEnabled) {
+    (void)hipGetLastError();
+    return 0;
+  }
+  return (int)e;
 }
 
 }  // extern "C"

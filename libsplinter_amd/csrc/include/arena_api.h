@@ -10,6 +10,7 @@
  */
 #ifndef SPLINTER_ARENA_API_H
 #define SPLINTER_ARENA_API_H
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -89,17 +90,65 @@ int spl_format_keys(char *out, int kstride, const uint64_t *ids, uint64_t first,
 int spl_format_values(uint8_t *out, int vstride, uint32_t *lens, const uint64_t *ids, uint64_t first, long n,
                       uint32_t ver, uint32_t len, hipStream_t stream);
 
-/* C1 routing (route_kernels.hip): pack a batch into world x cap per-destination rows
- * (shard = (fnv1a >> 40) % world); counts[world] is zeroed by the launcher and receives the
- * rows per destination (may exceed cap: ops beyond cap get pos = -1).  vals/lout/vout NULL for
- * key-only requests.  Gather: status[i] = pos[i] < 0 ? EAGAIN : rstatus[pos[i]], and likewise
- * lengths and min(rstride, ostride) value bytes. */
-int spl_route_pack(const char *keys, int kstride, const uint8_t *vals, int vstride, int vwidth,
-                   const uint32_t *lens, long n, int world, long cap, int32_t *counts, int64_t *pos,
-                   char *kout, uint32_t *lout, uint8_t *vout, hipStream_t stream);
-int spl_route_gather(const int64_t *pos, long n, const int32_t *rstatus, const uint32_t *rlens,
-                     const uint8_t *rvals, int rstride, int32_t *status, uint32_t *out_lens, uint8_t *out,
-                     int ostride, hipStream_t stream);
+/* In-place rows: row i of the launch is client op idx[i] and only the first *count rows are live
+ * (the own-shard ops of a routed step run on the client's arrays). */
+int spl_arena_set_idx(spl_arena_t a, const char *keys, int kstride, const uint8_t *vals, int vstride,
+                      const uint32_t *lens, const int32_t *idx, const int32_t *count, long n, int32_t *status,
+                      int max_retry, uint64_t *stats, hipStream_t stream);
+int spl_arena_get_idx(spl_arena_t a, const char *keys, int kstride, uint8_t *out, int ostride, uint32_t *out_lens,
+                      const int32_t *idx, const int32_t *count, long n, int32_t *status, int max_retry,
+                      uint64_t *stats, hipStream_t stream);
+
+/* ---- routed exchange (route_kernels.hip; parallel/xroute.py) ------------------------------------
+ * Pack one kind of a client batch straight into the owners' request blocks: shard =
+ * ((fnv1a >> 40) & 0xFFFFFF) % world; blk[d] = base of the block for owner d (device table),
+ * rows at blk[d] + off_k / off_l / off_v (key, u32 len, vw value bytes; vw = 0: keys only).
+ * counts[world] is zeroed here and receives every destination's rows (own included); own ops are
+ * listed in lidx (client indices); pos[i] = d*cap + j (remote), -2 (own), -1 (block full). */
+int spl_xr_pack(const char *keys, int ks, const uint8_t *vals, int vstride, const uint32_t *lens, long n, int world,
+                int rank, long cap, const uint64_t *blk, long off_k, long off_l, long off_v, int vw, int32_t *counts,
+                int32_t *lidx, int32_t *pos, hipStream_t stream);
+/* Responses into client order: remote ops read status / len / value row j of blk[d]; full ops get
+ * EAGAIN; own ops are left as the in-place kernels wrote them. */
+int spl_xr_gather(const int32_t *pos, long n, long cap, const uint64_t *blk, long off_s, long off_l, long off_v,
+                  int vw, int32_t *status, uint32_t *out_lens, uint8_t *out, int ostride, hipStream_t stream);
+
+#define SPL_XR_MAX_WORLD 64
+/* One routed step's owner side for spl_kvs_step_xr (all pointers device, except the tables). */
+typedef struct spl_xr_step {
+  int world, rank;
+  long cap_s, cap_g;            /* rows per request block: sets, gets */
+  int ks, vw;                   /* key record bytes; value prefix bytes per routed row */
+  /* the client batch (own ops run in place on these) */
+  const char *skeys; const uint8_t *svals; int svstride; const uint32_t *slens; int32_t *sstatus; long n_set;
+  const char *gkeys; uint8_t *gout; int gostride; uint32_t *glens; int32_t *gstatus; long n_get;
+  const int32_t *lidx_set, *lidx_get;  /* own client indices (NULL: world 1, the batch row for row) */
+  const int32_t *own_counts;           /* [world][2]: this rank's pack counts per destination (set, get);
+                                          the own entry [rank] is the own rows */
+  const int32_t *rcounts;              /* [world][2]: rows received from each source (set, get) */
+  uint64_t req[SPL_XR_MAX_WORLD];      /* request block of source s (this rank's window) */
+  uint64_t resp[SPL_XR_MAX_WORLD];     /* where this rank's responses to source s go */
+  long off_sk, off_sl, off_sv, off_gk; /* request block layout */
+  long off_ss, off_gs, off_gl, off_gv; /* response block layout */
+} spl_xr_step_t;
+
+/* Exchange windows: device memory a peer process maps (VMM dmabuf chunks, abstract socket `name`). */
+void *spl_xw_create(int device, size_t bytes, const char *name);
+void *spl_xw_attach(const char *name, int device);
+void *spl_xw_base(void *w);
+size_t spl_xw_bytes(void *w);
+void spl_xw_destroy(void *w);
+int spl_xw_peer(int device, int peer);
+
+/* Client-stream groups (arena_kernels.hip): one native call issues a KV step's slices on
+ * `writers` + `readers` concurrent streams. */
+void *spl_kvs_create(int writers, int readers);
+void spl_kvs_destroy(void *h);
+int spl_kvs_step(void *h, spl_arena_t a, hipStream_t origin, const char *skeys, int kstride, const uint8_t *svals,
+                 int vstride, const uint32_t *slens, long n_set, int32_t *sstatus, const char *gkeys, uint8_t *gout,
+                 int ostride, uint32_t *glens, long n_get, int32_t *gstatus, int max_retry, uint64_t *stats);
+int spl_kvs_step_xr(void *h, spl_arena_t a, hipStream_t origin, const spl_xr_step_t *x, int max_retry,
+                    uint64_t *stats);
 
 #ifdef __cplusplus
 }

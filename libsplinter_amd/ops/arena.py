@@ -104,21 +104,6 @@ class KvStreams:
                                     ptr(gkeys), ptr(gout), gout.shape[1] if gout is not None else 16, ptr(glens),
                                     n_get, ptr(gstatus), retries, arena.stats.data_ptr()), "kvs_step")
 
-    def step_seg(self, arena: "HbmArena", set_seg, get_seg, retries: int = 64):
-        """The owner side of a routed step on the same streams: ``set_seg`` = (keys, vals, lens, counts, cap,
-        status) and ``get_seg`` = (keys, counts, cap, out, lens, status) over segmented buffers
-        (parallel/routed.py); either may be None."""
-        ptr = lambda t: t.data_ptr() if t is not None else None  # noqa: E731
-        sk, sv, sl, sc, scap, ss = set_seg if set_seg is not None else (None, None, None, None, 1, None)
-        gk, gc, gcap, go, gl, gs = get_seg if get_seg is not None else (None, None, 1, None, None, None)
-        n_set = sk.shape[0] if sk is not None else 0
-        n_get = gk.shape[0] if gk is not None else 0
-        kstride = (sk if n_set else gk).shape[1]
-        _check(self._H.spl_kvs_step_seg(self.h, arena.desc, _stream(), ptr(sk), kstride, ptr(sv),
-                                        sv.shape[1] if sv is not None else 16, ptr(sl), n_set, ptr(ss), ptr(sc), scap,
-                                        ptr(gk), ptr(go), go.shape[1] if go is not None else 16, ptr(gl), n_get,
-                                        ptr(gs), ptr(gc), gcap, retries, arena.stats.data_ptr()), "kvs_step_seg")
-
     def close(self):
         if self.h:
             self._H.spl_kvs_destroy(self.h)

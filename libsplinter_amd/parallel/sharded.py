@@ -10,11 +10,12 @@ xGMI, executed by the owner's kernels, and the results are routed back.
 
 Collectives, all over the default (RCCL) group:
 
-  C1  routed set/get/unset/integer_op/meta/set_embeddings: ONE all-to-all-v of
-      packed request rows (key | args | value) and ONE of packed response
-      rows (status | len | value) per batch, after a count exchange.  xGMI is
-      point-to-point (7 links per GPU), so the all-to-all drives every link at
-      once; packing keeps it to 2 large messages instead of 3-4 small ones.
+  C1  routed set/get: parallel/xroute.py -- one request and one response
+      exchange per batch, own-shard ops executed in place, the blocks moved by
+      xGMI stores into peer-mapped windows (bench) or one all-to-all each (API).
+      unset/integer_op/meta/set_embeddings: ONE all-to-all-v of packed request
+      rows (key | args | value) and ONE of packed response rows per batch,
+      after a count exchange.
   C2  node-wide signal-group counters: all-reduce(sum) of the 64 u64 counters.
   C3  search query broadcast from rank 0.
   C4  search top-k merge: all-gather of each shard's local top-k (sim, dist,
@@ -171,7 +172,7 @@ class ShardedKV:
     def __init__(self, local, group: Optional[dist.ProcessGroup] = None):
         self.local = local
         self.group = group
-        self._rk = None
+        self._kvstreams = None
         if dist.is_available() and dist.is_initialized():
             self.world = dist.get_world_size(group)
             self.rank = dist.get_rank(group)
@@ -220,54 +221,81 @@ class ShardedKV:
         return shard_of(self.local.hash_keys(keys), self.world) == self.rank
 
     # -------------------------------------------------------- C1: ops ----
-    def _routed(self):
-        if self._rk is None:
-            from .routed import RoutedKV
-            self._rk = RoutedKV(self.local, self.group)
-        return self._rk
-
     def _exact_cap(self, keys: torch.Tensor) -> int:
         """Largest per-destination count of this batch over all ranks (one host sync):
-        the API path never returns EAGAIN for a full routing segment."""
+        the API path never returns EAGAIN for a full request block."""
         dest = shard_of(self.local.hash_keys(keys), self.world)
         c = torch.bincount(dest, minlength=self.world).max().reshape(1).to(torch.int64)
         self._c.all_reduce(c, op=dist.ReduceOp.MAX)
         return max(1, int(c.item()))
 
-    def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, cap: Optional[int] = None,
-            vwidth: Optional[int] = None, **kw) -> torch.Tensor:
-        """Routed set (C1).  ``cap``/``vwidth`` given (identical on every rank): no host
-        synchronisation (parallel/routed.py); otherwise both are measured on this batch."""
+    def _kvs(self):
+        if self._kvstreams is None:
+            from ..ops.arena import KvStreams
+            self._kvstreams = KvStreams(1, 1)
+        return self._kvstreams
+
+    def _xroute(self, keys, n_set, n_get, vw, cap, set_kind):
+        """A one-shot routed exchange (parallel/xroute.py) sized for this batch; the API path moves
+        the blocks with the collectives (rccl / host transport), bench.py keeps a persistent peer one."""
+        from .xroute import XRoute
+        # the block geometry must be identical on every rank: caps, key and value widths are agreed
+        # (a rank with an empty batch still takes part in the exchange)
+        return XRoute(self.local, n_set, n_get, vw, ks=keys.shape[1], group=self.group,
+                      transport="rccl" if self.local.device == "cuda" else "host",
+                      cap_s=cap if set_kind else 0, cap_g=0 if set_kind else cap)
+
+    def _agree_keys(self, keys: torch.Tensor) -> torch.Tensor:
+        """Key records widened to the widest of any rank's batch (16-B multiple)."""
+        m = torch.tensor([keys.shape[1]], dtype=torch.int64, device=keys.device)
+        self._c.all_reduce(m, op=dist.ReduceOp.MAX)
+        w = int(m.item())
+        if w != keys.shape[1]:
+            k2 = torch.zeros((keys.shape[0], w), dtype=torch.uint8, device=keys.device)
+            k2[:, : keys.shape[1]] = keys
+            keys = k2
+        return keys.contiguous()
+
+    def set(self, keys: torch.Tensor, vals: torch.Tensor, lens: torch.Tensor, vwidth: Optional[int] = None,
+            **kw) -> torch.Tensor:
+        """Routed set (C1): one request and one response exchange; only the used 16-B prefix of
+        the value rows travels (``vwidth``, measured on this batch when not given)."""
         if self.world == 1:
             return self.local.set(keys, vals, lens, **kw)
         if vwidth is None:
-            # ship only the used prefix of the value rows (16-B multiple): 150-B values in 256-B
-            # rows are 40 % less xGMI traffic
-            vwidth = (int(lens.max().item()) + 15) // 16 * 16 if lens.numel() else 16
-        vwidth = min(max(16, vwidth), vals.shape[1])
-        cap = self._exact_cap(keys) if cap is None else cap
-        return self._routed().set(keys, vals, lens, cap, vwidth, **kw)
+            m = torch.tensor([int(lens.max().item()) if lens.numel() else 1], dtype=torch.int64, device=keys.device)
+            self._c.all_reduce(m, op=dist.ReduceOp.MAX)
+            vwidth = (int(m.item()) + 15) // 16 * 16
+        vwidth = max(16, min(vwidth, (vals.shape[1] + 15) // 16 * 16))
+        if vals.shape[1] % 16 or vals.shape[1] < vwidth:
+            v2 = torch.zeros((vals.shape[0], max(vwidth, (vals.shape[1] + 15) // 16 * 16)), dtype=torch.uint8,
+                             device=vals.device)
+            v2[:, : vals.shape[1]] = vals
+            vals = v2
+        keys = self._agree_keys(keys)
+        xr = self._xroute(keys, keys.shape[0], 0, vwidth, self._exact_cap(keys), True)
+        try:
+            st, _, _, _ = xr.step(0, self._kvs() if self.local.device == "cuda" else None, keys.contiguous(),
+                                  vals.contiguous(), lens.to(torch.int32).contiguous(), None)
+        finally:
+            xr.close()
+        return st
 
-    def get(self, keys: torch.Tensor, cap: Optional[int] = None, width: Optional[int] = None,
+    def get(self, keys: torch.Tensor, width: Optional[int] = None,
             **kw) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
-        """Routed get (C1) -> (status, vals, lens).  With ``width`` the response rows
-        carry ``width`` value bytes (longer values: EMSGSIZE); without it, the longest
-        value any shard returns (one scalar all-reduce)."""
+        """Routed get (C1) -> (status, vals, lens).  Response rows carry ``width`` value bytes
+        (default: the shard's max_val); a longer value returns EMSGSIZE (-90)."""
         if self.world == 1:
             return self.local.get(keys, **kw)
-        rk = self._routed()
-        cap = self._exact_cap(keys) if cap is None else cap
-        op = rk.begin_get(keys, cap, width or (self.local.max_val + 15) // 16 * 16)
-        rk.execute(op, **kw)
-        if width is None:
-            t = op.t
-            w = torch.tensor([(int(t["rlens"].max().item()) + 15) // 16 * 16 if t["rlens"].numel() else 16],
-                             dtype=torch.int64, device=t["rvals"].device)
-            self._c.all_reduce(w, op=dist.ReduceOp.MAX)
-            op.width = max(16, min(int(w.item()), t["rvals"].shape[1]))
-            t["rvals"] = t["rvals"][:, :op.width].contiguous()
-        rk.respond(op)
-        return rk.finish(op)
+        width = width or (self.local.max_val + 15) // 16 * 16
+        keys = self._agree_keys(keys)
+        xr = self._xroute(keys, 0, keys.shape[0], width, self._exact_cap(keys), False)
+        try:
+            _, st, out, ln = xr.step(0, self._kvs() if self.local.device == "cuda" else None, None, None, None,
+                                     keys.contiguous())
+        finally:
+            xr.close()
+        return st, out, ln
 
     def unset(self, keys: torch.Tensor) -> torch.Tensor:
         if self.world == 1:
@@ -427,55 +455,6 @@ class GpuShard:
     def max_val(self):
         return self.arena.max_val
 
-    def set_seg(self, keys, vals, lens, counts, cap, **kw):
-        return self.arena.set_seg(keys, vals, lens, counts, cap, **kw)
-
-    def get_seg(self, keys, counts, cap, width, **kw):
-        return self.arena.get_seg(keys, counts, cap, width, **kw)
-
-    def route_pack(self, keys, vals, lens, vwidth, world, cap):
-        """spl_route_pack: -> (counts[world], pos[n], keys, lens, vals) of the world x cap segments."""
-        from .. import _native as N
-        from ..ops.arena import _check, _keys, _stream
-        keys = _keys(keys)
-        n, ks, dev = keys.shape[0], keys.shape[1], keys.device
-        counts = torch.empty(world, dtype=torch.int32, device=dev)
-        pos = torch.empty(n, dtype=torch.int64, device=dev)
-        kout = torch.empty((world * cap, ks), dtype=torch.uint8, device=dev)
-        lout = vout = None
-        vp = lp = 0
-        vstride = 0
-        if vals is not None:
-            vals, lens = vals.contiguous(), lens.contiguous()
-            assert lens.dtype in (torch.int32, torch.uint32) and vals.shape[0] == n and lens.shape[0] == n
-            lout = torch.empty(world * cap, dtype=torch.int32, device=dev)
-            vout = torch.empty((world * cap, vwidth), dtype=torch.uint8, device=dev)
-            vp, lp, vstride = vals.data_ptr(), lens.data_ptr(), vals.shape[1]
-        _check(N.hip_lib().spl_route_pack(keys.data_ptr(), ks, vp or None, vstride, vwidth, lp or None, n, world, cap,
-                                          counts.data_ptr(), pos.data_ptr(), kout.data_ptr(),
-                                          lout.data_ptr() if lout is not None else None,
-                                          vout.data_ptr() if vout is not None else None, _stream()), "route_pack")
-        return counts, pos, kout, lout, vout
-
-    def route_gather(self, pos, rstatus, rlens=None, rvals=None, width=0, out=None, out_lens=None, status=None):
-        """spl_route_gather: routed responses -> client order (status, vals, lens)."""
-        from .. import _native as N
-        from ..ops.arena import _check, _stream
-        n, dev = pos.shape[0], pos.device
-        status = torch.empty(n, dtype=torch.int32, device=dev) if status is None else status
-        if rlens is not None:
-            out_lens = torch.empty(n, dtype=torch.int32, device=dev) if out_lens is None else out_lens
-            out = torch.empty((n, width), dtype=torch.uint8, device=dev) if out is None else out
-            assert out.is_contiguous() and out.shape[0] == n
-        _check(N.hip_lib().spl_route_gather(pos.data_ptr(), n, rstatus.data_ptr(),
-                                            rlens.data_ptr() if rlens is not None else None,
-                                            rvals.data_ptr() if rvals is not None else None,
-                                            rvals.shape[1] if rvals is not None else 0, status.data_ptr(),
-                                            out_lens.data_ptr() if rlens is not None else None,
-                                            out.data_ptr() if rlens is not None else None,
-                                            out.shape[1] if rlens is not None else 0, _stream()), "route_gather")
-        return status, out, out_lens
-
     def integer_op(self, keys, ops, masks):
         return self.arena.integer_op(keys, ops, masks)
 
@@ -587,31 +566,6 @@ class HostShard:
     @property
     def max_val(self):
         return self.store.max_val
-
-    @staticmethod
-    def _live(n, counts, cap):
-        return (torch.arange(n) % cap) < torch.repeat_interleave(counts.to(torch.int64), cap)
-
-    def set_seg(self, keys, vals, lens, counts, cap, **kw):
-        live = self._live(keys.shape[0], counts, cap)
-        st = torch.full((keys.shape[0],), -22, dtype=torch.int32)
-        st[live] = self.set(keys[live], vals[live], lens[live], **kw)
-        return st
-
-    def get_seg(self, keys, counts, cap, width, **kw):
-        n = keys.shape[0]
-        live = self._live(n, counts, cap)
-        st = torch.full((n,), -22, dtype=torch.int32)
-        out = torch.zeros((n, width), dtype=torch.uint8)
-        lens = torch.zeros(n, dtype=torch.int32)
-        s, v, ln = self.get(keys[live], **kw)
-        big = ln > width
-        s = torch.where(big & (s == 0), torch.full_like(s, -90), s)  # EMSGSIZE, like the kernel
-        w = min(width, v.shape[1])
-        v = v[:, :w] * (s == 0).unsqueeze(1).to(torch.uint8)
-        st[live], lens[live] = s, torch.where(s == 0, ln, torch.zeros_like(ln))
-        out[live, :w] = v
-        return st, out, lens
 
     def integer_op(self, keys, ops, masks):
         st, res = [], []

@@ -166,66 +166,52 @@ def test_sharded_collectives_gloo(world, uniq):
         assert res.get(r) == "ok", res.get(r)
 
 
-def _routed_worker(rank, world, port, base, q):
-    """RoutedKV (parallel/routed.py): fixed-capacity segments, phase-split calls,
-    overflow -> EAGAIN, narrow response rows -> EMSGSIZE."""
+def _xroute_worker(rank, world, port, base, q):
+    """XRoute (parallel/xroute.py) on the host transport: one request / one response exchange,
+    own-shard ops in place, full blocks -> EAGAIN, narrow response rows -> EMSGSIZE."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from libsplinter_amd import Store, unlink
-        from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
         from libsplinter_amd.parallel.sharded import HostShard, shard_of
+        from libsplinter_amd.parallel.xroute import XRoute
         name = f"{base}_q{rank}"
         st = Store.create(name, slots=2048, max_val=128, embeddings=False)
         sh = HostShard(st)
-        rk = RoutedKV(sh, resp_group=dist.new_group(backend="gloo"))
         n = 120
         mine = [f"q{rank}_k{i}" for i in range(n)]
         K = _keys(mine)
         V, L = _vals([f"value-{m}-padding".encode() for m in mine])
-        cap = route_capacity(n, world)
-        op = rk.begin_set(K, V, L, cap, 32)
-        rk.execute(op)
-        rk.respond(op)
-        s = rk.finish(op)
+        xr = XRoute(sh, n, 0, 32, ks=32, resp_group=dist.new_group(backend="gloo"))
+        assert xr.transport == "host"
+        s, _, _, _ = xr.step(0, None, K, V, L, None)
         assert (s == 0).all(), s
+        # own-shard ops never entered the exchange: they sit only in this rank's store
+        own = shard_of(sh.hash_keys(K), world) == rank
+        assert int(xr.scnt[0][rank, 0]) == int(own.sum())
         dist.barrier()
         allk = [f"q{r}_k{i}" for r in range(world) for i in range(n)]
-        # two gets in flight at once: requests of both, then execute/respond/finish
-        half = len(allk) // 2
-        g1 = rk.begin_get(_keys(allk[:half]), route_capacity(half, world), 32)
-        g2 = rk.begin_get(_keys(allk[half:]), route_capacity(len(allk) - half, world), 32)
-        res = []
-        for g in (g1, g2):
-            rk.execute(g)
-        for g in (g1, g2):
-            rk.respond(g)
-        for g in (g1, g2):
-            res.append(rk.finish(g))
-        sts = torch.cat([r[0] for r in res])
-        vs = torch.cat([r[1] for r in res])
-        ls = torch.cat([r[2] for r in res])
+        xg = XRoute(sh, 0, len(allk), 32, ks=32)
+        _, sts, vs, ls = xg.step(1, None, None, None, None, _keys(allk))
         assert (sts == 0).all()
         for i, k in enumerate(allk):
             assert bytes(vs[i, : ls[i]].numpy()) == f"value-{k}-padding".encode()
         # response rows narrower than the values: EMSGSIZE, no bytes
-        s_, v_, l_ = rk.get(_keys(allk[:10]), route_capacity(10, world), 16)
+        xn = XRoute(sh, 0, 10, 16, ks=32)
+        _, s_, v_, l_ = xn.step(0, None, None, None, None, _keys(allk[:10]))
         assert (s_ == -90).all() and (l_ == 0).all(), (s_, l_)
-        # tight capacity: the excess ops of a full segment come back EAGAIN, the rest land
+        # tight capacity: the excess ops of a full block come back EAGAIN, the rest land
         ex = [f"x{rank}_{i}" for i in range(60)]
         KX = _keys(ex)
         VX, LX = _vals([b"x" * 8] * 60)
         tight = 60 // world - 3
-        sx = rk.set(KX, VX, LX, tight, 16)
+        xt = XRoute(sh, 60, 0, 16, ks=32, cap_s=tight, cap_g=0)
+        sx, _, _, _ = xt.step(0, None, KX, VX, LX, None)
         dest = shard_of(sh.hash_keys(KX), world)
         over = int((torch.bincount(dest, minlength=world) - tight).clamp(min=0).sum())
         assert int((sx == -11).sum()) == over and int((sx == 0).sum()) == 60 - over
         dist.barrier()
-        ok_keys = [k for k, s1 in zip(ex, sx.tolist()) if s1 == 0]
-        if ok_keys:
-            s2, _, _ = rk.get(_keys(ok_keys), len(ok_keys), 16)
-            assert (s2 == 0).all()
         q.put((rank, "ok"))
         st.close()
         unlink(name)
@@ -237,11 +223,11 @@ def _routed_worker(rank, world, port, base, q):
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_routed_kv_gloo(world, uniq):
+def test_xroute_gloo(world, uniq):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    ps = [ctx.Process(target=_routed_worker, args=(r, world, port, uniq, q)) for r in range(world)]
+    ps = [ctx.Process(target=_xroute_worker, args=(r, world, port, uniq, q)) for r in range(world)]
     for p in ps:
         p.start()
     res = {}
@@ -325,21 +311,21 @@ def test_chunked_uneven_all_to_all_gloo(world):
 
 
 def _routed_step_worker(rank, world, port, base, q, steps, n):
-    """The routed step of bench.py at N > 1 (pack -> request all-to-alls -> owner runs -> response
-    all-to-alls -> gather), software-pipelined as there: step i's requests are issued before step
-    i-1's responses are gathered.  Each step sets n new keys and gets n keys set by OTHER ranks in
-    earlier steps; at the end every get must have returned its key's value (integrity 0)."""
+    """The routed step of bench.py at N > 1 (XRoute: pack -> count exchange -> owner runs ->
+    response exchange -> gather), software-pipelined as there: step i's request is issued before
+    step i-1's responses are gathered, and the two parities' blocks are both live.  Each step sets
+    n new keys and gets n keys set by OTHER ranks two steps earlier; every get must return its
+    key's value (integrity 0)."""
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         from libsplinter_amd import Store, unlink
-        from libsplinter_amd.parallel.routed import RoutedKV, route_capacity
         from libsplinter_amd.parallel.sharded import HostShard
+        from libsplinter_amd.parallel.xroute import XRoute
         name = f"{base}_w{rank}"
         st = Store.create(name, slots=8192, max_val=64, embeddings=False)
-        rk = RoutedKV(HostShard(st), resp_group=dist.new_group(backend="gloo"))
-        cap = route_capacity(n, world)
+        xr = XRoute(HostShard(st), n, n, 32, ks=32, resp_group=dist.new_group(backend="gloo"))
 
         def val(k):
             return f"v:{k}".encode()
@@ -351,24 +337,23 @@ def _routed_step_worker(rank, world, port, base, q, steps, n):
                 sk = [f"s{i}_r{rank}_{j}" for j in range(n)]
                 K = _keys(sk)
                 V, L = _vals([val(k) for k in sk])
-                so = rk.begin_set(K, V, L, cap, 32)
-                go = None
+                gk = None
+                GK = None
                 if i >= 2:  # keys another rank set two steps ago: already finished everywhere
                     src = (rank + 1 + i) % world
                     gk = [f"s{i - 2}_r{src}_{j}" for j in range(n)]
-                    go = rk.begin_get(_keys(gk), cap, 32)
-                rk.execute(so)
-                if go is not None:
-                    rk.execute(go)
-                cur = (so, go, gk if go is not None else None)
+                    GK = _keys(gk)
+                outs = (torch.empty(n, dtype=torch.int32), torch.zeros((n, 32), dtype=torch.uint8),
+                        torch.empty(n, dtype=torch.int32), torch.empty(n, dtype=torch.int32))
+                xr.request(i, K, V, L, GK)
+                xr.execute(i, None, *outs)
+                cur = (i, outs, gk)
             if pending is not None:  # the previous step's responses, after this step's requests
-                pso, pgo, pgk = pending
-                rk.respond(pso)
-                s = rk.finish(pso)
-                bad += int((s != 0).sum())
-                if pgo is not None:
-                    rk.respond(pgo)
-                    gs, gv, gl = rk.finish(pgo)
+                pi, (ss, gv, gl, gs), pgk = pending
+                xr.respond(pi)
+                xr.finish(pi, ss, gv, gl, gs)
+                bad += int((ss != 0).sum())
+                if pgk is not None:
                     for j, k in enumerate(pgk):
                         ok = int(gs[j]) == 0 and bytes(gv[j, : gl[j]].numpy()) == val(k)
                         bad += 0 if ok else 1

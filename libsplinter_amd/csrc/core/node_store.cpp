@@ -12,6 +12,9 @@
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <unistd.h>
+#include <atomic>
+#include <thread>
+#include <vector>
 
 #include "splinter_ext.h"
 
@@ -214,6 +217,12 @@ NodeStore* NodeStore::open(const std::string& name, int* err) {
 }
 
 NodeStore::~NodeStore() {
+  if (scratch_) {
+    using Free = void (*)(void*);
+    static Free pf = (Free)hbm_symbol("spl_hbm_host_free");
+    if (scratch_pinned_ && pf) pf(scratch_);
+    else free(scratch_);
+  }
   if (event_fd_ >= 0) {
     if (desc_ && __atomic_load_n(&desc_->event_pid, __ATOMIC_ACQUIRE) == (int32_t)getpid()) {
       __atomic_store_n(&desc_->event_fd, -1, __ATOMIC_RELEASE);
@@ -363,6 +372,215 @@ int NodeStore::madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t
     }
   }
   return rc;
+}
+
+// ------------------------------------------------------------------ batches --
+// A batch is counting-sorted by owning shard into one scratch buffer (pinned when the HBM backend
+// is present, so HBM shards DMA straight from it), every shard's contiguous part runs on its own
+// thread (HBM shards: HbmStore::*_batch on that shard's GPU, all GPUs at once), and the outputs
+// are scattered back into client order.  Gathers and scatters run on kNodeBatchThreads threads.
+namespace {
+constexpr int kNodeBatchThreads = 8;
+
+template <class F>
+void par_range(long n, F&& f) {
+  const int t = n < 65536 ? 1 : kNodeBatchThreads;
+  if (t == 1) { f(0L, n); return; }
+  std::vector<std::thread> th;
+  for (int i = 0; i < t; ++i) th.emplace_back([&, i] { f(n * i / t, n * (i + 1) / t); });
+  for (auto& x : th) x.join();
+}
+}  // namespace
+
+struct NodeStore::Plan {
+  std::vector<long> perm;   // perm[k]: client op at sorted position k
+  std::vector<long> off;    // shard j's ops are sorted positions [off[j], off[j+1])
+  Plan(const char* keys, int kstride, long n, int nsh) : perm((size_t)n), off((size_t)nsh + 1, 0) {
+    std::vector<int32_t> dest((size_t)n);
+    const int cut = kstride < 64 ? kstride : 63;
+    par_range(n, [&](long b, long e) {
+      char k[64];
+      for (long i = b; i < e; ++i) {
+        std::memcpy(k, keys + i * kstride, (size_t)cut);
+        k[cut] = 0;
+        dest[(size_t)i] = node_shard_of(KeyRef(k).hash, nsh);
+      }
+    });
+    for (long i = 0; i < n; ++i) ++off[(size_t)dest[(size_t)i] + 1];
+    for (int j = 0; j < nsh; ++j) off[(size_t)j + 1] += off[(size_t)j];
+    std::vector<long> cur(off.begin(), off.end() - 1);
+    for (long i = 0; i < n; ++i) perm[(size_t)cur[(size_t)dest[(size_t)i]]++] = i;
+  }
+  // sorted copy of a column (rows of `w` bytes)
+  void gather(uint8_t* dst, const void* src, long w) const {
+    const long n = (long)perm.size();
+    par_range(n, [&](long b, long e) {
+      for (long k = b; k < e; ++k) std::memcpy(dst + k * w, (const uint8_t*)src + perm[(size_t)k] * w, (size_t)w);
+    });
+  }
+  void scatter(void* dst, const uint8_t* src, long w) const {
+    const long n = (long)perm.size();
+    par_range(n, [&](long b, long e) {
+      for (long k = b; k < e; ++k) std::memcpy((uint8_t*)dst + perm[(size_t)k] * w, src + k * w, (size_t)w);
+    });
+  }
+  template <class F>
+  void each_shard(int nsh, F&& f) const {
+    std::vector<std::thread> th;
+    for (int j = 0; j < nsh; ++j)
+      if (off[(size_t)j + 1] > off[(size_t)j]) th.emplace_back([&, j] { f(j, off[(size_t)j], off[(size_t)j + 1] - off[(size_t)j]); });
+    for (auto& x : th) x.join();
+  }
+};
+
+uint8_t* NodeStore::scratch(size_t bytes) {
+  if (scratch_bytes_ >= bytes) return scratch_;
+  using Alloc = void* (*)(size_t);
+  using Free = void (*)(void*);
+  static Alloc pa = (Alloc)hbm_symbol("spl_hbm_host_alloc");
+  static Free pf = (Free)hbm_symbol("spl_hbm_host_free");
+  if (scratch_) {
+    if (scratch_pinned_ && pf) pf(scratch_);
+    else free(scratch_);
+  }
+  scratch_ = nullptr;
+  scratch_bytes_ = 0;
+  scratch_pinned_ = false;
+  if (desc_->backend == 1 && pa) {
+    scratch_ = (uint8_t*)pa(bytes);
+    scratch_pinned_ = scratch_ != nullptr;
+  }
+  if (!scratch_) scratch_ = (uint8_t*)aligned_alloc(64, (bytes + 63) / 64 * 64);
+  if (scratch_) scratch_bytes_ = bytes;
+  return scratch_;
+}
+
+namespace {
+inline long a64(long x) { return (x + 63) & ~63L; }
+}
+
+long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
+                          long n, int32_t* status, int retries) {
+  const int nsh = nshards();
+  Plan pl(keys, kstride, n, nsh);
+  std::lock_guard<std::mutex> lk(scratch_mu_);
+  const long ob = 0, vb = a64(n * kstride), lb = vb + a64(n * (long)vstride), sb = lb + a64(n * 4);
+  uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
+  if (!S) return -1;
+  pl.gather(S + ob, keys, kstride);
+  pl.gather(S + vb, vals, vstride);
+  pl.gather(S + lb, lens, 4);
+  std::atomic<bool> fail{false};
+  pl.each_shard(nsh, [&](int j, long o, long m) {
+    StoreBase* sh = shards_[(size_t)j];
+    const char* k = (const char*)S + ob + o * kstride;
+    const uint8_t* v = S + vb + o * (long)vstride;
+    const uint32_t* l = (const uint32_t*)(S + lb) + o;
+    int32_t* st = (int32_t*)(S + sb) + o;
+    long r = sh->set_batch(k, kstride, v, vstride, l, m, st, retries);
+    if (r == kNoBatch) r = generic_set_batch(sh, k, kstride, v, vstride, l, m, st, retries, 4);
+    if (r < 0) fail = true;
+  });
+  if (fail) return -1;
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.scatter(status, S + sb, 4);
+  long ok = 0;
+  for (long i = 0; i < n; ++i) ok += status[i] == 0;
+  return ok;
+}
+
+long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
+                          int32_t* status, int retries) {
+  const int nsh = nshards();
+  Plan pl(keys, kstride, n, nsh);
+  std::lock_guard<std::mutex> lk(scratch_mu_);
+  const long ob = 0, sb = a64(n * kstride), lb = sb + a64(n * 4), vb = lb + a64(n * 4);
+  uint8_t* S = scratch((size_t)(vb + (out ? a64(n * (long)ostride) : 0)));
+  if (!S) return -1;
+  pl.gather(S + ob, keys, kstride);
+  std::atomic<bool> fail{false};
+  pl.each_shard(nsh, [&](int j, long o, long m) {
+    StoreBase* sh = shards_[(size_t)j];
+    const char* k = (const char*)S + ob + o * kstride;
+    uint8_t* v = out ? S + vb + o * (long)ostride : nullptr;
+    uint32_t* l = (uint32_t*)(S + lb) + o;
+    int32_t* st = (int32_t*)(S + sb) + o;
+    long r = sh->get_batch(k, kstride, v, ostride, l, m, st, retries);
+    if (r == kNoBatch) r = generic_get_batch(sh, k, kstride, v, ostride, l, m, st, retries, 4);
+    if (r < 0) fail = true;
+  });
+  if (fail) return -1;
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.scatter(status, S + sb, 4);
+  if (out_lens) pl.scatter(out_lens, S + lb, 4);
+  if (out) pl.scatter(out, S + vb, ostride);
+  long ok = 0;
+  for (long i = 0; i < n; ++i) ok += status[i] == 0;
+  return ok;
+}
+
+long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,
+                            int32_t* status, uint64_t* results) {
+  const int nsh = nshards();
+  Plan pl(keys, kstride, n, nsh);
+  std::lock_guard<std::mutex> lk(scratch_mu_);
+  const long kb = 0, pb = a64(n * kstride), mb = pb + a64(n * 4), sb = mb + a64(n * 8), rb = sb + a64(n * 4);
+  uint8_t* S = scratch((size_t)(rb + a64(n * 8)));
+  if (!S) return -1;
+  pl.gather(S + kb, keys, kstride);
+  pl.gather(S + pb, ops, 4);
+  if (masks) pl.gather(S + mb, masks, 8);
+  else std::memset(S + mb, 0, (size_t)(n * 8));
+  std::atomic<bool> fail{false};
+  pl.each_shard(nsh, [&](int j, long o, long m) {
+    StoreBase* sh = shards_[(size_t)j];
+    const char* k = (const char*)S + kb + o * kstride;
+    const int* op = (const int*)(S + pb) + o;
+    const uint64_t* mk = (const uint64_t*)(S + mb) + o;
+    int32_t* st = (int32_t*)(S + sb) + o;
+    uint64_t* rs = results ? (uint64_t*)(S + rb) + o : nullptr;
+    long r = sh->intop_batch(k, kstride, op, mk, m, st, rs);
+    if (r == kNoBatch) r = generic_intop_batch(sh, k, kstride, op, mk, m, st, rs, 4);
+    if (r < 0) fail = true;
+  });
+  if (fail) return -1;
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.scatter(status, S + sb, 4);
+  if (results) pl.scatter(results, S + rb, 8);
+  long ok = 0;
+  for (long i = 0; i < n; ++i) ok += status[i] == 0;
+  return ok;
+}
+
+long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) {
+  const int nsh = nshards();
+  Plan pl(keys, kstride, n, nsh);
+  std::lock_guard<std::mutex> lk(scratch_mu_);
+  const long kb = 0, vb = a64(n * kstride), sb = vb + n * (long)kEmbedBytes;
+  uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
+  if (!S) return -1;
+  pl.gather(S + kb, keys, kstride);
+  pl.gather(S + vb, vecs, (long)kEmbedBytes);
+  std::atomic<bool> fail{false};
+  pl.each_shard(nsh, [&](int j, long o, long m) {
+    StoreBase* sh = shards_[(size_t)j];
+    const char* k = (const char*)S + kb + o * kstride;
+    const float* v = (const float*)(S + vb + o * (long)kEmbedBytes);
+    int32_t* st = (int32_t*)(S + sb) + o;
+    long r = sh->set_embedding_batch(k, kstride, v, m, st);
+    if (r == kNoBatch) r = generic_set_embedding_batch(sh, k, kstride, v, m, nullptr, st, 4);
+    if (r < 0) fail = true;
+  });
+  if (fail) return -1;
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.scatter(status, S + sb, 4);
+  long ok = 0;
+  for (long i = 0; i < n; ++i) ok += status[i] == 0;
+  return ok;
 }
 
 }  // namespace spl

@@ -21,6 +21,7 @@
 // rank creates its own shard and joins it (spl_node_join), and any process then opens "node:NAME".
 #pragma once
 #include <atomic>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -130,8 +131,24 @@ class NodeStore final : public StoreBase {
   }
   int madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t timeout) override;
 
+  // host-array batches: hash-partitioned over the shards, every shard's part run concurrently
+  // (HBM shards: each on its own GPU through its device batch path)
+  long set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens, long n,
+                 int32_t* status, int retries) override;
+  long get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
+                 int32_t* status, int retries) override;
+  long intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n, int32_t* status,
+                   uint64_t* results) override;
+  long set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) override;
+
  private:
   NodeStore() = default;
+  struct Plan;  // node_store.cpp: a batch's shard partition
+  uint8_t* scratch(size_t bytes);
+  std::mutex scratch_mu_;
+  uint8_t* scratch_ = nullptr;
+  size_t scratch_bytes_ = 0;
+  bool scratch_pinned_ = false;
 
   std::string name_;
   NodeDesc* desc_ = nullptr;

@@ -448,8 +448,39 @@ class HbmStore final : public StoreBase {
   long search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap, spl_search_hit* out);
   int restore_from(const char* path);
 
+  // ------------------------------------------------------ host-array batches --
+  long set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens, long n,
+                 int32_t* status, int retries) override;
+  long get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
+                 int32_t* status, int retries) override;
+  long intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n, int32_t* status,
+                   uint64_t* results) override;
+  long set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) override;
+
  private:
   HbmStore() = default;
+  // Batch staging (batch_run): two chunk slots, each its own stream, device buffer and pinned
+  // host buffer, so chunk c+1's host-to-device copy overlaps chunk c's kernel and copy-back.
+  struct Stage {
+    hipStream_t s = nullptr;
+    uint8_t* d = nullptr;
+    size_t dbytes = 0;
+    uint8_t* h = nullptr;
+    size_t hbytes = 0;
+    std::vector<std::pair<std::pair<uint8_t*, const uint8_t*>, size_t>> out;  // pageable copy-outs after sync
+  };
+  Stage stg_[2];
+  std::mutex batch_mu_;
+  // One array of a batch: caller pointer, caller row stride, device row stride, input / output.
+  struct Col {
+    const void* user;
+    long ustride;  // caller bytes per op
+    long dstride;  // device bytes per op (16-B rows for key / value records)
+    bool in, out;
+    bool pinned;
+  };
+  template <class K>
+  long batch_run(long n, Col* cols, int ncols, K&& kernel);
   int setup_buffers();
   int ring(uint32_t op, uint32_t sub, const char* key, const void* in, uint32_t in_len, uint64_t arg, void* out,
            uint32_t out_cap, RingResult* r) {
@@ -786,6 +817,14 @@ HbmStore* HbmStore::open(const char* name, int* err) {
 
 HbmStore::~HbmStore() {
   DevGuard dg(device_);
+  for (auto& st : stg_) {
+    if (st.s) {
+      (void)hipStreamSynchronize(st.s);
+      (void)hipStreamDestroy(st.s);
+    }
+    if (st.d) (void)hipFree(st.d);
+    if (st.h) (void)hipHostFree(st.h);
+  }
   stop_proxy();
   ring_.stop();  // the worker reads the arena: drain it before the arena goes away
   if (stream_) (void)hipStreamSynchronize(stream_);
@@ -953,6 +992,209 @@ StoreBase* hbm_factory_impl(const char* name, size_t slots, size_t max_val, unsi
 
 }  // namespace spl
 
+namespace spl {
+
+namespace {
+
+bool host_pinned(const void* p) {
+  if (!p) return false;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+inline long al256(long x) { return (x + 255) & ~255L; }
+inline long r16(long x) { return (x + 15) & ~15L; }
+
+long count_ok(const int32_t* st, long n) {
+  long ok = 0;
+  for (long i = 0; i < n; ++i) ok += st[i] == 0;
+  return ok;
+}
+
+}  // namespace
+
+// Run a batch of n ops in chunks: per chunk, every input column goes to the device (a 2-D DMA from
+// the caller's array when it is pinned, else through the slot's pinned buffer), `kernel(m, dev
+// column pointers, stream)` runs, and every output column comes back the same way.  Key and value
+// records are widened to 16-B device rows (the 2-D copies re-stride them; pad bytes are zeroed).
+template <class K>
+long HbmStore::batch_run(long n, Col* cols, int ncols, K&& kernel) {
+  DevGuard dg(device_);
+  std::lock_guard<std::mutex> lk(batch_mu_);
+  long per = 0, hper = 0;
+  for (int c = 0; c < ncols; ++c) {
+    cols[c].pinned = host_pinned(cols[c].user);
+    per += cols[c].dstride;
+    if (!cols[c].pinned) hper += cols[c].ustride;
+  }
+  static const long budget = (long)(getenv("SPLINTER_BATCH_CHUNK_MB") ? atol(getenv("SPLINTER_BATCH_CHUNK_MB"))
+                                                                      : 96) << 20;
+  const long chunk = std::max(1L, std::min(n, budget / std::max(per, 1L)));
+  const size_t dneed = (size_t)(chunk * per + 256L * ncols), hneed = (size_t)(chunk * hper + 256L * ncols);
+  for (auto& st : stg_) {
+    if (!st.s && hipStreamCreateWithFlags(&st.s, hipStreamNonBlocking) != hipSuccess) return -1;
+    if (st.dbytes < dneed) {
+      if (st.d) (void)hipFree(st.d);
+      st.d = nullptr;
+      st.dbytes = 0;
+      if (hipMalloc((void**)&st.d, dneed) != hipSuccess) return -1;
+      st.dbytes = dneed;
+    }
+    if (hper > 0 && st.hbytes < hneed) {
+      if (st.h) (void)hipHostFree(st.h);
+      st.h = nullptr;
+      st.hbytes = 0;
+      if (hipHostMalloc((void**)&st.h, hneed, hipHostMallocPortable) != hipSuccess) return -1;
+      st.hbytes = hneed;
+    }
+  }
+  auto drain = [&](Stage& st) -> int {
+    if (hipStreamSynchronize(st.s) != hipSuccess) return -1;
+    for (auto& o : st.out) std::memcpy(o.first.first, o.first.second, o.second);
+    st.out.clear();
+    return 0;
+  };
+  int rc = 0;
+  for (long b = 0, ci = 0; b < n && rc == 0; b += chunk, ++ci) {
+    Stage& st = stg_[ci & 1];
+    if (drain(st) != 0) { rc = -1; break; }
+    const long m = std::min(chunk, n - b);
+    void* dptr[8];
+    uint8_t* dp = st.d;
+    uint8_t* hp = st.h;
+    for (int c = 0; c < ncols; ++c) {
+      Col& col = cols[c];
+      dptr[c] = dp;
+      uint8_t* user = (uint8_t*)col.user + b * col.ustride;
+      const long w = std::min(col.ustride, col.dstride);
+      if (col.in) {
+        if (col.dstride != col.ustride) (void)hipMemsetAsync(dp, 0, (size_t)(m * col.dstride), st.s);
+        const uint8_t* src = user;
+        if (!col.pinned) {
+          std::memcpy(hp, user, (size_t)(m * col.ustride));
+          src = hp;
+        }
+        if (hipMemcpy2DAsync(dp, (size_t)col.dstride, src, (size_t)col.ustride, (size_t)w, (size_t)m,
+                             hipMemcpyHostToDevice, st.s) != hipSuccess) { rc = -1; break; }
+      }
+      if (!col.pinned) hp += al256(m * col.ustride);
+      dp += al256(m * col.dstride);
+    }
+    if (rc) break;
+    if (kernel(m, dptr, st.s) != 0) { rc = -1; break; }
+    hp = st.h;
+    for (int c = 0; c < ncols; ++c) {
+      Col& col = cols[c];
+      uint8_t* user = (uint8_t*)col.user + b * col.ustride;
+      const long w = std::min(col.ustride, col.dstride);
+      if (col.out) {
+        uint8_t* dst = col.pinned ? user : hp;
+        if (hipMemcpy2DAsync(dst, (size_t)col.ustride, dptr[c], (size_t)col.dstride, (size_t)w, (size_t)m,
+                             hipMemcpyDeviceToHost, st.s) != hipSuccess) { rc = -1; break; }
+        if (!col.pinned) st.out.push_back({{user, hp}, (size_t)(m * col.ustride)});
+      }
+      if (!col.pinned) hp += al256(m * col.ustride);
+    }
+  }
+  for (auto& st : stg_)
+    if (st.s && drain(st) != 0) rc = -1;
+  return rc;
+}
+
+long HbmStore::set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
+                         long n, int32_t* status, int retries) {
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  Col cols[4] = {{keys, kstride, r16(kstride), true, false, false},
+                 {vals, vstride, r16(vstride), true, false, false},
+                 {lens, 4, 4, true, false, false},
+                 {status, 4, 4, false, true, false}};
+  const int ks = (int)r16(kstride), vs = (int)r16(vstride);
+  const spl_arena_t a = arena();
+  if (batch_run(n, cols, 4, [&](long m, void** d, hipStream_t st) {
+        return spl_arena_set(a, (const char*)d[0], ks, (const uint8_t*)d[1], vs, (const uint32_t*)d[2], m,
+                             (int32_t*)d[3], retries, nullptr, st);
+      }) != 0)
+    return -1;
+  return count_ok(status, n);
+}
+
+long HbmStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
+                         int32_t* status, int retries) {
+  std::vector<int32_t> tst;
+  std::vector<uint32_t> tln;
+  if (!status) { tst.resize((size_t)n); status = tst.data(); }
+  if (!out_lens) { tln.resize((size_t)n); out_lens = tln.data(); }
+  const int ks = (int)r16(kstride);
+  const long os = out ? r16(ostride) : 0;
+  Col cols[4] = {{keys, kstride, ks, true, false, false},
+                 {status, 4, 4, false, true, false},
+                 {out_lens, 4, 4, false, true, false},
+                 {out, ostride, os, false, true, false}};
+  const spl_arena_t a = arena();
+  if (batch_run(n, cols, out ? 4 : 3, [&](long m, void** d, hipStream_t st) {
+        return spl_arena_get(a, (const char*)d[0], ks, out ? (uint8_t*)d[3] : nullptr, out ? (int)os : 16,
+                             (uint32_t*)d[2], m, (int32_t*)d[1], retries, nullptr, st);
+      }) != 0)
+    return -1;
+  long ok = 0;
+  for (long i = 0; i < n; ++i) {
+    // a row narrower than the value: EMSGSIZE, as the per-call get into a short buffer
+    if (status[i] == 0 && out && out_lens[i] > (uint32_t)ostride) {
+      status[i] = -EMSGSIZE;
+      out_lens[i] = 0;
+    }
+    ok += status[i] == 0;
+  }
+  return ok;
+}
+
+long HbmStore::intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,
+                           int32_t* status, uint64_t* results) {
+  std::vector<int32_t> tst;
+  std::vector<uint64_t> tm;
+  if (!status) { tst.resize((size_t)n); status = tst.data(); }
+  if (!masks) { tm.assign((size_t)n, 0); masks = tm.data(); }
+  const int ks = (int)r16(kstride);
+  Col cols[5] = {{keys, kstride, ks, true, false, false},
+                 {ops, 4, 4, true, false, false},
+                 {masks, 8, 8, true, false, false},
+                 {status, 4, 4, false, true, false},
+                 {results, 8, 8, false, true, false}};
+  const spl_arena_t a = arena();
+  if (batch_run(n, cols, results ? 5 : 4, [&](long m, void** d, hipStream_t st) {
+        return spl_arena_intop(a, (const char*)d[0], ks, (const int*)d[1], (const uint64_t*)d[2], m, (int32_t*)d[3],
+                               results ? (uint64_t*)d[4] : nullptr, 64, st);
+      }) != 0)
+    return -1;
+  return count_ok(status, n);
+}
+
+long HbmStore::set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) {
+  if (geo_.stride != kSlotEmbedBytes) {
+    for (long i = 0; status && i < n; ++i) status[i] = -ENOTSUP;
+    return 0;
+  }
+  std::vector<int32_t> tst;
+  if (!status) { tst.resize((size_t)n); status = tst.data(); }
+  const int ks = (int)r16(kstride);
+  Col cols[3] = {{keys, kstride, ks, true, false, false},
+                 {vecs, (long)kEmbedBytes, (long)kEmbedBytes, true, false, false},
+                 {status, 4, 4, false, true, false}};
+  const spl_arena_t a = arena();
+  if (batch_run(n, cols, 3, [&](long m, void** d, hipStream_t st) {
+        return spl_arena_embed_set(a, (const char*)d[0], ks, (const float*)d[1], m, (int32_t*)d[2], st);
+      }) != 0)
+    return -1;
+  return count_ok(status, n);
+}
+
+}  // namespace spl
+
 extern "C" {
 
 spl::StoreBase* spl_hbm_factory(const char* name, size_t slots, size_t max_val, unsigned flags, int create, int* err) {
@@ -972,6 +1214,17 @@ uint32_t spl_hbm_ring_launches(spl_store* h) {
   auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
   return s ? s->ring_launches() : 0;
 }
+
+// Pinned, device-mapped host memory for batch arrays (splinter_ext.h spl_batch_alloc).
+void* spl_hbm_host_alloc(size_t bytes) {
+  void* p = nullptr;
+  if (hipHostMalloc(&p, bytes, hipHostMallocPortable | hipHostMallocMapped) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+void spl_hbm_host_free(void* p) { (void)hipHostFree(p); }
 
 int spl_hbm_device_count(void) {
   int n = 0;

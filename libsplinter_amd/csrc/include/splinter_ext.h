@@ -110,6 +110,28 @@ spl_store *spl_node_shard(spl_store *s, int i);
 int   spl_node_shard_of(const char *key, int nshards);
 int   spl_hbm_device_count(void);               /* libsplinter_hip.so */
 
+/* Host-array batches (batch_host.cpp): n fixed-stride NUL-padded key records (kstride <= 64), value
+ * rows of vstride / ostride bytes, per-op status 0 or -errno (EAGAIN -11, ENOENT -2, ENOSPC -28,
+ * EMSGSIZE -90, EPROTOTYPE -71, EINVAL -22, ESTALE -116).  Return: ops that succeeded (-2 on bad
+ * arguments).  hbm: stores run the batch through the device kernels (staged in chunks; arrays from
+ * spl_batch_alloc move by DMA without a staging copy); node: stores hash-partition the batch and
+ * run every shard's part concurrently on its own GPU; host stores loop over the per-call API on
+ * `threads` threads.  retries: EAGAIN retries per op (seqlock contention). */
+long  spl_set_batch(spl_store *s, const char *keys, int kstride, const uint8_t *vals, int vstride,
+                    const uint32_t *lens, long n, int32_t *status, int retries, int threads);
+long  spl_get_batch(spl_store *s, const char *keys, int kstride, uint8_t *out, int ostride, uint32_t *out_lens,
+                    long n, int32_t *status, int retries, int threads);
+long  spl_intop_batch(spl_store *s, const char *keys, int kstride, const int *ops, const uint64_t *masks, long n,
+                      int32_t *status, int threads);
+/* the same, with each op's resulting u64 value in results[i] */
+long  spl_intop_batch_ex(spl_store *s, const char *keys, int kstride, const int *ops, const uint64_t *masks, long n,
+                         int32_t *status, uint64_t *results, int threads);
+/* vecs [n][768] fp32; expect_epochs (optional): skip (-ESTALE) keys whose epoch moved (daemon write-back) */
+long  spl_set_embedding_batch(spl_store *s, const char *keys, int kstride, const float *vecs, long n,
+                              const uint64_t *expect_epochs, int32_t *status, int threads);
+void *spl_batch_alloc(size_t bytes);   /* pinned when the HBM backend is present; 64-B aligned */
+void  spl_batch_free(void *p);
+
 /* bulk helpers (host backends): key -> slot index, -1 if absent */
 long  spl_find_slot(spl_store *s, const char *key);
 uint64_t spl_hash_key(const char *key);

@@ -95,7 +95,32 @@ class StoreBase {
   virtual uint32_t shard_election(uint8_t* out_intent) = 0;
   virtual int shard_table(splinter_shard_bid_snapshot* out, size_t max) = 0;
   virtual int madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t timeout) = 0;
+
+  // Batched host-array ops (splinter_ext.h spl_*_batch; fixed-stride NUL-padded key records, value
+  // rows of vstride bytes, per-op status 0 / -errno).  A backend with a native batch path (HBM:
+  // staged through the device kernels; node: hash-partitioned over the shards concurrently)
+  // returns the number of ops that succeeded; kNoBatch makes the caller loop over the per-call API.
+  static constexpr long kNoBatch = -(1L << 62);
+  virtual long set_batch(const char*, int, const uint8_t*, int, const uint32_t*, long, int32_t*, int) {
+    return kNoBatch;
+  }
+  virtual long get_batch(const char*, int, uint8_t*, int, uint32_t*, long, int32_t*, int) { return kNoBatch; }
+  virtual long intop_batch(const char*, int, const int*, const uint64_t*, long, int32_t*, uint64_t*) {
+    return kNoBatch;
+  }
+  virtual long set_embedding_batch(const char*, int, const float*, long, int32_t*) { return kNoBatch; }
 };
+
+// The per-call loops behind spl_*_batch (batch_host.cpp), for backends without a native path and
+// for the host shards of a node store.
+long generic_set_batch(StoreBase* s, const char* keys, int kstride, const uint8_t* vals, int vstride,
+                       const uint32_t* lens, long n, int32_t* status, int retries, int threads);
+long generic_get_batch(StoreBase* s, const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens,
+                       long n, int32_t* status, int retries, int threads);
+long generic_intop_batch(StoreBase* s, const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,
+                         int32_t* status, uint64_t* results, int threads);
+long generic_set_embedding_batch(StoreBase* s, const char* keys, int kstride, const float* vecs, long n,
+                                 const uint64_t* expect_epochs, int32_t* status, int threads);
 
 // Factory entry point exported by libsplinter_hip.so for "hbm:" stores.
 typedef StoreBase* (*HbmFactory)(const char* name, size_t slots, size_t max_val,

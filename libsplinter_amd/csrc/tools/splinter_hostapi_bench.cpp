@@ -3,7 +3,12 @@
 // any store, including "hbm:NAME" stores served by the device command ring (cmd_ring.hpp).
 //
 //   splinter_hostapi_bench [--store NAME] [--threads T] [--seconds S] [--keys K]
-//                          [--value-len L] [--set-frac F] [--append-check N]
+//                          [--value-len L] [--set-frac F] [--append-check N] [--batch B]
+//
+// --batch B: the host-array batch ABI instead (splinter_ext.h spl_set_batch / spl_get_batch): K keys
+// prepopulated in batches, then for S seconds alternating set and get batches of B random keys from
+// arrays allocated with spl_batch_alloc (pinned: hbm: / node: stores DMA them); every op counts.
+// Afterwards every get of the last batch must have returned its key's value.
 //
 // Threads run a set/get mix over K prepopulated keys for S seconds; every call is timed.  One
 // JSON line: ops/s (every completed call, EAGAIN included, as splinter_stress counts), successful
@@ -35,6 +40,7 @@ struct Args {
   int value_len = 150;
   double set_frac = 0.5;
   int append_check = 0;
+  long batch = 0;
 };
 
 double pct(std::vector<float>& v, double p) {
@@ -48,6 +54,92 @@ std::string key_of(int i) {
   char b[32];
   snprintf(b, sizeof b, "hk%08d", i);
   return b;
+}
+
+// value of key i: "val:<i>|" then filler up to len bytes
+void fill_value(uint8_t* row, long i, int len) {
+  char head[32];
+  const int h = snprintf(head, sizeof head, "val:%ld|", i);
+  for (int q = 0; q < len; ++q) row[q] = q < h ? (uint8_t)head[q] : (uint8_t)('a' + (i + q) % 26);
+}
+
+int batch_main(const Args& a) {
+  using clk = std::chrono::steady_clock;
+  const int ks = 16, vs = (a.value_len + 15) / 16 * 16;
+  const long B = a.batch, K = a.keys;
+  int err = 0;
+  spl_store* st = spl_store_create(a.store.c_str(), (size_t)K * 2 + 1024, 256, SPL_CREATE_NO_EMBEDDINGS, &err);
+  if (!st) {
+    fprintf(stderr, "create %s failed: %s\n", a.store.c_str(), strerror(err));
+    return 1;
+  }
+  auto* keys = (char*)spl_batch_alloc((size_t)B * ks * 2);
+  auto* vals = (uint8_t*)spl_batch_alloc((size_t)B * vs);
+  auto* lens = (uint32_t*)spl_batch_alloc((size_t)B * 4);
+  auto* stat = (int32_t*)spl_batch_alloc((size_t)B * 4);
+  auto* out = (uint8_t*)spl_batch_alloc((size_t)B * vs);
+  auto* olen = (uint32_t*)spl_batch_alloc((size_t)B * 4);
+  std::vector<long> gid((size_t)B);
+  if (!keys || !vals || !lens || !stat || !out || !olen) { fprintf(stderr, "batch alloc failed\n"); return 1; }
+  auto key_row = [&](char* row, long i) {
+    memset(row, 0, ks);
+    snprintf(row, ks, "bk%010ld", i);
+  };
+  // prepopulate every key (values of length value_len)
+  long bad = 0;
+  for (long b = 0; b < K; b += B) {
+    const long m = std::min(B, K - b);
+    for (long j = 0; j < m; ++j) {
+      key_row(keys + j * ks, b + j);
+      fill_value(vals + j * vs, b + j, a.value_len);
+      lens[j] = (uint32_t)a.value_len;
+    }
+    const long ok = spl_set_batch(st, keys, ks, vals, vs, lens, m, stat, 64, a.threads);
+    bad += m - ok;
+  }
+  if (bad) { fprintf(stderr, "prepopulate: %ld failures\n", bad); return 1; }
+  // one set batch and one get batch of random keys, reused every round (the set rewrites values
+  // with the same content, so every get stays checkable)
+  char* gkeys = keys + B * ks;
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  for (long j = 0; j < B; ++j) {
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    const long i = (long)(x % (uint64_t)K);
+    key_row(keys + j * ks, i);
+    fill_value(vals + j * vs, i, a.value_len);
+    lens[j] = (uint32_t)a.value_len;
+    x ^= x << 13; x ^= x >> 7; x ^= x << 17;
+    gid[(size_t)j] = (long)(x % (uint64_t)K);
+    key_row(gkeys + j * ks, gid[(size_t)j]);
+  }
+  long ops = 0, okc = 0, rounds = 0;
+  const auto t0 = clk::now();
+  double el = 0;
+  do {
+    okc += spl_set_batch(st, keys, ks, vals, vs, lens, B, stat, 64, a.threads);
+    okc += spl_get_batch(st, gkeys, ks, out, vs, olen, B, stat, 64, a.threads);
+    ops += 2 * B;
+    ++rounds;
+    el = std::chrono::duration<double>(clk::now() - t0).count();
+  } while (el < a.seconds);
+  // the last get batch: every value intact
+  long wrong = 0;
+  for (long j = 0; j < B; ++j) {
+    uint8_t want[4096];
+    fill_value(want, gid[(size_t)j], a.value_len);
+    if (stat[j] != 0 || olen[j] != (uint32_t)a.value_len || memcmp(out + j * vs, want, (size_t)a.value_len) != 0)
+      ++wrong;
+  }
+  printf("{\"store\": \"%s\", \"backend\": \"%s\", \"batch\": %ld, \"rounds\": %ld, \"seconds\": %.3f, "
+         "\"ops_per_s\": %.1f, \"successful_ops_per_s\": %.1f, \"keys\": %ld, \"value_len\": %d, "
+         "\"get_check_failures\": %ld}\n",
+         a.store.c_str(), spl_store_backend(st), B, rounds, el, (double)ops / el, (double)okc / el, K, a.value_len,
+         wrong);
+  spl_batch_free(keys); spl_batch_free(vals); spl_batch_free(lens); spl_batch_free(stat); spl_batch_free(out);
+  spl_batch_free(olen);
+  spl_store_close(st);
+  spl_unlink(a.store.c_str());
+  return wrong ? 1 : 0;
 }
 
 }  // namespace
@@ -65,8 +157,10 @@ int main(int argc, char** argv) {
     else if (s == "--value-len") a.value_len = atoi(nxt());
     else if (s == "--set-frac") a.set_frac = atof(nxt());
     else if (s == "--append-check") a.append_check = atoi(nxt());
+    else if (s == "--batch") a.batch = atol(nxt());
     else { fprintf(stderr, "unknown option %s\n", s.c_str()); return 2; }
   }
+  if (a.batch > 0) return batch_main(a);
   const size_t max_val = 4096;
   if (splinter_create(a.store.c_str(), (size_t)a.keys * 2 + 1024, max_val) != 0) {
     fprintf(stderr, "create %s failed: %s\n", a.store.c_str(), strerror(errno));

@@ -447,12 +447,12 @@ def main():
 
     # N > 1: a host-sync-free software pipeline over the routed exchange (parallel/xroute.py).
     # Per step i (parity i % 2 double-buffers every exchange block and client output):
-    #   s_req : pack of batch i straight into the owners' request blocks + the count all-to-all
-    #           (waits for finish(i-2): no block is reused while anyone still reads it)
-    #   main  : embed_i, after the owner kernels of batch i-1 (no seqlock kernels beside the GEMMs)
     #   s_set : owner kernels of batch i on the 32 + 32 client streams (own ops in place, peers'
-    #           request blocks -> their response blocks), after its requests and embed_i
-    #   s_resp: the response collective + gather of batch i     (overlaps embed_{i+1})
+    #           request blocks -> their response blocks), after batch i's requests
+    #   main  : embed_i after them (no seqlock kernels beside the GEMMs), as in the local step
+    #   s_resp: the response collective + gather of batch i                 (overlaps embed_i)
+    #   s_req : pack of batch i+1 straight into the owners' request blocks + the count all-to-all
+    #           (waits for finish(i-1): no block is reused while anyone still reads it; overlaps embed_i)
     # All K steps' responses are delivered inside the timed region (device-wide sync at the end).
     xr = None
     if need_routed and n_set + n_get and kvs is not None:
@@ -469,28 +469,46 @@ def main():
                   torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")) for _ in range(2)]
         prev_exec = []
 
-    def step_routed(i):
+    requested = {}  # step -> its request event (issued ahead by the previous step of the same phase)
+
+    def _request(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
-        cur = torch.cuda.current_stream()
-        sst, gov, gln, gst = r_out[i % 2]
         with torch.cuda.stream(s_req):
             xr.request(i, SK if n_set else None, SV if n_set else None, SL if n_set else None, GK if n_get else None)
-            ev_req = s_req.record_event()
-        if embedder is not None:
-            for e in prev_exec:
-                cur.wait_event(e)
-            embedder.run()
-        ev_emb = cur.record_event()
-        prev_exec.clear()
-        s_set.wait_event(ev_req)
-        s_set.wait_event(ev_emb)
+            requested[i] = s_req.record_event()
+
+    def step_routed(i, last=False):
+        """One routed step, in the local step's order (KV phase, then the encoder), with the exchange
+        around it: the owner kernels of batch i run first, the encoder after them, and while it runs
+        the responses of batch i are gathered and batch i+1's records packed into the owners' blocks
+        (issued here unless i is the last step of its phase: no work of an uncounted step inside the
+        timed region)."""
+        cur = torch.cuda.current_stream()
+        sst, gov, gln, gst = r_out[i % 2]
+        # host submission throttle, as the local step: step i's launches are issued once embed_{i-1}
+        # has finished, so no KV dispatch waits queued beside the encoder
+        if args.throttle and throttle_ev[0] is not None:
+            throttle_ev[0].synchronize()
+        if i not in requested:
+            _request(i)
+        s_set.wait_event(requested.pop(i))
+        s_set.wait_stream(cur)
         with torch.cuda.stream(s_set):
             xr.execute(i, kvs, sst, gov, gln, gst)
-            prev_exec.append(s_set.record_event())
-        s_resp.wait_event(prev_exec[-1])
+            ev_exec = s_set.record_event()
+        if embedder is not None:
+            cur.wait_event(ev_exec)
+            embedder.run()
+            if args.throttle:
+                throttle_ev[0] = cur.record_event()
+        s_resp.wait_event(ev_exec)
         with torch.cuda.stream(s_resp):
             xr.respond(i)
             xr.finish(i, sst, gov, gln, gst)
+        if not last:
+            _request(i + 1)
+        if embedder is None:
+            cur.wait_stream(s_resp)
 
     if routed and xr is None:
         raise SystemExit("[bench] the routed step needs the native client-stream fan-out and a KV batch "
@@ -498,7 +516,7 @@ def main():
     step = step_routed if routed else step_local
 
     for i in range(args.warmup):
-        step(i)
+        step(i, last=i == args.warmup - 1) if routed else step(i)
     torch.cuda.synchronize()
     arena.reset_stats()
     if routed:
@@ -508,7 +526,7 @@ def main():
     prof(True)
     t_start = time.perf_counter()
     for i in range(args.steps):
-        step(args.warmup + i)
+        step(args.warmup + i, last=i == args.steps - 1) if routed else step(args.warmup + i)
     torch.cuda.synchronize()
     if routed:
         dist.barrier()
@@ -564,12 +582,13 @@ def main():
     # ---- N=1: the routed (N>1) step on one GPU, same streams and batches (outside the headline) ----
     routed1 = None
     if not routed and xr is not None and args.routed_steps > 0:
+        throttle_ev[0] = None
         for i in range(2):
-            step_routed(i)
+            step_routed(i, last=i == 1)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for i in range(args.routed_steps):
-            step_routed(2 + i)
+            step_routed(2 + i, last=i == args.routed_steps - 1)
         torch.cuda.synchronize()
         dtr = time.perf_counter() - t0
         routed1 = {"ops_per_s": (n_set + n_get) * args.routed_steps / dtr, "ms_per_step": dtr / args.routed_steps * 1e3}

@@ -1078,8 +1078,11 @@ long HbmStore::batch_run(long n, Col* cols, int ncols, K&& kernel) {
           std::memcpy(hp, user, (size_t)(m * col.ustride));
           src = hp;
         }
-        if (hipMemcpy2DAsync(dp, (size_t)col.dstride, src, (size_t)col.ustride, (size_t)w, (size_t)m,
-                             hipMemcpyHostToDevice, st.s) != hipSuccess) { rc = -1; break; }
+        const hipError_t e = col.dstride == col.ustride
+                                 ? hipMemcpyAsync(dp, src, (size_t)(m * col.ustride), hipMemcpyHostToDevice, st.s)
+                                 : hipMemcpy2DAsync(dp, (size_t)col.dstride, src, (size_t)col.ustride, (size_t)w,
+                                                    (size_t)m, hipMemcpyHostToDevice, st.s);
+        if (e != hipSuccess) { rc = -1; break; }
       }
       if (!col.pinned) hp += al256(m * col.ustride);
       dp += al256(m * col.dstride);
@@ -1093,8 +1096,11 @@ long HbmStore::batch_run(long n, Col* cols, int ncols, K&& kernel) {
       const long w = std::min(col.ustride, col.dstride);
       if (col.out) {
         uint8_t* dst = col.pinned ? user : hp;
-        if (hipMemcpy2DAsync(dst, (size_t)col.ustride, dptr[c], (size_t)col.dstride, (size_t)w, (size_t)m,
-                             hipMemcpyDeviceToHost, st.s) != hipSuccess) { rc = -1; break; }
+        const hipError_t e = col.dstride == col.ustride
+                                 ? hipMemcpyAsync(dst, dptr[c], (size_t)(m * col.ustride), hipMemcpyDeviceToHost, st.s)
+                                 : hipMemcpy2DAsync(dst, (size_t)col.ustride, dptr[c], (size_t)col.dstride, (size_t)w,
+                                                    (size_t)m, hipMemcpyDeviceToHost, st.s);
+        if (e != hipSuccess) { rc = -1; break; }
         if (!col.pinned) st.out.push_back({{user, hp}, (size_t)(m * col.ustride)});
       }
       if (!col.pinned) hp += al256(m * col.ustride);

@@ -79,7 +79,9 @@ def test_xr_pack_matches_reference(world, rank, capmode):
         assert torch.equal(vals[j[sel]], V[idx, :160])
     # gets: keys only
     g2, buf2, c2, l2, pos2 = _pack(K, None, None, world, rank, cap, 160)
-    assert torch.equal(c2, counts) and torch.equal(pos2 >= 0, rem)
+    assert torch.equal(c2, counts) and int((pos2 >= 0).sum()) == int(rem.sum())
+    if capmode == "auto":  # no block full: the same ops are remote (with a full one, which excess ops
+        assert torch.equal(pos2 >= 0, rem)  # overflow depends on the order of the block atomics)
 
 
 def test_xr_gather_matches_reference():

@@ -11,7 +11,7 @@
 //! side and by the `layout` test below.
 #![allow(non_camel_case_types)]
 
-use std::os::raw::{c_char, c_int, c_uint, c_ushort, c_void};
+use std::os::raw::{c_char, c_int, c_long, c_uint, c_ushort, c_void};
 
 pub const SPLINTER_MAGIC: u32 = 0x534C_4E54;
 pub const SPLINTER_VER: u32 = 4;
@@ -257,4 +257,27 @@ mod layout {
         assert_eq!(size_of::<splinter_header_snapshot_t>(), 48);
         assert_eq!(size_of::<splinter_shard_bid_snapshot>(), 40);
     }
+}
+
+/// Opaque handle of the libsplinter_amd extension API (splinter_ext.h).
+#[repr(C)]
+pub struct spl_store {
+    _private: [u8; 0],
+}
+
+// Host-array batches (splinter_ext.h spl_*_batch): fixed-stride NUL-padded key records, value rows
+// of vstride / ostride bytes, per-op status 0 / -errno; hbm: / node: stores run them on the GPUs.
+extern "C" {
+    pub fn spl_store_current() -> *mut spl_store;
+    pub fn spl_set_batch(s: *mut spl_store, keys: *const c_char, kstride: c_int, vals: *const u8, vstride: c_int,
+                         lens: *const u32, n: c_long, status: *mut i32, retries: c_int, threads: c_int) -> c_long;
+    pub fn spl_get_batch(s: *mut spl_store, keys: *const c_char, kstride: c_int, out: *mut u8, ostride: c_int,
+                         out_lens: *mut u32, n: c_long, status: *mut i32, retries: c_int, threads: c_int) -> c_long;
+    pub fn spl_intop_batch_ex(s: *mut spl_store, keys: *const c_char, kstride: c_int, ops: *const c_int,
+                              masks: *const u64, n: c_long, status: *mut i32, results: *mut u64, threads: c_int)
+                              -> c_long;
+    pub fn spl_set_embedding_batch(s: *mut spl_store, keys: *const c_char, kstride: c_int, vecs: *const f32,
+                                   n: c_long, expect_epochs: *const u64, status: *mut i32, threads: c_int) -> c_long;
+    pub fn spl_batch_alloc(bytes: usize) -> *mut c_void;
+    pub fn spl_batch_free(p: *mut c_void);
 }

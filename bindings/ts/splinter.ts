@@ -33,6 +33,16 @@ const SYMBOLS = {
   splinter_append: { parameters: ["buffer", "buffer", "usize", "buffer"], result: "i32" },
   splinter_get_header_snapshot: { parameters: ["buffer"], result: "i32" },
   spl_list_copy: { parameters: ["buffer", "usize"], result: "i64" },
+  // host-array batches (splinter_ext.h spl_*_batch) on the current store
+  spl_store_current: { parameters: [], result: "pointer" },
+  spl_set_batch: {
+    parameters: ["pointer", "buffer", "i32", "buffer", "i32", "buffer", "i64", "buffer", "i32", "i32"],
+    result: "i64",
+  },
+  spl_get_batch: {
+    parameters: ["pointer", "buffer", "i32", "buffer", "i32", "buffer", "i64", "buffer", "i32", "i32"],
+    result: "i64",
+  },
 } as const;
 
 type Lib = Record<keyof typeof SYMBOLS, (...a: unknown[]) => any>;
@@ -49,7 +59,8 @@ function loadLib(path: string): Lib {
     // bun:ffi uses the same type names for these signatures ("buffer" -> "ptr")
     // deno-lint-ignore no-explicit-any
     const { dlopen, FFIType } = require("bun:ffi") as any;
-    const map = (t: string) => (t === "buffer" ? FFIType.ptr : t === "usize" ? FFIType.u64 : (FFIType as any)[t]);
+    const map = (t: string) =>
+      t === "buffer" || t === "pointer" ? FFIType.ptr : t === "usize" ? FFIType.u64 : (FFIType as any)[t];
     const defs: Record<string, unknown> = {};
     for (const [k, v] of Object.entries(SYMBOLS)) {
       defs[k] = { args: v.parameters.map(map), returns: map(v.result) };
@@ -166,6 +177,42 @@ export class SplinterStore {
       return dec.decode(buf.subarray(0, n)).split("\0").filter((k) => k.length > 0);
     }
   }
+}
+
+/** Fixed-stride records for the batch calls: NUL-padded keys of `kstride` bytes, values of `vstride`. */
+function records(items: (string | Uint8Array)[], stride: number): Uint8Array {
+  const out = new Uint8Array(items.length * stride);
+  items.forEach((it, i) => {
+    const b = typeof it === "string" ? enc.encode(it) : it;
+    out.set(b.subarray(0, Math.min(b.length, stride)), i * stride);
+  });
+  return out;
+}
+
+/** Batched set / get through the host-array ABI (hbm: / node: stores run them on the GPUs). */
+export function setBatch(store: SplinterStore, keys: string[], values: (string | Uint8Array)[], threads = 8): Int32Array {
+  // deno-lint-ignore no-explicit-any
+  const lib = (store as any).lib as Lib;
+  const vb = values.map((v) => (typeof v === "string" ? enc.encode(v) : v));
+  const vstride = Math.max(16, Math.ceil(Math.max(1, ...vb.map((v) => v.length)) / 16) * 16);
+  const lens = new Uint32Array(vb.map((v) => v.length));
+  const status = new Int32Array(keys.length);
+  lib.spl_set_batch(lib.spl_store_current(), records(keys.map((k) => k + "\0"), 64), 64, records(vb, vstride),
+    vstride, new Uint8Array(lens.buffer), BigInt(keys.length), new Uint8Array(status.buffer), 64, threads);
+  return status;
+}
+
+export function getBatch(store: SplinterStore, keys: string[], width = 4096, threads = 8):
+  { status: Int32Array; values: (Uint8Array | null)[] } {
+  // deno-lint-ignore no-explicit-any
+  const lib = (store as any).lib as Lib;
+  const out = new Uint8Array(keys.length * width);
+  const lens = new Uint32Array(keys.length);
+  const status = new Int32Array(keys.length);
+  lib.spl_get_batch(lib.spl_store_current(), records(keys.map((k) => k + "\0"), 64), 64, out, width,
+    new Uint8Array(lens.buffer), BigInt(keys.length), new Uint8Array(status.buffer), 64, threads);
+  const values = Array.from(keys, (_, i) => (status[i] === 0 ? out.slice(i * width, i * width + lens[i]) : null));
+  return { status, values };
 }
 
 /** Polls a signal group (the reference binding's SplinterWatcher.nextSignal, 50 ms cadence). */

@@ -187,6 +187,14 @@ def _declare_core(L):
     _sig(L, "spl_madvise", c_int, S, c_u32, c_void_p, c_size_t, c_int, c_u64)
     _sig(L, "spl_find_slot", c_long, S, c_char_p)
     _sig(L, "spl_hash_key", c_u64, c_char_p)
+    # host-array batches (csrc/core/batch_host.cpp)
+    P = c_void_p
+    _sig(L, "spl_set_batch", c_long, S, P, c_int, P, c_int, P, c_long, P, c_int, c_int)
+    _sig(L, "spl_get_batch", c_long, S, P, c_int, P, c_int, P, c_long, P, c_int, c_int)
+    _sig(L, "spl_intop_batch_ex", c_long, S, P, c_int, P, P, c_long, P, P, c_int)
+    _sig(L, "spl_set_embedding_batch", c_long, S, P, c_int, P, c_long, P, P, c_int)
+    _sig(L, "spl_batch_alloc", P, c_size_t)
+    _sig(L, "spl_batch_free", None, P)
     _sig(L, "splinter_now", c_u64)
     # node stores (csrc/core/node_store.hpp)
     _sig(L, "spl_node_join", c_int, c_char_p, c_int, c_int, c_uint, c_size_t, c_size_t, c_uint)

@@ -36,7 +36,7 @@ enum : int32_t {
   kNoEnt = -2,     // -ENOENT
   kNoSpc = -28,    // -ENOSPC
   kMsgSize = -90,  // -EMSGSIZE
-  kProto = -71,    // EPROTOTYPE (host maps to errno EPROTOTYPE)
+  kProto = -91,    // -EPROTOTYPE (Linux errno 91)
   kInval = -22,
 };
 

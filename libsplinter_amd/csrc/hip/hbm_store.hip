@@ -92,7 +92,7 @@ int neg_to_errno(int32_t st) {
     case -2: return ENOENT;
     case -28: return ENOSPC;
     case -90: return EMSGSIZE;
-    case -71: return EPROTOTYPE;
+    case -91: return EPROTOTYPE;
     default: return EINVAL;
   }
 }

@@ -5,7 +5,7 @@
  * default stream).  Key batches are NUL-padded records of `kstride` bytes
  * (16, 32, 48 or 64); value batches are `vstride`-byte records (multiple of
  * 16) with explicit lengths.  Per-op status: 0 ok, -11 EAGAIN, -2 ENOENT,
- * -28 ENOSPC, -90 EMSGSIZE, -71 EPROTOTYPE, -22 EINVAL; unset returns the old
+ * -28 ENOSPC, -90 EMSGSIZE, -91 EPROTOTYPE, -22 EINVAL; unset returns the old
  * length (>= 0) on success.  Returns a hipError_t (0 = launched).
  */
 #ifndef SPLINTER_ARENA_API_H

@@ -112,7 +112,7 @@ int   spl_hbm_device_count(void);               /* libsplinter_hip.so */
 
 /* Host-array batches (batch_host.cpp): n fixed-stride NUL-padded key records (kstride <= 64), value
  * rows of vstride / ostride bytes, per-op status 0 or -errno (EAGAIN -11, ENOENT -2, ENOSPC -28,
- * EMSGSIZE -90, EPROTOTYPE -71, EINVAL -22, ESTALE -116).  Return: ops that succeeded (-2 on bad
+ * EMSGSIZE -90, EPROTOTYPE -91, EINVAL -22, ESTALE -116).  Return: ops that succeeded (-2 on bad
  * arguments).  hbm: stores run the batch through the device kernels (staged in chunks; arrays from
  * spl_batch_alloc move by DMA without a staging copy); node: stores hash-partition the batch and
  * run every shard's part concurrently on its own GPU; host stores loop over the per-call API on

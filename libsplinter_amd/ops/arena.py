@@ -8,7 +8,7 @@ graphs and ``torch.distributed`` collectives.
 Key batches are uint8 tensors ``[n, kstride]`` (NUL padded, kstride in
 {16,32,48,64}); value batches are uint8 ``[n, vstride]`` plus int32 lengths.
 Per-op status codes: 0 ok, -11 EAGAIN, -2 ENOENT, -28 ENOSPC, -90 EMSGSIZE,
--71 EPROTOTYPE, -22 EINVAL.
+-91 EPROTOTYPE, -22 EINVAL.
 """
 from __future__ import annotations
 
@@ -22,7 +22,7 @@ from ..utils.tracing import trace_range
 from .. import _native as N
 from ..store import Store
 
-OK, EAGAIN, ENOENT, ENOSPC, EMSGSIZE, EPROTOTYPE, EINVAL = 0, -11, -2, -28, -90, -71, -22
+OK, EAGAIN, ENOENT, ENOSPC, EMSGSIZE, EPROTOTYPE, EINVAL = 0, -11, -2, -28, -90, -91, -22
 META = {"set_label": 0, "unset_label": 1, "bump": 2, "epoch": 3, "watch": 4, "unwatch": 5, "pulse": 6,
         "system": 7, "retrain": 8, "type": 9, "ctime": 10, "atime": 11, "find": 12}
 SCAN_LIST, SCAN_LABELS, SCAN_EMBEDDED, SCAN_OCCUPIED, SCAN_ODD = 0, 1, 2, 3, 4

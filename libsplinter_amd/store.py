@@ -428,6 +428,87 @@ class Store:
         if self._L.spl_madvise(self._h, shard_id, None, 0, advice, timeout) != 0:
             _raise("madvise")
 
+    # ------------------------------------------------------------- batches --
+    # The host-array batch ABI (splinter_ext.h spl_*_batch): numpy arrays of fixed-stride NUL-padded
+    # key records in, per-op status (0 / -errno) out.  hbm: stores run them through the device
+    # kernels, node: stores over every shard concurrently, host stores on `threads` threads.
+    @staticmethod
+    def _keyrows(keys, kstride: int = 0) -> np.ndarray:
+        if isinstance(keys, np.ndarray) and keys.dtype == np.uint8 and keys.ndim == 2:
+            return np.ascontiguousarray(keys)
+        bs = [_k(k) for k in keys]
+        w = kstride or min(64, (max((len(b) for b in bs), default=1) + 1 + 15) // 16 * 16)
+        out = np.zeros((len(bs), w), dtype=np.uint8)
+        for i, b in enumerate(bs):
+            b = b[: min(63, w - 1)]
+            out[i, : len(b)] = np.frombuffer(b, dtype=np.uint8)
+        return out
+
+    def set_batch(self, keys, values, lens=None, retries: int = 64, threads: int = 8) -> np.ndarray:
+        """keys: [n, kstride] uint8 records or a list of str/bytes; values: [n, vstride] uint8 rows
+        (with lens) or a list of bytes.  -> int32 status [n]."""
+        K = self._keyrows(keys)
+        if isinstance(values, np.ndarray) and values.dtype == np.uint8 and values.ndim == 2:
+            V = np.ascontiguousarray(values)
+            L = np.ascontiguousarray(lens, dtype=np.uint32)
+        else:
+            vs = [v.encode() if isinstance(v, str) else bytes(v) for v in values]
+            w = max(16, (max((len(v) for v in vs), default=1) + 15) // 16 * 16)
+            V = np.zeros((len(vs), w), dtype=np.uint8)
+            L = np.zeros(len(vs), dtype=np.uint32)
+            for i, v in enumerate(vs):
+                V[i, : len(v)] = np.frombuffer(v, dtype=np.uint8)
+                L[i] = len(v)
+        n = K.shape[0]
+        assert V.shape[0] == n and L.shape[0] == n
+        st = np.zeros(n, dtype=np.int32)
+        r = self._L.spl_set_batch(self._h, K.ctypes.data, K.shape[1], V.ctypes.data, V.shape[1], L.ctypes.data, n,
+                                  st.ctypes.data, retries, threads)
+        if r < 0:
+            _raise("set_batch")
+        return st
+
+    def get_batch(self, keys, width: int = 0, retries: int = 64, threads: int = 8):
+        """-> (status int32 [n], values uint8 [n, width], lens uint32 [n]); width defaults to the
+        store's max value size (a longer value: status -EMSGSIZE)."""
+        K = self._keyrows(keys)
+        n = K.shape[0]
+        w = width or self.max_val
+        out = np.zeros((n, w), dtype=np.uint8)
+        ln = np.zeros(n, dtype=np.uint32)
+        st = np.zeros(n, dtype=np.int32)
+        r = self._L.spl_get_batch(self._h, K.ctypes.data, K.shape[1], out.ctypes.data, w, ln.ctypes.data, n,
+                                  st.ctypes.data, retries, threads)
+        if r < 0:
+            _raise("get_batch")
+        return st, out, ln
+
+    def integer_op_batch(self, keys, ops, masks=None, threads: int = 8):
+        """-> (status int32 [n], resulting u64 values [n])."""
+        K = self._keyrows(keys)
+        n = K.shape[0]
+        O = np.ascontiguousarray(ops, dtype=np.int32)
+        M = np.ascontiguousarray(masks if masks is not None else np.zeros(n), dtype=np.uint64)
+        st = np.zeros(n, dtype=np.int32)
+        res = np.zeros(n, dtype=np.uint64)
+        r = self._L.spl_intop_batch_ex(self._h, K.ctypes.data, K.shape[1], O.ctypes.data, M.ctypes.data, n,
+                                       st.ctypes.data, res.ctypes.data, threads)
+        if r < 0:
+            _raise("integer_op_batch")
+        return st, res
+
+    def set_embedding_batch(self, keys, vecs, threads: int = 8) -> np.ndarray:
+        K = self._keyrows(keys)
+        V = np.ascontiguousarray(vecs, dtype=np.float32)
+        n = K.shape[0]
+        assert V.shape == (n, 768)
+        st = np.zeros(n, dtype=np.int32)
+        r = self._L.spl_set_embedding_batch(self._h, K.ctypes.data, K.shape[1], V.ctypes.data, n, None,
+                                            st.ctypes.data, threads)
+        if r < 0:
+            _raise("set_embedding_batch")
+        return st
+
     # ---------------------------------------------------------------- misc --
     def find_slot(self, key) -> int:
         return self._L.spl_find_slot(self._h, _k(key))

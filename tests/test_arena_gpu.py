@@ -100,7 +100,7 @@ def test_integer_ops_and_meta(arena):
     V2, L2 = pack_values([b"abc"], 16)
     arena.set(K2, V2, L2)
     st, _ = arena.integer_op(K2, torch.tensor([4], dtype=torch.int32, device="cuda"))
-    assert st.item() == -71
+    assert st.item() == -91
 
 
 def test_embeddings_batch(arena):

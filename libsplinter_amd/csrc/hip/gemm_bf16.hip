@@ -105,11 +105,6 @@ struct EpiArgs {
   const uint16_t* lng;   // [N] LN gamma / beta of res (RES_LN_STATS)
   const uint16_t* lnb;
   float2* part;          // [M][N/128] (mean, M2) of out's rows per 128 columns (RES_*STATS)
-  // stream-K hand-off of split tiles (k_gemm_p<.., SK>): slot s = fp32 partial of the tile shared by
-  // blocks (in remapped order) s and s+1, published with flag[s] = gen
-  float4* skws;
-  uint32_t* skflag;
-  uint32_t skgen;
 };
 
 constexpr bool is_fold(int m) { return m == NOMIC_EPI_ROPE_FOLD || m == NOMIC_EPI_SWIGLU_FOLD; }
@@ -912,403 +907,23 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
   }
 }
 
-// ===========================================================================
-// Persistent 256x256 kernel with a REGISTER epilogue (variant 512, "p").
-//
-// One block per CU walks its tiles (blockIdx, +grid, ...; each through the
-// same XCD/L2-band remap as the launch-per-tile kernels) as ONE stream of
-// K-steps: the LDS-DMA stages of the next tile's first K-steps are issued
-// during the current tile's last phases, so a tile change costs no pipeline
-// refill.  The MFMA operands are swapped (W fragment as the A operand), so a
-// lane's accumulator holds C[m][n .. n+3] (four consecutive output columns of
-// one row) and the epilogue stores 8-B (16-B for fp32) chunks straight from
-// registers: no LDS round trip, no barrier, and the LDS buffers can keep the
-// next tile's stages in flight.  The epilogue's global ops are younger than
-// those stages, so the counted vmcnt waits of the next phases stay correct
-// (vmcnt retires in issue order: MI355X_MICROARCH.md, s_waitcnt).
-//
-// Epilogue layouts need pairs in one lane: SWIGLU weights are packed
-// [up16 | gate16] per 16 outputs (models/nomic.py pack_upgate) and the QKV
-// rows of each 64-wide head as [d0-15 | d32-47 | d16-31 | d48-63]
-// (pack_qkv), so x1 = acc[..][j=0] and x2 = acc[..][j=1] of the same lane.
-// ===========================================================================
-__device__ __forceinline__ uint2 pack4(const float* v) {
-  return make_uint2(pk2(v[0], v[1]), pk2(v[2], v[3]));
-}
-
-// AS: LDS-DMA from inline asm (glds_asm.hpp: counted lgkmcnt before the MFMA groups)
-template <int MODE, bool PERSIST, bool SK = false, int ILV = 0, bool AS = false>
-__global__ __launch_bounds__(kThreads2, 1) void k_gemm_p(const uint16_t* __restrict__ A, long lda,
-                                                         const uint16_t* __restrict__ W, long ldw, int K,
-                                                         int mtiles, int ntiles, EpiArgs ep) {
-  extern __shared__ __attribute__((aligned(16))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wr = wave >> 2, wn = wave & 3;
-  const int nb = mtiles * ntiles, G = gridDim.x;
-  const int nk = K / BK;  // >= 2 (launcher): a lookahead of two K-steps spans at most one tile change
-  // Stream-K (SK) for tile counts that do not divide over the G blocks: nb = q*G + r with G = p*r.
-  // Every block runs q whole tiles (ids v, v+G, ...) and then 1/p of one of the r remaining
-  // tiles (k-range part*nk/p ..), so all blocks carry the same q*nk + nk/p K-steps and none idles
-  // through a last partial wave of tiles.  v is the block's position in XCD order (blocks b, b+8,
-  // ... run on one XCD), so the p parts of a split tile run on one XCD.  The parts end their
-  // blocks' streams together: parts 1..p-1 store their fp32 partials, part 0 adds them and runs
-  // the epilogue -- all after the K loop, with nothing else live.
-  int my_tiles, total, k_first = 0, v = 0, q = 0, parts = 1;
-  if constexpr (SK) {
-    const int b = (int)blockIdx.x, x = b & 7, qq = G >> 3, rr = G & 7;
-    v = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + (b >> 3);
-    q = nb / G;
-    parts = G / (nb - q * G);
-    k_first = (v % parts) * (nk / parts);
-    my_tiles = q + 1;
-    total = q * nk + nk / parts;
-  } else {
-    my_tiles = PERSIST ? (nb - (int)blockIdx.x + G - 1) / G : 1;
-    total = my_tiles * nk;
-  }
-  if (my_tiles <= 0) return;
-
-  const int srow = lane >> 3, schunk = ((lane & 7) ^ srow) * 8;
-  // per-lane DMA source offsets (elements, 32-bit as in k_gemm256) of the current tile (C) and the
-  // next one (X): half h, instruction i -> row h*128 + (i*8 + wave)*8 + srow
-  uint32_t offAc[2][2], offBc[2][2], offAx[2][2], offBx[2][2];
-  long m0c = 0, n0c = 0;
-  auto tile_offsets = [&](int ti, uint32_t (&oa)[2][2], uint32_t (&ob)[2][2], long& m0, long& n0) {
-    int mt, nt;
-    if constexpr (SK) {
-      const int id = ti < q ? ti * G + v : q * G + v / parts;
-      mt = id / ntiles;
-      nt = id - mt * ntiles;
-    } else {
-      remap_tile((int)blockIdx.x + ti * G, nb, ntiles, ep.gn, mt, nt);
-    }
-    m0 = (long)mt * 256;
-    n0 = (long)nt * 256;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int r = h * 128 + (i * 8 + wave) * 8 + srow;
-        const long gr = (m0 + r < ep.M) ? m0 + r : ep.M - 1;  // clamp: tail rows re-read row M-1, never stored
-        oa[h][i] = (uint32_t)(gr * lda + schunk);
-        ob[h][i] = (uint32_t)((n0 + r) * ldw + schunk);
-      }
-  };
-  tile_offsets(0, offAc, offBc, m0c, n0c);
-  long m0x = m0c, n0x = n0c;
-  if (my_tiles > 1) tile_offsets(1, offAx, offBx, m0x, n0x);
-  else {
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) { offAx[h][i] = offAc[h][i]; offBx[h][i] = offBc[h][i]; }
-  }
-  int ti = 0, kt = 0;
-
-  // stage half-tile `which` (0 A0, 1 A1, 2 B0, 3 B1) of stream step g into buffer buf
-  auto stage_one = [&](int which, int g, int buf, int i) {
-    const bool nx = g >= (ti + 1) * nk;
-    const int tl = ti + (nx ? 1 : 0);
-    const int k0 = (g - tl * nk + (SK && tl == q ? k_first : 0)) * BK;
-    const uint16_t* base = (which < 2 ? A : W) + k0;
-    char* dst = smem + buf * kBufBytes + which * kHalfBytes;
-    const int h = which & 1;
-    const uint32_t off = which < 2 ? (nx ? offAx[h][i] : offAc[h][i]) : (nx ? offBx[h][i] : offBc[h][i]);
-    if constexpr (AS)
-      spl::glds16_asm(base + off, dst + (i * 8 + wave) * 1024);
-    else
-      __builtin_amdgcn_global_load_lds((gbl_void*)(base + off), (lds_void*)(dst + (i * 8 + wave) * 1024), 16, 0, 0);
-  };
-  auto stage = [&](int which, int g, int buf) {
-    stage_one(which, g, buf, 0);
-    stage_one(which, g, buf, 1);
-  };
-
-  const int frow = (lane & 15) * 128;
-  const int fsw0 = ((0 * 4 + (lane >> 4)) ^ (lane & 7)) << 4;
-  const int fsw1 = ((1 * 4 + (lane >> 4)) ^ (lane & 7)) << 4;
-  const int fq = lane >> 4, fr = lane & 15;
-
-  f32x4 acc[2][2][4][2];
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  // prologue, in the steady-state issue order: A0 B0 B1 A1 (t=0), A0 B0 B1 (t=1)
-  stage(0, 0, 0); stage(2, 0, 0); stage(3, 0, 0); stage(1, 0, 0);
-  if (total > 1) { stage(0, 1, 1); stage(2, 1, 1); stage(3, 1, 1); }
-
-  auto epilogue = [&]() {
-#pragma unroll
-    for (int qm = 0; qm < 2; ++qm)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const long m = m0c + qm * 128 + wr * 64 + i * 16 + fr;
-        if (m < ep.M) {
-#pragma unroll
-          for (int qn = 0; qn < 2; ++qn) {
-            const long nb0 = n0c + qn * 128 + wn * 32;  // this wave's 32-column group
-            if constexpr (MODE == NOMIC_EPI_STORE || MODE == NOMIC_EPI_RESIDUAL) {
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                const long n = nb0 + j * 16 + fq * 4;
-                float v[4] = {acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
-                              acc[qm][qn][i][j][3]};
-                if constexpr (MODE == NOMIC_EPI_RESIDUAL) {
-                  const uint2 rr = *(const uint2*)(ep.res + m * ep.ldr + n);
-                  v[0] += bf2f((uint16_t)(rr.x & 0xffff));
-                  v[1] += bf2f((uint16_t)(rr.x >> 16));
-                  v[2] += bf2f((uint16_t)(rr.y & 0xffff));
-                  v[3] += bf2f((uint16_t)(rr.y >> 16));
-                }
-                *(uint2*)(ep.out + m * ep.ldo + n) = pack4(v);
-              }
-            } else if constexpr (MODE == NOMIC_EPI_F32) {
-#pragma unroll
-              for (int j = 0; j < 2; ++j) {
-                const long n = nb0 + j * 16 + fq * 4;
-                *(float4*)((float*)ep.out + m * ep.ldo + n) =
-                    make_float4(acc[qm][qn][i][j][0], acc[qm][qn][i][j][1], acc[qm][qn][i][j][2],
-                                acc[qm][qn][i][j][3]);
-              }
-            } else if constexpr (MODE == NOMIC_EPI_SWIGLU) {
-              float o[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) o[e] = swiglu(acc[qm][qn][i][0][e], acc[qm][qn][i][1][e]);
-              *(uint2*)(ep.out + m * ep.ldo + nb0 / 2 + fq * 4) = pack4(o);
-            } else if constexpr (MODE == NOMIC_EPI_ROPE) {
-              const long head0 = nb0 & ~63L;
-              const int d = (int)(nb0 & 32) / 2 + fq * 4;  // packed half 0: d 0-15, half 1: d 16-31
-              float x1[4], x2[4];
-#pragma unroll
-              for (int e = 0; e < 4; ++e) {
-                x1[e] = acc[qm][qn][i][0][e];
-                x2[e] = acc[qm][qn][i][1][e];
-              }
-              if (head0 < ep.rope_cols) {
-                const float* cs = ep.rope + (long)ep.pos[m] * 64 + d * 2;
-#pragma unroll
-                for (int e = 0; e < 4; ++e) {
-                  const float c = cs[2 * e], s = cs[2 * e + 1];
-                  const float a = x1[e], b = x2[e];
-                  x1[e] = a * c - b * s;
-                  x2[e] = b * c + a * s;
-                }
-              }
-              *(uint2*)(ep.out + m * ep.ldo + head0 + d) = pack4(x1);
-              *(uint2*)(ep.out + m * ep.ldo + head0 + 32 + d) = pack4(x2);
-            }
-          }
-        }
-      }
-  };
-
-  bf16x8 af[4][2], b0[2][2], b1[2][2];
-  int relax = 0;
-  // as k_gemm256's: one quadrant's 16 MFMAs with the phase's stage before (ILV 0) or between them;
-  // swapped operands (W fragment as the A operand)
-  auto mma_phase = [&](f32x4 (&ac)[4][2], bf16x8 (&bf)[2][2], int which, int sg, int sbuf, bool go) {
-    if (ILV == 0 && go) stage(which, sg, sbuf);
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        if constexpr (ILV > 0) {
-          if (go && kk * 4 + i == ILV) stage_one(which, sg, sbuf, 0);
-          if (go && kk * 4 + i == ILV + 4) stage_one(which, sg, sbuf, 1);
-        }
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          ac[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bf[j][kk], af[i][kk], ac[i][j], 0, 0, 0);
-        if constexpr (ILV > 0) __builtin_amdgcn_sched_barrier(0);
-      }
-    __builtin_amdgcn_s_setprio(0);
-  };
-  for (int g = 0; g < total; ++g) {
-    const int buf = g & 1;
-    const char* hA0 = smem + buf * kBufBytes;
-    const char* hA1 = hA0 + kHalfBytes;
-    const char* hB0 = hA0 + 2 * kHalfBytes;
-    const char* hB1 = hA0 + 3 * kHalfBytes;
-    const bool n1 = g + 1 < total, n2 = g + 2 < total;
-    // ---- phase 1: quadrant (0,0)
-    // relax: the register epilogue's global stores of the previous tile (S per wave, younger
-    // than the stages these two phases wait for) may stay in flight: vmcnt retires in issue order,
-    // so the counts grow by S instead of draining the stores before the new tile's first MFMAs
-    wait_vm((n1 ? 10 : 4) + relax);
-    raw_barrier();
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      b0[j][0] = *(const bf16x8*)(hB0 + (wn * 32 + j * 16) * 128 + frow + fsw0);
-      b0[j][1] = *(const bf16x8*)(hB0 + (wn * 32 + j * 16) * 128 + frow + fsw1);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      af[i][0] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw0);
-      af[i][1] = *(const bf16x8*)(hA0 + (wr * 64 + i * 16) * 128 + frow + fsw1);
-    }
-    mma_phase(acc[0][0], b0, 1, g + 1, buf ^ 1, n1);
-    // ---- phase 2: quadrant (0,1)
-    wait_vm((n1 ? 10 : 2) + relax);
-    relax = 0;
-    raw_barrier();
-#pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      b1[j][0] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw0);
-      b1[j][1] = *(const bf16x8*)(hB1 + (wn * 32 + j * 16) * 128 + frow + fsw1);
-    }
-    mma_phase(acc[0][1], b1, 0, g + 2, buf, n2);
-    // ---- phase 3: quadrant (1,0)
-    wait_vm(n2 ? 10 : (n1 ? 8 : 0));
-    raw_barrier();
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      af[i][0] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw0);
-      af[i][1] = *(const bf16x8*)(hA1 + (wr * 64 + i * 16) * 128 + frow + fsw1);
-    }
-    mma_phase(acc[1][0], b0, 2, g + 2, buf, n2);
-    // ---- phase 4: quadrant (1,1), registers only (B1's last read was phase 2: a barrier ago)
-    mma_phase(acc[1][1], b1, 3, g + 2, buf, n2);
-
-    if (++kt < nk) continue;
-    // ---- tile done: register epilogue (lane: rows m, 4 consecutive columns per fragment) --------
-    epilogue();
-    // a full tile's SwiGLU epilogue issued exactly 16 store instructions per wave (2 x 4 x 2)
-    if constexpr (MODE == NOMIC_EPI_SWIGLU && !SK) relax = (m0c + 256 <= ep.M && n2) ? 16 : 0;
-#pragma unroll
-    for (int a = 0; a < 2; ++a)
-#pragma unroll
-      for (int b = 0; b < 2; ++b)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j) acc[a][b][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    kt = 0;
-    ++ti;
-    m0c = m0x;
-    n0c = n0x;
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int i = 0; i < 2; ++i) { offAc[h][i] = offAx[h][i]; offBc[h][i] = offBx[h][i]; }
-    if (ti + 1 < my_tiles) tile_offsets(ti + 1, offAx, offBx, m0x, n0x);
-  }
-  if constexpr (SK) {
-    // the split tile: parts 1..p-1 hand over, part 0 collects and writes
-    const int part = v % parts;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (part != 0) {
-      // a thread's 32 float4 are contiguous: one address + immediate offsets
-      float4* ws = ep.skws + (size_t)v * (256 * 256 / 4) + tid * 32;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const f32x4 c = acc[a][b][i][j];
-              ws[((a * 2 + b) * 4 + i) * 2 + j] = make_float4(c[0], c[1], c[2], c[3]);
-            }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {  // agent-scope release, then the flag (cdna guide §6 Guideline 16)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(ep.skflag + v, ep.skgen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
-    if (tid == 0) {
-      for (int o = 1; o < parts; ++o)
-        while (__hip_atomic_load(ep.skflag + v + o, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != ep.skgen)
-          __builtin_amdgcn_s_sleep(2);
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    for (int o = 1; o < parts; ++o) {
-      const float4* ws = ep.skws + (size_t)(v + o) * (256 * 256 / 4) + tid * 32;
-#pragma unroll
-      for (int a = 0; a < 2; ++a)
-#pragma unroll
-        for (int b = 0; b < 2; ++b)
-#pragma unroll
-          for (int i = 0; i < 4; ++i)
-#pragma unroll
-            for (int j = 0; j < 2; ++j) {
-              const float4 pp = ws[((a * 2 + b) * 4 + i) * 2 + j];
-              acc[a][b][i][j] += f32x4{pp.x, pp.y, pp.z, pp.w};
-            }
-    }
-    epilogue();
-  }
-}
-
 int g_num_cus = 256;  // MI355X: 256 CUs in 8 XCDs; refreshed from the device on first use
-
-// DMA interleave of the 256^2 kernels (k_gemm256 / k_gemm_p ILV): NOMIC_GEMM_ILV 0, 1 or 2
-int g_ilv = -1;
-int gemm_ilv() {
-  if (g_ilv < 0) {
-    const char* e = getenv("NOMIC_GEMM_ILV");
-    g_ilv = e && *e ? atoi(e) : 0;
-    if (g_ilv < 0 || g_ilv > 2) g_ilv = 0;
-  }
-  return g_ilv;
-}
 
 template <typename F>
 void allow_lds(F* f, int bytes) {
   (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
 }
 
-// register SwiGLU epilogue of the launch-per-tile 256^2 kernel (k_gemm256 EPI 1): NOMIC_SWIGLU_REG 1 / 0
-int g_swiglu_reg = -1;
-bool swiglu_reg_epi() {
-  if (g_swiglu_reg < 0) {
-    const char* e = getenv("NOMIC_SWIGLU_REG");
-    g_swiglu_reg = e && *e ? (atoi(e) != 0) : 0;
-  }
-  return g_swiglu_reg != 0;
-}
-
-// main loop of the launch-per-tile 256^2 kernel (NOMIC_GEMM_PP): 2 = peeled lockstep with asm LDS-DMA
-// (default), 1 = staggered ping-pong, 0 = the round-2 lockstep loop
-int g_pp = -1;
-int gemm_pp() {
-  if (g_pp < 0) {
-    const char* e = getenv("NOMIC_GEMM_PP");
-    // default 2 (peeled lockstep loop, asm LDS-DMA): SwiGLU 296.5 -> 285.2 us, embed 9.35 -> 9.20 ms
-    // (profiles/r3_gemm_asm_dma.md)
-    g_pp = e && *e ? atoi(e) : 2;
-    if (g_pp < 0 || g_pp > 2) g_pp = 2;
-  }
-  return g_pp;
-}
-
-// asm LDS-DMA in the 128^2 kernel (k_gemm_nt AS): NOMIC_GEMM_AS128 1 / 0
-int g_as128 = -1;
-int gemm_as128() {
-  if (g_as128 < 0) {
-    const char* e = getenv("NOMIC_GEMM_AS128");
-    g_as128 = e && *e ? (atoi(e) != 0) : 0;
-  }
-  return g_as128;
-}
-
+// Kernel choice (NOMIC_GEMM): 0 = auto, 128 = the 128^2 kernel, 256 = the 256^2 kernel.  The
+// persistent / stream-K 256^2 kernel (512-515), the DMA-interleave (ILV), ping-pong (PP), asm-DMA
+// 128^2 (AS128) and register-SwiGLU-epilogue knobs measured slower or equal and are gone; their A/B
+// history is in profiles/r1_gemm_*.jsonl .. r3_gemm_*.
 int g_variant = -1;
 int gemm_variant() {
   if (g_variant < 0) {
     const char* e = getenv("NOMIC_GEMM");
-    g_variant = e ? atoi(e) : 0;  // 0 = auto
+    const int v = e ? atoi(e) : 0;
+    g_variant = v == 128 || v == 256 ? v : 0;
   }
   return g_variant;
 }
@@ -1327,161 +942,37 @@ int band_width(int ntiles, int cap) {
   return 1;
 }
 
-// stream-K hand-off buffers, one set per stream (two streams' GEMMs in flight at once must not
-// share slots): cus slots of one 256x256 fp32 tile + flags; flags are compared with a per-launch
-// generation, so they are never reset
-struct SkWorkspace {
-  float4* ws = nullptr;
-  uint32_t* flag = nullptr;
-  uint32_t gen = 0;
-};
-SkWorkspace* sk_workspace(hipStream_t s, int cus) {
-  static std::mutex mu;
-  static std::map<hipStream_t, SkWorkspace> table;
-  std::lock_guard<std::mutex> g(mu);
-  auto it = table.find(s);
-  if (it != table.end()) return &it->second;
-  SkWorkspace w;
-  if (hipMalloc((void**)&w.ws, (size_t)cus * 256 * 256 * sizeof(float)) != hipSuccess) return nullptr;
-  if (hipMalloc((void**)&w.flag, (size_t)cus * sizeof(uint32_t)) != hipSuccess ||
-      hipMemset(w.flag, 0, (size_t)cus * sizeof(uint32_t)) != hipSuccess) {
-    (void)hipFree(w.ws);
-    return nullptr;
-  }
-  return &(table[s] = w);
-}
-
 template <int MODE>
 int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int N, int K, EpiArgs ep,
            hipStream_t s) {
   if (K % BK || N % BN || M <= 0) return (int)hipErrorInvalidValue;
   const long mpad = (M + 255) / 256 * 256;
-  // the 256^2 kernel runs 1 block/CU with a serial prologue/epilogue per tile: it wins only when
-  // there are several waves of tiles (measured, profiles/r1_gemm_ab.jsonl); small grids use 128^2
   const bool fits = N % 256 == 0 && mpad * lda < (1L << 31) && (long)N * ldw < (1L << 31);
   const int var = gemm_variant();
-  // auto: the persistent register-epilogue kernel when there are several waves of 256^2 tiles
-  // (measured per shape: profiles/r1_gemm_persistent_ab.jsonl); fewer tiles: the 128^2 kernel
-  const bool many = (mpad / 256) * (N / 256) >= 2048;
-  // the statistics epilogue exists in the 128^2 kernel only (its 16-lane row groups); the 256^2
-  // launch-per-tile kernel has the plain epilogues only
-  constexpr bool p_ok = MODE <= NOMIC_EPI_F32;
+  // the 256^2 kernel runs 1 block/CU with a serial prologue / epilogue per tile: it wins once there
+  // are several waves of tiles.  From 1024 tiles: the qkv projection at 32768 tokens (1152 tiles)
+  // measured 137.4 us on it against 144.5 us on the 128^2 kernel (round-3 trace); the SwiGLU GEMM
+  // has 3072.  The statistics epilogues exist in the 128^2 kernel only.
   constexpr bool k256_ok = MODE <= NOMIC_EPI_F32;
-  static const int cus = [] {
-    int d = 0, n = 0;
-    if (hipGetDevice(&d) == hipSuccess &&
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) == hipSuccess && n > 0)
-      g_num_cus = n;
-    return g_num_cus;
-  }();
-  const int nk = K / BK;
   const long tiles256 = fits ? (mpad / 256) * (N / 256) : 0;
-  // stream-K persistent kernel when the 256^2 tiles do not divide evenly over the CUs (T = 32768:
-  // N = 768 -> 384 tiles = 256 + 128, N = 2304 -> 1152 = 4 x 256 + 128): the r leftover tiles are
-  // cut into p = cus / r K-ranges, one per block
-  const long rem = tiles256 % cus;
-  const long sk_parts = rem ? cus / rem : 0;
-  const bool sk_ok = p_ok && fits && nk >= 2 && rem != 0 && cus % rem == 0 && sk_parts <= 8 && nk % sk_parts == 0;
-  if (sk_ok && var == 514) {
-    if constexpr (p_ok) {
-      static bool attr_sk = [] {
-        (void)hipFuncSetAttribute((const void*)k_gemm_p<MODE, true, true>,
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 2 * kBufBytes);
-        return true;
-      }();
-      (void)attr_sk;
-      SkWorkspace* w = sk_workspace(s, cus);
-      if (!w) return (int)hipErrorOutOfMemory;
-      ep.skws = w->ws;
-      ep.skflag = w->flag;
-      ep.skgen = ++w->gen;
-      hipLaunchKernelGGL((k_gemm_p<MODE, true, true>), dim3(cus), dim3(kThreads2), 2 * kBufBytes, s, A, lda, W, ldw, K,
-                         (int)(mpad / 256), N / 256, ep);
-    }
-    return (int)hipGetLastError();
-  }
-  // auto no longer takes the persistent kernel: on the encoder's SwiGLU shape (3072 tiles) the
-  // launch-per-tile k_gemm256 measured 1064 TFLOP/s against 1015 (1046 with ILV 2) for k_gemm_p
-  // (profiles/r3_gemm_ilv_ab.jsonl); NOMIC_GEMM=512 keeps it selectable
-  if (p_ok && fits && K >= 2 * BK && (var == 512 || var == 513 || var == 515)) {
-    static bool attr_p = [] {
-      allow_lds(k_gemm_p<MODE, true, false, 0, true>, 2 * kBufBytes);
-      allow_lds(k_gemm_p<MODE, true>, 2 * kBufBytes);
-      allow_lds(k_gemm_p<MODE, true, false, 1>, 2 * kBufBytes);
-      allow_lds(k_gemm_p<MODE, true, false, 2>, 2 * kBufBytes);
-      allow_lds(k_gemm_p<MODE, false>, 2 * kBufBytes);
-      return true;
-    }();
-    (void)attr_p;
-    const int mtiles = (int)(mpad / 256), ntiles = N / 256;
-    ep.gn = band_width(ntiles, 4);
-    const int tiles = mtiles * ntiles;
-    if constexpr (p_ok) {
-      const dim3 g(tiles < cus ? tiles : cus), b(kThreads2);
-      if (var == 513)
-        hipLaunchKernelGGL((k_gemm_p<MODE, false>), dim3(tiles), b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
-                           ep);
-      else if (var == 515)  // persistent, asm LDS-DMA
-        hipLaunchKernelGGL((k_gemm_p<MODE, true, false, 0, true>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles,
-                           ntiles, ep);
-      else if (gemm_ilv() == 1)
-        hipLaunchKernelGGL((k_gemm_p<MODE, true, false, 1>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
-                           ep);
-      else if (gemm_ilv() == 2)
-        hipLaunchKernelGGL((k_gemm_p<MODE, true, false, 2>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles,
-                           ep);
-      else
-        hipLaunchKernelGGL((k_gemm_p<MODE, true>), g, b, 2 * kBufBytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-    }
-    return (int)hipGetLastError();
-  }
-  if (k256_ok && fits && (var == 256 || (var == 0 && (mpad / 256) * (N / 256) >= 2048))) {
+  if (k256_ok && fits && (var == 256 || (var == 0 && tiles256 >= 1024))) {
     static bool attr = [] {
-      allow_lds(k_gemm256<MODE>, kLds2Bytes);
-      allow_lds(k_gemm256<MODE, 1>, kLds2Bytes);
-      allow_lds(k_gemm256<MODE, 2>, kLds2Bytes);
-      allow_lds(k_gemm256<MODE, 0, 0, 1>, kLds2Bytes);
       allow_lds(k_gemm256<MODE, 0, 0, 2>, kLds2Bytes);
-      if constexpr (MODE == NOMIC_EPI_SWIGLU) {
-        allow_lds(k_gemm256<MODE, 0, 1>, kLds2Bytes);
-        allow_lds(k_gemm256<MODE, 0, 1, 1>, kLds2Bytes);
-        allow_lds(k_gemm256<MODE, 0, 1, 2>, kLds2Bytes);
-      }
       return true;
     }();
     (void)attr;
     const int mtiles = (int)(mpad / 256), ntiles = N / 256;
     ep.gn = band_width(ntiles, 4);
-    if constexpr (k256_ok) {
-      const dim3 g(mtiles * ntiles), b(kThreads2);
-      if (gemm_pp() == 1 && gemm_ilv() == 0 && MODE == NOMIC_EPI_SWIGLU && swiglu_reg_epi())
-        hipLaunchKernelGGL((k_gemm256<MODE, 0, 1, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else if (gemm_pp() == 1 && gemm_ilv() == 0)
-        hipLaunchKernelGGL((k_gemm256<MODE, 0, 0, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else if (gemm_pp() == 2 && gemm_ilv() == 0 && MODE == NOMIC_EPI_SWIGLU && swiglu_reg_epi())
-        hipLaunchKernelGGL((k_gemm256<MODE, 0, 1, 2>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else if (gemm_pp() == 2 && gemm_ilv() == 0)
-        hipLaunchKernelGGL((k_gemm256<MODE, 0, 0, 2>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else if (MODE == NOMIC_EPI_SWIGLU && gemm_ilv() == 0 && swiglu_reg_epi())
-        hipLaunchKernelGGL((k_gemm256<MODE, 0, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else if (gemm_ilv() == 1)
-        hipLaunchKernelGGL((k_gemm256<MODE, 1>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else if (gemm_ilv() == 2)
-        hipLaunchKernelGGL((k_gemm256<MODE, 2>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-      else
-        hipLaunchKernelGGL((k_gemm256<MODE>), g, b, kLds2Bytes, s, A, lda, W, ldw, K, mtiles, ntiles, ep);
-    }
+    if constexpr (k256_ok)
+      hipLaunchKernelGGL((k_gemm256<MODE, 0, 0, 2>), dim3(mtiles * ntiles), dim3(kThreads2), kLds2Bytes, s, A, lda, W,
+                         ldw, K, mtiles, ntiles, ep);
     return (int)hipGetLastError();
   }
   const int mtiles = (int)((M + BM - 1) / BM), ntiles = N / BN;
   ep.gn = band_width(ntiles, 8);
   constexpr int lds = kLdsBytes + (needs_rowstats(MODE) ? BM * 8 : 0);
-  if (gemm_as128())
-    hipLaunchKernelGGL((k_gemm_nt<MODE, true>), dim3(mtiles * ntiles), dim3(kThreads), lds, s, A, lda, W, ldw, K,
-                       mtiles, ntiles, ep);
-  else
-    hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), lds, s, A, lda, W, ldw, K, mtiles,
-                       ntiles, ep);
+  hipLaunchKernelGGL(k_gemm_nt<MODE>, dim3(mtiles * ntiles), dim3(kThreads), lds, s, A, lda, W, ldw, K, mtiles, ntiles,
+                     ep);
   return (int)hipGetLastError();
 }
 
@@ -1489,35 +980,7 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
 
 extern "C" int nomic_gemm_set_variant(int variant) {
   const int prev = gemm_variant();
-  g_variant = variant;
-  return prev;
-}
-
-// A/B knob: ping-pong main loop of the 256^2 kernel (1) or the 4-phase lockstep loop (0); returns the previous one
-extern "C" int nomic_gemm_set_pp(int on) {
-  const int prev = gemm_pp();
-  g_pp = on < 0 || on > 2 ? 2 : on;
-  return prev;
-}
-
-// A/B knob: asm LDS-DMA in the 128^2 kernel (1) or the builtin (0); returns the previous setting
-extern "C" int nomic_gemm_set_as128(int on) {
-  const int prev = gemm_as128();
-  g_as128 = on ? 1 : 0;
-  return prev;
-}
-
-// A/B knob: register SwiGLU epilogue of the 256^2 kernel (1) or the fp32 LDS image (0); returns the previous one
-extern "C" int nomic_gemm_set_swiglu_reg(int on) {
-  const int prev = swiglu_reg_epi() ? 1 : 0;
-  g_swiglu_reg = on ? 1 : 0;
-  return prev;
-}
-
-// A/B knob: DMA interleave of the 256^2 kernels (0, 1, 2); returns the previous setting
-extern "C" int nomic_gemm_set_ilv(int ilv) {
-  const int prev = gemm_ilv();
-  g_ilv = ilv < 0 || ilv > 2 ? 0 : ilv;
+  g_variant = variant == 128 || variant == 256 ? variant : 0;
   return prev;
 }
 

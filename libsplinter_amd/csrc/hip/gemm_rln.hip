@@ -489,13 +489,14 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
   }
 }
 
+// Two selectable forms (NOMIC_RLN): 222 = PIPE 2 (3 W stages, 2 A stages), DMA interleave 2
+// (default, profiles/r3_rln_variants_ab.jsonl) and 220 = the same without the interleave (fallback).
+// The other A/B forms of round 3 are gone; their measurements stay in profiles/r3_rln_*.
 int g_rln_variant = -1;
 int rln_variant() {
   if (g_rln_variant < 0) {
     const char* e = getenv("NOMIC_RLN");
-    // PIPE * 10 + EPI (no DMA interleave), or 200 + PIPE * 10 + ILV (EPI 0), + 1000 for the identity-MFMA
-    // residual (EPI 2), + 2000 for the 2-pair W prefetch (PF 2); 222 = PIPE 2, ILV 2: profiles/r3_rln_variants_ab.jsonl
-    g_rln_variant = e && *e ? atoi(e) : 222;
+    g_rln_variant = e && *e && atoi(e) == 220 ? 220 : 222;
   }
   return g_rln_variant;
 }
@@ -534,38 +535,13 @@ extern "C" int nomic_gemm_res_ln(const void* A, long lda, const void* W, long ld
   const auto* g = (const uint16_t*)gamma;
   const auto* b = (const uint16_t*)beta;
   auto* o = (uint16_t*)out;
-  switch (rln_variant()) {
-    case 10: launch_rln<1, 0>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 20: launch_rln<2, 0>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 21: launch_rln<2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 30: launch_rln<3, 0>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 31: launch_rln<3, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 210: launch_rln<1, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 220: launch_rln<2, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 230: launch_rln<3, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 212: launch_rln<1, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 222: launch_rln<2, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 213: launch_rln<1, 0, 2, 3>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 222 + 1000: launch_rln<2, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 222 + 2000: launch_rln<2, 0, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 222 + 3000: launch_rln<2, 2, 2, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    // + 10000: the K loop's LDS-DMAs from inline asm (AS, glds_asm.hpp)
-    case 10222: launch_rln<2, 0, 2, 2, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 10220: launch_rln<2, 0, 2, 1, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 10020: launch_rln<2, 0, 2, 0, 1, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 12222: launch_rln<2, 0, 2, 2, 2, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    // + 20000: K steps rotated per block (ROT)
-    case 20222: launch_rln<2, 0, 2, 2, 1, false, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 30222: launch_rln<2, 0, 2, 2, 1, true, true>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 242: launch_rln<4, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    case 243: launch_rln<4, 0, 2, 3>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-    default: launch_rln<1, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo); break;
-  }
+  if (rln_variant() == 220) launch_rln<2, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
+  else launch_rln<2, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
   return (int)hipGetLastError();
 }
 
 extern "C" int nomic_gemm_res_ln_set_variant(int variant) {
   const int prev = rln_variant();
-  g_rln_variant = variant;
+  g_rln_variant = variant == 220 ? 220 : 222;
   return prev;
 }

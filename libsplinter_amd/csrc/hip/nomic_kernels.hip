@@ -95,148 +95,6 @@ __global__ __launch_bounds__(256) void k_ln(const uint16_t* __restrict__ x, cons
 // with V staged transposed in LDS so the B fragment is one 16-B read.
 constexpr int AQ = 64, AK = 64, HD = 64;
 
-__global__ __launch_bounds__(256) void k_attn(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
-                                              const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
-                                              int heads, float scale_log2) {
-  __shared__ __attribute__((aligned(16))) uint16_t Ks[AK * HD];   // [key][d], 16-B chunks xor-swizzled
-  __shared__ __attribute__((aligned(16))) uint16_t Vt[HD * AK];   // [d][key], 16-B chunks xor-swizzled
-  __shared__ __attribute__((aligned(16))) uint16_t Ps[4][16 * AK];  // per wave [q][key]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // qblocks hold 128-row blocks (k_attn2's unit); this kernel runs each as two 64-row halves
-  const int seq = qblocks[2 * (blockIdx.x >> 1)], qstart = qblocks[2 * (blockIdx.x >> 1) + 1] + (blockIdx.x & 1) * 64;
-  const int head = blockIdx.y;
-  const long s0 = cu[seq], len = cu[seq + 1] - s0;
-  if (qstart >= len) return;
-  const long ld = 3L * heads * HD;
-  const uint16_t* Qg = qkv + head * HD;
-  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
-  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
-
-  const int fr = lane & 15, fq = lane >> 4;
-  // Q fragments (A operand): row = fr, d = kk*32 + 8*fq
-  const long qrow = qstart + wave * 16 + fr;
-  bf16x8 qa[2];
-#pragma unroll
-  for (int kk = 0; kk < 2; ++kk) {
-    if (qrow < len) qa[kk] = *(const bf16x8*)(Qg + (s0 + qrow) * ld + kk * 32 + fq * 8);
-    else qa[kk] = bf16x8{};
-  }
-  f32x4 o[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) o[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float m[4], lsum[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) { m[r] = -1e30f; lsum[r] = 0.f; }
-
-  for (long k0 = 0; k0 < len; k0 += AK) {
-    __syncthreads();  // previous tile fully consumed
-    // stage K (row-major, swizzled) and V^T: 512 16-B chunks each, 2 per thread
-#pragma unroll
-    for (int it = 0; it < 2; ++it) {
-      const int q = tid + it * 256;
-      const int key = q >> 3, ch = q & 7;
-      uint4 kv = make_uint4(0, 0, 0, 0), vv = make_uint4(0, 0, 0, 0);
-      if (k0 + key < len) {
-        kv = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
-        vv = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
-      }
-      *(uint4*)(Ks + key * HD + ((ch ^ (key & 7)) << 3)) = kv;
-      const uint32_t w[4] = {vv.x, vv.y, vv.z, vv.w};
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        const int d = ch * 8 + e;
-        const uint16_t val = (uint16_t)((e & 1) ? (w[e >> 1] >> 16) : (w[e >> 1] & 0xffff));
-        const int kc = key >> 3;  // 16-B chunk of keys within the d-row
-        Vt[d * AK + (((kc ^ (d & 7)) << 3) | (key & 7))] = val;
-      }
-    }
-    __syncthreads();
-    // S = Q K^T : 4 key sub-tiles x 2 d-steps
-    f32x4 s[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      s[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int key = j * 16 + fr;
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk) {
-        const int ch = kk * 4 + fq;
-        const bf16x8 kb = *(const bf16x8*)(Ks + key * HD + ((ch ^ (key & 7)) << 3));
-        s[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa[kk], kb, s[j], 0, 0, 0);
-      }
-    }
-    // online softmax: rows (fq*4 + r), key col j*16 + fr
-    float rmax[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float mx = -1e30f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const bool valid = k0 + j * 16 + fr < len;
-        const float v = valid ? s[j][r] * scale_log2 : -1e30f;
-        s[j][r] = v;
-        mx = fmaxf(mx, v);
-      }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-      rmax[r] = mx;
-    }
-    float alpha[4];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const float mn = fmaxf(m[r], rmax[r]);
-      alpha[r] = exp2f(m[r] - mn);
-      m[r] = mn;
-      float ps = 0.f;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = exp2f(s[j][r] - mn);
-        s[j][r] = p;
-        ps += p;
-      }
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) ps += __shfl_xor(ps, off, 64);
-      lsum[r] = lsum[r] * alpha[r] + ps;
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[j][r] *= alpha[r];
-    // P -> LDS (bf16), per wave [16 q][64 keys], 16-B chunks swizzled by row
-    uint16_t* P = Ps[wave];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = fq * 4 + r, key = j * 16 + fr;
-        P[row * AK + ((((key >> 3) ^ (row & 7)) << 3) | (key & 7))] = (uint16_t)f2bf(s[j][r]);
-      }
-    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's P writes landed
-    __builtin_amdgcn_wave_barrier();
-    // O += P V : A = P[q = fr][key = kk*32 + 8 fq ..], B = V[key][d = j*16 + fr]
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int ch = kk * 4 + fq;
-      const bf16x8 pa = *(const bf16x8*)(P + fr * AK + ((ch ^ (fr & 7)) << 3));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int d = j * 16 + fr;
-        const bf16x8 vb = *(const bf16x8*)(Vt + d * AK + ((ch ^ (d & 7)) << 3));
-        o[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pa, vb, o[j], 0, 0, 0);
-      }
-    }
-  }
-  // normalise and store: row q = fq*4 + r, col d = j*16 + fr
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    const long q = qstart + wave * 16 + fq * 4 + r;
-    if (q >= len) continue;
-    const float inv = 1.f / lsum[r];
-    uint16_t* dst = out + (s0 + q) * (long)heads * HD + head * HD;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) dst[j * 16 + fr] = (uint16_t)f2bf(o[j][r] * inv);
-  }
-}
-
 // ---------------------------------------------------------- attention v2 --
 // One workgroup = 128 query rows of one (sequence, head); 4 waves x 32 rows
 // (two 16-row q-blocks per wave).  "Swapped" products keep every per-query
@@ -720,180 +578,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
   }
 }
 
-// k_attn4: k_attn3 with the tile loop software-pipelined inside each wave (the FA3 idea on one wave):
-// iteration t issues the QK^T MFMAs of tile t+1 BEFORE the softmax of tile t, so the matrix pipe works on
-// S(t+1) while the VALU exponentiates S(t); then PV(t).  K/V tiles: a 3-deep LDS ring (tiles t and t+1
-// are read in iteration t, t+2 is written at its end) and one register stage (t+2's global loads issued
-// at the top of iteration t): one barrier per tile, as in k_attn3.  Two score tiles live in registers
-// (+32 VGPRs: 253, two waves per SIMD; held to three it spills 78 registers).
-template <int W = 2>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_attn4(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
-                                               const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
-                                               int heads, float scale_log2) {
-  constexpr int KT = 64, NT = 256, NL = KT * 8 / NT;
-  __shared__ __attribute__((aligned(16))) char lds[3][2][KT * 128];  // [ring slot][K | V][key * 128 B]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hi = lane >> 5, q32 = lane & 31, li = lane & 15, tq = li >> 2, tp = li & 3;
-  const int nwg = gridDim.x, orig = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int nqb = nwg / heads, head = lid / nqb, qbi = lid - head * nqb;
-  const int seq = qblocks[2 * qbi], qstart = qblocks[2 * qbi + 1];
-  const long s0 = cu[seq], len = cu[seq + 1] - s0;
-  const long ld = 3L * heads * HD;
-  const uint16_t* Qg = qkv + head * HD;
-  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
-  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
-
-  const long qrow = qstart + wave * 32 + q32;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-    qf[ks] = qrow < len ? *(const bf16x8*)(Qg + (s0 + qrow) * ld + ks * 16 + hi * 8) : bf16x8{};
-  f32x16 o[2];
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
-  float m = -1e30f, l = 0.f;
-
-  uint4 rk[NL], rv[NL];
-  auto gload = [&](long k0) {
-#pragma unroll
-    for (int it = 0; it < NL; ++it) {
-      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
-      if (k0 + key < len) {
-        rk[it] = *(const uint4*)(Kg + (s0 + k0 + key) * ld + ch * 8);
-        rv[it] = *(const uint4*)(Vg + (s0 + k0 + key) * ld + ch * 8);
-      } else {
-        rk[it] = make_uint4(0, 0, 0, 0);
-        rv[it] = make_uint4(0, 0, 0, 0);
-      }
-    }
-  };
-  auto lwrite = [&](int slot) {
-#pragma unroll
-    for (int it = 0; it < NL; ++it) {
-      const int c = tid + it * NT, key = c >> 3, ch = c & 7;
-      *(uint4*)(lds[slot][0] + key * 128 + (k3sw(key, ch) << 4)) = rk[it];
-      *(uint4*)(lds[slot][1] + key * 128 + (v3sw(key, ch) << 4)) = rv[it];
-    }
-  };
-  auto qk = [&](f32x16 (&sc)[2], int slot) {
-    const char* Ks = lds[slot][0];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) sc[kb][r] = 0.f;
-      const int row = kb * 32 + q32;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + row * 128 + (k3sw(row, 2 * ks + hi) << 4));
-        sc[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], sc[kb], 0, 0, 0);
-      }
-    }
-  };
-
-  const int ntiles = (int)((len + KT - 1) / KT);
-  gload(0);
-  lwrite(0);
-  if (ntiles > 1) {
-    gload(KT);
-    lwrite(1);
-  }
-  __syncthreads();
-  f32x16 sa[2], sb[2];
-  qk(sa, 0);
-
-  // one pipelined tile: `cur` holds S(t) (computed), `nxt` receives S(t+1)
-  auto tile = [&](int t, f32x16 (&cur)[2], f32x16 (&nxt)[2]) {
-    const long k0 = (long)t * KT;
-    const int slot = t % 3;
-    if (t + 2 < ntiles) gload(k0 + 2 * KT);
-    if (t + 1 < ntiles) qk(nxt, (t + 1) % 3);  // S(t+1) on the matrix pipe ...
-    // ... while the VALU runs the online softmax of S(t)
-    if (k0 + KT > len) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= len) cur[kb][r] = -1e30f;
-    }
-    float mx = fmaxf(cur[0][0], cur[1][0]);
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(cur[0][r], cur[1][r]));
-    {
-      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
-    }
-    constexpr float kThr = 8.f;
-    const float mxs = mx * scale_log2;
-    if (!__all(mxs - m <= kThr)) {
-      const float mn = fmaxf(m, mxs);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      m = mn;
-      l *= alpha;
-#pragma unroll
-      for (int db = 0; db < 2; ++db) o[db] *= alpha;
-    }
-    const float nm = -m;
-    float ps = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(cur[kb][r], scale_log2, nm));
-        cur[kb][r] = p;
-        ps += p;
-      }
-    {
-      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(ps), __float_as_uint(ps), false, false);
-      ps = __uint_as_float(q[0]) + __uint_as_float(q[1]);
-    }
-    l += ps;
-    const char* Vs = lds[slot][1];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 pf;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)cur[kb][8 * st + j];
-        const int rowA = kb * 32 + 16 * st + 4 * hi + tq, rowB = rowA + 8;
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const int col = 32 * db + 16 * ((lane >> 4) & 1) + 4 * tp;
-          const int ch = col >> 3, off = (col & 7) * 2;
-          const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vs + rowA * 128 + (v3sw(rowA, ch) << 4) + off));
-          const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vs + rowB * 128 + (v3sw(rowB, ch) << 4) + off));
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, (v8i16)__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
-          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
-        }
-      }
-    // tile t+2 into the ring slot tile t-1 used: every wave finished that slot at the barrier closing t-1
-    if (t + 2 < ntiles) lwrite((t + 2) % 3);
-    __syncthreads();
-  };
-  for (int t = 0; t < ntiles; t += 2) {
-    tile(t, sa, sb);
-    if (t + 1 < ntiles) tile(t + 1, sb, sa);
-  }
-  if (qrow < len) {
-    const float inv = 1.f / l;
-    uint16_t* dst = out + (s0 + qrow) * (long)heads * HD + head * HD;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 w;
-        w.x = pk2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv);
-        w.y = pk2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
-        *(uint2*)(dst + 32 * db + 8 * g + 4 * hi) = w;
-      }
-  }
-}
-
 // ------------------------------------------------------------ mean pool --
 __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, const int32_t* __restrict__ cu,
                                               float* __restrict__ pooled, int normalize, spl_arena_t aa,
@@ -1090,14 +774,18 @@ int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, 
   return (int)hipGetLastError();
 }
 
-static int g_attn_variant = [] {  // NOMIC_ATTN overrides (A/B)
+// Two selectable forms (NOMIC_ATTN): 13 = k_attn3 (32x32x16 MFMA, default: 634 vs 514 TFLOP/s for
+// 6, profiles/r3_attn_k_attn3_ab.jsonl) and 6 = k_attn2 (16x16x32 MFMA, permlane reductions, packed
+// score math), the fallback.  The other A/B forms of rounds 1-3 are gone; their measurements stay in
+// profiles/r1_attn_* .. r3_attn_*.
+static int g_attn_variant = [] {
   const char* e = getenv("NOMIC_ATTN");
-  return e && *e ? atoi(e) : 13;
-}();  // measured: k_attn3 (32x32x16 MFMA, 3 waves/SIMD) 634 vs 514 TFLOP/s for 6 (profiles/r3_attn_k_attn3_ab.jsonl)
+  return e && *e && atoi(e) == 6 ? 6 : 13;
+}();
 
 int nomic_attention_set_variant(int v) {
   const int prev = g_attn_variant;
-  g_attn_variant = v;
+  g_attn_variant = v == 6 ? 6 : 13;
   return prev;
 }
 
@@ -1106,56 +794,11 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   if (nqb <= 0) return 0;
   if (heads * HD * 3 % 8) return (int)hipErrorInvalidValue;
   const float scale_log2 = scale * 1.4426950408889634f;
-  if (g_attn_variant == 5)
-    hipLaunchKernelGGL((k_attn2<0, false, true>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv,
-                       (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 6)
+  if (g_attn_variant == 6)
     hipLaunchKernelGGL((k_attn2<0, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
                        (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 7)  // 128-key tiles: half the barriers, 2x the MFMA work per sync
-    hipLaunchKernelGGL((k_attn2<0, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
-                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 9)  // 8 waves, 256-row q-blocks (the caller's table): half the K/V traffic
-    hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 8>), dim3(nqb * heads), dim3(512), 0, s,
-                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 8)  // 128-key tiles held to 2 waves/SIMD
-    hipLaunchKernelGGL((k_attn2<2, true, true, false, 128>), dim3(nqb * heads), dim3(256), 0, s,
-                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 17)  // k_attn3 software-pipelined (S(t+1) MFMAs beside softmax(t)), 2 waves/SIMD
-    hipLaunchKernelGGL((k_attn4<2>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2);
-  else if (g_attn_variant == 13)  // 32x32x16 MFMA form (k_attn3)
-    hipLaunchKernelGGL(k_attn3<false>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2);
-  else if (g_attn_variant == 14)  // 13 with K/V loads two tiles ahead
-    hipLaunchKernelGGL(k_attn3<true>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2);
-  else if (g_attn_variant == 16)  // 13 held to 4 waves per SIMD
-    hipLaunchKernelGGL((k_attn3<false, 4>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
-                       cu, qblocks, heads, scale_log2);
-  else if (g_attn_variant == 15)  // 14 held to 3 waves per SIMD
-    hipLaunchKernelGGL((k_attn3<true, 3>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
-                       cu, qblocks, heads, scale_log2);
-  else if (g_attn_variant == 10)  // 6 with the next tile's loads after the QK^T MFMAs
-    hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 4, true>), dim3(nqb * heads), dim3(256), 0, s,
-                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 11)  // 7 (128-key tiles) with late loads
-    hipLaunchKernelGGL((k_attn2<0, true, true, false, 128, 4, true>), dim3(nqb * heads), dim3(256), 0, s,
-                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 12)  // 9 (8 waves, 256-row q-blocks) with late loads
-    hipLaunchKernelGGL((k_attn2<0, true, true, false, 64, 8, true>), dim3(nqb * heads), dim3(512), 0, s,
-                       (const uint16_t*)qkv, (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 4)
-    hipLaunchKernelGGL((k_attn2<0, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out,
-                       cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 2)
-    hipLaunchKernelGGL((k_attn2<0>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 3)
-    hipLaunchKernelGGL((k_attn2<3>), dim3(nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2, heads);
   else
-    hipLaunchKernelGGL(k_attn, dim3(2 * nqb, heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
+    hipLaunchKernelGGL(k_attn3<false>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);
   return (int)hipGetLastError();
 }

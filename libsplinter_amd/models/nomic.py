@@ -82,14 +82,6 @@ def _lib():
         L.nomic_row_stats.restype = c_int
         L.nomic_gemm_set_variant.argtypes = [c_int]
         L.nomic_gemm_set_variant.restype = c_int
-        L.nomic_gemm_set_ilv.argtypes = [c_int]
-        L.nomic_gemm_set_ilv.restype = c_int
-        L.nomic_gemm_set_swiglu_reg.argtypes = [c_int]
-        L.nomic_gemm_set_swiglu_reg.restype = c_int
-        L.nomic_gemm_set_pp.argtypes = [c_int]
-        L.nomic_gemm_set_pp.restype = c_int
-        L.nomic_gemm_set_as128.argtypes = [c_int]
-        L.nomic_gemm_set_as128.restype = c_int
         L.nomic_attention_set_variant.argtypes = [c_int]
         L.nomic_attention_set_variant.restype = c_int
         L.nomic_embed_ln.argtypes = [P, c_long, P, P, P, P, c_float, P, P]

@@ -867,7 +867,11 @@ __device__ int32_t integer_op(const Arena& a, const KeyT<KW>& k, int op, uint64_
   if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
   uint8_t* v = a.value((size_t)i);
   // the slot is held (odd epoch): plain accesses, and byte-safe -- a value row starts at
-  // i * max_val, which is 8-B aligned only when max_val is
+  // i * max_val, which is 8-B aligned only when max_val is.  The previous holder may have run on
+  // another CU / XCD: acquire before reading (no stale L1 line) and release before publishing (the
+  // new value leaves this XCD's L2), else concurrent increments of one key lose updates
+  // (tests/test_batch_api.py: 400 increments over 40 keys in one batch).
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   uint64_t x;
   __builtin_memcpy(&x, v, 8);
   switch (op) {
@@ -880,6 +884,7 @@ __device__ int32_t integer_op(const Arena& a, const KeyT<KW>& k, int op, uint64_
     default: break;
   }
   __builtin_memcpy(v, &x, 8);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
   drain();
   aadd64(epoch_ptr(s), 1);
   if (result) *result = x;

@@ -152,9 +152,10 @@ def _timed_region_profiler():
     return toggle
 
 
-def daemon_run(enc, docs: int, seq: int, rank: int, world: int, routed: bool, rounds: int = 3):
-    """Time Splinference.process over `docs` pending documents of a fresh hbm: store (the daemon's
-    batched device path), `rounds` times after one warm-up round; the producer re-sets every
+def daemon_run(enc, docs: int, seq: int, rank: int, world: int, routed: bool, node: str, rounds: int = 3):
+    """Time Splinference.process over `docs` pending documents of this rank's shard of node store
+    `node` (the daemon's owner-computes path: each rank embeds its own shard, reference
+    splinference.cpp:500-552), `rounds` times after one warm-up round; the producer re-sets every
     document's text between rounds (outside the timing) so each round finds them all pending."""
     import numpy as np
     import torch
@@ -168,8 +169,10 @@ def daemon_run(enc, docs: int, seq: int, rank: int, world: int, routed: bool, ro
     rng = np.random.default_rng(300 + rank)
     texts = [" ".join(words[int(i)] for i in rng.integers(0, len(words), size=int(rng.integers(seq // 2, seq - 2))))
              for _ in range(docs)]
-    name = f"hbm:dm{os.getpid()}r{rank}"
+    from libsplinter_amd.store import NODE_HBM, node_join, node_leave, node_shard_name
+    name = node_shard_name(node, rank, NODE_HBM)
     st = Store.create(name, slots=max(4 * docs, 1024), max_val=4096, embeddings=True)
+    node_join(node, rank, world, NODE_HBM, st.slots, 4096, True)
     keys = [f"doc{rank}_{i:06d}" for i in range(docs)]
 
     def produce():
@@ -196,6 +199,7 @@ def daemon_run(enc, docs: int, seq: int, rank: int, world: int, routed: bool, ro
         return {"vectors_per_s": docs * rounds * world / dt.item(), "embedded": done, "expected": docs * rounds,
                 "stale": d.stats["stale"]}
     finally:
+        node_leave(node, rank)
         st.close()
         unlink(name)
 
@@ -266,9 +270,12 @@ def main():
     kpg = args.keys_per_gpu
     total_keys = kpg * world
     slots = int(kpg * args.slots_factor)
-    name = f"bench{os.getpid()}r{rank}"
+    # the ranks' arenas are the shards of ONE node store, node:<node_tag>kv (node_store.hpp): while the
+    # bench runs, any process of the node opens it through the C ABI (splinterctl -u node:..., the
+    # Rust / TS bindings) and reaches every rank's keys -- the benched store IS the product's
+    node_tag = f"bench{os.environ.get('MASTER_PORT', os.getpid())}"
     t0 = time.time()
-    arena = HbmArena.create(name, slots=slots, max_val=args.max_val, embeddings=False)
+    arena = HbmArena.join_node(f"{node_tag}kv", rank, world, slots=slots, max_val=args.max_val, embeddings=False)
     if not (os.environ.get("BENCH_SKIP_MOP") and args.mop == 1):  # diagnosis: stores are created hybrid
         arena.store.set_mop(args.mop)  # 1 = hybrid scrub, the reference's store default
     kv = ShardedKV(GpuShard(arena))
@@ -317,8 +324,8 @@ def main():
     sarena = None
     if args.search_keys > 0 and args.mode in ("embed", "mixed"):
         t1 = time.time()
-        sarena = HbmArena.create(f"sbench{os.getpid()}r{rank}", slots=int(args.search_keys * 1.25) + 4096,
-                                 max_val=64, embeddings=True)
+        sarena = HbmArena.join_node(f"{node_tag}vec", rank, world, slots=int(args.search_keys * 1.25) + 4096,
+                                    max_val=64, embeddings=True)
         g0 = torch.Generator(device="cuda")
         g0.manual_seed(77 + rank)
         ch = 1 << 20
@@ -638,7 +645,7 @@ def main():
     # documents of its own store (reference splinference.cpp:500-552)
     daemon = None
     if embedder is not None and args.daemon_docs > 0:
-        daemon = daemon_run(embedder.enc, args.daemon_docs, args.embed_seq, rank, world, routed)
+        daemon = daemon_run(embedder.enc, args.daemon_docs, args.embed_seq, rank, world, routed, f"{node_tag}dm")
 
     # ---- config #5 query phase: batched cosine top-10 over every rank's search arena ---------
     # (the vectors the embed phase wrote are in there too).  Rank 0's queries are broadcast (C3),
@@ -696,6 +703,7 @@ def main():
                 "random N(0,1) 768-d vectors in the search arenas",
         "config": {
             "model": "hbm-arena-v4 (128-B slots, 256-B values)" + (" + nomic-embed-text-v1.5" if embedder else ""),
+            "store": f"node:{node_tag}kv ({world} HBM shard{'s' if world > 1 else ''})",
             "keys_per_gpu": kpg, "slots_per_gpu": slots, "global_batch": args.batch * world,
             "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
             "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),

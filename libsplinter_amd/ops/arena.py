@@ -139,7 +139,30 @@ class HbmArena:
         n = name if name.startswith("hbm:") else "hbm:" + name
         return cls(Store.create(n, slots, max_val, embeddings=embeddings))
 
+    @classmethod
+    def join_node(cls, node: str, rank: int, world: int, slots: int, max_val: int,
+                  embeddings: bool = True) -> "HbmArena":
+        """This rank's shard of node store ``node:<node>`` (node_store.hpp): the shard arena
+        ``hbm:<node>.s<rank>`` on this process's GPU, registered with the node descriptor, so once
+        every rank has joined any process -- the CLI, a C / Rust / TS client -- opens
+        ``node:<node>`` and reaches every rank's keys through the C ABI.  ``close`` leaves the node."""
+        from ..store import NODE_HBM, node_join, node_shard_name
+        a = cls(Store.create(node_shard_name(node, rank, NODE_HBM), slots, max_val, embeddings=embeddings))
+        try:
+            node_join(node, rank, world, NODE_HBM, a.slots, max_val, embeddings)
+        except Exception:
+            a.store.close()
+            raise
+        a.node = (node, rank)
+        return a
+
+    node = None
+
     def close(self):
+        if self.node is not None:
+            from ..store import node_leave
+            node_leave(*self.node)
+            self.node = None
         self.store.close()
 
     @property

@@ -171,3 +171,32 @@ def test_native_tap_suite_on_hbm(prefix, shards):
     fails = [ln for ln in r.stdout.splitlines() if ln.startswith("not ok")]
     print(r.stdout[-400:])
     assert r.returncode == 0 and not fails, (fails, r.stderr[-2000:])
+
+
+def test_bench_store_is_a_node_store_the_cli_opens(uniq):
+    """bench.py's ranks create their arenas with HbmArena.join_node: the benched store is node
+    store node:<tag>kv, so a C-ABI client in another process (splinterctl) reads the keys the
+    batch kernels wrote, while the bench's process holds it (reference splinter.c:235-248: every
+    process maps the one store)."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, format_keys, format_values
+    a = HbmArena.join_node(f"{uniq}kv", 0, 1, slots=1 << 16, max_val=256, embeddings=False)
+    try:
+        K = format_keys(1000, "k", 10, 16)
+        V, L = format_values(1000, 7, 150, 256)
+        assert (a.set(K, V, L) == 0).all()
+        torch.cuda.synchronize()
+        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+        cli = os.path.join(ROOT, "libsplinter_amd", "bin", "splinterctl")
+        r = subprocess.run([cli, "-u", f"node:{uniq}kv", "get", "k0000000417"], capture_output=True, text=True,
+                           timeout=120, env=env)
+        assert r.returncode == 0 and "id:417|" in r.stdout, (r.stdout, r.stderr[-2000:])
+        # and the batch C ABI over the same node, from this process
+        from libsplinter_amd import store as S
+        with S.Store.open(f"node:{uniq}kv") as s:
+            st, out, ln = s.get_batch([f"k{i:010d}" for i in range(0, 1000, 7)], width=256)
+            assert (st == 0).all() and all(b"id:%d|" % i in bytes(out[j, : ln[j]])
+                                           for j, i in enumerate(range(0, 1000, 7)))
+    finally:
+        a.close()
+    assert not os.path.exists(f"/dev/shm/{uniq}kv.node")  # the last shard out removed the node

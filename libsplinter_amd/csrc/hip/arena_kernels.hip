@@ -446,6 +446,161 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
   flush_stats(a, st, stats, 0);
 }
 
+// ------------------------------------------------------- fused set + get -----
+// One grid for a whole KV step (spl_kvs_step with SPL_KVS_FUSED=1): the client streams' slices
+// (descriptors) of the set and the get batch are consumed by one launch instead of one dispatch per
+// slice.  With 32 + 32 client streams the per-slice dispatches are capped by the hardware queues
+// (about 2 set and 2 get dispatches resident at a time, profiles/r3_pmc_kv.md), and the step is
+// latency bound (79 % of set wave cycles wait on memory); here every CU holds waves of both kinds
+// at once.  Lane sequence over the concatenated op space [sets | gets] as the carried-retry kernels
+// (op c of a lane: first + (c / U) * stride + c % U): a round's U slots may hold sets and gets side
+// by side, their probes / claims in flight together; the value rows of the two kinds go through two
+// cooperative-copy passes (sets: write-through rows into the arena, as k_set_carry WT; gets: sc1
+// reads of arena rows, as k_get_carry FAST), then sets publish and gets re-validate.
+template <int U, int B>
+__global__ __launch_bounds__(B) void k_kv_fused(spl_arena_t aa, const char* skeys, const char* gkeys, int kstride,
+                                                const uint8_t* vals, int vstride, const uint32_t* lens, long n_set,
+                                                int32_t* sstatus, uint8_t* out, int ostride, uint32_t* out_lens,
+                                                long n_get, int32_t* gstatus, int max_retry, uint64_t* stats) {
+  __shared__ uint4 cp_p[2][B / 64][U * 64];
+  __shared__ uint2 cp_l[2][B / 64][U * 64];
+  const Arena a = to_dev(aa);
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  Stats st;
+  uint64_t muts = 0;
+  const long n = n_set + n_get;
+  const long stride = (long)gridDim.x * blockDim.x * U;
+  const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
+  long cursor = 0;
+  bool more = true;
+  Key k[U];
+  Claim c[U];
+  long op[U], sidx[U];
+  uint64_t e1[U];
+  uint32_t len[U];
+  int32_t rc[U];
+  int tries[U];
+  bool set[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) op[j] = -1;
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (;;) {
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (op[j] < 0 && more) {
+        const long i = first + (cursor / U) * stride + (cursor % U);
+        ++cursor;
+        if (i >= n) {
+          more = false;
+        } else {
+          set[j] = i < n_set;
+          const long r = set[j] ? i : i - n_set;
+          op[j] = r;
+          tries[j] = 0;
+          load_key(k[j], (set[j] ? skeys : gkeys) + r * (long)kstride, kstride);
+          len[j] = set[j] ? lens[r] : 0u;
+        }
+      }
+    }
+    bool busy = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) busy |= op[j] >= 0;
+    if (!__syncthreads_or(busy)) break;
+    // probes / claims of every slot of the round
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      rc[j] = kInval;
+      c[j] = Claim{-1, false, kInval};
+      if (op[j] < 0) continue;
+      ++st.attempts;
+      ++tries[j];
+      if (set[j]) {
+        if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride) c[j].rc = kMsgSize;
+        else c[j] = claim_set(a, k[j]);
+        rc[j] = c[j].rc;
+      } else {
+        uint32_t L = 0;
+        sidx[j] = locate_peek(a, k[j], &e1[j], &L);
+        len[j] = L;
+        rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
+        if (rc[j] == kOk && ((e1[j] & 1) || L > a.max_val)) rc[j] = kAgain;
+        else if (rc[j] == kOk && out && L > (uint32_t)ostride) rc[j] = kMsgSize;
+      }
+    }
+    // value rows: table 0 = sets (client row -> arena, write-through), table 1 = gets (arena -> client)
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const bool gs = op[j] >= 0 && set[j] && rc[j] == kOk;
+      const bool gg = out && op[j] >= 0 && !set[j] && rc[j] == kOk;
+      const uint64_t ss = gs ? (uint64_t)(vals + op[j] * (long)vstride) : 0;
+      const uint64_t sd = gs ? (uint64_t)a.value((size_t)c[j].idx) : 0;
+      cp_p[0][w][j * 64 + lane] = make_uint4((uint32_t)ss, (uint32_t)(ss >> 32), (uint32_t)sd, (uint32_t)(sd >> 32));
+      cp_l[0][w][j * 64 + lane] = make_uint2(gs ? len[j] : 0u, gs ? set_chunks(a, len[j], scrub, hybrid) : 0u);
+      const uint64_t gsrc = gg ? (uint64_t)a.value((size_t)sidx[j]) : 0;
+      const uint64_t gdst = gg ? (uint64_t)(out + op[j] * (long)ostride) : 0;
+      const uint32_t n16 = (len[j] + 15) >> 4;
+      cp_p[1][w][j * 64 + lane] = make_uint4((uint32_t)gsrc, (uint32_t)(gsrc >> 32), (uint32_t)gdst, (uint32_t)(gdst >> 32));
+      cp_l[1][w][j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? n16 : 0u);
+    }
+    __builtin_amdgcn_wave_barrier();
+    coop_copy<U * 64, 3>(cp_p[0][w], cp_l[0][w], lane, (int)((a.max_val + 255) >> 8), a.max_val);
+    coop_copy<U * 64, 0, true>(cp_p[1][w], cp_l[1][w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (op[j] >= 0 && set[j] && rc[j] == kOk) write_meta<3>(a, c[j], len[j]);
+    drain();
+    // gets: closing round trip, (hash, epoch) and the key words together
+    {
+      u32x4c_t he[U];
+      KeyProbe<16> kp[U];
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        const bool live = op[j] >= 0 && !set[j] && rc[j] == kOk;
+        const uint8_t* s = a.slot(live ? (size_t)sidx[j] : 0);
+        he[j] = ld16c(s + kOffHash);
+        kp[j].issue(s, k[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        vm_wait(he[j]);
+        kp[j].wait();
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j)
+        if (op[j] >= 0 && !set[j] && rc[j] == kOk &&
+            (hi64(he[j]) != e1[j] || lo64(he[j]) != k[j].hash || !kp[j].eq(k[j])))
+          rc[j] = kAgain;
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      if (op[j] < 0) continue;
+      const int32_t r = rc[j];
+      if (r == kAgain) {
+        ++st.again;
+        if (tries[j] <= max_retry) continue;  // carried into the next round
+      }
+      if (set[j]) {
+        if (r == kOk) {
+          finish_set(a, c[j]);
+          ++st.ok;
+          ++muts;
+          pulse_masks(a, c[j].wm, c[j].bl);
+          mark_dirty(a, (size_t)c[j].idx);
+        }
+        if (sstatus) sstatus[op[j]] = r;
+      } else {
+        if (r == kOk) ++st.ok;
+        else if (r == kNoEnt) ++st.miss;
+        if (out_lens) out_lens[op[j]] = r == kOk ? len[j] : 0;
+        if (gstatus) gstatus[op[j]] = r;
+      }
+      op[j] = -1;
+    }
+  }
+  flush_stats(a, st, stats, muts);
+}
+
 // ------------------------------------------------------------- unset ----
 __global__ __launch_bounds__(kBlock) void k_unset(spl_arena_t aa, const char* keys, int kstride, long n,
                                                   int32_t* status, int max_retry) {
@@ -1001,6 +1156,18 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
                  int ostride, uint32_t* glens, long n_get, int32_t* gstatus, int max_retry, uint64_t* stats) {
   auto* k = (KvStreams*)h;
   if (!k) return (int)hipErrorInvalidValue;
+  // SPL_KVS_FUSED=1: every stream's slice consumed by ONE grid on the origin stream (k_kv_fused)
+  static const int fused = env_int("SPL_KVS_FUSED", 0);
+  if (fused && n_set + n_get > 0) {
+    if ((kstride & 15) || kstride > 64 || (vstride & 15) || (ostride & 15)) return (int)hipErrorInvalidValue;
+    static const int wpc = env_int("SPL_KVS_FUSED_WG_PER_CU", 2);  // 194 VGPRs: 2 waves per SIMD resident
+    const long need = (n_set + n_get + 2 * 256 - 1) / (2 * 256);
+    const long cap = 256L * (wpc > 0 ? wpc : 8);
+    hipLaunchKernelGGL((k_kv_fused<2, 256>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
+                       skeys, gkeys, kstride, svals, vstride, slens, n_set, sstatus, gout, ostride, glens, n_get,
+                       gstatus, max_retry, stats);
+    return (int)hipGetLastError();
+  }
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
   const int nw = n_set > 0 ? k->nw : 0, nr = n_get > 0 ? k->nr : 0;

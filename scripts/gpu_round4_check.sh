@@ -21,3 +21,16 @@ for st in hbm:xb1 node:xb2; do
     --keys 8000000 --seconds 3 >> "$OUT/batch_api.jsonl" 2>&1 || { echo "batch $st failed"; exit 1; }
 done
 cat "$OUT/batch_api.jsonl"
+if [ -n "$EXTRA_OVERLAP" ]; then
+  timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --overlap-native 1 --embed-e2e 0 --host-api 0 \
+    --host-api-threads2 0 --daemon-docs 0 --routed-steps 0 > "$OUT/bench_overlap.json" 2> "$OUT/bench_overlap.err"
+  rc=$?; cat "$OUT/bench_overlap.json"; [ $rc -ne 0 ] && { tail -20 "$OUT/bench_overlap.err"; exit $rc; }
+fi
+if [ -n "$EXTRA_KV" ]; then
+  for f in 0 1; do
+    SPL_KVS_FUSED=$f timeout -k 10 300 python -u bench.py --mode kv --steps 20 --warmup 5 --host-api 0 \
+      --host-api-threads2 0 --routed-steps 0 > "$OUT/bench_kv_fused$f.json" 2> "$OUT/bench_kv_fused$f.err"
+    rc=$?; cat "$OUT/bench_kv_fused$f.json"; [ $rc -ne 0 ] && { tail -20 "$OUT/bench_kv_fused$f.err"; exit $rc; }
+  done
+fi
+exit 0

@@ -21,6 +21,12 @@ for st in hbm:xb1 node:xb2; do
     --keys 8000000 --seconds 3 >> "$OUT/batch_api.jsonl" 2>&1 || { echo "batch $st failed"; exit 1; }
 done
 cat "$OUT/batch_api.jsonl"
+if [ -n "$EXTRA_PROF" ]; then
+  # kernel + memory-copy trace of the batch ABI on hbm: (where the host-array batch time goes)
+  (cd /tmp && export TMPDIR=/tmp; cd "$GRAFT_REPO_ROOT" && timeout -k 10 120 rocprofv3 --kernel-trace --memory-copy-trace \
+    --stats -d "$OUT/prof_batch" -o run -- ./libsplinter_amd/bin/splinter_hostapi_bench --store hbm:xb3 --batch 2000000 \
+    --keys 4000000 --seconds 2 > "$OUT/batch_prof.json" 2>&1) || { echo "batch profile failed"; exit 1; }
+fi
 if [ -n "$EXTRA_OVERLAP" ]; then
   timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --overlap-native 1 --embed-e2e 0 --host-api 0 \
     --host-api-threads2 0 --daemon-docs 0 --routed-steps 0 > "$OUT/bench_overlap.json" 2> "$OUT/bench_overlap.err"

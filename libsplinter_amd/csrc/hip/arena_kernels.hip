@@ -457,8 +457,8 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
 // by side, their probes / claims in flight together; the value rows of the two kinds go through two
 // cooperative-copy passes (sets: write-through rows into the arena, as k_set_carry WT; gets: sc1
 // reads of arena rows, as k_get_carry FAST), then sets publish and gets re-validate.
-template <int U, int B>
-__global__ __launch_bounds__(B) void k_kv_fused(spl_arena_t aa, const char* skeys, const char* gkeys, int kstride,
+template <int U, int B, int KW = 16, int OCC = 1>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, const char* skeys, const char* gkeys, int kstride,
                                                 const uint8_t* vals, int vstride, const uint32_t* lens, long n_set,
                                                 int32_t* sstatus, uint8_t* out, int ostride, uint32_t* out_lens,
                                                 long n_get, int32_t* gstatus, int max_retry, uint64_t* stats) {
@@ -474,7 +474,7 @@ __global__ __launch_bounds__(B) void k_kv_fused(spl_arena_t aa, const char* skey
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
   long cursor = 0;
   bool more = true;
-  Key k[U];
+  KeyT<KW> k[U];
   Claim c[U];
   long op[U], sidx[U];
   uint64_t e1[U];
@@ -553,7 +553,7 @@ __global__ __launch_bounds__(B) void k_kv_fused(spl_arena_t aa, const char* skey
     // gets: closing round trip, (hash, epoch) and the key words together
     {
       u32x4c_t he[U];
-      KeyProbe<16> kp[U];
+      KeyProbe<KW> kp[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
         const bool live = op[j] >= 0 && !set[j] && rc[j] == kOk;
@@ -1160,12 +1160,17 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
   static const int fused = env_int("SPL_KVS_FUSED", 0);
   if (fused && n_set + n_get > 0) {
     if ((kstride & 15) || kstride > 64 || (vstride & 15) || (ostride & 15)) return (int)hipErrorInvalidValue;
-    static const int wpc = env_int("SPL_KVS_FUSED_WG_PER_CU", 2);  // 194 VGPRs: 2 waves per SIMD resident
+    // resident workgroups per CU: 2 at 194 VGPRs (KW 16), 3 with 16-B keys held in 4 words (<= 168)
+    static const int wpc = env_int("SPL_KVS_FUSED_WG_PER_CU", fused == 2 && kstride == 16 ? 3 : 2);
     const long need = (n_set + n_get + 2 * 256 - 1) / (2 * 256);
     const long cap = 256L * (wpc > 0 ? wpc : 8);
-    hipLaunchKernelGGL((k_kv_fused<2, 256>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
-                       skeys, gkeys, kstride, svals, vstride, slens, n_set, sstatus, gout, ostride, glens, n_get,
-                       gstatus, max_retry, stats);
+    const dim3 g((unsigned)(need < cap ? need : cap));
+    if (kstride == 16 && fused == 2)  // 16-B keys held as 4 words (fewer VGPRs)
+      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, origin, a, skeys, gkeys, kstride, svals, vstride,
+                         slens, n_set, sstatus, gout, ostride, glens, n_get, gstatus, max_retry, stats);
+    else
+      hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, origin, a, skeys, gkeys, kstride, svals, vstride,
+                         slens, n_set, sstatus, gout, ostride, glens, n_get, gstatus, max_retry, stats);
     return (int)hipGetLastError();
   }
   hipError_t e = hipEventRecord(k->start, origin);

@@ -33,7 +33,7 @@ if [ -n "$EXTRA_OVERLAP" ]; then
   rc=$?; cat "$OUT/bench_overlap.json"; [ $rc -ne 0 ] && { tail -20 "$OUT/bench_overlap.err"; exit $rc; }
 fi
 if [ -n "$EXTRA_KV" ]; then
-  for f in 0 1; do
+  for f in 0 1 2; do
     SPL_KVS_FUSED=$f timeout -k 10 300 python -u bench.py --mode kv --steps 20 --warmup 5 --host-api 0 \
       --host-api-threads2 0 --routed-steps 0 > "$OUT/bench_kv_fused$f.json" 2> "$OUT/bench_kv_fused$f.err"
     rc=$?; cat "$OUT/bench_kv_fused$f.json"; [ $rc -ne 0 ] && { tail -20 "$OUT/bench_kv_fused$f.err"; exit $rc; }

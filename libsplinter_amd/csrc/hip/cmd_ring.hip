@@ -18,8 +18,37 @@
 #include <time.h>
 #include <unistd.h>
 
+#include <set>
+#include <shared_mutex>
+
 #include "arena_dev.hpp"
 #include "cmd_ring.hpp"
+
+namespace spl {
+namespace {
+// Quiesce gate (RingQuiesce, cmd_ring.hpp).  Per-call ops hold it shared for their whole call;
+// store set-up holds it exclusive and first stops every live worker of the process: HIP calls made
+// while setting up a store (VMM maps, host registration, device memsets) may wait for the device's
+// queues, and a resident worker kept alive by another thread's traffic never drains.
+std::shared_mutex g_gate;
+std::mutex g_reg_mu;
+std::set<CmdRing*> g_rings;
+thread_local bool t_exclusive = false;
+}  // namespace
+
+RingQuiesce::RingQuiesce() {
+  if (t_exclusive) return;
+  g_gate.lock();
+  t_exclusive = held_ = true;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (CmdRing* r : g_rings) r->stop();
+}
+RingQuiesce::~RingQuiesce() {
+  if (!held_) return;
+  t_exclusive = false;
+  g_gate.unlock();
+}
+}  // namespace spl
 
 namespace spl {
 
@@ -587,6 +616,10 @@ int effective_cpus() {
 }  // namespace
 
 int CmdRing::init(int device, uint32_t pstride) {
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_rings.insert(this);
+  }
   device_ = device;
   pstride_ = (pstride + 15) & ~15u;
   if (pstride_ < kEmbedBytes) pstride_ = kEmbedBytes;
@@ -683,6 +716,8 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
                   uint64_t khash, const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap,
                   RingResult* r) {
   if (in_len > pstride_) { errno = EMSGSIZE; return -1; }
+  std::shared_lock<std::shared_mutex> gate(g_gate, std::defer_lock);
+  if (!t_exclusive) gate.lock();  // (a store set-up on this thread already holds it exclusive)
   // own an entry: start at a rotating ticket, CAS the host-only busy flag.  Consecutive tickets
   // map to different groups (entry = (t % groups) * per_group + t / groups), so concurrent
   // callers land on different worker waves -- which run in parallel -- instead of sharing one
@@ -833,6 +868,10 @@ void CmdRing::stop() {
 }
 
 CmdRing::~CmdRing() {
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_rings.erase(this);
+  }
   stop();
 #ifdef SPL_RING_STAMPS
   if (shared_) {

@@ -111,6 +111,20 @@ struct RingResult {
   uint64_t result = 0;
 };
 
+// Scope guard held while a store of this process is set up or torn down (hbm_store.hip): waits
+// for in-flight per-call ops, stops every live ring worker of the process and keeps new calls out
+// until the scope ends (they then relaunch their worker).  Re-entrant on one thread.
+class RingQuiesce {
+ public:
+  RingQuiesce();
+  ~RingQuiesce();
+  RingQuiesce(const RingQuiesce&) = delete;
+  RingQuiesce& operator=(const RingQuiesce&) = delete;
+
+ private:
+  bool held_ = false;
+};
+
 class CmdRing {
  public:
   // device: ordinal of the arena's GPU; pstride: payload bytes per entry (>= max value, vector)

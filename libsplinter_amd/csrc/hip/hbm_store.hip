@@ -816,6 +816,7 @@ HbmStore* HbmStore::open(const char* name, int* err) {
 }
 
 HbmStore::~HbmStore() {
+  RingQuiesce quiet;  // hipFree & co. may wait for the device: no resident worker of this process
   DevGuard dg(device_);
   for (auto& st : stg_) {
     if (st.s) {
@@ -982,6 +983,7 @@ int HbmStore::restore_from(const char* path) {
 }
 
 StoreBase* hbm_factory_impl(const char* name, size_t slots, size_t max_val, unsigned flags, int create, int* err) {
+  RingQuiesce quiet;  // no resident ring worker of this process while the new store is set up
   if (create) {
     const int dev = (int)((flags >> kCreateDeviceShift) & 0xFF) - 1;  // -1: the current device
     DevGuard dg(dev);

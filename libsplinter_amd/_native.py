@@ -237,10 +237,13 @@ def _declare_hip(L):
     _sig(L, "spl_arena_scan_range", c_int, A, c_int, c_u64, c_u32, c_u32, P, P, c_u32, P, P)
     _sig(L, "spl_kvs_create", P, c_int, c_int)
     _sig(L, "spl_kvs_destroy", None, P)
+    _sig(L, "spl_kvs_set_fused", c_int, P, c_int)
     _sig(L, "spl_kvs_step", c_int, P, A, P, P, c_int, P, c_int, P, c_long, P, P, P, c_int, P, c_long, P, c_int, P)
     _sig(L, "spl_kvs_step_xr", c_int, P, A, P, ctypes.POINTER(XrStep), c_int, P)
     if hasattr(L, "spl_hbm_ring_launches"):
         _sig(L, "spl_hbm_ring_launches", c_u32, c_void_p)
+    if hasattr(L, "spl_hbm_ring_mode"):
+        _sig(L, "spl_hbm_ring_mode", c_int, c_void_p)
     _sig(L, "spl_arena_purge", c_int, A, P)
     _sig(L, "spl_arena_gather_slots", c_int, A, P, c_long, P, P)
     _sig(L, "spl_hash_keys", c_int, P, c_int, c_long, P, P)

@@ -376,56 +376,85 @@ int NodeStore::madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t
 
 // ------------------------------------------------------------------ batches --
 // A batch is counting-sorted by owning shard into one scratch buffer (pinned when the HBM backend
-// is present, so HBM shards DMA straight from it), every shard's contiguous part runs on its own
-// thread (HBM shards: HbmStore::*_batch on that shard's GPU, all GPUs at once), and the outputs
-// are scattered back into client order.  Gathers and scatters run on kNodeBatchThreads threads.
+// is present, so HBM shards DMA straight from it).  Every shard's contiguous part runs on its own
+// thread -- gather its rows, run its batch (HBM shards: HbmStore::*_batch on that shard's GPU, all
+// GPUs at once), scatter its outputs back into client order -- so one shard's host copies overlap
+// the others' DMA and kernels.  The sort itself is parallel (per-thread histograms).
 namespace {
 constexpr int kNodeBatchThreads = 8;
 
 template <class F>
-void par_range(long n, F&& f) {
-  const int t = n < 65536 ? 1 : kNodeBatchThreads;
-  if (t == 1) { f(0L, n); return; }
+void par_range(long n, F&& f, int t = kNodeBatchThreads) {
+  if (n < 65536) t = 1;
+  if (t <= 1) { f(0L, n, 0); return; }
   std::vector<std::thread> th;
-  for (int i = 0; i < t; ++i) th.emplace_back([&, i] { f(n * i / t, n * (i + 1) / t); });
+  for (int i = 0; i < t; ++i) th.emplace_back([&, i] { f(n * i / t, n * (i + 1) / t, i); });
   for (auto& x : th) x.join();
+}
+
+// one row of w bytes (the common widths as fixed-size copies)
+inline void copy_row(uint8_t* d, const uint8_t* s, long w) {
+  switch (w) {
+    case 4: std::memcpy(d, s, 4); break;
+    case 8: std::memcpy(d, s, 8); break;
+    case 16: std::memcpy(d, s, 16); break;
+    case 32: std::memcpy(d, s, 32); break;
+    default: std::memcpy(d, s, (size_t)w);
+  }
 }
 }  // namespace
 
 struct NodeStore::Plan {
   std::vector<long> perm;   // perm[k]: client op at sorted position k
   std::vector<long> off;    // shard j's ops are sorted positions [off[j], off[j+1])
-  Plan(const char* keys, int kstride, long n, int nsh) : perm((size_t)n), off((size_t)nsh + 1, 0) {
+  int nsh;
+  Plan(const char* keys, int kstride, long n, int nsh_) : perm((size_t)n), off((size_t)nsh_ + 1, 0), nsh(nsh_) {
     std::vector<int32_t> dest((size_t)n);
     const int cut = kstride < 64 ? kstride : 63;
-    par_range(n, [&](long b, long e) {
+    const int T = n < 65536 ? 1 : kNodeBatchThreads;
+    std::vector<long> cnt((size_t)T * nsh, 0);
+    par_range(n, [&](long b, long e, int t) {
       char k[64];
+      long* c = cnt.data() + (size_t)t * nsh;
       for (long i = b; i < e; ++i) {
         std::memcpy(k, keys + i * kstride, (size_t)cut);
         k[cut] = 0;
-        dest[(size_t)i] = node_shard_of(KeyRef(k).hash, nsh);
+        const int d = node_shard_of(KeyRef(k).hash, nsh);
+        dest[(size_t)i] = d;
+        ++c[d];
       }
-    });
-    for (long i = 0; i < n; ++i) ++off[(size_t)dest[(size_t)i] + 1];
-    for (int j = 0; j < nsh; ++j) off[(size_t)j + 1] += off[(size_t)j];
-    std::vector<long> cur(off.begin(), off.end() - 1);
-    for (long i = 0; i < n; ++i) perm[(size_t)cur[(size_t)dest[(size_t)i]]++] = i;
+    }, T);
+    // stable placement: thread t's ops of shard j follow those of threads < t
+    std::vector<long> base((size_t)T * nsh);
+    long run = 0;
+    for (int j = 0; j < nsh; ++j) {
+      off[(size_t)j] = run;
+      for (int t = 0; t < T; ++t) {
+        base[(size_t)t * nsh + j] = run;
+        run += cnt[(size_t)t * nsh + j];
+      }
+    }
+    off[(size_t)nsh] = run;
+    par_range(n, [&](long b, long e, int t) {
+      long* p = base.data() + (size_t)t * nsh;
+      for (long i = b; i < e; ++i) perm[(size_t)p[dest[(size_t)i]]++] = i;
+    }, T);
   }
-  // sorted copy of a column (rows of `w` bytes)
-  void gather(uint8_t* dst, const void* src, long w) const {
-    const long n = (long)perm.size();
-    par_range(n, [&](long b, long e) {
-      for (long k = b; k < e; ++k) std::memcpy(dst + k * w, (const uint8_t*)src + perm[(size_t)k] * w, (size_t)w);
-    });
+  // threads per shard for its gathers / scatters
+  int sub() const { return nsh >= kNodeBatchThreads ? 1 : kNodeBatchThreads / nsh; }
+  // sorted copy of a column (rows of `w` bytes), sorted positions [k0, k1)
+  void gather(uint8_t* dst, const void* src, long w, long k0, long k1) const {
+    par_range(k1 - k0, [&](long b, long e, int) {
+      for (long k = k0 + b; k < k0 + e; ++k) copy_row(dst + k * w, (const uint8_t*)src + perm[(size_t)k] * w, w);
+    }, sub());
   }
-  void scatter(void* dst, const uint8_t* src, long w) const {
-    const long n = (long)perm.size();
-    par_range(n, [&](long b, long e) {
-      for (long k = b; k < e; ++k) std::memcpy((uint8_t*)dst + perm[(size_t)k] * w, src + k * w, (size_t)w);
-    });
+  void scatter(void* dst, const uint8_t* src, long w, long k0, long k1) const {
+    par_range(k1 - k0, [&](long b, long e, int) {
+      for (long k = k0 + b; k < k0 + e; ++k) copy_row((uint8_t*)dst + perm[(size_t)k] * w, src + k * w, w);
+    }, sub());
   }
   template <class F>
-  void each_shard(int nsh, F&& f) const {
+  void each_shard(F&& f) const {
     std::vector<std::thread> th;
     for (int j = 0; j < nsh; ++j)
       if (off[(size_t)j + 1] > off[(size_t)j]) th.emplace_back([&, j] { f(j, off[(size_t)j], off[(size_t)j + 1] - off[(size_t)j]); });
@@ -467,11 +496,14 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
   const long ob = 0, vb = a64(n * kstride), lb = vb + a64(n * (long)vstride), sb = lb + a64(n * 4);
   uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
   if (!S) return -1;
-  pl.gather(S + ob, keys, kstride);
-  pl.gather(S + vb, vals, vstride);
-  pl.gather(S + lb, lens, 4);
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
   std::atomic<bool> fail{false};
-  pl.each_shard(nsh, [&](int j, long o, long m) {
+  std::atomic<long> ok{0};
+  pl.each_shard([&](int j, long o, long m) {
+    pl.gather(S + ob, keys, kstride, o, o + m);
+    pl.gather(S + vb, vals, vstride, o, o + m);
+    pl.gather(S + lb, lens, 4, o, o + m);
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + ob + o * kstride;
     const uint8_t* v = S + vb + o * (long)vstride;
@@ -479,15 +511,11 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
     int32_t* st = (int32_t*)(S + sb) + o;
     long r = sh->set_batch(k, kstride, v, vstride, l, m, st, retries);
     if (r == kNoBatch) r = generic_set_batch(sh, k, kstride, v, vstride, l, m, st, retries, 4);
-    if (r < 0) fail = true;
+    if (r < 0) { fail = true; return; }
+    ok += r;
+    pl.scatter(status, S + sb, 4, o, o + m);
   });
-  if (fail) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
-  pl.scatter(status, S + sb, 4);
-  long ok = 0;
-  for (long i = 0; i < n; ++i) ok += status[i] == 0;
-  return ok;
+  return fail ? -1 : ok.load();
 }
 
 long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
@@ -498,9 +526,12 @@ long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostri
   const long ob = 0, sb = a64(n * kstride), lb = sb + a64(n * 4), vb = lb + a64(n * 4);
   uint8_t* S = scratch((size_t)(vb + (out ? a64(n * (long)ostride) : 0)));
   if (!S) return -1;
-  pl.gather(S + ob, keys, kstride);
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
   std::atomic<bool> fail{false};
-  pl.each_shard(nsh, [&](int j, long o, long m) {
+  std::atomic<long> ok{0};
+  pl.each_shard([&](int j, long o, long m) {
+    pl.gather(S + ob, keys, kstride, o, o + m);
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + ob + o * kstride;
     uint8_t* v = out ? S + vb + o * (long)ostride : nullptr;
@@ -508,17 +539,13 @@ long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostri
     int32_t* st = (int32_t*)(S + sb) + o;
     long r = sh->get_batch(k, kstride, v, ostride, l, m, st, retries);
     if (r == kNoBatch) r = generic_get_batch(sh, k, kstride, v, ostride, l, m, st, retries, 4);
-    if (r < 0) fail = true;
+    if (r < 0) { fail = true; return; }
+    ok += r;
+    pl.scatter(status, S + sb, 4, o, o + m);
+    if (out_lens) pl.scatter(out_lens, S + lb, 4, o, o + m);
+    if (out) pl.scatter(out, S + vb, ostride, o, o + m);
   });
-  if (fail) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
-  pl.scatter(status, S + sb, 4);
-  if (out_lens) pl.scatter(out_lens, S + lb, 4);
-  if (out) pl.scatter(out, S + vb, ostride);
-  long ok = 0;
-  for (long i = 0; i < n; ++i) ok += status[i] == 0;
-  return ok;
+  return fail ? -1 : ok.load();
 }
 
 long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,
@@ -529,12 +556,15 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
   const long kb = 0, pb = a64(n * kstride), mb = pb + a64(n * 4), sb = mb + a64(n * 8), rb = sb + a64(n * 4);
   uint8_t* S = scratch((size_t)(rb + a64(n * 8)));
   if (!S) return -1;
-  pl.gather(S + kb, keys, kstride);
-  pl.gather(S + pb, ops, 4);
-  if (masks) pl.gather(S + mb, masks, 8);
-  else std::memset(S + mb, 0, (size_t)(n * 8));
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
   std::atomic<bool> fail{false};
-  pl.each_shard(nsh, [&](int j, long o, long m) {
+  std::atomic<long> ok{0};
+  pl.each_shard([&](int j, long o, long m) {
+    pl.gather(S + kb, keys, kstride, o, o + m);
+    pl.gather(S + pb, ops, 4, o, o + m);
+    if (masks) pl.gather(S + mb, masks, 8, o, o + m);
+    else std::memset(S + mb + o * 8, 0, (size_t)(m * 8));
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + kb + o * kstride;
     const int* op = (const int*)(S + pb) + o;
@@ -543,16 +573,12 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
     uint64_t* rs = results ? (uint64_t*)(S + rb) + o : nullptr;
     long r = sh->intop_batch(k, kstride, op, mk, m, st, rs);
     if (r == kNoBatch) r = generic_intop_batch(sh, k, kstride, op, mk, m, st, rs, 4);
-    if (r < 0) fail = true;
+    if (r < 0) { fail = true; return; }
+    ok += r;
+    pl.scatter(status, S + sb, 4, o, o + m);
+    if (results) pl.scatter(results, S + rb, 8, o, o + m);
   });
-  if (fail) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
-  pl.scatter(status, S + sb, 4);
-  if (results) pl.scatter(results, S + rb, 8);
-  long ok = 0;
-  for (long i = 0; i < n; ++i) ok += status[i] == 0;
-  return ok;
+  return fail ? -1 : ok.load();
 }
 
 long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) {
@@ -562,25 +588,24 @@ long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* 
   const long kb = 0, vb = a64(n * kstride), sb = vb + n * (long)kEmbedBytes;
   uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
   if (!S) return -1;
-  pl.gather(S + kb, keys, kstride);
-  pl.gather(S + vb, vecs, (long)kEmbedBytes);
+  std::vector<int32_t> tmp;
+  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
   std::atomic<bool> fail{false};
-  pl.each_shard(nsh, [&](int j, long o, long m) {
+  std::atomic<long> ok{0};
+  pl.each_shard([&](int j, long o, long m) {
+    pl.gather(S + kb, keys, kstride, o, o + m);
+    pl.gather(S + vb, vecs, (long)kEmbedBytes, o, o + m);
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + kb + o * kstride;
     const float* v = (const float*)(S + vb + o * (long)kEmbedBytes);
     int32_t* st = (int32_t*)(S + sb) + o;
     long r = sh->set_embedding_batch(k, kstride, v, m, st);
     if (r == kNoBatch) r = generic_set_embedding_batch(sh, k, kstride, v, m, nullptr, st, 4);
-    if (r < 0) fail = true;
+    if (r < 0) { fail = true; return; }
+    ok += r;
+    pl.scatter(status, S + sb, 4, o, o + m);
   });
-  if (fail) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
-  pl.scatter(status, S + sb, 4);
-  long ok = 0;
-  for (long i = 0; i < n; ++i) ok += status[i] == 0;
-  return ok;
+  return fail ? -1 : ok.load();
 }
 
 }  // namespace spl

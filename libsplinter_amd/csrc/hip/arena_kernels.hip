@@ -447,76 +447,124 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
 }
 
 // ------------------------------------------------------- fused set + get -----
-// One grid for a whole KV step (spl_kvs_step with SPL_KVS_FUSED=1): the client streams' slices
-// (descriptors) of the set and the get batch are consumed by one launch instead of one dispatch per
-// slice.  With 32 + 32 client streams the per-slice dispatches are capped by the hardware queues
-// (about 2 set and 2 get dispatches resident at a time, profiles/r3_pmc_kv.md), and the step is
-// latency bound (79 % of set wave cycles wait on memory); here every CU holds waves of both kinds
-// at once.  Lane sequence over the concatenated op space [sets | gets] as the carried-retry kernels
-// (op c of a lane: first + (c / U) * stride + c % U): a round's U slots may hold sets and gets side
-// by side, their probes / claims in flight together; the value rows of the two kinds go through two
+// One grid for a whole KV step (spl_kvs_step / spl_kvs_step_xr in fused mode): the step's row
+// segments -- the client streams' slices of the set and the get batch, or a routed step's own rows
+// (through lidx) and every peer's request block -- are consumed by one launch instead of one
+// dispatch per slice.  With 32 + 32 client streams the per-slice dispatches are capped by the
+// hardware queues (about 2 set and 2 get dispatches resident at a time, profiles/r3_pmc_kv.md), and
+// the step is latency bound (79 % of set wave cycles wait on memory); here every CU holds waves of
+// both kinds at once.  The op space is the concatenation of the segments' LIVE rows (a request
+// block's count is read on the device); lane sequence as the carried-retry kernels (op c of a lane:
+// first + (c / U) * stride + c % U): a round's U slots may hold sets and gets side by side, their
+// probes / claims in flight together; the value rows of the two kinds go through two
 // cooperative-copy passes (sets: write-through rows into the arena, as k_set_carry WT; gets: sc1
 // reads of arena rows, as k_get_carry FAST), then sets publish and gets re-validate.
+constexpr int kFusedSegs = 32;  // segments per fused launch (sets + gets; a routed step: 2 x world)
+
+struct FSeg {
+  const char* keys;       // row r's key record at keys + row(r) * ks
+  uint8_t* vals;          // set: input value rows; get: output rows (null: no value output)
+  uint32_t* lens;         // set: input lengths; get: output lengths (nullable)
+  int32_t* status;        // per-row status (nullable)
+  const int32_t* idx;     // row map (own rows of a routed step), null: identity
+  const int32_t* count;   // live rows, read on the device (request blocks), null: n
+  long n;                 // rows (upper bound when count is set)
+  int vstride;            // value row bytes
+  int set;                // 1 set, 0 get
+};
+static_assert(sizeof(FSeg) == 64, "segment record");
+
+struct FSegs {
+  FSeg s[kFusedSegs];
+  int n;
+  int ks;
+};
+
 template <int U, int B, int KW = 16, int OCC = 1>
-__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, const char* skeys, const char* gkeys, int kstride,
-                                                const uint8_t* vals, int vstride, const uint32_t* lens, long n_set,
-                                                int32_t* sstatus, uint8_t* out, int ostride, uint32_t* out_lens,
-                                                long n_get, int32_t* gstatus, int max_retry, uint64_t* stats) {
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, FSegs tab,
+                                                                                         int max_retry, uint64_t* stats) {
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
+  __shared__ FSeg sg[kFusedSegs];
+  __shared__ long sstart[kFusedSegs + 1];
+  const int nseg = tab.n, ks = tab.ks;
+  if ((int)threadIdx.x < nseg) {
+    FSeg f = tab.s[threadIdx.x];
+    if (f.count) {
+      const long c = (long)*f.count;
+      f.n = c < 0 ? 0 : (c < f.n ? c : f.n);
+    }
+    sg[threadIdx.x] = f;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    long run = 0;
+    for (int q = 0; q < nseg; ++q) {
+      sstart[q] = run;
+      run += sg[q].n;
+    }
+    sstart[nseg] = run;
+  }
+  __syncthreads();
   const Arena a = to_dev(aa);
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
   Stats st;
   uint64_t muts = 0;
-  const long n = n_set + n_get;
+  const long n = sstart[nseg];
   const long stride = (long)gridDim.x * blockDim.x * U;
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
   long cursor = 0;
   bool more = true;
   KeyT<KW> k[U];
   Claim c[U];
-  long op[U], sidx[U];
+  long row[U], sidx[U];
+  int seg[U];  // -1: slot empty
   uint64_t e1[U];
   uint32_t len[U];
   int32_t rc[U];
   int tries[U];
   bool set[U];
 #pragma unroll
-  for (int j = 0; j < U; ++j) op[j] = -1;
+  for (int j = 0; j < U; ++j) seg[j] = -1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (;;) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      if (op[j] < 0 && more) {
+      if (seg[j] < 0 && more) {
         const long i = first + (cursor / U) * stride + (cursor % U);
         ++cursor;
         if (i >= n) {
           more = false;
         } else {
-          set[j] = i < n_set;
-          const long r = set[j] ? i : i - n_set;
-          op[j] = r;
+          int q = 0;
+          while (q + 1 < nseg && sstart[q + 1] <= i) ++q;
+          const FSeg& f = sg[q];
+          const long r = i - sstart[q];
+          seg[j] = q;
+          row[j] = f.idx ? (long)f.idx[r] : r;
+          set[j] = f.set != 0;
           tries[j] = 0;
-          load_key(k[j], (set[j] ? skeys : gkeys) + r * (long)kstride, kstride);
-          len[j] = set[j] ? lens[r] : 0u;
+          load_key(k[j], f.keys + row[j] * (long)ks, ks);
+          len[j] = set[j] ? f.lens[row[j]] : 0u;
         }
       }
     }
     bool busy = false;
 #pragma unroll
-    for (int j = 0; j < U; ++j) busy |= op[j] >= 0;
+    for (int j = 0; j < U; ++j) busy |= seg[j] >= 0;
     if (!__syncthreads_or(busy)) break;
     // probes / claims of every slot of the round
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       rc[j] = kInval;
       c[j] = Claim{-1, false, kInval};
-      if (op[j] < 0) continue;
+      if (seg[j] < 0) continue;
       ++st.attempts;
       ++tries[j];
+      const int vs = sg[seg[j]].vstride;
       if (set[j]) {
-        if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride) c[j].rc = kMsgSize;
+        if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vs) c[j].rc = kMsgSize;
         else c[j] = claim_set(a, k[j]);
         rc[j] = c[j].rc;
       } else {
@@ -525,20 +573,21 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
         len[j] = L;
         rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
         if (rc[j] == kOk && ((e1[j] & 1) || L > a.max_val)) rc[j] = kAgain;
-        else if (rc[j] == kOk && out && L > (uint32_t)ostride) rc[j] = kMsgSize;
+        else if (rc[j] == kOk && sg[seg[j]].vals && L > (uint32_t)vs) rc[j] = kMsgSize;
       }
     }
     // value rows: table 0 = sets (client row -> arena, write-through), table 1 = gets (arena -> client)
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      const bool gs = op[j] >= 0 && set[j] && rc[j] == kOk;
-      const bool gg = out && op[j] >= 0 && !set[j] && rc[j] == kOk;
-      const uint64_t ss = gs ? (uint64_t)(vals + op[j] * (long)vstride) : 0;
+      const FSeg* f = seg[j] >= 0 ? &sg[seg[j]] : nullptr;
+      const bool gs = f && set[j] && rc[j] == kOk;
+      const bool gg = f && f->vals && !set[j] && rc[j] == kOk;
+      const uint64_t ss = gs ? (uint64_t)(f->vals + row[j] * (long)f->vstride) : 0;
       const uint64_t sd = gs ? (uint64_t)a.value((size_t)c[j].idx) : 0;
       cp_p[0][w][j * 64 + lane] = make_uint4((uint32_t)ss, (uint32_t)(ss >> 32), (uint32_t)sd, (uint32_t)(sd >> 32));
       cp_l[0][w][j * 64 + lane] = make_uint2(gs ? len[j] : 0u, gs ? set_chunks(a, len[j], scrub, hybrid) : 0u);
       const uint64_t gsrc = gg ? (uint64_t)a.value((size_t)sidx[j]) : 0;
-      const uint64_t gdst = gg ? (uint64_t)(out + op[j] * (long)ostride) : 0;
+      const uint64_t gdst = gg ? (uint64_t)(f->vals + row[j] * (long)f->vstride) : 0;
       const uint32_t n16 = (len[j] + 15) >> 4;
       cp_p[1][w][j * 64 + lane] = make_uint4((uint32_t)gsrc, (uint32_t)(gsrc >> 32), (uint32_t)gdst, (uint32_t)(gdst >> 32));
       cp_l[1][w][j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? n16 : 0u);
@@ -548,7 +597,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     coop_copy<U * 64, 0, true>(cp_p[1][w], cp_l[1][w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
 #pragma unroll
     for (int j = 0; j < U; ++j)
-      if (op[j] >= 0 && set[j] && rc[j] == kOk) write_meta<3>(a, c[j], len[j]);
+      if (seg[j] >= 0 && set[j] && rc[j] == kOk) write_meta<3>(a, c[j], len[j]);
     drain();
     // gets: closing round trip, (hash, epoch) and the key words together
     {
@@ -556,7 +605,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       KeyProbe<KW> kp[U];
 #pragma unroll
       for (int j = 0; j < U; ++j) {
-        const bool live = op[j] >= 0 && !set[j] && rc[j] == kOk;
+        const bool live = seg[j] >= 0 && !set[j] && rc[j] == kOk;
         const uint8_t* s = a.slot(live ? (size_t)sidx[j] : 0);
         he[j] = ld16c(s + kOffHash);
         kp[j].issue(s, k[j]);
@@ -568,18 +617,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       }
 #pragma unroll
       for (int j = 0; j < U; ++j)
-        if (op[j] >= 0 && !set[j] && rc[j] == kOk &&
+        if (seg[j] >= 0 && !set[j] && rc[j] == kOk &&
             (hi64(he[j]) != e1[j] || lo64(he[j]) != k[j].hash || !kp[j].eq(k[j])))
           rc[j] = kAgain;
     }
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      if (op[j] < 0) continue;
+      if (seg[j] < 0) continue;
       const int32_t r = rc[j];
       if (r == kAgain) {
         ++st.again;
         if (tries[j] <= max_retry) continue;  // carried into the next round
       }
+      const FSeg& f = sg[seg[j]];
       if (set[j]) {
         if (r == kOk) {
           finish_set(a, c[j]);
@@ -588,17 +638,34 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
           pulse_masks(a, c[j].wm, c[j].bl);
           mark_dirty(a, (size_t)c[j].idx);
         }
-        if (sstatus) sstatus[op[j]] = r;
       } else {
         if (r == kOk) ++st.ok;
         else if (r == kNoEnt) ++st.miss;
-        if (out_lens) out_lens[op[j]] = r == kOk ? len[j] : 0;
-        if (gstatus) gstatus[op[j]] = r;
+        if (f.lens) f.lens[row[j]] = r == kOk ? len[j] : 0;
       }
-      op[j] = -1;
+      if (f.status) f.status[row[j]] = r;
+      seg[j] = -1;
     }
   }
   flush_stats(a, st, stats, muts);
+}
+
+// Launch the fused grid over `tab` (rows: an upper bound of the live rows); mode 2 with 16-B keys
+// holds them in 4 words at 3 workgroups per CU, otherwise 16 words at 2
+int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_retry, uint64_t* stats,
+                 hipStream_t s) {
+  if (rows <= 0) return 0;
+  const bool kw4 = mode == 2 && tab.ks == 16;
+  static const int wpc_env = env_int("SPL_KVS_FUSED_WG_PER_CU", 0);
+  const int wpc = wpc_env > 0 ? wpc_env : kw4 ? 3 : 2;
+  const long need = (rows + 2 * 256 - 1) / (2 * 256);
+  const long cap = 256L * wpc;
+  const dim3 g((unsigned)(need < cap ? need : cap));
+  if (kw4)
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats);
+  else
+    hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats);
+  return (int)hipGetLastError();
 }
 
 // ------------------------------------------------------------- unset ----
@@ -1090,6 +1157,7 @@ namespace {
 
 struct KvStreams {
   int nw = 0, nr = 0;
+  int fused = 2;  // spl_kvs_set_fused
   std::vector<hipStream_t> s;  // nw writers, then nr readers
   std::vector<hipEvent_t> done;
   hipEvent_t start = nullptr;
@@ -1133,7 +1201,16 @@ void* spl_kvs_create(int writers, int readers) {
     k->done.push_back(ev);
   }
   (void)hipEventCreateWithFlags(&k->start, hipEventDisableTiming);
+  k->fused = env_int("SPL_KVS_FUSED", 2);
   return k;
+}
+
+// 0: one launch per client stream's slice on that stream; 1 / 2: one fused grid (k_kv_fused)
+int spl_kvs_set_fused(void* h, int mode) {
+  auto* k = (KvStreams*)h;
+  if (!k || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  k->fused = mode;
+  return 0;
 }
 
 void spl_kvs_destroy(void* h) {
@@ -1156,22 +1233,18 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
                  int ostride, uint32_t* glens, long n_get, int32_t* gstatus, int max_retry, uint64_t* stats) {
   auto* k = (KvStreams*)h;
   if (!k) return (int)hipErrorInvalidValue;
-  // SPL_KVS_FUSED=1: every stream's slice consumed by ONE grid on the origin stream (k_kv_fused)
-  static const int fused = env_int("SPL_KVS_FUSED", 0);
+  // fused (default): every stream's slice consumed by ONE grid on the origin stream (k_kv_fused):
+  // 100M keys, 32 + 32 streams, 3.96 G ops/s per-slice dispatches (0) -> 4.15 G (1, 16-word keys)
+  // -> 4.85 G (2, 16-B keys in 4 words at 3 workgroups per CU), gpurun_out/r4d bench_kv_fused*.out
+  const int fused = k->fused;
   if (fused && n_set + n_get > 0) {
     if ((kstride & 15) || kstride > 64 || (vstride & 15) || (ostride & 15)) return (int)hipErrorInvalidValue;
-    // resident workgroups per CU: 2 at 194 VGPRs (KW 16), 3 with 16-B keys held in 4 words (<= 168)
-    static const int wpc = env_int("SPL_KVS_FUSED_WG_PER_CU", fused == 2 && kstride == 16 ? 3 : 2);
-    const long need = (n_set + n_get + 2 * 256 - 1) / (2 * 256);
-    const long cap = 256L * (wpc > 0 ? wpc : 8);
-    const dim3 g((unsigned)(need < cap ? need : cap));
-    if (kstride == 16 && fused == 2)  // 16-B keys held as 4 words (fewer VGPRs)
-      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, origin, a, skeys, gkeys, kstride, svals, vstride,
-                         slens, n_set, sstatus, gout, ostride, glens, n_get, gstatus, max_retry, stats);
-    else
-      hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, origin, a, skeys, gkeys, kstride, svals, vstride,
-                         slens, n_set, sstatus, gout, ostride, glens, n_get, gstatus, max_retry, stats);
-    return (int)hipGetLastError();
+    FSegs tab{};
+    tab.ks = kstride;
+    if (n_set > 0)
+      tab.s[tab.n++] = FSeg{skeys, (uint8_t*)svals, (uint32_t*)slens, sstatus, nullptr, nullptr, n_set, vstride, 1};
+    if (n_get > 0) tab.s[tab.n++] = FSeg{gkeys, gout, glens, gstatus, nullptr, nullptr, n_get, ostride, 0};
+    return launch_fused(a, tab, n_set + n_get, fused, max_retry, stats, origin);
   }
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
@@ -1214,9 +1287,42 @@ int spl_kvs_step_xr(void* h, spl_arena_t a, hipStream_t origin, const spl_xr_ste
   if (!k || !x || x->world < 1 || x->world > SPL_XR_MAX_WORLD || x->rank < 0 || x->rank >= x->world ||
       (x->world > 1 && (!x->lidx_set || !x->lidx_get || !x->own_counts || !x->rcounts)))
     return (int)hipErrorInvalidValue;
+  const int W = x->world, r = x->rank;
+  if (k->fused && 2 * W <= kFusedSegs && !(x->ks & 15) && x->ks <= 64 && !(x->svstride & 15) &&
+      !(x->gostride & 15) && !(x->vw & 15)) {
+    // one fused grid over every segment: own rows (in place) and each peer's request block
+    FSegs tab{};
+    tab.ks = x->ks;
+    long rows = 0;
+    for (int kind = 0; kind < 2; ++kind) {
+      const bool set = kind == 0;
+      const long n_own = set ? x->n_set : x->n_get;
+      const long cap = set ? x->cap_s : x->cap_g;
+      const int32_t* lidx = set ? x->lidx_set : x->lidx_get;
+      if (n_own <= 0 && W == 1) continue;
+      for (int sg = 0; sg < W; ++sg) {
+        FSeg f;
+        if (sg == r) {
+          f = set ? FSeg{x->skeys, (uint8_t*)x->svals, (uint32_t*)x->slens, x->sstatus, lidx, nullptr, 0, x->svstride, 1}
+                  : FSeg{x->gkeys, x->gout, x->glens, x->gstatus, lidx, nullptr, 0, x->gostride, 0};
+          f.count = lidx ? x->own_counts + r * 2 + kind : nullptr;
+          f.n = lidx ? cap : n_own;
+        } else {
+          uint8_t* q = (uint8_t*)x->req[sg];
+          uint8_t* p = (uint8_t*)x->resp[sg];
+          f = set ? FSeg{(const char*)(q + x->off_sk), q + x->off_sv, (uint32_t*)(q + x->off_sl),
+                         (int32_t*)(p + x->off_ss), nullptr, x->rcounts + sg * 2 + kind, cap, x->vw, 1}
+                  : FSeg{(const char*)(q + x->off_gk), p + x->off_gv, (uint32_t*)(p + x->off_gl),
+                         (int32_t*)(p + x->off_gs), nullptr, x->rcounts + sg * 2 + kind, cap, x->vw, 0};
+        }
+        tab.s[tab.n++] = f;
+        rows += f.n;
+      }
+    }
+    return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin);
+  }
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
-  const int W = x->world, r = x->rank;
   for (int kind = 0; kind < 2; ++kind) {
     const bool set = kind == 0;
     const long n_own = set ? x->n_set : x->n_get;

@@ -14,15 +14,23 @@
 #include <cstring>
 #include <immintrin.h>
 #include <sched.h>
+#include <fcntl.h>
+#include <linux/futex.h>
+#include <signal.h>
+#include <sys/mman.h>
 #include <sys/prctl.h>
+#include <sys/stat.h>
+#include <sys/syscall.h>
 #include <time.h>
 #include <unistd.h>
 
 #include <set>
+#include <vector>
 #include <shared_mutex>
 
 #include "arena_dev.hpp"
 #include "cmd_ring.hpp"
+#include "store_host.hpp"
 
 namespace spl {
 namespace {
@@ -615,26 +623,8 @@ int effective_cpus() {
 
 }  // namespace
 
-int CmdRing::init(int device, uint32_t pstride) {
-  {
-    std::lock_guard<std::mutex> lk(g_reg_mu);
-    g_rings.insert(this);
-  }
-  device_ = device;
-  pstride_ = (pstride + 15) & ~15u;
-  if (pstride_ < kEmbedBytes) pstride_ = kEmbedBytes;
-  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
-  if (hipHostMalloc((void**)&shared_, sizeof(RingShared), fl) != hipSuccess) return -1;
-  if (hipHostMalloc((void**)&cmds_, sizeof(RingCmd) * kRingEntries, fl) != hipSuccess) return -1;
-  if (hipHostMalloc((void**)&payload_, (size_t)pstride_ * kRingEntries, fl) != hipSuccess) return -1;
-  if (hipMalloc((void**)&scratch_, (size_t)pstride_ * kRingEntries) != hipSuccess) return -1;
-  if (hipMalloc((void**)&ctrl_, 64) != hipSuccess) return -1;
-  std::memset(shared_, 0, sizeof(RingShared));
-  std::memset(cmds_, 0, sizeof(RingCmd) * kRingEntries);
-  int khz = 100000;
-  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
-  clock_khz_ = khz > 0 ? khz : 100000;
-  idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
+void CmdRing::read_env() {
+  pid_ = (int32_t)getpid();
   spread_ = env_int("SPLINTER_RING_SPREAD", 1) != 0;
   yield_after_us_ = (uint64_t)env_int("SPLINTER_RING_SPIN_US", 20);
   cpus_ = effective_cpus();
@@ -644,12 +634,226 @@ int CmdRing::init(int device, uint32_t pstride) {
   // for 8 -> 6 us (means of 3 alternating rounds, profiles/r3_hostapi_sweep_s2.jsonl)
   first_sleep_ns_ = env_int("SPLINTER_RING_FIRST_SLEEP_NS", 6000);
   oversub_spin_us_ = (uint64_t)env_int("SPLINTER_RING_OVERSUB_SPIN_US", 0);
+  adaptive_ = env_int("SPLINTER_RING_ADAPTIVE_SLEEP", 1) != 0;
+}
+
+// Host-side buffers of a private ring: pinned, coherent, device-mapped (host view == device view).
+int CmdRing::alloc_host(size_t) {
+  const unsigned fl = hipHostMallocCoherent | hipHostMallocMapped;
+  if (hipHostMalloc((void**)&shared_, sizeof(RingShared), fl) != hipSuccess) return -1;
+  if (hipHostMalloc((void**)&cmds_, sizeof(RingCmd) * kRingEntries, fl) != hipSuccess) return -1;
+  if (hipHostMalloc((void**)&payload_, (size_t)pstride_ * kRingEntries, fl) != hipSuccess) return -1;
+  std::memset(shared_, 0, sizeof(RingShared));
+  std::memset(cmds_, 0, sizeof(RingCmd) * kRingEntries);
+  d_shared_ = shared_;
+  d_cmds_ = cmds_;
+  d_payload_ = payload_;
+  busy_ = own_.busy;
+  holder_ = own_.holder;
+  seqs_ = own_.seqs;
+  ticket_ = &own_.ticket;
+  return 0;
+}
+
+int CmdRing::init(int device, uint32_t pstride) {
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_rings.insert(this);
+  }
+  device_ = device;
+  pstride_ = (pstride + 15) & ~15u;
+  if (pstride_ < kEmbedBytes) pstride_ = kEmbedBytes;
+  read_env();
+  if (alloc_host(0) != 0) return -1;
+  if (hipMalloc((void**)&scratch_, (size_t)pstride_ * kRingEntries) != hipSuccess) return -1;
+  if (hipMalloc((void**)&ctrl_, 64) != hipSuccess) return -1;
+  int khz = 100000;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+  clock_khz_ = khz > 0 ? khz : 100000;
+  idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
 #ifndef SPL_RING_POLL4
   // default on: 1 thread p50 9.1 -> 7.3 us, 16 threads 1.18 -> 1.50 M ops/s (profiles/r3_hostapi_vram_ab.jsonl);
   // SPLINTER_RING_VRAM=0, or a failed VMM / BAR mapping, keeps everything in host memory
   if (env_int("SPLINTER_RING_VRAM", 1) != 0 && init_vram() != 0) vr_ = false;
 #endif
+  if (vr_) {
+    if (hipHostMalloc((void**)&vdone_, sizeof(RingDone) * kRingEntries, hipHostMallocCoherent | hipHostMallocMapped) !=
+        hipSuccess)
+      return -1;
+    std::memset(vdone_, 0, sizeof(RingDone) * kRingEntries);
+    d_vdone_ = vdone_;
+  }
   return 0;
+}
+
+namespace {
+// segment layout: header | RingShared | RingCmd[entries] | RingDone[entries] | payload
+struct SegLayout {
+  size_t shared, cmds, done, pay, total;
+  explicit SegLayout(uint32_t pstride) {
+    auto up = [](size_t v, size_t a) { return (v + a - 1) / a * a; };
+    shared = up(sizeof(RingSegHdr), 4096);
+    cmds = up(shared + sizeof(RingShared), 4096);
+    done = up(cmds + sizeof(RingCmd) * kRingEntries, 4096);
+    pay = up(done + sizeof(RingDone) * kRingEntries, 4096);
+    total = up(pay + (size_t)pstride * kRingEntries, 4096);
+  }
+};
+
+long futex_op(uint32_t* w, int op, uint32_t v, const timespec* ts) {
+  return syscall(SYS_futex, w, op, v, ts, nullptr, 0);
+}
+}  // namespace
+
+int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, const std::string& perm_path,
+                         const spl_arena_t& a) {
+  {
+    std::lock_guard<std::mutex> lk(g_reg_mu);
+    g_rings.insert(this);
+  }
+  mode_ = kServer;  // (a partial set-up is torn down as a server's)
+  device_ = device;
+  pstride_ = (pstride + 15) & ~15u;
+  if (pstride_ < kEmbedBytes) pstride_ = kEmbedBytes;
+  read_env();
+  arena_ = a;
+  if (hipMalloc((void**)&scratch_, (size_t)pstride_ * kRingEntries) != hipSuccess) return -1;
+  if (hipMalloc((void**)&ctrl_, 64) != hipSuccess) return -1;
+  int khz = 100000;
+  (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
+  clock_khz_ = khz > 0 ? khz : 100000;
+  idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
+  if (init_vram() != 0) return -1;
+  // the segment: created under the store's umask like its descriptor, fresh (a stale one of a
+  // crashed owner of the same name is truncated away), registered for the worker's stores
+  const SegLayout L(pstride_);
+  mode_t prev = env_umask_push();
+  const int fd = shm_open(seg.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  env_umask_pop(prev);
+  if (fd < 0) return -1;
+  if (ftruncate(fd, 0) != 0 || ftruncate(fd, (off_t)L.total) != 0) { close(fd); shm_unlink(seg.c_str()); return -1; }
+  void* p = mmap(nullptr, L.total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) { shm_unlink(seg.c_str()); return -1; }
+  seg_ = (RingSegHdr*)p;
+  seg_bytes_ = L.total;
+  seg_name_ = seg;
+  if (hipHostRegister(p, L.total, hipHostRegisterMapped) != hipSuccess) return -1;
+  seg_registered_ = true;
+  uint8_t* dp = nullptr;
+  if (hipHostGetDevicePointer((void**)&dp, p, 0) != hipSuccess) return -1;
+  uint8_t* hp = (uint8_t*)p;
+  shared_ = (RingShared*)(hp + L.shared);
+  d_shared_ = (RingShared*)(dp + L.shared);
+  cmds_ = (RingCmd*)(hp + L.cmds);
+  d_cmds_ = (RingCmd*)(dp + L.cmds);
+  vdone_ = (RingDone*)(hp + L.done);
+  d_vdone_ = (RingDone*)(dp + L.done);
+  payload_ = hp + L.pay;
+  d_payload_ = dp + L.pay;
+  busy_ = seg_->busy;
+  holder_ = seg_->holder;
+  seqs_ = seg_->seqs;
+  ticket_ = &seg_->ticket;
+  // the request chunk's descriptors, for clients' BAR mappings
+  char sock[96];
+  snprintf(sock, sizeof sock, "splinter-ring-%d-%s", (int)getpid(), seg.c_str() + (seg[0] == '/'));
+  if (vram_.serve(sock, perm_path) != 0) return -1;
+  std::memcpy(seg_->sock, sock, sizeof sock);
+  seg_->pstride = pstride_;
+  seg_->entries = kRingEntries;
+  seg_->version = 1;
+  seg_->owner_pid = pid_;
+  sup_ = std::thread([this] { supervise(); });
+  __atomic_store_n(&seg_->magic, kRingSegMagic, __ATOMIC_RELEASE);
+  return 0;
+}
+
+// The owner's supervisor: sleeps on the `want` futex; a client that found the worker gone bumps
+// it, and the worker is relaunched here (only the owner's HIP runtime holds the arena mapping the
+// worker runs on).  The 20 ms timeout only re-checks the stop flag.
+void CmdRing::supervise() {
+  uint32_t seen = __atomic_load_n(&seg_->want, __ATOMIC_ACQUIRE);
+  while (!sup_stop_.load(std::memory_order_acquire)) {
+    const timespec ts{0, 20 * 1000 * 1000};
+    (void)futex_op(&seg_->want, FUTEX_WAIT, seen, &ts);
+    const uint32_t w = __atomic_load_n(&seg_->want, __ATOMIC_ACQUIRE);
+    if (w == seen || sup_stop_.load(std::memory_order_acquire)) continue;
+    seen = w;
+    std::shared_lock<std::shared_mutex> gate(g_gate);  // not while this process sets up a store
+    if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(arena_);
+  }
+}
+
+int CmdRing::init_client(const std::string& seg, int device, uint32_t pstride) {
+  const int fd = shm_open(seg.c_str(), O_RDWR | O_CLOEXEC, 0666);
+  if (fd < 0) return -1;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || (size_t)st.st_size < sizeof(RingSegHdr)) { close(fd); return -1; }
+  void* p = mmap(nullptr, (size_t)st.st_size, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+  close(fd);
+  if (p == MAP_FAILED) return -1;
+  seg_ = (RingSegHdr*)p;
+  seg_bytes_ = (size_t)st.st_size;
+  auto fail = [this]() {
+    if (cmap_) munmap(cmap_, cmap_bytes_);
+    cmap_ = nullptr;
+    munmap(seg_, seg_bytes_);
+    seg_ = nullptr;
+    return -1;
+  };
+  if (__atomic_load_n(&seg_->magic, __ATOMIC_ACQUIRE) != kRingSegMagic || seg_->entries != (uint32_t)kRingEntries)
+    return fail();
+  const SegLayout L(seg_->pstride);
+  if (L.total > seg_bytes_ || seg_->pstride < ((pstride + 15) & ~15u) || server_gone()) return fail();
+  pstride_ = seg_->pstride;
+  std::vector<int> fds;
+  size_t chunk = 0;
+  char sock[97] = {0};
+  std::memcpy(sock, seg_->sock, 96);
+  if (VmmArena::fetch(sock, &fds, &chunk) != 0 || fds.empty()) return fail();
+  const size_t total = chunk * fds.size();
+  void* r = mmap(nullptr, total, PROT_NONE, MAP_PRIVATE | MAP_ANONYMOUS | MAP_NORESERVE, -1, 0);
+  bool ok = r != MAP_FAILED;
+  for (size_t i = 0; ok && i < fds.size(); ++i)
+    ok = mmap((uint8_t*)r + i * chunk, chunk, PROT_READ | PROT_WRITE, MAP_SHARED | MAP_FIXED, fds[i], 0) != MAP_FAILED;
+  for (int f : fds) close(f);
+  if (!ok) {
+    if (r != MAP_FAILED) munmap(r, total);
+    return fail();
+  }
+  cmap_ = r;
+  cmap_bytes_ = total;
+  const size_t door_b = 4096, cmd_b = sizeof(RingCmd) * kRingEntries;
+  uint8_t* h = (uint8_t*)r;
+  v_door_h_ = (uint32_t*)h;
+  v_cmds_h_ = (RingCmd*)(h + door_b);
+  v_pay_h_ = h + door_b + cmd_b;
+  uint8_t* hp = (uint8_t*)p;
+  shared_ = (RingShared*)(hp + L.shared);
+  cmds_ = (RingCmd*)(hp + L.cmds);
+  vdone_ = (RingDone*)(hp + L.done);
+  payload_ = hp + L.pay;
+  busy_ = seg_->busy;
+  holder_ = seg_->holder;
+  seqs_ = seg_->seqs;
+  ticket_ = &seg_->ticket;
+  device_ = device;
+  read_env();
+  vr_ = true;
+  mode_ = kClient;
+  return 0;
+}
+
+bool CmdRing::server_gone() const {
+  if (__atomic_load_n(&seg_->magic, __ATOMIC_ACQUIRE) != kRingSegMagic) return true;
+  const int32_t o = seg_->owner_pid;
+  return o <= 0 || (kill(o, 0) != 0 && errno == ESRCH);
+}
+
+void CmdRing::want_worker() {
+  __atomic_fetch_add(&seg_->want, 1u, __ATOMIC_RELEASE);
+  (void)futex_op(&seg_->want, FUTEX_WAKE, 1, nullptr);
 }
 
 // The request side in device memory: one VMM chunk (2 MiB granules) exported as a dmabuf and
@@ -662,10 +866,6 @@ int CmdRing::init_vram() {
   if (!h) return -1;
   uint8_t* d = (uint8_t*)vram_.base();
   if (hipMalloc((void**)&served_, sizeof(uint32_t) * kRingEntries) != hipSuccess) return -1;
-  if (hipHostMalloc((void**)&vdone_, sizeof(RingDone) * kRingEntries, hipHostMallocCoherent | hipHostMallocMapped) !=
-      hipSuccess)
-    return -1;
-  std::memset(vdone_, 0, sizeof(RingDone) * kRingEntries);
   // the clears go on a private non-blocking stream and only that stream is waited for: a device-wide
   // synchronize (or a null-stream memset) would also wait for every other store's resident ring
   // worker and for unrelated kernels, so opening a second store beside live traffic could block
@@ -690,7 +890,7 @@ void CmdRing::launch(const spl_arena_t& a) {
   std::lock_guard<std::mutex> lk(launch_mu_);
   if (__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) return;
   __atomic_store_n(&shared_->alive, 1u, __ATOMIC_RELEASE);
-  __atomic_fetch_add(&shared_->launches, 1u, __ATOMIC_RELAXED);
+  __atomic_fetch_add(seg_ ? &seg_->launches : &shared_->launches, 1u, __ATOMIC_RELAXED);
   int cur = 0;
   (void)hipGetDevice(&cur);
   if (cur != device_) (void)hipSetDevice(device_);
@@ -703,11 +903,11 @@ void CmdRing::launch(const spl_arena_t& a) {
   const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)kRingGroups};
   (void)hipMemcpyAsync(ctrl_, init, sizeof init, hipMemcpyHostToDevice, stream_);
   if (vr_)
-    hipLaunchKernelGGL(k_ring_worker<true>, dim3(kRingGroups), dim3(64), 0, stream_, a, v_cmds_d_, cmds_, shared_,
-                       v_door_d_, v_pay_d_, payload_, pstride_, scratch_, ctrl_, served_, vdone_, idle_ticks_);
+    hipLaunchKernelGGL(k_ring_worker<true>, dim3(kRingGroups), dim3(64), 0, stream_, a, v_cmds_d_, d_cmds_, d_shared_,
+                       v_door_d_, v_pay_d_, d_payload_, pstride_, scratch_, ctrl_, served_, d_vdone_, idle_ticks_);
   else
-    hipLaunchKernelGGL(k_ring_worker<false>, dim3(kRingGroups), dim3(64), 0, stream_, a, cmds_, cmds_, shared_,
-                       (const uint32_t*)nullptr, (const uint8_t*)nullptr, payload_, pstride_, scratch_, ctrl_,
+    hipLaunchKernelGGL(k_ring_worker<false>, dim3(kRingGroups), dim3(64), 0, stream_, a, d_cmds_, d_cmds_, d_shared_,
+                       (const uint32_t*)nullptr, (const uint8_t*)nullptr, d_payload_, pstride_, scratch_, ctrl_,
                        (uint32_t*)nullptr, (RingDone*)nullptr, idle_ticks_);
   if (cur != device_) (void)hipSetDevice(cur);
 }
@@ -715,19 +915,45 @@ void CmdRing::launch(const spl_arena_t& a) {
 int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen,
                   uint64_t khash, const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap,
                   RingResult* r) {
+  if (mode_ == kClient && (gone_.load(std::memory_order_acquire) || server_gone())) {
+    // the owner closed the store or died: this process serves itself from now on (the arena it
+    // imported stays valid in VMM mode)
+    gone_.store(true, std::memory_order_release);
+    std::unique_lock<std::mutex> lk(priv_mu_);
+    if (!priv_) {
+      RingQuiesce quiet;  // ring set-up makes HIP calls: as for a store set-up
+      auto p = std::make_unique<CmdRing>();
+      if (p->init(device_, pstride_) != 0) { errno = EIO; return -1; }
+      priv_ = std::move(p);
+    }
+    CmdRing* pr = priv_.get();
+    lk.unlock();
+    return pr->call(a, op, sub, key64, klen, khash, in, in_len, arg, out, out_cap, r);
+  }
+  return call_private(a, op, sub, key64, klen, khash, in, in_len, arg, out, out_cap, r);
+}
+
+int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen,
+                          uint64_t khash, const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap,
+                          RingResult* r) {
   if (in_len > pstride_) { errno = EMSGSIZE; return -1; }
   std::shared_lock<std::shared_mutex> gate(g_gate, std::defer_lock);
   if (!t_exclusive) gate.lock();  // (a store set-up on this thread already holds it exclusive)
-  // own an entry: start at a rotating ticket, CAS the host-only busy flag.  Consecutive tickets
-  // map to different groups (entry = (t % groups) * per_group + t / groups), so concurrent
-  // callers land on different worker waves -- which run in parallel -- instead of sharing one
-  // wave whose lanes would serve them with divergent ops
+  // own an entry: start at a rotating ticket, CAS the busy flag (in the shared segment for a ring
+  // server: every process's callers draw from one ticket).  Consecutive tickets map to different
+  // groups (entry = (t % groups) * per_group + t / groups), so concurrent callers land on
+  // different worker waves -- which run in parallel -- instead of sharing one wave whose lanes
+  // would serve them with divergent ops
   const bool spread = spread_;
   auto entry_of = [spread](uint32_t t) {
     t %= kRingEntries;
     return spread ? (t % kRingGroups) * kGroupEntries + t / kRingGroups : t;
   };
-  uint32_t t = ticket_.fetch_add(1, std::memory_order_relaxed);
+  auto finished = [this](uint32_t e) {
+    return vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == __atomic_load_n(&seqs_[e], __ATOMIC_ACQUIRE)
+               : __atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == (uint32_t)kRingDone;
+  };
+  uint32_t t = __atomic_fetch_add(ticket_, 1u, __ATOMIC_RELAXED);
   uint32_t e = entry_of(t);
   timespec t0;
   clock_gettime(CLOCK_MONOTONIC, &t0);
@@ -738,18 +964,19 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   };
   for (uint32_t spins = 0;; ++spins) {
     uint32_t z = 0;
-    if (busy_[e].compare_exchange_weak(z, 1u, std::memory_order_acquire)) break;
+    if (__atomic_compare_exchange_n(&busy_[e], &z, 1u, true, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) break;
     // an entry a timed-out caller abandoned (busy 2) is reclaimed once the worker has finished it
     z = 2;
-    const bool finished = vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == seqs_[e]
-                              : __atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == (uint32_t)kRingDone;
-    if (finished &&
-        busy_[e].compare_exchange_strong(z, 1u, std::memory_order_acquire)) {
+    if (finished(e) && __atomic_compare_exchange_n(&busy_[e], &z, 1u, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) {
       if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
       break;
     }
-    e = entry_of(++t);
     if ((spins & 63) == 63) {
+      // an entry held by a process that died is abandoned (its call is reclaimed once finished)
+      const int32_t h = __atomic_load_n(&holder_[e], __ATOMIC_RELAXED);
+      z = 1;
+      if (mode_ != kPrivate && h > 0 && h != pid_ && kill(h, 0) != 0 && errno == ESRCH)
+        (void)__atomic_compare_exchange_n(&busy_[e], &z, 2u, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
       _mm_pause();
       if (elapsed_us() > 30000000u) {  // every entry held for 30 s: the GPU stopped serving
         errno = EBUSY;
@@ -757,7 +984,9 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
       }
       sched_yield();
     }
+    e = entry_of(++t);
   }
+  __atomic_store_n(&holder_[e], pid_, __ATOMIC_RELAXED);
   RingCmd* c = cmds_ + e;
   uint32_t done_word = kRingDone;
   if (vr_) {
@@ -777,7 +1006,7 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     c->out_len = 0;  // written by the worker only when the op returns bytes
     uint32_t seq = seqs_[e] + 1;
     if (seq == 0) seq = 1;  // 0 is the initial "served" value
-    seqs_[e] = seq;
+    __atomic_store_n(&seqs_[e], seq, __ATOMIC_RELEASE);
     done_word = seq;
     _mm_sfence();
     *(volatile uint32_t*)(v_door_h_ + e) = seq;
@@ -794,7 +1023,12 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     if (in && in_len) std::memcpy(payload_ + (size_t)e * pstride_, in, in_len);
     __atomic_store_n(&shared_->state[e], (uint32_t)kRingReady, __ATOMIC_RELEASE);
   }
-  if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);
+  auto ensure_worker = [&]() {
+    if (__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) return;
+    if (mode_ == kClient) want_worker();
+    else launch(mode_ == kServer ? arena_ : a);
+  };
+  ensure_worker();
   clock_gettime(CLOCK_MONOTONIC, &t0);
   // Wait for completion: spin (a call is served in ~10 us), then give the CPU away between polls.
   // With more waiting callers than CPUs the process may run on (cgroup quota included), spinning
@@ -825,7 +1059,14 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
             (void)prctl(PR_SET_TIMERSLACK, 1000UL, 0, 0, 0);
             slack = true;
           }
-          const timespec ts{0, slept ? sleep_ns_ : first_sleep_ns_};
+          // the first sleep covers most of a call's expected latency under this load (EWMA of
+          // recent oversubscribed calls): one or two wakeups per call instead of one per ~5 us
+          long first = first_sleep_ns_;
+          if (adaptive_) {
+            const long est = ewma_ns_.load(std::memory_order_relaxed) * 5 / 8;
+            if (est > first) first = est < 100000 ? est : 100000;
+          }
+          const timespec ts{0, slept ? sleep_ns_ : first};
           slept = true;
           nanosleep(&ts, nullptr);
         } else {
@@ -833,14 +1074,21 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
         }
       }
       if ((spins & 1023) == 0) {
-        if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(a);  // worker idled out meanwhile
-        if (us > 30000000u) {  // the GPU stopped serving: abandon the entry (reclaimed once done)
-          busy_[e].store(2u, std::memory_order_release);
-          errno = ETIMEDOUT;
+        ensure_worker();  // the worker idled out meanwhile
+        const bool dead = mode_ == kClient && server_gone();
+        if (dead || us > 30000000u) {  // the GPU stopped serving: abandon the entry (reclaimed once done)
+          __atomic_store_n(&busy_[e], 2u, __ATOMIC_RELEASE);
+          if (dead) gone_.store(true, std::memory_order_release);
+          errno = dead ? EIO : ETIMEDOUT;
           return -1;
         }
       }
     }
+  }
+  if (slept && adaptive_) {  // latency of an oversubscribed call, for the next first sleeps
+    const long ns = (long)elapsed_us() * 1000;
+    const long o = ewma_ns_.load(std::memory_order_relaxed);
+    ewma_ns_.store(o + (ns - o) / 8, std::memory_order_relaxed);
   }
   if (vr_) {
     r->status = vdone_[e].status;
@@ -856,12 +1104,15 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   if (out && out_cap && r->out_len && r->status >= 0)
     std::memcpy(out, payload_ + (size_t)e * pstride_, r->out_len < out_cap ? r->out_len : out_cap);
   if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
-  busy_[e].store(0, std::memory_order_release);
+  __atomic_store_n(&busy_[e], 0u, __ATOMIC_RELEASE);
   return 0;
 }
 
 void CmdRing::stop() {
-  if (!shared_) return;
+  if (!shared_ || mode_ == kClient) {  // a client's only worker is its private fallback's
+    if (priv_) priv_->stop();
+    return;
+  }
   __atomic_store_n(&shared_->stop, 1u, __ATOMIC_RELEASE);
   if (stream_) (void)hipStreamSynchronize(stream_);
   __atomic_store_n(&shared_->stop, 0u, __ATOMIC_RELEASE);
@@ -871,6 +1122,22 @@ CmdRing::~CmdRing() {
   {
     std::lock_guard<std::mutex> lk(g_reg_mu);
     g_rings.erase(this);
+  }
+  priv_.reset();
+  if (mode_ == kClient) {
+    if (cmap_) munmap(cmap_, cmap_bytes_);
+    if (seg_) munmap(seg_, seg_bytes_);
+    return;
+  }
+  if (mode_ == kServer) {
+    // clients see the segment close first (their calls then fail over to private rings), then
+    // the supervisor and the worker stop
+    if (seg_) __atomic_store_n(&seg_->magic, 0u, __ATOMIC_RELEASE);
+    sup_stop_.store(true, std::memory_order_release);
+    if (sup_.joinable()) {
+      want_worker();
+      sup_.join();
+    }
   }
   stop();
 #ifdef SPL_RING_STAMPS
@@ -902,9 +1169,18 @@ CmdRing::~CmdRing() {
 #endif
   if (stream_) (void)hipStreamDestroy(stream_);
   if (served_) (void)hipFree(served_);
-  if (vdone_) (void)hipHostFree(vdone_);
   if (ctrl_) (void)hipFree(ctrl_);
   if (scratch_) (void)hipFree(scratch_);
+  if (mode_ == kServer) {
+    vram_.release();
+    if (seg_) {
+      if (seg_registered_) (void)hipHostUnregister(seg_);
+      munmap(seg_, seg_bytes_);
+      shm_unlink(seg_name_.c_str());
+    }
+    return;
+  }
+  if (vdone_) (void)hipHostFree(vdone_);
   if (payload_) (void)hipHostFree(payload_);
   if (cmds_) (void)hipHostFree(cmds_);
   if (shared_) (void)hipHostFree(shared_);

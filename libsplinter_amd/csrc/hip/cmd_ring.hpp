@@ -12,6 +12,12 @@
 //     with little op divergence inside a wave.  (One kernel, not one per group: streams share
 //     GPU_MAX_HW_QUEUES hardware queues, and a group queued behind another group's resident
 //     kernel would wait out that kernel's idle timeout.)
+// Ring server: the process that created the store (its owner) runs the store's ONE worker and
+// keeps the host side of the ring in a shared segment (RingSegHdr below); every other process that
+// opens the store submits its calls to that worker instead of launching its own, so a GPU carries
+// one polling worker per store, not one per client process, and the callers of every process share
+// the same wave rounds.  SPLINTER_RING_SHARED=0 (or a store without VMM chunks) keeps a worker
+// per process.
 // Host callers take entries in ticket order spread over the groups (consecutive calls land on
 // different waves, so up to kRingGroups concurrent callers are served in parallel waves, not
 // as divergent lanes of one wave): 1 thread p50 11.7 us, 16 threads 1.02 M ops/s at p50 14.9 us
@@ -36,7 +42,10 @@
 #include <atomic>
 #include <cstddef>
 #include <cstdint>
+#include <memory>
 #include <mutex>
+#include <string>
+#include <thread>
 
 #include "arena_api.h"
 #include "vmm_share.hpp"
@@ -125,12 +134,45 @@ class RingQuiesce {
   bool held_ = false;
 };
 
+// Shared ring segment of a store's ring SERVER: POSIX shm "<store>.ring", created by the store's
+// owner (the process that created the arena) and mapped by every process that opens the store.
+// It holds the host-side half of the ring -- entry ownership, sequence numbers, completion chunks,
+// output payloads, the worker's control words -- registered with the owner's HIP runtime so its one
+// resident worker writes completions straight into it; the request side (records, input payloads,
+// doorbells) is the owner's VRAM chunk, which every client maps through the PCIe BAR (dmabuf fds
+// from the owner's socket, `sock`).  A client process runs no worker kernel at all: it rings the
+// doorbell and, when the worker has idled out, bumps `want` (a futex) for the owner's supervisor
+// thread to relaunch it.  So a GPU carries one polling worker per store however many processes
+// issue per-call ops, and concurrent callers of every process are served in the same wave rounds.
+struct RingSegHdr {
+  uint32_t magic, version, pstride, entries;
+  int32_t owner_pid;
+  uint32_t want;     // futex word: bumped by a client that found the worker gone
+  uint32_t ticket;   // entry tickets of every process
+  uint32_t launches;
+  char sock[96];     // abstract socket serving the request chunk's dmabuf fds
+  uint32_t busy[kRingEntries];    // 0 free, 1 held, 2 abandoned (reclaimed once its call is done)
+  int32_t holder[kRingEntries];   // pid holding the entry (dead holders' entries are reclaimed)
+  uint32_t seqs[kRingEntries];    // last sequence number issued per entry
+};
+constexpr uint32_t kRingSegMagic = 0x52494e47;  // "RING"
+
 class CmdRing {
  public:
-  // device: ordinal of the arena's GPU; pstride: payload bytes per entry (>= max value, vector)
+  // Private ring of this process (its own worker).  device: ordinal of the arena's GPU; pstride:
+  // payload bytes per entry (>= max value, vector)
   int init(int device, uint32_t pstride);
+  // Ring server of a store this process owns: the private ring's worker, with its host side in the
+  // shared segment `seg` (shm name) so other processes can submit to it.  `perm_path`: file whose
+  // mode admits peers to the request chunk (the store's descriptor).  Needs the VRAM request mode.
+  int init_server(int device, uint32_t pstride, const std::string& seg, const std::string& perm_path,
+                  const spl_arena_t& a);
+  // Client of another process's (or this process's) ring server; no HIP call.  -1: no live server.
+  int init_client(const std::string& seg, int device, uint32_t pstride);
   ~CmdRing();
   bool ready() const { return shared_ != nullptr; }
+  bool shared_mode() const { return mode_ != kPrivate; }
+  int mode() const { return (int)mode_; }  // 0 private, 1 ring server, 2 client of a server
   // Blocking call: stage key / input, ring the doorbell, wait for DONE.  `in` may be null;
   // `out` (may be null) receives min(out_len, out_cap) payload bytes.  Returns 0 when the op ran
   // (its own status in r.status), -1 on a ring failure (errno set; e.g. ETIMEDOUT).
@@ -138,16 +180,42 @@ class CmdRing {
   int call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen, uint64_t khash,
            const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap, RingResult* r);
   void stop();
-  uint32_t launches() const { return shared_ ? shared_->launches : 0; }
+  uint32_t launches() const { return seg_ ? seg_->launches : shared_ ? shared_->launches : 0; }
 
  private:
+  enum Mode { kPrivate, kServer, kClient };
   void launch(const spl_arena_t& a);
-  RingShared* shared_ = nullptr;  // pinned host (coherent)
-  RingCmd* cmds_ = nullptr;       // pinned host (coherent)
-  uint8_t* payload_ = nullptr;    // pinned host (coherent), kRingEntries x pstride_
+  void want_worker();        // client: ask the owner's supervisor for a worker
+  bool server_gone() const;  // client: the owner closed the store or died
+  void supervise();          // server: relaunch the worker when a client asks
+  int call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen,
+                   uint64_t khash, const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap,
+                   RingResult* r);
+  int alloc_host(size_t seg_bytes);
+  Mode mode_ = kPrivate;
+  // host side: host / device views (the same pointer in the private ring's pinned allocations)
+  RingShared* shared_ = nullptr;  // worker control words (alive, stop)
+  RingShared* d_shared_ = nullptr;
+  RingCmd* cmds_ = nullptr;       // completion words (out_len) / the whole records (host mode)
+  RingCmd* d_cmds_ = nullptr;
+  uint8_t* payload_ = nullptr;    // output payloads, kRingEntries x pstride_
+  uint8_t* d_payload_ = nullptr;
+  RingDone* vdone_ = nullptr;     // VRAM mode completion chunks
+  RingDone* d_vdone_ = nullptr;
+  uint32_t* busy_ = nullptr;      // entry ownership (own_ or the segment)
+  int32_t* holder_ = nullptr;
+  uint32_t* seqs_ = nullptr;
+  uint32_t* ticket_ = nullptr;
+  struct Own {
+    uint32_t busy[kRingEntries] = {};
+    int32_t holder[kRingEntries] = {};
+    uint32_t seqs[kRingEntries] = {};
+    uint32_t ticket = 0;
+  } own_;
   uint8_t* scratch_ = nullptr;    // device, kRingEntries x pstride_ (+64 key)
   uint32_t pstride_ = 0;
   int device_ = 0;
+  int32_t pid_ = 0;
   uint64_t idle_ticks_ = 0;
   int clock_khz_ = 100000;
   bool spread_ = true;            // SPLINTER_RING_SPREAD: consecutive calls on different waves
@@ -165,18 +233,30 @@ class CmdRing {
   uint32_t* v_door_d_ = nullptr;
   uint8_t* v_pay_d_ = nullptr;
   uint32_t* served_ = nullptr;    // device: last sequence number served per entry
-  RingDone* vdone_ = nullptr;     // host (pinned, coherent): completion chunks
-  uint32_t seqs_[kRingEntries] = {};  // host: last sequence number issued per entry
   int init_vram();
+  // shared segment (server / client)
+  RingSegHdr* seg_ = nullptr;
+  size_t seg_bytes_ = 0;
+  std::string seg_name_;
+  bool seg_registered_ = false;
+  void* cmap_ = nullptr;          // client: BAR mapping of the owner's request chunk
+  size_t cmap_bytes_ = 0;
+  std::thread sup_;               // server: supervisor
+  std::atomic<bool> sup_stop_{false};
+  spl_arena_t arena_{};           // server: the arena its worker serves
+  std::atomic<bool> gone_{false}; // client: the server went away; calls use priv_
+  std::unique_ptr<CmdRing> priv_;
+  std::mutex priv_mu_;
   std::atomic<int> waiters_{0};   // host threads waiting on a completion right now
   long sleep_ns_ = 5000;          // SPLINTER_RING_SLEEP_NS: sleep between polls while oversubscribed
   long first_sleep_ns_ = 6000;    // SPLINTER_RING_FIRST_SLEEP_NS: the first of those sleeps (a call's bulk)
   uint64_t oversub_spin_us_ = 0;  // SPLINTER_RING_OVERSUB_SPIN_US: spin this long first while oversubscribed
+  bool adaptive_ = true;          // SPLINTER_RING_ADAPTIVE_SLEEP: first sleep from the latency EWMA
+  std::atomic<long> ewma_ns_{0};  // latency of recent oversubscribed calls
   uint8_t* ctrl_ = nullptr;       // device: {u64 last activity, u32 dying, u32 live waves}
   hipStream_t stream_ = nullptr;
-  std::atomic<uint32_t> busy_[kRingEntries] = {};
-  std::atomic<uint32_t> ticket_{0};
   std::mutex launch_mu_;
+  void read_env();
 };
 
 }  // namespace spl

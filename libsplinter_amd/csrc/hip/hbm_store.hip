@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <atomic>
+#include <memory>
 #include <mutex>
 #include <poll.h>
 #include <string>
@@ -119,7 +120,8 @@ class HbmStore final : public StoreBase {
     return a;
   }
   hipStream_t stream() const { return stream_; }
-  uint32_t ring_launches() const { return ring_.launches(); }
+  uint32_t ring_launches() const { return ring_ ? ring_->launches() : 0; }
+  int ring_mode() const { return ring_ ? ring_->mode() : -1; }
 
   int set_mop(unsigned mode) override {
     switch (mode) {
@@ -495,8 +497,8 @@ class HbmStore final : public StoreBase {
     } else {
       std::memset(k, 0, 64);
     }
-    if (!ring_.ready()) { errno = ENOSYS; return -1; }
-    return ring_.call(arena(), op, sub, k, klen, khash, in, in_len, arg, out, out_cap, r);
+    if (!ring_ || !ring_->ready()) { errno = ENOSYS; return -1; }
+    return ring_->call(arena(), op, sub, k, klen, khash, in, in_len, arg, out, out_cap, r);
   }
   static int st_ret(int32_t st) {
     if (st == 0) return 0;
@@ -645,7 +647,7 @@ class HbmStore final : public StoreBase {
   std::thread proxy_;
   std::atomic<bool> proxy_stop_{false};
   size_t vstride_ = 0;
-  CmdRing ring_;
+  std::unique_ptr<CmdRing> ring_;
   uint8_t* h_u32_ = nullptr;
   uint32_t* d_scan_idx_ = nullptr;
   uint64_t* d_scan_ep_ = nullptr;
@@ -675,7 +677,6 @@ int HbmStore::setup_buffers() {
   if (vstride_ < 128) vstride_ = 128;
   HIPCHECK(hipHostMalloc((void**)&h_u32_, 64));
   if (getenv("SPLINTER_HBM_NO_RING")) return 0;  // diagnosis only: batch kernels, no per-call API
-  if (ring_.init(device_, (uint32_t)std::max<size_t>(vstride_, kEmbedBytes)) != 0) return -1;
   // the shared descriptor page(s) become device-visible: kernels of every attached process
   // store the event-bus notify word there
   const size_t pg = (size_t)sysconf(_SC_PAGESIZE);
@@ -685,7 +686,21 @@ int HbmStore::setup_buffers() {
     void* dp = nullptr;
     if (hipHostGetDevicePointer(&dp, &desc_->notify, 0) == hipSuccess) d_notify_ = (uint32_t*)dp;
   }
-  return 0;
+  // Per-call ring: the owner hosts the store's ring server, other processes submit to it
+  // (cmd_ring.hpp RingSegHdr); SPLINTER_RING_SHARED=0, or no live server, gives a process its own
+  // worker as before
+  const uint32_t ps = (uint32_t)std::max<size_t>(vstride_, kEmbedBytes);
+  const char* sh = getenv("SPLINTER_RING_SHARED");
+  const bool shared = !(sh && !strcmp(sh, "0")) && vmm_mode_;
+  const std::string seg = name_ + ".ring";
+  ring_ = std::make_unique<CmdRing>();
+  if (shared && owner_) {
+    if (ring_->init_server(device_, ps, seg, "/dev/shm/" + name_ + ".hbm", arena()) == 0) return 0;
+    ring_ = std::make_unique<CmdRing>();
+  } else if (shared && ring_->init_client(seg, device_, ps) == 0) {
+    return 0;
+  }
+  return ring_->init(device_, ps);
 }
 
 static HbmDescriptor* map_descriptor(const std::string& name, bool create, int* err) {
@@ -827,7 +842,7 @@ HbmStore::~HbmStore() {
     if (st.h) (void)hipHostFree(st.h);
   }
   stop_proxy();
-  ring_.stop();  // the worker reads the arena: drain it before the arena goes away
+  ring_.reset();  // the worker (and a ring server's supervisor) reads the arena: gone before it
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (event_fd_ >= 0) {
     if (desc_ && __atomic_load_n(&desc_->control.event_bus.owner_pid, __ATOMIC_ACQUIRE) == (int32_t)getpid()) {
@@ -840,7 +855,6 @@ HbmStore::~HbmStore() {
     }
     close(event_fd_);
   }
-  ring_.stop();
   if (h_u32_) (void)hipHostFree(h_u32_);
   if (d_scan_idx_) (void)hipFree(d_scan_idx_);
   if (d_scan_ep_) (void)hipFree(d_scan_ep_);
@@ -1221,6 +1235,13 @@ int spl_hbm_arena(spl_store* h, spl_arena_t* out) {
 uint32_t spl_hbm_ring_launches(spl_store* h) {
   auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
   return s ? s->ring_launches() : 0;
+}
+
+// 0: the store's calls run on this process's own ring worker; 1: this process hosts the store's
+// ring server; 2: it submits to the owner's ring server (cmd_ring.hpp); -1: not an HBM store
+int spl_hbm_ring_mode(spl_store* h) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  return s ? s->ring_mode() : -1;
 }
 
 // Pinned, device-mapped host memory for batch arrays (splinter_ext.h spl_batch_alloc).

@@ -144,6 +144,8 @@ int spl_xw_peer(int device, int peer);
  * `writers` + `readers` concurrent streams. */
 void *spl_kvs_create(int writers, int readers);
 void spl_kvs_destroy(void *h);
+/* 0: one launch per client stream slice; 1 / 2 (default, SPL_KVS_FUSED): every slice in one fused grid */
+int spl_kvs_set_fused(void *h, int mode);
 int spl_kvs_step(void *h, spl_arena_t a, hipStream_t origin, const char *skeys, int kstride, const uint8_t *svals,
                  int vstride, const uint32_t *slens, long n_set, int32_t *sstatus, const char *gkeys, uint8_t *gout,
                  int ostride, uint32_t *glens, long n_get, int32_t *gstatus, int max_retry, uint64_t *stats);

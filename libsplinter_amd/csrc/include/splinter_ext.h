@@ -109,6 +109,9 @@ int   spl_node_nshards(spl_store *s);           /* -1 if s is not a node store *
 spl_store *spl_node_shard(spl_store *s, int i);
 int   spl_node_shard_of(const char *key, int nshards);
 int   spl_hbm_device_count(void);               /* libsplinter_hip.so */
+/* per-call ring of an hbm: store in this process: 0 its own worker, 1 this process hosts the
+ * store's ring server (the owner), 2 it submits to the owner's server; -1 not an hbm: store */
+int   spl_hbm_ring_mode(spl_store *s);          /* libsplinter_hip.so */
 
 /* Host-array batches (batch_host.cpp): n fixed-stride NUL-padded key records (kstride <= 64), value
  * rows of vstride / ostride bytes, per-op status 0 or -errno (EAGAIN -11, ENOENT -2, ENOSPC -28,

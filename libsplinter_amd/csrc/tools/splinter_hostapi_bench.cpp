@@ -4,6 +4,12 @@
 //
 //   splinter_hostapi_bench [--store NAME] [--threads T] [--seconds S] [--keys K]
 //                          [--value-len L] [--set-frac F] [--append-check N] [--batch B]
+//                          [--procs P]
+//
+// --procs P: P processes issue the calls (T threads each) against the one store: the parent
+// creates it (and, on hbm:, hosts its ring server), P-1 children -- spawned before the parent
+// touches the GPU, released through a pipe once the keys are in -- open it and submit to the same
+// server.  ops/s is the sum over processes; p50_us etc. are the parent's, procs_p50_us lists all.
 //
 // --batch B: the host-array batch ABI instead (splinter_ext.h spl_set_batch / spl_get_batch): K keys
 // prepopulated in batches, then for S seconds alternating set and get batches of B random keys from
@@ -25,7 +31,10 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include <dlfcn.h>
 #include <sched.h>
+#include <spawn.h>
+#include <sys/wait.h>
 #include <unistd.h>
 
 #include "splinter_ext.h"
@@ -41,6 +50,9 @@ struct Args {
   double set_frac = 0.5;
   int append_check = 0;
   long batch = 0;
+  int procs = 1;
+  bool attach = false;  // child of --procs: open the parent's store
+  int go_fd = -1;       // child: read one byte before starting
 };
 
 double pct(std::vector<float>& v, double p) {
@@ -144,47 +156,21 @@ int batch_main(const Args& a) {
 
 }  // namespace
 
-int main(int argc, char** argv) {
-  Args a;
-  a.store = "hbm:hostapi" + std::to_string(getpid());
-  for (int i = 1; i < argc; ++i) {
-    std::string s = argv[i];
-    auto nxt = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
-    if (s == "--store") a.store = nxt();
-    else if (s == "--threads") a.threads = atoi(nxt());
-    else if (s == "--seconds") a.seconds = atof(nxt());
-    else if (s == "--keys") a.keys = atoi(nxt());
-    else if (s == "--value-len") a.value_len = atoi(nxt());
-    else if (s == "--set-frac") a.set_frac = atof(nxt());
-    else if (s == "--append-check") a.append_check = atoi(nxt());
-    else if (s == "--batch") a.batch = atol(nxt());
-    else { fprintf(stderr, "unknown option %s\n", s.c_str()); return 2; }
-  }
-  if (a.batch > 0) return batch_main(a);
-  const size_t max_val = 4096;
-  if (splinter_create(a.store.c_str(), (size_t)a.keys * 2 + 1024, max_val) != 0) {
-    fprintf(stderr, "create %s failed: %s\n", a.store.c_str(), strerror(errno));
-    return 1;
-  }
-  std::string val(a.value_len, 'v');
-  // prepopulate in parallel (the same per-call path)
-  {
-    std::vector<std::thread> th;
-    std::atomic<int> bad{0};
-    for (int t = 0; t < a.threads; ++t)
-      th.emplace_back([&, t] {
-        for (int i = t; i < a.keys; i += a.threads) {
-          std::string k = key_of(i);
-          for (int r = 0; r < 100000; ++r) {  // EAGAIN = a racing claim: back off and retry
-            if (splinter_set(k.c_str(), val.data(), val.size()) == 0) break;
-            if (errno != EAGAIN || r == 99999) { fprintf(stderr, "set %s: %s\n", k.c_str(), strerror(errno)); ++bad; break; }
-            sched_yield();
-          }
-        }
-      });
-    for (auto& x : th) x.join();
-    if (bad) { fprintf(stderr, "prepopulate: %d failures\n", bad.load()); return 1; }
-  }
+// 0 own ring worker, 1 ring server host, 2 client of the owner's server (hbm: stores), -1 otherwise
+int ring_mode() {
+  using Mode = int (*)(spl_store*);
+  auto f = (Mode)dlsym(RTLD_DEFAULT, "spl_hbm_ring_mode");
+  return f && spl_store_current() ? f(spl_store_current()) : -1;
+}
+
+struct RunStats {
+  double el = 0;
+  uint64_t calls = 0, ok = 0, again = 0, fail = 0;
+  double p50 = 0, p90 = 0, p99 = 0, sp50 = 0, sp99 = 0, gp50 = 0, gp99 = 0;
+};
+
+// T threads, set/get mix over K keys for S seconds, every call timed
+RunStats run_calls(const Args& a, size_t max_val, const std::string& val) {
   using clk = std::chrono::steady_clock;
   std::atomic<bool> go{false}, stop{false};
   std::vector<std::vector<float>> lat_set(a.threads), lat_get(a.threads);
@@ -192,7 +178,7 @@ int main(int argc, char** argv) {
   std::vector<std::thread> th;
   for (int t = 0; t < a.threads; ++t)
     th.emplace_back([&, t] {
-      uint64_t x = 0x9E3779B97F4A7C15ull * (uint64_t)(t + 1);
+      uint64_t x = 0x9E3779B97F4A7C15ull * (uint64_t)(t + 1) + 0x5851F42D4C957F2Dull * (uint64_t)getpid();
       std::vector<char> buf(max_val);
       lat_set[t].reserve(1 << 20);
       lat_get[t].reserve(1 << 20);
@@ -218,18 +204,158 @@ int main(int argc, char** argv) {
   std::this_thread::sleep_for(std::chrono::duration<double>(a.seconds));
   stop.store(true);
   for (auto& x : th) x.join();
-  const double el = std::chrono::duration<double>(clk::now() - t0).count();
+  RunStats r;
+  r.el = std::chrono::duration<double>(clk::now() - t0).count();
   std::vector<float> ls, lg, la;
-  uint64_t tok = 0, tag = 0, tf = 0;
   for (int t = 0; t < a.threads; ++t) {
     ls.insert(ls.end(), lat_set[t].begin(), lat_set[t].end());
     lg.insert(lg.end(), lat_get[t].begin(), lat_get[t].end());
-    tok += ok[t]; tag += again[t]; tf += fail[t];
+    r.ok += ok[t]; r.again += again[t]; r.fail += fail[t];
   }
   la = ls;
   la.insert(la.end(), lg.begin(), lg.end());
-  const uint64_t calls = la.size();
-  int rc = tf ? 1 : 0;
+  r.calls = la.size();
+  r.p50 = pct(la, 0.5); r.p90 = pct(la, 0.9); r.p99 = pct(la, 0.99);
+  r.sp50 = pct(ls, 0.5); r.sp99 = pct(ls, 0.99); r.gp50 = pct(lg, 0.5); r.gp99 = pct(lg, 0.99);
+  return r;
+}
+
+// child of --procs: wait for the parent's go byte, open its store, run, report one line
+int attach_main(const Args& a) {
+  char b = 0;
+  if (a.go_fd >= 0) {
+    if (read(a.go_fd, &b, 1) != 1 || b != 'g') return 3;  // the parent gave up
+    close(a.go_fd);
+  }
+  if (splinter_open(a.store.c_str()) != 0) {
+    fprintf(stderr, "open %s failed: %s\n", a.store.c_str(), strerror(errno));
+    return 1;
+  }
+  const RunStats r = run_calls(a, 4096, std::string(a.value_len, 'v'));
+  printf("%llu %llu %llu %.6f %.3f\n", (unsigned long long)r.calls, (unsigned long long)r.ok,
+         (unsigned long long)r.fail, r.el, r.p50);
+  fflush(stdout);
+  splinter_close();
+  return r.fail ? 1 : 0;
+}
+
+int main(int argc, char** argv) {
+  Args a;
+  a.store = "hbm:hostapi" + std::to_string(getpid());
+  for (int i = 1; i < argc; ++i) {
+    std::string s = argv[i];
+    auto nxt = [&]() -> const char* { return i + 1 < argc ? argv[++i] : ""; };
+    if (s == "--store") a.store = nxt();
+    else if (s == "--threads") a.threads = atoi(nxt());
+    else if (s == "--seconds") a.seconds = atof(nxt());
+    else if (s == "--keys") a.keys = atoi(nxt());
+    else if (s == "--value-len") a.value_len = atoi(nxt());
+    else if (s == "--set-frac") a.set_frac = atof(nxt());
+    else if (s == "--append-check") a.append_check = atoi(nxt());
+    else if (s == "--batch") a.batch = atol(nxt());
+    else if (s == "--procs") a.procs = atoi(nxt());
+    else if (s == "--attach") a.attach = true;
+    else if (s == "--go-fd") a.go_fd = atoi(nxt());
+    else { fprintf(stderr, "unknown option %s\n", s.c_str()); return 2; }
+  }
+  if (a.batch > 0) return batch_main(a);
+  if (a.attach) return attach_main(a);
+  // --procs: children first, before this process touches the GPU (no fork of an initialised runtime)
+  struct Child {
+    pid_t pid;
+    int out;
+  };
+  std::vector<Child> kids;
+  int go[2] = {-1, -1};
+  if (a.procs > 1) {
+    if (pipe(go) != 0) return 1;
+    char self[4096];
+    const ssize_t n = readlink("/proc/self/exe", self, sizeof self - 1);
+    if (n <= 0) return 1;
+    self[n] = 0;
+    for (int c = 1; c < a.procs; ++c) {
+      int out[2];
+      if (pipe(out) != 0) return 1;
+      posix_spawn_file_actions_t fa;
+      posix_spawn_file_actions_init(&fa);
+      posix_spawn_file_actions_adddup2(&fa, out[1], 1);
+      posix_spawn_file_actions_addclose(&fa, out[0]);
+      posix_spawn_file_actions_addclose(&fa, go[1]);
+      const std::string th = std::to_string(a.threads), sec = std::to_string(a.seconds),
+                        ks = std::to_string(a.keys), vl = std::to_string(a.value_len),
+                        sf = std::to_string(a.set_frac), gf = std::to_string(go[0]);
+      const char* av[] = {self, "--attach", "--store", a.store.c_str(), "--threads", th.c_str(), "--seconds",
+                          sec.c_str(), "--keys", ks.c_str(), "--value-len", vl.c_str(), "--set-frac", sf.c_str(),
+                          "--go-fd", gf.c_str(), nullptr};
+      pid_t pid = 0;
+      const int rc = posix_spawn(&pid, self, &fa, nullptr, (char* const*)av, environ);
+      posix_spawn_file_actions_destroy(&fa);
+      close(out[1]);
+      if (rc != 0) { fprintf(stderr, "spawn failed: %s\n", strerror(rc)); return 1; }
+      kids.push_back({pid, out[0]});
+    }
+    close(go[0]);
+  }
+  auto release_kids = [&](char b) {
+    if (go[1] < 0) return;
+    for (size_t i = 0; i < kids.size(); ++i) (void)!write(go[1], &b, 1);
+    close(go[1]);
+    go[1] = -1;
+  };
+  const size_t max_val = 4096;
+  if (splinter_create(a.store.c_str(), (size_t)a.keys * 2 + 1024, max_val) != 0) {
+    fprintf(stderr, "create %s failed: %s\n", a.store.c_str(), strerror(errno));
+    release_kids('x');
+    return 1;
+  }
+  std::string val(a.value_len, 'v');
+  // prepopulate in parallel (the same per-call path)
+  {
+    std::vector<std::thread> th;
+    std::atomic<int> bad{0};
+    for (int t = 0; t < a.threads; ++t)
+      th.emplace_back([&, t] {
+        for (int i = t; i < a.keys; i += a.threads) {
+          std::string k = key_of(i);
+          for (int r = 0; r < 100000; ++r) {  // EAGAIN = a racing claim: back off and retry
+            if (splinter_set(k.c_str(), val.data(), val.size()) == 0) break;
+            if (errno != EAGAIN || r == 99999) { fprintf(stderr, "set %s: %s\n", k.c_str(), strerror(errno)); ++bad; break; }
+            sched_yield();
+          }
+        }
+      });
+    for (auto& x : th) x.join();
+    if (bad) { fprintf(stderr, "prepopulate: %d failures\n", bad.load()); release_kids('x'); return 1; }
+  }
+  release_kids('g');
+  const RunStats st = run_calls(a, max_val, val);
+  const double el = st.el;
+  uint64_t calls = st.calls, tok = st.ok, tag = st.again, tf = st.fail;
+  double total_rate = (double)st.calls / st.el, ok_rate = (double)st.ok / st.el;
+  std::string p50s = std::to_string(st.p50);
+  int kid_fail = 0;
+  for (auto& k : kids) {
+    char line[256] = {0};
+    size_t got = 0;
+    ssize_t r;
+    while (got < sizeof line - 1 && (r = read(k.out, line + got, sizeof line - 1 - got)) > 0) got += (size_t)r;
+    close(k.out);
+    int wst = 0;
+    (void)waitpid(k.pid, &wst, 0);
+    unsigned long long c = 0, o = 0, f = 0;
+    double kel = 0, kp50 = 0;
+    if (sscanf(line, "%llu %llu %llu %lf %lf", &c, &o, &f, &kel, &kp50) != 5 || kel <= 0 ||
+        !WIFEXITED(wst) || WEXITSTATUS(wst) != 0) {
+      ++kid_fail;
+      continue;
+    }
+    calls += c; tok += o; tf += f;
+    total_rate += (double)c / kel;
+    ok_rate += (double)o / kel;
+    p50s += ", " + std::to_string(kp50);
+  }
+  int rc = tf || kid_fail ? 1 : 0;
+  if (kid_fail) fprintf(stderr, "%d child process(es) failed\n", kid_fail);
 
   // concurrent append check
   int app_ok = -1;
@@ -273,13 +399,14 @@ int main(int argc, char** argv) {
       rc = 1;
     }
   }
-  printf("{\"store\": \"%s\", \"threads\": %d, \"seconds\": %.3f, \"calls\": %llu, \"ops_per_s\": %.1f, "
+  printf("{\"store\": \"%s\", \"threads\": %d, \"procs\": %d, \"seconds\": %.3f, \"calls\": %llu, \"ops_per_s\": %.1f, "
          "\"successful_ops_per_s\": %.1f, \"eagain\": %llu, \"failures\": %llu, "
          "\"p50_us\": %.2f, \"p90_us\": %.2f, \"p99_us\": %.2f, \"set_p50_us\": %.2f, \"set_p99_us\": %.2f, "
-         "\"get_p50_us\": %.2f, \"get_p99_us\": %.2f, \"value_len\": %d, \"set_frac\": %.2f, \"append_check\": %d}\n",
-         a.store.c_str(), a.threads, el, (unsigned long long)calls, (double)calls / el, (double)tok / el,
-         (unsigned long long)tag, (unsigned long long)tf, pct(la, 0.5), pct(la, 0.9), pct(la, 0.99), pct(ls, 0.5),
-         pct(ls, 0.99), pct(lg, 0.5), pct(lg, 0.99), a.value_len, a.set_frac, app_ok);
+         "\"get_p50_us\": %.2f, \"get_p99_us\": %.2f, \"procs_p50_us\": [%s], \"ring_mode\": %d, \"value_len\": %d, "
+         "\"set_frac\": %.2f, \"append_check\": %d}\n",
+         a.store.c_str(), a.threads, a.procs, el, (unsigned long long)calls, total_rate, ok_rate,
+         (unsigned long long)tag, (unsigned long long)tf, st.p50, st.p90, st.p99, st.sp50, st.sp99, st.gp50, st.gp99,
+         p50s.c_str(), ring_mode(), a.value_len, a.set_frac, app_ok);
   splinter_close();
   spl_unlink(a.store.c_str());
   return rc;

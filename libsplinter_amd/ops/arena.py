@@ -94,6 +94,10 @@ class KvStreams:
             raise RuntimeError("spl_kvs_create failed")
         self.writers, self.readers = writers, readers
 
+    def set_fused(self, mode: int):
+        """0: one launch per stream slice; 1 / 2 (default): every slice in one fused grid."""
+        _check(self._H.spl_kvs_set_fused(self.h, int(mode)), "kvs_set_fused")
+
     def step(self, arena: "HbmArena", skeys, svals, slens, sstatus, gkeys, gout, glens, gstatus, retries: int = 64):
         n_set = skeys.shape[0] if skeys is not None else 0
         n_get = gkeys.shape[0] if gkeys is not None else 0

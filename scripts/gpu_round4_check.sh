@@ -14,6 +14,21 @@ step() {  # step NAME CMD... : run with output to $OUT/NAME.{out,err}; stop on r
   echo "== $name rc=$rc"; tail -c 3000 "$OUT/$name.out"
   if [ $rc -ne 0 ]; then tail -20 "$OUT/$name.err"; exit $rc; fi
 }
+if [ -n "$PRE_TESTS" ]; then  # targeted tests first (new code), fail fast
+  step pre_tests timeout -k 10 600 python -u -m pytest $PRE_TESTS -x -v --timeout 150 --timeout-method thread
+fi
+if [ -n "$EXTRA_RING" ]; then
+  # per-call API: one process at 1 / 32 / 64 threads, 4 processes x 8 / 16 threads on the owner's ring
+  # server (default) and with a worker per process (SPLINTER_RING_SHARED=0); encoder beside 4 clients
+  H=./libsplinter_amd/bin/splinter_hostapi_bench
+  for t in 1 32 64; do step ring_t$t timeout -k 10 120 $H --store hbm:rt$t --threads $t --seconds 2 --keys 20000; done
+  for t in 8 16; do
+    step ring_p4t${t}_shared timeout -k 10 120 $H --store hbm:rp$t --procs 4 --threads $t --seconds 2 --keys 20000
+    step ring_p4t${t}_private env SPLINTER_RING_SHARED=0 timeout -k 10 120 $H --store hbm:rq$t --procs 4 --threads $t \
+      --seconds 2 --keys 20000
+  done
+  step ring_interference timeout -k 10 300 python -u scripts/ring_interference.py --clients 4 --threads 8 --steps 20
+fi
 if [ -z "$SKIP_BENCH" ]; then
   step bench timeout -k 10 300 python -u bench.py --steps 20 --warmup 5
   step bench2 timeout -k 10 300 python -u bench.py --gpus 2 --backend gloo --mode kv --keys-per-gpu 20000000 \

@@ -1,0 +1,96 @@
+"""Encoder step time beside per-call clients: one process owns an hbm: store and runs the encoder
+(the embedding daemon's work, EmbedPhase 64 x 512) while C clients in other processes hammer the
+store's per-call API (splinter_hostapi_bench --attach, 8 threads each).
+
+  shared   the clients submit to the owner's ONE ring server (cmd_ring.hpp RingSegHdr, default)
+  private  SPLINTER_RING_SHARED=0 in the clients: each runs its own resident ring worker
+
+Prints one JSON line: encoder ms/step alone and beside the clients in either mode, the slowdown,
+and the clients' aggregate ops/s.
+
+  python scripts/ring_interference.py [--clients 4] [--threads 8] [--steps 20]
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+
+from libsplinter_amd import Store  # noqa: E402
+from libsplinter_amd import _native as N  # noqa: E402
+from libsplinter_amd.models.bench_embed import EmbedPhase  # noqa: E402
+
+TOOL = os.path.join(ROOT, "libsplinter_amd", "bin", "splinter_hostapi_bench")
+
+
+def time_steps(ph, n):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        ph.run()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / n * 1e3
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--clients", type=int, default=4)
+    ap.add_argument("--threads", default="2,8", help="client threads per process, comma list")
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--keys", type=int, default=20000)
+    a = ap.parse_args()
+    name = f"hbm:ri{os.getpid()}"
+    st = Store.create(name, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
+    out = {"clients": a.clients, "cpus": len(os.sched_getaffinity(0)), "owner_ring_mode": N.hip_lib().spl_hbm_ring_mode(st.handle)}
+    try:
+        keys = [f"hk{i:08d}" for i in range(a.keys)]
+        status = st.set_batch(keys, [b"v" * 150] * a.keys)
+        assert int((status != 0).sum()) == 0
+        ph = EmbedPhase(batch=64, seq=512)
+        for _ in range(3):
+            ph.run()
+        out["encoder_ms_alone"] = round(time_steps(ph, a.steps), 3)
+        secs = max(3.0, a.steps * out["encoder_ms_alone"] / 1e3 * 3 + 2.0)
+        for threads in [int(t) for t in a.threads.split(",")]:
+            for mode in ("shared", "private"):
+                env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
+                           SPLINTER_RING_SHARED="1" if mode == "shared" else "0")
+                procs = [subprocess.Popen([TOOL, "--attach", "--store", name, "--threads", str(threads), "--seconds",
+                                           str(secs), "--keys", str(a.keys)], env=env, stdout=subprocess.PIPE,
+                                          stderr=subprocess.PIPE, text=True) for _ in range(a.clients)]
+                try:
+                    time.sleep(1.0)  # the clients are attached and calling
+                    ms = time_steps(ph, a.steps)
+                    rate, fails = 0.0, 0
+                    for p in procs:
+                        o, e = p.communicate(timeout=secs + 60)
+                        if p.returncode != 0:
+                            fails += 1
+                            print(e[-500:], file=sys.stderr)
+                            continue
+                        c, ok, f, el, p50 = o.split()[:5]
+                        rate += int(c) / float(el)
+                        fails += int(f)
+                finally:
+                    for p in procs:
+                        if p.poll() is None:
+                            p.kill()
+                out[f"{mode}_t{threads}"] = {"encoder_ms": round(ms, 3),
+                                             "slowdown_pct": round(100.0 * (ms / out["encoder_ms_alone"] - 1), 2),
+                                             "client_ops_per_s": round(rate, 1), "client_failures": fails}
+                print(json.dumps(out), file=sys.stderr, flush=True)
+        out["encoder_ms_alone_after"] = round(time_steps(ph, a.steps), 3)
+        ph.close()
+    finally:
+        st.close()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

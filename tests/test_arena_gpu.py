@@ -485,3 +485,52 @@ def test_acquire_free_get_cross_xcd_hot_keys(uniq):
         assert checked == len(outs) * hot * rep
     finally:
         a.close()
+
+
+@pytest.mark.parametrize("kstride", [16, 32])
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_kvs_step_modes_match_plain_kernels(uniq, kstride, mode):
+    """One KV step of 8 + 8 client streams (spl_kvs_step) -- per-slice launches (0) or one fused
+    grid (1, 2: the default) -- sets new and existing keys and gets present and missing ones with
+    the same results as the plain batch kernels."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, KvStreams, pack_keys, pack_values, unpack
+    rng = np.random.default_rng(kstride + mode)
+    a = HbmArena.create(uniq, slots=1 << 16, max_val=256, embeddings=False)
+    kvs = KvStreams(8, 8)
+    try:
+        kvs.set_fused(mode)
+        n = 20000
+        w = kstride - 1
+        keys = [f"k{i:0{min(w - 1, 12)}d}"[:w] for i in range(n)]
+        vals = [bytes(rng.integers(1, 255, size=int(rng.integers(1, 200)), dtype=np.uint8)) for _ in range(n)]
+        K = pack_keys(keys, kstride)
+        V, L = pack_values(vals, 256)
+        half = n // 2
+        assert (a.set(K[:half], V[:half], L[:half]) == 0).all()
+        # step: set the second half (new) and rewrite the first quarter; get the first half + misses
+        sidx = np.r_[np.arange(half, n), np.arange(0, half // 2)]
+        new_vals = {int(i): vals[int(i)][::-1] for i in sidx}
+        SV, SL = pack_values([new_vals[int(i)] for i in sidx], 256)
+        SK = K[torch.as_tensor(sidx, device=K.device)]
+        GK = torch.cat([K[:half], pack_keys([f"zz{i}"[:w] for i in range(500)], kstride)])
+        sst = torch.full((len(sidx),), 99, dtype=torch.int32, device="cuda")
+        gst = torch.full((GK.shape[0],), 99, dtype=torch.int32, device="cuda")
+        gout = torch.zeros((GK.shape[0], 256), dtype=torch.uint8, device="cuda")
+        glen = torch.zeros(GK.shape[0], dtype=torch.int32, device="cuda")
+        kvs.step(a, SK, SV, SL, sst, GK, gout, glen, gst)
+        torch.cuda.synchronize()
+        assert (sst == 0).all()
+        g = gst.cpu().numpy()
+        assert (g[half:] == -2).all()
+        assert (g[:half] == 0).all(), np.unique(g[:half])
+        got = unpack(gout[:half], glen[:half])
+        for i in range(half):  # a get racing a set of the same key sees the old or the new value
+            assert got[i] in (vals[i], new_vals.get(i, vals[i])), i
+        st, out, ol = a.get(K)
+        assert (st == 0).all()
+        final = unpack(out, ol)
+        assert all(final[i] == new_vals.get(i, vals[i]) for i in range(n))
+    finally:
+        kvs.close()
+        a.close()

@@ -247,3 +247,93 @@ def test_open_second_store_beside_live_ring_traffic(uniq):
         a.close()
     assert calls[0] > 100
     assert dt < 5.0, f"second store took {dt:.2f}s beside live traffic"
+
+
+_CLIENT = r"""
+import sys
+from libsplinter_amd import Store
+from libsplinter_amd import _native as N
+s = Store.open(sys.argv[1])
+mode = N.hip_lib().spl_hbm_ring_mode(s.handle)
+for i in range(200):
+    s.set(f"c{i}", f"child{i}".encode())
+for i in range(300):
+    s.integer_op("ctr", 4, 1)
+print(mode, s.get("o5").decode(), flush=True)
+if len(sys.argv) > 2:  # keep calling after the owner closed the store
+    print("ready", flush=True)
+    sys.stdin.readline()
+    s.set("after", b"owner-gone")
+    print(s.get("after").decode(), flush=True)
+s.close()
+"""
+
+
+def test_ring_server_shared_by_processes(uniq):
+    """The store's owner hosts ONE ring server (mode 1); a second process submits its per-call ops
+    to it (mode 2, no worker of its own): its sets are visible to the owner, and 300 + 300
+    concurrent device increments from both processes all land."""
+    from libsplinter_amd import Store
+    from libsplinter_amd import _native as N
+    s = Store.create(f"hbm:{uniq}", slots=4096, max_val=64, embeddings=False)
+    try:
+        assert N.hip_lib().spl_hbm_ring_mode(s.handle) == 1
+        s.set("ctr", b"0")
+        s.set_type("ctr", 1 << 2)
+        for i in range(10):
+            s.set(f"o{i}", f"owner{i}".encode())
+        p = subprocess.Popen([sys.executable, "-c", _CLIENT, f"hbm:{uniq}"], cwd=ROOT, env=ENV,
+                             stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        try:
+            for i in range(300):
+                s.integer_op("ctr", 4, 1)
+            out, err = p.communicate(timeout=90)
+        finally:
+            if p.poll() is None:
+                p.kill()
+        assert p.returncode == 0, err[-2000:]
+        mode, o5 = out.split()[:2]
+        assert mode == "2" and o5 == "owner5"
+        assert s.get_u64("ctr") == 600
+        assert all(s.get(f"c{i}") == f"child{i}".encode() for i in range(200))
+    finally:
+        s.close()
+
+
+def test_ring_client_survives_owner_close(uniq):
+    """A client whose owner closed the store falls back to a private ring worker on its own
+    import of the arena: later calls still work."""
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=4096, max_val=64, embeddings=False)
+    s.set("ctr", b"0")
+    s.set_type("ctr", 1 << 2)
+    s.set("o5", b"owner5")
+    p = subprocess.Popen([sys.executable, "-c", _CLIENT, f"hbm:{uniq}", "stay"], cwd=ROOT, env=ENV,
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        assert p.stdout.readline().split() == ["2", "owner5"]
+        assert p.stdout.readline().strip() == "ready"
+        s.close()
+        s = None
+        p.stdin.write("go\n")
+        p.stdin.flush()
+        out, err = p.communicate(timeout=90)
+    finally:
+        if p.poll() is None:
+            p.kill()
+        if s is not None:
+            s.close()
+    assert p.returncode == 0, err[-2000:]
+    assert out.strip() == "owner-gone"
+
+
+def test_hostapi_four_processes_one_server(uniq):
+    """4 processes x 8 threads against one hbm: store: every call served by the owner's one ring
+    server (the children are its clients)."""
+    tool = os.path.join(ROOT, "libsplinter_amd", "bin", "splinter_hostapi_bench")
+    r = subprocess.run([tool, "--store", f"hbm:{uniq}", "--procs", "4", "--threads", "8", "--seconds", "1.0",
+                        "--keys", "20000"], capture_output=True, text=True, timeout=150, env=ENV)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    print(json.dumps(res))
+    assert res["failures"] == 0 and res["ring_mode"] == 1 and len(res["procs_p50_us"]) == 4

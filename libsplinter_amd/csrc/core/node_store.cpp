@@ -376,10 +376,12 @@ int NodeStore::madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t
 
 // ------------------------------------------------------------------ batches --
 // A batch is counting-sorted by owning shard into one scratch buffer (pinned when the HBM backend
-// is present, so HBM shards DMA straight from it).  Every shard's contiguous part runs on its own
-// thread -- gather its rows, run its batch (HBM shards: HbmStore::*_batch on that shard's GPU, all
-// GPUs at once), scatter its outputs back into client order -- so one shard's host copies overlap
-// the others' DMA and kernels.  The sort itself is parallel (per-thread histograms).
+// is present, so HBM shards DMA straight from it), every shard's contiguous part runs on its own
+// thread (HBM shards: HbmStore::*_batch on that shard's GPU, all GPUs at once), and the outputs go
+// back into client order.  The copies walk the CLIENT order on kNodeBatchThreads threads: the
+// sort is stable per thread chunk, so each thread reads its rows sequentially and writes them to
+// one sequential stream per shard (no random row reads: 66.7 M ops/s with per-row gathers by
+// permutation, 4 HBM shards on one GPU, profiles/r4f).
 namespace {
 constexpr int kNodeBatchThreads = 8;
 
@@ -405,10 +407,10 @@ inline void copy_row(uint8_t* d, const uint8_t* s, long w) {
 }  // namespace
 
 struct NodeStore::Plan {
-  std::vector<long> perm;   // perm[k]: client op at sorted position k
+  std::vector<long> pos;    // pos[i]: sorted position of client op i
   std::vector<long> off;    // shard j's ops are sorted positions [off[j], off[j+1])
   int nsh;
-  Plan(const char* keys, int kstride, long n, int nsh_) : perm((size_t)n), off((size_t)nsh_ + 1, 0), nsh(nsh_) {
+  Plan(const char* keys, int kstride, long n, int nsh_) : pos((size_t)n), off((size_t)nsh_ + 1, 0), nsh(nsh_) {
     std::vector<int32_t> dest((size_t)n);
     const int cut = kstride < 64 ? kstride : 63;
     const int T = n < 65536 ? 1 : kNodeBatchThreads;
@@ -437,21 +439,20 @@ struct NodeStore::Plan {
     off[(size_t)nsh] = run;
     par_range(n, [&](long b, long e, int t) {
       long* p = base.data() + (size_t)t * nsh;
-      for (long i = b; i < e; ++i) perm[(size_t)p[dest[(size_t)i]]++] = i;
+      for (long i = b; i < e; ++i) pos[(size_t)i] = p[dest[(size_t)i]]++;
     }, T);
   }
-  // threads per shard for its gathers / scatters
-  int sub() const { return nsh >= kNodeBatchThreads ? 1 : kNodeBatchThreads / nsh; }
-  // sorted copy of a column (rows of `w` bytes), sorted positions [k0, k1)
-  void gather(uint8_t* dst, const void* src, long w, long k0, long k1) const {
-    par_range(k1 - k0, [&](long b, long e, int) {
-      for (long k = k0 + b; k < k0 + e; ++k) copy_row(dst + k * w, (const uint8_t*)src + perm[(size_t)k] * w, w);
-    }, sub());
+  // client column (rows of `w` bytes) -> sorted scratch column
+  void gather(uint8_t* dst, const void* src, long w) const {
+    par_range((long)pos.size(), [&](long b, long e, int) {
+      for (long i = b; i < e; ++i) copy_row(dst + pos[(size_t)i] * w, (const uint8_t*)src + i * w, w);
+    });
   }
-  void scatter(void* dst, const uint8_t* src, long w, long k0, long k1) const {
-    par_range(k1 - k0, [&](long b, long e, int) {
-      for (long k = k0 + b; k < k0 + e; ++k) copy_row((uint8_t*)dst + perm[(size_t)k] * w, src + k * w, w);
-    }, sub());
+  // sorted scratch column -> client column
+  void scatter(void* dst, const uint8_t* src, long w) const {
+    par_range((long)pos.size(), [&](long b, long e, int) {
+      for (long i = b; i < e; ++i) copy_row((uint8_t*)dst + i * w, src + pos[(size_t)i] * w, w);
+    });
   }
   template <class F>
   void each_shard(F&& f) const {
@@ -496,14 +497,12 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
   const long ob = 0, vb = a64(n * kstride), lb = vb + a64(n * (long)vstride), sb = lb + a64(n * 4);
   uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
   if (!S) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.gather(S + ob, keys, kstride);
+  pl.gather(S + vb, vals, vstride);
+  pl.gather(S + lb, lens, 4);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
-    pl.gather(S + ob, keys, kstride, o, o + m);
-    pl.gather(S + vb, vals, vstride, o, o + m);
-    pl.gather(S + lb, lens, 4, o, o + m);
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + ob + o * kstride;
     const uint8_t* v = S + vb + o * (long)vstride;
@@ -511,11 +510,12 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
     int32_t* st = (int32_t*)(S + sb) + o;
     long r = sh->set_batch(k, kstride, v, vstride, l, m, st, retries);
     if (r == kNoBatch) r = generic_set_batch(sh, k, kstride, v, vstride, l, m, st, retries, 4);
-    if (r < 0) { fail = true; return; }
-    ok += r;
-    pl.scatter(status, S + sb, 4, o, o + m);
+    if (r < 0) fail = true;
+    else ok += r;
   });
-  return fail ? -1 : ok.load();
+  if (fail) return -1;
+  if (status) pl.scatter(status, S + sb, 4);
+  return ok.load();
 }
 
 long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
@@ -526,12 +526,10 @@ long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostri
   const long ob = 0, sb = a64(n * kstride), lb = sb + a64(n * 4), vb = lb + a64(n * 4);
   uint8_t* S = scratch((size_t)(vb + (out ? a64(n * (long)ostride) : 0)));
   if (!S) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.gather(S + ob, keys, kstride);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
-    pl.gather(S + ob, keys, kstride, o, o + m);
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + ob + o * kstride;
     uint8_t* v = out ? S + vb + o * (long)ostride : nullptr;
@@ -539,13 +537,14 @@ long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostri
     int32_t* st = (int32_t*)(S + sb) + o;
     long r = sh->get_batch(k, kstride, v, ostride, l, m, st, retries);
     if (r == kNoBatch) r = generic_get_batch(sh, k, kstride, v, ostride, l, m, st, retries, 4);
-    if (r < 0) { fail = true; return; }
-    ok += r;
-    pl.scatter(status, S + sb, 4, o, o + m);
-    if (out_lens) pl.scatter(out_lens, S + lb, 4, o, o + m);
-    if (out) pl.scatter(out, S + vb, ostride, o, o + m);
+    if (r < 0) fail = true;
+    else ok += r;
   });
-  return fail ? -1 : ok.load();
+  if (fail) return -1;
+  if (status) pl.scatter(status, S + sb, 4);
+  if (out_lens) pl.scatter(out_lens, S + lb, 4);
+  if (out) pl.scatter(out, S + vb, ostride);
+  return ok.load();
 }
 
 long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,
@@ -556,15 +555,13 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
   const long kb = 0, pb = a64(n * kstride), mb = pb + a64(n * 4), sb = mb + a64(n * 8), rb = sb + a64(n * 4);
   uint8_t* S = scratch((size_t)(rb + a64(n * 8)));
   if (!S) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.gather(S + kb, keys, kstride);
+  pl.gather(S + pb, ops, 4);
+  if (masks) pl.gather(S + mb, masks, 8);
+  else std::memset(S + mb, 0, (size_t)(n * 8));
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
-    pl.gather(S + kb, keys, kstride, o, o + m);
-    pl.gather(S + pb, ops, 4, o, o + m);
-    if (masks) pl.gather(S + mb, masks, 8, o, o + m);
-    else std::memset(S + mb + o * 8, 0, (size_t)(m * 8));
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + kb + o * kstride;
     const int* op = (const int*)(S + pb) + o;
@@ -573,12 +570,13 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
     uint64_t* rs = results ? (uint64_t*)(S + rb) + o : nullptr;
     long r = sh->intop_batch(k, kstride, op, mk, m, st, rs);
     if (r == kNoBatch) r = generic_intop_batch(sh, k, kstride, op, mk, m, st, rs, 4);
-    if (r < 0) { fail = true; return; }
-    ok += r;
-    pl.scatter(status, S + sb, 4, o, o + m);
-    if (results) pl.scatter(results, S + rb, 8, o, o + m);
+    if (r < 0) fail = true;
+    else ok += r;
   });
-  return fail ? -1 : ok.load();
+  if (fail) return -1;
+  if (status) pl.scatter(status, S + sb, 4);
+  if (results) pl.scatter(results, S + rb, 8);
+  return ok.load();
 }
 
 long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) {
@@ -588,24 +586,23 @@ long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* 
   const long kb = 0, vb = a64(n * kstride), sb = vb + n * (long)kEmbedBytes;
   uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
   if (!S) return -1;
-  std::vector<int32_t> tmp;
-  if (!status) { tmp.resize((size_t)n); status = tmp.data(); }
+  pl.gather(S + kb, keys, kstride);
+  pl.gather(S + vb, vecs, (long)kEmbedBytes);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
-    pl.gather(S + kb, keys, kstride, o, o + m);
-    pl.gather(S + vb, vecs, (long)kEmbedBytes, o, o + m);
     StoreBase* sh = shards_[(size_t)j];
     const char* k = (const char*)S + kb + o * kstride;
     const float* v = (const float*)(S + vb + o * (long)kEmbedBytes);
     int32_t* st = (int32_t*)(S + sb) + o;
     long r = sh->set_embedding_batch(k, kstride, v, m, st);
     if (r == kNoBatch) r = generic_set_embedding_batch(sh, k, kstride, v, m, nullptr, st, 4);
-    if (r < 0) { fail = true; return; }
-    ok += r;
-    pl.scatter(status, S + sb, 4, o, o + m);
+    if (r < 0) fail = true;
+    else ok += r;
   });
-  return fail ? -1 : ok.load();
+  if (fail) return -1;
+  if (status) pl.scatter(status, S + sb, 4);
+  return ok.load();
 }
 
 }  // namespace spl

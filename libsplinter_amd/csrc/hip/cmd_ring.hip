@@ -648,9 +648,7 @@ int CmdRing::alloc_host(size_t) {
   d_shared_ = shared_;
   d_cmds_ = cmds_;
   d_payload_ = payload_;
-  busy_ = own_.busy;
-  holder_ = own_.holder;
-  seqs_ = own_.seqs;
+  ent_ = own_.ent;
   ticket_ = &own_.ticket;
   return 0;
 }
@@ -751,9 +749,7 @@ int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, c
   d_vdone_ = (RingDone*)(dp + L.done);
   payload_ = hp + L.pay;
   d_payload_ = dp + L.pay;
-  busy_ = seg_->busy;
-  holder_ = seg_->holder;
-  seqs_ = seg_->seqs;
+  ent_ = seg_->ent;
   ticket_ = &seg_->ticket;
   // the request chunk's descriptors, for clients' BAR mappings
   char sock[96];
@@ -834,9 +830,7 @@ int CmdRing::init_client(const std::string& seg, int device, uint32_t pstride) {
   cmds_ = (RingCmd*)(hp + L.cmds);
   vdone_ = (RingDone*)(hp + L.done);
   payload_ = hp + L.pay;
-  busy_ = seg_->busy;
-  holder_ = seg_->holder;
-  seqs_ = seg_->seqs;
+  ent_ = seg_->ent;
   ticket_ = &seg_->ticket;
   device_ = device;
   read_env();
@@ -950,7 +944,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     return spread ? (t % kRingGroups) * kGroupEntries + t / kRingGroups : t;
   };
   auto finished = [this](uint32_t e) {
-    return vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == __atomic_load_n(&seqs_[e], __ATOMIC_ACQUIRE)
+    return vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == __atomic_load_n(&ent_[e].seq, __ATOMIC_ACQUIRE)
                : __atomic_load_n(&shared_->state[e], __ATOMIC_ACQUIRE) == (uint32_t)kRingDone;
   };
   uint32_t t = __atomic_fetch_add(ticket_, 1u, __ATOMIC_RELAXED);
@@ -964,19 +958,19 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
   };
   for (uint32_t spins = 0;; ++spins) {
     uint32_t z = 0;
-    if (__atomic_compare_exchange_n(&busy_[e], &z, 1u, true, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) break;
+    if (__atomic_compare_exchange_n(&ent_[e].busy, &z, 1u, true, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) break;
     // an entry a timed-out caller abandoned (busy 2) is reclaimed once the worker has finished it
     z = 2;
-    if (finished(e) && __atomic_compare_exchange_n(&busy_[e], &z, 1u, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) {
+    if (finished(e) && __atomic_compare_exchange_n(&ent_[e].busy, &z, 1u, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) {
       if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
       break;
     }
     if ((spins & 63) == 63) {
       // an entry held by a process that died is abandoned (its call is reclaimed once finished)
-      const int32_t h = __atomic_load_n(&holder_[e], __ATOMIC_RELAXED);
+      const int32_t h = __atomic_load_n(&ent_[e].holder, __ATOMIC_RELAXED);
       z = 1;
       if (mode_ != kPrivate && h > 0 && h != pid_ && kill(h, 0) != 0 && errno == ESRCH)
-        (void)__atomic_compare_exchange_n(&busy_[e], &z, 2u, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+        (void)__atomic_compare_exchange_n(&ent_[e].busy, &z, 2u, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
       _mm_pause();
       if (elapsed_us() > 30000000u) {  // every entry held for 30 s: the GPU stopped serving
         errno = EBUSY;
@@ -986,7 +980,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     }
     e = entry_of(++t);
   }
-  __atomic_store_n(&holder_[e], pid_, __ATOMIC_RELAXED);
+  __atomic_store_n(&ent_[e].holder, pid_, __ATOMIC_RELAXED);
   RingCmd* c = cmds_ + e;
   uint32_t done_word = kRingDone;
   if (vr_) {
@@ -1004,9 +998,9 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     if (in && in_len) std::memcpy(v_pay_h_ + (size_t)e * pstride_, in, in_len);
     std::memcpy((void*)(v_cmds_h_ + e), &rc, sizeof rc);
     c->out_len = 0;  // written by the worker only when the op returns bytes
-    uint32_t seq = seqs_[e] + 1;
+    uint32_t seq = ent_[e].seq + 1;
     if (seq == 0) seq = 1;  // 0 is the initial "served" value
-    __atomic_store_n(&seqs_[e], seq, __ATOMIC_RELEASE);
+    __atomic_store_n(&ent_[e].seq, seq, __ATOMIC_RELEASE);
     done_word = seq;
     _mm_sfence();
     *(volatile uint32_t*)(v_door_h_ + e) = seq;
@@ -1077,7 +1071,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
         ensure_worker();  // the worker idled out meanwhile
         const bool dead = mode_ == kClient && server_gone();
         if (dead || us > 30000000u) {  // the GPU stopped serving: abandon the entry (reclaimed once done)
-          __atomic_store_n(&busy_[e], 2u, __ATOMIC_RELEASE);
+          __atomic_store_n(&ent_[e].busy, 2u, __ATOMIC_RELEASE);
           if (dead) gone_.store(true, std::memory_order_release);
           errno = dead ? EIO : ETIMEDOUT;
           return -1;
@@ -1104,7 +1098,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
   if (out && out_cap && r->out_len && r->status >= 0)
     std::memcpy(out, payload_ + (size_t)e * pstride_, r->out_len < out_cap ? r->out_len : out_cap);
   if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
-  __atomic_store_n(&busy_[e], 0u, __ATOMIC_RELEASE);
+  __atomic_store_n(&ent_[e].busy, 0u, __ATOMIC_RELEASE);
   return 0;
 }
 

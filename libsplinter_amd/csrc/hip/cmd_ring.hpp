@@ -108,10 +108,19 @@ struct RingShared {
 // VRAM mode completion, one 16-B chunk per entry in host memory, written by ONE device store (the
 // NVMe completion-entry pattern): the call's sequence number with its status and result, so an op
 // without output bytes completes with a single PCIe write and no drain of it
-struct alignas(16) RingDone {
+struct alignas(64) RingDone {  // one cache line per entry: a completion never disturbs another entry's poller
   uint32_t seq;
   int32_t status;
   uint64_t result;
+  uint8_t pad[48];
+};
+
+// Host-side ownership of one entry (own cache line: callers on different entries share no line)
+struct alignas(64) RingEntryCtl {
+  uint32_t busy;    // 0 free, 1 held, 2 abandoned (reclaimed once its call is done)
+  int32_t holder;   // pid holding the entry (a dead holder's entry is reclaimed)
+  uint32_t seq;     // last sequence number issued
+  uint32_t pad[13];
 };
 
 struct RingResult {
@@ -151,9 +160,7 @@ struct RingSegHdr {
   uint32_t ticket;   // entry tickets of every process
   uint32_t launches;
   char sock[96];     // abstract socket serving the request chunk's dmabuf fds
-  uint32_t busy[kRingEntries];    // 0 free, 1 held, 2 abandoned (reclaimed once its call is done)
-  int32_t holder[kRingEntries];   // pid holding the entry (dead holders' entries are reclaimed)
-  uint32_t seqs[kRingEntries];    // last sequence number issued per entry
+  RingEntryCtl ent[kRingEntries];
 };
 constexpr uint32_t kRingSegMagic = 0x52494e47;  // "RING"
 
@@ -202,15 +209,11 @@ class CmdRing {
   uint8_t* d_payload_ = nullptr;
   RingDone* vdone_ = nullptr;     // VRAM mode completion chunks
   RingDone* d_vdone_ = nullptr;
-  uint32_t* busy_ = nullptr;      // entry ownership (own_ or the segment)
-  int32_t* holder_ = nullptr;
-  uint32_t* seqs_ = nullptr;
+  RingEntryCtl* ent_ = nullptr;   // entry ownership (own_ or the segment)
   uint32_t* ticket_ = nullptr;
   struct Own {
-    uint32_t busy[kRingEntries] = {};
-    int32_t holder[kRingEntries] = {};
-    uint32_t seqs[kRingEntries] = {};
-    uint32_t ticket = 0;
+    RingEntryCtl ent[kRingEntries] = {};
+    alignas(64) uint32_t ticket = 0;
   } own_;
   uint8_t* scratch_ = nullptr;    // device, kRingEntries x pstride_ (+64 key)
   uint32_t pstride_ = 0;

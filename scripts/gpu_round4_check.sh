@@ -22,12 +22,17 @@ if [ -n "$EXTRA_RING" ]; then
   # server (default) and with a worker per process (SPLINTER_RING_SHARED=0); encoder beside 4 clients
   H=./libsplinter_amd/bin/splinter_hostapi_bench
   for t in 1 32 64; do step ring_t$t timeout -k 10 120 $H --store hbm:rt$t --threads $t --seconds 2 --keys 20000; done
+  for t in 32 64; do
+    step ring_t${t}_private env SPLINTER_RING_SHARED=0 timeout -k 10 120 $H --store hbm:ru$t --threads $t --seconds 2 \
+      --keys 20000
+  done
   for t in 8 16; do
     step ring_p4t${t}_shared timeout -k 10 120 $H --store hbm:rp$t --procs 4 --threads $t --seconds 2 --keys 20000
     step ring_p4t${t}_private env SPLINTER_RING_SHARED=0 timeout -k 10 120 $H --store hbm:rq$t --procs 4 --threads $t \
       --seconds 2 --keys 20000
   done
-  step ring_interference timeout -k 10 300 python -u scripts/ring_interference.py --clients 4 --threads 8 --steps 20
+  step ring_interference timeout -k 10 300 python -u scripts/ring_interference.py --clients 4 --threads ${RI_THREADS:-1,2,8} \
+    --steps 20
 fi
 if [ -z "$SKIP_BENCH" ]; then
   step bench timeout -k 10 300 python -u bench.py --steps 20 --warmup 5

@@ -736,7 +736,10 @@ int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, c
   seg_ = (RingSegHdr*)p;
   seg_bytes_ = L.total;
   seg_name_ = seg;
-  if (hipHostRegister(p, L.total, hipHostRegisterMapped) != hipSuccess) return -1;
+  // SPLINTER_RING_REG_FLAGS: hipHostRegister flags of the segment (measurement knob; default mapped)
+  const unsigned rf = (unsigned)strtoul(getenv("SPLINTER_RING_REG_FLAGS") ? getenv("SPLINTER_RING_REG_FLAGS") : "2",
+                                        nullptr, 0);
+  if (hipHostRegister(p, L.total, rf | hipHostRegisterMapped) != hipSuccess) return -1;
   seg_registered_ = true;
   uint8_t* dp = nullptr;
   if (hipHostGetDevicePointer((void**)&dp, p, 0) != hipSuccess) return -1;
@@ -751,6 +754,7 @@ int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, c
   d_payload_ = dp + L.pay;
   ent_ = seg_->ent;
   ticket_ = &seg_->ticket;
+  waiters_ = &seg_->waiters;
   // the request chunk's descriptors, for clients' BAR mappings
   char sock[96];
   snprintf(sock, sizeof sock, "splinter-ring-%d-%s", (int)getpid(), seg.c_str() + (seg[0] == '/'));
@@ -832,6 +836,7 @@ int CmdRing::init_client(const std::string& seg, int device, uint32_t pstride) {
   payload_ = hp + L.pay;
   ent_ = seg_->ent;
   ticket_ = &seg_->ticket;
+  waiters_ = &seg_->waiters;
   device_ = device;
   read_env();
   vr_ = true;
@@ -889,9 +894,24 @@ void CmdRing::launch(const spl_arena_t& a) {
   (void)hipGetDevice(&cur);
   if (cur != device_) (void)hipSetDevice(device_);
   if (!stream_) {  // created on first use: a store that never takes a per-call op claims no queue
-    int lo = 0, hi = 0;
-    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi);
+    // SPLINTER_RING_CUS=n: the worker's waves confined to n CUs spread over the chip (a CU-masked
+    // queue), so fewer of the encoder's workgroups share a CU with a polling wave
+    const int ncu = env_int("SPLINTER_RING_CUS", 0);
+    int total = 0;
+    (void)hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device_);
+    if (ncu > 0 && total > ncu) {
+      std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
+      for (int i = 0; i < ncu; ++i) {
+        const int cu = (int)((long)i * total / ncu);
+        mask[(size_t)cu / 32] |= 1u << (cu % 32);
+      }
+      if (hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()) != hipSuccess) stream_ = nullptr;
+    }
+    if (!stream_) {
+      int lo = 0, hi = 0;
+      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+      (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi);
+    }
   }
   // stream order: the previous worker (if still draining) has exited before ctrl is reset
   const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)kRingGroups};
@@ -1029,11 +1049,13 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
   // burns the quota every waiter shares -- the scheduler then throttles the whole process, the
   // 16 -> 32 thread collapse of profiles/r2_hostapi_ring_v3.md -- so while more callers wait than
   // there are CPUs every waiter sleeps ~2 us between polls (1 us timer slack): the calls stay in
-  // flight on the GPU without holding a CPU each.
-  waiters_.fetch_add(1, std::memory_order_relaxed);
+  // flight on the GPU without holding a CPU each.  A ring server's waiters are counted over every
+  // process that submits to it (the segment's counter: the processes share the same CPUs; a client
+  // that dies mid-call leaves its count behind, which only makes waiters sleep-poll sooner).
+  __atomic_fetch_add(waiters_, 1, __ATOMIC_RELAXED);
   struct Leave {
-    std::atomic<int>& w;
-    ~Leave() { w.fetch_sub(1, std::memory_order_relaxed); }
+    int32_t* w;
+    ~Leave() { __atomic_fetch_sub(w, 1, __ATOMIC_RELAXED); }
   } leave{waiters_};
   bool slept = false;
   for (uint64_t spins = 1;; ++spins) {
@@ -1045,7 +1067,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
       const uint64_t us = elapsed_us();
       // re-decided every poll round: once more callers wait than there are CPUs, EVERY waiter
       // (also those that started spinning before the others arrived) sleep-polls
-      const bool oversub = waiters_.load(std::memory_order_relaxed) > cpus_;
+      const bool oversub = __atomic_load_n(waiters_, __ATOMIC_RELAXED) > cpus_;
       if (us > (oversub ? oversub_spin_us_ : yield_after_us_) || (oversub && oversub_spin_us_ == 0)) {
         if (oversub) {
           static thread_local bool slack = false;

@@ -160,6 +160,7 @@ struct RingSegHdr {
   uint32_t ticket;   // entry tickets of every process
   uint32_t launches;
   char sock[96];     // abstract socket serving the request chunk's dmabuf fds
+  alignas(64) int32_t waiters;  // callers of every process waiting on a completion right now
   RingEntryCtl ent[kRingEntries];
 };
 constexpr uint32_t kRingSegMagic = 0x52494e47;  // "RING"
@@ -250,7 +251,8 @@ class CmdRing {
   std::atomic<bool> gone_{false}; // client: the server went away; calls use priv_
   std::unique_ptr<CmdRing> priv_;
   std::mutex priv_mu_;
-  std::atomic<int> waiters_{0};   // host threads waiting on a completion right now
+  int32_t waiters_own_ = 0;       // host threads of this process waiting on a completion right now
+  int32_t* waiters_ = &waiters_own_;  // ... or of every process of a ring server (segment)
   long sleep_ns_ = 5000;          // SPLINTER_RING_SLEEP_NS: sleep between polls while oversubscribed
   long first_sleep_ns_ = 6000;    // SPLINTER_RING_FIRST_SLEEP_NS: the first of those sleeps (a call's bulk)
   uint64_t oversub_spin_us_ = 0;  // SPLINTER_RING_OVERSUB_SPIN_US: spin this long first while oversubscribed

@@ -2,6 +2,7 @@
 #include "node_store.hpp"
 
 #include <cerrno>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -406,6 +407,31 @@ inline void copy_row(uint8_t* d, const uint8_t* s, long w) {
 }
 }  // namespace
 
+// SPLINTER_NODE_BATCH_TRACE=1: per batch, ms in plan / gather / shards / scatter on stderr
+struct BatchTrace {
+  bool on;
+  const char* what;
+  long n;
+  std::chrono::steady_clock::time_point t0, t;
+  double ms[4] = {0, 0, 0, 0};
+  BatchTrace(const char* w, long n_) : what(w), n(n_) {
+    static const bool env = getenv("SPLINTER_NODE_BATCH_TRACE") && atoi(getenv("SPLINTER_NODE_BATCH_TRACE")) != 0;
+    on = env;
+    if (on) t0 = t = std::chrono::steady_clock::now();
+  }
+  void mark(int i) {
+    if (!on) return;
+    const auto now = std::chrono::steady_clock::now();
+    ms[i] += std::chrono::duration<double, std::milli>(now - t).count();
+    t = now;
+  }
+  ~BatchTrace() {
+    if (on)
+      fprintf(stderr, "{\"node_batch\": \"%s\", \"n\": %ld, \"plan_ms\": %.2f, \"gather_ms\": %.2f, \"shards_ms\": %.2f, "
+              "\"scatter_ms\": %.2f}\n", what, n, ms[0], ms[1], ms[2], ms[3]);
+  }
+};
+
 struct NodeStore::Plan {
   std::vector<long> pos;    // pos[i]: sorted position of client op i
   std::vector<long> off;    // shard j's ops are sorted positions [off[j], off[j+1])
@@ -416,12 +442,10 @@ struct NodeStore::Plan {
     const int T = n < 65536 ? 1 : kNodeBatchThreads;
     std::vector<long> cnt((size_t)T * nsh, 0);
     par_range(n, [&](long b, long e, int t) {
-      char k[64];
       long* c = cnt.data() + (size_t)t * nsh;
       for (long i = b; i < e; ++i) {
-        std::memcpy(k, keys + i * kstride, (size_t)cut);
-        k[cut] = 0;
-        const int d = node_shard_of(KeyRef(k).hash, nsh);
+        const char* rec = keys + i * kstride;  // the canonical key: its bytes up to the first NUL
+        const int d = node_shard_of(fnv1a_n(rec, strnlen(rec, (size_t)cut)), nsh);
         dest[(size_t)i] = d;
         ++c[d];
       }
@@ -492,7 +516,9 @@ inline long a64(long x) { return (x + 63) & ~63L; }
 long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
                           long n, int32_t* status, int retries) {
   const int nsh = nshards();
+  BatchTrace tr("set", n);
   Plan pl(keys, kstride, n, nsh);
+  tr.mark(0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
   const long ob = 0, vb = a64(n * kstride), lb = vb + a64(n * (long)vstride), sb = lb + a64(n * 4);
   uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
@@ -500,6 +526,7 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
   pl.gather(S + ob, keys, kstride);
   pl.gather(S + vb, vals, vstride);
   pl.gather(S + lb, lens, 4);
+  tr.mark(1);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
@@ -513,20 +540,25 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
     if (r < 0) fail = true;
     else ok += r;
   });
+  tr.mark(2);
   if (fail) return -1;
   if (status) pl.scatter(status, S + sb, 4);
+  tr.mark(3);
   return ok.load();
 }
 
 long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
                           int32_t* status, int retries) {
   const int nsh = nshards();
+  BatchTrace tr("get", n);
   Plan pl(keys, kstride, n, nsh);
+  tr.mark(0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
   const long ob = 0, sb = a64(n * kstride), lb = sb + a64(n * 4), vb = lb + a64(n * 4);
   uint8_t* S = scratch((size_t)(vb + (out ? a64(n * (long)ostride) : 0)));
   if (!S) return -1;
   pl.gather(S + ob, keys, kstride);
+  tr.mark(1);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
@@ -540,17 +572,21 @@ long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostri
     if (r < 0) fail = true;
     else ok += r;
   });
+  tr.mark(2);
   if (fail) return -1;
   if (status) pl.scatter(status, S + sb, 4);
   if (out_lens) pl.scatter(out_lens, S + lb, 4);
   if (out) pl.scatter(out, S + vb, ostride);
+  tr.mark(3);
   return ok.load();
 }
 
 long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,
                             int32_t* status, uint64_t* results) {
   const int nsh = nshards();
+  BatchTrace tr("intop", n);
   Plan pl(keys, kstride, n, nsh);
+  tr.mark(0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
   const long kb = 0, pb = a64(n * kstride), mb = pb + a64(n * 4), sb = mb + a64(n * 8), rb = sb + a64(n * 4);
   uint8_t* S = scratch((size_t)(rb + a64(n * 8)));
@@ -559,6 +595,7 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
   pl.gather(S + pb, ops, 4);
   if (masks) pl.gather(S + mb, masks, 8);
   else std::memset(S + mb, 0, (size_t)(n * 8));
+  tr.mark(1);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
@@ -573,21 +610,26 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
     if (r < 0) fail = true;
     else ok += r;
   });
+  tr.mark(2);
   if (fail) return -1;
   if (status) pl.scatter(status, S + sb, 4);
   if (results) pl.scatter(results, S + rb, 8);
+  tr.mark(3);
   return ok.load();
 }
 
 long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) {
   const int nsh = nshards();
+  BatchTrace tr("set_embedding", n);
   Plan pl(keys, kstride, n, nsh);
+  tr.mark(0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
   const long kb = 0, vb = a64(n * kstride), sb = vb + n * (long)kEmbedBytes;
   uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
   if (!S) return -1;
   pl.gather(S + kb, keys, kstride);
   pl.gather(S + vb, vecs, (long)kEmbedBytes);
+  tr.mark(1);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
@@ -600,8 +642,10 @@ long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* 
     if (r < 0) fail = true;
     else ok += r;
   });
+  tr.mark(2);
   if (fail) return -1;
   if (status) pl.scatter(status, S + sb, 4);
+  tr.mark(3);
   return ok.load();
 }
 

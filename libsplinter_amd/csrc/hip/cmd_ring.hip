@@ -451,7 +451,7 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
   }
 }
 
-// Workgroup g serves entries g*kGroupEntries + lane (lanes 0..kGroupEntries-1).
+// Workgroup g serves entries g*per + lane (lanes 0..per-1, per = kRingEntries / groups).
 // ctrl (device): [0] u64 wall clock of the last served call (any group), [8] u32 dying,
 // [12] u32 live waves (set to gridDim.x by the launcher).
 // VR (VRAM requests): records, input payloads and doorbells live in device memory that the host
@@ -465,10 +465,10 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
                                                     const uint32_t* vdoor, const uint8_t* payload_in,
                                                     uint8_t* payload, uint32_t pstride, uint8_t* scratch,
                                                     uint8_t* ctrl, uint32_t* served, RingDone* vdone,
-                                                    uint64_t idle_ticks) {
+                                                    uint64_t idle_ticks, int per) {
   const int lane = threadIdx.x, g = blockIdx.x;
-  const bool mine = lane < kGroupEntries;
-  const int e = g * kGroupEntries + (mine ? lane : 0);
+  const bool mine = lane < per;
+  const int e = g * per + (mine ? lane : 0);
 #ifdef SPL_RING_STAMPS
   g_ent[g * 64 + lane] = e;
 #endif
@@ -635,6 +635,12 @@ void CmdRing::read_env() {
   first_sleep_ns_ = env_int("SPLINTER_RING_FIRST_SLEEP_NS", 6000);
   oversub_spin_us_ = (uint64_t)env_int("SPLINTER_RING_OVERSUB_SPIN_US", 0);
   adaptive_ = env_int("SPLINTER_RING_ADAPTIVE_SLEEP", 1) != 0;
+  // SPLINTER_RING_GROUPS: worker waves (1..32, a power of two; entries per wave = 256 / groups).  Each
+  // resident worker wave (233 VGPRs) keeps the encoder's 2-wave-per-SIMD GEMM workgroups off its CU
+  int g = env_int("SPLINTER_RING_GROUPS", kDefaultRingGroups);
+  int p2 = 1;
+  while (p2 * 2 <= g && p2 < kRingGroups) p2 *= 2;
+  groups_ = g < 1 ? 1 : p2;
 }
 
 // Host-side buffers of a private ring: pinned, coherent, device-mapped (host view == device view).
@@ -762,6 +768,7 @@ int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, c
   std::memcpy(seg_->sock, sock, sizeof sock);
   seg_->pstride = pstride_;
   seg_->entries = kRingEntries;
+  seg_->groups = (uint32_t)groups_;
   seg_->version = 1;
   seg_->owner_pid = pid_;
   sup_ = std::thread([this] { supervise(); });
@@ -839,6 +846,7 @@ int CmdRing::init_client(const std::string& seg, int device, uint32_t pstride) {
   waiters_ = &seg_->waiters;
   device_ = device;
   read_env();
+  if (seg_->groups >= 1 && seg_->groups <= (uint32_t)kRingGroups) groups_ = (int)seg_->groups;
   vr_ = true;
   mode_ = kClient;
   return 0;
@@ -914,15 +922,16 @@ void CmdRing::launch(const spl_arena_t& a) {
     }
   }
   // stream order: the previous worker (if still draining) has exited before ctrl is reset
-  const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)kRingGroups};
+  const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)groups_};
   (void)hipMemcpyAsync(ctrl_, init, sizeof init, hipMemcpyHostToDevice, stream_);
   if (vr_)
-    hipLaunchKernelGGL(k_ring_worker<true>, dim3(kRingGroups), dim3(64), 0, stream_, a, v_cmds_d_, d_cmds_, d_shared_,
-                       v_door_d_, v_pay_d_, d_payload_, pstride_, scratch_, ctrl_, served_, d_vdone_, idle_ticks_);
+    hipLaunchKernelGGL(k_ring_worker<true>, dim3(groups_), dim3(64), 0, stream_, a, v_cmds_d_, d_cmds_, d_shared_,
+                       v_door_d_, v_pay_d_, d_payload_, pstride_, scratch_, ctrl_, served_, d_vdone_, idle_ticks_,
+                       kRingEntries / groups_);
   else
-    hipLaunchKernelGGL(k_ring_worker<false>, dim3(kRingGroups), dim3(64), 0, stream_, a, d_cmds_, d_cmds_, d_shared_,
+    hipLaunchKernelGGL(k_ring_worker<false>, dim3(groups_), dim3(64), 0, stream_, a, d_cmds_, d_cmds_, d_shared_,
                        (const uint32_t*)nullptr, (const uint8_t*)nullptr, d_payload_, pstride_, scratch_, ctrl_,
-                       (uint32_t*)nullptr, (RingDone*)nullptr, idle_ticks_);
+                       (uint32_t*)nullptr, (RingDone*)nullptr, idle_ticks_, kRingEntries / groups_);
   if (cur != device_) (void)hipSetDevice(cur);
 }
 
@@ -959,9 +968,10 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
   // different worker waves -- which run in parallel -- instead of sharing one wave whose lanes
   // would serve them with divergent ops
   const bool spread = spread_;
-  auto entry_of = [spread](uint32_t t) {
+  const uint32_t G = (uint32_t)groups_, per = (uint32_t)(kRingEntries / groups_);
+  auto entry_of = [spread, G, per](uint32_t t) {
     t %= kRingEntries;
-    return spread ? (t % kRingGroups) * kGroupEntries + t / kRingGroups : t;
+    return spread ? (t % G) * per + t / G : t;
   };
   auto finished = [this](uint32_t e) {
     return vr_ ? __atomic_load_n(&vdone_[e].seq, __ATOMIC_ACQUIRE) == __atomic_load_n(&ent_[e].seq, __ATOMIC_ACQUIRE)

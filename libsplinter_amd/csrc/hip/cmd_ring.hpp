@@ -6,10 +6,13 @@
 // A kernel launch + copies + stream sync per call costs tens of µs; instead each process keeps
 //   * a ring of kEntries command records in pinned, host-coherent memory (one per lane),
 //   * a contiguous doorbell array state[kEntries],
-//   * ONE resident worker kernel (k_ring_worker) of kRingGroups one-wave workgroups on a
-//     high-priority stream; lane i of group g serves entry g*kGroupEntries+i and each group polls
-//     its doorbells in ONE 32-B read, so concurrent host threads' calls run in parallel waves
-//     with little op divergence inside a wave.  (One kernel, not one per group: streams share
+//   * ONE resident worker kernel (k_ring_worker) of `groups` one-wave workgroups on a
+//     high-priority stream (SPLINTER_RING_GROUPS, default 8); lane i of group g serves entry
+//     g*per+i (per = kRingEntries / groups) and each group polls its doorbells in one coalesced
+//     read, so concurrent host threads' calls run in parallel waves.  Few waves on purpose: a
+//     worker wave holds 233 VGPRs for its whole life, and a CU that hosts one cannot take the
+//     encoder's GEMM workgroups (2 waves per SIMD at 226-250 VGPRs), so 32 waves cost the
+//     encoder ~20 % beside live clients (profiles/r4g ring_interference).  (One kernel, not one per group: streams share
 //     GPU_MAX_HW_QUEUES hardware queues, and a group queued behind another group's resident
 //     kernel would wait out that kernel's idle timeout.)
 // Ring server: the process that created the store (its owner) runs the store's ONE worker and
@@ -83,9 +86,9 @@ static_assert(sizeof(RingCmd) == 128, "ring record");
 static_assert(offsetof(RingCmd, status) % 16 == 0 && offsetof(RingCmd, result) == offsetof(RingCmd, status) + 8,
               "the completion words must form one 16-B chunk");
 
-constexpr int kRingGroups = 32;                     // independent one-wave workers (one per concurrent caller up to 32)
-constexpr int kGroupEntries = 8;                    // entries per worker (lanes 0..7)
-constexpr int kRingEntries = kRingGroups * kGroupEntries;
+constexpr int kRingGroups = 32;                     // most one-wave workers (SPLINTER_RING_GROUPS)
+constexpr int kDefaultRingGroups = 8;               // default worker waves
+constexpr int kRingEntries = 256;                   // entries (per wave: kRingEntries / groups)
 
 struct RingShared {
   uint32_t state[kRingEntries];  // doorbells (one 32-B read per group)
@@ -159,6 +162,8 @@ struct RingSegHdr {
   uint32_t want;     // futex word: bumped by a client that found the worker gone
   uint32_t ticket;   // entry tickets of every process
   uint32_t launches;
+  uint32_t groups;   // worker waves (the server's SPLINTER_RING_GROUPS)
+  uint32_t pad0[3];
   char sock[96];     // abstract socket serving the request chunk's dmabuf fds
   alignas(64) int32_t waiters;  // callers of every process waiting on a completion right now
   RingEntryCtl ent[kRingEntries];
@@ -223,6 +228,7 @@ class CmdRing {
   uint64_t idle_ticks_ = 0;
   int clock_khz_ = 100000;
   bool spread_ = true;            // SPLINTER_RING_SPREAD: consecutive calls on different waves
+  int groups_ = kDefaultRingGroups;  // worker waves
   uint64_t yield_after_us_ = 20;  // SPLINTER_RING_SPIN_US: spin this long, then yield between polls
   int cpus_ = 1;                  // CPUs the process may run on (affinity, cgroup quota)
   // VRAM request mode (SPLINTER_RING_VRAM=1): records, input payloads and sequence-number doorbells

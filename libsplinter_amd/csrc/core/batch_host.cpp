@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <sched.h>
+#include <time.h>
 #include <thread>
 #include <vector>
 
@@ -61,7 +62,15 @@ inline void key_of(const char* rec, int kstride, char* out) {
 // EAGAIN = the slot's writer is mid-write; past a few immediate retries let it run (a preempted
 // writer on an oversubscribed host would otherwise exhaust the retries while it sleeps)
 inline void backoff(int t) {
-  if (t >= 4) sched_yield();
+  if (t < 4) return;
+  if (t < 16) {
+    sched_yield();
+    return;
+  }
+  // still held: the holder is likely preempted (more runnable threads than CPUs) -- sleep so it runs
+  const long us = 20L * (t - 15) < 1000 ? 20L * (t - 15) : 1000;
+  const timespec ts{0, us * 1000};
+  nanosleep(&ts, nullptr);
 }
 
 inline int32_t code_of(int rc) {

@@ -2,6 +2,7 @@
 #include "node_store.hpp"
 
 #include <cerrno>
+#include <memory>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -513,72 +514,127 @@ namespace {
 inline long a64(long x) { return (x + 63) & ~63L; }
 }
 
+namespace {
+// SPLINTER_NODE_BATCH_CHUNK: ops per pipeline chunk of a node batch (default 524288)
+long node_chunk_ops() {
+  const char* e = getenv("SPLINTER_NODE_BATCH_CHUNK");
+  const long v = e ? atol(e) : 0;
+  return v > 0 ? v : 524288L;
+}
+}  // namespace
+
+// HBM shards wait on their GPUs while the host prepares the next chunk; host shards would only
+// compete with it for CPUs, so their batches run as one chunk
+long NodeStore::chunk_for(long n) const { return std::min(n, desc_->backend == 1 ? node_chunk_ops() : n); }
+
+// Chunked two-stage pipeline: prep(c0, m, S) partitions and copies chunk [c0, c0+m) into scratch
+// half S (host threads), exec(plan, c0, m, S) runs every shard on it and copies the outputs back
+// (shard threads wait on their GPUs); chunk c+1 is prepared while chunk c executes.
+template <class Prep, class Exec>
+long NodeStore::pipeline(long n, long per, Prep&& prep, Exec&& exec) {
+  const long C = chunk_for(n);
+  const long nch = (n + C - 1) / C;
+  uint8_t* S0 = scratch((size_t)(per * (nch > 1 ? 2 : 1)));
+  if (!S0) return -1;
+  long ok = 0;
+  bool fail = false;
+  std::unique_ptr<Plan> cur = prep(0L, C, S0);
+  for (long c = 0; c < nch; ++c) {
+    const long c0 = c * C, m = std::min(C, n - c0);
+    uint8_t* S = S0 + (c & 1) * per;
+    long r = 0;
+    std::unique_ptr<Plan> next;
+    if (c + 1 < nch) {
+      std::thread th([&] { r = exec(*cur, c0, m, S); });
+      next = prep(c0 + C, std::min(C, n - c0 - C), S0 + ((c + 1) & 1) * per);
+      th.join();
+    } else {
+      r = exec(*cur, c0, m, S);
+    }
+    if (r < 0) fail = true;
+    else ok += r;
+    cur = std::move(next);
+  }
+  return fail ? -1 : ok;
+}
+
 long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens,
                           long n, int32_t* status, int retries) {
   const int nsh = nshards();
   BatchTrace tr("set", n);
-  Plan pl(keys, kstride, n, nsh);
-  tr.mark(0);
+  const long C = chunk_for(n);
+  const long ob = 0, vb = a64(C * kstride), lb = vb + a64(C * (long)vstride), sb = lb + a64(C * 4), per = sb + a64(C * 4);
   std::lock_guard<std::mutex> lk(scratch_mu_);
-  const long ob = 0, vb = a64(n * kstride), lb = vb + a64(n * (long)vstride), sb = lb + a64(n * 4);
-  uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
-  if (!S) return -1;
-  pl.gather(S + ob, keys, kstride);
-  pl.gather(S + vb, vals, vstride);
-  pl.gather(S + lb, lens, 4);
-  tr.mark(1);
-  std::atomic<bool> fail{false};
-  std::atomic<long> ok{0};
-  pl.each_shard([&](int j, long o, long m) {
-    StoreBase* sh = shards_[(size_t)j];
-    const char* k = (const char*)S + ob + o * kstride;
-    const uint8_t* v = S + vb + o * (long)vstride;
-    const uint32_t* l = (const uint32_t*)(S + lb) + o;
-    int32_t* st = (int32_t*)(S + sb) + o;
-    long r = sh->set_batch(k, kstride, v, vstride, l, m, st, retries);
-    if (r == kNoBatch) r = generic_set_batch(sh, k, kstride, v, vstride, l, m, st, retries, 4);
-    if (r < 0) fail = true;
-    else ok += r;
-  });
+  auto prep = [&](long c0, long m, uint8_t* S) {
+    auto pl = std::make_unique<Plan>(keys + c0 * kstride, kstride, m, nsh);
+    tr.mark(0);
+    pl->gather(S + ob, keys + c0 * kstride, kstride);
+    pl->gather(S + vb, vals + c0 * (long)vstride, vstride);
+    pl->gather(S + lb, lens + c0, 4);
+    tr.mark(1);
+    return pl;
+  };
+  auto exec = [&](const Plan& pl, long c0, long, uint8_t* S) -> long {
+    std::atomic<bool> fail{false};
+    std::atomic<long> ok{0};
+    pl.each_shard([&](int j, long o, long m) {
+      StoreBase* sh = shards_[(size_t)j];
+      const char* k = (const char*)S + ob + o * kstride;
+      const uint8_t* v = S + vb + o * (long)vstride;
+      const uint32_t* l = (const uint32_t*)(S + lb) + o;
+      int32_t* st = (int32_t*)(S + sb) + o;
+      long r = sh->set_batch(k, kstride, v, vstride, l, m, st, retries);
+      if (r == kNoBatch) r = generic_set_batch(sh, k, kstride, v, vstride, l, m, st, retries, 4);
+      if (r < 0) fail = true;
+      else ok += r;
+    });
+    if (fail) return -1;
+    if (status) pl.scatter(status + c0, S + sb, 4);
+    return ok.load();
+  };
+  const long r = pipeline(n, per, prep, exec);
   tr.mark(2);
-  if (fail) return -1;
-  if (status) pl.scatter(status, S + sb, 4);
-  tr.mark(3);
-  return ok.load();
+  return r;
 }
 
 long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostride, uint32_t* out_lens, long n,
                           int32_t* status, int retries) {
   const int nsh = nshards();
   BatchTrace tr("get", n);
-  Plan pl(keys, kstride, n, nsh);
-  tr.mark(0);
+  const long C = chunk_for(n);
+  const long ob = 0, sb = a64(C * kstride), lb = sb + a64(C * 4), vb = lb + a64(C * 4);
+  const long per = vb + (out ? a64(C * (long)ostride) : 0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
-  const long ob = 0, sb = a64(n * kstride), lb = sb + a64(n * 4), vb = lb + a64(n * 4);
-  uint8_t* S = scratch((size_t)(vb + (out ? a64(n * (long)ostride) : 0)));
-  if (!S) return -1;
-  pl.gather(S + ob, keys, kstride);
-  tr.mark(1);
-  std::atomic<bool> fail{false};
-  std::atomic<long> ok{0};
-  pl.each_shard([&](int j, long o, long m) {
-    StoreBase* sh = shards_[(size_t)j];
-    const char* k = (const char*)S + ob + o * kstride;
-    uint8_t* v = out ? S + vb + o * (long)ostride : nullptr;
-    uint32_t* l = (uint32_t*)(S + lb) + o;
-    int32_t* st = (int32_t*)(S + sb) + o;
-    long r = sh->get_batch(k, kstride, v, ostride, l, m, st, retries);
-    if (r == kNoBatch) r = generic_get_batch(sh, k, kstride, v, ostride, l, m, st, retries, 4);
-    if (r < 0) fail = true;
-    else ok += r;
-  });
+  auto prep = [&](long c0, long m, uint8_t* S) {
+    auto pl = std::make_unique<Plan>(keys + c0 * kstride, kstride, m, nsh);
+    tr.mark(0);
+    pl->gather(S + ob, keys + c0 * kstride, kstride);
+    tr.mark(1);
+    return pl;
+  };
+  auto exec = [&](const Plan& pl, long c0, long, uint8_t* S) -> long {
+    std::atomic<bool> fail{false};
+    std::atomic<long> ok{0};
+    pl.each_shard([&](int j, long o, long m) {
+      StoreBase* sh = shards_[(size_t)j];
+      const char* k = (const char*)S + ob + o * kstride;
+      uint8_t* v = out ? S + vb + o * (long)ostride : nullptr;
+      uint32_t* l = (uint32_t*)(S + lb) + o;
+      int32_t* st = (int32_t*)(S + sb) + o;
+      long r = sh->get_batch(k, kstride, v, ostride, l, m, st, retries);
+      if (r == kNoBatch) r = generic_get_batch(sh, k, kstride, v, ostride, l, m, st, retries, 4);
+      if (r < 0) fail = true;
+      else ok += r;
+    });
+    if (fail) return -1;
+    if (status) pl.scatter(status + c0, S + sb, 4);
+    if (out_lens) pl.scatter(out_lens + c0, S + lb, 4);
+    if (out) pl.scatter(out + c0 * (long)ostride, S + vb, ostride);
+    return ok.load();
+  };
+  const long r = pipeline(n, per, prep, exec);
   tr.mark(2);
-  if (fail) return -1;
-  if (status) pl.scatter(status, S + sb, 4);
-  if (out_lens) pl.scatter(out_lens, S + lb, 4);
-  if (out) pl.scatter(out, S + vb, ostride);
-  tr.mark(3);
-  return ok.load();
+  return r;
 }
 
 long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const uint64_t* masks, long n,

@@ -144,6 +144,9 @@ class NodeStore final : public StoreBase {
  private:
   NodeStore() = default;
   struct Plan;  // node_store.cpp: a batch's shard partition
+  template <class Prep, class Exec>
+  long pipeline(long n, long per, Prep&& prep, Exec&& exec);  // node_store.cpp: chunked batches
+  long chunk_for(long n) const;
   uint8_t* scratch(size_t bytes);
   std::mutex scratch_mu_;
   uint8_t* scratch_ = nullptr;

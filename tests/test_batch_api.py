@@ -131,3 +131,30 @@ def test_batch_api_hbm_large_pinned_and_pageable(uniq):
     assert r.returncode == 0, r.stderr[-2000:]
     res = json.loads(r.stdout.strip().splitlines()[-1])
     assert res["get_check_failures"] == 0 and res["backend"] == "hbm"
+
+
+@pytest.mark.gpu
+def test_batch_api_node_hbm_pipelined_chunks(uniq, monkeypatch):
+    """A node batch larger than SPLINTER_NODE_BATCH_CHUNK runs as pipelined chunks (the next chunk
+    partitioned while the shards execute the current one): every op lands in client order."""
+    monkeypatch.setenv("SPLINTER_NODE_SHARDS", "4")
+    monkeypatch.setenv("SPLINTER_NODE_BATCH_CHUNK", "7000")
+    from libsplinter_amd import store as S
+    s = S.Store.create(f"node:{uniq}", slots=4 * 16384, max_val=256, embeddings=False)
+    try:
+        n = 30000
+        K = np.zeros((n, 16), dtype=np.uint8)
+        V = np.zeros((n, 64), dtype=np.uint8)
+        for i in range(n):
+            k = f"pk{i:08d}".encode()
+            K[i, : len(k)] = np.frombuffer(k, dtype=np.uint8)
+            V[i, :48] = (i * 13 + np.arange(48)) % 251
+        L = np.full(n, 48, dtype=np.uint32)
+        assert (s.set_batch(K, V, L) == 0).all()
+        perm = np.random.default_rng(1).permutation(n)
+        st, out, ln = s.get_batch(K[perm], width=64)
+        assert (st == 0).all() and (ln == 48).all() and np.array_equal(out[:, :48], V[perm, :48])
+        assert all(s.get(f"pk{i:08d}") == bytes(V[i, :48]) for i in range(0, n, 997))
+    finally:
+        s.close()
+        S.unlink(f"node:{uniq}")

@@ -4,6 +4,8 @@ store's per-call API (splinter_hostapi_bench --attach, 8 threads each).
 
   shared   the clients submit to the owner's ONE ring server (cmd_ring.hpp RingSegHdr, default)
   private  SPLINTER_RING_SHARED=0 in the clients: each runs its own resident ring worker
+  cpu      the same clients on a host shm store (no GPU work at all): the host-side share of the
+           slowdown (CPU contention with the encoder's launching thread)
 
 Prints one JSON line: encoder ms/step alone and beside the clients in either mode, the slowdown,
 and the clients' aggregate ops/s.
@@ -44,6 +46,7 @@ def main():
     ap.add_argument("--threads", default="2,8", help="client threads per process, comma list")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--keys", type=int, default=20000)
+    ap.add_argument("--modes", default="shared,private,cpu")
     a = ap.parse_args()
     name = f"hbm:ri{os.getpid()}"
     st = Store.create(name, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
@@ -57,11 +60,15 @@ def main():
             ph.run()
         out["encoder_ms_alone"] = round(time_steps(ph, a.steps), 3)
         secs = max(3.0, a.steps * out["encoder_ms_alone"] / 1e3 * 3 + 2.0)
+        shm = f"ri{os.getpid()}shm"
+        hs = Store.create(shm, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
+        hs.set_batch(keys, [b"v" * 150] * a.keys)
         for threads in [int(t) for t in a.threads.split(",")]:
-            for mode in ("shared", "private"):
+            for mode in a.modes.split(","):
                 env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
                            SPLINTER_RING_SHARED="1" if mode == "shared" else "0")
-                procs = [subprocess.Popen([TOOL, "--attach", "--store", name, "--threads", str(threads), "--seconds",
+                target = shm if mode == "cpu" else name
+                procs = [subprocess.Popen([TOOL, "--attach", "--store", target, "--threads", str(threads), "--seconds",
                                            str(secs), "--keys", str(a.keys)], env=env, stdout=subprocess.PIPE,
                                           stderr=subprocess.PIPE, text=True) for _ in range(a.clients)]
                 try:
@@ -87,6 +94,9 @@ def main():
                 print(json.dumps(out), file=sys.stderr, flush=True)
         out["encoder_ms_alone_after"] = round(time_steps(ph, a.steps), 3)
         ph.close()
+        hs.close()
+        from libsplinter_amd import store as S
+        S.unlink(shm)
     finally:
         st.close()
     print(json.dumps(out), flush=True)

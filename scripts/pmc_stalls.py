@@ -7,7 +7,10 @@ WAIT_ANY (parked on s_waitcnt / barrier) + WAIT_INST_ANY (issue stalls) + ACTIVE
 (MI355X_MICROARCH.md, rocprofv3 PMC slots).  MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8
 XCDs x 1024 SIMDs).
 
-python scripts/pmc_stalls.py COUNTER_COLLECTION.csv [--md]
+python scripts/pmc_stalls.py COUNTER_COLLECTION.csv [--md] [--max-grid THREADS]
+
+--max-grid: only dispatches of at most THREADS work-items (e.g. a KV step's slices and fused grid,
+not the 2048-workgroup prepopulation inserts).
 """
 import csv
 import re
@@ -24,8 +27,13 @@ def main():
     path = sys.argv[1]
     per = defaultdict(dict)
     names, dur = {}, {}
+    max_grid = int(sys.argv[sys.argv.index("--max-grid") + 1]) if "--max-grid" in sys.argv else 0
     for r in csv.DictReader(open(path)):
         d = int(r["Dispatch_Id"])
+        if max_grid:
+            g = r.get("Grid_Size") or r.get("Grid_Size_X") or "0"
+            if int(g) > max_grid:
+                continue
         per[d][r["Counter_Name"]] = float(r["Counter_Value"])
         names[d] = r["Kernel_Name"]
         dur[d] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3

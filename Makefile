@@ -1,6 +1,7 @@
 # libsplinter_amd native build (host C++ with g++, device code with hipcc for gfx950).
 # Outputs stay in-tree (libsplinter_amd/lib, libsplinter_amd/bin) so they travel
-# with the repo snapshot to the GPU box.
+# with the repo snapshot to the GPU box; every link writes NAME.tmp and renames it into place, so a
+# snapshot taken during a build never holds a half-written library.
 CXX      ?= g++
 HIPCC    ?= /opt/rocm/bin/hipcc
 ARCH     ?= gfx950
@@ -36,10 +37,10 @@ $(LIB) $(BIN) build/hip:
 	mkdir -p $@
 
 $(LIB)/libsplinter.so: $(CORE_SRCS) $(CORE_HDRS) | $(LIB)
-	$(CXX) $(CXXFLAGS) -shared -o $@ $(CORE_SRCS) $(LDLIBS)
+	$(CXX) $(CXXFLAGS) -shared -o $@.tmp $(CORE_SRCS) $(LDLIBS) && mv -f $@.tmp $@
 
 $(LIB)/libsplinter_p.so: $(CORE_SRCS) $(CORE_HDRS) | $(LIB)
-	$(CXX) $(CXXFLAGS) -DSPLINTER_PERSISTENT -shared -o $@ $(CORE_SRCS) $(LDLIBS)
+	$(CXX) $(CXXFLAGS) -DSPLINTER_PERSISTENT -shared -o $@.tmp $(CORE_SRCS) $(LDLIBS) && mv -f $@.tmp $@
 
 build/hip/%.o: $(SRC)/hip/%.hip $(HIP_HDRS) | build/hip
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
@@ -51,7 +52,7 @@ build/hip/nomic_kernels.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form -fno-honor-
 build/hip/decoder_kernels.o: HIPFLAGS += -mllvm -amdgpu-mfma-vgpr-form
 
 $(LIB)/libsplinter_hip.so: $(HIP_OBJS) $(LIB)/libsplinter.so | $(LIB)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(HIP_OBJS) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
+	$(HIPCC) $(HIPFLAGS) -shared -o $@.tmp $(HIP_OBJS) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN' $(LDLIBS) && mv -f $@.tmp $@
 
 # A/B builds of the HIP backend for one process-level switch (SPLINTER_HIP_VARIANT=<V> loads
 # lib/libsplinter_hip_<V>.so): make hip-variant V=name VFLAGS="-DSOMETHING"
@@ -64,10 +65,10 @@ hip-variant: $(LIB)/libsplinter.so | $(LIB)
 	  -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
 
 $(BIN)/%: $(SRC)/tools/%.cpp $(LIB)/libsplinter.so $(CORE_HDRS) | $(BIN)
-	$(CXX) $(CXXFLAGS) -o $@ $< -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN/../lib' $(LDLIBS)
+	$(CXX) $(CXXFLAGS) -o $@.tmp $< -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN/../lib' $(LDLIBS) && mv -f $@.tmp $@
 
 $(BIN)/splinterctl: $(wildcard $(SRC)/cli/*.cpp $(SRC)/cli/*.hpp) $(LIB)/libsplinter.so | $(BIN)
-	$(CXX) $(CXXFLAGS) -I$(SRC)/cli -o $@ $(filter %.cpp,$^) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN/../lib' $(LDLIBS)
+	$(CXX) $(CXXFLAGS) -I$(SRC)/cli -o $@.tmp $(filter %.cpp,$^) -L$(LIB) -lsplinter -Wl,-rpath,'$$ORIGIN/../lib' $(LDLIBS) && mv -f $@.tmp $@
 	ln -sf splinterctl $(BIN)/splinter_cli
 
 test: host tools

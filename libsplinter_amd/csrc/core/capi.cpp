@@ -260,7 +260,10 @@ long spl_list_copy(char* buf, size_t cap) {
 int spl_unlink(const char* raw) {
   Parsed p = parse_name(raw);
   if (p.kind == Kind::File) return unlink(p.name.c_str());
-  if (p.kind == Kind::Hbm) return shm_unlink((p.name + ".hbm").c_str());
+  if (p.kind == Kind::Hbm) {
+    (void)shm_unlink((p.name + ".ring").c_str());  // the ring server's segment (a crashed owner's)
+    return shm_unlink((p.name + ".hbm").c_str());
+  }
   if (p.kind == Kind::Node) {
     // every shard of the node, then its descriptor.  The shard count and backend come straight from
     // the mapped descriptor (no NodeStore::open, which would import every arena and refuses a node

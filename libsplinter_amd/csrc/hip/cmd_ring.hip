@@ -728,14 +728,15 @@ int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, c
   clock_khz_ = khz > 0 ? khz : 100000;
   idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
   if (init_vram() != 0) return -1;
-  // the segment: created under the store's umask like its descriptor, fresh (a stale one of a
-  // crashed owner of the same name is truncated away), registered for the worker's stores
+  // the segment: created under the store's umask like its descriptor, and fresh: a stale one of a
+  // crashed owner of the same name is unlinked first (never truncated: its clients may still map it)
   const SegLayout L(pstride_);
+  (void)shm_unlink(seg.c_str());
   mode_t prev = env_umask_push();
-  const int fd = shm_open(seg.c_str(), O_RDWR | O_CREAT | O_CLOEXEC, 0666);
+  const int fd = shm_open(seg.c_str(), O_RDWR | O_CREAT | O_EXCL | O_CLOEXEC, 0666);
   env_umask_pop(prev);
   if (fd < 0) return -1;
-  if (ftruncate(fd, 0) != 0 || ftruncate(fd, (off_t)L.total) != 0) { close(fd); shm_unlink(seg.c_str()); return -1; }
+  if (ftruncate(fd, (off_t)L.total) != 0) { close(fd); shm_unlink(seg.c_str()); return -1; }
   void* p = mmap(nullptr, L.total, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
   close(fd);
   if (p == MAP_FAILED) { shm_unlink(seg.c_str()); return -1; }

@@ -52,7 +52,7 @@ if [ -n "$EXTRA_PROF" ]; then
     --keys 4000000 --seconds 2 > "$OUT/batch_prof.out" 2>&1) || { echo "batch profile failed"; exit 1; }
 fi
 if [ -n "$EXTRA_KV" ]; then
-  for f in 0 1 2; do
+  for f in ${KV_MODES:-0 1 2}; do
     step bench_kv_fused$f env SPL_KVS_FUSED=$f timeout -k 10 300 python -u bench.py --mode kv --steps 20 --warmup 5 \
       --host-api 0 --host-api-threads2 0 --routed-steps 0
   done

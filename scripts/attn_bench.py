@@ -22,17 +22,16 @@ def main():
     from libsplinter_amd.models.nomic import Batch, _chk, _lib, _stream
     L = _lib()
     b128 = Batch([[0] * a.seq for _ in range(a.docs)])
-    b256 = Batch([[0] * a.seq for _ in range(a.docs)], qblock=256)  # variant 9: 8-wave blocks of 256 rows
     qkv = torch.randn(b128.T_pad, 3 * 768, device="cuda").bfloat16()
     out = torch.empty(b128.T_pad, 768, device="cuda", dtype=torch.bfloat16)
-    cur = {"v": 6}
+    cur = {"v": 13}
 
     def run():
-        b = b256 if cur["v"] in (9, 12) else b128
+        b = b128
         _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
                                0.125, _stream()), "attn")
 
-    VARIANTS = tuple(int(v) for v in os.environ.get("ATTN_VARIANTS", "6,5,2").split(","))
+    VARIANTS = tuple(int(v) for v in os.environ.get("ATTN_VARIANTS", "13,14,6").split(","))
     times = {v: [] for v in VARIANTS}
     for _ in range(a.rounds):
         for v in VARIANTS:
@@ -46,7 +45,7 @@ def main():
             e.record()
             torch.cuda.synchronize()
             times[v].append(s.elapsed_time(e) / a.iters)
-    L.nomic_attention_set_variant(6)
+    L.nomic_attention_set_variant(13)
     fl = 4.0 * a.docs * a.seq * a.seq * 64 * 12
     for v in VARIANTS:
         t = np.array(times[v])

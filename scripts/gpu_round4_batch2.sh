@@ -14,6 +14,9 @@ step() {
 }
 step pre_tests timeout -k 10 600 python -u -m pytest tests/test_batch_api.py tests/test_ring_gpu.py tests/test_arena_gpu.py \
   -x -v -m gpu --timeout 150 --timeout-method thread
+step attn_tests timeout -k 10 300 python -u -m pytest tests/test_nomic_gpu.py -x -v -k attention --timeout 150 \
+  --timeout-method thread
+step attn_bench env ATTN_VARIANTS=13,14 timeout -k 10 200 python -u scripts/attn_bench.py --rounds 7
 for f in 2 3; do
   step kv_fused$f env SPL_KVS_FUSED=$f timeout -k 10 300 python -u bench.py --mode kv --steps 20 --warmup 5 \
     --host-api 0 --host-api-threads2 0 --routed-steps 0

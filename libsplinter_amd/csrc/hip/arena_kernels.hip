@@ -655,15 +655,15 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
 int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_retry, uint64_t* stats,
                  hipStream_t s) {
   if (rows <= 0) return 0;
-  const bool kw4 = mode >= 2 && tab.ks == 16;
+  // (measured and removed: 4 workgroups per CU at <= 128 VGPRs, 34 spilled: 4.43 vs 4.84 G ops/s,
+  // profiles/r4k/kv_fused3.out)
+  const bool kw4 = mode == 2 && tab.ks == 16;
   static const int wpc_env = env_int("SPL_KVS_FUSED_WG_PER_CU", 0);
-  const int wpc = wpc_env > 0 ? wpc_env : kw4 ? (mode == 3 ? 4 : 3) : 2;
+  const int wpc = wpc_env > 0 ? wpc_env : kw4 ? 3 : 2;
   const long need = (rows + 2 * 256 - 1) / (2 * 256);
   const long cap = 256L * wpc;
   const dim3 g((unsigned)(need < cap ? need : cap));
-  if (kw4 && mode == 3)  // (measurement: 4 workgroups per CU at <= 128 VGPRs)
-    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 4>), g, dim3(256), 0, s, a, tab, max_retry, stats);
-  else if (kw4)
+  if (kw4)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats);
   else
     hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats);
@@ -1210,7 +1210,7 @@ void* spl_kvs_create(int writers, int readers) {
 // 0: one launch per client stream's slice on that stream; 1 / 2: one fused grid (k_kv_fused)
 int spl_kvs_set_fused(void* h, int mode) {
   auto* k = (KvStreams*)h;
-  if (!k || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
+  if (!k || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
   k->fused = mode;
   return 0;
 }

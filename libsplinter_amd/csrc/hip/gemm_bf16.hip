@@ -955,7 +955,11 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
   // has 3072.  The statistics epilogues exist in the 128^2 kernel only.
   constexpr bool k256_ok = MODE <= NOMIC_EPI_F32;
   const long tiles256 = fits ? (mpad / 256) * (N / 256) : 0;
-  if (k256_ok && fits && (var == 256 || (var == 0 && tiles256 >= 1024))) {
+  static const long min_tiles = [] {  // NOMIC_GEMM256_MIN_TILES (A/B knob)
+    const char* e = getenv("NOMIC_GEMM256_MIN_TILES");
+    return e && atol(e) > 0 ? atol(e) : 1024L;
+  }();
+  if (k256_ok && fits && (var == 256 || (var == 0 && tiles256 >= min_tiles))) {
     static bool attr = [] {
       allow_lds(k_gemm256<MODE, 0, 0, 2>, kLds2Bytes);
       return true;

@@ -8,7 +8,6 @@
 //                    straight into arena slots under the seqlock     (K17 + K9)
 //   nomic_dequant    GGUF F32/F16/BF16/Q8_0/Q4_0/Q4_1/Q4_K/Q6_K -> bf16
 #include <hip/hip_runtime.h>
-#include "glds_asm.hpp"
 #include <cstdlib>
 #include <cstdint>
 
@@ -579,161 +578,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
   }
 }
 
-// k_attn3d: k_attn3 with its K / V tiles staged by LDS-DMA (global_load_lds_dwordx4, glds_asm.hpp)
-// into a 3-deep LDS ring instead of through registers one tile ahead: tile t+2's loads are issued
-// when tile t starts, so each load has two tiles of compute (not one) to land, and no staging
-// registers or LDS write pass remain.  The DMA writes each wave's 1 KB block lane-linearly, so the
-// XOR swizzles of k_attn3 are applied on the global side (lane L of a block loads the logical chunk
-// that belongs at physical chunk L & 7 of its key row).  Rows past the sequence end re-read its last
-// key (valid memory; their scores are masked and their probabilities exactly 0).
-__global__ __launch_bounds__(256) void k_attn3d(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
-                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
-                                                int heads, float scale_log2) {
-  constexpr int KT = 64, NB = 3;
-  __shared__ __attribute__((aligned(16))) char lds[NB][2][KT * 128];  // [buf][K | V][key * 128 B]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int hi = lane >> 5, q32 = lane & 31, li = lane & 15, tq = li >> 2, tp = li & 3;
-  const int nwg = gridDim.x, orig = blockIdx.x, q8 = nwg / 8, r8 = nwg % 8, xcd = orig % 8;
-  const int lid = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + orig / 8;
-  const int nqb = nwg / heads, head = lid / nqb, qbi = lid - head * nqb;
-  const int seq = qblocks[2 * qbi], qstart = qblocks[2 * qbi + 1];
-  const long s0 = cu[seq], len = cu[seq + 1] - s0;
-  const long ld = 3L * heads * HD;
-  const uint16_t* Qg = qkv + head * HD;
-  const uint16_t* Kg = qkv + (long)heads * HD + head * HD;
-  const uint16_t* Vg = qkv + 2L * heads * HD + head * HD;
-
-  const long qrow = qstart + wave * 32 + q32;
-  bf16x8 qf[4];
-#pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
-    qf[ks] = qrow < len ? *(const bf16x8*)(Qg + (s0 + qrow) * ld + ks * 16 + hi * 8) : bf16x8{};
-  f32x16 o[2];
-#pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) o[db][r] = 0.f;
-  float m = -1e30f, l = 0.f;
-
-  // per tile and wave: 2 K + 2 V DMA instructions, 8 key rows (1 KB) each; block b = i * 4 + wave
-  const int rb = lane >> 3, pc = lane & 7;
-  auto issue = [&](int t) {
-    const int buf = t % NB;
-    const long k0 = (long)t * KT;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int key = (i * 4 + wave) * 8 + rb;
-      const long kr = s0 + (k0 + key < len ? k0 + key : len - 1);
-      const int kc = pc ^ ((key >> 1) & 7), vc = pc ^ (((key >> 1) & 1) << 2);
-      spl::glds16_asm(Kg + kr * ld + kc * 8, lds[buf][0] + (i * 4 + wave) * 1024);
-      spl::glds16_asm(Vg + kr * ld + vc * 8, lds[buf][1] + (i * 4 + wave) * 1024);
-    }
-  };
-  const int ntiles = (int)((len + KT - 1) / KT);
-  if (ntiles > 0) issue(0);
-  if (ntiles > 1) issue(1);
-  for (int t = 0; t < ntiles; ++t) {
-    const int buf = t % NB;
-    const long k0 = (long)t * KT;
-    if (t + 2 < ntiles) {
-      issue(t + 2);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // tile t landed (t+1, t+2 may fly)
-    } else if (t + 1 < ntiles) {
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();  // every wave's rows of tile t are in LDS
-    const char* Ks = lds[buf][0];
-    const char* Vs = lds[buf][1];
-    f32x16 s[2];
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) s[kb][r] = 0.f;
-      const int row = kb * 32 + q32;
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks) {
-        const bf16x8 kf = *(const bf16x8*)(Ks + row * 128 + (k3sw(row, 2 * ks + hi) << 4));
-        s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
-      }
-    }
-    if (k0 + KT > len) {
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (k0 + kb * 32 + (r & 3) + 8 * (r >> 2) + 4 * hi >= len) s[kb][r] = -1e30f;
-    }
-    float mx = fmaxf(s[0][0], s[1][0]);
-#pragma unroll
-    for (int r = 1; r < 16; ++r) mx = fmaxf(mx, fmaxf(s[0][r], s[1][r]));
-    {
-      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
-      mx = fmaxf(__uint_as_float(q[0]), __uint_as_float(q[1]));
-    }
-    constexpr float kThr = 8.f;
-    const float mxs = mx * scale_log2;
-    if (!__all(mxs - m <= kThr)) {
-      const float mn = fmaxf(m, mxs);
-      const float alpha = __builtin_amdgcn_exp2f(m - mn);
-      m = mn;
-      l *= alpha;
-#pragma unroll
-      for (int db = 0; db < 2; ++db) o[db] *= alpha;
-    }
-    const float nm = -m;
-    float ps = 0.f;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[kb][r], scale_log2, nm));
-        s[kb][r] = p;
-        ps += p;
-      }
-    {
-      auto q = __builtin_amdgcn_permlane32_swap(__float_as_uint(ps), __float_as_uint(ps), false, false);
-      ps = __uint_as_float(q[0]) + __uint_as_float(q[1]);
-    }
-    l += ps;
-#pragma unroll
-    for (int kb = 0; kb < 2; ++kb)
-#pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8 pf;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) pf[j] = (__bf16)s[kb][8 * st + j];
-        const int rowA = kb * 32 + 16 * st + 4 * hi + tq, rowB = rowA + 8;
-#pragma unroll
-        for (int db = 0; db < 2; ++db) {
-          const int col = 32 * db + 16 * ((lane >> 4) & 1) + 4 * tp;
-          const int ch = col >> 3, off = (col & 7) * 2;
-          const v4i16 a = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vs + rowA * 128 + (v3sw(rowA, ch) << 4) + off));
-          const v4i16 b = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-              (lds_v4i16*)(Vs + rowB * 128 + (v3sw(rowB, ch) << 4) + off));
-          const bf16x8 vf = __builtin_bit_cast(bf16x8, (v8i16)__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7));
-          o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
-        }
-      }
-    __syncthreads();  // reads of buffer t % 3 done before tile t + 1 issues tile t + 3 into it
-  }
-  if (qrow < len) {
-    const float inv = 1.f / l;
-    uint16_t* dst = out + (s0 + qrow) * (long)heads * HD + head * HD;
-#pragma unroll
-    for (int db = 0; db < 2; ++db)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        uint2 w;
-        w.x = pk2(o[db][4 * g] * inv, o[db][4 * g + 1] * inv);
-        w.y = pk2(o[db][4 * g + 2] * inv, o[db][4 * g + 3] * inv);
-        *(uint2*)(dst + 32 * db + 8 * g + 4 * hi) = w;
-      }
-  }
-}
-
 // ------------------------------------------------------------ mean pool --
 __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, const int32_t* __restrict__ cu,
                                               float* __restrict__ pooled, int normalize, spl_arena_t aa,
@@ -932,9 +776,10 @@ int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, 
 
 // Two selectable forms (NOMIC_ATTN): 13 = k_attn3 (32x32x16 MFMA, default: 634 vs 514 TFLOP/s for
 // 6, profiles/r3_attn_k_attn3_ab.jsonl) and 6 = k_attn2 (16x16x32 MFMA, permlane reductions, packed
-// score math), the fallback.  The other A/B forms of rounds 1-3 are gone; their measurements stay in
+// score math), the fallback.  Measured and removed in round 4: K/V staged by LDS-DMA into a 3-deep
+// ring (505 vs 596 TFLOP/s, profiles/r4k/attn_bench.out).  The other A/B forms of rounds 1-3 are gone; their measurements stay in
 // profiles/r1_attn_* .. r3_attn_*.
-static int attn_norm(int v) { return v == 6 || v == 14 ? v : 13; }
+static int attn_norm(int v) { return v == 6 ? 6 : 13; }
 static int g_attn_variant = [] {
   const char* e = getenv("NOMIC_ATTN");
   return attn_norm(e && *e ? atoi(e) : 13);
@@ -954,9 +799,6 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   if (g_attn_variant == 6)
     hipLaunchKernelGGL((k_attn2<0, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
                        (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 14)
-    hipLaunchKernelGGL(k_attn3d, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
-                       qblocks, heads, scale_log2);
   else
     hipLaunchKernelGGL(k_attn3<false>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);

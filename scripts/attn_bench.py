@@ -31,7 +31,7 @@ def main():
         _chk(L.nomic_attention(qkv.data_ptr(), out.data_ptr(), b.cu.data_ptr(), b.qblocks.data_ptr(), b.nqb, 12,
                                0.125, _stream()), "attn")
 
-    VARIANTS = tuple(int(v) for v in os.environ.get("ATTN_VARIANTS", "13,14,6").split(","))
+    VARIANTS = tuple(int(v) for v in os.environ.get("ATTN_VARIANTS", "13,6").split(","))
     times = {v: [] for v in VARIANTS}
     for _ in range(a.rounds):
         for v in VARIANTS:

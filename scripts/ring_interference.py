@@ -6,6 +6,9 @@ store's per-call API (splinter_hostapi_bench --attach, 8 threads each).
   private  SPLINTER_RING_SHARED=0 in the clients: each runs its own resident ring worker
   cpu      the same clients on a host shm store (no GPU work at all): the host-side share of the
            slowdown (CPU contention with the encoder's launching thread)
+  idle     the clients call for 0.3 s and exit BEFORE the encoder is timed: with
+           SPLINTER_RING_IDLE_US set long, the owner's worker stays resident but idle
+--client-args: extra splinter_hostapi_bench arguments (e.g. "--set-frac 0": gets only)
 
 Prints one JSON line: encoder ms/step alone and beside the clients in either mode, the slowdown,
 and the clients' aggregate ops/s.
@@ -47,6 +50,7 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--keys", type=int, default=20000)
     ap.add_argument("--modes", default="shared,private,cpu")
+    ap.add_argument("--client-args", default="")
     a = ap.parse_args()
     name = f"hbm:ri{os.getpid()}"
     st = Store.create(name, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
@@ -66,13 +70,19 @@ def main():
         for threads in [int(t) for t in a.threads.split(",")]:
             for mode in a.modes.split(","):
                 env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0",
-                           SPLINTER_RING_SHARED="1" if mode == "shared" else "0")
+                           SPLINTER_RING_SHARED="0" if mode == "private" else "1")
                 target = shm if mode == "cpu" else name
+                dur = 0.3 if mode == "idle" else secs
                 procs = [subprocess.Popen([TOOL, "--attach", "--store", target, "--threads", str(threads), "--seconds",
-                                           str(secs), "--keys", str(a.keys)], env=env, stdout=subprocess.PIPE,
-                                          stderr=subprocess.PIPE, text=True) for _ in range(a.clients)]
+                                           str(dur), "--keys", str(a.keys)] + a.client_args.split(), env=env,
+                                          stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+                         for _ in range(a.clients)]
                 try:
-                    time.sleep(1.0)  # the clients are attached and calling
+                    if mode == "idle":
+                        for p in procs:
+                            p.wait(timeout=120)
+                    else:
+                        time.sleep(1.0)  # the clients are attached and calling
                     ms = time_steps(ph, a.steps)
                     rate, fails = 0.0, 0
                     for p in procs:

@@ -83,7 +83,9 @@ def main():
                             p.wait(timeout=120)
                     else:
                         time.sleep(1.0)  # the clients are attached and calling
+                    n0 = N.hip_lib().spl_hbm_ring_launches(st.handle)
                     ms = time_steps(ph, a.steps)
+                    launches = N.hip_lib().spl_hbm_ring_launches(st.handle) - n0
                     rate, fails = 0.0, 0
                     for p in procs:
                         o, e = p.communicate(timeout=secs + 60)
@@ -100,7 +102,8 @@ def main():
                             p.kill()
                 out[f"{mode}_t{threads}"] = {"encoder_ms": round(ms, 3),
                                              "slowdown_pct": round(100.0 * (ms / out["encoder_ms_alone"] - 1), 2),
-                                             "client_ops_per_s": round(rate, 1), "client_failures": fails}
+                                             "client_ops_per_s": round(rate, 1), "client_failures": fails,
+                                             "worker_launches_while_timed": launches}
                 print(json.dumps(out), file=sys.stderr, flush=True)
         out["encoder_ms_alone_after"] = round(time_steps(ph, a.steps), 3)
         ph.close()

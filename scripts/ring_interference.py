@@ -51,6 +51,9 @@ def main():
     ap.add_argument("--keys", type=int, default=20000)
     ap.add_argument("--modes", default="shared,private,cpu")
     ap.add_argument("--client-args", default="")
+    ap.add_argument("--settle", type=float, default=4.0,
+                    help="seconds between starting the clients and timing (their HIP start-up and store attach, "
+                         "which maps the arena into their GPU address space, are over by then)")
     a = ap.parse_args()
     name = f"hbm:ri{os.getpid()}"
     st = Store.create(name, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
@@ -63,7 +66,7 @@ def main():
         for _ in range(3):
             ph.run()
         out["encoder_ms_alone"] = round(time_steps(ph, a.steps), 3)
-        secs = max(3.0, a.steps * out["encoder_ms_alone"] / 1e3 * 3 + 2.0)
+        secs = max(3.0, a.steps * out["encoder_ms_alone"] / 1e3 * 3 + 2.0) + a.settle
         shm = f"ri{os.getpid()}shm"
         hs = Store.create(shm, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
         hs.set_batch(keys, [b"v" * 150] * a.keys)
@@ -82,7 +85,7 @@ def main():
                         for p in procs:
                             p.wait(timeout=120)
                     else:
-                        time.sleep(1.0)  # the clients are attached and calling
+                        time.sleep(a.settle)  # the clients are attached and calling
                     n0 = N.hip_lib().spl_hbm_ring_launches(st.handle)
                     ms = time_steps(ph, a.steps)
                     launches = N.hip_lib().spl_hbm_ring_launches(st.handle) - n0

@@ -186,6 +186,9 @@ class CmdRing {
   bool ready() const { return shared_ != nullptr; }
   bool shared_mode() const { return mode_ != kPrivate; }
   int mode() const { return (int)mode_; }  // 0 private, 1 ring server, 2 client of a server
+  // whether call() will run this process's own worker on the arena passed to it (a client of a
+  // live server passes nothing to the device)
+  bool needs_arena() const { return mode_ != kClient || gone_.load(std::memory_order_acquire) || server_gone(); }
   // Blocking call: stage key / input, ring the doorbell, wait for DONE.  `in` may be null;
   // `out` (may be null) receives min(out_len, out_cap) payload bytes.  Returns 0 when the op ran
   // (its own status in r.status), -1 on a ring failure (errno set; e.g. ETIMEDOUT).

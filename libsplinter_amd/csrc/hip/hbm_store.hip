@@ -122,6 +122,7 @@ class HbmStore final : public StoreBase {
   hipStream_t stream() const { return stream_; }
   uint32_t ring_launches() const { return ring_ ? ring_->launches() : 0; }
   int ring_mode() const { return ring_ ? ring_->mode() : -1; }
+  bool attach() { return ensure_mapped(); }
 
   int set_mop(unsigned mode) override {
     switch (mode) {
@@ -138,6 +139,7 @@ class HbmStore final : public StoreBase {
     return 0;
   }
   void purge() override {
+    if (!ensure_mapped()) return;
     DevGuard dg(device_);
     std::lock_guard<std::mutex> lk(mu_);
     spl_arena_purge(arena(), stream_);
@@ -261,7 +263,7 @@ class HbmStore final : public StoreBase {
     // Zero-copy, as the reference (splinter.c:747-762): a host pointer into the value region
     // through the CPU mapping of the arena's dmabuf chunks (VmmArena::host_map, PCIe BAR), with the
     // slot's epoch and length from one ring snapshot; the caller re-checks the epoch.
-    if (uint8_t* hb = host_base()) {
+    if (uint8_t* hb = ensure_mapped() ? host_base() : nullptr) {
       uint8_t c[128];
       RingResult r;
       if (ring(kRingSnapshot, 0, key, nullptr, 0, 0, c, sizeof c, &r) != 0) return nullptr;
@@ -498,6 +500,8 @@ class HbmStore final : public StoreBase {
       std::memset(k, 0, 64);
     }
     if (!ring_ || !ring_->ready()) { errno = ENOSYS; return -1; }
+    // a client of the owner's ring server needs no device mapping of the arena; its own worker does
+    if (ring_->needs_arena() && !ensure_mapped()) return -1;
     return ring_->call(arena(), op, sub, k, klen, khash, in, in_len, arg, out, out_cap, r);
   }
   static int st_ret(int32_t st) {
@@ -533,10 +537,11 @@ class HbmStore final : public StoreBase {
   // appended on the host; stops once `limit` matches are collected.
   static constexpr uint32_t kScanChunk = 1u << 22;
   void scan(int mode, uint64_t mask, std::vector<uint32_t>& idx, std::vector<uint64_t>& ep, size_t limit) {
-    DevGuard dg(device_);
-    std::lock_guard<std::mutex> lk(mu_);
     idx.clear();
     ep.clear();
+    if (!ensure_mapped()) return;
+    DevGuard dg(device_);
+    std::lock_guard<std::mutex> lk(mu_);
     if (ensure_scan_scratch() != 0) return;
     std::vector<uint32_t> hi;
     std::vector<uint64_t> he;
@@ -574,9 +579,10 @@ class HbmStore final : public StoreBase {
     return 0;
   }
   void fetch_cores(const std::vector<uint32_t>& idx) {
+    list_cache_.assign(idx.size() * 128, 0);
+    if (!ensure_mapped()) return;
     DevGuard dg(device_);
     std::lock_guard<std::mutex> lk(mu_);
-    list_cache_.assign(idx.size() * 128, 0);
     if (idx.empty() || ensure_scan_scratch() != 0) return;
     // reuse the scan scratch: kScanChunk indices (4 B) + kScanChunk/16 cores (128 B) per round
     const size_t per = kScanChunk / 16;
@@ -637,7 +643,29 @@ class HbmStore final : public StoreBase {
     return e && !strcmp(e, "0");
   }
   bool vmm_mode_ = false;
-  void* dbase_ = nullptr;  // raw_ + kAlignOffset
+  void* dbase_ = nullptr;  // raw_ + kAlignOffset (null until mapped: an opener attaches lazily)
+  // Lazy attach: an opener whose per-call ops go to the owner's ring server maps the arena into its
+  // own GPU address space only on the first op that needs it (batches, scans, search, raw pointers,
+  // checkpoints, a private ring).  A CLI call on a 100M-key node store then maps nothing.
+  std::vector<int> pend_fds_;
+  size_t pend_chunk_ = 0;
+  uint64_t pend_off_ = 0;
+  std::mutex map_mu_;
+  bool ensure_mapped() {
+    if (__atomic_load_n(&dbase_, __ATOMIC_ACQUIRE)) return true;
+    std::lock_guard<std::mutex> lk(map_mu_);
+    if (dbase_) return true;
+    if (pend_fds_.empty()) { errno = EIO; return false; }
+    RingQuiesce quiet;  // VMM map calls may wait for the device: no resident worker of this process
+    DevGuard dg(device_);
+    std::vector<int> fds;
+    fds.swap(pend_fds_);
+    if (vmm_.import(device_, fds, pend_chunk_) != 0) { errno = EACCES; return false; }
+    vmm_mode_ = true;
+    raw_ = vmm_.base();
+    __atomic_store_n(&dbase_, (void*)((uint8_t*)raw_ + pend_off_), __ATOMIC_RELEASE);
+    return true;
+  }
   HbmDescriptor* desc_ = nullptr;
   bool desc_registered_ = false;
   uint32_t* d_notify_ = nullptr;  // device address of desc_->notify (hipHostRegister)
@@ -811,15 +839,27 @@ HbmStore* HbmStore::open(const char* name, int* err) {
   if (d->version >= 3 && d->mode == 1) {
     std::vector<int> fds;
     size_t chunk = 0;
-    if (!d->sock[0] || VmmArena::fetch(d->sock, &fds, &chunk) != 0 || fds.size() != d->nchunks ||
-        s->vmm_.import(s->device_, fds, chunk) != 0) {
+    if (!d->sock[0] || VmmArena::fetch(d->sock, &fds, &chunk) != 0 || fds.size() != d->nchunks) {
+      for (int f : fds) close(f);
       *err = EACCES;
       delete s;
       return nullptr;
     }
     s->vmm_mode_ = true;
-    s->raw_ = s->vmm_.base();
-  } else if (hipIpcOpenMemHandle(&s->raw_, d->handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
+    s->pend_fds_ = std::move(fds);
+    s->pend_chunk_ = chunk;
+    s->pend_off_ = d->base_offset;
+    if (s->setup_buffers() != 0) { *err = EIO; delete s; return nullptr; }
+    // attach now unless the owner's ring server serves this process (SPLINTER_HBM_LAZY_ATTACH=0: always now)
+    const char* lz = getenv("SPLINTER_HBM_LAZY_ATTACH");
+    if ((s->ring_mode() != 2 || (lz && !strcmp(lz, "0"))) && !s->ensure_mapped()) {
+      *err = EACCES;
+      delete s;
+      return nullptr;
+    }
+    return s;
+  }
+  if (hipIpcOpenMemHandle(&s->raw_, d->handle, hipIpcMemLazyEnablePeerAccess) != hipSuccess) {
     *err = EACCES;
     s->raw_ = nullptr;
     delete s;
@@ -842,23 +882,23 @@ HbmStore::~HbmStore() {
     if (st.h) (void)hipHostFree(st.h);
   }
   stop_proxy();
-  ring_.reset();  // the worker (and a ring server's supervisor) reads the arena: gone before it
-  if (stream_) (void)hipStreamSynchronize(stream_);
   if (event_fd_ >= 0) {
     if (desc_ && __atomic_load_n(&desc_->control.event_bus.owner_pid, __ATOMIC_ACQUIRE) == (int32_t)getpid()) {
       __atomic_store_n(&desc_->control.event_bus.owner_fd, -1, __ATOMIC_RELEASE);
       __atomic_store_n(&desc_->control.event_bus.owner_pid, 0, __ATOMIC_RELEASE);
-      if (raw_) {
-        const int32_t own[2] = {-1, 0};
-        put_field(offsetof(splinter_header, event_bus) + offsetof(splinter_event_bus, owner_fd), own, 8);
-      }
+      // the device header's copy too, through the ring (still up: it goes below)
+      const int32_t own[2] = {-1, 0};
+      put_field(offsetof(splinter_header, event_bus) + offsetof(splinter_event_bus, owner_fd), own, 8);
     }
     close(event_fd_);
   }
+  ring_.reset();  // the worker (and a ring server's supervisor) reads the arena: gone before it
+  if (stream_) (void)hipStreamSynchronize(stream_);
   if (h_u32_) (void)hipHostFree(h_u32_);
   if (d_scan_idx_) (void)hipFree(d_scan_idx_);
   if (d_scan_ep_) (void)hipFree(d_scan_ep_);
   if (d_scan_cnt_) (void)hipFree(d_scan_cnt_);
+  for (int f : pend_fds_) close(f);
   if (raw_) {
     if (vmm_mode_) vmm_.release();
     else if (owner_) (void)hipFree(raw_);
@@ -880,6 +920,7 @@ HbmStore::~HbmStore() {
 long HbmStore::search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap,
                           spl_search_hit* out) {
   if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
+  if (!ensure_mapped()) return -1;
   DevGuard dg(device_);
   std::vector<float> sd((size_t)geo_.slots * 2);
   {
@@ -940,6 +981,7 @@ long HbmStore::search_all(const float* q, uint64_t mask, float min_sim, float ma
 // Checkpoint: stream the device image into a v4 store file (byte-identical
 // layout, so the host backend — or the reference library — can open it).
 int HbmStore::checkpoint(const char* path) {
+  if (!ensure_mapped()) return -1;
   DevGuard dg(device_);
   int fd = ::open(path, O_RDWR | O_CREAT | O_TRUNC | O_CLOEXEC, 0666);
   if (fd < 0) return -1;
@@ -967,6 +1009,7 @@ int HbmStore::checkpoint(const char* path) {
 }
 
 int HbmStore::restore_from(const char* path) {
+  if (!ensure_mapped()) return -1;
   DevGuard dg(device_);
   int fd = ::open(path, O_RDONLY | O_CLOEXEC);
   if (fd < 0) return -1;
@@ -1136,6 +1179,7 @@ long HbmStore::set_batch(const char* keys, int kstride, const uint8_t* vals, int
                  {lens, 4, 4, true, false, false},
                  {status, 4, 4, false, true, false}};
   const int ks = (int)r16(kstride), vs = (int)r16(vstride);
+  if (!ensure_mapped()) return -1;
   const spl_arena_t a = arena();
   if (batch_run(n, cols, 4, [&](long m, void** d, hipStream_t st) {
         return spl_arena_set(a, (const char*)d[0], ks, (const uint8_t*)d[1], vs, (const uint32_t*)d[2], m,
@@ -1157,6 +1201,7 @@ long HbmStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostrid
                  {status, 4, 4, false, true, false},
                  {out_lens, 4, 4, false, true, false},
                  {out, ostride, os, false, true, false}};
+  if (!ensure_mapped()) return -1;
   const spl_arena_t a = arena();
   if (batch_run(n, cols, out ? 4 : 3, [&](long m, void** d, hipStream_t st) {
         return spl_arena_get(a, (const char*)d[0], ks, out ? (uint8_t*)d[3] : nullptr, out ? (int)os : 16,
@@ -1187,6 +1232,7 @@ long HbmStore::intop_batch(const char* keys, int kstride, const int* ops, const 
                  {masks, 8, 8, true, false, false},
                  {status, 4, 4, false, true, false},
                  {results, 8, 8, false, true, false}};
+  if (!ensure_mapped()) return -1;
   const spl_arena_t a = arena();
   if (batch_run(n, cols, results ? 5 : 4, [&](long m, void** d, hipStream_t st) {
         return spl_arena_intop(a, (const char*)d[0], ks, (const int*)d[1], (const uint64_t*)d[2], m, (int32_t*)d[3],
@@ -1207,6 +1253,7 @@ long HbmStore::set_embedding_batch(const char* keys, int kstride, const float* v
   Col cols[3] = {{keys, kstride, ks, true, false, false},
                  {vecs, (long)kEmbedBytes, (long)kEmbedBytes, true, false, false},
                  {status, 4, 4, false, true, false}};
+  if (!ensure_mapped()) return -1;
   const spl_arena_t a = arena();
   if (batch_run(n, cols, 3, [&](long m, void** d, hipStream_t st) {
         return spl_arena_embed_set(a, (const char*)d[0], ks, (const float*)d[1], m, (int32_t*)d[2], st);
@@ -1227,6 +1274,7 @@ spl::StoreBase* spl_hbm_factory(const char* name, size_t slots, size_t max_val, 
 int spl_hbm_arena(spl_store* h, spl_arena_t* out) {
   auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
   if (!s || !out) return -2;
+  if (!s->attach()) return -5;  // an opener maps the arena on first device use
   *out = s->arena();
   return 0;
 }

@@ -917,9 +917,10 @@ void CmdRing::launch(const spl_arena_t& a) {
       if (hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()) != hipSuccess) stream_ = nullptr;
     }
     if (!stream_) {
+      // SPLINTER_RING_PRIORITY=0: the worker's queue at normal priority (measurement knob)
       int lo = 0, hi = 0;
       (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-      (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, hi);
+      (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, env_int("SPLINTER_RING_PRIORITY", 1) ? hi : 0);
     }
   }
   // stream order: the previous worker (if still draining) has exited before ctrl is reset

@@ -61,6 +61,9 @@ if [ -n "$EXTRA_OVERLAP" ]; then
   step bench_overlap timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --overlap-native 1 --embed-e2e 0 \
     --host-api 0 --host-api-threads2 0 --daemon-docs 0 --routed-steps 0
 fi
+if [ -n "$SMOKE" ]; then
+  step smoke timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()"
+fi
 if [ -z "$SKIP_TESTS" ]; then
   timeout -k 10 1000 python -u -m pytest tests -m gpu -v --timeout 150 --timeout-method thread ${PYTEST_ARGS} \
     > "$OUT/pytest_gpu.log" 2>&1

@@ -232,8 +232,8 @@ int attach_main(const Args& a) {
     return 1;
   }
   const RunStats r = run_calls(a, 4096, std::string(a.value_len, 'v'));
-  printf("%llu %llu %llu %.6f %.3f\n", (unsigned long long)r.calls, (unsigned long long)r.ok,
-         (unsigned long long)r.fail, r.el, r.p50);
+  printf("%llu %llu %llu %.6f %.3f %d\n", (unsigned long long)r.calls, (unsigned long long)r.ok,
+         (unsigned long long)r.fail, r.el, r.p50, ring_mode());
   fflush(stdout);
   splinter_close();
   return r.fail ? 1 : 0;
@@ -344,7 +344,7 @@ int main(int argc, char** argv) {
     (void)waitpid(k.pid, &wst, 0);
     unsigned long long c = 0, o = 0, f = 0;
     double kel = 0, kp50 = 0;
-    if (sscanf(line, "%llu %llu %llu %lf %lf", &c, &o, &f, &kel, &kp50) != 5 || kel <= 0 ||
+    if (sscanf(line, "%llu %llu %llu %lf %lf", &c, &o, &f, &kel, &kp50) < 5 || kel <= 0 ||
         !WIFEXITED(wst) || WEXITSTATUS(wst) != 0) {
       ++kid_fail;
       continue;

@@ -34,12 +34,19 @@ from libsplinter_amd.models.bench_embed import EmbedPhase  # noqa: E402
 TOOL = os.path.join(ROOT, "libsplinter_amd", "bin", "splinter_hostapi_bench")
 
 
+STEPS = []  # per-step encoder ms of the last time_steps (events on the encoder's stream)
+
+
 def time_steps(ph, n):
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
     t0 = time.perf_counter()
-    for _ in range(n):
+    ev[0].record()
+    for i in range(n):
         ph.run()
+        ev[i + 1].record()
     torch.cuda.synchronize()
+    STEPS[:] = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(n)]
     return (time.perf_counter() - t0) / n * 1e3
 
 
@@ -89,7 +96,7 @@ def main():
                     n0 = N.hip_lib().spl_hbm_ring_launches(st.handle)
                     ms = time_steps(ph, a.steps)
                     launches = N.hip_lib().spl_hbm_ring_launches(st.handle) - n0
-                    rate, fails = 0.0, 0
+                    rate, fails, modes = 0.0, 0, []
                     for p in procs:
                         o, e = p.communicate(timeout=secs + 60)
                         if p.returncode != 0:
@@ -97,6 +104,7 @@ def main():
                             print(e[-500:], file=sys.stderr)
                             continue
                         c, ok, f, el, p50 = o.split()[:5]
+                        modes.append(int(o.split()[5]) if len(o.split()) > 5 else None)
                         rate += int(c) / float(el)
                         fails += int(f)
                 finally:
@@ -106,7 +114,8 @@ def main():
                 out[f"{mode}_t{threads}"] = {"encoder_ms": round(ms, 3),
                                              "slowdown_pct": round(100.0 * (ms / out["encoder_ms_alone"] - 1), 2),
                                              "client_ops_per_s": round(rate, 1), "client_failures": fails,
-                                             "worker_launches_while_timed": launches}
+                                             "worker_launches_while_timed": launches, "client_ring_modes": modes,
+                                             "step_ms": STEPS[:]}
                 print(json.dumps(out), file=sys.stderr, flush=True)
         out["encoder_ms_alone_after"] = round(time_steps(ph, a.steps), 3)
         ph.close()

@@ -743,10 +743,8 @@ int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, c
   seg_ = (RingSegHdr*)p;
   seg_bytes_ = L.total;
   seg_name_ = seg;
-  // SPLINTER_RING_REG_FLAGS: hipHostRegister flags of the segment (measurement knob; default mapped)
-  const unsigned rf = (unsigned)strtoul(getenv("SPLINTER_RING_REG_FLAGS") ? getenv("SPLINTER_RING_REG_FLAGS") : "2",
-                                        nullptr, 0);
-  if (hipHostRegister(p, L.total, rf | hipHostRegisterMapped) != hipSuccess) return -1;
+  // (hipExtHostRegisterUncached measured no better: profiles/r4h t32_rf*, p4t8_rf*)
+  if (hipHostRegister(p, L.total, hipHostRegisterMapped) != hipSuccess) return -1;
   seg_registered_ = true;
   uint8_t* dp = nullptr;
   if (hipHostGetDevicePointer((void**)&dp, p, 0) != hipSuccess) return -1;
@@ -903,25 +901,11 @@ void CmdRing::launch(const spl_arena_t& a) {
   (void)hipGetDevice(&cur);
   if (cur != device_) (void)hipSetDevice(device_);
   if (!stream_) {  // created on first use: a store that never takes a per-call op claims no queue
-    // SPLINTER_RING_CUS=n: the worker's waves confined to n CUs spread over the chip (a CU-masked
-    // queue), so fewer of the encoder's workgroups share a CU with a polling wave
-    const int ncu = env_int("SPLINTER_RING_CUS", 0);
-    int total = 0;
-    (void)hipDeviceGetAttribute(&total, hipDeviceAttributeMultiprocessorCount, device_);
-    if (ncu > 0 && total > ncu) {
-      std::vector<uint32_t> mask((size_t)(total + 31) / 32, 0u);
-      for (int i = 0; i < ncu; ++i) {
-        const int cu = (int)((long)i * total / ncu);
-        mask[(size_t)cu / 32] |= 1u << (cu % 32);
-      }
-      if (hipExtStreamCreateWithCUMask(&stream_, (uint32_t)mask.size(), mask.data()) != hipSuccess) stream_ = nullptr;
-    }
-    if (!stream_) {
-      // SPLINTER_RING_PRIORITY=0: the worker's queue at normal priority (measurement knob)
-      int lo = 0, hi = 0;
-      (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-      (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, env_int("SPLINTER_RING_PRIORITY", 1) ? hi : 0);
-    }
+    // high priority (SPLINTER_RING_PRIORITY=0: normal); a CU-masked queue measured worse
+    // (profiles/r4h interf_cus*)
+    int lo = 0, hi = 0;
+    (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
+    (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, env_int("SPLINTER_RING_PRIORITY", 1) ? hi : 0);
   }
   // stream order: the previous worker (if still draining) has exited before ctrl is reset
   const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)groups_};

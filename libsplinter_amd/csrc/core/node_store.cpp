@@ -525,7 +525,11 @@ long node_chunk_ops() {
 
 // HBM shards wait on their GPUs while the host prepares the next chunk; host shards would only
 // compete with it for CPUs, so their batches run as one chunk
-long NodeStore::chunk_for(long n) const { return std::min(n, desc_->backend == 1 ? node_chunk_ops() : n); }
+long NodeStore::chunk_for(long n) const {
+  const char* e = getenv("SPLINTER_NODE_BATCH_PIPELINE");  // 1 / 0: force on / off (tests)
+  const bool on = e && *e ? atoi(e) != 0 : desc_->backend == 1;
+  return std::min(n, on ? node_chunk_ops() : n);
+}
 
 // Chunked two-stage pipeline: prep(c0, m, S) partitions and copies chunk [c0, c0+m) into scratch
 // half S (host threads), exec(plan, c0, m, S) runs every shard on it and copies the outputs back

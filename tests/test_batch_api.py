@@ -158,3 +158,20 @@ def test_batch_api_node_hbm_pipelined_chunks(uniq, monkeypatch):
     finally:
         s.close()
         S.unlink(f"node:{uniq}")
+
+
+def test_batch_api_node_store_shm_pipelined(monkeypatch):
+    """The chunked node-batch pipeline (partition of chunk i+1 beside the shards' work on chunk i),
+    forced on a host-shard node with small chunks: results in client order, op for op."""
+    monkeypatch.setenv("SPLINTER_NODE_SHARDS", "4")
+    monkeypatch.setenv("SPLINTER_NODE_BACKEND", "shm")
+    monkeypatch.setenv("SPLINTER_NODE_BATCH_PIPELINE", "1")
+    monkeypatch.setenv("SPLINTER_NODE_BATCH_CHUNK", "700")
+    from libsplinter_amd import store as S
+    name = f"node:bpp{os.getpid()}"
+    s = S.Store.create(name, slots=4 * 4096, max_val=256, embeddings=False)
+    try:
+        _check_store(S, s, n=5000)
+    finally:
+        s.close()
+        S.unlink(name)

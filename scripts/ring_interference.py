@@ -37,17 +37,25 @@ TOOL = os.path.join(ROOT, "libsplinter_amd", "bin", "splinter_hostapi_bench")
 STEPS = []  # per-step encoder ms of the last time_steps (events on the encoder's stream)
 
 
+SYNC = {}  # how long the device-wide synchronizes around the last time_steps took (ms)
+
+
 def time_steps(ph, n):
+    ts = time.perf_counter()
     torch.cuda.synchronize()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(n + 1)]
     t0 = time.perf_counter()
+    SYNC["before_ms"] = round((t0 - ts) * 1e3, 3)
     ev[0].record()
     for i in range(n):
         ph.run()
         ev[i + 1].record()
+    ev[n].synchronize()
+    t1 = time.perf_counter()
     torch.cuda.synchronize()
+    SYNC["after_ms"] = round((time.perf_counter() - t1) * 1e3, 3)
     STEPS[:] = [round(ev[i].elapsed_time(ev[i + 1]), 3) for i in range(n)]
-    return (time.perf_counter() - t0) / n * 1e3
+    return (t1 - t0) / n * 1e3
 
 
 def main():
@@ -115,7 +123,7 @@ def main():
                                              "slowdown_pct": round(100.0 * (ms / out["encoder_ms_alone"] - 1), 2),
                                              "client_ops_per_s": round(rate, 1), "client_failures": fails,
                                              "worker_launches_while_timed": launches, "client_ring_modes": modes,
-                                             "step_ms": STEPS[:]}
+                                             "step_ms": STEPS[:], "device_sync_ms": dict(SYNC)}
                 print(json.dumps(out), file=sys.stderr, flush=True)
         out["encoder_ms_alone_after"] = round(time_steps(ph, a.steps), 3)
         ph.close()

@@ -726,10 +726,10 @@ int CmdRing::init_server(int device, uint32_t pstride, const std::string& seg, c
   int khz = 100000;
   (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device);
   clock_khz_ = khz > 0 ? khz : 100000;
-  // a ring server's worker idles out after 1 s, not 5 ms: beside a running encoder, client traffic
-  // with a 5 ms timeout slowed the encoder's steps 11-18 %, a 1 s timeout 1.3 % (profiles/r4p;
-  // the resident idle worker costs ~1.2 %, profiles/r4o)
-  idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 1000000) / 1000u;
+  // 5 ms as a private worker: a device-wide synchronize in the owner (torch.cuda.synchronize)
+  // waits for the resident worker until it idles out (profiles/r4r/sync_probe: 1000 ms at a 1 s
+  // timeout), which cost the embedding daemon's loop 15x at 1 s (profiles/r4q/bench.out)
+  idle_ticks_ = (uint64_t)khz * (uint64_t)env_int("SPLINTER_RING_IDLE_US", 5000) / 1000u;
   if (init_vram() != 0) return -1;
   // the segment: created under the store's umask like its descriptor, and fresh: a stale one of a
   // crashed owner of the same name is unlinked first (never truncated: its clients may still map it)

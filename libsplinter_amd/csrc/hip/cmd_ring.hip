@@ -117,6 +117,21 @@ __device__ void pull(uint4* dst, const uint8_t* src, uint32_t from, uint32_t n16
   }
 }
 
+// arena value row -> host payload with agent-coherent loads (sc1: never a stale L1 line, so a get
+// needs no acquire fence), 8 in flight, system-scope stores
+__device__ void push_c(uint8_t* dst, const uint4* src, uint32_t n16) {
+  for (uint32_t b = 0; b < n16; b += 8) {
+    u32x4c_t t[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t[q] = ld16c(src + min(b + (uint32_t)q, n16 - 1));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) vm_wait(t[q]);
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      if (b + (uint32_t)q < n16) st16s(dst + 16 * (size_t)(b + q), u32x4s_t{t[q].x, t[q].y, t[q].z, t[q].w});
+  }
+}
+
 // device bytes -> host payload, n16 chunks: 8 loads in flight, system-scope stores
 __device__ void push(uint8_t* dst, const uint4* src, uint32_t n16) {
   for (uint32_t b = 0; b < n16; b += 8) {
@@ -213,7 +228,9 @@ __device__ __forceinline__ int32_t ring_get(const Arena& a, const Key& k, uint8_
   if (idx < 0) return kNoEnt;
   if ((e1 & 1) || L == kInsertMark) return kAgain;
   const uint8_t* s = a.slot((size_t)idx);
-  if (ald64_acq(s + kOffEpoch) != e1) return kAgain;  // acquire: this CU's L1 holds no stale value line
+  // no acquire fence: the value row is read with agent-coherent loads (push_c), as the batched
+  // acquire-free get (arena_kernels.hip k_get_carry FAST).  An agent-scope acquire costs a cache
+  // invalidate per call, and beside a running encoder it is the encoder's cache that goes
   RING_TS(3);
   *out_len = L;
   if (L > cap) return kMsgSize;
@@ -244,7 +261,7 @@ __device__ __forceinline__ int32_t ring_get(const Arena& a, const Key& k, uint8_
   // the value loads complete before their bytes are stored (data dependency) and the epoch
   // re-check is issued after those stores, so the seqlock order holds without draining the
   // host-bound stores here: the one drain before the DONE doorbell covers them
-  if (L) push(hp, (const uint4*)a.value((size_t)idx), (L + 15) >> 4);
+  if (L) push_c(hp, (const uint4*)a.value((size_t)idx), (L + 15) >> 4);
   const bool ok = slot_epoch(s) == e1 && slot_hash(s) == k.hash;
   RING_TS(4);
   return ok ? kOk : kAgain;

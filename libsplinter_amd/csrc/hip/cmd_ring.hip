@@ -42,7 +42,26 @@ std::shared_mutex g_gate;
 std::mutex g_reg_mu;
 std::set<CmdRing*> g_rings;
 thread_local bool t_exclusive = false;
+std::atomic<int> g_hold{0};  // spl_ring_hold: no worker of this process runs while > 0
 }  // namespace
+
+// A process's resident ring workers cost a heavy GPU job of the same process dearly while they are
+// resident (profiles/r4x: the encoder +84 % beside an idle resident worker: the queue scheduler
+// time-slices the worker's queue against the job's).  A process about to run such a job can hold
+// its rings: every worker stops, none relaunches until the hold is released, and per-call ops --
+// its own and its clients' -- wait meanwhile (they are served once the hold ends).
+void ring_hold(bool on) {
+  if (on) {
+    if (g_hold.fetch_add(1) == 0) {
+      std::lock_guard<std::mutex> lk(g_reg_mu);
+      for (CmdRing* r : g_rings) r->stop();
+    }
+    return;
+  }
+  if (g_hold.fetch_sub(1) != 1) return;
+  std::lock_guard<std::mutex> lk(g_reg_mu);
+  for (CmdRing* r : g_rings) r->resume();
+}
 
 RingQuiesce::RingQuiesce() {
   if (t_exclusive) return;
@@ -490,7 +509,7 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
   g_ent[g * 64 + lane] = e;
 #endif
   uint64_t last = wall_clock64();
-  uint32_t idle = 0;
+  uint32_t idle = 0, busy_rounds = 0;
   const uint32_t* door = VR ? &vdoor[e] : &sh->state[e];
   uint32_t seen = VR && mine ? served[e] : 0u, bell = 0u;
   for (;;) {
@@ -552,6 +571,13 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
       }
       __builtin_amdgcn_s_sleep(2);
       continue;
+    }
+    // a wave that never goes idle (every round has a call) still sees stop / dying every 64th round
+    if ((++busy_rounds & 63) == 0) {
+      if (ld32s(&sh->stop) != 0) break;
+      u32x4c_t cl = ld16c(ctrl);
+      vm_wait(cl);
+      if (cl.z != 0) break;
     }
     last = wall_clock64();
 #ifdef SPL_RING_STAMPS
@@ -914,6 +940,8 @@ int CmdRing::init_vram() {
 
 void CmdRing::launch(const spl_arena_t& a) {
   std::lock_guard<std::mutex> lk(launch_mu_);
+  if (mode_ == kPrivate) arena_ = a;  // (for resume)
+  if (g_hold.load(std::memory_order_acquire) > 0) return;  // held: the waiters retry later
   if (__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) return;
   __atomic_store_n(&shared_->alive, 1u, __ATOMIC_RELEASE);
   __atomic_fetch_add(seg_ ? &seg_->launches : &shared_->launches, 1u, __ATOMIC_RELAXED);
@@ -1138,6 +1166,12 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
   if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
   __atomic_store_n(&ent_[e].busy, 0u, __ATOMIC_RELEASE);
   return 0;
+}
+
+// after a hold: relaunch the worker if calls are waiting for it
+void CmdRing::resume() {
+  if (!shared_ || mode_ == kClient || !arena_.base) return;
+  if (__atomic_load_n(waiters_, __ATOMIC_RELAXED) > 0) launch(arena_);
 }
 
 void CmdRing::stop() {

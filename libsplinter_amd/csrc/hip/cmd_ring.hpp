@@ -170,6 +170,10 @@ struct RingSegHdr {
 };
 constexpr uint32_t kRingSegMagic = 0x52494e47;  // "RING"
 
+// Hold every ring worker of this process (stopped, no relaunch) until the matching release;
+// nestable.  Per-call ops wait meanwhile.  spl_ring_hold (arena_api.h) is the C entry point.
+void ring_hold(bool on);
+
 class CmdRing {
  public:
   // Private ring of this process (its own worker).  device: ordinal of the arena's GPU; pstride:
@@ -196,6 +200,7 @@ class CmdRing {
   int call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen, uint64_t khash,
            const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap, RingResult* r);
   void stop();
+  void resume();  // after ring_hold(false): relaunch if calls wait
   uint32_t launches() const { return seg_ ? seg_->launches : shared_ ? shared_->launches : 0; }
 
  private:

@@ -1285,6 +1285,10 @@ uint32_t spl_hbm_ring_launches(spl_store* h) {
   return s ? s->ring_launches() : 0;
 }
 
+// Hold (on != 0) / release every per-call ring worker of this process (cmd_ring.hpp ring_hold):
+// a process about to run a heavy GPU job keeps its resident workers off the GPU meanwhile.
+void spl_ring_hold(int on) { spl::ring_hold(on != 0); }
+
 // 0: the store's calls run on this process's own ring worker; 1: this process hosts the store's
 // ring server; 2: it submits to the owner's ring server (cmd_ring.hpp); -1: not an HBM store
 int spl_hbm_ring_mode(spl_store* h) {

@@ -112,6 +112,10 @@ int   spl_hbm_device_count(void);               /* libsplinter_hip.so */
 /* per-call ring of an hbm: store in this process: 0 its own worker, 1 this process hosts the
  * store's ring server (the owner), 2 it submits to the owner's server; -1 not an hbm: store */
 int   spl_hbm_ring_mode(spl_store *s);          /* libsplinter_hip.so */
+/* hold (on != 0) / release every per-call ring worker this process runs: no worker is resident
+ * while held (per-call ops wait and are served after the release); for a process about to run a
+ * heavy GPU job beside the store's clients (a resident worker costs it time-slices).  Nestable. */
+void  spl_ring_hold(int on);                    /* libsplinter_hip.so */
 
 /* Host-array batches (batch_host.cpp): n fixed-stride NUL-padded key records (kstride <= 64), value
  * rows of vstride / ostride bytes, per-op status 0 or -errno (EAGAIN -11, ENOENT -2, ENOSPC -28,

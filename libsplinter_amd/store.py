@@ -102,6 +102,23 @@ def node_leave(node: str, shard: int) -> None:
     N.core_lib().spl_node_leave(node.encode(), shard)
 
 
+class ring_hold:
+    """Context manager: no per-call ring worker of this process is resident inside the block
+    (``spl_ring_hold``; per-call ops -- this process's and the store's clients' -- wait and are
+    served afterwards).  For a process about to run a heavy GPU job beside the clients of stores
+    it owns: a resident worker costs that job queue time-slices (profiles/r4x)."""
+
+    def __enter__(self):
+        from . import _native as N
+        self._L = N.hip_lib()
+        self._L.spl_ring_hold(1)
+        return self
+
+    def __exit__(self, *exc):
+        self._L.spl_ring_hold(0)
+        return False
+
+
 class Store:
     """One open store.  Use :meth:`create`, :meth:`open` or :meth:`open_or_create`."""
 

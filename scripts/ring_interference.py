@@ -8,6 +8,8 @@ store's per-call API (splinter_hostapi_bench --attach, 8 threads each).
            slowdown (CPU contention with the encoder's launching thread)
   idle     the clients call for 0.3 s and exit BEFORE the encoder is timed: with
            SPLINTER_RING_IDLE_US set long, the owner's worker stays resident but idle
+  held     as shared, with each encoder step inside a ring hold (store.ring_hold: the owner's
+           worker is off the GPU during the step; calls wait for the gaps)
 --client-args: extra splinter_hostapi_bench arguments (e.g. "--set-frac 0": gets only)
 
 Prints one JSON line: encoder ms/step alone and beside the clients in either mode, the slowdown,
@@ -40,6 +42,19 @@ STEPS = []  # per-step encoder ms of the last time_steps (events on the encoder'
 SYNC = {}  # how long the device-wide synchronizes around the last time_steps took (ms)
 
 
+HOLD = [False]
+
+
+def _step(ph):
+    if HOLD[0]:
+        from libsplinter_amd.store import ring_hold
+        with ring_hold():
+            ph.run()
+            torch.cuda.current_stream().synchronize()
+    else:
+        ph.run()
+
+
 def time_steps(ph, n):
     # stream-level synchronisation only: a device-wide synchronize waits for this process's resident
     # ring worker, which does not idle out while clients call -- it would time the encoder after them
@@ -50,7 +65,7 @@ def time_steps(ph, n):
     SYNC["before_ms"] = round((t0 - ts) * 1e3, 3)
     ev[0].record()
     for i in range(n):
-        ph.run()
+        _step(ph)
         ev[i + 1].record()
     ev[n].synchronize()
     t1 = time.perf_counter()
@@ -96,6 +111,7 @@ def main():
                                            str(dur), "--keys", str(a.keys)] + a.client_args.split(), env=env,
                                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
                          for _ in range(a.clients)]
+                HOLD[0] = mode == "held"
                 try:
                     if mode == "idle":
                         for p in procs:
@@ -117,6 +133,7 @@ def main():
                         rate += int(c) / float(el)
                         fails += int(f)
                 finally:
+                    HOLD[0] = False
                     for p in procs:
                         if p.poll() is None:
                             p.kill()

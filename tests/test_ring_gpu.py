@@ -337,3 +337,44 @@ def test_hostapi_four_processes_one_server(uniq):
     res = json.loads(r.stdout.strip().splitlines()[-1])
     print(json.dumps(res))
     assert res["failures"] == 0 and res["ring_mode"] == 1 and len(res["procs_p50_us"]) == 4
+
+
+_HOLD_CLIENT = r"""
+import sys, time
+from libsplinter_amd import Store
+s = Store.open(sys.argv[1])
+print("ready", flush=True)
+sys.stdin.readline()
+t = time.perf_counter()
+s.set("held", b"after-hold")
+print(round((time.perf_counter() - t) * 1e3, 1), flush=True)
+s.close()
+"""
+
+
+def test_ring_hold_defers_calls_until_release(uniq):
+    """store.ring_hold in the owner: no ring worker runs inside the block, a client's call waits
+    and is served once the hold ends; the owner's own calls work again afterwards."""
+    from libsplinter_amd import Store
+    from libsplinter_amd.store import ring_hold
+    s = Store.create(f"hbm:{uniq}", slots=1024, max_val=64, embeddings=False)
+    p = subprocess.Popen([sys.executable, "-c", _HOLD_CLIENT, f"hbm:{uniq}"], cwd=ROOT, env=ENV,
+                         stdin=subprocess.PIPE, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        s.set("pre", b"1")
+        assert p.stdout.readline().strip() == "ready"
+        with ring_hold():
+            p.stdin.write("go\n")
+            p.stdin.flush()
+            time.sleep(0.4)
+            assert p.poll() is None  # the client's set is still waiting
+        out, err = p.communicate(timeout=60)
+        assert p.returncode == 0, err[-2000:]
+        assert float(out.strip()) >= 300.0
+        assert s.get("held") == b"after-hold"
+        s.set("post", b"2")
+        assert s.get("post") == b"2"
+    finally:
+        if p.poll() is None:
+            p.kill()
+        s.close()

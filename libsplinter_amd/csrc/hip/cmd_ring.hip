@@ -949,11 +949,12 @@ void CmdRing::launch(const spl_arena_t& a) {
   (void)hipGetDevice(&cur);
   if (cur != device_) (void)hipSetDevice(device_);
   if (!stream_) {  // created on first use: a store that never takes a per-call op claims no queue
-    // high priority (SPLINTER_RING_PRIORITY=0: normal); a CU-masked queue measured worse
-    // (profiles/r4h interf_cus*)
+    // normal priority (SPLINTER_RING_PRIORITY=1: high): a resident worker on a high-priority queue
+    // cost a concurrent encoder +84 %, on a normal one +30 % (profiles/r4y); a CU-masked queue
+    // measured worse (profiles/r4h interf_cus*)
     int lo = 0, hi = 0;
     (void)hipDeviceGetStreamPriorityRange(&lo, &hi);
-    (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, env_int("SPLINTER_RING_PRIORITY", 1) ? hi : 0);
+    (void)hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, env_int("SPLINTER_RING_PRIORITY", 0) ? hi : 0);
   }
   // stream order: the previous worker (if still draining) has exited before ctrl is reset
   const uint32_t init[4] = {0u, 0u, 0u, (uint32_t)groups_};

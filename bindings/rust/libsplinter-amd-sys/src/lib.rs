@@ -281,3 +281,9 @@ extern "C" {
     pub fn spl_batch_alloc(bytes: usize) -> *mut c_void;
     pub fn spl_batch_free(p: *mut c_void);
 }
+
+// libsplinter_hip.so (loaded by libsplinter.so on the first hbm: / node: store): the per-call ring
+extern "C" {
+    pub fn spl_hbm_ring_mode(s: *mut spl_store) -> c_int;
+    pub fn spl_ring_hold(on: c_int);
+}

@@ -7,12 +7,12 @@
 //   * a ring of kEntries command records in pinned, host-coherent memory (one per lane),
 //   * a contiguous doorbell array state[kEntries],
 //   * ONE resident worker kernel (k_ring_worker) of `groups` one-wave workgroups on a
-//     high-priority stream (SPLINTER_RING_GROUPS, default 8); lane i of group g serves entry
+//     normal-priority stream (SPLINTER_RING_GROUPS, default 32); lane i of group g serves entry
 //     g*per+i (per = kRingEntries / groups) and each group polls its doorbells in one coalesced
-//     read, so concurrent host threads' calls run in parallel waves.  Few waves on purpose: a
-//     worker wave holds 233 VGPRs for its whole life, and a CU that hosts one cannot take the
-//     encoder's GEMM workgroups (2 waves per SIMD at 226-250 VGPRs), so 32 waves cost the
-//     encoder ~20 % beside live clients (profiles/r4g ring_interference).  (One kernel, not one per group: streams share
+//     read, so concurrent host threads' calls run in parallel waves.  A resident worker costs a
+//     concurrent GPU job of the same process queue time-slices (+29 % for the encoder on a
+//     normal-priority queue, +84 % on a high-priority one, whatever the wave count: profiles/r4y),
+//     hence ring_hold() for processes that run such a job.  (One kernel, not one per group: streams share
 //     GPU_MAX_HW_QUEUES hardware queues, and a group queued behind another group's resident
 //     kernel would wait out that kernel's idle timeout.)
 // Ring server: the process that created the store (its owner) runs the store's ONE worker and
@@ -87,7 +87,8 @@ static_assert(offsetof(RingCmd, status) % 16 == 0 && offsetof(RingCmd, result) =
               "the completion words must form one 16-B chunk");
 
 constexpr int kRingGroups = 32;                     // most one-wave workers (SPLINTER_RING_GROUPS)
-constexpr int kDefaultRingGroups = 8;               // default worker waves
+constexpr int kDefaultRingGroups = 32;              // default worker waves (32 vs 8: 1.29-1.32 vs 1.05-1.09 M ops/s at
+                                                    // 64 host threads, no fall-off from 32 threads; profiles/r4ab)
 constexpr int kRingEntries = 256;                   // entries (per wave: kRingEntries / groups)
 
 struct RingShared {

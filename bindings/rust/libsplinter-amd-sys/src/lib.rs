@@ -286,4 +286,5 @@ extern "C" {
 extern "C" {
     pub fn spl_hbm_ring_mode(s: *mut spl_store) -> c_int;
     pub fn spl_ring_hold(on: c_int);
+    pub fn spl_hbm_ring_hold(s: *mut spl_store, on: c_int) -> c_int;
 }

@@ -246,6 +246,8 @@ def _declare_hip(L):
         _sig(L, "spl_hbm_ring_mode", c_int, c_void_p)
     if hasattr(L, "spl_ring_hold"):
         _sig(L, "spl_ring_hold", None, c_int)
+    if hasattr(L, "spl_hbm_ring_hold"):
+        _sig(L, "spl_hbm_ring_hold", c_int, c_void_p, c_int)
     _sig(L, "spl_arena_purge", c_int, A, P)
     _sig(L, "spl_arena_gather_slots", c_int, A, P, c_long, P, P)
     _sig(L, "spl_hash_keys", c_int, P, c_int, c_long, P, P)

@@ -560,7 +560,7 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
         continue;
       }
 #endif
-      if (ld32s(&sh->stop) != 0) break;
+      if ((ld32s(&sh->stop) | ld32s(&sh->hold)) != 0) break;
       u32x4c_t cl = ld16c(ctrl);
       vm_wait(cl);
       if (cl.z != 0) break;  // another group timed out: leave together
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
     }
     // a wave that never goes idle (every round has a call) still sees stop / dying every 64th round
     if ((++busy_rounds & 63) == 0) {
-      if (ld32s(&sh->stop) != 0) break;
+      if ((ld32s(&sh->stop) | ld32s(&sh->hold)) != 0) break;
       u32x4c_t cl = ld16c(ctrl);
       vm_wait(cl);
       if (cl.z != 0) break;
@@ -941,7 +941,8 @@ int CmdRing::init_vram() {
 void CmdRing::launch(const spl_arena_t& a) {
   std::lock_guard<std::mutex> lk(launch_mu_);
   if (mode_ == kPrivate) arena_ = a;  // (for resume)
-  if (g_hold.load(std::memory_order_acquire) > 0) return;  // held: the waiters retry later
+  // held (this process, or the store by any process): the waiters retry later
+  if (g_hold.load(std::memory_order_acquire) > 0 || __atomic_load_n(&shared_->hold, __ATOMIC_ACQUIRE)) return;
   if (__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) return;
   __atomic_store_n(&shared_->alive, 1u, __ATOMIC_RELEASE);
   __atomic_fetch_add(seg_ ? &seg_->launches : &shared_->launches, 1u, __ATOMIC_RELAXED);
@@ -1166,6 +1167,33 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     std::memcpy(out, payload_ + (size_t)e * pstride_, r->out_len < out_cap ? r->out_len : out_cap);
   if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
   __atomic_store_n(&ent_[e].busy, 0u, __ATOMIC_RELEASE);
+  return 0;
+}
+
+int CmdRing::hold(bool on) {
+  if (!shared_) { errno = ENOSYS; return -1; }
+  if (mode_ == kClient && gone_.load(std::memory_order_acquire) && priv_) return priv_->hold(on);
+  if (on) {
+    __atomic_fetch_add(&shared_->hold, 1u, __ATOMIC_ACQ_REL);
+    // the worker sees the flag within a poll round; wait until its last wave is out
+    timespec t0;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    while (__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) {
+      timespec n;
+      clock_gettime(CLOCK_MONOTONIC, &n);
+      if ((n.tv_sec - t0.tv_sec) * 1000000000L + (n.tv_nsec - t0.tv_nsec) > 10000000000L) {
+        errno = ETIMEDOUT;
+        return -1;
+      }
+      sched_yield();
+    }
+    return 0;
+  }
+  if (__atomic_sub_fetch(&shared_->hold, 1u, __ATOMIC_ACQ_REL) != 0) return 0;
+  if (__atomic_load_n(waiters_, __ATOMIC_RELAXED) > 0) {  // calls are waiting: a worker again
+    if (mode_ == kClient) want_worker();
+    else if (arena_.base) launch(arena_);
+  }
   return 0;
 }
 

@@ -96,7 +96,8 @@ struct RingShared {
   uint32_t alive;                // the worker is running or queued (cleared by its last wave)
   uint32_t stop;                 // ask the worker to exit
   uint32_t launches;             // host statistic
-  uint32_t pad[13];
+  uint32_t hold;                 // store-level holds (CmdRing::hold, any attached process): no worker
+  uint32_t pad[12];
 #ifdef SPL_RING_STAMPS
   // latency breakdown (make hip-variant V=stamps VFLAGS=-DSPL_RING_STAMPS): per entry, sums of
   // wall-clock ticks from "doorbell seen" to "record loaded", to "op done", to "completion
@@ -202,6 +203,10 @@ class CmdRing {
            const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap, RingResult* r);
   void stop();
   void resume();  // after ring_hold(false): relaunch if calls wait
+  // Store-level hold from any process attached to the store's ring (server, client or private):
+  // the worker exits and is not relaunched until every hold is released.  0, or -1 (ETIMEDOUT) if
+  // the worker did not exit within 10 s.
+  int hold(bool on);
   uint32_t launches() const { return seg_ ? seg_->launches : shared_ ? shared_->launches : 0; }
 
  private:

@@ -122,6 +122,7 @@ class HbmStore final : public StoreBase {
   hipStream_t stream() const { return stream_; }
   uint32_t ring_launches() const { return ring_ ? ring_->launches() : 0; }
   int ring_mode() const { return ring_ ? ring_->mode() : -1; }
+  int ring_hold(bool on) { return ring_ ? ring_->hold(on) : (errno = ENOSYS, -1); }
   bool attach() { return ensure_mapped(); }
 
   int set_mop(unsigned mode) override {
@@ -1288,6 +1289,16 @@ uint32_t spl_hbm_ring_launches(spl_store* h) {
 // Hold (on != 0) / release every per-call ring worker of this process (cmd_ring.hpp ring_hold):
 // a process about to run a heavy GPU job keeps its resident workers off the GPU meanwhile.
 void spl_ring_hold(int on) { spl::ring_hold(on != 0); }
+
+// Store-level hold, from any process that has the store open (the owner's ring server, a client
+// of it, or a private ring): the store's worker exits and stays off the GPU until every hold is
+// released; the store's per-call ops wait meanwhile.  For a process that runs a heavy GPU job
+// while another process hosts the store's ring.  0 / -1 (errno).
+int spl_hbm_ring_hold(spl_store* h, int on) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  if (!s) { errno = EINVAL; return -1; }
+  return s->ring_hold(on != 0);
+}
 
 // 0: the store's calls run on this process's own ring worker; 1: this process hosts the store's
 // ring server; 2: it submits to the owner's ring server (cmd_ring.hpp); -1: not an HBM store

@@ -116,6 +116,9 @@ int   spl_hbm_ring_mode(spl_store *s);          /* libsplinter_hip.so */
  * while held (per-call ops wait and are served after the release); for a process about to run a
  * heavy GPU job beside the store's clients (a resident worker costs it time-slices).  Nestable. */
 void  spl_ring_hold(int on);                    /* libsplinter_hip.so */
+/* the same for ONE store's ring from any process that has it open (e.g. a daemon whose store's
+ * ring server lives in another process): its worker exits and stays off until released */
+int   spl_hbm_ring_hold(spl_store *s, int on);  /* libsplinter_hip.so */
 
 /* Host-array batches (batch_host.cpp): n fixed-stride NUL-padded key records (kstride <= 64), value
  * rows of vstride / ostride bytes, per-op status 0 or -errno (EAGAIN -11, ENOENT -2, ENOSPC -28,

@@ -103,19 +103,31 @@ def node_leave(node: str, shard: int) -> None:
 
 
 class ring_hold:
-    """Context manager: no per-call ring worker of this process is resident inside the block
-    (``spl_ring_hold``; per-call ops -- this process's and the store's clients' -- wait and are
-    served afterwards).  For a process about to run a heavy GPU job beside the clients of stores
-    it owns: a resident worker costs that job queue time-slices (profiles/r4x)."""
+    """Context manager: no per-call ring worker is resident inside the block; per-call ops wait and
+    are served afterwards.  For a process about to run a heavy GPU job beside per-call clients: a
+    resident worker costs that job queue time-slices (profiles/r4y, r4z).
+
+    ``ring_hold()``: every ring worker THIS process runs (``spl_ring_hold``) -- the rings of the
+    stores it owns.  ``ring_hold(store)``: that hbm: store's ring, wherever its worker runs (e.g. a
+    daemon whose store's ring server lives in the owner's process; ``spl_hbm_ring_hold``)."""
+
+    def __init__(self, store: "Optional[Store]" = None):
+        self.store = store
 
     def __enter__(self):
         from . import _native as N
         self._L = N.hip_lib()
-        self._L.spl_ring_hold(1)
+        if self.store is None:
+            self._L.spl_ring_hold(1)
+        elif self._L.spl_hbm_ring_hold(self.store.handle, 1) != 0:
+            _raise("ring hold")
         return self
 
     def __exit__(self, *exc):
-        self._L.spl_ring_hold(0)
+        if self.store is None:
+            self._L.spl_ring_hold(0)
+        else:
+            self._L.spl_hbm_ring_hold(self.store.handle, 0)
         return False
 
 

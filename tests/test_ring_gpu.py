@@ -378,3 +378,40 @@ def test_ring_hold_defers_calls_until_release(uniq):
         if p.poll() is None:
             p.kill()
         s.close()
+
+
+_STORE_HOLDER = r"""
+import sys, time
+from libsplinter_amd import Store
+from libsplinter_amd.store import ring_hold
+s = Store.open(sys.argv[1])
+with ring_hold(s):
+    print("held", flush=True)
+    time.sleep(0.5)
+print("released", flush=True)
+s.close()
+"""
+
+
+def test_store_ring_hold_from_another_process(uniq):
+    """ring_hold(store) in a client process stops the OWNER's ring worker for that store: the
+    owner's own per-call op waits until the client releases, then completes."""
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=1024, max_val=64, embeddings=False)
+    p = subprocess.Popen([sys.executable, "-c", _STORE_HOLDER, f"hbm:{uniq}"], cwd=ROOT, env=ENV,
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    try:
+        s.set("pre", b"1")
+        assert p.stdout.readline().strip() == "held"
+        t = time.perf_counter()
+        s.set("during", b"2")  # waits for the release (~0.5 s)
+        dt = time.perf_counter() - t
+        out, err = p.communicate(timeout=60)
+        assert p.returncode == 0, err[-2000:]
+        assert out.strip() == "released"
+        assert dt >= 0.3, dt
+        assert s.get("during") == b"2"
+    finally:
+        if p.poll() is None:
+            p.kill()
+        s.close()

@@ -42,17 +42,29 @@ STEPS = []  # per-step encoder ms of the last time_steps (events on the encoder'
 SYNC = {}  # how long the device-wide synchronizes around the last time_steps took (ms)
 
 
-HOLD = [False]
+HOLD = [False, None]  # hold on?, the store to hold (None: this process's rings)
 
 
 def _step(ph):
     if HOLD[0]:
         from libsplinter_amd.store import ring_hold
-        with ring_hold():
+        with ring_hold(HOLD[1]):
             ph.run()
             torch.cuda.current_stream().synchronize()
     else:
         ph.run()
+
+
+_OWNER = r"""
+import sys
+from libsplinter_amd import Store
+st = Store.create(sys.argv[1], slots=2 * int(sys.argv[2]) + 1024, max_val=4096, embeddings=False)
+keys = [f"hk{i:08d}" for i in range(int(sys.argv[2]))]
+st.set_batch(keys, [b"v" * 150] * len(keys))
+print("ready", flush=True)
+sys.stdin.readline()
+st.close()
+"""
 
 
 def time_steps(ph, n):
@@ -82,17 +94,29 @@ def main():
     ap.add_argument("--keys", type=int, default=20000)
     ap.add_argument("--modes", default="shared,private,cpu")
     ap.add_argument("--client-args", default="")
+    ap.add_argument("--owner-proc", action="store_true",
+                    help="the store (and its ring server) is owned by a separate process; this encoder process "
+                         "is one of its clients (held mode then holds the store: ring_hold(store))")
     ap.add_argument("--settle", type=float, default=4.0,
                     help="seconds between starting the clients and timing (their HIP start-up and store attach, "
                          "which maps the arena into their GPU address space, are over by then)")
     a = ap.parse_args()
     name = f"hbm:ri{os.getpid()}"
-    st = Store.create(name, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
+    owner = None
+    if a.owner_proc:
+        owner = subprocess.Popen([sys.executable, "-c", _OWNER, name, str(a.keys)], stdin=subprocess.PIPE,
+                                 stdout=subprocess.PIPE, text=True, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+        assert owner.stdout.readline().strip() == "ready"
+        st = Store.open(name)
+        HOLD[1] = st
+    else:
+        st = Store.create(name, slots=2 * a.keys + 1024, max_val=4096, embeddings=False)
     out = {"clients": a.clients, "cpus": len(os.sched_getaffinity(0)), "owner_ring_mode": N.hip_lib().spl_hbm_ring_mode(st.handle)}
     try:
         keys = [f"hk{i:08d}" for i in range(a.keys)]
-        status = st.set_batch(keys, [b"v" * 150] * a.keys)
-        assert int((status != 0).sum()) == 0
+        if owner is None:
+            status = st.set_batch(keys, [b"v" * 150] * a.keys)
+            assert int((status != 0).sum()) == 0
         ph = EmbedPhase(batch=64, seq=512)
         for _ in range(3):
             ph.run()
@@ -150,6 +174,10 @@ def main():
         S.unlink(shm)
     finally:
         st.close()
+        if owner is not None:
+            owner.stdin.write("done\n")
+            owner.stdin.flush()
+            owner.wait(timeout=60)
     print(json.dumps(out), flush=True)
 
 

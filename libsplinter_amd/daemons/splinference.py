@@ -53,7 +53,8 @@ def log(*a):
 
 class Splinference:
     def __init__(self, store, encoder, tokenizer, group: int, vector_training: bool = False,
-                 batch_tokens: int = 1 << 16, normalize: bool = False, rank: Optional[int] = None):
+                 batch_tokens: int = 1 << 16, normalize: bool = False, rank: Optional[int] = None,
+                 hold_ring: Optional[bool] = None):
         import torch  # noqa: F401
         from ..store import SLOT_VARTEXT
         # `node`: the store clients use (signals, label map, bids, lane pulses); `store`: the one
@@ -66,6 +67,10 @@ class Splinference:
                 raise ValueError(f"rank {self.rank} outside the node's {store.nshards} shards")
             store = store.shard(self.rank)
         self.store = store
+        # hold_ring (SPLINTER_DAEMON_RING_HOLD=1): the store's per-call ring worker stays off the GPU
+        # while a pass embeds on it (store.ring_hold(store)): a resident worker costs the encoder
+        # queue time-slices (+29 %, profiles/r4z); clients' per-call ops wait for the pass instead
+        self.hold_ring = (os.environ.get("SPLINTER_DAEMON_RING_HOLD", "0") == "1") if hold_ring is None else hold_ring
         self.enc = encoder
         self.tok = tokenizer
         self.group = group
@@ -246,6 +251,29 @@ class Splinference:
             else:
                 good.append(i)
         order = sorted(good, key=lambda i: offs[i + 1] - offs[i])
+        if self.hold_ring and self.arena is not None:  # the HBM batches make no per-call op
+            from ..store import ring_hold
+            with ring_hold(self.store):
+                done = self._process_batches(order, ks, ids, offs, eps)
+        else:
+            done = self._process_batches(order, ks, ids, offs, eps)
+        # ctime backfill: wall time minus processing ticks (reference :530-537)
+        now_s, dt = int(time.time()), self._ticks() - tick0
+        if self.arena is not None and good:
+            K = self._keys_u8([ks[i] for i in good])
+            self.arena.meta("ctime", K, torch.full((len(good),), now_s, dtype=torch.int64, device=K.device))
+        else:
+            for i in good:
+                try:
+                    self.store.set_time(ks[i], 0, now_s, 0)
+                except Exception:  # noqa: BLE001
+                    pass
+        self.node.pulse(LANE_KEY)
+        self.stats["embedded"] += done
+        log(f"embedded {done}/{len(ks)} keys in {time.time() - t_start:.3f}s (ticks {dt})")
+        return done
+
+    def _process_batches(self, order, ks, ids, offs, eps) -> int:
         done = 0
         batch: List[int] = []
         ntok = 0
@@ -266,21 +294,6 @@ class Splinference:
                 ntok += n
         if inflight is not None:
             done += self._finish_hbm(inflight, ks, eps)
-        # ctime backfill: wall time minus processing ticks (reference :530-537)
-        now_s, dt = int(time.time()), self._ticks() - tick0
-        if self.arena is not None and good:
-            import torch
-            K = self._keys_u8([ks[i] for i in good])
-            self.arena.meta("ctime", K, torch.full((len(good),), now_s, dtype=torch.int64, device=K.device))
-        else:
-            for i in good:
-                try:
-                    self.store.set_time(ks[i], 0, now_s, 0)
-                except Exception:  # noqa: BLE001
-                    pass
-        self.node.pulse(LANE_KEY)
-        self.stats["embedded"] += done
-        log(f"embedded {done}/{len(ks)} keys in {time.time() - t_start:.3f}s (ticks {dt})")
         return done
 
     @staticmethod

@@ -111,7 +111,7 @@ def test_node_hbm_checkpoint_roundtrip(hbm_node, tmp_path):
 def test_dp_splinference_embeds_every_shard(hbm_node):
     """One daemon per shard (rank 0..3, oneshot), each embedding only its own shard's pending keys
     on its GPU; together they cover the node, and each vector equals the encoder's output for the
-    key's text."""
+    key's text.  Odd ranks embed inside a ring hold of their shard (hold_ring)."""
     import torch
     from libsplinter_amd.daemons.splinference import Splinference, build_encoder
     S, s, name = hbm_node
@@ -123,7 +123,7 @@ def test_dp_splinference_embeds_every_shard(hbm_node):
     enc, tok = build_encoder(None, True, layers=2, max_tokens=1 << 14)
     done = {}
     for r in range(4):
-        d = Splinference(s, enc, tok, group=3, rank=r)
+        d = Splinference(s, enc, tok, group=3, rank=r, hold_ring=bool(r & 1))
         assert d.arena is not None  # the shard's batched device path
         d.run(oneshot=True)
         done[r] = d.stats["embedded"]

@@ -14,7 +14,11 @@
 #include <sys/stat.h>
 #include <sys/syscall.h>
 #include <unistd.h>
+#include <emmintrin.h>
+#include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <functional>
 #include <thread>
 #include <vector>
 
@@ -380,19 +384,99 @@ int NodeStore::madvise(uint32_t id, void* addr, size_t len, int advice, uint64_t
 // A batch is counting-sorted by owning shard into one scratch buffer (pinned when the HBM backend
 // is present, so HBM shards DMA straight from it), every shard's contiguous part runs on its own
 // thread (HBM shards: HbmStore::*_batch on that shard's GPU, all GPUs at once), and the outputs go
-// back into client order.  The copies walk the CLIENT order on kNodeBatchThreads threads: the
-// sort is stable per thread chunk, so each thread reads its rows sequentially and writes them to
-// one sequential stream per shard (no random row reads: 66.7 M ops/s with per-row gathers by
-// permutation, 4 HBM shards on one GPU, profiles/r4f).
+// back into client order.  Two passes over the CLIENT order on batch_threads() pool threads: hash +
+// per-part shard histogram, then placement with the input rows copied as each op is placed (the
+// sort is stable per part, so each part reads its rows sequentially and writes one sequential
+// stream per shard: no random row reads -- 66.7 M ops/s with per-row gathers by permutation, 4 HBM
+// shards on one GPU, profiles/r4f).
 namespace {
-constexpr int kNodeBatchThreads = 8;
+// SPLINTER_NODE_BATCH_THREADS (default min(16, hardware threads)): host threads that partition and
+// copy a node batch (4 HBM shards on one GPU, 2M-op batches: 93 M ops/s before the pool, 105 M at
+// 8 threads, 122 M at 16 -- profiles/r4ae)
+int batch_threads() {
+  static const int t = [] {
+    const char* e = getenv("SPLINTER_NODE_BATCH_THREADS");
+    const int hw = (int)std::thread::hardware_concurrency();
+    const int v = e && *e ? atoi(e) : std::min(16, hw > 0 ? hw : 8);
+    return v < 1 ? 1 : v > 64 ? 64 : v;
+  }();
+  return t;
+}
+
+// Fork-join pool of batch_threads() - 1 sleeping workers (the caller is part 0): the partition and
+// the copies of every chunk run on it without creating threads.  One job at a time; a second
+// concurrent caller (the pipeline's output copies beside the next chunk's partition) gets false
+// and runs on threads of its own.  Re-created in a forked child; never destroyed (its workers
+// sleep through process exit).
+class BatchPool {
+ public:
+  explicit BatchPool(int n) : n_(n) {
+    for (int i = 1; i < n; ++i) std::thread([this, i] { loop(i); }).detach();
+  }
+  bool run(const std::function<void(int)>& f) {
+    std::unique_lock<std::mutex> busy(run_mu_, std::try_to_lock);
+    if (!busy.owns_lock()) return false;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      pending_ = n_ - 1;
+      ++gen_;
+    }
+    cv_.notify_all();
+    f(0);
+    std::unique_lock<std::mutex> lk(mu_);
+    done_.wait(lk, [&] { return pending_ == 0; });
+    job_ = nullptr;
+    return true;
+  }
+
+ private:
+  void loop(int i) {
+    uint64_t seen = 0;
+    for (;;) {
+      const std::function<void(int)>* f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return gen_ != seen; });
+        seen = gen_;
+        f = job_;
+      }
+      (*f)(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--pending_ == 0) done_.notify_one();
+    }
+  }
+  const int n_;
+  std::mutex run_mu_, mu_;
+  std::condition_variable cv_, done_;
+  const std::function<void(int)>* job_ = nullptr;
+  int pending_ = 0;
+  uint64_t gen_ = 0;
+};
+
+BatchPool& batch_pool() {
+  static std::mutex m;
+  static BatchPool* p = nullptr;
+  static pid_t pid = 0;
+  std::lock_guard<std::mutex> lk(m);
+  if (!p || pid != getpid()) {
+    p = new BatchPool(batch_threads());
+    pid = getpid();
+  }
+  return *p;
+}
+
+// parts a range of n ops is split into (the partition's per-part histograms follow the same split)
+inline int par_parts(long n) { return n < 65536 ? 1 : batch_threads(); }
 
 template <class F>
-void par_range(long n, F&& f, int t = kNodeBatchThreads) {
-  if (n < 65536) t = 1;
+void par_range(long n, F&& f) {
+  const int t = par_parts(n);
   if (t <= 1) { f(0L, n, 0); return; }
+  const std::function<void(int)> job = [&](int i) { f(n * i / t, n * (i + 1) / t, i); };
+  if (batch_pool().run(job)) return;
   std::vector<std::thread> th;
-  for (int i = 0; i < t; ++i) th.emplace_back([&, i] { f(n * i / t, n * (i + 1) / t, i); });
+  for (int i = 0; i < t; ++i) th.emplace_back(job, i);
   for (auto& x : th) x.join();
 }
 
@@ -406,6 +490,57 @@ inline void copy_row(uint8_t* d, const uint8_t* s, long w) {
     default: std::memcpy(d, s, (size_t)w);
   }
 }
+
+// length of key record r (NUL-padded, kstride bytes), capped at cut: one 16-byte compare when the
+// record is at least 16 bytes wide
+inline int key_len(const char* r, int kstride, int cut) {
+  if (kstride < 16) return (int)strnlen(r, (size_t)cut);
+  const __m128i v = _mm_loadu_si128((const __m128i*)r);
+  const unsigned z = (unsigned)_mm_movemask_epi8(_mm_cmpeq_epi8(v, _mm_setzero_si128()));
+  if (z) return std::min(__builtin_ctz(z), cut);
+  return cut <= 16 ? cut : 16 + (int)strnlen(r + 16, (size_t)(cut - 16));
+}
+
+// dest[i] = owning shard of key record i for i in [b, e), counted into cnt[shard].  FNV-1a is a
+// serial multiply chain per key, so runs of 4 equal-length keys (the common case: fixed-format
+// keys) are hashed side by side, 4 independent chains; == fnv1a_n(rec, strnlen(rec, cut)).
+void shard_keys(const char* keys, int kstride, int cut, long b, long e, int nsh, int32_t* dest, long* cnt) {
+  long i = b;
+  for (; i + 4 <= e; i += 4) {
+    const unsigned char* r0 = (const unsigned char*)keys + i * kstride;
+    const unsigned char *r1 = r0 + kstride, *r2 = r1 + kstride, *r3 = r2 + kstride;
+    const int l = key_len((const char*)r0, kstride, cut);
+    uint64_t h[4];
+    if (key_len((const char*)r1, kstride, cut) == l && key_len((const char*)r2, kstride, cut) == l &&
+        key_len((const char*)r3, kstride, cut) == l) {
+      uint64_t x0 = kFnvOffset, x1 = kFnvOffset, x2 = kFnvOffset, x3 = kFnvOffset;
+      for (int p = 0; p < l; ++p) {
+        x0 = (x0 ^ r0[p]) * kFnvPrime;
+        x1 = (x1 ^ r1[p]) * kFnvPrime;
+        x2 = (x2 ^ r2[p]) * kFnvPrime;
+        x3 = (x3 ^ r3[p]) * kFnvPrime;
+      }
+      h[0] = x0; h[1] = x1; h[2] = x2; h[3] = x3;
+    } else {
+      for (int k = 0; k < 4; ++k) {
+        const char* r = keys + (i + k) * kstride;
+        h[k] = fnv1a_n(r, (size_t)key_len(r, kstride, cut));
+      }
+    }
+    for (int k = 0; k < 4; ++k) {
+      const int d = node_shard_of(h[k], nsh);
+      dest[i + k] = d;
+      ++cnt[d];
+    }
+  }
+  for (; i < e; ++i) {
+    const char* rec = keys + i * kstride;
+    const int d = node_shard_of(fnv1a_n(rec, (size_t)key_len(rec, kstride, cut)), nsh);
+    dest[i] = d;
+    ++cnt[d];
+  }
+}
+
 }  // namespace
 
 // SPLINTER_NODE_BATCH_TRACE=1: per batch, ms in plan / gather / shards / scatter on stderr
@@ -434,25 +569,27 @@ struct BatchTrace {
 };
 
 struct NodeStore::Plan {
-  std::vector<long> pos;    // pos[i]: sorted position of client op i
-  std::vector<long> off;    // shard j's ops are sorted positions [off[j], off[j+1])
+  long n;
+  long* pos;      // pos[i]: sorted position of client op i
+  int32_t* dest;  // dest[i]: owning shard of client op i
+  std::vector<long> off;   // shard j's ops are sorted positions [off[j], off[j+1])
+  std::vector<long> base;  // [part][shard]: next sorted position of that part's ops of the shard
   int nsh;
-  Plan(const char* keys, int kstride, long n, int nsh_) : pos((size_t)n), off((size_t)nsh_ + 1, 0), nsh(nsh_) {
-    std::vector<int32_t> dest((size_t)n);
+  // slot: which of the store's two Plan buffers (pipeline halves) holds pos / dest
+  Plan(NodeStore& st, int slot, const char* keys, int kstride, long n_, int nsh_)
+      : n(n_), off((size_t)nsh_ + 1, 0), nsh(nsh_) {
+    auto& pv = st.plan_pos_[slot];
+    auto& dv = st.plan_dest_[slot];
+    if ((long)pv.size() < n) pv.resize((size_t)n);
+    if ((long)dv.size() < n) dv.resize((size_t)n);
+    pos = pv.data();
+    dest = dv.data();
     const int cut = kstride < 64 ? kstride : 63;
-    const int T = n < 65536 ? 1 : kNodeBatchThreads;
+    const int T = par_parts(n);
     std::vector<long> cnt((size_t)T * nsh, 0);
-    par_range(n, [&](long b, long e, int t) {
-      long* c = cnt.data() + (size_t)t * nsh;
-      for (long i = b; i < e; ++i) {
-        const char* rec = keys + i * kstride;  // the canonical key: its bytes up to the first NUL
-        const int d = node_shard_of(fnv1a_n(rec, strnlen(rec, (size_t)cut)), nsh);
-        dest[(size_t)i] = d;
-        ++c[d];
-      }
-    }, T);
-    // stable placement: thread t's ops of shard j follow those of threads < t
-    std::vector<long> base((size_t)T * nsh);
+    par_range(n, [&](long b, long e, int t) { shard_keys(keys, kstride, cut, b, e, nsh, dest, cnt.data() + (size_t)t * nsh); });
+    // stable placement: part t's ops of shard j follow those of parts < t
+    base.resize((size_t)T * nsh);
     long run = 0;
     for (int j = 0; j < nsh; ++j) {
       off[(size_t)j] = run;
@@ -462,21 +599,24 @@ struct NodeStore::Plan {
       }
     }
     off[(size_t)nsh] = run;
+  }
+  // the placement pass: pos[] filled in client order, put(i, q) copies op i's input rows to sorted
+  // position q as it goes (each part reads its rows sequentially and writes one stream per shard)
+  template <class F>
+  void place(F&& put) {
     par_range(n, [&](long b, long e, int t) {
       long* p = base.data() + (size_t)t * nsh;
-      for (long i = b; i < e; ++i) pos[(size_t)i] = p[dest[(size_t)i]]++;
-    }, T);
-  }
-  // client column (rows of `w` bytes) -> sorted scratch column
-  void gather(uint8_t* dst, const void* src, long w) const {
-    par_range((long)pos.size(), [&](long b, long e, int) {
-      for (long i = b; i < e; ++i) copy_row(dst + pos[(size_t)i] * w, (const uint8_t*)src + i * w, w);
+      for (long i = b; i < e; ++i) {
+        const long q = p[dest[i]]++;
+        pos[i] = q;
+        put(i, q);
+      }
     });
   }
   // sorted scratch column -> client column
   void scatter(void* dst, const uint8_t* src, long w) const {
-    par_range((long)pos.size(), [&](long b, long e, int) {
-      for (long i = b; i < e; ++i) copy_row((uint8_t*)dst + i * w, src + pos[(size_t)i] * w, w);
+    par_range(n, [&](long b, long e, int) {
+      for (long i = b; i < e; ++i) copy_row((uint8_t*)dst + i * w, src + pos[i] * w, w);
     });
   }
   template <class F>
@@ -542,7 +682,7 @@ long NodeStore::pipeline(long n, long per, Prep&& prep, Exec&& exec) {
   if (!S0) return -1;
   long ok = 0;
   bool fail = false;
-  std::unique_ptr<Plan> cur = prep(0L, C, S0);
+  std::unique_ptr<Plan> cur = prep(0L, C, S0, 0);
   for (long c = 0; c < nch; ++c) {
     const long c0 = c * C, m = std::min(C, n - c0);
     uint8_t* S = S0 + (c & 1) * per;
@@ -550,7 +690,7 @@ long NodeStore::pipeline(long n, long per, Prep&& prep, Exec&& exec) {
     std::unique_ptr<Plan> next;
     if (c + 1 < nch) {
       std::thread th([&] { r = exec(*cur, c0, m, S); });
-      next = prep(c0 + C, std::min(C, n - c0 - C), S0 + ((c + 1) & 1) * per);
+      next = prep(c0 + C, std::min(C, n - c0 - C), S0 + ((c + 1) & 1) * per, (int)((c + 1) & 1));
       th.join();
     } else {
       r = exec(*cur, c0, m, S);
@@ -569,12 +709,20 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
   const long C = chunk_for(n);
   const long ob = 0, vb = a64(C * kstride), lb = vb + a64(C * (long)vstride), sb = lb + a64(C * 4), per = sb + a64(C * 4);
   std::lock_guard<std::mutex> lk(scratch_mu_);
-  auto prep = [&](long c0, long m, uint8_t* S) {
-    auto pl = std::make_unique<Plan>(keys + c0 * kstride, kstride, m, nsh);
+  auto prep = [&](long c0, long m, uint8_t* S, int slot) {
+    const char* k = keys + c0 * kstride;
+    const uint8_t* v = vals + c0 * (long)vstride;
+    const uint32_t* l = lens + c0;
+    auto pl = std::make_unique<Plan>(*this, slot, k, kstride, m, nsh);
     tr.mark(0);
-    pl->gather(S + ob, keys + c0 * kstride, kstride);
-    pl->gather(S + vb, vals + c0 * (long)vstride, vstride);
-    pl->gather(S + lb, lens + c0, 4);
+    uint8_t* sk = S + ob;
+    uint8_t* sv = S + vb;
+    uint32_t* sl = (uint32_t*)(S + lb);
+    pl->place([&](long i, long q) {
+      copy_row(sk + q * kstride, (const uint8_t*)k + i * kstride, kstride);
+      copy_row(sv + q * (long)vstride, v + i * (long)vstride, vstride);
+      sl[q] = l[i];
+    });
     tr.mark(1);
     return pl;
   };
@@ -609,10 +757,12 @@ long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostri
   const long ob = 0, sb = a64(C * kstride), lb = sb + a64(C * 4), vb = lb + a64(C * 4);
   const long per = vb + (out ? a64(C * (long)ostride) : 0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
-  auto prep = [&](long c0, long m, uint8_t* S) {
-    auto pl = std::make_unique<Plan>(keys + c0 * kstride, kstride, m, nsh);
+  auto prep = [&](long c0, long m, uint8_t* S, int slot) {
+    const char* k = keys + c0 * kstride;
+    auto pl = std::make_unique<Plan>(*this, slot, k, kstride, m, nsh);
     tr.mark(0);
-    pl->gather(S + ob, keys + c0 * kstride, kstride);
+    uint8_t* sk = S + ob;
+    pl->place([&](long i, long q) { copy_row(sk + q * kstride, (const uint8_t*)k + i * kstride, kstride); });
     tr.mark(1);
     return pl;
   };
@@ -645,16 +795,20 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
                             int32_t* status, uint64_t* results) {
   const int nsh = nshards();
   BatchTrace tr("intop", n);
-  Plan pl(keys, kstride, n, nsh);
-  tr.mark(0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
+  Plan pl(*this, 0, keys, kstride, n, nsh);
+  tr.mark(0);
   const long kb = 0, pb = a64(n * kstride), mb = pb + a64(n * 4), sb = mb + a64(n * 8), rb = sb + a64(n * 4);
   uint8_t* S = scratch((size_t)(rb + a64(n * 8)));
   if (!S) return -1;
-  pl.gather(S + kb, keys, kstride);
-  pl.gather(S + pb, ops, 4);
-  if (masks) pl.gather(S + mb, masks, 8);
-  else std::memset(S + mb, 0, (size_t)(n * 8));
+  uint8_t* sk = S + kb;
+  int* sp = (int*)(S + pb);
+  uint64_t* sm = (uint64_t*)(S + mb);
+  pl.place([&](long i, long q) {
+    copy_row(sk + q * kstride, (const uint8_t*)keys + i * kstride, kstride);
+    sp[q] = ops[i];
+    sm[q] = masks ? masks[i] : 0;
+  });
   tr.mark(1);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
@@ -681,14 +835,18 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
 long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* vecs, long n, int32_t* status) {
   const int nsh = nshards();
   BatchTrace tr("set_embedding", n);
-  Plan pl(keys, kstride, n, nsh);
-  tr.mark(0);
   std::lock_guard<std::mutex> lk(scratch_mu_);
+  Plan pl(*this, 0, keys, kstride, n, nsh);
+  tr.mark(0);
   const long kb = 0, vb = a64(n * kstride), sb = vb + n * (long)kEmbedBytes;
   uint8_t* S = scratch((size_t)(sb + a64(n * 4)));
   if (!S) return -1;
-  pl.gather(S + kb, keys, kstride);
-  pl.gather(S + vb, vecs, (long)kEmbedBytes);
+  uint8_t* sk = S + kb;
+  uint8_t* sv = S + vb;
+  pl.place([&](long i, long q) {
+    copy_row(sk + q * kstride, (const uint8_t*)keys + i * kstride, kstride);
+    std::memcpy(sv + q * (long)kEmbedBytes, (const uint8_t*)vecs + i * (long)kEmbedBytes, kEmbedBytes);
+  });
   tr.mark(1);
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};

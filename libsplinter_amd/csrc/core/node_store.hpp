@@ -149,6 +149,8 @@ class NodeStore final : public StoreBase {
   long chunk_for(long n) const;
   uint8_t* scratch(size_t bytes);
   std::mutex scratch_mu_;
+  std::vector<long> plan_pos_[2];      // Plan storage per pipeline half (grown, never shrunk or
+  std::vector<int32_t> plan_dest_[2];  // zeroed again: no page faults on later batches)
   uint8_t* scratch_ = nullptr;
   size_t scratch_bytes_ = 0;
   bool scratch_pinned_ = false;

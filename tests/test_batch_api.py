@@ -175,3 +175,30 @@ def test_batch_api_node_store_shm_pipelined(monkeypatch):
     finally:
         s.close()
         S.unlink(name)
+
+
+def test_batch_api_node_store_after_fork(monkeypatch):
+    """The node batch thread pool is per process: a child forked after a batch (pool threads not
+    inherited) runs its own batches to completion."""
+    monkeypatch.setenv("SPLINTER_NODE_SHARDS", "4")
+    monkeypatch.setenv("SPLINTER_NODE_BACKEND", "shm")
+    from libsplinter_amd import store as S
+    name = f"node:bfk{os.getpid()}"
+    s = S.Store.create(name, slots=4 * 65536, max_val=64, embeddings=False)
+    try:
+        keys = [f"fk-{i:07d}" for i in range(70000)]  # above the threaded-partition threshold
+        assert (s.set_batch(keys, [b"parent"] * len(keys)) == 0).all()
+        pid = os.fork()
+        if pid == 0:
+            ok = False
+            try:
+                ok = bool((s.set_batch(keys, [b"child"] * len(keys)) == 0).all())
+            finally:
+                os._exit(0 if ok else 1)
+        _, code = os.waitpid(pid, 0)
+        assert os.WEXITSTATUS(code) == 0
+        st, out, ln = s.get_batch(keys, width=16)
+        assert (st == 0).all() and all(bytes(out[i, : ln[i]]) == b"child" for i in range(0, len(keys), 997))
+    finally:
+        s.close()
+        S.unlink(name)

@@ -409,7 +409,9 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma(spl_arena_t aa, cons
       sm.live[row] = h != 0 && (!mask || (bl & mask) == mask) && sel > kMinNorm2 && start + row >= t * kTile;
       sm.inv[row] = sel > 0.f ? rsqrtf(sel) : 0.f;
     }
-    raw_barrier();
+    // the live / inv stores must have landed before another wave reads them: a raw s_barrier does
+    // not wait for this wave's LDS stores
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     {
       const f32x4* invp = (const f32x4*)(sm.inv + fq * 4);  // rows 16i + 4fq + r, r = 0..3
       const int4* livp = (const int4*)(sm.live + fq * 4);

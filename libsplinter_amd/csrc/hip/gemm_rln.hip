@@ -114,7 +114,12 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 3); }
 // EPI 0: residual added in the epilogue (8-B loads); 1: LDS-staged epilogue; 2: the residual is
 // the first K step -- one MFMA per tile against an identity operand (acc = I . R, exact: 1.0 x a
 // bf16 value) with R fragments loaded in the prologue beside the first stages, so the epilogue
-// reads nothing.  PF: W fragment pairs read PF pairs ahead of their MFMAs.
+// reads nothing.  3 (K = 768, the o-proj): the residual is added during the K loop -- stage t
+// loads the lane's residual pieces of two of its 48 (m-tile, n-tile) accumulator tiles, stage t + 1
+// adds them -- so the epilogue only normalises and stores: the residual's 50 MB at M = 32768 no
+// longer arrive while every workgroup sits in its epilogue (o-proj 64.4 -> 58.9 us; the down
+// projection, K = 3072, lost 3 % with it: profiles/r4aq).  PF: W fragment pairs read PF pairs
+// ahead of their MFMAs.
 // AS: the K-loop's LDS-DMAs issued from inline asm (glds_asm.hpp: counted lgkmcnt before the MFMAs)
 // ROT: block b walks the K steps starting at step b mod nk (the sum is order-free up to fp32 rounding), so
 // the 256 blocks that start together fetch different W stages instead of all hitting the same L2 lines
@@ -132,6 +137,7 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
   constexpr int RW = kBM / WM, MT = RW / 16;           // rows and m-tiles per wave
   constexpr int GA = 8 / kWaves, GW = 48 / kWaves;     // LDS-DMA wave-instructions per wave per stage
   static_assert(EPI == 0 || WM == 2, "the LDS-staged epilogue splits the tile by wave rows");
+  static_assert(EPI != 3 || MT * kNT == 48, "EPI 3 spreads 48 accumulator tiles over 24 stages");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = WM == 2 ? wave >> 2 : 0, wn = wave & 3;
@@ -240,9 +246,40 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
       for (int j = 0; j < kNT; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     for (int s = -L; s < 0; ++s) issue(s);
   }
+  // EPI 3: residual pieces of accumulator tile u = (u / kNT, u % kNT), two tiles per stage
+  const long rmb = m0 + wr * RW + (lane & 15);
+  const int rcq = (lane >> 4) * 4;
+  uint2 rq[2] = {make_uint2(0, 0), make_uint2(0, 0)};
+  auto res_load = [&](int u, uint2& d) {
+    const int i = u / kNT, j = u % kNT;
+    const long m = rmb + 16 * i < M ? rmb + 16 * i : M - 1;
+    d = *(const uint2*)(res + m * ldr + wn * kWN + j * 16 + rcq);
+  };
+  auto res_add = [&](int u, const uint2& rr) {
+    const int i = u / kNT, j = u % kNT;
+    acc[i][j][0] += bf2f(rr.x & 0xffff);
+    acc[i][j][1] += bf2f(rr.x >> 16);
+    acc[i][j][2] += bf2f(rr.y & 0xffff);
+    acc[i][j][3] += bf2f(rr.y >> 16);
+  };
   for (int t = 0; t < nk; ++t) {
     wait_vm(younger(t));
     raw_barrier();  // stage t visible to every wave; every wave is done with stage t-1's slots
+    if constexpr (EPI == 3) {
+      // loaded one stage ahead of their add, issued before this stage's DMAs (older than them: the
+      // counted waits above stay exact); a chain of uniform branches keeps the tile indices static
+#pragma unroll
+      for (int k = 0; k < 24; ++k) {
+        if (t == k) {
+          if (k > 0) {
+            res_add(2 * (k - 1), rq[0]);
+            res_add(2 * (k - 1) + 1, rq[1]);
+          }
+          res_load(2 * k, rq[0]);
+          res_load(2 * k + 1, rq[1]);
+        }
+      }
+    }
     if (ILV == 0) issue(t);
     const char* bw = smem + (t % NW) * kWBytes;
     const char* ba = smem + (t % NA) * kABytes;
@@ -290,6 +327,10 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
 #pragma unroll
       for (int u = (kNT / 2) * ILV; u < kOps; ++u) issue_op(t, u);
     }
+  }
+  if constexpr (EPI == 3) {  // the last pair (the host runs EPI 3 at exactly 24 stages)
+    res_add(46, rq[0]);
+    res_add(47, rq[1]);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   raw_barrier();  // every wave is done with the rings: the LDS is the epilogue's
@@ -489,14 +530,16 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
   }
 }
 
-// Two selectable forms (NOMIC_RLN): 222 = PIPE 2 (3 W stages, 2 A stages), DMA interleave 2
-// (default, profiles/r3_rln_variants_ab.jsonl) and 220 = the same without the interleave (fallback).
-// The other A/B forms of round 3 are gone; their measurements stay in profiles/r3_rln_*.
+// Two selectable forms (NOMIC_RLN): 232 (default) = PIPE 2 (3 W stages, 2 A stages), DMA
+// interleave 2, and at K = 768 the residual added during the K loop (EPI 3, profiles/r4aq); 222 =
+// the same with the residual always added in the epilogue (fallback, the round-3 default).  The
+// other A/B forms of round 3 are gone; their measurements stay in profiles/r3_rln_*.
 int g_rln_variant = -1;
+int rln_pick(int v) { return v == 222 ? 222 : 232; }
 int rln_variant() {
   if (g_rln_variant < 0) {
     const char* e = getenv("NOMIC_RLN");
-    g_rln_variant = e && *e && atoi(e) == 220 ? 220 : 222;
+    g_rln_variant = rln_pick(e && *e ? atoi(e) : 232);
   }
   return g_rln_variant;
 }
@@ -535,13 +578,13 @@ extern "C" int nomic_gemm_res_ln(const void* A, long lda, const void* W, long ld
   const auto* g = (const uint16_t*)gamma;
   const auto* b = (const uint16_t*)beta;
   auto* o = (uint16_t*)out;
-  if (rln_variant() == 220) launch_rln<2, 0, 2, 1>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
+  if (rln_variant() == 232 && K / kBK == 24) launch_rln<2, 3, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
   else launch_rln<2, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
   return (int)hipGetLastError();
 }
 
 extern "C" int nomic_gemm_res_ln_set_variant(int variant) {
   const int prev = rln_variant();
-  g_rln_variant = variant == 220 ? 220 : 222;
+  g_rln_variant = rln_pick(variant);
   return prev;
 }

@@ -117,8 +117,8 @@ __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 3); }
 // reads nothing.  3 (K = 768, the o-proj): the residual is added during the K loop -- stage t
 // loads the lane's residual pieces of two of its 48 (m-tile, n-tile) accumulator tiles, stage t + 1
 // adds them -- so the epilogue only normalises and stores: the residual's 50 MB at M = 32768 no
-// longer arrive while every workgroup sits in its epilogue (o-proj 64.4 -> 58.9 us; the down
-// projection, K = 3072, lost 3 % with it: profiles/r4aq).  PF: W fragment pairs read PF pairs
+// longer arrive while every workgroup sits in its epilogue (o-proj 62.6 -> 56.3 us; the down
+// projection, K = 3072, gains nothing from it: 146.3 vs 147.1 us, profiles/r4aq).  PF: W fragment pairs read PF pairs
 // ahead of their MFMAs.
 // AS: the K-loop's LDS-DMAs issued from inline asm (glds_asm.hpp: counted lgkmcnt before the MFMAs)
 // ROT: block b walks the K steps starting at step b mod nk (the sum is order-free up to fp32 rounding), so
@@ -265,7 +265,7 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
   for (int t = 0; t < nk; ++t) {
     wait_vm(younger(t));
     raw_barrier();  // stage t visible to every wave; every wave is done with stage t-1's slots
-    if constexpr (EPI == 3) {
+    if (EPI == 3 && t < 24) {
       // loaded one stage ahead of their add, issued before this stage's DMAs (older than them: the
       // counted waits above stay exact); a chain of uniform branches keeps the tile indices static
 #pragma unroll
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(256 * WM, 1) void k_gemm_rln(const uint16_t* __rest
       for (int u = (kNT / 2) * ILV; u < kOps; ++u) issue_op(t, u);
     }
   }
-  if constexpr (EPI == 3) {  // the last pair (the host runs EPI 3 at exactly 24 stages)
+  if constexpr (EPI == 3) {  // the last pair (loaded at stage 23)
     res_add(46, rq[0]);
     res_add(47, rq[1]);
   }
@@ -578,7 +578,7 @@ extern "C" int nomic_gemm_res_ln(const void* A, long lda, const void* W, long ld
   const auto* g = (const uint16_t*)gamma;
   const auto* b = (const uint16_t*)beta;
   auto* o = (uint16_t*)out;
-  if (rln_variant() == 232 && K / kBK == 24) launch_rln<2, 3, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
+  if (rln_variant() == 232 && K / kBK >= 24 && K <= 768) launch_rln<2, 3, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
   else launch_rln<2, 0, 2, 2>(blocks, s, a, lda, w, ldw, K, M, r, ldr, g, b, eps, o, ldo);
   return (int)hipGetLastError();
 }

@@ -243,9 +243,12 @@ __device__ __forceinline__ rsrc_t tile_rsrc(const spl::dev::Arena& a, long t, lo
   return __builtin_amdgcn_make_buffer_rsrc(a.slot((size_t)tile_start(t, slot_end)), 0, kTile * 3200, kRsrcWord3);
 }
 
-// swizzle of the 16-B units of a 128-B row: conflict-free 8-lane phases of
-// the fragment reads (rows r..r+7, same unit)
-__device__ __forceinline__ int swz(int row) { return ((row >> 1) & 3) << 1; }
+// swizzle of the 16-B units of a 128-B row (unit bit 0 ^= row bit 2, unit bit 2 ^= row bit 1):
+// every gfx950 ds_read_b128 lane group of the fragment reads (16 lanes, rows fr = 0..15 of one or
+// two logical units) hits 16 distinct bank slots.  ((row >> 1) & 3) << 1, right for 8-lane phases,
+// left the 16-lane groups 2-way conflicted (48.7 % LDS conflict rate, profiles/r4au); the pass time
+// did not move with it (20.2 vs 19.9-20.0 ms, profiles/r4av): the LDS is not what bounds it.
+__device__ __forceinline__ int swz(int row) { return ((row >> 2) & 1) | (((row >> 1) & 1) << 2); }
 
 __device__ __forceinline__ bf16x8 load_qfrag(rsrc_t r, int voff, int qtile, int step) {
   return __builtin_bit_cast(bf16x8, __builtin_amdgcn_raw_buffer_load_b128(r, voff, (qtile * kSteps + step) * 1024, 0));

@@ -579,13 +579,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
 }
 
 // ------------------------------------------------------------ mean pool --
-__global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, const int32_t* __restrict__ cu,
+// One block per document of 16 waves (a document's rows in flight across 16 waves x 4 unrolled
+// rows: with 4 waves the 64 blocks of a 64-document batch waited on one row load at a time, 45 us)
+constexpr int kPoolWaves = 16, kPoolThreads = 64 * kPoolWaves;
+__global__ __launch_bounds__(kPoolThreads) void k_pool(const uint16_t* __restrict__ x, const int32_t* __restrict__ cu,
                                               float* __restrict__ pooled, int normalize, spl_arena_t aa,
                                               const int64_t* __restrict__ slots, const uint64_t* __restrict__ hashes,
                                               int32_t* __restrict__ status) {
-  __shared__ float part[4][D];
+  __shared__ float part[kPoolWaves][D];
   __shared__ float vec[D];
-  __shared__ float red[4];
+  __shared__ float red[kPoolWaves];
   __shared__ int lock_ok;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const long t0 = cu[b], t1 = cu[b + 1];
@@ -593,7 +596,8 @@ __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, co
 #pragma unroll
   for (int e = 0; e < 12; ++e) acc[e] = 0.f;
   // lane covers columns [lane*8, +8) and [512 + lane*4, +4)
-  for (long t = t0 + wave; t < t1; t += 4) {
+#pragma unroll 4
+  for (long t = t0 + wave; t < t1; t += kPoolWaves) {
     const uint16_t* row = x + t * D;
     float f[8];
     unpack8(*(const uint4*)(row + lane * 8), f);
@@ -610,8 +614,11 @@ __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, co
   __syncthreads();
   const float inv = t1 > t0 ? 1.f / (float)(t1 - t0) : 0.f;
   float ss = 0.f;
-  for (int c = tid; c < D; c += 256) {
-    const float v = (part[0][c] + part[1][c] + part[2][c] + part[3][c]) * inv;
+  for (int c = tid; c < D; c += kPoolThreads) {
+    float v = 0.f;
+#pragma unroll
+    for (int w = 0; w < kPoolWaves; ++w) v += part[w][c];
+    v *= inv;
     vec[c] = v;
     ss += v * v;
   }
@@ -620,9 +627,13 @@ __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, co
     if (lane == 0) red[wave] = ss;
   }
   __syncthreads();
-  const float scale = normalize ? rsqrtf(fmaxf(red[0] + red[1] + red[2] + red[3], 1e-24f)) : 1.f;
+  float rs = 0.f;
+  if (normalize)
+#pragma unroll
+    for (int w = 0; w < kPoolWaves; ++w) rs += red[w];
+  const float scale = normalize ? rsqrtf(fmaxf(rs, 1e-24f)) : 1.f;
   if (pooled)
-    for (int c = tid; c < D; c += 256) pooled[(long)b * D + c] = vec[c] * scale;
+    for (int c = tid; c < D; c += kPoolThreads) pooled[(long)b * D + c] = vec[c] * scale;
   if (!slots) return;
   // fused write-back into the arena slot (seqlock), reference set_embedding
   // semantics (/root/reference/splinter.c:567-588): CAS even->odd, copy, +1.
@@ -649,7 +660,7 @@ __global__ __launch_bounds__(256) void k_pool(const uint16_t* __restrict__ x, co
   __syncthreads();
   if (lock_ok == 1) {
     float* dst = (float*)(a.slot((size_t)si) + kOffEmbed);
-    for (int c = tid; c < D; c += 256) dst[c] = vec[c] * scale;
+    for (int c = tid; c < D; c += kPoolThreads) dst[c] = vec[c] * scale;
     release();
     __syncthreads();
     if (tid == 0) {
@@ -819,8 +830,8 @@ int dec_attn_prefill(const void* qkv, void* out, const int32_t* cu, const int32_
 int nomic_mean_pool(const void* x, const int32_t* cu, int B, float* pooled, int normalize, spl_arena_t arena,
                     const int64_t* slots, const uint64_t* hashes, int32_t* status, hipStream_t s) {
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(k_pool, dim3(B), dim3(256), 0, s, (const uint16_t*)x, cu, pooled, normalize, arena, slots, hashes,
-                     status);
+  hipLaunchKernelGGL(k_pool, dim3(B), dim3(kPoolThreads), 0, s, (const uint16_t*)x, cu, pooled, normalize, arena, slots,
+                     hashes, status);
   return (int)hipGetLastError();
 }
 

@@ -107,8 +107,17 @@ def parse():
                    help="after the timed loop, embed this many pending VARTEXT documents of an hbm: store through "
                         "the splinference daemon's own code path (Splinference.process: batched read, WordPiece, "
                         "encoder, vectors pooled into the slots, +2 epoch check, label updates), per rank; 0 = skip")
-    p.add_argument("--routed-steps", type=int, default=10,
-                   help="N=1: also time this many steps of the routed (N>1) step on one GPU -> routed_kv_ops_per_s")
+    p.add_argument("--exchange-ab", type=int, default=1, choices=[0, 1],
+                   help="N=1: after everything else, time the routed exchange honestly in FRESH child processes on "
+                        "this GPU: a 2-rank run (both ranks on this device, peer-window transport, gloo for the small "
+                        "collectives) and a 1-rank run at identical totals (--exchange-keys keys, --exchange-batch ops "
+                        "per step in all) -> exchange_2rank_ops_per_s / exchange_1rank_ops_per_s / exchange_ratio")
+    p.add_argument("--exchange-keys", type=int, default=40_000_000, help="total keys of the exchange A/B runs")
+    p.add_argument("--exchange-batch", type=int, default=8_000_000, help="total ops per step of the exchange A/B runs")
+    p.add_argument("--mixed5", type=int, default=10, metavar="STEPS",
+                   help="after the timed loop, time STEPS config-#5 mixed steps (embed a batch -> its vectors "
+                        "inserted into the search arena's slots -> a batched top-10 query of --search-queries "
+                        "queries over the whole arena, built from the vectors just written); 0 = skip")
     return p.parse_args()
 
 
@@ -204,6 +213,55 @@ def daemon_run(enc, docs: int, seq: int, rank: int, world: int, routed: bool, no
         unlink(name)
 
 
+def exchange_ab(args, dev: int, log):
+    """The routed exchange measured against the native step at identical totals, on this GPU, in fresh
+    child processes (subprocess, never exec): (a) 2 ranks, both on this device (peer-window transport,
+    gloo for the small collectives), keys and ops split between them; (b) 1 rank with every key and op.
+    Both KV-only, hybrid mop, same value size.  Returns ops/s of each, their ratio, the transport rank 0
+    of (a) settled on and why it fell back if it did, and the integrity failures of both runs."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    # pin both children to THIS physical device (on an 8-GPU node the 2-rank run would otherwise
+    # spread over two GPUs: a different comparison)
+    vis = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
+    phys = vis.split(",")[dev] if vis else str(dev)
+    env["HIP_VISIBLE_DEVICES"] = phys
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    common = ["--mode", "kv", "--steps", "10", "--warmup", "3", "--host-api", "0", "--host-api-threads2", "0",
+              "--embed-e2e", "0", "--daemon-docs", "0", "--search-keys", "0", "--exchange-ab", "0", "--mixed5", "0",
+              "--verify", "5000", "--value-len", str(args.value_len), "--mop", str(args.mop)]
+    me = os.path.abspath(__file__)
+    runs = {}
+    for w in (2, 1):
+        cmd = [sys.executable, me, "--gpus", str(w), "--keys-per-gpu", str(args.exchange_keys // w),
+               "--batch", str(args.exchange_batch // w)] + common
+        if w > 1:
+            cmd += ["--backend", "gloo", "--transport", "peer"]
+        try:
+            r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        except subprocess.TimeoutExpired:
+            log(f"[bench] exchange A/B: {w}-rank child timed out")
+            return None
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not line:
+            log(f"[bench] exchange A/B: {w}-rank child failed (rc {r.returncode}): {r.stderr[-600:]}")
+            return None
+        runs[w] = json.loads(line[-1])
+        log(f"[bench] exchange A/B: {w} rank(s) {runs[w]['value'] / 1e9:.3f} G ops/s, "
+            f"{runs[w]['ms_per_step']:.2f} ms/step, integrity {runs[w]['integrity_failures']}")
+    coll = runs[2]["config"].get("collectives") or ""
+    transport = "peer" if "transport peer" in coll else ("rccl" if "transport rccl" in coll else coll)
+    fb = coll.split("(fell back: ", 1)[1].split(")", 1)[0] if "(fell back: " in coll else None
+    return {"ops2": runs[2]["value"], "ops1": runs[1]["value"], "ratio": runs[2]["value"] / runs[1]["value"],
+            "transport": transport, "fallback": fb,
+            "integrity": runs[2]["integrity_failures"] + runs[1]["integrity_failures"],
+            "totals": {"keys": args.exchange_keys, "ops_per_step": args.exchange_batch, "steps": 10,
+                       "device": phys, "mode": "kv"}}
+
+
 def main():
     args = parse()
     # Hardware queues per priority level for this process (HIP default 4).  Each HIP stream the
@@ -242,7 +300,7 @@ def main():
         return
 
     routed = world > 1 or args.force_routed
-    need_routed = routed or (args.routed_steps > 0 and args.mode != "embed")
+    need_routed = routed
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dev = local % max(torch.cuda.device_count(), 1)
@@ -393,6 +451,20 @@ def main():
         g_status = torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")
         g_lens = torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")
 
+    # what actually launches the KV work of a step (reported in the JSON config)
+    if kvs is not None and int(os.environ.get("SPL_KVS_FUSED", "2")) != 0:
+        kv_launch = {"writer_streams": 1, "reader_streams": 1, "launches": 1,
+                     "how": f"fused: ONE grid (k_kv_fused) consumes all {len(set_parts)} set + {len(get_parts)} get "
+                            "client slices, launched on one stream"}
+    elif kvs is not None:
+        kv_launch = {"writer_streams": len(set_parts), "reader_streams": len(get_parts),
+                     "launches": len(set_parts) + len(get_parts),
+                     "how": "per slice: one launch per client slice, each on its own stream (SPL_KVS_FUSED=0)"}
+    else:
+        kv_launch = {"writer_streams": len(set_parts), "reader_streams": len(get_parts),
+                     "launches": len(set_parts) + len(get_parts),
+                     "how": "python client streams, one arena.set / arena.get launch per slice"}
+
     _phase_gap_ms = float(os.environ.get("BENCH_PHASE_GAP_MS", "0"))
     s_kvo = hip_stream("low") if (args.overlap_native and kvs is not None and embedder is not None
                                   and world == 1) else None
@@ -404,6 +476,21 @@ def main():
     # runs the encoder (profiles/r2_hw_queues.md), so submitting early costs more than the few
     # microseconds of launch latency it hides.
     throttle_ev = [None]
+    # encoder phase bracketed by events inside the timed steps (no host sync): its own time per step,
+    # so encoder TFLOP/s is quoted over encoder time, not over the mixed step
+    emb_events = []
+    timing_emb = [False]
+
+    def run_embed():
+        if timing_emb[0]:
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record()
+            embedder.run()
+            e1.record()
+            emb_events.append((e0, e1))
+        else:
+            embedder.run()
 
     def step_local(i):
         SK, SV, SL, GK, _ = batches[i % nbuf]
@@ -438,7 +525,7 @@ def main():
                 torch.cuda.synchronize()
                 time.sleep(_phase_gap_ms / 1e3)
             if s_emb is None:
-                embedder.run()
+                run_embed()
             else:
                 s_emb.wait_stream(cur)
                 with torch.cuda.stream(s_emb):
@@ -505,7 +592,7 @@ def main():
             ev_exec = s_set.record_event()
         if embedder is not None:
             cur.wait_event(ev_exec)
-            embedder.run()
+            run_embed()
             if args.throttle:
                 throttle_ev[0] = cur.record_event()
         s_resp.wait_event(ev_exec)
@@ -531,6 +618,7 @@ def main():
     torch.cuda.synchronize()
     prof = _timed_region_profiler()
     prof(True)
+    timing_emb[0] = True
     t_start = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i, last=i == args.steps - 1) if routed else step(args.warmup + i)
@@ -539,6 +627,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t_start
     prof(False)
+    timing_emb[0] = False
+    emb_phase_ms = (sum(a.elapsed_time(b) for a, b in emb_events) / len(emb_events)) if emb_events else None
     t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
     st = stats.clone()
     if routed:
@@ -547,21 +637,15 @@ def main():
     elapsed = t.item()
     attempts, ok, again, miss = [int(x) for x in st.tolist()]
 
-    # ---- integrity: sampled gets must parse and match their key ----------
-    integrity_fail = 0
-    if args.verify and n_get:
-        GK, gid = batches[0][3], batches[0][4]
-        m = min(args.verify, n_get)
-        if routed:
-            sts, outv, lens = kv.get(GK[:m])
-        else:
-            sts, outv, lens = arena.get(GK[:m])
-        o, ln, ids, s_ = outv.cpu().numpy(), lens.cpu().numpy(), gid[:m].cpu().numpy(), sts.cpu().numpy()
-        bad_status: dict = {}
-        for i in range(m):
+    # ---- integrity: the LAST timed step's own get outputs, sampled over the whole batch, must
+    # parse and carry their key's id with a consistent fill (the 'ver:|id:|data:' format is
+    # version-independent: any version a racing set wrote is valid), and its sets must have landed
+    def check_rows(s_, o, ln, ids, what):
+        fails, kinds = 0, {}
+        for i in range(len(ids)):
             if s_[i] != 0:
-                integrity_fail += 1
-                bad_status[int(s_[i])] = bad_status.get(int(s_[i]), 0) + 1
+                fails += 1
+                kinds[int(s_[i])] = kinds.get(int(s_[i]), 0) + 1
                 continue
             v = bytes(o[i, : ln[i]])
             try:
@@ -570,35 +654,52 @@ def main():
                 ident = int(rest.split(b"|", 1)[0])
                 fill = v[v.index(b"data:") + 5:]
                 if ident != ids[i] or fill != bytes([65 + ver % 26]) * len(fill):
-                    integrity_fail += 1
-                    bad_status["content"] = bad_status.get("content", 0) + 1
-                    if bad_status["content"] <= 3:
-                        log(f"[bench] bad value for id {ids[i]} (len {ln[i]}): {v[:60]!r}...{v[-20:]!r}")
+                    fails += 1
+                    kinds["content"] = kinds.get("content", 0) + 1
+                    if kinds["content"] <= 3:
+                        log(f"[bench] {what}: bad value for id {ids[i]} (len {ln[i]}): {v[:60]!r}...{v[-20:]!r}")
             except Exception:
-                integrity_fail += 1
-                bad_status["parse"] = bad_status.get("parse", 0) + 1
-                if bad_status["parse"] <= 3:
-                    log(f"[bench] unparsable value for id {ids[i]} (len {ln[i]}): {v[:60]!r}...{v[-20:]!r}")
-        if bad_status and rank == 0:
-            log(f"[bench] integrity failures by kind (rank 0): {bad_status}")
-        if routed:
-            x = torch.tensor([integrity_fail], device="cuda")
-            dist.all_reduce(x)
-            integrity_fail = int(x.item())
+                fails += 1
+                kinds["parse"] = kinds.get("parse", 0) + 1
+                if kinds["parse"] <= 3:
+                    log(f"[bench] {what}: unparsable value for id {ids[i]} (len {ln[i]}): {v[:60]!r}...{v[-20:]!r}")
+        if kinds:
+            log(f"[bench] {what}: integrity failures by kind (rank {rank}): {kinds}")
+        return fails
 
-    # ---- N=1: the routed (N>1) step on one GPU, same streams and batches (outside the headline) ----
-    routed1 = None
-    if not routed and xr is not None and args.routed_steps > 0:
-        throttle_ev[0] = None
-        for i in range(2):
-            step_routed(i, last=i == 1)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i in range(args.routed_steps):
-            step_routed(2 + i, last=i == args.routed_steps - 1)
-        torch.cuda.synchronize()
-        dtr = time.perf_counter() - t0
-        routed1 = {"ops_per_s": (n_set + n_get) * args.routed_steps / dtr, "ms_per_step": dtr / args.routed_steps * 1e3}
+    integrity_fail = integrity_rows = timed_set_fail = 0
+    integrity_source = None
+    last = args.warmup + args.steps - 1
+    if args.verify and n_get:
+        gid_last = batches[last % nbuf][4]
+        m = min(args.verify, n_get)
+        sel = torch.linspace(0, n_get - 1, m, device="cuda").long()
+        timed = None
+        if routed and xr is not None:
+            sst_l, gov_l, gln_l, gst_l = r_out[last % 2]
+            timed = (gst_l, gov_l, gln_l, sst_l)
+        elif kvs is not None:
+            timed = (g_status, gout, g_lens, s_status)
+        if timed is not None:
+            gs, go, gl, ss = timed
+            integrity_fail = check_rows(gs[sel].cpu().numpy(), go[sel].cpu().numpy(), gl[sel].cpu().numpy(),
+                                        gid_last[sel].cpu().numpy(), "timed gets")
+            timed_set_fail = int((ss[:n_set] != 0).sum().item()) if n_set else 0
+            integrity_rows = m
+            integrity_source = (f"the last timed step's own get outputs ({m} of {n_get} rows, strided over the "
+                                f"batch) + every status of its {n_set} sets")
+        else:  # python-stream fallback paths keep no statuses: fresh gets of that step's keys
+            GK = batches[last % nbuf][3]
+            sts, outv, lens = (kv.get if routed else arena.get)(GK[sel])
+            integrity_fail = check_rows(sts.cpu().numpy(), outv.cpu().numpy(), lens.cpu().numpy(),
+                                        gid_last[sel].cpu().numpy(), "fresh gets")
+            integrity_rows = m
+            integrity_source = f"fresh gets of the last timed step's keys ({m} rows)"
+        if routed:
+            x = torch.tensor([integrity_fail, timed_set_fail, integrity_rows], device="cuda")
+            dist.all_reduce(x)
+            integrity_fail, timed_set_fail, integrity_rows = [int(v) for v in x.tolist()]
+
 
     # ---- per-call C API (outside the timed region): splinter_set / splinter_get from host threads
     # through the device command ring of an hbm: store (tools/splinter_hostapi_bench.cpp)
@@ -679,13 +780,58 @@ def main():
         search = {"qps": args.search_queries * args.search_batches / dt, "ms_per_batch": dt / args.search_batches * 1e3,
                   "recall_at_10": recall, "keys_total": args.search_keys * world}
 
+    # ---- config #5 mixed steps: embed a batch -> its vectors inserted into the search arena's slots
+    # (the pooling kernel's seqlocked slot write) -> a batched top-10 query over the whole arena with
+    # queries built from the vectors just written (each must find its own document first) -------
+    mixed5 = None
+    if sarena is not None and embedder is not None and args.mixed5 > 0 and args.search_queries > 0:
+        skv5 = ShardedKV(GpuShard(sarena))
+        nq = args.search_queries
+        gq5 = torch.Generator(device="cuda")
+        gq5.manual_seed(99)
+        noise = torch.randn((nq, 768), device="cuda", generator=gq5)
+        pick = torch.arange(nq, device="cuda") % embedder.docs_per_step
+
+        def step5():
+            vec, _ = embedder.run()  # [docs, 768] fp32, also written into the documents' slots
+            v = vec[pick]
+            q = v + (0.01 / 768 ** 0.5) * v.norm(dim=1, keepdim=True) * noise  # ~1 % perturbation
+            return skv5.search(q, k=10)
+
+        step5()  # warm-up
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.mixed5):
+            res5 = step5()
+        torch.cuda.synchronize()
+        t5 = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device="cuda")
+        if world > 1:
+            dist.all_reduce(t5, op=dist.ReduceOp.MAX)
+        dt5 = t5.item()
+        # the last step's top-1 of every query must be the document its query was built from
+        keys5 = res5[3][:, 0].cpu().numpy()
+        want = embedder.keys[pick].cpu().numpy()
+        hit = float(sum(bytes(a).split(b"\0", 1)[0] == bytes(b).split(b"\0", 1)[0] for a, b in zip(keys5, want)))
+        mixed5 = {"ms_per_step": dt5 / args.mixed5 * 1e3, "qps": nq * args.mixed5 * world / dt5,
+                  "vectors_per_s": embedder.docs_per_step * args.mixed5 * world / dt5, "self_top1": hit / nq}
+
+    # ---- honest exchange measurement on this one GPU (N=1 only, after everything else): fresh child
+    # processes, never exec -- a 2-rank KV-only run with both ranks on this device (peer windows; gloo
+    # for the small collectives) and a 1-rank run at identical totals
+    xab = None
+    if world == 1 and args.exchange_ab and args.mode != "embed":
+        xab = exchange_ab(args, dev, log)
+
     kv_ops = (n_set + n_get) * args.steps * world
     kv_ops_s = kv_ops / elapsed if kv_ops else 0.0
-    emb_vps = emb_tps = emb_tflops = None
+    emb_vps = emb_tps = enc_tflops = None
     if embedder is not None:
         emb_vps = embedder.docs_per_step * args.steps * world / elapsed
         emb_tps = embedder.tokens_per_step * args.steps * world / elapsed
-        emb_tflops = embedder.flops_per_step * args.steps * world / elapsed / 1e12
+        if emb_phase_ms:  # encoder FLOPs over the encoder phase's own (event-timed) time
+            enc_tflops = embedder.flops_per_step / (emb_phase_ms * 1e-3) / 1e12
     value = kv_ops_s if args.mode != "embed" else emb_vps
     res = {
         "metric": "KV set/get ops/sec + Nomic-768d embed vectors/sec at 1/2/4/8 MI355X",
@@ -708,9 +854,15 @@ def main():
             "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
             "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),
             "mode": args.mode, "phases": "overlapped" if s_kvo is not None else "serial", "mop": args.mop, "value_len": args.value_len,
-            "writer_streams": nw, "reader_streams": nr,
+            # how the step's KV work is submitted: the batch is split into --writer-streams set slices and
+            # --reader-streams get slices (the config's concurrent clients); in the default fused mode ONE
+            # grid consumes every slice from one stream, so the streams that actually launch are counted here
+            "client_slices": {"writer": nw, "reader": nr},
+            "writer_streams": kv_launch["writer_streams"], "reader_streams": kv_launch["reader_streams"],
+            "kv_launches_per_step": kv_launch["launches"], "kv_submission": kv_launch["how"],
             "hw_queues_per_priority": int(os.environ["GPU_MAX_HW_QUEUES"]),
-            "collectives": (f"routed exchange, transport {xr.transport}: request / response rows "
+            "collectives": (f"routed exchange, transport {xr.transport}"
+                            + (f" (fell back: {xr.fallback_reason})" if xr.fallback_reason else "") + ": request / response rows "
                             + ("stored into the owners' peer-mapped windows over xGMI, "
                                if xr.transport == "peer" else "moved by one all-to-all per direction, ")
                             + "one count all-to-all + one response all-to-all per step") if routed and xr else None,
@@ -731,10 +883,14 @@ def main():
         "embed_e2e_ms_per_batch": e2e["ms_per_batch"] if e2e else None,
         "embed_e2e_tokens_per_batch": e2e["tokens_per_batch"] if e2e else None,
         "embed_e2e_write_failures": e2e["write_failures"] if e2e else None,
-        "embed_tflops": emb_tflops,
+        "embed_phase_ms_per_step": emb_phase_ms,
+        "encoder_tflops": enc_tflops,
         "kv_attempts": attempts, "kv_ok": ok, "kv_eagain_retries": again, "kv_miss": miss,
         "successful_ops_per_s": ok / elapsed if elapsed else 0.0,
         "integrity_failures": integrity_fail,
+        "integrity_rows_checked": integrity_rows,
+        "integrity_source": integrity_source,
+        "timed_set_failures": timed_set_fail,
         "host_api_threads": args.host_api if host_api else None,
         "host_api_ops_per_s": host_api["ops_per_s"] if host_api else None,
         "host_api_p50_us": host_api["p50_us"] if host_api else None,
@@ -742,8 +898,18 @@ def main():
         "host_api_threads2": args.host_api_threads2 if host_api2 else None,
         "host_api2_ops_per_s": host_api2["ops_per_s"] if host_api2 else None,
         "host_api2_p50_us": host_api2["p50_us"] if host_api2 else None,
-        "routed_kv_ops_per_s": routed1["ops_per_s"] if routed1 else (kv_ops_s if routed else None),
-        "routed_ms_per_step": routed1["ms_per_step"] if routed1 else None,
+        "routed_kv_ops_per_s": kv_ops_s if routed else None,
+        "exchange_2rank_ops_per_s": xab["ops2"] if xab else None,
+        "exchange_1rank_ops_per_s": xab["ops1"] if xab else None,
+        "exchange_ratio": xab["ratio"] if xab else None,
+        "exchange_transport": xab["transport"] if xab else None,
+        "exchange_fallback_reason": xab["fallback"] if xab else None,
+        "exchange_integrity_failures": xab["integrity"] if xab else None,
+        "exchange_totals": xab["totals"] if xab else None,
+        "mixed5_ms_per_step": mixed5["ms_per_step"] if mixed5 else None,
+        "mixed5_qps": mixed5["qps"] if mixed5 else None,
+        "mixed5_vectors_per_s": mixed5["vectors_per_s"] if mixed5 else None,
+        "mixed5_self_top1": mixed5["self_top1"] if mixed5 else None,
         "daemon_vectors_per_s": daemon["vectors_per_s"] if daemon else None,
         "daemon_docs_embedded": daemon["embedded"] if daemon else None,
         "daemon_docs_expected": daemon["expected"] if daemon else None,

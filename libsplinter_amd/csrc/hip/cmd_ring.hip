@@ -678,12 +678,15 @@ void CmdRing::read_env() {
   first_sleep_ns_ = env_int("SPLINTER_RING_FIRST_SLEEP_NS", 6000);
   oversub_spin_us_ = (uint64_t)env_int("SPLINTER_RING_OVERSUB_SPIN_US", 0);
   adaptive_ = env_int("SPLINTER_RING_ADAPTIVE_SLEEP", 1) != 0;
-  // SPLINTER_RING_GROUPS: worker waves (1..32, a power of two; entries per wave = 256 / groups).  Each
-  // resident worker wave (233 VGPRs) keeps the encoder's 2-wave-per-SIMD GEMM workgroups off its CU
+  // SPLINTER_RING_GROUPS: worker waves (4..32, a power of two; entries per wave = 256 / groups: a
+  // wave's 64 lanes serve at most 64 entries, so fewer than 4 waves would leave entries unserved and
+  // their calls would time out).  Each resident worker wave (233 VGPRs) keeps the encoder's
+  // 2-wave-per-SIMD GEMM workgroups off its CU
   int g = env_int("SPLINTER_RING_GROUPS", kDefaultRingGroups);
-  int p2 = 1;
+  int p2 = kRingMinGroups;
   while (p2 * 2 <= g && p2 < kRingGroups) p2 *= 2;
-  groups_ = g < 1 ? 1 : p2;
+  groups_ = p2;
+  static_assert(kRingEntries / kRingMinGroups <= 64, "one lane per entry");
 }
 
 // Host-side buffers of a private ring: pinned, coherent, device-mapped (host view == device view).
@@ -832,7 +835,15 @@ void CmdRing::supervise() {
     const uint32_t w = __atomic_load_n(&seg_->want, __ATOMIC_ACQUIRE);
     if (w == seen || sup_stop_.load(std::memory_order_acquire)) continue;
     seen = w;
-    std::shared_lock<std::shared_mutex> gate(g_gate);  // not while this process sets up a store
+    // not while this process sets up or tears down a store (it holds the gate exclusive); poll for the
+    // gate instead of blocking on it, so a teardown that joins this thread never waits on a supervisor
+    // that waits on the teardown's gate
+    std::shared_lock<std::shared_mutex> gate(g_gate, std::defer_lock);
+    while (!gate.try_lock()) {
+      if (sup_stop_.load(std::memory_order_acquire)) break;
+      usleep(200);
+    }
+    if (!gate.owns_lock()) continue;
     if (!__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) launch(arena_);
   }
 }
@@ -891,10 +902,19 @@ int CmdRing::init_client(const std::string& seg, int device, uint32_t pstride) {
   waiters_ = &seg_->waiters;
   device_ = device;
   read_env();
-  if (seg_->groups >= 1 && seg_->groups <= (uint32_t)kRingGroups) groups_ = (int)seg_->groups;
+  if (seg_->groups >= (uint32_t)kRingMinGroups && seg_->groups <= (uint32_t)kRingGroups) groups_ = (int)seg_->groups;
   vr_ = true;
   mode_ = kClient;
   return 0;
+}
+
+void CmdRing::stop_supervisor() {
+  if (mode_ != kServer) return;
+  sup_stop_.store(true, std::memory_order_release);
+  if (sup_.joinable()) {
+    want_worker();
+    sup_.join();
+  }
 }
 
 bool CmdRing::server_gone() const {
@@ -941,7 +961,9 @@ int CmdRing::init_vram() {
 void CmdRing::launch(const spl_arena_t& a) {
   std::lock_guard<std::mutex> lk(launch_mu_);
   if (mode_ == kPrivate) arena_ = a;  // (for resume)
+  if (!a.base) return;  // no arena mapped in this process (a lazily attached client): nothing to serve
   // held (this process, or the store by any process): the waiters retry later
+  if (__atomic_load_n(&shared_->hold, __ATOMIC_ACQUIRE)) reap_holds();
   if (g_hold.load(std::memory_order_acquire) > 0 || __atomic_load_n(&shared_->hold, __ATOMIC_ACQUIRE)) return;
   if (__atomic_load_n(&shared_->alive, __ATOMIC_ACQUIRE)) return;
   __atomic_store_n(&shared_->alive, 1u, __ATOMIC_RELEASE);
@@ -978,6 +1000,10 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
     // the owner closed the store or died: this process serves itself from now on (the arena it
     // imported stays valid in VMM mode)
     gone_.store(true, std::memory_order_release);
+    // the private worker runs on THIS process's mapping of the arena: a client that attached lazily
+    // and has not mapped it yet gets EAGAIN (HbmStore::ring maps it and calls again), never a worker
+    // launched on a null arena
+    if (!a.base) { errno = EAGAIN; return -1; }
     std::unique_lock<std::mutex> lk(priv_mu_);
     if (!priv_) {
       RingQuiesce quiet;  // ring set-up makes HIP calls: as for a store set-up
@@ -1023,20 +1049,23 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     return (uint64_t)(n.tv_sec - t0.tv_sec) * 1000000u + (uint64_t)((n.tv_nsec - t0.tv_nsec) / 1000);
   };
   for (uint32_t spins = 0;; ++spins) {
+    const uint32_t me = (uint32_t)pid_;
     uint32_t z = 0;
-    if (__atomic_compare_exchange_n(&ent_[e].busy, &z, 1u, true, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) break;
-    // an entry a timed-out caller abandoned (busy 2) is reclaimed once the worker has finished it
-    z = 2;
-    if (finished(e) && __atomic_compare_exchange_n(&ent_[e].busy, &z, 1u, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) {
+    if (__atomic_compare_exchange_n(&ent_[e].busy, &z, me, true, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) break;
+    // an entry a timed-out caller abandoned is reclaimed once the worker has finished it
+    z = kRingAbandoned;
+    if (finished(e) && __atomic_compare_exchange_n(&ent_[e].busy, &z, me, false, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED)) {
       if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
       break;
     }
     if ((spins & 63) == 63) {
-      // an entry held by a process that died is abandoned (its call is reclaimed once finished)
-      const int32_t h = __atomic_load_n(&ent_[e].holder, __ATOMIC_RELAXED);
-      z = 1;
-      if (mode_ != kPrivate && h > 0 && h != pid_ && kill(h, 0) != 0 && errno == ESRCH)
-        (void)__atomic_compare_exchange_n(&ent_[e].busy, &z, 2u, false, __ATOMIC_RELAXED, __ATOMIC_RELAXED);
+      // an entry held by a process that died is abandoned (its call is reclaimed once finished); the
+      // CAS only succeeds on the exact dead pid it read, so a live owner is never abandoned
+      const uint32_t h = __atomic_load_n(&ent_[e].busy, __ATOMIC_RELAXED);
+      z = h;
+      if (mode_ != kPrivate && h != 0 && h != kRingAbandoned && h != me && kill((pid_t)h, 0) != 0 && errno == ESRCH)
+        (void)__atomic_compare_exchange_n(&ent_[e].busy, &z, kRingAbandoned, false, __ATOMIC_RELAXED,
+                                          __ATOMIC_RELAXED);
       _mm_pause();
       if (elapsed_us() > 30000000u) {  // every entry held for 30 s: the GPU stopped serving
         errno = EBUSY;
@@ -1046,7 +1075,6 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     }
     e = entry_of(++t);
   }
-  __atomic_store_n(&ent_[e].holder, pid_, __ATOMIC_RELAXED);
   RingCmd* c = cmds_ + e;
   uint32_t done_word = kRingDone;
   if (vr_) {
@@ -1139,7 +1167,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
         ensure_worker();  // the worker idled out meanwhile
         const bool dead = mode_ == kClient && server_gone();
         if (dead || us > 30000000u) {  // the GPU stopped serving: abandon the entry (reclaimed once done)
-          __atomic_store_n(&ent_[e].busy, 2u, __ATOMIC_RELEASE);
+          __atomic_store_n(&ent_[e].busy, kRingAbandoned, __ATOMIC_RELEASE);
           if (dead) gone_.store(true, std::memory_order_release);
           errno = dead ? EIO : ETIMEDOUT;
           return -1;
@@ -1173,7 +1201,11 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
 int CmdRing::hold(bool on) {
   if (!shared_) { errno = ENOSYS; return -1; }
   if (mode_ == kClient && gone_.load(std::memory_order_acquire) && priv_) return priv_->hold(on);
+  RingShared::HoldSlot* hs = shared_->holds;
   if (on) {
+    const int slot = hold_slot(true);
+    if (slot < 0) { errno = EBUSY; return -1; }  // kRingHoldSlots processes hold the store already
+    __atomic_fetch_add(&hs[slot].count, 1u, __ATOMIC_ACQ_REL);
     __atomic_fetch_add(&shared_->hold, 1u, __ATOMIC_ACQ_REL);
     // the worker sees the flag within a poll round; wait until its last wave is out
     timespec t0;
@@ -1182,6 +1214,7 @@ int CmdRing::hold(bool on) {
       timespec n;
       clock_gettime(CLOCK_MONOTONIC, &n);
       if ((n.tv_sec - t0.tv_sec) * 1000000000L + (n.tv_nsec - t0.tv_nsec) > 10000000000L) {
+        hold(false);  // the hold was not granted: take it back (a caller that sees -1 never releases it)
         errno = ETIMEDOUT;
         return -1;
       }
@@ -1189,12 +1222,52 @@ int CmdRing::hold(bool on) {
     }
     return 0;
   }
+  const int slot = hold_slot(false);
+  if (slot < 0) { errno = EINVAL; return -1; }  // this process holds nothing
+  uint32_t c = __atomic_load_n(&hs[slot].count, __ATOMIC_ACQUIRE);
+  do {
+    if (c == 0) { errno = EINVAL; return -1; }
+  } while (!__atomic_compare_exchange_n(&hs[slot].count, &c, c - 1, true, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE));
   if (__atomic_sub_fetch(&shared_->hold, 1u, __ATOMIC_ACQ_REL) != 0) return 0;
   if (__atomic_load_n(waiters_, __ATOMIC_RELAXED) > 0) {  // calls are waiting: a worker again
     if (mode_ == kClient) want_worker();
     else if (arena_.base) launch(arena_);
   }
   return 0;
+}
+
+// This process's hold slot: the one carrying its pid, or (claim) a free one -- after taking back the
+// slots of holders that died when none is free.  A slot stays with its process until the process
+// dies (clearing it on release would race a second thread of the same process that found it).
+int CmdRing::hold_slot(bool claim) {
+  RingShared::HoldSlot* hs = shared_->holds;
+  for (int i = 0; i < kRingHoldSlots; ++i)
+    if (__atomic_load_n(&hs[i].pid, __ATOMIC_ACQUIRE) == pid_) return i;
+  if (!claim) return -1;
+  for (int pass = 0; pass < 2; ++pass) {
+    for (int i = 0; i < kRingHoldSlots; ++i) {
+      int32_t z = 0;
+      if (__atomic_compare_exchange_n(&hs[i].pid, &z, pid_, false, __ATOMIC_ACQ_REL, __ATOMIC_ACQUIRE)) return i;
+      if (z == pid_) return i;  // another thread of this process claimed it meanwhile
+    }
+    reap_holds();
+  }
+  return -1;
+}
+
+// A holder that died (crash, kill) leaves its count in shared_->hold and would keep every worker of
+// the store down for good: its slot's count is taken back (exchanged to 0 first, so two reapers never
+// both subtract it) and the slot freed.
+void CmdRing::reap_holds() {
+  RingShared::HoldSlot* hs = shared_->holds;
+  for (int i = 0; i < kRingHoldSlots; ++i) {
+    const int32_t p = __atomic_load_n(&hs[i].pid, __ATOMIC_ACQUIRE);
+    if (p <= 0 || p == pid_ || !(kill(p, 0) != 0 && errno == ESRCH)) continue;
+    const uint32_t c = __atomic_exchange_n(&hs[i].count, 0u, __ATOMIC_ACQ_REL);
+    if (c) __atomic_fetch_sub(&shared_->hold, c, __ATOMIC_ACQ_REL);
+    int32_t exp = p;
+    (void)__atomic_compare_exchange_n(&hs[i].pid, &exp, 0, false, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED);
+  }
 }
 
 // after a hold: relaunch the worker if calls are waiting for it
@@ -1228,11 +1301,7 @@ CmdRing::~CmdRing() {
     // clients see the segment close first (their calls then fail over to private rings), then
     // the supervisor and the worker stop
     if (seg_) __atomic_store_n(&seg_->magic, 0u, __ATOMIC_RELEASE);
-    sup_stop_.store(true, std::memory_order_release);
-    if (sup_.joinable()) {
-      want_worker();
-      sup_.join();
-    }
+    stop_supervisor();
   }
   stop();
 #ifdef SPL_RING_STAMPS

@@ -90,6 +90,8 @@ constexpr int kRingGroups = 32;                     // most one-wave workers (SP
 constexpr int kDefaultRingGroups = 32;              // default worker waves (32 vs 8: 1.29-1.32 vs 1.05-1.09 M ops/s at
                                                     // 64 host threads, no fall-off from 32 threads; profiles/r4ab)
 constexpr int kRingEntries = 256;                   // entries (per wave: kRingEntries / groups)
+constexpr int kRingMinGroups = kRingEntries / 64;   // a wave's 64 lanes serve at most 64 entries
+constexpr int kRingHoldSlots = 16;                  // processes that may hold a store's ring at once
 
 struct RingShared {
   uint32_t state[kRingEntries];  // doorbells (one 32-B read per group)
@@ -98,6 +100,12 @@ struct RingShared {
   uint32_t launches;             // host statistic
   uint32_t hold;                 // store-level holds (CmdRing::hold, any attached process): no worker
   uint32_t pad[12];
+  // who holds `hold`: one slot per holding process (pid, its count), so the count a holder that died
+  // left behind is taken back (CmdRing::reap_holds) instead of stopping the store's worker for good
+  struct HoldSlot {
+    int32_t pid;
+    uint32_t count;
+  } holds[kRingHoldSlots];
 #ifdef SPL_RING_STAMPS
   // latency breakdown (make hip-variant V=stamps VFLAGS=-DSPL_RING_STAMPS): per entry, sums of
   // wall-clock ticks from "doorbell seen" to "record loaded", to "op done", to "completion
@@ -120,12 +128,15 @@ struct alignas(64) RingDone {  // one cache line per entry: a completion never d
   uint8_t pad[48];
 };
 
-// Host-side ownership of one entry (own cache line: callers on different entries share no line)
+// Host-side ownership of one entry (own cache line: callers on different entries share no line).
+// `busy` is the owner's pid (0 free, kRingAbandoned abandoned -- reclaimed once its call is done):
+// ownership and the owner's identity are ONE word, taken by one CAS, so a live owner can never be
+// mistaken for a dead one between taking the entry and recording who took it.
+constexpr uint32_t kRingAbandoned = 0xffffffffu;
 struct alignas(64) RingEntryCtl {
-  uint32_t busy;    // 0 free, 1 held, 2 abandoned (reclaimed once its call is done)
-  int32_t holder;   // pid holding the entry (a dead holder's entry is reclaimed)
+  uint32_t busy;    // 0 free, pid of the holding process, or kRingAbandoned
   uint32_t seq;     // last sequence number issued
-  uint32_t pad[13];
+  uint32_t pad[14];
 };
 
 struct RingResult {
@@ -208,6 +219,9 @@ class CmdRing {
   // the worker did not exit within 10 s.
   int hold(bool on);
   uint32_t launches() const { return seg_ ? seg_->launches : shared_ ? shared_->launches : 0; }
+  // ring server: stop and join the supervisor thread (the store's teardown does this BEFORE it
+  // takes the quiesce gate, which the supervisor takes shared to relaunch a worker)
+  void stop_supervisor();
 
  private:
   enum Mode { kPrivate, kServer, kClient };
@@ -215,6 +229,8 @@ class CmdRing {
   void want_worker();        // client: ask the owner's supervisor for a worker
   bool server_gone() const;  // client: the owner closed the store or died
   void supervise();          // server: relaunch the worker when a client asks
+  void reap_holds();         // take back the hold counts of holder processes that died
+  int hold_slot(bool claim); // this process's slot in shared_->holds (-1: none / table full)
   int call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen,
                    uint64_t khash, const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap,
                    RingResult* r);

@@ -503,7 +503,14 @@ class HbmStore final : public StoreBase {
     if (!ring_ || !ring_->ready()) { errno = ENOSYS; return -1; }
     // a client of the owner's ring server needs no device mapping of the arena; its own worker does
     if (ring_->needs_arena() && !ensure_mapped()) return -1;
-    return ring_->call(arena(), op, sub, k, klen, khash, in, in_len, arg, out, out_cap, r);
+    const int rc = ring_->call(arena(), op, sub, k, klen, khash, in, in_len, arg, out, out_cap, r);
+    // the owner went away between the check above and the call: the call falls over to a private
+    // worker, which needs this process's own mapping of the arena -- map it and call once more
+    if (rc != 0 && errno == EAGAIN && ring_->needs_arena()) {
+      if (!ensure_mapped()) return -1;
+      return ring_->call(arena(), op, sub, k, klen, khash, in, in_len, arg, out, out_cap, r);
+    }
+    return rc;
   }
   static int st_ret(int32_t st) {
     if (st == 0) return 0;
@@ -872,6 +879,10 @@ HbmStore* HbmStore::open(const char* name, int* err) {
 }
 
 HbmStore::~HbmStore() {
+  // a ring server's supervisor takes the quiesce gate shared to relaunch the worker: stop it before
+  // this teardown takes the gate exclusive (it would otherwise wait on the gate while ~CmdRing joins
+  // it).  Clients that want a worker meanwhile keep polling until the segment closes, then fail over.
+  if (ring_) ring_->stop_supervisor();
   RingQuiesce quiet;  // hipFree & co. may wait for the device: no resident worker of this process
   DevGuard dg(device_);
   for (auto& st : stg_) {

@@ -160,6 +160,7 @@ class XRoute:
         if W == 1:
             transport = "local"
         self.transport = transport
+        self.fallback_reason = None  # why a requested peer transport fell back to rccl (None: it did not)
         i32 = dict(dtype=torch.int32, device=dev)
         # per parity: pack counts [kind][dest], sent counts [dest][kind], received [src][kind]
         self.cnt = [torch.zeros((2, W), **i32) for _ in range(2)]
@@ -196,8 +197,10 @@ class XRoute:
         dist.all_gather_object(devs, dev, group=self.group)
         ok = True
         own = L.spl_xw_create(dev, self.g.window_b, names[r].encode())
+        why = None
         if not own:
             ok = False
+            why = f"rank {r}: spl_xw_create of a {self.g.window_b}-B window failed"
         else:
             self._xw.append(own)
         dist.barrier(group=self.group)  # every window is being served
@@ -209,16 +212,25 @@ class XRoute:
                     continue
                 if L.spl_xw_peer(dev, int(devs[q])) != 0:
                     ok = False
+                    why = f"rank {r}: peer access device {dev} -> {devs[q]} refused"
                     break
                 h = L.spl_xw_attach(names[q].encode(), dev)
                 if not h:
                     ok = False
+                    why = f"rank {r}: attaching rank {q}'s window failed"
                     break
                 self._xw.append(h)
                 self._peer_base[q] = L.spl_xw_base(h)
-        ok = self._agree(ok)
+        mapped = self._agree(ok)
+        ok = mapped
         if ok:
             ok = self._agree(self._validate())
+            if not ok:
+                why = "marker round trip through the peer windows did not validate"
+        if not mapped and why is None:
+            why = "another rank could not map the windows"
+        if not ok:
+            self.fallback_reason = why
         dist.barrier(group=self.group)  # every peer is done with the windows before any is torn down
         if not ok:
             for h in reversed(self._xw):

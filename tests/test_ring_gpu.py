@@ -415,3 +415,98 @@ def test_store_ring_hold_from_another_process(uniq):
         if p.poll() is None:
             p.kill()
         s.close()
+
+
+_BUSY_OWNER = r"""
+import sys
+from libsplinter_amd import Store
+s = Store.create(sys.argv[1], slots=4096, max_val=64, embeddings=False)
+s.set("o", b"owner")
+print("ready", flush=True)
+sys.stdin.readline()
+s.close()
+print("closed", flush=True)
+"""
+
+_BUSY_CLIENT = r"""
+import sys, time
+from libsplinter_amd import Store
+s = Store.open(sys.argv[1])
+print("running", flush=True)
+t_end = time.time() + float(sys.argv[2])
+n = bad = err = 0
+while time.time() < t_end:
+    k = f"c{n % 64}"
+    v = f"v{n}".encode()
+    try:
+        s.set(k, v)
+        if s.get(k) != v:
+            bad += 1
+    except OSError:
+        err += 1  # a call in flight when the server vanished fails (EIO); the next one fails over
+    n += 1
+print(n, bad, err, flush=True)
+s.close()
+"""
+
+
+def test_owner_close_while_client_is_calling(uniq):
+    """The owner closes the store while a client process is issuing per-call ops through the owner's
+    ring server: the owner's teardown completes (it stops its supervisor before taking the quiesce
+    gate, so a supervisor woken by the client cannot block it), and the client's calls fall over to
+    a private worker with every set read back intact."""
+    name = f"hbm:{uniq}"
+    own = subprocess.Popen([sys.executable, "-c", _BUSY_OWNER, name], cwd=ROOT, env=ENV, stdin=subprocess.PIPE,
+                           stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+    cli = None
+    try:
+        assert own.stdout.readline().strip() == "ready"
+        cli = subprocess.Popen([sys.executable, "-c", _BUSY_CLIENT, name, "4.0"], cwd=ROOT, env=ENV,
+                               stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+        assert cli.stdout.readline().strip() == "running"
+        time.sleep(1.0)  # client traffic in flight on the owner's server
+        own.stdin.write("close\n")
+        own.stdin.flush()
+        out, err = own.communicate(timeout=60)
+        assert own.returncode == 0 and out.strip() == "closed", err[-2000:]
+        cout, cerr = cli.communicate(timeout=90)
+        assert cli.returncode == 0, cerr[-2000:]
+        n, bad, err = map(int, cout.split())
+        # no wrong bytes ever; at most the few calls in flight at the failover fail (EIO, never
+        # retried by the library: a set / get could be, an increment or append could not)
+        assert n > 100 and bad == 0 and err <= 4, (n, bad, err)
+    finally:
+        for p in (own, cli):
+            if p is not None and p.poll() is None:
+                p.kill()
+
+
+_DYING_HOLDER = r"""
+import os, sys
+from libsplinter_amd import Store
+from libsplinter_amd.store import ring_hold
+s = Store.open(sys.argv[1])
+h = ring_hold(s)
+h.__enter__()
+print("held", flush=True)
+os._exit(0)  # dies holding the store's ring
+"""
+
+
+def test_hold_of_a_dead_process_is_taken_back(uniq):
+    """A process that dies inside ring_hold(store) leaves its count in the store's hold word; the
+    owner's next call finds the holder dead, takes its count back and is served (instead of every
+    call on the store timing out)."""
+    from libsplinter_amd import Store
+    s = Store.create(f"hbm:{uniq}", slots=1024, max_val=64, embeddings=False)
+    try:
+        s.set("pre", b"1")
+        r = subprocess.run([sys.executable, "-c", _DYING_HOLDER, f"hbm:{uniq}"], cwd=ROOT, env=ENV,
+                           capture_output=True, text=True, timeout=90)
+        assert r.stdout.strip() == "held", r.stderr[-2000:]
+        t = time.perf_counter()
+        s.set("after", b"2")
+        assert time.perf_counter() - t < 10.0
+        assert s.get("after") == b"2"
+    finally:
+        s.close()

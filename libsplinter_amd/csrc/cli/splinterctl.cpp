@@ -1220,6 +1220,44 @@ int cmd_stats(int, char**) {
     uint64_t c = splinter_get_signal_count((uint8_t)g);
     if (c) printf("signal_group[%d]=%lu\n", g, (unsigned long)c);
   }
+  // probe-chain health of an hbm: / node: store (libsplinter_hip.so, one device pass): how far a hit
+  // and a miss probe, and the tombstones that make misses walk further
+  using ProbeFn = int (*)(spl_store*, spl_probe_stats*);
+  auto probe = (ProbeFn)dlsym(RTLD_DEFAULT, "spl_hbm_probe_stats");
+  spl_probe_stats ps{};
+  if (probe && probe(spl_store_current(), &ps) == 0) {
+    const double homes = (double)h.slots;
+    printf("probe_live=%lu\nprobe_tombstones=%lu\nprobe_virgin=%lu\nprobe_busy=%lu\n", (unsigned long)ps.live,
+           (unsigned long)ps.tombstones, (unsigned long)ps.virgin, (unsigned long)ps.busy);
+    printf("probe_hit_mean=%.3f\nprobe_hit_max=%lu\n", ps.live ? (double)ps.disp_sum / ps.live : 0.0,
+           (unsigned long)ps.disp_max);
+    if (ps.virgin)
+      printf("probe_miss_mean=%.3f\nprobe_miss_max=%lu\n", homes ? (double)ps.miss_sum / homes : 0.0,
+             (unsigned long)ps.miss_max);
+    else
+      printf("probe_miss_mean=%u\nprobe_miss_max=%u\n", h.slots, h.slots);  // no never-used slot: a miss scans all
+    static const char* lab[12] = {"1", "2", "3-4", "5-8", "9-16", "17-32", "33-64", "65-128", "129-256", "257-512",
+                                  "513-1024", ">1024"};
+    for (int b = 0; b < 12; ++b)
+      if (ps.hist[b]) printf("probe_hist[%s]=%lu\n", lab[b], (unsigned long)ps.hist[b]);
+    printf("rehash_runs=%lu\nrehash_moved=%lu\nrehash_reclaimed=%lu\n", (unsigned long)ps.rebuilds,
+           (unsigned long)ps.moved, (unsigned long)ps.reclaimed);
+  }
+  return 0;
+}
+
+// `rehash`: the tombstone rebuild of an hbm: / node: store (spl_hbm_rehash; exclusive maintenance)
+int cmd_rehash(int, char**) {
+  if (!need_store("rehash")) return 1;
+  using RehashFn = int (*)(spl_store*, uint64_t*);
+  auto fn = (RehashFn)dlsym(RTLD_DEFAULT, "spl_hbm_rehash");
+  uint64_t out[4] = {0, 0, 0, 0};
+  if (!fn || fn(spl_store_current(), out) != 0) {
+    fprintf(stderr, "rehash: only hbm: and node: stores of HBM shards (device pass), or the pass failed\n");
+    return 1;
+  }
+  printf("moved=%lu\nreclaimed=%lu\nclusters=%lu\nskipped=%lu\n", (unsigned long)out[0], (unsigned long)out[1],
+         (unsigned long)out[2], (unsigned long)out[3]);
   return 0;
 }
 
@@ -1488,7 +1526,9 @@ void register_modules() {
        [] { puts("Usage: search <query>|- [--file PATH] [--json] [--limit N] [--distance F] [--similarity F] [--bloom MASK] [--regex PATTERN]"); }},
       {"ingest", "Chunk a file or stdin into VARTEXT tandem keys.", cmd_ingest,
        [] { puts("Usage: ingest [file] [--key <key>] [--label <hex>]"); }},
-      {"stats", "Store occupancy, embeddings and signal counters.", cmd_stats, nullptr},
+      {"stats", "Store occupancy, embeddings, signal counters and (hbm/node) probe-chain health.", cmd_stats, nullptr},
+      {"rehash", "Rebuild probe chains: move keys into tombstones on their path, reclaim trailing ones (hbm/node, exclusive).",
+       cmd_rehash, [] { puts("Usage: rehash   (no other process may write to the store meanwhile)"); }},
       {"wasm", "Run a WASM module (binary or WAT) against the store.", cmd_wasm,
        [] { puts("Usage: wasm <plugin.wasm|plugin.wat> [function_name]\nExecutes a WASM module with access to the Splinter bus."); }},
       {"lua", "Run a Lua script against the store (splinter module).", cmd_lua,

@@ -52,7 +52,54 @@ struct Arena {
   __device__ __forceinline__ uint8_t* value(size_t i) const {
     return base + kHeaderBytes + (size_t)slots * stride + i * (size_t)max_val;
   }
+  // side region (splinter_layout.hpp): present when the allocation was made with it
+  __device__ __forceinline__ bool has_side() const { return flags & SPL_ARENA_SIDE; }
+  __device__ __forceinline__ bool has_vec16() const { return flags & SPL_ARENA_VEC16; }
+  __device__ __forceinline__ uint8_t* side() const { return base + side_offset(slots, stride, max_val); }
+  __device__ __forceinline__ float* nrm2() const { return (float*)(side() + side_nrm2_offset()); }
+  __device__ __forceinline__ uint16_t* vec16(size_t i) const {
+    return (uint16_t*)(side() + side_vec16_offset(slots)) + i * kEmbedDim;
+  }
 };
+
+// ---------------------------------------------------- bf16 vector copy ------
+// Vector of one slot, distributed over a wave as the embedding kernels hold it (lane l: float4
+// chunks l, l + 64, l + 128 of the 768 dims) -> the side region's bf16 copy (three 8-B stores per
+// lane, coalesced) and squared norm (wave sum; lane 0 stores it).  Called while the caller holds
+// the slot's seqlock, before its release fence: the copy is published with the fp32 vector.
+__device__ __forceinline__ void write_vec16_wave(const Arena& a, size_t idx, const float4 (&v)[3], int lane) {
+  if (!a.has_vec16()) return;
+  uint2* d = (uint2*)a.vec16(idx);
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+    const bf2_t lo = {(__bf16)v[c].x, (__bf16)v[c].y}, hi = {(__bf16)v[c].z, (__bf16)v[c].w};
+    d[lane + 64 * c] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+    ss += v[c].x * v[c].x + v[c].y * v[c].y + v[c].z * v[c].z + v[c].w * v[c].w;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if (lane == 0) a.nrm2()[idx] = ss;
+}
+// one thread's form (the ring worker, single lanes): the whole vector from `src` (768 floats)
+__device__ __forceinline__ void write_vec16_one(const Arena& a, size_t idx, const float* src) {
+  if (!a.has_vec16()) return;
+  uint2* d = (uint2*)a.vec16(idx);
+  float ss = 0.f;
+  for (uint32_t c = 0; c < kEmbedDim / 4; ++c) {
+    const float4 x = ((const float4*)src)[c];
+    typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+    const bf2_t lo = {(__bf16)x.x, (__bf16)x.y}, hi = {(__bf16)x.z, (__bf16)x.w};
+    d[c] = make_uint2(__builtin_bit_cast(uint32_t, lo), __builtin_bit_cast(uint32_t, hi));
+    ss += x.x * x.x + x.y * x.y + x.z * x.z + x.w * x.w;
+  }
+  a.nrm2()[idx] = ss;
+}
+// the slot holds no vector (fresh insert, unset, retrain): its norm 0 marks the copy dead
+__device__ __forceinline__ void clear_vec16(const Arena& a, size_t idx) {
+  if (a.has_vec16()) a.nrm2()[idx] = 0.f;
+}
 
 // ------------------------------------------------------------- atomics --
 __device__ __forceinline__ uint64_t ald64(const void* p) {
@@ -670,6 +717,7 @@ __device__ __forceinline__ void write_meta(const Arena& a, const Claim& c, uint3
     if (a.stride == kSlotEmbedBytes) {
       uint4* ev = (uint4*)(s + kOffEmbed);
       for (uint32_t q = 0; q < kEmbedBytes / 16; ++q) st16<MO>(ev + q, make_uint4(0, 0, 0, 0));
+      clear_vec16(a, (size_t)c.idx);
     }
   }
   ast32(s + kOffValLen, len);
@@ -699,6 +747,7 @@ __device__ __forceinline__ void write_set(const Arena& a, const Claim& c, const 
     if (a.stride == kSlotEmbedBytes) {
       uint4* ev = (uint4*)(s + kOffEmbed);
       for (uint32_t q = 0; q < kEmbedBytes / 16; ++q) st16<MO>(ev + q, make_uint4(0, 0, 0, 0));
+      clear_vec16(a, (size_t)c.idx);
     }
   }
   ast32(s + kOffValLen, len);
@@ -849,6 +898,7 @@ __device__ int32_t unset_op(const Arena& a, const KeyT<KW>& k, long* out_idx) {
   if (a.stride == kSlotEmbedBytes) {
     uint4* ev = (uint4*)(s + kOffEmbed);
     for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ev[c] = make_uint4(0, 0, 0, 0);
+    clear_vec16(a, (size_t)i);
   }
   release();
   ast64(epoch_ptr(s), 2);  // reference contract: unset rewinds the epoch to 2
@@ -1011,8 +1061,10 @@ __device__ int32_t meta_op(const Arena& a, const KeyT<KW>& k, int op, uint64_t a
     case 8:
       ast64(epoch_ptr(s), 3);
       drain();
-      if (a.stride == kSlotEmbedBytes)
+      if (a.stride == kSlotEmbedBytes) {
         for (uint32_t c = 0; c < kEmbedBytes / 16; ++c) ((uint4*)(s + kOffEmbed))[c] = make_uint4(0, 0, 0, 0);
+        clear_vec16(a, (size_t)idx);
+      }
       release();
       ast64(epoch_ptr(s), 4);
       *mut = true;

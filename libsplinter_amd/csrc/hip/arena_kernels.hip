@@ -765,8 +765,14 @@ __global__ __launch_bounds__(kBlock) void k_embed_set(spl_arena_t aa, const char
     if (rc == kOk) {
       const uint4* src = (const uint4*)(vecs + i * (long)kEmbedDim);
       uint4* dst = (uint4*)(s + kOffEmbed);
+      float4 v[3];
 #pragma unroll
-      for (int c = 0; c < 3; ++c) dst[lane + 64 * c] = src[lane + 64 * c];
+      for (int c = 0; c < 3; ++c) {
+        const uint4 x = src[lane + 64 * c];
+        dst[lane + 64 * c] = x;
+        v[c] = __builtin_bit_cast(float4, x);
+      }
+      write_vec16_wave(a, (size_t)idx, v, lane);
       release();
       __builtin_amdgcn_wave_barrier();
       if (lane == 0) {

@@ -412,6 +412,7 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
       if (slot_hash(s) != k.hash || !key_eq(s, k)) { aadd64(epoch_ptr(s), 1); return kNoEnt; }
       uint4* dst = (uint4*)(s + kOffEmbed);
       for (uint32_t q = 0; q < kEmbedBytes / 16; ++q) st16_wt(dst + q, ((const uint4*)pay)[q]);
+      write_vec16_one(a, (size_t)idx, (const float*)pay);
       drain();
       aadd64(epoch_ptr(s), 1);
       count_mutation(a, idx);

@@ -58,6 +58,8 @@ struct HbmDescriptor {
   uint32_t mode;                         // 0 hipIpc, 1 VMM chunks (vmm_share.hpp)
   uint32_t nchunks;
   uint64_t chunk_bytes;
+  uint32_t side_flags;                   // SPL_ARENA_SIDE | SPL_ARENA_VEC16: the allocation's side region
+  uint32_t pad2;
   char sock[96];                         // mode 1: abstract socket serving the chunk fds
   alignas(64) splinter_header control;  // host control plane (shard bids, event bus owner)
   alignas(64) uint32_t notify;          // event-bus doorbell: set by kernels / per-call writers,
@@ -115,7 +117,7 @@ class HbmStore final : public StoreBase {
     a.slots = geo_.slots;
     a.max_val = geo_.max_val;
     a.stride = geo_.stride;
-    a.flags = event_fd_ >= 0 ? 1u : 0u;
+    a.flags = (event_fd_ >= 0 ? SPL_ARENA_EVENTBUS : 0u) | side_flags_;
     a.notify = (uint64_t)(uintptr_t)d_notify_;
     return a;
   }
@@ -452,6 +454,8 @@ class HbmStore final : public StoreBase {
   int checkpoint(const char* path);
   long search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap, spl_search_hit* out);
   int restore_from(const char* path);
+  int probe_stats(ProbeStats* out);
+  int rehash(uint64_t out[4]);
 
   // ------------------------------------------------------ host-array batches --
   long set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens, long n,
@@ -651,6 +655,7 @@ class HbmStore final : public StoreBase {
     return e && !strcmp(e, "0");
   }
   bool vmm_mode_ = false;
+  uint32_t side_flags_ = 0;  // SPL_ARENA_SIDE / SPL_ARENA_VEC16 of the allocation (descriptor)
   void* dbase_ = nullptr;  // raw_ + kAlignOffset (null until mapped: an opener attaches lazily)
   // Lazy attach: an opener whose per-call ops go to the owner's ring server maps the arena into its
   // own GPU address space only on the first op that needs it (batches, scans, search, raw pointers,
@@ -768,13 +773,20 @@ HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool 
   s->owner_ = true;
   (void)hipGetDevice(&s->device_);
   const size_t total = s->geo_.total_bytes();
+  // the side region after the values (splinter_layout.hpp): probe statistics, and for an embedding
+  // store the bf16 vector copy the batched search streams (SPLINTER_HBM_VEC16=0: none)
+  const char* v16e = getenv("SPLINTER_HBM_VEC16");
+  const bool vec16 = emb && !(v16e && !strcmp(v16e, "0"));
+  const size_t side_off = side_offset(s->geo_.slots, s->geo_.stride, s->geo_.max_val);
+  const size_t alloc = side_off + side_bytes(s->geo_.slots, vec16) + 256;
+  s->side_flags_ = SPL_ARENA_SIDE | (vec16 ? SPL_ARENA_VEC16 : 0u);
   // VMM chunks (attachable by other processes at any size), else one hipMalloc allocation
   const char* ve = getenv("SPLINTER_HBM_VMM");
   const size_t chunk_mb = getenv("SPLINTER_HBM_CHUNK_MB") ? (size_t)atol(getenv("SPLINTER_HBM_CHUNK_MB")) : 1024;
-  if (!(ve && !strcmp(ve, "0")) && s->vmm_.create(s->device_, total + 256, (chunk_mb ? chunk_mb : 1024) << 20) == 0) {
+  if (!(ve && !strcmp(ve, "0")) && s->vmm_.create(s->device_, alloc, (chunk_mb ? chunk_mb : 1024) << 20) == 0) {
     s->vmm_mode_ = true;
     s->raw_ = s->vmm_.base();
-  } else if (hipMalloc(&s->raw_, total + 256) != hipSuccess) {
+  } else if (hipMalloc(&s->raw_, alloc) != hipSuccess) {
     *err = ENOMEM;
     delete s;
     return nullptr;
@@ -799,6 +811,9 @@ HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool 
   (void)hipMemsetAsync((uint8_t*)s->dbase_ + kHeaderBytes + s->geo_.slots_bytes(), 0, s->geo_.values_bytes(), s->stream_);
   if (s->geo_.embeddings())
     (void)hipMemsetAsync((uint8_t*)s->dbase_ + kHeaderBytes, 0, s->geo_.slots_bytes(), s->stream_);
+  // side header and squared norms zeroed (no vector yet); the bf16 rows are only read where a norm is set
+  (void)hipMemsetAsync((uint8_t*)s->dbase_ + side_off, 0,
+                       vec16 ? side_vec16_offset(s->geo_.slots) : kSideHdrBytes, s->stream_);
   spl_arena_init_slots(s->arena(), s->stream_);
   (void)hipStreamSynchronize(s->stream_);
   HbmDescriptor* d = s->desc_;
@@ -812,6 +827,7 @@ HbmStore* HbmStore::create(const char* name, size_t slots, size_t max_val, bool 
   d->owner_pid = (int32_t)getpid();
   std::memset(&d->handle, 0, sizeof d->handle);
   d->mode = s->vmm_mode_ ? 1u : 0u;
+  d->side_flags = s->side_flags_;
   if (s->vmm_mode_) {
     d->nchunks = (uint32_t)s->vmm_.chunks();
     d->chunk_bytes = s->vmm_.chunk();
@@ -843,6 +859,7 @@ HbmStore* HbmStore::open(const char* name, int* err) {
   s->geo_.max_val = d->max_val;
   s->geo_.stride = d->stride;
   s->device_ = (int)d->device;
+  s->side_flags_ = d->side_flags & (SPL_ARENA_SIDE | SPL_ARENA_VEC16);
   DevGuard dg(s->device_);
   if (d->version >= 3 && d->mode == 1) {
     std::vector<int> fds;
@@ -1048,7 +1065,70 @@ int HbmStore::restore_from(const char* path) {
   }
   (void)hipHostFree(pin);
   close(fd);
+  // the side region is not in the file: the bf16 vector copy is rebuilt from the restored vectors
+  if (rc == 0 && (side_flags_ & SPL_ARENA_VEC16)) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (spl_arena_vec16_rebuild(arena(), stream_) != 0 || hipStreamSynchronize(stream_) != hipSuccess) rc = -1;
+  }
   return rc;
+}
+
+// Probe-chain statistics (arena_maint.hip k_probe_stats) into *out (host).
+int HbmStore::probe_stats(ProbeStats* out) {
+  if (!ensure_mapped()) return -1;
+  DevGuard dg(device_);
+  std::lock_guard<std::mutex> lk(mu_);
+  ProbeStats* d = nullptr;
+  if (hipMallocAsync((void**)&d, sizeof(ProbeStats), stream_) != hipSuccess) return -1;
+  (void)hipMemsetAsync(d, 0, sizeof(ProbeStats), stream_);
+  int rc = spl_arena_probe_stats(arena(), d, stream_);
+  if (rc == 0) (void)hipMemcpyAsync(out, d, sizeof(ProbeStats), hipMemcpyDeviceToHost, stream_);
+  (void)hipFreeAsync(d, stream_);
+  if (hipStreamSynchronize(stream_) != hipSuccess) rc = -1;
+  if (rc == 0 && (side_flags_ & SPL_ARENA_SIDE)) {  // the maintenance counters live in the side header
+    ProbeStats side;
+    if (hipMemcpy(&side, (uint8_t*)dbase_ + side_offset(geo_.slots, geo_.stride, geo_.max_val), sizeof side,
+                  hipMemcpyDeviceToHost) == hipSuccess) {
+      out->rebuilds = side.rebuilds;
+      out->reclaimed = side.reclaimed;
+      out->moved = side.moved;
+    }
+  }
+  return rc == 0 ? 0 : -1;
+}
+
+// Tombstone rebuild (arena_maint.hip k_rehash).  EXCLUSIVE: the store's ring worker is held for the
+// pass and the caller guarantees that no batch op of any process runs on the arena meanwhile.
+// out: {moved, reclaimed, clusters, clusters past the per-wave tombstone cap}.
+int HbmStore::rehash(uint64_t out[4]) {
+  if (!ensure_mapped()) return -1;
+  DevGuard dg(device_);
+  const bool held = ring_ && ring_->ready() && ring_->hold(true) == 0;
+  int rc = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    uint64_t* d = nullptr;
+    if (hipMallocAsync((void**)&d, 32, stream_) != hipSuccess) rc = -1;
+    if (rc == 0) {
+      (void)hipMemsetAsync(d, 0, 32, stream_);
+      rc = spl_arena_rehash(arena(), d, stream_);
+      if (rc == 0) (void)hipMemcpyAsync(out, d, 32, hipMemcpyDeviceToHost, stream_);
+      (void)hipFreeAsync(d, stream_);
+    }
+    if (hipStreamSynchronize(stream_) != hipSuccess) rc = -1;
+    if (rc == 0 && (side_flags_ & SPL_ARENA_SIDE)) {
+      ProbeStats side;
+      uint8_t* sp = (uint8_t*)dbase_ + side_offset(geo_.slots, geo_.stride, geo_.max_val);
+      if (hipMemcpy(&side, sp, sizeof side, hipMemcpyDeviceToHost) == hipSuccess) {
+        side.rebuilds += 1;
+        side.moved += out[0];
+        side.reclaimed += out[1];
+        (void)hipMemcpy(sp, &side, sizeof side, hipMemcpyHostToDevice);
+      }
+    }
+  }
+  if (held) ring_->hold(false);
+  return rc == 0 ? 0 : -1;
 }
 
 StoreBase* hbm_factory_impl(const char* name, size_t slots, size_t max_val, unsigned flags, int create, int* err) {
@@ -1365,6 +1445,50 @@ long spl_hbm_search(spl_store* h, const float* query, uint64_t mask, float min_s
   const size_t keep = (size_t)std::min<long>((long)all.size(), std::max<long>(cap, 0));
   for (size_t i = 0; i < keep; ++i) out[i] = all[i];
   return total;
+}
+
+// Probe-chain statistics of an HBM store, or summed over the shards of a node store (maxima taken)
+int spl_hbm_probe_stats(spl_store* h, spl_probe_stats* out) {
+  static_assert(sizeof(spl_probe_stats) == sizeof(spl::ProbeStats), "ABI struct = ProbeStats");
+  if (!h || !out) return -2;
+  if (auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h)) return s->probe_stats((spl::ProbeStats*)out);
+  const int n = spl_node_nshards(h);
+  if (n < 1) return -2;
+  std::memset(out, 0, sizeof *out);
+  uint64_t* o = (uint64_t*)out;
+  for (int i = 0; i < n; ++i) {
+    auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+    spl::ProbeStats p;
+    if (!s || s->probe_stats(&p) != 0) return -1;
+    const uint64_t* v = (const uint64_t*)&p;
+    for (size_t f = 0; f < sizeof p / 8; ++f) {
+      const bool is_max = f == offsetof(spl::ProbeStats, disp_max) / 8 || f == offsetof(spl::ProbeStats, miss_max) / 8;
+      o[f] = is_max ? std::max(o[f], v[f]) : o[f] + v[f];
+    }
+  }
+  return 0;
+}
+
+// Tombstone rebuild of an HBM store / every shard of a node store (exclusive maintenance; see
+// HbmStore::rehash).  out (optional): {moved, reclaimed, clusters, skipped}, summed.
+int spl_hbm_rehash(spl_store* h, uint64_t* out) {
+  uint64_t tmp[4] = {0, 0, 0, 0};
+  if (!h) return -2;
+  if (auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h)) {
+    const int rc = s->rehash(tmp);
+    if (out) std::memcpy(out, tmp, sizeof tmp);
+    return rc;
+  }
+  const int n = spl_node_nshards(h);
+  if (n < 1) return -2;
+  uint64_t sum[4] = {0, 0, 0, 0};
+  for (int i = 0; i < n; ++i) {
+    auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+    if (!s || s->rehash(tmp) != 0) return -1;
+    for (int k = 0; k < 4; ++k) sum[k] += tmp[k];
+  }
+  if (out) std::memcpy(out, sum, sizeof sum);
+  return 0;
 }
 
 // checkpoint / restore of an HBM store, or of every shard of a node store (PATH.s<i>)

@@ -661,6 +661,15 @@ __global__ __launch_bounds__(kPoolThreads) void k_pool(const uint16_t* __restric
   if (lock_ok == 1) {
     float* dst = (float*)(a.slot((size_t)si) + kOffEmbed);
     for (int c = tid; c < D; c += kPoolThreads) dst[c] = vec[c] * scale;
+    if (a.has_vec16() && wave == 0) {  // the bf16 copy + squared norm (wave 0, the wave layout of write_vec16_wave)
+      float4 v[3];
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        const float* p = vec + 4 * (lane + 64 * c);
+        v[c] = make_float4(p[0] * scale, p[1] * scale, p[2] * scale, p[3] * scale);
+      }
+      write_vec16_wave(a, (size_t)si, v, lane);
+    }
     release();
     __syncthreads();
     if (tid == 0) {

@@ -461,6 +461,198 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma(spl_arena_t aa, cons
   wait_vm0();  // drain the trailing DMAs (next-tile prefetch of the last tile) before the LDS goes away
 }
 
+}  // namespace mf
+
+// ---------------------------------------------------------------------------
+// The same pass on the side region's bf16 copy (SPL_ARENA_VEC16 arenas, splinter_layout.hpp): every
+// slot's vector as 1536 contiguous bytes (half the fp32 row, no 3200-B stride) and its squared norm
+// precomputed by the writer.  The operands are the values the fp32 pass converts in registers
+// (v_cvt_pk_bf16_f32 = round to nearest even, as the writers store them) and the norm is the fp32
+// one, so the candidate bound and the result are the fp32 pass's.  K-chunks of 32 dims = 64 B per row:
+// a 16 KB chunk per 256-row tile, 4 LDS-DMA wave-instructions per wave, the A fragments read straight
+// as bf16 (one ds_read_b128 each).  Rows are 64 B, so a ds_read_b128 lane group (16 lanes) would hit
+// the same 4 banks for rows r and r + 4: the 16-B unit u of row r is stored at u ^ f((r >> 2) & 3)
+// with f = {0, 2, 3, 1}, which gives every gfx950 b128 lane group 16 distinct 4-bank groups (checked
+// by hand over the four groups); the XOR goes on the global source address (glds writes lane-linearly).
+namespace mf16 {
+using mf::bf16x8;
+using mf::f32x4;
+using mf::rsrc_t;
+using mf::lds_void;
+constexpr int kTile = mf::kTile, kThreads = mf::kThreads, kQ = mf::kQ, kNJ = mf::kNJ, kSteps = mf::kSteps;
+constexpr int kChunk = kTile * 64;        // 16 KB of bf16 per K-chunk
+constexpr int kRing = mf::kRing, kAhead = mf::kAhead, kDist = mf::kDist;
+constexpr int kDma = kChunk / 1024 / 4;   // 4 wave-instructions per wave per chunk
+constexpr int kRsrcWord3 = mf::kRsrcWord3;
+struct Smem {
+  char ring[kRing * kChunk];  // 64 KB
+  __attribute__((aligned(16))) float inv[kTile];
+  __attribute__((aligned(16))) int live[kTile];
+  uint32_t ncand[kQ];
+};
+__device__ __forceinline__ int fsw(int b) { return (0x1B2 >> (2 * b)) & 3; }  // {0, 2, 3, 1}[b]
+
+__device__ __forceinline__ rsrc_t tile_rsrc16(const spl::dev::Arena& a, long t, long slot_end) {
+  return __builtin_amdgcn_make_buffer_rsrc(a.vec16((size_t)mf::tile_start(t, slot_end)), 0, kTile * 1536, kRsrcWord3);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kThreads, 1) void k_search_mma16(spl_arena_t aa, const void* __restrict__ qf, int nq,
+                                                             long slot_begin, long slot_end, uint64_t mask,
+                                                             const float* __restrict__ thr_in, float* __restrict__ bmax,
+                                                             uint32_t* __restrict__ cnt, uint32_t* __restrict__ cand,
+                                                             int capb) {
+  __shared__ __attribute__((aligned(16))) Smem sm;
+  const spl::dev::Arena a = spl::dev::from_api(aa);
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int fr = lane & 15, fq = lane >> 4;
+  const long tile_base = slot_begin / kTile;
+  const long tile_end = (slot_end + kTile - 1) / kTile, G = gridDim.x;
+  const long t0 = tile_base + blockIdx.x;
+  if (t0 >= tile_end) return;  // block-uniform
+  if (MODE == 1) sm.ncand[threadIdx.x] = 0;
+
+  const rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(qf), 0, kQ * kD * 2, kRsrcWord3);
+  const int qvoff = lane * 16, qtile0 = wave * kNJ;
+  // DMA geometry: wave-instruction k of a chunk fills rows 64w + 16k .. +16 (1 KB), lane l -> row
+  // +(l >> 2), physical unit l & 3 <- logical unit (l & 3) ^ f(row >> 2)
+  int dvoff[kDma];
+#pragma unroll
+  for (int k = 0; k < kDma; ++k) {
+    const int row = wave * 64 + k * 16 + (lane >> 2);
+    dvoff[k] = row * 1536 + (((lane & 3) ^ fsw((row >> 2) & 3)) << 4);
+  }
+  const float* nrm2 = a.nrm2();
+  // fragment read: row 16i + fr, logical unit fq
+  const int rdo = fr * 64 + ((fq ^ fsw((fr >> 2) & 3)) << 4);
+
+  float thr[kNJ];
+#pragma unroll
+  for (int j = 0; j < kNJ; ++j) {
+    const int q = (qtile0 + j) * 16 + fr;
+    thr[j] = (MODE == 1 && q < nq) ? thr_in[q] : FLT_MAX;
+  }
+  auto issue = [&](rsrc_t er, int c, int slot) {
+    char* dst = sm.ring + slot * kChunk + wave * 64 * 64;
+#pragma unroll
+    for (int k = 0; k < kDma; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(er, (lds_void*)(dst + k * 1024), 16, dvoff[k], c * 64, 0, 0);
+  };
+  const long last = tile_end - 1;
+
+  bf16x8 b[kDist + 1][kNJ];
+#pragma unroll
+  for (int s = 0; s < kDist; ++s)
+#pragma unroll
+    for (int j = 0; j < kNJ; ++j) b[s][j] = mf::load_qfrag(qr, qvoff, qtile0 + j, s);
+  {
+    const rsrc_t er = tile_rsrc16(a, t0, slot_end);
+    for (int c = 0; c < kAhead; ++c) issue(er, c, c);
+  }
+
+  for (long t = t0; t < tile_end; t += G) {
+    const long start = mf::tile_start(t, slot_end);
+    const rsrc_t er_cur = tile_rsrc16(a, t, slot_end);
+    const rsrc_t er_next = tile_rsrc16(a, t + G < tile_end ? t + G : last, slot_end);
+    uint64_t h = 0, bl = 0;
+    float n2 = 0.f;
+    f32x4 acc[16][kNJ];
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+#pragma clang loop unroll(full)
+    for (int s = 0; s < kSteps; ++s) {
+      // in-order vmcnt accounting as k_search_mma: per step the query fragments (4 loads), at step 0
+      // the metadata (3 loads: hash, bloom, norm), then the chunk DMA (4): younger than chunk s's DMA
+      // at the top of step s are the two following steps' ops: 16, or 19 when one was a step 0; the
+      // prologue (fragments 0..2, then DMA 0..2) gives lower bounds 8 at s = 0 and 15 at s = 1
+      if (s == 0)
+        SPL_STEP_SYNC(8);
+      else if (s == 1)
+        SPL_STEP_SYNC(15);
+      else if (s == 2)
+        SPL_STEP_SYNC(19);
+      else
+        SPL_STEP_SYNC(16);
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j)
+        b[(s + kDist) % (kDist + 1)][j] = mf::load_qfrag(qr, qvoff, qtile0 + j, (s + kDist) % kSteps);
+      if (s == 0) {  // metadata of this wave's 64 rows, one per lane
+        const long row = start + wave * 64 + lane;
+        const uint8_t* sp = a.slot((size_t)row);
+        h = __builtin_nontemporal_load((const uint64_t*)(sp + spl::kOffHash));
+        bl = __builtin_nontemporal_load((const uint64_t*)(sp + spl::kOffBloom));
+        n2 = __builtin_nontemporal_load(nrm2 + row);
+      }
+      issue(s + kAhead < kSteps ? er_cur : er_next, (s + kAhead) % kSteps, (s + kAhead) % kRing);
+      const char* ch = sm.ring + (s % kRing) * kChunk + rdo;
+#pragma unroll
+      for (int i0 = 0; i0 < 16; i0 += 4) {
+        bf16x8 af[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) af[u] = *(const bf16x8*)(ch + (i0 + u) * 1024);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+#pragma unroll
+          for (int j = 0; j < kNJ; ++j)
+            acc[i0 + u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], b[s % (kDist + 1)][j], acc[i0 + u][j], 0, 0, 0);
+      }
+    }
+    {
+      constexpr float kMinNorm2 = MODE == 0 ? 2e-12f : 0.f;  // MODE 0 counts surely-live slots only
+      const int row = wave * 64 + lane;
+      sm.live[row] = h != 0 && (!mask || (bl & mask) == mask) && n2 > kMinNorm2 && start + row >= t * kTile;
+      sm.inv[row] = n2 > 0.f ? rsqrtf(n2) : 0.f;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    {
+      const f32x4* invp = (const f32x4*)(sm.inv + fq * 4);
+      const int4* livp = (const int4*)(sm.live + fq * 4);
+      float best[kNJ];
+#pragma unroll
+      for (int j = 0; j < kNJ; ++j) best[j] = -FLT_MAX;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const f32x4 iv = invp[i * 4];
+        const int4 lv = livp[i * 4];
+        const int lvr[4] = {lv.x, lv.y, lv.z, lv.w};
+#pragma unroll
+        for (int j = 0; j < kNJ; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const float sim = acc[i][j][r] * iv[r];
+            if (MODE == 0) {
+              if (lvr[r]) best[j] = fmaxf(best[j], sim);
+            } else if (sim >= thr[j] && lvr[r]) {
+              const int q = (qtile0 + j) * 16 + fr;
+              const uint32_t p = atomicAdd(&sm.ncand[q], 1u);
+              if (p < (uint32_t)capb) cand[((long)q * gridDim.x + blockIdx.x) * capb + p] = (uint32_t)(start + i * 16 + fq * 4 + r);
+            }
+          }
+      }
+      if (MODE == 0) {
+#pragma unroll
+        for (int j = 0; j < kNJ; ++j) {
+          const int q = (qtile0 + j) * 16 + fr;
+          float bj = fmaxf(best[j], __shfl_xor(best[j], 16, 64));
+          bj = fmaxf(bj, __shfl_xor(bj, 32, 64));
+          if (fq == 0 && q < nq) bmax[(t - tile_base) * nq + q] = bj;
+        }
+      }
+    }
+  }
+  if (MODE == 1) {
+    mf::raw_barrier();
+    const int q = threadIdx.x;
+    if (q < nq) cnt[(long)q * gridDim.x + blockIdx.x] = sm.ncand[q];
+  }
+  mf::wait_vm0();
+}
+}  // namespace mf16
+
+namespace mf {
 // fp32 re-score of the candidates of one query (block) and top-K selection;
 // same arithmetic as k_score_topk so the ranking is identical.  Candidates
 // come in block-private segments cand[q][b][0 .. min(cnt[q][b], capb)).
@@ -622,6 +814,21 @@ int spl_search_mma_pass(spl_arena_t a, const void* qfrag, int nq, long slot_begi
       (mode == 1 && (!thr || !cnt || !cand || capb <= 0)) || (mode == 0 && !bmax))
     return (int)hipErrorInvalidValue;
   const long tiles = (slot_end - slot_begin + mf::kTile - 1) / mf::kTile;
+  // the bf16 copy when the arena carries one (SPLINTER_SEARCH_VEC16=0: the fp32 rows)
+  static const bool v16_ok = [] {
+    const char* e = getenv("SPLINTER_SEARCH_VEC16");
+    return !(e && e[0] == '0');
+  }();
+  if ((a.flags & SPL_ARENA_VEC16) && v16_ok) {
+    const int g = mode == 0 ? (int)(grid < tiles ? grid : tiles) : grid;
+    if (mode == 0)
+      hipLaunchKernelGGL(mf16::k_search_mma16<0>, dim3(g), dim3(mf16::kThreads), 0, s, a, qfrag, nq, slot_begin,
+                         slot_end, mask, thr, bmax, cnt, cand, capb);
+    else
+      hipLaunchKernelGGL(mf16::k_search_mma16<1>, dim3(g), dim3(mf16::kThreads), 0, s, a, qfrag, nq, slot_begin,
+                         slot_end, mask, thr, bmax, cnt, cand, capb);
+    return (int)hipGetLastError();
+  }
   if (mode == 0) {
     const int g = (int)(grid < tiles ? grid : tiles);
     hipLaunchKernelGGL(mf::k_search_mma<0>, dim3(g), dim3(mf::kThreads), 0, s, a, qfrag, nq, slot_begin, slot_end,

@@ -22,9 +22,13 @@ typedef struct spl_arena {
   uint32_t slots;
   uint32_t max_val;
   uint32_t stride;    /* 128 or 3200 */
-  uint32_t flags;     /* bit0: event bus armed (maintain dirty mask) */
+  uint32_t flags;     /* SPL_ARENA_* */
   uint64_t notify;    /* device address of the host-mapped event-bus notify word (0 = none) */
 } spl_arena_t;
+
+#define SPL_ARENA_EVENTBUS 1u  /* event bus armed (maintain the dirty mask) */
+#define SPL_ARENA_SIDE     2u  /* the allocation carries the side region (splinter_layout.hpp) */
+#define SPL_ARENA_VEC16    4u  /* ... with the bf16 vector copy + squared norms (embedding stores) */
 
 #ifndef __HIP_PLATFORM_AMD__
 typedef void *hipStream_t;
@@ -83,6 +87,13 @@ int spl_arena_scan(spl_arena_t a, int mode, uint64_t mask, uint32_t *out_idx, ui
 int spl_arena_scan_range(spl_arena_t a, int mode, uint64_t mask, uint32_t first, uint32_t last, uint32_t *out_idx,
                          uint64_t *out_epoch, uint32_t cap, uint32_t *counter, hipStream_t stream);
 int spl_arena_purge(spl_arena_t a, hipStream_t stream);
+/* maintenance passes (arena_maint.hip): probe-chain statistics into a zeroed device ProbeStats
+ * (splinter_layout.hpp / spl_probe_stats); the tombstone rebuild (EXCLUSIVE access; counters:
+ * device u64[4] {moved, reclaimed, clusters, skipped}, zeroed); the bf16 vector copy rebuilt from
+ * the fp32 vectors (SPL_ARENA_VEC16 arenas) */
+int spl_arena_probe_stats(spl_arena_t a, void *out, hipStream_t stream);
+int spl_arena_rehash(spl_arena_t a, void *counters, hipStream_t stream);
+int spl_arena_vec16_rebuild(spl_arena_t a, hipStream_t stream);
 int spl_arena_gather_slots(spl_arena_t a, const uint32_t *idx, long n, uint8_t *out_core, hipStream_t stream);
 int spl_hash_keys(const char *keys, int kstride, long n, uint64_t *out, hipStream_t stream);
 int spl_format_keys(char *out, int kstride, const uint64_t *ids, uint64_t first, long n, const char *prefix_dev,

@@ -96,6 +96,24 @@ typedef struct spl_search_hit {
 long  spl_hbm_search(spl_store *s, const float *query, uint64_t mask, float min_sim, float max_dist, long cap,
                      spl_search_hit *out);
 
+/* Probe-chain health of an HBM store (summed over a node store's shards): one device pass over the
+ * slots.  disp_*: probe length of a hit per live key; miss_*: probe length of a miss averaged over
+ * every home position (a miss walks to the next never-used slot); hist[b]: live keys with probe
+ * length 1, 2, 3-4, 5-8, ..., > 1024.  rebuilds / reclaimed / moved: spl_hbm_rehash history. */
+typedef struct spl_probe_stats {
+  uint64_t live, tombstones, virgin, busy;
+  uint64_t disp_sum, disp_max, miss_sum, miss_max;
+  uint64_t hist[12];
+  uint64_t rebuilds, reclaimed, moved, pad;
+} spl_probe_stats;
+int   spl_hbm_probe_stats(spl_store *s, spl_probe_stats *out);
+/* Tombstone rebuild: every live key moves into the first tombstone on its own probe path and the
+ * tombstones left at the end of each cluster become never-used slots again, so misses stop at the
+ * cluster's new end.  EXCLUSIVE maintenance (like a compaction): no other process may run batch ops
+ * on the store meanwhile; the store's per-call ring is held for the pass.  out (optional):
+ * {keys moved, tombstones reclaimed, clusters, clusters with more than 1024 tombstones}. */
+int   spl_hbm_rehash(spl_store *s, uint64_t *out);
+
 /* Node stores ("node:NAME", node_store.hpp): one store over a node's per-GPU arenas, key-sharded
  * by ((fnv1a(key) >> 40) & 0xFFFFFF) % nshards.  splinter_create("node:NAME", slots, max_val)
  * creates every shard from one process (SPLINTER_NODE_SHARDS, SPLINTER_NODE_BACKEND=hbm|shm);

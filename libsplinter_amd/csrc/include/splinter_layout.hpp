@@ -34,6 +34,47 @@ constexpr size_t kOffHash = 0, kOffEpoch = 8, kOffValOff = 16, kOffValLen = 20,
                  kOffType = 24, kOffUser = 25, kOffWatch = 32, kOffCtime = 40,
                  kOffAtime = 48, kOffBloom = 56, kOffKey = 64, kOffEmbed = 128;
 
+// Side region of an HBM arena (not part of the v4 file format: runtime data of one allocation,
+// never checkpointed, rebuilt on restore).  It follows the value area at a 4-KiB boundary:
+//   [0, 4 KiB)            ArenaSide: probe-chain statistics written by the maintenance passes
+//   nrm2 [slots] float    embedding stores only: squared norm of each slot's vector (0 = none)
+//   vec16 [slots][768]    embedding stores only: the vector in bf16 (round to nearest even), the
+//                         operand the batched search's candidate pass streams (half the bytes of
+//                         the fp32 rows, contiguous); written under the slot's seqlock with the
+//                         fp32 vector by every embedding writer
+constexpr size_t kSideAlign = 4096;
+constexpr size_t kSideHdrBytes = 4096;
+constexpr size_t kVec16Bytes = kEmbedDim * 2;
+SPL_HD size_t side_align_up(size_t v) { return (v + kSideAlign - 1) / kSideAlign * kSideAlign; }
+// offset of the side region from the header, for a geometry
+SPL_HD size_t side_offset(size_t slots, size_t stride, size_t max_val) {
+  return side_align_up(kHeaderBytes + slots * stride + slots * max_val);
+}
+SPL_HD size_t side_nrm2_offset() { return kSideHdrBytes; }
+SPL_HD size_t side_vec16_offset(size_t slots) { return kSideHdrBytes + side_align_up(slots * 4); }
+SPL_HD size_t side_bytes(size_t slots, bool vec16) {
+  return vec16 ? side_vec16_offset(slots) + slots * kVec16Bytes : kSideHdrBytes;
+}
+
+// probe-chain statistics (ArenaSide, and spl_hbm_probe_stats): a pass over the slot array
+constexpr int kProbeBuckets = 12;  // probe lengths 1, 2, 3-4, 5-8, ..., 513-1024, > 1024
+struct ProbeStats {
+  uint64_t live;          // slots holding a key
+  uint64_t tombstones;    // hash 0, even epoch != 0 (unset / reclaimed): lookups walk past them
+  uint64_t virgin;        // hash 0, epoch 0: a chain ends here
+  uint64_t busy;          // odd epoch (a writer in flight)
+  uint64_t disp_sum;      // sum of (probe length of a hit) over live keys
+  uint64_t disp_max;
+  uint64_t miss_sum;      // sum over home positions of the probe length of a miss (to the next virgin)
+  uint64_t miss_max;
+  uint64_t hist[kProbeBuckets];  // live keys by probe length of a hit
+  uint64_t rebuilds;      // spl_hbm_rehash passes run on this arena
+  uint64_t reclaimed;     // tombstones turned back into virgin slots (purge / rehash)
+  uint64_t moved;         // keys moved toward their home slot (rehash)
+  uint64_t pad[1];
+};
+static_assert(sizeof(ProbeStats) % 16 == 0, "16-B rows");
+
 static_assert(sizeof(splinter_header) == kHeaderBytes, "v4 header must be 5440 B");
 static_assert(alignof(splinter_header) == 64, "header alignment");
 static_assert(sizeof(splinter_slot) == kSlotCoreBytes, "slot core must be 128 B");

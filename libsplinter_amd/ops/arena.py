@@ -343,6 +343,28 @@ class HbmArena:
     def header_view(self) -> torch.Tensor:
         return _device_view(self.desc.base, 5440)
 
+    # side region (csrc/include/splinter_layout.hpp): present on arenas created by this build
+    SIDE_ALIGN, SIDE_HDR = 4096, 4096
+
+    def _side_base(self) -> int:
+        al = lambda v: (v + self.SIDE_ALIGN - 1) // self.SIDE_ALIGN * self.SIDE_ALIGN  # noqa: E731
+        return self.desc.base + al(5440 + self.slots * self.stride + self.slots * self.max_val)
+
+    @property
+    def has_vec16(self) -> bool:
+        return bool(self.desc.flags & 4)
+
+    def vec16_view(self) -> Tuple[torch.Tensor, torch.Tensor]:
+        """(nrm2 [slots] fp32, vec16 [slots, 768] bf16): the side region's squared norms and bf16
+        vector copy that the batched search streams (zero copy)."""
+        if not self.has_vec16:
+            raise ValueError("arena has no bf16 vector copy")
+        al = lambda v: (v + self.SIDE_ALIGN - 1) // self.SIDE_ALIGN * self.SIDE_ALIGN  # noqa: E731
+        sb = self._side_base()
+        nrm2 = _device_view(sb + self.SIDE_HDR, self.slots * 4, dtype=torch.float32)
+        v16 = _device_view(sb + self.SIDE_HDR + al(self.slots * 4), self.slots * 768 * 2).view(torch.bfloat16)
+        return nrm2, v16.view(self.slots, 768)
+
     def checkpoint(self, path: str) -> None:
         torch.cuda.synchronize()
         if self._H.spl_hbm_checkpoint(self.store.handle, path.encode()) != 0:

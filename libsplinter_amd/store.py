@@ -566,6 +566,39 @@ class Store:
         e2 = self.epochs()
         return [int(i) for i in np.nonzero((e1 & 1) & (e1 == e2))[0]]
 
+    # ------------------------------------------------- probe-chain health (hbm: / node: of HBM) --
+    _PROBE_FIELDS = ("live", "tombstones", "virgin", "busy", "disp_sum", "disp_max", "miss_sum", "miss_max")
+
+    def probe_stats(self) -> dict:
+        """One device pass over the slots (spl_hbm_probe_stats): live / tombstone / never-used counts,
+        the probe length of a hit per live key (mean, max, histogram over 1, 2, 3-4, ..., >1024) and of
+        a miss averaged over every home position, plus the rehash history."""
+        L = N.hip_lib()
+        buf = (ctypes.c_uint64 * 24)()
+        L.spl_hbm_probe_stats.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.spl_hbm_probe_stats.restype = ctypes.c_int
+        if L.spl_hbm_probe_stats(self._h, buf) != 0:
+            _raise(f"probe_stats {self.name}")
+        v = list(buf)
+        d = dict(zip(self._PROBE_FIELDS, v[:8]))
+        d["hist"] = v[8:20]
+        d["rebuilds"], d["reclaimed"], d["moved"] = v[20:23]
+        d["hit_mean"] = d["disp_sum"] / d["live"] if d["live"] else 0.0
+        d["miss_mean"] = d["miss_sum"] / self.slots if d["virgin"] else float(self.slots)
+        return d
+
+    def rehash(self) -> dict:
+        """Tombstone rebuild (spl_hbm_rehash): keys move into tombstones on their own probe path and
+        the tombstones left at the end of each cluster become never-used slots.  Exclusive
+        maintenance: no other process may run batch ops on the store meanwhile."""
+        L = N.hip_lib()
+        out = (ctypes.c_uint64 * 4)()
+        L.spl_hbm_rehash.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.spl_hbm_rehash.restype = ctypes.c_int
+        if L.spl_hbm_rehash(self._h, out) != 0:
+            _raise(f"rehash {self.name}")
+        return dict(zip(("moved", "reclaimed", "clusters", "skipped"), list(out)))
+
     def __repr__(self):
         return (f"Store({self.name!r}, backend={self.backend}, slots={self.slots}, max_val={self.max_val}, "
                 f"embeddings={self.embeddings})")

@@ -453,6 +453,7 @@ class HbmStore final : public StoreBase {
   // ---------------------------------------------------- bulk / helpers --
   int checkpoint(const char* path);
   long search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap, spl_search_hit* out);
+  long search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask, spl_search_hit* out);
   int restore_from(const char* path);
   int probe_stats(ProbeStats* out);
   int rehash(uint64_t out[4]);
@@ -1007,6 +1008,157 @@ long HbmStore::search_all(const float* q, uint64_t mask, float min_sim, float ma
   return total;
 }
 
+// Batched top-k search of many queries (the C form of ops/search.py VectorSearch.search_batch, on the
+// MFMA passes of search_kernels.hip): per block of 256 queries a bf16 pass over a slot sample gives a
+// per-query candidate threshold (k-th largest per-tile maximum - 2 delta), a bf16 pass over the
+// whole arena (the side region's bf16 copy where the arena has one) emits the candidates above it,
+// and an fp32 re-score with the exact kernel's arithmetic ranks them; a query whose candidate
+// segment overflowed anywhere is redone with the exact kernel.  Results: out[q * k + j], ranked by
+// similarity desc, distance asc (reference splinter_cli_cmd_search.c:374-416); unused entries have
+// an empty key and emb = 0.  Returns nq, or -1.
+namespace {
+constexpr int kMmaQ = 256, kMmaTile = 256, kMmaGrid = 256, kCapb = 64, kExactQ = 16, kExactGrid = 512;
+constexpr float kDelta = 0.0078125f + 1.52587890625e-05f + 4e-4f;  // 2^-7 + 2^-16 + 4e-4 (ops/search.py DELTA)
+struct CandRec {
+  float sim, dist;
+  uint32_t idx, pad;
+};
+inline uint16_t f2bf_host(float f) {  // round to nearest even (finite inputs)
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  u += 0x7FFFu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+}  // namespace
+
+long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask,
+                            spl_search_hit* out) {
+  if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
+  if (nq <= 0 || k <= 0 || k > 32 || !q || !out) { errno = EINVAL; return -1; }
+  if (!ensure_mapped()) return -1;
+  DevGuard dg(device_);
+  std::lock_guard<std::mutex> lk(mu_);
+  const spl_arena_t a = arena();
+  const long slots = geo_.slots;
+  std::vector<CandRec> res((size_t)nq * k);
+  const bool bounded = max_dist < 3.0e38f;
+  const bool mma = nq >= 32 && slots >= kMmaTile;
+  long sample = std::min<long>(slots, std::max<long>((long)kMmaTile * 4096, slots / 16));
+  sample = std::max<long>(kMmaTile, sample / kMmaTile * kMmaTile);
+  // device buffers (stream-ordered)
+  float *d_q = nullptr, *d_thr = nullptr, *d_bmax = nullptr;
+  uint16_t* d_qf = nullptr;
+  uint32_t *d_cnt = nullptr, *d_cand = nullptr;
+  void *d_res = nullptr, *d_scr = nullptr;
+  const int lists = spl_search_lists(kExactGrid);
+  bool ok = hipMallocAsync((void**)&d_q, (size_t)kMmaQ * kEmbedBytes, stream_) == hipSuccess &&
+            hipMallocAsync(&d_res, (size_t)kMmaQ * 32 * sizeof(CandRec), stream_) == hipSuccess &&
+            hipMallocAsync(&d_scr, (size_t)lists * kExactQ * 32 * sizeof(CandRec), stream_) == hipSuccess;
+  if (ok && mma)
+    ok = hipMallocAsync((void**)&d_qf, (size_t)kMmaQ * kEmbedDim * 2, stream_) == hipSuccess &&
+         hipMallocAsync((void**)&d_thr, (size_t)kMmaQ * 4, stream_) == hipSuccess &&
+         hipMallocAsync((void**)&d_bmax, (size_t)(sample / kMmaTile) * kMmaQ * 4, stream_) == hipSuccess &&
+         hipMallocAsync((void**)&d_cnt, (size_t)kMmaQ * kMmaGrid * 4, stream_) == hipSuccess &&
+         hipMallocAsync((void**)&d_cand, (size_t)kMmaQ * kMmaGrid * kCapb * 4, stream_) == hipSuccess;
+  auto exact = [&](const float* hq, int n, CandRec* dst) -> bool {  // nq <= kExactQ per launch
+    for (int b = 0; b < n; b += kExactQ) {
+      const int m = std::min(kExactQ, n - b);
+      if (hipMemcpyAsync(d_q, hq + (size_t)b * kEmbedDim, (size_t)m * kEmbedBytes, hipMemcpyHostToDevice, stream_) !=
+              hipSuccess ||
+          spl_search(a, d_q, m, k, min_sim, max_dist, mask, kExactGrid, d_scr, d_res, stream_) != 0 ||
+          hipMemcpyAsync(dst + (size_t)b * k, d_res, (size_t)m * k * sizeof(CandRec), hipMemcpyDeviceToHost,
+                         stream_) != hipSuccess ||
+          hipStreamSynchronize(stream_) != hipSuccess)
+        return false;
+    }
+    return true;
+  };
+  std::vector<uint16_t> qb;
+  std::vector<uint16_t> qf;
+  std::vector<uint32_t> cnt;
+  std::vector<float> thr_h;
+  for (int b = 0; ok && b < nq; b += kMmaQ) {
+    const int n = std::min(kMmaQ, nq - b);
+    const float* hq = q + (size_t)b * kEmbedDim;
+    if (!mma) {
+      ok = exact(hq, n, res.data() + (size_t)b * k);
+      continue;
+    }
+    // normalised bf16 queries, zero-padded to 256, in fragment order [q/16][24 steps][4 kq][16 r][8]
+    qb.assign((size_t)kMmaQ * kEmbedDim, 0);
+    for (int i = 0; i < n; ++i) {
+      double nn = 0;
+      for (size_t d = 0; d < kEmbedDim; ++d) nn += (double)hq[i * kEmbedDim + d] * hq[i * kEmbedDim + d];
+      const float inv = nn > 1e-60 ? (float)(1.0 / std::sqrt(nn)) : 0.f;
+      for (size_t d = 0; d < kEmbedDim; ++d) qb[(size_t)i * kEmbedDim + d] = f2bf_host(hq[i * kEmbedDim + d] * inv);
+    }
+    qf.resize(qb.size());
+    for (int t = 0; t < kMmaQ / 16; ++t)
+      for (int st = 0; st < 24; ++st)
+        for (int kq = 0; kq < 4; ++kq)
+          for (int r = 0; r < 16; ++r)
+            std::memcpy(&qf[((((size_t)t * 24 + st) * 4 + kq) * 16 + r) * 8],
+                        &qb[(size_t)(t * 16 + r) * kEmbedDim + st * 32 + kq * 8], 16);
+    const float floor_v = min_sim - kDelta;
+    ok = hipMemcpyAsync(d_qf, qf.data(), qf.size() * 2, hipMemcpyHostToDevice, stream_) == hipSuccess &&
+         hipMemcpyAsync(d_q, hq, (size_t)n * kEmbedBytes, hipMemcpyHostToDevice, stream_) == hipSuccess;
+    if (ok && !bounded) {
+      ok = spl_search_mma_pass(a, d_qf, n, 0, sample, mask, 0, nullptr, d_bmax, nullptr, nullptr, 0, kMmaGrid,
+                               stream_) == 0 &&
+           spl_search_thr(d_bmax, (int)(sample / kMmaTile), n, k, 2 * kDelta, floor_v, d_thr, stream_) == 0;
+    } else if (ok) {
+      thr_h.assign((size_t)n, floor_v);
+      ok = hipMemcpyAsync(d_thr, thr_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream_) == hipSuccess;
+    }
+    ok = ok && hipMemsetAsync(d_cnt, 0, (size_t)n * kMmaGrid * 4, stream_) == hipSuccess &&
+         spl_search_mma_pass(a, d_qf, n, 0, slots, mask, 1, d_thr, nullptr, d_cnt, d_cand, kCapb, kMmaGrid,
+                             stream_) == 0 &&
+         spl_search_rescore(a, d_q, n, k, min_sim, max_dist, mask, d_cnt, d_cand, kMmaGrid, kCapb, d_res, stream_) ==
+             0;
+    cnt.resize((size_t)n * kMmaGrid);
+    ok = ok && hipMemcpyAsync(res.data() + (size_t)b * k, d_res, (size_t)n * k * sizeof(CandRec),
+                              hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+         hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+         hipStreamSynchronize(stream_) == hipSuccess;
+    // overflowed queries: the exact kernel
+    for (int i = 0; ok && i < n; ++i) {
+      bool over = false;
+      for (int g = 0; g < kMmaGrid && !over; ++g) over = cnt[(size_t)i * kMmaGrid + g] > (uint32_t)kCapb;
+      if (over) ok = exact(hq + (size_t)i * kEmbedDim, 1, res.data() + (size_t)(b + i) * k);
+    }
+  }
+  for (void* p : {(void*)d_q, (void*)d_thr, (void*)d_bmax, (void*)d_qf, (void*)d_cnt, (void*)d_cand, d_res, d_scr})
+    if (p) (void)hipFreeAsync(p, stream_);
+  (void)hipStreamSynchronize(stream_);
+  if (!ok) { errno = EIO; return -1; }
+  // slot indices -> keys and slot metadata (one gather of the slot cores)
+  std::vector<uint32_t> idx;
+  idx.reserve(res.size());
+  for (const CandRec& c : res)
+    if (c.idx != 0xffffffffu) idx.push_back(c.idx);
+  fetch_cores(idx);
+  size_t p = 0;
+  for (size_t i = 0; i < res.size(); ++i) {
+    spl_search_hit& h = out[i];
+    std::memset(&h, 0, sizeof h);
+    if (res[i].idx == 0xffffffffu) {
+      h.sim = -3.4e38f;
+      continue;
+    }
+    const uint8_t* core = list_cache_.data() + (p++) * 128;
+    std::memcpy(h.key, core + kOffKey, 64);
+    h.key[63] = 0;
+    h.emb = 1;
+    h.sim = res[i].sim;
+    h.dist = res[i].dist;
+    std::memcpy(&h.epoch, core + kOffEpoch, 8);
+    std::memcpy(&h.bloom, core + kOffBloom, 8);
+    std::memcpy(&h.len, core + kOffValLen, 4);
+    h.type = core[kOffType];
+  }
+  return nq;
+}
+
 // Checkpoint: stream the device image into a v4 store file (byte-identical
 // layout, so the host backend — or the reference library — can open it).
 int HbmStore::checkpoint(const char* path) {
@@ -1445,6 +1597,45 @@ long spl_hbm_search(spl_store* h, const float* query, uint64_t mask, float min_s
   const size_t keep = (size_t)std::min<long>((long)all.size(), std::max<long>(cap, 0));
   for (size_t i = 0; i < keep; ++i) out[i] = all[i];
   return total;
+}
+
+// Batched top-k search (HbmStore::search_batch) of an HBM store, or of a node store of HBM shards:
+// every shard answers every query on its GPU, and the per-shard top-k lists are merged per query
+// (similarity desc, distance asc) -- the in-process C4 merge.  out[nq * k]; returns nq or < 0.
+long spl_search_batch(spl_store* h, const float* queries, int nq, int k, float min_sim, float max_dist,
+                      uint64_t mask, spl_search_hit* out) {
+  if (!h || !queries || !out || nq <= 0 || k <= 0 || k > 32) return -2;
+  if (auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h))
+    return s->search_batch(queries, nq, k, min_sim, max_dist, mask, out);
+  const int n = spl_node_nshards(h);
+  if (n < 1) return -2;
+  std::vector<spl_search_hit> part((size_t)nq * k);
+  std::vector<std::vector<spl_search_hit>> all((size_t)nq);
+  for (int i = 0; i < n; ++i) {
+    auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+    if (!s || s->search_batch(queries, nq, k, min_sim, max_dist, mask, part.data()) != nq) return -1;
+    for (int qi = 0; qi < nq; ++qi)
+      for (int j = 0; j < k; ++j)
+        if (part[(size_t)qi * k + j].emb) all[qi].push_back(part[(size_t)qi * k + j]);
+  }
+  auto better = [](const spl_search_hit& a, const spl_search_hit& b) {
+    if (a.sim != b.sim) return a.sim > b.sim;
+    if (a.dist != b.dist) return a.dist < b.dist;
+    return strncmp(a.key, b.key, 64) < 0;
+  };
+  for (int qi = 0; qi < nq; ++qi) {
+    std::sort(all[qi].begin(), all[qi].end(), better);
+    for (int j = 0; j < k; ++j) {
+      spl_search_hit& o = out[(size_t)qi * k + j];
+      if ((size_t)j < all[qi].size()) {
+        o = all[qi][j];
+      } else {
+        std::memset(&o, 0, sizeof o);
+        o.sim = -3.4e38f;
+      }
+    }
+  }
+  return nq;
 }
 
 // Probe-chain statistics of an HBM store, or summed over the shards of a node store (maxima taken)

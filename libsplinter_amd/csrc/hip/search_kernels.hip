@@ -721,6 +721,48 @@ __global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __
 }
 }  // namespace mf
 
+// Candidate threshold per query for the batched search (ops/search.py search_batch, spl_search_batch):
+// thr[q] = max(k-th largest of bmax[0..T)[q] - 2 delta, floor); fewer than k tiles: floor.  One block
+// per query: every thread keeps the k largest of its strided share, then k rounds of a block max
+// (the winner drops its head).
+__global__ __launch_bounds__(256) void k_search_thr(const float* __restrict__ bmax, int T, int nq, int k, float delta2,
+                                                    float floor_v, float* __restrict__ thr) {
+  __shared__ float wv[4];
+  __shared__ int wi[4];
+  const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  float top[kMaxK];
+  int n = 0;
+  for (int t = tid; t < T; t += 256) {
+    const float v = bmax[(long)t * nq + q];
+    if (n == k && v <= top[k - 1]) continue;
+    int p = n < k ? n : k - 1;
+    while (p > 0 && top[p - 1] < v) { top[p] = top[p - 1]; --p; }
+    top[p] = v;
+    n = n < k ? n + 1 : n;
+  }
+  int head = 0;
+  float kth = -FLT_MAX;
+  for (int r = 0; r < k; ++r) {
+    float v = head < n ? top[head] : -FLT_MAX;
+    int who = tid;
+    for (int o = 32; o > 0; o >>= 1) {
+      const float ov = __shfl_xor(v, o, 64);
+      const int oi = __shfl_xor(who, o, 64);
+      if (ov > v || (ov == v && oi < who)) { v = ov; who = oi; }
+    }
+    if (lane == 0) { wv[wave] = v; wi[wave] = who; }
+    __syncthreads();
+    float bv = wv[0];
+    int bi = wi[0];
+    for (int w = 1; w < 4; ++w)
+      if (wv[w] > bv || (wv[w] == bv && wi[w] < bi)) { bv = wv[w]; bi = wi[w]; }
+    __syncthreads();
+    if (bi == tid) ++head;
+    kth = bv;
+  }
+  if (tid == 0) thr[q] = (T < k || kth == -FLT_MAX) ? floor_v : fmaxf(kth - delta2, floor_v);
+}
+
 // CLI `search` over an HBM store (reference splinter_cli_cmd_search.c:339-416): every candidate
 // slot -- live (hash != 0) and either carrying every bloom bit of `mask`, or, without a mask,
 // holding a value (the reference's splinter_list) -- gets {sim, dist}: cosine and euclidean
@@ -839,6 +881,13 @@ int spl_search_mma_pass(spl_arena_t a, const void* qfrag, int nq, long slot_begi
     hipLaunchKernelGGL(mf::k_search_mma<1>, dim3(grid), dim3(mf::kThreads), 0, s, a, qfrag, nq, slot_begin, slot_end,
                        mask, thr, bmax, cnt, cand, capb);
   }
+  return (int)hipGetLastError();
+}
+
+int spl_search_thr(const float* bmax, int tiles, int nq, int K, float delta2, float floor_v, float* thr,
+                   hipStream_t s) {
+  if (nq <= 0 || K <= 0 || K > kMaxK || tiles < 0 || !thr) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_search_thr, dim3(nq), dim3(256), 0, s, bmax, tiles, nq, K, delta2, floor_v, thr);
   return (int)hipGetLastError();
 }
 

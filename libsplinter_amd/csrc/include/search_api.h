@@ -29,6 +29,9 @@ int spl_search_mma_tile(void);
 int spl_search_mma_pass(spl_arena_t a, const void *qfrag, int nq, long slot_begin, long slot_end, uint64_t mask,
                         int mode, const float *thr, float *bmax, uint32_t *cnt, uint32_t *cand, int capb, int grid,
                         hipStream_t stream);
+/* per-query candidate threshold from a bmax pass: max(k-th largest of bmax[tiles][nq] - delta2, floor) */
+int spl_search_thr(const float *bmax, int tiles, int nq, int K, float delta2, float floor_v, float *thr,
+                   hipStream_t stream);
 /* Exact fp32 re-score of the candidate segments (queries [nq, 768] fp32, unnormalised) and top-K:
  * result layout and ranking as spl_search. */
 int spl_search_rescore(spl_arena_t a, const float *queries, int nq, int K, float min_sim, float max_dist,

@@ -96,6 +96,15 @@ typedef struct spl_search_hit {
 long  spl_hbm_search(spl_store *s, const float *query, uint64_t mask, float min_sim, float max_dist, long cap,
                      spl_search_hit *out);
 
+/* Batched top-k of many queries [nq][768] fp32 (host) over an HBM store, or over every shard of a node
+ * store of HBM shards (merged per query): the MFMA candidate passes (on the bf16 vector copy of the
+ * arena's side region) with an exact fp32 re-score, so the ranking is the exact brute force's
+ * (similarity desc, distance asc; reference splinter_cli_cmd_search.c:374-416).  k <= 32; min_sim,
+ * max_dist filters (-2 / 3.4e38 = off); mask: bloom labels a slot must carry (0 = any).  out[nq * k]:
+ * query q's hits at out[q * k ...], unused entries with an empty key and emb = 0.  Returns nq. */
+long  spl_search_batch(spl_store *s, const float *queries, int nq, int k, float min_sim, float max_dist,
+                       uint64_t mask, spl_search_hit *out);
+
 /* Probe-chain health of an HBM store (summed over a node store's shards): one device pass over the
  * slots.  disp_*: probe length of a hit per live key; miss_*: probe length of a miss averaged over
  * every home position (a miss walks to the next never-used slot); hist[b]: live keys with probe

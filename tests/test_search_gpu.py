@@ -252,3 +252,78 @@ def test_cli_search_on_hbm_uses_device_scoring(uniq):
     finally:
         stop.set()
         a.close()
+
+
+class _Hit(__import__("ctypes").Structure):
+    import ctypes as _c
+    _fields_ = [("key", _c.c_char * 64), ("sim", _c.c_float), ("dist", _c.c_float), ("epoch", _c.c_uint64),
+                ("bloom", _c.c_uint64), ("len", _c.c_uint32), ("type", _c.c_uint8), ("emb", _c.c_uint8),
+                ("pad", _c.c_uint8 * 2)]
+
+
+def _c_search_batch(store, q, k, min_sim=-2.0, max_dist=3.4e38, mask=0):
+    import ctypes
+    from libsplinter_amd import _native as N
+    L = N.hip_lib()
+    L.spl_search_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                   ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p]
+    L.spl_search_batch.restype = ctypes.c_long
+    qn = np.ascontiguousarray(q, dtype=np.float32)
+    out = (_Hit * (qn.shape[0] * k))()
+    rc = L.spl_search_batch(store.handle, qn.ctypes.data, qn.shape[0], k, min_sim, max_dist, mask, out)
+    assert rc == qn.shape[0], rc
+    return [[(out[i * k + j].key.decode(), out[i * k + j].sim) if out[i * k + j].emb else None for j in range(k)]
+            for i in range(qn.shape[0])]
+
+
+@pytest.mark.parametrize("node", [False, True])
+def test_c_abi_search_batch_matches_numpy(uniq, node):
+    """spl_search_batch (splinter_ext.h) from C types: an hbm: store and a node: store of two HBM shards
+    (merged per query) against a float64 numpy brute force over the same vectors."""
+    import torch
+    from libsplinter_amd import Store
+    from libsplinter_amd.store import NODE_HBM, node_join, node_leave, node_shard_name
+    from libsplinter_amd.ops.arena import HbmArena, pack_keys, pack_values
+    g = torch.Generator().manual_seed(9)
+    n, nq, k = 9000, 64, 10
+    vecs = _clustered(n, g).numpy()
+    names = [f"e{i}" for i in range(n)]
+    stores, arenas = [], []
+    try:
+        if node:
+            for r in range(2):
+                nm = node_shard_name(uniq, r, NODE_HBM)
+                st = Store.create(nm, slots=8192, max_val=32, embeddings=True)
+                node_join(uniq, r, 2, NODE_HBM, st.slots, 32, True)
+                stores.append(st)
+            top = Store.open(f"node:{uniq}")
+        else:
+            top = Store.create(f"hbm:{uniq}", slots=12007, max_val=32, embeddings=True)
+            stores.append(top)
+        ok = top.set_batch(names, [b"x"] * n)
+        assert int((ok != 0).sum()) == 0
+        st2 = top.set_embedding_batch(names, vecs)
+        assert int((st2 != 0).sum()) == 0
+        q = _clustered(nq, g).numpy() * 2.0
+        q[0] = vecs[77]
+        got = _c_search_batch(top, q, k)
+        v64 = vecs.astype(np.float64)
+        vn = np.linalg.norm(v64, axis=1)
+        for i in range(nq):
+            sims = v64 @ q[i].astype(np.float64) / (vn * np.linalg.norm(q[i].astype(np.float64)))
+            order = np.argsort(-sims, kind="stable")[:k]
+            want = [names[j] for j in order]
+            keys = [h[0] for h in got[i]]
+            # ties within fp32 rounding may swap neighbours: compare as sets plus the leader
+            assert set(keys) == set(want), (i, keys, want)
+            assert keys[0] == want[0]
+            np.testing.assert_allclose([h[1] for h in got[i]], sims[order], rtol=2e-5, atol=2e-5)
+        assert got[0][0][0] == "e77"
+        if node:
+            top.close()
+    finally:
+        for st in stores:
+            st.close()
+        if node:
+            for r in range(2):
+                node_leave(uniq, r)

@@ -25,6 +25,7 @@
 //                   restore, or for an arena whose copy is missing).
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <algorithm>
 
 #include "arena_api.h"
 #include "arena_dev.hpp"
@@ -101,7 +102,7 @@ __global__ __launch_bounds__(kStatThreads) void k_probe_stats(spl_arena_t aa, Pr
 
 // ---------------------------------------------------------------- rehash --
 constexpr int kRhWaves = 4;        // waves per block, each its own slot range
-constexpr int kRhHoles = 1024;     // tombstones a wave keeps track of per cluster (more: no further moves)
+constexpr int kRhHoles = 1024;     // tombstones a wave keeps track of per cluster (a power of two; more: the oldest dropped)
 
 struct RhCounters {
   unsigned long long moved, reclaimed, clusters, skipped;
@@ -168,50 +169,57 @@ __global__ __launch_bounds__(64 * kRhWaves) void k_rehash(spl_arena_t aa, uint64
       m &= m - 1;
       const uint64_t cs = base + l;  // cluster start
       ++clusters;
-      int nh = 0;                    // holes (tombstone positions, in cluster order; wave-uniform count)
+      // holes: tombstone positions in cluster order, a ring of kRhHoles (h0 = oldest); when it is full
+      // the oldest hole is dropped (left a tombstone): later keys rarely have homes that far back
+      int nh = 0, h0 = 0;
       bool overflow = false;
+      auto H = [&](int t) -> uint32_t& { return holes[(h0 + t) & (kRhHoles - 1)]; };
       int64_t rl_used = -1;          // cluster-relative position of the last slot holding an entry
       uint64_t pos = cs, steps = 0;
       while (steps < n) {
         const uint8_t* s = a.slot(pos);
         // one value for the whole wave (exclusive access: nothing changes under the pass)
-        const uint64_t h = __builtin_amdgcn_readfirstlane((uint32_t)ald64(s + kOffHash)) |
-                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(ald64(s + kOffHash) >> 32)) << 32);
+        const uint64_t hv = ald64(s + kOffHash);
+        const uint64_t h = __builtin_amdgcn_readfirstlane((uint32_t)hv) |
+                           ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(hv >> 32)) << 32);
         const uint64_t e = ald64(s + kOffEpoch);
         const bool odd = __builtin_amdgcn_readfirstlane((uint32_t)(e & 1)) != 0;
         const bool zero_e = __builtin_amdgcn_readfirstlane((uint32_t)(e != 0)) == 0;
         const int64_t rp = (int64_t)cyc(pos, cs, n);
         if (h == 0 && zero_e) break;  // cluster end
         if (h == 0 && !odd) {
-          if (nh < kRhHoles) {
-            if (lane == 0) holes[nh] = (uint32_t)pos;
-            ++nh;
-          } else {
+          if (nh == kRhHoles) {  // full: drop the oldest
+            h0 = (h0 + 1) & (kRhHoles - 1);
+            --nh;
             overflow = true;
           }
-        } else if (!odd && nh > 0 && !overflow) {
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) H(nh) = (uint32_t)pos;
+          __builtin_amdgcn_wave_barrier();
+          ++nh;
+        } else if (!odd && nh > 0) {
           // live key: the first hole on its own probe path (rel(home) <= rel(hole) < rel(pos))
           const uint64_t rh = cyc(h % n, cs, n);
-          __builtin_amdgcn_wave_barrier();
           int k = -1;
           for (int t0 = 0; t0 < nh && k < 0; t0 += 64) {
             const int t = t0 + lane;
-            const bool ok = t < nh && cyc(holes[t < nh ? t : 0], cs, n) >= rh && (int64_t)cyc(holes[t < nh ? t : 0], cs, n) < rp;
+            const uint64_t rq = t < nh ? cyc(H(t), cs, n) : 0;
+            const bool ok = t < nh && rq >= rh && (int64_t)rq < rp;
             const uint64_t bm = __ballot(ok);
             if (bm) k = t0 + __builtin_ctzll(bm);
           }
           if (k >= 0) {
-            const uint64_t q = holes[k];
+            const uint64_t q = H(k);
             move_entry(a, q, pos, lane);
             ++moved;
             // drop hole k (order kept); the vacated slot is the newest hole
             for (int t = k; t < nh - 1; ++t) {
-              const uint32_t v = holes[t + 1];
+              const uint32_t v = H(t + 1);
               __builtin_amdgcn_wave_barrier();
-              if (lane == 0) holes[t] = v;
+              if (lane == 0) H(t) = v;
               __builtin_amdgcn_wave_barrier();
             }
-            if (lane == 0) holes[nh - 1] = (uint32_t)pos;
+            if (lane == 0) H(nh - 1) = (uint32_t)pos;
             __builtin_amdgcn_wave_barrier();
             const int64_t rq = (int64_t)cyc(q, cs, n);
             rl_used = rq > rl_used ? rq : rl_used;
@@ -227,7 +235,7 @@ __global__ __launch_bounds__(64 * kRhWaves) void k_rehash(spl_arena_t aa, uint64
       // trailing tombstones (after the last slot holding an entry) become virgin: the cluster ends earlier
       __builtin_amdgcn_wave_barrier();
       for (int t = nh - 1; t >= 0; --t) {
-        const uint64_t q = holes[t];
+        const uint64_t q = H(t);
         if ((int64_t)cyc(q, cs, n) <= rl_used) break;
         if (lane == 0) *(uint64_t*)(a.slot(q) + kOffEpoch) = 0;
         ++reclaimed;
@@ -241,6 +249,107 @@ __global__ __launch_bounds__(64 * kRhWaves) void k_rehash(spl_arena_t aa, uint64
     atomicAdd(&cnt->reclaimed, reclaimed);
     atomicAdd(&cnt->clusters, clusters);
     atomicAdd(&cnt->skipped, skipped);
+  }
+}
+
+// ------------------------------------------------------------ full rebuild --
+// For an arena whose clusters have merged (few never-used slots left, e.g. high load under churn)
+// the in-place compaction degenerates into one wave walking the whole table; instead every live
+// entry is copied out, the slot array cleared, and the entries re-inserted in parallel (each at the
+// first free slot from its home: no tombstones at all afterwards).  Temporary memory: one record of
+// stride + max_val (+ the bf16 copy and norm) bytes per live entry.  Exclusive, as k_rehash.
+struct RbGeom {
+  uint32_t rec;      // bytes per record (16-B multiple)
+  uint32_t off_val;  // value row in the record
+  uint32_t off_v16;  // bf16 vector (vec16 arenas)
+  uint32_t off_n2;   // squared norm
+};
+__device__ __forceinline__ void copy16(uint8_t* d, const uint8_t* s, uint32_t bytes, int lane) {
+  const uint32_t n16 = bytes / 16;
+  for (uint32_t c = lane; c < n16; c += 64) ((uint4*)d)[c] = ((const uint4*)s)[c];
+  for (uint32_t b = n16 * 16 + lane; b < bytes; b += 64) d[b] = s[b];
+}
+
+__global__ __launch_bounds__(256) void k_rb_collect(spl_arena_t aa, uint32_t* __restrict__ idx,
+                                                    unsigned long long* __restrict__ count) {
+  const Arena a = from_api(aa);
+  const int lane = threadIdx.x & 63;
+  for (uint64_t base = blockIdx.x * 256ull; base < a.slots; base += gridDim.x * 256ull) {
+    const uint64_t i = base + threadIdx.x;
+    const bool live = i < a.slots && ald64(a.slot(i) + kOffHash) != 0;
+    const uint64_t bm = __ballot(live);
+    if (!bm) continue;
+    unsigned long long b0 = 0;
+    if (lane == 0) b0 = atomicAdd(count, (unsigned long long)__popcll(bm));
+    b0 = __shfl(b0, 0, 64);
+    if (live) idx[b0 + __popcll(bm & ((1ull << lane) - 1))] = (uint32_t)i;
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rb_gather(spl_arena_t aa, const uint32_t* __restrict__ idx, uint64_t n,
+                                                   uint8_t* __restrict__ tmp, RbGeom g) {
+  const Arena a = from_api(aa);
+  const int lane = threadIdx.x & 63;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < n; w += nw) {
+    const uint64_t i = idx[w];
+    uint8_t* r = tmp + w * g.rec;
+    copy16(r, a.slot(i), a.stride, lane);  // core (+ fp32 vector)
+    copy16(r + g.off_val, a.value(i), a.max_val, lane);
+    if (a.has_vec16()) {
+      copy16(r + g.off_v16, (const uint8_t*)a.vec16(i), kVec16Bytes, lane);
+      if (lane == 0) *(float*)(r + g.off_n2) = a.nrm2()[i];
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void k_rb_insert(spl_arena_t aa, const uint8_t* __restrict__ tmp, uint64_t n,
+                                                   RbGeom g, unsigned long long* __restrict__ fail) {
+  const Arena a = from_api(aa);
+  const int lane = threadIdx.x & 63;
+  const uint64_t ns = a.slots;
+  const uint64_t nw = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+  for (uint64_t w = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6; w < n; w += nw) {
+    const uint8_t* r = tmp + w * g.rec;
+    const uint64_t h = *(const uint64_t*)r, ep = *(const uint64_t*)(r + kOffEpoch);
+    const uint64_t home = h % ns;
+    // lane-parallel probe: 64 consecutive slots per round, the first virgin claimed by CAS 0 -> 1
+    int64_t tgt = -1;
+    for (uint64_t base = 0; base < ns && tgt < 0; base += 64) {
+      const uint64_t p = (home + base + lane) % ns;
+      const uint8_t* s = a.slot(p);
+      bool v = base + lane < ns && ald64(s + kOffHash) == 0 && ald64(s + kOffEpoch) == 0;
+      uint64_t bm = __ballot(v);
+      while (bm && tgt < 0) {
+        const int l = __builtin_ctzll(bm);
+        bm &= bm - 1;
+        bool got = false;
+        if (lane == l) got = acas64((void*)(a.slot(p) + kOffEpoch), 0, 1);
+        const uint64_t g2 = __ballot(got);
+        if (g2) tgt = (int64_t)((home + base + l) % ns);
+      }
+    }
+    if (tgt < 0) {
+      if (lane == 0) atomicAdd(fail, 1ull);
+      continue;
+    }
+    uint8_t* d = a.slot((uint64_t)tgt);
+    // record -> slot: bytes 16.. of the core (val_off stays the slot's own), vector, value, copy; then
+    // the key's hash and finally its epoch (a reader never sees the hash before the key bytes)
+    const uint32_t voff = *(const uint32_t*)(d + kOffValOff);
+    copy16(d + 16, r + 16, a.stride - 16, lane);
+    copy16(a.value((uint64_t)tgt), r + g.off_val, a.max_val, lane);
+    if (a.has_vec16()) {
+      copy16((uint8_t*)a.vec16((uint64_t)tgt), r + g.off_v16, kVec16Bytes, lane);
+      if (lane == 0) a.nrm2()[tgt] = *(const float*)(r + g.off_n2);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) {
+      *(uint32_t*)(d + kOffValOff) = voff;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      ast64(d + kOffHash, h);
+      ast64(d + kOffEpoch, ep < 2 ? 2 : ep);
+    }
   }
 }
 
@@ -287,6 +396,41 @@ int spl_arena_rehash(spl_arena_t a, void* counters, hipStream_t s) {
   const uint64_t waves = ((uint64_t)a.slots + range - 1) / range;
   const uint64_t blocks = (waves + kRhWaves - 1) / kRhWaves;
   hipLaunchKernelGGL(k_rehash, dim3((unsigned)blocks), dim3(64 * kRhWaves), 0, s, a, range, (RhCounters*)counters);
+  return (int)hipGetLastError();
+}
+
+// Full rebuild (see k_rb_*): live entries -> tmp, slot array cleared, entries re-inserted.
+// scratch_idx: device u32[slots]; tmp: device, slots_live * rec bytes (spl_arena_rebuild_rec);
+// count: device u64 (zeroed); fail: device u64 (zeroed, entries that found no free slot: 0).
+uint32_t spl_arena_rebuild_rec(spl_arena_t a) {
+  uint32_t rec = a.stride + ((a.max_val + 15) & ~15u);
+  if (a.flags & SPL_ARENA_VEC16) rec += (uint32_t)kVec16Bytes + 16;
+  return rec;
+}
+int spl_arena_rebuild_collect(spl_arena_t a, uint32_t* idx, void* count, hipStream_t s) {
+  long g = ((long)a.slots + 255) / 256;
+  if (g > 8192) g = 8192;
+  hipLaunchKernelGGL(k_rb_collect, dim3((unsigned)(g < 1 ? 1 : g)), dim3(256), 0, s, a, idx, (unsigned long long*)count);
+  return (int)hipGetLastError();
+}
+int spl_arena_rebuild_move(spl_arena_t a, const uint32_t* idx, uint64_t n, void* tmp, void* fail, hipStream_t s) {
+  RbGeom g;
+  g.off_val = a.stride;
+  g.off_v16 = a.stride + ((a.max_val + 15) & ~15u);
+  g.off_n2 = g.off_v16 + (uint32_t)kVec16Bytes;
+  g.rec = spl_arena_rebuild_rec(a);
+  const unsigned blocks = (unsigned)std::min<uint64_t>((n + 3) / 4 + 1, 16384);
+  hipLaunchKernelGGL(k_rb_gather, dim3(blocks), dim3(256), 0, s, a, idx, n, (uint8_t*)tmp, g);
+  // the slot array and the value rows to zero, then val_off / default type (spl_arena_init_slots);
+  // the squared norms to zero (no vector until re-inserted)
+  const size_t slot_bytes = (size_t)a.slots * a.stride, val_bytes = (size_t)a.slots * a.max_val;
+  (void)hipMemsetAsync((uint8_t*)a.base + spl::kHeaderBytes, 0, slot_bytes + val_bytes, s);
+  if (a.flags & SPL_ARENA_VEC16)
+    (void)hipMemsetAsync((uint8_t*)a.base + side_offset(a.slots, a.stride, a.max_val) + side_nrm2_offset(), 0,
+                         (size_t)a.slots * 4, s);
+  if (spl_arena_init_slots(a, s) != 0) return (int)hipGetLastError();
+  hipLaunchKernelGGL(k_rb_insert, dim3(blocks), dim3(256), 0, s, a, (const uint8_t*)tmp, n, g,
+                     (unsigned long long*)fail);
   return (int)hipGetLastError();
 }
 

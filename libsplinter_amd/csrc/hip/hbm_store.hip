@@ -1255,9 +1255,46 @@ int HbmStore::probe_stats(ProbeStats* out) {
 int HbmStore::rehash(uint64_t out[4]) {
   if (!ensure_mapped()) return -1;
   DevGuard dg(device_);
+  // strategy: in-place cluster compaction while never-used slots still split the table into short
+  // clusters; a full rebuild (copy out, clear, re-insert) once fewer than 5 % of the slots are
+  // never-used -- the clusters have merged and the compaction would walk them one wave each
+  ProbeStats ps;
+  if (probe_stats(&ps) != 0) return -1;
+  const bool full = ps.virgin * 20 < geo_.slots && ps.live > 0;
   const bool held = ring_ && ring_->ready() && ring_->hold(true) == 0;
   int rc = 0;
-  {
+  bool done = false;
+  if (full) {
+    std::lock_guard<std::mutex> lk(mu_);
+    const spl_arena_t a = arena();
+    uint32_t* d_idx = nullptr;
+    uint64_t* d_cnt = nullptr;
+    void* d_tmp = nullptr;
+    uint64_t hc[2] = {0, 0};
+    if (hipMalloc((void**)&d_idx, (size_t)geo_.slots * 4) == hipSuccess &&
+        hipMalloc((void**)&d_cnt, 16) == hipSuccess && hipMemsetAsync(d_cnt, 0, 16, stream_) == hipSuccess &&
+        spl_arena_rebuild_collect(a, d_idx, d_cnt, stream_) == 0 &&
+        hipMemcpyAsync(hc, d_cnt, 8, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+        hipStreamSynchronize(stream_) == hipSuccess &&
+        hipMalloc(&d_tmp, (size_t)hc[0] * spl_arena_rebuild_rec(a) + 16) == hipSuccess) {
+      // from here on the arena is rewritten: a failure is an error, never a fall-back
+      if (spl_arena_rebuild_move(a, d_idx, hc[0], d_tmp, d_cnt + 1, stream_) != 0 ||
+          hipMemcpyAsync(hc + 1, d_cnt + 1, 8, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
+          hipStreamSynchronize(stream_) != hipSuccess || hc[1] != 0)
+        rc = -1;
+      out[0] = hc[0];
+      out[1] = ps.tombstones;
+      out[2] = 0;
+      out[3] = hc[1];
+      done = true;
+    } else {
+      (void)hipGetLastError();  // allocation failed: the in-place compaction below instead
+    }
+    if (d_tmp) (void)hipFree(d_tmp);
+    if (d_cnt) (void)hipFree(d_cnt);
+    if (d_idx) (void)hipFree(d_idx);
+  }
+  if (!done) {
     std::lock_guard<std::mutex> lk(mu_);
     uint64_t* d = nullptr;
     if (hipMallocAsync((void**)&d, 32, stream_) != hipSuccess) rc = -1;
@@ -1268,6 +1305,9 @@ int HbmStore::rehash(uint64_t out[4]) {
       (void)hipFreeAsync(d, stream_);
     }
     if (hipStreamSynchronize(stream_) != hipSuccess) rc = -1;
+  }
+  {
+    std::lock_guard<std::mutex> lk(mu_);
     if (rc == 0 && (side_flags_ & SPL_ARENA_SIDE)) {
       ProbeStats side;
       uint8_t* sp = (uint8_t*)dbase_ + side_offset(geo_.slots, geo_.stride, geo_.max_val);

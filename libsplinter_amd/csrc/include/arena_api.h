@@ -94,6 +94,12 @@ int spl_arena_purge(spl_arena_t a, hipStream_t stream);
 int spl_arena_probe_stats(spl_arena_t a, void *out, hipStream_t stream);
 int spl_arena_rehash(spl_arena_t a, void *counters, hipStream_t stream);
 int spl_arena_vec16_rebuild(spl_arena_t a, hipStream_t stream);
+/* full rebuild (exclusive): collect the live slot indices (device u32[slots], count: device u64
+ * zeroed), then move them out to tmp (n * spl_arena_rebuild_rec bytes), clear the slot array and
+ * re-insert every entry (fail: device u64 zeroed, entries left without a slot: 0 when n <= slots) */
+uint32_t spl_arena_rebuild_rec(spl_arena_t a);
+int spl_arena_rebuild_collect(spl_arena_t a, uint32_t *idx, void *count, hipStream_t stream);
+int spl_arena_rebuild_move(spl_arena_t a, const uint32_t *idx, uint64_t n, void *tmp, void *fail, hipStream_t stream);
 int spl_arena_gather_slots(spl_arena_t a, const uint32_t *idx, long n, uint8_t *out_core, hipStream_t stream);
 int spl_hash_keys(const char *keys, int kstride, long n, uint64_t *out, hipStream_t stream);
 int spl_format_keys(char *out, int kstride, const uint64_t *ids, uint64_t first, long n, const char *prefix_dev,

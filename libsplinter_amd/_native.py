@@ -249,6 +249,11 @@ def _declare_hip(L):
     if hasattr(L, "spl_hbm_ring_hold"):
         _sig(L, "spl_hbm_ring_hold", c_int, c_void_p, c_int)
     _sig(L, "spl_arena_purge", c_int, A, P)
+    _sig(L, "spl_arena_vec16_rebuild", c_int, A, P)
+    _sig(L, "spl_arena_probe_stats", c_int, A, P, P)
+    _sig(L, "spl_hbm_probe_stats", c_int, P, P)
+    _sig(L, "spl_hbm_rehash", c_int, P, P)
+    _sig(L, "spl_search_batch", ctypes.c_long, P, P, c_int, c_int, ctypes.c_float, ctypes.c_float, c_u64, P)
     _sig(L, "spl_arena_gather_slots", c_int, A, P, c_long, P, P)
     _sig(L, "spl_hash_keys", c_int, P, c_int, c_long, P, P)
     _sig(L, "spl_format_keys", c_int, P, c_int, P, c_u64, c_long, P, c_int, c_int, P)

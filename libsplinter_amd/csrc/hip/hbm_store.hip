@@ -1037,7 +1037,7 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
   if (nq <= 0 || k <= 0 || k > 32 || !q || !out) { errno = EINVAL; return -1; }
   if (!ensure_mapped()) return -1;
   DevGuard dg(device_);
-  std::lock_guard<std::mutex> lk(mu_);
+  std::unique_lock<std::mutex> lk(mu_);  // released before fetch_cores, which takes it itself
   const spl_arena_t a = arena();
   const long slots = geo_.slots;
   std::vector<CandRec> res((size_t)nq * k);
@@ -1130,6 +1130,7 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
   for (void* p : {(void*)d_q, (void*)d_thr, (void*)d_bmax, (void*)d_qf, (void*)d_cnt, (void*)d_cand, d_res, d_scr})
     if (p) (void)hipFreeAsync(p, stream_);
   (void)hipStreamSynchronize(stream_);
+  lk.unlock();
   if (!ok) { errno = EIO; return -1; }
   // slot indices -> keys and slot metadata (one gather of the slot cores)
   std::vector<uint32_t> idx;

@@ -311,6 +311,7 @@ class Batch:
         pos[: self.T] = np.concatenate([np.arange(n, dtype=np.int32) for n in lens])
         qb = np.asarray([(i, q0) for i, n in enumerate(lens) for q0 in range(0, n, qblock)], np.int32).reshape(-1)
         self.nqb = qb.size // 2
+        self._ids_host, self._device, self._qblock, self._parts = ids, device, qblock, {}
         if str(device) == "cpu":
             self.ids, self.pos = torch.from_numpy(ids), torch.from_numpy(pos)
             self.cu, self.qblocks = torch.from_numpy(self.cu_host), torch.from_numpy(qb)
@@ -335,11 +336,31 @@ class Batch:
             o += n
         self.ids, self.pos, self.cu, self.qblocks = views
 
+    def split(self, parts: int):
+        """[(sub-batch, first row)]: the documents cut into `parts` contiguous groups of about equal token
+        counts, each a Batch of its own whose rows are rows [first, first + T) of this batch (cached)."""
+        if parts in self._parts:
+            return self._parts[parts]
+        lens = np.diff(self.cu_host)
+        cum = np.cumsum(lens)
+        cuts = [0] + [int(np.searchsorted(cum, self.T * j / parts, side="left")) + 1 for j in range(1, parts)] + [self.B]
+        out = []
+        for j in range(parts):
+            d0, d1 = cuts[j], cuts[j + 1]
+            if d1 <= d0:
+                continue
+            r0, r1 = int(self.cu_host[d0]), int(self.cu_host[d1])
+            seqs = [self._ids_host[self.cu_host[d]: self.cu_host[d + 1]].tolist() for d in range(d0, d1)]
+            out.append((Batch(seqs, self._device, self._qblock), r0))
+        self._parts[parts] = out
+        return out
+
 
 class NomicEncoder:
     """Batched bf16 forward on the gfx950 kernels (no torch compute in the hot path)."""
 
     def __init__(self, weights: NomicWeights, max_tokens: int = 1 << 17):
+        self._split_streams = None
         self.w = weights
         self.cfg = weights.cfg
         self.L = _lib()
@@ -395,8 +416,15 @@ class NomicEncoder:
     # NOMIC_SCHEDULE overrides; NOMIC_LN_FOLD=1 is the old spelling of "folded".
     schedule = os.environ.get("NOMIC_SCHEDULE", "folded" if os.environ.get("NOMIC_LN_FOLD", "0") != "0" else "fused")
 
+    # NOMIC_SPLIT=N (N > 1): the batch's documents in N groups, each group's layer chain on its own
+    # stream, issued layer by layer in turn, so one group's kernels fill the CUs another group's
+    # kernel leaves idle (a GEMM's last partial wave of tiles, its prologue burst / epilogue tail)
+    split_parts = int(os.environ.get("NOMIC_SPLIT", "1"))
+
     def hidden(self, b: Batch) -> torch.Tensor:
         """Final-layer hidden states [T, 768] (bf16) for a packed batch."""
+        if self.split_parts > 1 and self.schedule == "fused" and b.B >= 2 * self.split_parts:
+            return self._hidden_split(b, self.split_parts)
         if self.schedule == "folded":
             return self._hidden_folded(b)
         if self.schedule == "split":
@@ -432,6 +460,44 @@ class NomicEncoder:
             self._gemm(EPI_SWIGLU, x, lw["wupgate"], T, ffn)
             self._res_ln(ffn, lw["wdown"], T, x, lw["ln2_g"], lw["ln2_b"])
         return x[:T]
+
+    def _hidden_split(self, b: Batch, parts: int) -> torch.Tensor:
+        """The fused schedule over `parts` document groups on their own streams (NOMIC_SPLIT); every
+        group works on its own rows of the shared workspaces, so the hidden states land in rows [0, T)
+        exactly as the one-stream forward leaves them."""
+        cfg, L, w = self.cfg, self.L, self.w
+        assert b.max_len <= self.rope.shape[0]
+        self._ensure(b.T_pad)
+        subs = b.split(parts)
+        if self._split_streams is None or len(self._split_streams) < len(subs):
+            self._split_streams = [torch.cuda.Stream() for _ in subs]
+        cur = torch.cuda.current_stream()
+        streams = self._split_streams[: len(subs)]
+        for st in streams:
+            st.wait_stream(cur)
+        scale = 1.0 / math.sqrt(cfg.head_dim)
+        views = []
+        for (sb, r0), st in zip(subs, streams):
+            views.append((sb, st, self.x[r0:], self.attn[r0:], self.qkv[r0:], self.ffn[r0:]))
+        for sb, st, x, attn, qkv, ffn in views:
+            with torch.cuda.stream(st):
+                _chk(L.nomic_embed_ln(sb.ids.data_ptr(), sb.T, w.tok.data_ptr(), w.type_row.data_ptr(),
+                                      w.emb_g.data_ptr(), w.emb_b.data_ptr(), cfg.eps, x.data_ptr(), st.cuda_stream),
+                     "embed_ln")
+        for lw in w.layers:
+            for sb, st, x, attn, qkv, ffn in views:
+                with torch.cuda.stream(st):
+                    s_ = st.cuda_stream
+                    T = sb.T
+                    self._gemm(EPI_ROPE, x, lw["wqkv"], T, qkv, pos=sb.pos)
+                    _chk(L.nomic_attention(qkv.data_ptr(), attn.data_ptr(), sb.cu.data_ptr(), sb.qblocks.data_ptr(),
+                                           sb.nqb, cfg.heads, scale, s_), "attention")
+                    self._res_ln(attn, lw["wo"], T, x, lw["ln1_g"], lw["ln1_b"])
+                    self._gemm(EPI_SWIGLU, x, lw["wupgate"], T, ffn)
+                    self._res_ln(ffn, lw["wdown"], T, x, lw["ln2_g"], lw["ln2_b"])
+        for st in streams:
+            cur.wait_stream(st)
+        return self.x[: b.T]
 
     def _hidden_folded(self, b: Batch) -> torch.Tensor:
         """The forward with every post-LN folded into the GEMMs around it (K15): the residual GEMMs

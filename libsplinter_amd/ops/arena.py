@@ -330,7 +330,9 @@ class HbmArena:
         return _device_view(self.desc.base + offset, nbytes)
 
     def embedding_matrix(self) -> torch.Tensor:
-        """[slots, 768] fp32 strided view of every slot's vector (zero copy)."""
+        """[slots, 768] fp32 strided view of every slot's vector (zero copy).  Writes through this view
+        bypass the embedding writers: call :meth:`rebuild_vec16` afterwards so the side region's bf16
+        copy (what the batched search streams) matches."""
         assert self.embeddings
         base = self.desc.base + 5440 + 128
         flat = _device_view(base, self.slots * 3200 - 128, dtype=torch.float32)
@@ -353,6 +355,11 @@ class HbmArena:
     @property
     def has_vec16(self) -> bool:
         return bool(self.desc.flags & 4)
+
+    def rebuild_vec16(self) -> None:
+        """Recompute the bf16 vector copy and squared norms from the fp32 vectors (spl_arena_vec16_rebuild)."""
+        if self.has_vec16:
+            _check(self._H.spl_arena_vec16_rebuild(self.desc, _stream()), "arena_vec16_rebuild")
 
     def vec16_view(self) -> Tuple[torch.Tensor, torch.Tensor]:
         """(nrm2 [slots] fp32, vec16 [slots, 768] bf16): the side region's squared norms and bf16

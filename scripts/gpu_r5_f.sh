@@ -1,0 +1,12 @@
+#!/bin/bash
+set -o pipefail
+OUT=gpurun_out/r5f
+mkdir -p $OUT
+timeout -k 10 400 python -u -m pytest tests/test_search_gpu.py tests/test_arena_gpu.py tests/test_node_gpu.py -x -q --timeout 120 --timeout-method thread > $OUT/search_arena.txt 2>&1 || { tail -40 $OUT/search_arena.txt; exit 1; }
+tail -2 $OUT/search_arena.txt
+timeout -k 10 300 python scripts/search_bench.py > $OUT/search_bench.out 2>&1 || { tail -20 $OUT/search_bench.out; exit 1; }
+tail -3 $OUT/search_bench.out
+SPLINTER_SEARCH_VEC16=0 timeout -k 10 300 python scripts/search_bench.py > $OUT/search_bench_fp32.out 2>&1 || { tail -20 $OUT/search_bench_fp32.out; exit 1; }
+tail -3 $OUT/search_bench_fp32.out
+timeout -k 10 300 python scripts/gemm_pt_ab.py --ksweep 1 --encoder 0 > $OUT/gemm_pt_ab.jsonl 2> $OUT/gemm_pt_ab.err || { tail -20 $OUT/gemm_pt_ab.err; exit 1; }
+cat $OUT/gemm_pt_ab.jsonl

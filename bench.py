@@ -452,7 +452,13 @@ def main():
         g_lens = torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")
 
     # what actually launches the KV work of a step (reported in the JSON config)
-    if kvs is not None and int(os.environ.get("SPL_KVS_FUSED", "2")) != 0:
+    kv_mode = int(os.environ.get("SPL_KVS_FUSED", "2"))
+    if kvs is not None and kv_mode == 3:
+        kv_launch = {"writer_streams": len(set_parts), "reader_streams": len(get_parts), "launches": 1,
+                     "how": f"async: each of the {len(set_parts)} writer + {len(get_parts)} reader client streams posts "
+                            "its slice with a stream-ordered doorbell write (hipStreamWriteValue64); ONE resident "
+                            "server grid (k_kv_server) consumes the slices as they are posted"}
+    elif kvs is not None and kv_mode != 0:
         kv_launch = {"writer_streams": 1, "reader_streams": 1, "launches": 1,
                      "how": f"fused: ONE grid (k_kv_fused) consumes all {len(set_parts)} set + {len(get_parts)} get "
                             "client slices, launched on one stream"}
@@ -699,6 +705,8 @@ def main():
             x = torch.tensor([integrity_fail, timed_set_fail, integrity_rows], device="cuda")
             dist.all_reduce(x)
             integrity_fail, timed_set_fail, integrity_rows = [int(v) for v in x.tolist()]
+    # stream-posted server (SPL_KVS_FUSED=3): a server that gave up waiting for a post left slices unrun
+    kv_async_error = kvs.async_error() if (kvs is not None and kv_mode == 3) else None
 
 
     # ---- per-call C API (outside the timed region): splinter_set / splinter_get from host threads
@@ -890,7 +898,7 @@ def main():
         "integrity_failures": integrity_fail,
         "integrity_rows_checked": integrity_rows,
         "integrity_source": integrity_source,
-        "timed_set_failures": timed_set_fail,
+        "timed_set_failures": timed_set_fail, "kv_async_error": kv_async_error,
         "host_api_threads": args.host_api if host_api else None,
         "host_api_ops_per_s": host_api["ops_per_s"] if host_api else None,
         "host_api_p50_us": host_api["p50_us"] if host_api else None,

@@ -480,6 +480,134 @@ struct FSegs {
   int ks;
 };
 
+// A lane's U op slots in the fused / server round loops.
+template <int U, int KW>
+struct OpSlots {
+  KeyT<KW> k[U];
+  long row[U];
+  int seg[U];  // -1: slot empty
+  uint32_t len[U];
+  int tries[U];
+  bool set[U];
+};
+
+// Put row r of segment q (sg[q]) into the empty slot j.
+template <int U, int KW>
+__device__ __forceinline__ void fill_slot(OpSlots<U, KW>& o, int j, const FSeg& f, int q, long r, int ks) {
+  o.seg[j] = q;
+  o.row[j] = f.idx ? (long)f.idx[r] : r;
+  o.set[j] = f.set != 0;
+  o.tries[j] = 0;
+  load_key(o.k[j], f.keys + o.row[j] * (long)ks, ks);
+  o.len[j] = o.set[j] ? f.lens[o.row[j]] : 0u;
+}
+
+// One round over a lane's U slots: probes / claims of every occupied slot, the two cooperative row
+// copies (cp*0: set rows, cp*1: get rows; a wave-private LDS table each), set publication, get
+// re-validation, completion.  An op that met EAGAIN stays in its slot for the next round while
+// tries <= max_retry.  Called by every lane of the wave (the row copies are wave-cooperative).
+template <int U, int KW>
+__device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW>& o, bool scrub, bool hybrid,
+                                         int max_retry, Stats& st, uint64_t& muts, uint4* cpp0, uint2* cpl0,
+                                         uint4* cpp1, uint2* cpl1, int lane) {
+  Claim c[U];
+  long sidx[U];
+  uint64_t e1[U];
+  int32_t rc[U];
+  // probes / claims of every slot of the round
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    rc[j] = kInval;
+    c[j] = Claim{-1, false, kInval};
+    if (o.seg[j] < 0) continue;
+    ++st.attempts;
+    ++o.tries[j];
+    const int vs = sg[o.seg[j]].vstride;
+    if (o.set[j]) {
+      if (o.len[j] == 0 || o.len[j] > a.max_val || o.len[j] > (uint32_t)vs) c[j].rc = kMsgSize;
+      else c[j] = claim_set(a, o.k[j]);
+      rc[j] = c[j].rc;
+    } else {
+      uint32_t L = 0;
+      sidx[j] = locate_peek(a, o.k[j], &e1[j], &L);
+      o.len[j] = L;
+      rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
+      if (rc[j] == kOk && ((e1[j] & 1) || L > a.max_val)) rc[j] = kAgain;
+      else if (rc[j] == kOk && sg[o.seg[j]].vals && L > (uint32_t)vs) rc[j] = kMsgSize;
+    }
+  }
+  // value rows: table 0 = sets (client row -> arena, write-through), table 1 = gets (arena -> client)
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    const FSeg* f = o.seg[j] >= 0 ? &sg[o.seg[j]] : nullptr;
+    const bool gs = f && o.set[j] && rc[j] == kOk;
+    const bool gg = f && f->vals && !o.set[j] && rc[j] == kOk;
+    const uint64_t ss = gs ? (uint64_t)(f->vals + o.row[j] * (long)f->vstride) : 0;
+    const uint64_t sd = gs ? (uint64_t)a.value((size_t)c[j].idx) : 0;
+    cpp0[j * 64 + lane] = make_uint4((uint32_t)ss, (uint32_t)(ss >> 32), (uint32_t)sd, (uint32_t)(sd >> 32));
+    cpl0[j * 64 + lane] = make_uint2(gs ? o.len[j] : 0u, gs ? set_chunks(a, o.len[j], scrub, hybrid) : 0u);
+    const uint64_t gsrc = gg ? (uint64_t)a.value((size_t)sidx[j]) : 0;
+    const uint64_t gdst = gg ? (uint64_t)(f->vals + o.row[j] * (long)f->vstride) : 0;
+    const uint32_t n16 = (o.len[j] + 15) >> 4;
+    cpp1[j * 64 + lane] = make_uint4((uint32_t)gsrc, (uint32_t)(gsrc >> 32), (uint32_t)gdst, (uint32_t)(gdst >> 32));
+    cpl1[j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? n16 : 0u);
+  }
+  __builtin_amdgcn_wave_barrier();
+  coop_copy<U * 64, 3>(cpp0, cpl0, lane, (int)((a.max_val + 255) >> 8), a.max_val);
+  coop_copy<U * 64, 0, true>(cpp1, cpl1, lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
+#pragma unroll
+  for (int j = 0; j < U; ++j)
+    if (o.seg[j] >= 0 && o.set[j] && rc[j] == kOk) write_meta<3>(a, c[j], o.len[j]);
+  drain();
+  // gets: closing round trip, (hash, epoch) and the key words together
+  {
+    u32x4c_t he[U];
+    KeyProbe<KW> kp[U];
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      const bool live = o.seg[j] >= 0 && !o.set[j] && rc[j] == kOk;
+      const uint8_t* s = a.slot(live ? (size_t)sidx[j] : 0);
+      he[j] = ld16c(s + kOffHash);
+      kp[j].issue(s, o.k[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j) {
+      vm_wait(he[j]);
+      kp[j].wait();
+    }
+#pragma unroll
+    for (int j = 0; j < U; ++j)
+      if (o.seg[j] >= 0 && !o.set[j] && rc[j] == kOk &&
+          (hi64(he[j]) != e1[j] || lo64(he[j]) != o.k[j].hash || !kp[j].eq(o.k[j])))
+        rc[j] = kAgain;
+  }
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    if (o.seg[j] < 0) continue;
+    const int32_t r = rc[j];
+    if (r == kAgain) {
+      ++st.again;
+      if (o.tries[j] <= max_retry) continue;  // carried into the next round
+    }
+    const FSeg& f = sg[o.seg[j]];
+    if (o.set[j]) {
+      if (r == kOk) {
+        finish_set(a, c[j]);
+        ++st.ok;
+        ++muts;
+        pulse_masks(a, c[j].wm, c[j].bl);
+        mark_dirty(a, (size_t)c[j].idx);
+      }
+    } else {
+      if (r == kOk) ++st.ok;
+      else if (r == kNoEnt) ++st.miss;
+      if (f.lens) f.lens[o.row[j]] = r == kOk ? o.len[j] : 0;
+    }
+    if (f.status) f.status[o.row[j]] = r;
+    o.seg[j] = -1;
+  }
+}
+
 template <int U, int B, int KW = 16, int OCC = 1>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, FSegs tab,
                                                                                          int max_retry, uint64_t* stats) {
@@ -516,22 +644,14 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
   long cursor = 0;
   bool more = true;
-  KeyT<KW> k[U];
-  Claim c[U];
-  long row[U], sidx[U];
-  int seg[U];  // -1: slot empty
-  uint64_t e1[U];
-  uint32_t len[U];
-  int32_t rc[U];
-  int tries[U];
-  bool set[U];
+  OpSlots<U, KW> o;
 #pragma unroll
-  for (int j = 0; j < U; ++j) seg[j] = -1;
+  for (int j = 0; j < U; ++j) o.seg[j] = -1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   for (;;) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
-      if (seg[j] < 0 && more) {
+      if (o.seg[j] < 0 && more) {
         const long i = first + (cursor / U) * stride + (cursor % U);
         ++cursor;
         if (i >= n) {
@@ -539,115 +659,201 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
         } else {
           int q = 0;
           while (q + 1 < nseg && sstart[q + 1] <= i) ++q;
-          const FSeg& f = sg[q];
-          const long r = i - sstart[q];
-          seg[j] = q;
-          row[j] = f.idx ? (long)f.idx[r] : r;
-          set[j] = f.set != 0;
-          tries[j] = 0;
-          load_key(k[j], f.keys + row[j] * (long)ks, ks);
-          len[j] = set[j] ? f.lens[row[j]] : 0u;
+          fill_slot(o, j, sg[q], q, i - sstart[q], ks);
         }
       }
     }
     bool busy = false;
 #pragma unroll
-    for (int j = 0; j < U; ++j) busy |= seg[j] >= 0;
+    for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
     if (!__syncthreads_or(busy)) break;
-    // probes / claims of every slot of the round
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      rc[j] = kInval;
-      c[j] = Claim{-1, false, kInval};
-      if (seg[j] < 0) continue;
-      ++st.attempts;
-      ++tries[j];
-      const int vs = sg[seg[j]].vstride;
-      if (set[j]) {
-        if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vs) c[j].rc = kMsgSize;
-        else c[j] = claim_set(a, k[j]);
-        rc[j] = c[j].rc;
-      } else {
-        uint32_t L = 0;
-        sidx[j] = locate_peek(a, k[j], &e1[j], &L);
-        len[j] = L;
-        rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
-        if (rc[j] == kOk && ((e1[j] & 1) || L > a.max_val)) rc[j] = kAgain;
-        else if (rc[j] == kOk && sg[seg[j]].vals && L > (uint32_t)vs) rc[j] = kMsgSize;
-      }
-    }
-    // value rows: table 0 = sets (client row -> arena, write-through), table 1 = gets (arena -> client)
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const FSeg* f = seg[j] >= 0 ? &sg[seg[j]] : nullptr;
-      const bool gs = f && set[j] && rc[j] == kOk;
-      const bool gg = f && f->vals && !set[j] && rc[j] == kOk;
-      const uint64_t ss = gs ? (uint64_t)(f->vals + row[j] * (long)f->vstride) : 0;
-      const uint64_t sd = gs ? (uint64_t)a.value((size_t)c[j].idx) : 0;
-      cp_p[0][w][j * 64 + lane] = make_uint4((uint32_t)ss, (uint32_t)(ss >> 32), (uint32_t)sd, (uint32_t)(sd >> 32));
-      cp_l[0][w][j * 64 + lane] = make_uint2(gs ? len[j] : 0u, gs ? set_chunks(a, len[j], scrub, hybrid) : 0u);
-      const uint64_t gsrc = gg ? (uint64_t)a.value((size_t)sidx[j]) : 0;
-      const uint64_t gdst = gg ? (uint64_t)(f->vals + row[j] * (long)f->vstride) : 0;
-      const uint32_t n16 = (len[j] + 15) >> 4;
-      cp_p[1][w][j * 64 + lane] = make_uint4((uint32_t)gsrc, (uint32_t)(gsrc >> 32), (uint32_t)gdst, (uint32_t)(gdst >> 32));
-      cp_l[1][w][j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? n16 : 0u);
-    }
-    __builtin_amdgcn_wave_barrier();
-    coop_copy<U * 64, 3>(cp_p[0][w], cp_l[0][w], lane, (int)((a.max_val + 255) >> 8), a.max_val);
-    coop_copy<U * 64, 0, true>(cp_p[1][w], cp_l[1][w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
-#pragma unroll
-    for (int j = 0; j < U; ++j)
-      if (seg[j] >= 0 && set[j] && rc[j] == kOk) write_meta<3>(a, c[j], len[j]);
-    drain();
-    // gets: closing round trip, (hash, epoch) and the key words together
-    {
-      u32x4c_t he[U];
-      KeyProbe<KW> kp[U];
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        const bool live = seg[j] >= 0 && !set[j] && rc[j] == kOk;
-        const uint8_t* s = a.slot(live ? (size_t)sidx[j] : 0);
-        he[j] = ld16c(s + kOffHash);
-        kp[j].issue(s, k[j]);
-      }
-#pragma unroll
-      for (int j = 0; j < U; ++j) {
-        vm_wait(he[j]);
-        kp[j].wait();
-      }
-#pragma unroll
-      for (int j = 0; j < U; ++j)
-        if (seg[j] >= 0 && !set[j] && rc[j] == kOk &&
-            (hi64(he[j]) != e1[j] || lo64(he[j]) != k[j].hash || !kp[j].eq(k[j])))
-          rc[j] = kAgain;
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (seg[j] < 0) continue;
-      const int32_t r = rc[j];
-      if (r == kAgain) {
-        ++st.again;
-        if (tries[j] <= max_retry) continue;  // carried into the next round
-      }
-      const FSeg& f = sg[seg[j]];
-      if (set[j]) {
-        if (r == kOk) {
-          finish_set(a, c[j]);
-          ++st.ok;
-          ++muts;
-          pulse_masks(a, c[j].wm, c[j].bl);
-          mark_dirty(a, (size_t)c[j].idx);
-        }
-      } else {
-        if (r == kOk) ++st.ok;
-        else if (r == kNoEnt) ++st.miss;
-        if (f.lens) f.lens[row[j]] = r == kOk ? len[j] : 0;
-      }
-      if (f.status) f.status[row[j]] = r;
-      seg[j] = -1;
-    }
+    kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane);
   }
   flush_stats(a, st, stats, muts);
+}
+
+// ------------------------------------------------------ stream-posted server --
+// Asynchronous submission of a KV step (spl_kvs_set_fused mode 3): every client stream posts its
+// slice with a stream-ordered doorbell write (hipStreamWriteValue64 of the step's sequence number
+// into AsyncCtl::door[slot]) once its own preceding work is done, and ONE resident grid on the
+// server stream consumes the slices as they are posted: a workgroup claims a chunk of rows of a
+// posted slice (atomic on AsyncCtl::next[slot]), runs the fused round loop over it, and claims the
+// next, so slices start independently, in the order their streams reach the post, and no slice
+// waits for the others.  Slice boundaries are multiples of kAsyncAlign rows, so two slices never
+// share a cache line of the keys / values / outputs.  The grid ends when every slice is exhausted,
+// or -- a post that never comes -- after wait_ticks of s_memrealtime (100 MHz) without finding any
+// work, with AsyncCtl::err set (spl_kvs_async_error); every wave reaches one of the two exits.
+constexpr int kAsyncSegs = 64;     // client streams per server step (writers + readers)
+constexpr long kAsyncAlign = 128;  // slice boundary granularity (rows)
+
+struct AsyncCtl {
+  uint64_t door[kAsyncSegs];                 // last step sequence posted by each client stream
+  unsigned long long next[2][kAsyncSegs];    // rows of each slice claimed so far, banked by the step's
+                                             // parity: a server zeroes the other bank for the next step
+  uint32_t err;                              // a post did not arrive within the wait limit
+  uint32_t pad[15];
+};
+
+__host__ __device__ inline long async_bound(long n, int i, int parts) {  // first row of slice i of n rows
+  if (i <= 0) return 0;
+  if (i >= parts) return n;
+  const long b = (n * i / parts + kAsyncAlign - 1) / kAsyncAlign * kAsyncAlign;
+  return b < n ? b : n;
+}
+
+template <int U, int B, int KW = 16, int OCC = 1>
+__global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_server(
+    spl_arena_t aa, FSeg sset, FSeg sget, int nw, int nr, int ks, AsyncCtl* ctl, uint64_t seq, long chunk,
+    uint64_t wait_ticks, int spread, int max_retry, uint64_t* stats) {
+  __shared__ uint4 cp_p[2][B / 64][U * 64];
+  __shared__ uint2 cp_l[2][B / 64][U * 64];
+  __shared__ FSeg sg[2];  // 0: the set batch, 1: the get batch
+  __shared__ long sh_b, sh_e;
+  __shared__ int sh_kind, sh_state, sh_scan;
+  __shared__ uint64_t sh_exhausted, sh_posted, sh_idle;  // thread 0's scan state (LDS: no registers)
+  __shared__ unsigned long long sh_st[5];  // attempts, ok, again, miss, mutations of the chunks run
+  const int nseg = nw + nr;
+  if (threadIdx.x < 5) sh_st[threadIdx.x] = 0;
+  if (threadIdx.x == 0) {
+    sg[0] = sset;
+    sg[1] = sget;
+    sh_exhausted = 0;
+    sh_posted = 0;
+    // first slice looked at: spread over the slices (1) or in post-slot order, writers first (0);
+    // 2 (diagnosis only): every slice taken as posted
+    sh_scan = spread ? (int)(blockIdx.x % (unsigned)nseg) : 0;
+    sh_idle = __builtin_amdgcn_s_memrealtime();
+  }
+  const Arena a = to_dev(aa);
+  bool hybrid;
+  const bool scrub = scrub_flags(a, hybrid);
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  unsigned long long* next = ctl->next[seq & 1];
+  if (blockIdx.x == 0 && threadIdx.x < kAsyncSegs)  // the next step's bank (its last user has ended)
+    __hip_atomic_store(&ctl->next[(seq + 1) & 1][threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (;;) {
+    __syncthreads();  // the previous chunk's readers of sh_* are done
+    if (w == 0) {
+      // wave 0 claims: lane i looks at slice i (its post and how far it is claimed) in one round
+      // trip for all slices, then the first available slice at or after the last one served (a
+      // workgroup stays on a slice while it lasts) gets the atomic claim
+      const uint64_t all = nseg >= 64 ? ~0ull : ((1ull << nseg) - 1);
+      uint64_t exhausted = sh_exhausted, posted = sh_posted;
+      const int scan = sh_scan;
+      bool p = false, av = false;
+      long b = 0, e = 0;
+      if (lane < nseg && !((exhausted >> lane) & 1)) {
+        const bool isset = lane < nw;
+        const int parts = isset ? nw : nr, pi = isset ? lane : lane - nw;
+        const long n = sg[isset ? 0 : 1].n;
+        b = async_bound(n, pi, parts);
+        e = async_bound(n, pi + 1, parts);
+        // slot i is always rung by client stream i, in that stream's order, so door >= seq: this
+        // step's post has happened (an empty slice needs none)
+        p = b >= e || spread >= 2 || ((posted >> lane) & 1) ||
+            __hip_atomic_load(&ctl->door[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) >= seq;
+        if (p && b < e) {
+          const long nx = (long)__hip_atomic_load(&next[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          av = b + nx < e;  // next only grows: "not available" is final
+        }
+      }
+      posted |= __ballot(p);
+      exhausted |= __ballot(p && !av);
+      uint64_t avm = __ballot(av);
+      int state = 0, pick = scan;
+      long cb = 0, ce = 0;
+      while (avm) {
+        const uint64_t up = avm & (~0ull << scan);
+        const int i = __builtin_ctzll(up ? up : avm);
+        long c = 0;
+        if (lane == i) c = (long)atomicAdd(&next[i], (unsigned long long)chunk);
+        c = __shfl(c, i);
+        const long bi = __shfl(b, i), ei = __shfl(e, i);
+        if (bi + c < ei) {
+          cb = bi + c;
+          ce = cb + chunk < ei ? cb + chunk : ei;
+          pick = i;
+          state = 1;
+          break;
+        }
+        avm &= ~(1ull << i);
+        exhausted |= 1ull << i;
+      }
+      if (lane == 0) {
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+            if (state == 1) {
+          sh_idle = now;
+          sh_kind = pick < nw ? 0 : 1;
+          sh_b = cb;
+          sh_e = ce;
+        } else if (exhausted == all) {
+          state = 2;
+        } else if (now - sh_idle > wait_ticks) {
+          __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          state = 2;
+        }
+        sh_exhausted = exhausted;
+        sh_posted = posted;
+        sh_scan = pick;
+        sh_state = state;
+      }
+    }
+    __syncthreads();
+    const int state = sh_state;
+    if (state == 2) break;
+    if (state == 0) {
+      __builtin_amdgcn_s_sleep(32);
+      continue;
+    }
+    // a chunk ends with every slot empty: the slots are the chunk's own (nothing stays live across
+    // the claim above)
+    // (the chunk's counters too: added into LDS at its end, so only the claim state is live across)
+    OpSlots<U, KW> o;
+#pragma unroll
+    for (int j = 0; j < U; ++j) o.seg[j] = -1;
+    Stats st;
+    uint64_t muts = 0;
+    const int q = sh_kind;
+    const long end = sh_e;
+    long row = sh_b + (long)threadIdx.x * U;  // the lane's next row: U consecutive rows per B * U
+    int part = 0;
+    for (;;) {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (o.seg[j] < 0 && row < end) {
+          fill_slot(o, j, sg[q], q, row, ks);
+          if (++part == U) {
+            part = 0;
+            row += (long)B * U - (U - 1);
+          } else {
+            ++row;
+          }
+        }
+      }
+      bool busy = false;
+#pragma unroll
+      for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
+      if (!__syncthreads_or(busy)) break;
+      kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
+                      lane);
+    }
+    {
+      const uint64_t v[5] = {st.attempts, st.ok, st.again, st.miss, muts};
+#pragma unroll
+      for (int c = 0; c < 5; ++c)
+        if (v[c]) __hip_atomic_fetch_add(&sh_st[c], (unsigned long long)v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (stats)
+      for (int c = 0; c < 4; ++c)
+        if (sh_st[c]) aadd64(stats + c, sh_st[c]);
+    if (sh_st[4]) {
+      aadd64(&a.hdr()->epoch, sh_st[4]);
+      notify_host(a);
+    }
+  }
 }
 
 // Launch the fused grid over `tab` (rows: an upper bound of the live rows); mode 2 with 16-B keys
@@ -657,7 +863,7 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   if (rows <= 0) return 0;
   // (measured and removed: 4 workgroups per CU at <= 128 VGPRs, 34 spilled: 4.43 vs 4.84 G ops/s,
   // profiles/r4k/kv_fused3.out)
-  const bool kw4 = mode == 2 && tab.ks == 16;
+  const bool kw4 = mode >= 2 && tab.ks == 16;
   static const int wpc_env = env_int("SPL_KVS_FUSED_WG_PER_CU", 0);
   const int wpc = wpc_env > 0 ? wpc_env : kw4 ? 3 : 2;
   const long need = (rows + 2 * 256 - 1) / (2 * 256);
@@ -1169,7 +1375,58 @@ struct KvStreams {
   std::vector<hipStream_t> s;  // nw writers, then nr readers
   std::vector<hipEvent_t> done;
   hipEvent_t start = nullptr;
+  // mode 3 (stream-posted server): the last server grid's end event, the device control block
+  hipEvent_t srv_done = nullptr;
+  AsyncCtl* ctl = nullptr;
+  uint64_t seq = 0;
 };
+
+// The server grid of one step (mode 3), launched on the origin stream after every client stream's
+// post has been enqueued (a post queued behind the server dispatch on a shared hardware queue would
+// otherwise wait for the server's end).  A client stream posts once ITS preceding work is done; the
+// rows themselves are ordered by the origin stream (the server runs behind the origin's work), so
+// the posts gate each slice on its stream's readiness without a cross-stream event per step (the
+// event chain origin -> server stream -> origin cost ~300 us per step: profiles/r5/kv_async.md).
+int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& sset, const FSeg& sget, int ks,
+                   int max_retry, uint64_t* stats) {
+  const int nw = k->nw, nr = k->nr;  // slot i <-> client stream i, every step
+  if (sset.n + sget.n <= 0) return 0;
+  if (nw + nr > kAsyncSegs || ks != 16) return (int)hipErrorInvalidValue;
+  if (!k->ctl) {
+    if (hipMalloc(&k->ctl, sizeof(AsyncCtl)) != hipSuccess) return (int)hipErrorOutOfMemory;
+    if (hipMemset(k->ctl, 0, sizeof(AsyncCtl)) != hipSuccess) return (int)hipErrorUnknown;
+    if (hipEventCreateWithFlags(&k->srv_done, hipEventDisableTiming) != hipSuccess) return (int)hipErrorUnknown;
+  }
+  const uint64_t seq = ++k->seq;
+  hipError_t e;
+  // the posts: each client stream with rows in this step rings its slot once its own preceding work
+  // is done
+  for (int i = 0; i < nw + nr; ++i) {
+    const bool isset = i < nw;
+    const long n = isset ? sset.n : sget.n;
+    const int parts = isset ? nw : nr, pi = isset ? i : i - nw;
+    if (async_bound(n, pi, parts) >= async_bound(n, pi + 1, parts)) continue;
+    e = hipStreamWriteValue64(k->s[i], &k->ctl->door[i], seq, 0);
+    if (e != hipSuccess) return (int)e;
+  }
+  static const int wpc_env = env_int("SPL_KVS_FUSED_WG_PER_CU", 0);
+  const int wpc = wpc_env > 0 ? wpc_env : 3;
+  const long rows = sset.n + sget.n;
+  const long need = (rows + 2 * 256 - 1) / (2 * 256);
+  const long cap = 256L * wpc;
+  static const long chunk = [] {  // rows per claim: 4 rounds of a 256-thread workgroup at 2 ops per lane
+    const int c = env_int("SPL_KVS_ASYNC_CHUNK", 2048);
+    return (long)(c >= 512 ? c : 512);
+  }();
+  static const uint64_t wait_ticks = (uint64_t)env_int("SPL_KVS_ASYNC_WAIT_MS", 2000) * 100000ull;  // 100 MHz
+  static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
+  hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
+                     sset, sget, nw, nr, ks, k->ctl, seq, chunk, wait_ticks, spread, max_retry, stats);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  (void)hipEventRecord(k->srv_done, origin);
+  return 0;
+}
 
 }  // namespace
 
@@ -1213,12 +1470,25 @@ void* spl_kvs_create(int writers, int readers) {
   return k;
 }
 
-// 0: one launch per client stream's slice on that stream; 1 / 2: one fused grid (k_kv_fused)
+// 0: one launch per client stream's slice on that stream; 1 / 2: one fused grid (k_kv_fused);
+// 3: the client streams post their slices to a resident server grid (k_kv_server)
 int spl_kvs_set_fused(void* h, int mode) {
   auto* k = (KvStreams*)h;
-  if (!k || mode < 0 || mode > 2) return (int)hipErrorInvalidValue;
+  if (!k || mode < 0 || mode > 3) return (int)hipErrorInvalidValue;
   k->fused = mode;
   return 0;
+}
+
+// Mode 3: 1 when a server grid gave up waiting for a post (its step's unposted slices were not
+// run), and clears the flag; waits for the last step's server first.  0: none, <0: no server yet.
+int spl_kvs_async_error(void* h) {
+  auto* k = (KvStreams*)h;
+  if (!k || !k->ctl) return -1;
+  (void)hipEventSynchronize(k->srv_done);
+  uint32_t err = 0;
+  if (hipMemcpy(&err, &k->ctl->err, sizeof err, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (err) (void)hipMemset(&k->ctl->err, 0, sizeof err);
+  return err ? 1 : 0;
 }
 
 void spl_kvs_destroy(void* h) {
@@ -1230,6 +1500,8 @@ void spl_kvs_destroy(void* h) {
   }
   for (auto ev : k->done) (void)hipEventDestroy(ev);
   if (k->start) (void)hipEventDestroy(k->start);
+  if (k->srv_done) (void)hipEventDestroy(k->srv_done);
+  if (k->ctl) (void)hipFree(k->ctl);
   delete k;
 }
 
@@ -1245,6 +1517,12 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
   // 100M keys, 32 + 32 streams, 3.96 G ops/s per-slice dispatches (0) -> 4.15 G (1, 16-word keys)
   // -> 4.85 G (2, 16-B keys in 4 words at 3 workgroups per CU), gpurun_out/r4d bench_kv_fused*.out
   const int fused = k->fused;
+  if (fused == 3 && n_set + n_get > 0 && kstride == 16 && k->nw + k->nr <= kAsyncSegs) {
+    if ((vstride & 15) || (ostride & 15)) return (int)hipErrorInvalidValue;
+    const FSeg sset{skeys, (uint8_t*)svals, (uint32_t*)slens, sstatus, nullptr, nullptr, n_set, vstride, 1};
+    const FSeg sget{gkeys, gout, glens, gstatus, nullptr, nullptr, n_get, ostride, 0};
+    return kvs_step_async(k, a, origin, sset, sget, kstride, max_retry, stats);
+  }
   if (fused && n_set + n_get > 0) {
     if ((kstride & 15) || kstride > 64 || (vstride & 15) || (ostride & 15)) return (int)hipErrorInvalidValue;
     FSegs tab{};

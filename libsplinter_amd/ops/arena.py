@@ -84,8 +84,11 @@ def unpack(vals: torch.Tensor, lens: torch.Tensor) -> list:
 
 class KvStreams:
     """A group of concurrent client streams issuing one KV step natively (spl_kvs_*, hip/arena_kernels.hip):
-    ``writers`` streams share the set batch, ``readers`` the get batch, each slice its own launch
-    on its own stream; the current torch stream continues after all of them."""
+    ``writers`` streams share the set batch, ``readers`` the get batch; the current torch stream
+    continues after all of them.  Submission modes (``set_fused``; SPL_KVS_FUSED sets the default):
+    0 each slice its own launch on its own stream, 1 / 2 every slice in one fused grid on the
+    current stream, 3 each client stream posts its slice with a stream-ordered doorbell write and one
+    resident server grid consumes the slices as they are posted (16-B keys, <= 64 streams)."""
 
     def __init__(self, writers: int, readers: int):
         self._H = N.hip_lib()
@@ -95,8 +98,14 @@ class KvStreams:
         self.writers, self.readers = writers, readers
 
     def set_fused(self, mode: int):
-        """0: one launch per stream slice; 1 / 2 (default): every slice in one fused grid."""
+        """0: one launch per stream slice; 1 / 2 (default): every slice in one fused grid; 3: stream-posted
+        slices consumed by a resident server grid."""
         _check(self._H.spl_kvs_set_fused(self.h, int(mode)), "kvs_set_fused")
+
+    def async_error(self) -> int:
+        """Mode 3: 1 if a server grid gave up waiting for a slice's post (those rows did not run; the
+        flag is cleared), 0 if not, -1 before the first server step.  Waits for the last server grid."""
+        return int(self._H.spl_kvs_async_error(self.h))
 
     def step(self, arena: "HbmArena", skeys, svals, slens, sstatus, gkeys, gout, glens, gstatus, retries: int = 64):
         n_set = skeys.shape[0] if skeys is not None else 0

@@ -488,11 +488,12 @@ def test_acquire_free_get_cross_xcd_hot_keys(uniq):
 
 
 @pytest.mark.parametrize("kstride", [16, 32])
-@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
 def test_kvs_step_modes_match_plain_kernels(uniq, kstride, mode):
-    """One KV step of 8 + 8 client streams (spl_kvs_step) -- per-slice launches (0) or one fused
-    grid (1, 2: the default) -- sets new and existing keys and gets present and missing ones with
-    the same results as the plain batch kernels."""
+    """One KV step of 8 + 8 client streams (spl_kvs_step) -- per-slice launches (0), one fused
+    grid (1, 2: the default) or stream-posted slices on a server grid (3; 32-B keys take the fused
+    grid) -- sets new and existing keys and gets present and missing ones with the same results as
+    the plain batch kernels."""
     import torch
     from libsplinter_amd.ops.arena import HbmArena, KvStreams, pack_keys, pack_values, unpack
     rng = np.random.default_rng(kstride + mode)
@@ -531,6 +532,53 @@ def test_kvs_step_modes_match_plain_kernels(uniq, kstride, mode):
         assert (st == 0).all()
         final = unpack(out, ol)
         assert all(final[i] == new_vals.get(i, vals[i]) for i in range(n))
+    finally:
+        kvs.close()
+        a.close()
+
+
+def test_kvs_async_server_steps(uniq):
+    """Stream-posted server (mode 3) over 32 + 32 client streams for several steps in a row: slices
+    of every size (empty ones included: fewer rows than streams x 128-row alignment) all run, each
+    step's sets land and its gets return the previous step's values, and no server gives up."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, KvStreams, pack_keys, pack_values, unpack
+    rng = np.random.default_rng(7)
+    a = HbmArena.create(uniq, slots=1 << 17, max_val=256, embeddings=False)
+    kvs = KvStreams(32, 32)
+    try:
+        kvs.set_fused(3)
+        n = 30000
+        keys = [f"a{i:012d}" for i in range(n)]
+        K = pack_keys(keys, 16)
+        cur = [bytes([65 + i % 26]) * int(rng.integers(1, 150)) for i in range(n)]
+        V, L = pack_values(cur, 256)
+        assert (a.set(K, V, L) == 0).all()
+        for step, (ns, ng) in enumerate([(12000, 9000), (1000, 30000), (28000, 2000), (77, 4000)]):
+            sidx = rng.choice(n, ns, replace=False)
+            gidx = rng.choice(n, ng, replace=False)
+            gset = set(int(i) for i in sidx)
+            gidx = np.array([i for i in gidx if int(i) not in gset])
+            new = {int(i): bytes([97 + (int(i) + step) % 26]) * int(rng.integers(1, 200)) for i in sidx}
+            SV, SL = pack_values([new[int(i)] for i in sidx], 256)
+            SK = K[torch.as_tensor(sidx, device=K.device)]
+            GK = K[torch.as_tensor(gidx, device=K.device)]
+            sst = torch.full((len(sidx),), 99, dtype=torch.int32, device="cuda")
+            gst = torch.full((len(gidx),), 99, dtype=torch.int32, device="cuda")
+            gout = torch.zeros((len(gidx), 256), dtype=torch.uint8, device="cuda")
+            glen = torch.zeros(len(gidx), dtype=torch.int32, device="cuda")
+            kvs.step(a, SK, SV, SL, sst, GK, gout, glen, gst)
+            torch.cuda.synchronize()
+            assert kvs.async_error() == 0
+            assert (sst == 0).all(), np.unique(sst.cpu().numpy(), return_counts=True)
+            assert (gst == 0).all(), np.unique(gst.cpu().numpy(), return_counts=True)
+            got = unpack(gout, glen)
+            assert all(got[j] == cur[int(i)] for j, i in enumerate(gidx))
+            for i in sidx:
+                cur[int(i)] = new[int(i)]
+        st, out, ol = a.get(K)
+        assert (st == 0).all()
+        assert unpack(out, ol) == cur
     finally:
         kvs.close()
         a.close()

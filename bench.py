@@ -255,8 +255,9 @@ def exchange_ab(args, dev: int, log):
     coll = runs[2]["config"].get("collectives") or ""
     transport = "peer" if "transport peer" in coll else ("rccl" if "transport rccl" in coll else coll)
     fb = coll.split("(fell back: ", 1)[1].split(")", 1)[0] if "(fell back: " in coll else None
+    sync = "device flags" if "device-side posts" in coll else "collectives"
     return {"ops2": runs[2]["value"], "ops1": runs[1]["value"], "ratio": runs[2]["value"] / runs[1]["value"],
-            "transport": transport, "fallback": fb,
+            "transport": transport, "fallback": fb, "sync": sync, "sync_error": runs[2].get("xr_sync_error"),
             "integrity": runs[2]["integrity_failures"] + runs[1]["integrity_failures"],
             "totals": {"keys": args.exchange_keys, "ops_per_step": args.exchange_batch, "steps": 10,
                        "device": phys, "mode": "kv"}}
@@ -873,7 +874,9 @@ def main():
                             + (f" (fell back: {xr.fallback_reason})" if xr.fallback_reason else "") + ": request / response rows "
                             + ("stored into the owners' peer-mapped windows over xGMI, "
                                if xr.transport == "peer" else "moved by one all-to-all per direction, ")
-                            + "one count all-to-all + one response all-to-all per step") if routed and xr else None,
+                            + ("step ordered by device-side posts into the peer windows (no collective per step)"
+                               if xr.sync == "flags" else "one count all-to-all + one response all-to-all per step"))
+            if routed and xr else None,
             "search_keys_per_gpu": args.search_keys if sarena is not None else 0,
             # bytes each GPU stores into its W-1 peers per routed step (own-shard ops never leave the GPU):
             # set request key + len + value prefix and its status back, get request key and its status +
@@ -912,6 +915,8 @@ def main():
         "exchange_ratio": xab["ratio"] if xab else None,
         "exchange_transport": xab["transport"] if xab else None,
         "exchange_fallback_reason": xab["fallback"] if xab else None,
+        "exchange_sync": xab["sync"] if xab else None, "exchange_sync_error": xab["sync_error"] if xab else None,
+        "xr_sync_error": (xr.sync_error() if (routed and xr is not None) else None),
         "exchange_integrity_failures": xab["integrity"] if xab else None,
         "exchange_totals": xab["totals"] if xab else None,
         "mixed5_ms_per_step": mixed5["ms_per_step"] if mixed5 else None,

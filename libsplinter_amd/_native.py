@@ -222,6 +222,9 @@ def _declare_hip(L):
     _sig(L, "spl_xr_pack", c_int, P, c_int, P, c_int, P, c_long, c_int, c_int, c_long, P, c_long, c_long, c_long,
          c_int, P, P, P, P)
     _sig(L, "spl_xr_gather", c_int, P, c_long, c_long, P, c_long, c_long, c_long, c_int, P, P, P, c_int, P)
+    _sig(L, "spl_xr_post", c_int, P, c_int, c_int, c_int, c_int, ctypes.c_uint64, P, P)
+    _sig(L, "spl_xr_wait", c_int, P, c_int, c_int, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64, P, P)
+    _sig(L, "spl_xr_flag_bytes", c_long)
     _sig(L, "spl_xw_create", P, c_int, c_size_t, c_char_p)
     _sig(L, "spl_xw_attach", P, c_char_p, c_int)
     _sig(L, "spl_xw_base", P, P)

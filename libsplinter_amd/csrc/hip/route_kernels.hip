@@ -169,9 +169,73 @@ inline int route_grid(long n, long per_block) {
   return (int)g;
 }
 
+// ------------------------------------------------------- device-side step ordering --
+// The flag area at the end of every window (parallel/xroute.py XGeom.off_flag) orders a step
+// without a collective (SPLINTER_XR_SYNC=flags): a requester posts -- after its pack kernel, stream
+// order -- its per-kind row counts and then flag[parity][0][its rank] = seq into every owner's
+// window; an owner's one-workgroup wait kernel polls its own flags until every peer's seq has
+// arrived, and the owner grid behind it reads the counts.  Responses likewise (dir 1, no counts).
+// Every flag slot has one writer (its source rank) whose posts are stream-ordered, so "flag >= seq"
+// means "this step's post has landed".  Waits are bounded (s_memrealtime, 100 MHz): a post that never
+// comes sets *err and the wait kernel ends, so no grid is left spinning.
+constexpr int kXfFlagBytes = 2 * 2 * kMaxWorld * 8;  // [parity][dir][source] uint64
+// counts follow: [parity][source][kind] int32
+
+__global__ void k_xr_post(const uint64_t* flag_blk, int world, int rank, int par, int dir, uint64_t seq,
+                          const int32_t* counts) {
+  const int d = (int)threadIdx.x;
+  if (d >= world || d == rank) return;
+  uint8_t* f = (uint8_t*)flag_blk[d];
+  if (counts) {  // counts[kind * world + d]: this rank's rows for owner d
+    int32_t* c = (int32_t*)(f + kXfFlagBytes) + (par * kMaxWorld + rank) * 2;
+    __hip_atomic_store(c, counts[d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(c + 1, counts[world + d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  uint64_t* fl = (uint64_t*)f + (par * 2 + dir) * kMaxWorld + rank;
+  __hip_atomic_store(fl, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+__global__ void k_xr_wait(const uint8_t* own, int world, int rank, int par, int dir, uint64_t seq, uint64_t ticks,
+                          uint32_t* err) {
+  const int src = (int)threadIdx.x;
+  if (src >= world || src == rank) return;
+  const uint64_t* fl = (const uint64_t*)own + (par * 2 + dir) * kMaxWorld + src;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__hip_atomic_load(fl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < seq) {
+    if (__builtin_amdgcn_s_memrealtime() - t0 > ticks) {
+      __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+    __builtin_amdgcn_s_sleep(4);
+  }
+}
+
 }  // namespace
 
 extern "C" {
+
+// Device-side ordering of a routed step (see k_xr_post): post into every peer's flag area
+// (flag_blk: device table of the `world` windows' flag-area addresses; counts: the pack counts
+// [2][world] for dir 0, null for dir 1), or wait for every peer's post in this rank's own area.
+int spl_xr_post(const uint64_t* flag_blk, int world, int rank, int par, int dir, uint64_t seq, const int32_t* counts,
+                hipStream_t s) {
+  if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || (par & ~1) || (dir & ~1))
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_xr_post, dim3(1), dim3(kMaxWorld), 0, s, flag_blk, world, rank, par, dir, seq, counts);
+  return (int)hipGetLastError();
+}
+
+int spl_xr_wait(const void* own_flags, int world, int rank, int par, int dir, uint64_t seq, uint64_t timeout_ms,
+                uint32_t* err, hipStream_t s) {
+  if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || (par & ~1) || (dir & ~1) || !err)
+    return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_xr_wait, dim3(1), dim3(kMaxWorld), 0, s, (const uint8_t*)own_flags, world, rank, par, dir, seq,
+                     timeout_ms * 100000ull, err);
+  return (int)hipGetLastError();
+}
+
+// Bytes of the flag area (flags + counts) a window reserves for the device-side ordering.
+long spl_xr_flag_bytes(void) { return kXfFlagBytes + 2L * kMaxWorld * 2 * 4; }
 
 // Pack one batch kind (sets: vals/lens/vw given; gets: vals = lens = null, vw = 0).  counts[world]
 // is zeroed here and accumulates every destination's rows, the own destination included (its rows

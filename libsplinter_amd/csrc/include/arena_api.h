@@ -129,6 +129,15 @@ int spl_xr_pack(const char *keys, int ks, const uint8_t *vals, int vstride, cons
  * EAGAIN; own ops are left as the in-place kernels wrote them. */
 int spl_xr_gather(const int32_t *pos, long n, long cap, const uint64_t *blk, long off_s, long off_l, long off_v,
                   int vw, int32_t *status, uint32_t *out_lens, uint8_t *out, int ostride, hipStream_t stream);
+/* Device-side ordering of a step without a collective: post this rank's step sequence (dir 0 with
+ * its pack counts [2][world], dir 1 without) into every peer window's flag area (flag_blk: device
+ * table of the world flag-area addresses), or wait (one workgroup, bounded by timeout_ms; *err = 1
+ * on expiry) until every peer's post has reached this rank's own area. */
+int spl_xr_post(const uint64_t *flag_blk, int world, int rank, int par, int dir, uint64_t seq, const int32_t *counts,
+                hipStream_t stream);
+int spl_xr_wait(const void *own_flags, int world, int rank, int par, int dir, uint64_t seq, uint64_t timeout_ms,
+                uint32_t *err, hipStream_t stream);
+long spl_xr_flag_bytes(void);
 
 #define SPL_XR_MAX_WORLD 64
 /* One routed step's owner side for spl_kvs_step_xr (all pointers device, except the tables). */

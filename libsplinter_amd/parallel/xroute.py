@@ -37,6 +37,15 @@ Transports for the bytes (the collectives above are the same for both):
 * ``host``: the same protocol on CPU tensors with torch reference kernels (HostShard, gloo), so
   the exchange logic runs in the CPU test suite at world 8.
 
+Step ordering (``sync``): ``coll`` -- the count all-to-all and the response all-to-all above (RCCL
+takes device tensors, so on GPUs of their own the ranks never wait on the host); ``flags`` (peer
+transport, SPLINTER_XR_SYNC=flags) -- no collective per step: each rank posts its counts and a
+step sequence into its peers' windows from the device (route_kernels.hip ``spl_xr_post``) and
+waits for theirs with a one-workgroup bounded wait kernel (``spl_xr_wait``) in stream order, so
+no host sync is left in the step even where the collectives are gloo's (ranks sharing a GPU).
+Measured on that one-GPU rehearsal it is slower than the gloo-staged collectives (0.62-0.63 vs
+0.68 of the 1-rank step, profiles/r5/exchange_sync.md), so ``coll`` is the default.
+
 At world 1 every op is its own shard's: the step is the in-place execution alone.
 
 Fixed capacity per block (``route_capacity``: mean + 8 sigma + 64): an op whose block is full
@@ -60,6 +69,7 @@ import torch.distributed as dist
 from .sharded import _Coll, shard_of
 
 ALIGN = 256
+FLAG_BYTES = 2 * 2 * 64 * 8 + 2 * 64 * 2 * 4  # == spl_xr_flag_bytes()
 OWN, FULL = -2, -1
 EAGAIN, EMSGSIZE = -11, -90
 
@@ -99,7 +109,12 @@ class XGeom:
         self.off_gv = self.off_gl + _al(cap_g * 4)
         self.resp_b = self.off_gv + _al(cap_g * vw)
         self.par_b = world * (self.req_b + self.resp_b)
-        self.window_b = 2 * self.par_b
+        # device-side ordering (sync "flags"): [parity][dir][source] u64 step sequences, then
+        # [parity][source][kind] i32 row counts, 64 sources (route_kernels.hip kMaxWorld)
+        self.off_flag = 2 * self.par_b
+        self.flag_b = FLAG_BYTES
+        self.off_fcnt = self.off_flag + 2 * 2 * 64 * 8
+        self.window_b = self.off_flag + _al(self.flag_b)
 
     def req(self, p: int, s: int) -> int:
         """Offset of the request block from source s, parity p."""
@@ -161,6 +176,8 @@ class XRoute:
             transport = "local"
         self.transport = transport
         self.fallback_reason = None  # why a requested peer transport fell back to rccl (None: it did not)
+        self.sync = "coll"
+        self.wait_ms = int(os.environ.get("SPLINTER_XR_WAIT_MS", "20000"))
         i32 = dict(dtype=torch.int32, device=dev)
         # per parity: pack counts [kind][dest], sent counts [dest][kind], received [src][kind]
         self.cnt = [torch.zeros((2, W), **i32) for _ in range(2)]
@@ -175,6 +192,10 @@ class XRoute:
             if transport == "peer":
                 if not self._setup_peer():
                     transport = self.transport = "rccl"
+                else:
+                    # measured on the one-GPU rehearsal: flags 0.62-0.63 of the 1-rank step vs 0.68 with the
+                    # (gloo-staged) collectives (profiles/r5/exchange_sync.md), so collectives by default
+                    self.sync = "flags" if os.environ.get("SPLINTER_XR_SYNC", "") == "flags" else "coll"
             if transport in ("rccl", "host"):
                 self._win = torch.zeros(self.g.window_b, dtype=torch.uint8, device=dev)
                 self._send = torch.zeros(self.g.window_b, dtype=torch.uint8, device=dev)
@@ -196,6 +217,7 @@ class XRoute:
         devs = [None] * W
         dist.all_gather_object(devs, dev, group=self.group)
         ok = True
+        assert L.spl_xr_flag_bytes() == FLAG_BYTES
         own = L.spl_xw_create(dev, self.g.window_b, names[r].encode())
         why = None
         if not own:
@@ -203,6 +225,9 @@ class XRoute:
             why = f"rank {r}: spl_xw_create of a {self.g.window_b}-B window failed"
         else:
             self._xw.append(own)
+            from ..ops.arena import _device_view
+            _device_view(L.spl_xw_base(own) + self.g.off_flag, self.g.flag_b).zero_()  # no step posted yet
+            torch.cuda.synchronize()
         dist.barrier(group=self.group)  # every window is being served
         self._peer_base = [0] * W
         if ok:
@@ -289,6 +314,27 @@ class XRoute:
             if self.cuda:
                 self._pack_blk[p] = torch.tensor(pk, dtype=torch.int64, device="cuda")
                 self._gath_blk[p] = torch.tensor(gt, dtype=torch.int64, device="cuda")
+        if self.transport == "peer":
+            self._flag_blk = torch.tensor([self._peer_base[d] + g.off_flag for d in range(W)], dtype=torch.int64,
+                                          device="cuda")
+            self._own_flag = self._win_base + g.off_flag
+            self._xerr = torch.zeros(1, dtype=torch.int32, device="cuda")
+
+    def _post(self, i: int, direction: int, counts=None) -> None:
+        from .. import _native as N
+        from ..ops.arena import _check, _stream
+        _check(N.hip_lib().spl_xr_post(self._flag_blk.data_ptr(), self.world, self.rank, i & 1, direction, i + 1,
+                                       counts.data_ptr() if counts is not None else None, _stream()), "xr_post")
+
+    def _wait(self, i: int, direction: int) -> None:
+        from .. import _native as N
+        from ..ops.arena import _check, _stream
+        _check(N.hip_lib().spl_xr_wait(self._own_flag, self.world, self.rank, i & 1, direction, i + 1, self.wait_ms,
+                                       self._xerr.data_ptr(), _stream()), "xr_wait")
+
+    def sync_error(self) -> bool:
+        """True if a device-side wait (sync "flags") gave up on a peer's post (waits for the device)."""
+        return self.sync == "flags" and bool(self._xerr.item())
 
     def close(self):
         if self._xw:
@@ -320,7 +366,10 @@ class XRoute:
         else:
             self._pack_host(p, skeys, svals, slens, gkeys)
         self.scnt[p].copy_(self.cnt[p].t())
-        self._c.all_to_all(self.rcnt[p], self.scnt[p])
+        if self.sync == "flags":
+            self._post(i, 0, self.cnt[p])
+        else:
+            self._c.all_to_all(self.rcnt[p], self.scnt[p])
         if self.transport != "peer":
             n = self.world * self.g.req_b
             o = self.g.req(p, 0)
@@ -332,6 +381,8 @@ class XRoute:
         p = i & 1
         skeys, svals, slens, gkeys = self._batch[p]
         self._out = (sstatus, gout, glens, gstatus)
+        if self.world > 1 and self.sync == "flags":
+            self._wait(i, 0)  # every peer's request block and counts of step i are in this window
         if self.cuda:
             self._exec_dev(p, kvs, skeys, svals, slens, gkeys, sstatus, gout, glens, gstatus, retries)
         else:
@@ -342,7 +393,9 @@ class XRoute:
         if self.world == 1:
             return
         p = i & 1
-        if self.transport == "peer":
+        if self.sync == "flags":
+            self._post(i, 1)
+        elif self.transport == "peer":
             self._cr.all_to_all(self._token_r, self._token)
         else:
             n = self.world * self.g.resp_b
@@ -354,6 +407,8 @@ class XRoute:
         p = i & 1
         skeys, svals, slens, gkeys = self._batch[p]
         if self.world > 1:
+            if self.sync == "flags":
+                self._wait(i, 1)  # every owner's response rows of step i are in this window
             if self.cuda:
                 self._gather_dev(p, skeys, gkeys, sstatus, gout, glens, gstatus)
             else:
@@ -403,7 +458,10 @@ class XRoute:
         x.gostride = gout.shape[1] if gout is not None else 16
         if W > 1:
             x.lidx_set, x.lidx_get = self.lidx[p][0].data_ptr(), self.lidx[p][1].data_ptr()
-            x.own_counts, x.rcounts = self.scnt[p].data_ptr(), self.rcnt[p].data_ptr()
+            x.own_counts = self.scnt[p].data_ptr()
+            # received counts: the all-to-all's output, or (sync "flags") the posts in this window
+            x.rcounts = (self._own_flag + (self.g.off_fcnt - self.g.off_flag) + p * 64 * 2 * 4
+                         if self.sync == "flags" else self.rcnt[p].data_ptr())
             for s_ in range(W):
                 x.req[s_], x.resp[s_] = self._exec_req[p][s_], self._exec_resp[p][s_]
         x.off_sk, x.off_sl, x.off_sv, x.off_gk = g.off_sk, g.off_sl, g.off_sv, g.off_gk

@@ -39,7 +39,8 @@ def test_bench_two_rank_rehearsal_gloo():
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
-                        "--backend", "gloo", *SMALL], cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
+                        "--backend", "gloo", *SMALL, "--search-keys", "2000000"],  # two ranks share one GPU's HBM
+                       cwd=ROOT, capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0, r.stderr[-4000:]
     d = _json(r.stdout)
     assert d["n_gpus"] == 2 and d["integrity_failures"] == 0

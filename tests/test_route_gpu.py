@@ -209,7 +209,8 @@ for i in range(steps + 1):
 kv = ShardedKV(GpuShard(a))
 allids = torch.arange(n * world * steps, device="cuda")[::97]
 s_, v_, l_ = kv.get(format_keys(allids.numel(), "pk", 10, 16, ids=allids), width=160)
-res.update(checked=checked, bad=bad, setbad=setbad, api_bad=int((s_ != 0).sum()))
+res.update(checked=checked, bad=bad, setbad=setbad, api_bad=int((s_ != 0).sum()), sync=xr.sync,
+           sync_err=xr.sync_error())
 print("RES " + json.dumps(res), flush=True)
 xr.close()
 kvs.close()
@@ -219,12 +220,14 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.parametrize("transport", ["peer", "rccl"])
-def test_xroute_two_ranks_one_gpu(tmp_path, transport):
+@pytest.mark.parametrize("transport,sync", [("peer", "flags"), ("peer", "coll"), ("rccl", "coll")])
+def test_xroute_two_ranks_one_gpu(tmp_path, transport, sync):
     """Two ranks (processes) on device 0 run the pipelined routed step through the exchange: the
     peer transport maps each other's windows (VMM dmabuf) and stores request / response rows
-    directly; the rccl transport moves the blocks with collectives (gloo-staged here).  Gets of
-    the keys another rank set two steps earlier must all return their values (integrity 0)."""
+    directly, its steps ordered by device-side posts into the windows (flags) or by the count /
+    response collectives (coll); the rccl transport moves the blocks with collectives (gloo-staged
+    here).  Gets of the keys another rank set two steps earlier must all return their values
+    (integrity 0), and no device-side wait may give up."""
     import json
     import socket
     import subprocess
@@ -237,7 +240,7 @@ def test_xroute_two_ranks_one_gpu(tmp_path, transport):
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-               REPO=root, TAG=str(os.getpid()))
+               REPO=root, TAG=str(os.getpid()), SPLINTER_XR_SYNC=sync)
     ps = [subprocess.Popen([sys.executable, str(w), str(r), "2", transport], env=env, stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE, text=True) for r in range(2)]
     outs = []
@@ -253,7 +256,7 @@ def test_xroute_two_ranks_one_gpu(tmp_path, transport):
         assert rc == 0, (o + e)[-3000:]
         line = [x for x in o.splitlines() if x.startswith("RES ")][-1]
         res = json.loads(line[4:])
-        assert res["transport"] == transport, res
+        assert res["transport"] == transport and res["sync"] == sync and not res["sync_err"], res
         assert res["checked"] == 4 * 30000 and res["bad"] == 0 and res["setbad"] == 0 and res["api_bad"] == 0, res
 
 

@@ -509,7 +509,7 @@ __device__ __forceinline__ void fill_slot(OpSlots<U, KW>& o, int j, const FSeg& 
 template <int U, int KW>
 __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW>& o, bool scrub, bool hybrid,
                                          int max_retry, Stats& st, uint64_t& muts, uint4* cpp0, uint2* cpl0,
-                                         uint4* cpp1, uint2* cpl1, int lane) {
+                                         uint4* cpp1, uint2* cpl1, int lane, bool skip_len) {
   Claim c[U];
   long sidx[U];
   uint64_t e1[U];
@@ -536,6 +536,17 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
       else if (rc[j] == kOk && sg[o.seg[j]].vals && L > (uint32_t)vs) rc[j] = kMsgSize;
     }
   }
+  // an update that keeps its length leaves val_len alone (SPL_KVS_SKIP_LEN, default 1: KV-only 4.94-4.96
+  // vs 4.85-4.89 G ops/s, profiles/r5/kv_skip_len.md): the held claim
+  // makes the slot's val_len stable, and a 4-B write is a partial-line write (read-modify-write
+  // below the 64-B ECC granule of HBM3E); the loads are issued here and consumed after the row copies
+  uint32_t oldlen[U];
+#pragma unroll
+  for (int j = 0; j < U; ++j) {
+    oldlen[j] = 0xFFFFFFFFu;
+    if (skip_len && o.seg[j] >= 0 && o.set[j] && rc[j] == kOk && !c[j].fresh)
+      oldlen[j] = ald32(a.slot((size_t)c[j].idx) + kOffValLen);
+  }
   // value rows: table 0 = sets (client row -> arena, write-through), table 1 = gets (arena -> client)
 #pragma unroll
   for (int j = 0; j < U; ++j) {
@@ -557,7 +568,7 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
   coop_copy<U * 64, 0, true>(cpp1, cpl1, lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
 #pragma unroll
   for (int j = 0; j < U; ++j)
-    if (o.seg[j] >= 0 && o.set[j] && rc[j] == kOk) write_meta<3>(a, c[j], o.len[j]);
+    if (o.seg[j] >= 0 && o.set[j] && rc[j] == kOk && oldlen[j] != o.len[j]) write_meta<3>(a, c[j], o.len[j]);
   drain();
   // gets: closing round trip, (hash, epoch) and the key words together
   {
@@ -610,7 +621,8 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
 
 template <int U, int B, int KW = 16, int OCC = 1>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, FSegs tab,
-                                                                                         int max_retry, uint64_t* stats) {
+                                                                                         int max_retry, uint64_t* stats,
+                                                                                         int skip_len) {
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
   __shared__ FSeg sg[kFusedSegs];
@@ -667,7 +679,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
 #pragma unroll
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
     if (!__syncthreads_or(busy)) break;
-    kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane);
+    kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
+                    skip_len);
   }
   flush_stats(a, st, stats, muts);
 }
@@ -704,7 +717,7 @@ __host__ __device__ inline long async_bound(long n, int i, int parts) {  // firs
 template <int U, int B, int KW = 16, int OCC = 1>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_server(
     spl_arena_t aa, FSeg sset, FSeg sget, int nw, int nr, int ks, AsyncCtl* ctl, uint64_t seq, long chunk,
-    uint64_t wait_ticks, int spread, int max_retry, uint64_t* stats) {
+    uint64_t wait_ticks, int spread, int max_retry, uint64_t* stats, int skip_len) {
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
   __shared__ FSeg sg[2];  // 0: the set batch, 1: the get batch
@@ -835,7 +848,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
       if (!__syncthreads_or(busy)) break;
       kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
-                      lane);
+                      lane, skip_len);
     }
     {
       const uint64_t v[5] = {st.attempts, st.ok, st.again, st.miss, muts};
@@ -869,10 +882,11 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   const long need = (rows + 2 * 256 - 1) / (2 * 256);
   const long cap = 256L * wpc;
   const dim3 g((unsigned)(need < cap ? need : cap));
+  static const int skip_len = env_int("SPL_KVS_SKIP_LEN", 1);
   if (kw4)
-    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats);
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
   else
-    hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats);
+    hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
   return (int)hipGetLastError();
 }
 
@@ -1421,7 +1435,8 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   static const uint64_t wait_ticks = (uint64_t)env_int("SPL_KVS_ASYNC_WAIT_MS", 2000) * 100000ull;  // 100 MHz
   static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
   hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
-                     sset, sget, nw, nr, ks, k->ctl, seq, chunk, wait_ticks, spread, max_retry, stats);
+                     sset, sget, nw, nr, ks, k->ctl, seq, chunk, wait_ticks, spread, max_retry, stats,
+                     env_int("SPL_KVS_SKIP_LEN", 1));
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   (void)hipEventRecord(k->srv_done, origin);

@@ -34,6 +34,7 @@
 #include <dlfcn.h>
 #include <sched.h>
 #include <spawn.h>
+#include <sys/resource.h>
 #include <sys/wait.h>
 #include <unistd.h>
 
@@ -167,7 +168,13 @@ struct RunStats {
   double el = 0;
   uint64_t calls = 0, ok = 0, again = 0, fail = 0;
   double p50 = 0, p90 = 0, p99 = 0, sp50 = 0, sp99 = 0, gp50 = 0, gp99 = 0;
+  // process CPU over the timed window (every thread, the runtime's included): user / system
+  // seconds and context switches -- tells a CPU-bound caller population from a GPU-bound one
+  double usr = 0, sys = 0;
+  long vcsw = 0, ivcsw = 0;
 };
+
+inline double tv_s(const timeval& t) { return (double)t.tv_sec + 1e-6 * (double)t.tv_usec; }
 
 // T threads, set/get mix over K keys for S seconds, every call timed
 RunStats run_calls(const Args& a, size_t max_val, const std::string& val) {
@@ -199,6 +206,8 @@ RunStats run_calls(const Args& a, size_t max_val, const std::string& val) {
         else ++fail[t];
       }
     });
+  rusage ru0{}, ru1{};
+  getrusage(RUSAGE_SELF, &ru0);
   const auto t0 = clk::now();
   go.store(true, std::memory_order_release);
   std::this_thread::sleep_for(std::chrono::duration<double>(a.seconds));
@@ -206,6 +215,11 @@ RunStats run_calls(const Args& a, size_t max_val, const std::string& val) {
   for (auto& x : th) x.join();
   RunStats r;
   r.el = std::chrono::duration<double>(clk::now() - t0).count();
+  getrusage(RUSAGE_SELF, &ru1);
+  r.usr = tv_s(ru1.ru_utime) - tv_s(ru0.ru_utime);
+  r.sys = tv_s(ru1.ru_stime) - tv_s(ru0.ru_stime);
+  r.vcsw = ru1.ru_nvcsw - ru0.ru_nvcsw;
+  r.ivcsw = ru1.ru_nivcsw - ru0.ru_nivcsw;
   std::vector<float> ls, lg, la;
   for (int t = 0; t < a.threads; ++t) {
     ls.insert(ls.end(), lat_set[t].begin(), lat_set[t].end());
@@ -403,10 +417,13 @@ int main(int argc, char** argv) {
          "\"successful_ops_per_s\": %.1f, \"eagain\": %llu, \"failures\": %llu, "
          "\"p50_us\": %.2f, \"p90_us\": %.2f, \"p99_us\": %.2f, \"set_p50_us\": %.2f, \"set_p99_us\": %.2f, "
          "\"get_p50_us\": %.2f, \"get_p99_us\": %.2f, \"procs_p50_us\": [%s], \"ring_mode\": %d, \"value_len\": %d, "
-         "\"set_frac\": %.2f, \"append_check\": %d}\n",
+         "\"set_frac\": %.2f, \"append_check\": %d, \"cpu_usr_s\": %.3f, \"cpu_sys_s\": %.3f, "
+         "\"cpu_us_per_call\": %.2f, \"vcsw_per_call\": %.2f, \"ivcsw_per_call\": %.2f}\n",
          a.store.c_str(), a.threads, a.procs, el, (unsigned long long)calls, total_rate, ok_rate,
          (unsigned long long)tag, (unsigned long long)tf, st.p50, st.p90, st.p99, st.sp50, st.sp99, st.gp50, st.gp99,
-         p50s.c_str(), ring_mode(), a.value_len, a.set_frac, app_ok);
+         p50s.c_str(), ring_mode(), a.value_len, a.set_frac, app_ok, st.usr, st.sys,
+         st.calls ? 1e6 * (st.usr + st.sys) / (double)st.calls : 0.0,
+         st.calls ? (double)st.vcsw / (double)st.calls : 0.0, st.calls ? (double)st.ivcsw / (double)st.calls : 0.0);
   splinter_close();
   spl_unlink(a.store.c_str());
   return rc;

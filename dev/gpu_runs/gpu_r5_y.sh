@@ -9,3 +9,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smok
 tail -1 $OUT/smoke.txt
 timeout -k 10 900 python bench.py > $OUT/bench.out 2> $OUT/bench.err || { tail -20 $OUT/bench.err; exit 1; }
 tail -1 $OUT/bench.out
+# command-processor-woken worker probe (scripts/probes/cpwait_probe.hip)
+hipcc --offload-arch=gfx950 -O2 -o $OUT/cpwait_probe scripts/probes/cpwait_probe.hip 2> $OUT/cpwait_build.err || { tail -5 $OUT/cpwait_build.err; exit 1; }
+timeout -k 10 120 $OUT/cpwait_probe > $OUT/cpwait.jsonl 2> $OUT/cpwait.err || { tail -5 $OUT/cpwait.err; exit 1; }
+cat $OUT/cpwait.jsonl

@@ -182,3 +182,17 @@ def test_list_copy_for_ffi_bindings(store):
     buf = ctypes.create_string_buffer(need)
     n = L.spl_list_copy(buf, need)
     assert n == need and sorted(buf.raw[:n].split(b"\0")[:-1]) == [b"k1", b"key_two"]
+
+
+def test_hostapi_bench_reports_cpu_per_call(uniq):
+    """splinter_hostapi_bench on a shm store: every call succeeds, and the JSON line carries the
+    process CPU accounting of the timed window (user / system seconds, CPU us per call)."""
+    import json
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    tool = os.path.join(root, "libsplinter_amd", "bin", "splinter_hostapi_bench")
+    r = subprocess.run([tool, "--store", uniq, "--threads", "4", "--seconds", "0.3", "--keys", "2000"],
+                       capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stderr[-2000:]
+    res = json.loads(r.stdout.strip().splitlines()[-1])
+    assert res["failures"] == 0 and res["calls"] > 0
+    assert res["cpu_usr_s"] + res["cpu_sys_s"] > 0 and res["cpu_us_per_call"] > 0

@@ -10,7 +10,7 @@ export TMPDIR=/tmp
 for f in 0 2; do
   SPL_KVS_FUSED=$f timeout -s KILL 400 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
     SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$ROOT/$OUT/pmc_kv$f" -o run -- python3 bench.py --mode kv \
-    --steps 5 --warmup 2 --host-api 0 --host-api-threads2 0 --routed-steps 0 > "$OUT/kv$f.out" 2> "$OUT/kv$f.err"
+    --steps 5 --warmup 2 --host-api 0 --host-api-threads2 0 --exchange-ab 0 > "$OUT/kv$f.out" 2> "$OUT/kv$f.err"
   rc=$?
   echo "== kv$f rc=$rc"; tail -c 400 "$OUT/kv$f.out"
   if [ $rc -ne 0 ]; then tail -20 "$OUT/kv$f.err"; exit $rc; fi

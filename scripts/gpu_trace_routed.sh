@@ -6,7 +6,7 @@ OUT=${OUT:-gpurun_out/trace_routed}
 mkdir -p "$OUT"
 ROOT=$(pwd)
 export TMPDIR=/tmp
-ARGS="--steps 10 --warmup 3 --embed-e2e 0 --host-api 0 --host-api-threads2 0 --daemon-docs 0 --routed-steps 0"
+ARGS="--steps 10 --warmup 3 --embed-e2e 0 --host-api 0 --host-api-threads2 0 --daemon-docs 0"
 for mode in native routed; do
   extra=""; [ $mode = routed ] && extra="--force-routed"
   SPL_PROFILE_TIMED=1 timeout -k 10 400 rocprofv3 --kernel-trace --output-format csv -d "$ROOT/$OUT/tr_$mode" -o run \

@@ -479,16 +479,21 @@ using mf::bf16x8;
 using mf::f32x4;
 using mf::rsrc_t;
 using mf::lds_void;
-constexpr int kTile = mf::kTile, kThreads = mf::kThreads, kQ = mf::kQ, kNJ = mf::kNJ, kSteps = mf::kSteps;
-constexpr int kChunk = kTile * 64;        // 16 KB of bf16 per K-chunk
-constexpr int kRing = mf::kRing, kAhead = mf::kAhead, kDist = mf::kDist;
-constexpr int kDma = kChunk / 1024 / 4;   // 4 wave-instructions per wave per chunk
+constexpr int kTile = mf::kTile, kQ = mf::kQ, kNJ = mf::kNJ, kSteps = mf::kSteps;
+constexpr int kWaves = 8, kThreads = kWaves * 64;  // two waves per SIMD
+constexpr int kChunk = kTile * 64;        // 16 KB of bf16 slot rows per K-chunk
+constexpr int kQChunk = kQ * 64;          // 16 KB of bf16 query fragments per K-chunk
+constexpr int kRing = mf::kRing, kAhead = mf::kAhead;
+constexpr int kRows = kTile / kWaves;     // slot rows a wave stages (DMA, metadata): 32
+constexpr int kBlk = 8;                   // 16-row blocks per wave: one slot half
 constexpr int kRsrcWord3 = mf::kRsrcWord3;
 struct Smem {
-  char ring[kRing * kChunk];  // 64 KB
+  char ring[kRing][kChunk];   // 64 KB
+  char qring[kRing][kQChunk]; // 64 KB
   __attribute__((aligned(16))) float inv[kTile];
   __attribute__((aligned(16))) int live[kTile];
   uint32_t ncand[kQ];
+  float pmax[kQ];             // MODE 0: the upper slot half's per-query maxima
 };
 __device__ __forceinline__ int fsw(int b) { return (0x1B2 >> (2 * b)) & 3; }  // {0, 2, 3, 1}[b]
 
@@ -496,6 +501,14 @@ __device__ __forceinline__ rsrc_t tile_rsrc16(const spl::dev::Arena& a, long t, 
   return __builtin_amdgcn_make_buffer_rsrc(a.vec16((size_t)mf::tile_start(t, slot_end)), 0, kTile * 1536, kRsrcWord3);
 }
 
+// Two waves per SIMD: wave w owns the 64 queries of group w & 3 against slot half w >> 2 (8 x 4
+// accumulator tiles, 128 registers), so one wave's matrix work runs while its partner waits on the
+// DMA / barrier (with one wave per SIMD the two were serialised: without its MFMAs that pass took
+// 8.4 of its 13.5 ms, profiles/r5/search_probes).  The query fragments of a K-chunk (16 KB) arrive
+// by LDS-DMA beside the slot rows, so no wave stages them in registers three chunks ahead.
+// In-order vmcnt: a wave issues per step (the metadata, 3 loads, at step 0, then) the DMA of chunk
+// s + 3, 2 query + 2 row pieces; younger than chunk s's DMA at the top of step s: 8, or 11 when one
+// of the two steps after its issue was a step 0 (s = 1, 2).
 template <int MODE>
 __global__ __launch_bounds__(kThreads, 1) void k_search_mma16(spl_arena_t aa, const void* __restrict__ qf, int nq,
                                                              long slot_begin, long slot_end, uint64_t mask,
@@ -506,25 +519,27 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma16(spl_arena_t aa, co
   const spl::dev::Arena a = spl::dev::from_api(aa);
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fr = lane & 15, fq = lane >> 4;
+  const int qg = wave & 3, sh = wave >> 2;
   const long tile_base = slot_begin / kTile;
   const long tile_end = (slot_end + kTile - 1) / kTile, G = gridDim.x;
   const long t0 = tile_base + blockIdx.x;
   if (t0 >= tile_end) return;  // block-uniform
-  if (MODE == 1) sm.ncand[threadIdx.x] = 0;
+  if (MODE == 1 && tid < kQ) sm.ncand[tid] = 0;
 
   const rsrc_t qr = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(qf), 0, kQ * kD * 2, kRsrcWord3);
-  const int qvoff = lane * 16, qtile0 = wave * kNJ;
-  // DMA geometry: wave-instruction k of a chunk fills rows 64w + 16k .. +16 (1 KB), lane l -> row
-  // +(l >> 2), physical unit l & 3 <- logical unit (l & 3) ^ f(row >> 2)
-  int dvoff[kDma];
+  const int qtile0 = qg * kNJ;
+  // row DMA: wave-instruction k of a chunk fills rows 32w + 16k .. +16 (1 KB), lane l -> row +(l >> 2),
+  // physical unit l & 3 <- logical unit (l & 3) ^ f(row >> 2); query DMA: instruction k brings the
+  // 1-KB fragment block of 16-query tile 2w + k for the chunk's step (lane-linear, as read)
+  int dvoff[2];
 #pragma unroll
-  for (int k = 0; k < kDma; ++k) {
-    const int row = wave * 64 + k * 16 + (lane >> 2);
+  for (int k = 0; k < 2; ++k) {
+    const int row = wave * kRows + k * 16 + (lane >> 2);
     dvoff[k] = row * 1536 + (((lane & 3) ^ fsw((row >> 2) & 3)) << 4);
   }
   const float* nrm2 = a.nrm2();
-  // fragment read: row 16i + fr, logical unit fq
-  const int rdo = fr * 64 + ((fq ^ fsw((fr >> 2) & 3)) << 4);
+  // fragment read: row 16i + fr of this wave's slot half, logical unit fq
+  const int rdo = fr * 64 + ((fq ^ fsw((fr >> 2) & 3)) << 4) + sh * kBlk * 1024;
 
   float thr[kNJ];
 #pragma unroll
@@ -533,18 +548,16 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma16(spl_arena_t aa, co
     thr[j] = (MODE == 1 && q < nq) ? thr_in[q] : FLT_MAX;
   }
   auto issue = [&](rsrc_t er, int c, int slot) {
-    char* dst = sm.ring + slot * kChunk + wave * 64 * 64;
 #pragma unroll
-    for (int k = 0; k < kDma; ++k)
+    for (int k = 0; k < 2; ++k)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(qr, (lds_void*)(sm.qring[slot] + (2 * wave + k) * 1024), 16, lane * 16,
+                                               ((2 * wave + k) * kSteps + c) * 1024, 0, 0);
+    char* dst = sm.ring[slot] + wave * kRows * 64;
+#pragma unroll
+    for (int k = 0; k < 2; ++k)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(er, (lds_void*)(dst + k * 1024), 16, dvoff[k], c * 64, 0, 0);
   };
   const long last = tile_end - 1;
-
-  bf16x8 b[kDist + 1][kNJ];
-#pragma unroll
-  for (int s = 0; s < kDist; ++s)
-#pragma unroll
-    for (int j = 0; j < kNJ; ++j) b[s][j] = mf::load_qfrag(qr, qvoff, qtile0 + j, s);
   {
     const rsrc_t er = tile_rsrc16(a, t0, slot_end);
     for (int c = 0; c < kAhead; ++c) issue(er, c, c);
@@ -556,40 +569,33 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma16(spl_arena_t aa, co
     const rsrc_t er_next = tile_rsrc16(a, t + G < tile_end ? t + G : last, slot_end);
     uint64_t h = 0, bl = 0;
     float n2 = 0.f;
-    f32x4 acc[16][kNJ];
+    f32x4 acc[kBlk][kNJ];
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
+    for (int i = 0; i < kBlk; ++i)
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma clang loop unroll(full)
     for (int s = 0; s < kSteps; ++s) {
-      // in-order vmcnt accounting as k_search_mma: per step the query fragments (4 loads), at step 0
-      // the metadata (3 loads: hash, bloom, norm), then the chunk DMA (4): younger than chunk s's DMA
-      // at the top of step s are the two following steps' ops: 16, or 19 when one was a step 0; the
-      // prologue (fragments 0..2, then DMA 0..2) gives lower bounds 8 at s = 0 and 15 at s = 1
-      if (s == 0)
-        SPL_STEP_SYNC(8);
-      else if (s == 1)
-        SPL_STEP_SYNC(15);
-      else if (s == 2)
-        SPL_STEP_SYNC(19);
+      if (s == 1 || s == 2)
+        SPL_STEP_SYNC(11);
       else
-        SPL_STEP_SYNC(16);
-#pragma unroll
-      for (int j = 0; j < kNJ; ++j)
-        b[(s + kDist) % (kDist + 1)][j] = mf::load_qfrag(qr, qvoff, qtile0 + j, (s + kDist) % kSteps);
-      if (s == 0) {  // metadata of this wave's 64 rows, one per lane
-        const long row = start + wave * 64 + lane;
+        SPL_STEP_SYNC(8);
+      if (s == 0) {  // metadata of this wave's 32 rows (lanes 32-63 repeat 0-31)
+        const long row = start + wave * kRows + (lane & (kRows - 1));
         const uint8_t* sp = a.slot((size_t)row);
         h = __builtin_nontemporal_load((const uint64_t*)(sp + spl::kOffHash));
         bl = __builtin_nontemporal_load((const uint64_t*)(sp + spl::kOffBloom));
         n2 = __builtin_nontemporal_load(nrm2 + row);
       }
       issue(s + kAhead < kSteps ? er_cur : er_next, (s + kAhead) % kSteps, (s + kAhead) % kRing);
-      const char* ch = sm.ring + (s % kRing) * kChunk + rdo;
+      const char* qs = sm.qring[s % kRing] + lane * 16;
+      bf16x8 bq[kNJ];
 #pragma unroll
-      for (int i0 = 0; i0 < 16; i0 += 4) {
+      for (int j = 0; j < kNJ; ++j) bq[j] = *(const bf16x8*)(qs + (qtile0 + j) * 1024);
+      const char* ch = sm.ring[s % kRing] + rdo;
+#pragma unroll
+      for (int i0 = 0; i0 < kBlk; i0 += 4) {
         bf16x8 af[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) af[u] = *(const bf16x8*)(ch + (i0 + u) * 1024);
@@ -597,24 +603,26 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma16(spl_arena_t aa, co
         for (int u = 0; u < 4; ++u)
 #pragma unroll
           for (int j = 0; j < kNJ; ++j)
-            acc[i0 + u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], b[s % (kDist + 1)][j], acc[i0 + u][j], 0, 0, 0);
+            acc[i0 + u][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[u], bq[j], acc[i0 + u][j], 0, 0, 0);
       }
     }
     {
       constexpr float kMinNorm2 = MODE == 0 ? 2e-12f : 0.f;  // MODE 0 counts surely-live slots only
-      const int row = wave * 64 + lane;
-      sm.live[row] = h != 0 && (!mask || (bl & mask) == mask) && n2 > kMinNorm2 && start + row >= t * kTile;
-      sm.inv[row] = n2 > 0.f ? rsqrtf(n2) : 0.f;
+      const int row = wave * kRows + lane;
+      if (lane < kRows) {
+        sm.live[row] = h != 0 && (!mask || (bl & mask) == mask) && n2 > kMinNorm2 && start + row >= t * kTile;
+        sm.inv[row] = n2 > 0.f ? rsqrtf(n2) : 0.f;
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     {
-      const f32x4* invp = (const f32x4*)(sm.inv + fq * 4);
-      const int4* livp = (const int4*)(sm.live + fq * 4);
+      const f32x4* invp = (const f32x4*)(sm.inv + fq * 4 + sh * kBlk * 16);
+      const int4* livp = (const int4*)(sm.live + fq * 4 + sh * kBlk * 16);
       float best[kNJ];
 #pragma unroll
       for (int j = 0; j < kNJ; ++j) best[j] = -FLT_MAX;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < kBlk; ++i) {
         const f32x4 iv = invp[i * 4];
         const int4 lv = livp[i * 4];
         const int lvr[4] = {lv.x, lv.y, lv.z, lv.w};
@@ -628,25 +636,35 @@ __global__ __launch_bounds__(kThreads, 1) void k_search_mma16(spl_arena_t aa, co
             } else if (sim >= thr[j] && lvr[r]) {
               const int q = (qtile0 + j) * 16 + fr;
               const uint32_t p = atomicAdd(&sm.ncand[q], 1u);
-              if (p < (uint32_t)capb) cand[((long)q * gridDim.x + blockIdx.x) * capb + p] = (uint32_t)(start + i * 16 + fq * 4 + r);
+              if (p < (uint32_t)capb)
+                cand[((long)q * gridDim.x + blockIdx.x) * capb + p] = (uint32_t)(start + (sh * kBlk + i) * 16 + fq * 4 + r);
             }
           }
       }
-      if (MODE == 0) {
+      if (MODE == 0) {  // per query: max over the lane quads, then the two slot halves meet in LDS
+        float bj[kNJ];
 #pragma unroll
         for (int j = 0; j < kNJ; ++j) {
-          const int q = (qtile0 + j) * 16 + fr;
-          float bj = fmaxf(best[j], __shfl_xor(best[j], 16, 64));
-          bj = fmaxf(bj, __shfl_xor(bj, 32, 64));
-          if (fq == 0 && q < nq) bmax[(t - tile_base) * nq + q] = bj;
+          bj[j] = fmaxf(best[j], __shfl_xor(best[j], 16, 64));
+          bj[j] = fmaxf(bj[j], __shfl_xor(bj[j], 32, 64));
         }
+        if (sh == 1 && fq == 0)
+#pragma unroll
+          for (int j = 0; j < kNJ; ++j) sm.pmax[(qtile0 + j) * 16 + fr] = bj[j];
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (sh == 0 && fq == 0)
+#pragma unroll
+          for (int j = 0; j < kNJ; ++j) {
+            const int q = (qtile0 + j) * 16 + fr;
+            if (q < nq) bmax[(t - tile_base) * nq + q] = fmaxf(bj[j], sm.pmax[q]);
+          }
       }
     }
   }
   if (MODE == 1) {
     mf::raw_barrier();
     const int q = threadIdx.x;
-    if (q < nq) cnt[(long)q * gridDim.x + blockIdx.x] = sm.ncand[q];
+    if (q < nq && q < kQ) cnt[(long)q * gridDim.x + blockIdx.x] = sm.ncand[q];
   }
   mf::wait_vm0();
 }

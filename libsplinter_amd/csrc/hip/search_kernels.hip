@@ -697,36 +697,47 @@ __global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __
   __syncthreads();
   const float qn = qn_s;
   int c = 0;
+  // kRU candidates of a wave in flight at once (their slot headers and 3-KB rows loaded together):
+  // one candidate at a time left each wave on a chain of dependent loads per row
+  constexpr int kRU = 4;
+  const float4* q4 = (const float4*)Qs;
   for (int b = wave; b < nblk; b += kWaves) {
     const int n = min(cnt[(long)q * nblk + b], (uint32_t)capb);
     const uint32_t* seg = cand + ((long)q * nblk + b) * capb;
-    for (int t = 0; t < n; ++t) {
-      const uint32_t idx = seg[t];
-      const uint8_t* s = a.slot(idx);
-      const uint64_t h = *(const uint64_t*)(s + spl::kOffHash);
-      if (h == 0 || (mask && (*(const uint64_t*)(s + spl::kOffBloom) & mask) != mask)) continue;
-      const float4* v4 = (const float4*)(s + spl::kOffEmbed);
-      float4 e[3];
+    for (int t = 0; t < n; t += kRU) {
+      uint32_t idx[kRU];
+      uint64_t h[kRU], bl[kRU];
+      float4 e[kRU][3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) e[k] = v4[lane + 64 * k];
-      float en = 0.f;
+      for (int u = 0; u < kRU; ++u) idx[u] = seg[t + u < n ? t + u : t];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) en += e[k].x * e[k].x + e[k].y * e[k].y + e[k].z * e[k].z + e[k].w * e[k].w;
-      en = wave_sum(en);
-      if (en < 1e-12f) continue;
-      const float enr = sqrtf(en);
-      const float4* q4 = (const float4*)Qs;
-      float dot = 0.f;
+      for (int u = 0; u < kRU; ++u) {
+        const uint8_t* s = a.slot(idx[u]);
+        h[u] = *(const uint64_t*)(s + spl::kOffHash);
+        bl[u] = mask ? *(const uint64_t*)(s + spl::kOffBloom) : 0;
+        const float4* v4 = (const float4*)(s + spl::kOffEmbed);
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const float4 qq = q4[lane + 64 * k];
-        dot += e[k].x * qq.x + e[k].y * qq.y + e[k].z * qq.z + e[k].w * qq.w;
+        for (int k = 0; k < 3; ++k) e[u][k] = v4[lane + 64 * k];
       }
-      dot = wave_sum(dot);
-      const float sim = dot / (enr * sqrtf(qn) + 1e-30f);
-      const float dist = sqrtf(fmaxf(en + qn - 2.f * dot, 0.f));
-      if (sim < min_sim || dist > max_dist) continue;
-      if (lane == 0) c = insert(top[wave], c, K, Cand{sim, dist, idx, 0});
+#pragma unroll
+      for (int u = 0; u < kRU; ++u) {
+        if (t + u >= n || h[u] == 0 || (mask && (bl[u] & mask) != mask)) continue;  // wave-uniform
+        float en = 0.f, dot = 0.f;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+          const float4 qq = q4[lane + 64 * k];
+          en += e[u][k].x * e[u][k].x + e[u][k].y * e[u][k].y + e[u][k].z * e[u][k].z + e[u][k].w * e[u][k].w;
+          dot += e[u][k].x * qq.x + e[u][k].y * qq.y + e[u][k].z * qq.z + e[u][k].w * qq.w;
+        }
+        en = wave_sum(en);
+        if (en < 1e-12f) continue;
+        dot = wave_sum(dot);
+        const float enr = sqrtf(en);
+        const float sim = dot / (enr * sqrtf(qn) + 1e-30f);
+        const float dist = sqrtf(fmaxf(en + qn - 2.f * dot, 0.f));
+        if (sim < min_sim || dist > max_dist) continue;
+        if (lane == 0) c = insert(top[wave], c, K, Cand{sim, dist, idx[u], 0});
+      }
     }
   }
   if (lane == 0) tc[wave] = c;

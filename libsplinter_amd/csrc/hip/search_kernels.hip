@@ -676,18 +676,20 @@ namespace mf {
 // fp32 re-score of the candidates of one query (block) and top-K selection;
 // same arithmetic as k_score_topk so the ranking is identical.  Candidates
 // come in block-private segments cand[q][b][0 .. min(cnt[q][b], capb)).
-__global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __restrict__ queries, int K,
+// 16 waves per query block (4 per SIMD): the re-score is a gather of 3-KB rows bound by loads in flight
+constexpr int kRsWaves = 16;
+__global__ __launch_bounds__(kRsWaves * 64) void k_rescore(spl_arena_t aa, const float* __restrict__ queries, int K,
                                                  float min_sim, float max_dist, uint64_t mask,
                                                  const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ cand,
                                                  int nblk, int capb, Cand* __restrict__ result) {
   __shared__ __attribute__((aligned(16))) float Qs[kD];
   __shared__ float qn_s;
-  __shared__ Cand top[kWaves][kMaxK];
-  __shared__ int tc[kWaves];
+  __shared__ Cand top[kRsWaves][kMaxK];
+  __shared__ int tc[kRsWaves];
   const spl::dev::Arena a = spl::dev::from_api(aa);
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int i = tid; i < kD; i += 256) Qs[i] = queries[(long)q * kD + i];
-  if (tid < kWaves) tc[tid] = 0;
+  for (int i = tid; i < kD; i += kRsWaves * 64) Qs[i] = queries[(long)q * kD + i];
+  if (tid < kRsWaves) tc[tid] = 0;
   __syncthreads();
   if (tid == 0) {
     float s = 0.f;
@@ -701,7 +703,7 @@ __global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __
   // one candidate at a time left each wave on a chain of dependent loads per row
   constexpr int kRU = 4;
   const float4* q4 = (const float4*)Qs;
-  for (int b = wave; b < nblk; b += kWaves) {
+  for (int b = wave; b < nblk; b += kRsWaves) {
     const int n = min(cnt[(long)q * nblk + b], (uint32_t)capb);
     const uint32_t* seg = cand + ((long)q * nblk + b) * capb;
     for (int t = 0; t < n; t += kRU) {
@@ -745,7 +747,7 @@ __global__ __launch_bounds__(256) void k_rescore(spl_arena_t aa, const float* __
   if (tid == 0) {
     Cand L[kMaxK];
     int m = 0;
-    for (int w = 0; w < kWaves; ++w)
+    for (int w = 0; w < kRsWaves; ++w)
       for (int j = 0; j < tc[w]; ++j) m = insert(L, m, K, top[w][j]);
     for (int j = 0; j < K; ++j) result[(long)q * K + j] = j < m ? L[j] : Cand{-FLT_MAX, FLT_MAX, 0xffffffffu, 0};
   }
@@ -926,7 +928,7 @@ int spl_search_rescore(spl_arena_t a, const float* queries, int nq, int K, float
                        uint64_t mask, const uint32_t* cnt, const uint32_t* cand, int nblk, int capb, void* result,
                        hipStream_t s) {
   if (a.stride != 3200 || nq <= 0 || K <= 0 || K > kMaxK || nblk <= 0 || capb <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(mf::k_rescore, dim3(nq), dim3(256), 0, s, a, queries, K, min_sim, max_dist, mask, cnt, cand,
+  hipLaunchKernelGGL(mf::k_rescore, dim3(nq), dim3(mf::kRsWaves * 64), 0, s, a, queries, K, min_sim, max_dist, mask, cnt, cand,
                      nblk, capb, (Cand*)result);
   return (int)hipGetLastError();
 }

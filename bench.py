@@ -927,6 +927,9 @@ def main():
         "daemon_docs_embedded": daemon["embedded"] if daemon else None,
         "daemon_docs_expected": daemon["expected"] if daemon else None,
         "search_qps": search["qps"] if search else None,
+        "search_path": ("spl_search_batch (C ABI: device query prep, bf16 MFMA candidate passes, fp32 re-score, keys "
+                        "with the hits)" if GpuShard.capi_search else "ops/search.py VectorSearch.search_batch")
+        if search else None,
         "search_ms_per_batch": search["ms_per_batch"] if search else None,
         "search_recall_at_10": search["recall_at_10"] if search else None,
         "search_keys_total": search["keys_total"] if search else None,

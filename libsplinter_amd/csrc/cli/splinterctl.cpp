@@ -1246,14 +1246,30 @@ int cmd_stats(int, char**) {
   return 0;
 }
 
-// `rehash`: the tombstone rebuild of an hbm: / node: store (spl_hbm_rehash; exclusive maintenance)
-int cmd_rehash(int, char**) {
+// `rehash [--full]`: tombstone maintenance of an hbm: / node: store (spl_hbm_rehash_ex): the online
+// compaction by default (safe beside live clients), --full the exclusive rebuild
+int cmd_rehash(int argc, char** argv) {
   if (!need_store("rehash")) return 1;
-  using RehashFn = int (*)(spl_store*, uint64_t*);
-  auto fn = (RehashFn)dlsym(RTLD_DEFAULT, "spl_hbm_rehash");
+  unsigned flags = 0;
+  for (int i = 1; i < argc; ++i) {
+    if (!strcmp(argv[i], "--full")) flags |= 1u;  // SPL_REHASH_FULL
+    else {
+      fprintf(stderr, "rehash: unknown option %s\n", argv[i]);
+      return 1;
+    }
+  }
+  using RehashFn = int (*)(spl_store*, unsigned, uint64_t*);
+  auto fn = (RehashFn)dlsym(RTLD_DEFAULT, "spl_hbm_rehash_ex");
   uint64_t out[4] = {0, 0, 0, 0};
-  if (!fn || fn(spl_store_current(), out) != 0) {
-    fprintf(stderr, "rehash: only hbm: and node: stores of HBM shards (device pass), or the pass failed\n");
+  errno = 0;
+  if (!fn || fn(spl_store_current(), flags, out) != 0) {
+    if (errno == EBUSY)
+      fprintf(stderr, "rehash: busy (another maintenance pass is running%s)\n",
+              flags ? ", or this store's ring worker could not be held" : "");
+    else if (errno == ENOMEM)
+      fprintf(stderr, "rehash: the full rebuild's scratch does not fit on the device; run the online rehash\n");
+    else
+      fprintf(stderr, "rehash: only hbm: and node: stores of HBM shards (device pass), or the pass failed\n");
     return 1;
   }
   printf("moved=%lu\nreclaimed=%lu\nclusters=%lu\nskipped=%lu\n", (unsigned long)out[0], (unsigned long)out[1],
@@ -1527,8 +1543,8 @@ void register_modules() {
       {"ingest", "Chunk a file or stdin into VARTEXT tandem keys.", cmd_ingest,
        [] { puts("Usage: ingest [file] [--key <key>] [--label <hex>]"); }},
       {"stats", "Store occupancy, embeddings, signal counters and (hbm/node) probe-chain health.", cmd_stats, nullptr},
-      {"rehash", "Rebuild probe chains: move keys into tombstones on their path, reclaim trailing ones (hbm/node, exclusive).",
-       cmd_rehash, [] { puts("Usage: rehash   (no other process may write to the store meanwhile)"); }},
+      {"rehash", "Rebuild probe chains: move keys into tombstones on their path, reclaim trailing ones (hbm/node, online).",
+       cmd_rehash, [] { puts("Usage: rehash [--full]   (online beside live clients; --full: exclusive rebuild, stop every client first)"); }},
       {"wasm", "Run a WASM module (binary or WAT) against the store.", cmd_wasm,
        [] { puts("Usage: wasm <plugin.wasm|plugin.wat> [function_name]\nExecutes a WASM module with access to the Splinter bus."); }},
       {"lua", "Run a Lua script against the store (splinter module).", cmd_lua,

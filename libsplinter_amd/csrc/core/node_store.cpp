@@ -9,10 +9,12 @@
 #include <cstring>
 #include <fcntl.h>
 #include <poll.h>
+#include <signal.h>
 #include <sys/eventfd.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <sys/syscall.h>
+#include <time.h>
 #include <unistd.h>
 #include <emmintrin.h>
 #include <algorithm>
@@ -122,14 +124,139 @@ StoreBase* make_shard(const std::string& node, int i, uint32_t backend, bool cre
                 : (StoreBase*)HostStore::open(bare.c_str(), false, err);
 }
 
+// The stand-in of a shard whose owning rank process is gone: every op answers EAGAIN (the
+// reference's recoverable status, splinter.h:400-412) -- the key's shard is not served until its
+// rank's restarted process re-joins -- and the other shards of the node keep serving.
+class DownShard final : public StoreBase {
+ public:
+  explicit DownShard(Geometry g) : g_(g) {}
+  static int again() { errno = EAGAIN; return -1; }
+  const char* backend() const override { return "down"; }
+  Geometry geometry() const override { return g_; }
+  splinter_header* header_ptr() override { return nullptr; }
+  int set_mop(unsigned) override { return again(); }
+  int get_mop() override { return again(); }
+  void purge() override {}
+  int header_snapshot(splinter_header_snapshot_t*) override { return again(); }
+  uint8_t config_get() override { return 0; }
+  void config_or(uint8_t) override {}
+  void config_and(uint8_t) override {}
+  int set(const char*, const void*, size_t) override { return again(); }
+  int unset(const char*) override { return again(); }
+  int get(const char*, void*, size_t, size_t*) override { return again(); }
+  int list(char**, size_t, size_t* n) override { if (n) *n = 0; return 0; }
+  int poll(const char*, uint64_t) override { return again(); }
+  int slot_snapshot(const char*, splinter_slot_snapshot_t*) override { return again(); }
+  int append(const char*, const void*, size_t, size_t*) override { return again(); }
+  const void* raw_ptr(const char*, size_t*, uint64_t*) override { errno = EAGAIN; return nullptr; }
+  uint64_t epoch_of(const char*) override { errno = EAGAIN; return 0; }
+  int set_as_system(const char*) override { return again(); }
+  int set_embedding(const char*, const float*) override { return again(); }
+  int get_embedding(const char*, float*) override { return again(); }
+  int set_named_type(const char*, uint16_t) override { return again(); }
+  int set_slot_time(const char*, unsigned short, uint64_t, size_t) override { return again(); }
+  int integer_op(const char*, splinter_integer_op_t, const void*) override { return again(); }
+  int bump(const char*) override { return again(); }
+  int retrain(const char*) override { return again(); }
+  int set_label(const char*, uint64_t) override { return again(); }
+  int unset_label(const char*, uint64_t) override { return again(); }
+  int watch_register(const char*, uint8_t) override { return again(); }
+  int watch_unregister(const char*, uint8_t) override { return again(); }
+  int watch_label_register(uint64_t, uint8_t) override { return again(); }
+  int pulse_keygroup(const char*) override { return again(); }
+  void pulse_slot(splinter_slot*) override {}
+  uint64_t signal_count(uint8_t) override { return 0; }
+  int signal_add(uint8_t, uint64_t) override { return again(); }
+  void enumerate(uint64_t, void (*)(const char*, uint64_t, void*), void*) override {}
+  int event_bus_init() override { return again(); }
+  int event_bus_open() override { return again(); }
+  void event_bus_dirty(uint64_t* out, size_t words) override { for (size_t i = 0; i < words; ++i) out[i] = 0; }
+  int shard_claim_ex(uint32_t, uint32_t, uint8_t, uint8_t, uint64_t, uint64_t) override { return again(); }
+  int shard_rebid(uint32_t, uint8_t, uint8_t, uint64_t) override { return again(); }
+  int shard_release(uint32_t) override { return again(); }
+  uint32_t shard_election(uint8_t*) override { return 0; }
+  int shard_table(splinter_shard_bid_snapshot*, size_t) override { return 0; }
+  int madvise(uint32_t, void*, size_t, int, uint64_t) override { return again(); }
+  static long fill(int32_t* st, long n) {
+    if (st)
+      for (long i = 0; i < n; ++i) st[i] = -EAGAIN;
+    return 0;
+  }
+  long set_batch(const char*, int, const uint8_t*, int, const uint32_t*, long n, int32_t* st, int) override {
+    return fill(st, n);
+  }
+  long get_batch(const char*, int, uint8_t*, int, uint32_t* ol, long n, int32_t* st, int) override {
+    if (ol)
+      for (long i = 0; i < n; ++i) ol[i] = 0;
+    return fill(st, n);
+  }
+  long intop_batch(const char*, int, const int*, const uint64_t*, long n, int32_t* st, uint64_t*) override {
+    return fill(st, n);
+  }
+  long set_embedding_batch(const char*, int, const float*, long n, int32_t* st) override { return fill(st, n); }
+
+ private:
+  Geometry g_;
+};
+
+uint64_t mono_ns() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+
+bool pid_gone(int32_t pid) { return pid > 0 && kill((pid_t)pid, 0) != 0 && errno == ESRCH; }
+
 }  // namespace
 
 std::string node_shard_name(const std::string& node, int i, uint32_t backend) {
   return std::string(backend == 1 ? "hbm:" : "shm:") + node + ".s" + std::to_string(i);
 }
 
-StoreBase* NodeStore::route(const char* key) const {
-  return shards_[node_shard_of(KeyRef(key).hash, (int)shards_.size())];
+StoreBase* NodeStore::route(const char* key) {
+  refresh();
+  return at(node_shard_of(KeyRef(key).hash, (int)shards_.size()));
+}
+
+// Degraded mode: see node_store.hpp.  Joined nodes only (a node created whole by one process owns
+// every shard itself: shard_pid 0).
+void NodeStore::refresh(bool force) {
+  constexpr uint64_t kRefreshNs = 20 * 1000 * 1000;
+  const uint64_t now = mono_ns();
+  if (!force && now < next_refresh_ns_.load(std::memory_order_relaxed)) return;
+  std::lock_guard<std::mutex> lk(refresh_mu_);
+  next_refresh_ns_.store(now + kRefreshNs, std::memory_order_relaxed);
+  for (int i = 0; i < nshards(); ++i) {
+    const int32_t pid = __atomic_load_n(&desc_->shard_pid[i], __ATOMIC_ACQUIRE);
+    const uint32_t g = __atomic_load_n(&desc_->shard_gen[i], __ATOMIC_ACQUIRE);
+    const bool ready = (__atomic_load_n(&desc_->ready_mask, __ATOMIC_ACQUIRE) >> i) & 1ull;
+    StoreBase* want = real_[(size_t)i];
+    const bool owned = __atomic_load_n(&desc_->shard_flags[i], __ATOMIC_ACQUIRE) & kShardOwned;
+    if (g != gen_[(size_t)i] && ready && !(owned && pid_gone(pid))) {
+      // the shard re-joined (its rank restarted): open the new shard store
+      int err = 0;
+      StoreBase* sh = make_shard(name_, i, desc_->backend, false, 0, 0, false, -1, &err);
+      const Geometry geo = sh ? sh->geometry() : Geometry{};
+      if (sh && geo.slots == desc_->slots_per_shard && geo.max_val == desc_->max_val && geo.stride == desc_->stride) {
+        retired_.push_back(real_[(size_t)i]);
+        real_[(size_t)i] = sh;
+        gen_[(size_t)i] = g;
+        want = sh;
+      } else {
+        delete sh;
+        want = down_;
+      }
+    } else if (g != gen_[(size_t)i] || !ready || (owned && pid_gone(pid))) {
+      want = down_;
+    }
+    __atomic_store_n(&shards_[(size_t)i], want, __ATOMIC_RELEASE);
+  }
+}
+
+int NodeStore::shard_state(int i) {
+  if (i < 0 || i >= nshards()) return -1;
+  refresh(true);
+  return at(i) == down_ ? 1 : 0;
 }
 
 Geometry NodeStore::geometry() const {
@@ -175,6 +302,7 @@ NodeStore* NodeStore::create(const std::string& name, size_t slots, size_t max_v
       s->owner_ = false;
       for (auto* x : s->shards_) delete x;
       s->shards_.clear();
+      s->real_.clear();
       for (int j = 0; j < i; ++j) spl_unlink(node_shard_name(name, j, backend).c_str());
       delete s;
       shm_unlink((name + ".node").c_str());
@@ -182,8 +310,11 @@ NodeStore* NodeStore::create(const std::string& name, size_t slots, size_t max_v
       return nullptr;
     }
     s->shards_.push_back(sh);
+    s->real_.push_back(sh);
+    s->gen_.push_back(0);
     d->ready_mask |= 1ull << i;
   }
+  s->down_ = new DownShard(s->shards_[0]->geometry());
   d->version = 1;
   __atomic_store_n(&d->magic, kNodeMagic, __ATOMIC_RELEASE);
   return s;
@@ -218,7 +349,11 @@ NodeStore* NodeStore::open(const std::string& name, int* err) {
       return nullptr;
     }
     s->shards_.push_back(sh);
+    s->real_.push_back(sh);
+    s->gen_.push_back(__atomic_load_n(&d->shard_gen[i], __ATOMIC_ACQUIRE));
   }
+  s->down_ = new DownShard(s->shards_[0]->geometry());
+  s->refresh(true);
   return s;
 }
 
@@ -236,7 +371,9 @@ NodeStore::~NodeStore() {
     }
     close(event_fd_);
   }
-  for (auto* sh : shards_) delete sh;
+  for (auto* sh : real_) delete sh;
+  for (auto* sh : retired_) delete sh;
+  delete down_;
   if (desc_) {
     // an HBM node lives as long as its creator (the arenas are its allocations); a host-shard node
     // persists like any shm store until spl_unlink("node:NAME")
@@ -258,11 +395,14 @@ int NodeStore::set_mop(unsigned mode) {
 
 int NodeStore::header_snapshot(splinter_header_snapshot_t* out) {
   if (!out) return -2;
-  if (shards_[0]->header_snapshot(out) != 0) return -1;
-  uint64_t epoch = out->epoch;
-  for (size_t i = 1; i < shards_.size(); ++i) {
+  refresh();
+  StoreBase* f = first_up();
+  if (f->header_snapshot(out) != 0) return -1;
+  uint64_t epoch = 0;
+  for (int i = 0; i < nshards(); ++i) {  // a down shard's writes are not counted until it re-joins
     splinter_header_snapshot_t h;
-    if (shards_[i]->header_snapshot(&h) != 0) return -1;
+    if (at(i) == down_) continue;
+    if (at(i)->header_snapshot(&h) != 0) return -1;
     epoch += h.epoch;
   }
   out->epoch = epoch;  // every write bumps its shard's global epoch: the sum is the node's
@@ -730,7 +870,7 @@ long NodeStore::set_batch(const char* keys, int kstride, const uint8_t* vals, in
     std::atomic<bool> fail{false};
     std::atomic<long> ok{0};
     pl.each_shard([&](int j, long o, long m) {
-      StoreBase* sh = shards_[(size_t)j];
+      StoreBase* sh = at(j);
       const char* k = (const char*)S + ob + o * kstride;
       const uint8_t* v = S + vb + o * (long)vstride;
       const uint32_t* l = (const uint32_t*)(S + lb) + o;
@@ -770,7 +910,7 @@ long NodeStore::get_batch(const char* keys, int kstride, uint8_t* out, int ostri
     std::atomic<bool> fail{false};
     std::atomic<long> ok{0};
     pl.each_shard([&](int j, long o, long m) {
-      StoreBase* sh = shards_[(size_t)j];
+      StoreBase* sh = at(j);
       const char* k = (const char*)S + ob + o * kstride;
       uint8_t* v = out ? S + vb + o * (long)ostride : nullptr;
       uint32_t* l = (uint32_t*)(S + lb) + o;
@@ -813,7 +953,7 @@ long NodeStore::intop_batch(const char* keys, int kstride, const int* ops, const
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
-    StoreBase* sh = shards_[(size_t)j];
+    StoreBase* sh = at(j);
     const char* k = (const char*)S + kb + o * kstride;
     const int* op = (const int*)(S + pb) + o;
     const uint64_t* mk = (const uint64_t*)(S + mb) + o;
@@ -851,7 +991,7 @@ long NodeStore::set_embedding_batch(const char* keys, int kstride, const float* 
   std::atomic<bool> fail{false};
   std::atomic<long> ok{0};
   pl.each_shard([&](int j, long o, long m) {
-    StoreBase* sh = shards_[(size_t)j];
+    StoreBase* sh = at(j);
     const char* k = (const char*)S + kb + o * kstride;
     const float* v = (const float*)(S + vb + o * (long)kEmbedBytes);
     int32_t* st = (int32_t*)(S + sb) + o;
@@ -877,8 +1017,17 @@ extern "C" {
 // A rank's shard joins node NAME (the shard store itself -- node_shard_name(NAME, shard, backend)
 // -- is created by the caller first).  The first rank creates the node descriptor; every rank must
 // pass the same geometry.  0 on success, -1 with errno.
+int spl_node_join_ex(const char* name, int shard, int nshards, unsigned backend, size_t slots_per_shard,
+                     size_t max_val, unsigned stride, unsigned flags);
 int spl_node_join(const char* name, int shard, int nshards, unsigned backend, size_t slots_per_shard, size_t max_val,
                   unsigned stride) {
+  return spl_node_join_ex(name, shard, nshards, backend, slots_per_shard, max_val, stride, backend == 1 ? 1u : 0u);
+}
+
+// flags SPL_NODE_OWNED (1): the shard is served only while this process lives (HBM shards always are:
+// spl_node_join sets it for them); a host shard joined without it outlives its rank like any shm store
+int spl_node_join_ex(const char* name, int shard, int nshards, unsigned backend, size_t slots_per_shard,
+                     size_t max_val, unsigned stride, unsigned flags) {
   if (!name || shard < 0 || nshards < 1 || nshards > spl::kNodeMaxShards || shard >= nshards || backend > 1 ||
       slots_per_shard == 0 || slots_per_shard > UINT32_MAX || max_val == 0 || max_val > UINT32_MAX ||
       (stride != spl::kSlotCoreBytes && stride != spl::kSlotEmbedBytes)) {
@@ -909,6 +1058,11 @@ int spl_node_join(const char* name, int shard, int nshards, unsigned backend, si
     errno = EINVAL;
     return -1;
   }
+  // ownership: this process serves the shard from now on; a re-join (a restarted rank) moves the
+  // generation, so open node stores re-open the shard (NodeStore::refresh)
+  __atomic_store_n(&d->shard_flags[shard], (flags | (backend == 1 ? 1u : 0u)) & spl::kShardOwned, __ATOMIC_RELEASE);
+  __atomic_store_n(&d->shard_pid[shard], (int32_t)getpid(), __ATOMIC_RELEASE);
+  __atomic_fetch_add(&d->shard_gen[shard], 1u, __ATOMIC_ACQ_REL);
   __atomic_fetch_or(&d->ready_mask, 1ull << shard, __ATOMIC_ACQ_REL);
   spl::unmap_desc(d);
   return 0;
@@ -944,6 +1098,101 @@ spl_store* spl_node_shard(spl_store* h, int i) {
   auto* n = dynamic_cast<NodeStore*>((spl::StoreBase*)h);
   return n ? (spl_store*)n->shard(i) : nullptr;
 }
+// Checkpoint / restore of any store (the unit a restarted rank recovers from): a host store writes
+// its mapped v4 image to `path` (tmp + rename), an hbm: store streams its device image
+// (spl_hbm_checkpoint), a node store checkpoints every serving shard to PATH.s<i>.  Restore loads
+// such an image into an OPEN store of the same geometry -- exclusive: no other process may use the
+// store meanwhile (a restarting rank restores before it joins).  0 on success, -1 with errno.
+static int host_checkpoint(spl::HostStore* hs, const char* path) {
+  const std::string tmp = std::string(path) + ".tmp";
+  const int fd = ::open(tmp.c_str(), O_WRONLY | O_CREAT | O_TRUNC | O_CLOEXEC, 0644);
+  if (fd < 0) return -1;
+  const uint8_t* p = hs->base();
+  size_t left = hs->total_bytes();
+  while (left) {
+    const ssize_t w = ::write(fd, p, left);
+    if (w <= 0) {
+      const int e = errno;
+      ::close(fd);
+      ::unlink(tmp.c_str());
+      errno = e;
+      return -1;
+    }
+    p += w;
+    left -= (size_t)w;
+  }
+  if (::fsync(fd) != 0 || ::close(fd) != 0 || ::rename(tmp.c_str(), path) != 0) return -1;
+  return 0;
+}
+
+static int host_restore(spl::HostStore* hs, const char* path) {
+  const int fd = ::open(path, O_RDONLY | O_CLOEXEC);
+  if (fd < 0) return -1;
+  struct stat st;
+  if (fstat(fd, &st) != 0 || (size_t)st.st_size != hs->total_bytes()) {
+    ::close(fd);
+    errno = EINVAL;  // another geometry
+    return -1;
+  }
+  std::vector<uint8_t> img(hs->total_bytes());
+  size_t got = 0;
+  while (got < img.size()) {
+    const ssize_t r = ::read(fd, img.data() + got, img.size() - got);
+    if (r <= 0) {
+      ::close(fd);
+      errno = EIO;
+      return -1;
+    }
+    got += (size_t)r;
+  }
+  ::close(fd);
+  const auto* H = (const splinter_header*)img.data();
+  const spl::Geometry g = hs->geometry();
+  if (H->magic != spl::kMagic || H->version != spl::kVersion || H->slots != g.slots || H->max_val_sz != g.max_val) {
+    errno = EINVAL;
+    return -1;
+  }
+  std::memcpy(hs->base(), img.data(), img.size());
+  __atomic_thread_fence(__ATOMIC_SEQ_CST);
+  return 0;
+}
+
+int spl_store_checkpoint(spl_store* h, const char* path) {
+  auto* b = (spl::StoreBase*)h;
+  if (!b || !path) { errno = EINVAL; return -1; }
+  if (auto* hs = dynamic_cast<spl::HostStore*>(b)) return host_checkpoint(hs, path);
+  if (auto* n = dynamic_cast<NodeStore*>(b)) {
+    for (int i = 0; i < n->nshards(); ++i) {
+      if (n->shard_state(i) != 0) continue;  // a down shard keeps its last checkpoint
+      const std::string p = std::string(path) + ".s" + std::to_string(i);
+      if (spl_store_checkpoint((spl_store*)n->shard(i), p.c_str()) != 0) return -1;
+    }
+    return 0;
+  }
+  using Fn = int (*)(spl_store*, const char*);
+  static Fn f = (Fn)spl::hbm_symbol("spl_hbm_checkpoint");
+  if (!f) { errno = ENOSYS; return -1; }
+  return f(h, path);
+}
+
+int spl_store_restore(spl_store* h, const char* path) {
+  auto* b = (spl::StoreBase*)h;
+  if (!b || !path) { errno = EINVAL; return -1; }
+  if (auto* hs = dynamic_cast<spl::HostStore*>(b)) return host_restore(hs, path);
+  if (dynamic_cast<NodeStore*>(b)) { errno = ENOTSUP; return -1; }  // per shard, by the shard's rank
+  using Fn = int (*)(spl_store*, const char*);
+  static Fn f = (Fn)spl::hbm_symbol("spl_hbm_restore");
+  if (!f) { errno = ENOSYS; return -1; }
+  return f(h, path);
+}
+
+// state of shard i of an open node store: 0 serving, 1 down (its rank's process is gone; ops on its
+// keys return EAGAIN until the rank re-joins), -1 not a node store / no such shard
+int spl_node_shard_state(spl_store* h, int i) {
+  auto* n = dynamic_cast<NodeStore*>((spl::StoreBase*)h);
+  return n ? n->shard_state(i) : -1;
+}
+
 // owning shard of a key under an n-way node (== parallel/sharded.py shard_of)
 int spl_node_shard_of(const char* key, int nshards) {
   if (!key || nshards < 1) return -1;

@@ -32,6 +32,9 @@ namespace spl {
 
 constexpr uint32_t kNodeMagic = 0x45444f4e;  // "NODE"
 constexpr int kNodeMaxShards = 64;
+// a shard whose memory lives and dies with its rank's process (HBM shards always; host shards when
+// the rank joins with SPL_NODE_OWNED): it is down while that process is gone
+constexpr uint32_t kShardOwned = 1u;
 
 struct NodeDesc {
   uint32_t magic;
@@ -47,6 +50,12 @@ struct NodeDesc {
   int32_t event_pid;         // node event bus: owner pid and fd of the forwarded eventfd
   int32_t event_fd;
   int32_t pad1;
+  // rank ownership of joined shards (spl_node_join): the owning process and how many times the
+  // shard has joined -- a rank restarted from its checkpoint re-joins with gen + 1, and every open
+  // node store then re-opens that shard (NodeStore::refresh)
+  int32_t shard_pid[kNodeMaxShards];
+  uint32_t shard_gen[kNodeMaxShards];
+  uint32_t shard_flags[kNodeMaxShards];  // kShardOwned: served only while shard_pid lives
   alignas(64) splinter_header control;  // node-level logic-shard bid table (shard_bids only)
 };
 
@@ -61,18 +70,24 @@ class NodeStore final : public StoreBase {
   ~NodeStore() override;
 
   int nshards() const { return (int)shards_.size(); }
-  StoreBase* shard(int i) const { return (i >= 0 && i < nshards()) ? shards_[i] : nullptr; }
-  StoreBase* route(const char* key) const;
+  StoreBase* shard(int i) const { return (i >= 0 && i < nshards()) ? __atomic_load_n(&shards_[i], __ATOMIC_ACQUIRE) : nullptr; }
+  StoreBase* route(const char* key);
+  // Degraded mode (joined nodes): a shard whose owning rank process is gone answers every op with
+  // EAGAIN (DownShard) while the other shards keep serving; when the rank's restarted process
+  // re-joins (shard_gen moved) the shard is re-opened.  Checked at most every kRefreshNs per store.
+  void refresh(bool force = false);
+  // 0 serving, 1 down (owner gone), -1 no such shard
+  int shard_state(int i);
 
   const char* backend() const override { return "node"; }
   Geometry geometry() const override;
   splinter_header* header_ptr() override { return &desc_->control; }
 
   int set_mop(unsigned mode) override;
-  int get_mop() override { return shards_[0]->get_mop(); }
+  int get_mop() override { return first_up()->get_mop(); }
   void purge() override { for (auto* s : shards_) s->purge(); }
   int header_snapshot(splinter_header_snapshot_t* out) override;
-  uint8_t config_get() override { return shards_[0]->config_get(); }
+  uint8_t config_get() override { return first_up()->config_get(); }
   void config_or(uint8_t m) override { for (auto* s : shards_) s->config_or(m); }
   void config_and(uint8_t m) override { for (auto* s : shards_) s->config_and(m); }
 
@@ -109,7 +124,7 @@ class NodeStore final : public StoreBase {
   int pulse_keygroup(const char* k) override { return k ? route(k)->pulse_keygroup(k) : -2; }
   void pulse_slot(splinter_slot*) override {}
   uint64_t signal_count(uint8_t g) override;
-  int signal_add(uint8_t g, uint64_t delta) override { return shards_[0]->signal_add(g, delta); }
+  int signal_add(uint8_t g, uint64_t delta) override { return first_up()->signal_add(g, delta); }
   void enumerate(uint64_t mask, void (*cb)(const char*, uint64_t, void*), void* ud) override {
     for (auto* s : shards_) s->enumerate(mask, cb, ud);
   }
@@ -155,10 +170,24 @@ class NodeStore final : public StoreBase {
   size_t scratch_bytes_ = 0;
   bool scratch_pinned_ = false;
 
+  StoreBase* at(int i) const { return __atomic_load_n(&shards_[(size_t)i], __ATOMIC_ACQUIRE); }
+  // node-wide reads (mop, config, the node signal counter) from the first serving shard
+  StoreBase* first_up() const {
+    for (int i = 0; i < nshards(); ++i)
+      if (at(i) != down_) return at(i);
+    return at(0);
+  }
+
   std::string name_;
   NodeDesc* desc_ = nullptr;
   bool owner_ = false;  // created the descriptor and every shard
-  std::vector<StoreBase*> shards_;
+  std::vector<StoreBase*> shards_;   // routing table (entries swapped atomically by refresh)
+  std::vector<StoreBase*> real_;     // the opened shard stores (a down shard keeps its handle here)
+  std::vector<uint32_t> gen_;        // shard_gen of each opened handle
+  std::vector<StoreBase*> retired_;  // handles replaced by a re-open (another thread may still hold one)
+  StoreBase* down_ = nullptr;        // the EAGAIN stand-in of down shards
+  std::mutex refresh_mu_;
+  std::atomic<uint64_t> next_refresh_ns_{0};
   int event_fd_ = -1;
 };
 

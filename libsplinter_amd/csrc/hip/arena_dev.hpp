@@ -288,6 +288,8 @@ __device__ __forceinline__ void vm_wait2(u32x2c_t& a, u32x2c_t& b) {
   asm volatile("s_waitcnt vmcnt(0)" : "+v"(a), "+v"(b)::"memory");
 }
 __device__ __forceinline__ uint64_t lo64(const u32x4c_t& v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ uint64_t u64of(const u32x2c_t& v) { return ((uint64_t)v.y << 32) | v.x; }
+__device__ __forceinline__ void vm_wait1(u32x2c_t& a) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(a)::"memory"); }
 __device__ __forceinline__ uint64_t hi64(const u32x4c_t& v) { return ((uint64_t)v.w << 32) | v.z; }
 
 // Stored-key probe in 16-B chunks: chunk 0 always, the rest only where our key + NUL reaches
@@ -325,19 +327,55 @@ __device__ __forceinline__ uint64_t slot_hash(const uint8_t* s) { return ald64(s
 __device__ __forceinline__ uint64_t slot_epoch(const uint8_t* s) { return ald64(s + kOffEpoch); }
 __device__ __forceinline__ uint64_t* epoch_ptr(uint8_t* s) { return (uint64_t*)(s + kOffEpoch); }
 
-// Locate `k`; returns the slot index or -1.  Pure lookup (no seqlock).
+// ------------------------------------------------------ online maintenance --
+// The maintenance pass (arena_maint.hip k_rehash) moves live entries toward their home slots
+// while batch and per-call ops keep running: each move holds BOTH slots' seqlocks (destination
+// tombstone and source claimed by epoch CAS), publishes the entry at the destination, then
+// releases the source as a tombstone.  A hit is covered by the slot's own seqlock.  An "absent"
+// outcome is not: a probe can pass the destination before the entry lands there and reach the
+// source after it was cleared.  So the side header's MaintRec::seq is odd while a pass runs, and
+// an absent outcome (get miss, insert decision, unset / update of a missing key) is trusted only
+// when seq was even before the probe's loads and is unchanged after them; otherwise the op
+// reports EAGAIN (retry).  Reference contract: a miss only after the whole chain was scanned
+// (/root/reference/splinter.c:431-464), purge beside live ops (splinter.c:302-318).
+constexpr long kMaintMiss = -2;  // probe result: absent, but a maintenance pass overlapped it
+__device__ __forceinline__ uint64_t* maint_ptr(const Arena& a) { return (uint64_t*)(a.side() + kSideMaintOff); }
+// seq before a probe: acquire-ordered, no later load of the probe can be performed before it
+__device__ __forceinline__ uint64_t maint_begin(const Arena& a) {
+  return a.has_side() ? __hip_atomic_load(maint_ptr(a), __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) : 0;
+}
+// after a probe that found nothing: every load of the probe has returned (the fence waits
+// vmcnt(0)) before seq is read again
+__device__ __forceinline__ bool maint_quiet(const Arena& a, uint64_t s0) {
+  if (!a.has_side()) return true;
+  if (s0 & 1) return false;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  return ald64(maint_ptr(a)) == s0;
+}
+// the same check with seq already re-read by the caller after its probe loads returned
+__device__ __forceinline__ bool maint_same(uint64_t s0, uint64_t s1) { return !(s0 & 1) && s0 == s1; }
+// seq word load issued without a wait (batched into a round trip the caller waits for anyway)
+__device__ __forceinline__ const void* maint_addr(const Arena& a) {
+  // no side region: the header's (magic, version) word, constant and even
+  return a.has_side() ? (const void*)maint_ptr(a) : (const void*)a.base;
+}
+
+// Locate `k`; returns the slot index, -1 (absent) or kMaintMiss.  Pure lookup (no seqlock).
 template <int KW>
 __device__ __forceinline__ long find(const Arena& a, const KeyT<KW>& k) {
+  const uint64_t s0 = maint_begin(a);
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
     const uint64_t sh = slot_hash(s);
     if (sh == k.hash && key_eq(s, k)) return (long)idx;
-    if (sh == 0 && slot_epoch(s) == 0) return -1;
+    if (sh == 0 && slot_epoch(s) == 0) break;
     if (++idx == a.slots) idx = 0;
   }
-  return -1;
+  return maint_quiet(a, s0) ? -1 : kMaintMiss;
 }
+// status of a failed find
+__device__ __forceinline__ int32_t miss_rc(long i) { return i == kMaintMiss ? kAgain : kNoEnt; }
 
 // ------------------------------------------------------------- signals --
 __device__ __forceinline__ void pulse(const Arena& a, const uint8_t* s) {
@@ -492,8 +530,10 @@ __device__ __forceinline__ void clear_claim(const Arena& a, long idx) {
   aadd64(epoch_ptr(s), 1);
 }
 
+// s0: the maintenance seq read before this probe (maint_begin, or a value the caller waited for
+// before issuing the probe's loads); an insert is decided only when no pass overlapped the probe.
 template <int KW>
-__device__ Claim claim_set(const Arena& a, const KeyT<KW>& k) {
+__device__ Claim claim_set(const Arena& a, const KeyT<KW>& k, uint64_t s0) {
   const size_t home = (size_t)(k.hash % a.slots);
   long free_idx = -1;
   uint64_t free_ep = 0;
@@ -558,6 +598,13 @@ __device__ Claim claim_set(const Arena& a, const KeyT<KW>& k) {
   drain();
   ast64(fs + kOffHash, k.hash);
   drain();
+  // the insert is decided on "absent": not while a maintenance pass may be moving our key (the
+  // claim and its publication have drained, so this read is performed after them and after the
+  // probe -- a pass that starts later sees our claim as a busy slot and never moves across it)
+  if (!maint_same(s0, ald64(maint_addr(a)))) {
+    clear_claim(a, free_idx);
+    return Claim{-1, false, kAgain};
+  }
   // Re-validate the chain while holding the claim (the claim CAS + publish drains make
   // our claim visible before these reads, so of two racing inserters at least one sees
   // the other).  "Earlier claimant wins" alone is unsafe: the later inserter may not see
@@ -619,7 +666,7 @@ __device__ __forceinline__ void cas_wait(uint64_t& r) { asm volatile("s_waitcnt 
 // claim_set; the round trips per lane drop from 2U to (longest chain + 1).
 template <int U, int KW>
 __device__ __forceinline__ void claim_many(const Arena& a, const KeyT<KW> (&k)[U], const bool (&active)[U],
-                                          Claim (&c)[U]) {
+                                          Claim (&c)[U], uint64_t s0) {
   constexpr int kProbeRounds = 4;
   size_t idx[U];
   bool pend[U], slow[U], cas[U];
@@ -701,7 +748,7 @@ __device__ __forceinline__ void claim_many(const Arena& a, const KeyT<KW> (&k)[U
     }
 #pragma unroll
   for (int j = 0; j < U; ++j)
-    if (slow[j] || pend[j]) c[j] = claim_set(a, k[j]);
+    if (slow[j] || pend[j]) c[j] = claim_set(a, k[j], s0);
 }
 
 // Slot metadata part of a set (everything but the value bytes): fresh-slot defaults and val_len.
@@ -767,7 +814,7 @@ __device__ int32_t set_op(const Arena& a, const KeyT<KW>& k, const uint8_t* val,
   if (len == 0 || len > a.max_val) return kMsgSize;
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
-  const Claim c = claim_set(a, k);
+  const Claim c = claim_set(a, k, maint_begin(a));
   if (c.rc != kOk) return c.rc;
   write_set<MO>(a, c, val, len, scrub, hybrid);
   if constexpr (MO == 0) release();
@@ -780,6 +827,7 @@ __device__ int32_t set_op(const Arena& a, const KeyT<KW>& k, const uint8_t* val,
 // GET: seqlock read into out (may be null: size query).
 template <int MO = 0, int KW>
 __device__ int32_t get_op(const Arena& a, const KeyT<KW>& k, uint8_t* out, uint32_t out_cap, uint32_t* out_len) {
+  const uint64_t s0 = maint_begin(a);
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
@@ -802,19 +850,22 @@ __device__ int32_t get_op(const Arena& a, const KeyT<KW>& k, uint8_t* out, uint3
         return (e2 == e1 && slot_hash(s) == k.hash) ? kOk : kAgain;
       }
     } else if (sh == 0 && slot_epoch(s) == 0) {
-      return kNoEnt;
+      break;
     }
     if (++idx == a.slots) idx = 0;
   }
-  return kNoEnt;
+  return maint_quiet(a, s0) ? kNoEnt : kAgain;
 }
 
 // One-round-trip probe for batched gets: hash, epoch, length and the key
 // words of each probed slot are loaded together; returns the slot index with
 // its epoch / length as observed, or -1 for a miss.  The caller validates the
 // whole read afterwards (key words again with the data, epoch unchanged).
+// s0: the maintenance seq read (and waited for) before this probe; a miss is -1 only when no pass
+// overlapped the probe, else kMaintMiss.
 template <int KW>
-__device__ __forceinline__ long locate_peek(const Arena& a, const KeyT<KW>& k, uint64_t* e1, uint32_t* len) {
+__device__ __forceinline__ long locate_peek(const Arena& a, const KeyT<KW>& k, uint64_t* e1, uint32_t* len,
+                                            uint64_t s0) {
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
@@ -831,10 +882,10 @@ __device__ __forceinline__ long locate_peek(const Arena& a, const KeyT<KW>& k, u
       *len = L;
       return (long)idx;
     }
-    if (sh == 0 && e == 0) return -1;
+    if (sh == 0 && e == 0) break;
     if (++idx == a.slots) idx = 0;
   }
-  return -1;
+  return maint_quiet(a, s0) ? -1 : kMaintMiss;
 }
 
 // Copy n16 16-B chunks with 8 loads in flight per batch (see write_value).
@@ -854,6 +905,7 @@ __device__ __forceinline__ void copy_chunks(uint4* dst, const uint4* src, uint32
 // Returns the slot index holding k (possibly mid-write), or -1 for a miss.
 template <int KW>
 __device__ __forceinline__ long locate(const Arena& a, const KeyT<KW>& k) {
+  const uint64_t s0 = maint_begin(a);
   size_t idx = (size_t)(k.hash % a.slots);
   for (uint32_t i = 0; i < a.slots; ++i) {
     const uint8_t* s = a.slot(idx);
@@ -861,18 +913,18 @@ __device__ __forceinline__ long locate(const Arena& a, const KeyT<KW>& k) {
     if (sh == k.hash) {
       if (key_eq(s, k)) return (long)idx;
     } else if (sh == 0 && slot_epoch(s) == 0) {
-      return -1;
+      break;
     }
     if (++idx == a.slots) idx = 0;
   }
-  return -1;
+  return maint_quiet(a, s0) ? -1 : kMaintMiss;
 }
 
 // UNSET: returns the old length (>= 0) or a negative status.
 template <int KW>
 __device__ int32_t unset_op(const Arena& a, const KeyT<KW>& k, long* out_idx) {
   const long i = find(a, k);
-  if (i < 0) return kNoEnt;
+  if (i < 0) return miss_rc(i);
   uint8_t* s = a.slot((size_t)i);
   const uint64_t e = slot_epoch(s);
   if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
@@ -910,7 +962,7 @@ __device__ int32_t unset_op(const Arena& a, const KeyT<KW>& k, long* out_idx) {
 template <int KW>
 __device__ int32_t integer_op(const Arena& a, const KeyT<KW>& k, int op, uint64_t m, uint64_t* result, long* out_idx) {
   const long i = find(a, k);
-  if (i < 0) return kNoEnt;
+  if (i < 0) return miss_rc(i);
   uint8_t* s = a.slot((size_t)i);
   if (!(ald8(s + kOffType) & SPL_SLOT_TYPE_BIGUINT)) return kProto;
   const uint64_t e = slot_epoch(s);
@@ -951,7 +1003,7 @@ __device__ int32_t append_op(const Arena& a, const KeyT<KW>& k, const uint8_t* s
                              uint32_t* new_len, long* out_idx) {
   if (len == 0) return kInval;
   const long i = find(a, k);
-  if (i < 0) return kNoEnt;
+  if (i < 0) return miss_rc(i);
   uint8_t* s = a.slot((size_t)i);
   const uint64_t e = slot_epoch(s);
   if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
@@ -996,7 +1048,7 @@ __device__ __forceinline__ uint64_t parse_u64(const uint8_t* p, uint32_t n) {
 template <int KW>
 __device__ int32_t named_type_op(const Arena& a, const KeyT<KW>& k, uint8_t mask, long* out_idx) {
   const long i = find(a, k);
-  if (i < 0) return kNoEnt;
+  if (i < 0) return miss_rc(i);
   uint8_t* s = a.slot((size_t)i);
   const uint64_t e = slot_epoch(s);
   if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
@@ -1027,6 +1079,9 @@ __device__ int32_t named_type_op(const Arena& a, const KeyT<KW>& k, uint8_t mask
 //     11 set atime, 12 find (out = slot index)
 // *mut: the op changed the slot (global epoch +1; dirty mask already marked here).
 template <int KW>
+__device__ int32_t meta_apply(const Arena& a, const KeyT<KW>& k, int op, uint64_t arg, uint64_t* out, bool* mut,
+                              long idx);
+template <int KW>
 __device__ int32_t meta_op(const Arena& a, const KeyT<KW>& k, int op, uint64_t arg, uint64_t* out, bool* mut) {
   *mut = false;
   *out = 0;
@@ -1036,8 +1091,24 @@ __device__ int32_t meta_op(const Arena& a, const KeyT<KW>& k, int op, uint64_t a
     if (rc == kOk) { *mut = true; mark_dirty(a, (size_t)idx); }
     return rc;
   }
+  // ops that change a slot WITHOUT claiming its seqlock (labels, watchers, system / times, the
+  // reference's unconditional retrain stores) could land on an entry a maintenance pass is copying
+  // and be lost with its old slot: they run only outside a pass, and report EAGAIN when a pass
+  // overlapped them (each is idempotent: the retry re-applies it where the entry now lives)
+  const bool unlocked = op == 0 || op == 1 || op == 4 || op == 5 || op == 7 || op == 8 || op == 10 || op == 11;
+  const uint64_t s0 = maint_begin(a);
+  if (unlocked && (s0 & 1)) return kAgain;
   const long idx = find(a, k);
-  if (idx < 0) return kNoEnt;
+  if (idx < 0) return miss_rc(idx);
+  const int32_t rc = meta_apply(a, k, op, arg, out, mut, idx);
+  if (unlocked && rc == kOk && !maint_quiet(a, s0)) return kAgain;
+  return rc;
+}
+
+template <int KW>
+__device__ int32_t meta_apply(const Arena& a, const KeyT<KW>& k, int op, uint64_t arg, uint64_t* out, bool* mut,
+                              long idx) {
+  (void)k;
   uint8_t* s = a.slot((size_t)idx);
   switch (op) {
     case 0: aor64((uint64_t*)(s + kOffBloom), arg); *mut = true; mark_dirty(a, idx); return kOk;

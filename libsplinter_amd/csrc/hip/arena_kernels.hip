@@ -216,6 +216,7 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
   uint32_t len[U];
   long op[U];
   int tries[U];
+  uint64_t ms = maint_begin(a);  // maintenance seq, re-read after every round's drain (arena_dev.hpp)
 #pragma unroll
   for (int j = 0; j < U; ++j) op[j] = -1;
   for (;;) {
@@ -247,7 +248,7 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
         ++st.attempts;
         ++tries[j];
         if (len[j] == 0 || len[j] > a.max_val || len[j] > (uint32_t)vstride) c[j].rc = kMsgSize;
-        else c[j] = claim_set(a, k[j]);
+        else c[j] = claim_set(a, k[j], ms);
       }
     }
     // value rows through the cooperative copy (wave-private table), metadata per lane
@@ -265,7 +266,11 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
 #pragma unroll
     for (int j = 0; j < U; ++j)
       if (op[j] >= 0 && c[j].rc == kOk) write_meta<WT ? 3 : 0>(a, c[j], len[j]);
-    drain();
+    {
+      u32x2c_t mw = ld8c(maint_addr(a));
+      vm_wait1(mw);  // = drain(): the round's stores and this load
+      ms = u64of(mw);
+    }
     if constexpr (!WT) {
       __syncthreads();
       if (threadIdx.x == 0) release();
@@ -322,6 +327,7 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
   int32_t rc[U];
   uint32_t len[U];
   int tries[U];
+  uint64_t ms = maint_begin(a);  // maintenance seq, re-read after every round's copies
 #pragma unroll
   for (int j = 0; j < U; ++j) op[j] = -1;
   for (;;) {
@@ -355,8 +361,8 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
         ++st.attempts;
         ++tries[j];
         len[j] = 0;
-        sidx[j] = locate_peek(a, k[j], &e1[j], &len[j]);
-        rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
+        sidx[j] = locate_peek(a, k[j], &e1[j], &len[j], ms);
+        rc[j] = sidx[j] >= 0 ? kOk : sidx[j] == kMaintMiss ? kAgain : kNoEnt;
       }
     }
     if constexpr (FAST) {
@@ -398,7 +404,11 @@ __global__ __launch_bounds__(B) void k_get_carry(spl_arena_t aa, const char* key
       __builtin_amdgcn_wave_barrier();
       coop_copy<U * 64, 0, FAST>(cp_p[w], cp_l[w], lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
     }
-    drain();
+    {
+      u32x2c_t mw = ld8c(maint_addr(a));
+      vm_wait1(mw);  // = drain()
+      ms = u64of(mw);
+    }
     if constexpr (FAST) {
       // closing round trip: (hash, epoch) and the key words of every op of the lane together
       u32x4c_t he[U];
@@ -506,10 +516,12 @@ __device__ __forceinline__ void fill_slot(OpSlots<U, KW>& o, int j, const FSeg& 
 // copies (cp*0: set rows, cp*1: get rows; a wave-private LDS table each), set publication, get
 // re-validation, completion.  An op that met EAGAIN stays in its slot for the next round while
 // tries <= max_retry.  Called by every lane of the wave (the row copies are wave-cooperative).
+// ms: the arena's maintenance seq as read (and waited for) before this round's probes; re-read in
+// the round's closing round trip for the next round (arena_dev.hpp, online maintenance).
 template <int U, int KW>
 __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW>& o, bool scrub, bool hybrid,
                                          int max_retry, Stats& st, uint64_t& muts, uint4* cpp0, uint2* cpl0,
-                                         uint4* cpp1, uint2* cpl1, int lane, bool skip_len) {
+                                         uint4* cpp1, uint2* cpl1, int lane, bool skip_len, uint64_t& ms) {
   Claim c[U];
   long sidx[U];
   uint64_t e1[U];
@@ -525,13 +537,13 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
     const int vs = sg[o.seg[j]].vstride;
     if (o.set[j]) {
       if (o.len[j] == 0 || o.len[j] > a.max_val || o.len[j] > (uint32_t)vs) c[j].rc = kMsgSize;
-      else c[j] = claim_set(a, o.k[j]);
+      else c[j] = claim_set(a, o.k[j], ms);
       rc[j] = c[j].rc;
     } else {
       uint32_t L = 0;
-      sidx[j] = locate_peek(a, o.k[j], &e1[j], &L);
+      sidx[j] = locate_peek(a, o.k[j], &e1[j], &L, ms);
       o.len[j] = L;
-      rc[j] = sidx[j] < 0 ? kNoEnt : kOk;
+      rc[j] = sidx[j] >= 0 ? kOk : sidx[j] == kMaintMiss ? kAgain : kNoEnt;
       if (rc[j] == kOk && ((e1[j] & 1) || L > a.max_val)) rc[j] = kAgain;
       else if (rc[j] == kOk && sg[o.seg[j]].vals && L > (uint32_t)vs) rc[j] = kMsgSize;
     }
@@ -581,11 +593,14 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
       he[j] = ld16c(s + kOffHash);
       kp[j].issue(s, o.k[j]);
     }
+    u32x2c_t mw = ld8c(maint_addr(a));  // the next round's maintenance seq, in the same round trip
 #pragma unroll
     for (int j = 0; j < U; ++j) {
       vm_wait(he[j]);
       kp[j].wait();
     }
+    vm_wait1(mw);
+    ms = u64of(mw);
 #pragma unroll
     for (int j = 0; j < U; ++j)
       if (o.seg[j] >= 0 && !o.set[j] && rc[j] == kOk &&
@@ -660,6 +675,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
 #pragma unroll
   for (int j = 0; j < U; ++j) o.seg[j] = -1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint64_t ms = maint_begin(a);
   for (;;) {
 #pragma unroll
     for (int j = 0; j < U; ++j) {
@@ -680,7 +696,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
     if (!__syncthreads_or(busy)) break;
     kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
-                    skip_len);
+                    skip_len, ms);
   }
   flush_stats(a, st, stats, muts);
 }
@@ -725,6 +741,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   __shared__ int sh_kind, sh_state, sh_scan;
   __shared__ uint64_t sh_exhausted, sh_posted, sh_idle;  // thread 0's scan state (LDS: no registers)
   __shared__ unsigned long long sh_st[5];  // attempts, ok, again, miss, mutations of the chunks run
+  __shared__ long sh_tb[kAsyncSegs], sh_te[kAsyncSegs];  // timeout: rows of unposted slices this group took
   const int nseg = nw + nr;
   if (threadIdx.x < 5) sh_st[threadIdx.x] = 0;
   if (threadIdx.x == 0) {
@@ -792,28 +809,59 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
         avm &= ~(1ull << i);
         exhausted |= 1ull << i;
       }
+      int timed = 0;
       if (lane == 0) {
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-            if (state == 1) {
+        if (state == 1) {
           sh_idle = now;
           sh_kind = pick < nw ? 0 : 1;
           sh_b = cb;
           sh_e = ce;
+          // the slice's keys / values were written by the client stream's work before its post:
+          // an agent acquire after the poll, before any wave of the group reads them (this CU's L1
+          // may hold lines of the previous step's rows), MI355X guide "Valid forms", consumer side
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         } else if (exhausted == all) {
           state = 2;
         } else if (now - sh_idle > wait_ticks) {
           __hip_atomic_store(&ctl->err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           state = 2;
+          timed = 1;
         }
         sh_exhausted = exhausted;
         sh_posted = posted;
         sh_scan = pick;
         sh_state = state;
       }
+      // a post that never came: every row of an unposted slice that no group has claimed is taken
+      // (one claim of the whole remainder) and reported EAGAIN, so no status is left stale
+      timed = __shfl(timed, 0, 64);
+      long tb = 0, te = 0;
+      if (timed && lane < nseg && !((exhausted >> lane) & 1) && !((posted >> lane) & 1) && b < e) {
+        const long c = (long)atomicAdd(&next[lane], (unsigned long long)(e - b));
+        if (b + c < e) {
+          tb = b + c;
+          te = e;
+        }
+      }
+      if (lane < kAsyncSegs) {
+        sh_tb[lane] = tb;
+        sh_te[lane] = te;
+      }
     }
     __syncthreads();
     const int state = sh_state;
-    if (state == 2) break;
+    if (state == 2) {
+      for (int i = 0; i < nseg; ++i) {
+        const FSeg& f = sg[i < nw ? 0 : 1];
+        for (long r = sh_tb[i] + (long)threadIdx.x; r < sh_te[i]; r += B) {
+          if (f.status) f.status[r] = kAgain;
+          if (!f.set && f.lens) f.lens[r] = 0;
+        }
+      }
+      break;
+    }
     if (state == 0) {
       __builtin_amdgcn_s_sleep(32);
       continue;
@@ -826,6 +874,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     for (int j = 0; j < U; ++j) o.seg[j] = -1;
     Stats st;
     uint64_t muts = 0;
+    uint64_t ms = maint_begin(a);
     const int q = sh_kind;
     const long end = sh_e;
     long row = sh_b + (long)threadIdx.x * U;  // the lane's next row: U consecutive rows per B * U
@@ -848,7 +897,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
       if (!__syncthreads_or(busy)) break;
       kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
-                      lane, skip_len);
+                      lane, skip_len, ms);
     }
     {
       const uint64_t v[5] = {st.attempts, st.ok, st.again, st.miss, muts};
@@ -973,7 +1022,7 @@ __global__ __launch_bounds__(kBlock) void k_embed_set(spl_arena_t aa, const char
     long idx = find(a, k);
     int32_t rc = kOk;
     uint8_t* s = idx >= 0 ? a.slot((size_t)idx) : nullptr;
-    if (idx < 0) rc = kNoEnt;
+    if (idx < 0) rc = miss_rc(idx);
     else if (a.stride != kSlotEmbedBytes) rc = kInval;
     bool locked = false;
     if (rc == kOk && lane == 0) {
@@ -1018,7 +1067,7 @@ __global__ __launch_bounds__(kBlock) void k_embed_get(spl_arena_t aa, const char
     load_key(k, keys + i * (long)kstride, kstride);
     long idx = find(a, k);
     int32_t rc = kOk;
-    if (idx < 0) rc = kNoEnt;
+    if (idx < 0) rc = miss_rc(idx);
     else if (a.stride != kSlotEmbedBytes) rc = kInval;
     if (rc == kOk) {
       const uint8_t* s = a.slot((size_t)idx);

@@ -192,11 +192,12 @@ struct Spec {
 // write-back fence on this latency path (MO 3 of arena_dev.hpp; readers are unchanged).  A value
 // row that is not a multiple of 16 B ends in bytewise plain stores: those take the release path.
 // reg: the value is in sp (len <= kSpec * 16, max_val a multiple of 16); else in the staged row.
+// ms: the arena's maintenance seq, loaded with the request record (waited before the probe).
 __device__ __forceinline__ int32_t ring_set(const Arena& a, const Key& k, const uint8_t* pay, const Spec& sp,
-                                            bool reg, uint32_t len, bool scrub, bool hybrid) {
+                                            bool reg, uint32_t len, bool scrub, bool hybrid, uint64_t ms) {
   if (len == 0 || len > a.max_val) return kMsgSize;
   RING_TS(1);
-  const Claim c = claim_set(a, k);
+  const Claim c = claim_set(a, k, ms);
   RING_TS(2);
   if (c.rc != kOk) return c.rc;
   if (reg) {
@@ -238,13 +239,14 @@ __device__ __forceinline__ int32_t ring_set(const Arena& a, const Key& k, const 
 // GET for one lane straight into the host payload: one-round-trip probe, acquire, copy
 // (arena -> host, system-scope stores), then the seqlock re-check; on EAGAIN the host ignores
 // the bytes it may have received.
-__device__ __forceinline__ int32_t ring_get(const Arena& a, const Key& k, uint8_t* hp, uint32_t cap, uint32_t* out_len) {
+__device__ __forceinline__ int32_t ring_get(const Arena& a, const Key& k, uint8_t* hp, uint32_t cap, uint32_t* out_len,
+                                            uint64_t ms) {
   uint64_t e1 = 0;
   uint32_t L = 0;
   RING_TS(1);
-  const long idx = locate_peek(a, k, &e1, &L);
+  const long idx = locate_peek(a, k, &e1, &L, ms);
   RING_TS(2);
-  if (idx < 0) return kNoEnt;
+  if (idx < 0) return miss_rc(idx);
   if ((e1 & 1) || L == kInsertMark) return kAgain;
   const uint8_t* s = a.slot((size_t)idx);
   // no acquire fence: the value row is read with agent-coherent loads (push_c), as the batched
@@ -299,6 +301,12 @@ __device__ int32_t serve(const spl_arena_t& aa, const RingCmd* c, const uint8_t*
   const splinter_header* H = (const splinter_header*)aa.base;
   const uint32_t owner = __hip_atomic_load(&H->event_bus.owner_pid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint8_t cflags = ald8(&H->core_flags);
+  // the maintenance seq (arena_dev.hpp, online maintenance) rides along: waited with the record,
+  // so it is read before any probe load of the op
+  const uint8_t* mp = (aa.flags & SPL_ARENA_SIDE)
+                          ? (const uint8_t*)aa.base + side_offset(aa.slots, aa.stride, aa.max_val) + kSideMaintOff
+                          : (const uint8_t*)aa.base;
+  u32x2c_t mw = ld8c(mp);
   // ONE round of system-scope loads: record header (32 B + key length), key (64 B) and the
   // first kSpec payload chunks (speculative: the length is in the header)
   u32x4s_t h0 = ld16s(c), h1 = ld16s((const uint8_t*)c + 16), h3 = ld16s((const uint8_t*)c + 48);
@@ -315,6 +323,8 @@ __device__ int32_t serve(const spl_arena_t& aa, const RingCmd* c, const uint8_t*
   for (int q = 0; q < 4; ++q) sys_wait(kk[q]);
 #pragma unroll
   for (uint32_t q = 0; q < kSpec; ++q) sys_wait(sp.c[q]);
+  vm_wait1(mw);
+  const uint64_t ms = u64of(mw);
   const uint32_t op = h0.x, sub = h0.y, len = h0.z, cap = h0.w;
 #ifdef SPL_RING_STAMPS
   *t_loaded = wall_clock64();
@@ -361,8 +371,8 @@ __device__ int32_t serve(const spl_arena_t& aa, const RingCmd* c, const uint8_t*
   // hit lines this CU's L1 holds from before another XCD's write (acquire first: L1 invalidate), and
   // plain stores leave dirty lines in this XCD's L2 that a reader on another XCD would not see
   // (release after: L2 write-back), both at agent scope
-  if (op == kRingSet) return ring_set(a, k, pay, sp, reg, len, scrub, hybrid);
-  if (op == kRingGet) return ring_get(a, k, hp, cap, out_len);
+  if (op == kRingSet) return ring_set(a, k, pay, sp, reg, len, scrub, hybrid, ms);
+  if (op == kRingGet) return ring_get(a, k, hp, cap, out_len, ms);
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
   const int32_t rc = serve_plain(a, k, op, sub, len, cap, arg, hp, pay, out_len, result);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
@@ -405,7 +415,7 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
     case kRingEmbedSet: {
       if (a.stride != kSlotEmbedBytes) return kInval;
       idx = find(a, k);
-      if (idx < 0) return kNoEnt;
+      if (idx < 0) return miss_rc(idx);
       uint8_t* s = a.slot((size_t)idx);
       const uint64_t e = slot_epoch(s);
       if ((e & 1) || !acas64(epoch_ptr(s), e, e + 1)) return kAgain;
@@ -421,7 +431,7 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
     case kRingEmbedGet: {
       if (a.stride != kSlotEmbedBytes) return kInval;
       idx = find(a, k);
-      if (idx < 0) return kNoEnt;
+      if (idx < 0) return miss_rc(idx);
       const uint8_t* s = a.slot((size_t)idx);
       const uint64_t e1 = ald64_acq(s + kOffEpoch);
       if (e1 & 1) return kAgain;
@@ -433,7 +443,7 @@ __device__ int32_t serve_plain(const Arena& a, const Key& k, uint32_t op, uint32
     }
     case kRingSnapshot: {
       idx = find(a, k);
-      if (idx < 0) return kNoEnt;
+      if (idx < 0) return miss_rc(idx);
       const uint8_t* s = a.slot((size_t)idx);
       for (int q = 0; q < 16; ++q) st64s(hp + 8 * q, ald64(s + 8 * q));
       *out_len = 128;

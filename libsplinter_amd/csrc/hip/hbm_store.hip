@@ -27,6 +27,7 @@
 #include <sys/eventfd.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
+#include <signal.h>
 #include <sys/syscall.h>
 #include <unistd.h>
 #include <vector>
@@ -456,7 +457,8 @@ class HbmStore final : public StoreBase {
   long search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask, spl_search_hit* out);
   int restore_from(const char* path);
   int probe_stats(ProbeStats* out);
-  int rehash(uint64_t out[4]);
+  int rehash(uint64_t out[4], unsigned flags = 0);
+  int maint_seq(uint64_t* seq);
 
   // ------------------------------------------------------ host-array batches --
   long set_batch(const char* keys, int kstride, const uint8_t* vals, int vstride, const uint32_t* lens, long n,
@@ -1023,12 +1025,6 @@ struct CandRec {
   float sim, dist;
   uint32_t idx, pad;
 };
-inline uint16_t f2bf_host(float f) {  // round to nearest even (finite inputs)
-  uint32_t u;
-  std::memcpy(&u, &f, 4);
-  u += 0x7FFFu + ((u >> 16) & 1u);
-  return (uint16_t)(u >> 16);
-}
 }  // namespace
 
 long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask,
@@ -1057,7 +1053,7 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
   if (ok && mma)
     ok = hipMallocAsync((void**)&d_qf, (size_t)kMmaQ * kEmbedDim * 2, stream_) == hipSuccess &&
          hipMallocAsync((void**)&d_thr, (size_t)kMmaQ * 4, stream_) == hipSuccess &&
-         hipMallocAsync((void**)&d_bmax, (size_t)(sample / kMmaTile) * kMmaQ * 4, stream_) == hipSuccess &&
+         hipMallocAsync((void**)&d_bmax, (size_t)std::max<long>(sample / kMmaTile, 1) * kMmaQ * 4, stream_) == hipSuccess &&
          hipMallocAsync((void**)&d_cnt, (size_t)kMmaQ * kMmaGrid * 4, stream_) == hipSuccess &&
          hipMallocAsync((void**)&d_cand, (size_t)kMmaQ * kMmaGrid * kCapb * 4, stream_) == hipSuccess;
   auto exact = [&](const float* hq, int n, CandRec* dst) -> bool {  // nq <= kExactQ per launch
@@ -1073,35 +1069,23 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
     }
     return true;
   };
-  std::vector<uint16_t> qb;
-  std::vector<uint16_t> qf;
-  std::vector<uint32_t> cnt;
-  std::vector<float> thr_h;
+  std::vector<uint32_t> over;
+  std::vector<float> thr_h, redo;
+  // a distance bound with no effective similarity floor makes every live slot a candidate (every
+  // query would overflow its segments and be redone alone): those batches go to the exact kernel
+  // directly, kExactQ queries per arena scan
+  const bool exact_only = !mma || (bounded && min_sim <= -1.f);
   for (int b = 0; ok && b < nq; b += kMmaQ) {
     const int n = std::min(kMmaQ, nq - b);
     const float* hq = q + (size_t)b * kEmbedDim;
-    if (!mma) {
+    if (exact_only) {
       ok = exact(hq, n, res.data() + (size_t)b * k);
       continue;
     }
-    // normalised bf16 queries, zero-padded to 256, in fragment order [q/16][24 steps][4 kq][16 r][8]
-    qb.assign((size_t)kMmaQ * kEmbedDim, 0);
-    for (int i = 0; i < n; ++i) {
-      double nn = 0;
-      for (size_t d = 0; d < kEmbedDim; ++d) nn += (double)hq[i * kEmbedDim + d] * hq[i * kEmbedDim + d];
-      const float inv = nn > 1e-60 ? (float)(1.0 / std::sqrt(nn)) : 0.f;
-      for (size_t d = 0; d < kEmbedDim; ++d) qb[(size_t)i * kEmbedDim + d] = f2bf_host(hq[i * kEmbedDim + d] * inv);
-    }
-    qf.resize(qb.size());
-    for (int t = 0; t < kMmaQ / 16; ++t)
-      for (int st = 0; st < 24; ++st)
-        for (int kq = 0; kq < 4; ++kq)
-          for (int r = 0; r < 16; ++r)
-            std::memcpy(&qf[((((size_t)t * 24 + st) * 4 + kq) * 16 + r) * 8],
-                        &qb[(size_t)(t * 16 + r) * kEmbedDim + st * 32 + kq * 8], 16);
+    // queries up once (fp32); the bf16 fragment operand is built on the device (spl_search_qprep)
     const float floor_v = min_sim - kDelta;
-    ok = hipMemcpyAsync(d_qf, qf.data(), qf.size() * 2, hipMemcpyHostToDevice, stream_) == hipSuccess &&
-         hipMemcpyAsync(d_q, hq, (size_t)n * kEmbedBytes, hipMemcpyHostToDevice, stream_) == hipSuccess;
+    ok = hipMemcpyAsync(d_q, hq, (size_t)n * kEmbedBytes, hipMemcpyHostToDevice, stream_) == hipSuccess &&
+         spl_search_qprep(d_q, n, d_qf, stream_) == 0;
     if (ok && !bounded) {
       ok = spl_search_mma_pass(a, d_qf, n, 0, sample, mask, 0, nullptr, d_bmax, nullptr, nullptr, 0, kMmaGrid,
                                stream_) == 0 &&
@@ -1110,21 +1094,30 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
       thr_h.assign((size_t)n, floor_v);
       ok = hipMemcpyAsync(d_thr, thr_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream_) == hipSuccess;
     }
+    // (the overflow flags reuse d_bmax: the threshold is built by then)
     ok = ok && hipMemsetAsync(d_cnt, 0, (size_t)n * kMmaGrid * 4, stream_) == hipSuccess &&
          spl_search_mma_pass(a, d_qf, n, 0, slots, mask, 1, d_thr, nullptr, d_cnt, d_cand, kCapb, kMmaGrid,
                              stream_) == 0 &&
          spl_search_rescore(a, d_q, n, k, min_sim, max_dist, mask, d_cnt, d_cand, kMmaGrid, kCapb, d_res, stream_) ==
-             0;
-    cnt.resize((size_t)n * kMmaGrid);
+             0 &&
+         spl_search_overflow(d_cnt, n, kMmaGrid, kCapb, (uint32_t*)d_bmax, stream_) == 0;
+    over.resize((size_t)n);
     ok = ok && hipMemcpyAsync(res.data() + (size_t)b * k, d_res, (size_t)n * k * sizeof(CandRec),
                               hipMemcpyDeviceToHost, stream_) == hipSuccess &&
-         hipMemcpyAsync(cnt.data(), d_cnt, cnt.size() * 4, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+         hipMemcpyAsync(over.data(), d_bmax, (size_t)n * 4, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
          hipStreamSynchronize(stream_) == hipSuccess;
-    // overflowed queries: the exact kernel
-    for (int i = 0; ok && i < n; ++i) {
-      bool over = false;
-      for (int g = 0; g < kMmaGrid && !over; ++g) over = cnt[(size_t)i * kMmaGrid + g] > (uint32_t)kCapb;
-      if (over) ok = exact(hq + (size_t)i * kEmbedDim, 1, res.data() + (size_t)(b + i) * k);
+    // overflowed queries: the exact kernel, kExactQ of them per launch
+    std::vector<int> oi;
+    for (int i = 0; ok && i < n; ++i)
+      if (over[(size_t)i]) oi.push_back(i);
+    if (ok && !oi.empty()) {
+      redo.resize(oi.size() * kEmbedDim);
+      for (size_t j = 0; j < oi.size(); ++j)
+        std::memcpy(&redo[j * kEmbedDim], hq + (size_t)oi[j] * kEmbedDim, kEmbedBytes);
+      std::vector<CandRec> rr(oi.size() * (size_t)k);
+      ok = exact(redo.data(), (int)oi.size(), rr.data());
+      for (size_t j = 0; ok && j < oi.size(); ++j)
+        std::memcpy(&res[(size_t)(b + oi[j]) * k], &rr[j * k], (size_t)k * sizeof(CandRec));
     }
   }
   for (void* p : {(void*)d_q, (void*)d_thr, (void*)d_bmax, (void*)d_qf, (void*)d_cnt, (void*)d_cand, d_res, d_scr})
@@ -1250,78 +1243,132 @@ int HbmStore::probe_stats(ProbeStats* out) {
   return rc == 0 ? 0 : -1;
 }
 
-// Tombstone rebuild (arena_maint.hip k_rehash).  EXCLUSIVE: the store's ring worker is held for the
-// pass and the caller guarantees that no batch op of any process runs on the arena meanwhile.
-// out: {moved, reclaimed, clusters, clusters past the per-wave tombstone cap}.
-int HbmStore::rehash(uint64_t out[4]) {
+// Tombstone maintenance (arena_maint.hip).  Default: the ONLINE cluster compaction -- keys move
+// under both slots' seqlocks while every process keeps running batch and per-call ops; the pass is
+// bracketed by the side header's maintenance seq (odd while it runs: "absent" outcomes and
+// inserts report EAGAIN meanwhile).  SPL_REHASH_FULL: the full rebuild (copy out, clear, re-insert)
+// -- EXCLUSIVE, the caller guarantees that no op of any process runs on the arena; refused with
+// EBUSY when this store's ring worker cannot be held, with ENOMEM (and the scratch size on stderr)
+// when the scratch cannot be allocated.  out: {moved, reclaimed, clusters, clusters past the
+// per-wave tombstone cap}.
+int HbmStore::rehash(uint64_t out[4], unsigned flags) {
   if (!ensure_mapped()) return -1;
+  if (!(side_flags_ & SPL_ARENA_SIDE)) { errno = ENOTSUP; return -1; }
   DevGuard dg(device_);
-  // strategy: in-place cluster compaction while never-used slots still split the table into short
-  // clusters; a full rebuild (copy out, clear, re-insert) once fewer than 5 % of the slots are
-  // never-used -- the clusters have merged and the compaction would walk them one wave each
+  out[0] = out[1] = out[2] = out[3] = 0;
   ProbeStats ps;
   if (probe_stats(&ps) != 0) return -1;
-  const bool full = ps.virgin * 20 < geo_.slots && ps.live > 0;
-  const bool held = ring_ && ring_->ready() && ring_->hold(true) == 0;
-  int rc = 0;
-  bool done = false;
-  if (full) {
-    std::lock_guard<std::mutex> lk(mu_);
-    const spl_arena_t a = arena();
-    uint32_t* d_idx = nullptr;
-    uint64_t* d_cnt = nullptr;
-    void* d_tmp = nullptr;
-    uint64_t hc[2] = {0, 0};
-    if (hipMalloc((void**)&d_idx, (size_t)geo_.slots * 4) == hipSuccess &&
-        hipMalloc((void**)&d_cnt, 16) == hipSuccess && hipMemsetAsync(d_cnt, 0, 16, stream_) == hipSuccess &&
-        spl_arena_rebuild_collect(a, d_idx, d_cnt, stream_) == 0 &&
-        hipMemcpyAsync(hc, d_cnt, 8, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
-        hipStreamSynchronize(stream_) == hipSuccess &&
-        hipMalloc(&d_tmp, (size_t)hc[0] * spl_arena_rebuild_rec(a) + 16) == hipSuccess) {
-      // from here on the arena is rewritten: a failure is an error, never a fall-back
-      if (spl_arena_rebuild_move(a, d_idx, hc[0], d_tmp, d_cnt + 1, stream_) != 0 ||
-          hipMemcpyAsync(hc + 1, d_cnt + 1, 8, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
-          hipStreamSynchronize(stream_) != hipSuccess || hc[1] != 0)
-        rc = -1;
-      out[0] = hc[0];
-      out[1] = ps.tombstones;
-      out[2] = 0;
-      out[3] = hc[1];
-      done = true;
-    } else {
-      (void)hipGetLastError();  // allocation failed: the in-place compaction below instead
+  uint8_t* const side = (uint8_t*)dbase_ + side_offset(geo_.slots, geo_.stride, geo_.max_val);
+  const spl_arena_t a = arena();
+  // a pass left open by a process that died (seq odd, its pid gone) is closed first
+  {
+    MaintRec mr;
+    if (hipMemcpy(&mr, side + kSideMaintOff, sizeof mr, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    if (mr.seq & 1) {
+      const bool alive = mr.pid > 0 && (::kill((pid_t)mr.pid, 0) == 0 || errno == EPERM);
+      if (alive) { errno = EBUSY; return -1; }
+      std::lock_guard<std::mutex> lk(mu_);
+      uint64_t* d = nullptr;
+      if (hipMallocAsync((void**)&d, 8, stream_) != hipSuccess) return -1;
+      const int rc = spl_arena_maint_mark(a, 0, 0, 0, d, stream_);
+      (void)hipFreeAsync(d, stream_);
+      if (rc != 0 || hipStreamSynchronize(stream_) != hipSuccess) return -1;
+      fprintf(stderr, "[splinter] closed a maintenance pass left open by pid %d\n", mr.pid);
     }
-    if (d_tmp) (void)hipFree(d_tmp);
-    if (d_cnt) (void)hipFree(d_cnt);
-    if (d_idx) (void)hipFree(d_idx);
   }
-  if (!done) {
+  int rc = 0;
+  if (flags & SPL_REHASH_FULL) {
+    const bool need_hold = ring_ && ring_->ready();
+    const bool held = need_hold && ring_->hold(true) == 0;
+    if (need_hold && !held) { errno = EBUSY; return -1; }
+    {
+      RingQuiesce quiet;  // hipMalloc / hipFree may wait for the device: no resident worker of this process
+      std::lock_guard<std::mutex> lk(mu_);
+      uint32_t* d_idx = nullptr;
+      uint64_t* d_cnt = nullptr;
+      void* d_tmp = nullptr;
+      uint64_t hc[2] = {0, 0};
+      size_t scratch = 0;
+      bool alloc_ok = hipMalloc((void**)&d_idx, (size_t)geo_.slots * 4) == hipSuccess &&
+                      hipMalloc((void**)&d_cnt, 16) == hipSuccess && hipMemsetAsync(d_cnt, 0, 16, stream_) == hipSuccess &&
+                      spl_arena_rebuild_collect(a, d_idx, d_cnt, stream_) == 0 &&
+                      hipMemcpyAsync(hc, d_cnt, 8, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
+                      hipStreamSynchronize(stream_) == hipSuccess;
+      if (alloc_ok) {
+        scratch = (size_t)hc[0] * spl_arena_rebuild_rec(a) + 16;
+        alloc_ok = hipMalloc(&d_tmp, scratch) == hipSuccess;
+      }
+      if (!alloc_ok) {
+        (void)hipGetLastError();
+        size_t fr = 0, tot = 0;
+        (void)hipMemGetInfo(&fr, &tot);
+        fprintf(stderr, "[splinter] rehash --full: cannot allocate %zu B of scratch (%lu live entries x %u B; %zu B free "
+                "on the device); the arena is unchanged -- run the online rehash instead\n",
+                scratch ? scratch : (size_t)geo_.slots * 4, (unsigned long)hc[0], spl_arena_rebuild_rec(a), fr);
+        errno = ENOMEM;
+        rc = -1;
+      } else {
+        // from here on the arena is rewritten: a failure is an error
+        if (spl_arena_rebuild_move(a, d_idx, hc[0], d_tmp, d_cnt + 1, stream_) != 0 ||
+            hipMemcpyAsync(hc + 1, d_cnt + 1, 8, hipMemcpyDeviceToHost, stream_) != hipSuccess ||
+            hipStreamSynchronize(stream_) != hipSuccess || hc[1] != 0)
+          rc = -1;
+        out[0] = hc[0];
+        out[1] = ps.tombstones;
+        out[3] = hc[1];
+      }
+      if (d_tmp) (void)hipFree(d_tmp);
+      if (d_cnt) (void)hipFree(d_cnt);
+      if (d_idx) (void)hipFree(d_idx);
+    }
+    if (held) ring_->hold(false);
+  } else {
     std::lock_guard<std::mutex> lk(mu_);
     uint64_t* d = nullptr;
-    if (hipMallocAsync((void**)&d, 32, stream_) != hipSuccess) rc = -1;
-    if (rc == 0) {
-      (void)hipMemsetAsync(d, 0, 32, stream_);
-      rc = spl_arena_rehash(arena(), d, stream_);
+    // d[0..4]: the pass counters (moved, reclaimed, clusters, skipped, largest displacement);
+    // d[6] / d[7]: the open / close results
+    if (hipMallocAsync((void**)&d, 64, stream_) != hipSuccess) return -1;
+    timespec ts;
+    clock_gettime(CLOCK_REALTIME, &ts);
+    const uint64_t t0 = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+    uint64_t won = 0;
+    (void)hipMemsetAsync(d, 0, 64, stream_);
+    rc = spl_arena_maint_mark(a, 1, (int)getpid(), t0, d + 6, stream_);
+    if (rc == 0) rc = hipMemcpyAsync(&won, d + 6, 8, hipMemcpyDeviceToHost, stream_) == hipSuccess ? 0 : -1;
+    if (rc == 0) rc = hipStreamSynchronize(stream_) == hipSuccess ? 0 : -1;
+    if (rc == 0 && !won) {
+      errno = EBUSY;  // another process's pass is running
+      rc = -1;
+    } else if (rc == 0) {
+      rc = spl_arena_rehash(a, d, stream_);
+      // the pass is closed whatever the walk returned: an open seq would turn every miss into EAGAIN
+      if (spl_arena_maint_mark(a, 0, 0, 0, d + 7, stream_) != 0) rc = -1;
       if (rc == 0) (void)hipMemcpyAsync(out, d, 32, hipMemcpyDeviceToHost, stream_);
-      (void)hipFreeAsync(d, stream_);
+      if (hipStreamSynchronize(stream_) != hipSuccess) rc = -1;
     }
-    if (hipStreamSynchronize(stream_) != hipSuccess) rc = -1;
+    (void)hipFreeAsync(d, stream_);
+    (void)hipStreamSynchronize(stream_);
   }
-  {
+  if (rc == 0) {
     std::lock_guard<std::mutex> lk(mu_);
-    if (rc == 0 && (side_flags_ & SPL_ARENA_SIDE)) {
-      ProbeStats side;
-      uint8_t* sp = (uint8_t*)dbase_ + side_offset(geo_.slots, geo_.stride, geo_.max_val);
-      if (hipMemcpy(&side, sp, sizeof side, hipMemcpyDeviceToHost) == hipSuccess) {
-        side.rebuilds += 1;
-        side.moved += out[0];
-        side.reclaimed += out[1];
-        (void)hipMemcpy(sp, &side, sizeof side, hipMemcpyHostToDevice);
-      }
+    ProbeStats sd;
+    if (hipMemcpy(&sd, side, sizeof sd, hipMemcpyDeviceToHost) == hipSuccess) {
+      sd.rebuilds += 1;
+      sd.moved += out[0];
+      sd.reclaimed += out[1];
+      (void)hipMemcpy(side, &sd, sizeof sd, hipMemcpyHostToDevice);
     }
   }
-  if (held) ring_->hold(false);
   return rc == 0 ? 0 : -1;
+}
+
+// The maintenance seq of the arena (odd while a pass runs), for hosts that enumerate and want to
+// know whether a pass overlapped them.
+int HbmStore::maint_seq(uint64_t* seq) {
+  if (!ensure_mapped() || !(side_flags_ & SPL_ARENA_SIDE)) return -1;
+  DevGuard dg(device_);
+  const uint8_t* side = (const uint8_t*)dbase_ + side_offset(geo_.slots, geo_.stride, geo_.max_val);
+  return hipMemcpy(seq, side + kSideMaintOff, 8, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 
 StoreBase* hbm_factory_impl(const char* name, size_t slots, size_t max_val, unsigned flags, int create, int* err) {
@@ -1641,8 +1688,9 @@ long spl_hbm_search(spl_store* h, const float* query, uint64_t mask, float min_s
 }
 
 // Batched top-k search (HbmStore::search_batch) of an HBM store, or of a node store of HBM shards:
-// every shard answers every query on its GPU, and the per-shard top-k lists are merged per query
-// (similarity desc, distance asc) -- the in-process C4 merge.  out[nq * k]; returns nq or < 0.
+// every shard answers every query on its GPU, all shards concurrently, and the per-shard top-k
+// lists are merged per query (similarity desc, distance asc) -- the in-process C4 merge.
+// out[nq * k]; returns nq or < 0.
 long spl_search_batch(spl_store* h, const float* queries, int nq, int k, float min_sim, float max_dist,
                       uint64_t mask, spl_search_hit* out) {
   if (!h || !queries || !out || nq <= 0 || k <= 0 || k > 32) return -2;
@@ -1650,14 +1698,26 @@ long spl_search_batch(spl_store* h, const float* queries, int nq, int k, float m
     return s->search_batch(queries, nq, k, min_sim, max_dist, mask, out);
   const int n = spl_node_nshards(h);
   if (n < 1) return -2;
-  std::vector<spl_search_hit> part((size_t)nq * k);
+  // every shard answers every query at once: one host thread per shard, each driving its own
+  // store's stream on its own GPU (was one shard after another, each with its own synchronise)
+  std::vector<std::vector<spl_search_hit>> part((size_t)n, std::vector<spl_search_hit>((size_t)nq * k));
+  std::vector<long> rc((size_t)n, -1);
+  {
+    std::vector<std::thread> th;
+    th.reserve((size_t)n);
+    for (int i = 0; i < n; ++i)
+      th.emplace_back([&, i] {
+        auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+        rc[(size_t)i] = s ? s->search_batch(queries, nq, k, min_sim, max_dist, mask, part[(size_t)i].data()) : -1;
+      });
+    for (auto& t : th) t.join();
+  }
   std::vector<std::vector<spl_search_hit>> all((size_t)nq);
   for (int i = 0; i < n; ++i) {
-    auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
-    if (!s || s->search_batch(queries, nq, k, min_sim, max_dist, mask, part.data()) != nq) return -1;
+    if (rc[(size_t)i] != nq) return -1;
     for (int qi = 0; qi < nq; ++qi)
       for (int j = 0; j < k; ++j)
-        if (part[(size_t)qi * k + j].emb) all[qi].push_back(part[(size_t)qi * k + j]);
+        if (part[(size_t)i][(size_t)qi * k + j].emb) all[qi].push_back(part[(size_t)i][(size_t)qi * k + j]);
   }
   auto better = [](const spl_search_hit& a, const spl_search_hit& b) {
     if (a.sim != b.sim) return a.sim > b.sim;
@@ -1701,13 +1761,14 @@ int spl_hbm_probe_stats(spl_store* h, spl_probe_stats* out) {
   return 0;
 }
 
-// Tombstone rebuild of an HBM store / every shard of a node store (exclusive maintenance; see
-// HbmStore::rehash).  out (optional): {moved, reclaimed, clusters, skipped}, summed.
-int spl_hbm_rehash(spl_store* h, uint64_t* out) {
+// Tombstone maintenance of an HBM store / every shard of a node store (see HbmStore::rehash:
+// online compaction by default, SPL_REHASH_FULL the exclusive full rebuild).  out (optional):
+// {moved, reclaimed, clusters, skipped}, summed.
+int spl_hbm_rehash_ex(spl_store* h, unsigned flags, uint64_t* out) {
   uint64_t tmp[4] = {0, 0, 0, 0};
   if (!h) return -2;
   if (auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h)) {
-    const int rc = s->rehash(tmp);
+    const int rc = s->rehash(tmp, flags);
     if (out) std::memcpy(out, tmp, sizeof tmp);
     return rc;
   }
@@ -1716,11 +1777,17 @@ int spl_hbm_rehash(spl_store* h, uint64_t* out) {
   uint64_t sum[4] = {0, 0, 0, 0};
   for (int i = 0; i < n; ++i) {
     auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
-    if (!s || s->rehash(tmp) != 0) return -1;
+    if (!s || s->rehash(tmp, flags) != 0) return -1;
     for (int k = 0; k < 4; ++k) sum[k] += tmp[k];
   }
   if (out) std::memcpy(out, sum, sizeof sum);
   return 0;
+}
+int spl_hbm_rehash(spl_store* h, uint64_t* out) { return spl_hbm_rehash_ex(h, 0, out); }
+
+int spl_hbm_maint_seq(spl_store* h, uint64_t* seq) {
+  auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)h);
+  return s && seq ? s->maint_seq(seq) : -2;
 }
 
 // checkpoint / restore of an HBM store, or of every shard of a node store (PATH.s<i>)

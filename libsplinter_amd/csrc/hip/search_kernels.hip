@@ -855,6 +855,46 @@ __global__ __launch_bounds__(256) void k_score_all(spl_arena_t aa, const float* 
 
 }  // namespace
 
+// ---------------------------------------------------------- query prep --
+// The batched search's query operand on the device (was a host loop per 256-query block): one
+// workgroup per query slot of the 256-query block -- L2 norm (fp32 sum of squares over the wave
+// reduction), normalised, rounded to bf16, stored in the candidate pass's fragment order
+// [16 q-tiles][24 steps][4 kq][16 r][8]: dims [32 step + 8 kq, +8) of query 16 tile + r.  Query
+// slots >= n are zero.
+__global__ __launch_bounds__(256) void k_search_qprep(const float* __restrict__ q, int n, uint16_t* __restrict__ qf) {
+  const int qi = blockIdx.x, t = threadIdx.x;
+  __shared__ float red[4];
+  float v[3] = {0.f, 0.f, 0.f};
+  if (qi < n) {
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = q[(long)qi * 768 + t + 256 * c];
+  }
+  float ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  if ((t & 63) == 0) red[t >> 6] = ss;
+  __syncthreads();
+  const float tot = red[0] + red[1] + red[2] + red[3];
+  const float inv = tot > 1e-30f ? rsqrtf(tot) : 0.f;
+  const int tile = qi >> 4, r = qi & 15;
+#pragma unroll
+  for (int c = 0; c < 3; ++c) {
+    const int d = t + 256 * c;
+    const int st = d >> 5, kq = (d >> 3) & 3, e = d & 7;
+    qf[((((long)tile * 24 + st) * 4 + kq) * 16 + r) * 8 + e] = __builtin_bit_cast(uint16_t, (__bf16)(v[c] * inv));
+  }
+}
+
+// over[q] = 1 when query q's candidate segment overflowed in any block (cnt[q][g] > capb)
+__global__ __launch_bounds__(256) void k_search_over(const uint32_t* __restrict__ cnt, int nblk, int capb,
+                                                     uint32_t* __restrict__ over) {
+  const int qi = blockIdx.x;
+  bool o = false;
+  for (int g = threadIdx.x; g < nblk; g += 256) o |= cnt[(long)qi * nblk + g] > (uint32_t)capb;
+  o = __syncthreads_or(o);
+  if (threadIdx.x == 0) over[qi] = o ? 1u : 0u;
+}
+
 extern "C" {
 
 int spl_arena_score_all(spl_arena_t a, const float* query, float min_sim, float max_dist, uint64_t mask, void* out,
@@ -869,6 +909,18 @@ int spl_arena_score_all(spl_arena_t a, const float* query, float min_sim, float 
 
 
 int spl_search_lists(int grid) { return grid * kWaves; }
+
+int spl_search_qprep(const float* queries, int nq, void* qfrag, hipStream_t s) {
+  if (nq <= 0 || nq > mf::kQ || !queries || !qfrag) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_search_qprep, dim3(mf::kQ), dim3(256), 0, s, queries, nq, (uint16_t*)qfrag);
+  return (int)hipGetLastError();
+}
+
+int spl_search_overflow(const uint32_t* cnt, int nq, int nblk, int capb, uint32_t* over, hipStream_t s) {
+  if (nq <= 0 || nblk <= 0 || !cnt || !over) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_search_over, dim3(nq), dim3(256), 0, s, cnt, nblk, capb, over);
+  return (int)hipGetLastError();
+}
 
 // queries [nq, 768] fp32 (nq <= 16), K <= 32.  `scratch` must hold
 // grid * 4 * nq * K candidates (16 B each); result [nq, K] candidates

@@ -93,6 +93,9 @@ int spl_arena_purge(spl_arena_t a, hipStream_t stream);
  * the fp32 vectors (SPL_ARENA_VEC16 arenas) */
 int spl_arena_probe_stats(spl_arena_t a, void *out, hipStream_t stream);
 int spl_arena_rehash(spl_arena_t a, void *counters, hipStream_t stream);
+/* open (begin 1) / close (0) an online maintenance pass (side header MaintRec::seq odd while open);
+ * ok: device u64, 1 when the open won (no other pass was running) */
+int spl_arena_maint_mark(spl_arena_t a, int begin, int pid, uint64_t t0_ns, void *ok, hipStream_t stream);
 int spl_arena_vec16_rebuild(spl_arena_t a, hipStream_t stream);
 /* full rebuild (exclusive): collect the live slot indices (device u32[slots], count: device u64
  * zeroed), then move them out to tmp (n * spl_arena_rebuild_rec bytes), clear the slot array and

@@ -29,6 +29,11 @@ int spl_search_mma_tile(void);
 int spl_search_mma_pass(spl_arena_t a, const void *qfrag, int nq, long slot_begin, long slot_end, uint64_t mask,
                         int mode, const float *thr, float *bmax, uint32_t *cnt, uint32_t *cand, int capb, int grid,
                         hipStream_t stream);
+/* queries [nq <= 256, 768] fp32 (device) -> qfrag as spl_search_mma_pass takes it (normalised,
+ * bf16, zero-padded to 256 queries, fragment order) */
+int spl_search_qprep(const float *queries, int nq, void *qfrag, hipStream_t stream);
+/* over[q] = 1 when cnt[q][0..nblk) has a segment count > capb (the query must be redone exactly) */
+int spl_search_overflow(const uint32_t *cnt, int nq, int nblk, int capb, uint32_t *over, hipStream_t stream);
 /* per-query candidate threshold from a bmax pass: max(k-th largest of bmax[tiles][nq] - delta2, floor) */
 int spl_search_thr(const float *bmax, int tiles, int nq, int K, float delta2, float floor_v, float *thr,
                    hipStream_t stream);

@@ -116,12 +116,30 @@ typedef struct spl_probe_stats {
   uint64_t rebuilds, reclaimed, moved, pad;
 } spl_probe_stats;
 int   spl_hbm_probe_stats(spl_store *s, spl_probe_stats *out);
-/* Tombstone rebuild: every live key moves into the first tombstone on its own probe path and the
- * tombstones left at the end of each cluster become never-used slots again, so misses stop at the
- * cluster's new end.  EXCLUSIVE maintenance (like a compaction): no other process may run batch ops
- * on the store meanwhile; the store's per-call ring is held for the pass.  out (optional):
- * {keys moved, tombstones reclaimed, clusters, clusters with more than 1024 tombstones}. */
-int   spl_hbm_rehash(spl_store *s, uint64_t *out);
+/* Tombstone maintenance: every live key moves into the first tombstone on its own probe path and
+ * the tombstones left at the end of each cluster become never-used slots again, so misses stop at
+ * the cluster's new end.  ONLINE: safe beside batch and per-call ops of every process -- each move
+ * holds both slots' seqlocks, and while the pass runs "absent" outcomes (get miss, insert of a new
+ * key, unset / update of a missing key) report EAGAIN instead (the key may be mid-move); hits and
+ * updates of present keys proceed.  flags SPL_REHASH_FULL: the full rebuild instead (copy out,
+ * clear, re-insert: no tombstones left at all), EXCLUSIVE -- the caller guarantees that no op of
+ * any process runs on the store; -1/EBUSY when this store's ring cannot be held, -1/ENOMEM (the
+ * scratch size on stderr) when its scratch cannot be allocated.  -1/EBUSY also when another
+ * process's pass is running.  out (optional): {keys moved, tombstones reclaimed, clusters,
+ * clusters with more than 512 tombstones}. */
+#define SPL_REHASH_FULL 1u
+int   spl_hbm_rehash_ex(spl_store *s, unsigned flags, uint64_t *out);
+int   spl_hbm_rehash(spl_store *s, uint64_t *out);  /* = spl_hbm_rehash_ex(s, 0, out) */
+/* The maintenance seq of an hbm: store (odd while a pass runs; +2 per pass): a host that enumerates
+ * reads it before and after, and enumerates again when it changed. */
+int   spl_hbm_maint_seq(spl_store *s, uint64_t *seq);
+
+/* Checkpoint / restore of any store: a host store writes its v4 image (tmp + rename), an hbm: store
+ * streams its device image, a node store writes every serving shard to PATH.s<i>.  Restore loads an
+ * image into an open store of the same geometry (hbm: / host; exclusive -- a restarting rank
+ * restores its shard before it joins).  0, or -1 with errno. */
+int   spl_store_checkpoint(spl_store *s, const char *path);
+int   spl_store_restore(spl_store *s, const char *path);
 
 /* Node stores ("node:NAME", node_store.hpp): one store over a node's per-GPU arenas, key-sharded
  * by ((fnv1a(key) >> 40) & 0xFFFFFF) % nshards.  splinter_create("node:NAME", slots, max_val)
@@ -130,9 +148,18 @@ int   spl_hbm_rehash(spl_store *s, uint64_t *out);
  * opens "node:NAME".  backend: 0 host shm shards, 1 HBM shards; stride 128 or 3200. */
 int   spl_node_join(const char *name, int shard, int nshards, unsigned backend, size_t slots_per_shard,
                     size_t max_val, unsigned stride);
+/* flags SPL_NODE_OWNED: the shard is served only while the joining process lives (HBM shards
+ * always: spl_node_join sets it for them); otherwise a host shard outlives its rank like any shm
+ * store.  A shard that joins again (a restarted rank) is re-opened by every open node store. */
+#define SPL_NODE_OWNED 1u
+int   spl_node_join_ex(const char *name, int shard, int nshards, unsigned backend, size_t slots_per_shard,
+                       size_t max_val, unsigned stride, unsigned flags);
 int   spl_node_leave(const char *name, int shard);
 int   spl_node_shard_name(const char *name, int shard, unsigned backend, char *out, size_t cap);
 int   spl_node_nshards(spl_store *s);           /* -1 if s is not a node store */
+/* Degraded mode of a joined node: 0 shard i serves, 1 its rank's process is gone (ops on its keys
+ * return -1/EAGAIN, batch rows -EAGAIN, until the rank's restarted process re-joins), -1 no shard. */
+int   spl_node_shard_state(spl_store *s, int shard);
 spl_store *spl_node_shard(spl_store *s, int i);
 int   spl_node_shard_of(const char *key, int nshards);
 int   spl_hbm_device_count(void);               /* libsplinter_hip.so */

@@ -75,6 +75,21 @@ struct ProbeStats {
 };
 static_assert(sizeof(ProbeStats) % 16 == 0, "16-B rows");
 
+// Online maintenance record, at kSideMaintOff of the side header (its own 128-B line, past the
+// ProbeStats block the host rewrites): `seq` is odd while a maintenance pass moves entries
+// (arena_maint.hip k_rehash), `pid` / `t0_ns` name the process that opened the pass, so a pass
+// whose process died can be closed by the next one (HbmStore::rehash).  Device probes read `seq`
+// around every "absent" outcome (arena_dev.hpp maint_quiet).
+constexpr size_t kSideMaintOff = 256;
+struct MaintRec {
+  uint64_t seq;
+  int32_t pid;
+  uint32_t pad;
+  uint64_t t0_ns;
+  uint64_t passes;  // passes completed
+};
+static_assert(kSideMaintOff >= sizeof(ProbeStats) && kSideMaintOff % 128 == 0, "maint record line");
+
 static_assert(sizeof(splinter_header) == kHeaderBytes, "v4 header must be 5440 B");
 static_assert(alignof(splinter_header) == 64, "header alignment");
 static_assert(sizeof(splinter_slot) == kSlotCoreBytes, "slot core must be 128 B");

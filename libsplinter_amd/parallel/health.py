@@ -13,6 +13,10 @@ On a sharded node a dead rank would leave every peer blocked in its next collect
   ``EXIT_PEER_LOST`` via ``os._exit`` (a blocked collective cannot be interrupted from Python; the
   launcher, torchrun or bench.py, then reports the failure).  Never a re-exec;
 * ``guarded(fn)``: run a step, turning a collective error into the same non-zero exit.
+
+Degraded serving instead of the exit: ``Liveness(degrade=True)`` with parallel/elastic.py (the node
+store answers EAGAIN for a lost rank's shard; a supervisor restarts the rank as a fresh process
+that restores its checkpoint and re-joins).
 """
 from __future__ import annotations
 
@@ -41,15 +45,52 @@ def _default_store():
     return c10d._get_default_store()
 
 
+class Heartbeat:
+    """Rank ``rank``'s heartbeat on a key-value store (``splinter/hb/<rank>`` = wall time, every
+    ``period_s``).  A rank restarted as a fresh process (parallel/elastic.py) is no member of the old
+    process group, but beats on the same store, so its survivors see it back."""
+
+    def __init__(self, store, rank: int, period_s: float = 1.0):
+        self.store, self.rank, self.period = store, rank, period_s
+        self._stop = threading.Event()
+        self.beat()
+        self._t = threading.Thread(target=self._run, name="splinter-heartbeat", daemon=True)
+        self._t.start()
+
+    def beat(self):
+        self.store.set(f"splinter/hb/{self.rank}", repr(time.time()))
+
+    def _run(self):
+        while not self._stop.wait(self.period):
+            try:
+                self.beat()
+            except Exception:  # the store is gone: nothing left to tell
+                return
+
+    def stop(self):
+        self._stop.set()
+        self._t.join(self.period * 4)
+
+
 class Liveness:
+    """Heartbeat + peer monitor.  Default: a lost peer ends this process (EXIT_PEER_LOST).
+    ``degrade=True``: the loss is reported (``on_lost(rank)``) and this rank keeps running -- its
+    node-store shard keeps serving, ops on the lost rank's shard answer EAGAIN (node_store.hpp) --
+    and a peer whose heartbeat comes back (its restarted process) is reported by ``on_back(rank)``."""
+
     def __init__(self, period_s: float = 1.0, timeout_s: float = 10.0, exit_code: int = EXIT_PEER_LOST,
-                 on_lost=None):
+                 on_lost=None, degrade: bool = False, on_back=None, store=None):
         self.rank, self.world = dist.get_rank(), dist.get_world_size()
         self.period, self.timeout, self.exit_code = period_s, timeout_s, exit_code
-        self.on_lost = on_lost  # test hook: called instead of os._exit
-        self.store = _default_store()
+        self.on_lost = on_lost  # called instead of os._exit
+        self.on_back = on_back
+        self.degrade = degrade
+        # the heartbeat keys' store: the process group's (default) or one the caller shares with
+        # processes outside the group (a restarted rank, parallel/elastic.py)
+        self.store = store if store is not None else _default_store()
         self._stop = threading.Event()
         self.lost: Optional[int] = None
+        self.down = set()
         self._beat()
         self._t = threading.Thread(target=self._run, name="splinter-liveness", daemon=True)
         self._t.start()
@@ -59,12 +100,19 @@ class Liveness:
 
     def _lost(self, who: int, why: str):
         self.lost = who
-        msg = f"[splinter] rank {self.rank}: peer {who} lost ({why}); exiting with {self.exit_code}"
-        print(msg, file=sys.stderr, flush=True)
+        self.down.add(who)
+        tail = "serving degraded" if self.degrade else f"exiting with {self.exit_code}"
+        print(f"[splinter] rank {self.rank}: peer {who} lost ({why}); {tail}", file=sys.stderr, flush=True)
         if self.on_lost is not None:
             self.on_lost(who)
             return
         os._exit(self.exit_code)
+
+    def _back(self, who: int):
+        self.down.discard(who)
+        print(f"[splinter] rank {self.rank}: peer {who} back", file=sys.stderr, flush=True)
+        if self.on_back is not None:
+            self.on_back(who)
 
     def _run(self):
         start = time.time()
@@ -77,12 +125,18 @@ class Liveness:
                         continue
                     key = f"splinter/hb/{r}"
                     if not self.store.check([key]):
-                        if now - start > self.timeout:
-                            return self._lost(r, "no heartbeat")
+                        if now - start > self.timeout and r not in self.down:
+                            self._lost(r, "no heartbeat")
+                            if not self.degrade:
+                                return
                         continue
-                    last = float(self.store.get(key).decode())
-                    if now - last > self.timeout:
-                        return self._lost(r, f"heartbeat {now - last:.1f} s old")
+                    age = now - float(self.store.get(key).decode())
+                    if age > self.timeout and r not in self.down:
+                        self._lost(r, f"heartbeat {age:.1f} s old")
+                        if not self.degrade:
+                            return
+                    elif age <= self.timeout and r in self.down:
+                        self._back(r)
             except Exception as e:  # the store (hosted by rank 0) is gone
                 if self._stop.is_set():
                     return

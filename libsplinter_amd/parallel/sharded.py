@@ -475,6 +475,8 @@ class GpuShard:
         return core[:, KEY_BYTES:]
 
     def search(self, q, k, min_sim, max_dist, label_mask):
+        if q.shape[0] >= 32 and self.capi_search:
+            return self._search_capi(q, k, min_sim, max_dist, label_mask)
         from ..ops.search import VectorSearch
         if self._search is None:
             self._search = VectorSearch(self.arena, grid=self._grid)
@@ -488,6 +490,22 @@ class GpuShard:
         sim = torch.where(valid, sim, torch.full_like(sim, -1e30))
         dst = torch.where(valid, dst, torch.full_like(dst, 3.4e38))
         return sim, dst, rows
+
+    # many-query searches go through the product C ABI (spl_search_batch on this shard's store: device
+    # query prep, MFMA candidate passes, fp32 re-score, keys fetched with the hits); False: the
+    # Python driver of the same kernels (ops/search.py VectorSearch.search_batch)
+    capi_search = os.environ.get("SPLINTER_SEARCH_CAPI", "1") != "0"
+
+    def _search_capi(self, q, k, min_sim, max_dist, label_mask):
+        hits = self.arena.store.search_batch(q.detach().float().cpu().numpy(), k, min_sim, max_dist, label_mask)
+        valid = hits["emb"] != 0
+        sim = np.where(valid, hits["sim"], np.float32(-1e30)).astype(np.float32)
+        dst = np.where(valid, hits["dist"], np.float32(3.4e38)).astype(np.float32)
+        rows = np.zeros((hits.shape[0], hits.shape[1], KEY_BYTES), dtype=np.uint8)
+        rows[...] = np.frombuffer(hits["key"].tobytes(), dtype=np.uint8).reshape(hits.shape[0], hits.shape[1], 64)
+        rows *= valid[..., None].astype(np.uint8)
+        dev = q.device
+        return (torch.from_numpy(sim).to(dev), torch.from_numpy(dst).to(dev), torch.from_numpy(rows).to(dev))
 
     def enumerate(self, mask):
         from ..ops.arena import SCAN_LABELS, SCAN_LIST

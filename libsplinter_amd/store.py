@@ -90,11 +90,18 @@ def node_shard_of(key, nshards: int) -> int:
 
 
 def node_join(node: str, shard: int, nshards: int, backend: int, slots_per_shard: int, max_val: int,
-              embeddings: bool) -> None:
+              embeddings: bool, owned: Optional[bool] = None) -> None:
     """Register this rank's shard store (created first, as node_shard_name(...)) with node `node`;
-    once every shard has joined, any process can open "node:<node>"."""
+    once every shard has joined, any process can open "node:<node>".  ``owned``: the shard is served
+    only while this process lives (default: HBM shards yes, host shards no) -- see
+    spl_node_join_ex and parallel/elastic.py."""
     stride = 3200 if embeddings else 128
-    if N.core_lib().spl_node_join(node.encode(), shard, nshards, backend, slots_per_shard, max_val, stride) != 0:
+    flags = (1 if (owned if owned is not None else backend == NODE_HBM) else 0)
+    L = N.core_lib()
+    L.spl_node_join_ex.restype = ctypes.c_int
+    L.spl_node_join_ex.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_uint, ctypes.c_size_t,
+                                   ctypes.c_size_t, ctypes.c_uint, ctypes.c_uint]
+    if L.spl_node_join_ex(node.encode(), shard, nshards, backend, slots_per_shard, max_val, stride, flags) != 0:
         _raise(f"node_join {node}")
 
 
@@ -587,17 +594,74 @@ class Store:
         d["miss_mean"] = d["miss_sum"] / self.slots if d["virgin"] else float(self.slots)
         return d
 
-    def rehash(self) -> dict:
-        """Tombstone rebuild (spl_hbm_rehash): keys move into tombstones on their own probe path and
-        the tombstones left at the end of each cluster become never-used slots.  Exclusive
-        maintenance: no other process may run batch ops on the store meanwhile."""
+    def rehash(self, full: bool = False) -> dict:
+        """Tombstone maintenance (spl_hbm_rehash_ex): keys move into tombstones on their own probe path
+        and the tombstones left at the end of each cluster become never-used slots.  Online by
+        default -- safe beside live batch / per-call ops of any process (moves hold both slots'
+        seqlocks; misses and new inserts report EAGAIN while the pass runs).  ``full``: the exclusive
+        rebuild (no other op of any process may run meanwhile)."""
         L = N.hip_lib()
         out = (ctypes.c_uint64 * 4)()
-        L.spl_hbm_rehash.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
-        L.spl_hbm_rehash.restype = ctypes.c_int
-        if L.spl_hbm_rehash(self._h, out) != 0:
+        L.spl_hbm_rehash_ex.argtypes = [ctypes.c_void_p, ctypes.c_uint, ctypes.c_void_p]
+        L.spl_hbm_rehash_ex.restype = ctypes.c_int
+        if L.spl_hbm_rehash_ex(self._h, 1 if full else 0, out) != 0:
             _raise(f"rehash {self.name}")
         return dict(zip(("moved", "reclaimed", "clusters", "skipped"), list(out)))
+
+    # ------------------------------------------------ checkpoint / degraded node --
+    def checkpoint(self, path: str) -> None:
+        """Write the store's v4 image to `path` (spl_store_checkpoint: host stores tmp + rename, hbm:
+        stores their device image, a node store every serving shard to PATH.s<i>)."""
+        L = N.core_lib()
+        L.spl_store_checkpoint.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        L.spl_store_checkpoint.restype = ctypes.c_int
+        if L.spl_store_checkpoint(self._h, path.encode()) != 0:
+            _raise(f"checkpoint {self.name} -> {path}")
+
+    def restore(self, path: str) -> None:
+        """Load a checkpoint image of the same geometry into this store (exclusive: a restarting rank
+        restores its shard before it joins its node)."""
+        L = N.core_lib()
+        L.spl_store_restore.argtypes = [ctypes.c_void_p, ctypes.c_char_p]
+        L.spl_store_restore.restype = ctypes.c_int
+        if L.spl_store_restore(self._h, path.encode()) != 0:
+            _raise(f"restore {self.name} <- {path}")
+
+    def shard_state(self, shard: int) -> int:
+        """Node stores: 0 shard serves, 1 down (its rank's process is gone: ops on its keys raise
+        SplinterBusy / batch rows -EAGAIN until the rank re-joins), -1 no such shard."""
+        L = N.core_lib()
+        L.spl_node_shard_state.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.spl_node_shard_state.restype = ctypes.c_int
+        return int(L.spl_node_shard_state(self._h, shard))
+
+    # numpy view of spl_search_hit (splinter_ext.h): key[64], sim, dist, epoch, bloom, len, type, emb, pad[2]
+    _HIT_DTYPE = np.dtype([("key", "S64"), ("sim", "<f4"), ("dist", "<f4"), ("epoch", "<u8"), ("bloom", "<u8"),
+                           ("len", "<u4"), ("type", "u1"), ("emb", "u1"), ("pad", "u1", (2,))])
+
+    def search_batch(self, queries, k: int = 10, min_sim: float = -2.0, max_dist: float = 3.4e38,
+                     mask: int = 0) -> np.ndarray:
+        """Batched top-k (spl_search_batch, the C ABI product path): queries [nq, 768] fp32 (host)
+        -> structured hits [nq, k] (fields of spl_search_hit; ``emb`` 0 marks an unused entry).  An
+        hbm: store, or a node: store of HBM shards (all shards concurrently, merged per query)."""
+        q = np.ascontiguousarray(np.asarray(queries, dtype=np.float32).reshape(-1, 768))
+        out = np.zeros((q.shape[0], k), dtype=self._HIT_DTYPE)
+        L = N.hip_lib()
+        rc = L.spl_search_batch(self._h, q.ctypes.data, q.shape[0], k, float(min_sim), float(max_dist), mask,
+                                out.ctypes.data)
+        if rc != q.shape[0]:
+            _raise(f"search_batch {self.name}")
+        return out
+
+    def maint_seq(self) -> int:
+        """The arena's maintenance seq (odd while a rehash pass runs; spl_hbm_maint_seq)."""
+        L = N.hip_lib()
+        v = ctypes.c_uint64(0)
+        L.spl_hbm_maint_seq.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+        L.spl_hbm_maint_seq.restype = ctypes.c_int
+        if L.spl_hbm_maint_seq(self._h, ctypes.byref(v)) != 0:
+            _raise(f"maint_seq {self.name}")
+        return int(v.value)
 
     def __repr__(self):
         return (f"Store({self.name!r}, backend={self.backend}, slots={self.slots}, max_val={self.max_val}, "

@@ -49,6 +49,7 @@ def main():
             m = min(step, a.slots - b)
             lab = torch.randint(0, 4096, (m,), device="cuda", generator=g)
             em[b: b + m] = centers[lab] + 0.5 * torch.randn(m, 768, device="cuda", generator=g)
+        ar.rebuild_vec16()  # raw writes through the view bypass the vector writers: recompute the bf16 copy
         torch.cuda.synchronize()
 
         cfg = NomicConfig()

@@ -537,6 +537,60 @@ def test_kvs_step_modes_match_plain_kernels(uniq, kstride, mode):
         a.close()
 
 
+def test_kvs_async_server_reads_producer_kernel_output(uniq):
+    """Mode 3 (stream-posted server): every step's set keys / values and get keys are rewritten by
+    device kernels on the origin stream immediately before the step is posted -- no host
+    synchronisation in between -- into the SAME buffers each step, so a server CU that kept a stale
+    L1 copy of the previous step's rows (no acquire after the post) would store or fetch the
+    previous step's keys / data (verdict round 5, item 6: k_kv_server's agent acquire)."""
+    import torch
+    from libsplinter_amd.ops.arena import HbmArena, KvStreams, format_keys, format_values
+    a = HbmArena.create(uniq, slots=1 << 17, max_val=256, embeddings=False)
+    kvs = KvStreams(32, 32)
+    try:
+        kvs.set_fused(3)
+        n, ns, ng = 40000, 12000, 12000
+        ids = torch.arange(n, device="cuda")
+        V0, L0 = format_values(n, 1, 100, 256, ids=ids)
+        assert (a.set(format_keys(n, "p", 9, 16, ids=ids), V0, L0) == 0).all()
+        ver = np.ones(n, dtype=np.int64)
+        SK = torch.empty((ns, 16), dtype=torch.uint8, device="cuda")
+        SV = torch.empty((ns, 256), dtype=torch.uint8, device="cuda")
+        SL = torch.empty(ns, dtype=torch.int32, device="cuda")
+        GK = torch.empty((ng, 16), dtype=torch.uint8, device="cuda")
+        sst = torch.empty(ns, dtype=torch.int32, device="cuda")
+        gst = torch.empty(ng, dtype=torch.int32, device="cuda")
+        gout = torch.empty((ng, 256), dtype=torch.uint8, device="cuda")
+        glen = torch.empty(ng, dtype=torch.int32, device="cuda")
+        for step in range(8):
+            perm = torch.randperm(n, device="cuda")
+            sidx, gidx = perm[:ns], perm[ns:ns + ng]
+            SK.copy_(format_keys(ns, "p", 9, 16, ids=sidx))
+            v, ln = format_values(ns, step + 2, 60 + 10 * step, 256, ids=sidx)
+            SV.copy_(v)
+            SL.copy_(ln)
+            GK.copy_(format_keys(ng, "p", 9, 16, ids=gidx))
+            kvs.step(a, SK, SV, SL, sst, GK, gout, glen, gst)  # posted right behind the producers
+            torch.cuda.synchronize()
+            assert kvs.async_error() == 0
+            assert (sst == 0).all(), np.unique(sst.cpu().numpy(), return_counts=True)
+            assert (gst == 0).all(), np.unique(gst.cpu().numpy(), return_counts=True)
+            gh, o, lh = gidx.cpu().numpy(), gout.cpu().numpy(), glen.cpu().numpy()
+            for j in range(0, ng, 7):
+                val = bytes(o[j, : lh[j]])
+                assert val.startswith(b"ver:%d|id:" % ver[gh[j]]), (step, j, val[:24], ver[gh[j]])
+                assert int(val.split(b"|id:", 1)[1].split(b"|", 1)[0]) == gh[j]
+            ver[sidx.cpu().numpy()] = step + 2
+        st, out, ol = a.get(format_keys(n, "p", 9, 16, ids=ids))
+        assert (st == 0).all()
+        o, lh = out.cpu().numpy(), ol.cpu().numpy()
+        for i in range(0, n, 13):
+            assert bytes(o[i, : lh[i]]).startswith(b"ver:%d|id:%d|" % (ver[i], i))
+    finally:
+        kvs.close()
+        a.close()
+
+
 def test_kvs_async_server_steps(uniq):
     """Stream-posted server (mode 3) over 32 + 32 client streams for several steps in a row: slices
     of every size (empty ones included: fewer rows than streams x 128-row alignment) all run, each

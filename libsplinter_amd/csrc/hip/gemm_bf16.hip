@@ -909,11 +909,6 @@ __global__ __launch_bounds__(kThreads2, 1) void k_gemm256(const uint16_t* __rest
 
 }  // namespace
 
-// gemm_pt.hip: the persistent 256^2 kernel with a register epilogue (-1: shape / mode not taken)
-int spl_gemm_pt(int mode, const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int N, int K,
-                uint16_t* out, long ldo, const float* rope, const int32_t* pos, int rope_cols, int gn_cap,
-                hipStream_t s);
-
 namespace {
 
 int g_num_cus = 256;  // MI355X: 256 CUs in 8 XCDs; refreshed from the device on first use
@@ -925,14 +920,15 @@ void allow_lds(F* f, int bytes) {
 
 // Kernel choice (NOMIC_GEMM): 0 = auto, 128 = the 128^2 kernel, 256 = the 256^2 kernel.  The
 // persistent / stream-K 256^2 kernel (512-515), the DMA-interleave (ILV), ping-pong (PP), asm-DMA
-// 128^2 (AS128) and register-SwiGLU-epilogue knobs measured slower or equal and are gone; their A/B
-// history is in profiles/r1_gemm_*.jsonl .. r3_gemm_*.
+// 128^2 (AS128), register-SwiGLU-epilogue and persistent register-epilogue (300, gemm_pt.hip, round
+// 5) knobs measured slower or equal and are gone; their A/B history is in profiles/r1_gemm_*.jsonl
+// .. r3_gemm_*, r5/gemm_pt_ab_r5c.jsonl.
 int g_variant = -1;
 int gemm_variant() {
   if (g_variant < 0) {
     const char* e = getenv("NOMIC_GEMM");
     const int v = e ? atoi(e) : 0;
-    g_variant = v == 128 || v == 256 || v == 300 ? v : 0;
+    g_variant = v == 128 || v == 256 ? v : 0;
   }
   return g_variant;
 }
@@ -958,11 +954,6 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
   const long mpad = (M + 255) / 256 * 256;
   const bool fits = N % 256 == 0 && mpad * lda < (1L << 31) && (long)N * ldw < (1L << 31);
   const int var = gemm_variant();
-  // 300: the persistent kernel (gemm_pt.hip) where it takes the mode and shape
-  if (var == 300 && (MODE == NOMIC_EPI_STORE || MODE == NOMIC_EPI_SWIGLU || MODE == NOMIC_EPI_ROPE)) {
-    const int rc = spl_gemm_pt(MODE, A, lda, W, ldw, M, N, K, ep.out, ep.ldo, ep.rope, ep.pos, ep.rope_cols, 4, s);
-    if (rc >= 0) return rc;
-  }
   // the 256^2 kernel runs 1 block/CU with a serial prologue / epilogue per tile: it wins once there
   // are several waves of tiles.  From 1024 tiles: the qkv projection at 32768 tokens (1152 tiles)
   // measured 137.4 us on it against 144.5 us on the 128^2 kernel (round-3 trace); the SwiGLU GEMM
@@ -998,7 +989,7 @@ int launch(const uint16_t* A, long lda, const uint16_t* W, long ldw, long M, int
 
 extern "C" int nomic_gemm_set_variant(int variant) {
   const int prev = gemm_variant();
-  g_variant = variant == 128 || variant == 256 || variant == 300 ? variant : 0;
+  g_variant = variant == 128 || variant == 256 ? variant : 0;
   return prev;
 }
 

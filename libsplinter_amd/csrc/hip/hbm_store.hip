@@ -454,7 +454,11 @@ class HbmStore final : public StoreBase {
   // ---------------------------------------------------- bulk / helpers --
   int checkpoint(const char* path);
   long search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap, spl_search_hit* out);
-  long search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask, spl_search_hit* out);
+  long search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask, spl_search_hit* out,
+                   int sample_div = 1);
+  int device() const { return device_; }
+  struct SearchScratch;
+  SearchScratch* ss_ = nullptr;
   int restore_from(const char* path);
   int probe_stats(ProbeStats* out);
   int rehash(uint64_t out[4], unsigned flags = 0);
@@ -714,6 +718,30 @@ static hipStream_t control_stream(int device) {
   return s[device];
 }
 
+// Search scratch of a store (grown, kept across calls: no allocation per call).
+struct HbmStore::SearchScratch {
+  float* q = nullptr;        // [256][768] fp32 queries
+  void* res = nullptr;       // [256][32] CandRec
+  void* scr = nullptr;       // exact kernel's lists
+  uint16_t* qf = nullptr;    // [256][768] bf16 fragment operand
+  float* thr = nullptr;      // [256]
+  float* bmax = nullptr;     // [sample tiles][256] (also the overflow flags)
+  size_t bmax_bytes = 0;
+  uint32_t* cnt = nullptr;   // [256][grid]
+  uint32_t* cand = nullptr;  // [256][grid][capb]
+  void* cores = nullptr;     // [256][32][128] slot cores of the results
+  hipEvent_t ev = nullptr;   // stream_ -> search stream ordering
+  // pinned host staging (queries up, results / cores / overflow flags down): pageable copies go
+  // through the runtime's staging buffer, which the shards of a node search would share
+  uint8_t* hp = nullptr;
+  float* hq() const { return (float*)hp; }
+  void* hres() const { return hp + kHq; }
+  uint8_t* hcores() const { return hp + kHq + kHres; }
+  uint32_t* hover() const { return (uint32_t*)(hp + kHq + kHres + kHcores); }
+  static constexpr size_t kHq = 256 * (size_t)kEmbedBytes, kHres = 256 * 32 * 16, kHcores = 256 * 32 * 128,
+                          kHover = 256 * 4, kHbytes = kHq + kHres + kHcores + kHover;
+};
+
 int HbmStore::setup_buffers() {
   stream_ = control_stream(device_);
   if (!stream_) return -1;
@@ -927,6 +955,15 @@ HbmStore::~HbmStore() {
   ring_.reset();  // the worker (and a ring server's supervisor) reads the arena: gone before it
   if (stream_) (void)hipStreamSynchronize(stream_);
   if (h_u32_) (void)hipHostFree(h_u32_);
+  if (ss_) {
+    for (void* p : {(void*)ss_->q, ss_->res, ss_->scr, (void*)ss_->qf, (void*)ss_->thr, (void*)ss_->bmax,
+                    (void*)ss_->cnt, (void*)ss_->cand, ss_->cores})
+      if (p) (void)hipFree(p);
+    if (ss_->ev) (void)hipEventDestroy(ss_->ev);
+    if (ss_->hp) (void)hipHostFree(ss_->hp);
+    delete ss_;
+    ss_ = nullptr;
+  }
   if (d_scan_idx_) (void)hipFree(d_scan_idx_);
   if (d_scan_ep_) (void)hipFree(d_scan_ep_);
   if (d_scan_cnt_) (void)hipFree(d_scan_cnt_);
@@ -1027,45 +1064,80 @@ struct CandRec {
 };
 }  // namespace
 
+
+// Searches of shards that share a device run on their own streams (slot > 0: node fan-out), so
+// they overlap; slot 0 is the device's control stream (a lone store adds no hardware queue).
+static hipStream_t search_stream(int device, int slot) {
+  if (slot <= 0) return control_stream(device);
+  static std::mutex mu;
+  static hipStream_t s[64][4] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (device < 0 || device >= 64) device = 0;
+  slot = (slot - 1) & 3;
+  if (!s[device][slot]) (void)hipStreamCreateWithFlags(&s[device][slot], hipStreamNonBlocking);
+  return s[device][slot];
+}
+thread_local int g_search_slot = 0;
+
 long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask,
-                            spl_search_hit* out) {
+                            spl_search_hit* out, int sample_div) {
   if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
   if (nq <= 0 || k <= 0 || k > 32 || !q || !out) { errno = EINVAL; return -1; }
   if (!ensure_mapped()) return -1;
   DevGuard dg(device_);
-  std::unique_lock<std::mutex> lk(mu_);  // released before fetch_cores, which takes it itself
+  std::unique_lock<std::mutex> lk(mu_);
   const spl_arena_t a = arena();
   const long slots = geo_.slots;
+  hipStream_t ss = search_stream(device_, g_search_slot);
   std::vector<CandRec> res((size_t)nq * k);
+  std::vector<uint8_t> cores((size_t)nq * k * 128);
   const bool bounded = max_dist < 3.0e38f;
   const bool mma = nq >= 32 && slots >= kMmaTile;
-  long sample = std::min<long>(slots, std::max<long>((long)kMmaTile * 4096, slots / 16));
+  // the threshold sample: a node's shards split one store's sample between them
+  const int div = sample_div > 1 ? sample_div : 1;
+  long sample = std::min<long>(slots, std::max<long>((long)kMmaTile * 4096 / div, slots / 16));
   sample = std::max<long>(kMmaTile, sample / kMmaTile * kMmaTile);
-  // device buffers (stream-ordered)
-  float *d_q = nullptr, *d_thr = nullptr, *d_bmax = nullptr;
-  uint16_t* d_qf = nullptr;
-  uint32_t *d_cnt = nullptr, *d_cand = nullptr;
-  void *d_res = nullptr, *d_scr = nullptr;
+  // scratch (kept across calls; the stream-ordered allocations happen once per store)
+  if (!ss_) ss_ = new SearchScratch();
+  SearchScratch& S = *ss_;
   const int lists = spl_search_lists(kExactGrid);
-  bool ok = hipMallocAsync((void**)&d_q, (size_t)kMmaQ * kEmbedBytes, stream_) == hipSuccess &&
-            hipMallocAsync(&d_res, (size_t)kMmaQ * 32 * sizeof(CandRec), stream_) == hipSuccess &&
-            hipMallocAsync(&d_scr, (size_t)lists * kExactQ * 32 * sizeof(CandRec), stream_) == hipSuccess;
-  if (ok && mma)
-    ok = hipMallocAsync((void**)&d_qf, (size_t)kMmaQ * kEmbedDim * 2, stream_) == hipSuccess &&
-         hipMallocAsync((void**)&d_thr, (size_t)kMmaQ * 4, stream_) == hipSuccess &&
-         hipMallocAsync((void**)&d_bmax, (size_t)std::max<long>(sample / kMmaTile, 1) * kMmaQ * 4, stream_) == hipSuccess &&
-         hipMallocAsync((void**)&d_cnt, (size_t)kMmaQ * kMmaGrid * 4, stream_) == hipSuccess &&
-         hipMallocAsync((void**)&d_cand, (size_t)kMmaQ * kMmaGrid * kCapb * 4, stream_) == hipSuccess;
-  auto exact = [&](const float* hq, int n, CandRec* dst) -> bool {  // nq <= kExactQ per launch
+  bool ok = true;
+  if (!S.q) {
+    ok = hipMallocAsync((void**)&S.q, (size_t)kMmaQ * kEmbedBytes, ss) == hipSuccess &&
+         hipMallocAsync(&S.res, (size_t)kMmaQ * 32 * sizeof(CandRec), ss) == hipSuccess &&
+         hipMallocAsync(&S.scr, (size_t)lists * kExactQ * 32 * sizeof(CandRec), ss) == hipSuccess &&
+         hipMallocAsync((void**)&S.qf, (size_t)kMmaQ * kEmbedDim * 2, ss) == hipSuccess &&
+         hipMallocAsync((void**)&S.thr, (size_t)kMmaQ * 4, ss) == hipSuccess &&
+         hipMallocAsync((void**)&S.cnt, (size_t)kMmaQ * kMmaGrid * 4, ss) == hipSuccess &&
+         hipMallocAsync((void**)&S.cand, (size_t)kMmaQ * kMmaGrid * kCapb * 4, ss) == hipSuccess &&
+         hipMallocAsync(&S.cores, (size_t)kMmaQ * 32 * 128, ss) == hipSuccess &&
+         hipEventCreateWithFlags(&S.ev, hipEventDisableTiming) == hipSuccess &&
+         hipHostMalloc((void**)&S.hp, SearchScratch::kHbytes) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
+  }
+  const size_t bmax_need = (size_t)std::max<long>(sample / kMmaTile, 1) * kMmaQ * 4;
+  if (ok && S.bmax_bytes < bmax_need) {
+    if (S.bmax) (void)hipFreeAsync(S.bmax, ss);
+    S.bmax = nullptr;
+    ok = hipMallocAsync((void**)&S.bmax, bmax_need, ss) == hipSuccess;
+    S.bmax_bytes = ok ? bmax_need : 0;
+  }
+  // everything written to the arena through this store's stream is visible to the search stream
+  ok = ok && hipEventRecord(S.ev, stream_) == hipSuccess && hipStreamWaitEvent(ss, S.ev, 0) == hipSuccess;
+  static_assert(sizeof(CandRec) == 16, "pinned result staging assumes 16-B records");
+  auto exact = [&](const float* hq, int n, CandRec* dst, uint8_t* cdst) -> bool {  // nq <= kExactQ per launch
     for (int b = 0; b < n; b += kExactQ) {
       const int m = std::min(kExactQ, n - b);
-      if (hipMemcpyAsync(d_q, hq + (size_t)b * kEmbedDim, (size_t)m * kEmbedBytes, hipMemcpyHostToDevice, stream_) !=
-              hipSuccess ||
-          spl_search(a, d_q, m, k, min_sim, max_dist, mask, kExactGrid, d_scr, d_res, stream_) != 0 ||
-          hipMemcpyAsync(dst + (size_t)b * k, d_res, (size_t)m * k * sizeof(CandRec), hipMemcpyDeviceToHost,
-                         stream_) != hipSuccess ||
-          hipStreamSynchronize(stream_) != hipSuccess)
+      std::memcpy(S.hq(), hq + (size_t)b * kEmbedDim, (size_t)m * kEmbedBytes);
+      if (hipMemcpyAsync(S.q, S.hq(), (size_t)m * kEmbedBytes, hipMemcpyHostToDevice, ss) != hipSuccess ||
+          spl_search(a, S.q, m, k, min_sim, max_dist, mask, kExactGrid, S.scr, S.res, ss) != 0 ||
+          spl_search_cores(a, S.res, m * k, S.cores, ss) != 0 ||
+          hipMemcpyAsync(S.hres(), S.res, (size_t)m * k * sizeof(CandRec), hipMemcpyDeviceToHost, ss) != hipSuccess ||
+          hipMemcpyAsync(S.hcores(), S.cores, (size_t)m * k * 128, hipMemcpyDeviceToHost, ss) != hipSuccess ||
+          hipStreamSynchronize(ss) != hipSuccess)
         return false;
+      std::memcpy(dst + (size_t)b * k, S.hres(), (size_t)m * k * sizeof(CandRec));
+      std::memcpy(cdst + (size_t)b * k * 128, S.hcores(), (size_t)m * k * 128);
     }
     return true;
   };
@@ -1079,33 +1151,39 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
     const int n = std::min(kMmaQ, nq - b);
     const float* hq = q + (size_t)b * kEmbedDim;
     if (exact_only) {
-      ok = exact(hq, n, res.data() + (size_t)b * k);
+      ok = exact(hq, n, res.data() + (size_t)b * k, cores.data() + (size_t)b * k * 128);
       continue;
     }
     // queries up once (fp32); the bf16 fragment operand is built on the device (spl_search_qprep)
     const float floor_v = min_sim - kDelta;
-    ok = hipMemcpyAsync(d_q, hq, (size_t)n * kEmbedBytes, hipMemcpyHostToDevice, stream_) == hipSuccess &&
-         spl_search_qprep(d_q, n, d_qf, stream_) == 0;
+    std::memcpy(S.hq(), hq, (size_t)n * kEmbedBytes);
+    ok = hipMemcpyAsync(S.q, S.hq(), (size_t)n * kEmbedBytes, hipMemcpyHostToDevice, ss) == hipSuccess &&
+         spl_search_qprep(S.q, n, S.qf, ss) == 0;
     if (ok && !bounded) {
-      ok = spl_search_mma_pass(a, d_qf, n, 0, sample, mask, 0, nullptr, d_bmax, nullptr, nullptr, 0, kMmaGrid,
-                               stream_) == 0 &&
-           spl_search_thr(d_bmax, (int)(sample / kMmaTile), n, k, 2 * kDelta, floor_v, d_thr, stream_) == 0;
+      ok = spl_search_mma_pass(a, S.qf, n, 0, sample, mask, 0, nullptr, S.bmax, nullptr, nullptr, 0, kMmaGrid, ss) ==
+               0 &&
+           spl_search_thr(S.bmax, (int)(sample / kMmaTile), n, k, 2 * kDelta, floor_v, S.thr, ss) == 0;
     } else if (ok) {
       thr_h.assign((size_t)n, floor_v);
-      ok = hipMemcpyAsync(d_thr, thr_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, stream_) == hipSuccess;
+      ok = hipMemcpyAsync(S.thr, thr_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, ss) == hipSuccess;
     }
-    // (the overflow flags reuse d_bmax: the threshold is built by then)
-    ok = ok && hipMemsetAsync(d_cnt, 0, (size_t)n * kMmaGrid * 4, stream_) == hipSuccess &&
-         spl_search_mma_pass(a, d_qf, n, 0, slots, mask, 1, d_thr, nullptr, d_cnt, d_cand, kCapb, kMmaGrid,
-                             stream_) == 0 &&
-         spl_search_rescore(a, d_q, n, k, min_sim, max_dist, mask, d_cnt, d_cand, kMmaGrid, kCapb, d_res, stream_) ==
-             0 &&
-         spl_search_overflow(d_cnt, n, kMmaGrid, kCapb, (uint32_t*)d_bmax, stream_) == 0;
+    // (the overflow flags reuse S.bmax: the threshold is built by then)
+    ok = ok && hipMemsetAsync(S.cnt, 0, (size_t)n * kMmaGrid * 4, ss) == hipSuccess &&
+         spl_search_mma_pass(a, S.qf, n, 0, slots, mask, 1, S.thr, nullptr, S.cnt, S.cand, kCapb, kMmaGrid, ss) == 0 &&
+         spl_search_rescore(a, S.q, n, k, min_sim, max_dist, mask, S.cnt, S.cand, kMmaGrid, kCapb, S.res, ss) == 0 &&
+         spl_search_overflow(S.cnt, n, kMmaGrid, kCapb, (uint32_t*)S.bmax, ss) == 0 &&
+         spl_search_cores(a, S.res, n * k, S.cores, ss) == 0;
     over.resize((size_t)n);
-    ok = ok && hipMemcpyAsync(res.data() + (size_t)b * k, d_res, (size_t)n * k * sizeof(CandRec),
-                              hipMemcpyDeviceToHost, stream_) == hipSuccess &&
-         hipMemcpyAsync(over.data(), d_bmax, (size_t)n * 4, hipMemcpyDeviceToHost, stream_) == hipSuccess &&
-         hipStreamSynchronize(stream_) == hipSuccess;
+    ok = ok &&
+         hipMemcpyAsync(S.hres(), S.res, (size_t)n * k * sizeof(CandRec), hipMemcpyDeviceToHost, ss) == hipSuccess &&
+         hipMemcpyAsync(S.hcores(), S.cores, (size_t)n * k * 128, hipMemcpyDeviceToHost, ss) == hipSuccess &&
+         hipMemcpyAsync(S.hover(), S.bmax, (size_t)n * 4, hipMemcpyDeviceToHost, ss) == hipSuccess &&
+         hipStreamSynchronize(ss) == hipSuccess;
+    if (ok) {
+      std::memcpy(res.data() + (size_t)b * k, S.hres(), (size_t)n * k * sizeof(CandRec));
+      std::memcpy(cores.data() + (size_t)b * k * 128, S.hcores(), (size_t)n * k * 128);
+      std::memcpy(over.data(), S.hover(), (size_t)n * 4);
+    }
     // overflowed queries: the exact kernel, kExactQ of them per launch
     std::vector<int> oi;
     for (int i = 0; ok && i < n; ++i)
@@ -1115,23 +1193,16 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
       for (size_t j = 0; j < oi.size(); ++j)
         std::memcpy(&redo[j * kEmbedDim], hq + (size_t)oi[j] * kEmbedDim, kEmbedBytes);
       std::vector<CandRec> rr(oi.size() * (size_t)k);
-      ok = exact(redo.data(), (int)oi.size(), rr.data());
-      for (size_t j = 0; ok && j < oi.size(); ++j)
+      std::vector<uint8_t> rc(oi.size() * (size_t)k * 128);
+      ok = exact(redo.data(), (int)oi.size(), rr.data(), rc.data());
+      for (size_t j = 0; ok && j < oi.size(); ++j) {
         std::memcpy(&res[(size_t)(b + oi[j]) * k], &rr[j * k], (size_t)k * sizeof(CandRec));
+        std::memcpy(&cores[(size_t)(b + oi[j]) * k * 128], &rc[j * k * 128], (size_t)k * 128);
+      }
     }
   }
-  for (void* p : {(void*)d_q, (void*)d_thr, (void*)d_bmax, (void*)d_qf, (void*)d_cnt, (void*)d_cand, d_res, d_scr})
-    if (p) (void)hipFreeAsync(p, stream_);
-  (void)hipStreamSynchronize(stream_);
   lk.unlock();
   if (!ok) { errno = EIO; return -1; }
-  // slot indices -> keys and slot metadata (one gather of the slot cores)
-  std::vector<uint32_t> idx;
-  idx.reserve(res.size());
-  for (const CandRec& c : res)
-    if (c.idx != 0xffffffffu) idx.push_back(c.idx);
-  fetch_cores(idx);
-  size_t p = 0;
   for (size_t i = 0; i < res.size(); ++i) {
     spl_search_hit& h = out[i];
     std::memset(&h, 0, sizeof h);
@@ -1139,7 +1210,7 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
       h.sim = -3.4e38f;
       continue;
     }
-    const uint8_t* core = list_cache_.data() + (p++) * 128;
+    const uint8_t* core = cores.data() + i * 128;
     std::memcpy(h.key, core + kOffKey, 64);
     h.key[63] = 0;
     h.emb = 1;
@@ -1705,10 +1776,21 @@ long spl_search_batch(spl_store* h, const float* queries, int nq, int k, float m
   {
     std::vector<std::thread> th;
     th.reserve((size_t)n);
+    // shards on one device search on streams of their own (spl::search_stream), and split the
+    // threshold sample of one store between them
+    std::vector<int> slot((size_t)n, 0);
+    for (int i = 0; i < n; ++i) {
+      auto* si = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
+      for (int j = 0; si && j < i; ++j) {
+        auto* sj = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, j));
+        if (sj && sj->device() == si->device()) ++slot[(size_t)i];
+      }
+    }
     for (int i = 0; i < n; ++i)
       th.emplace_back([&, i] {
+        spl::g_search_slot = slot[(size_t)i];
         auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
-        rc[(size_t)i] = s ? s->search_batch(queries, nq, k, min_sim, max_dist, mask, part[(size_t)i].data()) : -1;
+        rc[(size_t)i] = s ? s->search_batch(queries, nq, k, min_sim, max_dist, mask, part[(size_t)i].data(), n) : -1;
       });
     for (auto& t : th) t.join();
   }

@@ -885,6 +885,23 @@ __global__ __launch_bounds__(256) void k_search_qprep(const float* __restrict__ 
   }
 }
 
+// slot cores (128 B) of a result list, gathered on the device so the hits leave with their keys
+// in the same copy: res[n] Cand -> out[n][128] (zeros for an empty entry).  8 lanes per entry.
+__global__ __launch_bounds__(256) void k_search_cores(spl_arena_t aa, const Cand* __restrict__ res, int n,
+                                                      uint4* __restrict__ out) {
+  const int i = blockIdx.x * 32 + (threadIdx.x >> 3), c = threadIdx.x & 7;
+  if (i >= n) return;
+  const uint32_t idx = res[i].idx;
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (idx < aa.slots) {
+    const uint8_t* s = (const uint8_t*)aa.base + spl::kHeaderBytes + (size_t)idx * aa.stride + 16 * c;
+    const uint64_t a = __hip_atomic_load((const uint64_t*)s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t b = __hip_atomic_load((const uint64_t*)(s + 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    v = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
+  }
+  out[(size_t)i * 8 + c] = v;
+}
+
 // over[q] = 1 when query q's candidate segment overflowed in any block (cnt[q][g] > capb)
 __global__ __launch_bounds__(256) void k_search_over(const uint32_t* __restrict__ cnt, int nblk, int capb,
                                                      uint32_t* __restrict__ over) {
@@ -913,6 +930,13 @@ int spl_search_lists(int grid) { return grid * kWaves; }
 int spl_search_qprep(const float* queries, int nq, void* qfrag, hipStream_t s) {
   if (nq <= 0 || nq > mf::kQ || !queries || !qfrag) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(k_search_qprep, dim3(mf::kQ), dim3(256), 0, s, queries, nq, (uint16_t*)qfrag);
+  return (int)hipGetLastError();
+}
+
+int spl_search_cores(spl_arena_t a, const void* result, int n, void* out_cores, hipStream_t s) {
+  if (n <= 0 || !result || !out_cores) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_search_cores, dim3((unsigned)((n + 31) / 32)), dim3(256), 0, s, a, (const Cand*)result, n,
+                     (uint4*)out_cores);
   return (int)hipGetLastError();
 }
 

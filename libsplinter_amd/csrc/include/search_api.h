@@ -32,6 +32,8 @@ int spl_search_mma_pass(spl_arena_t a, const void *qfrag, int nq, long slot_begi
 /* queries [nq <= 256, 768] fp32 (device) -> qfrag as spl_search_mma_pass takes it (normalised,
  * bf16, zero-padded to 256 queries, fragment order) */
 int spl_search_qprep(const float *queries, int nq, void *qfrag, hipStream_t stream);
+/* slot cores (128 B each) of n result entries (spl_search result layout) -> out_cores[n][128] */
+int spl_search_cores(spl_arena_t a, const void *result, int n, void *out_cores, hipStream_t stream);
 /* over[q] = 1 when cnt[q][0..nblk) has a segment count > capb (the query must be redone exactly) */
 int spl_search_overflow(const uint32_t *cnt, int nq, int nblk, int capb, uint32_t *over, hipStream_t stream);
 /* per-query candidate threshold from a bmax pass: max(k-th largest of bmax[tiles][nq] - delta2, floor) */

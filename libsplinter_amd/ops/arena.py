@@ -86,7 +86,7 @@ class KvStreams:
     """A group of concurrent client streams issuing one KV step natively (spl_kvs_*, hip/arena_kernels.hip):
     ``writers`` streams share the set batch, ``readers`` the get batch; the current torch stream
     continues after all of them.  Submission modes (``set_fused``; SPL_KVS_FUSED sets the default):
-    0 each slice its own launch on its own stream, 1 / 2 every slice in one fused grid on the
+    0 each slice its own launch on its own stream, 2 every slice in one fused grid on the
     current stream, 3 each client stream posts its slice with a stream-ordered doorbell write and one
     resident server grid consumes the slices as they are posted (16-B keys, <= 64 streams)."""
 
@@ -98,8 +98,8 @@ class KvStreams:
         self.writers, self.readers = writers, readers
 
     def set_fused(self, mode: int):
-        """0: one launch per stream slice; 1 / 2 (default): every slice in one fused grid; 3: stream-posted
-        slices consumed by a resident server grid."""
+        """0: one launch per stream slice; 2 (default; 1 is taken as 2): every slice in one fused grid; 3:
+        stream-posted slices consumed by a resident server grid."""
         _check(self._H.spl_kvs_set_fused(self.h, int(mode)), "kvs_set_fused")
 
     def async_error(self) -> int:

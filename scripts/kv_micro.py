@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Micro-benchmark of the HBM arena kernels: set-only, get-only and concurrent
-set||get batches on a prepopulated arena.  SPLINTER_ARENA_MO selects the
-payload memory-ordering discipline (see csrc/hip/arena_dev.hpp)."""
+set||get batches on a prepopulated arena."""
 import argparse
 import json
 import os
@@ -67,7 +66,7 @@ def main():
         cur.wait_stream(s1)
         cur.wait_stream(s2)
 
-    res = {"mo": int(os.environ.get("SPLINTER_ARENA_MO", "0")), "keys": args.keys, "batch": args.batch,
+    res = {"keys": args.keys, "batch": args.batch,
            "fill_s": round(fill, 3)}
     for name, fn in [("set", lambda: a.set(K, V, L)), ("get", lambda: a.get(K, out=out)), ("set||get", both)]:
         mn, med = timeit(fn)

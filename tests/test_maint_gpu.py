@@ -183,7 +183,7 @@ def test_rehash_online_beside_live_kv_steps(uniq, emb):
     import threading
     import torch
     from libsplinter_amd.ops.arena import HbmArena, KvStreams, format_values
-    slots = 1 << 20 if not emb else 1 << 15
+    slots = 1 << 22 if not emb else 1 << 17
     ar = HbmArena.create(f"{uniq}", slots=slots, max_val=64, embeddings=emb)
     kv = KvStreams(4, 4)
     try:
@@ -199,18 +199,28 @@ def test_rehash_online_beside_live_kv_steps(uniq, emb):
         ver = np.ones(live.size, dtype=np.int64)
         res, err = [], []
 
+        passes = 6
+
         def worker():
             try:
-                for _ in range(3):
+                for _ in range(passes):
                     res.append(ar.store.rehash())
             except Exception as e:  # noqa: BLE001
                 err.append(e)
 
+        from libsplinter_amd.ops.arena import _device_view
+        seqv = _device_view(ar._side_base() + 256, 8, dtype=torch.int64)  # MaintRec::seq
+        seqs = []
+
         n_set = n_get = min(16384, live.size // 8)
         steps, false_miss, live_again, dead_seen = 0, 0, 0, {}
         t = threading.Thread(target=worker)
-        t.start()
-        while (t.is_alive() or steps < 8) and steps < 2000:
+        # a few steps queued first, so the passes open beside KV work already on the GPU
+        t_started = False
+        while (not t_started or t.is_alive() or steps < 8) and steps < 4000:
+            if not t_started and steps >= 4:
+                t.start()
+                t_started = True
             batch = []
             for _ in range(4):  # queued back to back: the GPU runs them beside the pass's kernels
                 pick = rng.choice(live.size, size=n_set + n_get, replace=False)
@@ -222,6 +232,7 @@ def test_rehash_online_beside_live_kv_steps(uniq, emb):
                 gl = torch.empty(gk.shape[0], dtype=torch.int32, device="cuda")
                 gst = torch.empty(gk.shape[0], dtype=torch.int32, device="cuda")
                 kv.step(ar, _keys(live[si]), V, Lv, sst, gk, go, gl, gst)
+                seqs.append(seqv.clone())  # the seq as the stream passes this step: odd = a pass was running
                 batch.append((si, gi, sst, go, gl, gst, ver[gi].copy()))
                 ver[si] = steps + 2
                 steps += 1
@@ -241,16 +252,19 @@ def test_rehash_online_beside_live_kv_steps(uniq, emb):
                         assert v.startswith(b"ver:%d|id:%d|" % (gv[i], live[gi[i]])), (v[:20], gv[i], live[gi[i]])
         t.join()
         assert not err, err
-        assert len(res) == 3
+        assert len(res) == passes
+        overlapped = int(sum(int(x.item()) & 1 for x in seqs))
         st2 = ar.store.probe_stats()
-        print(dict(emb=emb, steps=steps, rehash=res, dead_status=dead_seen, live_again=live_again,
+        print(dict(emb=emb, steps=steps, overlapped_steps=overlapped, rehash=res, dead_status=dead_seen,
+                   live_again=live_again,
                    before=(st1["miss_mean"], st1["tombstones"]), after=(st2["miss_mean"], st2["tombstones"])))
         assert false_miss == 0 and live_again == 0, (false_miss, live_again)
         assert set(dead_seen) <= {-2, -11}
         assert st2["live"] == live.size and st2["busy"] == 0
         assert st2["tombstones"] < st1["tombstones"]
         assert st2["miss_mean"] < st1["miss_mean"] or st1["virgin"] == 0
-        assert ar.store.maint_seq() == 6
+        assert ar.store.maint_seq() == 2 * passes
+        assert overlapped > 0  # KV steps really ran while a pass was open
         _check_values(ar, live, ver)
         _no_duplicates(ar, live.size)
         sd, _, _ = ar.get(_keys(dead))

@@ -114,6 +114,10 @@ def parse():
                         "per step in all) -> exchange_2rank_ops_per_s / exchange_1rank_ops_per_s / exchange_ratio")
     p.add_argument("--exchange-keys", type=int, default=40_000_000, help="total keys of the exchange A/B runs")
     p.add_argument("--exchange-batch", type=int, default=8_000_000, help="total ops per step of the exchange A/B runs")
+    p.add_argument("--kv-async-ab", type=int, default=1, choices=[0, 1],
+                   help="N=1: config #2's literal form in the record -- KV-only steps with the 32 writer + 32 "
+                        "reader client streams each posting its own slice to the resident server grid "
+                        "(SPL_KVS_FUSED=3), beside the fused grid, both in fresh child processes")
     p.add_argument("--mixed5", type=int, default=10, metavar="STEPS",
                    help="after the timed loop, time STEPS config-#5 mixed steps (embed a batch -> its vectors "
                         "inserted into the search arena's slots -> a batched top-10 query of --search-queries "
@@ -261,6 +265,49 @@ def exchange_ab(args, dev: int, log):
             "integrity": runs[2]["integrity_failures"] + runs[1]["integrity_failures"],
             "totals": {"keys": args.exchange_keys, "ops_per_step": args.exchange_batch, "steps": 10,
                        "device": phys, "mode": "kv"}}
+
+
+def kv_async_ab(args, dev: int, log):
+    """Config #2 as written -- 32 concurrent writer + 32 reader client streams, each submitting its own
+    slice -- against the default fused grid: two KV-only children at the bench's keys and batch (fresh
+    processes, never exec), SPL_KVS_FUSED=3 (each stream posts its slice with a stream-ordered doorbell;
+    the resident k_kv_server grid consumes posted slices) and SPL_KVS_FUSED=2.  Returns both rates,
+    their ratio and both runs' integrity failures."""
+    import subprocess
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    vis = env.get("HIP_VISIBLE_DEVICES") or env.get("CUDA_VISIBLE_DEVICES")
+    env["HIP_VISIBLE_DEVICES"] = vis.split(",")[dev] if vis else str(dev)
+    env.pop("CUDA_VISIBLE_DEVICES", None)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    cmd = [sys.executable, os.path.abspath(__file__), "--gpus", "1", "--mode", "kv", "--steps", "10", "--warmup", "3",
+           "--keys-per-gpu", str(args.keys_per_gpu), "--batch", str(args.batch), "--value-len", str(args.value_len),
+           "--writer-streams", str(args.writer_streams), "--reader-streams", str(args.reader_streams),
+           "--host-api", "0", "--host-api-threads2", "0", "--embed-e2e", "0", "--daemon-docs", "0",
+           "--search-keys", "0", "--exchange-ab", "0", "--kv-async-ab", "0", "--mixed5", "0", "--verify", "5000"]
+    runs = {}
+    for mode in ("3", "2"):
+        e = dict(env, SPL_KVS_FUSED=mode)
+        try:
+            r = subprocess.run(cmd, env=e, capture_output=True, text=True, timeout=600)
+        except subprocess.TimeoutExpired:
+            log(f"[bench] kv async A/B: SPL_KVS_FUSED={mode} child timed out")
+            return None
+        line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+        if r.returncode != 0 or not line:
+            log(f"[bench] kv async A/B: SPL_KVS_FUSED={mode} child failed (rc {r.returncode}): {r.stderr[-600:]}")
+            return None
+        runs[mode] = json.loads(line[-1])
+        log(f"[bench] kv async A/B: SPL_KVS_FUSED={mode} {runs[mode]['value'] / 1e9:.3f} G ops/s, "
+            f"{runs[mode]['ms_per_step']:.2f} ms/step, {runs[mode]['config']['kv_submission']}, "
+            f"integrity {runs[mode]['integrity_failures']}")
+    a, f = runs["3"], runs["2"]
+    return {"async": a["value"], "fused": f["value"], "ratio": a["value"] / f["value"],
+            "async_ms": a["ms_per_step"], "fused_ms": f["ms_per_step"],
+            "submission": a["config"]["kv_submission"], "writer_streams": a["config"]["writer_streams"],
+            "reader_streams": a["config"]["reader_streams"],
+            "integrity": a["integrity_failures"] + f["integrity_failures"]}
 
 
 def main():
@@ -832,6 +879,9 @@ def main():
     xab = None
     if world == 1 and args.exchange_ab and args.mode != "embed":
         xab = exchange_ab(args, dev, log)
+    kab = None
+    if world == 1 and args.kv_async_ab and args.mode != "embed":
+        kab = kv_async_ab(args, dev, log)
 
     kv_ops = (n_set + n_get) * args.steps * world
     kv_ops_s = kv_ops / elapsed if kv_ops else 0.0
@@ -918,6 +968,14 @@ def main():
         "exchange_sync": xab["sync"] if xab else None, "exchange_sync_error": xab["sync_error"] if xab else None,
         "xr_sync_error": (xr.sync_error() if (routed and xr is not None) else None),
         "exchange_integrity_failures": xab["integrity"] if xab else None,
+        # config #2 literally: every one of the client streams submits its own slice (SPL_KVS_FUSED=3)
+        "kv_async_ops_per_s": kab["async"] if kab else None,
+        "kv_fused_only_ops_per_s": kab["fused"] if kab else None,
+        "kv_async_ratio": kab["ratio"] if kab else None,
+        "kv_async_ms_per_step": kab["async_ms"] if kab else None,
+        "kv_async_submission": kab["submission"] if kab else None,
+        "kv_async_streams": {"writer": kab["writer_streams"], "reader": kab["reader_streams"]} if kab else None,
+        "kv_async_integrity_failures": kab["integrity"] if kab else None,
         "exchange_totals": xab["totals"] if xab else None,
         "mixed5_ms_per_step": mixed5["ms_per_step"] if mixed5 else None,
         "mixed5_qps": mixed5["qps"] if mixed5 else None,

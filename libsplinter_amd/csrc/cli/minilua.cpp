@@ -392,6 +392,7 @@ struct Stat {
   std::vector<std::shared_ptr<Block>> blocks;
   std::shared_ptr<Block> els;
   std::shared_ptr<FuncBody> fn;
+  std::vector<int> attribs;  // S_LOCAL: per name 0, 1 <const>, 2 <close>
   int line = 0;
 };
 
@@ -578,8 +579,21 @@ struct Parser {
         s->k = S_LOCAL;
         do {
           s->names.push_back(name());
-          if (accept('<')) { name(); expect('>'); }  // <const>/<close> attribs: accepted, ignored
+          int at = 0;
+          if (accept('<')) {
+            const std::string a = name();
+            if (a == "const") at = 1;
+            else if (a == "close") at = 2;
+            else err("unknown attribute '" + a + "'");
+            expect('>');
+          }
+          s->attribs.push_back(at);
         } while (accept(','));
+        {
+          int closes = 0;
+          for (int a : s->attribs) closes += a == 2;
+          if (closes > 1) err("multiple to-be-closed variables in local list");
+        }
         if (accept('=')) s->exprs = exprlist();
         return s;
       case T_BREAK:
@@ -828,6 +842,7 @@ struct Scope {
   Values varargs;
   bool has_varargs = false;
   Heap* heap;
+  std::vector<Value> tbc;  // to-be-closed values of this block (`local x <close>`), in declaration order
 };
 
 struct Heap {
@@ -869,7 +884,17 @@ struct Exec {
     }
     return f;
   }
-  explicit Exec(Interp& in) : I(in) {}
+  explicit Exec(Interp& in) : I(in) { I.scope_stacks.push_back(&live); }
+  ~Exec() {
+    auto& v = I.scope_stacks;
+    for (size_t i = v.size(); i-- > 0;)
+      if (v[i] == &live) {
+        v.erase(v.begin() + (long)i);
+        break;
+      }
+  }
+  Exec(const Exec&) = delete;
+  Exec& operator=(const Exec&) = delete;
 
   std::shared_ptr<Value> lookup(Scope* s, const std::string& n) {
     for (; s; s = s->parent.get()) {
@@ -1125,6 +1150,14 @@ struct Exec {
       }
       case E_NAME: {
         if (auto c = lookup(s, e->name)) return *c;
+        if (I.env_used) {
+          if (auto env = lookup(s, "_ENV")) {
+            if (env->t != Value::Tab && env->t != Value::Str)
+              rt(e.get(), std::string("attempt to index a ") + type_name(*env) + " value (upvalue '_ENV')");
+            return I.index(*env, Value::string(e->name));
+          }
+          if (e->name == "_ENV") return Value::table(I.globals);
+        }
         return I.globals->get(Value::string(e->name));
       }
       case E_INDEX: return index(eval(e->a, s), eval(e->b, s), e.get());
@@ -1155,8 +1188,18 @@ struct Exec {
 
   void assign(const ExprP& t, const Value& v, Scope* s) {
     if (t->k == E_NAME) {
-      if (auto c = lookup(s, t->name)) *c = v;
-      else I.globals->set(Value::string(t->name), v);
+      if (auto c = lookup(s, t->name)) {
+        *c = v;
+      } else if (I.env_used && t->name != "_ENV") {
+        if (auto env = lookup(s, "_ENV")) {
+          if (env->t != Value::Tab) rt(t.get(), std::string("attempt to index a ") + type_name(*env) + " value (upvalue '_ENV')");
+          I.setindex(*env, Value::string(t->name), v);
+        } else {
+          I.globals->set(Value::string(t->name), v);
+        }
+      } else {
+        I.globals->set(Value::string(t->name), v);
+      }
     } else {
       Value o = eval(t->a, s);
       if (o.t != Value::Tab && I.metamethod(o, "__newindex").t == Value::Nil)
@@ -1165,11 +1208,46 @@ struct Exec {
     }
   }
 
+  // `local x <close>`: the block's to-be-closed values get __close(value, error) in reverse order
+  // when the block ends -- normally, by break / return / goto, or by an error (Lua 5.4 sec. 3.3.8).
+  // An error in a closing method replaces the block's error and the remaining methods still run.
+  void close_tbc(Scope* sc, Value err, bool errored) {
+    std::unique_ptr<LuaError> raised;
+    while (!sc->tbc.empty()) {
+      Value v = std::move(sc->tbc.back());
+      sc->tbc.pop_back();
+      Value h = I.metamethod(v, "__close");
+      if (h.t == Value::Nil) continue;
+      try {
+        I.call(h, {v, errored ? err : Value()});
+      } catch (LuaError& e) {
+        err = e.value;
+        errored = true;
+        raised = std::make_unique<LuaError>(e.value, e.what());
+      }
+    }
+    if (raised) throw LuaError(raised->value, raised->what());
+  }
+  Flow run_closing(const std::shared_ptr<Block>& b, const std::shared_ptr<Scope>& sc) {
+    Flow f = F_NORMAL;
+    try {
+      f = run_stats(b, sc);
+    } catch (LuaError& e) {
+      if (sc->tbc.empty()) throw;
+      close_tbc(sc.get(), e.value, true);
+      throw;
+    } catch (...) {  // a coroutine being closed: its pending variables are closed too
+      if (!sc->tbc.empty()) close_tbc(sc.get(), Value(), false);
+      throw;
+    }
+    if (!sc->tbc.empty()) close_tbc(sc.get(), Value(), false);
+    return f;
+  }
   Flow exec_block(const std::shared_ptr<Block>& b, const std::shared_ptr<Scope>& parent) {
     auto sc = push(parent);
     Flow f = F_NORMAL;
     try {
-      f = run_stats(b, sc);
+      f = run_closing(b, sc);
     } catch (...) {
       pop();
       throw;
@@ -1184,8 +1262,15 @@ struct Exec {
     switch (st->k) {
       case S_LOCAL: {
         Values v = eval_list(st->exprs, s);
-        for (size_t i = 0; i < st->names.size(); ++i)
-          s->vars[st->names[i]] = std::make_shared<Value>(i < v.size() ? v[i] : Value());
+        for (size_t i = 0; i < st->names.size(); ++i) {
+          Value x = i < v.size() ? v[i] : Value();
+          if (st->attribs.size() > i && st->attribs[i] == 2 && x.truthy()) {  // nil / false: nothing to close
+            if (I.metamethod(x, "__close").t == Value::Nil)
+              rt(nullptr, "variable '" + st->names[i] + "' got a non-closable value");
+            s->tbc.push_back(x);
+          }
+          s->vars[st->names[i]] = std::make_shared<Value>(std::move(x));
+        }
         return F_NORMAL;
       }
       case S_LOCALFUNC: {
@@ -1219,7 +1304,7 @@ struct Exec {
           Flow f = F_NORMAL;
           bool done = false;
           try {
-            f = run_stats(st->body, inner);
+            f = run_closing(st->body, inner);
             if (f == F_NORMAL) done = eval(st->e, inner.get()).truthy();
           } catch (...) {
             pop();
@@ -1937,7 +2022,26 @@ Interp::Interp() {
       throw LuaError("bad argument #2 to 'setmetatable' (nil or table expected)");
     if (I.metamethod(t, "__metatable").t != Value::Nil) throw LuaError("cannot change a protected metatable");
     t.tab->meta = m.t == Value::Tab ? m.tab : nullptr;
+    // marked for finalization when the metatable has __gc at this point (a field added later does not count)
+    if (m.t == Value::Tab && m.tab->get(Value::string("__gc")).t != Value::Nil &&
+        std::find(I.finalizers.begin(), I.finalizers.end(), t.tab) == I.finalizers.end())
+      I.finalizers.push_back(t.tab);
     return Values{t};
+  });
+  reg(G, "collectgarbage", [](Interp& I, Values& a) -> Values {
+    const std::string opt = a.empty() || a[0].t == Value::Nil ? "collect" : check_str(a, 0, "collectgarbage");
+    if (opt == "collect" || opt == "step") {
+      I.run_finalizers(false);
+      return Values{opt == "step" ? Value::boolean(true) : Value::integer(0)};
+    }
+    if (opt == "count") {  // KB in use, estimated from the live objects (tables and scopes)
+      const double kb = I.heap ? (double)(I.heap->tables.size() * 96 + I.heap->scopes.size() * 112) / 1024.0 : 0.0;
+      return Values{Value::number(kb)};
+    }
+    if (opt == "isrunning") return Values{Value::boolean(true)};
+    if (opt == "incremental" || opt == "generational") return Values{Value::string("incremental")};
+    if (opt == "stop" || opt == "restart" || opt == "setpause" || opt == "setstepmul") return Values{Value::integer(0)};
+    throw LuaError("bad argument #1 to 'collectgarbage' (invalid option '" + opt + "')");
   });
   reg(G, "getmetatable", [](Interp& I, Values& a) {
     Value v = arg_at(a, 0);
@@ -2728,7 +2832,8 @@ Interp::Interp() {
   });
 
   // load / loadstring / dofile: compile a chunk into a vararg function of the global scope
-  auto compile = [](Interp& I, const std::string& src, const std::string& name) -> Value {
+  auto compile = [](Interp& I, const std::string& src, const std::string& name, const Value* env = nullptr) -> Value {
+    if (src.find("_ENV") != std::string::npos) I.env_used = true;
     Parser P(src, name);
     auto body = std::make_shared<FuncBody>();
     body->block = P.block();
@@ -2738,6 +2843,13 @@ Interp::Interp() {
     auto f = std::make_shared<Function>();
     f->body = body;
     f->env = I.root;
+    if (env) {  // load(chunk, name, mode, env): the chunk's free names resolve in `env` (its _ENV upvalue)
+      I.env_used = true;
+      auto sc = std::make_shared<Scope>();
+      sc->parent = I.root;
+      sc->vars["_ENV"] = std::make_shared<Value>(*env);
+      f->env = sc;
+    }
     f->name = name;
     return Value::function(f);
   };
@@ -2757,8 +2869,10 @@ Interp::Interp() {
       throw LuaError("bad argument #1 to 'load' (string expected)");
     }
     const std::string name = a.size() > 1 && a[1].t == Value::Str ? *a[1].s : "=(load)";
+    if (a.size() > 2 && a[2].t == Value::Str && a[2].s->find('t') == std::string::npos)
+      return Values{Value(), Value::string("attempt to load a text chunk (mode is '" + *a[2].s + "')")};
     try {
-      return Values{compile(I, src, name)};
+      return Values{compile(I, src, name, a.size() > 3 ? &a[3] : nullptr)};
     } catch (const LuaError& e) {
       return Values{Value(), Value::string(e.what())};
     }
@@ -2779,7 +2893,7 @@ Interp::Interp() {
   reg(G, "loadfile", [compile, slurp](Interp& I, Values& a) {
     const std::string path = check_str(a, 0, "loadfile");
     try {
-      return Values{compile(I, slurp(path), path)};
+      return Values{compile(I, slurp(path), path, a.size() > 2 ? &a[2] : nullptr)};
     } catch (const LuaError& e) {
       return Values{Value(), Value::string(e.what())};
     }
@@ -2905,11 +3019,375 @@ Interp::Interp() {
     return Values{it, Value::string(s), Value::integer(0)};
   });
 
-  for (const char* lib : {"string", "table", "math", "os", "coroutine", "io", "utf8"})
+
+  // string.pack / string.unpack / string.packsize (Lua 5.4 sec. 6.4.2): < > = endianness, ![n] maximum
+  // alignment, b B h H l L j J T i[n] I[n] (n = 1..16) integers, f d n floats, s[n] length-prefixed and
+  // z zero-terminated strings, x one pad byte, X<op> alignment to op, spaces ignored
+  struct PackOpt {
+    char k;       // 'i' signed, 'u' unsigned, 'f' float, 'd' double, 's' prefixed string, 'z', 'x' pad, 'X' align, ' ' none
+    int size;     // bytes (the length prefix for 's')
+    int align;    // alignment requirement (already limited by the maximum alignment)
+  };
+  struct PackState {
+    const std::string& fmt;
+    size_t p = 0;
+    bool little = true;
+    int maxalign = 1;
+    explicit PackState(const std::string& f) : fmt(f) {}
+    int num(int dflt) {
+      if (p >= fmt.size() || !isdigit((unsigned char)fmt[p])) return dflt;
+      int n = 0;
+      while (p < fmt.size() && isdigit((unsigned char)fmt[p]) && n < 1000) n = n * 10 + (fmt[p++] - '0');
+      return n;
+    }
+    int isize(int dflt, const char* fn) {
+      const int n = num(dflt);
+      if (n < 1 || n > 16) throw LuaError(std::string("bad argument #1 to '") + fn + "' (integral size (" +
+                                          std::to_string(n) + ") out of limits [1,16])");
+      return n;
+    }
+    // next option; false at the end of the format
+    bool next(PackOpt* o, const char* fn) {
+      for (;;) {
+        if (p >= fmt.size()) return false;
+        const char c = fmt[p++];
+        o->align = 1;
+        switch (c) {
+          case ' ': continue;
+          case '<': case '=': little = true; continue;
+          case '>': little = false; continue;
+          case '!': maxalign = num(8); continue;
+          case 'b': *o = {'i', 1, 1}; break;
+          case 'B': *o = {'u', 1, 1}; break;
+          case 'h': *o = {'i', 2, 2}; break;
+          case 'H': *o = {'u', 2, 2}; break;
+          case 'l': case 'j': *o = {'i', 8, 8}; break;
+          case 'L': case 'J': case 'T': *o = {'u', 8, 8}; break;
+          case 'i': { const int n = isize(4, fn); *o = {'i', n, n}; break; }
+          case 'I': { const int n = isize(4, fn); *o = {'u', n, n}; break; }
+          case 'f': *o = {'f', 4, 4}; break;
+          case 'd': case 'n': *o = {'d', 8, 8}; break;
+          case 's': { const int n = isize(8, fn); *o = {'s', n, n}; break; }
+          case 'z': *o = {'z', 0, 1}; return true;
+          case 'x': *o = {'x', 1, 1}; return true;
+          case 'X': {
+            PackOpt t{};
+            const size_t at = p;
+            if (!next(&t, fn) || t.k == 'z' || t.k == 's' || t.k == 'x' || t.k == 'X' || t.size == 0) {
+              p = at;
+              throw LuaError(std::string("bad argument #1 to '") + fn + "' (invalid next option for option 'X')");
+            }
+            *o = {'X', 0, t.size};
+            break;
+          }
+          default:
+            throw LuaError(std::string("bad argument #1 to '") + fn + "' (invalid format option '" + c + "')");
+        }
+        const int al = o->align < maxalign ? o->align : maxalign;
+        if (al > 1 && (al & (al - 1)))
+          throw LuaError(std::string("bad argument #1 to '") + fn + "' (format asks for alignment not power of 2)");
+        o->align = al;
+        return true;
+      }
+    }
+  };
+  auto pad_to = [](size_t pos, int align) -> size_t { return align > 1 ? (align - pos % (size_t)align) % (size_t)align : 0; };
+  auto put_int = [](std::string& out, uint64_t v, int size, bool little, bool neg) {
+    std::string b((size_t)size, '\0');
+    for (int i = 0; i < size; ++i) b[(size_t)i] = (char)(i < 8 ? (v >> (8 * i)) & 0xff : (neg ? 0xff : 0));
+    if (!little) std::reverse(b.begin(), b.end());
+    out += b;
+  };
+  reg(S, "pack", [pad_to, put_int](Interp&, Values& a) {
+    const std::string fmt = check_str(a, 0, "pack");
+    PackState st(fmt);
+    std::string out;
+    size_t arg = 1;
+    PackOpt o{};
+    while (st.next(&o, "pack")) {
+      out.append(pad_to(out.size(), o.align), '\0');
+      switch (o.k) {
+        case 'i': case 'u': {
+          const int64_t v = check_int(a, arg, "pack");
+          if (o.size < 8) {
+            if (o.k == 'i') {
+              const int64_t lim = (int64_t)1 << (o.size * 8 - 1);
+              if (v < -lim || v >= lim) throw LuaError("bad argument #" + std::to_string(arg + 1) + " to 'pack' (integer overflow)");
+            } else if ((uint64_t)v >= ((uint64_t)1 << (o.size * 8))) {
+              throw LuaError("bad argument #" + std::to_string(arg + 1) + " to 'pack' (unsigned overflow)");
+            }
+          }
+          put_int(out, (uint64_t)v, o.size, st.little, o.k == 'i' && v < 0);
+          ++arg;
+          break;
+        }
+        case 'f': case 'd': {
+          const double d = check_num(a, arg++, "pack");
+          uint64_t bits = 0;
+          if (o.k == 'f') {
+            const float f = (float)d;
+            uint32_t b32;
+            std::memcpy(&b32, &f, 4);
+            bits = b32;
+          } else {
+            std::memcpy(&bits, &d, 8);
+          }
+          put_int(out, bits, o.size, st.little, false);
+          break;
+        }
+        case 's': {
+          const std::string v = check_str(a, arg++, "pack");
+          if (o.size < 8 && (uint64_t)v.size() >= ((uint64_t)1 << (o.size * 8)))
+            throw LuaError("bad argument #" + std::to_string(arg) + " to 'pack' (string length does not fit in given size)");
+          put_int(out, (uint64_t)v.size(), o.size, st.little, false);
+          out += v;
+          break;
+        }
+        case 'z': {
+          const std::string v = check_str(a, arg++, "pack");
+          if (v.find('\0') != std::string::npos)
+            throw LuaError("bad argument #" + std::to_string(arg) + " to 'pack' (string contains zeros)");
+          out += v;
+          out += '\0';
+          break;
+        }
+        case 'x': out += '\0'; break;
+        case 'X': break;
+      }
+    }
+    return Values{Value::string(out)};
+  });
+  reg(S, "packsize", [pad_to](Interp&, Values& a) {
+    const std::string fmt = check_str(a, 0, "packsize");
+    PackState st(fmt);
+    size_t n = 0;
+    PackOpt o{};
+    while (st.next(&o, "packsize")) {
+      if (o.k == 's' || o.k == 'z') throw LuaError("bad argument #1 to 'packsize' (variable-length format)");
+      n += pad_to(n, o.align) + (size_t)o.size;
+    }
+    return Values{Value::integer((int64_t)n)};
+  });
+  reg(S, "unpack", [pad_to](Interp&, Values& a) {
+    const std::string fmt = check_str(a, 0, "unpack");
+    const std::string data = check_str(a, 1, "unpack");
+    int64_t init = a.size() > 2 && a[2].t != Value::Nil ? check_int(a, 2, "unpack") : 1;
+    if (init < 0) init = (int64_t)data.size() + init + 1;
+    if (init < 1 || init - 1 > (int64_t)data.size()) throw LuaError("bad argument #3 to 'unpack' (initial position out of string)");
+    size_t pos = (size_t)init - 1;
+    PackState st(fmt);
+    Values out;
+    PackOpt o{};
+    auto need = [&](size_t n) {
+      if (pos + n > data.size()) throw LuaError("bad argument #2 to 'unpack' (data string too short)");
+    };
+    auto get_int = [&](int size, bool sign) -> uint64_t {
+      need((size_t)size);
+      uint64_t v = 0;
+      for (int i = 0; i < size; ++i) {
+        const uint8_t byte = (uint8_t)data[pos + (size_t)(st.little ? i : size - 1 - i)];
+        if (i < 8) v |= (uint64_t)byte << (8 * i);
+        else if (byte != ((sign && (int64_t)v < 0) ? 0xff : 0))
+          throw LuaError(std::to_string(size) + "-byte integer does not fit into Lua Integer");
+      }
+      if (sign && size < 8 && (v >> (size * 8 - 1)) & 1) v |= ~(uint64_t)0 << (size * 8);
+      pos += (size_t)size;
+      return v;
+    };
+    while (st.next(&o, "unpack")) {
+      const size_t pad = pad_to(pos, o.align);
+      need(pad);
+      pos += pad;
+      switch (o.k) {
+        case 'i': out.push_back(Value::integer((int64_t)get_int(o.size, true))); break;
+        case 'u': out.push_back(Value::integer((int64_t)get_int(o.size, false))); break;
+        case 'f': {
+          const uint32_t b = (uint32_t)get_int(4, false);
+          float f;
+          std::memcpy(&f, &b, 4);
+          out.push_back(Value::number(f));
+          break;
+        }
+        case 'd': {
+          const uint64_t b = get_int(8, false);
+          double d;
+          std::memcpy(&d, &b, 8);
+          out.push_back(Value::number(d));
+          break;
+        }
+        case 's': {
+          const uint64_t n = get_int(o.size, false);
+          need((size_t)n);
+          out.push_back(Value::string(data.substr(pos, (size_t)n)));
+          pos += (size_t)n;
+          break;
+        }
+        case 'z': {
+          const size_t e = data.find('\0', pos);
+          if (e == std::string::npos) throw LuaError("bad argument #2 to 'unpack' (unfinished string for format 'z')");
+          out.push_back(Value::string(data.substr(pos, e - pos)));
+          pos = e + 1;
+          break;
+        }
+        case 'x': need(1); ++pos; break;
+        case 'X': break;
+      }
+    }
+    out.push_back(Value::integer((int64_t)pos + 1));
+    return out;
+  });
+
+  // debug (the subset a tree-walking interpreter can give): traceback, getinfo, get/setmetatable
+  // without __metatable protection, getregistry, sethook/gethook (no hooks run), getlocal /
+  // getupvalue (no indexed locals or upvalues here: nil)
+  auto D = std::make_shared<Table>();
+  G->set(Value::string("debug"), Value::table(D));
+  registry = std::make_shared<Table>();
+  reg(D, "traceback", [](Interp& I, Values& a) {
+    size_t at = a.size() > 0 && a[0].t == Value::Co ? 1 : 0;  // optional thread argument
+    Value m = arg_at(a, at);
+    if (m.t != Value::Nil && m.t != Value::Str && !m.is_num()) return Values{m};
+    std::string s = m.t == Value::Nil ? "" : (m.t == Value::Str ? *m.s : tostring(m)) + "\n";
+    s += "stack traceback:\n\t" + I.chunk + ":" + std::to_string(I.line) + ": in function <" + I.chunk + ">\n\t[C]: in ?";
+    return Values{Value::string(s)};
+  });
+  reg(D, "getinfo", [](Interp& I, Values& a) {
+    size_t at = a.size() > 0 && a[0].t == Value::Co ? 1 : 0;
+    Value f = arg_at(a, at);
+    auto t = std::make_shared<Table>();
+    t->set(Value::string("source"), Value::string("@" + I.chunk));
+    t->set(Value::string("short_src"), Value::string(I.chunk));
+    if (f.t == Value::Fn) {
+      const bool native = (bool)f.fn->native;
+      t->set(Value::string("what"), Value::string(native ? "C" : "Lua"));
+      t->set(Value::string("func"), f);
+      t->set(Value::string("currentline"), Value::integer(-1));
+      t->set(Value::string("linedefined"), Value::integer(native ? -1 : 0));
+      t->set(Value::string("nparams"), Value::integer(native ? 0 : (int64_t)f.fn->body->params.size()));
+      t->set(Value::string("isvararg"), Value::boolean(native || f.fn->body->vararg));
+      if (native) t->set(Value::string("source"), Value::string("=[C]")), t->set(Value::string("short_src"), Value::string("[C]"));
+      if (!f.fn->name.empty()) t->set(Value::string("name"), Value::string(f.fn->name));
+    } else if (f.is_num()) {
+      const int64_t level = toint_strict(f, "getinfo");
+      if (level < 0 || level > I.depth) return Values{Value()};
+      t->set(Value::string("what"), Value::string(level == 0 ? "C" : "Lua"));
+      t->set(Value::string("currentline"), Value::integer(level == 0 ? -1 : I.line));
+    } else {
+      throw LuaError("bad argument #1 to 'getinfo' (function or level expected)");
+    }
+    t->set(Value::string("nups"), Value::integer(0));
+    t->set(Value::string("istailcall"), Value::boolean(false));
+    return Values{Value::table(t)};
+  });
+  reg(D, "getmetatable", [](Interp& I, Values& a) {
+    Value v = arg_at(a, 0);
+    std::shared_ptr<Table> m = v.t == Value::Tab ? v.tab->meta : v.t == Value::Str ? I.string_meta : nullptr;
+    return Values{m ? Value::table(m) : Value()};
+  });
+  reg(D, "setmetatable", [](Interp& I, Values& a) {
+    Value v = arg_at(a, 0), m = arg_at(a, 1);
+    if (m.t != Value::Nil && m.t != Value::Tab) throw LuaError("bad argument #2 to 'setmetatable' (nil or table expected)");
+    if (v.t == Value::Tab) v.tab->meta = m.t == Value::Tab ? m.tab : nullptr;
+    else if (v.t == Value::Str) I.string_meta = m.t == Value::Tab ? m.tab : nullptr;
+    else throw LuaError("debug.setmetatable: only tables and strings carry metatables here");
+    return Values{v};
+  });
+  reg(D, "getregistry", [](Interp& I, Values&) { return Values{Value::table(I.registry)}; });
+  reg(D, "sethook", [](Interp&, Values&) { return Values{}; });
+  reg(D, "gethook", [](Interp&, Values&) { return Values{Value()}; });
+  reg(D, "getlocal", [](Interp&, Values&) { return Values{Value()}; });
+  reg(D, "getupvalue", [](Interp&, Values&) { return Values{Value()}; });
+  reg(D, "setupvalue", [](Interp&, Values&) { return Values{Value()}; });
+  reg(D, "upvalueid", [](Interp&, Values&) { return Values{Value()}; });
+
+  for (const char* lib : {"string", "table", "math", "os", "coroutine", "io", "utf8", "debug"})
     modules[lib] = G->get(Value::string(lib));
 }
 
+// __gc (collectgarbage): a mark phase from the roots -- globals, registry, string metatable, loaded
+// modules and the scope stacks of every running or suspended call -- through tables, metatables,
+// closures' scopes and coroutines; marked tables it did not reach are finalized (reverse marking
+// order), as are, at close (all), the rest.  Values held only by a native function's C++ frame
+// while it runs are not roots (a finalizer may then run early; the object itself stays valid).
+// Errors in finalizers are dropped (warnings off).
+void Interp::run_finalizers(bool all) {
+  for (int round = 0; round < 64 && !finalizers.empty(); ++round) {
+    std::unordered_set<const void*> seen;
+    if (!all) {
+      std::vector<const Table*> tw;
+      std::vector<const Scope*> sw;
+      std::function<void(const Value&)> val = [&](const Value& v) {
+        switch (v.t) {
+          case Value::Tab:
+            if (v.tab && seen.insert(v.tab.get()).second) tw.push_back(v.tab.get());
+            break;
+          case Value::Fn:
+            if (v.fn && seen.insert(v.fn.get()).second && v.fn->env && seen.insert(v.fn->env.get()).second)
+              sw.push_back(v.fn->env.get());
+            break;
+          case Value::Co:
+            if (v.co && seen.insert(v.co.get()).second) {
+              val(v.co->fn);
+              for (const Value& x : v.co->transfer) val(x);
+            }
+            break;
+          default: break;
+        }
+      };
+      auto scope = [&](const std::shared_ptr<Scope>& sc) {
+        if (sc && seen.insert(sc.get()).second) sw.push_back(sc.get());
+      };
+      val(Value::table(globals));
+      if (registry) val(Value::table(registry));
+      if (string_meta) val(Value::table(string_meta));
+      for (auto& m : modules) val(m.second);
+      scope(root);
+      for (auto* st : scope_stacks)
+        for (auto& sc : *st) scope(sc);
+      while (!tw.empty() || !sw.empty()) {
+        if (!tw.empty()) {
+          const Table* t = tw.back();
+          tw.pop_back();
+          for (auto& e : t->entries) {
+            val(e.first);
+            val(e.second);
+          }
+          if (t->meta) val(Value::table(t->meta));
+        } else {
+          const Scope* sc = sw.back();
+          sw.pop_back();
+          for (auto& c : sc->vars)
+            if (c.second) val(*c.second);
+          for (auto& x : sc->varargs) val(x);
+          for (auto& x : sc->tbc) val(x);
+          if (sc->parent && seen.insert(sc->parent.get()).second) sw.push_back(sc->parent.get());
+        }
+      }
+    }
+    std::vector<std::shared_ptr<Table>> dead;
+    for (size_t i = finalizers.size(); i-- > 0;)
+      if (all || !seen.count(finalizers[i].get())) {
+        dead.push_back(std::move(finalizers[i]));
+        finalizers.erase(finalizers.begin() + (long)i);
+      }
+    if (dead.empty()) break;
+    for (auto& t : dead) {
+      Value h = t->meta ? t->meta->get(Value::string("__gc")) : Value();
+      if (h.t == Value::Nil) continue;
+      try {
+        call(h, {Value::table(t)});
+      } catch (const LuaError&) {
+      }
+    }
+    if (!all) break;  // objects a finalizer released wait for the next cycle, as in Lua
+  }
+}
+
 Interp::~Interp() {
+  try {
+    run_finalizers(true);
+  } catch (...) {
+  }
   // Move every live table's and scope's contents into one graveyard first (moves destroy
   // nothing, so no registered object disappears while the sets are walked), then drop it.
   std::vector<Value> grave;
@@ -2951,6 +3429,7 @@ Value Interp::global(const std::string& name) const { return globals->get(Value:
 
 Values Interp::run(const std::string& src, const std::string& chunkname, const std::vector<std::string>& args) {
   chunk = chunkname;
+  if (src.find("_ENV") != std::string::npos) env_used = true;
   Parser P(src, chunkname);
   auto body = std::make_shared<FuncBody>();
   body->block = P.block();

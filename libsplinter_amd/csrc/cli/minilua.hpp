@@ -131,6 +131,16 @@ struct Interp {
   std::string chunk;
   Heap* heap = nullptr;       // objects created while this interpreter is current
   Heap* prev_heap = nullptr;  // restored on destruction (nested interpreters)
+  // `_ENV` resolution is on once a chunk names `_ENV` or load() gets an env table: free names then
+  // resolve through the innermost `_ENV` local (Lua 5.4 sec. 2.2), else the globals
+  bool env_used = false;
+  // tables whose metatable had __gc when it was set (Lua 5.4 sec. 2.5.3), in marking order;
+  // finalized by collectgarbage() once nothing else holds them, and all of them at close
+  std::vector<std::shared_ptr<Table>> finalizers;
+  void run_finalizers(bool all);
+  // the scope stacks of every running or suspended Lua call (roots of collectgarbage's mark phase)
+  std::vector<std::vector<std::shared_ptr<Scope>>*> scope_stacks;
+  std::shared_ptr<Table> registry;  // debug.getregistry()
 };
 
 std::string tostring(const Value& v);

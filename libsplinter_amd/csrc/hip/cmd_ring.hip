@@ -1029,10 +1029,41 @@ int CmdRing::call(const spl_arena_t& a, uint32_t op, uint32_t sub, const char ke
   return call_private(a, op, sub, key64, klen, khash, in, in_len, arg, out, out_cap, r);
 }
 
+#ifdef SPL_RING_STAMPS
+// Host half of the per-call latency breakdown (stamps build): per call, CLOCK_MONOTONIC ns from
+// entry to owning a ring entry, to the record + payload + doorbell written through the BAR, to the
+// completion observed, to the return; the wait's time inside nanosleep (CPU released) and its
+// sleeps.  Summed per thread, folded into the process totals when the thread exits, printed by
+// ~CmdRing beside the worker's device-side segments.
+struct HostStampSums {
+  std::atomic<uint64_t> n{0}, own{0}, post{0}, wait{0}, slept{0}, sleeps{0}, fin{0};
+};
+static HostStampSums g_hstamps;
+struct HostStampLocal {
+  uint64_t n = 0, own = 0, post = 0, wait = 0, slept = 0, sleeps = 0, fin = 0;
+  void flush() {
+    g_hstamps.n += n, g_hstamps.own += own, g_hstamps.post += post, g_hstamps.wait += wait;
+    g_hstamps.slept += slept, g_hstamps.sleeps += sleeps, g_hstamps.fin += fin;
+    n = own = post = wait = slept = sleeps = fin = 0;
+  }
+  ~HostStampLocal() { flush(); }
+};
+static thread_local HostStampLocal t_hstamps;
+static inline uint64_t mono_ns() {
+  timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (uint64_t)t.tv_sec * 1000000000ull + (uint64_t)t.tv_nsec;
+}
+#define HOST_TS(v) const uint64_t v = mono_ns()
+#else
+#define HOST_TS(v) ((void)0)
+#endif
+
 int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const char key64[64], uint32_t klen,
                           uint64_t khash, const void* in, uint32_t in_len, uint64_t arg, void* out, uint32_t out_cap,
                           RingResult* r) {
   if (in_len > pstride_) { errno = EMSGSIZE; return -1; }
+  HOST_TS(hs0);
   std::shared_lock<std::shared_mutex> gate(g_gate, std::defer_lock);
   if (!t_exclusive) gate.lock();  // (a store set-up on this thread already holds it exclusive)
   // own an entry: start at a rotating ticket, CAS the busy flag (in the shared segment for a ring
@@ -1086,6 +1117,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     }
     e = entry_of(++t);
   }
+  HOST_TS(hs1);
   RingCmd* c = cmds_ + e;
   uint32_t done_word = kRingDone;
   if (vr_) {
@@ -1128,6 +1160,10 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     else launch(mode_ == kServer ? arena_ : a);
   };
   ensure_worker();
+  HOST_TS(hs2);
+#ifdef SPL_RING_STAMPS
+  uint64_t hslept = 0, hsleeps = 0;
+#endif
   clock_gettime(CLOCK_MONOTONIC, &t0);
   // Wait for completion: spin (a call is served in ~10 us), then give the CPU away between polls.
   // With more waiting callers than CPUs the process may run on (cgroup quota included), spinning
@@ -1169,7 +1205,14 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
           }
           const timespec ts{0, slept ? sleep_ns_ : first};
           slept = true;
+#ifdef SPL_RING_STAMPS
+          const uint64_t z0 = mono_ns();
           nanosleep(&ts, nullptr);
+          hslept += mono_ns() - z0;
+          ++hsleeps;
+#else
+          nanosleep(&ts, nullptr);
+#endif
         } else {
           sched_yield();
         }
@@ -1186,6 +1229,7 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
       }
     }
   }
+  HOST_TS(hs3);
   if (slept && adaptive_) {  // latency of an oversubscribed call, for the next first sleeps
     const long ns = (long)elapsed_us() * 1000;
     const long o = ewma_ns_.load(std::memory_order_relaxed);
@@ -1206,6 +1250,15 @@ int CmdRing::call_private(const spl_arena_t& a, uint32_t op, uint32_t sub, const
     std::memcpy(out, payload_ + (size_t)e * pstride_, r->out_len < out_cap ? r->out_len : out_cap);
   if (!vr_) __atomic_store_n(&shared_->state[e], (uint32_t)kRingFree, __ATOMIC_RELEASE);
   __atomic_store_n(&ent_[e].busy, 0u, __ATOMIC_RELEASE);
+#ifdef SPL_RING_STAMPS
+  {
+    HostStampLocal& h = t_hstamps;
+    const uint64_t hs4 = mono_ns();
+    ++h.n, h.own += hs1 - hs0, h.post += hs2 - hs1, h.wait += hs3 - hs2, h.fin += hs4 - hs3;
+    h.slept += hslept, h.sleeps += hsleeps;
+    if ((h.n & 1023) == 0) h.flush();
+  }
+#endif
   return 0;
 }
 
@@ -1340,6 +1393,16 @@ CmdRing::~CmdRing() {
       fprintf(stderr, "{\"op\": \"%s\", \"n\": %llu, \"seg_us\": [%.3f, %.3f, %.3f, %.3f]}\n", k ? "get" : "set",
               (unsigned long long)v[4], v[0] * us, v[1] * us, v[2] * us, v[3] * us);
     }
+  }
+  t_hstamps.flush();
+  if (const uint64_t n = g_hstamps.n.load()) {
+    const double k = 1e-3 / (double)n;  // ns sums -> us per call
+    fprintf(stderr,
+            "{\"host_stamps\": %llu, \"own_entry_us\": %.3f, \"post_record_doorbell_us\": %.3f, "
+            "\"doorbell_to_completion_seen_us\": %.3f, \"of_it_asleep_us\": %.3f, \"sleeps_per_call\": %.3f, "
+            "\"completion_to_return_us\": %.3f}\n",
+            (unsigned long long)n, g_hstamps.own.load() * k, g_hstamps.post.load() * k, g_hstamps.wait.load() * k,
+            g_hstamps.slept.load() * k, (double)g_hstamps.sleeps.load() / (double)n, g_hstamps.fin.load() * k);
   }
 #endif
   if (stream_) (void)hipStreamDestroy(stream_);

@@ -74,7 +74,7 @@ def test_asan_lua_and_wasm_interpreters(uniq, tmp_path):
         _run([ctl, "-u", st, "lua", str(lua)])
         # patterns, metatables and coroutines (one thread per coroutine; a suspended one is unwound
         # and joined at interpreter teardown)
-        for script in ("lua_patterns_meta.lua", "lua_coroutines.lua", "lua_stdlib.lua"):
+        for script in ("lua_patterns_meta.lua", "lua_coroutines.lua", "lua_stdlib.lua", "lua_more.lua"):
             _run([ctl, "-u", st, "lua", os.path.join(ROOT, "tests", "data", script)])
     finally:
         subprocess.run([ctl, "-u", st, "unset", "src"], capture_output=True, env=ENV)

@@ -29,6 +29,9 @@ def test_bench_single_gpu_contract():
               "vs_baseline", "dtype", "data", "config"):
         assert k in d, k
     assert d["n_gpus"] == 1 and d["steps"] == 2 and d["integrity_failures"] == 0 and d["value"] > 0
+    # config #2 literally (every client stream posts its own slice) beside the fused grid
+    assert d["kv_async_ops_per_s"] > 0 and d["kv_async_integrity_failures"] == 0, d.get("kv_async_submission")
+    assert d["kv_async_streams"] == {"writer": 32, "reader": 32}
 
 
 def test_bench_two_rank_rehearsal_gloo():

@@ -667,6 +667,8 @@ def main():
         step(i, last=i == args.warmup - 1) if routed else step(i)
     torch.cuda.synchronize()
     arena.reset_stats()
+    if xr is not None:
+        xr.phase_reset()  # SPLINTER_XR_PHASES=1: attribute the timed steps only
     if routed:
         dist.barrier()
     torch.cuda.synchronize()
@@ -784,6 +786,8 @@ def main():
         for _ in range(2):  # warm-up: tokenizer threads, and both key sets' varlen shapes (first-shape GEMM setup)
             pipe.run()
         torch.cuda.synchronize()
+        pipe.t_wait = pipe.t_tok = 0.0
+        pipe.calls = 0
         t0 = time.perf_counter()
         fails_d = torch.zeros((), dtype=torch.int64, device="cuda")
         for _ in range(args.embed_e2e):  # write failures counted on the device: no per-batch host sync
@@ -795,7 +799,9 @@ def main():
             dist.all_reduce(te, op=dist.ReduceOp.MAX)
         dt = te.item()
         e2e = {"vectors_per_s": pipe.docs * args.embed_e2e * world / dt, "ms_per_batch": dt / args.embed_e2e * 1e3,
-               "tokens_per_batch": pipe.tokens, "write_failures": fails}
+               "tokens_per_batch": pipe.tokens, "write_failures": fails,
+               "host_wait_ms": pipe.t_wait / max(pipe.calls, 1) * 1e3,
+               "host_tokenize_ms": pipe.t_tok / max(pipe.calls, 1) * 1e3}
         pipe.close()
 
     # ---- the embedding daemon itself, owner computes: each rank's daemon embeds the pending
@@ -944,6 +950,10 @@ def main():
         "embed_e2e_ms_per_batch": e2e["ms_per_batch"] if e2e else None,
         "embed_e2e_tokens_per_batch": e2e["tokens_per_batch"] if e2e else None,
         "embed_e2e_write_failures": e2e["write_failures"] if e2e else None,
+        # per batch on the host: waiting for the GPU vs tokenizing + packing the next batch (a wait
+        # near 0 means the tokenizer, not the encoder, bounds the pipeline)
+        "embed_e2e_host_wait_ms": e2e["host_wait_ms"] if e2e else None,
+        "embed_e2e_host_tokenize_ms": e2e["host_tokenize_ms"] if e2e else None,
         "embed_phase_ms_per_step": emb_phase_ms,
         "encoder_tflops": enc_tflops,
         "kv_attempts": attempts, "kv_ok": ok, "kv_eagain_retries": again, "kv_miss": miss,
@@ -968,6 +978,8 @@ def main():
         "exchange_sync": xab["sync"] if xab else None, "exchange_sync_error": xab["sync_error"] if xab else None,
         "xr_sync_error": (xr.sync_error() if (routed and xr is not None) else None),
         "exchange_integrity_failures": xab["integrity"] if xab else None,
+        # SPLINTER_XR_PHASES=1 on a routed run: device ms per phase of a timed step, host ms in collectives
+        "xr_phases_ms": xr.phase_summary() if xr is not None else None,
         # config #2 literally: every one of the client streams submits its own slice (SPL_KVS_FUSED=3)
         "kv_async_ops_per_s": kab["async"] if kab else None,
         "kv_fused_only_ops_per_s": kab["fused"] if kab else None,

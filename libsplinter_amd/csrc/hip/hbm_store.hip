@@ -17,9 +17,12 @@
 #include <cstring>
 #include <fcntl.h>
 #include <algorithm>
+#include <cfloat>
+#include <functional>
 #include <cmath>
 #include <atomic>
 #include <memory>
+#include <condition_variable>
 #include <mutex>
 #include <poll.h>
 #include <string>
@@ -102,6 +105,63 @@ int neg_to_errno(int32_t st) {
 }
 
 }  // namespace
+
+// Candidate thresholds shared by the shards of one node search (spl_search_batch on node:): per
+// 256-query block every participating shard posts the k largest sampled tile maxima of each query
+// (k_search_thr's topv: k real slots of ITS arena at or above each value) and continues with the
+// threshold of their union -- the k-th largest over all shards' samples minus the bf16 margin, a
+// lower bound of every query's k-th best similarity over the whole node, as tight as one store
+// sampling the same slots -- so the shards' candidate and re-score work stays what one store of
+// all the slots would do instead of growing with the shard count.  A shard with nothing to post
+// (exact kernel, distance-bounded batch) posts nothing and takes the result; a shard that stops
+// early (error) leaves, so nobody waits for it.
+struct SearchSync {
+  std::mutex mu;
+  std::condition_variable cv;
+  int active = 0, arrived = 0;
+  uint64_t gen = 0;
+  std::vector<std::vector<float>> posts;
+  std::vector<float> result;
+  int m = 0, k = 0;
+  float delta2 = 0.f, floor_v = 0.f;
+  explicit SearchSync(int n) : active(n) {}
+  void release() {
+    result.assign((size_t)m, floor_v);
+    std::vector<float> u;
+    for (int i = 0; i < m; ++i) {
+      u.clear();
+      for (auto& p : posts)
+        for (int j = 0; j < k; ++j) {
+          const float v = p[(size_t)i * k + j];
+          if (v > -FLT_MAX) u.push_back(v);
+        }
+      if ((int)u.size() >= k) {
+        std::nth_element(u.begin(), u.begin() + (k - 1), u.end(), std::greater<float>());
+        result[(size_t)i] = std::max(u[(size_t)(k - 1)] - delta2, floor_v);
+      }
+    }
+    posts.clear();
+    arrived = 0;
+    ++gen;
+    cv.notify_all();
+  }
+  // topv: [mq][kq] or nullptr; thr: [mq] out
+  void merge(const float* topv, int mq, int kq, float d2, float fl, float* thr) {
+    std::unique_lock<std::mutex> l(mu);
+    m = mq, k = kq, delta2 = d2, floor_v = fl;
+    if (topv) posts.emplace_back(topv, topv + (size_t)mq * kq);
+    ++arrived;
+    const uint64_t g = gen;
+    if (arrived >= active) release();
+    else cv.wait(l, [&] { return gen != g; });
+    for (int i = 0; i < mq && i < (int)result.size(); ++i) thr[i] = result[(size_t)i];
+  }
+  void leave() {
+    std::lock_guard<std::mutex> l(mu);
+    --active;
+    if (arrived > 0 && arrived >= active) release();
+  }
+};
 
 class HbmStore final : public StoreBase {
  public:
@@ -455,7 +515,7 @@ class HbmStore final : public StoreBase {
   int checkpoint(const char* path);
   long search_all(const float* q, uint64_t mask, float min_sim, float max_dist, long cap, spl_search_hit* out);
   long search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask, spl_search_hit* out,
-                   int sample_div = 1);
+                   int sample_div = 1, SearchSync* sync = nullptr);
   int device() const { return device_; }
   struct SearchScratch;
   SearchScratch* ss_ = nullptr;
@@ -1080,7 +1140,7 @@ static hipStream_t search_stream(int device, int slot) {
 thread_local int g_search_slot = 0;
 
 long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float max_dist, uint64_t mask,
-                            spl_search_hit* out, int sample_div) {
+                            spl_search_hit* out, int sample_div, SearchSync* sync) {
   if (!geo_.embeddings()) { errno = ENOTSUP; return -1; }
   if (nq <= 0 || k <= 0 || k > 32 || !q || !out) { errno = EINVAL; return -1; }
   if (!ensure_mapped()) return -1;
@@ -1147,25 +1207,41 @@ long HbmStore::search_batch(const float* q, int nq, int k, float min_sim, float 
   // query would overflow its segments and be redone alone): those batches go to the exact kernel
   // directly, kExactQ queries per arena scan
   const bool exact_only = !mma || (bounded && min_sim <= -1.f);
-  for (int b = 0; ok && b < nq; b += kMmaQ) {
+  for (int b = 0; ok && b < nq; b += kMmaQ) {  // (a shard that fails leaves the node's threshold merge)
     const int n = std::min(kMmaQ, nq - b);
     const float* hq = q + (size_t)b * kEmbedDim;
+    const float floor_v = min_sim - kDelta;
     if (exact_only) {
+      if (sync) {  // a shard on the exact kernel still takes part in the block's threshold merge
+        thr_h.assign((size_t)n, floor_v);
+        sync->merge(nullptr, n, k, 2 * kDelta, floor_v, thr_h.data());
+      }
       ok = exact(hq, n, res.data() + (size_t)b * k, cores.data() + (size_t)b * k * 128);
       continue;
     }
     // queries up once (fp32); the bf16 fragment operand is built on the device (spl_search_qprep)
-    const float floor_v = min_sim - kDelta;
     std::memcpy(S.hq(), hq, (size_t)n * kEmbedBytes);
     ok = hipMemcpyAsync(S.q, S.hq(), (size_t)n * kEmbedBytes, hipMemcpyHostToDevice, ss) == hipSuccess &&
          spl_search_qprep(S.q, n, S.qf, ss) == 0;
     if (ok && !bounded) {
+      // node search: the k largest sampled maxima per query come back (staged in S.cnt, which the
+      // candidate pass clears afterwards) for the shards' union threshold
+      float* topv_d = sync ? (float*)S.cnt : nullptr;
       ok = spl_search_mma_pass(a, S.qf, n, 0, sample, mask, 0, nullptr, S.bmax, nullptr, nullptr, 0, kMmaGrid, ss) ==
                0 &&
-           spl_search_thr(S.bmax, (int)(sample / kMmaTile), n, k, 2 * kDelta, floor_v, S.thr, ss) == 0;
-    } else if (ok) {
+           spl_search_thr_topk(S.bmax, (int)(sample / kMmaTile), n, k, 2 * kDelta, floor_v, S.thr, topv_d, ss) == 0;
+      if (sync) {
+        float* tv = (float*)S.hres();  // pinned staging, free until the results come back
+        const bool got = ok && hipMemcpyAsync(tv, topv_d, (size_t)n * k * 4, hipMemcpyDeviceToHost, ss) == hipSuccess &&
+                         hipStreamSynchronize(ss) == hipSuccess;
+        float* th = (float*)S.hover();
+        sync->merge(got ? tv : nullptr, n, k, 2 * kDelta, floor_v, th);
+        ok = got && hipMemcpyAsync(S.thr, th, (size_t)n * 4, hipMemcpyHostToDevice, ss) == hipSuccess;
+      }
+    } else {
       thr_h.assign((size_t)n, floor_v);
-      ok = hipMemcpyAsync(S.thr, thr_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, ss) == hipSuccess;
+      if (sync) sync->merge(nullptr, n, k, 2 * kDelta, floor_v, thr_h.data());
+      ok = ok && hipMemcpyAsync(S.thr, thr_h.data(), (size_t)n * 4, hipMemcpyHostToDevice, ss) == hipSuccess;
     }
     // (the overflow flags reuse S.bmax: the threshold is built by then)
     ok = ok && hipMemsetAsync(S.cnt, 0, (size_t)n * kMmaGrid * 4, ss) == hipSuccess &&
@@ -1786,11 +1862,14 @@ long spl_search_batch(spl_store* h, const float* queries, int nq, int k, float m
         if (sj && sj->device() == si->device()) ++slot[(size_t)i];
       }
     }
+    spl::SearchSync sync(n);
     for (int i = 0; i < n; ++i)
       th.emplace_back([&, i] {
         spl::g_search_slot = slot[(size_t)i];
         auto* s = dynamic_cast<spl::HbmStore*>((spl::StoreBase*)spl_node_shard(h, i));
-        rc[(size_t)i] = s ? s->search_batch(queries, nq, k, min_sim, max_dist, mask, part[(size_t)i].data(), n) : -1;
+        rc[(size_t)i] =
+            s ? s->search_batch(queries, nq, k, min_sim, max_dist, mask, part[(size_t)i].data(), n, &sync) : -1;
+        sync.leave();
       });
     for (auto& t : th) t.join();
   }

@@ -764,8 +764,10 @@ __global__ __launch_bounds__(kRsWaves * 64) void k_rescore(spl_arena_t aa, const
 // thr[q] = max(k-th largest of bmax[0..T)[q] - 2 delta, floor); fewer than k tiles: floor.  One block
 // per query: every thread keeps the k largest of its strided share, then k rounds of a block max
 // (the winner drops its head).
+// topv (optional): the k largest themselves, [nq][k] descending (-FLT_MAX past the tiles), for a
+// node search that merges the shards' samples (HbmStore::search_batch, SearchSync).
 __global__ __launch_bounds__(256) void k_search_thr(const float* __restrict__ bmax, int T, int nq, int k, float delta2,
-                                                    float floor_v, float* __restrict__ thr) {
+                                                    float floor_v, float* __restrict__ thr, float* __restrict__ topv) {
   __shared__ float wv[4];
   __shared__ int wi[4];
   const int q = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -798,6 +800,7 @@ __global__ __launch_bounds__(256) void k_search_thr(const float* __restrict__ bm
     __syncthreads();
     if (bi == tid) ++head;
     kth = bv;
+    if (topv && tid == 0) topv[(long)q * k + r] = bv;
   }
   if (tid == 0) thr[q] = (T < k || kth == -FLT_MAX) ? floor_v : fmaxf(kth - delta2, floor_v);
 }
@@ -1001,8 +1004,13 @@ int spl_search_mma_pass(spl_arena_t a, const void* qfrag, int nq, long slot_begi
 
 int spl_search_thr(const float* bmax, int tiles, int nq, int K, float delta2, float floor_v, float* thr,
                    hipStream_t s) {
+  return spl_search_thr_topk(bmax, tiles, nq, K, delta2, floor_v, thr, nullptr, s);
+}
+
+int spl_search_thr_topk(const float* bmax, int tiles, int nq, int K, float delta2, float floor_v, float* thr,
+                        float* topv, hipStream_t s) {
   if (nq <= 0 || K <= 0 || K > kMaxK || tiles < 0 || !thr) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_search_thr, dim3(nq), dim3(256), 0, s, bmax, tiles, nq, K, delta2, floor_v, thr);
+  hipLaunchKernelGGL(k_search_thr, dim3(nq), dim3(256), 0, s, bmax, tiles, nq, K, delta2, floor_v, thr, topv);
   return (int)hipGetLastError();
 }
 

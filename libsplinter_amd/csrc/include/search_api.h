@@ -39,6 +39,10 @@ int spl_search_overflow(const uint32_t *cnt, int nq, int nblk, int capb, uint32_
 /* per-query candidate threshold from a bmax pass: max(k-th largest of bmax[tiles][nq] - delta2, floor) */
 int spl_search_thr(const float *bmax, int tiles, int nq, int K, float delta2, float floor_v, float *thr,
                    hipStream_t stream);
+// the same, and the k largest sampled tile maxima per query into topv [nq][K] (descending,
+// -FLT_MAX past the sample): a node search merges them over its shards
+int spl_search_thr_topk(const float* bmax, int tiles, int nq, int K, float delta2, float floor_v, float* thr,
+                        float* topv, hipStream_t s);
 /* Exact fp32 re-score of the candidate segments (queries [nq, 768] fp32, unnormalised) and top-K:
  * result layout and ranking as spl_search. */
 int spl_search_rescore(spl_arena_t a, const float *queries, int nq, int K, float min_sim, float max_dist,

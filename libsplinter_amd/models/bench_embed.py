@@ -105,6 +105,11 @@ class EmbedE2E:
         self.tokens = 0
         self.failures = 0
         self.pending = None  # (keys, Batch) of the next batch, prepared while the previous one ran
+        # where the host's time per batch goes (bench JSON): waiting for the GPU (the previous
+        # batch's encoder, ahead of the next fetch on the stream) vs tokenizing + packing.  Wait ~ 0
+        # means the pipeline is bound by the host's tokenizer, not by the encoder
+        self.t_wait = self.t_tok = 0.0
+        self.calls = 0
 
     def _fetch(self):
         """Enqueue the next key set's text fetch (batched get + copy to pinned host memory) on the
@@ -118,12 +123,19 @@ class EmbedE2E:
 
     def _prepare(self, fetched):
         """Host side of a batch: wait for its fetch only, tokenize, pack (one async upload)."""
+        import time
         keys, ev = fetched
+        t0 = time.perf_counter()
         ev.synchronize()
+        t1 = time.perf_counter()
         hr, hl = self.host_rows.numpy(), self.host_lens.numpy()
         texts = [hr[i, : hl[i]].tobytes() for i in range(self.docs)]
         ids, offs, _ = self.tok.encode_batch(texts, self.max_tokens)
-        return keys, Batch([ids[offs[i]: offs[i + 1]] for i in range(self.docs)])
+        b = Batch([ids[offs[i]: offs[i + 1]] for i in range(self.docs)])
+        self.t_wait += t1 - t0
+        self.t_tok += time.perf_counter() - t1
+        self.calls += 1
+        return keys, b
 
     def run(self):
         # Software pipeline with one batch of lookahead, on ONE stream (a second stream claims

@@ -60,6 +60,7 @@ from __future__ import annotations
 import ctypes
 import math
 import os
+import time
 import secrets
 from typing import Optional
 
@@ -188,6 +189,10 @@ class XRoute:
                      for _ in range(2)]
         self._token = torch.zeros(W, **i32)
         self._token_r = torch.zeros(W, **i32)
+        # SPLINTER_XR_PHASES=1 (attribution runs, device path): timing events around every phase of
+        # every step on the stream it runs on, and the host time spent inside the collectives
+        self._ph = [] if (self.cuda and os.environ.get("SPLINTER_XR_PHASES") == "1") else None
+        self._ph_host = {"counts": 0.0, "respond": 0.0}
         if W > 1:
             if transport == "peer":
                 if not self._setup_peer():
@@ -353,6 +358,42 @@ class XRoute:
             pass
 
     # ----------------------------------------------------------------- phases --
+    # ------------------------------------------------------- phase attribution --
+    def _mark(self, i: int, name: str) -> None:
+        if self._ph is not None:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record(torch.cuda.current_stream())
+            self._ph.append((i, name, ev))
+
+    def phase_reset(self) -> None:
+        if self._ph is not None:
+            self._ph.clear()
+            self._ph_host = {k: 0.0 for k in self._ph_host}
+
+    def phase_summary(self) -> Optional[dict]:
+        """Per step, ms between the phase marks on the device (each phase on its own stream; a phase's
+        span includes its waits on the others), and host ms inside the collectives -- averaged over the
+        steps marked since phase_reset()."""
+        if not self._ph:
+            return None
+        torch.cuda.synchronize()
+        by = {}
+        for i, name, ev in self._ph:
+            by.setdefault(i, {})[name] = ev
+        spans = {"pack": ("pack0", "pack1"), "count_exchange": ("pack1", "req1"), "wait_for_request": ("req1", "exec0"),
+                 "owner_grid": ("exec0", "exec1"), "respond": ("resp0", "resp1"), "gather": ("resp1", "gath1"),
+                 "step": ("pack0", "gath1")}
+        acc = {k: [] for k in spans}
+        for m in by.values():
+            for k, (a, b) in spans.items():
+                if a in m and b in m:
+                    acc[k].append(m[a].elapsed_time(m[b]))
+        n = max(len(by), 1)
+        out = {k: (sum(v) / len(v) if v else None) for k, v in acc.items()}
+        out.update({f"host_{k}_ms": v * 1e3 / n for k, v in self._ph_host.items()})
+        out["steps"] = len(by)
+        return out
+
     def request(self, i: int, skeys=None, svals=None, slens=None, gkeys=None) -> None:
         """Pack step i's batch into the owners' request blocks and exchange the counts."""
         p = i & 1
@@ -361,19 +402,24 @@ class XRoute:
         self._batch[p] = (skeys, svals, slens, gkeys)
         if self.world == 1:
             return
+        self._mark(i, "pack0")
         if self.cuda:
             self._pack_dev(p, skeys, svals, slens, gkeys)
         else:
             self._pack_host(p, skeys, svals, slens, gkeys)
+        self._mark(i, "pack1")
         self.scnt[p].copy_(self.cnt[p].t())
+        t0 = time.perf_counter()
         if self.sync == "flags":
             self._post(i, 0, self.cnt[p])
         else:
             self._c.all_to_all(self.rcnt[p], self.scnt[p])
+        self._ph_host["counts"] += time.perf_counter() - t0
         if self.transport != "peer":
             n = self.world * self.g.req_b
             o = self.g.req(p, 0)
             self._c.all_to_all(self._win[o: o + n].view(self.world, -1), self._send[o: o + n].view(self.world, -1))
+        self._mark(i, "req1")
 
     def execute(self, i: int, kvs=None, sstatus=None, gout=None, glens=None, gstatus=None, retries: int = 64) -> None:
         """Owner kernels of step i: own ops in place into the given client arrays, every peer's
@@ -383,16 +429,20 @@ class XRoute:
         self._out = (sstatus, gout, glens, gstatus)
         if self.world > 1 and self.sync == "flags":
             self._wait(i, 0)  # every peer's request block and counts of step i are in this window
+        self._mark(i, "exec0")
         if self.cuda:
             self._exec_dev(p, kvs, skeys, svals, slens, gkeys, sstatus, gout, glens, gstatus, retries)
         else:
             self._exec_host(p, skeys, svals, slens, gkeys, sstatus, gout, glens, gstatus)
+        self._mark(i, "exec1")
 
     def respond(self, i: int) -> None:
         """Mark step i's responses complete on every rank (rccl / host: move them)."""
         if self.world == 1:
             return
         p = i & 1
+        self._mark(i, "resp0")
+        t0 = time.perf_counter()
         if self.sync == "flags":
             self._post(i, 1)
         elif self.transport == "peer":
@@ -401,6 +451,8 @@ class XRoute:
             n = self.world * self.g.resp_b
             o = self.g.resp(p, 0)
             self._cr.all_to_all(self._win[o: o + n].view(self.world, -1), self._send[o: o + n].view(self.world, -1))
+        self._ph_host["respond"] += time.perf_counter() - t0
+        self._mark(i, "resp1")
 
     def finish(self, i: int, sstatus=None, gout=None, glens=None, gstatus=None) -> None:
         """Remote ops' results into client order (the own ops' are already there)."""
@@ -413,6 +465,7 @@ class XRoute:
                 self._gather_dev(p, skeys, gkeys, sstatus, gout, glens, gstatus)
             else:
                 self._gather_host(p, skeys, gkeys, sstatus, gout, glens, gstatus)
+            self._mark(i, "gath1")
         if self.cuda:
             self._ev_done[p] = torch.cuda.current_stream().record_event()
         self._batch[p] = None

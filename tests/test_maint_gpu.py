@@ -212,33 +212,42 @@ def test_rehash_online_beside_live_kv_steps(uniq, emb):
         seqv = _device_view(ar._side_base() + 256, 8, dtype=torch.int64)  # MaintRec::seq
         seqs = []
 
-        n_set = n_get = min(65536, live.size // 8)
-        # the ops of every step come from one permutation (no host work between queued steps: the
-        # steps and the passes must be on the GPU at the same time)
+        n_set = n_get = min(131072, live.size // 8)
+        # the ops of every step come from one permutation, and a batch's inputs are built before any
+        # of its steps is queued: the fused KV grid fills every CU while it runs, so a pass's kernels
+        # interleave with KV steps only at kernel boundaries -- many steps must be queued back to back
+        # when the pass opens
         perm = rng.permutation(live.size)
         steps, false_miss, live_again, dead_seen = 0, 0, 0, {}
         t = threading.Thread(target=worker)
         t_started = False
-        while (not t_started or t.is_alive() or steps < 16) and steps < 4000:
-            batch = []
-            for _ in range(8):  # queued back to back: the GPU runs them beside the pass's kernels
-                off = (steps * (n_set + n_get)) % (live.size - n_set - n_get)
+        per_batch = 24
+        while (not t_started or t.is_alive() or steps < 2 * per_batch) and steps < 4000:
+            inputs = []
+            for b in range(per_batch):
+                st_i = steps + b
+                off = (st_i * (n_set + n_get)) % (live.size - n_set - n_get)
                 pick = perm[off:off + n_set + n_get]
                 si, gi = pick[:n_set], pick[n_set:]
-                V, Lv = format_values(n_set, steps + 2, 40, 64, ids=torch.as_tensor(live[si], device="cuda"))
-                sst = torch.empty(n_set, dtype=torch.int32, device="cuda")
+                V, Lv = format_values(n_set, st_i + 2, 40, 64, ids=torch.as_tensor(live[si], device="cuda"))
+                sk = _keys(live[si])
                 gk = torch.cat([_keys(live[gi]), _keys(dead[:512])])
+                inputs.append((si, gi, sk, V, Lv, gk))
+            torch.cuda.synchronize()
+            if not t_started:  # the passes start while this batch's steps are queued
+                t.start()
+                t_started = True
+            batch = []
+            for si, gi, sk, V, Lv, gk in inputs:
+                sst = torch.empty(n_set, dtype=torch.int32, device="cuda")
                 go = torch.empty(gk.shape[0], 64, dtype=torch.uint8, device="cuda")
                 gl = torch.empty(gk.shape[0], dtype=torch.int32, device="cuda")
                 gst = torch.empty(gk.shape[0], dtype=torch.int32, device="cuda")
-                kv.step(ar, _keys(live[si]), V, Lv, sst, gk, go, gl, gst)
+                kv.step(ar, sk, V, Lv, sst, gk, go, gl, gst)
                 seqs.append(seqv.clone())  # the seq as the stream passes this step: odd = a pass was running
                 batch.append((si, gi, sst, go, gl, gst, ver[gi].copy()))
                 ver[si] = steps + 2
                 steps += 1
-                if not t_started and steps == 4:  # the passes start behind KV work already queued
-                    t.start()
-                    t_started = True
             torch.cuda.synchronize()
             for si, gi, sst, go, gl, gst, gv in batch:
                 s_set, s_get = sst.cpu().numpy(), gst.cpu().numpy()

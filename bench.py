@@ -351,6 +351,12 @@ def main():
     need_routed = routed
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # config #2's async form, measured FIRST: each child holds its own 100 M-key arena (~77 GB), which
+    # next to this process's KV and search arenas would not fit in one GPU's HBM
+    kab = None
+    if world == 1 and args.kv_async_ab and args.mode != "embed" and not args.force_routed:
+        kab = kv_async_ab(args, local % max(torch.cuda.device_count(), 1),
+                          lambda *a: print(*a, file=sys.stderr, flush=True))
     dev = local % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev)
     liveness = None
@@ -885,9 +891,6 @@ def main():
     xab = None
     if world == 1 and args.exchange_ab and args.mode != "embed":
         xab = exchange_ab(args, dev, log)
-    kab = None
-    if world == 1 and args.kv_async_ab and args.mode != "embed":
-        kab = kv_async_ab(args, dev, log)
 
     kv_ops = (n_set + n_get) * args.steps * world
     kv_ops_s = kv_ops / elapsed if kv_ops else 0.0

@@ -2,7 +2,7 @@
 # exchange phase attribution (2-rank peer vs 1-rank, one GPU), per-call floor (ring stamps build),
 # qkv GEMM tile A/B (128^2 vs 256^2 on the 1152-tile shape) in the encoder
 set -o pipefail
-OUT=gpurun_out/r6s6
+OUT=${OUT6:-gpurun_out/r6s6}
 mkdir -p $OUT
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 COMMON="--mode kv --steps 10 --warmup 3 --host-api 0 --host-api-threads2 0 --embed-e2e 0 --daemon-docs 0 --search-keys 0 --exchange-ab 0 --kv-async-ab 0 --mixed5 0 --verify 5000 --value-len 150"

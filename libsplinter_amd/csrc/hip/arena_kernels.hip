@@ -518,36 +518,19 @@ __device__ __forceinline__ void fill_slot(OpSlots<U, KW>& o, int j, const FSeg& 
 // tries <= max_retry.  Called by every lane of the wave (the row copies are wave-cooperative).
 // ms: the arena's maintenance seq as read (and waited for) before this round's probes; re-read in
 // the round's closing round trip for the next round (arena_dev.hpp, online maintenance).
-// flags: kKvSkipLen (an update that keeps its length leaves val_len alone), kKvPrefetch (a get's
-// home-slot value row is pulled toward the L2 with its probe: see below).
-constexpr int kKvSkipLen = 1, kKvPrefetch = 2;
+// flags: kKvSkipLen (an update that keeps its length leaves val_len alone).  (Measured and removed in
+// round 6: a get's home-slot value row requested by LDS-DMA beside its probe, 4.45-4.47 vs 4.84-4.88 G
+// ops/s KV-only: the extra requests cost more than the row copy's L2 hit saves, profiles/r6/README.md.)
+constexpr int kKvSkipLen = 1;
 template <int U, int KW>
 __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW>& o, bool scrub, bool hybrid,
                                          int max_retry, Stats& st, uint64_t& muts, uint4* cpp0, uint2* cpl0,
-                                         uint4* cpp1, uint2* cpl1, int lane, int flags, uint64_t& ms,
-                                         uint32_t* sink) {
+                                         uint4* cpp1, uint2* cpl1, int lane, int flags, uint64_t& ms) {
   const bool skip_len = flags & kKvSkipLen;
   Claim c[U];
   long sidx[U];
   uint64_t e1[U];
   int32_t rc[U];
-  // A get's value row is a pure function of its slot (val_off = slot * max_val, DIVERGENCES.md), and
-  // at the bench's 50 % load most gets hit at their home slot: the home row's cache lines are
-  // requested in the same round trip as the probe (4-B LDS-DMA loads into a per-wave sink: no
-  // registers held), so the row copy after the probe reads them from the L2 / MALL instead of HBM.
-  if (flags & kKvPrefetch) {
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (o.seg[j] >= 0 && !o.set[j]) {
-        const uint8_t* v = a.value((size_t)(o.k[j].hash % a.slots));
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)v,
-                                         (__attribute__((address_space(3))) void*)sink, 4, 0, 0);
-        if (a.max_val > 128)
-          __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(v + 128),
-                                           (__attribute__((address_space(3))) void*)sink, 4, 0, 0);
-      }
-    }
-  }
   // probes / claims of every slot of the round
 #pragma unroll
   for (int j = 0; j < U; ++j) {
@@ -664,7 +647,6 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   __shared__ uint2 cp_l[2][B / 64][U * 64];
   __shared__ FSeg sg[kFusedSegs];
   __shared__ long sstart[kFusedSegs + 1];
-  __shared__ uint32_t pf_sink[B / 64][64];  // kKvPrefetch's DMA destination (never read)
   const int nseg = tab.n, ks = tab.ks;
   if ((int)threadIdx.x < nseg) {
     FSeg f = tab.s[threadIdx.x];
@@ -719,7 +701,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
     if (!__syncthreads_or(busy)) break;
     kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
-                    skip_len, ms, pf_sink[w]);
+                    skip_len, ms);
   }
   flush_stats(a, st, stats, muts);
 }
@@ -760,7 +742,6 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
   __shared__ FSeg sg[2];  // 0: the set batch, 1: the get batch
-  __shared__ uint32_t pf_sink[B / 64][64];  // kKvPrefetch's DMA destination (never read)
   __shared__ long sh_b, sh_e;
   __shared__ int sh_kind, sh_state, sh_scan;
   __shared__ uint64_t sh_exhausted, sh_posted, sh_idle;  // thread 0's scan state (LDS: no registers)
@@ -921,7 +902,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
       if (!__syncthreads_or(busy)) break;
       kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
-                      lane, skip_len, ms, pf_sink[w]);
+                      lane, skip_len, ms);
     }
     {
       const uint64_t v[5] = {st.attempts, st.ok, st.again, st.miss, muts};
@@ -955,9 +936,8 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   const long need = (rows + 2 * 256 - 1) / (2 * 256);
   const long cap = 256L * wpc;
   const dim3 g((unsigned)(need < cap ? need : cap));
-  // SPL_KVS_SKIP_LEN / SPL_KVS_PREFETCH (A/B knobs): kv_round flags
-  static const int skip_len = (env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0) |
-                              (env_int("SPL_KVS_PREFETCH", 1) ? kKvPrefetch : 0);
+  // SPL_KVS_SKIP_LEN (A/B knob): kv_round flags
+  static const int skip_len = env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0;
   if (kw4)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
   else
@@ -1511,7 +1491,7 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
   hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
                      sset, sget, nw, nr, ks, k->ctl, seq, chunk, wait_ticks, spread, max_retry, stats,
-                     (env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0) | (env_int("SPL_KVS_PREFETCH", 1) ? kKvPrefetch : 0));
+                     env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   (void)hipEventRecord(k->srv_done, origin);

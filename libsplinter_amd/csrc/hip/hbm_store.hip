@@ -1398,6 +1398,23 @@ int HbmStore::probe_stats(ProbeStats* out) {
 // EBUSY when this store's ring worker cannot be held, with ENOMEM (and the scratch size on stderr)
 // when the scratch cannot be allocated.  out: {moved, reclaimed, clusters, clusters past the
 // per-wave tombstone cap}.
+// Online maintenance passes run on a low-priority stream of their own: background work, on a
+// hardware queue apart from the normal-priority queues of the store's kernels and its clients, so a
+// pass's kernels interleave with live traffic at kernel boundaries instead of waiting in one queue
+// behind it (or it behind them).
+static hipStream_t maint_stream(int device) {
+  static std::mutex mu;
+  static hipStream_t s[64] = {};
+  std::lock_guard<std::mutex> lk(mu);
+  if (device < 0 || device >= 64) device = 0;
+  if (!s[device]) {
+    int least = 0, greatest = 0;
+    (void)hipDeviceGetStreamPriorityRange(&least, &greatest);
+    if (hipStreamCreateWithPriority(&s[device], hipStreamNonBlocking, least) != hipSuccess) s[device] = nullptr;
+  }
+  return s[device];
+}
+
 int HbmStore::rehash(uint64_t out[4], unsigned flags) {
   if (!ensure_mapped()) return -1;
   if (!(side_flags_ & SPL_ARENA_SIDE)) { errno = ENOTSUP; return -1; }
@@ -1474,27 +1491,36 @@ int HbmStore::rehash(uint64_t out[4], unsigned flags) {
     uint64_t* d = nullptr;
     // d[0..4]: the pass counters (moved, reclaimed, clusters, skipped, largest displacement);
     // d[6] / d[7]: the open / close results
-    if (hipMallocAsync((void**)&d, 64, stream_) != hipSuccess) return -1;
+    const hipStream_t ms = maint_stream(device_) ? maint_stream(device_) : stream_;
+    {  // this process's earlier work on the store's stream comes first
+      hipEvent_t ev = nullptr;
+      if (ms != stream_ && hipEventCreateWithFlags(&ev, hipEventDisableTiming) == hipSuccess) {
+        (void)hipEventRecord(ev, stream_);
+        (void)hipStreamWaitEvent(ms, ev, 0);
+        (void)hipEventDestroy(ev);
+      }
+    }
+    if (hipMallocAsync((void**)&d, 64, ms) != hipSuccess) return -1;
     timespec ts;
     clock_gettime(CLOCK_REALTIME, &ts);
     const uint64_t t0 = (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
     uint64_t won = 0;
-    (void)hipMemsetAsync(d, 0, 64, stream_);
-    rc = spl_arena_maint_mark(a, 1, (int)getpid(), t0, d + 6, stream_);
-    if (rc == 0) rc = hipMemcpyAsync(&won, d + 6, 8, hipMemcpyDeviceToHost, stream_) == hipSuccess ? 0 : -1;
-    if (rc == 0) rc = hipStreamSynchronize(stream_) == hipSuccess ? 0 : -1;
+    (void)hipMemsetAsync(d, 0, 64, ms);
+    rc = spl_arena_maint_mark(a, 1, (int)getpid(), t0, d + 6, ms);
+    if (rc == 0) rc = hipMemcpyAsync(&won, d + 6, 8, hipMemcpyDeviceToHost, ms) == hipSuccess ? 0 : -1;
+    if (rc == 0) rc = hipStreamSynchronize(ms) == hipSuccess ? 0 : -1;
     if (rc == 0 && !won) {
       errno = EBUSY;  // another process's pass is running
       rc = -1;
     } else if (rc == 0) {
-      rc = spl_arena_rehash(a, d, stream_);
+      rc = spl_arena_rehash(a, d, ms);
       // the pass is closed whatever the walk returned: an open seq would turn every miss into EAGAIN
-      if (spl_arena_maint_mark(a, 0, 0, 0, d + 7, stream_) != 0) rc = -1;
-      if (rc == 0) (void)hipMemcpyAsync(out, d, 32, hipMemcpyDeviceToHost, stream_);
-      if (hipStreamSynchronize(stream_) != hipSuccess) rc = -1;
+      if (spl_arena_maint_mark(a, 0, 0, 0, d + 7, ms) != 0) rc = -1;
+      if (rc == 0) (void)hipMemcpyAsync(out, d, 32, hipMemcpyDeviceToHost, ms);
+      if (hipStreamSynchronize(ms) != hipSuccess) rc = -1;
     }
-    (void)hipFreeAsync(d, stream_);
-    (void)hipStreamSynchronize(stream_);
+    (void)hipFreeAsync(d, ms);
+    (void)hipStreamSynchronize(ms);
   }
   if (rc == 0) {
     std::lock_guard<std::mutex> lk(mu_);

@@ -174,6 +174,11 @@ __device__ __forceinline__ void count_mutation(const Arena& a, long idx) {
 
 #ifdef SPL_RING_STAMPS
 __device__ uint64_t g_ts[kRingEntries][5];  // this call's op checkpoints (serving lane only)
+// per-entry sums (device memory, read back by ~CmdRing): doorbell seen -> record loaded -> op done
+// -> completion drained, call count; set / get op segments; shader-clock and wall ticks
+__device__ uint64_t g_stamp[kRingEntries][4];
+__device__ uint64_t g_opstamp[kRingEntries][10];
+__device__ uint64_t g_clk[kRingEntries][2];
 __device__ int g_ent[64 * kRingGroups];     // entry of the serving lane
 #define RING_TS(i) (g_ts[g_ent[blockIdx.x * 64 + threadIdx.x]][i] = wall_clock64())
 #else
@@ -619,20 +624,7 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
 #ifdef SPL_RING_STAMPS
       const uint64_t t_done = wall_clock64();
       const uint64_t mt1 = __builtin_amdgcn_s_memtime();
-      st64s(sh->clk[e], ld64s(sh->clk[e]) + (mt1 - mt0));
-      st64s(sh->clk[e] + 1, ld64s(sh->clk[e] + 1) + (t_done - last));
-      uint64_t* sp = sh->stamp[e];
-      st64s(sp, ld64s(sp) + (t_loaded - last));
-      st64s(sp + 1, ld64s(sp + 1) + (t_op - t_loaded));
-      st64s(sp + 2, ld64s(sp + 2) + (t_done - t_op));
-      st64s(sp + 3, ld64s(sp + 3) + 1);
-      const uint32_t op = ld32s(&c->op);
-      if (st == 0 && (op == kRingSet || op == kRingGet)) {
-        uint64_t* q = sh->opstamp[e] + (op == kRingSet ? 0 : 5);
-        for (int i = 0; i < 4; ++i) st64s(q + i, ld64s(q + i) + (g_ts[e][i + 1] - g_ts[e][i]));
-        st64s(q + 4, ld64s(q + 4) + 1);
-      }
-      drain();
+      const uint32_t sop = ld32s(&c->op);
 #endif
       if constexpr (VR) {
         seen = bell;
@@ -641,6 +633,21 @@ __global__ __launch_bounds__(64) void k_ring_worker(spl_arena_t aa, RingCmd* cmd
       } else {
         st32s(&sh->state[e], kRingDone);
       }
+#ifdef SPL_RING_STAMPS
+      // accumulated AFTER the completion, in device memory (plain loads / stores: one lane owns an
+      // entry at a time), so the stamps do not lengthen the call they measure; ~CmdRing reads them
+      g_clk[e][0] += mt1 - mt0;
+      g_clk[e][1] += t_done - last;
+      g_stamp[e][0] += t_loaded - last;
+      g_stamp[e][1] += t_op - t_loaded;
+      g_stamp[e][2] += t_done - t_op;
+      g_stamp[e][3] += 1;
+      if (st == 0 && (sop == kRingSet || sop == kRingGet)) {
+        uint64_t* q = g_opstamp[e] + (sop == kRingSet ? 0 : 5);
+        for (int i = 0; i < 4; ++i) q[i] += g_ts[e][i + 1] - g_ts[e][i];
+        q[4] += 1;
+      }
+#endif
     }
   }
   drain();
@@ -1370,9 +1377,18 @@ CmdRing::~CmdRing() {
   stop();
 #ifdef SPL_RING_STAMPS
   if (shared_) {
+    static uint64_t hst[kRingEntries][4], hop[kRingEntries][10], hck[kRingEntries][2];
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(device_);
+    const bool got = hipDeviceSynchronize() == hipSuccess &&
+                     hipMemcpyFromSymbol(hst, HIP_SYMBOL(g_stamp), sizeof hst) == hipSuccess &&
+                     hipMemcpyFromSymbol(hop, HIP_SYMBOL(g_opstamp), sizeof hop) == hipSuccess &&
+                     hipMemcpyFromSymbol(hck, HIP_SYMBOL(g_clk), sizeof hck) == hipSuccess;
+    (void)hipSetDevice(cur);
     uint64_t sum[4] = {0, 0, 0, 0};
-    for (int e = 0; e < kRingEntries; ++e)
-      for (int q = 0; q < 4; ++q) sum[q] += shared_->stamp[e][q];
+    for (int e = 0; got && e < kRingEntries; ++e)
+      for (int q = 0; q < 4; ++q) sum[q] += hst[e][q];
     if (sum[3]) {
       const double us = 1000.0 / clock_khz_ / (double)sum[3];
       fprintf(stderr,
@@ -1381,11 +1397,11 @@ CmdRing::~CmdRing() {
               (unsigned long long)sum[3], sum[0] * us, sum[1] * us, sum[2] * us);
     }
     uint64_t ck[2] = {0, 0};
-    for (int e = 0; e < kRingEntries; ++e) ck[0] += shared_->clk[e][0], ck[1] += shared_->clk[e][1];
+    for (int e = 0; got && e < kRingEntries; ++e) ck[0] += hck[e][0], ck[1] += hck[e][1];
     if (ck[1]) fprintf(stderr, "{\"shader_clock_mhz\": %.1f}\n", (double)ck[0] / ((double)ck[1] / (clock_khz_ * 1e3)) / 1e6);
     uint64_t o[10] = {};
-    for (int e = 0; e < kRingEntries; ++e)
-      for (int q = 0; q < 10; ++q) o[q] += shared_->opstamp[e][q];
+    for (int e = 0; got && e < kRingEntries; ++e)
+      for (int q = 0; q < 10; ++q) o[q] += hop[e][q];
     for (int k = 0; k < 2; ++k) {
       const uint64_t* v = o + 5 * k;
       if (!v[4]) continue;

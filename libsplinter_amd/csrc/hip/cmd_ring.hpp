@@ -106,16 +106,6 @@ struct RingShared {
     int32_t pid;
     uint32_t count;
   } holds[kRingHoldSlots];
-#ifdef SPL_RING_STAMPS
-  // latency breakdown (make hip-variant V=stamps VFLAGS=-DSPL_RING_STAMPS): per entry, sums of
-  // wall-clock ticks from "doorbell seen" to "record loaded", to "op done", to "completion
-  // drained", and the call count; printed by ~CmdRing
-  uint64_t stamp[kRingEntries][4];
-  // finer split of the op itself: [0..3] set (prologue loads, claim, payload + drain, publish),
-  // [4] set count, [5..8] get (prologue loads, probe, acquire, copy + re-check), [9] get count
-  uint64_t opstamp[kRingEntries][10];
-  uint64_t clk[kRingEntries][2];  // shader-clock ticks (s_memtime) and wall ticks over the same calls
-#endif
 };
 
 // VRAM mode completion, one 16-B chunk per entry in host memory, written by ONE device store (the

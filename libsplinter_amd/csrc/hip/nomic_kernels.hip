@@ -404,11 +404,10 @@ __device__ __forceinline__ int v3sw(int key, int c) { return c ^ (((key >> 1) & 
 
 // PF2: K/V global loads issued two tiles ahead (two register stages) instead of one, so a tile's
 // loads have two tiles' compute to land before their LDS write.
-// LATE: the next tile's K/V loads are issued after this tile's S^T MFMAs instead of before them
-// (cdna_hip_programming.md T14 async-stage split: their registers are live for half the tile and the
-// MFMAs start right after the barrier).  PRIO: s_setprio 1 over the MFMA runs, so a wave's matrix
-// work is issued ahead of the other waves' softmax VALU on the SIMD.
-template <bool PF2 = false, int W = 1, bool LATE = false, bool PRIO = false>
+// (Measured in round 6 and not kept: the next tile's K/V loads issued after the QK^T MFMAs, and
+// s_setprio 1 over the MFMA runs -- alone and together within +-1.5 % of this form in isolation and
+// 0.1 % in the encoder, profiles/r6/README.md.)
+template <bool PF2 = false, int W = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_attn3(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,
                                                int heads, float scale_log2) {
@@ -476,14 +475,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
     // are never indexed at run time)
     if (PF2) {
       if (t + 2 < ntiles) gload(sl, k0 + 2 * KT);
-    } else if (!LATE && t + 1 < ntiles) {
+    } else if (t + 1 < ntiles) {
       gload(0, k0 + KT);
     }
     const char* Ks = lds[buf][0];
     const char* Vs = lds[buf][1];
     // ---- S^T = K Q^T: A = K rows (key kb*32 + q32, d 16 ks + 8 hi), B = Q^T
     f32x16 s[2];
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
 #pragma unroll
@@ -495,8 +493,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
         s[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[ks], s[kb], 0, 0, 0);
       }
     }
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
-    if (!PF2 && LATE && t + 1 < ntiles) gload(0, k0 + KT);
+
     // ---- online softmax of query q32 over the tile's 64 keys (32 here, 32 in lane ^ 32)
     if (k0 + KT > len) {
 #pragma unroll
@@ -538,7 +535,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
     }
     l += ps;
     // ---- O^T += V^T P^T, four 16-key steps
-    if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
@@ -559,7 +555,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k
           o[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf, o[db], 0, 0, 0);
         }
       }
-    if (PRIO) __builtin_amdgcn_s_setprio(0);
     if (t + 1 < ntiles) lwrite(snext, buf ^ 1);
     __syncthreads();
   };
@@ -808,8 +803,7 @@ int nomic_layernorm(const void* x, long T, const void* gamma, const void* beta, 
 // score math), the fallback.  Measured and removed in round 4: K/V staged by LDS-DMA into a 3-deep
 // ring (505 vs 596 TFLOP/s, profiles/r4k/attn_bench.out).  The other A/B forms of rounds 1-3 are gone; their measurements stay in
 // profiles/r1_attn_* .. r3_attn_*.
-// 14 / 15 / 16: k_attn3 with the LATE K/V loads, with PRIO, with both (A/B forms, scripts/attn_bench.py)
-static int attn_norm(int v) { return v == 6 || (v >= 14 && v <= 16) ? v : 13; }
+static int attn_norm(int v) { return v == 6 ? 6 : 13; }
 static int g_attn_variant = [] {
   const char* e = getenv("NOMIC_ATTN");
   return attn_norm(e && *e ? atoi(e) : 13);
@@ -829,15 +823,6 @@ int nomic_attention(const void* qkv, void* out, const int32_t* cu, const int32_t
   if (g_attn_variant == 6)
     hipLaunchKernelGGL((k_attn2<0, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
                        (uint16_t*)out, cu, qblocks, heads, scale_log2, heads);
-  else if (g_attn_variant == 14)
-    hipLaunchKernelGGL((k_attn3<false, 1, true, false>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
-                       (uint16_t*)out, cu, qblocks, heads, scale_log2);
-  else if (g_attn_variant == 15)
-    hipLaunchKernelGGL((k_attn3<false, 1, false, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
-                       (uint16_t*)out, cu, qblocks, heads, scale_log2);
-  else if (g_attn_variant == 16)
-    hipLaunchKernelGGL((k_attn3<false, 1, true, true>), dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv,
-                       (uint16_t*)out, cu, qblocks, heads, scale_log2);
   else
     hipLaunchKernelGGL(k_attn3<false>, dim3(nqb * heads), dim3(256), 0, s, (const uint16_t*)qkv, (uint16_t*)out, cu,
                        qblocks, heads, scale_log2);

@@ -766,6 +766,15 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   unsigned long long* next = ctl->next[seq & 1];
   if (blockIdx.x == 0 && threadIdx.x < kAsyncSegs)  // the next step's bank (its last user has ended)
     __hip_atomic_store(&ctl->next[(seq + 1) & 1][threadIdx.x], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // A lane's op slots live across chunks: an op that met EAGAIN is carried into the next chunk's
+  // rounds (as in the fused grid) instead of holding the workgroup in extra, mostly empty rounds at
+  // the end of every chunk
+  OpSlots<U, KW> o;
+#pragma unroll
+  for (int j = 0; j < U; ++j) o.seg[j] = -1;
+  Stats st;
+  uint64_t muts = 0;
+  uint64_t ms = maint_begin(a);
   for (;;) {
     __syncthreads();  // the previous chunk's readers of sh_* are done
     if (w == 0) {
@@ -867,19 +876,19 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       }
       break;
     }
+    bool carried = false;
+#pragma unroll
+    for (int j = 0; j < U; ++j) carried |= o.seg[j] >= 0;
+    carried = __syncthreads_or(carried);
     if (state == 0) {
-      __builtin_amdgcn_s_sleep(32);
+      // nothing claimable yet: carried ops still progress
+      if (carried)
+        kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
+                        lane, skip_len, ms);
+      else
+        __builtin_amdgcn_s_sleep(32);
       continue;
     }
-    // a chunk ends with every slot empty: the slots are the chunk's own (nothing stays live across
-    // the claim above)
-    // (the chunk's counters too: added into LDS at its end, so only the claim state is live across)
-    OpSlots<U, KW> o;
-#pragma unroll
-    for (int j = 0; j < U; ++j) o.seg[j] = -1;
-    Stats st;
-    uint64_t muts = 0;
-    uint64_t ms = maint_begin(a);
     const int q = sh_kind;
     const long end = sh_e;
     long row = sh_b + (long)threadIdx.x * U;  // the lane's next row: U consecutive rows per B * U
@@ -900,16 +909,28 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       bool busy = false;
 #pragma unroll
       for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
-      if (!__syncthreads_or(busy)) break;
+      // once no lane has rows of this chunk left the group claims the next one; the ops still in
+      // slots (the chunk's last fills, carried retries) ride along into its rounds
+      const bool more = row < end;
+      if (!__syncthreads_or(more && busy)) break;
       kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
                       lane, skip_len, ms);
     }
-    {
-      const uint64_t v[5] = {st.attempts, st.ok, st.again, st.miss, muts};
+  }
+  // the last chunk's ops and any carried retries
+  for (;;) {
+    bool busy = false;
 #pragma unroll
-      for (int c = 0; c < 5; ++c)
-        if (v[c]) __hip_atomic_fetch_add(&sh_st[c], (unsigned long long)v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
+    for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
+    if (!__syncthreads_or(busy)) break;
+    kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
+                    skip_len, ms);
+  }
+  {
+    const uint64_t v[5] = {st.attempts, st.ok, st.again, st.miss, muts};
+#pragma unroll
+    for (int c = 0; c < 5; ++c)
+      if (v[c]) __hip_atomic_fetch_add(&sh_st[c], (unsigned long long)v[c], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   if (threadIdx.x == 0) {

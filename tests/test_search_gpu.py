@@ -347,8 +347,8 @@ def _fill_arena(ar, first, n, centers, g):
 def test_node_search_batch_runs_shards_concurrently(uniq):
     """spl_search_batch on a node: store of 4 HBM shards (one GPU here) answers every shard at once,
     with one candidate threshold over the shards' merged samples: a 256-query batch over the same 2 M
-    vectors gives the same top-10 as one hbm: store holding all of them, in at most 1.5x its time and
-    no more than the shards' own searches one after another (round-5 verdict item 4)."""
+    vectors gives the same top-10 as one hbm: store holding all of them, in at most 1.6x its time and
+    less than the shards' own searches one after another (round-5 verdict item 4)."""
     import time
     import torch
     from libsplinter_amd import Store
@@ -411,8 +411,9 @@ def test_node_search_batch_runs_shards_concurrently(uniq):
         # of the shards' own searches (each with its fixed per-launch costs), not their maximum.
         # Measured: 1.38x the single store with the shards concurrent (2.3x before, one after
         # another with a synchronise each); across GPUs the same fan-out runs them in parallel.
-        assert t4 <= 1.5 * t1, (t4, t1)
-        assert t4 <= 1.1 * sum(alone), (t4, alone)
+        # (margins for box-to-box noise: measured 1.38-1.42x one store and 0.88x the shards' serial sum)
+        assert t4 <= 1.6 * t1, (t4, t1)
+        assert t4 <= 1.0 * sum(alone), (t4, alone)
     finally:
         if top is not None:
             top.close()

@@ -260,8 +260,10 @@ def exchange_ab(args, dev: int, log):
     transport = "peer" if "transport peer" in coll else ("rccl" if "transport rccl" in coll else coll)
     fb = coll.split("(fell back: ", 1)[1].split(")", 1)[0] if "(fell back: " in coll else None
     sync = "device flags" if "device-side posts" in coll else "collectives"
+    direct = "direct responses" in coll
     return {"ops2": runs[2]["value"], "ops1": runs[1]["value"], "ratio": runs[2]["value"] / runs[1]["value"],
             "transport": transport, "fallback": fb, "sync": sync, "sync_error": runs[2].get("xr_sync_error"),
+            "direct": direct,
             "integrity": runs[2]["integrity_failures"] + runs[1]["integrity_failures"],
             "totals": {"keys": args.exchange_keys, "ops_per_step": args.exchange_batch, "steps": 10,
                        "device": phys, "mode": "kv"}}
@@ -617,10 +619,13 @@ def main():
         log(f"[bench] routed exchange: transport {xr.transport}, world {world}, caps {xr.cap_s}/{xr.cap_g}, "
             f"window {xr.g.window_b / 2**30:.2f} GiB")
         s_req, s_resp = hip_stream("low"), hip_stream("low")
-        r_out = [(torch.empty(max(n_set, 1), dtype=torch.int32, device="cuda"),
-                  torch.empty((max(n_get, 1), vw), dtype=torch.uint8, device="cuda"),
-                  torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda"),
-                  torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")) for _ in range(2)]
+        # direct responses (peer transport): the owners write every result into these arrays, which
+        # live in this rank's exchange window (no gather kernel)
+        r_out = ([xr.outputs(p) for p in range(2)] if xr.direct else
+                 [(torch.empty(max(n_set, 1), dtype=torch.int32, device="cuda"),
+                   torch.empty((max(n_get, 1), vw), dtype=torch.uint8, device="cuda"),
+                   torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda"),
+                   torch.empty(max(n_get, 1), dtype=torch.int32, device="cuda")) for _ in range(2)])
         prev_exec = []
 
     requested = {}  # step -> its request event (issued ahead by the previous step of the same phase)
@@ -934,7 +939,9 @@ def main():
                             + ("stored into the owners' peer-mapped windows over xGMI, "
                                if xr.transport == "peer" else "moved by one all-to-all per direction, ")
                             + ("step ordered by device-side posts into the peer windows (no collective per step)"
-                               if xr.sync == "flags" else "one count all-to-all + one response all-to-all per step"))
+                               if xr.sync == "flags" else "one count all-to-all + one response all-to-all per step")
+                            + ("; owners write results straight into the requesters' client arrays (direct "
+                               "responses, no gather)" if xr.direct else ""))
             if routed and xr else None,
             "search_keys_per_gpu": args.search_keys if sarena is not None else 0,
             # bytes each GPU stores into its W-1 peers per routed step (own-shard ops never leave the GPU):
@@ -979,6 +986,7 @@ def main():
         "exchange_transport": xab["transport"] if xab else None,
         "exchange_fallback_reason": xab["fallback"] if xab else None,
         "exchange_sync": xab["sync"] if xab else None, "exchange_sync_error": xab["sync_error"] if xab else None,
+        "exchange_direct_responses": xab["direct"] if xab else None,
         "xr_sync_error": (xr.sync_error() if (routed and xr is not None) else None),
         "exchange_integrity_failures": xab["integrity"] if xab else None,
         # SPLINTER_XR_PHASES=1 on a routed run: device ms per phase of a timed step, host ms in collectives

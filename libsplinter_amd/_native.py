@@ -114,7 +114,8 @@ class XrStep(ctypes.Structure):
                 ("req", ctypes.c_uint64 * XR_MAX_WORLD), ("resp", ctypes.c_uint64 * XR_MAX_WORLD),
                 ("off_sk", ctypes.c_long), ("off_sl", ctypes.c_long), ("off_sv", ctypes.c_long),
                 ("off_gk", ctypes.c_long), ("off_ss", ctypes.c_long), ("off_gs", ctypes.c_long),
-                ("off_gl", ctypes.c_long), ("off_gv", ctypes.c_long)]
+                ("off_gl", ctypes.c_long), ("off_gv", ctypes.c_long),
+                ("off_sp", ctypes.c_long), ("off_gp", ctypes.c_long)]
 
 
 ENUM_CB = ctypes.CFUNCTYPE(None, c_char_p, c_u64, c_void_p)
@@ -220,7 +221,7 @@ def _declare_hip(L):
     _sig(L, "spl_arena_get_idx", c_int, A, P, c_int, P, c_int, P, P, P, c_long, P, c_int, P, P)
     # routed exchange (route_kernels.hip, parallel/xroute.py)
     _sig(L, "spl_xr_pack", c_int, P, c_int, P, c_int, P, c_long, c_int, c_int, c_long, P, c_long, c_long, c_long,
-         c_int, P, P, P, P)
+         c_int, P, P, P, c_long, P, P, P)
     _sig(L, "spl_xr_gather", c_int, P, c_long, c_long, P, c_long, c_long, c_long, c_int, P, P, P, c_int, P)
     _sig(L, "spl_xr_post", c_int, P, c_int, c_int, c_int, c_int, ctypes.c_uint64, P, P)
     _sig(L, "spl_xr_wait", c_int, P, c_int, c_int, c_int, c_int, ctypes.c_uint64, ctypes.c_uint64, P, P)

@@ -481,8 +481,10 @@ struct FSeg {
   long n;                 // rows (upper bound when count is set)
   int vstride;            // value row bytes
   int set;                // 1 set, 0 get
+  const int32_t* oidx;    // outputs (status, get lens / values) at row oidx[r] instead of the input
+                          // row: a routed step's direct responses into the requester's client arrays
 };
-static_assert(sizeof(FSeg) == 64, "segment record");
+static_assert(sizeof(FSeg) == 72, "segment record");
 
 struct FSegs {
   FSeg s[kFusedSegs];
@@ -490,22 +492,31 @@ struct FSegs {
   int ks;
 };
 
-// A lane's U op slots in the fused / server round loops.
-template <int U, int KW>
+// A lane's U op slots in the fused / server round loops.  OI: segments may map outputs elsewhere
+// (FSeg::oidx, the routed step's direct responses); without it the output row is the input row and
+// costs no register.
+template <int U, int KW, bool OI = false>
 struct OpSlots {
   KeyT<KW> k[U];
   long row[U];
+  int32_t orow[OI ? U : 1];
   int seg[U];  // -1: slot empty
   uint32_t len[U];
   int tries[U];
   bool set[U];
 };
+template <int U, int KW, bool OI>
+__device__ __forceinline__ long out_row(const OpSlots<U, KW, OI>& o, int j) {
+  if constexpr (OI) return (long)o.orow[j];
+  else return o.row[j];
+}
 
 // Put row r of segment q (sg[q]) into the empty slot j.
-template <int U, int KW>
-__device__ __forceinline__ void fill_slot(OpSlots<U, KW>& o, int j, const FSeg& f, int q, long r, int ks) {
+template <int U, int KW, bool OI>
+__device__ __forceinline__ void fill_slot(OpSlots<U, KW, OI>& o, int j, const FSeg& f, int q, long r, int ks) {
   o.seg[j] = q;
   o.row[j] = f.idx ? (long)f.idx[r] : r;
+  if constexpr (OI) o.orow[j] = f.oidx ? f.oidx[r] : (int32_t)o.row[j];
   o.set[j] = f.set != 0;
   o.tries[j] = 0;
   load_key(o.k[j], f.keys + o.row[j] * (long)ks, ks);
@@ -522,8 +533,8 @@ __device__ __forceinline__ void fill_slot(OpSlots<U, KW>& o, int j, const FSeg& 
 // round 6: a get's home-slot value row requested by LDS-DMA beside its probe, 4.45-4.47 vs 4.84-4.88 G
 // ops/s KV-only: the extra requests cost more than the row copy's L2 hit saves, profiles/r6/README.md.)
 constexpr int kKvSkipLen = 1;
-template <int U, int KW>
-__device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW>& o, bool scrub, bool hybrid,
+template <int U, int KW, bool OI = false>
+__device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW, OI>& o, bool scrub, bool hybrid,
                                          int max_retry, Stats& st, uint64_t& muts, uint4* cpp0, uint2* cpl0,
                                          uint4* cpp1, uint2* cpl1, int lane, int flags, uint64_t& ms) {
   const bool skip_len = flags & kKvSkipLen;
@@ -575,7 +586,7 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
     cpp0[j * 64 + lane] = make_uint4((uint32_t)ss, (uint32_t)(ss >> 32), (uint32_t)sd, (uint32_t)(sd >> 32));
     cpl0[j * 64 + lane] = make_uint2(gs ? o.len[j] : 0u, gs ? set_chunks(a, o.len[j], scrub, hybrid) : 0u);
     const uint64_t gsrc = gg ? (uint64_t)a.value((size_t)sidx[j]) : 0;
-    const uint64_t gdst = gg ? (uint64_t)(f->vals + o.row[j] * (long)f->vstride) : 0;
+    const uint64_t gdst = gg ? (uint64_t)(f->vals + out_row(o, j) * (long)f->vstride) : 0;
     const uint32_t n16 = (o.len[j] + 15) >> 4;
     cpp1[j * 64 + lane] = make_uint4((uint32_t)gsrc, (uint32_t)(gsrc >> 32), (uint32_t)gdst, (uint32_t)(gdst >> 32));
     cpl1[j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? n16 : 0u);
@@ -632,14 +643,14 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
     } else {
       if (r == kOk) ++st.ok;
       else if (r == kNoEnt) ++st.miss;
-      if (f.lens) f.lens[o.row[j]] = r == kOk ? o.len[j] : 0;
+      if (f.lens) f.lens[out_row(o, j)] = r == kOk ? o.len[j] : 0;
     }
-    if (f.status) f.status[o.row[j]] = r;
+    if (f.status) f.status[out_row(o, j)] = r;
     o.seg[j] = -1;
   }
 }
 
-template <int U, int B, int KW = 16, int OCC = 1>
+template <int U, int B, int KW = 16, int OCC = 1, bool OI = false>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, FSegs tab,
                                                                                          int max_retry, uint64_t* stats,
                                                                                          int skip_len) {
@@ -676,7 +687,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
   long cursor = 0;
   bool more = true;
-  OpSlots<U, KW> o;
+  OpSlots<U, KW, OI> o;
 #pragma unroll
   for (int j = 0; j < U; ++j) o.seg[j] = -1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -700,7 +711,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
 #pragma unroll
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
     if (!__syncthreads_or(busy)) break;
-    kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
+    kv_round<U, KW, OI>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
                     skip_len, ms);
   }
   flush_stats(a, st, stats, muts);
@@ -959,8 +970,15 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   const dim3 g((unsigned)(need < cap ? need : cap));
   // SPL_KVS_SKIP_LEN (A/B knob): kv_round flags
   static const int skip_len = env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0;
-  if (kw4)
+  // segments with an output map (direct routed responses) take the OI form of the grid
+  bool oi = false;
+  for (int q = 0; q < tab.n; ++q) oi |= tab.s[q].oidx != nullptr;
+  if (kw4 && oi)
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
+  else if (kw4)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
+  else if (oi)
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 16, 1, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
   else
     hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
   return (int)hipGetLastError();
@@ -1693,6 +1711,9 @@ int spl_kvs_step_xr(void* h, spl_arena_t a, hipStream_t origin, const spl_xr_ste
                          (int32_t*)(p + x->off_ss), nullptr, x->rcounts + sg * 2 + kind, cap, x->vw, 1}
                   : FSeg{(const char*)(q + x->off_gk), p + x->off_gv, (uint32_t*)(p + x->off_gl),
                          (int32_t*)(p + x->off_gs), nullptr, x->rcounts + sg * 2 + kind, cap, x->vw, 0};
+          // direct responses: results at the op's client index in source sg's client arrays
+          const long op = set ? x->off_sp : x->off_gp;
+          if (op > 0) f.oidx = (const int32_t*)(q + op);
         }
         tab.s[tab.n++] = f;
         rows += f.n;
@@ -1700,6 +1721,7 @@ int spl_kvs_step_xr(void* h, spl_arena_t a, hipStream_t origin, const spl_xr_ste
     }
     return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin);
   }
+  if (W > 1 && (x->off_sp > 0 || x->off_gp > 0)) return (int)hipErrorInvalidValue;  // direct: the fused grid only
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
   for (int kind = 0; kind < 2; ++kind) {

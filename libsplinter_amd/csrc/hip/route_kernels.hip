@@ -46,12 +46,13 @@ __device__ __forceinline__ int shard_of_hash(uint64_t h, int world) {
 struct XKind {
   long off_k, off_l, off_v;  // byte offsets of keys / lens / value rows in a block (off_l, off_v: sets)
   int vw;                    // value bytes per row (16-B multiple; 0: no values)
+  long off_p;                // direct responses: the client-index column (<= 0: none)
 };
 
 __global__ __launch_bounds__(kRB) void k_xpack(const char* keys, int ks, const uint8_t* vals, int vstride,
                                                const uint32_t* lens, long n, int world, int rank, long cap,
                                                const uint64_t* blk, XKind kd, int32_t* counts, int32_t* lidx,
-                                               int32_t* pos) {
+                                               int32_t* pos, int32_t* full_status, uint32_t* full_lens) {
   __shared__ int s_cnt[kMaxWorld];
   __shared__ int s_base[kMaxWorld];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -97,6 +98,10 @@ __global__ __launch_bounds__(kRB) void k_xpack(const char* keys, int ks, const u
           }
         }
         pos[i] = p;
+        if (p == kPosFull && full_status) {  // direct responses: no gather will mark it
+          full_status[i] = kAgain;
+          if (full_lens) full_lens[i] = 0u;
+        }
       }
       if (row >= 0) {
         uint4* kr = (uint4*)(b + kd.off_k + row * (long)ks);
@@ -104,6 +109,7 @@ __global__ __launch_bounds__(kRB) void k_xpack(const char* keys, int ks, const u
         for (int c = 0; c < 4; ++c)
           if (c * 16 < ks) kr[c] = make_uint4(k[j].w[4 * c], k[j].w[4 * c + 1], k[j].w[4 * c + 2], k[j].w[4 * c + 3]);
         if (kd.vw) *(uint32_t*)(b + kd.off_l + row * 4) = lens[i];
+        if (kd.off_p > 0) *(int32_t*)(b + kd.off_p + row * 4) = (int32_t)i;
       }
       if (kd.vw) {
         // value prefixes, wave-cooperatively: the wave's 64 rows of this item index, lanes walk the
@@ -242,18 +248,19 @@ long spl_xr_flag_bytes(void) { return kXfFlagBytes + 2L * kMaxWorld * 2 * 4; }
 // are lidx entries).  blk: device table of `world` block base pointers (the own entry is unused).
 int spl_xr_pack(const char* keys, int ks, const uint8_t* vals, int vstride, const uint32_t* lens, long n, int world,
                 int rank, long cap, const uint64_t* blk, long off_k, long off_l, long off_v, int vw, int32_t* counts,
-                int32_t* lidx, int32_t* pos, hipStream_t s) {
+                int32_t* lidx, int32_t* pos, long off_p, int32_t* full_status, uint32_t* full_lens, hipStream_t s) {
   if (world < 1 || world > kMaxWorld || rank < 0 || rank >= world || cap < 0) return (int)hipErrorInvalidValue;
   if ((ks & 15) || ks <= 0 || ks > 64 || (off_k & 15)) return (int)hipErrorInvalidValue;
   if (vw && (!vals || !lens || (vstride & 15) || (vw & 15) || vw > vstride || (off_v & 15) || (off_l & 3)))
     return (int)hipErrorInvalidValue;
-  if (cap * (long)world > INT32_MAX) return (int)hipErrorInvalidValue;
+  if (cap * (long)world > INT32_MAX || n > INT32_MAX || (off_p > 0 && (off_p & 3))) return (int)hipErrorInvalidValue;
   hipError_t e = hipMemsetAsync(counts, 0, sizeof(int32_t) * (size_t)world, s);
   if (e != hipSuccess) return (int)e;
   if (n <= 0) return 0;
-  const XKind kd{off_k, off_l, off_v, vw};
+  const XKind kd{off_k, off_l, off_v, vw, off_p};
   hipLaunchKernelGGL(k_xpack, dim3(route_grid(n, (long)kRB * kRU)), dim3(kRB), 0, s, keys, ks, vals, vstride, lens, n,
-                     world, rank, cap, blk, kd, counts, lidx, pos);
+                     world, rank, cap, blk, kd, counts, lidx, pos, off_p > 0 ? full_status : nullptr,
+                     off_p > 0 ? full_lens : nullptr);
   return (int)hipGetLastError();
 }
 

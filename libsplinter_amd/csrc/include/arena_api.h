@@ -124,10 +124,14 @@ int spl_arena_get_idx(spl_arena_t a, const char *keys, int kstride, uint8_t *out
  * ((fnv1a >> 40) & 0xFFFFFF) % world; blk[d] = base of the block for owner d (device table),
  * rows at blk[d] + off_k / off_l / off_v (key, u32 len, vw value bytes; vw = 0: keys only).
  * counts[world] is zeroed here and receives every destination's rows (own included); own ops are
- * listed in lidx (client indices); pos[i] = d*cap + j (remote), -2 (own), -1 (block full). */
+ * listed in lidx (client indices); pos[i] = d*cap + j (remote), -2 (own), -1 (block full).
+ * Direct responses (off_p > 0): every remote row also carries its client index, an int32 at
+ * blk[d] + off_p + 4j, so the owner writes the op's result straight into the requester's client
+ * arrays; an op whose block is full gets EAGAIN in full_status (and len 0 in full_lens) here. */
 int spl_xr_pack(const char *keys, int ks, const uint8_t *vals, int vstride, const uint32_t *lens, long n, int world,
                 int rank, long cap, const uint64_t *blk, long off_k, long off_l, long off_v, int vw, int32_t *counts,
-                int32_t *lidx, int32_t *pos, hipStream_t stream);
+                int32_t *lidx, int32_t *pos, long off_p, int32_t *full_status, uint32_t *full_lens,
+                hipStream_t stream);
 /* Responses into client order: remote ops read status / len / value row j of blk[d]; full ops get
  * EAGAIN; own ops are left as the in-place kernels wrote them. */
 int spl_xr_gather(const int32_t *pos, long n, long cap, const uint64_t *blk, long off_s, long off_l, long off_v,
@@ -159,6 +163,10 @@ typedef struct spl_xr_step {
   uint64_t resp[SPL_XR_MAX_WORLD];     /* where this rank's responses to source s go */
   long off_sk, off_sl, off_sv, off_gk; /* request block layout */
   long off_ss, off_gs, off_gl, off_gv; /* response block layout */
+  /* direct responses (> 0): the request block's client-index columns; resp[s] is then source s's
+   * client output area (its status / lens / value rows at off_ss.. in client order, value rows vw
+   * bytes apart) and each result is written at its op's client index; <= 0: response blocks */
+  long off_sp, off_gp;
 } spl_xr_step_t;
 
 /* Exchange windows: device memory a peer process maps (VMM dmabuf chunks, abstract socket `name`). */

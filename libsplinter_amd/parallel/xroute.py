@@ -95,21 +95,35 @@ class XGeom:
     window (per rank) = 2 parities x [REQ block from source 0..W-1 | RESP block from owner 0..W-1]
       REQ  = set keys cap_s x ks | set lens cap_s x 4 | set values cap_s x vw | get keys cap_g x ks
       RESP = set status cap_s x 4 | get status cap_g x 4 | get lens cap_g x 4 | get values cap_g x vw
+    direct responses (peer transport): REQ also carries the ops' client indices (set cap_s x 4 | get
+    cap_g x 4) and the RESP blocks are replaced by this rank's client output arrays, which the owners
+    write in client order:
+      OUT  = set status n_set x 4 | get status n_get x 4 | get lens n_get x 4 | get values n_get x vw
     """
 
-    def __init__(self, world: int, cap_s: int, cap_g: int, ks: int, vw: int):
+    def __init__(self, world: int, cap_s: int, cap_g: int, ks: int, vw: int, n_set: int = 0, n_get: int = 0,
+                 direct: bool = False):
         self.world, self.cap_s, self.cap_g, self.ks, self.vw = world, cap_s, cap_g, ks, vw
+        self.direct = direct
         self.off_sk = 0
         self.off_sl = _al(cap_s * ks)
         self.off_sv = self.off_sl + _al(cap_s * 4)
         self.off_gk = self.off_sv + _al(cap_s * vw)
         self.req_b = self.off_gk + _al(cap_g * ks)
+        self.off_sp = self.off_gp = -1
+        if direct:
+            self.off_sp = self.req_b
+            self.off_gp = self.off_sp + _al(cap_s * 4)
+            self.req_b = self.off_gp + _al(cap_g * 4)
+            rs, rg = n_set, n_get  # the OUT area: client order
+        else:
+            rs, rg = cap_s, cap_g  # a response block per owner
         self.off_ss = 0
-        self.off_gs = _al(cap_s * 4)
-        self.off_gl = self.off_gs + _al(cap_g * 4)
-        self.off_gv = self.off_gl + _al(cap_g * 4)
-        self.resp_b = self.off_gv + _al(cap_g * vw)
-        self.par_b = world * (self.req_b + self.resp_b)
+        self.off_gs = _al(rs * 4)
+        self.off_gl = self.off_gs + _al(rg * 4)
+        self.off_gv = self.off_gl + _al(rg * 4)
+        self.resp_b = self.off_gv + _al(rg * vw)
+        self.par_b = world * self.req_b + (self.resp_b if direct else world * self.resp_b)
         # device-side ordering (sync "flags"): [parity][dir][source] u64 step sequences, then
         # [parity][source][kind] i32 row counts, 64 sources (route_kernels.hip kMaxWorld)
         self.off_flag = 2 * self.par_b
@@ -122,12 +136,14 @@ class XGeom:
         return p * self.par_b + s * self.req_b
 
     def resp(self, p: int, o: int) -> int:
-        """Offset of the response block from owner o, parity p."""
-        return p * self.par_b + self.world * self.req_b + o * self.resp_b
+        """Offset of the response block from owner o, parity p (the OUT area when direct)."""
+        return p * self.par_b + self.world * self.req_b + (0 if self.direct else o * self.resp_b)
 
     def wire_bytes(self, n_set_remote: float, n_get_remote: float) -> float:
         """Bytes a rank stores into its peers per step: request rows + response rows."""
-        return n_set_remote * (self.ks + 4 + self.vw + 4) + n_get_remote * (self.ks + 4 + 4 + self.vw)
+        extra = 4 if self.direct else 0
+        return (n_set_remote * (self.ks + 4 + self.vw + 4 + extra)
+                + n_get_remote * (self.ks + 4 + 4 + self.vw + extra))
 
 
 def _view(t: torch.Tensor, off: int, rows: int, width: int, dtype=torch.uint8) -> torch.Tensor:
@@ -176,6 +192,14 @@ class XRoute:
         if W == 1:
             transport = "local"
         self.transport = transport
+        # direct responses (peer transport, fused owner grid): owners write results straight into the
+        # requester's client output arrays (outputs(p)) -- no response blocks, no gather kernel
+        # (profiles/r6/README.md: the gather was 0.38 of the 2-rank step's 2.79 ms)
+        self.direct = (transport == "peer" and self.cuda and W > 1
+                       and os.environ.get("SPLINTER_XR_DIRECT", "1") != "0"
+                       and os.environ.get("SPL_KVS_FUSED", "2") != "0")
+        if self.direct:
+            self.g = XGeom(W, self.cap_s, self.cap_g, ks, vw, n_set, n_get, direct=True)
         self.fallback_reason = None  # why a requested peer transport fell back to rccl (None: it did not)
         self.sync = "coll"
         self.wait_ms = int(os.environ.get("SPLINTER_XR_WAIT_MS", "20000"))
@@ -197,6 +221,8 @@ class XRoute:
             if transport == "peer":
                 if not self._setup_peer():
                     transport = self.transport = "rccl"
+                    self.direct = False
+                    self.g = XGeom(W, self.cap_s, self.cap_g, ks, vw)
                 else:
                     # measured on the one-GPU rehearsal: flags 0.62-0.63 of the 1-rank step vs 0.68 with the
                     # (gloo-staged) collectives (profiles/r5/exchange_sync.md), so collectives by default
@@ -358,6 +384,21 @@ class XRoute:
             pass
 
     # ----------------------------------------------------------------- phases --
+    def outputs(self, p: int):
+        """Direct responses: this rank's client output arrays of parity p -- (set status [n_set] int32,
+        get values [n_get, vw] uint8, get lens [n_get] int32, get status [n_get] int32) -- in its own
+        window, where the owners write the results.  Pass them to execute / finish for every step of
+        that parity (i & 1 == p), and read a step's results before the next request of its parity."""
+        assert self.direct, "outputs(): direct responses only (peer transport)"
+        from ..ops.arena import _device_view
+        g, base = self.g, self._win_base + self.g.resp(p, self.rank)
+        u8 = lambda off, nb: _device_view(base + off, nb)  # noqa: E731
+        ss = u8(g.off_ss, self.n_set * 4).view(torch.int32)
+        gs = u8(g.off_gs, self.n_get * 4).view(torch.int32)
+        gl = u8(g.off_gl, self.n_get * 4).view(torch.int32)
+        gv = u8(g.off_gv, self.n_get * self.vw).view(self.n_get, self.vw)
+        return ss, gv, gl, gs
+
     # ------------------------------------------------------- phase attribution --
     def _mark(self, i: int, name: str) -> None:
         if self._ph is not None:
@@ -461,7 +502,9 @@ class XRoute:
         if self.world > 1:
             if self.sync == "flags":
                 self._wait(i, 1)  # every owner's response rows of step i are in this window
-            if self.cuda:
+            if self.direct:
+                pass  # the owners wrote every result in place; block-full ops were marked by the pack
+            elif self.cuda:
                 self._gather_dev(p, skeys, gkeys, sstatus, gout, glens, gstatus)
             else:
                 self._gather_host(p, skeys, gkeys, sstatus, gout, glens, gstatus)
@@ -481,17 +524,22 @@ class XRoute:
         assert ns <= self.n_set and ng <= self.n_get
         tab = self._pack_blk[p].data_ptr()
         cnt = self.cnt[p]
+        # direct responses: the client-index columns, and block-full ops marked EAGAIN in this rank's
+        # output arrays right here (no gather follows)
+        out = self.outputs(p) if self.direct else None
         if ns:
             assert skeys.shape[1] == self.ks and svals.shape[1] >= self.vw and svals.is_contiguous()
             _check(L.spl_xr_pack(skeys.data_ptr(), self.ks, svals.data_ptr(), svals.shape[1], slens.data_ptr(), ns, W, r,
                                  self.cap_s, tab, g.off_sk, g.off_sl, g.off_sv, self.vw, cnt[0].data_ptr(),
-                                 self.lidx[p][0].data_ptr(), self.pos[p][0].data_ptr(), s), "xr_pack set")
+                                 self.lidx[p][0].data_ptr(), self.pos[p][0].data_ptr(), g.off_sp,
+                                 out[0].data_ptr() if out else None, None, s), "xr_pack set")
         else:
             cnt[0].zero_()
         if ng:
             assert gkeys.shape[1] == self.ks
             _check(L.spl_xr_pack(gkeys.data_ptr(), self.ks, None, 0, None, ng, W, r, self.cap_g, tab, g.off_gk, 0, 0, 0,
-                                 cnt[1].data_ptr(), self.lidx[p][1].data_ptr(), self.pos[p][1].data_ptr(), s),
+                                 cnt[1].data_ptr(), self.lidx[p][1].data_ptr(), self.pos[p][1].data_ptr(), g.off_gp,
+                                 out[3].data_ptr() if out else None, out[2].data_ptr() if out else None, s),
                    "xr_pack get")
         else:
             cnt[1].zero_()
@@ -519,6 +567,14 @@ class XRoute:
                 x.req[s_], x.resp[s_] = self._exec_req[p][s_], self._exec_resp[p][s_]
         x.off_sk, x.off_sl, x.off_sv, x.off_gk = g.off_sk, g.off_sl, g.off_sv, g.off_gk
         x.off_ss, x.off_gs, x.off_gl, x.off_gv = g.off_ss, g.off_gs, g.off_gl, g.off_gv
+        x.off_sp, x.off_gp = g.off_sp, g.off_gp  # -1 unless direct
+        if self.direct and W > 1:  # the owners write into these: they must be this rank's outputs(p)
+            o = self.outputs(p)
+            assert ((sstatus is None or sstatus.data_ptr() == o[0].data_ptr())
+                    and (gout is None or (gout.data_ptr() == o[1].data_ptr() and gout.shape[1] == self.vw))
+                    and (glens is None or glens.data_ptr() == o[2].data_ptr())
+                    and (gstatus is None or gstatus.data_ptr() == o[3].data_ptr())), \
+                "direct responses: pass the arrays of outputs(i & 1) to execute()"
         _check(N.hip_lib().spl_kvs_step_xr(kvs.h, self.local.arena.desc, _stream(), ctypes.byref(x), retries,
                                            self.local.arena.stats.data_ptr()), "kvs_step_xr")
 
@@ -659,6 +715,18 @@ class XRoute:
         dev = self.dev
         ns = skeys.shape[0] if skeys is not None else 0
         ng = gkeys.shape[0] if gkeys is not None else 0
+        if self.direct:  # the results land in this rank's output arrays: copied out for the caller
+            ss, gv, gl, gs = self.outputs(i & 1)
+            self.request(i, skeys, svals, slens, gkeys)
+            self.execute(i, kvs, ss, gv, gl, gs)
+            self.respond(i)
+            self.finish(i, ss, gv, gl, gs)
+            if gout is None:
+                gout = gv[:ng].clone()
+            else:
+                w = min(self.vw, gout.shape[1])
+                gout[:ng, :w] = gv[:ng, :w]
+            return ss[:ns].clone(), gs[:ng].clone(), gout, gl[:ng].clone()
         sstatus = torch.empty(ns, dtype=torch.int32, device=dev)
         gstatus = torch.empty(ng, dtype=torch.int32, device=dev)
         glens = torch.empty(ng, dtype=torch.int32, device=dev)

@@ -32,7 +32,8 @@ def _pack(K, V, L, world, rank, cap, vw):
     lp = L.data_ptr() if L is not None else None
     rc = N.hip_lib().spl_xr_pack(K.data_ptr(), ks, vp, V.shape[1] if V is not None else 0, lp, n, world, rank, cap,
                                  tab.data_ptr(), g.off_sk if V is not None else g.off_gk, g.off_sl, g.off_sv,
-                                 vw if V is not None else 0, counts.data_ptr(), lidx.data_ptr(), pos.data_ptr(), s)
+                                 vw if V is not None else 0, counts.data_ptr(), lidx.data_ptr(), pos.data_ptr(), -1,
+                                 None, None, s)
     assert rc == 0
     torch.cuda.synchronize()
     return g, buf, counts, lidx, pos
@@ -169,10 +170,11 @@ a = HbmArena.create(f"xrp{os.environ['TAG']}r{rank}", slots=1 << 18, max_val=256
 kvs = KvStreams(4, 4)
 n, steps = 30000, 6
 xr = XRoute(GpuShard(a), n, n, 160, ks=16, resp_group=dist.new_group(backend="gloo"), transport=transport)
-res = {"transport": xr.transport}
-outs = [(torch.empty(n, dtype=torch.int32, device="cuda"), torch.zeros((n, 160), dtype=torch.uint8, device="cuda"),
-         torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"))
-        for _ in range(2)]
+res = {"transport": xr.transport, "direct": xr.direct}
+outs = ([xr.outputs(p) for p in range(2)] if xr.direct else
+        [(torch.empty(n, dtype=torch.int32, device="cuda"), torch.zeros((n, 160), dtype=torch.uint8, device="cuda"),
+          torch.empty(n, dtype=torch.int32, device="cuda"), torch.empty(n, dtype=torch.int32, device="cuda"))
+         for _ in range(2)])
 bad = checked = setbad = 0
 pend = None
 batches = []
@@ -220,14 +222,17 @@ dist.destroy_process_group()
 """
 
 
-@pytest.mark.parametrize("transport,sync", [("peer", "flags"), ("peer", "coll"), ("rccl", "coll")])
-def test_xroute_two_ranks_one_gpu(tmp_path, transport, sync):
+@pytest.mark.parametrize("transport,sync,direct", [("peer", "flags", "1"), ("peer", "coll", "1"), ("peer", "coll", "0"),
+                                                   ("rccl", "coll", "0")])
+def test_xroute_two_ranks_one_gpu(tmp_path, transport, sync, direct):
     """Two ranks (processes) on device 0 run the pipelined routed step through the exchange: the
-    peer transport maps each other's windows (VMM dmabuf) and stores request / response rows
-    directly, its steps ordered by device-side posts into the windows (flags) or by the count /
-    response collectives (coll); the rccl transport moves the blocks with collectives (gloo-staged
-    here).  Gets of the keys another rank set two steps earlier must all return their values
-    (integrity 0), and no device-side wait may give up."""
+    peer transport maps each other's windows (VMM dmabuf) and stores request rows directly, and
+    either the owners write every result straight into the requester's client arrays (direct
+    responses, no gather) or into response blocks the requester gathers; its steps are ordered by
+    device-side posts into the windows (flags) or by the count / response collectives (coll); the
+    rccl transport moves the blocks with collectives (gloo-staged here).  Gets of the keys another
+    rank set two steps earlier must all return their values (integrity 0), and no device-side wait
+    may give up."""
     import json
     import socket
     import subprocess
@@ -240,7 +245,7 @@ def test_xroute_two_ranks_one_gpu(tmp_path, transport, sync):
     port = s.getsockname()[1]
     s.close()
     env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
-               REPO=root, TAG=str(os.getpid()), SPLINTER_XR_SYNC=sync)
+               REPO=root, TAG=str(os.getpid()), SPLINTER_XR_SYNC=sync, SPLINTER_XR_DIRECT=direct)
     ps = [subprocess.Popen([sys.executable, str(w), str(r), "2", transport], env=env, stdout=subprocess.PIPE,
                            stderr=subprocess.PIPE, text=True) for r in range(2)]
     outs = []
@@ -257,6 +262,7 @@ def test_xroute_two_ranks_one_gpu(tmp_path, transport, sync):
         line = [x for x in o.splitlines() if x.startswith("RES ")][-1]
         res = json.loads(line[4:])
         assert res["transport"] == transport and res["sync"] == sync and not res["sync_err"], res
+        assert res["direct"] == (transport == "peer" and direct == "1"), res
         assert res["checked"] == 4 * 30000 and res["bad"] == 0 and res["setbad"] == 0 and res["api_bad"] == 0, res
 
 

@@ -1,7 +1,7 @@
 #!/bin/bash
 # round-6 validation: GPU suite, smoke, default bench, timed-region kernel trace of the mixed step
 set -o pipefail
-OUT=gpurun_out/r6final
+OUT=${OUTF:-gpurun_out/r6final}
 mkdir -p $OUT
 export TMPDIR=/tmp
 timeout -k 10 1200 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread > $OUT/pytest_gpu.txt 2>&1; echo "suite rc=$?"

@@ -791,7 +791,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     if (w == 0) {
       // wave 0 claims: lane i looks at slice i (its post and how far it is claimed) in one round
       // trip for all slices, then the first available slice at or after the last one served (a
-      // workgroup stays on a slice while it lasts) gets the atomic claim
+      // workgroup stays on a slice while it lasts) gets the atomic claim.  The lane index is
+      // laundered per claim: values derived from it are recomputed here (once per chunk) instead of
+      // being hoisted out of the loop and held -- spilled -- across the round body
+      int lane = threadIdx.x & 63;
+      asm volatile("" : "+v"(lane));
       const uint64_t all = nseg >= 64 ? ~0ull : ((1ull << nseg) - 1);
       uint64_t exhausted = sh_exhausted, posted = sh_posted;
       const int scan = sh_scan;
@@ -1528,7 +1532,7 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   }();
   static const uint64_t wait_ticks = (uint64_t)env_int("SPL_KVS_ASYNC_WAIT_MS", 2000) * 100000ull;  // 100 MHz
   static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
-  hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
+    hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
                      sset, sget, nw, nr, ks, k->ctl, seq, chunk, wait_ticks, spread, max_retry, stats,
                      env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0);
   e = hipGetLastError();

@@ -76,11 +76,13 @@ __device__ __forceinline__ uint64_t block_sum(uint64_t v) {
   return t;
 }
 
+// Per-lane counters of one launch, 32-bit (a lane sees at most its share of the batch times the retry
+// bound), widened in flush_stats: 5 registers instead of 10 in the round loops
 struct Stats {
-  uint64_t attempts = 0, ok = 0, again = 0, miss = 0;
+  uint32_t attempts = 0, ok = 0, again = 0, miss = 0;
 };
 
-__device__ __forceinline__ void flush_stats(const Arena& a, Stats st, uint64_t* stats, uint64_t mutations) {
+__device__ __forceinline__ void flush_stats(const Arena& a, Stats st, uint64_t* stats, uint32_t mutations) {
   const uint64_t at = block_sum(st.attempts);
   const uint64_t ok = block_sum(st.ok);
   const uint64_t ag = block_sum(st.again);
@@ -206,7 +208,7 @@ __global__ __launch_bounds__(B) void k_set_carry(spl_arena_t aa, const char* key
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
   Stats st;
-  uint64_t muts = 0;
+  uint32_t muts = 0;
   const long stride = (long)gridDim.x * blockDim.x * U;
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
   long cursor = 0;
@@ -535,7 +537,7 @@ __device__ __forceinline__ void fill_slot(OpSlots<U, KW, OI>& o, int j, const FS
 constexpr int kKvSkipLen = 1;
 template <int U, int KW, bool OI = false>
 __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW, OI>& o, bool scrub, bool hybrid,
-                                         int max_retry, Stats& st, uint64_t& muts, uint4* cpp0, uint2* cpl0,
+                                         int max_retry, Stats& st, uint32_t& muts, uint4* cpp0, uint2* cpl0,
                                          uint4* cpp1, uint2* cpl1, int lane, int flags, uint64_t& ms) {
   const bool skip_len = flags & kKvSkipLen;
   Claim c[U];
@@ -681,7 +683,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   bool hybrid;
   const bool scrub = scrub_flags(a, hybrid);
   Stats st;
-  uint64_t muts = 0;
+  uint32_t muts = 0;
   const long n = sstart[nseg];
   const long stride = (long)gridDim.x * blockDim.x * U;
   const long first = (long)blockIdx.x * blockDim.x * U + (long)threadIdx.x * U;
@@ -784,7 +786,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
 #pragma unroll
   for (int j = 0; j < U; ++j) o.seg[j] = -1;
   Stats st;
-  uint64_t muts = 0;
+  uint32_t muts = 0;
   uint64_t ms = maint_begin(a);
   for (;;) {
     __syncthreads();  // the previous chunk's readers of sh_* are done
@@ -1011,7 +1013,7 @@ __global__ __launch_bounds__(kBlock) void k_intop(spl_arena_t aa, const char* ke
                                                   const uint64_t* masks, long n, int32_t* status, uint64_t* results,
                                                   int max_retry) {
   const Arena a = to_dev(aa);
-  uint64_t muts = 0;
+  uint32_t muts = 0;
   Stats st;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     Key k;
@@ -1039,7 +1041,7 @@ __global__ __launch_bounds__(kBlock) void k_intop(spl_arena_t aa, const char* ke
 __global__ __launch_bounds__(kBlock) void k_meta(spl_arena_t aa, const char* keys, int kstride, int op,
                                                  const uint64_t* args, long n, int32_t* status, uint64_t* out) {
   const Arena a = to_dev(aa);
-  uint64_t muts = 0;
+  uint32_t muts = 0;
   Stats st;
   for (long i = blockIdx.x * (long)blockDim.x + threadIdx.x; i < n; i += (long)gridDim.x * blockDim.x) {
     Key k;
@@ -1063,7 +1065,7 @@ __global__ __launch_bounds__(kBlock) void k_embed_set(spl_arena_t aa, const char
   const int lane = threadIdx.x & 63;
   const long wave = (blockIdx.x * (long)blockDim.x + threadIdx.x) >> 6;
   const long nwaves = ((long)gridDim.x * blockDim.x) >> 6;
-  uint64_t muts = 0;
+  uint32_t muts = 0;
   Stats st;
   for (long i = wave; i < n; i += nwaves) {
     Key k;

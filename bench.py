@@ -69,6 +69,10 @@ def parse():
     p.add_argument("--overlap-native", type=int, default=0, choices=[0, 1],
                    help="1: the native KV fan-out (32+32 client streams) runs concurrently with the embed batch "
                         "(KV forked from its own origin stream, the encoder on the current stream)")
+    p.add_argument("--overlap-kv-cus", type=int, default=0, choices=[0, 8, 16, 24],
+                   help="with --overlap-native 1: the KV origin stream is confined to N CUs per XCD (CU mask; the "
+                        "fused grid is sized to them) while the encoder keeps every CU, so encoder kernels fill "
+                        "the other CUs while the KV grid runs and the whole chip once it ends")
     p.add_argument("--force-routed", action="store_true",
                    help="run the N>1 routed step (pack -> all-to-all -> owner kernels -> all-to-all -> gather) "
                         "even at N=1, to measure the routing overhead on one GPU")
@@ -528,8 +532,14 @@ def main():
                      "how": "python client streams, one arena.set / arena.get launch per slice"}
 
     _phase_gap_ms = float(os.environ.get("BENCH_PHASE_GAP_MS", "0"))
-    s_kvo = hip_stream("low") if (args.overlap_native and kvs is not None and embedder is not None
-                                  and world == 1) else None
+    s_kvo = None
+    if args.overlap_native and kvs is not None and embedder is not None and world == 1:
+        if args.overlap_kv_cus:
+            from libsplinter_amd.utils.streams import cu_mask_bits, masked_stream
+            s_kvo = masked_stream(cu_mask_bits(args.overlap_kv_cus))
+            log(f"[bench] overlapped phases: KV grid on {8 * args.overlap_kv_cus} CUs, encoder on every CU")
+        else:
+            s_kvo = hip_stream("low")
 
 
     # Host submission throttle (--throttle): the next step's KV launches are issued only once
@@ -926,7 +936,9 @@ def main():
             "keys_per_gpu": kpg, "slots_per_gpu": slots, "global_batch": args.batch * world,
             "set_frac": args.set_frac, "seq_len": args.embed_seq if embedder else None,
             "parallelism": f"hash-shard{world}" + (" + dp" if embedder else ""),
-            "mode": args.mode, "phases": "overlapped" if s_kvo is not None else "serial", "mop": args.mop, "value_len": args.value_len,
+            "mode": args.mode, "phases": ("serial" if s_kvo is None else
+                                                 f"overlapped (KV grid on {8 * args.overlap_kv_cus} CUs)"
+                                                 if args.overlap_kv_cus else "overlapped"), "mop": args.mop, "value_len": args.value_len,
             # how the step's KV work is submitted: the batch is split into --writer-streams set slices and
             # --reader-streams get slices (the config's concurrent clients); in the default fused mode ONE
             # grid consumes every slice from one stream, so the streams that actually launch are counted here

@@ -8,6 +8,7 @@
 // 8 blocks/CU x 256 CUs, one op per thread.  Global-epoch increments and
 // retry statistics are reduced per block (one atomic per block instead of one
 // per op: a single contended word saturates near 88 M atomics/s on MI355X).
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <cstdio>
@@ -961,6 +962,23 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   }
 }
 
+// CUs a stream's kernels may occupy: the popcount of its CU mask (the whole device for an unmasked
+// stream; a runtime query, no device round trip)
+int stream_cus(hipStream_t s) {
+  int dev = 0, n = 0;
+  (void)hipGetDevice(&dev);
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+  uint32_t m[16] = {};
+  if (s != nullptr && hipExtStreamGetCUMask(s, 16, m) == hipSuccess) {
+    int c = 0;
+    for (uint32_t w : m) c += __builtin_popcount(w);
+    if (c > 0 && c < n) n = c;
+  } else {
+    (void)hipGetLastError();
+  }
+  return n;
+}
+
 // Launch the fused grid over `tab` (rows: an upper bound of the live rows); mode 2 with 16-B keys
 // holds them in 4 words at 3 workgroups per CU, otherwise 16 words at 2
 int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_retry, uint64_t* stats,
@@ -972,7 +990,9 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   static const int wpc_env = env_int("SPL_KVS_FUSED_WG_PER_CU", 0);
   const int wpc = wpc_env > 0 ? wpc_env : kw4 ? 3 : 2;
   const long need = (rows + 2 * 256 - 1) / (2 * 256);
-  const long cap = 256L * wpc;
+  // the grid is resident (every workgroup walks its lane stream to the end): sized to the CUs the
+  // launch stream may use, so a CU-masked stream (hipExtStreamCreateWithCUMask) gets no second wave
+  const long cap = (long)stream_cus(s) * wpc;
   const dim3 g((unsigned)(need < cap ? need : cap));
   // SPL_KVS_SKIP_LEN (A/B knob): kv_round flags
   static const int skip_len = env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0;
@@ -1527,7 +1547,7 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   const int wpc = wpc_env > 0 ? wpc_env : 3;
   const long rows = sset.n + sget.n;
   const long need = (rows + 2 * 256 - 1) / (2 * 256);
-  const long cap = 256L * wpc;
+  const long cap = (long)stream_cus(origin) * wpc;  // resident grid: the CUs the origin stream may use
   static const long chunk = [] {  // rows per claim: 4 rounds of a 256-thread workgroup at 2 ops per lane
     const int c = env_int("SPL_KVS_ASYNC_CHUNK", 2048);
     return (long)(c >= 512 ? c : 512);

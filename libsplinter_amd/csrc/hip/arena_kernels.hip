@@ -653,14 +653,20 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
   }
 }
 
-template <int U, int B, int KW = 16, int OCC = 1, bool OI = false>
+// DYN: rows are claimed by workgroups in chunks from a launch-wide counter (*claim, zeroed before the
+// launch) instead of walked as fixed lane streams, so the workgroups finish together; the chunk
+// shrinks toward the end (a share of what is left per workgroup, >= one round of the group).
+template <int U, int B, int KW = 16, int OCC = 1, bool OI = false, bool DYN = false>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, FSegs tab,
                                                                                          int max_retry, uint64_t* stats,
-                                                                                         int skip_len) {
+                                                                                         int skip_len,
+                                                                                         unsigned long long* claim,
+                                                                                         long chunk, int chunk_div) {
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
   __shared__ FSeg sg[kFusedSegs];
   __shared__ long sstart[kFusedSegs + 1];
+  __shared__ long sh_c, sh_cs;  // DYN: the claimed chunk's first row and size
   const int nseg = tab.n, ks = tab.ks;
   if ((int)threadIdx.x < nseg) {
     FSeg f = tab.s[threadIdx.x];
@@ -695,25 +701,66 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   for (int j = 0; j < U; ++j) o.seg[j] = -1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint64_t ms = maint_begin(a);
+  int32_t row = 0, end = 0;  // DYN: the lane's next row of the group's chunk, and the chunk's end (rows < 2^31)
+  int part = 0;
   for (;;) {
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (o.seg[j] < 0 && more) {
-        const long i = first + (cursor / U) * stride + (cursor % U);
-        ++cursor;
-        if (i >= n) {
+    if constexpr (DYN) {
+      if (more && !__syncthreads_or(row < end)) {  // no lane has rows of the chunk left: claim the next
+        if (threadIdx.x == 0) {
+          const long left = n - (end > 0 ? end : 0);
+          long c = left / ((long)chunk_div * gridDim.x);
+          c = c < chunk ? c : chunk;
+          c = c > (long)B * U ? c : (long)B * U;
+          sh_c = (long)atomicAdd(claim, (unsigned long long)c);
+          sh_cs = c;
+        }
+        __syncthreads();
+        const long c0 = sh_c, cs = sh_cs;
+        if (c0 >= n) {
           more = false;
         } else {
+          row = (int32_t)(c0 + (long)threadIdx.x * U);
+          end = (int32_t)(c0 + cs < n ? c0 + cs : n);
+          part = 0;
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (o.seg[j] < 0 && row < end) {
           int q = 0;
-          while (q + 1 < nseg && sstart[q + 1] <= i) ++q;
-          fill_slot(o, j, sg[q], q, i - sstart[q], ks);
+          while (q + 1 < nseg && sstart[q + 1] <= row) ++q;
+          fill_slot(o, j, sg[q], q, row - sstart[q], ks);
+          if (++part == U) {
+            part = 0;
+            row += B * U - (U - 1);
+          } else {
+            ++row;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < U; ++j) {
+        if (o.seg[j] < 0 && more) {
+          const long i = first + (cursor / U) * stride + (cursor % U);
+          ++cursor;
+          if (i >= n) {
+            more = false;
+          } else {
+            int q = 0;
+            while (q + 1 < nseg && sstart[q + 1] <= i) ++q;
+            fill_slot(o, j, sg[q], q, i - sstart[q], ks);
+          }
         }
       }
     }
     bool busy = false;
 #pragma unroll
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
-    if (!__syncthreads_or(busy)) break;
+    if (!__syncthreads_or(busy)) {
+      if (DYN && more) continue;  // (uniform: every lane's chunk rows are used up) the next claim
+      break;
+    }
     kv_round<U, KW, OI>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
                     skip_len, ms);
   }
@@ -982,7 +1029,7 @@ int stream_cus(hipStream_t s) {
 // Launch the fused grid over `tab` (rows: an upper bound of the live rows); mode 2 with 16-B keys
 // holds them in 4 words at 3 workgroups per CU, otherwise 16 words at 2
 int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_retry, uint64_t* stats,
-                 hipStream_t s) {
+                 hipStream_t s, unsigned long long* claim = nullptr) {
   if (rows <= 0) return 0;
   // (measured and removed: 4 workgroups per CU at <= 128 VGPRs, 34 spilled: 4.43 vs 4.84 G ops/s,
   // profiles/r4k/kv_fused3.out)
@@ -999,14 +1046,33 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   // segments with an output map (direct routed responses) take the OI form of the grid
   bool oi = false;
   for (int q = 0; q < tab.n; ++q) oi |= tab.s[q].oidx != nullptr;
-  if (kw4 && oi)
-    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
+  // rows claimed in chunks from a launch-wide counter (the caller's KvStreams context holds it) instead
+  // of fixed lane streams: KV-only 4.96-5.00 vs 4.82-4.84 G ops/s, chunk <= 4096 rows shrinking to a
+  // half of the rows left per workgroup (profiles/r6/kv_dyn_chunks.jsonl); SPL_KVS_DYN=0: the fixed
+  // lane streams, SPL_KVS_DYN_CHUNK / SPL_KVS_DYN_DIV: the chunk cap and the shrink divisor
+  static const int dyn = env_int("SPL_KVS_DYN", 1);
+  static const long dchunk = std::max(512, env_int("SPL_KVS_DYN_CHUNK", 4096));
+  static const int ddiv = std::max(1, env_int("SPL_KVS_DYN_DIV", 2));
+  if (dyn && claim && kw4 && rows < (1L << 31) - (1L << 20)) {
+    const hipError_t e = hipMemsetAsync(claim, 0, sizeof *claim, s);
+    if (e != hipSuccess) return (int)e;
+    if (oi)
+      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true, true>), g, dim3(256), 0, s, a, tab, max_retry, stats,
+                         skip_len, claim, dchunk, ddiv);
+    else
+      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, false, true>), g, dim3(256), 0, s, a, tab, max_retry, stats,
+                         skip_len, claim, dchunk, ddiv);
+  } else if (kw4 && oi)
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len,
+                       nullptr, 0L, 1);
   else if (kw4)
-    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len, nullptr,
+                       0L, 1);
   else if (oi)
-    hipLaunchKernelGGL((k_kv_fused<2, 256, 16, 1, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 16, 1, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len,
+                       nullptr, 0L, 1);
   else
-    hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len);
+    hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len, nullptr, 0L, 1);
   return (int)hipGetLastError();
 }
 
@@ -1513,6 +1579,14 @@ struct KvStreams {
   hipEvent_t srv_done = nullptr;
   AsyncCtl* ctl = nullptr;
   uint64_t seq = 0;
+  unsigned long long* claim = nullptr;  // SPL_KVS_DYN: the fused grid's chunk counter
+  unsigned long long* claim_buf() {
+    if (!claim && hipMalloc((void**)&claim, 256) != hipSuccess) {
+      (void)hipGetLastError();
+      claim = nullptr;
+    }
+    return claim;
+  }
 };
 
 // The server grid of one step (mode 3), launched on the origin stream after every client stream's
@@ -1554,7 +1628,7 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   }();
   static const uint64_t wait_ticks = (uint64_t)env_int("SPL_KVS_ASYNC_WAIT_MS", 2000) * 100000ull;  // 100 MHz
   static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
-    hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
+  hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
                      sset, sget, nw, nr, ks, k->ctl, seq, chunk, wait_ticks, spread, max_retry, stats,
                      env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0);
   e = hipGetLastError();
@@ -1639,6 +1713,7 @@ void spl_kvs_destroy(void* h) {
   if (k->start) (void)hipEventDestroy(k->start);
   if (k->srv_done) (void)hipEventDestroy(k->srv_done);
   if (k->ctl) (void)hipFree(k->ctl);
+  if (k->claim) (void)hipFree(k->claim);
   delete k;
 }
 
@@ -1667,7 +1742,7 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
     if (n_set > 0)
       tab.s[tab.n++] = FSeg{skeys, (uint8_t*)svals, (uint32_t*)slens, sstatus, nullptr, nullptr, n_set, vstride, 1};
     if (n_get > 0) tab.s[tab.n++] = FSeg{gkeys, gout, glens, gstatus, nullptr, nullptr, n_get, ostride, 0};
-    return launch_fused(a, tab, n_set + n_get, fused, max_retry, stats, origin);
+    return launch_fused(a, tab, n_set + n_get, fused, max_retry, stats, origin, k->claim_buf());
   }
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
@@ -1745,7 +1820,7 @@ int spl_kvs_step_xr(void* h, spl_arena_t a, hipStream_t origin, const spl_xr_ste
         rows += f.n;
       }
     }
-    return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin);
+    return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin, k->claim_buf());
   }
   if (W > 1 && (x->off_sp > 0 || x->off_gp > 0)) return (int)hipErrorInvalidValue;  // direct: the fused grid only
   hipError_t e = hipEventRecord(k->start, origin);

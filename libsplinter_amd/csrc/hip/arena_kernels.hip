@@ -653,15 +653,19 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
   }
 }
 
-// DYN: rows are claimed by workgroups in chunks from a launch-wide counter (*claim, zeroed before the
-// launch) instead of walked as fixed lane streams, so the workgroups finish together; the chunk
-// shrinks toward the end (a share of what is left per workgroup, >= one round of the group).
+// DYN: rows are claimed by workgroups in chunks from a launch-wide counter instead of walked as fixed
+// lane streams, so the workgroups finish together; the chunk shrinks toward the end (a share of what
+// is left per workgroup, >= one round of the group).  The counter word is [tag (24 bits) | rows
+// claimed (40)]: a launch owns a word of its context's ring (KvStreams::claim_slot) under its own tag,
+// and the first claim that finds another tag there starts the count at 0 -- no reset before the
+// launch, and launches on different streams never share a word.
 template <int U, int B, int KW = 16, int OCC = 1, bool OI = false, bool DYN = false>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, FSegs tab,
                                                                                          int max_retry, uint64_t* stats,
                                                                                          int skip_len,
                                                                                          unsigned long long* claim,
-                                                                                         long chunk, int chunk_div) {
+                                                                                         uint32_t tag, long chunk,
+                                                                                         int chunk_div) {
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
   __shared__ FSeg sg[kFusedSegs];
@@ -711,7 +715,13 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
           long c = left / ((long)chunk_div * gridDim.x);
           c = c < chunk ? c : chunk;
           c = c > (long)B * U ? c : (long)B * U;
-          sh_c = (long)atomicAdd(claim, (unsigned long long)c);
+          // the word still carries an older launch's tag: install ours with a zero count (one CAS of the
+          // launch wins, the others fail once); then every claim is one atomic add
+          unsigned long long cur = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if ((cur >> 40) != tag)
+            __hip_atomic_compare_exchange_strong(claim, &cur, (unsigned long long)tag << 40, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sh_c = (long)(atomicAdd(claim, (unsigned long long)c) & ((1ull << 40) - 1));
           sh_cs = c;
         }
         __syncthreads();
@@ -1029,7 +1039,7 @@ int stream_cus(hipStream_t s) {
 // Launch the fused grid over `tab` (rows: an upper bound of the live rows); mode 2 with 16-B keys
 // holds them in 4 words at 3 workgroups per CU, otherwise 16 words at 2
 int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_retry, uint64_t* stats,
-                 hipStream_t s, unsigned long long* claim = nullptr) {
+                 hipStream_t s, unsigned long long* claim = nullptr, uint32_t tag = 0) {
   if (rows <= 0) return 0;
   // (measured and removed: 4 workgroups per CU at <= 128 VGPRs, 34 spilled: 4.43 vs 4.84 G ops/s,
   // profiles/r4k/kv_fused3.out)
@@ -1054,25 +1064,23 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   static const long dchunk = std::max(512, env_int("SPL_KVS_DYN_CHUNK", 4096));
   static const int ddiv = std::max(1, env_int("SPL_KVS_DYN_DIV", 2));
   if (dyn && claim && kw4 && rows < (1L << 31) - (1L << 20)) {
-    const hipError_t e = hipMemsetAsync(claim, 0, sizeof *claim, s);
-    if (e != hipSuccess) return (int)e;
     if (oi)
       hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true, true>), g, dim3(256), 0, s, a, tab, max_retry, stats,
-                         skip_len, claim, dchunk, ddiv);
+                         skip_len, claim, tag, dchunk, ddiv);
     else
       hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, false, true>), g, dim3(256), 0, s, a, tab, max_retry, stats,
-                         skip_len, claim, dchunk, ddiv);
+                         skip_len, claim, tag, dchunk, ddiv);
   } else if (kw4 && oi)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len,
-                       nullptr, 0L, 1);
+                       nullptr, 0u, 0L, 1);
   else if (kw4)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len, nullptr,
-                       0L, 1);
+                       0u, 0L, 1);
   else if (oi)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 16, 1, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len,
-                       nullptr, 0L, 1);
+                       nullptr, 0u, 0L, 1);
   else
-    hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len, nullptr, 0L, 1);
+    hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len, nullptr, 0u, 0L, 1);
   return (int)hipGetLastError();
 }
 
@@ -1579,13 +1587,25 @@ struct KvStreams {
   hipEvent_t srv_done = nullptr;
   AsyncCtl* ctl = nullptr;
   uint64_t seq = 0;
-  unsigned long long* claim = nullptr;  // SPL_KVS_DYN: the fused grid's chunk counter
-  unsigned long long* claim_buf() {
-    if (!claim && hipMalloc((void**)&claim, 256) != hipSuccess) {
-      (void)hipGetLastError();
-      claim = nullptr;
+  // SPL_KVS_DYN: the fused grids' chunk counters, one word per launch from a ring of kClaimRing words
+  // (a word is reused kClaimRing launches later, long after its launch has ended), tagged per launch
+  static constexpr int kClaimRing = 1024;
+  unsigned long long* claim = nullptr;
+  uint32_t launches = 0;
+  unsigned long long* claim_slot(uint32_t* tag) {
+    if (!claim) {
+      if (hipMalloc((void**)&claim, kClaimRing * sizeof *claim) != hipSuccess ||
+          hipMemset(claim, 0, kClaimRing * sizeof *claim) != hipSuccess) {
+        (void)hipGetLastError();
+        if (claim) (void)hipFree(claim);
+        claim = nullptr;
+        return nullptr;
+      }
     }
-    return claim;
+    uint32_t id = __atomic_add_fetch(&launches, 1u, __ATOMIC_RELAXED) & 0xFFFFFFu;
+    if (id == 0) id = __atomic_add_fetch(&launches, 1u, __ATOMIC_RELAXED) & 0xFFFFFFu;  // 0: a zeroed word's tag
+    *tag = id;
+    return claim + (*tag % kClaimRing);
   }
 };
 
@@ -1742,7 +1762,9 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
     if (n_set > 0)
       tab.s[tab.n++] = FSeg{skeys, (uint8_t*)svals, (uint32_t*)slens, sstatus, nullptr, nullptr, n_set, vstride, 1};
     if (n_get > 0) tab.s[tab.n++] = FSeg{gkeys, gout, glens, gstatus, nullptr, nullptr, n_get, ostride, 0};
-    return launch_fused(a, tab, n_set + n_get, fused, max_retry, stats, origin, k->claim_buf());
+    uint32_t tag = 0;
+    unsigned long long* cw = k->claim_slot(&tag);
+    return launch_fused(a, tab, n_set + n_get, fused, max_retry, stats, origin, cw, tag);
   }
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
@@ -1820,7 +1842,9 @@ int spl_kvs_step_xr(void* h, spl_arena_t a, hipStream_t origin, const spl_xr_ste
         rows += f.n;
       }
     }
-    return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin, k->claim_buf());
+    uint32_t tag = 0;
+    unsigned long long* cw = k->claim_slot(&tag);
+    return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin, cw, tag);
   }
   if (W > 1 && (x->off_sp > 0 || x->off_gp > 0)) return (int)hipErrorInvalidValue;  // direct: the fused grid only
   hipError_t e = hipEventRecord(k->start, origin);

@@ -653,13 +653,19 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
   }
 }
 
-// DYN: rows are claimed by workgroups in chunks from a launch-wide counter instead of walked as fixed
-// lane streams, so the workgroups finish together; the chunk shrinks toward the end (a share of what
-// is left per workgroup, >= one round of the group).  The counter word is [tag (24 bits) | rows
-// claimed (40)]: a launch owns a word of its context's ring (KvStreams::claim_slot) under its own tag,
-// and the first claim that finds another tag there starts the count at 0 -- no reset before the
-// launch, and launches on different streams never share a word.
-template <int U, int B, int KW = 16, int OCC = 1, bool OI = false, bool DYN = false>
+// SCHED, how a workgroup's lanes get their rows and when its round loop ends:
+//   0 kSchedBarrier: fixed lane streams (lane i of the grid: rows i, i + stride, ...), the loop's exit
+//     test a workgroup barrier each round (the round-5 form);
+//   1 kSchedChunks: workgroups claim chunks of rows from a launch-wide counter (shrinking toward the
+//     end), so they finish together.  The counter word is [tag (24 bits) | rows claimed (40)]: a launch
+//     owns a word of its context's ring (KvStreams::claim_slot) under its own tag, and the first claim
+//     that finds another tag there installs this launch's with one CAS, every claim then one atomic add;
+//   2 kSchedWaves (default): fixed lane streams, the exit test a wave vote, so the four waves of a
+//     group never wait for each other.
+// Per-wave chunk claims were measured too and lost (the claim round trip stalls the whole wave;
+// profiles/r6/README.md).
+constexpr int kSchedBarrier = 0, kSchedChunks = 1, kSchedWaves = 2;
+template <int U, int B, int KW = 16, int OCC = 1, bool OI = false, int SCHED = kSchedBarrier>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_fused(spl_arena_t aa, FSegs tab,
                                                                                          int max_retry, uint64_t* stats,
                                                                                          int skip_len,
@@ -670,7 +676,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   __shared__ uint2 cp_l[2][B / 64][U * 64];
   __shared__ FSeg sg[kFusedSegs];
   __shared__ long sstart[kFusedSegs + 1];
-  __shared__ long sh_c, sh_cs;  // DYN: the claimed chunk's first row and size
+  __shared__ long sh_c, sh_cs;  // kSchedChunks: the claimed chunk's first row and size
   const int nseg = tab.n, ks = tab.ks;
   if ((int)threadIdx.x < nseg) {
     FSeg f = tab.s[threadIdx.x];
@@ -705,10 +711,10 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
   for (int j = 0; j < U; ++j) o.seg[j] = -1;
   const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
   uint64_t ms = maint_begin(a);
-  int32_t row = 0, end = 0;  // DYN: the lane's next row of the group's chunk, and the chunk's end (rows < 2^31)
+  int32_t row = 0, end = 0;  // kSchedChunks: the lane's next row of the group's chunk, the chunk's end (< 2^31)
   int part = 0;
   for (;;) {
-    if constexpr (DYN) {
+    if constexpr (SCHED == kSchedChunks) {
       if (more && !__syncthreads_or(row < end)) {  // no lane has rows of the chunk left: claim the next
         if (threadIdx.x == 0) {
           const long left = n - (end > 0 ? end : 0);
@@ -767,8 +773,8 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     bool busy = false;
 #pragma unroll
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
-    if (!__syncthreads_or(busy)) {
-      if (DYN && more) continue;  // (uniform: every lane's chunk rows are used up) the next claim
+    if (!(SCHED == kSchedWaves ? __any(busy) : __syncthreads_or(busy))) {
+      if (SCHED == kSchedChunks && more) continue;  // (uniform: every lane's chunk rows are used up) the next claim
       break;
     }
     kv_round<U, KW, OI>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
@@ -1056,20 +1062,27 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   // segments with an output map (direct routed responses) take the OI form of the grid
   bool oi = false;
   for (int q = 0; q < tab.n; ++q) oi |= tab.s[q].oidx != nullptr;
-  // rows claimed in chunks from a launch-wide counter (the caller's KvStreams context holds it) instead
-  // of fixed lane streams: KV-only 4.96-5.00 vs 4.82-4.84 G ops/s, chunk <= 4096 rows shrinking to a
-  // half of the rows left per workgroup (profiles/r6/kv_dyn_chunks.jsonl); SPL_KVS_DYN=0: the fixed
-  // lane streams, SPL_KVS_DYN_CHUNK / SPL_KVS_DYN_DIV: the chunk cap and the shrink divisor
-  static const int dyn = env_int("SPL_KVS_DYN", 1);
-  static const long dchunk = std::max(512, env_int("SPL_KVS_DYN_CHUNK", 4096));
-  static const int ddiv = std::max(1, env_int("SPL_KVS_DYN_DIV", 2));
-  if (dyn && claim && kw4 && rows < (1L << 31) - (1L << 20)) {
+  // SPL_KVS_SCHED (kSched*, above): 2 = fixed lane streams with the wave-vote exit (default), 1 = workgroup
+  // chunk claims (SPL_KVS_CHUNK rows at most, shrinking to (rows left) / (SPL_KVS_CHUNK_DIV x groups)),
+  // 0 = fixed lane streams with the per-round workgroup barrier.  KV-only 4.97-4.99 / 4.97-5.00 /
+  // 4.74-4.84 G ops/s (profiles/r6/kv_dyn_chunks.jsonl)
+  static const int sched = env_int("SPL_KVS_SCHED", kSchedWaves);
+  static const long dchunk = std::max(512, env_int("SPL_KVS_CHUNK", 4096));
+  static const int ddiv = std::max(1, env_int("SPL_KVS_CHUNK_DIV", 2));
+  if (kw4 && sched == kSchedChunks && claim && rows < (1L << 31) - (1L << 20)) {
     if (oi)
-      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true, true>), g, dim3(256), 0, s, a, tab, max_retry, stats,
+      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true, kSchedChunks>), g, dim3(256), 0, s, a, tab, max_retry, stats,
                          skip_len, claim, tag, dchunk, ddiv);
     else
-      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, false, true>), g, dim3(256), 0, s, a, tab, max_retry, stats,
-                         skip_len, claim, tag, dchunk, ddiv);
+      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, false, kSchedChunks>), g, dim3(256), 0, s, a, tab, max_retry,
+                         stats, skip_len, claim, tag, dchunk, ddiv);
+  } else if (kw4 && sched == kSchedWaves) {
+    if (oi)
+      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true, kSchedWaves>), g, dim3(256), 0, s, a, tab, max_retry, stats,
+                         skip_len, nullptr, 0u, 0L, 1);
+    else
+      hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, false, kSchedWaves>), g, dim3(256), 0, s, a, tab, max_retry,
+                         stats, skip_len, nullptr, 0u, 0L, 1);
   } else if (kw4 && oi)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len,
                        nullptr, 0u, 0L, 1);
@@ -1587,7 +1600,7 @@ struct KvStreams {
   hipEvent_t srv_done = nullptr;
   AsyncCtl* ctl = nullptr;
   uint64_t seq = 0;
-  // SPL_KVS_DYN: the fused grids' chunk counters, one word per launch from a ring of kClaimRing words
+  // kSchedChunks: the fused grids' chunk counters, one word per launch from a ring of kClaimRing words
   // (a word is reused kClaimRing launches later, long after its launch has ended), tagged per launch
   static constexpr int kClaimRing = 1024;
   unsigned long long* claim = nullptr;

@@ -812,7 +812,9 @@ __host__ __device__ inline long async_bound(long n, int i, int parts) {  // firs
   return b < n ? b : n;
 }
 
-template <int U, int B, int KW = 16, int OCC = 1>
+// WV: inside a chunk each wave runs its rows' rounds on its own (the loop's exit a wave vote) and the
+// waves meet only at the next claim, as the fused grid's kSchedWaves form
+template <int U, int B, int KW = 16, int OCC = 1, bool WV = false>
 __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k_kv_server(
     spl_arena_t aa, FSeg sset, FSeg sget, int nw, int nr, int ks, AsyncCtl* ctl, uint64_t seq, long chunk,
     uint64_t wait_ticks, int spread, int max_retry, uint64_t* stats, int skip_len) {
@@ -993,7 +995,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       // once no lane has rows of this chunk left the group claims the next one; the ops still in
       // slots (the chunk's last fills, carried retries) ride along into its rounds
       const bool more = row < end;
-      if (!__syncthreads_or(more && busy)) break;
+      if (!(WV ? __any(more && busy) : __syncthreads_or(more && busy))) break;
       kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
                       lane, skip_len, ms);
     }
@@ -1003,10 +1005,11 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     bool busy = false;
 #pragma unroll
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
-    if (!__syncthreads_or(busy)) break;
+    if (!(WV ? __any(busy) : __syncthreads_or(busy))) break;
     kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
                     skip_len, ms);
   }
+  __syncthreads();  // (WV: every wave's drain is done before the group's totals are read)
   {
     const uint64_t v[5] = {st.attempts, st.ok, st.again, st.miss, muts};
 #pragma unroll
@@ -1661,9 +1664,15 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   }();
   static const uint64_t wait_ticks = (uint64_t)env_int("SPL_KVS_ASYNC_WAIT_MS", 2000) * 100000ull;  // 100 MHz
   static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
-  hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), dim3((unsigned)(need < cap ? need : cap)), dim3(256), 0, origin, a,
-                     sset, sget, nw, nr, ks, k->ctl, seq, chunk, wait_ticks, spread, max_retry, stats,
-                     env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0);
+  static const int wv = env_int("SPL_KVS_ASYNC_WV", 1);
+  const dim3 grid((unsigned)(need < cap ? need : cap));
+  const int flags = env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0;
+  if (wv)
+    hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3, true>), grid, dim3(256), 0, origin, a, sset, sget, nw, nr, ks, k->ctl,
+                       seq, chunk, wait_ticks, spread, max_retry, stats, flags);
+  else
+    hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3>), grid, dim3(256), 0, origin, a, sset, sget, nw, nr, ks, k->ctl, seq,
+                       chunk, wait_ticks, spread, max_retry, stats, flags);
   e = hipGetLastError();
   if (e != hipSuccess) return (int)e;
   (void)hipEventRecord(k->srv_done, origin);

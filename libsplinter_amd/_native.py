@@ -242,6 +242,7 @@ def _declare_hip(L):
     _sig(L, "spl_kvs_create", P, c_int, c_int)
     _sig(L, "spl_kvs_destroy", None, P)
     _sig(L, "spl_kvs_set_fused", c_int, P, c_int)
+    _sig(L, "spl_kvs_set_sched", c_int, P, c_int)
     _sig(L, "spl_kvs_async_error", c_int, P)
     _sig(L, "spl_kvs_step", c_int, P, A, P, P, c_int, P, c_int, P, c_long, P, P, P, c_int, P, c_long, P, c_int, P)
     _sig(L, "spl_kvs_step_xr", c_int, P, A, P, ctypes.POINTER(XrStep), c_int, P)

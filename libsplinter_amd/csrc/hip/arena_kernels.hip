@@ -1048,7 +1048,7 @@ int stream_cus(hipStream_t s) {
 // Launch the fused grid over `tab` (rows: an upper bound of the live rows); mode 2 with 16-B keys
 // holds them in 4 words at 3 workgroups per CU, otherwise 16 words at 2
 int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_retry, uint64_t* stats,
-                 hipStream_t s, unsigned long long* claim = nullptr, uint32_t tag = 0) {
+                 hipStream_t s, unsigned long long* claim = nullptr, uint32_t tag = 0, int sched_set = -1) {
   if (rows <= 0) return 0;
   // (measured and removed: 4 workgroups per CU at <= 128 VGPRs, 34 spilled: 4.43 vs 4.84 G ops/s,
   // profiles/r4k/kv_fused3.out)
@@ -1069,7 +1069,8 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   // chunk claims (SPL_KVS_CHUNK rows at most, shrinking to (rows left) / (SPL_KVS_CHUNK_DIV x groups)),
   // 0 = fixed lane streams with the per-round workgroup barrier.  KV-only 4.97-4.99 / 4.97-5.00 /
   // 4.74-4.84 G ops/s (profiles/r6/kv_dyn_chunks.jsonl)
-  static const int sched = env_int("SPL_KVS_SCHED", kSchedWaves);
+  static const int sched_env = env_int("SPL_KVS_SCHED", kSchedWaves);
+  const int sched = sched_set >= 0 ? sched_set : sched_env;  // spl_kvs_set_sched, else the environment
   static const long dchunk = std::max(512, env_int("SPL_KVS_CHUNK", 4096));
   static const int ddiv = std::max(1, env_int("SPL_KVS_CHUNK_DIV", 2));
   if (kw4 && sched == kSchedChunks && claim && rows < (1L << 31) - (1L << 20)) {
@@ -1608,6 +1609,7 @@ struct KvStreams {
   static constexpr int kClaimRing = 1024;
   unsigned long long* claim = nullptr;
   uint32_t launches = 0;
+  int sched = -1;  // spl_kvs_set_sched (kSched*); -1: SPL_KVS_SCHED
   unsigned long long* claim_slot(uint32_t* tag) {
     if (!claim) {
       if (hipMalloc((void**)&claim, kClaimRing * sizeof *claim) != hipSuccess ||
@@ -1732,6 +1734,15 @@ int spl_kvs_set_fused(void* h, int mode) {
   return 0;
 }
 
+// The fused grid's scheduling for this context (kSchedBarrier 0, kSchedChunks 1, kSchedWaves 2; -1:
+// SPL_KVS_SCHED)
+int spl_kvs_set_sched(void* h, int sched) {
+  auto* k = (KvStreams*)h;
+  if (!k || sched < -1 || sched > kSchedWaves) return (int)hipErrorInvalidValue;
+  k->sched = sched;
+  return 0;
+}
+
 // Mode 3: 1 when a server grid gave up waiting for a post (its step's unposted slices were not
 // run), and clears the flag; waits for the last step's server first.  0: none, <0: no server yet.
 int spl_kvs_async_error(void* h) {
@@ -1786,7 +1797,7 @@ int spl_kvs_step(void* h, spl_arena_t a, hipStream_t origin, const char* skeys, 
     if (n_get > 0) tab.s[tab.n++] = FSeg{gkeys, gout, glens, gstatus, nullptr, nullptr, n_get, ostride, 0};
     uint32_t tag = 0;
     unsigned long long* cw = k->claim_slot(&tag);
-    return launch_fused(a, tab, n_set + n_get, fused, max_retry, stats, origin, cw, tag);
+    return launch_fused(a, tab, n_set + n_get, fused, max_retry, stats, origin, cw, tag, k->sched);
   }
   hipError_t e = hipEventRecord(k->start, origin);
   if (e != hipSuccess) return (int)e;
@@ -1866,7 +1877,7 @@ int spl_kvs_step_xr(void* h, spl_arena_t a, hipStream_t origin, const spl_xr_ste
     }
     uint32_t tag = 0;
     unsigned long long* cw = k->claim_slot(&tag);
-    return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin, cw, tag);
+    return launch_fused(a, tab, rows, k->fused, max_retry, stats, origin, cw, tag, k->sched);
   }
   if (W > 1 && (x->off_sp > 0 || x->off_gp > 0)) return (int)hipErrorInvalidValue;  // direct: the fused grid only
   hipError_t e = hipEventRecord(k->start, origin);

@@ -183,6 +183,9 @@ void *spl_kvs_create(int writers, int readers);
 void spl_kvs_destroy(void *h);
 /* 0: one launch per client stream slice; 1 / 2 (default, SPL_KVS_FUSED): every slice in one fused grid */
 int spl_kvs_set_fused(void *h, int mode);
+// fused-grid scheduling of this context: 0 fixed lane streams + workgroup barrier per round, 1 chunk claims,
+// 2 fixed lane streams + wave-vote exit (the SPL_KVS_SCHED default); -1: back to SPL_KVS_SCHED
+int spl_kvs_set_sched(void *h, int sched);
 int spl_kvs_step(void *h, spl_arena_t a, hipStream_t origin, const char *skeys, int kstride, const uint8_t *svals,
                  int vstride, const uint32_t *slens, long n_set, int32_t *sstatus, const char *gkeys, uint8_t *gout,
                  int ostride, uint32_t *glens, long n_get, int32_t *gstatus, int max_retry, uint64_t *stats);

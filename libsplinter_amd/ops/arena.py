@@ -102,6 +102,12 @@ class KvStreams:
         stream-posted slices consumed by a resident server grid."""
         _check(self._H.spl_kvs_set_fused(self.h, int(mode)), "kvs_set_fused")
 
+    def set_sched(self, sched: int):
+        """Fused-grid scheduling (mode 2): 0 fixed lane streams with a workgroup barrier per round, 1
+        workgroups claim row chunks from a launch-wide counter, 2 fixed lane streams with a wave-vote
+        exit (default, SPL_KVS_SCHED); -1 returns to the environment's choice."""
+        _check(self._H.spl_kvs_set_sched(self.h, int(sched)), "kvs_set_sched")
+
     def async_error(self) -> int:
         """Mode 3: 1 if a server grid gave up waiting for a slice's post (those rows did not run; the
         flag is cleared), 0 if not, -1 before the first server step.  Waits for the last server grid."""

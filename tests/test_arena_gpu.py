@@ -488,19 +488,24 @@ def test_acquire_free_get_cross_xcd_hot_keys(uniq):
 
 
 @pytest.mark.parametrize("kstride", [16, 32])
-@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+@pytest.mark.parametrize("mode", [0, 1, 2, 3, "2s0", "2s1"])
 def test_kvs_step_modes_match_plain_kernels(uniq, kstride, mode):
     """One KV step of 8 + 8 client streams (spl_kvs_step) -- per-slice launches (0), one fused
-    grid (1, 2: the default) or stream-posted slices on a server grid (3; 32-B keys take the fused
-    grid) -- sets new and existing keys and gets present and missing ones with the same results as
-    the plain batch kernels."""
+    grid (1, 2: the default; "2s0" / "2s1": its workgroup-barrier and chunk-claim schedules) or
+    stream-posted slices on a server grid (3; 32-B keys take the fused grid) -- sets new and
+    existing keys and gets present and missing ones with the same results as the plain batch
+    kernels."""
     import torch
     from libsplinter_amd.ops.arena import HbmArena, KvStreams, pack_keys, pack_values, unpack
-    rng = np.random.default_rng(kstride + mode)
+    sched = -1
+    if isinstance(mode, str):
+        mode, sched = int(mode[0]), int(mode[2:])
+    rng = np.random.default_rng(kstride + mode + 7 * sched)
     a = HbmArena.create(uniq, slots=1 << 16, max_val=256, embeddings=False)
     kvs = KvStreams(8, 8)
     try:
         kvs.set_fused(mode)
+        kvs.set_sched(sched)
         n = 20000
         w = kstride - 1
         keys = [f"k{i:0{min(w - 1, 12)}d}"[:w] for i in range(n)]

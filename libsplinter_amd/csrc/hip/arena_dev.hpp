@@ -519,7 +519,7 @@ struct Claim {
   bool fresh;     // true: insert into a free slot
   int32_t rc;
   uint64_t wm = 0, bl = 0;  // watcher mask / bloom labels read while holding the slot (pulse_masks)
-  uint64_t ep = 0;          // the held (odd) epoch: finish_set_store publishes ep + 1
+  uint64_t ep = 0;          // the held (odd) epoch
 };
 
 __device__ __forceinline__ void clear_claim(const Arena& a, long idx) {
@@ -646,111 +646,6 @@ __device__ Claim claim_set(const Arena& a, const KeyT<KW>& k, uint64_t s0) {
   return Claim{free_idx, true, kOk, 0, 0, free_ep + 1};
 }
 
-// Returning 8-B compare-and-swap issued WITHOUT a wait (the agent-scope form hipcc emits for
-// acas64); the result is valid only after cas_wait.  Lets a lane put the claims of all its ops in
-// flight together instead of one memory round trip per op.
-__device__ __forceinline__ uint64_t cas64_issue(void* p, uint64_t expect, uint64_t want) {
-  typedef unsigned long long u64x2_t __attribute__((ext_vector_type(2)));
-  const u64x2_t d = {want, expect};
-  uint64_t r;
-  asm volatile("global_atomic_cmpswap_x2 %0, %1, %2, off sc0" : "=v"(r) : "v"(p), "v"(d) : "memory");
-  return r;
-}
-__device__ __forceinline__ void cas_wait(uint64_t& r) { asm volatile("s_waitcnt vmcnt(0)" : "+v"(r)::"memory"); }
-
-// Claims of U ops of one lane at once (the update path of claim_set, batched): probe rounds over
-// the ops still searching -- every round issues the (hash, epoch), watcher / label and key loads of
-// all of them and waits once -- then one round of compare-and-swaps for every op that found its
-// key.  An op whose chain ends before its key (an insert) or runs past kProbeRounds slots falls
-// back to claim_set, which re-probes and runs the insert protocol.  Same outcomes as U calls of
-// claim_set; the round trips per lane drop from 2U to (longest chain + 1).
-template <int U, int KW>
-__device__ __forceinline__ void claim_many(const Arena& a, const KeyT<KW> (&k)[U], const bool (&active)[U],
-                                          Claim (&c)[U], uint64_t s0) {
-  constexpr int kProbeRounds = 4;
-  size_t idx[U];
-  bool pend[U], slow[U], cas[U];
-  uint64_t exp[U];
-#pragma unroll
-  for (int j = 0; j < U; ++j) {
-    c[j] = Claim{-1, false, kInval};
-    pend[j] = active[j];
-    slow[j] = false;
-    cas[j] = false;
-    exp[j] = 0;
-    idx[j] = active[j] ? (size_t)(k[j].hash % a.slots) : 0;
-  }
-  for (int r = 0; r < kProbeRounds; ++r) {
-    bool any = false;
-#pragma unroll
-    for (int j = 0; j < U; ++j) any |= pend[j];
-    if (!any) break;
-    // per op: (hash, epoch) 16 B, watcher mask and labels 8 B each, the first two key chunks
-    u32x4c_t he[U], k0[U], k1[U];
-    u32x2c_t wm[U], bl[U];
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      const uint8_t* s = a.slot(idx[j]);
-      if (pend[j]) {
-        he[j] = ld16c(s + kOffHash);
-        wm[j] = ld8c(s + kOffWatch);
-        bl[j] = ld8c(s + kOffBloom);
-        k0[j] = ld16c(s + kOffKey);
-        k1[j] = u32x4c_t{0u, 0u, 0u, 0u};
-        if (k[j].len >= 16) k1[j] = ld16c(s + kOffKey + 16);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (pend[j]) {
-        vm_wait(he[j], k0[j], k1[j]);
-        vm_wait2(wm[j], bl[j]);
-      }
-    }
-#pragma unroll
-    for (int j = 0; j < U; ++j) {
-      if (!pend[j]) continue;
-      const uint64_t sh = lo64(he[j]), e = hi64(he[j]);
-      const bool keq = k0[j].x == k[j].word(0) && k0[j].y == k[j].word(1) && k0[j].z == k[j].word(2) &&
-                       k0[j].w == k[j].word(3) &&
-                       (k[j].len < 16 || (k1[j].x == k[j].word(4) && k1[j].y == k[j].word(5) &&
-                                          k1[j].z == k[j].word(6) && k1[j].w == k[j].word(7)));
-      if (k[j].len >= 32) {  // key + NUL past two chunks: the per-op path compares it whole
-        pend[j] = false;
-        slow[j] = true;
-      } else if (sh == k[j].hash && keq) {
-        pend[j] = false;
-        if (e & 1) {
-          c[j].rc = kAgain;
-        } else {
-          c[j] = Claim{(long)idx[j], false, kOk, ((uint64_t)wm[j].y << 32) | wm[j].x,
-                       ((uint64_t)bl[j].y << 32) | bl[j].x, e + 1};
-          exp[j] = e;
-          cas[j] = true;
-        }
-      } else if (sh == 0 && e == 0) {  // chain ends: not present -> insert protocol
-        pend[j] = false;
-        slow[j] = true;
-      } else if (++idx[j] == a.slots) {
-        idx[j] = 0;
-      }
-    }
-  }
-  uint64_t old[U];
-#pragma unroll
-  for (int j = 0; j < U; ++j)
-    if (cas[j]) old[j] = cas64_issue(epoch_ptr(a.slot((size_t)c[j].idx)), exp[j], exp[j] + 1);
-#pragma unroll
-  for (int j = 0; j < U; ++j)
-    if (cas[j]) {
-      cas_wait(old[j]);
-      if (old[j] != exp[j]) c[j] = Claim{-1, false, kAgain};
-    }
-#pragma unroll
-  for (int j = 0; j < U; ++j)
-    if (slow[j] || pend[j]) c[j] = claim_set(a, k[j], s0);
-}
-
 // Slot metadata part of a set (everything but the value bytes): fresh-slot defaults and val_len.
 template <int MO = 0>
 __device__ __forceinline__ void write_meta(const Arena& a, const Claim& c, uint32_t len) {
@@ -800,14 +695,9 @@ __device__ __forceinline__ void write_set(const Arena& a, const Claim& c, const 
   ast32(s + kOffValLen, len);
 }
 
+// (A plain store of the held epoch + 1 instead of the atomic add measured neutral in round 6, KV-only
+// 4.86-4.94 vs 4.92-4.93 G ops/s; a lane-batched claim of U ops, claim_many, was pruned in round 4.)
 __device__ __forceinline__ void finish_set(const Arena& a, const Claim& c) { aadd64(epoch_ptr(a.slot((size_t)c.idx)), 1); }
-// The same publication as a plain agent-scope (sc1) 8-B store of the next even epoch: while the
-// epoch is odd only its holder changes it (every claim is a CAS from an even value), so the store
-// equals the increment and spares the memory-side read-modify-write of an atomic.
-__device__ __forceinline__ void finish_set_store(const Arena& a, const Claim& c) {
-  ast64(epoch_ptr(a.slot((size_t)c.idx)), c.ep + 1);
-}
-
 // Single-op SET (insert or update) with its own release.
 template <int MO = 0, int KW>
 __device__ int32_t set_op(const Arena& a, const KeyT<KW>& k, const uint8_t* val, uint32_t len, long* out_idx) {

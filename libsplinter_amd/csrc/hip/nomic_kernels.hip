@@ -408,7 +408,8 @@ __device__ __forceinline__ int v3sw(int key, int c) { return c ^ (((key >> 1) & 
 // s_setprio 1 over the MFMA runs -- alone and together within +-1.5 % of this form in isolation and
 // 0.1 % in the encoder, profiles/r6/README.md.  Also measured then and not kept: the two S^T chains
 // interleaved with four-way partial max / sum chains (neutral), and no row max after the first tile
-// with an overflow-guarded exact path (-2 % in isolation, neutral in the encoder), attn_forms2_ab.)
+// with an overflow-guarded exact path (-2 % in isolation, neutral in the encoder), attn_forms2_ab; and
+// W = 4, four waves per SIMD at <= 128 VGPRs with 13 spilled: 105 vs 84 us per layer.)
 template <bool PF2 = false, int W = 1>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(W))) void k_attn3(const uint16_t* __restrict__ qkv, uint16_t* __restrict__ out,
                                                const int32_t* __restrict__ cu, const int32_t* __restrict__ qblocks,

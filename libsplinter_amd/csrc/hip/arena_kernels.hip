@@ -133,11 +133,11 @@ __global__ void k_init_slots(spl_arena_t aa) {
 // stored bytewise so it cannot spill into the next row); 0xFFFFFFFF: no limit.
 // MO: store flavour of the destination rows (st16<MO>); LD1: source rows read with 16-B `sc1` loads
 // (L1-bypassing, so a reader needs no L1-invalidating acquire before them).
-template <int NE, int MO = 0, bool LD1 = false>
+template <int NE, int MO = 0, bool LD1 = false, int kUnr = 4>
 __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
                                           int groups, uint32_t rowb) {
   const int q = lane >> 4, cl = lane & 15;
-  constexpr int kUnr = 4;  // 8 rows in flight cost 80 VGPRs (1 wave/SIMD); 4 keep the kernel at 2
+  // kUnr x 4 rows in flight per wave (kUnr 4: 16 rows; the round-1 note: 8 cost 80 VGPRs at 1 wave/SIMD)
   for (int e0 = 0; e0 < NE; e0 += 4 * kUnr) {
     uint4 P[kUnr];
     uint2 L[kUnr];
@@ -158,8 +158,10 @@ __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const ui
           t[u] = u32x4c_t{0u, 0u, 0u, 0u};
           if (c < n16) t[u] = ld16c(src + c);
         }
-        static_assert(kUnr == 4, "one wait ties the four loads");
-        asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3])::"memory");
+        static_assert(kUnr % 4 == 0, "each wait ties four loads");
+#pragma unroll
+        for (int u = 0; u < kUnr; u += 4)
+          asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[u]), "+v"(t[u + 1]), "+v"(t[u + 2]), "+v"(t[u + 3])::"memory");
 #pragma unroll
         for (int u = 0; u < kUnr; ++u) d[u] = make_uint4(t[u].x, t[u].y, t[u].z, t[u].w);
       } else {
@@ -185,6 +187,93 @@ __device__ __forceinline__ void coop_copy(const uint4* __restrict__ ep, const ui
         else st16<MO>(dst + c, v);
       }
     }
+  }
+}
+
+// The same copy with the source rows staged through LDS by LDS-DMA (global_load_lds_dwordx4: a
+// wave instruction moves 4 rows x 16 chunks into 1 KB of LDS without passing through VGPRs), so NB x 4
+// rows are in flight per wave instead of 16 while the registers the round body needs stay free; the
+// stores read the chunks back from LDS (ds_read_b128 of the lane's own 16 B) and go out as in
+// coop_copy.  One 256-B group per row (max_val <= 256); `stage`: the wave's NB KB of LDS.
+// LD1: the DMA carries `sc1` (L1-bypassing, as ld16c).
+__device__ __forceinline__ void dma16(const void* gsrc, uint32_t lds_base, bool sc1) {
+  uint32_t save;
+  if (sc1)
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off sc1\n\ts_mov_b32 m0, %0"
+                 : "=&s"(save)
+                 : "v"(gsrc), "s"(lds_base)
+                 : "memory");
+  else
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(save)
+                 : "v"(gsrc), "s"(lds_base)
+                 : "memory");
+}
+
+// NR > 0: NR more row instructions per batch go through registers beside the NB staged ones
+// (4 (NB + NR) rows in flight).
+template <int NE, int MO = 0, bool LD1 = false, int NB = 6, int NR = 0>
+__device__ __forceinline__ void coop_copy_dma(const uint4* __restrict__ ep, const uint2* __restrict__ el, int lane,
+                                              uint32_t rowb, uint4* stage) {
+  const int q = lane >> 4, cl = lane & 15;
+  const uint32_t sbase =
+      __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)stage);
+  constexpr int NT = NB + NR;
+  auto put = [&](int e, uint4 v, uint32_t c) {  // chunk c of entry e's row: masked, to its destination
+    const uint2 L = el[e];
+    if (c >= L.y) return;
+    const uint32_t n16 = (L.x + 15) >> 4;
+    if (c >= n16) v = make_uint4(0, 0, 0, 0);
+    if (c == n16 - 1 && (L.x & 15)) {
+      const int r = (int)(L.x & 15);
+      v.x &= keep_mask(r); v.y &= keep_mask(r - 4); v.z &= keep_mask(r - 8); v.w &= keep_mask(r - 12);
+    }
+    const uint4 P = ep[e];
+    uint4* dst = (uint4*)(((uint64_t)P.w << 32) | P.z);
+    if (c * 16 + 16 > rowb) store_partial((uint8_t*)(dst + c), v, rowb - c * 16);
+    else st16<MO>(dst + c, v);
+  };
+  for (int e0 = 0; e0 < NE; e0 += 4 * NT) {
+    // issue: row e0 + 4u + q, chunk cl of every instruction u; u < NB into stage[u KB + lane 16 B]
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int e = e0 + 4 * u + q;
+      if (e >= NE) break;
+      const uint4 P = ep[e];
+      const uint32_t n16 = (el[e].x + 15) >> 4;
+      const uint4* src = (const uint4*)(((uint64_t)P.y << 32) | P.x);
+      if ((uint32_t)cl < n16) dma16(src + cl, sbase + u * 1024, LD1);
+    }
+    u32x4c_t t[NR > 0 ? NR : 1];
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int e = e0 + 4 * (NB + u) + q;
+      t[u] = u32x4c_t{0u, 0u, 0u, 0u};
+      if (e < NE) {
+        const uint4 P = ep[e];
+        const uint32_t n16 = (el[e].x + 15) >> 4;
+        const uint4* src = (const uint4*)(((uint64_t)P.y << 32) | P.x);
+        if ((uint32_t)cl < n16) t[u] = LD1 ? ld16c(src + cl) : __builtin_bit_cast(u32x4c_t, src[cl]);
+      }
+    }
+    // this wave's DMAs and register loads have landed
+    if constexpr (NR == 4)
+      asm volatile("s_waitcnt vmcnt(0)" : "+v"(t[0]), "+v"(t[1]), "+v"(t[2]), "+v"(t[3])::"memory");
+    else
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int e = e0 + 4 * u + q;
+      if (e >= NE) break;
+      put(e, stage[u * 64 + lane], (uint32_t)cl);
+    }
+#pragma unroll
+    for (int u = 0; u < NR; ++u) {
+      const int e = e0 + 4 * (NB + u) + q;
+      if (e < NE) put(e, make_uint4(t[u].x, t[u].y, t[u].z, t[u].w), (uint32_t)cl);
+    }
+    // the next batch's DMAs overwrite the stage: every ds_read of this one has returned
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
 }
 
@@ -536,10 +625,16 @@ __device__ __forceinline__ void fill_slot(OpSlots<U, KW, OI>& o, int j, const FS
 // round 6: a get's home-slot value row requested by LDS-DMA beside its probe, 4.45-4.47 vs 4.84-4.88 G
 // ops/s KV-only: the extra requests cost more than the row copy's L2 hit saves, profiles/r6/README.md.)
 constexpr int kKvSkipLen = 1;
+// kKvCopyDma: the round's row copies stage their source rows through LDS by LDS-DMA (coop_copy_dma)
+constexpr int kKvCopyDma = 4;
+// (SPL_KVS_COPY_DMA=1, default: KV-only 5.15-5.29 vs 4.92-4.99 G ops/s; 16 more rows per batch through
+// registers beside the staged 24 measured the same, 5.21-5.30: profiles/r6/README.md)
+constexpr int kKvStageKB = 6;  // LDS-DMA stage per wave (KB): 24 rows in flight
 template <int U, int KW, bool OI = false>
 __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW, OI>& o, bool scrub, bool hybrid,
                                          int max_retry, Stats& st, uint32_t& muts, uint4* cpp0, uint2* cpl0,
-                                         uint4* cpp1, uint2* cpl1, int lane, int flags, uint64_t& ms) {
+                                         uint4* cpp1, uint2* cpl1, int lane, int flags, uint64_t& ms,
+                                         uint4* stage = nullptr) {
   const bool skip_len = flags & kKvSkipLen;
   Claim c[U];
   long sidx[U];
@@ -595,8 +690,18 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
     cpl1[j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? n16 : 0u);
   }
   __builtin_amdgcn_wave_barrier();
-  coop_copy<U * 64, 3>(cpp0, cpl0, lane, (int)((a.max_val + 255) >> 8), a.max_val);
-  coop_copy<U * 64, 0, true>(cpp1, cpl1, lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
+#ifndef SPL_KV_COPY_UNR
+#define SPL_KV_COPY_UNR 4
+#endif
+#ifndef SPL_KV_DIAG_NO_COPY
+  if ((flags & kKvCopyDma) && stage && a.max_val <= 256) {
+    coop_copy_dma<U * 64, 3, false, kKvStageKB>(cpp0, cpl0, lane, a.max_val, stage);
+    coop_copy_dma<U * 64, 0, true, kKvStageKB>(cpp1, cpl1, lane, 0xFFFFFFFFu, stage);
+  } else {
+    coop_copy<U * 64, 3, false, SPL_KV_COPY_UNR>(cpp0, cpl0, lane, (int)((a.max_val + 255) >> 8), a.max_val);
+    coop_copy<U * 64, 0, true, SPL_KV_COPY_UNR>(cpp1, cpl1, lane, (int)((a.max_val + 255) >> 8), 0xFFFFFFFFu);
+  }
+#endif
 #pragma unroll
   for (int j = 0; j < U; ++j)
     if (o.seg[j] >= 0 && o.set[j] && rc[j] == kOk && oldlen[j] != o.len[j]) write_meta<3>(a, c[j], o.len[j]);
@@ -674,6 +779,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
                                                                                          int chunk_div) {
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
+  __shared__ uint4 cp_stage[B / 64][kKvStageKB * 64];  // kKvCopyDma: the waves' LDS-DMA stages
   __shared__ FSeg sg[kFusedSegs];
   __shared__ long sstart[kFusedSegs + 1];
   __shared__ long sh_c, sh_cs;  // kSchedChunks: the claimed chunk's first row and size
@@ -778,7 +884,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       break;
     }
     kv_round<U, KW, OI>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
-                    skip_len, ms);
+                    skip_len, ms, cp_stage[w]);
   }
   flush_stats(a, st, stats, muts);
 }
@@ -820,6 +926,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     uint64_t wait_ticks, int spread, int max_retry, uint64_t* stats, int skip_len) {
   __shared__ uint4 cp_p[2][B / 64][U * 64];
   __shared__ uint2 cp_l[2][B / 64][U * 64];
+  __shared__ uint4 cp_stage[B / 64][kKvStageKB * 64];  // kKvCopyDma: the waves' LDS-DMA stages
   __shared__ FSeg sg[2];  // 0: the set batch, 1: the get batch
   __shared__ long sh_b, sh_e;
   __shared__ int sh_kind, sh_state, sh_scan;
@@ -967,7 +1074,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       // nothing claimable yet: carried ops still progress
       if (carried)
         kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
-                        lane, skip_len, ms);
+                        lane, skip_len, ms, cp_stage[w]);
       else
         __builtin_amdgcn_s_sleep(32);
       continue;
@@ -997,7 +1104,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
       const bool more = row < end;
       if (!(WV ? __any(more && busy) : __syncthreads_or(more && busy))) break;
       kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w],
-                      lane, skip_len, ms);
+                      lane, skip_len, ms, cp_stage[w]);
     }
   }
   // the last chunk's ops and any carried retries
@@ -1007,7 +1114,7 @@ __global__ __launch_bounds__(B) __attribute__((amdgpu_waves_per_eu(OCC))) void k
     for (int j = 0; j < U; ++j) busy |= o.seg[j] >= 0;
     if (!(WV ? __any(busy) : __syncthreads_or(busy))) break;
     kv_round<U, KW>(a, sg, o, scrub, hybrid, max_retry, st, muts, cp_p[0][w], cp_l[0][w], cp_p[1][w], cp_l[1][w], lane,
-                    skip_len, ms);
+                    skip_len, ms, cp_stage[w]);
   }
   __syncthreads();  // (WV: every wave's drain is done before the group's totals are read)
   {
@@ -1061,7 +1168,8 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   const long cap = (long)stream_cus(s) * wpc;
   const dim3 g((unsigned)(need < cap ? need : cap));
   // SPL_KVS_SKIP_LEN (A/B knob): kv_round flags
-  static const int skip_len = env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0;
+  static const int skip_len = (env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0) |
+                              (env_int("SPL_KVS_COPY_DMA", 1) ? kKvCopyDma : 0);
   // segments with an output map (direct routed responses) take the OI form of the grid
   bool oi = false;
   for (int q = 0; q < tab.n; ++q) oi |= tab.s[q].oidx != nullptr;
@@ -1668,7 +1776,7 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
   static const int wv = env_int("SPL_KVS_ASYNC_WV", 1);
   const dim3 grid((unsigned)(need < cap ? need : cap));
-  const int flags = env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0;
+  const int flags = (env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0) | (env_int("SPL_KVS_COPY_DMA", 1) ? kKvCopyDma : 0);
   if (wv)
     hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3, true>), grid, dim3(256), 0, origin, a, sset, sget, nw, nr, ks, k->ctl,
                        seq, chunk, wait_ticks, spread, max_retry, stats, flags);

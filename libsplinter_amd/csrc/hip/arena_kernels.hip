@@ -1201,9 +1201,15 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   else if (kw4)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 4, 3>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len, nullptr,
                        0u, 0L, 1);
+  else if (oi && sched == kSchedWaves)
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 16, 1, true, kSchedWaves>), g, dim3(256), 0, s, a, tab, max_retry, stats,
+                       skip_len, nullptr, 0u, 0L, 1);
   else if (oi)
     hipLaunchKernelGGL((k_kv_fused<2, 256, 16, 1, true>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len,
                        nullptr, 0u, 0L, 1);
+  else if (sched == kSchedWaves)
+    hipLaunchKernelGGL((k_kv_fused<2, 256, 16, 1, false, kSchedWaves>), g, dim3(256), 0, s, a, tab, max_retry, stats,
+                       skip_len, nullptr, 0u, 0L, 1);
   else
     hipLaunchKernelGGL((k_kv_fused<2, 256>), g, dim3(256), 0, s, a, tab, max_retry, stats, skip_len, nullptr, 0u, 0L, 1);
   return (int)hipGetLastError();

@@ -630,6 +630,11 @@ constexpr int kKvCopyDma = 4;
 // (SPL_KVS_COPY_DMA=1, default: KV-only 5.15-5.29 vs 4.92-4.99 G ops/s; 16 more rows per batch through
 // registers beside the staged 24 measured the same, 5.21-5.30: profiles/r6/README.md)
 constexpr int kKvStageKB = 6;  // LDS-DMA stage per wave (KB): 24 rows in flight
+// kKvPadOut (SPL_KVS_PAD_OUT, default 1): a get's output row is written through the next 64-B boundary
+// inside its stride (zeros past the value), so the row's last line is a whole-line write, not a partial
+// one (a read-modify-write below the HBM3E ECC granule): KV-only 5.35-5.47 vs 5.15-5.24 G ops/s, mixed
+// step 12.06-12.10 vs 12.30 ms (profiles/r6/README.md)
+constexpr int kKvPadOut = 8;
 template <int U, int KW, bool OI = false>
 __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots<U, KW, OI>& o, bool scrub, bool hybrid,
                                          int max_retry, Stats& st, uint32_t& muts, uint4* cpp0, uint2* cpl0,
@@ -687,7 +692,14 @@ __device__ __forceinline__ void kv_round(const Arena& a, const FSeg* sg, OpSlots
     const uint64_t gdst = gg ? (uint64_t)(f->vals + out_row(o, j) * (long)f->vstride) : 0;
     const uint32_t n16 = (o.len[j] + 15) >> 4;
     cpp1[j * 64 + lane] = make_uint4((uint32_t)gsrc, (uint32_t)(gsrc >> 32), (uint32_t)gdst, (uint32_t)(gdst >> 32));
-    cpl1[j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? n16 : 0u);
+    // kKvPadOut: the output row is written to the next 64-B boundary (zeros past the value, inside the
+    // row's stride), so its last line is a whole-line write instead of a partial one
+    uint32_t wend = n16;
+    if ((flags & kKvPadOut) && gg) {
+      const uint32_t pad = (n16 + 3u) & ~3u, cap = (uint32_t)f->vstride >> 4;
+      wend = pad < cap ? pad : (cap > n16 ? cap : n16);
+    }
+    cpl1[j * 64 + lane] = make_uint2(gg ? n16 * 16 : 0u, gg ? wend : 0u);
   }
   __builtin_amdgcn_wave_barrier();
 #ifndef SPL_KV_COPY_UNR
@@ -1169,7 +1181,8 @@ int launch_fused(spl_arena_t a, const FSegs& tab, long rows, int mode, int max_r
   const dim3 g((unsigned)(need < cap ? need : cap));
   // SPL_KVS_SKIP_LEN (A/B knob): kv_round flags
   static const int skip_len = (env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0) |
-                              (env_int("SPL_KVS_COPY_DMA", 1) ? kKvCopyDma : 0);
+                              (env_int("SPL_KVS_COPY_DMA", 1) ? kKvCopyDma : 0) |
+                              (env_int("SPL_KVS_PAD_OUT", 1) ? kKvPadOut : 0);
   // segments with an output map (direct routed responses) take the OI form of the grid
   bool oi = false;
   for (int q = 0; q < tab.n; ++q) oi |= tab.s[q].oidx != nullptr;
@@ -1782,7 +1795,8 @@ int kvs_step_async(KvStreams* k, spl_arena_t a, hipStream_t origin, const FSeg& 
   static const int spread = env_int("SPL_KVS_ASYNC_SPREAD", 1);
   static const int wv = env_int("SPL_KVS_ASYNC_WV", 1);
   const dim3 grid((unsigned)(need < cap ? need : cap));
-  const int flags = (env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0) | (env_int("SPL_KVS_COPY_DMA", 1) ? kKvCopyDma : 0);
+  const int flags = (env_int("SPL_KVS_SKIP_LEN", 1) ? kKvSkipLen : 0) | (env_int("SPL_KVS_COPY_DMA", 1) ? kKvCopyDma : 0) |
+                    (env_int("SPL_KVS_PAD_OUT", 1) ? kKvPadOut : 0);
   if (wv)
     hipLaunchKernelGGL((k_kv_server<2, 256, 4, 3, true>), grid, dim3(256), 0, origin, a, sset, sget, nw, nr, ks, k->ctl,
                        seq, chunk, wait_ticks, spread, max_retry, stats, flags);
